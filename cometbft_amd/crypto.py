@@ -1,0 +1,212 @@
+"""Python mirror of the reference's crypto boundary for Ed25519, backed by the
+gfx950 verifier in libcmtverify.so.
+
+Reference interfaces mirrored
+  crypto.PubKey.VerifySignature(msg, sig) bool      /root/reference/crypto/crypto.go:25
+  ed25519.PubKey.VerifySignature                    /root/reference/crypto/ed25519/ed25519.go:148-155
+  crypto.BatchVerifier {Add, Verify}                upstream CometBFT v0.38 (not in this v0.34 tree;
+                                                    see SURVEY.md section 8b and INTEGRATION.md)
+  ed25519.NewBatchVerifier()                        upstream, same
+
+Every verdict is computed on the GPU. There is no CPU fallback in this package.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+from typing import Sequence
+
+import numpy as np
+
+from . import _native as N
+
+MODE_GO_STDLIB = N.MODE_GO_STDLIB
+MODE_ZIP215 = N.MODE_ZIP215
+
+PUBKEY_SIZE = 32     # crypto/ed25519/ed25519.go:24
+SIGNATURE_SIZE = 64  # crypto/ed25519/ed25519.go:28
+
+
+def _u8(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+
+
+class Context:
+    """One device context (stream, fixed-base table, staging buffers)."""
+
+    def __init__(self, device: int = -1, default_mode: int = MODE_GO_STDLIB):
+        L = N.lib()
+        cfg = N.cmtv_config(device=device, default_mode=default_mode, flags=0, reserved=0)
+        h = ctypes.c_void_p()
+        N.check(L.cmtv_open(ctypes.byref(cfg), ctypes.byref(h)), "cmtv_open")
+        self._h = h
+        self.default_mode = default_mode
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if self._h:
+            N.lib().cmtv_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def stream(self) -> int:
+        return N.lib().cmtv_stream(self._h) or 0
+
+    def stats(self) -> dict:
+        st = N.cmtv_stats()
+        N.check(N.lib().cmtv_stats_get(self._h, ctypes.byref(st)), "cmtv_stats_get")
+        return {k: getattr(st, k) for k, _ in st._fields_}
+
+    # -------------------------------------------------------------- batches
+    def verify(self, pk: np.ndarray, sig: np.ndarray, msg: np.ndarray, msg_off: np.ndarray,
+               mode: int | None = None, bitmap: bool = False):
+        """Verdicts for n signatures held in host arrays (pk n x 32, sig n x 64,
+        flat msg bytes + n+1 uint32 offsets). Returns uint8[n] (and the uint64
+        bitmap when bitmap=True)."""
+        mode = self.default_mode if mode is None else mode
+        pk = np.ascontiguousarray(pk, dtype=np.uint8).reshape(-1, 32)
+        sig = np.ascontiguousarray(sig, dtype=np.uint8).reshape(-1, 64)
+        n = pk.shape[0]
+        if sig.shape[0] != n or len(msg_off) != n + 1:
+            raise ValueError("pk / sig / msg_off sizes disagree")
+        msg = np.ascontiguousarray(msg, dtype=np.uint8)
+        if msg.size == 0:
+            msg = np.zeros(1, np.uint8)
+        off = np.ascontiguousarray(msg_off, dtype=np.uint32)
+        valid = np.zeros(max(n, 1), np.uint8)
+        words = np.zeros(max((n + 63) // 64, 1), np.uint64)
+        rc = N.lib().cmtv_verify_ed25519(self._h, n, _u8(pk), _u8(sig), _u8(msg),
+                                         off.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), mode, _u8(valid),
+                                         words.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)))
+        N.check(rc, "cmtv_verify_ed25519")
+        if bitmap:
+            return valid[:n], words[: (n + 63) // 64]
+        return valid[:n]
+
+    def verify_device(self, n: int, d_pk: int, d_sig: int, d_msg: int, d_off: int, mode: int,
+                      d_valid: int = 0, d_bitmap: int = 0, stream: int = 0) -> None:
+        """Enqueue verification over device-resident buffers (raw pointers)."""
+        rc = N.lib().cmtv_verify_ed25519_device(self._h, n, d_pk, d_sig, d_msg, d_off, mode, d_valid or None,
+                                                d_bitmap or None, stream or None)
+        N.check(rc, "cmtv_verify_ed25519_device")
+
+    # -------------------------------------------------------------- test data
+    def pubkeys(self, seeds: np.ndarray) -> np.ndarray:
+        seeds = np.ascontiguousarray(seeds, dtype=np.uint8).reshape(-1, 32)
+        out = np.zeros_like(seeds)
+        N.check(N.lib().cmtv_pubkeys_ed25519(self._h, seeds.shape[0], _u8(seeds), _u8(out)), "cmtv_pubkeys_ed25519")
+        return out
+
+    def sign(self, seeds: np.ndarray, msg: np.ndarray, msg_off: np.ndarray, key_idx=None) -> np.ndarray:
+        seeds = np.ascontiguousarray(seeds, dtype=np.uint8).reshape(-1, 32)
+        off = np.ascontiguousarray(msg_off, dtype=np.uint32)
+        n = len(off) - 1
+        msg = np.ascontiguousarray(msg, dtype=np.uint8)
+        if msg.size == 0:
+            msg = np.zeros(1, np.uint8)
+        out = np.zeros((max(n, 1), 64), np.uint8)
+        kp = None
+        if key_idx is not None:
+            key_idx = np.ascontiguousarray(key_idx, dtype=np.uint32)
+            kp = key_idx.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
+        rc = N.lib().cmtv_sign_ed25519(self._h, n, _u8(seeds), kp, _u8(msg),
+                                       off.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), _u8(out))
+        N.check(rc, "cmtv_sign_ed25519")
+        return out[:n]
+
+
+_default_ctx = None
+_default_lock = threading.Lock()
+
+
+def default_context() -> Context:
+    global _default_ctx
+    with _default_lock:
+        if _default_ctx is None:
+            _default_ctx = Context()
+        return _default_ctx
+
+
+def pack_messages(msgs: Sequence[bytes]):
+    off = np.zeros(len(msgs) + 1, dtype=np.uint32)
+    if msgs:
+        off[1:] = np.cumsum([len(m) for m in msgs], dtype=np.uint64).astype(np.uint32)
+    buf = np.frombuffer(b"".join(msgs) + b"\0", dtype=np.uint8).copy()
+    return buf, off
+
+
+class PubKey(bytes):
+    """ed25519.PubKey (crypto/ed25519/ed25519.go:133): raw 32 bytes."""
+
+    def verify_signature(self, msg: bytes, sig: bytes, ctx: Context | None = None,
+                         mode: int = MODE_GO_STDLIB) -> bool:
+        """PubKey.VerifySignature (ed25519.go:148-155) as a batch of one on the
+        GPU. Wrong-length keys raise like Go's panic; wrong-length signatures
+        return False."""
+        if len(sig) != SIGNATURE_SIZE:
+            return False
+        if len(self) != PUBKEY_SIZE:
+            raise ValueError(f"ed25519: bad public key length: {len(self)}")
+        ctx = ctx or default_context()
+        m, off = pack_messages([bytes(msg)])
+        v = ctx.verify(np.frombuffer(bytes(self), np.uint8), np.frombuffer(bytes(sig), np.uint8), m, off, mode)
+        return bool(v[0])
+
+
+class BatchVerifier:
+    """crypto.BatchVerifier (upstream v0.38): Add(key, msg, sig) then
+    Verify() -> (bool, list[bool]). Malformed entries are accepted by add() and
+    come back invalid; a wrong-length key is also reported by bad_key_index so
+    a caller replaying the reference loop can raise at the same index."""
+
+    def __init__(self, ctx: Context | None = None, mode: int = MODE_GO_STDLIB):
+        self.ctx = ctx or default_context()
+        self.mode = mode
+        h = ctypes.c_void_p()
+        N.check(N.lib().cmtv_batch_new(self.ctx.handle, mode, ctypes.byref(h)), "cmtv_batch_new")
+        self._h = h
+        self.bad_key_index = -1
+
+    def __del__(self):
+        try:
+            if self._h:
+                N.lib().cmtv_batch_free(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+    def __len__(self):
+        return N.lib().cmtv_batch_len(self._h)
+
+    def add(self, key: bytes, msg: bytes, sig: bytes) -> None:
+        k = np.frombuffer(bytes(key) + b"\0", np.uint8)
+        m = np.frombuffer(bytes(msg) + b"\0", np.uint8)
+        s = np.frombuffer(bytes(sig) + b"\0", np.uint8)
+        N.check(N.lib().cmtv_batch_add(self._h, _u8(k), len(key), _u8(m), len(msg), _u8(s), len(sig)),
+                "cmtv_batch_add")
+
+    def verify(self):
+        n = len(self)
+        out = np.zeros(max(n, 1), np.uint8)
+        ok = ctypes.c_int(0)
+        bad = ctypes.c_int64(-1)
+        N.check(N.lib().cmtv_batch_verify(self._h, _u8(out), ctypes.byref(ok), ctypes.byref(bad)),
+                "cmtv_batch_verify")
+        self.bad_key_index = bad.value
+        return bool(ok.value), [bool(x) for x in out[:n]]
+
+    def reset(self):
+        N.lib().cmtv_batch_reset(self._h)
+
+
+def new_batch_verifier(ctx: Context | None = None, mode: int = MODE_GO_STDLIB) -> BatchVerifier:
+    """ed25519.NewBatchVerifier() (upstream)."""
+    return BatchVerifier(ctx, mode)

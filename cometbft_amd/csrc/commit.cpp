@@ -1,0 +1,407 @@
+// commit.cpp -- host side above the device verifier: CanonicalVote sign-bytes,
+// the crypto.BatchVerifier mirror and the VerifyCommit* replay.
+//
+// The reference verifies a commit with a sequential loop that calls
+// PubKey.VerifySignature per CommitSig (types/validator_set.go:667-826). Here
+// the signatures that loop could reach are verified in ONE device batch and the
+// loop is then replayed in index order over the verdicts, so the returned
+// error (first bad signature, early exits, tallies, panics) is exactly the
+// reference's. Error strings are produced with the reference's formats.
+#include <cinttypes>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/cmtverify.h"
+#include "runtime_internal.h"
+
+namespace {
+
+// ------------------------------------------------------------------ encoding
+
+void put_uvarint(std::string& out, uint64_t v) {
+  while (v >= 0x80) {
+    out.push_back((char)((v & 0x7F) | 0x80));
+    v >>= 7;
+  }
+  out.push_back((char)v);
+}
+
+void put_bytes_field(std::string& out, uint8_t tag, const uint8_t* p, size_t n) {
+  out.push_back((char)tag);
+  put_uvarint(out, n);
+  out.append(reinterpret_cast<const char*>(p), n);
+}
+
+void put_sfixed64(std::string& out, uint8_t tag, int64_t v) {
+  out.push_back((char)tag);
+  uint64_t u = (uint64_t)v;
+  for (int i = 0; i < 8; i++) out.push_back((char)(u >> (8 * i)));
+}
+
+bool block_id_is_zero(const cmtv_block_id* b) {
+  return !b || (b->hash_len == 0 && b->psh_total == 0 && b->psh_hash_len == 0);
+}
+
+// CanonicalBlockID (canonical.pb.go:370) or nothing when IsZero (canonical.go:18-33)
+void put_canonical_block_id(std::string& out, const cmtv_block_id* b) {
+  if (block_id_is_zero(b)) return;
+  std::string psh;
+  if (b->psh_total != 0) {
+    psh.push_back(0x08);
+    put_uvarint(psh, b->psh_total);
+  }
+  if (b->psh_hash_len) put_bytes_field(psh, 0x12, b->psh_hash, b->psh_hash_len);
+  std::string cb;
+  if (b->hash_len) put_bytes_field(cb, 0x0A, b->hash, b->hash_len);
+  put_bytes_field(cb, 0x12, reinterpret_cast<const uint8_t*>(psh.data()), psh.size());
+  put_bytes_field(out, 0x22, reinterpret_cast<const uint8_t*>(cb.data()), cb.size());
+}
+
+// VoteSignBytes (types/vote.go:93): uvarint(len) || CanonicalVote
+// (canonical.pb.go:517-567; Timestamp = gogoproto StdTime {1: seconds, 2: nanos})
+void vote_sign_bytes(std::string& out, const char* chain_id, size_t chain_id_len, int32_t vtype, int64_t height,
+                     int32_t round, const cmtv_block_id* bid, int64_t ts_sec, int32_t ts_nanos) {
+  std::string body;
+  if (vtype != 0) {
+    body.push_back(0x08);
+    put_uvarint(body, (uint64_t)(int64_t)vtype);
+  }
+  if (height != 0) put_sfixed64(body, 0x11, height);
+  if (round != 0) put_sfixed64(body, 0x19, (int64_t)round);
+  put_canonical_block_id(body, bid);
+  std::string ts;
+  if (ts_sec != 0) {
+    ts.push_back(0x08);
+    put_uvarint(ts, (uint64_t)ts_sec);
+  }
+  if (ts_nanos != 0) {
+    ts.push_back(0x10);
+    put_uvarint(ts, (uint64_t)(int64_t)ts_nanos);
+  }
+  put_bytes_field(body, 0x2A, reinterpret_cast<const uint8_t*>(ts.data()), ts.size());
+  if (chain_id_len) put_bytes_field(body, 0x32, reinterpret_cast<const uint8_t*>(chain_id), chain_id_len);
+  out.clear();
+  put_uvarint(out, body.size());
+  out += body;
+}
+
+// ------------------------------------------------------------------ formatting
+
+std::string hex_upper(const uint8_t* p, size_t n) {
+  static const char* d = "0123456789ABCDEF";
+  std::string s;
+  s.reserve(2 * n);
+  for (size_t i = 0; i < n; i++) {
+    s.push_back(d[p[i] >> 4]);
+    s.push_back(d[p[i] & 15]);
+  }
+  return s;
+}
+
+// BlockID.String() (types/block.go:1217): "%v:%v" Hash, PartSetHeader
+// PartSetHeader.String() (types/part_set.go:103): "%v:%X" Total, Fingerprint(Hash)
+std::string block_id_string(const cmtv_block_id* b) {
+  uint8_t fp[6] = {0};
+  if (b && b->psh_hash_len) std::memcpy(fp, b->psh_hash, b->psh_hash_len < 6 ? b->psh_hash_len : 6);
+  std::string s = b ? hex_upper(b->hash, b->hash_len) : std::string();
+  s += ":" + std::to_string(b ? b->psh_total : 0) + ":" + hex_upper(fp, 6);
+  return s;
+}
+
+bool block_id_equals(const cmtv_block_id* a, const cmtv_block_id* b) {
+  auto eq = [](const uint8_t* x, uint32_t nx, const uint8_t* y, uint32_t ny) {
+    return nx == ny && (nx == 0 || std::memcmp(x, y, nx) == 0);
+  };
+  return eq(a->hash, a->hash_len, b->hash, b->hash_len) && a->psh_total == b->psh_total &&
+         eq(a->psh_hash, a->psh_hash_len, b->psh_hash, b->psh_hash_len);
+}
+
+void set_msg(char* buf, size_t cap, const std::string& s) {
+  if (!buf || cap == 0) return;
+  size_t n = s.size() < cap - 1 ? s.size() : cap - 1;
+  std::memcpy(buf, s.data(), n);
+  buf[n] = 0;
+}
+
+constexpr uint8_t kFlagAbsent = 1, kFlagCommit = 2, kFlagNil = 3;
+constexpr int32_t kPrecommit = 2;
+
+}  // namespace
+
+// ------------------------------------------------------------------ BatchVerifier
+
+struct cmtv_batch {
+  cmtv_ctx* ctx;
+  uint32_t mode;
+  std::vector<uint8_t> pk, sig, msg;
+  std::vector<uint32_t> off{0};
+  std::vector<uint8_t> forced_invalid;  // bad sig length
+  int64_t bad_key = -1;                 // first entry with a bad key length
+};
+
+extern "C" {
+
+int64_t cmtv_vote_sign_bytes(const char* chain_id, size_t chain_id_len, int32_t vote_type, int64_t height,
+                             int32_t round, const cmtv_block_id* block_id, int64_t ts_seconds, int32_t ts_nanos,
+                             uint8_t* out, size_t cap) {
+  if ((!chain_id && chain_id_len) || (!out && cap)) return CMTV_EINVAL;
+  std::string s;
+  vote_sign_bytes(s, chain_id, chain_id_len, vote_type, height, round, block_id, ts_seconds, ts_nanos);
+  if (s.size() <= cap) std::memcpy(out, s.data(), s.size());
+  return (int64_t)s.size();
+}
+
+int cmtv_batch_new(cmtv_ctx* ctx, uint32_t mode, cmtv_batch** out) {
+  if (!ctx || !out || mode > CMTV_MODE_ZIP215) return CMTV_EINVAL;
+  auto* b = new (std::nothrow) cmtv_batch();
+  if (!b) return CMTV_ENOMEM;
+  b->ctx = ctx;
+  b->mode = mode;
+  *out = b;
+  return CMTV_OK;
+}
+
+int cmtv_batch_add(cmtv_batch* b, const uint8_t* pk, size_t pk_len, const uint8_t* msg, size_t msg_len,
+                   const uint8_t* sig, size_t sig_len) {
+  if (!b || (!pk && pk_len) || (!msg && msg_len) || (!sig && sig_len)) return CMTV_EINVAL;
+  if (b->msg.size() + msg_len > 0xFFFFFFFFull) return CMTV_EINVAL;
+  const size_t idx = b->off.size() - 1;
+  uint8_t kbuf[32] = {0}, sbuf[64] = {0};
+  const bool key_ok = pk_len == 32, sig_ok = sig_len == 64;
+  if (key_ok) std::memcpy(kbuf, pk, 32);
+  if (sig_ok) std::memcpy(sbuf, sig, 64);
+  if (!key_ok && b->bad_key < 0) b->bad_key = (int64_t)idx;
+  b->pk.insert(b->pk.end(), kbuf, kbuf + 32);
+  b->sig.insert(b->sig.end(), sbuf, sbuf + 64);
+  if (msg_len) b->msg.insert(b->msg.end(), msg, msg + msg_len);
+  b->off.push_back((uint32_t)b->msg.size());
+  b->forced_invalid.push_back(!(key_ok && sig_ok));
+  return CMTV_OK;
+}
+
+size_t cmtv_batch_len(const cmtv_batch* b) { return b ? b->off.size() - 1 : 0; }
+
+void cmtv_batch_reset(cmtv_batch* b) {
+  if (!b) return;
+  b->pk.clear();
+  b->sig.clear();
+  b->msg.clear();
+  b->off.assign(1, 0);
+  b->forced_invalid.clear();
+  b->bad_key = -1;
+}
+
+void cmtv_batch_free(cmtv_batch* b) { delete b; }
+
+int cmtv_batch_verify(cmtv_batch* b, uint8_t* out_valid, int* all_ok, int64_t* bad_key_index) {
+  if (!b || !all_ok) return CMTV_EINVAL;
+  const size_t n = cmtv_batch_len(b);
+  if (bad_key_index) *bad_key_index = b->bad_key;
+  *all_ok = 0;  // an empty batch verifies nothing
+  if (n == 0) return CMTV_OK;
+  if (!out_valid) return CMTV_EINVAL;
+  std::unique_lock<std::mutex> lk;
+  int rc = cmtv::ctx_lock(b->ctx, lk);
+  if (rc != CMTV_OK) return rc;
+  rc = cmtv::verify_host_locked(b->ctx, n, b->pk.data(), b->sig.data(), b->msg.data(), b->off.data(), b->mode,
+                                out_valid, nullptr);
+  if (rc != CMTV_OK) return rc;
+  int ok = 1;
+  for (size_t i = 0; i < n; i++) {
+    if (b->forced_invalid[i]) out_valid[i] = 0;
+    ok &= out_valid[i] != 0;
+  }
+  *all_ok = ok;
+  return CMTV_OK;
+}
+
+// ------------------------------------------------------------------ VerifyCommit*
+
+int cmtv_verify_commit(cmtv_ctx* ctx, uint32_t kind, uint32_t mode, const char* chain_id, size_t chain_id_len,
+                       const cmtv_valset* vals, const cmtv_block_id* block_id, int64_t height,
+                       const cmtv_commit* commit, uint64_t trust_num, uint64_t trust_den, cmtv_commit_result* res,
+                       char* msg_buf, size_t msg_cap) {
+  if (!ctx || !vals || !commit || !res || kind > CMTV_VERIFY_COMMIT_LIGHT_TRUSTING || mode > CMTV_MODE_ZIP215)
+    return CMTV_EINVAL;
+  if ((!chain_id && chain_id_len) || (vals->n_vals && (!vals->pubkeys || !vals->pk_off || !vals->voting_power)))
+    return CMTV_EINVAL;
+  const uint32_t nsig = commit->n_sigs;
+  if (nsig && (!commit->flags || !commit->ts_seconds || !commit->ts_nanos || !commit->sigs || !commit->sig_off))
+    return CMTV_EINVAL;
+  if (kind == CMTV_VERIFY_COMMIT_LIGHT_TRUSTING && nsig && (!commit->val_addrs || (vals->n_vals && !vals->addrs)))
+    return CMTV_EINVAL;
+  if (kind != CMTV_VERIFY_COMMIT_LIGHT_TRUSTING && !block_id) return CMTV_EINVAL;
+  std::memset(res, 0, sizeof(*res));
+  res->sig_index = -1;
+  set_msg(msg_buf, msg_cap, "");
+
+  auto fail = [&](int32_t code, int32_t idx, const std::string& m) {
+    res->code = code;
+    res->sig_index = idx;
+    set_msg(msg_buf, msg_cap, m);
+    return CMTV_ECOMMIT;
+  };
+
+  int64_t total = 0;
+  for (uint32_t i = 0; i < vals->n_vals; i++) total += vals->voting_power[i];
+
+  // --- preamble checks and the threshold (validator_set.go:670-684, 779-790)
+  int64_t needed = 0;
+  std::unordered_map<std::string, uint32_t> by_addr;
+  if (kind == CMTV_VERIFY_COMMIT_LIGHT_TRUSTING) {
+    if (trust_den == 0) return fail(CMTV_COMMIT_ERR_TRUST_LEVEL, -1, "trustLevel has zero Denominator");
+    __int128 prod = (__int128)total * (__int128)(int64_t)trust_num;
+    if (prod > INT64_MAX || prod < INT64_MIN)
+      return fail(CMTV_COMMIT_ERR_TRUST_LEVEL, -1,
+                  "int64 overflow while calculating voting power needed. please provide smaller trustLevel numerator");
+    needed = (int64_t)prod / (int64_t)trust_den;
+    for (uint32_t i = 0; i < vals->n_vals; i++)
+      by_addr.emplace(std::string(reinterpret_cast<const char*>(vals->addrs + 20 * (size_t)i), 20), i);
+  } else {
+    if (vals->n_vals != nsig) {
+      char b[128];
+      std::snprintf(b, sizeof b, "Invalid commit -- wrong set size: %u vs %u", vals->n_vals, nsig);
+      return fail(CMTV_COMMIT_ERR_SET_SIZE, -1, b);
+    }
+    if (height != commit->height) {
+      char b[128];
+      std::snprintf(b, sizeof b, "Invalid commit -- wrong height: %" PRId64 " vs %" PRId64, height, commit->height);
+      return fail(CMTV_COMMIT_ERR_HEIGHT, -1, b);
+    }
+    if (!block_id_equals(block_id, &commit->block_id))
+      return fail(CMTV_COMMIT_ERR_BLOCK_ID, -1,
+                  "invalid commit -- wrong block ID: want " + block_id_string(block_id) + ", got " +
+                      block_id_string(&commit->block_id));
+    needed = total * 2 / 3;
+  }
+
+  // --- plan: which signatures the reference loop can reach, assuming every
+  // verdict is valid; the loop stops at the first error, so nothing beyond the
+  // planned set is ever examined.
+  std::vector<uint32_t> plan_idx, plan_val;
+  {
+    int64_t tally = 0;
+    std::unordered_map<uint32_t, uint32_t> seen;
+    for (uint32_t idx = 0; idx < nsig; idx++) {
+      const uint8_t flag = commit->flags[idx];
+      uint32_t vi = idx;
+      if (kind == CMTV_VERIFY_COMMIT) {
+        if (flag == kFlagAbsent) continue;
+        if (flag != kFlagCommit && flag != kFlagNil) break;  // panics here
+      } else {
+        if (flag != kFlagCommit) continue;
+        if (kind == CMTV_VERIFY_COMMIT_LIGHT_TRUSTING) {
+          auto it = by_addr.find(std::string(reinterpret_cast<const char*>(commit->val_addrs + 20 * (size_t)idx), 20));
+          if (it == by_addr.end()) continue;
+          vi = it->second;
+          if (seen.count(vi)) break;  // double vote error here
+          seen.emplace(vi, idx);
+        }
+      }
+      if (vals->pk_off[vi + 1] - vals->pk_off[vi] != 32) break;  // panics here
+      plan_idx.push_back(idx);
+      plan_val.push_back(vi);
+      if (kind != CMTV_VERIFY_COMMIT) {
+        tally += vals->voting_power[vi];
+        if (tally > needed) break;
+      }
+    }
+  }
+
+  // --- one device batch for the planned signatures
+  const size_t m = plan_idx.size();
+  std::vector<uint8_t> pk(32 * m), sg(64 * m, 0), msgs, valid(m, 0);
+  std::vector<uint32_t> off(m + 1, 0);
+  std::vector<uint8_t> sig_len_ok(m, 0);
+  std::string sb;
+  const cmtv_block_id empty{};
+  for (size_t j = 0; j < m; j++) {
+    const uint32_t idx = plan_idx[j], vi = plan_val[j];
+    std::memcpy(&pk[32 * j], vals->pubkeys + vals->pk_off[vi], 32);
+    const uint32_t s0 = commit->sig_off[idx], s1 = commit->sig_off[idx + 1];
+    if (s1 - s0 == 64) {
+      std::memcpy(&sg[64 * j], commit->sigs + s0, 64);
+      sig_len_ok[j] = 1;
+    }
+    // Commit.GetVote(idx) (types/block.go:784): CommitSig.BlockID(commit.BlockID)
+    const cmtv_block_id* vb = commit->flags[idx] == kFlagCommit ? &commit->block_id : &empty;
+    vote_sign_bytes(sb, chain_id, chain_id_len, kPrecommit, commit->height, commit->round, vb,
+                    commit->ts_seconds[idx], commit->ts_nanos[idx]);
+    msgs.insert(msgs.end(), sb.begin(), sb.end());
+    off[j + 1] = (uint32_t)msgs.size();
+  }
+  if (m) {
+    std::unique_lock<std::mutex> lk;
+    int rc = cmtv::ctx_lock(ctx, lk);
+    if (rc != CMTV_OK) return rc;
+    rc = cmtv::verify_host_locked(ctx, m, pk.data(), sg.data(), msgs.data(), off.data(), mode, valid.data(), nullptr);
+    if (rc != CMTV_OK) return rc;
+    for (size_t j = 0; j < m; j++)
+      if (!sig_len_ok[j]) valid[j] = 0;  // crypto/ed25519/ed25519.go:150
+  }
+  res->n_verified = (uint32_t)m;
+
+  // --- replay the reference loop over the verdicts
+  auto wrong_sig = [&](uint32_t idx) {
+    const uint32_t s0 = commit->sig_off[idx], s1 = commit->sig_off[idx + 1];
+    return fail(CMTV_COMMIT_ERR_WRONG_SIGNATURE, (int32_t)idx,
+                "wrong signature (#" + std::to_string(idx) + "): " + hex_upper(commit->sigs + s0, s1 - s0));
+  };
+  auto bad_pk = [&](uint32_t idx, uint32_t vi) {
+    return fail(CMTV_COMMIT_PANIC_BAD_PUBKEY, (int32_t)idx,
+                "ed25519: bad public key length: " + std::to_string(vals->pk_off[vi + 1] - vals->pk_off[vi]));
+  };
+  int64_t tally = 0;
+  size_t j = 0;
+  std::unordered_map<uint32_t, uint32_t> seen;
+  for (uint32_t idx = 0; idx < nsig; idx++) {
+    const uint8_t flag = commit->flags[idx];
+    if (kind == CMTV_VERIFY_COMMIT) {
+      if (flag == kFlagAbsent) continue;
+      if (flag != kFlagCommit && flag != kFlagNil)
+        return fail(CMTV_COMMIT_PANIC_UNKNOWN_FLAG, (int32_t)idx, "Unknown BlockIDFlag: " + std::to_string(flag));
+      if (vals->pk_off[idx + 1] - vals->pk_off[idx] != 32) return bad_pk(idx, idx);
+      if (j >= m || plan_idx[j] != idx || !valid[j]) return wrong_sig(idx);
+      j++;
+      if (flag == kFlagCommit) tally += vals->voting_power[idx];
+    } else {
+      if (flag != kFlagCommit) continue;
+      uint32_t vi = idx;
+      if (kind == CMTV_VERIFY_COMMIT_LIGHT_TRUSTING) {
+        auto it = by_addr.find(std::string(reinterpret_cast<const char*>(commit->val_addrs + 20 * (size_t)idx), 20));
+        if (it == by_addr.end()) continue;
+        vi = it->second;
+        auto sit = seen.find(vi);
+        if (sit != seen.end()) {
+          // Validator.String(): "Validator{%v %v VP:%v A:%v}" (types/validator.go)
+          std::string vs = "Validator{" + hex_upper(vals->addrs + 20 * (size_t)vi, 20) + " PubKeyEd25519{" +
+                           hex_upper(vals->pubkeys + vals->pk_off[vi], vals->pk_off[vi + 1] - vals->pk_off[vi]) +
+                           "} VP:" + std::to_string(vals->voting_power[vi]) + " A:" +
+                           std::to_string(vals->proposer_priority ? vals->proposer_priority[vi] : 0) + "}";
+          return fail(CMTV_COMMIT_ERR_DOUBLE_VOTE, (int32_t)idx,
+                      "double vote from " + vs + " (" + std::to_string(sit->second) + " and " + std::to_string(idx) +
+                          ")");
+        }
+        seen.emplace(vi, idx);
+      }
+      if (vals->pk_off[vi + 1] - vals->pk_off[vi] != 32) return bad_pk(idx, vi);
+      if (j >= m || plan_idx[j] != idx || !valid[j]) return wrong_sig(idx);
+      j++;
+      tally += vals->voting_power[vi];
+      if (tally > needed) return CMTV_OK;
+    }
+  }
+  if (kind == CMTV_VERIFY_COMMIT && tally > needed) return CMTV_OK;
+  res->got = tally;
+  res->needed = needed;
+  char b[160];
+  std::snprintf(b, sizeof b, "invalid commit -- insufficient voting power: got %" PRId64 ", needed more than %" PRId64,
+                tally, needed);
+  return fail(CMTV_COMMIT_ERR_NOT_ENOUGH_POWER, -1, b);
+}
+
+}  // extern "C"

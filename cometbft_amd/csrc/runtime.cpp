@@ -1,0 +1,348 @@
+// runtime.cpp -- libcmtverify host runtime: contexts, streams, pinned staging,
+// chunked kernel launches and the C ABI of include/cmtverify.h.
+//
+// One context = one device + one HIP stream + the device-resident fixed-base
+// table + growable device/pinned buffers. Calls on a context are serialised
+// by its mutex and start with hipSetDevice (cgo callers migrate threads).
+// There is no CPU verification path: if the device is unusable every call
+// fails with a negative code and the caller decides what to do.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "../../include/cmtverify.h"
+#include "kernels.h"
+#include "runtime_internal.h"
+
+namespace {
+
+constexpr uint32_t kChunk = 1u << 18;  // signatures per launch (A-table scratch = kChunk * 1280 B)
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(bytes, 4096);
+    want = want + want / 4;
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+struct HostBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(bytes, 4096);
+    want = want + want / 4;
+    hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+}  // namespace
+
+struct cmtv_ctx {
+  int device = 0;
+  uint32_t default_mode = CMTV_MODE_GO_STDLIB;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool timing_pending = false;
+  uint32_t* d_btab = nullptr;
+  DevBuf d_atab, d_in, d_out;
+  HostBuf h_in, h_out;
+  std::mutex mu;
+  cmtv_stats stats{};
+};
+
+namespace cmtv {
+
+static int hip_fail(hipError_t e) {
+  if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) return CMTV_ENOMEM;
+  return CMTV_EHIP;
+}
+
+static void harvest_timing(cmtv_ctx* ctx) {
+  if (!ctx->timing_pending) return;
+  if (hipEventSynchronize(ctx->ev1) == hipSuccess) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1) == hipSuccess) {
+      ctx->stats.last_kernel_ms = ms;
+      ctx->stats.device_ms += ms;
+    }
+  }
+  ctx->timing_pending = false;
+}
+
+// Enqueue verification of n signatures whose inputs are in device memory.
+static int enqueue_verify(cmtv_ctx* ctx, size_t n, const uint8_t* d_pk, const uint8_t* d_sig, const uint8_t* d_msg,
+                          const uint32_t* d_off, uint32_t mode, uint8_t* d_valid, uint64_t* d_bitmap,
+                          hipStream_t s) {
+  if (n == 0) return CMTV_OK;
+  const size_t lanes = std::min<size_t>(n, kChunk);
+  const size_t lanes_padded = (lanes + 63) / 64 * 64;
+  hipError_t e = ctx->d_atab.ensure(lanes_padded * kAtabWordsPerLane * sizeof(uint32_t));
+  if (e != hipSuccess) return hip_fail(e);
+  harvest_timing(ctx);
+  if ((e = hipEventRecord(ctx->ev0, s)) != hipSuccess) return hip_fail(e);
+  for (size_t c = 0; c < n; c += kChunk) {
+    const uint32_t cn = (uint32_t)std::min<size_t>(kChunk, n - c);
+    e = launch_verify(mode, cn, d_pk + 32 * c, d_sig + 64 * c, d_msg, d_off + c, ctx->d_btab,
+                      static_cast<uint32_t*>(ctx->d_atab.p), d_valid ? d_valid + c : nullptr,
+                      d_bitmap ? d_bitmap + c / 64 : nullptr, s);
+    if (e != hipSuccess) return hip_fail(e);
+    ctx->stats.kernel_launches++;
+  }
+  if ((e = hipEventRecord(ctx->ev1, s)) != hipSuccess) return hip_fail(e);
+  ctx->timing_pending = true;
+  ctx->stats.calls++;
+  ctx->stats.signatures += n;
+  return CMTV_OK;
+}
+
+static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+int verify_host_locked(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
+                       const uint32_t* msg_off, uint32_t mode, uint8_t* out_valid, uint64_t* out_bitmap) {
+  if (n == 0) return CMTV_OK;
+  const size_t msg_bytes = msg_off[n];
+  // staging layout: [pk n*32][sig n*64][off (n+1)*4][msg msg_bytes + 16]
+  const size_t o_pk = 0, o_sig = align_up(o_pk + 32 * n, 256), o_off = align_up(o_sig + 64 * n, 256);
+  const size_t o_msg = align_up(o_off + 4 * (n + 1), 256), in_bytes = align_up(o_msg + msg_bytes + 16, 256);
+  const size_t words = (n + 63) / 64;
+  const size_t o_bm = 0, o_valid = align_up(8 * words, 256), out_bytes = align_up(o_valid + n, 256);
+  hipError_t e;
+  if ((e = ctx->h_in.ensure(in_bytes)) != hipSuccess) return hip_fail(e);
+  if ((e = ctx->d_in.ensure(in_bytes)) != hipSuccess) return hip_fail(e);
+  if ((e = ctx->h_out.ensure(out_bytes)) != hipSuccess) return hip_fail(e);
+  if ((e = ctx->d_out.ensure(out_bytes)) != hipSuccess) return hip_fail(e);
+  auto* hin = static_cast<uint8_t*>(ctx->h_in.p);
+  std::memcpy(hin + o_pk, pk, 32 * n);
+  std::memcpy(hin + o_sig, sig, 64 * n);
+  std::memcpy(hin + o_off, msg_off, 4 * (n + 1));
+  if (msg_bytes) std::memcpy(hin + o_msg, msg, msg_bytes);
+  std::memset(hin + o_msg + msg_bytes, 0, 16);
+  auto* din = static_cast<uint8_t*>(ctx->d_in.p);
+  auto* dout = static_cast<uint8_t*>(ctx->d_out.p);
+  if ((e = hipMemcpyAsync(din, hin, in_bytes, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess) return hip_fail(e);
+  int rc = enqueue_verify(ctx, n, din + o_pk, din + o_sig, din + o_msg, reinterpret_cast<uint32_t*>(din + o_off), mode,
+                          dout + o_valid, reinterpret_cast<uint64_t*>(dout + o_bm), ctx->stream);
+  if (rc != CMTV_OK) return rc;
+  auto* hout = static_cast<uint8_t*>(ctx->h_out.p);
+  if ((e = hipMemcpyAsync(hout, dout, out_bytes, hipMemcpyDeviceToHost, ctx->stream)) != hipSuccess) return hip_fail(e);
+  if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return hip_fail(e);
+  harvest_timing(ctx);
+  uint64_t invalid = 0;
+  const uint8_t* hv = hout + o_valid;
+  for (size_t i = 0; i < n; i++) invalid += hv[i] == 0;
+  ctx->stats.invalid += invalid;
+  if (out_valid) std::memcpy(out_valid, hv, n);
+  if (out_bitmap) std::memcpy(out_bitmap, hout + o_bm, 8 * words);
+  return CMTV_OK;
+}
+
+int ctx_lock(cmtv_ctx* ctx, std::unique_lock<std::mutex>& lk) {
+  lk = std::unique_lock<std::mutex>(ctx->mu);
+  return hipSetDevice(ctx->device) == hipSuccess ? CMTV_OK : CMTV_ENODEV;
+}
+
+uint32_t ctx_default_mode(const cmtv_ctx* ctx) { return ctx->default_mode; }
+
+}  // namespace cmtv
+
+using namespace cmtv;
+
+extern "C" {
+
+int cmtv_abi_version(void) { return CMTV_ABI_VERSION; }
+
+const char* cmtv_strerror(int code) {
+  switch (code) {
+    case CMTV_OK: return "ok";
+    case CMTV_EINVAL: return "invalid argument";
+    case CMTV_ENODEV: return "no usable gfx950 device";
+    case CMTV_ENOMEM: return "out of device or pinned host memory";
+    case CMTV_EHIP: return "HIP runtime error";
+    case CMTV_ERCCL: return "collective communication error";
+    case CMTV_ECOMMIT: return "commit verification failed";
+    default: return "unknown error";
+  }
+}
+
+int cmtv_open(const cmtv_config* cfg, cmtv_ctx** out) {
+  if (!out) return CMTV_EINVAL;
+  *out = nullptr;
+  if (cfg && (cfg->flags != 0 || cfg->default_mode > CMTV_MODE_ZIP215)) return CMTV_EINVAL;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return CMTV_ENODEV;
+  int dev = 0;
+  if (cfg && cfg->device >= 0) {
+    dev = cfg->device;
+  } else if (hipGetDevice(&dev) != hipSuccess) {
+    dev = 0;
+  }
+  if (dev >= ndev) return CMTV_ENODEV;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return CMTV_ENODEV;
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return CMTV_ENODEV;
+  if (hipSetDevice(dev) != hipSuccess) return CMTV_ENODEV;
+  auto* ctx = new (std::nothrow) cmtv_ctx();
+  if (!ctx) return CMTV_ENOMEM;
+  ctx->device = dev;
+  ctx->default_mode = cfg ? cfg->default_mode : CMTV_MODE_GO_STDLIB;
+  hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreate(&ctx->ev0);
+  if (e == hipSuccess) e = hipEventCreate(&ctx->ev1);
+  if (e == hipSuccess) e = hipMalloc(&ctx->d_btab, kBtabWords * sizeof(uint32_t));
+  if (e == hipSuccess) e = launch_btab_init(ctx->d_btab, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (e != hipSuccess) {
+    cmtv_close(ctx);
+    return hip_fail(e);
+  }
+  *out = ctx;
+  return CMTV_OK;
+}
+
+void cmtv_close(cmtv_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  ctx->d_atab.release();
+  ctx->d_in.release();
+  ctx->d_out.release();
+  ctx->h_in.release();
+  ctx->h_out.release();
+  if (ctx->d_btab) (void)hipFree(ctx->d_btab);
+  if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+  if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+void* cmtv_stream(cmtv_ctx* ctx) { return ctx ? static_cast<void*>(ctx->stream) : nullptr; }
+
+int cmtv_stats_get(cmtv_ctx* ctx, cmtv_stats* out) {
+  if (!ctx || !out) return CMTV_EINVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  (void)hipSetDevice(ctx->device);
+  harvest_timing(ctx);
+  *out = ctx->stats;
+  return CMTV_OK;
+}
+
+int cmtv_verify_ed25519(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
+                        const uint32_t* msg_off, uint32_t mode, uint8_t* out_valid, uint64_t* out_bitmap) {
+  if (!ctx || mode > CMTV_MODE_ZIP215 || n > (1ull << 31)) return CMTV_EINVAL;
+  if (n == 0) return CMTV_OK;
+  if (!pk || !sig || !msg_off || (!msg && msg_off[n] != 0) || (!out_valid && !out_bitmap)) return CMTV_EINVAL;
+  for (size_t i = 0; i < n; i++)
+    if (msg_off[i + 1] < msg_off[i]) return CMTV_EINVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  if (hipSetDevice(ctx->device) != hipSuccess) return CMTV_ENODEV;
+  return verify_host_locked(ctx, n, pk, sig, msg, msg_off, mode, out_valid, out_bitmap);
+}
+
+int cmtv_verify_ed25519_device(cmtv_ctx* ctx, size_t n, const void* d_pk, const void* d_sig, const void* d_msg,
+                               const void* d_msg_off, uint32_t mode, void* d_valid, void* d_bitmap, void* stream) {
+  if (!ctx || mode > CMTV_MODE_ZIP215 || n > (1ull << 31)) return CMTV_EINVAL;
+  if (n == 0) return CMTV_OK;
+  if (!d_pk || !d_sig || !d_msg || !d_msg_off || (!d_valid && !d_bitmap)) return CMTV_EINVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  if (hipSetDevice(ctx->device) != hipSuccess) return CMTV_ENODEV;
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  return enqueue_verify(ctx, n, static_cast<const uint8_t*>(d_pk), static_cast<const uint8_t*>(d_sig),
+                        static_cast<const uint8_t*>(d_msg), static_cast<const uint32_t*>(d_msg_off), mode,
+                        static_cast<uint8_t*>(d_valid), static_cast<uint64_t*>(d_bitmap), s);
+}
+
+int cmtv_pubkeys_ed25519(cmtv_ctx* ctx, size_t n, const uint8_t* seeds, uint8_t* out_pk) {
+  if (!ctx || n > (1ull << 31) || (n && (!seeds || !out_pk))) return CMTV_EINVAL;
+  if (n == 0) return CMTV_OK;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  if (hipSetDevice(ctx->device) != hipSuccess) return CMTV_ENODEV;
+  hipError_t e;
+  if ((e = ctx->d_in.ensure(32 * n)) != hipSuccess) return hip_fail(e);
+  if ((e = ctx->d_out.ensure(32 * n)) != hipSuccess) return hip_fail(e);
+  if ((e = hipMemcpyAsync(ctx->d_in.p, seeds, 32 * n, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess)
+    return hip_fail(e);
+  for (size_t c = 0; c < n; c += kChunk) {
+    const uint32_t cn = (uint32_t)std::min<size_t>(kChunk, n - c);
+    if ((e = launch_pubkey(cn, static_cast<uint8_t*>(ctx->d_in.p) + 32 * c, ctx->d_btab,
+                           static_cast<uint8_t*>(ctx->d_out.p) + 32 * c, ctx->stream)) != hipSuccess)
+      return hip_fail(e);
+  }
+  if ((e = hipMemcpyAsync(out_pk, ctx->d_out.p, 32 * n, hipMemcpyDeviceToHost, ctx->stream)) != hipSuccess)
+    return hip_fail(e);
+  if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return hip_fail(e);
+  return CMTV_OK;
+}
+
+int cmtv_sign_ed25519(cmtv_ctx* ctx, size_t n, const uint8_t* seeds, const uint32_t* key_idx, const uint8_t* msg,
+                      const uint32_t* msg_off, uint8_t* out_sig) {
+  if (!ctx || n > (1ull << 31)) return CMTV_EINVAL;
+  if (n == 0) return CMTV_OK;
+  if (!seeds || !msg_off || !out_sig || (!msg && msg_off[n] != 0)) return CMTV_EINVAL;
+  size_t nseeds = n;
+  if (key_idx) {
+    nseeds = 0;
+    for (size_t i = 0; i < n; i++) nseeds = std::max<size_t>(nseeds, (size_t)key_idx[i] + 1);
+  }
+  for (size_t i = 0; i < n; i++)
+    if (msg_off[i + 1] < msg_off[i]) return CMTV_EINVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  if (hipSetDevice(ctx->device) != hipSuccess) return CMTV_ENODEV;
+  const size_t msg_bytes = msg_off[n];
+  const size_t o_seed = 0, o_idx = align_up(32 * nseeds, 256), o_off = align_up(o_idx + (key_idx ? 4 * n : 0), 256);
+  const size_t o_msg = align_up(o_off + 4 * (n + 1), 256), in_bytes = align_up(o_msg + msg_bytes + 16, 256);
+  hipError_t e;
+  if ((e = ctx->h_in.ensure(in_bytes)) != hipSuccess) return hip_fail(e);
+  if ((e = ctx->d_in.ensure(in_bytes)) != hipSuccess) return hip_fail(e);
+  if ((e = ctx->d_out.ensure(64 * n)) != hipSuccess) return hip_fail(e);
+  auto* hin = static_cast<uint8_t*>(ctx->h_in.p);
+  std::memcpy(hin + o_seed, seeds, 32 * nseeds);
+  if (key_idx) std::memcpy(hin + o_idx, key_idx, 4 * n);
+  std::memcpy(hin + o_off, msg_off, 4 * (n + 1));
+  if (msg_bytes) std::memcpy(hin + o_msg, msg, msg_bytes);
+  auto* din = static_cast<uint8_t*>(ctx->d_in.p);
+  if ((e = hipMemcpyAsync(din, hin, in_bytes, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess) return hip_fail(e);
+  for (size_t c = 0; c < n; c += kChunk) {
+    const uint32_t cn = (uint32_t)std::min<size_t>(kChunk, n - c);
+    if ((e = launch_sign(cn, key_idx ? din + o_seed : din + o_seed + 32 * c, key_idx ? din + o_idx + 4 * c : nullptr,
+                         din + o_msg,
+                         din + o_off + 4 * c, ctx->d_btab, static_cast<uint8_t*>(ctx->d_out.p) + 64 * c,
+                         ctx->stream)) != hipSuccess)
+      return hip_fail(e);
+  }
+  if ((e = hipMemcpyAsync(out_sig, ctx->d_out.p, 64 * n, hipMemcpyDeviceToHost, ctx->stream)) != hipSuccess)
+    return hip_fail(e);
+  if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return hip_fail(e);
+  return CMTV_OK;
+}
+
+}  // extern "C"

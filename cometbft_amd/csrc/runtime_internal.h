@@ -1,0 +1,19 @@
+// runtime_internal.h -- functions shared between runtime.cpp and the host-side
+// commit / batch layers (commit.cpp). Not part of the C ABI.
+#pragma once
+#include <stdint.h>
+#include <stddef.h>
+#include <mutex>
+
+struct cmtv_ctx;
+
+namespace cmtv {
+
+// Locks the context and makes its device current on this thread.
+int ctx_lock(cmtv_ctx* ctx, std::unique_lock<std::mutex>& lk);
+uint32_t ctx_default_mode(const cmtv_ctx* ctx);
+// Host buffers in, verdicts out; caller holds the context lock.
+int verify_host_locked(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
+                       const uint32_t* msg_off, uint32_t mode, uint8_t* out_valid, uint64_t* out_bitmap);
+
+}  // namespace cmtv

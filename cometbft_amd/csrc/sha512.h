@@ -1,0 +1,133 @@
+// sha512.h -- per-lane SHA-512 over (prefix || message) for gfx950.
+//
+// The Ed25519 challenge k = SHA-512(R || A || M) (Go crypto/ed25519 Verify,
+// reference call site /root/reference/crypto/ed25519/ed25519.go:154) and the
+// RFC 8032 signing hashes all have the shape "32- or 64-byte prefix held in
+// registers, then a message in global memory". The padded stream is produced
+// on the fly, 64-bit word by 64-bit word; 64-bit rotates lower to
+// v_alignbit_b32 pairs. Two 128-byte compressions cover a commit vote
+// (64 + 109..161 bytes).
+#pragma once
+#include <stdint.h>
+
+#ifndef CMTV_HD
+#define CMTV_HD __host__ __device__ __forceinline__
+#endif
+
+namespace cmtv {
+
+CMTV_HD uint64_t sha512_k(int i) {
+  constexpr uint64_t K[80] = {
+      0x428a2f98d728ae22ULL, 0x7137449123ef65cdULL, 0xb5c0fbcfec4d3b2fULL, 0xe9b5dba58189dbbcULL,
+      0x3956c25bf348b538ULL, 0x59f111f1b605d019ULL, 0x923f82a4af194f9bULL, 0xab1c5ed5da6d8118ULL,
+      0xd807aa98a3030242ULL, 0x12835b0145706fbeULL, 0x243185be4ee4b28cULL, 0x550c7dc3d5ffb4e2ULL,
+      0x72be5d74f27b896fULL, 0x80deb1fe3b1696b1ULL, 0x9bdc06a725c71235ULL, 0xc19bf174cf692694ULL,
+      0xe49b69c19ef14ad2ULL, 0xefbe4786384f25e3ULL, 0x0fc19dc68b8cd5b5ULL, 0x240ca1cc77ac9c65ULL,
+      0x2de92c6f592b0275ULL, 0x4a7484aa6ea6e483ULL, 0x5cb0a9dcbd41fbd4ULL, 0x76f988da831153b5ULL,
+      0x983e5152ee66dfabULL, 0xa831c66d2db43210ULL, 0xb00327c898fb213fULL, 0xbf597fc7beef0ee4ULL,
+      0xc6e00bf33da88fc2ULL, 0xd5a79147930aa725ULL, 0x06ca6351e003826fULL, 0x142929670a0e6e70ULL,
+      0x27b70a8546d22ffcULL, 0x2e1b21385c26c926ULL, 0x4d2c6dfc5ac42aedULL, 0x53380d139d95b3dfULL,
+      0x650a73548baf63deULL, 0x766a0abb3c77b2a8ULL, 0x81c2c92e47edaee6ULL, 0x92722c851482353bULL,
+      0xa2bfe8a14cf10364ULL, 0xa81a664bbc423001ULL, 0xc24b8b70d0f89791ULL, 0xc76c51a30654be30ULL,
+      0xd192e819d6ef5218ULL, 0xd69906245565a910ULL, 0xf40e35855771202aULL, 0x106aa07032bbd1b8ULL,
+      0x19a4c116b8d2d0c8ULL, 0x1e376c085141ab53ULL, 0x2748774cdf8eeb99ULL, 0x34b0bcb5e19b48a8ULL,
+      0x391c0cb3c5c95a63ULL, 0x4ed8aa4ae3418acbULL, 0x5b9cca4f7763e373ULL, 0x682e6ff3d6b2b8a3ULL,
+      0x748f82ee5defb2fcULL, 0x78a5636f43172f60ULL, 0x84c87814a1f0ab72ULL, 0x8cc702081a6439ecULL,
+      0x90befffa23631e28ULL, 0xa4506cebde82bde9ULL, 0xbef9a3f7b2c67915ULL, 0xc67178f2e372532bULL,
+      0xca273eceea26619cULL, 0xd186b8c721c0c207ULL, 0xeada7dd6cde0eb1eULL, 0xf57d4f7fee6ed178ULL,
+      0x06f067aa72176fbaULL, 0x0a637dc5a2c898a6ULL, 0x113f9804bef90daeULL, 0x1b710b35131c471bULL,
+      0x28db77f523047d84ULL, 0x32caab7b40c72493ULL, 0x3c9ebe0a15c9bebcULL, 0x431d67c49c100d4cULL,
+      0x4cc5d4becb3e42b6ULL, 0x597f299cfc657e2aULL, 0x5fcb6fab3ad6faecULL, 0x6c44198c4a475817ULL};
+  return K[i];
+}
+
+CMTV_HD uint64_t rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+
+CMTV_HD void sha512_compress(uint64_t st[8], uint64_t w[16]) {
+  uint64_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+#pragma unroll
+  for (int i = 0; i < 80; i++) {
+    uint64_t wi;
+    if (i < 16) {
+      wi = w[i & 15];
+    } else {
+      const uint64_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
+      const uint64_t s0 = rotr64(w15, 1) ^ rotr64(w15, 8) ^ (w15 >> 7);
+      const uint64_t s1 = rotr64(w2, 19) ^ rotr64(w2, 61) ^ (w2 >> 6);
+      wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
+      w[i & 15] = wi;
+    }
+    const uint64_t S1 = rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41);
+    const uint64_t ch = (e & f) ^ (~e & g);
+    const uint64_t t1 = h + S1 + ch + sha512_k(i) + wi;
+    const uint64_t S0 = rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39);
+    const uint64_t maj = (a & b) ^ (a & c) ^ (b & c);
+    h = g;
+    g = f;
+    f = e;
+    e = d + t1;
+    d = c;
+    c = b;
+    b = a;
+    a = t1 + S0 + maj;
+  }
+  st[0] += a; st[1] += b; st[2] += c; st[3] += d;
+  st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+
+// SHA-512(prefix[0 .. 4*PW) || msg[0 .. mlen)); prefix as little-endian byte
+// words. Output: 64 digest bytes as 16 little-endian 32-bit words.
+template <int PW>
+CMTV_HD void sha512_prefixed(uint32_t out[16], const uint32_t pre[PW], const uint8_t* msg, uint32_t mlen) {
+  constexpr uint32_t PB = 4 * PW;
+  uint64_t st[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL,
+                    0xa54ff53a5f1d36f1ULL, 0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL,
+                    0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
+  const uint32_t total = PB + mlen;
+  const uint32_t nblocks = (total + 17 + 127) / 128;
+  const uint64_t bitlen = (uint64_t)total * 8;
+  const uint32_t lenpos = nblocks * 128 - 8;  // the 64-bit big-endian bit length
+  auto tail_byte = [&](uint32_t pos) -> uint32_t {
+    if (pos < total) return msg[pos - PB];
+    if (pos == total) return 0x80;
+    if (pos >= lenpos) return (uint32_t)(bitlen >> (8 * (7 - (pos - lenpos)))) & 0xff;
+    return 0;
+  };
+  // block 0 holds the whole register prefix (PB <= 64), so prefix indexing is static
+  {
+    uint64_t w[16];
+#pragma unroll
+    for (int t = 0; t < 16; t++) {
+      uint64_t word = 0;
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        const uint32_t pos = 8 * t + j;
+        const uint32_t byte = (pos < PB) ? ((pre[pos >> 2] >> (8 * (pos & 3))) & 0xff) : tail_byte(pos);
+        word = (word << 8) | byte;
+      }
+      w[t] = word;
+    }
+    sha512_compress(st, w);
+  }
+  for (uint32_t b = 1; b < nblocks; b++) {
+    uint64_t w[16];
+#pragma unroll
+    for (int t = 0; t < 16; t++) {
+      uint64_t word = 0;
+#pragma unroll
+      for (int j = 0; j < 8; j++) word = (word << 8) | tail_byte(b * 128 + 8 * t + j);
+      w[t] = word;
+    }
+    sha512_compress(st, w);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    // digest bytes are big-endian per 64-bit state word
+    const uint64_t v = st[i];
+    const uint32_t hi = (uint32_t)(v >> 32), lo = (uint32_t)v;
+    out[2 * i] = __builtin_bswap32(hi);
+    out[2 * i + 1] = __builtin_bswap32(lo);
+  }
+}
+
+}  // namespace cmtv

@@ -1,0 +1,291 @@
+// verify_core.h -- per-signature Ed25519 verification pipeline (one signature
+// per lane), shared by the gfx950 kernels in verify.hip.
+//
+// Restates Go 1.19 crypto/ed25519.Verify as reached from
+// /root/reference/crypto/ed25519/ed25519.go:148-155 (MODE_GO_STDLIB) and the
+// ZIP-215 cofactored check (MODE_ZIP215):
+//
+//   sig[63] & 0xE0 == 0,  s < L,  A = decode(pk) (non-canonical accepted)
+//   k  = SHA-512(R || A || M) mod L
+//   R' = [s]B - [k]A      (Straus, shared doublings, fixed windows)
+//   GO_STDLIB: encode(R') == R bytes      ZIP215: [8](R' - decode(R)) == O
+//
+// Scalar multiplication layout (SIMD-uniform schedule):
+//   * [k](-A): signed radix-16 digits in [-8, 7], per-lane table of
+//     (1..8)(-A) in cached form, 64 additions;
+//   * [s]B:   signed radix-256 digits in [-128, 127], shared table of
+//     (1..128)B in affine niels form, 32 mixed additions;
+//   * 256 doublings shared by both.
+// Every lane of a wave executes exactly the same instruction stream (no wNAF,
+// no data-dependent branches); the digit only selects table rows.
+#pragma once
+#include "fe25519.h"
+#include "ge25519.h"
+#include "sc25519.h"
+#include "sha512.h"
+
+namespace cmtv {
+
+enum : uint32_t { MODE_GO_STDLIB = 0, MODE_ZIP215 = 1 };
+
+// B-table row layout: 32 words per entry (ypx[10], ymx[10], xy2d[10], pad[2]).
+constexpr int BTAB_ROW_WORDS = 32;
+constexpr int BTAB_ENTRIES = 128;
+// A-table: 8 cached points x 40 words per lane.
+constexpr int ATAB_WORDS = 8 * 40;
+
+// canonical encoding words of the base point (y = 4/5, x even)
+CMTV_HD void basepoint_words(uint32_t w[8]) {
+  w[0] = 0x66666658u;
+#pragma unroll
+  for (int i = 1; i < 8; i++) w[i] = 0x66666666u;
+}
+
+CMTV_HD void cached_neg_point(ge_p3& r, const ge_p3& p) {
+  fe_neg(r.X, p.X);
+  fe_carry(r.X);
+  r.Y = p.Y;
+  r.Z = p.Z;
+  fe_neg(r.T, p.T);
+  fe_carry(r.T);
+}
+
+// [m]B for m = 1..128 in affine niels form (one entry; used by the table
+// initialisation kernel and by host-side tests)
+CMTV_HD void btab_entry(uint32_t row[BTAB_ROW_WORDS], int m) {
+  uint32_t bw[8];
+  basepoint_words(bw);
+  ge_p3 B, acc;
+  p3_frombytes(B, bw);
+  ge_cached Bc;
+  p3_to_cached(Bc, B);
+  p3_identity(acc);
+  ge_efgh t;
+  ge_p2 q;
+  for (int bit = 7; bit >= 0; bit--) {
+    p3_to_p2(q, acc);
+    p2_dbl(t, q);
+    efgh_to_p3(acc, t);
+    ge_add_cached(t, acc, Bc, false);
+    ge_p3 added;
+    efgh_to_p3(added, t);
+    const bool take = (m >> bit) & 1;
+    fe_select(acc.X, acc.X, added.X, take);
+    fe_select(acc.Y, acc.Y, added.Y, take);
+    fe_select(acc.Z, acc.Z, added.Z, take);
+    fe_select(acc.T, acc.T, added.T, take);
+  }
+  fe zi, x, y, ypx, ymx, xy, d2;
+  fe_invert(zi, acc.Z);
+  fe_mul(x, acc.X, zi);
+  fe_mul(y, acc.Y, zi);
+  fe_add(ypx, y, x);
+  fe_carry(ypx);
+  fe_sub(ymx, y, x);
+  fe_carry(ymx);
+  fe_mul(xy, x, y);
+  fe_const_d2(d2);
+  fe_mul(xy, xy, d2);
+  for (int i = 0; i < 10; i++) {
+    row[i] = ypx.v[i];
+    row[10 + i] = ymx.v[i];
+    row[20 + i] = xy.v[i];
+  }
+  row[30] = 0;
+  row[31] = 0;
+}
+
+// acc = [s]B + [k]P  where the ATab holds (1..8)P in cached form.
+// ATab: .load(int e, ge_cached&) for e in 0..7 (multiple e+1).
+// BTab: .load(int e, ge_niels&) for e in 0..127 (multiple e+1).
+template <bool WITH_P, class ATab, class BTab>
+CMTV_HD void straus_double_scalarmult(ge_p3& out, const uint32_t k[8], const uint32_t s[8], const ATab& atab,
+                                      const BTab& btab) {
+  uint32_t tk[8], ts[8];
+  sc_bias(tk, k, 0x88888888u);
+  sc_bias(ts, s, 0x80808080u);
+  ge_p2 cur;
+  p2_identity(cur);
+  ge_p3 P;
+  ge_efgh t;
+  for (int j = 0; j < 32; j++) {
+#pragma unroll
+    for (int half = 0; half < 2; half++) {
+      ge_cached ea;
+      int dA = 0;
+      if (WITH_P) {
+        dA = (int)sc_shift_out(tk, 4) - 8;
+        const int ia = dA < 0 ? -dA : dA;
+        atab.load(ia > 0 ? ia - 1 : 0, ea);
+        if (ia == 0) cached_identity(ea);
+      }
+      ge_niels eb;
+      int dB = 0;
+      if (half == 1) {
+        dB = (int)sc_shift_out(ts, 8) - 128;
+        const int ib = dB < 0 ? -dB : dB;
+        btab.load(ib > 0 ? ib - 1 : 0, eb);
+        if (ib == 0) niels_identity(eb);
+      }
+      p2_dbl(t, cur);
+      efgh_to_p2(cur, t);
+      p2_dbl(t, cur);
+      efgh_to_p2(cur, t);
+      p2_dbl(t, cur);
+      efgh_to_p2(cur, t);
+      p2_dbl(t, cur);
+      if (WITH_P) {
+        efgh_to_p3(P, t);
+        ge_add_cached(t, P, ea, dA < 0);
+      }
+      if (half == 1) {
+        efgh_to_p3(P, t);
+        ge_add_niels(t, P, eb, dB < 0);
+      }
+      efgh_to_p2(cur, t);
+    }
+  }
+  efgh_to_p3(out, t);
+}
+
+// Builds (1..8)P in cached form through the ATab's .store(e, cached).
+template <class ATab>
+CMTV_HD void build_cached_table(ATab& atab, const ge_p3& P) {
+  ge_cached Pc, c;
+  p3_to_cached(Pc, P);
+  atab.store(0, Pc);
+  ge_efgh t;
+  ge_p2 q;
+  ge_p3 cur;
+  p3_to_p2(q, P);
+  p2_dbl(t, q);
+  efgh_to_p3(cur, t);
+  p3_to_cached(c, cur);
+  atab.store(1, c);
+  for (int e = 2; e < 8; e++) {
+    ge_add_cached(t, cur, Pc, false);
+    efgh_to_p3(cur, t);
+    p3_to_cached(c, cur);
+    atab.store(e, c);
+  }
+}
+
+// Full single-signature verification. pk/sig as little-endian words.
+template <uint32_t MODE, class ATab, class BTab>
+CMTV_HD bool verify_one(const uint32_t pkw[8], const uint32_t sigw[16], const uint8_t* msg, uint32_t mlen,
+                        ATab& atab, const BTab& btab) {
+  const uint32_t* Rw = sigw;
+  const uint32_t* Sw = sigw + 8;
+  bool ok = (Sw[7] & 0xE0000000u) == 0;  // sig[63] & 224
+  ok = ok && true;
+  const bool s_ok = sc_is_canonical(Sw);
+  ge_p3 A;
+  const bool a_ok = p3_frombytes(A, pkw);
+  ok = ok && s_ok && a_ok;
+
+  uint32_t pre[16], h[16], k[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    pre[i] = Rw[i];
+    pre[8 + i] = pkw[i];
+  }
+  sha512_prefixed<16>(h, pre, msg, mlen);
+  sc_reduce512(k, h);
+
+  ge_p3 nA;
+  cached_neg_point(nA, A);
+  build_cached_table(atab, nA);
+  ge_p3 Rp;
+  straus_double_scalarmult<true>(Rp, k, Sw, atab, btab);
+
+  if (MODE == MODE_GO_STDLIB) {
+    uint32_t enc[8];
+    p3_tobytes(enc, Rp.X, Rp.Y, Rp.Z);
+    uint32_t diff = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) diff |= enc[i] ^ Rw[i];
+    return ok && diff == 0;
+  } else {
+    ge_p3 R;
+    const bool r_ok = p3_frombytes(R, Rw);
+    ge_cached Rc;
+    p3_to_cached(Rc, R);
+    ge_efgh t;
+    ge_add_cached(t, Rp, Rc, true);
+    ge_p2 q;
+    efgh_to_p2(q, t);
+    for (int i = 0; i < 3; i++) {
+      p2_dbl(t, q);
+      efgh_to_p2(q, t);
+    }
+    const bool ident = fe_iszero(q.X) && fe_equal(q.Y, q.Z);
+    return ok && r_ok && ident;
+  }
+}
+
+// RFC 8032 key expansion: h = SHA-512(seed); a = clamp(h[0:32]) mod L, prefix = h[32:64]
+CMTV_HD void expand_seed(uint32_t a_modl[8], uint32_t prefix[8], const uint32_t seed[8]) {
+  uint32_t h[16];
+  sha512_prefixed<8>(h, seed, nullptr, 0);
+  uint32_t a[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) a[i] = (i < 8) ? h[i] : 0;
+  a[0] &= 0xFFFFFFF8u;
+  a[7] &= 0x7FFFFFFFu;
+  a[7] |= 0x40000000u;
+  sc_reduce512(a_modl, a);
+#pragma unroll
+  for (int i = 0; i < 8; i++) prefix[i] = h[8 + i];
+}
+
+struct NullATab {
+  CMTV_HD void load(int, ge_cached&) const {}
+  CMTV_HD void store(int, const ge_cached&) {}
+};
+
+template <class BTab>
+CMTV_HD void scalarmult_base(ge_p3& out, const uint32_t s[8], const BTab& btab) {
+  const uint32_t zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  NullATab na;
+  straus_double_scalarmult<false>(out, zero, s, na, btab);
+}
+
+template <class BTab>
+CMTV_HD void pubkey_from_seed(uint32_t pk[8], const uint32_t seed[8], const BTab& btab) {
+  uint32_t a[8], prefix[8];
+  expand_seed(a, prefix, seed);
+  ge_p3 A;
+  scalarmult_base(A, a, btab);
+  p3_tobytes(pk, A.X, A.Y, A.Z);
+}
+
+template <class BTab>
+CMTV_HD void sign_one(uint32_t sig[16], const uint32_t seed[8], const uint8_t* msg, uint32_t mlen,
+                      const BTab& btab) {
+  uint32_t a[8], prefix[8], pk[8], rh[16], r[8], kh[16], k[8], pre[16];
+  expand_seed(a, prefix, seed);
+  ge_p3 P;
+  scalarmult_base(P, a, btab);
+  p3_tobytes(pk, P.X, P.Y, P.Z);
+  sha512_prefixed<8>(rh, prefix, msg, mlen);
+  sc_reduce512(r, rh);
+  scalarmult_base(P, r, btab);
+  uint32_t Rw[8];
+  p3_tobytes(Rw, P.X, P.Y, P.Z);
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    pre[i] = Rw[i];
+    pre[8 + i] = pk[i];
+  }
+  sha512_prefixed<16>(kh, pre, msg, mlen);
+  sc_reduce512(k, kh);
+  uint32_t s[8];
+  sc_muladd(s, k, a, r);
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    sig[i] = Rw[i];
+    sig[8 + i] = s[i];
+  }
+}
+
+}  // namespace cmtv

@@ -1,0 +1,226 @@
+/*
+ * cmtverify.h -- C ABI of libcmtverify.so, the MI355X (gfx950) batch Ed25519
+ * verifier behind CometBFT's commit-verification path.
+ *
+ * Drop-in boundary. The reference (Tendermint/CometBFT v0.34.28, pure Go,
+ * CGO_ENABLED=0 at /root/reference/Makefile:11) verifies one signature at a
+ * time through the Go interface
+ *     crypto.PubKey.VerifySignature(msg, sig []byte) bool
+ *         /root/reference/crypto/crypto.go:25
+ *         /root/reference/crypto/ed25519/ed25519.go:148-155
+ * called from the tally loops of
+ *     ValidatorSet.VerifyCommit            types/validator_set.go:667-714
+ *     ValidatorSet.VerifyCommitLight       types/validator_set.go:722-765
+ *     ValidatorSet.VerifyCommitLightTrusting types/validator_set.go:775-826
+ * Every entry point below is what a cgo binding for that path binds (see
+ * INTEGRATION.md for the Go side: crypto.BatchVerifier and the rewritten
+ * VerifyCommit* bodies that replay the reference loop over the verdicts).
+ *
+ * Conventions
+ *   - Return 0 on success, a negative CMTV_E* code otherwise; never abort, no
+ *     exceptions cross the ABI. Verdicts are only meaningful on success.
+ *   - Caller-owned host buffers are read during the call only; the library
+ *     copies them into its own pinned staging and keeps no pointer after
+ *     returning (cgo pointer rules).
+ *   - Thread-safe: a context serialises its own calls with a mutex and calls
+ *     hipSetDevice on entry (Go goroutines migrate between OS threads).
+ *   - Messages: one flat byte buffer + (n+1) uint32 offsets; message i is
+ *     msg[msg_off[i] .. msg_off[i+1]).
+ *   - Bitmaps: uint64 words, bit (i % 64) of word (i / 64) = verdict of i.
+ *   - Modes: CMTV_MODE_GO_STDLIB reproduces Go 1.19 crypto/ed25519.Verify (the
+ *     semantics this reference runs); CMTV_MODE_ZIP215 is the cofactored
+ *     ZIP-215 rule of upstream curve25519-voi.
+ */
+#ifndef CMTVERIFY_H
+#define CMTVERIFY_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CMTV_ABI_VERSION 1
+
+enum {
+  CMTV_OK = 0,
+  CMTV_EINVAL = -1,  /* bad argument (null pointer, n too large, bad mode) */
+  CMTV_ENODEV = -2,  /* no usable gfx950 device                           */
+  CMTV_ENOMEM = -3,  /* device or pinned host allocation failed           */
+  CMTV_EHIP = -4,    /* HIP runtime error (launch, copy, sync)            */
+  CMTV_ERCCL = -5,   /* collective failure (multi-device gather)          */
+  CMTV_ECOMMIT = -6  /* commit verification failed: see the message out   */
+};
+
+enum { CMTV_MODE_GO_STDLIB = 0, CMTV_MODE_ZIP215 = 1 };
+
+typedef struct cmtv_ctx cmtv_ctx;
+typedef struct cmtv_batch cmtv_batch;
+
+typedef struct cmtv_config {
+  int32_t device;        /* HIP device ordinal; -1 = current device          */
+  uint32_t default_mode; /* mode used by cmtv_batch_* and cmtv_verify_commit */
+  uint32_t flags;        /* reserved, must be 0                              */
+  uint32_t reserved;
+} cmtv_config;
+
+typedef struct cmtv_stats {
+  uint64_t calls;          /* verify calls                        */
+  uint64_t signatures;     /* signatures verified                 */
+  uint64_t invalid;        /* signatures rejected                 */
+  uint64_t kernel_launches;
+  double device_ms;        /* summed kernel time (HIP events)     */
+  double last_kernel_ms;   /* the most recent verify kernel       */
+} cmtv_stats;
+
+/* ------------------------------------------------------------ lifecycle */
+
+/* Opens a context on one device: creates its stream, uploads the fixed-base
+ * table of (1..128)B (built on the device), allocates pinned staging.
+ * Replaces: nothing in the reference (it has no device state). */
+int cmtv_open(const cmtv_config* cfg, cmtv_ctx** out);
+void cmtv_close(cmtv_ctx* ctx);
+const char* cmtv_strerror(int code);
+int cmtv_abi_version(void);
+int cmtv_stats_get(cmtv_ctx* ctx, cmtv_stats* out);
+/* hipStream_t of the context (as void*), for callers that order their own
+ * work with it (bench, multi-GPU gather). */
+void* cmtv_stream(cmtv_ctx* ctx);
+
+/* ------------------------------------------------------------ verification */
+
+/* Batch verification from host buffers: n signatures, pk n x 32 bytes,
+ * sig n x 64 bytes. out_valid: n bytes (0/1), out_bitmap (optional, may be
+ * NULL): ceil(n/64) words. Each verdict equals
+ *   PubKey(pk_i).VerifySignature(msg_i, sig_i)   crypto/ed25519/ed25519.go:148
+ * for 32-byte keys and 64-byte signatures (callers handle other lengths, see
+ * cmtv_batch_add). Blocking. */
+int cmtv_verify_ed25519(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
+                        const uint32_t* msg_off, uint32_t mode, uint8_t* out_valid, uint64_t* out_bitmap);
+
+/* Same, all buffers already resident in device memory (HBM); enqueued on
+ * `stream` (hipStream_t, NULL = the context stream), non-blocking. d_valid
+ * (n bytes) and d_bitmap (ceil(n/64) words) may each be NULL. */
+int cmtv_verify_ed25519_device(cmtv_ctx* ctx, size_t n, const void* d_pk, const void* d_sig, const void* d_msg,
+                               const void* d_msg_off, uint32_t mode, void* d_valid, void* d_bitmap, void* stream);
+
+/* ------------------------------------------------------------ crypto.BatchVerifier mirror */
+
+/* crypto.BatchVerifier as upstream CometBFT v0.38 defines it (not in this
+ * v0.34 reference; the Go side is in INTEGRATION.md):
+ *   Add(key PubKey, msg, sig []byte) error ;  Verify() (bool, []bool)
+ * cmtv_batch_add never fails on malformed input: a signature whose length is
+ * not 64 is recorded as invalid (ed25519.go:150); a key whose length is not 32
+ * is recorded and reported as invalid with *deferred_panic set by
+ * cmtv_batch_verify, so the Go replay can panic at the same index the
+ * reference's sequential loop would (Go's ed25519.Verify panics on it). */
+int cmtv_batch_new(cmtv_ctx* ctx, uint32_t mode, cmtv_batch** out);
+int cmtv_batch_add(cmtv_batch* b, const uint8_t* pk, size_t pk_len, const uint8_t* msg, size_t msg_len,
+                   const uint8_t* sig, size_t sig_len);
+size_t cmtv_batch_len(const cmtv_batch* b);
+/* out_valid: len bytes; *all_ok = 1 iff every entry is valid; bad_key_index:
+ * first entry whose key length was not 32 (or -1). */
+int cmtv_batch_verify(cmtv_batch* b, uint8_t* out_valid, int* all_ok, int64_t* bad_key_index);
+void cmtv_batch_reset(cmtv_batch* b);
+void cmtv_batch_free(cmtv_batch* b);
+
+/* ------------------------------------------------------------ commit verification */
+
+/* A commit and its validator set in struct-of-arrays form.
+ *   types/block.go:575-600  Commit / CommitSig / BlockIDFlag (Absent=1, Commit=2, Nil=3)
+ *   types/validator_set.go  ValidatorSet (Validators[i].PubKey, .VotingPower, .Address)
+ * Sign-bytes are produced by the library's CanonicalVote encoder
+ * (types/vote.go:93, types/canonical.go:56, canonical.pb.go:517). */
+typedef struct cmtv_block_id {
+  const uint8_t* hash;
+  uint32_t hash_len;
+  uint32_t psh_total;
+  const uint8_t* psh_hash;
+  uint32_t psh_hash_len;
+} cmtv_block_id;
+
+typedef struct cmtv_commit {
+  int64_t height;
+  int32_t round;
+  cmtv_block_id block_id;
+  uint32_t n_sigs;
+  const uint8_t* flags;          /* n_sigs BlockIDFlag bytes              */
+  const int64_t* ts_seconds;     /* n_sigs Unix seconds of CommitSig.Timestamp */
+  const int32_t* ts_nanos;       /* n_sigs nanoseconds                    */
+  const uint8_t* sigs;           /* concatenated signatures               */
+  const uint32_t* sig_off;       /* n_sigs+1 offsets into sigs            */
+  const uint8_t* val_addrs;      /* n_sigs x 20 (ValidatorAddress); may be NULL unless LightTrusting */
+} cmtv_commit;
+
+typedef struct cmtv_valset {
+  uint32_t n_vals;
+  const uint8_t* pubkeys;        /* concatenated public keys              */
+  const uint32_t* pk_off;        /* n_vals+1 offsets into pubkeys         */
+  const int64_t* voting_power;   /* n_vals                                */
+  const uint8_t* addrs;          /* n_vals x 20; required for LightTrusting */
+  const int64_t* proposer_priority; /* n_vals, optional (only printed in the
+                                       double-vote error, Validator.String()) */
+} cmtv_valset;
+
+enum { CMTV_VERIFY_COMMIT = 0, CMTV_VERIFY_COMMIT_LIGHT = 1, CMTV_VERIFY_COMMIT_LIGHT_TRUSTING = 2 };
+
+enum {
+  CMTV_COMMIT_OK = 0,
+  CMTV_COMMIT_ERR_SET_SIZE = 1,        /* ErrInvalidCommitSignatures        */
+  CMTV_COMMIT_ERR_HEIGHT = 2,          /* ErrInvalidCommitHeight            */
+  CMTV_COMMIT_ERR_BLOCK_ID = 3,        /* "invalid commit -- wrong block ID" */
+  CMTV_COMMIT_ERR_WRONG_SIGNATURE = 4, /* "wrong signature (#%d): %X"       */
+  CMTV_COMMIT_ERR_NOT_ENOUGH_POWER = 5,/* ErrNotEnoughVotingPowerSigned     */
+  CMTV_COMMIT_ERR_DOUBLE_VOTE = 6,     /* "double vote from %v (%d and %d)" */
+  CMTV_COMMIT_ERR_TRUST_LEVEL = 7,     /* zero denominator / int64 overflow */
+  CMTV_COMMIT_PANIC_BAD_PUBKEY = 8,    /* the reference panics here (Go ed25519.Verify) */
+  CMTV_COMMIT_PANIC_UNKNOWN_FLAG = 9   /* the reference panics here (CommitSig.BlockID) */
+};
+
+typedef struct cmtv_commit_result {
+  int32_t code;        /* CMTV_COMMIT_*                                      */
+  int32_t sig_index;   /* index the error refers to, or -1                   */
+  int64_t got;         /* ErrNotEnoughVotingPowerSigned.Got                  */
+  int64_t needed;      /* ErrNotEnoughVotingPowerSigned.Needed               */
+  uint32_t n_verified; /* signatures sent to the device                      */
+  uint32_t reserved;
+} cmtv_commit_result;
+
+/* VerifyCommit / VerifyCommitLight / VerifyCommitLightTrusting
+ * (types/validator_set.go:667 / 722 / 775). Verifies every signature the
+ * reference loop could reach in one device batch, then replays the reference
+ * loop in index order over the verdicts, so the first error, the early exits
+ * and the tallies are exactly the reference's. `msg_buf` (may be NULL)
+ * receives the reference's error string (NUL-terminated, truncated to
+ * msg_cap). trust_num/trust_den are only read for LIGHT_TRUSTING (the
+ * validator set need not match the commit; matching is by address).
+ * Returns CMTV_OK when the commit verifies, CMTV_ECOMMIT when the reference
+ * would return an error (details in *res), another negative code on a
+ * library failure. */
+int cmtv_verify_commit(cmtv_ctx* ctx, uint32_t kind, uint32_t mode, const char* chain_id, size_t chain_id_len,
+                       const cmtv_valset* vals, const cmtv_block_id* block_id, int64_t height,
+                       const cmtv_commit* commit, uint64_t trust_num, uint64_t trust_den, cmtv_commit_result* res,
+                       char* msg_buf, size_t msg_cap);
+
+/* CanonicalVote sign-bytes (types/vote.go:93 VoteSignBytes) for a commit
+ * signature: writes up to cap bytes, returns the length (or negative code). */
+int64_t cmtv_vote_sign_bytes(const char* chain_id, size_t chain_id_len, int32_t vote_type, int64_t height,
+                             int32_t round, const cmtv_block_id* block_id, int64_t ts_seconds, int32_t ts_nanos,
+                             uint8_t* out, size_t cap);
+
+/* ------------------------------------------------------------ test-data generation */
+
+/* RFC 8032 key generation and deterministic signing on the device (the
+ * reference's crypto/ed25519 GenPrivKeyFromSecret / PrivKey.Sign,
+ * ed25519.go:122,57), for synthetic validator sets and commits.
+ * key_idx (optional): signature i uses seeds[key_idx[i]]. Blocking. */
+int cmtv_pubkeys_ed25519(cmtv_ctx* ctx, size_t n, const uint8_t* seeds, uint8_t* out_pk);
+int cmtv_sign_ed25519(cmtv_ctx* ctx, size_t n, const uint8_t* seeds, const uint32_t* key_idx, const uint8_t* msg,
+                      const uint32_t* msg_off, uint8_t* out_sig);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CMTVERIFY_H */

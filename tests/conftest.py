@@ -1,0 +1,39 @@
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")
+
+
+@pytest.fixture(scope="session")
+def corpus():
+    with open(os.path.join(ROOT, "tests", "golden", "corpus.json")) as f:
+        doc = json.load(f)
+    vecs = doc["vectors"]
+    pk = np.array([np.frombuffer(bytes.fromhex(v["pk"]), np.uint8) for v in vecs])
+    sig = np.array([np.frombuffer(bytes.fromhex(v["sig"]), np.uint8) for v in vecs])
+    msgs = [bytes.fromhex(v["msg"]) for v in vecs]
+    go = np.array([v["go"] for v in vecs], np.uint8)
+    zip215 = np.array([v["zip215"] for v in vecs], np.uint8)
+    cats = [v["cat"] for v in vecs]
+    return {"pk": pk, "sig": sig, "msgs": msgs, "go": go, "zip215": zip215, "cats": cats}
+
+
+@pytest.fixture(scope="session")
+def gpu_ctx():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from cometbft_amd import Context
+
+    return Context(device=0)

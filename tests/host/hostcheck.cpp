@@ -1,0 +1,84 @@
+// Host-side build of the device math (cometbft_amd/csrc/verify_core.h) with
+// operand-bound assertions on (CMTV_BOUNDS_CHECK). Test infrastructure only:
+// lets the per-lane pipeline be checked against the oracle without a GPU.
+//   input  (stdin):  u32 n, then n x { u8 mode, u8 pk[32], u8 sig[64], u32 mlen, u8 msg[mlen] }
+//   output (stdout): n bytes of verdicts
+//   argv[1] == "sign": n x { u8 seed[32], u32 mlen, msg } -> n x { pk[32], sig[64] }
+#define CMTV_HD inline
+#define CMTV_BOUNDS_CHECK 1
+#include <cstdio>
+#include <cstring>
+#include <vector>
+#include "../../cometbft_amd/csrc/verify_core.h"
+
+using namespace cmtv;
+
+struct HostBTab {
+  std::vector<uint32_t> rows;
+  HostBTab() : rows(BTAB_ENTRIES * BTAB_ROW_WORDS) {
+    for (int m = 1; m <= BTAB_ENTRIES; m++) btab_entry(&rows[(m - 1) * BTAB_ROW_WORDS], m);
+  }
+  void load(int e, ge_niels& r) const {
+    const uint32_t* p = &rows[e * BTAB_ROW_WORDS];
+    for (int i = 0; i < 10; i++) {
+      r.ypx.v[i] = p[i];
+      r.ymx.v[i] = p[10 + i];
+      r.xy2d.v[i] = p[20 + i];
+    }
+  }
+};
+
+struct HostATab {
+  ge_cached t[8];
+  void load(int e, ge_cached& r) const { r = t[e]; }
+  void store(int e, const ge_cached& r) { t[e] = r; }
+};
+
+static void to_words(uint32_t* w, const uint8_t* b, int nw) {
+  for (int i = 0; i < nw; i++) w[i] = b[4 * i] | (b[4 * i + 1] << 8) | (b[4 * i + 2] << 16) | ((uint32_t)b[4 * i + 3] << 24);
+}
+static void from_words(uint8_t* b, const uint32_t* w, int nw) {
+  for (int i = 0; i < nw; i++)
+    for (int j = 0; j < 4; j++) b[4 * i + j] = (uint8_t)(w[i] >> (8 * j));
+}
+
+int main(int argc, char** argv) {
+  HostBTab bt;
+  uint32_t n;
+  if (fread(&n, 4, 1, stdin) != 1) return 1;
+  const bool sign = argc > 1 && !strcmp(argv[1], "sign");
+  for (uint32_t i = 0; i < n; i++) {
+    if (sign) {
+      uint8_t seed[32];
+      uint32_t mlen;
+      if (fread(seed, 32, 1, stdin) != 1 || fread(&mlen, 4, 1, stdin) != 1) return 1;
+      std::vector<uint8_t> msg(mlen + 1);
+      if (mlen && fread(msg.data(), mlen, 1, stdin) != 1) return 1;
+      uint32_t sw[8], pk[8], sig[16];
+      to_words(sw, seed, 8);
+      pubkey_from_seed(pk, sw, bt);
+      sign_one(sig, sw, msg.data(), mlen, bt);
+      uint8_t out[96];
+      from_words(out, pk, 8);
+      from_words(out + 32, sig, 16);
+      fwrite(out, 96, 1, stdout);
+      continue;
+    }
+    uint8_t mode, pk[32], sig[64];
+    uint32_t mlen;
+    if (fread(&mode, 1, 1, stdin) != 1 || fread(pk, 32, 1, stdin) != 1 || fread(sig, 64, 1, stdin) != 1 ||
+        fread(&mlen, 4, 1, stdin) != 1)
+      return 1;
+    std::vector<uint8_t> msg(mlen + 1);
+    if (mlen && fread(msg.data(), mlen, 1, stdin) != 1) return 1;
+    uint32_t pkw[8], sigw[16];
+    to_words(pkw, pk, 8);
+    to_words(sigw, sig, 16);
+    HostATab at;
+    bool v = mode ? verify_one<MODE_ZIP215>(pkw, sigw, msg.data(), mlen, at, bt)
+                  : verify_one<MODE_GO_STDLIB>(pkw, sigw, msg.data(), mlen, at, bt);
+    uint8_t o = v;
+    fwrite(&o, 1, 1, stdout);
+  }
+  return 0;
+}

@@ -1,0 +1,109 @@
+"""CPU tests: the oracle is pinned before it is trusted.
+
+ - RFC 8032 section 7.1 test vectors 1-3 (keygen, sign, verify)
+ - libsodium 1.0.18 agreement on honest signatures (when loadable)
+ - sign-bytes known-answer vectors from /root/reference/types/vote_test.go:60-137
+ - the C restatement (oracle/liboracle.so) equals the Python big-int
+   restatement on every corpus vector, both modes
+"""
+import ctypes
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import coracle
+from oracle import ed25519_ref as E
+from oracle import signbytes as SB
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+RFC8032 = [
+    ("9d61b19deffd5a60ba844af492ec2cc44449c5697b326919703bac031cae7f60",
+     "d75a980182b10ab7d54bfed3c964073a0ee172f3daa62325af021a68f707511a", "",
+     "e5564300c360ac729086e2cc806e828a84877f1eb8e5d974d873e065224901555fb8821590a33bacc61e39701cf9b46bd25bf5f0595bbe24655141438e7a100b"),
+    ("4ccd089b28ff96da9db6c346ec114e0f5b8a319f35aba624da8cf6ed4fb8a6fb",
+     "3d4017c3e843895a92b70aa74d1b7ebc9c982ccf2ec4968cc0cd55f12af4660c", "72",
+     "92a009a9f0d4cab8720e820b5f642540a2b27b5416503f8fb3762223ebdb69da085ac1e43e15996e458f3613d0f11d8c387b2eaeb4302aeeb00d291612bb0c00"),
+    ("c5aa8df43f9f837bedb7442f31dcb7b166d38535076f094b85ce3a2e0b4458f7",
+     "fc51cd8e6218a1a38da47ed00230f0580816ed13ba3303ac5deb911548908025", "af82",
+     "6291d657deec24024827e69c3abe01a30ce548a284743a445e3680d7db5ac3ac18ff9b538d16f290ae67f760984dc6594a7c15e9716ed28dc027beceea1ec40a"),
+]
+
+
+@pytest.mark.parametrize("sk,pk,msg,sig", RFC8032)
+def test_rfc8032_vectors(sk, pk, msg, sig):
+    sk, pk, msg, sig = map(bytes.fromhex, (sk, pk, msg, sig))
+    assert E.pubkey_from_seed(sk) == pk
+    assert E.sign(sk, msg) == sig
+    for mode in (E.MODE_GO_STDLIB, E.MODE_ZIP215):
+        assert E.verify(pk, msg, sig, mode)
+        out = coracle.verify_batch(np.frombuffer(pk, np.uint8), np.frombuffer(sig, np.uint8),
+                                   *coracle.pack_msgs([msg]), mode)
+        assert out[0] == 1
+    assert bytes(coracle.pubkeys_from_seeds(np.frombuffer(sk, np.uint8))[0]) == pk
+    assert bytes(coracle.sign_batch(np.frombuffer(sk, np.uint8), *coracle.pack_msgs([msg]))[0]) == sig
+
+
+def _sodium():
+    for p in ("/opt/conda/lib/libsodium.so", "libsodium.so.23"):
+        try:
+            so = ctypes.CDLL(p)
+            so.sodium_init()
+            return so
+        except OSError:
+            continue
+    return None
+
+
+def test_libsodium_agrees_on_honest_signatures():
+    so = _sodium()
+    if so is None:
+        pytest.skip("libsodium not loadable")
+    rng = np.random.default_rng(7)
+    for i in range(40):
+        seed = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
+        msg = rng.integers(0, 256, int(rng.integers(0, 300)), dtype=np.uint8).tobytes()
+        pk = ctypes.create_string_buffer(32)
+        sk = ctypes.create_string_buffer(64)
+        so.crypto_sign_seed_keypair(pk, sk, seed)
+        sig = ctypes.create_string_buffer(64)
+        so.crypto_sign_detached(sig, None, msg, ctypes.c_ulonglong(len(msg)), sk)
+        assert E.pubkey_from_seed(seed) == pk.raw
+        assert E.sign(seed, msg) == sig.raw
+        assert E.verify(pk.raw, msg, sig.raw)
+
+
+def test_signbytes_kat():
+    with open(os.path.join(ROOT, "tests", "golden", "signbytes_kat.json")) as f:
+        kat = json.load(f)
+    for c in kat["cases"]:
+        got = SB.vote_sign_bytes(c["chain_id"], c["type"], c["height"], c["round"], None,
+                                 kat["go_zero_time_seconds"], 0)
+        assert got == bytes.fromhex(c["want"].replace(" ", ""))
+
+
+@pytest.mark.parametrize("mode,key", [(0, "go"), (1, "zip215")])
+def test_c_oracle_matches_python_oracle_on_corpus(corpus, mode, key):
+    m, off = coracle.pack_msgs(corpus["msgs"])
+    out = coracle.verify_batch(corpus["pk"], corpus["sig"], m, off, mode, nthreads=4)
+    assert np.array_equal(out, corpus[key])
+
+
+def test_corpus_verdicts_recomputed_sample(corpus):
+    """Re-derive a sample of stored verdicts with the Python oracle."""
+    idx = list(range(0, len(corpus["msgs"]), 37))
+    for i in idx:
+        pk, sig, m = bytes(corpus["pk"][i]), bytes(corpus["sig"][i]), corpus["msgs"][i]
+        assert int(E.verify(pk, m, sig, E.MODE_GO_STDLIB)) == corpus["go"][i]
+        assert int(E.verify(pk, m, sig, E.MODE_ZIP215)) == corpus["zip215"][i]
+
+
+def test_bad_lengths_follow_go():
+    seed = bytes(range(32))
+    pk, sig = E.pubkey_from_seed(seed), E.sign(seed, b"m")
+    assert not E.verify(pk, b"m", sig[:63])
+    assert not E.verify(pk, b"m", sig + b"\0")
+    with pytest.raises(E.BadPublicKeyLength):
+        E.verify(pk[:31], b"m", sig)

@@ -1,0 +1,272 @@
+"""bench.py -- headline benchmark: Ed25519 commit-signature verification on MI355X.
+
+Metric (BASELINE.json): "Ed25519 verifs/sec at 1/2/4/8 GPUs + p50 VerifyCommit
+latency, 150 vals".
+
+Step = verify one synthetic 10,000-validator commit (BASELINE.json configs[1])
+per GPU: its (pk, sig, sign-bytes) already resident in HBM, the gfx950 verify
+kernel writes the per-signature verdict bytes and the packed verdict bitmap;
+for N > 1 each rank verifies its own commit (weak scaling, no data-path
+collective) and the bitmaps are all-gathered over RCCL so every rank holds the
+job's full verdict vector (the exchange the caller needs).
+
+Extra fields on the JSON line:
+  roofline       -- VALU integer-MAC roofline of the verify kernel: algorithmic
+                    work = 300,000 32x32->64 MACs per verification
+                    per launch / the kernel's mean duration (HIP events on the
+                    launch stream); peak = measured v_mad_u64_u32 rate
+                    (tools/microbench, profiles/r01_int_rates.txt)
+  cpu_baseline   -- oracle/liboracle.so (C restatement of the Go-1.19 verify) on
+                    the host cores, bounded sample, rank 0 only
+  latency_150    -- p50/p99 of cmtv_verify_commit (VerifyCommit, 150 validators:
+                    sign-bytes + H2D + kernel + D2H + reference-loop replay),
+                    beside the oracle's single-core sequential VerifyCommit time
+Run: python bench.py [--gpus N --steps K --warmup W]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Ed25519 verifs/sec at 1/2/4/8 GPUs + p50 VerifyCommit latency, 150 vals"
+MACS_PER_VERIFY = 300_000          # 3,000 field mults x 100 limb MACs
+INT_MAC_PEAK_T = 33.0              # measured v_mad_u64_u32 lane-ops/s, 1e12 (profiles/r01_int_rates.txt)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--n", type=int, default=10_000, help="signatures per GPU per step")
+    ap.add_argument("--mode", choices=["go", "zip215"], default="go")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU-seconds of oracle work for cpu_baseline")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--latency-iters", type=int, default=200)
+    ap.add_argument("--no-latency", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_threads() -> int:
+    for k in ("OMP_NUM_THREADS", "CMTV_CPU_THREADS"):
+        v = os.environ.get(k)
+        if v and v.isdigit() and int(v) > 0:
+            return min(int(v), os.cpu_count() or 1)
+    return min(16, os.cpu_count() or 1)
+
+
+def cpu_baseline(pk, sig, m, off, mode, cpu_seconds):
+    """The oracle (C restatement of Go 1.19 crypto/ed25519.Verify) on the host
+    cores over the same commit, repeated to a bounded amount of CPU work."""
+    from oracle import coracle  # the checker / CPU baseline only
+
+    threads = cpu_threads()
+    n = len(off) - 1
+    t = time.perf_counter()
+    out = coracle.verify_batch(pk, sig, m, off, mode, nthreads=threads)
+    first = time.perf_counter() - t
+    assert out.all(), "oracle rejected an honest synthetic signature"
+    reps = max(1, int(cpu_seconds / max(first * threads, 1e-3)))
+    t = time.perf_counter()
+    for _ in range(reps):
+        coracle.verify_batch(pk, sig, m, off, mode, nthreads=threads)
+    dt = time.perf_counter() - t
+    # single-core figure on a short slice
+    sl = min(n, 400)
+    t = time.perf_counter()
+    coracle.verify_batch(pk[:sl], sig[:sl], m, off[: sl + 1], mode, nthreads=1)
+    one = sl / (time.perf_counter() - t)
+    return {"value": round(reps * n / dt, 1), "unit": "verifs/s", "cores": threads, "kind": "port",
+            "sample": f"{n}-signature synthetic commit x {reps} passes, {threads} threads, oracle/liboracle.so "
+                      f"(C restatement of Go 1.19 ed25519.Verify)",
+            "single_core_verifs_per_s": round(one, 1), "seconds": round(dt, 2),
+            "host_cpu": _cpu_model()}
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def latency_150(ctx, mode, iters):
+    """p50/p99 VerifyCommit latency for a 150-validator commit (host API, end to end)."""
+    from cometbft_amd import testutil as TU
+
+    sv = TU.make_validator_set(ctx, 150)
+    commit, msgs, sigs = TU.make_commit(ctx, sv, height=1000)
+    bid = TU.block_id_for_height(1000)
+    for _ in range(20):
+        sv.valset.verify_commit(TU.CHAIN_ID, bid, 1000, commit, ctx=ctx, mode=mode)
+    ts = []
+    for _ in range(iters):
+        t = time.perf_counter()
+        sv.valset.verify_commit(TU.CHAIN_ID, bid, 1000, commit, ctx=ctx, mode=mode)
+        ts.append(time.perf_counter() - t)
+    ts = np.array(ts) * 1e3
+    res = {"n_validators": 150, "iters": iters, "p50_ms": round(float(np.percentile(ts, 50)), 4),
+           "p99_ms": round(float(np.percentile(ts, 99)), 4),
+           "path": "cmtv_verify_commit: sign-bytes + H2D + kernel + D2H + VerifyCommit replay"}
+    # the reference's shape: one core verifying 150 signatures sequentially
+    from oracle import coracle
+
+    m, off = coracle.pack_msgs(msgs)
+    pks = np.array([np.frombuffer(v.pub_key, np.uint8) for v in sv.valset.validators])
+    cts = []
+    for _ in range(5):
+        t = time.perf_counter()
+        coracle.verify_batch(pks, sigs, m, off, mode, nthreads=1)
+        cts.append(time.perf_counter() - t)
+    res["cpu_single_core_p50_ms"] = round(float(np.median(cts)) * 1e3, 3)
+    return res
+
+
+def load_traffic():
+    p = os.path.join(ROOT, "profiles", "r01_traffic.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        return d.get("bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"# note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from cometbft_amd import Context, pack_messages
+    from cometbft_amd import testutil as TU
+
+    mode = 0 if args.mode == "go" else 1
+    ctx = Context(device=local)
+    n = args.n
+    height = 1000 + rank
+    sv = TU.make_validator_set(ctx, n)
+    msgs = TU.commit_messages(n, height)
+    m, off = pack_messages(msgs)
+    sigs = ctx.sign(sv.seeds, m, off)
+    pk = np.ascontiguousarray(sv.pubkeys)
+
+    d_pk = torch.from_numpy(pk.copy()).to(dev)
+    d_sig = torch.from_numpy(sigs.copy()).to(dev)
+    d_msg = torch.from_numpy(np.concatenate([m, np.zeros(16, np.uint8)])).to(dev)
+    d_off = torch.from_numpy(off.view(np.int32).copy()).to(dev)
+    d_valid = torch.zeros(n, dtype=torch.uint8, device=dev)
+    words = (n + 63) // 64
+    d_bm = torch.zeros(words, dtype=torch.int64, device=dev)
+    d_all = torch.zeros(world * words, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sptr = stream.cuda_stream
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+
+    def step(i=None):
+        if i is not None:
+            ev[i][0].record(stream)
+        ctx.verify_device(n, d_pk.data_ptr(), d_sig.data_ptr(), d_msg.data_ptr(), d_off.data_ptr(), mode,
+                          d_valid.data_ptr(), d_bm.data_ptr(), sptr)
+        if i is not None:
+            ev[i][1].record(stream)
+        if world > 1:
+            dist.all_gather_into_tensor(d_all, d_bm)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+    # correctness of the timed work: every honest signature accepted, bitmap full
+    ok_local = int(d_valid.sum().item()) == n
+    full = (1 << 64) - 1
+    bm = d_bm.cpu().numpy().view(np.uint64)
+    tail = n % 64
+    exp_words = np.full(words, full, dtype=np.uint64)
+    if tail:
+        exp_words[-1] = np.uint64((1 << tail) - 1)
+    ok_local = ok_local and np.array_equal(bm, exp_words)
+    if world > 1:
+        t = torch.tensor([elapsed, 0.0 if ok_local else 1.0], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, bad = float(t[0].item()), float(t[1].item())
+        ok = bad == 0.0
+        allw = d_all.cpu().numpy().view(np.uint64).reshape(world, words)
+        ok = ok and all(np.array_equal(allw[r], exp_words) for r in range(world))
+    else:
+        ok = ok_local
+
+    if rank == 0:
+        total = world * n * args.steps
+        value = total / elapsed
+        achieved = n * MACS_PER_VERIFY / (kernel_ms * 1e-3) / 1e12
+        line = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "verifs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic",
+            "config": {"workload": "configs[1]: one synthetic 10,000-validator commit per GPU per step "
+                                   "(inputs resident in HBM; RCCL all-gather of verdict bitmaps when N>1)",
+                       "sigs_per_gpu": n, "mode": args.mode, "msg_bytes_mean": round(float(m.size) / n, 1),
+                       "parallelism": f"dp{world}", "verdicts_ok": bool(ok)},
+            "roofline": {"bound": "valu_int", "achieved": round(achieved, 3), "peak": INT_MAC_PEAK_T,
+                         "unit": "TMAC/s", "frac": round(achieved / INT_MAC_PEAK_T, 4),
+                         "traffic": load_traffic(), "kernel_ms": round(kernel_ms, 4),
+                         "work": f"{MACS_PER_VERIFY} int32 MACs/verify x {n} verifies per launch"},
+        }
+        if not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(pk, sigs, m, off, mode, args.cpu_seconds)
+            line["cpu_baseline"]["gpu_over_cpu"] = round(value / world / line["cpu_baseline"]["value"], 1)
+        if not args.no_latency:
+            line["latency_150"] = latency_150(ctx, mode, args.latency_iters)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if not ok:
+        sys.exit(3)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,234 @@
+"""VerifyCommit / VerifyCommitLight / VerifyCommitLightTrusting through the GPU
+batch + replay (cmtv_verify_commit), mirroring the reference's tests:
+
+  types/validator_set_test.go:670-744  TestValidatorSet_VerifyCommit_All
+  types/validator_set_test.go:746-769  ..._VerifyCommit_CheckAllSignatures
+  types/validator_set_test.go:771-792  ..._VerifyCommitLight_ReturnsAsSoonAsMajority...
+  types/validator_set_test.go:794-815  ..._VerifyCommitLightTrusting_ReturnsAsSoonAs...
+  types/validator_set_test.go:1520-1574 ..._VerifyCommitLightTrusting(+ErrorsOnOverflow)
+  light/verifier_test.go:120           ErrNotEnoughVotingPowerSigned{Got: 50, Needed: 93}
+
+Signatures are produced by the oracle signer (RFC 8032); sign-bytes by the
+oracle encoder, so the library's encoder is exercised against an independent one.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+from cometbft_amd import types as T
+from oracle import ed25519_ref as E
+from oracle import signbytes as SB
+
+pytestmark = pytest.mark.gpu
+
+CHAIN = "Lalande21185"
+MAX_TOTAL_VOTING_POWER = (2**63 - 1) // 8
+
+
+def _bid(tag=b"blk"):
+    return T.BlockID(hashlib.sha256(tag).digest(), T.PartSetHeader(1, hashlib.sha256(tag + b"p").digest()))
+
+
+def _bid_tuple(b: T.BlockID):
+    return (b.hash, b.part_set_header.total, b.part_set_header.hash)
+
+
+class Val:
+    def __init__(self, i, power):
+        self.seed = hashlib.sha256(b"test-val-%d" % i).digest()
+        self.pk = E.pubkey_from_seed(self.seed)
+        self.v = T.Validator(self.pk, power)
+
+    def sign_vote(self, chain, height, round_, bid, ts, flag=T.BLOCK_ID_FLAG_COMMIT):
+        b = _bid_tuple(bid) if flag == T.BLOCK_ID_FLAG_COMMIT else None
+        msg = SB.vote_sign_bytes(chain, T.PRECOMMIT_TYPE, height, round_, b, *ts)
+        return T.CommitSig(flag, self.v.address, ts, E.sign(self.seed, msg))
+
+
+def _valset(n, power, start=0):
+    vals = [Val(start + i, power) for i in range(n)]
+    vals.sort(key=lambda x: x.v.address)
+    return vals, T.ValidatorSet([x.v for x in vals])
+
+
+def _commit(vals, chain, height, round_, bid, flags=None):
+    sigs = []
+    for i, v in enumerate(vals):
+        f = T.BLOCK_ID_FLAG_COMMIT if flags is None else flags[i]
+        if f == T.BLOCK_ID_FLAG_ABSENT:
+            sigs.append(T.new_commit_sig_absent())
+        else:
+            sigs.append(v.sign_vote(chain, height, round_, bid, (1_600_000_000 + i, 1000 * i), f))
+    return T.Commit(height, round_, bid, sigs)
+
+
+def _err(fn):
+    try:
+        fn()
+    except Exception as e:  # noqa: BLE001
+        return e
+    return None
+
+
+def test_verify_commit_all(gpu_ctx):
+    vals, vset = _valset(1, 1000)
+    bid, h = _bid(), 12345
+    commit = _commit(vals, CHAIN, h, 2, bid)
+    vote2 = vals[0].sign_vote("EpsilonEridani", h, 2, bid, (1_600_000_000, 0))
+    cases = [
+        ("good", CHAIN, bid, h, commit, None),
+        ("wrong signature (#0)", "EpsilonEridani", bid, h, commit, T.ErrWrongSignature),
+        ("wrong block ID", CHAIN, _bid(b"random"), h, commit, T.ErrWrongBlockID),
+        ("wrong height", CHAIN, bid, h - 1, commit, T.ErrInvalidCommitHeight),
+        ("wrong set size: 1 vs 0", CHAIN, bid, h, T.Commit(h, 2, bid, []), T.ErrInvalidCommitSignatures),
+        ("wrong set size: 1 vs 2", CHAIN, bid, h,
+         T.Commit(h, 2, bid, [commit.signatures[0], T.new_commit_sig_absent()]), T.ErrInvalidCommitSignatures),
+        ("insufficient voting power: got 0, needed more than 666", CHAIN, bid, h,
+         T.Commit(h, 2, bid, [T.new_commit_sig_absent()]), T.ErrNotEnoughVotingPowerSigned),
+        ("wrong signature (#0)", CHAIN, bid, h, T.Commit(h, 2, bid, [vote2]), T.ErrWrongSignature),
+    ]
+    for desc, chain, b, height, c, exc in cases:
+        for fn in (vset.verify_commit, vset.verify_commit_light):
+            e = _err(lambda: fn(chain, b, height, c, ctx=gpu_ctx))
+            if exc is None:
+                assert e is None, (desc, e)
+            else:
+                assert isinstance(e, exc), (desc, fn.__name__, e)
+                assert desc in str(e), (desc, str(e))
+
+
+def test_error_strings_exact(gpu_ctx):
+    vals, vset = _valset(1, 1000)
+    bid, h = _bid(), 7
+    commit = _commit(vals, CHAIN, h, 0, bid)
+    e = _err(lambda: vset.verify_commit(CHAIN, bid, h + 1, commit, ctx=gpu_ctx))
+    assert str(e) == "Invalid commit -- wrong height: 8 vs 7"
+    other = _bid(b"other")
+    e = _err(lambda: vset.verify_commit(CHAIN, other, h, commit, ctx=gpu_ctx))
+    want = ("invalid commit -- wrong block ID: want %s:1:%s, got %s:1:%s" %
+            (other.hash.hex().upper(), other.part_set_header.hash[:6].hex().upper(),
+             bid.hash.hex().upper(), bid.part_set_header.hash[:6].hex().upper()))
+    assert str(e) == want
+    e = _err(lambda: vset.verify_commit("nope", bid, h, commit, ctx=gpu_ctx))
+    assert str(e) == "wrong signature (#0): " + commit.signatures[0].signature.hex().upper()
+
+
+def test_verify_commit_checks_all_signatures(gpu_ctx):
+    vals, vset = _valset(4, 10)
+    bid, h = _bid(), 3
+    commit = _commit(vals, "test_chain_id", h, 0, bid)
+    commit.signatures[3] = vals[3].sign_vote("CentaurusA", h, 0, bid, commit.signatures[3].timestamp)
+    e = _err(lambda: vset.verify_commit("test_chain_id", bid, h, commit, ctx=gpu_ctx))
+    assert isinstance(e, T.ErrWrongSignature) and "wrong signature (#3)" in str(e)
+    # ... while VerifyCommitLight returns as soon as +2/3 signed (#3 never checked)
+    assert vset.verify_commit_light("test_chain_id", bid, h, commit, ctx=gpu_ctx) is None
+
+
+def test_light_trusting_returns_at_trust_level(gpu_ctx):
+    vals, vset = _valset(4, 10)
+    bid, h = _bid(), 3
+    commit = _commit(vals, "test_chain_id", h, 0, bid)
+    commit.signatures[2] = vals[2].sign_vote("CentaurusA", h, 0, bid, commit.signatures[2].timestamp)
+    assert vset.verify_commit_light_trusting("test_chain_id", commit, (1, 3), ctx=gpu_ctx) is None
+
+
+def test_light_trusting_overlap(gpu_ctx):
+    vals, original = _valset(6, 1, start=100)
+    bid = _bid(b"lt")
+    commit = _commit(vals, "test_chain_id", 1, 1, bid)
+    _, newset = _valset(2, 1, start=500)
+    assert original.verify_commit_light_trusting("test_chain_id", commit, (1, 3), ctx=gpu_ctx) is None
+    e = _err(lambda: newset.verify_commit_light_trusting("test_chain_id", commit, (1, 3), ctx=gpu_ctx))
+    assert isinstance(e, T.ErrNotEnoughVotingPowerSigned)
+    merged = T.ValidatorSet(newset.validators + original.validators)
+    assert merged.verify_commit_light_trusting("test_chain_id", commit, (1, 3), ctx=gpu_ctx) is None
+
+
+def test_light_trusting_overflow_and_zero_denominator(gpu_ctx):
+    vals, vset = _valset(1, MAX_TOTAL_VOTING_POWER, start=900)
+    bid = _bid(b"of")
+    commit = _commit(vals, "test_chain_id", 1, 1, bid)
+    e = _err(lambda: vset.verify_commit_light_trusting("test_chain_id", commit, (25, 55), ctx=gpu_ctx))
+    assert isinstance(e, T.ErrTrustLevel) and "int64 overflow" in str(e)
+    e = _err(lambda: vset.verify_commit_light_trusting("test_chain_id", commit, (1, 0), ctx=gpu_ctx))
+    assert str(e) == "trustLevel has zero Denominator"
+
+
+def test_light_trusting_double_vote(gpu_ctx):
+    vals, vset = _valset(3, 10, start=40)
+    bid = _bid(b"dv")
+    commit = _commit(vals, "c", 5, 0, bid)
+    commit.signatures[2] = commit.signatures[0]  # validator 0 signs twice
+    e = _err(lambda: vset.verify_commit_light_trusting("c", commit, (9, 10), ctx=gpu_ctx))
+    assert isinstance(e, T.ErrDoubleVote)
+    assert str(e).startswith("double vote from Validator{%s PubKeyEd25519{%s} VP:10 A:0} (0 and 2)" %
+                             (vals[0].v.address.hex().upper(), vals[0].pk.hex().upper()))
+
+
+def test_not_enough_power_values(gpu_ctx):
+    # light/verifier_test.go:120 style: ErrNotEnoughVotingPowerSigned{Got: 50, Needed: 93}
+    vals, vset = _valset(14, 10, start=200)
+    bid = _bid(b"ne")
+    flags = [T.BLOCK_ID_FLAG_COMMIT] * 5 + [T.BLOCK_ID_FLAG_ABSENT] * 9
+    commit = _commit(vals, "c", 9, 0, bid, flags)
+    e = _err(lambda: vset.verify_commit_light("c", bid, 9, commit, ctx=gpu_ctx))
+    assert isinstance(e, T.ErrNotEnoughVotingPowerSigned) and (e.got, e.needed) == (50, 93)
+    assert str(e) == "invalid commit -- insufficient voting power: got 50, needed more than 93"
+
+
+def test_nil_votes_and_absent(gpu_ctx):
+    vals, vset = _valset(6, 10, start=300)
+    bid = _bid(b"nil")
+    flags = [T.BLOCK_ID_FLAG_COMMIT] * 5 + [T.BLOCK_ID_FLAG_NIL]
+    commit = _commit(vals, "c", 4, 0, bid, flags)
+    # nil vote is verified (its sign-bytes carry no BlockID) but not tallied
+    assert vset.verify_commit("c", bid, 4, commit, ctx=gpu_ctx) is None
+    commit.signatures[5] = vals[5].sign_vote("c", 4, 0, bid, commit.signatures[5].timestamp, T.BLOCK_ID_FLAG_COMMIT)
+    commit.signatures[5].block_id_flag = T.BLOCK_ID_FLAG_NIL  # signed for the block, claims nil
+    e = _err(lambda: vset.verify_commit("c", bid, 4, commit, ctx=gpu_ctx))
+    assert isinstance(e, T.ErrWrongSignature) and e.index == 5
+    # Light skips nil votes entirely
+    assert vset.verify_commit_light("c", bid, 4, commit, ctx=gpu_ctx) is None
+
+
+def test_reference_panics_are_surfaced(gpu_ctx):
+    vals, vset = _valset(3, 10, start=700)
+    bid = _bid(b"pn")
+    commit = _commit(vals, "c", 2, 0, bid)
+    commit.signatures[1].block_id_flag = 9
+    e = _err(lambda: vset.verify_commit("c", bid, 2, commit, ctx=gpu_ctx))
+    assert isinstance(e, T.ReferencePanic) and "Unknown BlockIDFlag" in str(e)
+    commit = _commit(vals, "c", 2, 0, bid)
+    bad = T.ValidatorSet([vset.validators[0], T.Validator(vset.validators[1].pub_key[:31], 10),
+                          vset.validators[2]])
+    e = _err(lambda: bad.verify_commit("c", bid, 2, commit, ctx=gpu_ctx))
+    assert isinstance(e, T.ReferencePanic) and "bad public key length: 31" in str(e)
+    # a bad signature BEFORE the bad key is reported first, like the sequential loop
+    commit.signatures[0] = vals[0].sign_vote("zz", 2, 0, bid, commit.signatures[0].timestamp)
+    e = _err(lambda: bad.verify_commit("c", bid, 2, commit, ctx=gpu_ctx))
+    assert isinstance(e, T.ErrWrongSignature) and e.index == 0
+
+
+def test_wrong_signature_lengths_are_invalid(gpu_ctx):
+    vals, vset = _valset(2, 10, start=800)
+    bid = _bid(b"len")
+    commit = _commit(vals, "c", 2, 0, bid)
+    commit.signatures[1].signature = commit.signatures[1].signature[:63]
+    e = _err(lambda: vset.verify_commit("c", bid, 2, commit, ctx=gpu_ctx))
+    assert isinstance(e, T.ErrWrongSignature) and e.index == 1
+
+
+def test_large_commit_first_error_in_index_order(gpu_ctx):
+    from cometbft_amd import testutil as TU
+
+    sv = TU.make_validator_set(gpu_ctx, 1000)
+    commit, msgs, sigs = TU.make_commit(gpu_ctx, sv, height=77)
+    bid = TU.block_id_for_height(77)
+    assert sv.valset.verify_commit(TU.CHAIN_ID, bid, 77, commit, ctx=gpu_ctx) is None
+    for bad in (911, 250):
+        s = bytearray(commit.signatures[bad].signature)
+        s[3] ^= 1
+        commit.signatures[bad].signature = bytes(s)
+    e = _err(lambda: sv.valset.verify_commit(TU.CHAIN_ID, bid, 77, commit, ctx=gpu_ctx))
+    assert isinstance(e, T.ErrWrongSignature) and e.index == 250

@@ -10,7 +10,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcmtverify.so")
+LIB_PATH = os.environ.get("CMTV_LIBRARY") or os.path.join(_HERE, "libcmtverify.so")
 
 CMTV_OK = 0
 CMTV_EINVAL = -1

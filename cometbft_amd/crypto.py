@@ -93,9 +93,11 @@ class Context:
 
     def verify_device(self, n: int, d_pk: int, d_sig: int, d_msg: int, d_off: int, mode: int,
                       d_valid: int = 0, d_bitmap: int = 0, stream: int = 0) -> None:
-        """Enqueue verification over device-resident buffers (raw pointers)."""
+        """Enqueue verification over device-resident buffers (raw pointers) on
+        `stream` (a hipStream_t handle; 0 = the null stream, which is what
+        torch's default stream reports)."""
         rc = N.lib().cmtv_verify_ed25519_device(self._h, n, d_pk, d_sig, d_msg, d_off, mode, d_valid or None,
-                                                d_bitmap or None, stream or None)
+                                                d_bitmap or None, ctypes.c_void_p(stream) if stream else None)
         N.check(rc, "cmtv_verify_ed25519_device")
 
     # -------------------------------------------------------------- test data

@@ -26,6 +26,16 @@
 #define CMTV_HD __host__ __device__ __forceinline__
 #endif
 
+// Scheduling fence between field operations. Without it the AMDGPU machine
+// scheduler interleaves the 100-product DAGs of neighbouring multiplications
+// for ILP and needs >512 VGPRs; fencing each multiply bounds the live set to
+// one operation's working set so the verify kernel fits its occupancy target.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define CMTV_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define CMTV_SCHED_FENCE() ((void)0)
+#endif
+
 #ifdef CMTV_BOUNDS_CHECK
 #include <cassert>
 #define CMTV_ASSERT(x) assert(x)
@@ -132,6 +142,7 @@ CMTV_HD void fe_reduce64(fe& h, uint64_t h0, uint64_t h1, uint64_t h2, uint64_t 
 }
 
 CMTV_HD void fe_mul(fe& h, const fe& f, const fe& g) {
+  CMTV_SCHED_FENCE();
 #ifdef CMTV_BOUNDS_CHECK
   for (int i = 0; i < 10; i++) CMTV_ASSERT(f.v[i] < MUL_BOUND && g.v[i] < MUL_BOUND);
 #endif
@@ -174,9 +185,11 @@ CMTV_HD void fe_mul(fe& h, const fe& f, const fe& g) {
                 CMTV_MUL64(f4, g5) + CMTV_MUL64(f5, g4) + CMTV_MUL64(f6, g3) + CMTV_MUL64(f7, g2) +
                 CMTV_MUL64(f8, g1) + CMTV_MUL64(f9, g0);
   fe_reduce64(h, h0, h1, h2, h3, h4, h5, h6, h7, h8, h9);
+  CMTV_SCHED_FENCE();
 }
 
 CMTV_HD void fe_sq(fe& h, const fe& f) {
+  CMTV_SCHED_FENCE();
 #ifdef CMTV_BOUNDS_CHECK
   for (int i = 0; i < 10; i++) CMTV_ASSERT(f.v[i] < ((i & 1) ? SQ_ODD_BOUND : MUL_BOUND));
 #endif
@@ -207,10 +220,15 @@ CMTV_HD void fe_sq(fe& h, const fe& f) {
   uint64_t h9 = CMTV_MUL64(f0_2, f9) + CMTV_MUL64(f1_2, f8) + CMTV_MUL64(f2_2, f7) + CMTV_MUL64(f3_2, f6) +
                 CMTV_MUL64(f4_2, f5);
   fe_reduce64(h, h0, h1, h2, h3, h4, h5, h6, h7, h8, h9);
+  CMTV_SCHED_FENCE();
 }
 
+// Kept as a rolled loop: the exponentiation chains call it with n up to 100,
+// and an unrolled chain would stream hundreds of KB of code through the
+// instruction cache once per wave.
 CMTV_HD void fe_sqn(fe& h, const fe& f, int n) {
   fe_sq(h, f);
+#pragma unroll 1
   for (int i = 1; i < n; i++) fe_sq(h, h);
 }
 

@@ -90,49 +90,104 @@ CMTV_HD void p2_dbl(ge_efgh& r, const ge_p2& p) {
   fe_carry(r.f);
 }
 
-// p + q  (q cached). neg = true computes p - q.
-CMTV_HD void ge_add_cached(ge_efgh& r, const ge_p3& p, const ge_cached& q, bool neg) {
-  fe ymx, ypx, a, b, c, d2;
-  fe_sub(ymx, p.Y, p.X);
-  fe_add(ypx, p.Y, p.X);
-  fe qa, qb;
-  fe_select(qa, q.YmX, q.YpX, neg);
-  fe_select(qb, q.YpX, q.YmX, neg);
-  fe_mul(a, ymx, qa);
-  fe_mul(b, ypx, qb);
-  fe_mul(c, p.T, q.T2d);
-  fe_mul(d2, p.Z, q.Z);
-  fe_add(d2, d2, d2);
-  fe_carry(d2);
-  fe_sub(r.e, b, a);  // E = B - A
-  fe_add(r.h, b, a);  // H = B + A
-  fe F, G;
-  fe_sub(F, d2, c);   // D - C
-  fe_add(G, d2, c);   // D + C
-  fe_select(r.f, F, G, neg);
-  fe_select(r.g, G, F, neg);
+// p + q  (q cached). Operands are consumed in an order that lets the T and Z
+// inputs die early (register pressure is the occupancy limiter).
+CMTV_HD void ge_add_cached(ge_efgh& r, const ge_p3& p, const ge_cached& q) {
+  fe t0, t1;
+  fe_mul(r.g, p.T, q.T2d);  // C
+  fe_mul(r.f, p.Z, q.Z);    // Z1 Z2
+  fe_add(r.f, r.f, r.f);
+  fe_carry(r.f);            // D = 2 Z1 Z2
+  fe_sub(t0, p.Y, p.X);
+  fe_mul(t0, t0, q.YmX);    // A
+  fe_add(t1, p.Y, p.X);
+  fe_mul(t1, t1, q.YpX);    // B
+  fe_sub(r.e, t1, t0);      // E = B - A
+  fe_add(r.h, t1, t0);      // H = B + A
+  fe_add(t0, r.f, r.g);     // G = D + C
+  fe_sub(r.f, r.f, r.g);    // F = D - C
+  r.g = t0;
 }
 
-// p + q (q affine niels). neg = true computes p - q.
-CMTV_HD void ge_add_niels(ge_efgh& r, const ge_p3& p, const ge_niels& q, bool neg) {
-  fe ymx, ypx, a, b, c, d2;
-  fe_sub(ymx, p.Y, p.X);
-  fe_add(ypx, p.Y, p.X);
-  fe qa, qb;
-  fe_select(qa, q.ymx, q.ypx, neg);
-  fe_select(qb, q.ypx, q.ymx, neg);
-  fe_mul(a, ymx, qa);
-  fe_mul(b, ypx, qb);
-  fe_mul(c, p.T, q.xy2d);
-  fe_add(d2, p.Z, p.Z);
-  fe_carry(d2);
-  fe_sub(r.e, b, a);
-  fe_add(r.h, b, a);
-  fe F, G;
-  fe_sub(F, d2, c);
-  fe_add(G, d2, c);
-  fe_select(r.f, F, G, neg);
-  fe_select(r.g, G, F, neg);
+// p + q (q affine niels, Z2 = 1)
+CMTV_HD void ge_add_niels(ge_efgh& r, const ge_p3& p, const ge_niels& q) {
+  fe t0, t1;
+  fe_mul(r.g, p.T, q.xy2d);  // C
+  fe_add(r.f, p.Z, p.Z);
+  fe_carry(r.f);             // D = 2 Z1
+  fe_sub(t0, p.Y, p.X);
+  fe_mul(t0, t0, q.ymx);     // A
+  fe_add(t1, p.Y, p.X);
+  fe_mul(t1, t1, q.ypx);     // B
+  fe_sub(r.e, t1, t0);
+  fe_add(r.h, t1, t0);
+  fe_add(t0, r.f, r.g);
+  fe_sub(r.f, r.f, r.g);
+  r.g = t0;
+}
+
+// p + q with q = (neg ? -1 : 1) * table[e] (or the identity when ident),
+// streamed from a table one coordinate at a time so only one 10-word
+// coordinate of the addend is ever live. Tab::load_fe(e, c, fe&) with c in
+// {0: Y+X, 1: Y-X, 2: Z, 3: 2dT} (cached, NZ = true) or {0: y+x, 1: y-x,
+// 2: 2dxy} (niels, NZ = false, Z2 = 1). Negation swaps the (Y+X, Y-X) reads
+// and negates 2dT; both are per-lane selects, not branches.
+template <bool NZ, class Tab>
+CMTV_HD void ge_add_table(ge_efgh& r, const ge_p3& p, const Tab& tab, int e, bool neg, bool ident) {
+  fe q, t0, t1;
+  const int cT = NZ ? 3 : 2;
+  tab.load_fe(e, cT, q);
+  {
+    fe qn;
+    fe_neg(qn, q);
+    fe_select(q, q, qn, neg);
+#pragma unroll
+    for (int i = 0; i < 10; i++) q.v[i] = ident ? 0u : q.v[i];
+  }
+  fe_mul(r.g, p.T, q);  // C
+  if (NZ) {
+    tab.load_fe(e, 2, q);
+#pragma unroll
+    for (int i = 0; i < 10; i++) q.v[i] = ident ? (i == 0 ? 1u : 0u) : q.v[i];
+    fe_mul(r.f, p.Z, q);
+    fe_add(r.f, r.f, r.f);
+  } else {
+    fe_add(r.f, p.Z, p.Z);
+  }
+  fe_carry(r.f);  // D
+  tab.load_fe(e, neg ? 0 : 1, q);
+#pragma unroll
+  for (int i = 0; i < 10; i++) q.v[i] = ident ? (i == 0 ? 1u : 0u) : q.v[i];
+  fe_sub(t0, p.Y, p.X);
+  fe_mul(t0, t0, q);  // A
+  tab.load_fe(e, neg ? 1 : 0, q);
+#pragma unroll
+  for (int i = 0; i < 10; i++) q.v[i] = ident ? (i == 0 ? 1u : 0u) : q.v[i];
+  fe_add(t1, p.Y, p.X);
+  fe_mul(t1, t1, q);  // B
+  fe_sub(r.e, t1, t0);
+  fe_add(r.h, t1, t0);
+  fe_add(t0, r.f, r.g);
+  fe_sub(r.f, r.f, r.g);
+  r.g = t0;
+}
+
+// -q for cached / niels forms: swap (Y+X, Y-X), negate the 2dT term.
+// `neg` is a per-lane flag (digit sign), so this is a select, not a branch.
+CMTV_HD void cached_cneg(ge_cached& q, bool neg) {
+  fe a = q.YpX, t;
+  fe_select(q.YpX, q.YpX, q.YmX, neg);
+  fe_select(q.YmX, q.YmX, a, neg);
+  fe_neg(t, q.T2d);
+  fe_select(q.T2d, q.T2d, t, neg);
+}
+
+CMTV_HD void niels_cneg(ge_niels& q, bool neg) {
+  fe a = q.ypx, t;
+  fe_select(q.ypx, q.ypx, q.ymx, neg);
+  fe_select(q.ymx, q.ymx, a, neg);
+  fe_neg(t, q.xy2d);
+  fe_select(q.xy2d, q.xy2d, t, neg);
 }
 
 CMTV_HD void p3_to_cached(ge_cached& r, const ge_p3& p) {
@@ -162,47 +217,42 @@ CMTV_HD void niels_identity(ge_niels& r) {
 // when the sign bit is set (x = 0 with the sign bit set is accepted).
 // Returns false when no square root exists.
 CMTV_HD bool p3_frombytes(ge_p3& h, const uint32_t w[8]) {
-  fe y, y2, u, v, v3, v7, t, r, check, one, d;
+  fe y, u, v, r0, t, one;
   fe_frombytes(y, w);
   fe_1(one);
-  fe_const_d(d);
-  fe_sq(y2, y);
-  fe_sub(u, y2, one);     // u = y^2 - 1
-  fe_mul(v, y2, d);
-  fe_add(v, v, one);      // v = d y^2 + 1
-  fe_sq(v3, v);
-  fe_mul(v3, v3, v);      // v^3
-  fe_sq(v7, v3);
-  fe_mul(v7, v7, v);      // v^7
-  fe_mul(t, u, v7);
-  fe_pow22523(t, t);      // (u v^7)^((p-5)/8)
-  fe_mul(r, u, v3);
-  fe_mul(r, r, t);        // r = u v^3 (u v^7)^((p-5)/8)
-  fe_sq(check, r);
-  fe_mul(check, check, v);  // v r^2
-  fe uc = u;
-  fe_carry(uc);
-  fe uneg;
-  fe_neg(uneg, uc);
-  const bool correct = fe_equal(check, uc);
-  const bool flipped = fe_equal(check, uneg);
-  fe sqm1, r2;
-  fe_const_sqrtm1(sqm1);
-  fe_mul(r2, r, sqm1);
-  fe_select(r, r, r2, flipped);
+  fe_sq(t, y);
+  fe_sub(u, t, one);  // u = y^2 - 1
+  fe_const_d(v);
+  fe_mul(v, t, v);
+  fe_add(v, v, one);  // v = d y^2 + 1
+  fe_sq(t, v);        // v^2
+  fe_mul(r0, t, v);   // v^3
+  fe_sq(t, t);        // v^4
+  fe_mul(r0, u, r0);  // u v^3
+  fe_mul(t, r0, t);   // u v^7
+  fe_pow22523(t, t);  // (u v^7)^((p-5)/8)
+  fe_mul(r0, r0, t);  // r = u v^3 (u v^7)^((p-5)/8)
+  fe_sq(t, r0);
+  fe_mul(t, t, v);    // check = v r^2
+  fe_carry(u);
+  const bool correct = fe_equal(t, u);
+  fe_neg(v, u);
+  const bool flipped = fe_equal(t, v);
+  fe_const_sqrtm1(t);
+  fe_mul(t, r0, t);
+  fe_select(r0, r0, t, flipped);
   // Absolute(): the non-negative (even) root
-  fe rn;
-  fe_neg(rn, r);
-  fe_carry(rn);
-  fe_select(r, r, rn, fe_isneg(r));
-  // sign bit selects the negative root
-  fe_neg(rn, r);
-  fe_carry(rn);
-  fe_select(r, r, rn, (w[7] >> 31) != 0);
-  h.X = r;
+  fe_neg(t, r0);
+  fe_carry(t);
+  fe_select(r0, r0, t, fe_isneg(r0));
+  // the sign bit selects the negative root (x = 0 stays 0)
+  fe_neg(t, r0);
+  fe_carry(t);
+  fe_select(r0, r0, t, (w[7] >> 31) != 0);
+  h.X = r0;
   h.Y = y;
   fe_1(h.Z);
-  fe_mul(h.T, r, y);
+  fe_mul(h.T, r0, y);
   return correct || flipped;
 }
 

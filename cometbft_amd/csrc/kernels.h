@@ -5,7 +5,7 @@
 
 namespace cmtv {
 
-constexpr uint32_t kBtabWords = 128 * 32;   // (1..128)B, 32 words per row
+constexpr uint32_t kBtabWords = 128 * 36;   // (1..128)B, 36 words per row
 constexpr uint32_t kAtabWordsPerLane = 320; // (1..8)(-A), 40 words per point
 
 hipError_t launch_btab_init(uint32_t* d_rows, hipStream_t s);

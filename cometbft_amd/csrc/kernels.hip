@@ -10,8 +10,8 @@
 //   pk   : n x 32 B   (row i = 8 words, read as 2 x dwordx4)
 //   sig  : n x 64 B   (row i = 16 words, 4 x dwordx4)
 //   msg  : flat bytes + (n+1) u32 offsets
-//   btab : 128 rows x 32 words (ypx, ymx, 2dxy; 10 limbs each; 2 pad) = 16 KiB,
-//          L1/L2-resident, rows gathered per lane as 8 x dwordx4
+//   btab : 128 rows x 36 words (ypx, ymx, 2dxy; 10 limbs + 2 pad each) = 18 KiB,
+//          L1/L2-resident; one coordinate gathered per lane as 2 x dwordx4 + dwordx2
 //   atab : per-lane (1..8)(-A) cached table, word-major / lane-minor
 //          [(e*40 + w) * stride + lane] so each of the 40 word loads of a row
 //          is one coalesced 256-byte wave access when lanes share the digit
@@ -21,52 +21,48 @@
 #include "kernels.h"
 #include "verify_core.h"
 
+// Minimum waves per SIMD the verify kernel is compiled for (the second
+// __launch_bounds__ argument): caps VGPRs at 512 / waves.
+#ifndef CMTV_VERIFY_WAVES_PER_EU
+#define CMTV_VERIFY_WAVES_PER_EU 2
+#endif
+
 namespace cmtv {
 
 struct DevBTab {
   const uint32_t* __restrict__ rows;
-  __device__ __forceinline__ void load(int e, ge_niels& r) const {
-    const uint4* p = reinterpret_cast<const uint4*>(rows + e * BTAB_ROW_WORDS);
-    uint32_t w[32];
-#pragma unroll
-    for (int q = 0; q < 8; q++) {
-      const uint4 v = p[q];
-      w[4 * q] = v.x;
-      w[4 * q + 1] = v.y;
-      w[4 * q + 2] = v.z;
-      w[4 * q + 3] = v.w;
-    }
-#pragma unroll
-    for (int i = 0; i < 10; i++) {
-      r.ypx.v[i] = w[i];
-      r.ymx.v[i] = w[10 + i];
-      r.xy2d.v[i] = w[20 + i];
-    }
+  // one niels coordinate (10 words at a 16-byte aligned offset): 2 x dwordx4 + dwordx2
+  __device__ __forceinline__ void load_fe(int e, int c, fe& r) const {
+    const uint32_t* p = rows + e * BTAB_ROW_WORDS + c * BTAB_COORD_WORDS;
+    const uint4 a = *reinterpret_cast<const uint4*>(p);
+    const uint4 b = *reinterpret_cast<const uint4*>(p + 4);
+    const uint2 d = *reinterpret_cast<const uint2*>(p + 8);
+    r.v[0] = a.x; r.v[1] = a.y; r.v[2] = a.z; r.v[3] = a.w;
+    r.v[4] = b.x; r.v[5] = b.y; r.v[6] = b.z; r.v[7] = b.w;
+    r.v[8] = d.x; r.v[9] = d.y;
   }
 };
 
+// Per-lane (1..8)(-A) table, word-major / lane-minor: word w of entry e for
+// lane l lives at base[(e * 40 + w) * stride + l], so a wave's load of one
+// word is a 256-byte coalesced access whenever its lanes share the entry.
 struct DevATab {
   uint32_t* __restrict__ base;
   uint32_t stride;
   uint32_t lane;
-  __device__ __forceinline__ void load(int e, ge_cached& r) const {
-    const uint32_t* p = base + (size_t)(e * 40) * stride + lane;
+  __device__ __forceinline__ void load_fe(int e, int c, fe& r) const {
+    const uint32_t* p = base + (uint32_t)((e * 4 + c) * 10) * stride + lane;
 #pragma unroll
-    for (int i = 0; i < 10; i++) {
-      r.YpX.v[i] = p[(size_t)i * stride];
-      r.YmX.v[i] = p[(size_t)(10 + i) * stride];
-      r.Z.v[i] = p[(size_t)(20 + i) * stride];
-      r.T2d.v[i] = p[(size_t)(30 + i) * stride];
-    }
+    for (int i = 0; i < 10; i++) r.v[i] = p[i * stride];
   }
   __device__ __forceinline__ void store(int e, const ge_cached& r) {
-    uint32_t* p = base + (size_t)(e * 40) * stride + lane;
+    uint32_t* p = base + (uint32_t)(e * 40) * stride + lane;
 #pragma unroll
     for (int i = 0; i < 10; i++) {
-      p[(size_t)i * stride] = r.YpX.v[i];
-      p[(size_t)(10 + i) * stride] = r.YmX.v[i];
-      p[(size_t)(20 + i) * stride] = r.Z.v[i];
-      p[(size_t)(30 + i) * stride] = r.T2d.v[i];
+      p[i * stride] = r.YpX.v[i];
+      p[(10 + i) * stride] = r.YmX.v[i];
+      p[(20 + i) * stride] = r.Z.v[i];
+      p[(30 + i) * stride] = r.T2d.v[i];
     }
   }
 };
@@ -93,7 +89,7 @@ __global__ __launch_bounds__(64) void k_btab_init(uint32_t* __restrict__ rows) {
 }
 
 template <uint32_t MODE>
-__global__ __launch_bounds__(64) void k_verify(uint32_t n, const uint32_t* __restrict__ pk,
+__global__ __launch_bounds__(64, CMTV_VERIFY_WAVES_PER_EU) void k_verify(uint32_t n, const uint32_t* __restrict__ pk,
                                                const uint32_t* __restrict__ sig, const uint8_t* __restrict__ msg,
                                                const uint32_t* __restrict__ off, const uint32_t* __restrict__ btab,
                                                uint32_t* __restrict__ atab, uint8_t* __restrict__ out_valid,
@@ -101,13 +97,10 @@ __global__ __launch_bounds__(64) void k_verify(uint32_t n, const uint32_t* __res
   const uint32_t gid = blockIdx.x * 64 + threadIdx.x;
   const bool active = gid < n;
   const uint32_t i = active ? gid : n - 1;
-  uint32_t pkw[8], sigw[16];
-  load_words(pkw, pk + 8 * (size_t)i, 2);
-  load_words(sigw, sig + 16 * (size_t)i, 4);
   const uint32_t m0 = off[i], m1 = off[i + 1];
   DevATab at{atab, gridDim.x * 64u, gid};
   DevBTab bt{btab};
-  bool v = verify_one<MODE>(pkw, sigw, msg + m0, m1 - m0, at, bt);
+  bool v = verify_one<MODE>(pk + 8 * (size_t)i, sig + 16 * (size_t)i, msg + m0, m1 - m0, at, bt);
   v = v && active;
   if (active && out_valid) out_valid[gid] = v ? 1 : 0;
   const uint64_t mask = __ballot(v);

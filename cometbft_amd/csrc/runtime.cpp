@@ -275,7 +275,7 @@ int cmtv_verify_ed25519_device(cmtv_ctx* ctx, size_t n, const void* d_pk, const 
   if (!d_pk || !d_sig || !d_msg || !d_msg_off || (!d_valid && !d_bitmap)) return CMTV_EINVAL;
   std::lock_guard<std::mutex> g(ctx->mu);
   if (hipSetDevice(ctx->device) != hipSuccess) return CMTV_ENODEV;
-  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the HIP null stream
   return enqueue_verify(ctx, n, static_cast<const uint8_t*>(d_pk), static_cast<const uint8_t*>(d_sig),
                         static_cast<const uint8_t*>(d_msg), static_cast<const uint32_t*>(d_msg_off), mode,
                         static_cast<uint8_t*>(d_valid), static_cast<uint64_t*>(d_bitmap), s);

@@ -75,10 +75,20 @@ CMTV_HD void sha512_compress(uint64_t st[8], uint64_t w[16]) {
   st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
 
+CMTV_HD uint32_t funnel_bytes(uint32_t hi, uint32_t lo, uint32_t sh) {
+  return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * sh));  // v_alignbyte_b32
+}
+
 // SHA-512(prefix[0 .. 4*PW) || msg[0 .. mlen)); prefix as little-endian byte
 // words. Output: 64 digest bytes as 16 little-endian 32-bit words.
+//
+// The message is read with 4-byte aligned loads and re-aligned in registers
+// (the per-lane message offset has arbitrary alignment); only words holding
+// at least one message byte are loaded, so nothing past msg[mlen-1]'s
+// 4-byte word is touched.
 template <int PW>
 CMTV_HD void sha512_prefixed(uint32_t out[16], const uint32_t pre[PW], const uint8_t* msg, uint32_t mlen) {
+  static_assert(PW % 2 == 0 && PW <= 16, "prefix must be whole 64-bit words inside block 0");
   constexpr uint32_t PB = 4 * PW;
   uint64_t st[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL,
                     0xa54ff53a5f1d36f1ULL, 0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL,
@@ -86,36 +96,48 @@ CMTV_HD void sha512_prefixed(uint32_t out[16], const uint32_t pre[PW], const uin
   const uint32_t total = PB + mlen;
   const uint32_t nblocks = (total + 17 + 127) / 128;
   const uint64_t bitlen = (uint64_t)total * 8;
-  const uint32_t lenpos = nblocks * 128 - 8;  // the 64-bit big-endian bit length
-  auto tail_byte = [&](uint32_t pos) -> uint32_t {
-    if (pos < total) return msg[pos - PB];
-    if (pos == total) return 0x80;
-    if (pos >= lenpos) return (uint32_t)(bitlen >> (8 * (7 - (pos - lenpos)))) & 0xff;
-    return 0;
+  const uintptr_t addr = (uintptr_t)msg;
+  const uint32_t sh = (uint32_t)(addr & 3);
+  const uint32_t* mw = (const uint32_t*)(addr - sh);  // aligned base
+  const uint32_t nwords = (sh + mlen + 3) / 4;         // aligned words holding message bytes
+  auto aligned = [&](uint32_t j) -> uint32_t { return j < nwords ? mw[j] : 0u; };
+  // little-endian stream word at byte position pos (pos % 4 == 0, pos >= PB)
+  auto tail_word = [&](uint32_t pos, uint32_t lo, uint32_t hi) -> uint32_t {
+    uint32_t v = funnel_bytes(hi, lo, sh);
+    const int r = (int)total - (int)pos;  // message bytes left in this word
+    if (r >= 4) return v;
+    if (r < 0) return 0u;
+    const uint32_t keep = r == 0 ? 0u : (0xFFFFFFFFu >> (32 - 8 * r));
+    return (v & keep) | (0x80u << (8 * r));
   };
-  // block 0 holds the whole register prefix (PB <= 64), so prefix indexing is static
-  {
+  auto be64 = [](uint32_t lo_word, uint32_t hi_word) -> uint64_t {
+    return ((uint64_t)__builtin_bswap32(lo_word) << 32) | __builtin_bswap32(hi_word);
+  };
+#pragma unroll 1
+  for (uint32_t b = 0; b < nblocks; b++) {
     uint64_t w[16];
+    // message-relative aligned word index of this block's first tail byte
+    const uint32_t q0 = (b == 0) ? 0u : b * 128 - PB;
+    const uint32_t j0 = q0 / 4;
+    uint32_t prev = aligned(j0);
 #pragma unroll
     for (int t = 0; t < 16; t++) {
-      uint64_t word = 0;
+      uint32_t lw[2];
 #pragma unroll
-      for (int j = 0; j < 8; j++) {
-        const uint32_t pos = 8 * t + j;
-        const uint32_t byte = (pos < PB) ? ((pre[pos >> 2] >> (8 * (pos & 3))) & 0xff) : tail_byte(pos);
-        word = (word << 8) | byte;
+      for (int h = 0; h < 2; h++) {
+        const uint32_t off = 8 * t + 4 * h;  // byte offset inside the block
+        if (b == 0 && off < PB) {
+          lw[h] = pre[off / 4];
+        } else {
+          const uint32_t pos = b * 128 + off;
+          const uint32_t jj = (pos - PB) / 4 + 1;
+          const uint32_t next = aligned(jj);
+          lw[h] = tail_word(pos, prev, next);
+          prev = next;
+        }
       }
-      w[t] = word;
-    }
-    sha512_compress(st, w);
-  }
-  for (uint32_t b = 1; b < nblocks; b++) {
-    uint64_t w[16];
-#pragma unroll
-    for (int t = 0; t < 16; t++) {
-      uint64_t word = 0;
-#pragma unroll
-      for (int j = 0; j < 8; j++) word = (word << 8) | tail_byte(b * 128 + 8 * t + j);
+      uint64_t word = be64(lw[0], lw[1]);
+      if (b == nblocks - 1 && t == 15) word = bitlen;
       w[t] = word;
     }
     sha512_compress(st, w);

@@ -28,8 +28,10 @@ namespace cmtv {
 
 enum : uint32_t { MODE_GO_STDLIB = 0, MODE_ZIP215 = 1 };
 
-// B-table row layout: 32 words per entry (ypx[10], ymx[10], xy2d[10], pad[2]).
-constexpr int BTAB_ROW_WORDS = 32;
+// B-table row layout: 36 words per entry, each coordinate 16-byte aligned:
+// ypx[10] pad[2] ymx[10] pad[2] xy2d[10] pad[2].
+constexpr int BTAB_ROW_WORDS = 36;
+constexpr int BTAB_COORD_WORDS = 12;
 constexpr int BTAB_ENTRIES = 128;
 // A-table: 8 cached points x 40 words per lane.
 constexpr int ATAB_WORDS = 8 * 40;
@@ -66,7 +68,7 @@ CMTV_HD void btab_entry(uint32_t row[BTAB_ROW_WORDS], int m) {
     p3_to_p2(q, acc);
     p2_dbl(t, q);
     efgh_to_p3(acc, t);
-    ge_add_cached(t, acc, Bc, false);
+    ge_add_cached(t, acc, Bc);
     ge_p3 added;
     efgh_to_p3(added, t);
     const bool take = (m >> bit) & 1;
@@ -86,18 +88,20 @@ CMTV_HD void btab_entry(uint32_t row[BTAB_ROW_WORDS], int m) {
   fe_mul(xy, x, y);
   fe_const_d2(d2);
   fe_mul(xy, xy, d2);
+  for (int i = 0; i < BTAB_ROW_WORDS; i++) row[i] = 0;
   for (int i = 0; i < 10; i++) {
     row[i] = ypx.v[i];
-    row[10 + i] = ymx.v[i];
-    row[20 + i] = xy.v[i];
+    row[BTAB_COORD_WORDS + i] = ymx.v[i];
+    row[2 * BTAB_COORD_WORDS + i] = xy.v[i];
   }
-  row[30] = 0;
-  row[31] = 0;
 }
 
 // acc = [s]B + [k]P  where the ATab holds (1..8)P in cached form.
-// ATab: .load(int e, ge_cached&) for e in 0..7 (multiple e+1).
-// BTab: .load(int e, ge_niels&) for e in 0..127 (multiple e+1).
+// ATab: .load_fe(int e, int c, fe&) for e in 0..7 (multiple e+1), c = cached coordinate.
+// BTab: .load_fe(int e, int c, fe&) for e in 0..127 (multiple e+1), c = niels coordinate.
+// Loops are kept rolled (#pragma unroll 1): the body is ~20 inlined field
+// multiplications, and the whole loop must stay resident in the instruction
+// cache that the CU's waves share.
 template <bool WITH_P, class ATab, class BTab>
 CMTV_HD void straus_double_scalarmult(ge_p3& out, const uint32_t k[8], const uint32_t s[8], const ATab& atab,
                                       const BTab& btab) {
@@ -108,52 +112,38 @@ CMTV_HD void straus_double_scalarmult(ge_p3& out, const uint32_t k[8], const uin
   p2_identity(cur);
   ge_p3 P;
   ge_efgh t;
-  for (int j = 0; j < 32; j++) {
-#pragma unroll
-    for (int half = 0; half < 2; half++) {
-      ge_cached ea;
-      int dA = 0;
-      if (WITH_P) {
-        dA = (int)sc_shift_out(tk, 4) - 8;
-        const int ia = dA < 0 ? -dA : dA;
-        atab.load(ia > 0 ? ia - 1 : 0, ea);
-        if (ia == 0) cached_identity(ea);
-      }
-      ge_niels eb;
-      int dB = 0;
-      if (half == 1) {
-        dB = (int)sc_shift_out(ts, 8) - 128;
-        const int ib = dB < 0 ? -dB : dB;
-        btab.load(ib > 0 ? ib - 1 : 0, eb);
-        if (ib == 0) niels_identity(eb);
-      }
+#pragma unroll 1
+  for (int w = 0; w < 64; w++) {
+#pragma unroll 1
+    for (int d = 0; d < 3; d++) {
       p2_dbl(t, cur);
-      efgh_to_p2(cur, t);
-      p2_dbl(t, cur);
-      efgh_to_p2(cur, t);
-      p2_dbl(t, cur);
-      efgh_to_p2(cur, t);
-      p2_dbl(t, cur);
-      if (WITH_P) {
-        efgh_to_p3(P, t);
-        ge_add_cached(t, P, ea, dA < 0);
-      }
-      if (half == 1) {
-        efgh_to_p3(P, t);
-        ge_add_niels(t, P, eb, dB < 0);
-      }
       efgh_to_p2(cur, t);
     }
+    p2_dbl(t, cur);
+    if (WITH_P) {
+      const int dA = (int)sc_shift_out(tk, 4) - 8;
+      const int ia = dA < 0 ? -dA : dA;
+      efgh_to_p3(P, t);
+      ge_add_table<true>(t, P, atab, ia > 0 ? ia - 1 : 0, dA < 0, ia == 0);
+    }
+    if (w & 1) {
+      const int dB = (int)sc_shift_out(ts, 8) - 128;
+      const int ib = dB < 0 ? -dB : dB;
+      efgh_to_p3(P, t);
+      ge_add_table<false>(t, P, btab, ib > 0 ? ib - 1 : 0, dB < 0, ib == 0);
+    }
+    efgh_to_p2(cur, t);
   }
   efgh_to_p3(out, t);
 }
 
-// Builds (1..8)P in cached form through the ATab's .store(e, cached).
+// Builds (1..8)P in cached form through the ATab (.store / .load_fe); P's own
+// cached form is re-read from entry 0 rather than kept in registers.
 template <class ATab>
 CMTV_HD void build_cached_table(ATab& atab, const ge_p3& P) {
-  ge_cached Pc, c;
-  p3_to_cached(Pc, P);
-  atab.store(0, Pc);
+  ge_cached c;
+  p3_to_cached(c, P);
+  atab.store(0, c);
   ge_efgh t;
   ge_p2 q;
   ge_p3 cur;
@@ -162,58 +152,69 @@ CMTV_HD void build_cached_table(ATab& atab, const ge_p3& P) {
   efgh_to_p3(cur, t);
   p3_to_cached(c, cur);
   atab.store(1, c);
+#pragma unroll 1
   for (int e = 2; e < 8; e++) {
-    ge_add_cached(t, cur, Pc, false);
+    ge_add_table<true>(t, cur, atab, 0, false, false);
     efgh_to_p3(cur, t);
     p3_to_cached(c, cur);
     atab.store(e, c);
   }
 }
 
-// Full single-signature verification. pk/sig as little-endian words.
+// Full single-signature verification. pk / sig are read through pointers
+// (little-endian 32-bit words) at the points they are needed, so neither is
+// held in registers across the scalar multiplication.
 template <uint32_t MODE, class ATab, class BTab>
-CMTV_HD bool verify_one(const uint32_t pkw[8], const uint32_t sigw[16], const uint8_t* msg, uint32_t mlen,
+CMTV_HD bool verify_one(const uint32_t* pk_ptr, const uint32_t* sig_ptr, const uint8_t* msg, uint32_t mlen,
                         ATab& atab, const BTab& btab) {
-  const uint32_t* Rw = sigw;
-  const uint32_t* Sw = sigw + 8;
-  bool ok = (Sw[7] & 0xE0000000u) == 0;  // sig[63] & 224
-  ok = ok && true;
-  const bool s_ok = sc_is_canonical(Sw);
-  ge_p3 A;
-  const bool a_ok = p3_frombytes(A, pkw);
-  ok = ok && s_ok && a_ok;
-
-  uint32_t pre[16], h[16], k[8];
+  uint32_t w[16];
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
-    pre[i] = Rw[i];
-    pre[8 + i] = pkw[i];
-  }
-  sha512_prefixed<16>(h, pre, msg, mlen);
-  sc_reduce512(k, h);
+  for (int i = 0; i < 8; i++) w[i] = sig_ptr[8 + i];  // S
+  bool ok = (w[7] & 0xE0000000u) == 0 && sc_is_canonical(w);  // sig[63] & 224, S < L
+  uint32_t ts[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) ts[i] = w[i];
 
+  ge_p3 A;
+#pragma unroll
+  for (int i = 0; i < 8; i++) w[i] = pk_ptr[i];
+  ok = p3_frombytes(A, w) && ok;
   ge_p3 nA;
   cached_neg_point(nA, A);
   build_cached_table(atab, nA);
-  ge_p3 Rp;
-  straus_double_scalarmult<true>(Rp, k, Sw, atab, btab);
 
+  uint32_t h[16], k[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    w[i] = sig_ptr[i];  // R
+    w[8 + i] = pk_ptr[i];
+  }
+  sha512_prefixed<16>(h, w, msg, mlen);
+  sc_reduce512(k, h);
+
+  ge_p3 Rp;
+  straus_double_scalarmult<true>(Rp, k, ts, atab, btab);
+
+#pragma unroll
+  for (int i = 0; i < 8; i++) w[i] = sig_ptr[i];  // R
   if (MODE == MODE_GO_STDLIB) {
     uint32_t enc[8];
     p3_tobytes(enc, Rp.X, Rp.Y, Rp.Z);
     uint32_t diff = 0;
 #pragma unroll
-    for (int i = 0; i < 8; i++) diff |= enc[i] ^ Rw[i];
+    for (int i = 0; i < 8; i++) diff |= enc[i] ^ w[i];
     return ok && diff == 0;
   } else {
     ge_p3 R;
-    const bool r_ok = p3_frombytes(R, Rw);
+    const bool r_ok = p3_frombytes(R, w);
     ge_cached Rc;
     p3_to_cached(Rc, R);
     ge_efgh t;
-    ge_add_cached(t, Rp, Rc, true);
+    cached_cneg(Rc, true);
+    ge_add_cached(t, Rp, Rc);
     ge_p2 q;
     efgh_to_p2(q, t);
+#pragma unroll 1
     for (int i = 0; i < 3; i++) {
       p2_dbl(t, q);
       efgh_to_p2(q, t);
@@ -239,7 +240,7 @@ CMTV_HD void expand_seed(uint32_t a_modl[8], uint32_t prefix[8], const uint32_t 
 }
 
 struct NullATab {
-  CMTV_HD void load(int, ge_cached&) const {}
+  CMTV_HD void load_fe(int, int, fe&) const {}
   CMTV_HD void store(int, const ge_cached&) {}
 };
 

@@ -100,7 +100,8 @@ int cmtv_verify_ed25519(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_
                         const uint32_t* msg_off, uint32_t mode, uint8_t* out_valid, uint64_t* out_bitmap);
 
 /* Same, all buffers already resident in device memory (HBM); enqueued on
- * `stream` (hipStream_t, NULL = the context stream), non-blocking. d_valid
+ * `stream` (a hipStream_t; NULL = the HIP null stream, as in every HIP API;
+ * cmtv_stream() gives the context's own stream), non-blocking. d_valid
  * (n bytes) and d_bitmap (ceil(n/64) words) may each be NULL. */
 int cmtv_verify_ed25519_device(cmtv_ctx* ctx, size_t n, const void* d_pk, const void* d_sig, const void* d_msg,
                                const void* d_msg_off, uint32_t mode, void* d_valid, void* d_bitmap, void* stream);

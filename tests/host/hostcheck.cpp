@@ -18,19 +18,17 @@ struct HostBTab {
   HostBTab() : rows(BTAB_ENTRIES * BTAB_ROW_WORDS) {
     for (int m = 1; m <= BTAB_ENTRIES; m++) btab_entry(&rows[(m - 1) * BTAB_ROW_WORDS], m);
   }
-  void load(int e, ge_niels& r) const {
-    const uint32_t* p = &rows[e * BTAB_ROW_WORDS];
-    for (int i = 0; i < 10; i++) {
-      r.ypx.v[i] = p[i];
-      r.ymx.v[i] = p[10 + i];
-      r.xy2d.v[i] = p[20 + i];
-    }
+  void load_fe(int e, int c, fe& r) const {
+    const uint32_t* p = &rows[e * BTAB_ROW_WORDS + c * BTAB_COORD_WORDS];
+    for (int i = 0; i < 10; i++) r.v[i] = p[i];
   }
 };
 
 struct HostATab {
   ge_cached t[8];
-  void load(int e, ge_cached& r) const { r = t[e]; }
+  void load_fe(int e, int c, fe& r) const {
+    r = c == 0 ? t[e].YpX : c == 1 ? t[e].YmX : c == 2 ? t[e].Z : t[e].T2d;
+  }
   void store(int e, const ge_cached& r) { t[e] = r; }
 };
 
@@ -69,14 +67,16 @@ int main(int argc, char** argv) {
     if (fread(&mode, 1, 1, stdin) != 1 || fread(pk, 32, 1, stdin) != 1 || fread(sig, 64, 1, stdin) != 1 ||
         fread(&mlen, 4, 1, stdin) != 1)
       return 1;
-    std::vector<uint8_t> msg(mlen + 1);
-    if (mlen && fread(msg.data(), mlen, 1, stdin) != 1) return 1;
+    // place the message at a varying misalignment (the device reads aligned words)
+    std::vector<uint8_t> buf(mlen + 16, 0xEE);
+    uint8_t* mp = buf.data() + 4 + (i % 4);
+    if (mlen && fread(mp, mlen, 1, stdin) != 1) return 1;
     uint32_t pkw[8], sigw[16];
     to_words(pkw, pk, 8);
     to_words(sigw, sig, 16);
     HostATab at;
-    bool v = mode ? verify_one<MODE_ZIP215>(pkw, sigw, msg.data(), mlen, at, bt)
-                  : verify_one<MODE_GO_STDLIB>(pkw, sigw, msg.data(), mlen, at, bt);
+    bool v = mode ? verify_one<MODE_ZIP215>(pkw, sigw, mp, mlen, at, bt)
+                  : verify_one<MODE_GO_STDLIB>(pkw, sigw, mp, mlen, at, bt);
     uint8_t o = v;
     fwrite(&o, 1, 1, stdout);
   }

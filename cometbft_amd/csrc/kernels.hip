@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include "kernels.h"
+#include "quad.h"
 #include "verify_core.h"
 
 // Minimum waves per SIMD the verify kernel is compiled for (the second
@@ -40,6 +41,43 @@ struct DevBTab {
     r.v[0] = a.x; r.v[1] = a.y; r.v[2] = a.z; r.v[3] = a.w;
     r.v[4] = b.x; r.v[5] = b.y; r.v[6] = b.z; r.v[7] = b.w;
     r.v[8] = d.x; r.v[9] = d.y;
+  }
+};
+
+// B-table access for the quad kernel: each lane reads its own coordinate
+// (word offset `off` inside the row) of entry e.
+struct DevBTabQ {
+  const uint32_t* __restrict__ rows;
+  __device__ __forceinline__ void load_coord(int e, int off, fe& r) const {
+    const uint32_t* p = rows + e * BTAB_ROW_WORDS + off;
+    const uint4 a = *reinterpret_cast<const uint4*>(p);
+    const uint4 b = *reinterpret_cast<const uint4*>(p + 4);
+    const uint2 d = *reinterpret_cast<const uint2*>(p + 8);
+    r.v[0] = a.x; r.v[1] = a.y; r.v[2] = a.z; r.v[3] = a.w;
+    r.v[4] = b.x; r.v[5] = b.y; r.v[6] = b.z; r.v[7] = b.w;
+    r.v[8] = d.x; r.v[9] = d.y;
+  }
+};
+
+// Quad policy (quad.h): 4 consecutive lanes = one signature; operand exchange
+// inside the quad is a DPP quad_perm move. update_dpp with old = src and
+// bound_ctrl off: the mov_dpp(bound_ctrl:1) form miscompiles on ROCm 7.2 /
+// gfx950 once DPP-combine folds it into the consumers (lanes 0-1 of a quad
+// read wrong values; found with tools/dbg/quad_debug.hip).
+struct DevQuad {
+  __device__ __forceinline__ int lane() const { return threadIdx.x & 3; }
+  template <int PAT>
+  __device__ __forceinline__ uint32_t dpp(uint32_t x) const {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, PAT, 0xF, 0xF, false);
+  }
+  template <int PAT>
+  __device__ __forceinline__ void perm(fe& o, const fe& v) const {
+#pragma unroll
+    for (int i = 0; i < 10; i++) o.v[i] = dpp<PAT>(v.v[i]);
+  }
+  template <int PAT>
+  __device__ __forceinline__ uint32_t perm32(uint32_t x) const {
+    return dpp<PAT>(x);
   }
 };
 
@@ -107,6 +145,36 @@ __global__ __launch_bounds__(64, CMTV_VERIFY_WAVES_PER_EU) void k_verify(uint32_
   if (threadIdx.x == 0 && out_bitmap) out_bitmap[gid >> 6] = mask;
 }
 
+// One signature per quad of lanes (quad.h): for batches too small to fill the
+// chip at one signature per lane, this cuts per-signature latency ~2x.
+// Verdict bits: lane 0 of each quad votes in a ballot; the 16 quad bits of a
+// wave are compacted into one 16-bit slice of the bitmap.
+template <uint32_t MODE>
+__global__ __launch_bounds__(64, 2) void k_verify_quad(uint32_t n, const uint32_t* __restrict__ pk,
+                                                       const uint32_t* __restrict__ sig,
+                                                       const uint8_t* __restrict__ msg,
+                                                       const uint32_t* __restrict__ off,
+                                                       const uint32_t* __restrict__ btab,
+                                                       uint8_t* __restrict__ out_valid,
+                                                       uint64_t* __restrict__ out_bitmap) {
+  const uint32_t gid = blockIdx.x * 64 + threadIdx.x;
+  const uint32_t s = gid >> 2;
+  const bool active = s < n;
+  const uint32_t i = active ? s : n - 1;
+  const uint32_t m0 = off[i], m1 = off[i + 1];
+  DevQuad q;
+  DevBTabQ bt{btab};
+  bool v = q_verify<MODE>(q, pk + 8 * (size_t)i, sig + 16 * (size_t)i, msg + m0, m1 - m0, bt);
+  v = v && active;
+  if (active && (threadIdx.x & 3) == 0 && out_valid) out_valid[s] = v ? 1 : 0;
+  uint64_t x = __ballot(v && (threadIdx.x & 3) == 0) & 0x1111111111111111ull;
+  x = (x | (x >> 3)) & 0x0303030303030303ull;
+  x = (x | (x >> 6)) & 0x000F000F000F000Full;
+  x = (x | (x >> 12)) & 0x000000FF000000FFull;
+  x = (x | (x >> 24)) & 0xFFFFull;
+  if (threadIdx.x == 0 && out_bitmap) reinterpret_cast<uint16_t*>(out_bitmap)[gid >> 6] = (uint16_t)x;
+}
+
 __global__ __launch_bounds__(64) void k_pubkey(uint32_t n, const uint32_t* __restrict__ seeds,
                                                const uint32_t* __restrict__ btab, uint32_t* __restrict__ out_pk) {
   const uint32_t gid = blockIdx.x * 64 + threadIdx.x;
@@ -144,15 +212,25 @@ hipError_t launch_btab_init(uint32_t* d_rows, hipStream_t s) {
 
 hipError_t launch_verify(uint32_t mode, uint32_t n, const void* pk, const void* sig, const void* msg,
                          const void* off, const uint32_t* btab, uint32_t* atab, void* valid, void* bitmap,
-                         hipStream_t s) {
+                         bool quad, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  const dim3 grid(blocks_for(n)), block(64);
   auto pkp = static_cast<const uint32_t*>(pk);
   auto sgp = static_cast<const uint32_t*>(sig);
   auto mp = static_cast<const uint8_t*>(msg);
   auto op = static_cast<const uint32_t*>(off);
   auto vp = static_cast<uint8_t*>(valid);
   auto bp = static_cast<uint64_t*>(bitmap);
+  if (quad) {
+    // one 64-lane block = 16 signatures; whole groups of 4 blocks so every
+    // 16-bit slice of every bitmap word is written
+    const dim3 grid(((n + 63) / 64) * 4), block(64);
+    if (mode == MODE_ZIP215)
+      hipLaunchKernelGGL(k_verify_quad<MODE_ZIP215>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp);
+    else
+      hipLaunchKernelGGL(k_verify_quad<MODE_GO_STDLIB>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp);
+    return hipGetLastError();
+  }
+  const dim3 grid(blocks_for(n)), block(64);
   if (mode == MODE_ZIP215)
     hipLaunchKernelGGL(k_verify<MODE_ZIP215>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, atab, vp, bp);
   else

@@ -1,0 +1,305 @@
+// quad.h -- 4 lanes per signature ("quad"): coordinate-parallel edwards25519
+// arithmetic for latency-bound batches (a 10k-signature commit fills only
+// ~157 of the chip's 1,024 SIMDs at one signature per lane).
+//
+// Lane c of a quad holds coordinate c of every point:
+//   extended point  (X, Y, Z, T)            lane 0: X, 1: Y, 2: Z, 3: T
+//   cached addend   (Y-X, Y+X, Z, 2dT)      ordered so lane c's product in
+//                                           round 1 of an addition is local
+// A doubling or an addition is two rounds of ONE field multiplication per
+// lane (HWCD 4-way formulas) instead of 7-8 sequential multiplications, with
+// operands exchanged inside the quad by DPP quad_perm moves (a VALU operand
+// modifier on gfx950, no LDS round trip).
+//
+// Everything is written against a Quad policy:
+//   int lane() const;                               this lane's coordinate index
+//   template <int PAT> void perm(fe& o, const fe& v) const;
+//                          lane c receives v from lane (PAT >> 2c) & 3
+//   template <int PAT> uint32_t perm32(uint32_t x) const;
+// The device policy lowers perm to v_mov_b32_dpp quad_perm; the host test
+// policy (tests/host/quadcheck.cpp) runs 4 threads in lockstep, so the same
+// source is checked against the oracle on the CPU.
+//
+// Control flow is uniform across a quad (digits, verdicts and mode are per
+// signature); only data differs per lane, via pick() selects.
+#pragma once
+#include "verify_core.h"
+
+namespace cmtv {
+
+// quad_perm codes
+constexpr int QP_B0 = 0x00, QP_B1 = 0x55, QP_B2 = 0xAA, QP_B3 = 0xFF;  // broadcast lane k
+constexpr int QP_SWAP01 = (1 << 0) | (0 << 2) | (2 << 4) | (3 << 6);    // [1,0,2,3]
+
+// h = {a, b, c, d}[lane]
+CMTV_HD void fe_pick(fe& h, int lane, const fe& a, const fe& b, const fe& c, const fe& d) {
+  const bool l1 = lane & 1, l2 = lane & 2;
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    const uint32_t lo = l1 ? b.v[i] : a.v[i];
+    const uint32_t hi = l1 ? d.v[i] : c.v[i];
+    h.v[i] = l2 ? hi : lo;
+  }
+}
+
+// the identity point's coordinate for this lane: (0, 1, 1, 0)
+CMTV_HD void q_identity(fe& v, int lane) {
+  fe_0(v);
+  v.v[0] = (lane == 1 || lane == 2) ? 1u : 0u;
+}
+
+// the identity's cached coordinate: (Y-X, Y+X, Z, 2dT) = (1, 1, 1, 0)
+CMTV_HD void q_cached_identity(fe& v, int lane) {
+  fe_0(v);
+  v.v[0] = (lane != 3) ? 1u : 0u;
+}
+
+// Doubling (dbl-2008-hwcd, a = -1, outputs negated as in ge25519.h p2_dbl):
+//   round 1: lane c squares {X, Y, Z, X+Y}[c]      -> A, B, C', K
+//   round 2: lane c multiplies {E'F', MS, F'M, E'S}[c]
+// Input T (lane 3) is ignored; output is a full extended point.
+template <class Q>
+CMTV_HD void q_dbl(const Q& q, fe& v) {
+  const int lane = q.lane();
+  fe a, b, m;
+  q.template perm<QP_B0>(a, v);
+  q.template perm<QP_B1>(b, v);
+  fe_add(a, a, b);  // X + Y
+  fe_select(m, v, a, lane == 3);
+  fe_sq(m, m);
+  fe S, M, E, F;
+  q.template perm<QP_B0>(a, m);  // A = X^2
+  q.template perm<QP_B1>(b, m);  // B = Y^2
+  fe_add(S, a, b);
+  fe_carry(S);                   // S = A + B
+  fe_sub(M, a, b);               // M = A - B
+  q.template perm<QP_B3>(a, m);  // K = (X+Y)^2
+  fe_sub(E, S, a);               // E' = S - K
+  q.template perm<QP_B2>(b, m);  // C' = Z^2
+  fe_add(F, b, b);
+  fe_add(F, F, M);
+  fe_carry(F);                   // F' = 2C' + M
+  fe_pick(a, lane, E, M, F, E);
+  fe_pick(b, lane, F, S, M, S);
+  fe_mul(v, a, b);
+}
+
+// Addition v += Q where c is this lane's coordinate of Q in cached form
+// (Y2-X2, Y2+X2, Z2, 2dT2); for an affine niels addend pass Z2 = 1.
+//   round 1: lane c computes {(Y1-X1)(Y2-X2), (Y1+X1)(Y2+X2), Z1 Z2, T1 2dT2}[c]
+//   round 2: lane c computes {EF, GH, FG, EH}[c]
+template <class Q>
+CMTV_HD void q_add(const Q& q, fe& v, const fe& c) {
+  const int lane = q.lane();
+  fe x, y, t;
+  q.template perm<QP_B0>(x, v);
+  q.template perm<QP_B1>(y, v);
+  fe_sub(t, y, x);
+  fe_add(y, y, x);
+  fe_pick(x, lane, t, y, v, v);
+  fe_mul(t, x, c);
+  fe A, B, D, C;
+  q.template perm<QP_B0>(A, t);
+  q.template perm<QP_B1>(B, t);
+  q.template perm<QP_B2>(D, t);
+  q.template perm<QP_B3>(C, t);
+  fe_add(D, D, D);
+  fe_carry(D);
+  fe E, H;
+  fe_sub(E, B, A);
+  fe_add(H, B, A);
+  fe_sub(A, D, C);  // F
+  fe_add(B, D, C);  // G
+  fe_pick(x, lane, E, B, A, E);
+  fe_pick(y, lane, A, H, B, H);
+  fe_mul(v, x, y);
+}
+
+// this lane's cached-form coordinate of the extended point v
+template <class Q>
+CMTV_HD void q_to_cached(const Q& q, fe& c, const fe& v) {
+  const int lane = q.lane();
+  fe x, y, s, d2;
+  q.template perm<QP_B0>(x, v);
+  q.template perm<QP_B1>(y, v);
+  fe_sub(s, y, x);
+  fe_add(y, y, x);
+  fe_const_d2(d2);
+  fe_mul(d2, v, d2);
+  fe_pick(c, lane, s, y, v, d2);
+}
+
+// conditional negation of a cached addend: swap (Y-X, Y+X), negate 2dT
+template <class Q>
+CMTV_HD void q_cached_cneg(const Q& q, fe& c, bool neg) {
+  fe s, n;
+  q.template perm<QP_SWAP01>(s, c);
+  fe_neg(n, c);
+  fe_select(s, s, n, q.lane() == 3);
+  fe_select(c, c, s, neg);
+}
+
+}  // namespace cmtv
+
+namespace cmtv {
+
+// y (255 bits, sign stripped) < p ?  -- the canonical-encoding test for R
+CMTV_HD bool y_is_canonical(const uint32_t w[8]) {
+  const uint32_t top = w[7] & 0x7FFFFFFFu;
+  bool all_ones = top == 0x7FFFFFFFu;
+#pragma unroll
+  for (int i = 1; i < 7; i++) all_ones = all_ones && w[i] == 0xFFFFFFFFu;
+  return !(all_ones && w[0] >= 0xFFFFFFEDu);
+}
+
+// One signature per quad. Every lane returns the same verdict.
+//   phase 1: lanes {0,2} decode A, lanes {1,3} decode R (same code, different
+//            data, so the two square-root chains run simultaneously); every
+//            lane hashes k = SHA-512(R || A || M) mod L
+//   phase 2: (1..8)(-A) in cached form, one coordinate per lane, in registers
+//   phase 3: Straus over signed radix-16 (k) / radix-256 (s) digits
+//   final  : GO_STDLIB -- R canonical and R' == R projectively (equivalent to
+//            encode(R') == R bytes, with no inversion); ZIP215 -- [8](R' - R) == O
+struct NullProbe {
+  CMTV_HD void snap(int, const fe&) const {}
+};
+
+template <uint32_t MODE, class Q, class BTab, class Probe = NullProbe>
+CMTV_HD bool q_verify(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig_ptr, const uint8_t* msg,
+                      uint32_t mlen, const BTab& btab, const Probe& probe = Probe()) {
+  const int lane = q.lane();
+  uint32_t w[16];
+#pragma unroll
+  for (int i = 0; i < 8; i++) w[i] = sig_ptr[8 + i];
+  const bool s_ok = (w[7] & 0xE0000000u) == 0 && sc_is_canonical(w);
+  uint32_t ts[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) ts[i] = w[i];
+
+  // ---- phase 1: decode A (even lanes) and R (odd lanes)
+  const uint32_t* src = (lane & 1) ? sig_ptr : pk_ptr;
+#pragma unroll
+  for (int i = 0; i < 8; i++) w[i] = src[i];
+  fe v, rc;
+  bool a_ok, r_ok, r_canon;
+  {
+    ge_p3 P;
+    const bool dec = p3_frombytes(P, w);
+    const bool canon = y_is_canonical(w) && !(fe_iszero(P.X) && (w[7] >> 31));
+    fe x, y, t, one;
+    fe_1(one);
+    q.template perm<QP_B0>(x, P.X);
+    q.template perm<QP_B0>(y, P.Y);
+    q.template perm<QP_B0>(t, P.T);
+    fe_pick(v, lane, x, y, one, t);  // A
+    q.template perm<QP_B1>(x, P.X);
+    q.template perm<QP_B1>(y, P.Y);
+    q.template perm<QP_B1>(t, P.T);
+    fe_pick(rc, lane, x, y, one, t);  // R
+    a_ok = q.template perm32<QP_B0>(dec ? 1u : 0u) != 0;
+    r_ok = q.template perm32<QP_B1>(dec ? 1u : 0u) != 0;
+    r_canon = q.template perm32<QP_B1>(canon ? 1u : 0u) != 0;
+    // -A: negate X (lane 0) and T (lane 3)
+    fe_neg(t, v);
+    fe_carry(t);
+    fe_select(v, v, t, lane == 0 || lane == 3);
+  }
+  probe.snap(0, v);
+  probe.snap(1, rc);
+  uint32_t k[8];
+  {
+    uint32_t h[16];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      w[i] = sig_ptr[i];
+      w[8 + i] = pk_ptr[i];
+    }
+    sha512_prefixed<16>(h, w, msg, mlen);
+    sc_reduce512(k, h);
+  }
+  {
+    fe kk;
+#pragma unroll
+    for (int i = 0; i < 8; i++) kk.v[i] = k[i];
+    kk.v[8] = s_ok | (a_ok << 1) | (r_ok << 2) | (r_canon << 3);
+    kk.v[9] = 0;
+    probe.snap(2, kk);
+  }
+
+  // ---- phase 2: (1..8)(-A), this lane's cached coordinate of each
+  fe tab[8];
+  q_to_cached(q, tab[0], v);
+  q_dbl(q, v);
+  q_to_cached(q, tab[1], v);
+#pragma unroll
+  for (int e = 2; e < 8; e++) {
+    q_add(q, v, tab[0]);
+    q_to_cached(q, tab[e], v);
+  }
+  probe.snap(3, tab[0]);
+  probe.snap(4, tab[1]);
+  probe.snap(5, tab[7]);
+
+  // ---- phase 3: Straus
+  uint32_t tk[8];
+  sc_bias(tk, k, 0x88888888u);
+  sc_bias(ts, ts, 0x80808080u);
+  q_identity(v, lane);
+  // lane -> offset of its niels coordinate in a B-table row (y-x, y+x, 1, 2dxy)
+  const int boff = lane == 0 ? BTAB_COORD_WORDS : (lane == 3 ? 2 * BTAB_COORD_WORDS : 0);
+#pragma unroll 1
+  for (int win = 0; win < 64; win++) {
+#pragma unroll 1
+    for (int d = 0; d < 4; d++) q_dbl(q, v);
+    {
+      const int dA = (int)sc_shift_out(tk, 4) - 8;
+      const int ia = dA < 0 ? -dA : dA;
+      fe c;
+      q_cached_identity(c, lane);
+#pragma unroll
+      for (int e = 0; e < 8; e++) fe_select(c, c, tab[e], ia == e + 1);
+      q_cached_cneg(q, c, dA < 0);
+      q_add(q, v, c);
+    }
+    if (win & 1) {
+      const int dB = (int)sc_shift_out(ts, 8) - 128;
+      const int ib = dB < 0 ? -dB : dB;
+      fe c;
+      btab.load_coord(ib > 0 ? ib - 1 : 0, boff, c);
+      const bool one = lane == 2 || (ib == 0 && lane != 3);
+#pragma unroll
+      for (int i = 0; i < 10; i++) c.v[i] = (ib == 0 || lane == 2) ? ((one && i == 0) ? 1u : 0u) : c.v[i];
+      q_cached_cneg(q, c, dB < 0);
+      q_add(q, v, c);
+    }
+    if (win < 4) probe.snap(6 + win, v);
+  }
+  probe.snap(10, v);
+
+  // ---- final check
+  if (MODE == MODE_GO_STDLIB) {
+    fe z, t;
+    q.template perm<QP_B2>(z, v);  // Z'
+    fe_mul(t, z, rc);              // lane 0: x_R Z', lane 1: y_R Z'
+    const bool eq = fe_equal(t, v);
+    const bool e0 = q.template perm32<QP_B0>(eq ? 1u : 0u) != 0;
+    const bool e1 = q.template perm32<QP_B1>(eq ? 1u : 0u) != 0;
+    return s_ok && a_ok && r_ok && r_canon && e0 && e1;
+  } else {
+    fe c;
+    q_to_cached(q, c, rc);
+    q_cached_cneg(q, c, true);
+    q_add(q, v, c);
+#pragma unroll 1
+    for (int d = 0; d < 3; d++) q_dbl(q, v);
+    fe z;
+    q.template perm<QP_B2>(z, v);
+    const bool x0 = fe_iszero(v);      // meaningful on lane 0
+    const bool yz = fe_equal(v, z);    // meaningful on lane 1
+    const bool e0 = q.template perm32<QP_B0>(x0 ? 1u : 0u) != 0;
+    const bool e1 = q.template perm32<QP_B1>(yz ? 1u : 0u) != 0;
+    return s_ok && a_ok && r_ok && e0 && e1;
+  }
+}
+
+}  // namespace cmtv

@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -22,6 +23,9 @@
 namespace {
 
 constexpr uint32_t kChunk = 1u << 18;  // signatures per launch (A-table scratch = kChunk * 1280 B)
+// crossover between the quad (4 lanes / signature) and lane (1 lane / signature)
+// kernels; measured on MI355X, overridable with CMTV_QUAD_MAX
+constexpr size_t kQuadMaxDefault = 40000;
 
 struct DevBuf {
   void* p = nullptr;
@@ -78,6 +82,7 @@ struct cmtv_ctx {
   HostBuf h_in, h_out;
   std::mutex mu;
   cmtv_stats stats{};
+  size_t quad_max = kQuadMaxDefault;  // batches up to this size use the quad kernel
 };
 
 namespace cmtv {
@@ -104,17 +109,23 @@ static int enqueue_verify(cmtv_ctx* ctx, size_t n, const uint8_t* d_pk, const ui
                           const uint32_t* d_off, uint32_t mode, uint8_t* d_valid, uint64_t* d_bitmap,
                           hipStream_t s) {
   if (n == 0) return CMTV_OK;
-  const size_t lanes = std::min<size_t>(n, kChunk);
-  const size_t lanes_padded = (lanes + 63) / 64 * 64;
-  hipError_t e = ctx->d_atab.ensure(lanes_padded * kAtabWordsPerLane * sizeof(uint32_t));
-  if (e != hipSuccess) return hip_fail(e);
+  // Small batches cannot fill the chip at one signature per lane: use the
+  // 4-lanes-per-signature kernel below the crossover (quad.h).
+  const bool quad = n <= ctx->quad_max;
+  hipError_t e = hipSuccess;
+  if (!quad) {
+    const size_t lanes = std::min<size_t>(n, kChunk);
+    const size_t lanes_padded = (lanes + 63) / 64 * 64;
+    e = ctx->d_atab.ensure(lanes_padded * kAtabWordsPerLane * sizeof(uint32_t));
+    if (e != hipSuccess) return hip_fail(e);
+  }
   harvest_timing(ctx);
   if ((e = hipEventRecord(ctx->ev0, s)) != hipSuccess) return hip_fail(e);
   for (size_t c = 0; c < n; c += kChunk) {
     const uint32_t cn = (uint32_t)std::min<size_t>(kChunk, n - c);
     e = launch_verify(mode, cn, d_pk + 32 * c, d_sig + 64 * c, d_msg, d_off + c, ctx->d_btab,
                       static_cast<uint32_t*>(ctx->d_atab.p), d_valid ? d_valid + c : nullptr,
-                      d_bitmap ? d_bitmap + c / 64 : nullptr, s);
+                      d_bitmap ? d_bitmap + c / 64 : nullptr, quad, s);
     if (e != hipSuccess) return hip_fail(e);
     ctx->stats.kernel_launches++;
   }
@@ -215,6 +226,7 @@ int cmtv_open(const cmtv_config* cfg, cmtv_ctx** out) {
   if (!ctx) return CMTV_ENOMEM;
   ctx->device = dev;
   ctx->default_mode = cfg ? cfg->default_mode : CMTV_MODE_GO_STDLIB;
+  if (const char* qm = std::getenv("CMTV_QUAD_MAX")) ctx->quad_max = (size_t)std::strtoull(qm, nullptr, 10);
   hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&ctx->ev0);
   if (e == hipSuccess) e = hipEventCreate(&ctx->ev1);

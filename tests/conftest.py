@@ -37,3 +37,24 @@ def gpu_ctx():
     from cometbft_amd import Context
 
     return Context(device=0)
+
+
+@pytest.fixture(scope="session")
+def gpu_ctx_lane():
+    """A context that always uses the one-signature-per-lane kernel
+    (CMTV_QUAD_MAX=0), so small batches exercise both kernels."""
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from cometbft_amd import Context
+
+    old = os.environ.get("CMTV_QUAD_MAX")
+    os.environ["CMTV_QUAD_MAX"] = "0"
+    try:
+        return Context(device=0)
+    finally:
+        if old is None:
+            del os.environ["CMTV_QUAD_MAX"]
+        else:
+            os.environ["CMTV_QUAD_MAX"] = old

@@ -1,0 +1,92 @@
+// Host emulation of the 4-lane quad kernel (cometbft_amd/csrc/quad.h): four
+// std::threads run the same source in lockstep and exchange DPP quad_perm
+// operands through a barrier. Test infrastructure only.
+//   stdin/stdout protocol as hostcheck.cpp (verify mode only).
+#define CMTV_HD inline
+#define CMTV_BOUNDS_CHECK 1
+#include <barrier>
+#include <cstdio>
+#include <cstring>
+#include <thread>
+#include <vector>
+#include "../../cometbft_amd/csrc/quad.h"
+
+using namespace cmtv;
+
+struct Exchange {
+  std::barrier<> bar{4};
+  fe slot[4];
+};
+
+struct HostQuad {
+  int ln;
+  Exchange* ex;
+  int lane() const { return ln; }
+  template <int PAT>
+  void perm(fe& o, const fe& v) const {
+    ex->slot[ln] = v;
+    ex->bar.arrive_and_wait();
+    const fe r = ex->slot[(PAT >> (2 * ln)) & 3];
+    ex->bar.arrive_and_wait();
+    o = r;
+  }
+  template <int PAT>
+  uint32_t perm32(uint32_t x) const {
+    fe t, o;
+    fe_0(t);
+    t.v[0] = x;
+    perm<PAT>(o, t);
+    return o.v[0];
+  }
+};
+
+struct HostBTab {
+  std::vector<uint32_t> rows;
+  HostBTab() : rows(BTAB_ENTRIES * BTAB_ROW_WORDS) {
+    for (int m = 1; m <= BTAB_ENTRIES; m++) btab_entry(&rows[(m - 1) * BTAB_ROW_WORDS], m);
+  }
+  void load_coord(int e, int off, fe& r) const {
+    const uint32_t* p = &rows[e * BTAB_ROW_WORDS + off];
+    for (int i = 0; i < 10; i++) r.v[i] = p[i];
+  }
+};
+
+static void to_words(uint32_t* w, const uint8_t* b, int nw) {
+  for (int i = 0; i < nw; i++) w[i] = b[4 * i] | (b[4 * i + 1] << 8) | (b[4 * i + 2] << 16) | ((uint32_t)b[4 * i + 3] << 24);
+}
+
+int main() {
+  HostBTab bt;
+  uint32_t n;
+  if (fread(&n, 4, 1, stdin) != 1) return 1;
+  for (uint32_t i = 0; i < n; i++) {
+    uint8_t mode, pk[32], sig[64];
+    uint32_t mlen;
+    if (fread(&mode, 1, 1, stdin) != 1 || fread(pk, 32, 1, stdin) != 1 || fread(sig, 64, 1, stdin) != 1 ||
+        fread(&mlen, 4, 1, stdin) != 1)
+      return 1;
+    std::vector<uint8_t> buf(mlen + 16, 0xEE);
+    uint8_t* mp = buf.data() + 4 + (i % 4);
+    if (mlen && fread(mp, mlen, 1, stdin) != 1) return 1;
+    uint32_t pkw[8], sigw[16];
+    to_words(pkw, pk, 8);
+    to_words(sigw, sig, 16);
+    Exchange ex;
+    bool res[4];
+    std::vector<std::thread> th;
+    for (int l = 0; l < 4; l++)
+      th.emplace_back([&, l] {
+        HostQuad q{l, &ex};
+        res[l] = mode ? q_verify<MODE_ZIP215>(q, pkw, sigw, mp, mlen, bt)
+                      : q_verify<MODE_GO_STDLIB>(q, pkw, sigw, mp, mlen, bt);
+      });
+    for (auto& t : th) t.join();
+    if (res[0] != res[1] || res[0] != res[2] || res[0] != res[3]) {
+      fprintf(stderr, "lanes disagree on vector %u\n", i);
+      return 2;
+    }
+    uint8_t o = res[0];
+    fwrite(&o, 1, 1, stdout);
+  }
+  return 0;
+}

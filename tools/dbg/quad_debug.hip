@@ -1,0 +1,209 @@
+// Debug tool: runs the quad pipeline (quad.h) for one signature on the GPU and
+// under the host lockstep emulation, and reports the first probe snapshot
+// where they differ. Also prints DPP quad_perm semantics.
+#include <hip/hip_runtime.h>
+
+#include <barrier>
+#include <cstdio>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "../../cometbft_amd/csrc/quad.h"
+
+using namespace cmtv;
+
+constexpr int NSNAP = 11;
+
+template <int VAR>
+struct DevQuad {
+  __device__ int lane() const { return threadIdx.x & 3; }
+  template <int PAT>
+  __device__ uint32_t one(uint32_t x) const {
+    if (VAR == 0) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, PAT, 0xF, 0xF, true);
+    if (VAR == 1) return (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, PAT, 0xF, 0xF, false);
+    if (VAR == 2) {
+      const int src = (threadIdx.x & ~3) | ((PAT >> (2 * (threadIdx.x & 3))) & 3);
+      return (uint32_t)__shfl((int)x, src, 64);
+    }
+    // VAR 3: ds_swizzle in quad-perm mode (offset bit 15 = 1: QDMode)
+    return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x8000 | PAT);
+  }
+  template <int PAT>
+  __device__ void perm(fe& o, const fe& v) const {
+    for (int i = 0; i < 10; i++) o.v[i] = one<PAT>(v.v[i]);
+  }
+  template <int PAT>
+  __device__ uint32_t perm32(uint32_t x) const { return one<PAT>(x); }
+};
+struct DevBTabQ {
+  const uint32_t* rows;
+  __device__ void load_coord(int e, int off, fe& r) const {
+    const uint32_t* p = rows + e * BTAB_ROW_WORDS + off;
+    for (int i = 0; i < 10; i++) r.v[i] = p[i];
+  }
+};
+struct DevProbe {
+  uint32_t* out;
+  __device__ void snap(int id, const fe& v) const {
+    if (threadIdx.x < 4)
+      for (int i = 0; i < 10; i++) out[(id * 4 + threadIdx.x) * 10 + i] = v.v[i];
+  }
+};
+
+__global__ void k_btab(uint32_t* rows) {
+  int m = threadIdx.x + 1;
+  if (m <= BTAB_ENTRIES) btab_entry(rows + (m - 1) * BTAB_ROW_WORDS, m);
+}
+
+template <int VAR>
+__global__ void k_probe(const uint32_t* pk, const uint32_t* sig, const uint8_t* msg, uint32_t mlen,
+                        const uint32_t* btab, uint32_t* snaps, int* verdict) {
+  DevQuad<VAR> q;
+  DevBTabQ bt{btab};
+  DevProbe pr{snaps};
+  bool v = q_verify<MODE_GO_STDLIB>(q, pk, sig, msg, mlen, bt, pr);
+  verdict[threadIdx.x] = v;
+}
+
+template <int PAT>
+__global__ void k_dpp(int* out) {
+  out[threadIdx.x] = __builtin_amdgcn_mov_dpp((int)(threadIdx.x * 10), PAT, 0xF, 0xF, true);
+}
+
+struct Exchange {
+  std::barrier<> bar{4};
+  fe slot[4];
+};
+struct HostQuad {
+  int ln;
+  Exchange* ex;
+  int lane() const { return ln; }
+  template <int PAT>
+  void perm(fe& o, const fe& v) const {
+    ex->slot[ln] = v;
+    ex->bar.arrive_and_wait();
+    const fe r = ex->slot[(PAT >> (2 * ln)) & 3];
+    ex->bar.arrive_and_wait();
+    o = r;
+  }
+  template <int PAT>
+  uint32_t perm32(uint32_t x) const {
+    fe t, o;
+    fe_0(t);
+    t.v[0] = x;
+    perm<PAT>(o, t);
+    return o.v[0];
+  }
+};
+struct HostBTabQ {
+  const uint32_t* rows;
+  void load_coord(int e, int off, fe& r) const {
+    for (int i = 0; i < 10; i++) r.v[i] = rows[e * BTAB_ROW_WORDS + off + i];
+  }
+};
+struct HostProbe {
+  uint32_t* out;
+  int ln;
+  void snap(int id, const fe& v) const {
+    for (int i = 0; i < 10; i++) out[(id * 4 + ln) * 10 + i] = v.v[i];
+  }
+};
+
+static void hex2w(uint32_t* w, const char* hex, int nw) {
+  for (int i = 0; i < 4 * nw; i++) {
+    unsigned b;
+    sscanf(hex + 2 * i, "%2x", &b);
+    ((uint8_t*)w)[i] = (uint8_t)b;
+  }
+}
+
+int main() {
+  {
+    int* d;
+    (void)hipMalloc(&d, 256);
+    int h[64];
+    hipLaunchKernelGGL(k_dpp<0x55>, dim3(1), dim3(64), 0, 0, d);
+    (void)hipMemcpy(h, d, 256, hipMemcpyDeviceToHost);
+    printf("dpp B1:");
+    for (int i = 0; i < 8; i++) printf(" %d", h[i]);
+    hipLaunchKernelGGL(k_dpp<(1 | (0 << 2) | (2 << 4) | (3 << 6))>, dim3(1), dim3(64), 0, 0, d);
+    (void)hipMemcpy(h, d, 256, hipMemcpyDeviceToHost);
+    printf("\ndpp SWAP01:");
+    for (int i = 0; i < 8; i++) printf(" %d", h[i]);
+    printf("\n");
+  }
+  // RFC 8032 test 2
+  uint32_t pk[8], sig[16];
+  hex2w(pk, "3d4017c3e843895a92b70aa74d1b7ebc9c982ccf2ec4968cc0cd55f12af4660c", 8);
+  hex2w(sig, "92a009a9f0d4cab8720e820b5f642540a2b27b5416503f8fb3762223ebdb69da085ac1e43e15996e458f3613d0f11d8c387b2eaeb4302aeeb00d291612bb0c00", 16);
+  uint8_t msg[4] = {0x72, 0, 0, 0};
+  uint32_t mlen = 1;
+
+  std::vector<uint32_t> btab(BTAB_ENTRIES * BTAB_ROW_WORDS);
+  for (int m = 1; m <= BTAB_ENTRIES; m++) btab_entry(&btab[(m - 1) * BTAB_ROW_WORDS], m);
+
+  // host emulation
+  std::vector<uint32_t> hs(NSNAP * 40, 0);
+  bool hres[4];
+  {
+    Exchange ex;
+    std::vector<std::thread> th;
+    for (int l = 0; l < 4; l++)
+      th.emplace_back([&, l] {
+        HostQuad q{l, &ex};
+        HostBTabQ bt{btab.data()};
+        HostProbe pr{hs.data(), l};
+        hres[l] = q_verify<MODE_GO_STDLIB>(q, pk, sig, msg, mlen, bt, pr);
+      });
+    for (auto& t : th) t.join();
+  }
+  // device
+  uint32_t *dpk, *dsig, *dbt, *dsn;
+  uint8_t* dmsg;
+  int* dv;
+  (void)hipMalloc(&dpk, 32);
+  (void)hipMalloc(&dsig, 64);
+  (void)hipMalloc(&dmsg, 16);
+  (void)hipMalloc(&dbt, btab.size() * 4);
+  (void)hipMalloc(&dsn, NSNAP * 40 * 4);
+  (void)hipMalloc(&dv, 64 * 4);
+  (void)hipMemcpy(dpk, pk, 32, hipMemcpyHostToDevice);
+  (void)hipMemcpy(dsig, sig, 64, hipMemcpyHostToDevice);
+  (void)hipMemcpy(dmsg, msg, 4, hipMemcpyHostToDevice);
+  // device-built table must equal the host-built one
+  hipLaunchKernelGGL(k_btab, dim3(1), dim3(128), 0, 0, dbt);
+  std::vector<uint32_t> dbtab(btab.size());
+  (void)hipMemcpy(dbtab.data(), dbt, btab.size() * 4, hipMemcpyDeviceToHost);
+  printf("btab device==host: %d\n", (int)(dbtab == btab));
+  auto run = [&](auto kern, const char* name) {
+    (void)hipMemset(dsn, 0, NSNAP * 40 * 4);
+    hipLaunchKernelGGL(kern, dim3(1), dim3(64), 0, 0, dpk, dsig, dmsg, mlen, dbt, dsn, dv);
+    std::vector<uint32_t> ds(NSNAP * 40);
+    int dres[64];
+    (void)hipMemcpy(ds.data(), dsn, ds.size() * 4, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(dres, dv, 256, hipMemcpyDeviceToHost);
+    printf("[%s] host verdict %d%d%d%d device verdict %d%d%d%d\n", name, hres[0], hres[1], hres[2], hres[3], dres[0],
+           dres[1], dres[2], dres[3]);
+    for (int id = 0; id < NSNAP; id++) {
+      bool same = true;
+      for (int j = 0; j < 40; j++) same = same && hs[id * 40 + j] == ds[id * 40 + j];
+      if (!same) {
+        printf("  first diff at snap %d\n", id);
+        for (int l = 0; l < 4; l++) {
+          printf("  lane %d host:", l);
+          for (int i = 0; i < 10; i++) printf(" %07x", hs[(id * 4 + l) * 10 + i]);
+          printf("\n  lane %d dev :", l);
+          for (int i = 0; i < 10; i++) printf(" %07x", ds[(id * 4 + l) * 10 + i]);
+          printf("\n");
+        }
+        break;
+      }
+    }
+  };
+  run(k_probe<0>, "mov_dpp");
+  run(k_probe<1>, "update_dpp");
+  run(k_probe<2>, "shfl");
+  run(k_probe<3>, "ds_swizzle");
+  return 0;
+}

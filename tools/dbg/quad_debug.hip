@@ -50,6 +50,25 @@ struct DevProbe {
       for (int i = 0; i < 10; i++) out[(id * 4 + threadIdx.x) * 10 + i] = v.v[i];
   }
 };
+// timing probe: s_memtime at every snapshot point (lane 0 writes)
+struct TimeProbe {
+  unsigned long long* out;
+  __device__ void snap(int id, const fe& v) const {
+    asm volatile("" ::"v"(v.v[0]));
+    unsigned long long t = __builtin_amdgcn_s_memtime();
+    if (threadIdx.x == 0) out[id] = t;
+  }
+};
+__global__ void k_time(const uint32_t* pk, const uint32_t* sig, const uint8_t* msg, uint32_t mlen,
+                       const uint32_t* btab, unsigned long long* ts, int* verdict) {
+  DevQuad<1> q;
+  DevBTabQ bt{btab};
+  if (threadIdx.x == 0) ts[15] = __builtin_amdgcn_s_memtime();
+  TimeProbe pr{ts};
+  bool v = q_verify<MODE_GO_STDLIB>(q, pk, sig, msg, mlen, bt, pr);
+  verdict[threadIdx.x] = v;
+  if (threadIdx.x == 0) ts[14] = __builtin_amdgcn_s_memtime();
+}
 
 __global__ void k_btab(uint32_t* rows) {
   int m = threadIdx.x + 1;
@@ -201,6 +220,18 @@ int main() {
       }
     }
   };
+  {
+    unsigned long long* dts;
+    (void)hipMalloc(&dts, 16 * 8);
+    for (int rep = 0; rep < 3; rep++) {
+      hipLaunchKernelGGL(k_time, dim3(1), dim3(64), 0, 0, dpk, dsig, dmsg, mlen, dbt, dts, dv);
+      unsigned long long ts[16];
+      (void)hipMemcpy(ts, dts, 16 * 8, hipMemcpyDeviceToHost);
+      printf("cycles: decode %llu sha %llu table %llu win0 %llu win1 %llu win2 %llu win3 %llu loop(64) %llu final %llu total %llu\n",
+             ts[0] - ts[15], ts[2] - ts[1], ts[3] - ts[2], ts[6] - ts[5], ts[7] - ts[6], ts[8] - ts[7], ts[9] - ts[8],
+             ts[10] - ts[5], ts[14] - ts[10], ts[14] - ts[15]);
+    }
+  }
   run(k_probe<0>, "mov_dpp");
   run(k_probe<1>, "update_dpp");
   run(k_probe<2>, "shfl");

@@ -7,8 +7,8 @@ C++ replay of ValidatorSet.VerifyCommit* over device verdicts. This package is
 the Python binding used by tests and bench.py; see DESIGN.md.
 """
 from . import _native
-from .crypto import (MODE_GO_STDLIB, MODE_ZIP215, BatchVerifier, Context, PubKey, default_context,
+from .crypto import (MODE_GO_STDLIB, MODE_ZIP215, BatchVerifier, Context, KeySet, PubKey, default_context,
                      new_batch_verifier, pack_messages)
 
-__all__ = ["MODE_GO_STDLIB", "MODE_ZIP215", "BatchVerifier", "Context", "PubKey", "default_context",
+__all__ = ["MODE_GO_STDLIB", "MODE_ZIP215", "BatchVerifier", "Context", "KeySet", "PubKey", "default_context",
            "new_batch_verifier", "pack_messages", "_native"]

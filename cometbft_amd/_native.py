@@ -42,6 +42,8 @@ COMMIT_PANIC_UNKNOWN_FLAG = 9
 EXPORTS = (
     "cmtv_open", "cmtv_close", "cmtv_strerror", "cmtv_abi_version", "cmtv_stats_get", "cmtv_stream",
     "cmtv_verify_ed25519", "cmtv_verify_ed25519_device",
+    "cmtv_register_keys", "cmtv_keyset_free", "cmtv_keyset_len", "cmtv_verify_ed25519_indexed",
+    "cmtv_verify_ed25519_indexed_device",
     "cmtv_batch_new", "cmtv_batch_add", "cmtv_batch_len", "cmtv_batch_verify", "cmtv_batch_reset",
     "cmtv_batch_free", "cmtv_verify_commit", "cmtv_vote_sign_bytes", "cmtv_pubkeys_ed25519", "cmtv_sign_ed25519",
 )
@@ -120,6 +122,16 @@ def lib() -> ctypes.CDLL:
     L.cmtv_verify_ed25519.restype = ctypes.c_int
     L.cmtv_verify_ed25519_device.argtypes = [vp, sz, vp, vp, vp, vp, u32, vp, vp, vp]
     L.cmtv_verify_ed25519_device.restype = ctypes.c_int
+    L.cmtv_register_keys.argtypes = [vp, sz, _u8p, ctypes.POINTER(vp)]
+    L.cmtv_register_keys.restype = ctypes.c_int
+    L.cmtv_keyset_free.argtypes = [vp]
+    L.cmtv_keyset_free.restype = None
+    L.cmtv_keyset_len.argtypes = [vp]
+    L.cmtv_keyset_len.restype = sz
+    L.cmtv_verify_ed25519_indexed.argtypes = [vp, vp, sz, u32p, _u8p, _u8p, u32p, u32, _u8p, ctypes.POINTER(u64)]
+    L.cmtv_verify_ed25519_indexed.restype = ctypes.c_int
+    L.cmtv_verify_ed25519_indexed_device.argtypes = [vp, vp, sz, vp, vp, vp, vp, u32, vp, vp, vp]
+    L.cmtv_verify_ed25519_indexed_device.restype = ctypes.c_int
     L.cmtv_batch_new.argtypes = [vp, u32, ctypes.POINTER(vp)]
     L.cmtv_batch_new.restype = ctypes.c_int
     L.cmtv_batch_add.argtypes = [vp, _u8p, sz, _u8p, sz, _u8p, sz]

@@ -100,6 +100,45 @@ class Context:
                                                 d_bitmap or None, ctypes.c_void_p(stream) if stream else None)
         N.check(rc, "cmtv_verify_ed25519_device")
 
+    # -------------------------------------------------------------- registered keys
+    def register_keys(self, pk: np.ndarray) -> "KeySet":
+        """Decode n 32-byte keys once and build their combs on the device
+        (cmtv_register_keys); verify_indexed then needs no decompression of
+        A and no doublings. 512 KiB of HBM per key."""
+        return KeySet(self, pk)
+
+    def verify_indexed(self, keys: "KeySet", key_idx: np.ndarray, sig: np.ndarray, msg: np.ndarray,
+                       msg_off: np.ndarray, mode: int | None = None, bitmap: bool = False):
+        """Verdicts for n signatures, signature i by registered key key_idx[i];
+        same verdicts as verify(keys.pk[key_idx], ...)."""
+        mode = self.default_mode if mode is None else mode
+        key_idx = np.ascontiguousarray(key_idx, dtype=np.uint32).reshape(-1)
+        sig = np.ascontiguousarray(sig, dtype=np.uint8).reshape(-1, 64)
+        n = key_idx.shape[0]
+        if sig.shape[0] != n or len(msg_off) != n + 1:
+            raise ValueError("key_idx / sig / msg_off sizes disagree")
+        msg = np.ascontiguousarray(msg, dtype=np.uint8)
+        if msg.size == 0:
+            msg = np.zeros(1, np.uint8)
+        off = np.ascontiguousarray(msg_off, dtype=np.uint32)
+        valid = np.zeros(max(n, 1), np.uint8)
+        words = np.zeros(max((n + 63) // 64, 1), np.uint64)
+        u32p = ctypes.POINTER(ctypes.c_uint32)
+        rc = N.lib().cmtv_verify_ed25519_indexed(self._h, keys.handle, n, key_idx.ctypes.data_as(u32p), _u8(sig),
+                                                 _u8(msg), off.ctypes.data_as(u32p), mode, _u8(valid),
+                                                 words.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)))
+        N.check(rc, "cmtv_verify_ed25519_indexed")
+        if bitmap:
+            return valid[:n], words[: (n + 63) // 64]
+        return valid[:n]
+
+    def verify_indexed_device(self, keys: "KeySet", n: int, d_key_idx: int, d_sig: int, d_msg: int, d_off: int,
+                              mode: int, d_valid: int = 0, d_bitmap: int = 0, stream: int = 0) -> None:
+        rc = N.lib().cmtv_verify_ed25519_indexed_device(self._h, keys.handle, n, d_key_idx, d_sig, d_msg, d_off,
+                                                        mode, d_valid or None, d_bitmap or None,
+                                                        ctypes.c_void_p(stream) if stream else None)
+        N.check(rc, "cmtv_verify_ed25519_indexed_device")
+
     # -------------------------------------------------------------- test data
     def pubkeys(self, seeds: np.ndarray) -> np.ndarray:
         seeds = np.ascontiguousarray(seeds, dtype=np.uint8).reshape(-1, 32)
@@ -123,6 +162,36 @@ class Context:
                                        off.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), _u8(out))
         N.check(rc, "cmtv_sign_ed25519")
         return out[:n]
+
+
+class KeySet:
+    """Registered public keys (cmtv_keyset): per-key combs resident in HBM."""
+
+    def __init__(self, ctx: Context, pk: np.ndarray):
+        pk = np.ascontiguousarray(pk, dtype=np.uint8).reshape(-1, 32)
+        h = ctypes.c_void_p()
+        N.check(N.lib().cmtv_register_keys(ctx.handle, pk.shape[0], _u8(pk), ctypes.byref(h)), "cmtv_register_keys")
+        self._h = h
+        self.ctx = ctx  # keeps the context alive while the key set is
+        self.pk = pk.copy()
+
+    @property
+    def handle(self):
+        return self._h
+
+    def __len__(self):
+        return N.lib().cmtv_keyset_len(self._h)
+
+    def free(self):
+        if self._h:
+            N.lib().cmtv_keyset_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
 
 
 _default_ctx = None

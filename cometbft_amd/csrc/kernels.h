@@ -7,11 +7,19 @@ namespace cmtv {
 
 constexpr uint32_t kBtabWords = 128 * 36;   // (1..128)B, 36 words per row
 constexpr uint32_t kAtabWordsPerLane = 320; // (1..8)(-A), 40 words per point
+constexpr uint32_t kCombWords = 32 * 128 * 32;     // one registered-key comb (keyed.h), 512 KiB
+constexpr uint32_t kCombScratchWordsPerKey = 128 * 320;  // prefix products while building
 
 hipError_t launch_btab_init(uint32_t* d_rows, hipStream_t s);
 hipError_t launch_verify(uint32_t mode, uint32_t n, const void* pk, const void* sig, const void* msg,
                          const void* off, const uint32_t* btab, uint32_t* atab, void* valid, void* bitmap,
                          bool quad, hipStream_t s);
+hipError_t launch_comb_build(uint32_t n_keys, const void* keys_pk, uint8_t* keys_ok, uint32_t* tabs,
+                             uint32_t* scratch, bool negate, hipStream_t s);
+hipError_t launch_verify_keyed(uint32_t mode, uint32_t n, uint32_t n_keys, const void* key_idx, const void* sig,
+                               const void* msg, const void* off, const uint32_t* keys_pk, const uint8_t* keys_ok,
+                               const uint32_t* ktabs, const uint32_t* bcomb, void* valid, void* bitmap,
+                               hipStream_t s);
 hipError_t launch_pubkey(uint32_t n, const void* seeds, const uint32_t* btab, void* out_pk, hipStream_t s);
 hipError_t launch_sign(uint32_t n, const void* seeds, const void* key_idx, const void* msg, const void* off,
                        const uint32_t* btab, void* out_sig, hipStream_t s);

@@ -4,6 +4,9 @@
 //   k_verify<MODE>: one signature per lane: SHA-512 + mod-L + decompression +
 //                   Straus [s]B - [k]A + GO_STDLIB / ZIP215 final check, then a
 //                   wavefront ballot packs 64 verdicts into one bitmap word
+//   k_verify_quad<MODE>: the same, one signature per quad of lanes (small batches)
+//   k_comb_build  : registered-key combs (keyed.h), one workgroup per key
+//   k_verify_keyed<MODE>: one signature per lane against a registered key
 //   k_pubkey / k_sign : RFC 8032 key generation and signing (synthetic data)
 //
 // Memory layout (HBM):
@@ -19,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include "kernels.h"
+#include "keyed.h"
 #include "quad.h"
 #include "verify_core.h"
 
@@ -175,6 +179,83 @@ __global__ __launch_bounds__(64, 2) void k_verify_quad(uint32_t n, const uint32_
   if (threadIdx.x == 0 && out_bitmap) reinterpret_cast<uint16_t*>(out_bitmap)[gid >> 6] = (uint16_t)x;
 }
 
+// Prefix products of comb_build_column, word-major / lane-minor per launch.
+struct DevCombScratch {
+  uint32_t* __restrict__ base;
+  uint32_t stride;
+  uint32_t lane;
+  __device__ __forceinline__ void store(int j, const fe& v) {
+#pragma unroll
+    for (int i = 0; i < 10; i++) base[(size_t)(j * 10 + i) * stride + lane] = v.v[i];
+  }
+  __device__ __forceinline__ void load(int j, fe& v) const {
+#pragma unroll
+    for (int i = 0; i < 10; i++) v.v[i] = base[(size_t)(j * 10 + i) * stride + lane];
+  }
+};
+
+// Comb of (negate ? -P : P) for n_keys encoded points; workgroup = key,
+// thread = multiple d = 1..128. keys_ok[key] records whether P decoded.
+__global__ __launch_bounds__(128) void k_comb_build(const uint32_t* __restrict__ keys_pk, uint8_t* __restrict__ keys_ok,
+                                                    uint32_t* __restrict__ tabs, uint32_t* __restrict__ scratch,
+                                                    int negate) {
+  const uint32_t key = blockIdx.x;
+  uint32_t w[8];
+  load_words(w, keys_pk + 8 * (size_t)key, 2);
+  ge_p3 A, nA;
+  const bool ok = p3_frombytes(A, w);
+  if (negate) {
+    cached_neg_point(nA, A);
+    A = nA;
+  }
+  if (threadIdx.x == 0 && keys_ok) keys_ok[key] = ok ? 1 : 0;
+  DevCombScratch sc{scratch, gridDim.x * 128u, blockIdx.x * 128u + threadIdx.x};
+  comb_build_column(tabs + (size_t)key * COMB_TABLE_WORDS, A, (int)threadIdx.x + 1, sc);
+}
+
+// One comb window as a table source: 32-word rows, coordinates at 8-byte
+// aligned offsets 0 / 40 / 80 bytes -> 5 x dwordx2 per coordinate.
+struct DevCombWindow {
+  const uint32_t* __restrict__ rows;
+  __device__ __forceinline__ void load_fe(int e, int c, fe& r) const {
+    const uint2* p = reinterpret_cast<const uint2*>(rows + e * COMB_ROW_WORDS + c * 10);
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+      const uint2 v = p[i];
+      r.v[2 * i] = v.x;
+      r.v[2 * i + 1] = v.y;
+    }
+  }
+};
+
+#ifndef CMTV_KEYED_WAVES_PER_EU
+#define CMTV_KEYED_WAVES_PER_EU 2
+#endif
+
+// One signature per lane by registered key key_idx[i] (keyed.h). An index
+// outside the key set yields an invalid verdict, never an out-of-bounds read.
+template <uint32_t MODE>
+__global__ __launch_bounds__(64, CMTV_KEYED_WAVES_PER_EU) void k_verify_keyed(
+    uint32_t n, uint32_t n_keys, const uint32_t* __restrict__ key_idx, const uint32_t* __restrict__ sig,
+    const uint8_t* __restrict__ msg, const uint32_t* __restrict__ off, const uint32_t* __restrict__ keys_pk,
+    const uint8_t* __restrict__ keys_ok, const uint32_t* __restrict__ ktabs, const uint32_t* __restrict__ bcomb,
+    uint8_t* __restrict__ out_valid, uint64_t* __restrict__ out_bitmap) {
+  const uint32_t gid = blockIdx.x * 64 + threadIdx.x;
+  const bool active = gid < n;
+  const uint32_t i = active ? gid : n - 1;
+  const uint32_t m0 = off[i], m1 = off[i + 1];
+  uint32_t kid = key_idx[i];
+  const bool kin = kid < n_keys;
+  kid = kin ? kid : 0;
+  bool v = verify_keyed<MODE, DevCombWindow>(keys_pk + 8 * (size_t)kid, kin && keys_ok[kid] != 0,
+                                             sig + 16 * (size_t)i, msg + m0, m1 - m0,
+                                             ktabs + (size_t)kid * COMB_TABLE_WORDS, bcomb);
+  v = v && active;
+  if (active && out_valid) out_valid[gid] = v ? 1 : 0;
+  const uint64_t mask = __ballot(v);
+  if (threadIdx.x == 0 && out_bitmap) out_bitmap[gid >> 6] = mask;
+}
+
 __global__ __launch_bounds__(64) void k_pubkey(uint32_t n, const uint32_t* __restrict__ seeds,
                                                const uint32_t* __restrict__ btab, uint32_t* __restrict__ out_pk) {
   const uint32_t gid = blockIdx.x * 64 + threadIdx.x;
@@ -235,6 +316,35 @@ hipError_t launch_verify(uint32_t mode, uint32_t n, const void* pk, const void* 
     hipLaunchKernelGGL(k_verify<MODE_ZIP215>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, atab, vp, bp);
   else
     hipLaunchKernelGGL(k_verify<MODE_GO_STDLIB>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, atab, vp, bp);
+  return hipGetLastError();
+}
+
+hipError_t launch_comb_build(uint32_t n_keys, const void* keys_pk, uint8_t* keys_ok, uint32_t* tabs,
+                             uint32_t* scratch, bool negate, hipStream_t s) {
+  if (n_keys == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_comb_build, dim3(n_keys), dim3(128), 0, s, static_cast<const uint32_t*>(keys_pk), keys_ok, tabs,
+                     scratch, negate ? 1 : 0);
+  return hipGetLastError();
+}
+
+hipError_t launch_verify_keyed(uint32_t mode, uint32_t n, uint32_t n_keys, const void* key_idx, const void* sig,
+                               const void* msg, const void* off, const uint32_t* keys_pk, const uint8_t* keys_ok,
+                               const uint32_t* ktabs, const uint32_t* bcomb, void* valid, void* bitmap,
+                               hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  auto ki = static_cast<const uint32_t*>(key_idx);
+  auto sgp = static_cast<const uint32_t*>(sig);
+  auto mp = static_cast<const uint8_t*>(msg);
+  auto op = static_cast<const uint32_t*>(off);
+  auto vp = static_cast<uint8_t*>(valid);
+  auto bp = static_cast<uint64_t*>(bitmap);
+  const dim3 grid(blocks_for(n)), block(64);
+  if (mode == MODE_ZIP215)
+    hipLaunchKernelGGL(k_verify_keyed<MODE_ZIP215>, grid, block, 0, s, n, n_keys, ki, sgp, mp, op, keys_pk, keys_ok,
+                       ktabs, bcomb, vp, bp);
+  else
+    hipLaunchKernelGGL(k_verify_keyed<MODE_GO_STDLIB>, grid, block, 0, s, n, n_keys, ki, sgp, mp, op, keys_pk,
+                       keys_ok, ktabs, bcomb, vp, bp);
   return hipGetLastError();
 }
 

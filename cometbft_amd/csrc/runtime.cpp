@@ -83,6 +83,16 @@ struct cmtv_ctx {
   std::mutex mu;
   cmtv_stats stats{};
   size_t quad_max = kQuadMaxDefault;  // batches up to this size use the quad kernel
+  uint32_t* d_bcomb = nullptr;        // comb of B for registered-key verification (built lazily)
+};
+
+struct cmtv_keyset {
+  cmtv_ctx* ctx = nullptr;
+  size_t n = 0;
+  uint32_t* d_pk = nullptr;   // n x 8 words, the keys' original bytes
+  uint8_t* d_ok = nullptr;    // n decode flags
+  uint32_t* d_tab = nullptr;  // n x kCombWords
+  std::vector<uint8_t> pk;    // host copy (n x 32)
 };
 
 namespace cmtv {
@@ -137,6 +147,55 @@ static int enqueue_verify(cmtv_ctx* ctx, size_t n, const uint8_t* d_pk, const ui
 }
 
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// keys per comb-build launch (prefix-product scratch = 160 KiB per key)
+constexpr uint32_t kCombKeyChunk = 256;
+
+// Comb of B (keyed.h), built on first use; caller holds the context lock.
+static int ensure_bcomb(cmtv_ctx* ctx) {
+  if (ctx->d_bcomb) return CMTV_OK;
+  const uint32_t bw[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
+                          0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};
+  DevBuf scratch, bpk;
+  uint32_t* tab = nullptr;
+  hipError_t e = hipMalloc(&tab, kCombWords * sizeof(uint32_t));
+  if (e == hipSuccess) e = scratch.ensure(kCombScratchWordsPerKey * sizeof(uint32_t));
+  if (e == hipSuccess) e = bpk.ensure(sizeof(bw));
+  if (e == hipSuccess) e = hipMemcpyAsync(bpk.p, bw, sizeof(bw), hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess)
+    e = launch_comb_build(1, bpk.p, nullptr, tab, static_cast<uint32_t*>(scratch.p), false, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  scratch.release();
+  bpk.release();
+  if (e != hipSuccess) {
+    if (tab) (void)hipFree(tab);
+    return hip_fail(e);
+  }
+  ctx->d_bcomb = tab;
+  return CMTV_OK;
+}
+
+static int enqueue_verify_keyed(cmtv_ctx* ctx, const cmtv_keyset* ks, size_t n, const uint32_t* d_idx,
+                                const uint8_t* d_sig, const uint8_t* d_msg, const uint32_t* d_off, uint32_t mode,
+                                uint8_t* d_valid, uint64_t* d_bitmap, hipStream_t s) {
+  if (n == 0) return CMTV_OK;
+  harvest_timing(ctx);
+  hipError_t e;
+  if ((e = hipEventRecord(ctx->ev0, s)) != hipSuccess) return hip_fail(e);
+  for (size_t c = 0; c < n; c += kChunk) {
+    const uint32_t cn = (uint32_t)std::min<size_t>(kChunk, n - c);
+    e = launch_verify_keyed(mode, cn, (uint32_t)ks->n, d_idx + c, d_sig + 64 * c, d_msg, d_off + c, ks->d_pk,
+                            ks->d_ok, ks->d_tab, ctx->d_bcomb, d_valid ? d_valid + c : nullptr,
+                            d_bitmap ? d_bitmap + c / 64 : nullptr, s);
+    if (e != hipSuccess) return hip_fail(e);
+    ctx->stats.kernel_launches++;
+  }
+  if ((e = hipEventRecord(ctx->ev1, s)) != hipSuccess) return hip_fail(e);
+  ctx->timing_pending = true;
+  ctx->stats.calls++;
+  ctx->stats.signatures += n;
+  return CMTV_OK;
+}
 
 int verify_host_locked(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
                        const uint32_t* msg_off, uint32_t mode, uint8_t* out_valid, uint64_t* out_bitmap) {
@@ -251,6 +310,7 @@ void cmtv_close(cmtv_ctx* ctx) {
   ctx->h_in.release();
   ctx->h_out.release();
   if (ctx->d_btab) (void)hipFree(ctx->d_btab);
+  if (ctx->d_bcomb) (void)hipFree(ctx->d_bcomb);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -291,6 +351,114 @@ int cmtv_verify_ed25519_device(cmtv_ctx* ctx, size_t n, const void* d_pk, const 
   return enqueue_verify(ctx, n, static_cast<const uint8_t*>(d_pk), static_cast<const uint8_t*>(d_sig),
                         static_cast<const uint8_t*>(d_msg), static_cast<const uint32_t*>(d_msg_off), mode,
                         static_cast<uint8_t*>(d_valid), static_cast<uint64_t*>(d_bitmap), s);
+}
+
+int cmtv_register_keys(cmtv_ctx* ctx, size_t n_keys, const uint8_t* pk, cmtv_keyset** out) {
+  if (!out) return CMTV_EINVAL;
+  *out = nullptr;
+  // 512 KiB of comb per key; 2^20 keys would already be 512 GiB
+  if (!ctx || n_keys == 0 || n_keys > (1u << 20) || !pk) return CMTV_EINVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  if (hipSetDevice(ctx->device) != hipSuccess) return CMTV_ENODEV;
+  int rc = ensure_bcomb(ctx);
+  if (rc != CMTV_OK) return rc;
+  auto* ks = new (std::nothrow) cmtv_keyset();
+  if (!ks) return CMTV_ENOMEM;
+  ks->ctx = ctx;
+  ks->n = n_keys;
+  ks->pk.assign(pk, pk + 32 * n_keys);
+  DevBuf scratch;
+  hipError_t e = hipMalloc(&ks->d_pk, 32 * n_keys);
+  if (e == hipSuccess) e = hipMalloc(&ks->d_ok, n_keys);
+  if (e == hipSuccess) e = hipMalloc(&ks->d_tab, n_keys * (size_t)kCombWords * sizeof(uint32_t));
+  if (e == hipSuccess)
+    e = scratch.ensure((size_t)std::min<size_t>(n_keys, kCombKeyChunk) * kCombScratchWordsPerKey * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMemcpyAsync(ks->d_pk, pk, 32 * n_keys, hipMemcpyHostToDevice, ctx->stream);
+  for (size_t c = 0; e == hipSuccess && c < n_keys; c += kCombKeyChunk) {
+    const uint32_t cn = (uint32_t)std::min<size_t>(kCombKeyChunk, n_keys - c);
+    e = launch_comb_build(cn, ks->d_pk + 8 * c, ks->d_ok + c, ks->d_tab + c * (size_t)kCombWords,
+                          static_cast<uint32_t*>(scratch.p), true, ctx->stream);
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  scratch.release();
+  if (e != hipSuccess) {
+    cmtv_keyset_free(ks);
+    return hip_fail(e);
+  }
+  *out = ks;
+  return CMTV_OK;
+}
+
+void cmtv_keyset_free(cmtv_keyset* ks) {
+  if (!ks) return;
+  (void)hipSetDevice(ks->ctx->device);
+  if (ks->d_pk) (void)hipFree(ks->d_pk);
+  if (ks->d_ok) (void)hipFree(ks->d_ok);
+  if (ks->d_tab) (void)hipFree(ks->d_tab);
+  delete ks;
+}
+
+size_t cmtv_keyset_len(const cmtv_keyset* ks) { return ks ? ks->n : 0; }
+
+int cmtv_verify_ed25519_indexed(cmtv_ctx* ctx, const cmtv_keyset* ks, size_t n, const uint32_t* key_idx,
+                                const uint8_t* sig, const uint8_t* msg, const uint32_t* msg_off, uint32_t mode,
+                                uint8_t* out_valid, uint64_t* out_bitmap) {
+  if (!ctx || !ks || ks->ctx != ctx || mode > CMTV_MODE_ZIP215 || n > (1ull << 31)) return CMTV_EINVAL;
+  if (n == 0) return CMTV_OK;
+  if (!key_idx || !sig || !msg_off || (!msg && msg_off[n] != 0) || (!out_valid && !out_bitmap)) return CMTV_EINVAL;
+  for (size_t i = 0; i < n; i++)
+    if (msg_off[i + 1] < msg_off[i] || key_idx[i] >= ks->n) return CMTV_EINVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  if (hipSetDevice(ctx->device) != hipSuccess) return CMTV_ENODEV;
+  const size_t msg_bytes = msg_off[n];
+  // staging layout: [key_idx n*4][sig n*64][off (n+1)*4][msg msg_bytes + 16]
+  const size_t o_idx = 0, o_sig = align_up(4 * n, 256), o_off = align_up(o_sig + 64 * n, 256);
+  const size_t o_msg = align_up(o_off + 4 * (n + 1), 256), in_bytes = align_up(o_msg + msg_bytes + 16, 256);
+  const size_t words = (n + 63) / 64;
+  const size_t o_bm = 0, o_valid = align_up(8 * words, 256), out_bytes = align_up(o_valid + n, 256);
+  hipError_t e;
+  if ((e = ctx->h_in.ensure(in_bytes)) != hipSuccess) return hip_fail(e);
+  if ((e = ctx->d_in.ensure(in_bytes)) != hipSuccess) return hip_fail(e);
+  if ((e = ctx->h_out.ensure(out_bytes)) != hipSuccess) return hip_fail(e);
+  if ((e = ctx->d_out.ensure(out_bytes)) != hipSuccess) return hip_fail(e);
+  auto* hin = static_cast<uint8_t*>(ctx->h_in.p);
+  std::memcpy(hin + o_idx, key_idx, 4 * n);
+  std::memcpy(hin + o_sig, sig, 64 * n);
+  std::memcpy(hin + o_off, msg_off, 4 * (n + 1));
+  if (msg_bytes) std::memcpy(hin + o_msg, msg, msg_bytes);
+  std::memset(hin + o_msg + msg_bytes, 0, 16);
+  auto* din = static_cast<uint8_t*>(ctx->d_in.p);
+  auto* dout = static_cast<uint8_t*>(ctx->d_out.p);
+  if ((e = hipMemcpyAsync(din, hin, in_bytes, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess) return hip_fail(e);
+  int rc = enqueue_verify_keyed(ctx, ks, n, reinterpret_cast<uint32_t*>(din + o_idx), din + o_sig, din + o_msg,
+                                reinterpret_cast<uint32_t*>(din + o_off), mode, dout + o_valid,
+                                reinterpret_cast<uint64_t*>(dout + o_bm), ctx->stream);
+  if (rc != CMTV_OK) return rc;
+  auto* hout = static_cast<uint8_t*>(ctx->h_out.p);
+  if ((e = hipMemcpyAsync(hout, dout, out_bytes, hipMemcpyDeviceToHost, ctx->stream)) != hipSuccess) return hip_fail(e);
+  if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return hip_fail(e);
+  harvest_timing(ctx);
+  uint64_t invalid = 0;
+  const uint8_t* hv = hout + o_valid;
+  for (size_t i = 0; i < n; i++) invalid += hv[i] == 0;
+  ctx->stats.invalid += invalid;
+  if (out_valid) std::memcpy(out_valid, hv, n);
+  if (out_bitmap) std::memcpy(out_bitmap, hout + o_bm, 8 * words);
+  return CMTV_OK;
+}
+
+int cmtv_verify_ed25519_indexed_device(cmtv_ctx* ctx, const cmtv_keyset* ks, size_t n, const void* d_key_idx,
+                                       const void* d_sig, const void* d_msg, const void* d_msg_off, uint32_t mode,
+                                       void* d_valid, void* d_bitmap, void* stream) {
+  if (!ctx || !ks || ks->ctx != ctx || mode > CMTV_MODE_ZIP215 || n > (1ull << 31)) return CMTV_EINVAL;
+  if (n == 0) return CMTV_OK;
+  if (!d_key_idx || !d_sig || !d_msg || !d_msg_off || (!d_valid && !d_bitmap)) return CMTV_EINVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  if (hipSetDevice(ctx->device) != hipSuccess) return CMTV_ENODEV;
+  return enqueue_verify_keyed(ctx, ks, n, static_cast<const uint32_t*>(d_key_idx),
+                              static_cast<const uint8_t*>(d_sig), static_cast<const uint8_t*>(d_msg),
+                              static_cast<const uint32_t*>(d_msg_off), mode, static_cast<uint8_t*>(d_valid),
+                              static_cast<uint64_t*>(d_bitmap), static_cast<hipStream_t>(stream));
 }
 
 int cmtv_pubkeys_ed25519(cmtv_ctx* ctx, size_t n, const uint8_t* seeds, uint8_t* out_pk) {

@@ -161,6 +161,41 @@ CMTV_HD void build_cached_table(ATab& atab, const ge_p3& P) {
   }
 }
 
+// Final equation against the signature's R bytes (sig_ptr[0..7]):
+//   GO_STDLIB: encode(R') == R bytes (Go bytes.Equal after Point.Bytes)
+//   ZIP215:    [8](R' - decode(R)) == O, R decoded with the same rules as A
+template <uint32_t MODE>
+CMTV_HD bool check_R(const ge_p3& Rp, const uint32_t* sig_ptr) {
+  uint32_t w[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) w[i] = sig_ptr[i];  // R
+  if (MODE == MODE_GO_STDLIB) {
+    uint32_t enc[8];
+    p3_tobytes(enc, Rp.X, Rp.Y, Rp.Z);
+    uint32_t diff = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) diff |= enc[i] ^ w[i];
+    return diff == 0;
+  } else {
+    ge_p3 R;
+    const bool r_ok = p3_frombytes(R, w);
+    ge_cached Rc;
+    p3_to_cached(Rc, R);
+    ge_efgh t;
+    cached_cneg(Rc, true);
+    ge_add_cached(t, Rp, Rc);
+    ge_p2 q;
+    efgh_to_p2(q, t);
+#pragma unroll 1
+    for (int i = 0; i < 3; i++) {
+      p2_dbl(t, q);
+      efgh_to_p2(q, t);
+    }
+    const bool ident = fe_iszero(q.X) && fe_equal(q.Y, q.Z);
+    return r_ok && ident;
+  }
+}
+
 // Full single-signature verification. pk / sig are read through pointers
 // (little-endian 32-bit words) at the points they are needed, so neither is
 // held in registers across the scalar multiplication.
@@ -194,34 +229,7 @@ CMTV_HD bool verify_one(const uint32_t* pk_ptr, const uint32_t* sig_ptr, const u
 
   ge_p3 Rp;
   straus_double_scalarmult<true>(Rp, k, ts, atab, btab);
-
-#pragma unroll
-  for (int i = 0; i < 8; i++) w[i] = sig_ptr[i];  // R
-  if (MODE == MODE_GO_STDLIB) {
-    uint32_t enc[8];
-    p3_tobytes(enc, Rp.X, Rp.Y, Rp.Z);
-    uint32_t diff = 0;
-#pragma unroll
-    for (int i = 0; i < 8; i++) diff |= enc[i] ^ w[i];
-    return ok && diff == 0;
-  } else {
-    ge_p3 R;
-    const bool r_ok = p3_frombytes(R, w);
-    ge_cached Rc;
-    p3_to_cached(Rc, R);
-    ge_efgh t;
-    cached_cneg(Rc, true);
-    ge_add_cached(t, Rp, Rc);
-    ge_p2 q;
-    efgh_to_p2(q, t);
-#pragma unroll 1
-    for (int i = 0; i < 3; i++) {
-      p2_dbl(t, q);
-      efgh_to_p2(q, t);
-    }
-    const bool ident = fe_iszero(q.X) && fe_equal(q.Y, q.Z);
-    return ok && r_ok && ident;
-  }
+  return check_R<MODE>(Rp, sig_ptr) && ok;
 }
 
 // RFC 8032 key expansion: h = SHA-512(seed); a = clamp(h[0:32]) mod L, prefix = h[32:64]

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define CMTV_ABI_VERSION 1
+#define CMTV_ABI_VERSION 2
 
 enum {
   CMTV_OK = 0,
@@ -57,6 +57,7 @@ enum { CMTV_MODE_GO_STDLIB = 0, CMTV_MODE_ZIP215 = 1 };
 
 typedef struct cmtv_ctx cmtv_ctx;
 typedef struct cmtv_batch cmtv_batch;
+typedef struct cmtv_keyset cmtv_keyset;
 
 typedef struct cmtv_config {
   int32_t device;        /* HIP device ordinal; -1 = current device          */
@@ -105,6 +106,38 @@ int cmtv_verify_ed25519(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_
  * (n bytes) and d_bitmap (ceil(n/64) words) may each be NULL. */
 int cmtv_verify_ed25519_device(cmtv_ctx* ctx, size_t n, const void* d_pk, const void* d_sig, const void* d_msg,
                                const void* d_msg_off, uint32_t mode, void* d_valid, void* d_bitmap, void* stream);
+
+/* ------------------------------------------------------------ registered keys */
+
+/* A validator set signs commit after commit with the same keys (blocksync,
+ * light-client and state-sync replay: blockchain/v0/reactor.go:366-400,
+ * light/verifier.go:60-125, both ending in the VerifyCommit* loops above).
+ * The reference decodes each key again inside every
+ * PubKey.VerifySignature (crypto/ed25519/ed25519.go:154). cmtv_register_keys
+ * decodes n_keys 32-byte keys once and builds, per key, the radix-256 comb
+ * (e+1)*256^j*(-A) (j < 32, e < 128; 512 KiB of HBM per key), so that
+ * indexed verification needs no decompression of A and no doublings.
+ * Verdicts are identical to cmtv_verify_ed25519's on the same (pk, msg, sig):
+ * a key that fails to decode makes every signature under it invalid, and the
+ * key's original bytes are what SHA-512(R || A || M) hashes. Blocking. The
+ * key set belongs to `ctx`: free it before cmtv_close(ctx). */
+int cmtv_register_keys(cmtv_ctx* ctx, size_t n_keys, const uint8_t* pk, cmtv_keyset** out);
+void cmtv_keyset_free(cmtv_keyset* ks);
+size_t cmtv_keyset_len(const cmtv_keyset* ks);
+
+/* Verification of n signatures where signature i is by registered key
+ * key_idx[i] (every index must be < cmtv_keyset_len: CMTV_EINVAL otherwise).
+ * Buffers and outputs as in cmtv_verify_ed25519. Blocking. */
+int cmtv_verify_ed25519_indexed(cmtv_ctx* ctx, const cmtv_keyset* ks, size_t n, const uint32_t* key_idx,
+                                const uint8_t* sig, const uint8_t* msg, const uint32_t* msg_off, uint32_t mode,
+                                uint8_t* out_valid, uint64_t* out_bitmap);
+
+/* Same with device-resident inputs, enqueued on `stream` (NULL = HIP null
+ * stream), non-blocking. An out-of-range d_key_idx entry gives an invalid
+ * verdict (the kernel never reads outside the key set). */
+int cmtv_verify_ed25519_indexed_device(cmtv_ctx* ctx, const cmtv_keyset* ks, size_t n, const void* d_key_idx,
+                                       const void* d_sig, const void* d_msg, const void* d_msg_off, uint32_t mode,
+                                       void* d_valid, void* d_bitmap, void* stream);
 
 /* ------------------------------------------------------------ crypto.BatchVerifier mirror */
 

@@ -4,12 +4,16 @@
 //   input  (stdin):  u32 n, then n x { u8 mode, u8 pk[32], u8 sig[64], u32 mlen, u8 msg[mlen] }
 //   output (stdout): n bytes of verdicts
 //   argv[1] == "sign": n x { u8 seed[32], u32 mlen, msg } -> n x { pk[32], sig[64] }
+//   argv[1] == "keyed": verify input as above, through registered-key combs
+//                       (keyed.h; one comb per distinct pk)
 #define CMTV_HD inline
 #define CMTV_BOUNDS_CHECK 1
 #include <cstdio>
 #include <cstring>
+#include <map>
+#include <string>
 #include <vector>
-#include "../../cometbft_amd/csrc/verify_core.h"
+#include "../../cometbft_amd/csrc/keyed.h"
 
 using namespace cmtv;
 
@@ -32,6 +36,25 @@ struct HostATab {
   void store(int e, const ge_cached& r) { t[e] = r; }
 };
 
+struct HostScratch {
+  fe q[COMB_WINDOWS];
+  void store(int j, const fe& v) { q[j] = v; }
+  void load(int j, fe& v) const { v = q[j]; }
+};
+
+// comb of P (negated when neg) as the runtime's k_comb_build produces it
+static std::vector<uint32_t> host_comb(const uint32_t pkw[8], bool neg, bool* ok) {
+  std::vector<uint32_t> tab(COMB_TABLE_WORDS);
+  ge_p3 A, nA;
+  *ok = p3_frombytes(A, pkw);
+  cached_neg_point(nA, A);
+  for (int d = 1; d <= COMB_ENTRIES; d++) {
+    HostScratch sc;
+    comb_build_column(tab.data(), neg ? nA : A, d, sc);
+  }
+  return tab;
+}
+
 static void to_words(uint32_t* w, const uint8_t* b, int nw) {
   for (int i = 0; i < nw; i++) w[i] = b[4 * i] | (b[4 * i + 1] << 8) | (b[4 * i + 2] << 16) | ((uint32_t)b[4 * i + 3] << 24);
 }
@@ -45,6 +68,15 @@ int main(int argc, char** argv) {
   uint32_t n;
   if (fread(&n, 4, 1, stdin) != 1) return 1;
   const bool sign = argc > 1 && !strcmp(argv[1], "sign");
+  const bool keyed = argc > 1 && !strcmp(argv[1], "keyed");
+  std::vector<uint32_t> bcomb;
+  std::map<std::string, std::pair<bool, std::vector<uint32_t>>> combs;
+  if (keyed) {
+    uint32_t bw[8];
+    bool bok;
+    basepoint_words(bw);
+    bcomb = host_comb(bw, false, &bok);
+  }
   for (uint32_t i = 0; i < n; i++) {
     if (sign) {
       uint8_t seed[32];
@@ -74,6 +106,21 @@ int main(int argc, char** argv) {
     uint32_t pkw[8], sigw[16];
     to_words(pkw, pk, 8);
     to_words(sigw, sig, 16);
+    if (keyed) {
+      auto it = combs.find(std::string((const char*)pk, 32));
+      if (it == combs.end()) {
+        bool kok;
+        auto tab = host_comb(pkw, true, &kok);
+        it = combs.emplace(std::string((const char*)pk, 32), std::make_pair(kok, std::move(tab))).first;
+      }
+      const bool kok = it->second.first;
+      const uint32_t* kt = it->second.second.data();
+      bool v = mode ? verify_keyed<MODE_ZIP215, CombWindow>(pkw, kok, sigw, mp, mlen, kt, bcomb.data())
+                    : verify_keyed<MODE_GO_STDLIB, CombWindow>(pkw, kok, sigw, mp, mlen, kt, bcomb.data());
+      uint8_t o = v;
+      fwrite(&o, 1, 1, stdout);
+      continue;
+    }
     HostATab at;
     bool v = mode ? verify_one<MODE_ZIP215>(pkw, sigw, mp, mlen, at, bt)
                   : verify_one<MODE_GO_STDLIB>(pkw, sigw, mp, mlen, at, bt);

@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_strerror():
     lib = N.lib()
-    assert lib.cmtv_abi_version() == 1
+    assert lib.cmtv_abi_version() == 2
     for code in (N.CMTV_OK, N.CMTV_EINVAL, N.CMTV_ENODEV, N.CMTV_ENOMEM, N.CMTV_EHIP, N.CMTV_ERCCL, N.CMTV_ECOMMIT):
         assert lib.cmtv_strerror(code)
 
@@ -96,3 +96,15 @@ def test_commit_vote_sign_bytes_lengths():
     assert all(100 <= len(m) <= 161 for m in msgs)
     nil = TU.commit_messages(4, 1000, flags=[T.BLOCK_ID_FLAG_NIL] * 4)
     assert all(len(m) < 50 for m in nil)
+
+
+def test_keyset_entry_points_reject_bad_arguments_without_gpu():
+    lib = N.lib()
+    ks = ctypes.c_void_p()
+    assert lib.cmtv_register_keys(None, 1, None, ctypes.byref(ks)) == N.CMTV_EINVAL
+    assert lib.cmtv_register_keys(None, 1, None, None) == N.CMTV_EINVAL
+    assert lib.cmtv_keyset_len(None) == 0
+    lib.cmtv_keyset_free(None)
+    assert lib.cmtv_verify_ed25519_indexed(None, None, 1, None, None, None, None, 0, None, None) == N.CMTV_EINVAL
+    assert lib.cmtv_verify_ed25519_indexed_device(None, None, 1, None, None, None, None, 0, None, None,
+                                                  None) == N.CMTV_EINVAL

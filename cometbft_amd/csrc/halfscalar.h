@@ -1,0 +1,321 @@
+// halfscalar.h -- half-size scalar decomposition for signature verification.
+//
+// Verification asks whether R' = [s]B - [k]A equals R. For any integers
+// (k1, k2) with k1 == k2 * k (mod 8L),
+//
+//     [k2](R' - R) = [k2 s mod L]B - [k1]A - [k2]R
+//
+// because every point of edwards25519 has order dividing 8L (so [k2 k]A =
+// [k1]A even for A with a torsion component) and B has order L. The partial
+// extended Euclid on (8L, k) yields such a pair with |k1|, |k2| ~ 2^127
+// (Antipa et al., "Accelerated verification of ECDSA signatures", SAC 2005;
+// Pornin, "Optimized lattice basis reduction in dimension 2", 2020), which
+// halves the doublings of the variable-base part: 34 four-bit windows shared
+// by A, R and the two halves of the fixed-base scalar instead of 64.
+//
+// Exactness (the verdicts must equal Go 1.19 crypto/ed25519.Verify's,
+// /root/reference/crypto/ed25519/ed25519.go:148-155):
+//   * k2 is chosen ODD, and 0 < |k2| < L, so gcd(k2, 8L) = 1 and
+//     [k2]X = O  <=>  X = O.  Cofactorless (GO_STDLIB) mode therefore checks
+//     R' == R exactly; with R canonical this is encode(R') == R bytes.
+//   * ZIP215 mode checks [8][k2](R' - R) = O  <=>  [8](R' - R) = O.
+//   * If no odd-k2 pair fits 134 bits (probability ~5e-5 for a random k, or
+//     a quotient >= 2^31 appears), the decomposition is marked `wide` and the
+//     caller uses k1 = k, k2 = 1 over 64 windows -- the same equation, so no
+//     input changes its verdict, only its cost.
+//
+// Arithmetic: the Euclid runs on 8-word values kept left-normalised (r0's top
+// bit at bit 255, both remainders shifted by the same e), so each quotient
+// comes from the top 64 bits in one f64 division, corrected by at most a few
+// add/subtract steps; t values are 6-word two's complement.
+#pragma once
+#include <math.h>
+#include <stdint.h>
+
+#include "sc25519.h"
+
+#ifndef CMTV_HD
+#define CMTV_HD __host__ __device__ __forceinline__
+#endif
+
+namespace cmtv {
+
+constexpr int HS_WINDOWS = 34;      // 4-bit windows for normal pairs (136 bits)
+constexpr int HS_WIDE_WINDOWS = 64; // k1 = k, k2 = 1
+constexpr int HS_MAX_BITS = 134;    // (2^134 + bias) < 16^34 for the signed-digit bias
+constexpr int HS_MAX_STEPS = 192;   // Euclid steps before giving up (typical: ~75)
+
+struct HalfScalars {
+  uint32_t k1[8];  // >= 0
+  uint32_t k2[8];  // |k2|, odd
+  bool k2_neg;
+  bool wide;
+};
+
+CMTV_HD uint32_t hs_N(int i) {  // 8L
+  const uint32_t N[8] = {0xe7ae9f68u, 0xc09318d2u, 0x17bce6b2u, 0xa6f7cef5u, 0u, 0u, 0u, 0x80000000u};
+  return N[i];
+}
+
+CMTV_HD int hs_clz(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return x ? __clz((int)x) : 32;
+#else
+  return x ? __builtin_clz(x) : 32;
+#endif
+}
+
+// bit length of an 8-word value
+CMTV_HD int hs_bitlen8(const uint32_t r[8]) {
+  int bl = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) bl = r[i] ? 32 * i + 32 - hs_clz(r[i]) : bl;
+  return bl;
+}
+
+// |t| bit length and sign of a 6-word two's complement value
+CMTV_HD int hs_bitlen6s(const uint32_t t[6], bool& neg) {
+  neg = (t[5] >> 31) != 0;
+  uint32_t m[6];
+  uint64_t c = 1;
+#pragma unroll
+  for (int i = 0; i < 6; i++) {
+    const uint64_t v = (uint64_t)(neg ? ~t[i] : t[i]) + (neg ? c : 0);
+    m[i] = (uint32_t)v;
+    c = v >> 32;
+  }
+  int bl = 0;
+#pragma unroll
+  for (int i = 0; i < 6; i++) bl = m[i] ? 32 * i + 32 - hs_clz(m[i]) : bl;
+  return bl;
+}
+
+// r <<= sh (0 <= sh < 32), 8 words
+CMTV_HD void hs_shl8(uint32_t r[8], int sh) {
+#pragma unroll
+  for (int i = 7; i > 0; i--) r[i] = (uint32_t)(((((uint64_t)r[i] << 32) | r[i - 1]) << sh) >> 32);
+  r[0] <<= sh;
+}
+
+// r >>= sh (0 <= sh < 32), 8 words
+CMTV_HD void hs_shr8(uint32_t r[8], int sh) {
+#pragma unroll
+  for (int i = 0; i < 7; i++) r[i] = (uint32_t)(((((uint64_t)r[i + 1] << 32) | r[i]) >> sh));
+  r[7] >>= sh;
+}
+
+// one Euclid step on normalised (r0, r1): rr = r0 - q r1 with q = floor(r0 / r1),
+// tt = t0 - q t1. Returns false if q does not fit the one-word estimate.
+CMTV_HD bool hs_step(uint32_t rr[8], uint32_t tt[6], const uint32_t r0[8], const uint32_t r1[8],
+                     const uint32_t t0[6], const uint32_t t1[6]) {
+  if (r1[7] == 0) return false;  // r1 < r0 / 2^31: quotient too wide for one word
+  const uint64_t a = ((uint64_t)r0[7] << 32) | r0[6];
+  const uint64_t b = ((uint64_t)r1[7] << 32) | r1[6];
+  const double qd = floor((double)a / (double)b);
+  uint32_t q = qd >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)qd;
+  // x = r0 - q r1 as 9-word two's complement; y = t0 - q t1 (6 words)
+  uint32_t x[9];
+  {
+    uint64_t mc = 0;
+    int64_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const uint64_t p = (uint64_t)q * r1[i] + mc;
+      mc = p >> 32;
+      acc += (int64_t)r0[i] - (int64_t)(uint32_t)p;
+      x[i] = (uint32_t)acc;
+      acc >>= 32;
+    }
+    acc -= (int64_t)mc;
+    x[8] = (uint32_t)acc;
+  }
+  {
+    uint64_t mc = 0;
+    int64_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+      const uint64_t p = (uint64_t)q * t1[i] + mc;
+      mc = p >> 32;
+      acc += (int64_t)t0[i] - (int64_t)(uint32_t)p;
+      tt[i] = (uint32_t)acc;
+      acc >>= 32;
+    }
+  }
+  // the estimate is within a few units of q: fix it up (rarely entered)
+  bool ok = true;
+#pragma unroll 1
+  for (int it = 0; (x[8] >> 31) && it < 4; it++) {  // x < 0: add r1 back
+    uint64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const uint64_t v = (uint64_t)x[i] + r1[i] + c;
+      x[i] = (uint32_t)v;
+      c = v >> 32;
+    }
+    x[8] += (uint32_t)c;
+    c = 0;
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+      const uint64_t v = (uint64_t)tt[i] + t1[i] + c;
+      tt[i] = (uint32_t)v;
+      c = v >> 32;
+    }
+  }
+  ok = ok && !(x[8] >> 31);
+#pragma unroll 1
+  for (int it = 0; it < 4; it++) {  // x >= r1: subtract once more
+    int64_t acc = 0;
+    uint32_t y[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      acc += (int64_t)x[i] - (int64_t)r1[i];
+      y[i] = (uint32_t)acc;
+      acc >>= 32;
+    }
+    acc += (int64_t)x[8];
+    if (acc < 0) break;
+#pragma unroll
+    for (int i = 0; i < 8; i++) x[i] = y[i];
+    x[8] = (uint32_t)acc;
+    acc = 0;
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+      acc += (int64_t)tt[i] - (int64_t)t1[i];
+      tt[i] = (uint32_t)acc;
+      acc >>= 32;
+    }
+  }
+  ok = ok && x[8] == 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) rr[i] = x[i];
+  return ok;
+}
+
+// (k1, k2) with k1 == k2 k (mod 8L), k2 odd, both < 2^134, or wide.
+CMTV_HD void half_scalars(HalfScalars& h, const uint32_t k[8]) {
+  uint32_t r0[8], r1[8], t0[6], t1[6];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    r0[i] = hs_N(i);  // already normalised: bit 255 set
+    r1[i] = k[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 6; i++) {
+    t0[i] = 0;
+    t1[i] = i == 0 ? 1u : 0u;
+  }
+  int e = 0;  // common left shift of r0, r1
+  bool ok = true;
+#pragma unroll 1
+  for (int step = 0; step < HS_MAX_STEPS; step++) {
+    const int bl1 = (r1[7] ? 256 - hs_clz(r1[7]) : hs_bitlen8(r1)) - e;
+    if (bl1 <= 127) break;
+    uint32_t rr[8], tt[6];
+    if (!hs_step(rr, tt, r0, r1, t0, t1)) {
+      ok = false;
+      break;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      r0[i] = r1[i];
+      r1[i] = rr[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+      t0[i] = t1[i];
+      t1[i] = tt[i];
+    }
+    // renormalise: r0's top bit back to bit 255
+#pragma unroll 1
+    while (r0[7] == 0) {
+#pragma unroll
+      for (int i = 7; i > 0; i--) {
+        r0[i] = r0[i - 1];
+        r1[i] = r1[i - 1];
+      }
+      r0[0] = 0;
+      r1[0] = 0;
+      e += 32;
+    }
+    const int sh = hs_clz(r0[7]);
+    hs_shl8(r0, sh);
+    hs_shl8(r1, sh);
+    e += sh;
+    if (step == HS_MAX_STEPS - 1) ok = false;
+  }
+
+  // candidates with odd t: (r1, t1); else (r0, t0) [t0 odd then] or one more
+  // step (r2, t2) [t2 = t0 - q t1 odd then]
+  bool n1, n0, n2;
+  const int b1 = hs_bitlen6s(t1, n1);
+  const int c1 = (hs_bitlen8(r1) - e) > b1 ? (hs_bitlen8(r1) - e) : b1;
+  const bool t1_odd = t1[0] & 1;
+  uint32_t r2[8], t2[6];
+  bool ok2 = false;
+  if (ok && !t1_odd) ok2 = hs_step(r2, t2, r0, r1, t0, t1);
+  const int br0 = hs_bitlen8(r0) - e, bt0 = hs_bitlen6s(t0, n0);
+  const int c0 = br0 > bt0 ? br0 : bt0;
+  int c2 = 1 << 20;
+  if (ok2) {
+    const int br2 = hs_bitlen8(r2) - e, bt2 = hs_bitlen6s(t2, n2);
+    c2 = br2 > bt2 ? br2 : bt2;
+  }
+  // choose: 1 if t1 odd, else the smaller of 0 and 2
+  const int pick = t1_odd ? 1 : (c2 < c0 ? 2 : 0);
+  const int cost = pick == 1 ? c1 : (pick == 2 ? c2 : c0);
+  h.wide = !ok || cost > HS_MAX_BITS;
+  uint32_t rs[8], ts[6];
+#pragma unroll
+  for (int i = 0; i < 8; i++) rs[i] = pick == 1 ? r1[i] : (pick == 2 ? r2[i] : r0[i]);
+#pragma unroll
+  for (int i = 0; i < 6; i++) ts[i] = pick == 1 ? t1[i] : (pick == 2 ? t2[i] : t0[i]);
+  // denormalise r (e <= 129 whenever the pair is used)
+  int ew = h.wide ? 0 : e;
+#pragma unroll 1
+  while (ew >= 32) {
+#pragma unroll
+    for (int i = 0; i < 7; i++) rs[i] = rs[i + 1];
+    rs[7] = 0;
+    ew -= 32;
+  }
+  hs_shr8(rs, ew);
+  bool tneg = (ts[5] >> 31) != 0;
+  uint64_t c = 1;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t w = i < 6 ? ts[i] : (tneg ? 0xFFFFFFFFu : 0u);
+    const uint64_t v = (uint64_t)(tneg ? ~w : w) + (tneg ? c : 0);
+    h.k2[i] = (uint32_t)v;
+    c = v >> 32;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    h.k1[i] = h.wide ? k[i] : rs[i];
+    h.k2[i] = h.wide ? (i == 0 ? 1u : 0u) : h.k2[i];
+  }
+  h.k2_neg = !h.wide && tneg;
+}
+
+// u = k2 * s mod L (signed k2 = neg ? -mag : mag), s < L
+CMTV_HD void hs_bscalar(uint32_t u[8], const uint32_t k2mag[8], bool neg, const uint32_t s[8]) {
+  uint32_t z[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) z[i] = 0;
+  sc_muladd(u, k2mag, s, z);
+  // L - u (and 0 stays 0)
+  uint32_t d[8];
+  int64_t acc = 0;
+  uint32_t nz = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    acc += (int64_t)sc_L(i) - (int64_t)u[i];
+    d[i] = (uint32_t)acc;
+    acc >>= 32;
+    nz |= u[i];
+  }
+  const bool flip = neg && nz != 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) u[i] = flip ? d[i] : u[i];
+}
+
+}  // namespace cmtv

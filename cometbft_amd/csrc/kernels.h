@@ -5,7 +5,7 @@
 
 namespace cmtv {
 
-constexpr uint32_t kBtabWords = 128 * 36;   // (1..128)B, 36 words per row
+constexpr uint32_t kBtabWords = 2 * 128 * 36;  // (1..128)B, (1..128)[2^124]B; 36 words per row
 constexpr uint32_t kAtabWordsPerLane = 320; // (1..8)(-A), 40 words per point
 constexpr uint32_t kCombWords = 32 * 128 * 32;     // one registered-key comb (keyed.h), 512 KiB
 constexpr uint32_t kCombScratchWordsPerKey = 128 * 320;  // prefix products while building

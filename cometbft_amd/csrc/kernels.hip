@@ -13,7 +13,8 @@
 //   pk   : n x 32 B   (row i = 8 words, read as 2 x dwordx4)
 //   sig  : n x 64 B   (row i = 16 words, 4 x dwordx4)
 //   msg  : flat bytes + (n+1) u32 offsets
-//   btab : 128 rows x 36 words (ypx, ymx, 2dxy; 10 limbs + 2 pad each) = 18 KiB,
+//   btab : 2 x 128 rows x 36 words (ypx, ymx, 2dxy; 10 limbs + 2 pad each) = 36 KiB:
+//          (1..128)B, then (1..128)[2^124]B (quad kernel's high-half table),
 //          L1/L2-resident; one coordinate gathered per lane as 2 x dwordx4 + dwordx2
 //   atab : per-lane (1..8)(-A) cached table, word-major / lane-minor
 //          [(e*40 + w) * stride + lane] so each of the 40 word loads of a row
@@ -28,6 +29,10 @@
 
 // Minimum waves per SIMD the verify kernel is compiled for (the second
 // __launch_bounds__ argument): caps VGPRs at 512 / waves.
+#ifndef CMTV_QUAD_WAVES_PER_EU
+#define CMTV_QUAD_WAVES_PER_EU 1
+#endif
+
 #ifndef CMTV_VERIFY_WAVES_PER_EU
 #define CMTV_VERIFY_WAVES_PER_EU 2
 #endif
@@ -83,6 +88,7 @@ struct DevQuad {
   __device__ __forceinline__ uint32_t perm32(uint32_t x) const {
     return dpp<PAT>(x);
   }
+  __device__ __forceinline__ bool any(bool x) const { return __ballot(x) != 0; }
 };
 
 // Per-lane (1..8)(-A) table, word-major / lane-minor: word w of entry e for
@@ -121,13 +127,14 @@ __device__ __forceinline__ void load_words(uint32_t* w, const uint32_t* __restri
   }
 }
 
+// rows 0..127: (1..128)B; rows 128..255: (1..128)[2^124]B
 __global__ __launch_bounds__(64) void k_btab_init(uint32_t* __restrict__ rows) {
-  const int m = blockIdx.x * 64 + threadIdx.x + 1;
-  if (m > BTAB_ENTRIES) return;
+  const int e = blockIdx.x * 64 + threadIdx.x;
+  if (e >= 2 * BTAB_ENTRIES) return;
   uint32_t row[BTAB_ROW_WORDS];
-  btab_entry(row, m);
+  btab_entry(row, (e % BTAB_ENTRIES) + 1, e >= BTAB_ENTRIES);
 #pragma unroll
-  for (int i = 0; i < BTAB_ROW_WORDS; i++) rows[(m - 1) * BTAB_ROW_WORDS + i] = row[i];
+  for (int i = 0; i < BTAB_ROW_WORDS; i++) rows[e * BTAB_ROW_WORDS + i] = row[i];
 }
 
 template <uint32_t MODE>
@@ -153,8 +160,28 @@ __global__ __launch_bounds__(64, CMTV_VERIFY_WAVES_PER_EU) void k_verify(uint32_
 // chip at one signature per lane, this cuts per-signature latency ~2x.
 // Verdict bits: lane 0 of each quad votes in a ballot; the 16 quad bits of a
 // wave are compacted into one 16-bit slice of the bitmap.
+// Quad (0..8)(-A) table in LDS: entry e, limb pair k of lane t at
+// slot (e * 5 + k) * 64 + t -- a wave's ds_read_b64 covers 512 contiguous
+// bytes whatever entries its 16 signatures pick, so lookups are conflict-free.
+struct DevATabQ {
+  uint2* lds;
+  uint32_t t;
+  __device__ __forceinline__ void store(int e, const fe& c) {
+#pragma unroll
+    for (int k = 0; k < 5; k++) lds[(e * 5 + k) * 64 + t] = make_uint2(c.v[2 * k], c.v[2 * k + 1]);
+  }
+  __device__ __forceinline__ void load(int e, fe& c) const {
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+      const uint2 x = lds[(e * 5 + k) * 64 + t];
+      c.v[2 * k] = x.x;
+      c.v[2 * k + 1] = x.y;
+    }
+  }
+};
+
 template <uint32_t MODE>
-__global__ __launch_bounds__(64, 2) void k_verify_quad(uint32_t n, const uint32_t* __restrict__ pk,
+__global__ __launch_bounds__(64, CMTV_QUAD_WAVES_PER_EU) void k_verify_quad(uint32_t n, const uint32_t* __restrict__ pk,
                                                        const uint32_t* __restrict__ sig,
                                                        const uint8_t* __restrict__ msg,
                                                        const uint32_t* __restrict__ off,
@@ -168,7 +195,9 @@ __global__ __launch_bounds__(64, 2) void k_verify_quad(uint32_t n, const uint32_
   const uint32_t m0 = off[i], m1 = off[i + 1];
   DevQuad q;
   DevBTabQ bt{btab};
-  bool v = q_verify<MODE>(q, pk + 8 * (size_t)i, sig + 16 * (size_t)i, msg + m0, m1 - m0, bt);
+  __shared__ uint2 tab_lds[2 * 9 * 5 * 64];  // (0..8)(-A), (0..8)(-/+R): 45 KiB per wave
+  DevATabQ ta{tab_lds, threadIdx.x}, tr{tab_lds + 9 * 5 * 64, threadIdx.x};
+  bool v = q_verify<MODE>(q, pk + 8 * (size_t)i, sig + 16 * (size_t)i, msg + m0, m1 - m0, bt, ta, tr);
   v = v && active;
   if (active && (threadIdx.x & 3) == 0 && out_valid) out_valid[s] = v ? 1 : 0;
   uint64_t x = __ballot(v && (threadIdx.x & 3) == 0) & 0x1111111111111111ull;
@@ -287,7 +316,7 @@ __global__ __launch_bounds__(64) void k_sign(uint32_t n, const uint32_t* __restr
 static inline unsigned blocks_for(uint32_t n) { return (n + 63) / 64; }
 
 hipError_t launch_btab_init(uint32_t* d_rows, hipStream_t s) {
-  hipLaunchKernelGGL(k_btab_init, dim3(blocks_for(BTAB_ENTRIES)), dim3(64), 0, s, d_rows);
+  hipLaunchKernelGGL(k_btab_init, dim3(blocks_for(2 * BTAB_ENTRIES)), dim3(64), 0, s, d_rows);
   return hipGetLastError();
 }
 

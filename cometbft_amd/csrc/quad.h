@@ -16,6 +16,7 @@
 //   template <int PAT> void perm(fe& o, const fe& v) const;
 //                          lane c receives v from lane (PAT >> 2c) & 3
 //   template <int PAT> uint32_t perm32(uint32_t x) const;
+//   bool any(bool x) const;   x on any lane of the wave (uniform loop bounds)
 // The device policy lowers perm to v_mov_b32_dpp quad_perm; the host test
 // policy (tests/host/quadcheck.cpp) runs 4 threads in lockstep, so the same
 // source is checked against the oracle on the CPU.
@@ -23,6 +24,7 @@
 // Control flow is uniform across a quad (digits, verdicts and mode are per
 // signature); only data differs per lane, via pick() selects.
 #pragma once
+#include "halfscalar.h"
 #include "verify_core.h"
 
 namespace cmtv {
@@ -156,17 +158,108 @@ CMTV_HD bool y_is_canonical(const uint32_t w[8]) {
 //   phase 1: lanes {0,2} decode A, lanes {1,3} decode R (same code, different
 //            data, so the two square-root chains run simultaneously); every
 //            lane hashes k = SHA-512(R || A || M) mod L
-//   phase 2: (1..8)(-A) in cached form, one coordinate per lane, in registers
-//   phase 3: Straus over signed radix-16 (k) / radix-256 (s) digits
-//   final  : GO_STDLIB -- R canonical and R' == R projectively (equivalent to
-//            encode(R') == R bytes, with no inversion); ZIP215 -- [8](R' - R) == O
+//   phase 2: half-size scalars k1 == k2 k (mod 8L), u = k2 s mod L
+//   phase 3: (0..8)(-A) and (0..8)(-/+R) in cached form, one coordinate per
+//            lane, in the ATab policy's storage (LDS on the device)
+//   phase 4: Straus over 34 (wide: 64) 4-bit windows: per window 4 shared
+//            doublings, one A and one R addition (signed radix-16 digits) and
+//            one fixed-base addition (signed radix-256 digits of u's low half
+//            against (1..128)B on even windows, of its high half against
+//            (1..128)[2^124]B on odd ones)
+//   final  : X = [k2](R' - R) is O (GO_STDLIB, with R canonical: encode(R')
+//            == R bytes; no inversion) or [8]X = O (ZIP215)
+// (0..8)P in cached form (entry 0 = the identity), one coordinate per lane;
+// v holds this lane's coordinate of P and is clobbered.
+template <class Q, class ATab>
+CMTV_HD void q_build_table(const Q& q, ATab& tab, fe& v) {
+  const int lane = q.lane();
+  fe c1, c;
+  q_cached_identity(c, lane);
+  tab.store(0, c);
+  q_to_cached(q, c1, v);
+  tab.store(1, c1);
+  q_dbl(q, v);
+  q_to_cached(q, c, v);
+  tab.store(2, c);
+#pragma unroll 1
+  for (int e = 3; e <= 8; e++) {
+    q_add(q, v, c1);
+    q_to_cached(q, c, v);
+    tab.store(e, c);
+  }
+}
+
+// Signed radix-16 digit stream of x (|digits| <= 8) read from the top with
+// sc_shift_out(t, 4): wide -> 64 windows, else HS_WINDOWS = 34 windows
+// (x < 2^134), left-aligned so the first shift_out yields the top digit.
+CMTV_HD void hs_digits16(uint32_t t[8], const uint32_t x[8], bool wide) {
+  uint32_t a[8], b[8];
+  sc_bias(a, x, 0x88888888u);
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t bias = i < 4 ? 0x88888888u : (i == 4 ? 0x88u : 0u);
+    const uint64_t v = (uint64_t)x[i] + bias + c;
+    b[i] = (uint32_t)v;
+    c = v >> 32;
+  }
+  // b < 2^136: shift left by 120 bits (3 words + 24 bits)
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t hi = i >= 3 ? b[i - 3] : 0u;
+    const uint32_t lo = i >= 4 ? b[i - 4] : 0u;
+    const uint32_t sh = (hi << 24) | (lo >> 8);
+    t[i] = wide ? a[i] : sh;
+  }
+}
+
+// Signed radix-256 digit streams of u < L split at 2^128, each read from the
+// top with sc_shift_out(t, 8): tLo yields digits 16..0 of u mod 2^128
+// (17 digits), tHi digits 15..0 of u >> 128 (< 2^125, 16 digits).
+CMTV_HD void hs_digits256(uint32_t tLo[8], uint32_t tHi[8], const uint32_t u[8]) {
+  uint32_t lo[5];
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 5; i++) {
+    const uint64_t v = (uint64_t)(i < 4 ? u[i] : 0u) + (i < 4 ? 0x80808080u : 0x80u) + c;
+    lo[i] = (uint32_t)v;
+    c = v >> 32;
+  }
+  // lo < 2^136: shift left by 120 bits
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t hi = (i >= 3 && i - 3 < 5) ? lo[i - 3] : 0u;
+    const uint32_t lw = (i >= 4 && i - 4 < 5) ? lo[i - 4] : 0u;
+    tLo[i] = (hi << 24) | (lw >> 8);
+  }
+  c = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint64_t v = (uint64_t)u[4 + i] + 0x80808080u + c;
+    tHi[4 + i] = (uint32_t)v;
+    tHi[i] = 0;
+    c = v >> 32;
+  }
+}
+
 struct NullProbe {
   CMTV_HD void snap(int, const fe&) const {}
 };
 
-template <uint32_t MODE, class Q, class BTab, class Probe = NullProbe>
+// Table policy for the per-signature (0..8)(-A) cached table (entry 0 = the
+// identity), one coordinate per lane:
+//   void store(int e, const fe& c);  void load(int e, fe& c) const;
+// The device policy keeps it in LDS (a per-lane slot, so no barrier is needed
+// and a lookup is 5 ds_read_b64 instead of an 8-way register select).
+struct QArrayTab {  // plain-array table policy (host checks, debug kernels)
+  fe t[9];
+  CMTV_HD void store(int e, const fe& c) { t[e] = c; }
+  CMTV_HD void load(int e, fe& c) const { c = t[e]; }
+};
+
+template <uint32_t MODE, class Q, class BTab, class ATab, class Probe = NullProbe>
 CMTV_HD bool q_verify(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig_ptr, const uint8_t* msg,
-                      uint32_t mlen, const BTab& btab, const Probe& probe = Probe()) {
+                      uint32_t mlen, const BTab& btab, ATab& tabA, ATab& tabR, const Probe& probe = Probe()) {
   const int lane = q.lane();
   uint32_t w[16];
 #pragma unroll
@@ -226,80 +319,98 @@ CMTV_HD bool q_verify(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig_pt
     probe.snap(2, kk);
   }
 
-  // ---- phase 2: (1..8)(-A), this lane's cached coordinate of each
-  fe tab[8];
-  q_to_cached(q, tab[0], v);
-  q_dbl(q, v);
-  q_to_cached(q, tab[1], v);
+  // ---- phase 2: half-size scalars (halfscalar.h) and the fixed-base scalar
+  //   X = [u]B + [k1](-A) + [|k2|](k2 < 0 ? R : -R) = [k2](R' - R),
+  //   u = k2 s mod L; the window count is uniform over the wave
+  HalfScalars hs;
+  half_scalars(hs, k);
+  uint32_t u[8];
+  hs_bscalar(u, hs.k2, hs.k2_neg, ts);
+  const bool wide = q.any(hs.wide);
+  const int W = wide ? HS_WIDE_WINDOWS : HS_WINDOWS;
+  {
+    fe kk;
 #pragma unroll
-  for (int e = 2; e < 8; e++) {
-    q_add(q, v, tab[0]);
-    q_to_cached(q, tab[e], v);
+    for (int i = 0; i < 8; i++) kk.v[i] = hs.k1[i];
+    kk.v[8] = hs.k2[0];
+    kk.v[9] = (hs.k2_neg ? 1u : 0u) | (hs.wide ? 2u : 0u);
+    probe.snap(11, kk);
   }
-  probe.snap(3, tab[0]);
-  probe.snap(4, tab[1]);
-  probe.snap(5, tab[7]);
 
-  // ---- phase 3: Straus
-  uint32_t tk[8];
-  sc_bias(tk, k, 0x88888888u);
-  sc_bias(ts, ts, 0x80808080u);
+  // ---- phase 3: (0..8)(-A) and (0..8)(-/+R), this lane's cached coordinate
+  {
+    fe t;
+    fe_neg(t, rc);
+    fe_carry(t);
+    fe_select(rc, rc, t, !hs.k2_neg && (lane == 0 || lane == 3));
+  }
+  q_build_table(q, tabA, v);
+  q_build_table(q, tabR, rc);
+
+  // ---- phase 4: Straus over W shared 4-bit windows
+  uint32_t tA[8], tR[8], tLo[8], tHi[8];
+  hs_digits16(tA, hs.k1, wide);
+  hs_digits16(tR, hs.k2, wide);
+  hs_digits256(tLo, tHi, u);
   q_identity(v, lane);
   // lane -> offset of its niels coordinate in a B-table row (y-x, y+x, 1, 2dxy)
   const int boff = lane == 0 ? BTAB_COORD_WORDS : (lane == 3 ? 2 * BTAB_COORD_WORDS : 0);
 #pragma unroll 1
-  for (int win = 0; win < 64; win++) {
+  for (int win = W - 1; win >= 0; win--) {
+    if (win != W - 1) {
 #pragma unroll 1
-    for (int d = 0; d < 4; d++) q_dbl(q, v);
+      for (int d = 0; d < 4; d++) q_dbl(q, v);
+    }
     {
-      const int dA = (int)sc_shift_out(tk, 4) - 8;
-      const int ia = dA < 0 ? -dA : dA;
+      const int dA = (int)sc_shift_out(tA, 4) - 8;
       fe c;
-      q_cached_identity(c, lane);
-#pragma unroll
-      for (int e = 0; e < 8; e++) fe_select(c, c, tab[e], ia == e + 1);
+      tabA.load(dA < 0 ? -dA : dA, c);
       q_cached_cneg(q, c, dA < 0);
       q_add(q, v, c);
     }
-    if (win & 1) {
-      const int dB = (int)sc_shift_out(ts, 8) - 128;
+    {
+      const int dR = (int)sc_shift_out(tR, 4) - 8;
+      fe c;
+      tabR.load(dR < 0 ? -dR : dR, c);
+      q_cached_cneg(q, c, dR < 0);
+      q_add(q, v, c);
+    }
+    if (win <= 32 && ((win & 1) == 0 || win <= 31)) {
+      // even windows: digit win/2 of u mod 2^128 against (1..128)B;
+      // odd windows: digit (win-1)/2 of u >> 128 against (1..128)[2^124]B
+      const bool odd = win & 1;
+      int dB;
+      if (odd)
+        dB = (int)sc_shift_out(tHi, 8) - 128;
+      else
+        dB = (int)sc_shift_out(tLo, 8) - 128;
       const int ib = dB < 0 ? -dB : dB;
       fe c;
-      btab.load_coord(ib > 0 ? ib - 1 : 0, boff, c);
+      btab.load_coord((ib > 0 ? ib - 1 : 0) + (odd ? BTAB_ENTRIES : 0), boff, c);
       const bool one = lane == 2 || (ib == 0 && lane != 3);
 #pragma unroll
       for (int i = 0; i < 10; i++) c.v[i] = (ib == 0 || lane == 2) ? ((one && i == 0) ? 1u : 0u) : c.v[i];
       q_cached_cneg(q, c, dB < 0);
       q_add(q, v, c);
     }
-    if (win < 4) probe.snap(6 + win, v);
+    if (win >= W - 4) probe.snap(6 + (W - 1 - win), v);
   }
   probe.snap(10, v);
 
-  // ---- final check
-  if (MODE == MODE_GO_STDLIB) {
-    fe z, t;
-    q.template perm<QP_B2>(z, v);  // Z'
-    fe_mul(t, z, rc);              // lane 0: x_R Z', lane 1: y_R Z'
-    const bool eq = fe_equal(t, v);
-    const bool e0 = q.template perm32<QP_B0>(eq ? 1u : 0u) != 0;
-    const bool e1 = q.template perm32<QP_B1>(eq ? 1u : 0u) != 0;
-    return s_ok && a_ok && r_ok && r_canon && e0 && e1;
-  } else {
-    fe c;
-    q_to_cached(q, c, rc);
-    q_cached_cneg(q, c, true);
-    q_add(q, v, c);
+  // ---- final check: X = O (GO_STDLIB: R' == R with R canonical, i.e.
+  //      encode(R') == R bytes) / [8]X = O (ZIP215)
+  if (MODE == MODE_ZIP215) {
 #pragma unroll 1
     for (int d = 0; d < 3; d++) q_dbl(q, v);
-    fe z;
-    q.template perm<QP_B2>(z, v);
-    const bool x0 = fe_iszero(v);      // meaningful on lane 0
-    const bool yz = fe_equal(v, z);    // meaningful on lane 1
-    const bool e0 = q.template perm32<QP_B0>(x0 ? 1u : 0u) != 0;
-    const bool e1 = q.template perm32<QP_B1>(yz ? 1u : 0u) != 0;
-    return s_ok && a_ok && r_ok && e0 && e1;
   }
+  fe z;
+  q.template perm<QP_B2>(z, v);
+  const bool x0 = fe_iszero(v);    // meaningful on lane 0
+  const bool yz = fe_equal(v, z);  // meaningful on lane 1
+  const bool e0 = q.template perm32<QP_B0>(x0 ? 1u : 0u) != 0;
+  const bool e1 = q.template perm32<QP_B1>(yz ? 1u : 0u) != 0;
+  if (MODE == MODE_GO_STDLIB) return s_ok && a_ok && r_ok && r_canon && e0 && e1;
+  return s_ok && a_ok && r_ok && e0 && e1;
 }
 
 }  // namespace cmtv

@@ -53,12 +53,25 @@ CMTV_HD void cached_neg_point(ge_p3& r, const ge_p3& p) {
 }
 
 // [m]B for m = 1..128 in affine niels form (one entry; used by the table
-// initialisation kernel and by host-side tests)
-CMTV_HD void btab_entry(uint32_t row[BTAB_ROW_WORDS], int m) {
+// initialisation kernel and by host-side tests). Rows 128..255 of the device
+// table hold [m 2^124]B (hi = 1), the second fixed-base table of the
+// half-size-scalar verifier (halfscalar.h).
+CMTV_HD void btab_entry(uint32_t row[BTAB_ROW_WORDS], int m, bool hi = false) {
   uint32_t bw[8];
   basepoint_words(bw);
   ge_p3 B, acc;
   p3_frombytes(B, bw);
+  if (hi) {
+    ge_efgh t;
+    ge_p2 q;
+    p3_to_p2(q, B);
+#pragma unroll 1
+    for (int i = 0; i < 124; i++) {
+      p2_dbl(t, q);
+      efgh_to_p2(q, t);
+    }
+    efgh_to_p3(B, t);
+  }
   ge_cached Bc;
   p3_to_cached(Bc, B);
   p3_identity(acc);

@@ -1,0 +1,23 @@
+// Host build of cometbft_amd/csrc/halfscalar.h (the device source): reads
+// n x 32-byte little-endian scalars k on stdin, writes per scalar
+// k1 (32 B) | |k2| (32 B) | flags (1 B: bit0 k2 negative, bit1 wide). Test
+// infrastructure only (tests/test_host_math.py checks the invariants).
+#define CMTV_HD inline
+#include <cstdio>
+#include "../../cometbft_amd/csrc/halfscalar.h"
+
+int main() {
+  uint32_t n;
+  if (fread(&n, 4, 1, stdin) != 1) return 1;
+  for (uint32_t i = 0; i < n; i++) {
+    uint32_t k[8];
+    if (fread(k, 4, 8, stdin) != 8) return 1;
+    cmtv::HalfScalars h;
+    cmtv::half_scalars(h, k);
+    uint8_t f = (h.k2_neg ? 1 : 0) | (h.wide ? 2 : 0);
+    fwrite(h.k1, 4, 8, stdout);
+    fwrite(h.k2, 4, 8, stdout);
+    fwrite(&f, 1, 1, stdout);
+  }
+  return 0;
+}

@@ -4,7 +4,7 @@
 //   stdin/stdout protocol as hostcheck.cpp (verify mode only).
 #define CMTV_HD inline
 #define CMTV_BOUNDS_CHECK 1
-#include <barrier>
+#include <atomic>
 #include <cstdio>
 #include <cstring>
 #include <thread>
@@ -13,8 +13,25 @@
 
 using namespace cmtv;
 
+// sense-reversing spin barrier for the 4 lane threads (a futex barrier makes
+// the ~10^5 exchanges per signature dominate the run time)
+struct SpinBarrier {
+  std::atomic<int> count{0};
+  std::atomic<int> gen{0};
+  void arrive_and_wait() {
+    const int g = gen.load(std::memory_order_acquire);
+    if (count.fetch_add(1, std::memory_order_acq_rel) == 3) {
+      count.store(0, std::memory_order_relaxed);
+      gen.store(g + 1, std::memory_order_release);
+      return;
+    }
+    for (int spins = 0; gen.load(std::memory_order_acquire) == g; spins++)
+      if (spins > 256) std::this_thread::yield();
+  }
+};
+
 struct Exchange {
-  std::barrier<> bar{4};
+  SpinBarrier bar;
   fe slot[4];
 };
 
@@ -38,12 +55,13 @@ struct HostQuad {
     perm<PAT>(o, t);
     return o.v[0];
   }
+  bool any(bool x) const { return x; }  // the four lanes of one quad agree
 };
 
 struct HostBTab {
   std::vector<uint32_t> rows;
-  HostBTab() : rows(BTAB_ENTRIES * BTAB_ROW_WORDS) {
-    for (int m = 1; m <= BTAB_ENTRIES; m++) btab_entry(&rows[(m - 1) * BTAB_ROW_WORDS], m);
+  HostBTab() : rows(2 * BTAB_ENTRIES * BTAB_ROW_WORDS) {
+    for (int e = 0; e < 2 * BTAB_ENTRIES; e++) btab_entry(&rows[e * BTAB_ROW_WORDS], e % BTAB_ENTRIES + 1, e >= BTAB_ENTRIES);
   }
   void load_coord(int e, int off, fe& r) const {
     const uint32_t* p = &rows[e * BTAB_ROW_WORDS + off];
@@ -77,8 +95,9 @@ int main() {
     for (int l = 0; l < 4; l++)
       th.emplace_back([&, l] {
         HostQuad q{l, &ex};
-        res[l] = mode ? q_verify<MODE_ZIP215>(q, pkw, sigw, mp, mlen, bt)
-                      : q_verify<MODE_GO_STDLIB>(q, pkw, sigw, mp, mlen, bt);
+        QArrayTab ta, tr;
+        res[l] = mode ? q_verify<MODE_ZIP215>(q, pkw, sigw, mp, mlen, bt, ta, tr)
+                      : q_verify<MODE_GO_STDLIB>(q, pkw, sigw, mp, mlen, bt, ta, tr);
       });
     for (auto& t : th) t.join();
     if (res[0] != res[1] || res[0] != res[2] || res[0] != res[3]) {

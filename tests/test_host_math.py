@@ -13,15 +13,27 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "tests", "host", "hostcheck.cpp")
 BIN = os.path.join(ROOT, "build", "hostcheck")
+QSRC = os.path.join(ROOT, "tests", "host", "quadcheck.cpp")
+QBIN = os.path.join(ROOT, "build", "quadcheck")
 
 
 @pytest.fixture(scope="module")
 def hostcheck():
-    os.makedirs(os.path.dirname(BIN), exist_ok=True)
-    deps = [SRC] + [os.path.join(ROOT, "cometbft_amd", "csrc", f) for f in os.listdir(os.path.join(ROOT, "cometbft_amd", "csrc")) if f.endswith(".h")]
-    if not os.path.exists(BIN) or os.path.getmtime(BIN) < max(os.path.getmtime(d) for d in deps):
-        subprocess.run(["g++", "-O2", "-std=c++17", "-o", BIN, SRC], check=True)
-    return BIN
+    return _build(SRC, BIN, ["-std=c++17"])
+
+
+@pytest.fixture(scope="module")
+def quadcheck():
+    return _build(QSRC, QBIN, ["-std=c++20", "-pthread"])
+
+
+def _build(src, binary, flags):
+    os.makedirs(os.path.dirname(binary), exist_ok=True)
+    hdr = os.path.join(ROOT, "cometbft_amd", "csrc")
+    deps = [src] + [os.path.join(hdr, f) for f in os.listdir(hdr) if f.endswith(".h")]
+    if not os.path.exists(binary) or os.path.getmtime(binary) < max(os.path.getmtime(d) for d in deps):
+        subprocess.run(["g++", "-O2"] + flags + ["-o", binary, src], check=True)
+    return binary
 
 
 def _run(binary, arg, corpus, idx, mode):
@@ -59,3 +71,49 @@ def test_keyed_pipeline_matches_corpus(hostcheck, corpus, mode):
     want = (corpus["go"] if mode == 0 else corpus["zip215"])[idx]
     bad = np.nonzero(got != want)[0]
     assert bad.size == 0, [(idx[int(i)], corpus["cats"][idx[int(i)]]) for i in bad[:10]]
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_quad_pipeline_matches_corpus(quadcheck, corpus, mode):
+    """The 4-lane quad kernel's source (quad.h), four host threads in lockstep
+    standing in for the DPP quad_perm exchanges (every adversarial vector and
+    a slice of the honest ones: the lockstep emulation is ~40 ms a vector)."""
+    idx = _keyed_subset(corpus)[::3]
+    got = _run(quadcheck, None, corpus, idx, mode)
+    want = (corpus["go"] if mode == 0 else corpus["zip215"])[idx]
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(idx[int(i)], corpus["cats"][idx[int(i)]]) for i in bad[:10]]
+
+
+HSRC = os.path.join(ROOT, "tests", "host", "halfcheck.cpp")
+HBIN = os.path.join(ROOT, "build", "halfcheck")
+L = 2**252 + 27742317777372353535851937790883648493
+
+
+def test_half_scalar_decomposition():
+    """halfscalar.h (the device source, host-compiled): k1 == k2 k (mod 8L),
+    k2 odd, 0 <= k1 < 2^134 and 0 < |k2| < 2^134 unless flagged wide (then
+    k1 = k, k2 = 1). Random scalars plus the boundary ones; the wide rate
+    must stay rare (it only costs time, never changes a verdict)."""
+    binary = _build(HSRC, HBIN, ["-std=c++17"])
+    rng = np.random.default_rng(215)
+    ks = [0, 1, 2, 3, L - 1, L - 2, 2**127, 2**128 - 1, 2**134, 2**252]
+    ks += [int.from_bytes(rng.bytes(32), "little") % L for _ in range(20000)]
+    buf = struct.pack("<I", len(ks)) + b"".join(k.to_bytes(32, "little") for k in ks)
+    out = subprocess.run([binary], input=buf, capture_output=True, check=True, timeout=120).stdout
+    assert len(out) == 65 * len(ks)
+    wide = 0
+    for j, k in enumerate(ks):
+        rec = out[65 * j: 65 * (j + 1)]
+        k1 = int.from_bytes(rec[:32], "little")
+        k2 = int.from_bytes(rec[32:64], "little")
+        f = rec[64]
+        if f & 2:
+            wide += 1
+            assert (k1, k2, f & 1) == (k, 1, 0), j
+            continue
+        s2 = -k2 if f & 1 else k2
+        assert k2 & 1, j
+        assert k1 < 2**134 and 0 < k2 < 2**134, j
+        assert (k1 - s2 * k) % (8 * L) == 0, j
+    assert wide <= 20, wide

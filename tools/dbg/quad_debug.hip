@@ -13,7 +13,7 @@
 
 using namespace cmtv;
 
-constexpr int NSNAP = 11;
+constexpr int NSNAP = 12;
 
 template <int VAR>
 struct DevQuad {
@@ -35,6 +35,7 @@ struct DevQuad {
   }
   template <int PAT>
   __device__ uint32_t perm32(uint32_t x) const { return one<PAT>(x); }
+  __device__ bool any(bool x) const { return __ballot(x) != 0; }
 };
 struct DevBTabQ {
   const uint32_t* rows;
@@ -59,13 +60,29 @@ struct TimeProbe {
     if (threadIdx.x == 0) out[id] = t;
   }
 };
-__global__ void k_time(const uint32_t* pk, const uint32_t* sig, const uint8_t* msg, uint32_t mlen,
+struct LdsTab {  // same layout as kernels.hip's DevATabQ
+  uint2* lds;
+  uint32_t t;
+  __device__ void store(int e, const fe& c) {
+    for (int k = 0; k < 5; k++) lds[(e * 5 + k) * 64 + t] = make_uint2(c.v[2 * k], c.v[2 * k + 1]);
+  }
+  __device__ void load(int e, fe& c) const {
+    for (int k = 0; k < 5; k++) {
+      const uint2 x = lds[(e * 5 + k) * 64 + t];
+      c.v[2 * k] = x.x;
+      c.v[2 * k + 1] = x.y;
+    }
+  }
+};
+__global__ __launch_bounds__(64, 1) void k_time(const uint32_t* pk, const uint32_t* sig, const uint8_t* msg, uint32_t mlen,
                        const uint32_t* btab, unsigned long long* ts, int* verdict) {
   DevQuad<1> q;
   DevBTabQ bt{btab};
   if (threadIdx.x == 0) ts[15] = __builtin_amdgcn_s_memtime();
   TimeProbe pr{ts};
-  bool v = q_verify<MODE_GO_STDLIB>(q, pk, sig, msg, mlen, bt, pr);
+  __shared__ uint2 lds[2 * 9 * 5 * 64];
+  LdsTab ta{lds, threadIdx.x}, tr{lds + 9 * 5 * 64, threadIdx.x};
+  bool v = q_verify<MODE_GO_STDLIB>(q, pk, sig, msg, mlen, bt, ta, tr, pr);
   verdict[threadIdx.x] = v;
   if (threadIdx.x == 0) ts[14] = __builtin_amdgcn_s_memtime();
 }
@@ -81,7 +98,8 @@ __global__ void k_probe(const uint32_t* pk, const uint32_t* sig, const uint8_t* 
   DevQuad<VAR> q;
   DevBTabQ bt{btab};
   DevProbe pr{snaps};
-  bool v = q_verify<MODE_GO_STDLIB>(q, pk, sig, msg, mlen, bt, pr);
+  QArrayTab at, at2;
+  bool v = q_verify<MODE_GO_STDLIB>(q, pk, sig, msg, mlen, bt, at, at2, pr);
   verdict[threadIdx.x] = v;
 }
 
@@ -114,6 +132,7 @@ struct HostQuad {
     perm<PAT>(o, t);
     return o.v[0];
   }
+  bool any(bool x) const { return x; }
 };
 struct HostBTabQ {
   const uint32_t* rows;
@@ -159,8 +178,8 @@ int main() {
   uint8_t msg[4] = {0x72, 0, 0, 0};
   uint32_t mlen = 1;
 
-  std::vector<uint32_t> btab(BTAB_ENTRIES * BTAB_ROW_WORDS);
-  for (int m = 1; m <= BTAB_ENTRIES; m++) btab_entry(&btab[(m - 1) * BTAB_ROW_WORDS], m);
+  std::vector<uint32_t> btab(2 * BTAB_ENTRIES * BTAB_ROW_WORDS);
+  for (int e = 0; e < 2 * BTAB_ENTRIES; e++) btab_entry(&btab[e * BTAB_ROW_WORDS], e % BTAB_ENTRIES + 1, e >= BTAB_ENTRIES);
 
   // host emulation
   std::vector<uint32_t> hs(NSNAP * 40, 0);
@@ -173,7 +192,8 @@ int main() {
         HostQuad q{l, &ex};
         HostBTabQ bt{btab.data()};
         HostProbe pr{hs.data(), l};
-        hres[l] = q_verify<MODE_GO_STDLIB>(q, pk, sig, msg, mlen, bt, pr);
+        QArrayTab at, at2;
+        hres[l] = q_verify<MODE_GO_STDLIB>(q, pk, sig, msg, mlen, bt, at, at2, pr);
       });
     for (auto& t : th) t.join();
   }
@@ -191,7 +211,7 @@ int main() {
   (void)hipMemcpy(dsig, sig, 64, hipMemcpyHostToDevice);
   (void)hipMemcpy(dmsg, msg, 4, hipMemcpyHostToDevice);
   // device-built table must equal the host-built one
-  hipLaunchKernelGGL(k_btab, dim3(1), dim3(128), 0, 0, dbt);
+  hipLaunchKernelGGL(k_btab, dim3(1), dim3(256), 0, 0, dbt);
   std::vector<uint32_t> dbtab(btab.size());
   (void)hipMemcpy(dbtab.data(), dbt, btab.size() * 4, hipMemcpyDeviceToHost);
   printf("btab device==host: %d\n", (int)(dbtab == btab));
@@ -227,9 +247,9 @@ int main() {
       hipLaunchKernelGGL(k_time, dim3(1), dim3(64), 0, 0, dpk, dsig, dmsg, mlen, dbt, dts, dv);
       unsigned long long ts[16];
       (void)hipMemcpy(ts, dts, 16 * 8, hipMemcpyDeviceToHost);
-      printf("cycles: decode %llu sha %llu table %llu win0 %llu win1 %llu win2 %llu win3 %llu loop(64) %llu final %llu total %llu\n",
-             ts[0] - ts[15], ts[2] - ts[1], ts[3] - ts[2], ts[6] - ts[5], ts[7] - ts[6], ts[8] - ts[7], ts[9] - ts[8],
-             ts[10] - ts[5], ts[14] - ts[10], ts[14] - ts[15]);
+      printf("cycles: decode %llu sha %llu halfscalar %llu tables+win0 %llu win1 %llu win2 %llu win3 %llu loop(rest) %llu final %llu total %llu\n",
+             ts[0] - ts[15], ts[2] - ts[1], ts[11] - ts[2], ts[6] - ts[11], ts[7] - ts[6], ts[8] - ts[7], ts[9] - ts[8],
+             ts[10] - ts[6], ts[14] - ts[10], ts[14] - ts[15]);
     }
   }
   run(k_probe<0>, "mov_dpp");

@@ -25,9 +25,14 @@
 //     input changes its verdict, only its cost.
 //
 // Arithmetic: the Euclid runs on 8-word values kept left-normalised (r0's top
-// bit at bit 255, both remainders shifted by the same e), so each quotient
-// comes from the top 64 bits in one f64 division, corrected by at most a few
-// add/subtract steps; t values are 6-word two's complement.
+// bit at bit 255, both remainders shifted by the same e) and t values in
+// 6-word two's complement. Lehmer rounds run ~9 Euclid steps at a time on the
+// 30-bit leading digits (single-word cofactors, exact quotients by f64
+// division) and apply the 2x2 cofactor matrix to the full values once per
+// round: ~10 multi-word updates per scalar instead of ~75. A round that
+// cannot certify a quotient falls back to one exact multi-word step, whose
+// quotient comes from the top 64 bits in one f64 division corrected by at
+// most a few add/subtract steps.
 #pragma once
 #include <math.h>
 #include <stdint.h>
@@ -43,7 +48,8 @@ namespace cmtv {
 constexpr int HS_WINDOWS = 34;      // 4-bit windows for normal pairs (136 bits)
 constexpr int HS_WIDE_WINDOWS = 64; // k1 = k, k2 = 1
 constexpr int HS_MAX_BITS = 134;    // (2^134 + bias) < 16^34 for the signed-digit bias
-constexpr int HS_MAX_STEPS = 192;   // Euclid steps before giving up (typical: ~75)
+constexpr int HS_MAX_ROUNDS = 192;  // outer rounds before giving up (Lehmer: ~10; exact steps: ~75)
+constexpr int HS_MAX_INNER = 40;    // Lehmer inner steps per round (30-bit digits: ~9)
 
 struct HalfScalars {
   uint32_t k1[8];  // >= 0
@@ -191,7 +197,76 @@ CMTV_HD bool hs_step(uint32_t rr[8], uint32_t tt[6], const uint32_t r0[8], const
   return ok;
 }
 
+// floor(a / b) for 0 <= a < 2^31, 0 < b < 2^31: the correctly rounded f64
+// quotient never reaches the next integer (a/b = n - m/b sits at least 2^-31
+// below n relative, far more than an f64 ulp), so truncation is exact
+CMTV_HD uint32_t hs_udiv31(uint32_t a, uint32_t b) { return (uint32_t)((double)a / (double)b); }
+
+// Lehmer's inner loop (Knuth TAOCP vol. 2, 4.5.2, Algorithm L) on the 30-bit
+// leading digits u = r0 >> h', v = r1 >> h' of the normalised pair (h the
+// digits' bit position at true scale): returns the cofactor matrix of the
+// Euclid steps whose quotients the digits determine for certain
+// (floor((u+A)/(v+C)) == floor((u+B)/(v+D))), and stops before any step whose
+// divisor might already be below 2^127, where the exact Euclid stops: after
+// the accepted steps the true divisor lies in 2^h (v + min(C,D), v + max(C,D)).
+// B == 0 on return: no step was certain.
+CMTV_HD void hs_lehmer(int32_t& A, int32_t& B, int32_t& C, int32_t& D, uint32_t u, uint32_t v, int h) {
+  const int32_t thr = h >= 127 ? 1 : (int32_t)(1u << (127 - h));
+  int32_t a = 1, b = 0, c = 0, d = 1;
+  int32_t uu = (int32_t)u, vv = (int32_t)v;
+#pragma unroll 1
+  for (int it = 0; it < HS_MAX_INNER; it++) {
+    const int32_t vc = vv + c, vd = vv + d;
+    const int32_t lo = vc < vd ? vc : vd;
+    if (lo < thr) break;  // divisor not certainly >= 2^127 (also keeps vc, vd > 0)
+    const uint32_t q = hs_udiv31((uint32_t)(uu + a), (uint32_t)vc);
+    // the other corner must give the same quotient: 0 <= (u+b) - q (v+d) < v+d
+    const int64_t x = (int64_t)(uu + b) - (int64_t)q * vd;
+    if (x < 0 || x >= vd) break;
+    const int32_t nc = (int32_t)((int64_t)a - (int64_t)q * c);
+    const int32_t nd = (int32_t)((int64_t)b - (int64_t)q * d);
+    const int32_t nv = (int32_t)((int64_t)uu - (int64_t)q * vv);
+    a = c;
+    b = d;
+    c = nc;
+    d = nd;
+    uu = vv;
+    vv = nv;
+  }
+  A = a;
+  B = b;
+  C = c;
+  D = d;
+}
+
+// out = P x + Q y modulo 2^(32 W), for cofactors P, Q of opposite signs (or
+// zero) and an exact result in range: evaluated as |P| x - |Q| y or
+// |Q| y - |P| x on unsigned words (x, y two's complement when W = 6)
+template <int W>
+CMTV_HD void hs_lin(uint32_t out[W], int32_t P, const uint32_t x[], int32_t Q, const uint32_t y[]) {
+  const bool pneg = Q > 0;  // then P <= 0 and the positive term is Q y
+  const uint32_t pm = P < 0 ? (uint32_t)(-(int64_t)P) : (uint32_t)P;
+  const uint32_t qm = Q < 0 ? (uint32_t)(-(int64_t)Q) : (uint32_t)Q;
+  const uint32_t mp = pneg ? qm : pm;  // multiplier of the positive term
+  const uint32_t mq = pneg ? pm : qm;
+  uint64_t cp = 0, cq = 0;
+  int64_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < W; i++) {
+    const uint64_t tp = (uint64_t)mp * (pneg ? y[i] : x[i]) + cp;
+    const uint64_t tq = (uint64_t)mq * (pneg ? x[i] : y[i]) + cq;
+    cp = tp >> 32;
+    cq = tq >> 32;
+    acc += (int64_t)(uint32_t)tp - (int64_t)(uint32_t)tq;
+    out[i] = (uint32_t)acc;
+    acc >>= 32;
+  }
+}
+
 // (k1, k2) with k1 == k2 k (mod 8L), k2 odd, both < 2^134, or wide.
+// LEHMER = false: one exact Euclid step per round (the schedule the host test
+// compares against); both give the same pair.
+template <bool LEHMER = true>
 CMTV_HD void half_scalars(HalfScalars& h, const uint32_t k[8]) {
   uint32_t r0[8], r1[8], t0[6], t1[6];
 #pragma unroll
@@ -207,23 +282,49 @@ CMTV_HD void half_scalars(HalfScalars& h, const uint32_t k[8]) {
   int e = 0;  // common left shift of r0, r1
   bool ok = true;
 #pragma unroll 1
-  for (int step = 0; step < HS_MAX_STEPS; step++) {
+  for (int round = 0; round < HS_MAX_ROUNDS; round++) {
     const int bl1 = (r1[7] ? 256 - hs_clz(r1[7]) : hs_bitlen8(r1)) - e;
     if (bl1 <= 127) break;
-    uint32_t rr[8], tt[6];
-    if (!hs_step(rr, tt, r0, r1, t0, t1)) {
+    if (round == HS_MAX_ROUNDS - 1) {
       ok = false;
       break;
     }
+    int32_t A = 1, B = 0, C = 0, D = 1;
+    if (LEHMER) hs_lehmer(A, B, C, D, r0[7] >> 2, r1[7] >> 2, 226 - e);
+    if (B == 0) {
+      // no quotient certain from the leading digits: one exact step
+      uint32_t rr[8], tt[6];
+      if (!hs_step(rr, tt, r0, r1, t0, t1)) {
+        ok = false;
+        break;
+      }
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
-      r0[i] = r1[i];
-      r1[i] = rr[i];
-    }
+      for (int i = 0; i < 8; i++) {
+        r0[i] = r1[i];
+        r1[i] = rr[i];
+      }
 #pragma unroll
-    for (int i = 0; i < 6; i++) {
-      t0[i] = t1[i];
-      t1[i] = tt[i];
+      for (int i = 0; i < 6; i++) {
+        t0[i] = t1[i];
+        t1[i] = tt[i];
+      }
+    } else {
+      // (r0, r1) <- (A r0 + B r1, C r0 + D r1), likewise (t0, t1)
+      uint32_t s0[8], s1[8], u0[6], u1[6];
+      hs_lin<8>(s0, A, r0, B, r1);
+      hs_lin<8>(s1, C, r0, D, r1);
+      hs_lin<6>(u0, A, t0, B, t1);
+      hs_lin<6>(u1, C, t0, D, t1);
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        r0[i] = s0[i];
+        r1[i] = s1[i];
+      }
+#pragma unroll
+      for (int i = 0; i < 6; i++) {
+        t0[i] = u0[i];
+        t1[i] = u1[i];
+      }
     }
     // renormalise: r0's top bit back to bit 255
 #pragma unroll 1
@@ -241,7 +342,6 @@ CMTV_HD void half_scalars(HalfScalars& h, const uint32_t k[8]) {
     hs_shl8(r0, sh);
     hs_shl8(r1, sh);
     e += sh;
-    if (step == HS_MAX_STEPS - 1) ok = false;
   }
 
   // candidates with odd t: (r1, t1); else (r0, t0) [t0 odd then] or one more

@@ -1,9 +1,11 @@
 // Host build of cometbft_amd/csrc/halfscalar.h (the device source): reads
 // n x 32-byte little-endian scalars k on stdin, writes per scalar
-// k1 (32 B) | |k2| (32 B) | flags (1 B: bit0 k2 negative, bit1 wide). Test
+// k1 (32 B) | |k2| (32 B) | flags (1 B: bit0 k2 negative, bit1 wide),
+// twice: Lehmer schedule, then exact single steps. Test
 // infrastructure only (tests/test_host_math.py checks the invariants).
 #define CMTV_HD inline
 #include <cstdio>
+#include <initializer_list>
 #include "../../cometbft_amd/csrc/halfscalar.h"
 
 int main() {
@@ -12,12 +14,15 @@ int main() {
   for (uint32_t i = 0; i < n; i++) {
     uint32_t k[8];
     if (fread(k, 4, 8, stdin) != 8) return 1;
-    cmtv::HalfScalars h;
-    cmtv::half_scalars(h, k);
-    uint8_t f = (h.k2_neg ? 1 : 0) | (h.wide ? 2 : 0);
-    fwrite(h.k1, 4, 8, stdout);
-    fwrite(h.k2, 4, 8, stdout);
-    fwrite(&f, 1, 1, stdout);
+    cmtv::HalfScalars h, g;
+    cmtv::half_scalars<true>(h, k);   // Lehmer rounds (the device schedule)
+    cmtv::half_scalars<false>(g, k);  // one exact Euclid step per round
+    for (const cmtv::HalfScalars* x : {&h, &g}) {
+      uint8_t f = (x->k2_neg ? 1 : 0) | (x->wide ? 2 : 0);
+      fwrite(x->k1, 4, 8, stdout);
+      fwrite(x->k2, 4, 8, stdout);
+      fwrite(&f, 1, 1, stdout);
+    }
   }
   return 0;
 }

@@ -94,17 +94,19 @@ def test_half_scalar_decomposition():
     """halfscalar.h (the device source, host-compiled): k1 == k2 k (mod 8L),
     k2 odd, 0 <= k1 < 2^134 and 0 < |k2| < 2^134 unless flagged wide (then
     k1 = k, k2 = 1). Random scalars plus the boundary ones; the wide rate
-    must stay rare (it only costs time, never changes a verdict)."""
+    must stay rare (it only costs time, never changes a verdict). The Lehmer
+    schedule must give exactly the pair of the one-step-per-round Euclid."""
     binary = _build(HSRC, HBIN, ["-std=c++17"])
     rng = np.random.default_rng(215)
     ks = [0, 1, 2, 3, L - 1, L - 2, 2**127, 2**128 - 1, 2**134, 2**252]
     ks += [int.from_bytes(rng.bytes(32), "little") % L for _ in range(20000)]
     buf = struct.pack("<I", len(ks)) + b"".join(k.to_bytes(32, "little") for k in ks)
     out = subprocess.run([binary], input=buf, capture_output=True, check=True, timeout=120).stdout
-    assert len(out) == 65 * len(ks)
+    assert len(out) == 130 * len(ks)
     wide = 0
     for j, k in enumerate(ks):
-        rec = out[65 * j: 65 * (j + 1)]
+        rec = out[130 * j: 130 * j + 65]
+        assert rec == out[130 * j + 65: 130 * (j + 1)], j  # Lehmer == exact steps
         k1 = int.from_bytes(rec[:32], "little")
         k2 = int.from_bytes(rec[32:64], "little")
         f = rec[64]

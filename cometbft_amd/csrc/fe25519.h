@@ -235,11 +235,12 @@ CMTV_HD void fe_sqn(fe& h, const fe& f, int n) {
 // load 255 bits (bit 255 ignored) from 8 little-endian 32-bit words; the value
 // may be >= p (Go's field.Element.SetBytes accepts non-canonical input)
 CMTV_HD void fe_frombytes(fe& h, const uint32_t w[8]) {
+  // word-sized shifts (pos is a constant): no 64-bit pairing of array words
   auto bits = [&](int pos, uint32_t mask) -> uint32_t {
     const int wi = pos >> 5, sh = pos & 31;
-    uint64_t x = (uint64_t)w[wi];
-    if (wi < 7) x |= (uint64_t)w[wi + 1] << 32;
-    return (uint32_t)(x >> sh) & mask;
+    uint32_t x = w[wi] >> sh;
+    if (wi < 7 && sh) x |= w[wi + 1] << (32 - sh);
+    return x & mask;
   };
   h.v[0] = bits(0, M26);
   h.v[1] = bits(26, M25);

@@ -96,17 +96,19 @@ CMTV_HD int hs_bitlen6s(const uint32_t t[6], bool& neg) {
   return bl;
 }
 
-// r <<= sh (0 <= sh < 32), 8 words
+// r <<= sh (0 <= sh < 32), 8 words. Word-sized shifts only: pairing two
+// array words into a 64-bit value lets the compiler merge their loads, which
+// keeps the whole array in scratch memory on the device.
 CMTV_HD void hs_shl8(uint32_t r[8], int sh) {
 #pragma unroll
-  for (int i = 7; i > 0; i--) r[i] = (uint32_t)(((((uint64_t)r[i] << 32) | r[i - 1]) << sh) >> 32);
+  for (int i = 7; i > 0; i--) r[i] = (r[i] << sh) | ((r[i - 1] >> (31 - sh)) >> 1);
   r[0] <<= sh;
 }
 
 // r >>= sh (0 <= sh < 32), 8 words
 CMTV_HD void hs_shr8(uint32_t r[8], int sh) {
 #pragma unroll
-  for (int i = 0; i < 7; i++) r[i] = (uint32_t)(((((uint64_t)r[i + 1] << 32) | r[i]) >> sh));
+  for (int i = 0; i < 7; i++) r[i] = (r[i] >> sh) | ((r[i + 1] << (31 - sh)) << 1);
   r[7] >>= sh;
 }
 
@@ -115,9 +117,10 @@ CMTV_HD void hs_shr8(uint32_t r[8], int sh) {
 CMTV_HD bool hs_step(uint32_t rr[8], uint32_t tt[6], const uint32_t r0[8], const uint32_t r1[8],
                      const uint32_t t0[6], const uint32_t t1[6]) {
   if (r1[7] == 0) return false;  // r1 < r0 / 2^31: quotient too wide for one word
-  const uint64_t a = ((uint64_t)r0[7] << 32) | r0[6];
-  const uint64_t b = ((uint64_t)r1[7] << 32) | r1[6];
-  const double qd = floor((double)a / (double)b);
+  // the top 64 bits of each as an f64 (one rounding of the exact value)
+  const double a = (double)r0[7] * 4294967296.0 + (double)r0[6];
+  const double b = (double)r1[7] * 4294967296.0 + (double)r1[6];
+  const double qd = floor(a / b);
   uint32_t q = qd >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)qd;
   // x = r0 - q r1 as 9-word two's complement; y = t0 - q t1 (6 words)
   uint32_t x[9];

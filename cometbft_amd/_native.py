@@ -41,7 +41,7 @@ COMMIT_PANIC_UNKNOWN_FLAG = 9
 # every symbol include/cmtverify.h declares (checked by tests/test_abi.py)
 EXPORTS = (
     "cmtv_open", "cmtv_close", "cmtv_strerror", "cmtv_abi_version", "cmtv_stats_get", "cmtv_stream",
-    "cmtv_verify_ed25519", "cmtv_verify_ed25519_device",
+    "cmtv_verify_ed25519", "cmtv_verify_ed25519_device", "cmtv_verify_sr25519", "cmtv_verify_sr25519_device",
     "cmtv_register_keys", "cmtv_keyset_free", "cmtv_keyset_len", "cmtv_verify_ed25519_indexed",
     "cmtv_verify_ed25519_indexed_device",
     "cmtv_batch_new", "cmtv_batch_add", "cmtv_batch_len", "cmtv_batch_verify", "cmtv_batch_reset",
@@ -122,6 +122,10 @@ def lib() -> ctypes.CDLL:
     L.cmtv_verify_ed25519.restype = ctypes.c_int
     L.cmtv_verify_ed25519_device.argtypes = [vp, sz, vp, vp, vp, vp, u32, vp, vp, vp]
     L.cmtv_verify_ed25519_device.restype = ctypes.c_int
+    L.cmtv_verify_sr25519.argtypes = [vp, sz, _u8p, _u8p, _u8p, u32p, _u8p, ctypes.POINTER(u64)]
+    L.cmtv_verify_sr25519.restype = ctypes.c_int
+    L.cmtv_verify_sr25519_device.argtypes = [vp, sz, vp, vp, vp, vp, vp, vp, vp]
+    L.cmtv_verify_sr25519_device.restype = ctypes.c_int
     L.cmtv_register_keys.argtypes = [vp, sz, _u8p, ctypes.POINTER(vp)]
     L.cmtv_register_keys.restype = ctypes.c_int
     L.cmtv_keyset_free.argtypes = [vp]

@@ -100,6 +100,37 @@ class Context:
                                                 d_bitmap or None, ctypes.c_void_p(stream) if stream else None)
         N.check(rc, "cmtv_verify_ed25519_device")
 
+    # -------------------------------------------------------------- sr25519
+    def verify_sr25519(self, pk: np.ndarray, sig: np.ndarray, msg: np.ndarray, msg_off: np.ndarray,
+                       bitmap: bool = False):
+        """sr25519 verdicts (crypto/sr25519/pubkey.go:34-60) for n 32-byte keys
+        and 64-byte signatures in host arrays; layout as verify()."""
+        pk = np.ascontiguousarray(pk, dtype=np.uint8).reshape(-1, 32)
+        sig = np.ascontiguousarray(sig, dtype=np.uint8).reshape(-1, 64)
+        n = pk.shape[0]
+        if sig.shape[0] != n or len(msg_off) != n + 1:
+            raise ValueError("pk / sig / msg_off sizes disagree")
+        msg = np.ascontiguousarray(msg, dtype=np.uint8)
+        if msg.size == 0:
+            msg = np.zeros(1, np.uint8)
+        off = np.ascontiguousarray(msg_off, dtype=np.uint32)
+        valid = np.zeros(max(n, 1), np.uint8)
+        words = np.zeros(max((n + 63) // 64, 1), np.uint64)
+        rc = N.lib().cmtv_verify_sr25519(self._h, n, _u8(pk), _u8(sig), _u8(msg),
+                                         off.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), _u8(valid),
+                                         words.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)))
+        N.check(rc, "cmtv_verify_sr25519")
+        if bitmap:
+            return valid[:n], words[: (n + 63) // 64]
+        return valid[:n]
+
+    def verify_sr25519_device(self, n: int, d_pk: int, d_sig: int, d_msg: int, d_off: int, d_valid: int = 0,
+                              d_bitmap: int = 0, stream: int = 0) -> None:
+        """Enqueue sr25519 verification over device-resident buffers."""
+        rc = N.lib().cmtv_verify_sr25519_device(self._h, n, d_pk, d_sig, d_msg, d_off, d_valid or None,
+                                                d_bitmap or None, ctypes.c_void_p(stream) if stream else None)
+        N.check(rc, "cmtv_verify_sr25519_device")
+
     # -------------------------------------------------------------- registered keys
     def register_keys(self, pk: np.ndarray) -> "KeySet":
         """Decode n 32-byte keys once and build their combs on the device
@@ -230,6 +261,56 @@ class PubKey(bytes):
         m, off = pack_messages([bytes(msg)])
         v = ctx.verify(np.frombuffer(bytes(self), np.uint8), np.frombuffer(bytes(sig), np.uint8), m, off, mode)
         return bool(v[0])
+
+
+class Sr25519PubKey(bytes):
+    """sr25519.PubKey (crypto/sr25519/pubkey.go:21): raw key bytes."""
+
+    def verify_signature(self, msg: bytes, sig: bytes, ctx: Context | None = None) -> bool:
+        """PubKey.VerifySignature (pubkey.go:34-60) as a batch of one on the
+        GPU: len(sig) != 64 -> False; the key is copied into a zeroed 32-byte
+        array (shorter keys zero-padded, longer ones truncated) as Go's copy()
+        does."""
+        if len(sig) != SIGNATURE_SIZE:
+            return False
+        key = (bytes(self) + bytes(PUBKEY_SIZE))[:PUBKEY_SIZE]
+        ctx = ctx or default_context()
+        m, off = pack_messages([bytes(msg)])
+        v = ctx.verify_sr25519(np.frombuffer(key, np.uint8), np.frombuffer(bytes(sig), np.uint8), m, off)
+        return bool(v[0])
+
+
+class Sr25519BatchVerifier:
+    """Batch form of sr25519 PubKey.VerifySignature with the BatchVerifier
+    shape (add / verify -> (bool, list[bool])); every verdict comes from the
+    GPU kernel, entries with a wrong signature length are invalid."""
+
+    def __init__(self, ctx: Context | None = None):
+        self.ctx = ctx or default_context()
+        self.reset()
+
+    def __len__(self):
+        return len(self._msgs)
+
+    def reset(self):
+        self._pk, self._sig, self._msgs, self._len_ok = [], [], [], []
+
+    def add(self, key: bytes, msg: bytes, sig: bytes) -> None:
+        self._pk.append((bytes(key) + bytes(PUBKEY_SIZE))[:PUBKEY_SIZE])
+        self._len_ok.append(len(sig) == SIGNATURE_SIZE)
+        self._sig.append(bytes(sig) if len(sig) == SIGNATURE_SIZE else bytes(SIGNATURE_SIZE))
+        self._msgs.append(bytes(msg))
+
+    def verify(self):
+        n = len(self._msgs)
+        if n == 0:
+            return True, []
+        m, off = pack_messages(self._msgs)
+        pk = np.frombuffer(b"".join(self._pk), np.uint8)
+        sig = np.frombuffer(b"".join(self._sig), np.uint8)
+        v = self.ctx.verify_sr25519(pk, sig, m, off)
+        out = [bool(x) and ok for x, ok in zip(v, self._len_ok)]
+        return all(out), out
 
 
 class BatchVerifier:

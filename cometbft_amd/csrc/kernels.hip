@@ -22,6 +22,7 @@
 //          magnitude, and at most 8 distinct 256-byte segments otherwise.
 #include <hip/hip_runtime.h>
 
+#include "devtables.h"
 #include "kernels.h"
 #include "keyed.h"
 #include "quad.h"
@@ -38,20 +39,6 @@
 #endif
 
 namespace cmtv {
-
-struct DevBTab {
-  const uint32_t* __restrict__ rows;
-  // one niels coordinate (10 words at a 16-byte aligned offset): 2 x dwordx4 + dwordx2
-  __device__ __forceinline__ void load_fe(int e, int c, fe& r) const {
-    const uint32_t* p = rows + e * BTAB_ROW_WORDS + c * BTAB_COORD_WORDS;
-    const uint4 a = *reinterpret_cast<const uint4*>(p);
-    const uint4 b = *reinterpret_cast<const uint4*>(p + 4);
-    const uint2 d = *reinterpret_cast<const uint2*>(p + 8);
-    r.v[0] = a.x; r.v[1] = a.y; r.v[2] = a.z; r.v[3] = a.w;
-    r.v[4] = b.x; r.v[5] = b.y; r.v[6] = b.z; r.v[7] = b.w;
-    r.v[8] = d.x; r.v[9] = d.y;
-  }
-};
 
 // B-table access for the quad kernel: each lane reads its own coordinate
 // (word offset `off` inside the row) of entry e.
@@ -89,30 +76,6 @@ struct DevQuad {
     return dpp<PAT>(x);
   }
   __device__ __forceinline__ bool any(bool x) const { return __ballot(x) != 0; }
-};
-
-// Per-lane (1..8)(-A) table, word-major / lane-minor: word w of entry e for
-// lane l lives at base[(e * 40 + w) * stride + l], so a wave's load of one
-// word is a 256-byte coalesced access whenever its lanes share the entry.
-struct DevATab {
-  uint32_t* __restrict__ base;
-  uint32_t stride;
-  uint32_t lane;
-  __device__ __forceinline__ void load_fe(int e, int c, fe& r) const {
-    const uint32_t* p = base + (uint32_t)((e * 4 + c) * 10) * stride + lane;
-#pragma unroll
-    for (int i = 0; i < 10; i++) r.v[i] = p[i * stride];
-  }
-  __device__ __forceinline__ void store(int e, const ge_cached& r) {
-    uint32_t* p = base + (uint32_t)(e * 40) * stride + lane;
-#pragma unroll
-    for (int i = 0; i < 10; i++) {
-      p[i * stride] = r.YpX.v[i];
-      p[(10 + i) * stride] = r.YmX.v[i];
-      p[(20 + i) * stride] = r.Z.v[i];
-      p[(30 + i) * stride] = r.T2d.v[i];
-    }
-  }
 };
 
 __device__ __forceinline__ void load_words(uint32_t* w, const uint32_t* __restrict__ src, int nquads) {

@@ -18,6 +18,7 @@
 
 #include "../../include/cmtverify.h"
 #include "kernels.h"
+#include "merlin.h"
 #include "runtime_internal.h"
 
 namespace {
@@ -84,6 +85,8 @@ struct cmtv_ctx {
   cmtv_stats stats{};
   size_t quad_max = kQuadMaxDefault;  // batches up to this size use the quad kernel
   uint32_t* d_bcomb = nullptr;        // comb of B for registered-key verification (built lazily)
+  uint16_t* d_srprog = nullptr;       // sr25519 transcript program (merlin.h)
+  int sr_nops = 0;
 };
 
 struct cmtv_keyset {
@@ -120,8 +123,10 @@ static int enqueue_verify(cmtv_ctx* ctx, size_t n, const uint8_t* d_pk, const ui
                           hipStream_t s) {
   if (n == 0) return CMTV_OK;
   // Small batches cannot fill the chip at one signature per lane: use the
-  // 4-lanes-per-signature kernel below the crossover (quad.h).
-  const bool quad = n <= ctx->quad_max;
+  // 4-lanes-per-signature kernel below the crossover (quad.h). sr25519 has
+  // the lane kernel only.
+  const bool sr = mode == kModeSr25519;
+  const bool quad = !sr && n <= ctx->quad_max;
   hipError_t e = hipSuccess;
   if (!quad) {
     const size_t lanes = std::min<size_t>(n, kChunk);
@@ -133,9 +138,14 @@ static int enqueue_verify(cmtv_ctx* ctx, size_t n, const uint8_t* d_pk, const ui
   if ((e = hipEventRecord(ctx->ev0, s)) != hipSuccess) return hip_fail(e);
   for (size_t c = 0; c < n; c += kChunk) {
     const uint32_t cn = (uint32_t)std::min<size_t>(kChunk, n - c);
-    e = launch_verify(mode, cn, d_pk + 32 * c, d_sig + 64 * c, d_msg, d_off + c, ctx->d_btab,
-                      static_cast<uint32_t*>(ctx->d_atab.p), d_valid ? d_valid + c : nullptr,
-                      d_bitmap ? d_bitmap + c / 64 : nullptr, quad, s);
+    if (sr)
+      e = launch_verify_sr25519(cn, d_pk + 32 * c, d_sig + 64 * c, d_msg, d_off + c, ctx->d_btab,
+                                static_cast<uint32_t*>(ctx->d_atab.p), ctx->d_srprog, ctx->sr_nops,
+                                d_valid ? d_valid + c : nullptr, d_bitmap ? d_bitmap + c / 64 : nullptr, s);
+    else
+      e = launch_verify(mode, cn, d_pk + 32 * c, d_sig + 64 * c, d_msg, d_off + c, ctx->d_btab,
+                        static_cast<uint32_t*>(ctx->d_atab.p), d_valid ? d_valid + c : nullptr,
+                        d_bitmap ? d_bitmap + c / 64 : nullptr, quad, s);
     if (e != hipSuccess) return hip_fail(e);
     ctx->stats.kernel_launches++;
   }
@@ -291,6 +301,10 @@ int cmtv_open(const cmtv_config* cfg, cmtv_ctx** out) {
   if (e == hipSuccess) e = hipEventCreate(&ctx->ev1);
   if (e == hipSuccess) e = hipMalloc(&ctx->d_btab, kBtabWords * sizeof(uint32_t));
   if (e == hipSuccess) e = launch_btab_init(ctx->d_btab, ctx->stream);
+  uint16_t prog[SR_PROGRAM_MAX];
+  ctx->sr_nops = sr_build_program(prog);
+  if (e == hipSuccess) e = hipMalloc(&ctx->d_srprog, sizeof(prog));
+  if (e == hipSuccess) e = hipMemcpyAsync(ctx->d_srprog, prog, sizeof(prog), hipMemcpyHostToDevice, ctx->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
   if (e != hipSuccess) {
     cmtv_close(ctx);
@@ -311,6 +325,7 @@ void cmtv_close(cmtv_ctx* ctx) {
   ctx->h_out.release();
   if (ctx->d_btab) (void)hipFree(ctx->d_btab);
   if (ctx->d_bcomb) (void)hipFree(ctx->d_bcomb);
+  if (ctx->d_srprog) (void)hipFree(ctx->d_srprog);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -351,6 +366,31 @@ int cmtv_verify_ed25519_device(cmtv_ctx* ctx, size_t n, const void* d_pk, const 
   return enqueue_verify(ctx, n, static_cast<const uint8_t*>(d_pk), static_cast<const uint8_t*>(d_sig),
                         static_cast<const uint8_t*>(d_msg), static_cast<const uint32_t*>(d_msg_off), mode,
                         static_cast<uint8_t*>(d_valid), static_cast<uint64_t*>(d_bitmap), s);
+}
+
+int cmtv_verify_sr25519(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
+                        const uint32_t* msg_off, uint8_t* out_valid, uint64_t* out_bitmap) {
+  if (!ctx || n > (1ull << 31)) return CMTV_EINVAL;
+  if (n == 0) return CMTV_OK;
+  if (!pk || !sig || !msg_off || (!msg && msg_off[n] != 0) || (!out_valid && !out_bitmap)) return CMTV_EINVAL;
+  for (size_t i = 0; i < n; i++)
+    if (msg_off[i + 1] < msg_off[i]) return CMTV_EINVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  if (hipSetDevice(ctx->device) != hipSuccess) return CMTV_ENODEV;
+  return verify_host_locked(ctx, n, pk, sig, msg, msg_off, kModeSr25519, out_valid, out_bitmap);
+}
+
+int cmtv_verify_sr25519_device(cmtv_ctx* ctx, size_t n, const void* d_pk, const void* d_sig, const void* d_msg,
+                               const void* d_msg_off, void* d_valid, void* d_bitmap, void* stream) {
+  if (!ctx || n > (1ull << 31)) return CMTV_EINVAL;
+  if (n == 0) return CMTV_OK;
+  if (!d_pk || !d_sig || !d_msg || !d_msg_off || (!d_valid && !d_bitmap)) return CMTV_EINVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  if (hipSetDevice(ctx->device) != hipSuccess) return CMTV_ENODEV;
+  return enqueue_verify(ctx, n, static_cast<const uint8_t*>(d_pk), static_cast<const uint8_t*>(d_sig),
+                        static_cast<const uint8_t*>(d_msg), static_cast<const uint32_t*>(d_msg_off), kModeSr25519,
+                        static_cast<uint8_t*>(d_valid), static_cast<uint64_t*>(d_bitmap),
+                        static_cast<hipStream_t>(stream));
 }
 
 int cmtv_register_keys(cmtv_ctx* ctx, size_t n_keys, const uint8_t* pk, cmtv_keyset** out) {

@@ -12,6 +12,10 @@ namespace cmtv {
 // Locks the context and makes its device current on this thread.
 int ctx_lock(cmtv_ctx* ctx, std::unique_lock<std::mutex>& lk);
 uint32_t ctx_default_mode(const cmtv_ctx* ctx);
+// Internal pseudo-mode selecting the sr25519 kernel in verify_host_locked /
+// enqueue paths (the ABI's mode argument is Ed25519-only).
+constexpr uint32_t kModeSr25519 = 0x100;
+
 // Host buffers in, verdicts out; caller holds the context lock.
 int verify_host_locked(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
                        const uint32_t* msg_off, uint32_t mode, uint8_t* out_valid, uint64_t* out_bitmap);

@@ -1,0 +1,71 @@
+// sr25519.hip -- gfx950 kernel for sr25519 (schnorrkel / ristretto255) batch
+// verification (BASELINE configs[4]; reference path
+// /root/reference/crypto/sr25519/pubkey.go:34-60).
+//
+//   k_verify_sr25519: one signature per lane (sr25519.h): merlin transcript
+//     interpreted from a byte-code program with the Keccak state in LDS,
+//     ristretto255 decoding of A and R, Straus [s]B - [k]A over the Ed25519
+//     kernel's field, point formulas and fixed-base table, ristretto equality;
+//     a wavefront ballot packs 64 verdicts into one bitmap word.
+//
+// Memory layout: inputs exactly as the Ed25519 kernels (pk n x 32 B, sig
+// n x 64 B, msg flat bytes + (n+1) u32 offsets); the transcript program (at
+// most SR_PROGRAM_MAX u16) is read with uniform scalar loads; the per-lane
+// 200-byte STROBE state lives in LDS lane-interleaved (word w of lane l at
+// word w*64 + l: conflict-free for any per-lane byte position).
+#include <hip/hip_runtime.h>
+
+#include "devtables.h"
+#include "kernels.h"
+#include "sr25519.h"
+
+namespace cmtv {
+
+// STROBE state of one lane in LDS (50 words, lane-interleaved)
+struct LdsStrobeState {
+  uint32_t* __restrict__ lds;
+  uint32_t lane;
+  __device__ __forceinline__ void xor_byte(int pos, uint32_t b) {
+    uint32_t* p = lds + (pos >> 2) * 64 + lane;
+    *p ^= (b & 0xFFu) << (8 * (pos & 3));
+  }
+  __device__ __forceinline__ uint32_t word(int i) const { return lds[i * 64 + lane]; }
+  __device__ __forceinline__ void set_word(int i, uint32_t x) { lds[i * 64 + lane] = x; }
+};
+
+__global__ __launch_bounds__(64, 2) void k_verify_sr25519(uint32_t n, const uint32_t* __restrict__ pk,
+                                                          const uint32_t* __restrict__ sig,
+                                                          const uint8_t* __restrict__ msg,
+                                                          const uint32_t* __restrict__ off,
+                                                          const uint32_t* __restrict__ btab,
+                                                          uint32_t* __restrict__ atab,
+                                                          const uint16_t* __restrict__ prog, int nops,
+                                                          uint8_t* __restrict__ out_valid,
+                                                          uint64_t* __restrict__ out_bitmap) {
+  __shared__ uint32_t st_lds[50 * 64];
+  const uint32_t gid = blockIdx.x * 64 + threadIdx.x;
+  const bool active = gid < n;
+  const uint32_t i = active ? gid : n - 1;
+  const uint32_t m0 = off[i], m1 = off[i + 1];
+  DevATab at{atab, gridDim.x * 64u, gid};
+  DevBTab bt{btab};
+  LdsStrobeState st{st_lds, threadIdx.x};
+  bool v = sr_verify_one(pk + 8 * (size_t)i, sig + 16 * (size_t)i, msg + m0, m1 - m0, prog, nops, st, at, bt);
+  v = v && active;
+  if (active && out_valid) out_valid[gid] = v ? 1 : 0;
+  const uint64_t mask = __ballot(v);
+  if (threadIdx.x == 0 && out_bitmap) out_bitmap[gid >> 6] = mask;
+}
+
+hipError_t launch_verify_sr25519(uint32_t n, const void* pk, const void* sig, const void* msg, const void* off,
+                                 const uint32_t* btab, uint32_t* atab, const uint16_t* prog, int nops, void* valid,
+                                 void* bitmap, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_verify_sr25519, dim3((n + 63) / 64), dim3(64), 0, s, n, static_cast<const uint32_t*>(pk),
+                     static_cast<const uint32_t*>(sig), static_cast<const uint8_t*>(msg),
+                     static_cast<const uint32_t*>(off), btab, atab, prog, nops, static_cast<uint8_t*>(valid),
+                     static_cast<uint64_t*>(bitmap));
+  return hipGetLastError();
+}
+
+}  // namespace cmtv

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define CMTV_ABI_VERSION 2
+#define CMTV_ABI_VERSION 3
 
 enum {
   CMTV_OK = 0,
@@ -106,6 +106,25 @@ int cmtv_verify_ed25519(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_
  * (n bytes) and d_bitmap (ceil(n/64) words) may each be NULL. */
 int cmtv_verify_ed25519_device(cmtv_ctx* ctx, size_t n, const void* d_pk, const void* d_sig, const void* d_msg,
                                const void* d_msg_off, uint32_t mode, void* d_valid, void* d_bitmap, void* stream);
+
+/* ------------------------------------------------------------ sr25519 */
+
+/* sr25519 (schnorrkel over ristretto255) batch verification, BASELINE
+ * configs[4]. Each verdict equals
+ *   sr25519.PubKey(pk_i).VerifySignature(msg_i, sig_i)   crypto/sr25519/pubkey.go:34-60
+ * (go-schnorrkel v1.0.0: signing context "" + msg, ristretto255 decoding of the
+ * key and of R, the schnorrkel marker bit sig[63] & 0x80, canonical s, merlin
+ * challenge, R' = [s]B - [k]A compared with ristretto equality) for 32-byte
+ * keys and 64-byte signatures; callers apply pubkey.go's length rules
+ * (len(sig) != 64 -> false; the key is copied into a zeroed 32-byte array).
+ * Buffers, ownership and blocking behaviour as cmtv_verify_ed25519. */
+int cmtv_verify_sr25519(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
+                        const uint32_t* msg_off, uint8_t* out_valid, uint64_t* out_bitmap);
+
+/* Same with device-resident inputs, enqueued on `stream` (as
+ * cmtv_verify_ed25519_device). */
+int cmtv_verify_sr25519_device(cmtv_ctx* ctx, size_t n, const void* d_pk, const void* d_sig, const void* d_msg,
+                               const void* d_msg_off, void* d_valid, void* d_bitmap, void* stream);
 
 /* ------------------------------------------------------------ registered keys */
 

@@ -795,3 +795,303 @@ void oracle_sign_batch(size_t n, const uint8_t *seeds, const uint32_t *key_idx, 
   }
   for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
 }
+
+/* ================================================================ sr25519
+ * schnorrkel / merlin / ristretto255 restatement (go-schnorrkel v1.0.0,
+ * gtank/merlin v0.1.1, gtank/ristretto255 v0.1.2), reached from
+ * /root/reference/crypto/sr25519/pubkey.go:34-60. Same semantics as
+ * oracle/sr25519_ref.py (the Python restatement, pinned against published
+ * vectors in tests/test_sr25519_oracle.py); this C copy is the fast checker
+ * and the CPU baseline for the sr25519 kernel. */
+
+static const uint64_t KECCAK_RC[24] = {
+    0x0000000000000001ULL, 0x0000000000008082ULL, 0x800000000000808AULL, 0x8000000080008000ULL,
+    0x000000000000808BULL, 0x0000000080000001ULL, 0x8000000080008081ULL, 0x8000000000008009ULL,
+    0x000000000000008AULL, 0x0000000000000088ULL, 0x0000000080008009ULL, 0x000000008000000AULL,
+    0x000000008000808BULL, 0x800000000000008BULL, 0x8000000000008089ULL, 0x8000000000008003ULL,
+    0x8000000000008002ULL, 0x8000000000000080ULL, 0x000000000000800AULL, 0x800000008000000AULL,
+    0x8000000080008081ULL, 0x8000000000008080ULL, 0x0000000080000001ULL, 0x8000000080008008ULL};
+/* rotation of lane x + 5y */
+static const int KECCAK_ROT[25] = {0, 1, 62, 28, 27, 36, 44, 6, 55, 20, 3, 10, 43,
+                                   25, 39, 41, 45, 15, 21, 8, 18, 2, 61, 56, 14};
+
+static uint64_t rol64(uint64_t x, int n) { return n ? (x << n) | (x >> (64 - n)) : x; }
+
+static void keccak_f1600(uint64_t a[25]) {
+  for (int rnd = 0; rnd < 24; rnd++) {
+    uint64_t c[5], d[5], b[25];
+    for (int x = 0; x < 5; x++) c[x] = a[x] ^ a[x + 5] ^ a[x + 10] ^ a[x + 15] ^ a[x + 20];
+    for (int x = 0; x < 5; x++) d[x] = c[(x + 4) % 5] ^ rol64(c[(x + 1) % 5], 1);
+    for (int i = 0; i < 25; i++) a[i] ^= d[i % 5];
+    for (int x = 0; x < 5; x++)
+      for (int y = 0; y < 5; y++) b[y + 5 * ((2 * x + 3 * y) % 5)] = rol64(a[x + 5 * y], KECCAK_ROT[x + 5 * y]);
+    for (int y = 0; y < 5; y++)
+      for (int x = 0; x < 5; x++)
+        a[x + 5 * y] = b[x + 5 * y] ^ (~b[(x + 1) % 5 + 5 * y] & b[(x + 2) % 5 + 5 * y]);
+    a[0] ^= KECCAK_RC[rnd];
+  }
+}
+
+enum { STROBE_R = 166, SF_I = 1, SF_A = 2, SF_C = 4, SF_T = 8, SF_M = 16, SF_K = 32 };
+typedef struct {
+  uint64_t st[25]; /* little-endian byte view below (x86 host) */
+  int pos, pos_begin, cur_flags;
+} strobe_t;
+
+static uint8_t *sbytes(strobe_t *s) { return (uint8_t *)s->st; }
+
+static void strobe_run_f(strobe_t *s) {
+  sbytes(s)[s->pos] ^= (uint8_t)s->pos_begin;
+  sbytes(s)[s->pos + 1] ^= 0x04;
+  sbytes(s)[STROBE_R + 1] ^= 0x80;
+  keccak_f1600(s->st);
+  s->pos = 0;
+  s->pos_begin = 0;
+}
+static void strobe_absorb(strobe_t *s, const uint8_t *p, size_t n) {
+  for (size_t i = 0; i < n; i++) {
+    sbytes(s)[s->pos++] ^= p[i];
+    if (s->pos == STROBE_R) strobe_run_f(s);
+  }
+}
+static void strobe_squeeze(strobe_t *s, uint8_t *out, size_t n) {
+  for (size_t i = 0; i < n; i++) {
+    out[i] = sbytes(s)[s->pos];
+    sbytes(s)[s->pos++] = 0;
+    if (s->pos == STROBE_R) strobe_run_f(s);
+  }
+}
+static void strobe_begin_op(strobe_t *s, int flags, int more) {
+  if (more) return; /* callers only continue an op with the same flags */
+  uint8_t hdr[2] = {(uint8_t)s->pos_begin, (uint8_t)flags};
+  s->pos_begin = s->pos + 1;
+  s->cur_flags = flags;
+  strobe_absorb(s, hdr, 2);
+  if ((flags & (SF_C | SF_K)) && s->pos != 0) strobe_run_f(s);
+}
+static void strobe_meta_ad(strobe_t *s, const uint8_t *p, size_t n, int more) {
+  strobe_begin_op(s, SF_M | SF_A, more);
+  strobe_absorb(s, p, n);
+}
+static void strobe_ad(strobe_t *s, const uint8_t *p, size_t n, int more) {
+  strobe_begin_op(s, SF_A, more);
+  strobe_absorb(s, p, n);
+}
+static void transcript_append(strobe_t *s, const char *label, const uint8_t *m, size_t n) {
+  uint8_t len[4] = {(uint8_t)n, (uint8_t)(n >> 8), (uint8_t)(n >> 16), (uint8_t)(n >> 24)};
+  strobe_meta_ad(s, (const uint8_t *)label, strlen(label), 0);
+  strobe_meta_ad(s, len, 4, 1);
+  strobe_ad(s, m, n, 0);
+}
+static void transcript_challenge(strobe_t *s, const char *label, uint8_t *out, size_t n) {
+  uint8_t len[4] = {(uint8_t)n, (uint8_t)(n >> 8), (uint8_t)(n >> 16), (uint8_t)(n >> 24)};
+  strobe_meta_ad(s, (const uint8_t *)label, strlen(label), 0);
+  strobe_meta_ad(s, len, 4, 1);
+  strobe_begin_op(s, SF_I | SF_A | SF_C, 0);
+  strobe_squeeze(s, out, n);
+}
+static void transcript_init(strobe_t *s, const char *label) {
+  memset(s, 0, sizeof *s);
+  static const uint8_t hdr[6] = {1, STROBE_R + 2, 1, 0, 1, 96};
+  memcpy(sbytes(s), hdr, 6);
+  memcpy(sbytes(s) + 6, "STROBEv1.0.2", 12);
+  keccak_f1600(s->st);
+  strobe_meta_ad(s, (const uint8_t *)"Merlin v1.0", 11, 0);
+  transcript_append(s, "dom-sep", (const uint8_t *)label, strlen(label));
+}
+
+/* merlin.NewTranscript("SigningContext") + AppendMessage("", ctx={}) +
+ * AppendMessage("sign-bytes", msg) + proto-name / sign:pk / sign:R, then
+ * 64 challenge bytes reduced mod L */
+static void sr_challenge(uint8_t k[32], const uint8_t pk[32], const uint8_t R[32], const uint8_t *msg, size_t mlen) {
+  strobe_t s;
+  transcript_init(&s, "SigningContext");
+  transcript_append(&s, "", NULL, 0);
+  transcript_append(&s, "sign-bytes", msg, mlen);
+  transcript_append(&s, "proto-name", (const uint8_t *)"Schnorr-sig", 11);
+  transcript_append(&s, "sign:pk", pk, 32);
+  transcript_append(&s, "sign:R", R, 32);
+  uint8_t kb[64];
+  transcript_challenge(&s, "sign:c", kb, 64);
+  sc_reduce64(k, kb);
+}
+
+/* RFC 9496 SQRT_RATIO_M1: r = |sqrt(u/v)| or |sqrt(i u/v)|; returns was_square */
+static int fe_sqrt_ratio_m1(fe *r, const fe *u, const fe *v) {
+  fe v3, v7, t, check, nu, nui;
+  fe_sq(&v3, v); fe_mul(&v3, &v3, v);
+  fe_sq(&v7, &v3); fe_mul(&v7, &v7, v);
+  fe_mul(&t, u, &v7);
+  fe_pow22523(&t, &t);
+  fe_mul(&t, &t, &v3);
+  fe_mul(r, &t, u);
+  fe_sq(&check, r); fe_mul(&check, &check, v);
+  fe_neg(&nu, u);
+  fe_mul(&nui, &nu, &FE_SQRTM1);
+  const int correct = fe_equal(&check, u), flipped = fe_equal(&check, &nu), flipped_i = fe_equal(&check, &nui);
+  if (flipped || flipped_i) fe_mul(r, r, &FE_SQRTM1);
+  if (fe_isneg(r)) fe_neg(r, r);
+  return correct || flipped;
+}
+
+/* RFC 9496 4.3.1 DECODE; 0 on success */
+static int ristretto_decode(ge_p3 *h, const uint8_t in[32]) {
+  fe s;
+  uint8_t chk[32];
+  fe_frombytes(&s, in);
+  fe_tobytes(chk, &s);
+  if ((in[31] & 0x80) || memcmp(chk, in, 32) != 0) return -1; /* non-canonical */
+  if (in[0] & 1) return -1;                                     /* negative */
+  fe ss, u1, u2, u2sq, v, t, one, invsqrt, den_x, den_y;
+  fe_1(&one);
+  fe_sq(&ss, &s);
+  fe_sub(&u1, &one, &ss);
+  fe_add(&u2, &one, &ss);
+  fe_sq(&u2sq, &u2);
+  fe_sq(&t, &u1); fe_mul(&t, &t, &FE_D); fe_neg(&t, &t);
+  fe_sub(&v, &t, &u2sq);
+  fe_mul(&t, &v, &u2sq);
+  const int was_square = fe_sqrt_ratio_m1(&invsqrt, &one, &t);
+  fe_mul(&den_x, &invsqrt, &u2);
+  fe_mul(&den_y, &invsqrt, &den_x); fe_mul(&den_y, &den_y, &v);
+  fe_add(&t, &s, &s); fe_mul(&h->X, &t, &den_x);
+  if (fe_isneg(&h->X)) fe_neg(&h->X, &h->X);
+  fe_mul(&h->Y, &u1, &den_y);
+  fe_1(&h->Z);
+  fe_mul(&h->T, &h->X, &h->Y);
+  if (!was_square || fe_isneg(&h->T) || fe_iszero(&h->Y)) return -1;
+  return 0;
+}
+
+static fe FE_INVSQRT_A_MINUS_D;
+static pthread_once_t sr_once = PTHREAD_ONCE_INIT;
+static void sr_init(void) {
+  pthread_once(&g_once, init_constants);
+  fe one, amd;
+  fe_1(&one);
+  fe_neg(&amd, &one);
+  fe_sub(&amd, &amd, &FE_D); /* a - d = -1 - d */
+  fe_sqrt_ratio_m1(&FE_INVSQRT_A_MINUS_D, &one, &amd);
+}
+
+/* RFC 9496 4.3.2 ENCODE */
+static void ristretto_encode(uint8_t out[32], const ge_p3 *p) {
+  fe u1, u2, t, invsqrt, den1, den2, zinv, ix, iy, ench, x, y, deninv, one;
+  fe_1(&one);
+  fe_add(&u1, &p->Z, &p->Y);
+  fe_sub(&t, &p->Z, &p->Y);
+  fe_mul(&u1, &u1, &t);
+  fe_mul(&u2, &p->X, &p->Y);
+  fe_sq(&t, &u2); fe_mul(&t, &t, &u1);
+  fe_sqrt_ratio_m1(&invsqrt, &one, &t);
+  fe_mul(&den1, &invsqrt, &u1);
+  fe_mul(&den2, &invsqrt, &u2);
+  fe_mul(&zinv, &den1, &den2); fe_mul(&zinv, &zinv, &p->T);
+  fe_mul(&ix, &p->X, &FE_SQRTM1);
+  fe_mul(&iy, &p->Y, &FE_SQRTM1);
+  fe_mul(&ench, &den1, &FE_INVSQRT_A_MINUS_D);
+  fe_mul(&t, &p->T, &zinv);
+  if (fe_isneg(&t)) { x = iy; y = ix; deninv = ench; }
+  else { x = p->X; y = p->Y; deninv = den2; }
+  fe_mul(&t, &x, &zinv);
+  if (fe_isneg(&t)) fe_neg(&y, &y);
+  fe_sub(&t, &p->Z, &y);
+  fe_mul(&t, &deninv, &t);
+  if (fe_isneg(&t)) fe_neg(&t, &t);
+  fe_tobytes(out, &t);
+}
+
+/* sr25519.PubKey.VerifySignature for a 32-byte key and 64-byte signature */
+int oracle_sr25519_verify_one(const uint8_t *pk, const uint8_t *msg, size_t mlen, const uint8_t *sig) {
+  pthread_once(&sr_once, sr_init);
+  ge_p3 A, R, Rp;
+  if (ristretto_decode(&A, pk) != 0) return 0;
+  if (!(sig[63] & 0x80)) return 0;
+  if (ristretto_decode(&R, sig) != 0) return 0;
+  uint8_t s[32], k[32];
+  memcpy(s, sig + 32, 32);
+  s[31] &= 0x7f;
+  if (!sc_is_canonical(s)) return 0;
+  sr_challenge(k, pk, sig, msg, mlen);
+  ge_p3 negA = A;
+  fe_neg(&negA.X, &A.X);
+  fe_neg(&negA.T, &A.T);
+  double_scalarmult_vartime(&Rp, k, &negA, s);
+  fe l, r;
+  fe_mul(&l, &Rp.X, &R.Y); fe_mul(&r, &Rp.Y, &R.X);
+  if (fe_equal(&l, &r)) return 1;
+  fe_mul(&l, &Rp.Y, &R.Y); fe_mul(&r, &Rp.X, &R.X);
+  return fe_equal(&l, &r);
+}
+
+static void *sr_worker(void *arg) {
+  job_t *j = (job_t *)arg;
+  for (size_t i = j->lo; i < j->hi; i++)
+    j->out[i] = (uint8_t)oracle_sr25519_verify_one(j->pk + 32 * i, j->msg + j->off[i], j->off[i + 1] - j->off[i],
+                                                   j->sig + 64 * i);
+  return NULL;
+}
+
+void oracle_sr25519_verify_batch(size_t n, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
+                                 const uint32_t *msg_off, uint8_t *out, int nthreads) {
+  pthread_once(&sr_once, sr_init);
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 256) nthreads = 256;
+  pthread_t th[256];
+  job_t jobs[256];
+  for (int t = 0; t < nthreads; t++) {
+    jobs[t] = (job_t){n * t / nthreads, n * (t + 1) / nthreads, pk, sig, msg, msg_off, 0, out};
+    pthread_create(&th[t], NULL, sr_worker, &jobs[t]);
+  }
+  for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+}
+
+/* MiniSecretKey.ExpandEd25519 -> (key = clamp(h[0:32]) / 8, nonce = h[32:64]) */
+static void sr_expand(uint8_t key[32], uint8_t nonce[32], const uint8_t mini[32]) {
+  uint8_t h[64];
+  sha512_ctx c;
+  sha512_init(&c); sha512_update(&c, mini, 32); sha512_final(&c, h);
+  h[0] &= 248; h[31] &= 63; h[31] |= 64;
+  for (int i = 0; i < 32; i++) key[i] = (uint8_t)((h[i] >> 3) | (i < 31 ? h[i + 1] << 5 : 0));
+  memcpy(nonce, h + 32, 32);
+}
+
+void oracle_sr25519_pubkey(const uint8_t mini[32], uint8_t pk[32]) {
+  pthread_once(&sr_once, sr_init);
+  uint8_t key[32], nonce[32];
+  sr_expand(key, nonce, mini);
+  ge_p3 A;
+  scalarmult_base(&A, key);
+  ristretto_encode(pk, &A);
+}
+
+/* SecretKey.Sign with the deterministic witness of oracle/sr25519_ref.py:
+ * r = SHA-512("cmtverify/sr25519-witness" || nonce || msg) mod L */
+void oracle_sr25519_sign(const uint8_t mini[32], const uint8_t *msg, size_t mlen, uint8_t sig[64]) {
+  pthread_once(&sr_once, sr_init);
+  uint8_t key[32], nonce[32], pk[32], rh[64], r[32], k[32];
+  sr_expand(key, nonce, mini);
+  ge_p3 P;
+  scalarmult_base(&P, key);
+  ristretto_encode(pk, &P);
+  sha512_ctx c;
+  sha512_init(&c);
+  sha512_update(&c, (const uint8_t *)"cmtverify/sr25519-witness", 25);
+  sha512_update(&c, nonce, 32);
+  sha512_update(&c, msg, mlen);
+  sha512_final(&c, rh);
+  sc_reduce64(r, rh);
+  scalarmult_base(&P, r);
+  ristretto_encode(sig, &P);
+  sr_challenge(k, pk, sig, msg, mlen);
+  sc_muladd(sig + 32, k, key, r);
+  sig[63] |= 0x80;
+}
+
+void oracle_sr25519_sign_batch(size_t n, const uint8_t *minis, const uint32_t *key_idx, const uint8_t *msg,
+                               const uint32_t *msg_off, uint8_t *sig) {
+  for (size_t i = 0; i < n; i++) {
+    size_t kid = key_idx ? key_idx[i] : i;
+    oracle_sr25519_sign(minis + 32 * kid, msg + msg_off[i], msg_off[i + 1] - msg_off[i], sig + 64 * i);
+  }
+}

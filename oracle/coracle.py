@@ -35,6 +35,12 @@ def lib():
         L.oracle_sign_batch.restype = None
         L.oracle_pubkey_from_seed.argtypes = [u8p, u8p]
         L.oracle_pubkey_from_seed.restype = None
+        L.oracle_sr25519_verify_batch.argtypes = [ctypes.c_size_t, u8p, u8p, u8p, u32p, u8p, ctypes.c_int]
+        L.oracle_sr25519_verify_batch.restype = None
+        L.oracle_sr25519_pubkey.argtypes = [u8p, u8p]
+        L.oracle_sr25519_pubkey.restype = None
+        L.oracle_sr25519_sign_batch.argtypes = [ctypes.c_size_t, u8p, u32p, u8p, u32p, u8p]
+        L.oracle_sr25519_sign_batch.restype = None
         _lib = L
     return _lib
 
@@ -85,4 +91,44 @@ def sign_batch(seeds: np.ndarray, msg: np.ndarray, off: np.ndarray, key_idx=None
         key_idx = np.ascontiguousarray(key_idx, dtype=np.uint32)
         kp = _p(key_idx, ctypes.c_uint32)
     lib().oracle_sign_batch(n, _p(seeds), kp, _p(msg), _p(off, ctypes.c_uint32), _p(out), nthreads)
+    return out[:n]
+
+
+# ---- sr25519 (schnorrkel / ristretto255): crypto/sr25519/pubkey.go:34-60
+
+def sr25519_verify_batch(pk: np.ndarray, sig: np.ndarray, msg: np.ndarray, off: np.ndarray,
+                         nthreads: int = 1) -> np.ndarray:
+    n = len(off) - 1
+    pk = np.ascontiguousarray(pk, dtype=np.uint8)
+    sig = np.ascontiguousarray(sig, dtype=np.uint8)
+    msg = np.ascontiguousarray(msg, dtype=np.uint8)
+    if msg.size == 0:
+        msg = np.zeros(1, np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.uint32)
+    out = np.zeros(max(n, 1), dtype=np.uint8)
+    lib().oracle_sr25519_verify_batch(n, _p(pk), _p(sig), _p(msg), _p(off, ctypes.c_uint32), _p(out), nthreads)
+    return out[:n]
+
+
+def sr25519_pubkeys(minis: np.ndarray) -> np.ndarray:
+    minis = np.ascontiguousarray(minis, dtype=np.uint8).reshape(-1, 32)
+    out = np.zeros_like(minis)
+    for i in range(len(minis)):
+        lib().oracle_sr25519_pubkey(_p(minis[i]), _p(out[i]))
+    return out
+
+
+def sr25519_sign_batch(minis: np.ndarray, msg: np.ndarray, off: np.ndarray, key_idx=None) -> np.ndarray:
+    n = len(off) - 1
+    minis = np.ascontiguousarray(minis, dtype=np.uint8)
+    msg = np.ascontiguousarray(msg, dtype=np.uint8)
+    if msg.size == 0:
+        msg = np.zeros(1, np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.uint32)
+    out = np.zeros((max(n, 1), 64), dtype=np.uint8)
+    kp = None
+    if key_idx is not None:
+        key_idx = np.ascontiguousarray(key_idx, dtype=np.uint32)
+        kp = _p(key_idx, ctypes.c_uint32)
+    lib().oracle_sr25519_sign_batch(n, _p(minis), kp, _p(msg), _p(off, ctypes.c_uint32), _p(out))
     return out[:n]

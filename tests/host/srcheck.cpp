@@ -1,0 +1,70 @@
+// Host-side build of the sr25519 device pipeline (cometbft_amd/csrc/sr25519.h,
+// merlin.h, keccak.h) with operand-bound assertions on. Test infrastructure
+// only: checks the kernel source against the sr25519 corpus without a GPU.
+//   input  (stdin):  u32 n, then n x { u8 pk[32], u8 sig[64], u32 mlen, u8 msg[mlen] }
+//   output (stdout): n bytes of verdicts
+//   argv[1] == "challenge": n x 64 challenge bytes instead (transcript only)
+#define CMTV_HD inline
+#define CMTV_BOUNDS_CHECK 1
+#include <cstdio>
+#include <cstring>
+#include <vector>
+#include "../../cometbft_amd/csrc/sr25519.h"
+
+using namespace cmtv;
+
+struct HostBTab {
+  std::vector<uint32_t> rows;
+  HostBTab() : rows(BTAB_ENTRIES * BTAB_ROW_WORDS) {
+    for (int m = 1; m <= BTAB_ENTRIES; m++) btab_entry(&rows[(m - 1) * BTAB_ROW_WORDS], m);
+  }
+  void load_fe(int e, int c, fe& r) const {
+    const uint32_t* p = &rows[e * BTAB_ROW_WORDS + c * BTAB_COORD_WORDS];
+    for (int i = 0; i < 10; i++) r.v[i] = p[i];
+  }
+};
+
+struct HostATab {
+  ge_cached t[8];
+  void load_fe(int e, int c, fe& r) const {
+    r = c == 0 ? t[e].YpX : c == 1 ? t[e].YmX : c == 2 ? t[e].Z : t[e].T2d;
+  }
+  void store(int e, const ge_cached& r) { t[e] = r; }
+};
+
+static void to_words(uint32_t* w, const uint8_t* b, int nw) {
+  for (int i = 0; i < nw; i++) w[i] = b[4 * i] | (b[4 * i + 1] << 8) | (b[4 * i + 2] << 16) | ((uint32_t)b[4 * i + 3] << 24);
+}
+
+int main(int argc, char** argv) {
+  const bool chal = argc > 1 && !strcmp(argv[1], "challenge");
+  HostBTab bt;
+  uint16_t prog[SR_PROGRAM_MAX];
+  const int nops = sr_build_program(prog);
+  uint32_t n;
+  if (fread(&n, 4, 1, stdin) != 1) return 1;
+  for (uint32_t i = 0; i < n; i++) {
+    uint8_t pkb[32], sigb[64];
+    uint32_t mlen;
+    if (fread(pkb, 1, 32, stdin) != 32 || fread(sigb, 1, 64, stdin) != 64 || fread(&mlen, 4, 1, stdin) != 1) return 1;
+    // message at an odd offset inside a word-aligned buffer: exercises the
+    // aligned-word reads of the transcript
+    std::vector<uint32_t> buf((mlen + 16) / 4 + 2, 0);
+    uint8_t* msg = reinterpret_cast<uint8_t*>(buf.data()) + 1 + (i % 3);
+    if (mlen && fread(msg, 1, mlen, stdin) != mlen) return 1;
+    uint32_t pk[8], sig[16];
+    to_words(pk, pkb, 8);
+    to_words(sig, sigb, 16);
+    ArrayStrobeState st;
+    if (chal) {
+      uint32_t out[16];
+      sr_transcript(out, st, prog, nops, msg, mlen, pk, sig);
+      fwrite(out, 4, 16, stdout);
+      continue;
+    }
+    HostATab at;
+    const uint8_t v = sr_verify_one(pk, sig, msg, mlen, prog, nops, st, at, bt) ? 1 : 0;
+    fwrite(&v, 1, 1, stdout);
+  }
+  return 0;
+}

@@ -21,6 +21,8 @@ Extra fields on the JSON line:
   latency_150    -- p50/p99 of cmtv_verify_commit (VerifyCommit, 150 validators:
                     sign-bytes + H2D + kernel + D2H + reference-loop replay),
                     beside the oracle's single-core sequential VerifyCommit time
+  sr25519        -- configs[4]: 10k sr25519 verifications per step (N=1 only),
+                    with the C restatement on the host cores as its CPU baseline
 Run: python bench.py [--gpus N --steps K --warmup W]
 """
 from __future__ import annotations
@@ -52,6 +54,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--latency-iters", type=int, default=200)
     ap.add_argument("--no-latency", action="store_true")
+    ap.add_argument("--no-sr25519", action="store_true", help="skip the configs[4] sr25519 side measurement")
     return ap.parse_args()
 
 
@@ -89,6 +92,65 @@ def cpu_baseline(pk, sig, m, off, mode, cpu_seconds):
                       f"(C restatement of Go 1.19 ed25519.Verify)",
             "single_core_verifs_per_s": round(one, 1), "seconds": round(dt, 2),
             "host_cpu": _cpu_model()}
+
+
+def sr25519_line(ctx, dev, n, steps, cpu_seconds, with_cpu):
+    """configs[4]: sr25519 batch verification of a 10k-signature batch (150
+    keys, 116-byte messages), inputs resident in HBM, timed with HIP events on
+    the launch stream; the C restatement (oracle/liboracle.so) on the host
+    cores as its CPU baseline."""
+    import torch
+    from oracle import coracle  # synthetic data + CPU baseline only
+
+    rng = np.random.default_rng(4)
+    minis = rng.integers(0, 256, (150, 32), dtype=np.uint8)
+    kidx = (np.arange(n) % 150).astype(np.uint32)
+    msgs = [rng.integers(0, 256, 116, dtype=np.uint8).tobytes() for _ in range(n)]
+    m, off = coracle.pack_msgs(msgs)
+    sig = coracle.sr25519_sign_batch(minis, m, off, key_idx=kidx)
+    pk = coracle.sr25519_pubkeys(minis)[kidx]
+    d_pk = torch.from_numpy(np.ascontiguousarray(pk)).to(dev)
+    d_sig = torch.from_numpy(sig).to(dev)
+    d_m = torch.from_numpy(m).to(dev)
+    d_off = torch.from_numpy(off.view(np.int32)).to(dev)
+    d_valid = torch.zeros(n, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def run():
+        ctx.verify_sr25519_device(n, d_pk.data_ptr(), d_sig.data_ptr(), d_m.data_ptr(), d_off.data_ptr(),
+                                  d_valid.data_ptr(), 0, stream.cuda_stream)
+
+    for _ in range(3):
+        run()
+    torch.cuda.synchronize(dev)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    t0 = time.perf_counter()
+    for a, b in evs:
+        a.record(stream)
+        run()
+        b.record(stream)
+    torch.cuda.synchronize(dev)
+    wall = (time.perf_counter() - t0) / steps
+    kms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    res = {"workload": f"configs[4]: {n} sr25519 signatures over 150 keys, 116-byte messages, inputs in HBM",
+           "value": round(n / wall, 1), "unit": "verifs/s", "ms_per_step": round(wall * 1e3, 4),
+           "kernel_ms": round(kms, 4), "verdicts_ok": bool(int(d_valid.sum().item()) == n)}
+    if with_cpu:
+        threads = cpu_threads()
+        t = time.perf_counter()
+        out = coracle.sr25519_verify_batch(pk, sig, m, off, nthreads=threads)
+        first = time.perf_counter() - t
+        assert out.all()
+        reps = max(1, int(cpu_seconds / max(first * threads, 1e-3)))
+        t = time.perf_counter()
+        for _ in range(reps):
+            coracle.sr25519_verify_batch(pk, sig, m, off, nthreads=threads)
+        dt = time.perf_counter() - t
+        res["cpu_baseline"] = {"value": round(reps * n / dt, 1), "unit": "verifs/s", "cores": threads, "kind": "port",
+                               "sample": f"{n}-signature batch x {reps} passes, {threads} threads, oracle/liboracle.so "
+                                         f"(C restatement of go-schnorrkel verify)", "seconds": round(dt, 2)}
+        res["cpu_baseline"]["gpu_over_cpu"] = round(res["value"] / res["cpu_baseline"]["value"], 1)
+    return res
 
 
 def _cpu_model():
@@ -260,6 +322,8 @@ def main():
             line["cpu_baseline"]["gpu_over_cpu"] = round(value / world / line["cpu_baseline"]["value"], 1)
         if not args.no_latency:
             line["latency_150"] = latency_150(ctx, mode, args.latency_iters)
+        if not args.no_sr25519 and world == 1:
+            line["sr25519"] = sr25519_line(ctx, dev, 10_000, 20, args.cpu_seconds / 4, not args.no_cpu_baseline)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

@@ -40,43 +40,7 @@
 
 namespace cmtv {
 
-// B-table access for the quad kernel: each lane reads its own coordinate
-// (word offset `off` inside the row) of entry e.
-struct DevBTabQ {
-  const uint32_t* __restrict__ rows;
-  __device__ __forceinline__ void load_coord(int e, int off, fe& r) const {
-    const uint32_t* p = rows + e * BTAB_ROW_WORDS + off;
-    const uint4 a = *reinterpret_cast<const uint4*>(p);
-    const uint4 b = *reinterpret_cast<const uint4*>(p + 4);
-    const uint2 d = *reinterpret_cast<const uint2*>(p + 8);
-    r.v[0] = a.x; r.v[1] = a.y; r.v[2] = a.z; r.v[3] = a.w;
-    r.v[4] = b.x; r.v[5] = b.y; r.v[6] = b.z; r.v[7] = b.w;
-    r.v[8] = d.x; r.v[9] = d.y;
-  }
-};
 
-// Quad policy (quad.h): 4 consecutive lanes = one signature; operand exchange
-// inside the quad is a DPP quad_perm move. update_dpp with old = src and
-// bound_ctrl off: the mov_dpp(bound_ctrl:1) form miscompiles on ROCm 7.2 /
-// gfx950 once DPP-combine folds it into the consumers (lanes 0-1 of a quad
-// read wrong values; found with tools/dbg/quad_debug.hip).
-struct DevQuad {
-  __device__ __forceinline__ int lane() const { return threadIdx.x & 3; }
-  template <int PAT>
-  __device__ __forceinline__ uint32_t dpp(uint32_t x) const {
-    return (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, PAT, 0xF, 0xF, false);
-  }
-  template <int PAT>
-  __device__ __forceinline__ void perm(fe& o, const fe& v) const {
-#pragma unroll
-    for (int i = 0; i < 10; i++) o.v[i] = dpp<PAT>(v.v[i]);
-  }
-  template <int PAT>
-  __device__ __forceinline__ uint32_t perm32(uint32_t x) const {
-    return dpp<PAT>(x);
-  }
-  __device__ __forceinline__ bool any(bool x) const { return __ballot(x) != 0; }
-};
 
 __device__ __forceinline__ void load_words(uint32_t* w, const uint32_t* __restrict__ src, int nquads) {
   const uint4* p = reinterpret_cast<const uint4*>(src);
@@ -123,25 +87,6 @@ __global__ __launch_bounds__(64, CMTV_VERIFY_WAVES_PER_EU) void k_verify(uint32_
 // chip at one signature per lane, this cuts per-signature latency ~2x.
 // Verdict bits: lane 0 of each quad votes in a ballot; the 16 quad bits of a
 // wave are compacted into one 16-bit slice of the bitmap.
-// Quad (0..8)(-A) table in LDS: entry e, limb pair k of lane t at
-// slot (e * 5 + k) * 64 + t -- a wave's ds_read_b64 covers 512 contiguous
-// bytes whatever entries its 16 signatures pick, so lookups are conflict-free.
-struct DevATabQ {
-  uint2* lds;
-  uint32_t t;
-  __device__ __forceinline__ void store(int e, const fe& c) {
-#pragma unroll
-    for (int k = 0; k < 5; k++) lds[(e * 5 + k) * 64 + t] = make_uint2(c.v[2 * k], c.v[2 * k + 1]);
-  }
-  __device__ __forceinline__ void load(int e, fe& c) const {
-#pragma unroll
-    for (int k = 0; k < 5; k++) {
-      const uint2 x = lds[(e * 5 + k) * 64 + t];
-      c.v[2 * k] = x.x;
-      c.v[2 * k + 1] = x.y;
-    }
-  }
-};
 
 template <uint32_t MODE>
 __global__ __launch_bounds__(64, CMTV_QUAD_WAVES_PER_EU) void k_verify_quad(uint32_t n, const uint32_t* __restrict__ pk,

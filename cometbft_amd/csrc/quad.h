@@ -257,68 +257,17 @@ struct QArrayTab {  // plain-array table policy (host checks, debug kernels)
   CMTV_HD void load(int e, fe& c) const { c = t[e]; }
 };
 
-template <uint32_t MODE, class Q, class BTab, class ATab, class Probe = NullProbe>
-CMTV_HD bool q_verify(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig_ptr, const uint8_t* msg,
-                      uint32_t mlen, const BTab& btab, ATab& tabA, ATab& tabR, const Probe& probe = Probe()) {
+// Phases 2-4 of a quad verification, shared by the Ed25519 (q_verify) and
+// sr25519 (q_verify_sr, sr25519_quad.h) kernels. In: v = this lane's
+// coordinate of -A, rc = of R (both extended, Z = 1), k the challenge, ts the
+// fixed-base scalar s. Out: v = this lane's coordinate of
+//   X = [u]B + [k1](-A) + [|k2|](k2 < 0 ? R : -R) = [k2](R' - R),   R' = [s]B - [k]A
+// with (k1, k2) the half-size pair of k (halfscalar.h) and u = k2 s mod L.
+// rc is clobbered.
+template <class Q, class BTab, class ATab, class Probe>
+CMTV_HD void q_straus_half(const Q& q, fe& v, fe& rc, const uint32_t k[8], const uint32_t ts[8], const BTab& btab,
+                           ATab& tabA, ATab& tabR, const Probe& probe) {
   const int lane = q.lane();
-  uint32_t w[16];
-#pragma unroll
-  for (int i = 0; i < 8; i++) w[i] = sig_ptr[8 + i];
-  const bool s_ok = (w[7] & 0xE0000000u) == 0 && sc_is_canonical(w);
-  uint32_t ts[8];
-#pragma unroll
-  for (int i = 0; i < 8; i++) ts[i] = w[i];
-
-  // ---- phase 1: decode A (even lanes) and R (odd lanes)
-  const uint32_t* src = (lane & 1) ? sig_ptr : pk_ptr;
-#pragma unroll
-  for (int i = 0; i < 8; i++) w[i] = src[i];
-  fe v, rc;
-  bool a_ok, r_ok, r_canon;
-  {
-    ge_p3 P;
-    const bool dec = p3_frombytes(P, w);
-    const bool canon = y_is_canonical(w) && !(fe_iszero(P.X) && (w[7] >> 31));
-    fe x, y, t, one;
-    fe_1(one);
-    q.template perm<QP_B0>(x, P.X);
-    q.template perm<QP_B0>(y, P.Y);
-    q.template perm<QP_B0>(t, P.T);
-    fe_pick(v, lane, x, y, one, t);  // A
-    q.template perm<QP_B1>(x, P.X);
-    q.template perm<QP_B1>(y, P.Y);
-    q.template perm<QP_B1>(t, P.T);
-    fe_pick(rc, lane, x, y, one, t);  // R
-    a_ok = q.template perm32<QP_B0>(dec ? 1u : 0u) != 0;
-    r_ok = q.template perm32<QP_B1>(dec ? 1u : 0u) != 0;
-    r_canon = q.template perm32<QP_B1>(canon ? 1u : 0u) != 0;
-    // -A: negate X (lane 0) and T (lane 3)
-    fe_neg(t, v);
-    fe_carry(t);
-    fe_select(v, v, t, lane == 0 || lane == 3);
-  }
-  probe.snap(0, v);
-  probe.snap(1, rc);
-  uint32_t k[8];
-  {
-    uint32_t h[16];
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      w[i] = sig_ptr[i];
-      w[8 + i] = pk_ptr[i];
-    }
-    sha512_prefixed<16>(h, w, msg, mlen);
-    sc_reduce512(k, h);
-  }
-  {
-    fe kk;
-#pragma unroll
-    for (int i = 0; i < 8; i++) kk.v[i] = k[i];
-    kk.v[8] = s_ok | (a_ok << 1) | (r_ok << 2) | (r_canon << 3);
-    kk.v[9] = 0;
-    probe.snap(2, kk);
-  }
-
   // ---- phase 2: half-size scalars (halfscalar.h) and the fixed-base scalar
   //   X = [u]B + [k1](-A) + [|k2|](k2 < 0 ? R : -R) = [k2](R' - R),
   //   u = k2 s mod L; the window count is uniform over the wave
@@ -396,6 +345,72 @@ CMTV_HD bool q_verify(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig_pt
     if (win >= W - 4) probe.snap(6 + (W - 1 - win), v);
   }
   probe.snap(10, v);
+}
+
+template <uint32_t MODE, class Q, class BTab, class ATab, class Probe = NullProbe>
+CMTV_HD bool q_verify(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig_ptr, const uint8_t* msg,
+                      uint32_t mlen, const BTab& btab, ATab& tabA, ATab& tabR, const Probe& probe = Probe()) {
+  const int lane = q.lane();
+  uint32_t w[16];
+#pragma unroll
+  for (int i = 0; i < 8; i++) w[i] = sig_ptr[8 + i];
+  const bool s_ok = (w[7] & 0xE0000000u) == 0 && sc_is_canonical(w);
+  uint32_t ts[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) ts[i] = w[i];
+
+  // ---- phase 1: decode A (even lanes) and R (odd lanes)
+  const uint32_t* src = (lane & 1) ? sig_ptr : pk_ptr;
+#pragma unroll
+  for (int i = 0; i < 8; i++) w[i] = src[i];
+  fe v, rc;
+  bool a_ok, r_ok, r_canon;
+  {
+    ge_p3 P;
+    const bool dec = p3_frombytes(P, w);
+    const bool canon = y_is_canonical(w) && !(fe_iszero(P.X) && (w[7] >> 31));
+    fe x, y, t, one;
+    fe_1(one);
+    q.template perm<QP_B0>(x, P.X);
+    q.template perm<QP_B0>(y, P.Y);
+    q.template perm<QP_B0>(t, P.T);
+    fe_pick(v, lane, x, y, one, t);  // A
+    q.template perm<QP_B1>(x, P.X);
+    q.template perm<QP_B1>(y, P.Y);
+    q.template perm<QP_B1>(t, P.T);
+    fe_pick(rc, lane, x, y, one, t);  // R
+    a_ok = q.template perm32<QP_B0>(dec ? 1u : 0u) != 0;
+    r_ok = q.template perm32<QP_B1>(dec ? 1u : 0u) != 0;
+    r_canon = q.template perm32<QP_B1>(canon ? 1u : 0u) != 0;
+    // -A: negate X (lane 0) and T (lane 3)
+    fe_neg(t, v);
+    fe_carry(t);
+    fe_select(v, v, t, lane == 0 || lane == 3);
+  }
+  probe.snap(0, v);
+  probe.snap(1, rc);
+  uint32_t k[8];
+  {
+    uint32_t h[16];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      w[i] = sig_ptr[i];
+      w[8 + i] = pk_ptr[i];
+    }
+    sha512_prefixed<16>(h, w, msg, mlen);
+    sc_reduce512(k, h);
+  }
+  {
+    fe kk;
+#pragma unroll
+    for (int i = 0; i < 8; i++) kk.v[i] = k[i];
+    kk.v[8] = s_ok | (a_ok << 1) | (r_ok << 2) | (r_canon << 3);
+    kk.v[9] = 0;
+    probe.snap(2, kk);
+  }
+
+  // ---- phases 2-4: v <- this lane's coordinate of X = [k2](R' - R)
+  q_straus_half(q, v, rc, k, ts, btab, tabA, tabR, probe);
 
   // ---- final check: X = O (GO_STDLIB: R' == R with R canonical, i.e.
   //      encode(R') == R bytes) / [8]X = O (ZIP215)

@@ -123,10 +123,10 @@ static int enqueue_verify(cmtv_ctx* ctx, size_t n, const uint8_t* d_pk, const ui
                           hipStream_t s) {
   if (n == 0) return CMTV_OK;
   // Small batches cannot fill the chip at one signature per lane: use the
-  // 4-lanes-per-signature kernel below the crossover (quad.h). sr25519 has
-  // the lane kernel only.
+  // 4-lanes-per-signature kernel below the crossover (quad.h,
+  // sr25519_quad.h).
   const bool sr = mode == kModeSr25519;
-  const bool quad = !sr && n <= ctx->quad_max;
+  const bool quad = n <= ctx->quad_max;
   hipError_t e = hipSuccess;
   if (!quad) {
     const size_t lanes = std::min<size_t>(n, kChunk);
@@ -141,7 +141,7 @@ static int enqueue_verify(cmtv_ctx* ctx, size_t n, const uint8_t* d_pk, const ui
     if (sr)
       e = launch_verify_sr25519(cn, d_pk + 32 * c, d_sig + 64 * c, d_msg, d_off + c, ctx->d_btab,
                                 static_cast<uint32_t*>(ctx->d_atab.p), ctx->d_srprog, ctx->sr_nops,
-                                d_valid ? d_valid + c : nullptr, d_bitmap ? d_bitmap + c / 64 : nullptr, s);
+                                d_valid ? d_valid + c : nullptr, d_bitmap ? d_bitmap + c / 64 : nullptr, quad, s);
     else
       e = launch_verify(mode, cn, d_pk + 32 * c, d_sig + 64 * c, d_msg, d_off + c, ctx->d_btab,
                         static_cast<uint32_t*>(ctx->d_atab.p), d_valid ? d_valid + c : nullptr,

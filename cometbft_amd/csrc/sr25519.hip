@@ -2,6 +2,9 @@
 // verification (BASELINE configs[4]; reference path
 // /root/reference/crypto/sr25519/pubkey.go:34-60).
 //
+//   k_verify_sr25519_quad: one signature per quad of lanes (sr25519_quad.h),
+//     half-size scalars and 34 shared windows like the Ed25519 quad kernel;
+//     the runtime uses it below the same batch-size crossover
 //   k_verify_sr25519: one signature per lane (sr25519.h): merlin transcript
 //     interpreted from a byte-code program with the Keccak state in LDS,
 //     ristretto255 decoding of A and R, Straus [s]B - [k]A over the Ed25519
@@ -18,6 +21,7 @@
 #include "devtables.h"
 #include "kernels.h"
 #include "sr25519.h"
+#include "sr25519_quad.h"
 
 namespace cmtv {
 
@@ -57,10 +61,52 @@ __global__ __launch_bounds__(64, 2) void k_verify_sr25519(uint32_t n, const uint
   if (threadIdx.x == 0 && out_bitmap) out_bitmap[gid >> 6] = mask;
 }
 
+// One signature per quad of lanes (sr25519_quad.h): 16 signatures per wave;
+// the LDS holds the quad tables (45 KiB) and, before they are built, the
+// lanes' STROBE states (12.5 KiB) in the same space.
+__global__ __launch_bounds__(64, 1) void k_verify_sr25519_quad(uint32_t n, const uint32_t* __restrict__ pk,
+                                                               const uint32_t* __restrict__ sig,
+                                                               const uint8_t* __restrict__ msg,
+                                                               const uint32_t* __restrict__ off,
+                                                               const uint32_t* __restrict__ btab,
+                                                               const uint16_t* __restrict__ prog, int nops,
+                                                               uint8_t* __restrict__ out_valid,
+                                                               uint64_t* __restrict__ out_bitmap) {
+  __shared__ uint2 tab_lds[2 * 9 * 5 * 64];  // (0..8)(-A), (0..8)(-/+R); STROBE states first
+  const uint32_t s = blockIdx.x * 16 + (threadIdx.x >> 2);
+  const bool active = s < n;
+  const uint32_t i = active ? s : n - 1;
+  const uint32_t m0 = off[i], m1 = off[i + 1];
+  DevQuad q;
+  DevBTabQ bt{btab};
+  DevATabQ ta{tab_lds, threadIdx.x}, tr{tab_lds + 9 * 5 * 64, threadIdx.x};
+  LdsStrobeState st{reinterpret_cast<uint32_t*>(tab_lds), threadIdx.x};
+  bool v = q_verify_sr(q, pk + 8 * (size_t)i, sig + 16 * (size_t)i, msg + m0, m1 - m0, prog, nops, st, bt, ta, tr);
+  v = v && active;
+  if (active && (threadIdx.x & 3) == 0 && out_valid) out_valid[s] = v ? 1 : 0;
+  // compact bit 4j -> bit j (16 verdicts of this wave); 4 consecutive blocks
+  // fill one 64-bit bitmap word, each writes its 16-bit slice
+  uint64_t x = __ballot(v && (threadIdx.x & 3) == 0) & 0x1111111111111111ull;
+  x = (x | (x >> 3)) & 0x0303030303030303ull;
+  x = (x | (x >> 6)) & 0x000F000F000F000Full;
+  x = (x | (x >> 12)) & 0x000000FF000000FFull;
+  x = (x | (x >> 24)) & 0xFFFFull;
+  if (threadIdx.x == 0 && out_bitmap) reinterpret_cast<uint16_t*>(out_bitmap)[blockIdx.x] = (uint16_t)x;
+}
+
 hipError_t launch_verify_sr25519(uint32_t n, const void* pk, const void* sig, const void* msg, const void* off,
                                  const uint32_t* btab, uint32_t* atab, const uint16_t* prog, int nops, void* valid,
-                                 void* bitmap, hipStream_t s) {
+                                 void* bitmap, bool quad, hipStream_t s) {
   if (n == 0) return hipSuccess;
+  if (quad) {
+    // one 64-lane block = 16 signatures; whole groups of 4 blocks so every
+    // 16-bit slice of every bitmap word is written
+    hipLaunchKernelGGL(k_verify_sr25519_quad, dim3(((n + 63) / 64) * 4), dim3(64), 0, s, n,
+                       static_cast<const uint32_t*>(pk), static_cast<const uint32_t*>(sig),
+                       static_cast<const uint8_t*>(msg), static_cast<const uint32_t*>(off), btab, prog, nops,
+                       static_cast<uint8_t*>(valid), static_cast<uint64_t*>(bitmap));
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_verify_sr25519, dim3((n + 63) / 64), dim3(64), 0, s, n, static_cast<const uint32_t*>(pk),
                      static_cast<const uint32_t*>(sig), static_cast<const uint8_t*>(msg),
                      static_cast<const uint32_t*>(off), btab, atab, prog, nops, static_cast<uint8_t*>(valid),

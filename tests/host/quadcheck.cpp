@@ -10,6 +10,7 @@
 #include <thread>
 #include <vector>
 #include "../../cometbft_amd/csrc/quad.h"
+#include "../../cometbft_amd/csrc/sr25519_quad.h"
 
 using namespace cmtv;
 
@@ -73,14 +74,18 @@ static void to_words(uint32_t* w, const uint8_t* b, int nw) {
   for (int i = 0; i < nw; i++) w[i] = b[4 * i] | (b[4 * i + 1] << 8) | (b[4 * i + 2] << 16) | ((uint32_t)b[4 * i + 3] << 24);
 }
 
-int main() {
+int main(int argc, char** argv) {
+  // argv[1] == "sr": sr25519 records { pk[32], sig[64], u32 mlen, msg } (no mode byte)
+  const bool sr = argc > 1 && !strcmp(argv[1], "sr");
+  uint16_t prog[SR_PROGRAM_MAX];
+  const int nops = sr_build_program(prog);
   HostBTab bt;
   uint32_t n;
   if (fread(&n, 4, 1, stdin) != 1) return 1;
   for (uint32_t i = 0; i < n; i++) {
-    uint8_t mode, pk[32], sig[64];
+    uint8_t mode = 0, pk[32], sig[64];
     uint32_t mlen;
-    if (fread(&mode, 1, 1, stdin) != 1 || fread(pk, 32, 1, stdin) != 1 || fread(sig, 64, 1, stdin) != 1 ||
+    if ((!sr && fread(&mode, 1, 1, stdin) != 1) || fread(pk, 32, 1, stdin) != 1 || fread(sig, 64, 1, stdin) != 1 ||
         fread(&mlen, 4, 1, stdin) != 1)
       return 1;
     std::vector<uint8_t> buf(mlen + 16, 0xEE);
@@ -96,8 +101,12 @@ int main() {
       th.emplace_back([&, l] {
         HostQuad q{l, &ex};
         QArrayTab ta, tr;
-        res[l] = mode ? q_verify<MODE_ZIP215>(q, pkw, sigw, mp, mlen, bt, ta, tr)
-                      : q_verify<MODE_GO_STDLIB>(q, pkw, sigw, mp, mlen, bt, ta, tr);
+        ArrayStrobeState st;
+        if (sr)
+          res[l] = q_verify_sr(q, pkw, sigw, mp, mlen, prog, nops, st, bt, ta, tr);
+        else
+          res[l] = mode ? q_verify<MODE_ZIP215>(q, pkw, sigw, mp, mlen, bt, ta, tr)
+                        : q_verify<MODE_GO_STDLIB>(q, pkw, sigw, mp, mlen, bt, ta, tr);
       });
     for (auto& t : th) t.join();
     if (res[0] != res[1] || res[0] != res[2] || res[0] != res[3]) {

@@ -174,3 +174,23 @@ def test_device_pipeline_matches_corpus(srcheck, vectors):
     got = np.frombuffer(_run_srcheck(srcheck, vectors, idx), np.uint8)
     bad = np.nonzero(got != vectors["valid"])[0]
     assert bad.size == 0, [(int(i), vectors["cats"][int(i)]) for i in bad[:10]]
+
+
+QSRC = os.path.join(ROOT, "tests", "host", "quadcheck.cpp")
+QBIN = os.path.join(ROOT, "build", "quadcheck")
+
+
+def test_quad_pipeline_matches_corpus(vectors):
+    """sr25519_quad.h (the quad kernel's source: half-size scalars, E[4]
+    final check), four host threads in lockstep for the DPP exchanges, over
+    every non-honest vector and a slice of the honest ones."""
+    hdr = os.path.join(ROOT, "cometbft_amd", "csrc")
+    deps = [QSRC] + [os.path.join(hdr, f) for f in os.listdir(hdr) if f.endswith(".h")]
+    if not os.path.exists(QBIN) or os.path.getmtime(QBIN) < max(os.path.getmtime(d) for d in deps):
+        subprocess.run(["g++", "-O2", "-std=c++20", "-pthread", "-o", QBIN, QSRC], check=True)
+    cats = vectors["cats"]
+    idx = [i for i, c in enumerate(cats) if c != "honest"] + [i for i, c in enumerate(cats) if c == "honest"][::3]
+    got = np.frombuffer(_run_srcheck(QBIN, vectors, sorted(idx), "sr"), np.uint8)
+    exp = vectors["valid"][sorted(idx)]
+    bad = np.nonzero(got != exp)[0]
+    assert bad.size == 0, [(sorted(idx)[int(i)], cats[sorted(idx)[int(i)]]) for i in bad[:10]]

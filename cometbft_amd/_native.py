@@ -45,7 +45,7 @@ EXPORTS = (
     "cmtv_register_keys", "cmtv_keyset_free", "cmtv_keyset_len", "cmtv_verify_ed25519_indexed",
     "cmtv_verify_ed25519_indexed_device",
     "cmtv_batch_new", "cmtv_batch_add", "cmtv_batch_len", "cmtv_batch_verify", "cmtv_batch_reset",
-    "cmtv_batch_free", "cmtv_verify_commit", "cmtv_vote_sign_bytes", "cmtv_pubkeys_ed25519", "cmtv_sign_ed25519",
+    "cmtv_batch_free", "cmtv_verify_commit", "cmtv_verify_commits", "cmtv_verdict_cache", "cmtv_vote_sign_bytes", "cmtv_pubkeys_ed25519", "cmtv_sign_ed25519",
 )
 
 
@@ -64,7 +64,8 @@ class cmtv_config(ctypes.Structure):
 class cmtv_stats(ctypes.Structure):
     _fields_ = [("calls", ctypes.c_uint64), ("signatures", ctypes.c_uint64), ("invalid", ctypes.c_uint64),
                 ("kernel_launches", ctypes.c_uint64), ("device_ms", ctypes.c_double),
-                ("last_kernel_ms", ctypes.c_double)]
+                ("last_kernel_ms", ctypes.c_double), ("cache_hits", ctypes.c_uint64),
+                ("cache_entries", ctypes.c_uint64)]
 
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -152,6 +153,13 @@ def lib() -> ctypes.CDLL:
                                      ctypes.POINTER(cmtv_block_id), i64, ctypes.POINTER(cmtv_commit), u64, u64,
                                      ctypes.POINTER(cmtv_commit_result), ctypes.c_char_p, sz]
     L.cmtv_verify_commit.restype = ctypes.c_int
+    L.cmtv_verify_commits.argtypes = [vp, u32, u32, ctypes.c_char_p, sz, sz, ctypes.POINTER(cmtv_valset),
+                                      ctypes.POINTER(cmtv_block_id), ctypes.POINTER(i64), ctypes.POINTER(cmtv_commit),
+                                      u64, u64, ctypes.POINTER(cmtv_commit_result), ctypes.POINTER(ctypes.c_int),
+                                      ctypes.c_char_p, sz]
+    L.cmtv_verify_commits.restype = ctypes.c_int
+    L.cmtv_verdict_cache.argtypes = [vp, sz]
+    L.cmtv_verdict_cache.restype = ctypes.c_int
     L.cmtv_vote_sign_bytes.argtypes = [ctypes.c_char_p, sz, i32, i64, i32, ctypes.POINTER(cmtv_block_id), i64, i32,
                                        _u8p, sz]
     L.cmtv_vote_sign_bytes.restype = i64

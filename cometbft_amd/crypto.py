@@ -65,6 +65,10 @@ class Context:
         N.check(N.lib().cmtv_stats_get(self._h, ctypes.byref(st)), "cmtv_stats_get")
         return {k: getattr(st, k) for k, _ in st._fields_}
 
+    def verdict_cache(self, max_entries: int) -> None:
+        """cmtv_verdict_cache: keep the last max_entries verdicts (0 = off)."""
+        N.check(N.lib().cmtv_verdict_cache(self._h, max_entries), "cmtv_verdict_cache")
+
     # -------------------------------------------------------------- batches
     def verify(self, pk: np.ndarray, sig: np.ndarray, msg: np.ndarray, msg_off: np.ndarray,
                mode: int | None = None, bitmap: bool = False):

@@ -130,6 +130,257 @@ void set_msg(char* buf, size_t cap, const std::string& s) {
 constexpr uint8_t kFlagAbsent = 1, kFlagCommit = 2, kFlagNil = 3;
 constexpr int32_t kPrecommit = 2;
 
+// ------------------------------------------------------------------ VerifyCommit*
+
+// Signatures of one or more commits, gathered for one device batch.
+struct SigBatch {
+  std::vector<uint8_t> pk, sg, msgs, len_ok;
+  std::vector<uint32_t> off{0};
+  std::string sb;
+  size_t size() const { return off.size() - 1; }
+  // key (32 bytes), the CommitSig's signature and the vote's sign-bytes
+  void add(const uint8_t* key, const uint8_t* sig, uint32_t sig_len, const char* chain_id, size_t chain_id_len,
+           const cmtv_commit* c, uint32_t idx) {
+    static const cmtv_block_id empty{};
+    pk.insert(pk.end(), key, key + 32);
+    const size_t o = sg.size();
+    sg.resize(o + 64, 0);
+    if (sig_len == 64) std::memcpy(&sg[o], sig, 64);
+    len_ok.push_back(sig_len == 64);
+    // Commit.GetVote(idx) (types/block.go:784): CommitSig.BlockID(commit.BlockID)
+    const cmtv_block_id* vb = c->flags[idx] == kFlagCommit ? &c->block_id : &empty;
+    vote_sign_bytes(sb, chain_id, chain_id_len, kPrecommit, c->height, c->round, vb, c->ts_seconds[idx],
+                    c->ts_nanos[idx]);
+    msgs.insert(msgs.end(), sb.begin(), sb.end());
+    off.push_back((uint32_t)msgs.size());
+  }
+};
+
+// One VerifyCommit* evaluation: preamble + plan (job_prepare), then the
+// reference loop replayed over device verdicts (job_replay).
+struct CommitJob {
+  uint32_t kind;
+  const char* chain_id;
+  size_t chain_id_len;
+  const cmtv_valset* vals;
+  const cmtv_block_id* block_id;
+  int64_t height;
+  const cmtv_commit* commit;
+  uint64_t trust_num, trust_den;
+  cmtv_commit_result* res;
+  char* msg_buf;
+  size_t msg_cap;
+  // state
+  int early = 1;  // != 1: the preamble already decided (return code)
+  int64_t needed = 0;
+  std::unordered_map<std::string, uint32_t> by_addr;
+  std::vector<uint32_t> plan_idx, plan_val;
+  size_t first = 0;  // batch index of plan item 0
+
+  int fail(int32_t code, int32_t idx, const std::string& m) {
+    res->code = code;
+    res->sig_index = idx;
+    set_msg(msg_buf, msg_cap, m);
+    return CMTV_ECOMMIT;
+  }
+};
+
+int job_check_args(uint32_t kind, const char* chain_id, size_t chain_id_len, const cmtv_valset* vals,
+                   const cmtv_block_id* block_id, const cmtv_commit* commit, cmtv_commit_result* res) {
+  if (!vals || !commit || !res || kind > CMTV_VERIFY_COMMIT_LIGHT_TRUSTING) return CMTV_EINVAL;
+  if ((!chain_id && chain_id_len) || (vals->n_vals && (!vals->pubkeys || !vals->pk_off || !vals->voting_power)))
+    return CMTV_EINVAL;
+  const uint32_t nsig = commit->n_sigs;
+  if (nsig && (!commit->flags || !commit->ts_seconds || !commit->ts_nanos || !commit->sigs || !commit->sig_off))
+    return CMTV_EINVAL;
+  if (kind == CMTV_VERIFY_COMMIT_LIGHT_TRUSTING && nsig && (!commit->val_addrs || (vals->n_vals && !vals->addrs)))
+    return CMTV_EINVAL;
+  if (kind != CMTV_VERIFY_COMMIT_LIGHT_TRUSTING && !block_id) return CMTV_EINVAL;
+  return CMTV_OK;
+}
+
+// Preamble checks and the threshold (validator_set.go:670-684, 779-790), then
+// the plan: which signatures the reference loop can reach, assuming every
+// verdict is valid (the loop stops at its first error, so nothing beyond the
+// plan is ever examined). Appends the planned signatures to B; with
+// `prefetch` a light call also appends its commit's other non-absent
+// signatures (verdicts for the verdict cache only).
+void job_prepare(CommitJob& J, SigBatch& B, bool prefetch) {
+  const cmtv_valset* vals = J.vals;
+  const cmtv_commit* commit = J.commit;
+  std::memset(J.res, 0, sizeof(*J.res));
+  J.res->sig_index = -1;
+  set_msg(J.msg_buf, J.msg_cap, "");
+  const uint32_t nsig = commit->n_sigs;
+  int64_t total = 0;
+  for (uint32_t i = 0; i < vals->n_vals; i++) total += vals->voting_power[i];
+
+  if (J.kind == CMTV_VERIFY_COMMIT_LIGHT_TRUSTING) {
+    if (J.trust_den == 0) {
+      J.early = J.fail(CMTV_COMMIT_ERR_TRUST_LEVEL, -1, "trustLevel has zero Denominator");
+      return;
+    }
+    __int128 prod = (__int128)total * (__int128)(int64_t)J.trust_num;
+    if (prod > INT64_MAX || prod < INT64_MIN) {
+      J.early = J.fail(CMTV_COMMIT_ERR_TRUST_LEVEL, -1,
+                       "int64 overflow while calculating voting power needed. please provide smaller trustLevel "
+                       "numerator");
+      return;
+    }
+    J.needed = (int64_t)prod / (int64_t)J.trust_den;
+    for (uint32_t i = 0; i < vals->n_vals; i++)
+      J.by_addr.emplace(std::string(reinterpret_cast<const char*>(vals->addrs + 20 * (size_t)i), 20), i);
+  } else {
+    if (vals->n_vals != nsig) {
+      char b[128];
+      std::snprintf(b, sizeof b, "Invalid commit -- wrong set size: %u vs %u", vals->n_vals, nsig);
+      J.early = J.fail(CMTV_COMMIT_ERR_SET_SIZE, -1, b);
+      return;
+    }
+    if (J.height != commit->height) {
+      char b[128];
+      std::snprintf(b, sizeof b, "Invalid commit -- wrong height: %" PRId64 " vs %" PRId64, J.height, commit->height);
+      J.early = J.fail(CMTV_COMMIT_ERR_HEIGHT, -1, b);
+      return;
+    }
+    if (!block_id_equals(J.block_id, &commit->block_id)) {
+      J.early = J.fail(CMTV_COMMIT_ERR_BLOCK_ID, -1,
+                       "invalid commit -- wrong block ID: want " + block_id_string(J.block_id) + ", got " +
+                           block_id_string(&commit->block_id));
+      return;
+    }
+    J.needed = total * 2 / 3;
+  }
+
+  int64_t tally = 0;
+  std::unordered_map<uint32_t, uint32_t> seen;
+  for (uint32_t idx = 0; idx < nsig; idx++) {
+    const uint8_t flag = commit->flags[idx];
+    uint32_t vi = idx;
+    if (J.kind == CMTV_VERIFY_COMMIT) {
+      if (flag == kFlagAbsent) continue;
+      if (flag != kFlagCommit && flag != kFlagNil) break;  // panics here
+    } else {
+      if (flag != kFlagCommit) continue;
+      if (J.kind == CMTV_VERIFY_COMMIT_LIGHT_TRUSTING) {
+        auto it = J.by_addr.find(std::string(reinterpret_cast<const char*>(commit->val_addrs + 20 * (size_t)idx), 20));
+        if (it == J.by_addr.end()) continue;
+        vi = it->second;
+        if (seen.count(vi)) break;  // double vote error here
+        seen.emplace(vi, idx);
+      }
+    }
+    if (vals->pk_off[vi + 1] - vals->pk_off[vi] != 32) break;  // panics here
+    J.plan_idx.push_back(idx);
+    J.plan_val.push_back(vi);
+    if (J.kind != CMTV_VERIFY_COMMIT) {
+      tally += vals->voting_power[vi];
+      if (tally > J.needed) break;
+    }
+  }
+
+  J.first = B.size();
+  for (size_t j = 0; j < J.plan_idx.size(); j++) {
+    const uint32_t idx = J.plan_idx[j], vi = J.plan_val[j];
+    const uint32_t s0 = commit->sig_off[idx], s1 = commit->sig_off[idx + 1];
+    B.add(vals->pubkeys + vals->pk_off[vi], commit->sigs + s0, s1 - s0, J.chain_id, J.chain_id_len, commit, idx);
+  }
+  if (prefetch && J.kind == CMTV_VERIFY_COMMIT_LIGHT) {
+    // the VerifyCommit calls that follow a light call in blocksync verify
+    // every non-absent signature: verify the rest now, in the same batch
+    std::vector<uint8_t> planned(nsig, 0);
+    for (uint32_t idx : J.plan_idx) planned[idx] = 1;
+    for (uint32_t idx = 0; idx < nsig; idx++) {
+      const uint8_t flag = commit->flags[idx];
+      if (planned[idx] || (flag != kFlagCommit && flag != kFlagNil)) continue;
+      if (vals->pk_off[idx + 1] - vals->pk_off[idx] != 32) continue;
+      const uint32_t s0 = commit->sig_off[idx], s1 = commit->sig_off[idx + 1];
+      B.add(vals->pubkeys + vals->pk_off[idx], commit->sigs + s0, s1 - s0, J.chain_id, J.chain_id_len, commit, idx);
+    }
+  }
+}
+
+int batch_verify(cmtv_ctx* ctx, SigBatch& B, uint32_t mode, std::vector<uint8_t>& valid) {
+  const size_t m = B.size();
+  valid.assign(m, 0);
+  if (!m) return CMTV_OK;
+  if (B.msgs.empty()) B.msgs.push_back(0);
+  const int rc = cmtv::verify_host_locked(ctx, m, B.pk.data(), B.sg.data(), B.msgs.data(), B.off.data(), mode,
+                                          valid.data(), nullptr);
+  if (rc != CMTV_OK) return rc;
+  for (size_t j = 0; j < m; j++)
+    if (!B.len_ok[j]) valid[j] = 0;  // crypto/ed25519/ed25519.go:150
+  return CMTV_OK;
+}
+
+// The reference loop (validator_set.go:685-713, 740-764, 793-825) over the
+// verdicts of the planned signatures.
+int job_replay(CommitJob& J, const std::vector<uint8_t>& all_valid) {
+  if (J.early != 1) return J.early;
+  const cmtv_valset* vals = J.vals;
+  const cmtv_commit* commit = J.commit;
+  const uint32_t nsig = commit->n_sigs;
+  const size_t m = J.plan_idx.size();
+  const uint8_t* valid = all_valid.data() + J.first;
+  J.res->n_verified = (uint32_t)m;
+  auto wrong_sig = [&](uint32_t idx) {
+    const uint32_t s0 = commit->sig_off[idx], s1 = commit->sig_off[idx + 1];
+    return J.fail(CMTV_COMMIT_ERR_WRONG_SIGNATURE, (int32_t)idx,
+                  "wrong signature (#" + std::to_string(idx) + "): " + hex_upper(commit->sigs + s0, s1 - s0));
+  };
+  auto bad_pk = [&](uint32_t idx, uint32_t vi) {
+    return J.fail(CMTV_COMMIT_PANIC_BAD_PUBKEY, (int32_t)idx,
+                  "ed25519: bad public key length: " + std::to_string(vals->pk_off[vi + 1] - vals->pk_off[vi]));
+  };
+  int64_t tally = 0;
+  size_t j = 0;
+  std::unordered_map<uint32_t, uint32_t> seen;
+  for (uint32_t idx = 0; idx < nsig; idx++) {
+    const uint8_t flag = commit->flags[idx];
+    if (J.kind == CMTV_VERIFY_COMMIT) {
+      if (flag == kFlagAbsent) continue;
+      if (flag != kFlagCommit && flag != kFlagNil)
+        return J.fail(CMTV_COMMIT_PANIC_UNKNOWN_FLAG, (int32_t)idx, "Unknown BlockIDFlag: " + std::to_string(flag));
+      if (vals->pk_off[idx + 1] - vals->pk_off[idx] != 32) return bad_pk(idx, idx);
+      if (j >= m || J.plan_idx[j] != idx || !valid[j]) return wrong_sig(idx);
+      j++;
+      if (flag == kFlagCommit) tally += vals->voting_power[idx];
+    } else {
+      if (flag != kFlagCommit) continue;
+      uint32_t vi = idx;
+      if (J.kind == CMTV_VERIFY_COMMIT_LIGHT_TRUSTING) {
+        auto it = J.by_addr.find(std::string(reinterpret_cast<const char*>(commit->val_addrs + 20 * (size_t)idx), 20));
+        if (it == J.by_addr.end()) continue;
+        vi = it->second;
+        auto sit = seen.find(vi);
+        if (sit != seen.end()) {
+          // Validator.String(): "Validator{%v %v VP:%v A:%v}" (types/validator.go)
+          std::string vs = "Validator{" + hex_upper(vals->addrs + 20 * (size_t)vi, 20) + " PubKeyEd25519{" +
+                           hex_upper(vals->pubkeys + vals->pk_off[vi], vals->pk_off[vi + 1] - vals->pk_off[vi]) +
+                           "} VP:" + std::to_string(vals->voting_power[vi]) + " A:" +
+                           std::to_string(vals->proposer_priority ? vals->proposer_priority[vi] : 0) + "}";
+          return J.fail(CMTV_COMMIT_ERR_DOUBLE_VOTE, (int32_t)idx,
+                        "double vote from " + vs + " (" + std::to_string(sit->second) + " and " +
+                            std::to_string(idx) + ")");
+        }
+        seen.emplace(vi, idx);
+      }
+      if (vals->pk_off[vi + 1] - vals->pk_off[vi] != 32) return bad_pk(idx, vi);
+      if (j >= m || J.plan_idx[j] != idx || !valid[j]) return wrong_sig(idx);
+      j++;
+      tally += vals->voting_power[vi];
+      if (tally > J.needed) return CMTV_OK;
+    }
+  }
+  if (J.kind == CMTV_VERIFY_COMMIT && tally > J.needed) return CMTV_OK;
+  J.res->got = tally;
+  J.res->needed = J.needed;
+  char b[160];
+  std::snprintf(b, sizeof b, "invalid commit -- insufficient voting power: got %" PRId64 ", needed more than %" PRId64,
+                tally, J.needed);
+  return J.fail(CMTV_COMMIT_ERR_NOT_ENOUGH_POWER, -1, b);
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------ BatchVerifier
@@ -225,183 +476,53 @@ int cmtv_verify_commit(cmtv_ctx* ctx, uint32_t kind, uint32_t mode, const char* 
                        const cmtv_valset* vals, const cmtv_block_id* block_id, int64_t height,
                        const cmtv_commit* commit, uint64_t trust_num, uint64_t trust_den, cmtv_commit_result* res,
                        char* msg_buf, size_t msg_cap) {
-  if (!ctx || !vals || !commit || !res || kind > CMTV_VERIFY_COMMIT_LIGHT_TRUSTING || mode > CMTV_MODE_ZIP215)
+  if (!ctx || mode > CMTV_MODE_ZIP215) return CMTV_EINVAL;
+  int rc = job_check_args(kind, chain_id, chain_id_len, vals, block_id, commit, res);
+  if (rc != CMTV_OK) return rc;
+  CommitJob J{kind, chain_id, chain_id_len, vals, block_id, height, commit, trust_num, trust_den, res, msg_buf,
+              msg_cap};
+  std::unique_lock<std::mutex> lk;
+  rc = cmtv::ctx_lock(ctx, lk);
+  if (rc != CMTV_OK) return rc;
+  SigBatch B;
+  job_prepare(J, B, cmtv::cache_enabled(ctx));
+  std::vector<uint8_t> valid;
+  rc = batch_verify(ctx, B, mode, valid);
+  if (rc != CMTV_OK) return rc;
+  return job_replay(J, valid);
+}
+
+int cmtv_verify_commits(cmtv_ctx* ctx, uint32_t kind, uint32_t mode, const char* chain_id, size_t chain_id_len,
+                        size_t n, const cmtv_valset* vals, const cmtv_block_id* block_ids, const int64_t* heights,
+                        const cmtv_commit* commits, uint64_t trust_num, uint64_t trust_den,
+                        cmtv_commit_result* results, int* rcs, char* msg_bufs, size_t msg_cap) {
+  if (!ctx || mode > CMTV_MODE_ZIP215 || n > (1u << 24)) return CMTV_EINVAL;
+  if (n == 0) return CMTV_OK;
+  if (!vals || !commits || !results || !rcs || !heights ||
+      (kind != CMTV_VERIFY_COMMIT_LIGHT_TRUSTING && !block_ids))
     return CMTV_EINVAL;
-  if ((!chain_id && chain_id_len) || (vals->n_vals && (!vals->pubkeys || !vals->pk_off || !vals->voting_power)))
-    return CMTV_EINVAL;
-  const uint32_t nsig = commit->n_sigs;
-  if (nsig && (!commit->flags || !commit->ts_seconds || !commit->ts_nanos || !commit->sigs || !commit->sig_off))
-    return CMTV_EINVAL;
-  if (kind == CMTV_VERIFY_COMMIT_LIGHT_TRUSTING && nsig && (!commit->val_addrs || (vals->n_vals && !vals->addrs)))
-    return CMTV_EINVAL;
-  if (kind != CMTV_VERIFY_COMMIT_LIGHT_TRUSTING && !block_id) return CMTV_EINVAL;
-  std::memset(res, 0, sizeof(*res));
-  res->sig_index = -1;
-  set_msg(msg_buf, msg_cap, "");
-
-  auto fail = [&](int32_t code, int32_t idx, const std::string& m) {
-    res->code = code;
-    res->sig_index = idx;
-    set_msg(msg_buf, msg_cap, m);
-    return CMTV_ECOMMIT;
-  };
-
-  int64_t total = 0;
-  for (uint32_t i = 0; i < vals->n_vals; i++) total += vals->voting_power[i];
-
-  // --- preamble checks and the threshold (validator_set.go:670-684, 779-790)
-  int64_t needed = 0;
-  std::unordered_map<std::string, uint32_t> by_addr;
-  if (kind == CMTV_VERIFY_COMMIT_LIGHT_TRUSTING) {
-    if (trust_den == 0) return fail(CMTV_COMMIT_ERR_TRUST_LEVEL, -1, "trustLevel has zero Denominator");
-    __int128 prod = (__int128)total * (__int128)(int64_t)trust_num;
-    if (prod > INT64_MAX || prod < INT64_MIN)
-      return fail(CMTV_COMMIT_ERR_TRUST_LEVEL, -1,
-                  "int64 overflow while calculating voting power needed. please provide smaller trustLevel numerator");
-    needed = (int64_t)prod / (int64_t)trust_den;
-    for (uint32_t i = 0; i < vals->n_vals; i++)
-      by_addr.emplace(std::string(reinterpret_cast<const char*>(vals->addrs + 20 * (size_t)i), 20), i);
-  } else {
-    if (vals->n_vals != nsig) {
-      char b[128];
-      std::snprintf(b, sizeof b, "Invalid commit -- wrong set size: %u vs %u", vals->n_vals, nsig);
-      return fail(CMTV_COMMIT_ERR_SET_SIZE, -1, b);
-    }
-    if (height != commit->height) {
-      char b[128];
-      std::snprintf(b, sizeof b, "Invalid commit -- wrong height: %" PRId64 " vs %" PRId64, height, commit->height);
-      return fail(CMTV_COMMIT_ERR_HEIGHT, -1, b);
-    }
-    if (!block_id_equals(block_id, &commit->block_id))
-      return fail(CMTV_COMMIT_ERR_BLOCK_ID, -1,
-                  "invalid commit -- wrong block ID: want " + block_id_string(block_id) + ", got " +
-                      block_id_string(&commit->block_id));
-    needed = total * 2 / 3;
-  }
-
-  // --- plan: which signatures the reference loop can reach, assuming every
-  // verdict is valid; the loop stops at the first error, so nothing beyond the
-  // planned set is ever examined.
-  std::vector<uint32_t> plan_idx, plan_val;
-  {
-    int64_t tally = 0;
-    std::unordered_map<uint32_t, uint32_t> seen;
-    for (uint32_t idx = 0; idx < nsig; idx++) {
-      const uint8_t flag = commit->flags[idx];
-      uint32_t vi = idx;
-      if (kind == CMTV_VERIFY_COMMIT) {
-        if (flag == kFlagAbsent) continue;
-        if (flag != kFlagCommit && flag != kFlagNil) break;  // panics here
-      } else {
-        if (flag != kFlagCommit) continue;
-        if (kind == CMTV_VERIFY_COMMIT_LIGHT_TRUSTING) {
-          auto it = by_addr.find(std::string(reinterpret_cast<const char*>(commit->val_addrs + 20 * (size_t)idx), 20));
-          if (it == by_addr.end()) continue;
-          vi = it->second;
-          if (seen.count(vi)) break;  // double vote error here
-          seen.emplace(vi, idx);
-        }
-      }
-      if (vals->pk_off[vi + 1] - vals->pk_off[vi] != 32) break;  // panics here
-      plan_idx.push_back(idx);
-      plan_val.push_back(vi);
-      if (kind != CMTV_VERIFY_COMMIT) {
-        tally += vals->voting_power[vi];
-        if (tally > needed) break;
-      }
-    }
-  }
-
-  // --- one device batch for the planned signatures
-  const size_t m = plan_idx.size();
-  std::vector<uint8_t> pk(32 * m), sg(64 * m, 0), msgs, valid(m, 0);
-  std::vector<uint32_t> off(m + 1, 0);
-  std::vector<uint8_t> sig_len_ok(m, 0);
-  std::string sb;
-  const cmtv_block_id empty{};
-  for (size_t j = 0; j < m; j++) {
-    const uint32_t idx = plan_idx[j], vi = plan_val[j];
-    std::memcpy(&pk[32 * j], vals->pubkeys + vals->pk_off[vi], 32);
-    const uint32_t s0 = commit->sig_off[idx], s1 = commit->sig_off[idx + 1];
-    if (s1 - s0 == 64) {
-      std::memcpy(&sg[64 * j], commit->sigs + s0, 64);
-      sig_len_ok[j] = 1;
-    }
-    // Commit.GetVote(idx) (types/block.go:784): CommitSig.BlockID(commit.BlockID)
-    const cmtv_block_id* vb = commit->flags[idx] == kFlagCommit ? &commit->block_id : &empty;
-    vote_sign_bytes(sb, chain_id, chain_id_len, kPrecommit, commit->height, commit->round, vb,
-                    commit->ts_seconds[idx], commit->ts_nanos[idx]);
-    msgs.insert(msgs.end(), sb.begin(), sb.end());
-    off[j + 1] = (uint32_t)msgs.size();
-  }
-  if (m) {
-    std::unique_lock<std::mutex> lk;
-    int rc = cmtv::ctx_lock(ctx, lk);
+  for (size_t c = 0; c < n; c++) {
+    const int rc = job_check_args(kind, chain_id, chain_id_len, &vals[c], block_ids ? &block_ids[c] : nullptr,
+                                  &commits[c], &results[c]);
     if (rc != CMTV_OK) return rc;
-    rc = cmtv::verify_host_locked(ctx, m, pk.data(), sg.data(), msgs.data(), off.data(), mode, valid.data(), nullptr);
-    if (rc != CMTV_OK) return rc;
-    for (size_t j = 0; j < m; j++)
-      if (!sig_len_ok[j]) valid[j] = 0;  // crypto/ed25519/ed25519.go:150
   }
-  res->n_verified = (uint32_t)m;
-
-  // --- replay the reference loop over the verdicts
-  auto wrong_sig = [&](uint32_t idx) {
-    const uint32_t s0 = commit->sig_off[idx], s1 = commit->sig_off[idx + 1];
-    return fail(CMTV_COMMIT_ERR_WRONG_SIGNATURE, (int32_t)idx,
-                "wrong signature (#" + std::to_string(idx) + "): " + hex_upper(commit->sigs + s0, s1 - s0));
-  };
-  auto bad_pk = [&](uint32_t idx, uint32_t vi) {
-    return fail(CMTV_COMMIT_PANIC_BAD_PUBKEY, (int32_t)idx,
-                "ed25519: bad public key length: " + std::to_string(vals->pk_off[vi + 1] - vals->pk_off[vi]));
-  };
-  int64_t tally = 0;
-  size_t j = 0;
-  std::unordered_map<uint32_t, uint32_t> seen;
-  for (uint32_t idx = 0; idx < nsig; idx++) {
-    const uint8_t flag = commit->flags[idx];
-    if (kind == CMTV_VERIFY_COMMIT) {
-      if (flag == kFlagAbsent) continue;
-      if (flag != kFlagCommit && flag != kFlagNil)
-        return fail(CMTV_COMMIT_PANIC_UNKNOWN_FLAG, (int32_t)idx, "Unknown BlockIDFlag: " + std::to_string(flag));
-      if (vals->pk_off[idx + 1] - vals->pk_off[idx] != 32) return bad_pk(idx, idx);
-      if (j >= m || plan_idx[j] != idx || !valid[j]) return wrong_sig(idx);
-      j++;
-      if (flag == kFlagCommit) tally += vals->voting_power[idx];
-    } else {
-      if (flag != kFlagCommit) continue;
-      uint32_t vi = idx;
-      if (kind == CMTV_VERIFY_COMMIT_LIGHT_TRUSTING) {
-        auto it = by_addr.find(std::string(reinterpret_cast<const char*>(commit->val_addrs + 20 * (size_t)idx), 20));
-        if (it == by_addr.end()) continue;
-        vi = it->second;
-        auto sit = seen.find(vi);
-        if (sit != seen.end()) {
-          // Validator.String(): "Validator{%v %v VP:%v A:%v}" (types/validator.go)
-          std::string vs = "Validator{" + hex_upper(vals->addrs + 20 * (size_t)vi, 20) + " PubKeyEd25519{" +
-                           hex_upper(vals->pubkeys + vals->pk_off[vi], vals->pk_off[vi + 1] - vals->pk_off[vi]) +
-                           "} VP:" + std::to_string(vals->voting_power[vi]) + " A:" +
-                           std::to_string(vals->proposer_priority ? vals->proposer_priority[vi] : 0) + "}";
-          return fail(CMTV_COMMIT_ERR_DOUBLE_VOTE, (int32_t)idx,
-                      "double vote from " + vs + " (" + std::to_string(sit->second) + " and " + std::to_string(idx) +
-                          ")");
-        }
-        seen.emplace(vi, idx);
-      }
-      if (vals->pk_off[vi + 1] - vals->pk_off[vi] != 32) return bad_pk(idx, vi);
-      if (j >= m || plan_idx[j] != idx || !valid[j]) return wrong_sig(idx);
-      j++;
-      tally += vals->voting_power[vi];
-      if (tally > needed) return CMTV_OK;
-    }
-  }
-  if (kind == CMTV_VERIFY_COMMIT && tally > needed) return CMTV_OK;
-  res->got = tally;
-  res->needed = needed;
-  char b[160];
-  std::snprintf(b, sizeof b, "invalid commit -- insufficient voting power: got %" PRId64 ", needed more than %" PRId64,
-                tally, needed);
-  return fail(CMTV_COMMIT_ERR_NOT_ENOUGH_POWER, -1, b);
+  std::vector<CommitJob> jobs;
+  jobs.reserve(n);
+  for (size_t c = 0; c < n; c++)
+    jobs.push_back(CommitJob{kind, chain_id, chain_id_len, &vals[c], block_ids ? &block_ids[c] : nullptr, heights[c],
+                             &commits[c], trust_num, trust_den, &results[c], msg_bufs ? msg_bufs + c * msg_cap : nullptr,
+                             msg_bufs ? msg_cap : 0});
+  std::unique_lock<std::mutex> lk;
+  int rc = cmtv::ctx_lock(ctx, lk);
+  if (rc != CMTV_OK) return rc;
+  SigBatch B;
+  const bool prefetch = cmtv::cache_enabled(ctx);
+  for (auto& J : jobs) job_prepare(J, B, prefetch);
+  std::vector<uint8_t> valid;
+  rc = batch_verify(ctx, B, mode, valid);
+  if (rc != CMTV_OK) return rc;
+  for (size_t c = 0; c < n; c++) rcs[c] = job_replay(jobs[c], valid);
+  return CMTV_OK;
 }
 
 }  // extern "C"

@@ -14,6 +14,8 @@
 #include <cstring>
 #include <mutex>
 #include <new>
+#include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/cmtverify.h"
@@ -70,6 +72,74 @@ struct HostBuf {
   }
 };
 
+// Verdict cache (cmtv_verdict_cache): a ring of the last `cap` verdicts,
+// indexed by a 64-bit hash of (mode, signature); a hit also compares the full
+// key bytes (mode, pk, sig, msg), so it returns exactly the device verdict.
+struct VerdictCache {
+  struct Entry {
+    std::string key;
+    uint64_t h = 0;
+    uint8_t verdict = 0;
+    bool used = false;
+  };
+  size_t cap = 0;
+  size_t next = 0;
+  std::vector<Entry> ring;
+  std::unordered_multimap<uint64_t, size_t> index;
+
+  static uint64_t hash(uint32_t mode, const uint8_t* sig) {
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ mode;
+    for (int i = 0; i < 8; i++) {
+      uint64_t w;
+      std::memcpy(&w, sig + 8 * i, 8);
+      h = (h ^ w) * 0xBF58476D1CE4E5B9ull;
+      h ^= h >> 31;
+    }
+    return h;
+  }
+  static void make_key(std::string& k, uint32_t mode, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
+                       size_t mlen) {
+    k.resize(1 + 32 + 64 + mlen);
+    k[0] = (char)(mode == cmtv::kModeSr25519 ? 0x80 : mode);  // scheme + verdict mode
+    std::memcpy(&k[1], pk, 32);
+    std::memcpy(&k[33], sig, 64);
+    if (mlen) std::memcpy(&k[97], msg, mlen);
+  }
+  void reset(size_t c) {
+    cap = c;
+    next = 0;
+    ring.clear();
+    ring.resize(c);
+    index.clear();
+  }
+  // verdict or -1
+  int find(uint64_t h, const std::string& k) const {
+    auto r = index.equal_range(h);
+    for (auto it = r.first; it != r.second; ++it)
+      if (ring[it->second].key == k) return ring[it->second].verdict;
+    return -1;
+  }
+  void insert(uint64_t h, std::string&& k, uint8_t v) {
+    if (!cap) return;
+    Entry& e = ring[next];
+    if (e.used) {
+      auto r = index.equal_range(e.h);
+      for (auto it = r.first; it != r.second; ++it)
+        if (it->second == next) {
+          index.erase(it);
+          break;
+        }
+    }
+    e.key = std::move(k);
+    e.h = h;
+    e.verdict = v;
+    e.used = true;
+    index.emplace(h, next);
+    next = (next + 1) % cap;
+  }
+  size_t size() const { return index.size(); }
+};
+
 }  // namespace
 
 struct cmtv_ctx {
@@ -87,6 +157,7 @@ struct cmtv_ctx {
   uint32_t* d_bcomb = nullptr;        // comb of B for registered-key verification (built lazily)
   uint16_t* d_srprog = nullptr;       // sr25519 transcript program (merlin.h)
   int sr_nops = 0;
+  VerdictCache cache;                 // cmtv_verdict_cache (off by default)
 };
 
 struct cmtv_keyset {
@@ -207,8 +278,65 @@ static int enqueue_verify_keyed(cmtv_ctx* ctx, const cmtv_keyset* ks, size_t n, 
   return CMTV_OK;
 }
 
+static int verify_host_device(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
+                              const uint32_t* msg_off, uint32_t mode, uint8_t* out_valid, uint64_t* out_bitmap);
+
+bool cache_enabled(const cmtv_ctx* ctx) { return ctx->cache.cap != 0; }
+
 int verify_host_locked(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
                        const uint32_t* msg_off, uint32_t mode, uint8_t* out_valid, uint64_t* out_bitmap) {
+  if (n == 0) return CMTV_OK;
+  if (!ctx->cache.cap) return verify_host_device(ctx, n, pk, sig, msg, msg_off, mode, out_valid, out_bitmap);
+  // cache lookups; the misses go to the device as one compacted batch
+  std::vector<uint8_t> valid(n);
+  std::vector<size_t> miss;
+  std::vector<uint64_t> hs(n);
+  std::vector<std::string> keys(n);
+  for (size_t i = 0; i < n; i++) {
+    hs[i] = VerdictCache::hash(mode, sig + 64 * i);
+    VerdictCache::make_key(keys[i], mode, pk + 32 * i, sig + 64 * i, msg + msg_off[i], msg_off[i + 1] - msg_off[i]);
+    const int v = ctx->cache.find(hs[i], keys[i]);
+    if (v < 0)
+      miss.push_back(i);
+    else
+      valid[i] = (uint8_t)v;
+  }
+  ctx->stats.cache_hits += n - miss.size();
+  if (!miss.empty()) {
+    const size_t m = miss.size();
+    std::vector<uint8_t> mpk(32 * m), msg_(64 * m), mmsg, mv(m);
+    std::vector<uint32_t> moff(m + 1, 0);
+    for (size_t j = 0; j < m; j++) {
+      const size_t i = miss[j];
+      std::memcpy(&mpk[32 * j], pk + 32 * i, 32);
+      std::memcpy(&msg_[64 * j], sig + 64 * i, 64);
+      mmsg.insert(mmsg.end(), msg + msg_off[i], msg + msg_off[i + 1]);
+      moff[j + 1] = (uint32_t)mmsg.size();
+    }
+    if (mmsg.empty()) mmsg.push_back(0);
+    const int rc = verify_host_device(ctx, m, mpk.data(), msg_.data(), mmsg.data(), moff.data(), mode, mv.data(),
+                                      nullptr);
+    if (rc != CMTV_OK) return rc;
+    for (size_t j = 0; j < m; j++) {
+      const size_t i = miss[j];
+      valid[i] = mv[j];
+      ctx->cache.insert(hs[i], std::move(keys[i]), mv[j]);
+    }
+  }
+  if (out_valid) std::memcpy(out_valid, valid.data(), n);
+  if (out_bitmap) {
+    const size_t words = (n + 63) / 64;
+    for (size_t w = 0; w < words; w++) {
+      uint64_t x = 0;
+      for (size_t b = 0; b < 64 && 64 * w + b < n; b++) x |= (uint64_t)(valid[64 * w + b] & 1) << b;
+      out_bitmap[w] = x;
+    }
+  }
+  return CMTV_OK;
+}
+
+static int verify_host_device(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
+                              const uint32_t* msg_off, uint32_t mode, uint8_t* out_valid, uint64_t* out_bitmap) {
   if (n == 0) return CMTV_OK;
   const size_t msg_bytes = msg_off[n];
   // staging layout: [pk n*32][sig n*64][off (n+1)*4][msg msg_bytes + 16]
@@ -339,7 +467,15 @@ int cmtv_stats_get(cmtv_ctx* ctx, cmtv_stats* out) {
   std::lock_guard<std::mutex> g(ctx->mu);
   (void)hipSetDevice(ctx->device);
   harvest_timing(ctx);
+  ctx->stats.cache_entries = ctx->cache.size();
   *out = ctx->stats;
+  return CMTV_OK;
+}
+
+int cmtv_verdict_cache(cmtv_ctx* ctx, size_t max_entries) {
+  if (!ctx || max_entries > (1u << 26)) return CMTV_EINVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  ctx->cache.reset(max_entries);
   return CMTV_OK;
 }
 

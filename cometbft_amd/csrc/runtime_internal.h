@@ -16,7 +16,11 @@ uint32_t ctx_default_mode(const cmtv_ctx* ctx);
 // enqueue paths (the ABI's mode argument is Ed25519-only).
 constexpr uint32_t kModeSr25519 = 0x100;
 
-// Host buffers in, verdicts out; caller holds the context lock.
+// Whether cmtv_verdict_cache is on (commit.cpp then prefetches light calls).
+bool cache_enabled(const cmtv_ctx* ctx);
+
+// Host buffers in, verdicts out (through the verdict cache when enabled);
+// caller holds the context lock.
 int verify_host_locked(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
                        const uint32_t* msg_off, uint32_t mode, uint8_t* out_valid, uint64_t* out_bitmap);
 

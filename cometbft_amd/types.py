@@ -258,24 +258,75 @@ def _verify(vals: ValidatorSet, kind, chain_id, block_id, height, commit, num, d
     rc = N.lib().cmtv_verify_commit(ctx.handle, kind, mode, cid, len(cid), ctypes.byref(vs), bidp, height,
                                     ctypes.byref(cm), num, den, ctypes.byref(res), buf, len(buf))
     N.check(rc, "cmtv_verify_commit")
+    err = _error_for(rc, res, buf.value.decode())
+    if err is not None:
+        raise err
+    return None
+
+
+def _error_for(rc, res, msg):
+    """The exception the reference's VerifyCommit* would produce (None = nil)."""
     if rc == N.CMTV_OK:
         return None
-    msg = buf.value.decode()
     code = res.code
     if code == N.COMMIT_ERR_SET_SIZE:
-        raise ErrInvalidCommitSignatures(msg)
+        return ErrInvalidCommitSignatures(msg)
     if code == N.COMMIT_ERR_HEIGHT:
-        raise ErrInvalidCommitHeight(msg)
+        return ErrInvalidCommitHeight(msg)
     if code == N.COMMIT_ERR_BLOCK_ID:
-        raise ErrWrongBlockID(msg)
+        return ErrWrongBlockID(msg)
     if code == N.COMMIT_ERR_WRONG_SIGNATURE:
-        raise ErrWrongSignature(msg, res.sig_index)
+        return ErrWrongSignature(msg, res.sig_index)
     if code == N.COMMIT_ERR_NOT_ENOUGH_POWER:
-        raise ErrNotEnoughVotingPowerSigned(msg, res.got, res.needed)
+        return ErrNotEnoughVotingPowerSigned(msg, res.got, res.needed)
     if code == N.COMMIT_ERR_DOUBLE_VOTE:
-        raise ErrDoubleVote(msg)
+        return ErrDoubleVote(msg)
     if code == N.COMMIT_ERR_TRUST_LEVEL:
-        raise ErrTrustLevel(msg)
+        return ErrTrustLevel(msg)
     if code in (N.COMMIT_PANIC_BAD_PUBKEY, N.COMMIT_PANIC_UNKNOWN_FLAG):
-        raise ReferencePanic(msg)
-    raise CommitError(msg)
+        return ReferencePanic(msg)
+    return CommitError(msg)
+
+
+def verify_commits(kind: int, chain_id: str, items, ctx: Context | None = None, mode: int = MODE_GO_STDLIB,
+                   trust_level=(1, 3)):
+    """Cross-height batching (cmtv_verify_commits): items is a sequence of
+    (ValidatorSet, BlockID | None, height, Commit). All their signatures go to
+    the device in ONE batch; returns, per item, None (the reference's nil) or
+    the exception its VerifyCommit* would have returned -- not raised, so one
+    bad height does not hide the others."""
+    ctx = ctx or default_context()
+    n = len(items)
+    if n == 0:
+        return []
+    keep = []
+    vs_arr = (N.cmtv_valset * n)()
+    cm_arr = (N.cmtv_commit * n)()
+    bid_arr = (N.cmtv_block_id * n)()
+    heights = (ctypes.c_int64 * n)()
+    for c, (vals, block_id, height, commit) in enumerate(items):
+        vs, kv = vals._pack()
+        cm, kc = _pack_commit(commit)
+        vs_arr[c], cm_arr[c] = vs, cm
+        keep += [kv, kc]
+        if block_id is not None:
+            bid, kb = block_id._c()
+            bid_arr[c] = bid
+            keep.append(kb)
+        heights[c] = height
+    res = (N.cmtv_commit_result * n)()
+    rcs = (ctypes.c_int * n)()
+    cap = 1024
+    bufs = ctypes.create_string_buffer(n * cap)
+    cid = chain_id.encode()
+    num, den = trust_level if kind == N.VERIFY_COMMIT_LIGHT_TRUSTING else (0, 0)
+    rc = N.lib().cmtv_verify_commits(ctx.handle, kind, mode, cid, len(cid), n, vs_arr,
+                                     bid_arr if kind != N.VERIFY_COMMIT_LIGHT_TRUSTING else None, heights, cm_arr,
+                                     num, den, res, rcs, bufs, cap)
+    N.check(rc, "cmtv_verify_commits")
+    raw = bufs.raw
+    out = []
+    for c in range(n):
+        msg = raw[c * cap: (c + 1) * cap].split(b"\0", 1)[0].decode()
+        out.append(_error_for(rcs[c], res[c], msg))
+    return out

@@ -73,6 +73,8 @@ typedef struct cmtv_stats {
   uint64_t kernel_launches;
   double device_ms;        /* summed kernel time (HIP events)     */
   double last_kernel_ms;   /* the most recent verify kernel       */
+  uint64_t cache_hits;     /* verdicts served by the verdict cache */
+  uint64_t cache_entries;  /* verdicts currently cached           */
 } cmtv_stats;
 
 /* ------------------------------------------------------------ lifecycle */
@@ -106,6 +108,23 @@ int cmtv_verify_ed25519(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_
  * (n bytes) and d_bitmap (ceil(n/64) words) may each be NULL. */
 int cmtv_verify_ed25519_device(cmtv_ctx* ctx, size_t n, const void* d_pk, const void* d_sig, const void* d_msg,
                                const void* d_msg_off, uint32_t mode, void* d_valid, void* d_bitmap, void* stream);
+
+/* ------------------------------------------------------------ verdict cache */
+
+/* Blocksync verifies each commit three times with the same (key, sign-bytes,
+ * signature) triples: VerifyCommitLight in the reactor, then VerifyCommit
+ * twice (blockchain/v0/reactor.go:366-400 -> state/validation.go:93,
+ * state/execution.go:135). cmtv_verdict_cache(ctx, max_entries) keeps the
+ * verdicts of the last max_entries verifications of the context (0 disables
+ * and clears). Entries are matched on the full (mode, key, signature,
+ * message) bytes, so a hit returns exactly the verdict the device would
+ * compute. With the cache on, cmtv_verify_commit / cmtv_verify_commits also
+ * verify a light call's remaining non-absent signatures in the same device
+ * batch (their verdicts only fill the cache; the replay never reads them),
+ * so the two full VerifyCommit calls that follow need no device work.
+ * Applies to the host-buffer entry points (cmtv_verify_ed25519, batch,
+ * commit). */
+int cmtv_verdict_cache(cmtv_ctx* ctx, size_t max_entries);
 
 /* ------------------------------------------------------------ sr25519 */
 
@@ -255,6 +274,20 @@ int cmtv_verify_commit(cmtv_ctx* ctx, uint32_t kind, uint32_t mode, const char* 
                        const cmtv_valset* vals, const cmtv_block_id* block_id, int64_t height,
                        const cmtv_commit* commit, uint64_t trust_num, uint64_t trust_den, cmtv_commit_result* res,
                        char* msg_buf, size_t msg_cap);
+
+/* Cross-height batching (blocksync / light-client replay):
+ * n commits, each with its own validator set, block ID and height, verified
+ * with ONE device batch for all their signatures, then each commit's
+ * reference loop replayed over its verdicts. Per commit i the outcome equals
+ * cmtv_verify_commit(ctx, kind, mode, chain_id, vals[i], block_ids[i] (unused
+ * for LIGHT_TRUSTING), heights[i], commits[i], ...): rcs[i] gets its return
+ * code (CMTV_OK / CMTV_ECOMMIT), results[i] its details and msg_bufs +
+ * i * msg_cap (may be NULL) its error string. Returns CMTV_OK when every
+ * commit was evaluated, a negative library code otherwise. */
+int cmtv_verify_commits(cmtv_ctx* ctx, uint32_t kind, uint32_t mode, const char* chain_id, size_t chain_id_len,
+                        size_t n, const cmtv_valset* vals, const cmtv_block_id* block_ids, const int64_t* heights,
+                        const cmtv_commit* commits, uint64_t trust_num, uint64_t trust_den,
+                        cmtv_commit_result* results, int* rcs, char* msg_bufs, size_t msg_cap);
 
 /* CanonicalVote sign-bytes (types/vote.go:93 VoteSignBytes) for a commit
  * signature: writes up to cap bytes, returns the length (or negative code). */

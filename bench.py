@@ -21,6 +21,9 @@ Extra fields on the JSON line:
   latency_150    -- p50/p99 of cmtv_verify_commit (VerifyCommit, 150 validators:
                     sign-bytes + H2D + kernel + D2H + reference-loop replay),
                     beside the oracle's single-core sequential VerifyCommit time
+  replay_150     -- blocksync replay per height (light + 2 x full VerifyCommit of
+                    a 150-validator commit): plain, with the verdict cache, and
+                    with cross-height batching (N=1 only)
   sr25519        -- configs[4]: 10k sr25519 verifications per step (N=1 only),
                     with the C restatement on the host cores as its CPU baseline
 Run: python bench.py [--gpus N --steps K --warmup W]
@@ -151,6 +154,49 @@ def sr25519_line(ctx, dev, n, steps, cpu_seconds, with_cpu):
                                          f"(C restatement of go-schnorrkel verify)", "seconds": round(dt, 2)}
         res["cpu_baseline"]["gpu_over_cpu"] = round(res["value"] / res["cpu_baseline"]["value"], 1)
     return res
+
+
+def replay_line(dev_index, heights=60, n_vals=150):
+    """SURVEY 8f ranks 2-3 on the blocksync pattern: per height
+    VerifyCommitLight + VerifyCommit + VerifyCommit of one 150-validator
+    commit (blockchain/v0/reactor.go:366-400), end to end through the host API
+    (sign-bytes, H2D, kernel, D2H, replay), plain vs with the verdict cache;
+    and cross-height batching (cmtv_verify_commits) of the same commits."""
+    from cometbft_amd import Context
+    from cometbft_amd import testutil as TU
+    from cometbft_amd import types as T
+
+    plain = Context(device=dev_index)
+    cached = Context(device=dev_index)
+    cached.verdict_cache(1 << 20)
+    sv = TU.make_validator_set(plain, n_vals)
+    chain = []
+    for h in range(2000, 2000 + heights):
+        commit, _, _ = TU.make_commit(plain, sv, h)
+        chain.append((sv.valset, TU.block_id_for_height(h), h, commit))
+
+    def blocksync(ctx):
+        for vals, bid, h, c in chain:
+            vals.verify_commit_light(TU.CHAIN_ID, bid, h, c, ctx=ctx)
+            vals.verify_commit(TU.CHAIN_ID, bid, h, c, ctx=ctx)
+            vals.verify_commit(TU.CHAIN_ID, bid, h, c, ctx=ctx)
+
+    blocksync(plain)  # warm-up
+    t = time.perf_counter()
+    blocksync(plain)
+    t_plain = (time.perf_counter() - t) / heights
+    t = time.perf_counter()
+    blocksync(cached)  # cold cache: one device call per height
+    t_cached = (time.perf_counter() - t) / heights
+    T.verify_commits(0, TU.CHAIN_ID, chain, ctx=plain)
+    t = time.perf_counter()
+    errs = T.verify_commits(0, TU.CHAIN_ID, chain, ctx=plain)
+    t_batch = (time.perf_counter() - t) / heights
+    assert all(e is None for e in errs)
+    return {"workload": f"{heights} heights x {n_vals}-validator commits, blocksync pattern (light + 2 x full)",
+            "ms_per_height_plain": round(t_plain * 1e3, 4), "ms_per_height_verdict_cache": round(t_cached * 1e3, 4),
+            "ms_per_height_cross_height_batch": round(t_batch * 1e3, 4),
+            "note": "host API end to end; cross-height = one cmtv_verify_commits (VerifyCommit) over all heights"}
 
 
 def _cpu_model():
@@ -322,6 +368,8 @@ def main():
             line["cpu_baseline"]["gpu_over_cpu"] = round(value / world / line["cpu_baseline"]["value"], 1)
         if not args.no_latency:
             line["latency_150"] = latency_150(ctx, mode, args.latency_iters)
+        if not args.no_latency and world == 1:
+            line["replay_150"] = replay_line(local)
         if not args.no_sr25519 and world == 1:
             line["sr25519"] = sr25519_line(ctx, dev, 10_000, 20, args.cpu_seconds / 4, not args.no_cpu_baseline)
         print(json.dumps(line), flush=True)

@@ -7,7 +7,10 @@
 // loop is then replayed in index order over the verdicts, so the returned
 // error (first bad signature, early exits, tallies, panics) is exactly the
 // reference's. Error strings are produced with the reference's formats.
+#include <hip/hip_runtime.h>
+
 #include <cinttypes>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <new>
@@ -17,6 +20,7 @@
 
 #include "../../include/cmtverify.h"
 #include "runtime_internal.h"
+#include "signbytes.h"
 
 namespace {
 
@@ -132,12 +136,60 @@ constexpr int32_t kPrecommit = 2;
 
 // ------------------------------------------------------------------ VerifyCommit*
 
-// Signatures of one or more commits, gathered for one device batch.
+// The CanonicalVote fields before the timestamp (type, height, round,
+// BlockID unless nil): the per-commit part of a signature's sign-bytes.
+void vote_prefix(std::string& body, int32_t vtype, int64_t height, int32_t round, const cmtv_block_id* bid) {
+  body.clear();
+  if (vtype != 0) {
+    body.push_back(0x08);
+    put_uvarint(body, (uint64_t)(int64_t)vtype);
+  }
+  if (height != 0) put_sfixed64(body, 0x11, height);
+  if (round != 0) put_sfixed64(body, 0x19, (int64_t)round);
+  put_canonical_block_id(body, bid);
+}
+
+// Signatures of one or more commits, gathered for one device batch. Host
+// mode: sign-bytes encoded here (needed for the verdict cache's keys).
+// Templated mode: one SbTemplate per commit and
+// (flag, seconds, nanos) per signature; the device writes the sign-bytes.
 struct SigBatch {
+  bool templated = false;
   std::vector<uint8_t> pk, sg, msgs, len_ok;
   std::vector<uint32_t> off{0};
   std::string sb;
+  // templated
+  std::vector<cmtv::SbTemplate> tmpls;
+  std::vector<uint8_t> blob, tflag;
+  std::vector<uint32_t> tidx;
+  std::vector<int64_t> tsec;
+  std::vector<int32_t> tnanos;
+  const cmtv_commit* cur = nullptr;  // commit of the last template
+
   size_t size() const { return off.size() - 1; }
+
+  void ensure_template(const char* chain_id, size_t chain_id_len, const cmtv_commit* c) {
+    if (cur == c && !tmpls.empty()) return;
+    static const cmtv_block_id empty{};
+    cmtv::SbTemplate t{};
+    std::string part;
+    vote_prefix(part, kPrecommit, c->height, c->round, &c->block_id);
+    t.pre_commit_off = (uint32_t)blob.size();
+    t.pre_commit_len = (uint32_t)part.size();
+    blob.insert(blob.end(), part.begin(), part.end());
+    vote_prefix(part, kPrecommit, c->height, c->round, &empty);
+    t.pre_nil_off = (uint32_t)blob.size();
+    t.pre_nil_len = (uint32_t)part.size();
+    blob.insert(blob.end(), part.begin(), part.end());
+    part.clear();
+    if (chain_id_len) put_bytes_field(part, 0x32, reinterpret_cast<const uint8_t*>(chain_id), chain_id_len);
+    t.post_off = (uint32_t)blob.size();
+    t.post_len = (uint32_t)part.size();
+    blob.insert(blob.end(), part.begin(), part.end());
+    tmpls.push_back(t);
+    cur = c;
+  }
+
   // key (32 bytes), the CommitSig's signature and the vote's sign-bytes
   void add(const uint8_t* key, const uint8_t* sig, uint32_t sig_len, const char* chain_id, size_t chain_id_len,
            const cmtv_commit* c, uint32_t idx) {
@@ -148,9 +200,18 @@ struct SigBatch {
     if (sig_len == 64) std::memcpy(&sg[o], sig, 64);
     len_ok.push_back(sig_len == 64);
     // Commit.GetVote(idx) (types/block.go:784): CommitSig.BlockID(commit.BlockID)
-    const cmtv_block_id* vb = c->flags[idx] == kFlagCommit ? &c->block_id : &empty;
-    vote_sign_bytes(sb, chain_id, chain_id_len, kPrecommit, c->height, c->round, vb, c->ts_seconds[idx],
-                    c->ts_nanos[idx]);
+    const bool for_block = c->flags[idx] == kFlagCommit;
+    if (templated) {
+      ensure_template(chain_id, chain_id_len, c);
+      tidx.push_back((uint32_t)tmpls.size() - 1);
+      tflag.push_back(for_block ? 1 : 0);
+      tsec.push_back(c->ts_seconds[idx]);
+      tnanos.push_back(c->ts_nanos[idx]);
+      off.push_back(off.back() + cmtv::sb_msg_len(tmpls.back(), for_block, c->ts_seconds[idx], c->ts_nanos[idx]));
+      return;
+    }
+    vote_sign_bytes(sb, chain_id, chain_id_len, kPrecommit, c->height, c->round, for_block ? &c->block_id : &empty,
+                    c->ts_seconds[idx], c->ts_nanos[idx]);
     msgs.insert(msgs.end(), sb.begin(), sb.end());
     off.push_back((uint32_t)msgs.size());
   }
@@ -184,6 +245,15 @@ struct CommitJob {
     return CMTV_ECOMMIT;
   }
 };
+
+// CMTV_HOST_SIGNBYTES=1 forces host-side encoding (A/B measurement, tests)
+bool templated_enabled() {
+  static const bool on = [] {
+    const char* v = std::getenv("CMTV_HOST_SIGNBYTES");
+    return !(v && v[0] == '1');
+  }();
+  return on;
+}
 
 int job_check_args(uint32_t kind, const char* chain_id, size_t chain_id_len, const cmtv_valset* vals,
                    const cmtv_block_id* block_id, const cmtv_commit* commit, cmtv_commit_result* res) {
@@ -304,9 +374,16 @@ int batch_verify(cmtv_ctx* ctx, SigBatch& B, uint32_t mode, std::vector<uint8_t>
   const size_t m = B.size();
   valid.assign(m, 0);
   if (!m) return CMTV_OK;
-  if (B.msgs.empty()) B.msgs.push_back(0);
-  const int rc = cmtv::verify_host_locked(ctx, m, B.pk.data(), B.sg.data(), B.msgs.data(), B.off.data(), mode,
-                                          valid.data(), nullptr);
+  int rc;
+  if (B.templated) {
+    rc = cmtv::verify_templated_locked(ctx, m, B.pk.data(), B.sg.data(), B.off.data(), B.tmpls.data(), B.tmpls.size(),
+                                       B.blob.data(), B.blob.size(), B.tidx.data(), B.tflag.data(), B.tsec.data(),
+                                       B.tnanos.data(), mode, valid.data());
+  } else {
+    if (B.msgs.empty()) B.msgs.push_back(0);
+    rc = cmtv::verify_host_locked(ctx, m, B.pk.data(), B.sg.data(), B.msgs.data(), B.off.data(), mode, valid.data(),
+                                  nullptr);
+  }
   if (rc != CMTV_OK) return rc;
   for (size_t j = 0; j < m; j++)
     if (!B.len_ok[j]) valid[j] = 0;  // crypto/ed25519/ed25519.go:150
@@ -485,7 +562,9 @@ int cmtv_verify_commit(cmtv_ctx* ctx, uint32_t kind, uint32_t mode, const char* 
   rc = cmtv::ctx_lock(ctx, lk);
   if (rc != CMTV_OK) return rc;
   SigBatch B;
-  job_prepare(J, B, cmtv::cache_enabled(ctx));
+  const bool cache = cmtv::cache_enabled(ctx);
+  B.templated = !cache && templated_enabled();
+  job_prepare(J, B, cache);
   std::vector<uint8_t> valid;
   rc = batch_verify(ctx, B, mode, valid);
   if (rc != CMTV_OK) return rc;
@@ -517,6 +596,7 @@ int cmtv_verify_commits(cmtv_ctx* ctx, uint32_t kind, uint32_t mode, const char*
   if (rc != CMTV_OK) return rc;
   SigBatch B;
   const bool prefetch = cmtv::cache_enabled(ctx);
+  B.templated = !prefetch && templated_enabled();
   for (auto& J : jobs) job_prepare(J, B, prefetch);
   std::vector<uint8_t> valid;
   rc = batch_verify(ctx, B, mode, valid);

@@ -21,6 +21,7 @@
 #include "../../include/cmtverify.h"
 #include "kernels.h"
 #include "merlin.h"
+#include "signbytes.h"
 #include "runtime_internal.h"
 
 namespace {
@@ -371,6 +372,59 @@ static int verify_host_device(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const 
   ctx->stats.invalid += invalid;
   if (out_valid) std::memcpy(out_valid, hv, n);
   if (out_bitmap) std::memcpy(out_bitmap, hout + o_bm, 8 * words);
+  return CMTV_OK;
+}
+
+int verify_templated_locked(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_t* sig, const uint32_t* msg_off,
+                            const void* tmpls, size_t n_tmpls, const uint8_t* blob, size_t blob_len,
+                            const uint32_t* tidx, const uint8_t* commit_flag, const int64_t* sec,
+                            const int32_t* nanos, uint32_t mode, uint8_t* out_valid) {
+  if (n == 0) return CMTV_OK;
+  const size_t msg_bytes = msg_off[n];
+  const size_t tb = n_tmpls * sizeof(SbTemplate);
+  // staging: [pk][sig][off][tidx][flag][sec][nanos][templates][blob] | device only: [msg]
+  const size_t o_pk = 0, o_sig = align_up(32 * n, 256), o_off = align_up(o_sig + 64 * n, 256);
+  const size_t o_tidx = align_up(o_off + 4 * (n + 1), 256), o_flag = align_up(o_tidx + 4 * n, 256);
+  const size_t o_sec = align_up(o_flag + n, 256), o_nanos = align_up(o_sec + 8 * n, 256);
+  const size_t o_tmpl = align_up(o_nanos + 4 * n, 256), o_blob = align_up(o_tmpl + tb, 256);
+  const size_t in_bytes = align_up(o_blob + blob_len + 16, 256);
+  const size_t o_msg = in_bytes, dev_bytes = align_up(o_msg + msg_bytes + 16, 256);
+  const size_t o_valid = 0, out_bytes = align_up(n, 256);
+  hipError_t e;
+  if ((e = ctx->h_in.ensure(in_bytes)) != hipSuccess) return hip_fail(e);
+  if ((e = ctx->d_in.ensure(dev_bytes)) != hipSuccess) return hip_fail(e);
+  if ((e = ctx->h_out.ensure(out_bytes)) != hipSuccess) return hip_fail(e);
+  if ((e = ctx->d_out.ensure(out_bytes)) != hipSuccess) return hip_fail(e);
+  auto* hin = static_cast<uint8_t*>(ctx->h_in.p);
+  std::memcpy(hin + o_pk, pk, 32 * n);
+  std::memcpy(hin + o_sig, sig, 64 * n);
+  std::memcpy(hin + o_off, msg_off, 4 * (n + 1));
+  std::memcpy(hin + o_tidx, tidx, 4 * n);
+  std::memcpy(hin + o_flag, commit_flag, n);
+  std::memcpy(hin + o_sec, sec, 8 * n);
+  std::memcpy(hin + o_nanos, nanos, 4 * n);
+  std::memcpy(hin + o_tmpl, tmpls, tb);
+  if (blob_len) std::memcpy(hin + o_blob, blob, blob_len);
+  auto* din = static_cast<uint8_t*>(ctx->d_in.p);
+  auto* dout = static_cast<uint8_t*>(ctx->d_out.p);
+  if ((e = hipMemcpyAsync(din, hin, in_bytes, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess) return hip_fail(e);
+  if ((e = hipMemsetAsync(din + o_msg + msg_bytes, 0, 16, ctx->stream)) != hipSuccess) return hip_fail(e);
+  if ((e = launch_sign_bytes((uint32_t)n, din + o_tmpl, din + o_blob, reinterpret_cast<uint32_t*>(din + o_tidx),
+                             din + o_flag, reinterpret_cast<int64_t*>(din + o_sec),
+                             reinterpret_cast<int32_t*>(din + o_nanos), reinterpret_cast<uint32_t*>(din + o_off),
+                             din + o_msg, ctx->stream)) != hipSuccess)
+    return hip_fail(e);
+  int rc = enqueue_verify(ctx, n, din + o_pk, din + o_sig, din + o_msg, reinterpret_cast<uint32_t*>(din + o_off), mode,
+                          dout + o_valid, nullptr, ctx->stream);
+  if (rc != CMTV_OK) return rc;
+  auto* hout = static_cast<uint8_t*>(ctx->h_out.p);
+  if ((e = hipMemcpyAsync(hout, dout, out_bytes, hipMemcpyDeviceToHost, ctx->stream)) != hipSuccess) return hip_fail(e);
+  if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return hip_fail(e);
+  harvest_timing(ctx);
+  uint64_t invalid = 0;
+  for (size_t i = 0; i < n; i++) invalid += hout[o_valid + i] == 0;
+  ctx->stats.invalid += invalid;
+  std::memcpy(out_valid, hout + o_valid, n);
   return CMTV_OK;
 }
 

@@ -24,4 +24,13 @@ bool cache_enabled(const cmtv_ctx* ctx);
 int verify_host_locked(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
                        const uint32_t* msg_off, uint32_t mode, uint8_t* out_valid, uint64_t* out_bitmap);
 
+// Commit signatures whose sign-bytes are written on the device from per-commit
+// templates (signbytes.h): tmpls is an array of n_tmpls SbTemplate over
+// `blob`; msg_off must hold the message offsets from sb_msg_len. Verdicts only
+// (no cache). Caller holds the context lock.
+int verify_templated_locked(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_t* sig, const uint32_t* msg_off,
+                            const void* tmpls, size_t n_tmpls, const uint8_t* blob, size_t blob_len,
+                            const uint32_t* tidx, const uint8_t* commit_flag, const int64_t* sec,
+                            const int32_t* nanos, uint32_t mode, uint8_t* out_valid);
+
 }  // namespace cmtv

@@ -232,3 +232,39 @@ def test_large_commit_first_error_in_index_order(gpu_ctx):
         commit.signatures[bad].signature = bytes(s)
     e = _err(lambda: sv.valset.verify_commit(TU.CHAIN_ID, bid, 77, commit, ctx=gpu_ctx))
     assert isinstance(e, T.ErrWrongSignature) and e.index == 250
+
+
+@pytest.mark.parametrize("chain", ["", "c", "x" * 50])
+def test_device_sign_bytes_templating(gpu_ctx, chain):
+    """with the verdict cache off, cmtv_verify_commit ships
+    one CanonicalVote template per commit and (flag, seconds, nanos) per
+    signature, and k_sign_bytes writes the sign-bytes on the device. The
+    signatures here are made by the oracle over the oracle encoder's bytes
+    (pinned by types/vote_test.go's KATs), so any byte the device writes
+    differently fails verification. Timestamps cover zero, negative, one- to
+    ten-byte varints and the Go zero time; rounds, heights and nil votes vary."""
+    from cometbft_amd import Context
+
+    secs = [0, 1, 127, 128, 2**40, -1, -62135596800, 1_700_000_000]
+    nanos = [0, 1, 127, 128, 999_999_999, 5]
+    vals, vset = _valset(len(secs) * 2, 10)
+    for height, round_ in [(1, 0), (2**40 + 3, 1), (5, 2**31 - 1)]:
+        bid = _bid(b"t%d" % height)
+        sigs = []
+        for i, v in enumerate(vals):
+            ts = (secs[i % len(secs)], nanos[(i * 5) % len(nanos)])
+            flag = T.BLOCK_ID_FLAG_NIL if i % 4 == 3 else T.BLOCK_ID_FLAG_COMMIT
+            sigs.append(v.sign_vote(chain, height, round_, bid, ts, flag))
+        commit = T.Commit(height, round_, bid, sigs)
+        assert _err(lambda: vset.verify_commit(chain, bid, height, commit, ctx=gpu_ctx)) is None
+        assert _err(lambda: vset.verify_commit_light(chain, bid, height, commit, ctx=gpu_ctx)) is None
+        # the host-encoding path (taken when the verdict cache is on) agrees
+        cached = Context(device=0)
+        cached.verdict_cache(64)
+        assert _err(lambda: vset.verify_commit(chain, bid, height, commit, ctx=cached)) is None
+        # and a flipped timestamp nanosecond is caught by the device bytes
+        bad = T.Commit(height, round_, bid, [T.CommitSig(s.block_id_flag, s.validator_address,
+                                                         (s.timestamp[0], s.timestamp[1] ^ 1), s.signature)
+                                             if j == 5 else s for j, s in enumerate(sigs)])
+        e = _err(lambda: vset.verify_commit(chain, bid, height, bad, ctx=gpu_ctx))
+        assert isinstance(e, T.ErrWrongSignature) and e.index == 5

@@ -10,6 +10,11 @@
 
 namespace cmtv {
 
+// wave-uniform predicate (verify_one_half's loop bound)
+struct DevWave {
+  __device__ __forceinline__ bool any(bool x) const { return __ballot(x) != 0; }
+};
+
 struct DevBTab {
   const uint32_t* __restrict__ rows;
   // one niels coordinate (10 words at a 16-byte aligned offset): 2 x dwordx4 + dwordx2

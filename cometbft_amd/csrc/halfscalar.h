@@ -421,4 +421,57 @@ CMTV_HD void hs_bscalar(uint32_t u[8], const uint32_t k2mag[8], bool neg, const 
   for (int i = 0; i < 8; i++) u[i] = flip ? d[i] : u[i];
 }
 
+// Signed radix-16 digit stream of x (|digits| <= 8) read from the top with
+// sc_shift_out(t, 4): wide -> 64 windows, else HS_WINDOWS = 34 windows
+// (x < 2^134), left-aligned so the first shift_out yields the top digit.
+CMTV_HD void hs_digits16(uint32_t t[8], const uint32_t x[8], bool wide) {
+  uint32_t a[8], b[8];
+  sc_bias(a, x, 0x88888888u);
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t bias = i < 4 ? 0x88888888u : (i == 4 ? 0x88u : 0u);
+    const uint64_t v = (uint64_t)x[i] + bias + c;
+    b[i] = (uint32_t)v;
+    c = v >> 32;
+  }
+  // b < 2^136: shift left by 120 bits (3 words + 24 bits)
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t hi = i >= 3 ? b[i - 3] : 0u;
+    const uint32_t lo = i >= 4 ? b[i - 4] : 0u;
+    const uint32_t sh = (hi << 24) | (lo >> 8);
+    t[i] = wide ? a[i] : sh;
+  }
+}
+
+// Signed radix-256 digit streams of u < L split at 2^128, each read from the
+// top with sc_shift_out(t, 8): tLo yields digits 16..0 of u mod 2^128
+// (17 digits), tHi digits 15..0 of u >> 128 (< 2^125, 16 digits).
+CMTV_HD void hs_digits256(uint32_t tLo[8], uint32_t tHi[8], const uint32_t u[8]) {
+  uint32_t lo[5];
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 5; i++) {
+    const uint64_t v = (uint64_t)(i < 4 ? u[i] : 0u) + (i < 4 ? 0x80808080u : 0x80u) + c;
+    lo[i] = (uint32_t)v;
+    c = v >> 32;
+  }
+  // lo < 2^136: shift left by 120 bits
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t hi = (i >= 3 && i - 3 < 5) ? lo[i - 3] : 0u;
+    const uint32_t lw = (i >= 4 && i - 4 < 5) ? lo[i - 4] : 0u;
+    tLo[i] = (hi << 24) | (lw >> 8);
+  }
+  c = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint64_t v = (uint64_t)u[4 + i] + 0x80808080u + c;
+    tHi[4 + i] = (uint32_t)v;
+    tHi[i] = 0;
+    c = v >> 32;
+  }
+}
+
 }  // namespace cmtv

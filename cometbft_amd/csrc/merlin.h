@@ -31,19 +31,17 @@
 namespace cmtv {
 
 constexpr int STROBE_R = 166;
-enum : uint32_t { SF_I = 1, SF_A = 2, SF_C = 4, SF_T = 8, SF_M = 16, SF_K = 32 };
+constexpr uint32_t SF_I = 1, SF_A = 2, SF_C = 4, SF_T = 8, SF_M = 16, SF_K = 32;
 
 // program opcodes (16-bit)
-enum : uint32_t {
-  SOP_LIT = 0x000,    // absorb literal byte (low 8 bits)
-  SOP_BEGIN = 0x100,  // STROBE begin_op(flags = low 8 bits), not "more"
-  SOP_MLEN = 0x200,   // absorb byte (low bits) of LE32(mlen)
-  SOP_MSG = 0x300,    // absorb the whole message
-  SOP_PK = 0x400,     // absorb the 32 key bytes
-  SOP_R = 0x500,      // absorb the 32 R bytes
-  SOP_INIT = 0x600,   // STROBE-128 initial state + F
-  SOP_PRF64 = 0x700,  // begin_op(I|A|C) (+ forced F): 64 output bytes = state[0..63]
-};
+constexpr uint32_t SOP_LIT = 0x000;    // absorb literal byte (low 8 bits)
+constexpr uint32_t SOP_BEGIN = 0x100;  // STROBE begin_op(flags = low 8 bits), not "more"
+constexpr uint32_t SOP_MLEN = 0x200;   // absorb byte (low bits) of LE32(mlen)
+constexpr uint32_t SOP_MSG = 0x300;    // absorb the whole message
+constexpr uint32_t SOP_PK = 0x400;     // absorb the 32 key bytes
+constexpr uint32_t SOP_R = 0x500;      // absorb the 32 R bytes
+constexpr uint32_t SOP_INIT = 0x600;   // STROBE-128 initial state + F
+constexpr uint32_t SOP_PRF64 = 0x700;  // begin_op(I|A|C) (+ forced F): 64 output bytes = state[0..63]
 constexpr int SR_PROGRAM_MAX = 160;
 
 // Host: append a STROBE/merlin operation sequence to the program.

@@ -159,6 +159,7 @@ struct cmtv_ctx {
   uint16_t* d_srprog = nullptr;       // sr25519 transcript program (merlin.h)
   int sr_nops = 0;
   VerdictCache cache;                 // cmtv_verdict_cache (off by default)
+  size_t lane_chunk = kChunk;         // signatures per lane-kernel launch (env CMTV_LANE_CHUNK)
 };
 
 struct cmtv_keyset {
@@ -201,15 +202,16 @@ static int enqueue_verify(cmtv_ctx* ctx, size_t n, const uint8_t* d_pk, const ui
   const bool quad = n <= ctx->quad_max;
   hipError_t e = hipSuccess;
   if (!quad) {
-    const size_t lanes = std::min<size_t>(n, kChunk);
+    const size_t lanes = std::min<size_t>(n, ctx->lane_chunk);
     const size_t lanes_padded = (lanes + 63) / 64 * 64;
     e = ctx->d_atab.ensure(lanes_padded * kAtabWordsPerLane * sizeof(uint32_t));
     if (e != hipSuccess) return hip_fail(e);
   }
   harvest_timing(ctx);
   if ((e = hipEventRecord(ctx->ev0, s)) != hipSuccess) return hip_fail(e);
-  for (size_t c = 0; c < n; c += kChunk) {
-    const uint32_t cn = (uint32_t)std::min<size_t>(kChunk, n - c);
+  const size_t chunk = quad ? kChunk : ctx->lane_chunk;
+  for (size_t c = 0; c < n; c += chunk) {
+    const uint32_t cn = (uint32_t)std::min<size_t>(chunk, n - c);
     if (sr)
       e = launch_verify_sr25519(cn, d_pk + 32 * c, d_sig + 64 * c, d_msg, d_off + c, ctx->d_btab,
                                 static_cast<uint32_t*>(ctx->d_atab.p), ctx->d_srprog, ctx->sr_nops,
@@ -478,6 +480,10 @@ int cmtv_open(const cmtv_config* cfg, cmtv_ctx** out) {
   ctx->device = dev;
   ctx->default_mode = cfg ? cfg->default_mode : CMTV_MODE_GO_STDLIB;
   if (const char* qm = std::getenv("CMTV_QUAD_MAX")) ctx->quad_max = (size_t)std::strtoull(qm, nullptr, 10);
+  if (const char* lc = std::getenv("CMTV_LANE_CHUNK")) {
+    const size_t v = (size_t)std::strtoull(lc, nullptr, 10) / 64 * 64;
+    if (v >= 64 && v <= kChunk) ctx->lane_chunk = v;
+  }
   hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&ctx->ev0);
   if (e == hipSuccess) e = hipEventCreate(&ctx->ev1);

@@ -21,6 +21,7 @@
 #pragma once
 #include "fe25519.h"
 #include "ge25519.h"
+#include "halfscalar.h"
 #include "sc25519.h"
 #include "sha512.h"
 
@@ -41,6 +42,15 @@ CMTV_HD void basepoint_words(uint32_t w[8]) {
   w[0] = 0x66666658u;
 #pragma unroll
   for (int i = 1; i < 8; i++) w[i] = 0x66666666u;
+}
+
+// y (255 bits, sign stripped) < p ?  -- the canonical-encoding test for R
+CMTV_HD bool y_is_canonical(const uint32_t w[8]) {
+  const uint32_t top = w[7] & 0x7FFFFFFFu;
+  bool all_ones = top == 0x7FFFFFFFu;
+#pragma unroll
+  for (int i = 1; i < 7; i++) all_ones = all_ones && w[i] == 0xFFFFFFFFu;
+  return !(all_ones && w[0] >= 0xFFFFFFEDu);
 }
 
 CMTV_HD void cached_neg_point(ge_p3& r, const ge_p3& p) {
@@ -243,6 +253,126 @@ CMTV_HD bool verify_one(const uint32_t* pk_ptr, const uint32_t* sig_ptr, const u
   ge_p3 Rp;
   straus_double_scalarmult<true>(Rp, k, ts, atab, btab);
   return check_R<MODE>(Rp, sig_ptr) && ok;
+}
+
+// Wave-uniform predicate for loop bounds (the device policy ballots; one
+// lane per "wave" on the host)
+struct HostWave {
+  CMTV_HD bool any(bool x) const { return x; }
+};
+
+// Half-size-scalar form of verify_one (halfscalar.h): with (k1, k2) the
+// half-size pair of k and u = k2 s mod L,
+//   X = [u]B + [k1](-A) + [|k2|](k2 < 0 ? R : -R) = [k2](R' - R)
+// over 34 shared 4-bit windows (64 when the pair is wide): per window four
+// doublings, one (1..8)(-A) and one (1..8)(-/+R) addition, and one fixed-base
+// addition (u mod 2^128 against (1..128)B on even windows, u >> 128 against
+// (1..128)[2^124]B on odd ones). k2 is odd, so X = O <=> R' = R and
+// [8]X = O <=> [8](R' - R) = O: the verdicts are verify_one's.
+//   GO_STDLIB: R canonical (and decodable) and X = O  -- encode(R') == R bytes
+//   ZIP215:    R decodable and [8]X = O
+// atabA / atabR: two (1..8)P cached tables; btab rows 0..255 (both tables).
+template <uint32_t MODE, class ATab, class BTab, class Wave = HostWave>
+CMTV_HD bool verify_one_half(const uint32_t* pk_ptr, const uint32_t* sig_ptr, const uint8_t* msg, uint32_t mlen,
+                             ATab& atabA, ATab& atabR, const BTab& btab, const Wave& wave = Wave()) {
+  uint32_t w[16];
+#pragma unroll
+  for (int i = 0; i < 8; i++) w[i] = sig_ptr[8 + i];  // S
+  bool ok = (w[7] & 0xE0000000u) == 0 && sc_is_canonical(w);  // sig[63] & 224, S < L
+  uint32_t ts[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) ts[i] = w[i];
+
+  // k = SHA-512(R || A || M) mod L, then the half-size pair and u
+  uint32_t k[8];
+  {
+    uint32_t h[16];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      w[i] = sig_ptr[i];  // R
+      w[8 + i] = pk_ptr[i];
+    }
+    sha512_prefixed<16>(h, w, msg, mlen);
+    sc_reduce512(k, h);
+  }
+  HalfScalars hs;
+  half_scalars(hs, k);
+  uint32_t u[8];
+  hs_bscalar(u, hs.k2, hs.k2_neg, ts);
+  const bool wide = wave.any(hs.wide);
+  const int W = wide ? HS_WIDE_WINDOWS : HS_WINDOWS;
+
+  // tables: (1..8)(-A), (1..8)(k2 < 0 ? R : -R)
+  {
+    ge_p3 P, nP;
+#pragma unroll
+    for (int i = 0; i < 8; i++) w[i] = pk_ptr[i];
+    ok = p3_frombytes(P, w) && ok;
+    cached_neg_point(nP, P);
+    build_cached_table(atabA, nP);
+#pragma unroll
+    for (int i = 0; i < 8; i++) w[i] = sig_ptr[i];
+    const bool r_ok = p3_frombytes(P, w);
+    if (MODE == MODE_GO_STDLIB) ok = ok && r_ok && y_is_canonical(w) && !(fe_iszero(P.X) && (w[7] >> 31));
+    else ok = ok && r_ok;
+    cached_neg_point(nP, P);
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+      nP.X.v[i] = hs.k2_neg ? P.X.v[i] : nP.X.v[i];
+      nP.T.v[i] = hs.k2_neg ? P.T.v[i] : nP.T.v[i];
+    }
+    build_cached_table(atabR, nP);
+  }
+
+  uint32_t tA[8], tR[8], tLo[8], tHi[8];
+  hs_digits16(tA, hs.k1, wide);
+  hs_digits16(tR, hs.k2, wide);
+  hs_digits256(tLo, tHi, u);
+  ge_p2 cur;
+  p2_identity(cur);
+  ge_p3 P;
+  ge_efgh t;
+#pragma unroll 1
+  for (int win = W - 1; win >= 0; win--) {
+#pragma unroll 1
+    for (int d = 0; d < 3; d++) {
+      p2_dbl(t, cur);
+      efgh_to_p2(cur, t);
+    }
+    p2_dbl(t, cur);
+    {
+      const int dA = (int)sc_shift_out(tA, 4) - 8;
+      const int ia = dA < 0 ? -dA : dA;
+      efgh_to_p3(P, t);
+      ge_add_table<true>(t, P, atabA, ia > 0 ? ia - 1 : 0, dA < 0, ia == 0);
+    }
+    {
+      const int dR = (int)sc_shift_out(tR, 4) - 8;
+      const int ir = dR < 0 ? -dR : dR;
+      efgh_to_p3(P, t);
+      ge_add_table<true>(t, P, atabR, ir > 0 ? ir - 1 : 0, dR < 0, ir == 0);
+    }
+    if (win <= 32 && ((win & 1) == 0 || win <= 31)) {
+      const bool odd = win & 1;
+      int dB;
+      if (odd)
+        dB = (int)sc_shift_out(tHi, 8) - 128;
+      else
+        dB = (int)sc_shift_out(tLo, 8) - 128;
+      const int ib = dB < 0 ? -dB : dB;
+      efgh_to_p3(P, t);
+      ge_add_table<false>(t, P, btab, (ib > 0 ? ib - 1 : 0) + (odd ? BTAB_ENTRIES : 0), dB < 0, ib == 0);
+    }
+    efgh_to_p2(cur, t);
+  }
+  if (MODE == MODE_ZIP215) {
+#pragma unroll 1
+    for (int d = 0; d < 3; d++) {
+      p2_dbl(t, cur);
+      efgh_to_p2(cur, t);
+    }
+  }
+  return ok && fe_iszero(cur.X) && fe_equal(cur.Y, cur.Z);
 }
 
 // RFC 8032 key expansion: h = SHA-512(seed); a = clamp(h[0:32]) mod L, prefix = h[32:64]

@@ -4,6 +4,8 @@
 //   input  (stdin):  u32 n, then n x { u8 mode, u8 pk[32], u8 sig[64], u32 mlen, u8 msg[mlen] }
 //   output (stdout): n bytes of verdicts
 //   argv[1] == "sign": n x { u8 seed[32], u32 mlen, msg } -> n x { pk[32], sig[64] }
+//   argv[1] == "half":  verify input as above, through verify_one_half (the
+//                       lane kernel's half-size-scalar pipeline)
 //   argv[1] == "keyed": verify input as above, through registered-key combs
 //                       (keyed.h; one comb per distinct pk)
 #define CMTV_HD inline
@@ -19,8 +21,8 @@ using namespace cmtv;
 
 struct HostBTab {
   std::vector<uint32_t> rows;
-  HostBTab() : rows(BTAB_ENTRIES * BTAB_ROW_WORDS) {
-    for (int m = 1; m <= BTAB_ENTRIES; m++) btab_entry(&rows[(m - 1) * BTAB_ROW_WORDS], m);
+  HostBTab() : rows(2 * BTAB_ENTRIES * BTAB_ROW_WORDS) {
+    for (int e = 0; e < 2 * BTAB_ENTRIES; e++) btab_entry(&rows[e * BTAB_ROW_WORDS], e % BTAB_ENTRIES + 1, e >= BTAB_ENTRIES);
   }
   void load_fe(int e, int c, fe& r) const {
     const uint32_t* p = &rows[e * BTAB_ROW_WORDS + c * BTAB_COORD_WORDS];
@@ -69,6 +71,7 @@ int main(int argc, char** argv) {
   if (fread(&n, 4, 1, stdin) != 1) return 1;
   const bool sign = argc > 1 && !strcmp(argv[1], "sign");
   const bool keyed = argc > 1 && !strcmp(argv[1], "keyed");
+  const bool half = argc > 1 && !strcmp(argv[1], "half");
   std::vector<uint32_t> bcomb;
   std::map<std::string, std::pair<bool, std::vector<uint32_t>>> combs;
   if (keyed) {
@@ -121,9 +124,14 @@ int main(int argc, char** argv) {
       fwrite(&o, 1, 1, stdout);
       continue;
     }
-    HostATab at;
-    bool v = mode ? verify_one<MODE_ZIP215>(pkw, sigw, mp, mlen, at, bt)
-                  : verify_one<MODE_GO_STDLIB>(pkw, sigw, mp, mlen, at, bt);
+    HostATab at, ar;
+    bool v;
+    if (half)
+      v = mode ? verify_one_half<MODE_ZIP215>(pkw, sigw, mp, mlen, at, ar, bt)
+               : verify_one_half<MODE_GO_STDLIB>(pkw, sigw, mp, mlen, at, ar, bt);
+    else
+      v = mode ? verify_one<MODE_ZIP215>(pkw, sigw, mp, mlen, at, bt)
+               : verify_one<MODE_GO_STDLIB>(pkw, sigw, mp, mlen, at, bt);
     uint8_t o = v;
     fwrite(&o, 1, 1, stdout);
   }

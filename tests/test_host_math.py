@@ -47,6 +47,17 @@ def _run(binary, arg, corpus, idx, mode):
 
 
 @pytest.mark.parametrize("mode", [0, 1])
+def test_half_scalar_lane_pipeline_matches_corpus(hostcheck, corpus, mode):
+    """verify_one_half (the lane kernel: half-size scalars, 34 windows, R
+    table, X = [k2](R' - R)) over the whole corpus at every misalignment."""
+    idx = list(range(len(corpus["msgs"])))
+    got = _run(hostcheck, "half", corpus, idx, mode)
+    want = corpus["go"] if mode == 0 else corpus["zip215"]
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(int(i), corpus["cats"][int(i)]) for i in bad[:10]]
+
+
+@pytest.mark.parametrize("mode", [0, 1])
 def test_generic_pipeline_matches_corpus(hostcheck, corpus, mode):
     idx = list(range(len(corpus["msgs"])))
     got = _run(hostcheck, None, corpus, idx, mode)

@@ -86,35 +86,47 @@ CMTV_HD void q_dbl(const Q& q, fe& v) {
   fe_mul(v, a, b);
 }
 
+// quad_perm code: lane c reads lane s_c
+constexpr int qp(int s0, int s1, int s2, int s3) { return s0 | (s1 << 2) | (s2 << 4) | (s3 << 6); }
+
 // Addition v += Q where c is this lane's coordinate of Q in cached form
 // (Y2-X2, Y2+X2, Z2, 2dT2); for an affine niels addend pass Z2 = 1.
 //   round 1: lane c computes {(Y1-X1)(Y2-X2), (Y1+X1)(Y2+X2), Z1 Z2, T1 2dT2}[c]
-//   round 2: lane c computes {EF, GH, FG, EH}[c]
+//            = {A, B, D/2, C}
+//   round 2: lane c computes {EF, GH, FG, EH}[c], E = B-A, F = D-C, G = D+C,
+//            H = B+A
+// Each round-2 operand is P +- Q with P and Q read from a per-lane source
+// lane by ONE quad_perm each (op1 = {B-A, D+C, D-C, B-A}, op2 = {D-C, B+A,
+// D+C, B+A}), so no lane computes values it does not multiply.
 template <class Q>
 CMTV_HD void q_add(const Q& q, fe& v, const fe& c) {
   const int lane = q.lane();
-  fe x, y, t;
-  q.template perm<QP_B0>(x, v);
-  q.template perm<QP_B1>(y, v);
-  fe_sub(t, y, x);
-  fe_add(y, y, x);
-  fe_pick(x, lane, t, y, v, v);
-  fe_mul(t, x, c);
-  fe A, B, D, C;
-  q.template perm<QP_B0>(A, t);
-  q.template perm<QP_B1>(B, t);
-  q.template perm<QP_B2>(D, t);
-  q.template perm<QP_B3>(C, t);
-  fe_add(D, D, D);
-  fe_carry(D);
-  fe E, H;
-  fe_sub(E, B, A);
-  fe_add(H, B, A);
-  fe_sub(A, D, C);  // F
-  fe_add(B, D, C);  // G
-  fe_pick(x, lane, E, B, A, E);
-  fe_pick(y, lane, A, H, B, H);
-  fe_mul(v, x, y);
+  fe p, x, t;
+  // round 1 operand: lanes 0/1: Y -+ X; lanes 2/3: own Z / T
+  q.template perm<qp(1, 1, 2, 3)>(p, v);  // Y, Y, Z, T
+  q.template perm<QP_B0>(x, v);           // X
+  fe_neg(t, x);
+  fe_select(x, x, t, lane == 0);
+#pragma unroll
+  for (int i = 0; i < 10; i++) x.v[i] = lane >= 2 ? 0u : x.v[i];
+  fe_add(p, p, x);
+  fe_mul(t, p, c);
+  // D = 2 Z1 Z2 on lane 2; all four carried
+  fe_add(x, t, t);
+  fe_select(t, t, x, lane == 2);
+  fe_carry(t);  // lanes: A, B, D, C
+  fe o1, o2, n;
+  q.template perm<qp(1, 2, 2, 1)>(o1, t);  // B, D, D, B
+  q.template perm<qp(0, 3, 3, 0)>(x, t);   // A, C, C, A
+  fe_neg(n, x);
+  fe_select(x, n, x, lane == 1);
+  fe_add(o1, o1, x);                       // B-A, D+C, D-C, B-A
+  q.template perm<qp(2, 1, 2, 1)>(o2, t);  // D, B, D, B
+  q.template perm<qp(3, 0, 3, 0)>(x, t);   // C, A, C, A
+  fe_neg(n, x);
+  fe_select(x, x, n, lane == 0);
+  fe_add(o2, o2, x);                       // D-C, B+A, D+C, B+A
+  fe_mul(v, o1, o2);
 }
 
 // this lane's cached-form coordinate of the extended point v

@@ -210,6 +210,12 @@ def _cpu_model():
     return "unknown"
 
 
+def ctx_device(ctx) -> int:
+    import torch
+
+    return torch.cuda.current_device()
+
+
 def latency_150(ctx, mode, iters):
     """p50/p99 VerifyCommit latency for a 150-validator commit (host API, end to end)."""
     from cometbft_amd import testutil as TU
@@ -228,6 +234,23 @@ def latency_150(ctx, mode, iters):
     res = {"n_validators": 150, "iters": iters, "p50_ms": round(float(np.percentile(ts, 50)), 4),
            "p99_ms": round(float(np.percentile(ts, 99)), 4),
            "path": "cmtv_verify_commit: sign-bytes + H2D + kernel + D2H + VerifyCommit replay"}
+    # the same commit on a context that keeps the validator set's registered
+    # keys (cmtv_keyset_cache; the set is registered by the first call)
+    from cometbft_amd import Context
+
+    kctx = Context(device=ctx_device(ctx))
+    kctx.keyset_cache(4)
+    for _ in range(20):
+        sv.valset.verify_commit(TU.CHAIN_ID, bid, 1000, commit, ctx=kctx, mode=mode)
+    kts = []
+    for _ in range(iters):
+        t = time.perf_counter()
+        sv.valset.verify_commit(TU.CHAIN_ID, bid, 1000, commit, ctx=kctx, mode=mode)
+        kts.append(time.perf_counter() - t)
+    kts = np.array(kts) * 1e3
+    res["keyset_cache"] = {"p50_ms": round(float(np.percentile(kts, 50)), 4),
+                           "p99_ms": round(float(np.percentile(kts, 99)), 4),
+                           "path": "same, validator set registered once (cmtv_keyset_cache): keyed quad kernel"}
     # the reference's shape: one core verifying 150 signatures sequentially
     from oracle import coracle
 

@@ -45,7 +45,7 @@ EXPORTS = (
     "cmtv_register_keys", "cmtv_keyset_free", "cmtv_keyset_len", "cmtv_verify_ed25519_indexed",
     "cmtv_verify_ed25519_indexed_device",
     "cmtv_batch_new", "cmtv_batch_add", "cmtv_batch_len", "cmtv_batch_verify", "cmtv_batch_reset",
-    "cmtv_batch_free", "cmtv_verify_commit", "cmtv_verify_commits", "cmtv_verdict_cache", "cmtv_vote_sign_bytes", "cmtv_pubkeys_ed25519", "cmtv_sign_ed25519",
+    "cmtv_batch_free", "cmtv_verify_commit", "cmtv_verify_commits", "cmtv_verdict_cache", "cmtv_keyset_cache", "cmtv_vote_sign_bytes", "cmtv_pubkeys_ed25519", "cmtv_sign_ed25519",
 )
 
 
@@ -158,6 +158,8 @@ def lib() -> ctypes.CDLL:
                                       u64, u64, ctypes.POINTER(cmtv_commit_result), ctypes.POINTER(ctypes.c_int),
                                       ctypes.c_char_p, sz]
     L.cmtv_verify_commits.restype = ctypes.c_int
+    L.cmtv_keyset_cache.argtypes = [vp, sz]
+    L.cmtv_keyset_cache.restype = ctypes.c_int
     L.cmtv_verdict_cache.argtypes = [vp, sz]
     L.cmtv_verdict_cache.restype = ctypes.c_int
     L.cmtv_vote_sign_bytes.argtypes = [ctypes.c_char_p, sz, i32, i64, i32, ctypes.POINTER(cmtv_block_id), i64, i32,

@@ -65,6 +65,11 @@ class Context:
         N.check(N.lib().cmtv_stats_get(self._h, ctypes.byref(st)), "cmtv_stats_get")
         return {k: getattr(st, k) for k, _ in st._fields_}
 
+    def keyset_cache(self, max_sets: int) -> None:
+        """cmtv_keyset_cache: registered key sets of up to max_sets validator
+        sets for cmtv_verify_commit(s) (0 = off)."""
+        N.check(N.lib().cmtv_keyset_cache(self._h, max_sets), "cmtv_keyset_cache")
+
     def verdict_cache(self, max_entries: int) -> None:
         """cmtv_verdict_cache: keep the last max_entries verdicts (0 = off)."""
         N.check(N.lib().cmtv_verdict_cache(self._h, max_entries), "cmtv_verdict_cache")

@@ -165,6 +165,11 @@ struct SigBatch {
   std::vector<int64_t> tsec;
   std::vector<int32_t> tnanos;
   const cmtv_commit* cur = nullptr;  // commit of the last template
+  // validator indices, for registered-key verification when every signature
+  // comes from one validator set (cmtv_keyset_cache)
+  std::vector<uint32_t> kidx;
+  const cmtv_valset* vs = nullptr;
+  bool one_vs = true;
 
   size_t size() const { return off.size() - 1; }
 
@@ -191,9 +196,13 @@ struct SigBatch {
   }
 
   // key (32 bytes), the CommitSig's signature and the vote's sign-bytes
-  void add(const uint8_t* key, const uint8_t* sig, uint32_t sig_len, const char* chain_id, size_t chain_id_len,
-           const cmtv_commit* c, uint32_t idx) {
+  void add(const cmtv_valset* vals, uint32_t vi, const uint8_t* sig, uint32_t sig_len, const char* chain_id,
+           size_t chain_id_len, const cmtv_commit* c, uint32_t idx) {
     static const cmtv_block_id empty{};
+    const uint8_t* key = vals->pubkeys + vals->pk_off[vi];
+    if (!vs) vs = vals;
+    one_vs = one_vs && vs == vals;
+    kidx.push_back(vi);
     pk.insert(pk.end(), key, key + 32);
     const size_t o = sg.size();
     sg.resize(o + 64, 0);
@@ -353,7 +362,7 @@ void job_prepare(CommitJob& J, SigBatch& B, bool prefetch) {
   for (size_t j = 0; j < J.plan_idx.size(); j++) {
     const uint32_t idx = J.plan_idx[j], vi = J.plan_val[j];
     const uint32_t s0 = commit->sig_off[idx], s1 = commit->sig_off[idx + 1];
-    B.add(vals->pubkeys + vals->pk_off[vi], commit->sigs + s0, s1 - s0, J.chain_id, J.chain_id_len, commit, idx);
+    B.add(vals, vi, commit->sigs + s0, s1 - s0, J.chain_id, J.chain_id_len, commit, idx);
   }
   if (prefetch && J.kind == CMTV_VERIFY_COMMIT_LIGHT) {
     // the VerifyCommit calls that follow a light call in blocksync verify
@@ -365,7 +374,7 @@ void job_prepare(CommitJob& J, SigBatch& B, bool prefetch) {
       if (planned[idx] || (flag != kFlagCommit && flag != kFlagNil)) continue;
       if (vals->pk_off[idx + 1] - vals->pk_off[idx] != 32) continue;
       const uint32_t s0 = commit->sig_off[idx], s1 = commit->sig_off[idx + 1];
-      B.add(vals->pubkeys + vals->pk_off[idx], commit->sigs + s0, s1 - s0, J.chain_id, J.chain_id_len, commit, idx);
+      B.add(vals, idx, commit->sigs + s0, s1 - s0, J.chain_id, J.chain_id_len, commit, idx);
     }
   }
 }
@@ -376,9 +385,17 @@ int batch_verify(cmtv_ctx* ctx, SigBatch& B, uint32_t mode, std::vector<uint8_t>
   if (!m) return CMTV_OK;
   int rc;
   if (B.templated) {
+    // one validator set of 32-byte keys: its registered key set (built on
+    // first use by cmtv_keyset_cache) replaces decompression and doublings
+    const cmtv_keyset* ks = nullptr;
+    if (cmtv::keyset_cache_enabled(ctx) && B.one_vs && B.vs->n_vals) {
+      bool packed = true;
+      for (uint32_t i = 0; i <= B.vs->n_vals && packed; i++) packed = B.vs->pk_off[i] == 32 * i;
+      if (packed) ks = cmtv::keyset_for_locked(ctx, B.vs->pubkeys, B.vs->n_vals);
+    }
     rc = cmtv::verify_templated_locked(ctx, m, B.pk.data(), B.sg.data(), B.off.data(), B.tmpls.data(), B.tmpls.size(),
                                        B.blob.data(), B.blob.size(), B.tidx.data(), B.tflag.data(), B.tsec.data(),
-                                       B.tnanos.data(), mode, valid.data());
+                                       B.tnanos.data(), mode, valid.data(), ks, B.kidx.data());
   } else {
     if (B.msgs.empty()) B.msgs.push_back(0);
     rc = cmtv::verify_host_locked(ctx, m, B.pk.data(), B.sg.data(), B.msgs.data(), B.off.data(), mode, valid.data(),

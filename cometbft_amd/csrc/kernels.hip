@@ -7,6 +7,7 @@
 //   k_verify_quad<MODE>: the same, one signature per quad of lanes (small batches)
 //   k_comb_build  : registered-key combs (keyed.h), one workgroup per key
 //   k_verify_keyed<MODE>: one signature per lane against a registered key
+//   k_verify_keyed_quad<MODE>: the same, one signature per quad of lanes
 //   k_pubkey / k_sign : RFC 8032 key generation and signing (synthetic data)
 //
 // Memory layout (HBM):
@@ -25,6 +26,7 @@
 #include "devtables.h"
 #include "kernels.h"
 #include "keyed.h"
+#include "keyed_quad.h"
 #include "quad.h"
 #include "verify_core.h"
 
@@ -198,6 +200,35 @@ __global__ __launch_bounds__(64, CMTV_KEYED_WAVES_PER_EU) void k_verify_keyed(
   if (threadIdx.x == 0 && out_bitmap) out_bitmap[gid >> 6] = mask;
 }
 
+// One signature per quad of lanes by registered key (keyed_quad.h), for
+// latency-bound batches; 16 signatures per 64-lane block.
+template <uint32_t MODE>
+__global__ __launch_bounds__(64, 1) void k_verify_keyed_quad(
+    uint32_t n, uint32_t n_keys, const uint32_t* __restrict__ key_idx, const uint32_t* __restrict__ sig,
+    const uint8_t* __restrict__ msg, const uint32_t* __restrict__ off, const uint32_t* __restrict__ keys_pk,
+    const uint8_t* __restrict__ keys_ok, const uint32_t* __restrict__ ktabs, const uint32_t* __restrict__ bcomb,
+    uint8_t* __restrict__ out_valid, uint64_t* __restrict__ out_bitmap) {
+  const uint32_t gid = blockIdx.x * 64 + threadIdx.x;
+  const uint32_t s = gid >> 2;
+  const bool active = s < n;
+  const uint32_t i = active ? s : n - 1;
+  const uint32_t m0 = off[i], m1 = off[i + 1];
+  uint32_t kid = key_idx[i];
+  const bool kin = kid < n_keys;
+  kid = kin ? kid : 0;
+  DevQuad q;
+  bool v = q_verify_keyed<MODE>(q, keys_pk + 8 * (size_t)kid, kin && keys_ok[kid] != 0, sig + 16 * (size_t)i,
+                                msg + m0, m1 - m0, ktabs + (size_t)kid * COMB_TABLE_WORDS, bcomb);
+  v = v && active;
+  if (active && (threadIdx.x & 3) == 0 && out_valid) out_valid[s] = v ? 1 : 0;
+  uint64_t x = __ballot(v && (threadIdx.x & 3) == 0) & 0x1111111111111111ull;
+  x = (x | (x >> 3)) & 0x0303030303030303ull;
+  x = (x | (x >> 6)) & 0x000F000F000F000Full;
+  x = (x | (x >> 12)) & 0x000000FF000000FFull;
+  x = (x | (x >> 24)) & 0xFFFFull;
+  if (threadIdx.x == 0 && out_bitmap) reinterpret_cast<uint16_t*>(out_bitmap)[gid >> 6] = (uint16_t)x;
+}
+
 __global__ __launch_bounds__(64) void k_pubkey(uint32_t n, const uint32_t* __restrict__ seeds,
                                                const uint32_t* __restrict__ btab, uint32_t* __restrict__ out_pk) {
   const uint32_t gid = blockIdx.x * 64 + threadIdx.x;
@@ -272,7 +303,7 @@ hipError_t launch_comb_build(uint32_t n_keys, const void* keys_pk, uint8_t* keys
 hipError_t launch_verify_keyed(uint32_t mode, uint32_t n, uint32_t n_keys, const void* key_idx, const void* sig,
                                const void* msg, const void* off, const uint32_t* keys_pk, const uint8_t* keys_ok,
                                const uint32_t* ktabs, const uint32_t* bcomb, void* valid, void* bitmap,
-                               hipStream_t s) {
+                               bool quad, hipStream_t s) {
   if (n == 0) return hipSuccess;
   auto ki = static_cast<const uint32_t*>(key_idx);
   auto sgp = static_cast<const uint32_t*>(sig);
@@ -280,6 +311,16 @@ hipError_t launch_verify_keyed(uint32_t mode, uint32_t n, uint32_t n_keys, const
   auto op = static_cast<const uint32_t*>(off);
   auto vp = static_cast<uint8_t*>(valid);
   auto bp = static_cast<uint64_t*>(bitmap);
+  if (quad) {
+    const dim3 grid(((n + 63) / 64) * 4), block(64);
+    if (mode == MODE_ZIP215)
+      hipLaunchKernelGGL(k_verify_keyed_quad<MODE_ZIP215>, grid, block, 0, s, n, n_keys, ki, sgp, mp, op, keys_pk,
+                         keys_ok, ktabs, bcomb, vp, bp);
+    else
+      hipLaunchKernelGGL(k_verify_keyed_quad<MODE_GO_STDLIB>, grid, block, 0, s, n, n_keys, ki, sgp, mp, op, keys_pk,
+                         keys_ok, ktabs, bcomb, vp, bp);
+    return hipGetLastError();
+  }
   const dim3 grid(blocks_for(n)), block(64);
   if (mode == MODE_ZIP215)
     hipLaunchKernelGGL(k_verify_keyed<MODE_ZIP215>, grid, block, 0, s, n, n_keys, ki, sgp, mp, op, keys_pk, keys_ok,

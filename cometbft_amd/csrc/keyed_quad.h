@@ -1,0 +1,112 @@
+// keyed_quad.h -- registered-key verification (keyed.h) with one signature
+// per quad of lanes (quad.h), for latency-bound batches: a 10k-signature
+// commit against a registered validator set, or a 150-validator commit.
+//
+// Same verdict as verify_keyed<MODE> (and so verify_one<MODE>) on every input:
+//   R' = sum_j T_B[j][s_j] + T_A[j][k_j]     32 + 32 comb additions, no doublings
+//   GO_STDLIB: R canonical, decodable, and R' == R projectively
+//              (X' = x_R Z', Y' = y_R Z': encode(R') == R bytes, no inversion)
+//   ZIP215:    R decodable and [8](R' - R) == O
+// Every lane decodes R (the same bytes); lane c then keeps coordinate c.
+#pragma once
+#include "keyed.h"
+#include "quad.h"
+
+namespace cmtv {
+
+// lane c's cached coordinate (Y-X, Y+X, Z = 1, 2dT) of comb row `row`
+// (affine niels: y+x[10] y-x[10] 2dxy[10] pad[2]); e < 0: the identity
+template <class Q>
+CMTV_HD void q_comb_coord(const Q& q, fe& c, const uint32_t* row, bool ident) {
+  const int lane = q.lane();
+  const int off = lane == 0 ? 10 : (lane == 3 ? 20 : 0);
+#pragma unroll
+  for (int i = 0; i < 10; i++) c.v[i] = row[off + i];
+  const bool one = lane == 2 || (ident && lane != 3);
+#pragma unroll
+  for (int i = 0; i < 10; i++) c.v[i] = (ident || lane == 2) ? ((one && i == 0) ? 1u : 0u) : c.v[i];
+}
+
+template <uint32_t MODE, class Q>
+CMTV_HD bool q_verify_keyed(const Q& q, const uint32_t* key_pk, bool key_ok, const uint32_t* sig_ptr,
+                            const uint8_t* msg, uint32_t mlen, const uint32_t* ktab, const uint32_t* bcomb) {
+  const int lane = q.lane();
+  uint32_t w[16];
+#pragma unroll
+  for (int i = 0; i < 8; i++) w[i] = sig_ptr[8 + i];  // S
+  bool ok = key_ok && (w[7] & 0xE0000000u) == 0 && sc_is_canonical(w);
+  uint32_t ts[8], tk[8];
+  sc_bias(ts, w, 0x80808080u);
+  {
+    uint32_t h[16], k[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      w[i] = sig_ptr[i];  // R
+      w[8 + i] = key_pk[i];
+    }
+    sha512_prefixed<16>(h, w, msg, mlen);
+    sc_reduce512(k, h);
+    sc_bias(tk, k, 0x80808080u);
+  }
+  // R, decoded on every lane; rc = this lane's coordinate (x, y, 1, t)
+  fe rc;
+  {
+#pragma unroll
+    for (int i = 0; i < 8; i++) w[i] = sig_ptr[i];
+    ge_p3 R;
+    const bool r_ok = p3_frombytes(R, w);
+    fe one;
+    fe_1(one);
+    fe_pick(rc, lane, R.X, R.Y, one, R.T);
+    if (MODE == MODE_GO_STDLIB) ok = ok && r_ok && y_is_canonical(w) && !(fe_iszero(R.X) && (w[7] >> 31));
+    else ok = ok && r_ok;
+  }
+
+  fe v;
+  q_identity(v, lane);
+#pragma unroll 1
+  for (int it = 0; it < COMB_WINDOWS; it++) {
+    const int j = COMB_WINDOWS - 1 - it;
+    {
+      const int dA = (int)sc_shift_out(tk, 8) - 128;
+      const int ia = dA < 0 ? -dA : dA;
+      fe c;
+      q_comb_coord(q, c, ktab + ((size_t)j * COMB_ENTRIES + (ia > 0 ? ia - 1 : 0)) * COMB_ROW_WORDS, ia == 0);
+      q_cached_cneg(q, c, dA < 0);
+      q_add(q, v, c);
+    }
+    {
+      const int dB = (int)sc_shift_out(ts, 8) - 128;
+      const int ib = dB < 0 ? -dB : dB;
+      fe c;
+      q_comb_coord(q, c, bcomb + ((size_t)j * COMB_ENTRIES + (ib > 0 ? ib - 1 : 0)) * COMB_ROW_WORDS, ib == 0);
+      q_cached_cneg(q, c, dB < 0);
+      q_add(q, v, c);
+    }
+  }
+
+  if (MODE == MODE_GO_STDLIB) {
+    fe z, t;
+    q.template perm<QP_B2>(z, v);  // Z'
+    fe_mul(t, z, rc);              // lane 0: x_R Z', lane 1: y_R Z'
+    const bool eq = fe_equal(t, v);
+    const bool e0 = q.template perm32<QP_B0>(eq ? 1u : 0u) != 0;
+    const bool e1 = q.template perm32<QP_B1>(eq ? 1u : 0u) != 0;
+    return ok && e0 && e1;
+  }
+  fe c;
+  q_to_cached(q, c, rc);
+  q_cached_cneg(q, c, true);
+  q_add(q, v, c);
+#pragma unroll 1
+  for (int d = 0; d < 3; d++) q_dbl(q, v);
+  fe z;
+  q.template perm<QP_B2>(z, v);
+  const bool x0 = fe_iszero(v);    // lane 0
+  const bool yz = fe_equal(v, z);  // lane 1
+  const bool e0 = q.template perm32<QP_B0>(x0 ? 1u : 0u) != 0;
+  const bool e1 = q.template perm32<QP_B1>(yz ? 1u : 0u) != 0;
+  return ok && e0 && e1;
+}
+
+}  // namespace cmtv

@@ -30,6 +30,8 @@ constexpr uint32_t kChunk = 1u << 18;  // signatures per launch (A-table scratch
 // crossover between the quad (4 lanes / signature) and lane (1 lane / signature)
 // kernels; measured on MI355X, overridable with CMTV_QUAD_MAX
 constexpr size_t kQuadMaxDefault = 40000;
+// the same crossover for registered-key verification (env CMTV_KEYED_QUAD_MAX)
+constexpr size_t kKeyedQuadMaxDefault = 16384;
 
 struct DevBuf {
   void* p = nullptr;
@@ -160,6 +162,11 @@ struct cmtv_ctx {
   int sr_nops = 0;
   VerdictCache cache;                 // cmtv_verdict_cache (off by default)
   size_t lane_chunk = kChunk;         // signatures per lane-kernel launch (env CMTV_LANE_CHUNK)
+  size_t keyed_quad_max = kKeyedQuadMaxDefault;  // registered-key batches up to this use the quad kernel
+  // cmtv_keyset_cache: validator sets (their concatenated keys) -> registered
+  // key sets, used by cmtv_verify_commit(s); FIFO of at most keyset_cap
+  size_t keyset_cap = 0;
+  std::vector<std::pair<std::string, cmtv_keyset*>> keysets;
 };
 
 struct cmtv_keyset {
@@ -270,7 +277,7 @@ static int enqueue_verify_keyed(cmtv_ctx* ctx, const cmtv_keyset* ks, size_t n, 
     const uint32_t cn = (uint32_t)std::min<size_t>(kChunk, n - c);
     e = launch_verify_keyed(mode, cn, (uint32_t)ks->n, d_idx + c, d_sig + 64 * c, d_msg, d_off + c, ks->d_pk,
                             ks->d_ok, ks->d_tab, ctx->d_bcomb, d_valid ? d_valid + c : nullptr,
-                            d_bitmap ? d_bitmap + c / 64 : nullptr, s);
+                            d_bitmap ? d_bitmap + c / 64 : nullptr, n <= ctx->keyed_quad_max, s);
     if (e != hipSuccess) return hip_fail(e);
     ctx->stats.kernel_launches++;
   }
@@ -380,7 +387,8 @@ static int verify_host_device(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const 
 int verify_templated_locked(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_t* sig, const uint32_t* msg_off,
                             const void* tmpls, size_t n_tmpls, const uint8_t* blob, size_t blob_len,
                             const uint32_t* tidx, const uint8_t* commit_flag, const int64_t* sec,
-                            const int32_t* nanos, uint32_t mode, uint8_t* out_valid) {
+                            const int32_t* nanos, uint32_t mode, uint8_t* out_valid, const cmtv_keyset* ks,
+                            const uint32_t* key_idx) {
   if (n == 0) return CMTV_OK;
   const size_t msg_bytes = msg_off[n];
   const size_t tb = n_tmpls * sizeof(SbTemplate);
@@ -398,7 +406,10 @@ int verify_templated_locked(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const ui
   if ((e = ctx->h_out.ensure(out_bytes)) != hipSuccess) return hip_fail(e);
   if ((e = ctx->d_out.ensure(out_bytes)) != hipSuccess) return hip_fail(e);
   auto* hin = static_cast<uint8_t*>(ctx->h_in.p);
-  std::memcpy(hin + o_pk, pk, 32 * n);
+  if (ks)
+    std::memcpy(hin + o_pk, key_idx, 4 * n);  // key indices in the key slot
+  else
+    std::memcpy(hin + o_pk, pk, 32 * n);
   std::memcpy(hin + o_sig, sig, 64 * n);
   std::memcpy(hin + o_off, msg_off, 4 * (n + 1));
   std::memcpy(hin + o_tidx, tidx, 4 * n);
@@ -416,8 +427,11 @@ int verify_templated_locked(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const ui
                              reinterpret_cast<int32_t*>(din + o_nanos), reinterpret_cast<uint32_t*>(din + o_off),
                              din + o_msg, ctx->stream)) != hipSuccess)
     return hip_fail(e);
-  int rc = enqueue_verify(ctx, n, din + o_pk, din + o_sig, din + o_msg, reinterpret_cast<uint32_t*>(din + o_off), mode,
-                          dout + o_valid, nullptr, ctx->stream);
+  int rc = ks ? enqueue_verify_keyed(ctx, ks, n, reinterpret_cast<uint32_t*>(din + o_pk), din + o_sig, din + o_msg,
+                                     reinterpret_cast<uint32_t*>(din + o_off), mode, dout + o_valid, nullptr,
+                                     ctx->stream)
+              : enqueue_verify(ctx, n, din + o_pk, din + o_sig, din + o_msg, reinterpret_cast<uint32_t*>(din + o_off),
+                               mode, dout + o_valid, nullptr, ctx->stream);
   if (rc != CMTV_OK) return rc;
   auto* hout = static_cast<uint8_t*>(ctx->h_out.p);
   if ((e = hipMemcpyAsync(hout, dout, out_bytes, hipMemcpyDeviceToHost, ctx->stream)) != hipSuccess) return hip_fail(e);
@@ -480,6 +494,7 @@ int cmtv_open(const cmtv_config* cfg, cmtv_ctx** out) {
   ctx->device = dev;
   ctx->default_mode = cfg ? cfg->default_mode : CMTV_MODE_GO_STDLIB;
   if (const char* qm = std::getenv("CMTV_QUAD_MAX")) ctx->quad_max = (size_t)std::strtoull(qm, nullptr, 10);
+  if (const char* kq = std::getenv("CMTV_KEYED_QUAD_MAX")) ctx->keyed_quad_max = (size_t)std::strtoull(kq, nullptr, 10);
   if (const char* lc = std::getenv("CMTV_LANE_CHUNK")) {
     const size_t v = (size_t)std::strtoull(lc, nullptr, 10) / 64 * 64;
     if (v >= 64 && v <= kChunk) ctx->lane_chunk = v;
@@ -514,6 +529,8 @@ void cmtv_close(cmtv_ctx* ctx) {
   if (ctx->d_btab) (void)hipFree(ctx->d_btab);
   if (ctx->d_bcomb) (void)hipFree(ctx->d_bcomb);
   if (ctx->d_srprog) (void)hipFree(ctx->d_srprog);
+  for (auto& e : ctx->keysets) cmtv_keyset_free(e.second);
+  ctx->keysets.clear();
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -596,6 +613,27 @@ int cmtv_register_keys(cmtv_ctx* ctx, size_t n_keys, const uint8_t* pk, cmtv_key
   if (!ctx || n_keys == 0 || n_keys > (1u << 20) || !pk) return CMTV_EINVAL;
   std::lock_guard<std::mutex> g(ctx->mu);
   if (hipSetDevice(ctx->device) != hipSuccess) return CMTV_ENODEV;
+  return cmtv::register_keys_locked(ctx, n_keys, pk, out);
+}
+
+int cmtv_keyset_cache(cmtv_ctx* ctx, size_t max_sets) {
+  if (!ctx || max_sets > 4096) return CMTV_EINVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  if (hipSetDevice(ctx->device) != hipSuccess) return CMTV_ENODEV;
+  (void)hipStreamSynchronize(ctx->stream);
+  while (ctx->keysets.size() > max_sets) {
+    cmtv_keyset_free(ctx->keysets.front().second);
+    ctx->keysets.erase(ctx->keysets.begin());
+  }
+  ctx->keyset_cap = max_sets;
+  return CMTV_OK;
+}
+
+}  // extern "C"
+
+namespace cmtv {
+
+int register_keys_locked(cmtv_ctx* ctx, size_t n_keys, const uint8_t* pk, cmtv_keyset** out) {
   int rc = ensure_bcomb(ctx);
   if (rc != CMTV_OK) return rc;
   auto* ks = new (std::nothrow) cmtv_keyset();
@@ -624,6 +662,27 @@ int cmtv_register_keys(cmtv_ctx* ctx, size_t n_keys, const uint8_t* pk, cmtv_key
   *out = ks;
   return CMTV_OK;
 }
+
+const cmtv_keyset* keyset_for_locked(cmtv_ctx* ctx, const uint8_t* pk32, size_t n_keys) {
+  if (!ctx->keyset_cap || n_keys == 0) return nullptr;
+  std::string key(reinterpret_cast<const char*>(pk32), 32 * n_keys);
+  for (auto& e : ctx->keysets)
+    if (e.first == key) return e.second;
+  cmtv_keyset* ks = nullptr;
+  if (register_keys_locked(ctx, n_keys, pk32, &ks) != CMTV_OK) return nullptr;  // generic path instead
+  if (ctx->keysets.size() >= ctx->keyset_cap) {
+    cmtv_keyset_free(ctx->keysets.front().second);
+    ctx->keysets.erase(ctx->keysets.begin());
+  }
+  ctx->keysets.emplace_back(std::move(key), ks);
+  return ks;
+}
+
+bool keyset_cache_enabled(const cmtv_ctx* ctx) { return ctx->keyset_cap != 0; }
+
+}  // namespace cmtv
+
+extern "C" {
 
 void cmtv_keyset_free(cmtv_keyset* ks) {
   if (!ks) return;

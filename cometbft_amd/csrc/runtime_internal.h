@@ -6,6 +6,7 @@
 #include <mutex>
 
 struct cmtv_ctx;
+struct cmtv_keyset;
 
 namespace cmtv {
 
@@ -26,11 +27,19 @@ int verify_host_locked(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_t
 
 // Commit signatures whose sign-bytes are written on the device from per-commit
 // templates (signbytes.h): tmpls is an array of n_tmpls SbTemplate over
-// `blob`; msg_off must hold the message offsets from sb_msg_len. Verdicts only
-// (no cache). Caller holds the context lock.
+// `blob`; msg_off must hold the message offsets from sb_msg_len. With ks the
+// keys are registered (key_idx into ks, no pk). Verdicts only (no verdict
+// cache). Caller holds the context lock.
 int verify_templated_locked(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_t* sig, const uint32_t* msg_off,
                             const void* tmpls, size_t n_tmpls, const uint8_t* blob, size_t blob_len,
                             const uint32_t* tidx, const uint8_t* commit_flag, const int64_t* sec,
-                            const int32_t* nanos, uint32_t mode, uint8_t* out_valid);
+                            const int32_t* nanos, uint32_t mode, uint8_t* out_valid,
+                            const cmtv_keyset* ks = nullptr, const uint32_t* key_idx = nullptr);
+
+// cmtv_keyset_cache: the registered key set of these n 32-byte keys (built on
+// first use), or NULL when the cache is off or registration failed.
+const cmtv_keyset* keyset_for_locked(cmtv_ctx* ctx, const uint8_t* pk32, size_t n_keys);
+bool keyset_cache_enabled(const cmtv_ctx* ctx);
+int register_keys_locked(cmtv_ctx* ctx, size_t n_keys, const uint8_t* pk, cmtv_keyset** out);
 
 }  // namespace cmtv

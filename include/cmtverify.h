@@ -126,6 +126,15 @@ int cmtv_verify_ed25519_device(cmtv_ctx* ctx, size_t n, const void* d_pk, const 
  * commit). */
 int cmtv_verdict_cache(cmtv_ctx* ctx, size_t max_entries);
 
+/* A node verifies commit after commit against the same validator set.
+ * cmtv_keyset_cache(ctx, max_sets) keeps the registered key sets
+ * (cmtv_register_keys) of up to max_sets validator sets, built the first time
+ * cmtv_verify_commit / cmtv_verify_commits see a set whose keys are all 32
+ * bytes; later commits of that set are verified by key index (no
+ * decompression of A, no doublings; same verdicts). Applies when the verdict
+ * cache is off. 0 disables and frees the cached sets. 512 KiB of HBM per key. */
+int cmtv_keyset_cache(cmtv_ctx* ctx, size_t max_sets);
+
 /* ------------------------------------------------------------ sr25519 */
 
 /* sr25519 (schnorrkel over ristretto255) batch verification, BASELINE

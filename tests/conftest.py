@@ -41,20 +41,23 @@ def gpu_ctx():
 
 @pytest.fixture(scope="session")
 def gpu_ctx_lane():
-    """A context that always uses the one-signature-per-lane kernel
-    (CMTV_QUAD_MAX=0), so small batches exercise both kernels."""
+    """A context that always uses the one-signature-per-lane kernels
+    (CMTV_QUAD_MAX=0, CMTV_KEYED_QUAD_MAX=0), so small batches exercise both
+    kernel shapes."""
     import torch
 
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from cometbft_amd import Context
 
-    old = os.environ.get("CMTV_QUAD_MAX")
-    os.environ["CMTV_QUAD_MAX"] = "0"
+    old = {k: os.environ.get(k) for k in ("CMTV_QUAD_MAX", "CMTV_KEYED_QUAD_MAX")}
+    for k in old:
+        os.environ[k] = "0"
     try:
         return Context(device=0)
     finally:
-        if old is None:
-            del os.environ["CMTV_QUAD_MAX"]
-        else:
-            os.environ["CMTV_QUAD_MAX"] = old
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v

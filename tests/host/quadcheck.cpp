@@ -11,6 +11,9 @@
 #include <vector>
 #include "../../cometbft_amd/csrc/quad.h"
 #include "../../cometbft_amd/csrc/sr25519_quad.h"
+#include "../../cometbft_amd/csrc/keyed_quad.h"
+#include <map>
+#include <string>
 
 using namespace cmtv;
 
@@ -70,6 +73,25 @@ struct HostBTab {
   }
 };
 
+struct HostScratch {
+  fe q[COMB_WINDOWS];
+  void store(int j, const fe& v) { q[j] = v; }
+  void load(int j, fe& v) const { v = q[j]; }
+};
+
+// comb of P (negated when neg), as the runtime's k_comb_build produces it
+static std::vector<uint32_t> host_comb(const uint32_t pkw[8], bool neg, bool* ok) {
+  std::vector<uint32_t> tab(COMB_TABLE_WORDS);
+  ge_p3 A, nA;
+  *ok = p3_frombytes(A, pkw);
+  cached_neg_point(nA, A);
+  for (int d = 1; d <= COMB_ENTRIES; d++) {
+    HostScratch sc;
+    comb_build_column(tab.data(), neg ? nA : A, d, sc);
+  }
+  return tab;
+}
+
 static void to_words(uint32_t* w, const uint8_t* b, int nw) {
   for (int i = 0; i < nw; i++) w[i] = b[4 * i] | (b[4 * i + 1] << 8) | (b[4 * i + 2] << 16) | ((uint32_t)b[4 * i + 3] << 24);
 }
@@ -77,6 +99,16 @@ static void to_words(uint32_t* w, const uint8_t* b, int nw) {
 int main(int argc, char** argv) {
   // argv[1] == "sr": sr25519 records { pk[32], sig[64], u32 mlen, msg } (no mode byte)
   const bool sr = argc > 1 && !strcmp(argv[1], "sr");
+  // argv[1] == "keyed": Ed25519 records, verified through registered-key combs (keyed_quad.h)
+  const bool keyed = argc > 1 && !strcmp(argv[1], "keyed");
+  std::vector<uint32_t> bcomb;
+  std::map<std::string, std::pair<bool, std::vector<uint32_t>>> combs;
+  if (keyed) {
+    uint32_t bw[8];
+    bool bok;
+    basepoint_words(bw);
+    bcomb = host_comb(bw, false, &bok);
+  }
   uint16_t prog[SR_PROGRAM_MAX];
   const int nops = sr_build_program(prog);
   HostBTab bt;
@@ -94,6 +126,18 @@ int main(int argc, char** argv) {
     uint32_t pkw[8], sigw[16];
     to_words(pkw, pk, 8);
     to_words(sigw, sig, 16);
+    bool kok = false;
+    const uint32_t* kt = nullptr;
+    if (keyed) {
+      auto it = combs.find(std::string((const char*)pk, 32));
+      if (it == combs.end()) {
+        bool o;
+        auto tab = host_comb(pkw, true, &o);
+        it = combs.emplace(std::string((const char*)pk, 32), std::make_pair(o, std::move(tab))).first;
+      }
+      kok = it->second.first;
+      kt = it->second.second.data();
+    }
     Exchange ex;
     bool res[4];
     std::vector<std::thread> th;
@@ -104,6 +148,9 @@ int main(int argc, char** argv) {
         ArrayStrobeState st;
         if (sr)
           res[l] = q_verify_sr(q, pkw, sigw, mp, mlen, prog, nops, st, bt, ta, tr);
+        else if (keyed)
+          res[l] = mode ? q_verify_keyed<MODE_ZIP215>(q, pkw, kok, sigw, mp, mlen, kt, bcomb.data())
+                        : q_verify_keyed<MODE_GO_STDLIB>(q, pkw, kok, sigw, mp, mlen, kt, bcomb.data());
         else
           res[l] = mode ? q_verify<MODE_ZIP215>(q, pkw, sigw, mp, mlen, bt, ta, tr)
                         : q_verify<MODE_GO_STDLIB>(q, pkw, sigw, mp, mlen, bt, ta, tr);

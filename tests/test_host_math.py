@@ -130,3 +130,15 @@ def test_half_scalar_decomposition():
         assert k1 < 2**134 and 0 < k2 < 2**134, j
         assert (k1 - s2 * k) % (8 * L) == 0, j
     assert wide <= 20, wide
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_keyed_quad_pipeline_matches_corpus(quadcheck, corpus, mode):
+    """keyed_quad.h (registered-key combs, one signature per DPP quad; four
+    host threads in lockstep) over the non-honest vectors and a slice of the
+    honest ones."""
+    idx = _keyed_subset(corpus)[::2]
+    got = _run(quadcheck, "keyed", corpus, idx, mode)
+    want = (corpus["go"] if mode == 0 else corpus["zip215"])[idx]
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(idx[int(i)], corpus["cats"][idx[int(i)]]) for i in bad[:10]]

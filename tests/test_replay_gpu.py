@@ -139,3 +139,46 @@ def test_verdict_cache_eviction(chain):
     tiny.verdict_cache(7)
     assert _blocksync(tiny, chain) == _blocksync(plain, chain)
     assert tiny.stats()["cache_entries"] == 7
+
+
+@pytest.mark.parametrize("kind", [0, 1, 2])
+def test_keyset_cache_matches_plain(chain, kind):
+    """cmtv_keyset_cache: commits of a registered validator set are verified
+    by key index (keyed_quad.h / keyed.h) with outcomes identical to the
+    generic path's, for single and cross-height calls."""
+    plain = Context(device=0)
+    keyed = Context(device=0)
+    keyed.keyset_cache(4)
+
+    def run(ctx):
+        out = []
+        for vals, bid, height, commit in chain:
+            if kind == 0:
+                out.append(_outcome(lambda: vals.verify_commit(TU.CHAIN_ID, bid, height, commit, ctx=ctx)))
+            elif kind == 1:
+                out.append(_outcome(lambda: vals.verify_commit_light(TU.CHAIN_ID, bid, height, commit, ctx=ctx)))
+            else:
+                out.append(_outcome(lambda: vals.verify_commit_light_trusting(TU.CHAIN_ID, commit, ctx=ctx)))
+        items = [(v, b if kind != 2 else None, h, c) for v, b, h, c in chain]
+        out += [_as_outcome(e) for e in T.verify_commits(kind, TU.CHAIN_ID, items, ctx=ctx)]
+        return out
+
+    assert run(keyed) == run(plain)
+
+
+def test_keyset_cache_bad_key_in_set(gpu_ctx):
+    """A validator set holding an undecodable key: that validator's signature
+    is invalid on the keyed path exactly as on the generic one."""
+    sv = TU.make_validator_set(gpu_ctx, 6)
+    commit, _, _ = TU.make_commit(gpu_ctx, sv, 77)
+    vals = sv.valset
+    bad = T.ValidatorSet([T.Validator(v.pub_key, v.voting_power) for v in vals.validators])
+    # y = 2 has no square root on edwards25519: the key does not decode
+    bad.validators[3] = T.Validator((2).to_bytes(32, "little"), bad.validators[3].voting_power)
+    plain = Context(device=0)
+    keyed = Context(device=0)
+    keyed.keyset_cache(2)
+    bid = TU.block_id_for_height(77)
+    a = _outcome(lambda: bad.verify_commit(TU.CHAIN_ID, bid, 77, commit, ctx=plain))
+    b = _outcome(lambda: bad.verify_commit(TU.CHAIN_ID, bid, 77, commit, ctx=keyed))
+    assert a == b and a is not None and a[0] == "ErrWrongSignature"

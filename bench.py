@@ -24,6 +24,10 @@ Extra fields on the JSON line:
   replay_150     -- blocksync replay per height (light + 2 x full VerifyCommit of
                     a 150-validator commit): plain, with the verdict cache, and
                     with cross-height batching (N=1 only)
+  replay_c3      -- configs[2]: 100k commits x 150 validators (15M signatures)
+                    sharded by height across the N ranks (strong scaling),
+                    registered-key kernel + RCCL bitmap all-gather, 1% flipped
+                    signatures checked exactly; the generic kernel beside it
   sr25519        -- configs[4]: 10k sr25519 verifications per step (N=1 only),
                     with the C restatement on the host cores as its CPU baseline
 Run: python bench.py [--gpus N --steps K --warmup W]
@@ -57,6 +61,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--latency-iters", type=int, default=200)
     ap.add_argument("--no-latency", action="store_true")
+    ap.add_argument("--no-c3", action="store_true", help="skip the configs[2] 15M-signature replay side line")
+    ap.add_argument("--c3-heights", type=int, default=100_000, help="configs[2] commits (150 validators each)")
     ap.add_argument("--no-sr25519", action="store_true", help="skip the configs[4] sr25519 side measurement")
     return ap.parse_args()
 
@@ -197,6 +203,116 @@ def replay_line(dev_index, heights=60, n_vals=150):
             "ms_per_height_plain": round(t_plain * 1e3, 4), "ms_per_height_verdict_cache": round(t_cached * 1e3, 4),
             "ms_per_height_cross_height_batch": round(t_batch * 1e3, 4),
             "note": "host API end to end; cross-height = one cmtv_verify_commits (VerifyCommit) over all heights"}
+
+
+def c3_line(ctx, dev, world, rank, mode, steps=3, n_heights=100_000, n_vals=150):
+    """configs[2]: blocksync / light-client replay of 100k commits x 150
+    validators (15M signatures, every message and signature distinct).
+    Contiguous height ranges are sharded across the ranks (strong scaling: the
+    total is fixed); each rank registers the 150 keys once (cmtv_register_keys)
+    and verifies its shard by key index (cmtv_verify_ed25519_indexed_device,
+    inputs resident in HBM); the per-rank verdict bitmaps are all-gathered over
+    RCCL. 1% of the signatures (seed 42, global indices) carry one flipped bit
+    and must be rejected: the gathered verdicts are checked exactly. The
+    generic kernel (A decoded per signature) is timed on the same shard."""
+    import torch
+    import torch.distributed as dist
+    from cometbft_amd import parallel as P
+    from cometbft_amd import testutil as TU
+
+    per_h = -(-n_heights // world)
+    lo, hi = min(n_heights, rank * per_h), min(n_heights, (rank + 1) * per_h)
+    nh, n, total = hi - lo, (hi - lo) * n_vals, n_heights * n_vals
+    t_gen = time.perf_counter()
+    sv = TU.make_validator_set(ctx, n_vals)
+    ks = ctx.register_keys(sv.pubkeys)
+    m, off = TU.replay_messages(1 + lo, nh, n_vals)
+    kidx = np.tile(np.arange(n_vals, dtype=np.uint32), nh)
+    sig = ctx.sign(sv.seeds, m, off, kidx)
+    rng = np.random.default_rng(42)
+    flip = rng.choice(total, total // 100, replace=False)
+    bit = rng.integers(0, 512, flip.size)
+    g0 = lo * n_vals
+
+    def expected(r):
+        a = min(n_heights, r * per_h) * n_vals
+        b = min(n_heights, (r + 1) * per_h) * n_vals
+        e = np.ones(b - a, np.uint8)
+        e[flip[(flip >= a) & (flip < b)] - a] = 0
+        return e
+
+    sel = (flip >= g0) & (flip < g0 + n)
+    li, lb = flip[sel] - g0, bit[sel]
+    sig[li, lb // 8] ^= (1 << (lb % 8)).astype(np.uint8)
+    t_gen = time.perf_counter() - t_gen
+
+    words = -(-per_h * n_vals // 64)
+    d_idx = torch.from_numpy(kidx).to(dev)
+    d_sig = torch.from_numpy(sig).to(dev)
+    d_msg = torch.from_numpy(m).to(dev)
+    d_off = torch.from_numpy(off.view(np.int32)).to(dev)
+    d_valid = torch.zeros(max(n, 1), dtype=torch.uint8, device=dev)
+    d_bm = torch.zeros(words, dtype=torch.int64, device=dev)
+    d_all = torch.zeros(world * words, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sptr = stream.cuda_stream
+    del m, sig
+
+    def timed(fn, k):
+        fn()  # warm-up
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t = time.perf_counter()
+        for _ in range(k):
+            fn()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t
+        if world > 1:
+            x = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(x, op=dist.ReduceOp.MAX)
+            el = float(x.item())
+        return el / k
+
+    def keyed():
+        ctx.verify_indexed_device(ks, n, d_idx.data_ptr(), d_sig.data_ptr(), d_msg.data_ptr(), d_off.data_ptr(),
+                                  mode, d_valid.data_ptr(), d_bm.data_ptr(), sptr)
+        if world > 1:
+            dist.all_gather_into_tensor(d_all, d_bm)
+        else:
+            d_all.copy_(d_bm)
+
+    t_keyed = timed(keyed, steps)
+    ok = np.array_equal(d_valid[:n].cpu().numpy(), expected(rank))
+    allw = d_all.cpu().numpy().view(np.uint64).reshape(world, words)
+    for r in range(world):
+        e = expected(r)
+        ok = ok and np.array_equal(P.unpack_bitmap(allw[r], e.size), e)
+    del d_idx
+    d_pk = torch.from_numpy(np.ascontiguousarray(sv.pubkeys[kidx])).to(dev)
+
+    def generic():
+        ctx.verify_device(n, d_pk.data_ptr(), d_sig.data_ptr(), d_msg.data_ptr(), d_off.data_ptr(), mode,
+                          d_valid.data_ptr(), d_bm.data_ptr(), sptr)
+
+    t_generic = timed(generic, 1)
+    ok = ok and np.array_equal(d_valid[:n].cpu().numpy(), expected(rank))
+    if world > 1:
+        x = torch.tensor([0.0 if ok else 1.0], dtype=torch.float64, device=dev)
+        dist.all_reduce(x, op=dist.ReduceOp.MAX)
+        ok = float(x.item()) == 0.0
+    del d_pk, d_sig, d_msg, d_off, d_valid
+    torch.cuda.empty_cache()
+    return {"workload": f"configs[2]: {n_heights} commits x {n_vals} validators = {total} signatures, "
+                        f"sharded by height over {world} GPU(s), 1% bit-flipped (seed 42)",
+            "scaling": "strong", "sigs_per_gpu": n, "value": round(total / t_keyed, 1), "unit": "verifs/s",
+            "ms_per_pass": round(t_keyed * 1e3, 3), "steps": steps,
+            "path": "registered keys (cmtv_verify_ed25519_indexed_device) + RCCL all-gather of bitmaps",
+            "generic_value": round(total / t_generic, 1), "generic_ms_per_pass": round(t_generic * 1e3, 3),
+            "verdicts_ok": bool(ok), "setup_s": round(t_gen, 2)}
 
 
 def _cpu_model():
@@ -360,6 +476,8 @@ def main():
     else:
         ok = ok_local
 
+    c3 = None if args.no_c3 else c3_line(ctx, dev, world, rank, mode, n_heights=args.c3_heights)
+
     if rank == 0:
         total = world * n * args.steps
         value = total / elapsed
@@ -395,11 +513,13 @@ def main():
             line["replay_150"] = replay_line(local)
         if not args.no_sr25519 and world == 1:
             line["sr25519"] = sr25519_line(ctx, dev, 10_000, 20, args.cpu_seconds / 4, not args.no_cpu_baseline)
+        if c3 is not None:
+            line["replay_c3"] = c3
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
-    if not ok:
+    if not ok or (c3 is not None and not c3["verdicts_ok"]):
         sys.exit(3)
 
 

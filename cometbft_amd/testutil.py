@@ -87,3 +87,74 @@ def make_commit(ctx: Context, sv: SyntheticValidators, height: int, round_: int 
         else:
             css.append(CommitSig(flags[i], sv.valset.validators[i].address, timestamp(height, i), bytes(sigs[i])))
     return Commit(height, round_, bid, css), msgs, sigs
+
+
+_TEMPLATE_HEIGHT = 1000
+
+
+def _varint5(v: np.ndarray) -> np.ndarray:
+    """5-byte protobuf varints of v (2^28 <= v < 2^35), shape (len(v), 5)."""
+    v = v.astype(np.uint64)
+    out = np.empty((v.shape[0], 5), np.uint8)
+    for k in range(5):
+        b = (v >> np.uint64(7 * k)) & np.uint64(0x7F)
+        out[:, k] = (b | np.uint64(0x80 if k < 4 else 0)).astype(np.uint8)
+    return out
+
+
+def replay_messages(h0: int, n_heights: int, n_vals: int, chunk: int = 8192):
+    """Sign-bytes of the synthetic commits at heights h0 .. h0+n_heights-1
+    (n_vals validators each, all BlockIDFlagCommit), in (height, validator)
+    order, as (msg u8, msg_off u32[n+1]) -- the same bytes as concatenating
+    commit_messages(n_vals, h) over h (tests/test_testutil.py), built without
+    calling the encoder per message so configs[2]'s 15M messages take seconds.
+    Like pack_messages, msg carries one trailing zero byte.
+
+    Across heights a validator's CanonicalVote differs only in the sfixed64
+    height, the two 32-byte BlockID hashes and the timestamp's seconds (a
+    5-byte varint for every height here), all at fixed offsets: the encoder's
+    output at one template height is patched per height."""
+    assert n_vals <= 1_000_000 and h0 >= 1 and EPOCH_2023 + h0 + n_heights < 2**35
+    th = _TEMPLATE_HEIGHT
+    tmpl = commit_messages(n_vals, th)
+    tbid = block_id_for_height(th)
+    lens = np.array([len(t) for t in tmpl], np.int64)
+    lh = int(lens.sum())
+    base = np.frombuffer(b"".join(tmpl), np.uint8)
+    starts = np.concatenate([[0], np.cumsum(lens)[:-1]])
+
+    def where(t: bytes, needle: bytes) -> int:
+        p = t.find(needle)
+        assert p >= 0 and t.find(needle, p + 1) < 0, "template field not unique"
+        return p
+
+    # per validator: byte offsets (in the height's block) of its height,
+    # block hash, parts hash and seconds fields
+    fields = []
+    for i, t in enumerate(tmpl):
+        sec, _ = timestamp(th, i)
+        assert sec == EPOCH_2023 + th  # i < 1e6 microseconds
+        s = int(starts[i])
+        fields.append((s + where(t, int(th).to_bytes(8, "little")), s + where(t, tbid.hash),
+                       s + where(t, tbid.part_set_header.hash), s + where(t, bytes(_varint5(np.array([sec]))[0]))))
+
+    msg = np.zeros(n_heights * lh + 1, np.uint8)  # + pad byte, as pack_messages
+    for c0 in range(0, n_heights, chunk):
+        c1 = min(n_heights, c0 + chunk)
+        hs = np.arange(h0 + c0, h0 + c1, dtype=np.int64)
+        hb = hs.astype("<i8").view(np.uint8).reshape(-1, 8)
+        bh = np.frombuffer(b"".join(hashlib.sha256(b"block%d" % h).digest() for h in hs), np.uint8).reshape(-1, 32)
+        ph = np.frombuffer(b"".join(hashlib.sha256(b"parts%d" % h).digest() for h in hs), np.uint8).reshape(-1, 32)
+        sb = _varint5(EPOCH_2023 + hs)
+        blk = msg[c0 * lh:c1 * lh].reshape(c1 - c0, lh)
+        blk[:] = base
+        for fh, fb, fp, fs in fields:
+            blk[:, fh:fh + 8] = hb
+            blk[:, fb:fb + 32] = bh
+            blk[:, fp:fp + 32] = ph
+            blk[:, fs:fs + 5] = sb
+    off = np.empty(n_heights * n_vals + 1, np.int64)
+    off[:-1] = (np.arange(n_heights, dtype=np.int64)[:, None] * lh + starts[None, :]).reshape(-1)
+    off[-1] = n_heights * lh
+    assert off[-1] < 2**32
+    return msg, off.astype(np.uint32)

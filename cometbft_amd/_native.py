@@ -40,7 +40,8 @@ COMMIT_PANIC_UNKNOWN_FLAG = 9
 
 # every symbol include/cmtverify.h declares (checked by tests/test_abi.py)
 EXPORTS = (
-    "cmtv_open", "cmtv_close", "cmtv_strerror", "cmtv_abi_version", "cmtv_stats_get", "cmtv_stream",
+    "cmtv_open", "cmtv_open_devices", "cmtv_device_count", "cmtv_device_ordinal", "cmtv_device_stream", "cmtv_sync",
+    "cmtv_verify_ed25519_sharded_device", "cmtv_verify_ed25519_indexed_sharded_device", "cmtv_close", "cmtv_strerror", "cmtv_abi_version", "cmtv_stats_get", "cmtv_stream",
     "cmtv_verify_ed25519", "cmtv_verify_ed25519_device", "cmtv_verify_sr25519", "cmtv_verify_sr25519_device",
     "cmtv_register_keys", "cmtv_keyset_free", "cmtv_keyset_len", "cmtv_verify_ed25519_indexed",
     "cmtv_verify_ed25519_indexed_device",
@@ -65,7 +66,9 @@ class cmtv_stats(ctypes.Structure):
     _fields_ = [("calls", ctypes.c_uint64), ("signatures", ctypes.c_uint64), ("invalid", ctypes.c_uint64),
                 ("kernel_launches", ctypes.c_uint64), ("device_ms", ctypes.c_double),
                 ("last_kernel_ms", ctypes.c_double), ("cache_hits", ctypes.c_uint64),
-                ("cache_entries", ctypes.c_uint64)]
+                ("cache_entries", ctypes.c_uint64), ("keyed_launches", ctypes.c_uint64),
+                ("sharded_calls", ctypes.c_uint64), ("gathers", ctypes.c_uint64),
+                ("faults_injected", ctypes.c_uint64), ("n_devices", ctypes.c_uint32), ("rccl", ctypes.c_uint32)]
 
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -109,6 +112,22 @@ def lib() -> ctypes.CDLL:
     u32p = ctypes.POINTER(ctypes.c_uint32)
     L.cmtv_open.argtypes = [ctypes.POINTER(cmtv_config), ctypes.POINTER(vp)]
     L.cmtv_open.restype = ctypes.c_int
+    vpp = ctypes.POINTER(vp)
+    szp = ctypes.POINTER(sz)
+    L.cmtv_open_devices.argtypes = [ctypes.POINTER(cmtv_config), ctypes.POINTER(i32), sz, ctypes.POINTER(vp)]
+    L.cmtv_open_devices.restype = ctypes.c_int
+    L.cmtv_device_count.argtypes = [vp]
+    L.cmtv_device_count.restype = ctypes.c_int
+    L.cmtv_device_ordinal.argtypes = [vp, ctypes.c_int]
+    L.cmtv_device_ordinal.restype = ctypes.c_int
+    L.cmtv_device_stream.argtypes = [vp, ctypes.c_int]
+    L.cmtv_device_stream.restype = vp
+    L.cmtv_sync.argtypes = [vp]
+    L.cmtv_sync.restype = ctypes.c_int
+    L.cmtv_verify_ed25519_sharded_device.argtypes = [vp, szp, vpp, vpp, vpp, vpp, u32, vpp, vpp, szp]
+    L.cmtv_verify_ed25519_sharded_device.restype = ctypes.c_int
+    L.cmtv_verify_ed25519_indexed_sharded_device.argtypes = [vp, vp, szp, vpp, vpp, vpp, vpp, u32, vpp, vpp, szp]
+    L.cmtv_verify_ed25519_indexed_sharded_device.restype = ctypes.c_int
     L.cmtv_close.argtypes = [vp]
     L.cmtv_close.restype = None
     L.cmtv_strerror.argtypes = [ctypes.c_int]

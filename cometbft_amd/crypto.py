@@ -32,15 +32,60 @@ def _u8(a: np.ndarray):
 
 
 class Context:
-    """One device context (stream, fixed-base table, staging buffers)."""
+    """A verification context (cmtv_open / cmtv_open_devices): per device a
+    stream, fixed-base tables and staging buffers.
 
-    def __init__(self, device: int = -1, default_mode: int = MODE_GO_STDLIB):
+    devices=None opens one device (`device`, -1 = the current one); a list of
+    HIP ordinals opens one context over all of them (batches are sharded and
+    their verdict bitmaps all-gathered over RCCL); devices=[] takes the list
+    from CMTVERIFY_DEVICES, or every visible gfx950 device."""
+
+    def __init__(self, device: int = -1, default_mode: int = MODE_GO_STDLIB, devices: Sequence[int] | None = None):
         L = N.lib()
         cfg = N.cmtv_config(device=device, default_mode=default_mode, flags=0, reserved=0)
         h = ctypes.c_void_p()
-        N.check(L.cmtv_open(ctypes.byref(cfg), ctypes.byref(h)), "cmtv_open")
+        if devices is None:
+            N.check(L.cmtv_open(ctypes.byref(cfg), ctypes.byref(h)), "cmtv_open")
+        else:
+            arr = (ctypes.c_int32 * max(len(devices), 1))(*devices)
+            N.check(L.cmtv_open_devices(ctypes.byref(cfg), arr, len(devices), ctypes.byref(h)), "cmtv_open_devices")
         self._h = h
         self.default_mode = default_mode
+
+    @property
+    def n_devices(self) -> int:
+        return N.lib().cmtv_device_count(self._h)
+
+    def device_ordinal(self, g: int) -> int:
+        return N.lib().cmtv_device_ordinal(self._h, g)
+
+    def device_stream(self, g: int) -> int:
+        return N.lib().cmtv_device_stream(self._h, g) or 0
+
+    def sync(self) -> None:
+        N.check(N.lib().cmtv_sync(self._h), "cmtv_sync")
+
+    def verify_sharded_device(self, n_shard: Sequence[int], d_pk, d_sig, d_msg, d_off, mode: int, d_bitmap_all,
+                              d_valid=None, keys: "KeySet | None" = None) -> int:
+        """cmtv_verify_ed25519[_indexed]_sharded_device: shard g's device
+        pointers (ints) on the context's g-th device (d_pk holds key indices
+        when `keys` is given); returns W, the bitmap words per shard. The
+        gathered bitmap on every device is G x W words. Non-blocking."""
+        G = len(n_shard)
+        vp = ctypes.c_void_p
+        arr = lambda xs: (vp * G)(*[vp(x) if x else None for x in xs])  # noqa: E731
+        ns = (ctypes.c_size_t * G)(*n_shard)
+        w = ctypes.c_size_t(0)
+        dv = arr(d_valid) if d_valid is not None else None
+        if keys is None:
+            rc = N.lib().cmtv_verify_ed25519_sharded_device(self._h, ns, arr(d_pk), arr(d_sig), arr(d_msg), arr(d_off),
+                                                            mode, dv, arr(d_bitmap_all), ctypes.byref(w))
+        else:
+            rc = N.lib().cmtv_verify_ed25519_indexed_sharded_device(self._h, keys.handle, ns, arr(d_pk), arr(d_sig),
+                                                                    arr(d_msg), arr(d_off), mode, dv,
+                                                                    arr(d_bitmap_all), ctypes.byref(w))
+        N.check(rc, "cmtv_verify_ed25519_sharded_device")
+        return w.value
 
     @property
     def handle(self):

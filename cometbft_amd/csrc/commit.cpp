@@ -149,14 +149,28 @@ void vote_prefix(std::string& body, int32_t vtype, int64_t height, int32_t round
   put_canonical_block_id(body, bid);
 }
 
+// Two validator sets hold the same keys (so one registered key set serves
+// both): the same arrays, or equal key bytes.
+bool same_keys(const cmtv_valset* a, const cmtv_valset* b) {
+  if (a == b) return true;
+  if (a->n_vals != b->n_vals) return false;
+  if (a->pubkeys == b->pubkeys && a->pk_off == b->pk_off) return true;
+  for (uint32_t i = 0; i <= a->n_vals; i++)
+    if (a->pk_off[i] != b->pk_off[i]) return false;
+  const uint32_t bytes = a->pk_off[a->n_vals];
+  return bytes == 0 || std::memcmp(a->pubkeys, b->pubkeys, bytes) == 0;
+}
+
 // Signatures of one or more commits, gathered for one device batch. Host
 // mode: sign-bytes encoded here (needed for the verdict cache's keys).
 // Templated mode: one SbTemplate per commit and
 // (flag, seconds, nanos) per signature; the device writes the sign-bytes.
+// Message offsets are 64-bit here: a cross-height batch can exceed 4 GiB of
+// sign-bytes, and batch_verify splits it into device batches below 2 GiB.
 struct SigBatch {
   bool templated = false;
   std::vector<uint8_t> pk, sg, msgs, len_ok;
-  std::vector<uint32_t> off{0};
+  std::vector<uint64_t> off{0};
   std::string sb;
   // templated
   std::vector<cmtv::SbTemplate> tmpls;
@@ -166,9 +180,10 @@ struct SigBatch {
   std::vector<int32_t> tnanos;
   const cmtv_commit* cur = nullptr;  // commit of the last template
   // validator indices, for registered-key verification when every signature
-  // comes from one validator set (cmtv_keyset_cache)
+  // comes from validator sets with the same keys (cmtv_keyset_cache)
   std::vector<uint32_t> kidx;
   const cmtv_valset* vs = nullptr;
+  const cmtv_valset* last_vs = nullptr;
   bool one_vs = true;
 
   size_t size() const { return off.size() - 1; }
@@ -200,8 +215,11 @@ struct SigBatch {
            size_t chain_id_len, const cmtv_commit* c, uint32_t idx) {
     static const cmtv_block_id empty{};
     const uint8_t* key = vals->pubkeys + vals->pk_off[vi];
-    if (!vs) vs = vals;
-    one_vs = one_vs && vs == vals;
+    if (!vs) vs = last_vs = vals;
+    if (one_vs && vals != last_vs) {  // compare each new set once
+      one_vs = same_keys(vs, vals);
+      last_vs = vals;
+    }
     kidx.push_back(vi);
     pk.insert(pk.end(), key, key + 32);
     const size_t o = sg.size();
@@ -222,7 +240,7 @@ struct SigBatch {
     vote_sign_bytes(sb, chain_id, chain_id_len, kPrecommit, c->height, c->round, for_block ? &c->block_id : &empty,
                     c->ts_seconds[idx], c->ts_nanos[idx]);
     msgs.insert(msgs.end(), sb.begin(), sb.end());
-    off.push_back((uint32_t)msgs.size());
+    off.push_back(msgs.size());
   }
 };
 
@@ -299,14 +317,27 @@ void job_prepare(CommitJob& J, SigBatch& B, bool prefetch) {
       J.early = J.fail(CMTV_COMMIT_ERR_TRUST_LEVEL, -1, "trustLevel has zero Denominator");
       return;
     }
-    __int128 prod = (__int128)total * (__int128)(int64_t)J.trust_num;
-    if (prod > INT64_MAX || prod < INT64_MIN) {
+    // safeMul (types/validator_set.go:1086-1105) with Go's wrapping int64
+    // arithmetic: -MinInt64 stays MinInt64, MaxInt64 / MinInt64 == 0
+    const int64_t a = total, b = (int64_t)J.trust_num;
+    int64_t prod = 0;
+    bool overflow = false;
+    if (a != 0 && b != 0) {
+      const int64_t abs_b = b < 0 ? (int64_t)(0 - (uint64_t)b) : b;
+      const int64_t abs_a = a < 0 ? (int64_t)(0 - (uint64_t)a) : a;
+      overflow = abs_a > INT64_MAX / abs_b;
+      if (!overflow) prod = (int64_t)((uint64_t)a * (uint64_t)b);
+    }
+    if (overflow) {
       J.early = J.fail(CMTV_COMMIT_ERR_TRUST_LEVEL, -1,
                        "int64 overflow while calculating voting power needed. please provide smaller trustLevel "
                        "numerator");
       return;
     }
-    J.needed = (int64_t)prod / (int64_t)J.trust_den;
+    // Go: MinInt64 / -1 == MinInt64 (no trap); the zero denominator is
+    // rejected above
+    const int64_t den = (int64_t)J.trust_den;
+    J.needed = (den == -1) ? (int64_t)(0 - (uint64_t)prod) : prod / den;
     for (uint32_t i = 0; i < vals->n_vals; i++)
       J.by_addr.emplace(std::string(reinterpret_cast<const char*>(vals->addrs + 20 * (size_t)i), 20), i);
   } else {
@@ -379,29 +410,48 @@ void job_prepare(CommitJob& J, SigBatch& B, bool prefetch) {
   }
 }
 
+// Largest message span of one device batch (offsets are 32-bit on the
+// device); CMTV_MAX_BATCH_MSG_BYTES lowers it (tests of the split).
+uint64_t max_batch_msg_bytes() {
+  const char* v = std::getenv("CMTV_MAX_BATCH_MSG_BYTES");
+  const uint64_t x = v ? std::strtoull(v, nullptr, 10) : 0;
+  return (x && x < (1ull << 31)) ? x : (1ull << 31);
+}
+
 int batch_verify(cmtv_ctx* ctx, SigBatch& B, uint32_t mode, std::vector<uint8_t>& valid) {
   const size_t m = B.size();
   valid.assign(m, 0);
   if (!m) return CMTV_OK;
-  int rc;
-  if (B.templated) {
-    // one validator set of 32-byte keys: its registered key set (built on
-    // first use by cmtv_keyset_cache) replaces decompression and doublings
-    const cmtv_keyset* ks = nullptr;
-    if (cmtv::keyset_cache_enabled(ctx) && B.one_vs && B.vs->n_vals) {
-      bool packed = true;
-      for (uint32_t i = 0; i <= B.vs->n_vals && packed; i++) packed = B.vs->pk_off[i] == 32 * i;
-      if (packed) ks = cmtv::keyset_for_locked(ctx, B.vs->pubkeys, B.vs->n_vals);
-    }
-    rc = cmtv::verify_templated_locked(ctx, m, B.pk.data(), B.sg.data(), B.off.data(), B.tmpls.data(), B.tmpls.size(),
-                                       B.blob.data(), B.blob.size(), B.tidx.data(), B.tflag.data(), B.tsec.data(),
-                                       B.tnanos.data(), mode, valid.data(), ks, B.kidx.data());
-  } else {
-    if (B.msgs.empty()) B.msgs.push_back(0);
-    rc = cmtv::verify_host_locked(ctx, m, B.pk.data(), B.sg.data(), B.msgs.data(), B.off.data(), mode, valid.data(),
-                                  nullptr);
+  // one validator set of 32-byte keys: its registered key set (built on
+  // first use by cmtv_keyset_cache) replaces decompression and doublings
+  const cmtv_keyset* ks = nullptr;
+  if (B.templated && cmtv::keyset_cache_enabled(ctx) && B.one_vs && B.vs->n_vals) {
+    bool packed = true;
+    for (uint32_t i = 0; i <= B.vs->n_vals && packed; i++) packed = B.vs->pk_off[i] == 32 * i;
+    if (packed) ks = cmtv::keyset_for_locked(ctx, B.vs->pubkeys, B.vs->n_vals);
   }
-  if (rc != CMTV_OK) return rc;
+  if (!B.templated && B.msgs.empty()) B.msgs.push_back(0);
+  std::vector<uint32_t> off32;
+  const uint64_t kMaxBatchMsgBytes = max_batch_msg_bytes();
+  for (size_t a = 0; a < m;) {
+    // [a, b): the longest run whose sign-bytes span < 2 GiB
+    size_t b = a + 1;
+    while (b < m && B.off[b + 1] - B.off[a] < kMaxBatchMsgBytes) b++;
+    if (B.off[b] - B.off[a] >= kMaxBatchMsgBytes) return CMTV_EINVAL;  // one message of >= 2 GiB
+    off32.resize(b - a + 1);
+    for (size_t i = a; i <= b; i++) off32[i - a] = (uint32_t)(B.off[i] - B.off[a]);
+    int rc;
+    if (B.templated)
+      rc = cmtv::verify_templated_locked(ctx, b - a, ks ? nullptr : B.pk.data() + 32 * a, B.sg.data() + 64 * a,
+                                         off32.data(), B.tmpls.data(), B.tmpls.size(), B.blob.data(), B.blob.size(),
+                                         B.tidx.data() + a, B.tflag.data() + a, B.tsec.data() + a,
+                                         B.tnanos.data() + a, mode, valid.data() + a, ks, B.kidx.data() + a);
+    else
+      rc = cmtv::verify_host_locked(ctx, b - a, B.pk.data() + 32 * a, B.sg.data() + 64 * a,
+                                    B.msgs.data() + B.off[a], off32.data(), mode, valid.data() + a, nullptr);
+    if (rc != CMTV_OK) return rc;
+    a = b;
+  }
   for (size_t j = 0; j < m; j++)
     if (!B.len_ok[j]) valid[j] = 0;  // crypto/ed25519/ed25519.go:150
   return CMTV_OK;

@@ -1,19 +1,26 @@
-// runtime.cpp -- libcmtverify host runtime: contexts, streams, pinned staging,
-// chunked kernel launches and the C ABI of include/cmtverify.h.
+// runtime.cpp -- libcmtverify host runtime: contexts over one or more
+// devices, streams, pinned staging, sharded kernel launches, the RCCL bitmap
+// all-gather and the C ABI of include/cmtverify.h.
 //
-// One context = one device + one HIP stream + the device-resident fixed-base
-// table + growable device/pinned buffers. Calls on a context are serialised
-// by its mutex and start with hipSetDevice (cgo callers migrate threads).
-// There is no CPU verification path: if the device is unusable every call
-// fails with a negative code and the caller decides what to do.
+// A context = one or more devices, each with its own HIP stream, fixed-base
+// tables, growable device / pinned buffers and lane-kernel scratch. Calls on a
+// context are serialised by its mutex and set the device they touch (cgo
+// callers migrate threads). Host-buffer batches are split into contiguous
+// 64-aligned shards, one per device, and the shards' verdict bitmaps are
+// all-gathered over RCCL (xGMI) when the context has several devices
+// (SURVEY.md 8e). There is no CPU verification path: if a device is unusable
+// every call fails with a negative code and the caller decides what to do.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <mutex>
 #include <new>
+#include <random>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -23,6 +30,7 @@
 #include "merlin.h"
 #include "signbytes.h"
 #include "runtime_internal.h"
+#include "shard.h"
 
 namespace {
 
@@ -32,6 +40,9 @@ constexpr uint32_t kChunk = 1u << 18;  // signatures per launch (A-table scratch
 constexpr size_t kQuadMaxDefault = 40000;
 // the same crossover for registered-key verification (env CMTV_KEYED_QUAD_MAX)
 constexpr size_t kKeyedQuadMaxDefault = 16384;
+// signatures per device below which a batch is not sharded (env CMTV_SHARD_MIN)
+constexpr size_t kShardMinDefault = 8192;
+constexpr int kMaxDevices = 64;
 
 struct DevBuf {
   void* p = nullptr;
@@ -75,9 +86,54 @@ struct HostBuf {
   }
 };
 
+// SipHash-2-4 (Aumasson & Bernstein), keyed per process: the verdict cache's
+// index, so a peer cannot aim many entries at one bucket.
+uint64_t rotl(uint64_t x, int b) { return (x << b) | (x >> (64 - b)); }
+
+struct SipKey {
+  uint64_t k0, k1;
+  SipKey() {
+    std::random_device rd;
+    k0 = ((uint64_t)rd() << 32) ^ rd();
+    k1 = ((uint64_t)rd() << 32) ^ rd();
+  }
+};
+
+uint64_t siphash24(const SipKey& key, const uint8_t* p, size_t n) {
+  uint64_t v0 = 0x736f6d6570736575ull ^ key.k0, v1 = 0x646f72616e646f6dull ^ key.k1;
+  uint64_t v2 = 0x6c7967656e657261ull ^ key.k0, v3 = 0x7465646279746573ull ^ key.k1;
+  auto round = [&] {
+    v0 += v1; v1 = rotl(v1, 13); v1 ^= v0; v0 = rotl(v0, 32);
+    v2 += v3; v3 = rotl(v3, 16); v3 ^= v2;
+    v0 += v3; v3 = rotl(v3, 21); v3 ^= v0;
+    v2 += v1; v1 = rotl(v1, 17); v1 ^= v2; v2 = rotl(v2, 32);
+  };
+  const size_t full = n & ~(size_t)7;
+  for (size_t i = 0; i < full; i += 8) {
+    uint64_t m;
+    std::memcpy(&m, p + i, 8);
+    v3 ^= m;
+    round();
+    round();
+    v0 ^= m;
+  }
+  uint64_t b = (uint64_t)n << 56;
+  for (size_t i = full; i < n; i++) b |= (uint64_t)p[i] << (8 * (i - full));
+  v3 ^= b;
+  round();
+  round();
+  v0 ^= b;
+  v2 ^= 0xff;
+  round();
+  round();
+  round();
+  round();
+  return v0 ^ v1 ^ v2 ^ v3;
+}
+
 // Verdict cache (cmtv_verdict_cache): a ring of the last `cap` verdicts,
-// indexed by a 64-bit hash of (mode, signature); a hit also compares the full
-// key bytes (mode, pk, sig, msg), so it returns exactly the device verdict.
+// indexed by a keyed hash of the full key (scheme + mode, pk, sig, msg); a hit
+// also compares the key bytes, so it returns exactly the device verdict.
 struct VerdictCache {
   struct Entry {
     std::string key;
@@ -85,20 +141,14 @@ struct VerdictCache {
     uint8_t verdict = 0;
     bool used = false;
   };
+  SipKey sk;
   size_t cap = 0;
   size_t next = 0;
   std::vector<Entry> ring;
   std::unordered_multimap<uint64_t, size_t> index;
 
-  static uint64_t hash(uint32_t mode, const uint8_t* sig) {
-    uint64_t h = 0x9E3779B97F4A7C15ull ^ mode;
-    for (int i = 0; i < 8; i++) {
-      uint64_t w;
-      std::memcpy(&w, sig + 8 * i, 8);
-      h = (h ^ w) * 0xBF58476D1CE4E5B9ull;
-      h ^= h >> 31;
-    }
-    return h;
+  uint64_t hash(const std::string& k) const {
+    return siphash24(sk, reinterpret_cast<const uint8_t*>(k.data()), k.size());
   }
   static void make_key(std::string& k, uint32_t mode, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
                        size_t mlen) {
@@ -143,38 +193,154 @@ struct VerdictCache {
   size_t size() const { return index.size(); }
 };
 
+// ---------------------------------------------------------------- RCCL (dlopen)
+// Resolved at run time with RTLD_LOCAL so the library loads (and a context
+// falls back to peer copies) where librccl is absent, and so RCCL's symbols
+// never interpose on a host process that carries its own copy.
+typedef void* ncclComm_t;
+typedef int ncclResult_t;
+constexpr int kNcclUint64 = 5;  // ncclDataType_t ncclUint64 (rccl.h)
+
+struct Rccl {
+  bool ok = false;
+  ncclResult_t (*CommInitAll)(ncclComm_t*, int, const int*) = nullptr;
+  ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*AllGather)(const void*, void*, size_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*GroupStart)() = nullptr;
+  ncclResult_t (*GroupEnd)() = nullptr;
+};
+
+const Rccl& rccl() {
+  static Rccl r = [] {
+    Rccl x;
+    void* h = nullptr;
+    for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
+      if ((h = dlopen(name, RTLD_NOW | RTLD_LOCAL)) != nullptr) break;
+    if (!h) return x;
+    x.CommInitAll = reinterpret_cast<decltype(x.CommInitAll)>(dlsym(h, "ncclCommInitAll"));
+    x.CommDestroy = reinterpret_cast<decltype(x.CommDestroy)>(dlsym(h, "ncclCommDestroy"));
+    x.AllGather = reinterpret_cast<decltype(x.AllGather)>(dlsym(h, "ncclAllGather"));
+    x.GroupStart = reinterpret_cast<decltype(x.GroupStart)>(dlsym(h, "ncclGroupStart"));
+    x.GroupEnd = reinterpret_cast<decltype(x.GroupEnd)>(dlsym(h, "ncclGroupEnd"));
+    x.ok = x.CommInitAll && x.CommDestroy && x.AllGather && x.GroupStart && x.GroupEnd;
+    return x;
+  }();
+  return r;
+}
+
+// Kernel timing: HIP event pairs recorded around each verification on its
+// stream, harvested without blocking once complete (so device-resident calls
+// stay asynchronous).
+struct Timing {
+  struct Pair {
+    hipEvent_t a = nullptr, b = nullptr;
+  };
+  std::vector<Pair> free_;
+  std::deque<Pair> pending;
+  hipError_t begin(Pair& p, hipStream_t s) {
+    if (free_.empty()) {
+      Pair q;
+      hipError_t e = hipEventCreate(&q.a);
+      if (e == hipSuccess) e = hipEventCreate(&q.b);
+      if (e != hipSuccess) return e;
+      free_.push_back(q);
+    }
+    p = free_.back();
+    free_.pop_back();
+    hipError_t e = hipEventRecord(p.a, s);
+    if (e != hipSuccess) free_.push_back(p);
+    return e;
+  }
+  hipError_t end(const Pair& p, hipStream_t s) {
+    hipError_t e = hipEventRecord(p.b, s);
+    if (e != hipSuccess) {
+      free_.push_back(p);
+      return e;
+    }
+    pending.push_back(p);
+    return hipSuccess;
+  }
+  void abandon(const Pair& p) { free_.push_back(p); }
+  // completed pairs -> stats; blocking waits for all of them
+  void harvest(cmtv_stats& st, bool blocking) {
+    while (!pending.empty()) {
+      Pair p = pending.front();
+      if (blocking || pending.size() > 64) {
+        if (hipEventSynchronize(p.b) != hipSuccess) break;
+      } else if (hipEventQuery(p.b) != hipSuccess) {
+        break;
+      }
+      float ms = 0.f;
+      if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+        st.last_kernel_ms = ms;
+        st.device_ms += ms;
+      }
+      pending.pop_front();
+      free_.push_back(p);
+    }
+  }
+  void release() {
+    for (auto& p : pending) free_.push_back(p);
+    pending.clear();
+    for (auto& p : free_) {
+      if (p.a) (void)hipEventDestroy(p.a);
+      if (p.b) (void)hipEventDestroy(p.b);
+    }
+    free_.clear();
+  }
+};
+
 }  // namespace
 
-struct cmtv_ctx {
-  int device = 0;
-  uint32_t default_mode = CMTV_MODE_GO_STDLIB;
+// Per-device state of a context.
+struct CmtvDev {
+  int ordinal = 0;
   hipStream_t stream = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  bool timing_pending = false;
   uint32_t* d_btab = nullptr;
-  DevBuf d_atab, d_in, d_out;
+  uint32_t* d_bcomb = nullptr;   // comb of B for registered-key verification (built lazily)
+  uint16_t* d_srprog = nullptr;  // sr25519 transcript program (merlin.h)
+  DevBuf d_atab, d_in, d_out, d_all;
   HostBuf h_in, h_out;
+  // The lane kernels' A-table scratch is shared by every launch on this
+  // device, whatever stream it is enqueued on: each lane launch waits for the
+  // previous one (atab_done) so calls on different streams cannot overwrite
+  // each other's tables.
+  hipEvent_t atab_done = nullptr;
+  bool atab_used = false;
+  hipEvent_t done = nullptr;  // cross-device ordering for peer-copy gathers
+  Timing timing;
+  ncclComm_t comm = nullptr;
+};
+
+struct cmtv_ctx {
+  std::vector<CmtvDev> devs;  // devs[0]: single-device and device-resident calls
+  bool rccl = false;          // gathers over an RCCL communicator
+  uint32_t default_mode = CMTV_MODE_GO_STDLIB;
   std::mutex mu;
   cmtv_stats stats{};
   size_t quad_max = kQuadMaxDefault;  // batches up to this size use the quad kernel
-  uint32_t* d_bcomb = nullptr;        // comb of B for registered-key verification (built lazily)
-  uint16_t* d_srprog = nullptr;       // sr25519 transcript program (merlin.h)
+  size_t keyed_quad_max = kKeyedQuadMaxDefault;
+  size_t lane_chunk = kChunk;         // signatures per lane-kernel launch (env CMTV_LANE_CHUNK)
+  size_t shard_min = kShardMinDefault;
   int sr_nops = 0;
   VerdictCache cache;                 // cmtv_verdict_cache (off by default)
-  size_t lane_chunk = kChunk;         // signatures per lane-kernel launch (env CMTV_LANE_CHUNK)
-  size_t keyed_quad_max = kKeyedQuadMaxDefault;  // registered-key batches up to this use the quad kernel
   // cmtv_keyset_cache: validator sets (their concatenated keys) -> registered
   // key sets, used by cmtv_verify_commit(s); FIFO of at most keyset_cap
   size_t keyset_cap = 0;
   std::vector<std::pair<std::string, cmtv_keyset*>> keysets;
+  // CMTV_FAULT_AT: 1-based index of the verification launch that fails
+  uint64_t fault_at = 0, launch_seq = 0;
 };
 
 struct cmtv_keyset {
+  struct PerDev {
+    uint32_t* d_pk = nullptr;   // n x 8 words, the keys' original bytes
+    uint8_t* d_ok = nullptr;    // n decode flags
+    uint32_t* d_tab = nullptr;  // n x kCombWords
+  };
   cmtv_ctx* ctx = nullptr;
   size_t n = 0;
-  uint32_t* d_pk = nullptr;   // n x 8 words, the keys' original bytes
-  uint8_t* d_ok = nullptr;    // n decode flags
-  uint32_t* d_tab = nullptr;  // n x kCombWords
+  std::vector<PerDev> dev;    // one per device of the context
   std::vector<uint8_t> pk;    // host copy (n x 32)
 };
 
@@ -185,23 +351,32 @@ static int hip_fail(hipError_t e) {
   return CMTV_EHIP;
 }
 
-static void harvest_timing(cmtv_ctx* ctx) {
-  if (!ctx->timing_pending) return;
-  if (hipEventSynchronize(ctx->ev1) == hipSuccess) {
-    float ms = 0.f;
-    if (hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1) == hipSuccess) {
-      ctx->stats.last_kernel_ms = ms;
-      ctx->stats.device_ms += ms;
-    }
+static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+static void harvest(cmtv_ctx* ctx, bool blocking) {
+  for (auto& d : ctx->devs) {
+    (void)hipSetDevice(d.ordinal);
+    d.timing.harvest(ctx->stats, blocking);
   }
-  ctx->timing_pending = false;
 }
 
-// Enqueue verification of n signatures whose inputs are in device memory.
-static int enqueue_verify(cmtv_ctx* ctx, size_t n, const uint8_t* d_pk, const uint8_t* d_sig, const uint8_t* d_msg,
-                          const uint32_t* d_off, uint32_t mode, uint8_t* d_valid, uint64_t* d_bitmap,
-                          hipStream_t s) {
+// CMTV_FAULT_AT: true when this verification launch is the one to fail
+static bool fault_hit(cmtv_ctx* ctx) {
+  ctx->launch_seq++;
+  if (ctx->fault_at && ctx->launch_seq == ctx->fault_at) {
+    ctx->stats.faults_injected++;
+    return true;
+  }
+  return false;
+}
+
+// Enqueue verification of n signatures whose inputs are in device memory of
+// device D (current on this thread).
+static int enqueue_verify(cmtv_ctx* ctx, CmtvDev& D, size_t n, const uint8_t* d_pk, const uint8_t* d_sig,
+                          const uint8_t* d_msg, const uint32_t* d_off, uint32_t mode, uint8_t* d_valid,
+                          uint64_t* d_bitmap, hipStream_t s) {
   if (n == 0) return CMTV_OK;
+  if (fault_hit(ctx)) return CMTV_EHIP;
   // Small batches cannot fill the chip at one signature per lane: use the
   // 4-lanes-per-signature kernel below the crossover (quad.h,
   // sr25519_quad.h).
@@ -211,40 +386,51 @@ static int enqueue_verify(cmtv_ctx* ctx, size_t n, const uint8_t* d_pk, const ui
   if (!quad) {
     const size_t lanes = std::min<size_t>(n, ctx->lane_chunk);
     const size_t lanes_padded = (lanes + 63) / 64 * 64;
-    e = ctx->d_atab.ensure(lanes_padded * kAtabWordsPerLane * sizeof(uint32_t));
-    if (e != hipSuccess) return hip_fail(e);
+    if (lanes_padded * kAtabWordsPerLane * sizeof(uint32_t) > D.d_atab.cap) {
+      // growing frees the old scratch: every earlier user must be done
+      if (D.atab_used && (e = hipEventSynchronize(D.atab_done)) != hipSuccess) return hip_fail(e);
+      if ((e = D.d_atab.ensure(lanes_padded * kAtabWordsPerLane * sizeof(uint32_t))) != hipSuccess)
+        return hip_fail(e);
+    }
+    if (D.atab_used && (e = hipStreamWaitEvent(s, D.atab_done, 0)) != hipSuccess) return hip_fail(e);
   }
-  harvest_timing(ctx);
-  if ((e = hipEventRecord(ctx->ev0, s)) != hipSuccess) return hip_fail(e);
+  D.timing.harvest(ctx->stats, false);
+  Timing::Pair tp;
+  if ((e = D.timing.begin(tp, s)) != hipSuccess) return hip_fail(e);
   const size_t chunk = quad ? kChunk : ctx->lane_chunk;
   for (size_t c = 0; c < n; c += chunk) {
     const uint32_t cn = (uint32_t)std::min<size_t>(chunk, n - c);
     if (sr)
-      e = launch_verify_sr25519(cn, d_pk + 32 * c, d_sig + 64 * c, d_msg, d_off + c, ctx->d_btab,
-                                static_cast<uint32_t*>(ctx->d_atab.p), ctx->d_srprog, ctx->sr_nops,
+      e = launch_verify_sr25519(cn, d_pk + 32 * c, d_sig + 64 * c, d_msg, d_off + c, D.d_btab,
+                                static_cast<uint32_t*>(D.d_atab.p), D.d_srprog, ctx->sr_nops,
                                 d_valid ? d_valid + c : nullptr, d_bitmap ? d_bitmap + c / 64 : nullptr, quad, s);
     else
-      e = launch_verify(mode, cn, d_pk + 32 * c, d_sig + 64 * c, d_msg, d_off + c, ctx->d_btab,
-                        static_cast<uint32_t*>(ctx->d_atab.p), d_valid ? d_valid + c : nullptr,
+      e = launch_verify(mode, cn, d_pk + 32 * c, d_sig + 64 * c, d_msg, d_off + c, D.d_btab,
+                        static_cast<uint32_t*>(D.d_atab.p), d_valid ? d_valid + c : nullptr,
                         d_bitmap ? d_bitmap + c / 64 : nullptr, quad, s);
-    if (e != hipSuccess) return hip_fail(e);
+    if (e != hipSuccess) {
+      D.timing.abandon(tp);
+      return hip_fail(e);
+    }
     ctx->stats.kernel_launches++;
   }
-  if ((e = hipEventRecord(ctx->ev1, s)) != hipSuccess) return hip_fail(e);
-  ctx->timing_pending = true;
+  if (!quad) {
+    if ((e = hipEventRecord(D.atab_done, s)) != hipSuccess) return hip_fail(e);
+    D.atab_used = true;
+  }
+  if ((e = D.timing.end(tp, s)) != hipSuccess) return hip_fail(e);
   ctx->stats.calls++;
   ctx->stats.signatures += n;
   return CMTV_OK;
 }
 
-static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
-
 // keys per comb-build launch (prefix-product scratch = 160 KiB per key)
 constexpr uint32_t kCombKeyChunk = 256;
 
-// Comb of B (keyed.h), built on first use; caller holds the context lock.
-static int ensure_bcomb(cmtv_ctx* ctx) {
-  if (ctx->d_bcomb) return CMTV_OK;
+// Comb of B (keyed.h) on device D, built on first use; caller holds the
+// context lock and D is current.
+static int ensure_bcomb(CmtvDev& D) {
+  if (D.d_bcomb) return CMTV_OK;
   const uint32_t bw[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
                           0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};
   DevBuf scratch, bpk;
@@ -252,44 +438,290 @@ static int ensure_bcomb(cmtv_ctx* ctx) {
   hipError_t e = hipMalloc(&tab, kCombWords * sizeof(uint32_t));
   if (e == hipSuccess) e = scratch.ensure(kCombScratchWordsPerKey * sizeof(uint32_t));
   if (e == hipSuccess) e = bpk.ensure(sizeof(bw));
-  if (e == hipSuccess) e = hipMemcpyAsync(bpk.p, bw, sizeof(bw), hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(bpk.p, bw, sizeof(bw), hipMemcpyHostToDevice, D.stream);
   if (e == hipSuccess)
-    e = launch_comb_build(1, bpk.p, nullptr, tab, static_cast<uint32_t*>(scratch.p), false, ctx->stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    e = launch_comb_build(1, bpk.p, nullptr, tab, static_cast<uint32_t*>(scratch.p), false, D.stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(D.stream);
   scratch.release();
   bpk.release();
   if (e != hipSuccess) {
     if (tab) (void)hipFree(tab);
     return hip_fail(e);
   }
-  ctx->d_bcomb = tab;
+  D.d_bcomb = tab;
   return CMTV_OK;
 }
 
-static int enqueue_verify_keyed(cmtv_ctx* ctx, const cmtv_keyset* ks, size_t n, const uint32_t* d_idx,
-                                const uint8_t* d_sig, const uint8_t* d_msg, const uint32_t* d_off, uint32_t mode,
-                                uint8_t* d_valid, uint64_t* d_bitmap, hipStream_t s) {
+static int enqueue_verify_keyed(cmtv_ctx* ctx, CmtvDev& D, const cmtv_keyset::PerDev& K, size_t n_keys, size_t n,
+                                const uint32_t* d_idx, const uint8_t* d_sig, const uint8_t* d_msg,
+                                const uint32_t* d_off, uint32_t mode, uint8_t* d_valid, uint64_t* d_bitmap,
+                                hipStream_t s) {
   if (n == 0) return CMTV_OK;
-  harvest_timing(ctx);
+  if (fault_hit(ctx)) return CMTV_EHIP;
+  D.timing.harvest(ctx->stats, false);
+  Timing::Pair tp;
   hipError_t e;
-  if ((e = hipEventRecord(ctx->ev0, s)) != hipSuccess) return hip_fail(e);
+  if ((e = D.timing.begin(tp, s)) != hipSuccess) return hip_fail(e);
   for (size_t c = 0; c < n; c += kChunk) {
     const uint32_t cn = (uint32_t)std::min<size_t>(kChunk, n - c);
-    e = launch_verify_keyed(mode, cn, (uint32_t)ks->n, d_idx + c, d_sig + 64 * c, d_msg, d_off + c, ks->d_pk,
-                            ks->d_ok, ks->d_tab, ctx->d_bcomb, d_valid ? d_valid + c : nullptr,
+    e = launch_verify_keyed(mode, cn, (uint32_t)n_keys, d_idx + c, d_sig + 64 * c, d_msg, d_off + c, K.d_pk, K.d_ok,
+                            K.d_tab, D.d_bcomb, d_valid ? d_valid + c : nullptr,
                             d_bitmap ? d_bitmap + c / 64 : nullptr, n <= ctx->keyed_quad_max, s);
-    if (e != hipSuccess) return hip_fail(e);
+    if (e != hipSuccess) {
+      D.timing.abandon(tp);
+      return hip_fail(e);
+    }
     ctx->stats.kernel_launches++;
+    ctx->stats.keyed_launches++;
   }
-  if ((e = hipEventRecord(ctx->ev1, s)) != hipSuccess) return hip_fail(e);
-  ctx->timing_pending = true;
+  if ((e = D.timing.end(tp, s)) != hipSuccess) return hip_fail(e);
   ctx->stats.calls++;
   ctx->stats.signatures += n;
   return CMTV_OK;
 }
 
+// ---------------------------------------------------------------- sharding
+
+// Bitmap all-gather: device g's shard occupies words [g W, (g+1) W) of
+// bufs[g] (G x W words each); afterwards every bufs[g] holds all shards.
+// RCCL all-gather in place when the context has a communicator, else peer
+// copies (a context over a repeated device ordinal). Enqueued on the device
+// streams.
+static int gather_bitmaps(cmtv_ctx* ctx, size_t G, size_t W, uint64_t* const* bufs) {
+  if (G <= 1) return CMTV_OK;
+  ctx->stats.gathers++;
+  if (ctx->rccl) {
+    const Rccl& R = rccl();
+    if (R.GroupStart() != 0) return CMTV_ERCCL;
+    int bad = 0;
+    for (size_t g = 0; g < G; g++) {
+      CmtvDev& D = ctx->devs[g];
+      (void)hipSetDevice(D.ordinal);
+      bad |= R.AllGather(bufs[g] + g * W, bufs[g], W, kNcclUint64, D.comm, D.stream) != 0;
+    }
+    if (R.GroupEnd() != 0 || bad) return CMTV_ERCCL;
+    return CMTV_OK;
+  }
+  hipError_t e;
+  for (size_t h = 0; h < G; h++) {
+    (void)hipSetDevice(ctx->devs[h].ordinal);
+    if ((e = hipEventRecord(ctx->devs[h].done, ctx->devs[h].stream)) != hipSuccess) return hip_fail(e);
+  }
+  for (size_t g = 0; g < G; g++) {
+    CmtvDev& D = ctx->devs[g];
+    (void)hipSetDevice(D.ordinal);
+    for (size_t h = 0; h < G; h++) {
+      if (h == g) continue;
+      CmtvDev& H = ctx->devs[h];
+      if ((e = hipStreamWaitEvent(D.stream, H.done, 0)) != hipSuccess) return hip_fail(e);
+      if ((e = hipMemcpyPeerAsync(bufs[g] + h * W, D.ordinal, bufs[h] + h * W, H.ordinal, W * 8, D.stream)) !=
+          hipSuccess)
+        return hip_fail(e);
+    }
+  }
+  // the copies read other devices' buffers: finish them before those
+  // devices' next kernels may write
+  for (size_t g = 0; g < G; g++) {
+    (void)hipSetDevice(ctx->devs[g].ordinal);
+    if ((e = hipStreamSynchronize(ctx->devs[g].stream)) != hipSuccess) return hip_fail(e);
+  }
+  return CMTV_OK;
+}
+
+// A batch in host memory: generic (pk rows), registered keys (key_idx into
+// ks) or sr25519; messages either host-encoded (msg) or written on the
+// device from per-commit CanonicalVote templates (signbytes.h).
+struct HostBatch {
+  size_t n = 0;
+  uint32_t mode = 0;
+  const uint8_t* pk = nullptr;
+  const cmtv_keyset* ks = nullptr;
+  const uint32_t* key_idx = nullptr;
+  const uint8_t* sig = nullptr;
+  const uint32_t* msg_off = nullptr;
+  const uint8_t* msg = nullptr;
+  const SbTemplate* tmpls = nullptr;
+  size_t n_tmpls = 0;
+  const uint8_t* blob = nullptr;
+  size_t blob_len = 0;
+  const uint32_t* tidx = nullptr;
+  const uint8_t* tflag = nullptr;
+  const int64_t* sec = nullptr;
+  const int32_t* nanos = nullptr;
+};
+
+// Stage rows [a, b) of B on device g and enqueue sign-bytes (templated) and
+// verification; verdict bytes to D.d_out (when want_valid), bitmap words to
+// `bitmap` (device memory of D).
+static int enqueue_shard(cmtv_ctx* ctx, size_t g, const HostBatch& B, size_t a, size_t b, bool want_valid,
+                         uint64_t* bitmap, size_t& o_valid_out) {
+  CmtvDev& D = ctx->devs[g];
+  const size_t m = b - a;
+  const bool keyed = B.ks != nullptr, tpl = B.msg == nullptr;
+  const size_t mb = (size_t)B.msg_off[b] - B.msg_off[a];
+  const size_t key_bytes = keyed ? 4 * m : 32 * m;
+  const size_t o_key = 0, o_sig = align_up(key_bytes, 256), o_off = align_up(o_sig + 64 * m, 256);
+  size_t o_tidx = 0, o_flag = 0, o_sec = 0, o_nanos = 0, o_tmpl = 0, o_blob = 0, in_bytes, o_msg, dev_bytes;
+  const size_t tb = B.n_tmpls * sizeof(SbTemplate);
+  if (tpl) {
+    o_tidx = align_up(o_off + 4 * (m + 1), 256);
+    o_flag = align_up(o_tidx + 4 * m, 256);
+    o_sec = align_up(o_flag + m, 256);
+    o_nanos = align_up(o_sec + 8 * m, 256);
+    o_tmpl = align_up(o_nanos + 4 * m, 256);
+    o_blob = align_up(o_tmpl + tb, 256);
+    in_bytes = align_up(o_blob + B.blob_len + 16, 256);
+    o_msg = in_bytes;  // device only: k_sign_bytes writes the messages here
+    dev_bytes = align_up(o_msg + mb + 16, 256);
+  } else {
+    o_msg = align_up(o_off + 4 * (m + 1), 256);
+    in_bytes = align_up(o_msg + mb + 16, 256);
+    dev_bytes = in_bytes;
+  }
+  const size_t o_valid = 0, out_bytes = align_up(std::max<size_t>(m, 1), 256);
+  o_valid_out = o_valid;
+  hipError_t e;
+  (void)hipSetDevice(D.ordinal);
+  if ((e = D.h_in.ensure(in_bytes)) != hipSuccess) return hip_fail(e);
+  if ((e = D.d_in.ensure(dev_bytes)) != hipSuccess) return hip_fail(e);
+  if ((e = D.d_out.ensure(out_bytes)) != hipSuccess) return hip_fail(e);
+  auto* hin = static_cast<uint8_t*>(D.h_in.p);
+  if (keyed)
+    std::memcpy(hin + o_key, B.key_idx + a, 4 * m);
+  else
+    std::memcpy(hin + o_key, B.pk + 32 * a, 32 * m);
+  std::memcpy(hin + o_sig, B.sig + 64 * a, 64 * m);
+  auto* hoff = reinterpret_cast<uint32_t*>(hin + o_off);
+  const uint32_t base = B.msg_off[a];
+  for (size_t i = 0; i <= m; i++) hoff[i] = B.msg_off[a + i] - base;
+  if (tpl) {
+    std::memcpy(hin + o_tidx, B.tidx + a, 4 * m);
+    std::memcpy(hin + o_flag, B.tflag + a, m);
+    std::memcpy(hin + o_sec, B.sec + a, 8 * m);
+    std::memcpy(hin + o_nanos, B.nanos + a, 4 * m);
+    std::memcpy(hin + o_tmpl, B.tmpls, tb);
+    if (B.blob_len) std::memcpy(hin + o_blob, B.blob, B.blob_len);
+  } else {
+    if (mb) std::memcpy(hin + o_msg, B.msg + base, mb);
+    std::memset(hin + o_msg + mb, 0, 16);
+  }
+  auto* din = static_cast<uint8_t*>(D.d_in.p);
+  auto* dout = static_cast<uint8_t*>(D.d_out.p);
+  if ((e = hipMemcpyAsync(din, hin, in_bytes, hipMemcpyHostToDevice, D.stream)) != hipSuccess) return hip_fail(e);
+  if (tpl) {
+    if ((e = hipMemsetAsync(din + o_msg + mb, 0, 16, D.stream)) != hipSuccess) return hip_fail(e);
+    if ((e = launch_sign_bytes((uint32_t)m, din + o_tmpl, din + o_blob, reinterpret_cast<uint32_t*>(din + o_tidx),
+                               din + o_flag, reinterpret_cast<int64_t*>(din + o_sec),
+                               reinterpret_cast<int32_t*>(din + o_nanos), reinterpret_cast<uint32_t*>(din + o_off),
+                               din + o_msg, D.stream)) != hipSuccess)
+      return hip_fail(e);
+  }
+  uint8_t* dv = want_valid ? dout + o_valid : nullptr;
+  if (keyed)
+    return enqueue_verify_keyed(ctx, D, B.ks->dev[g], B.ks->n, m, reinterpret_cast<uint32_t*>(din + o_key),
+                                din + o_sig, din + o_msg, reinterpret_cast<uint32_t*>(din + o_off), B.mode, dv,
+                                bitmap, D.stream);
+  return enqueue_verify(ctx, D, m, din + o_key, din + o_sig, din + o_msg, reinterpret_cast<uint32_t*>(din + o_off),
+                        B.mode, dv, bitmap, D.stream);
+}
+
+// Verdicts of a host batch, sharded over the context's devices. Caller holds
+// the lock.
+static int run_host_batch_(cmtv_ctx* ctx, const HostBatch& B, uint8_t* out_valid, uint64_t* out_bitmap) {
+  const size_t n = B.n;
+  if (n == 0) return CMTV_OK;
+  const ShardPlan P = plan_shards(n, ctx->devs.size(), ctx->shard_min);
+  const size_t words = (n + 63) / 64;
+  hipError_t e;
+  uint64_t* bufs[kMaxDevices];
+  for (size_t g = 0; g < P.G; g++) {
+    CmtvDev& D = ctx->devs[g];
+    (void)hipSetDevice(D.ordinal);
+    if ((e = D.d_all.ensure(8 * std::max<size_t>(P.G * P.W, 1))) != hipSuccess) return hip_fail(e);
+    bufs[g] = static_cast<uint64_t*>(D.d_all.p);
+  }
+  size_t o_valid = 0;
+  for (size_t g = 0; g < P.G; g++) {
+    const size_t a = P.lo(g, n), b = P.hi(g, n);
+    if (a == b) {
+      // an empty trailing shard still takes part in the gather
+      (void)hipSetDevice(ctx->devs[g].ordinal);
+      if ((e = hipMemsetAsync(bufs[g] + g * P.W, 0, 8 * P.W, ctx->devs[g].stream)) != hipSuccess) return hip_fail(e);
+      continue;
+    }
+    const int rc = enqueue_shard(ctx, g, B, a, b, P.G == 1, bufs[g] + g * P.W, o_valid);
+    if (rc != CMTV_OK) return rc;
+  }
+  if (P.G > 1) {
+    ctx->stats.sharded_calls++;
+    const int rc = gather_bitmaps(ctx, P.G, P.W, bufs);
+    if (rc != CMTV_OK) return rc;
+  }
+  // results from device 0: verdict bytes + bitmap (one device) or the
+  // gathered bitmap (several)
+  CmtvDev& D0 = ctx->devs[0];
+  (void)hipSetDevice(D0.ordinal);
+  const size_t o_bm = 0, o_v = align_up(8 * words, 256);
+  const size_t out_bytes = P.G == 1 ? align_up(o_v + n, 256) : 8 * words;
+  if ((e = D0.h_out.ensure(out_bytes)) != hipSuccess) return hip_fail(e);
+  auto* hout = static_cast<uint8_t*>(D0.h_out.p);
+  if ((e = hipMemcpyAsync(hout + o_bm, bufs[0], 8 * words, hipMemcpyDeviceToHost, D0.stream)) != hipSuccess)
+    return hip_fail(e);
+  if (P.G == 1 &&
+      (e = hipMemcpyAsync(hout + o_v, static_cast<uint8_t*>(D0.d_out.p) + o_valid, n, hipMemcpyDeviceToHost,
+                          D0.stream)) != hipSuccess)
+    return hip_fail(e);
+  for (size_t g = 0; g < P.G; g++) {
+    (void)hipSetDevice(ctx->devs[g].ordinal);
+    if ((e = hipStreamSynchronize(ctx->devs[g].stream)) != hipSuccess) return hip_fail(e);
+  }
+  (void)hipSetDevice(D0.ordinal);
+  harvest(ctx, false);
+  (void)hipSetDevice(D0.ordinal);
+  const uint64_t* bm = reinterpret_cast<const uint64_t*>(hout + o_bm);
+  uint64_t valid_count = 0;
+  for (size_t w = 0; w < words; w++) valid_count += (uint64_t)__builtin_popcountll(bm[w]);
+  ctx->stats.invalid += n - valid_count;
+  if (out_bitmap) std::memcpy(out_bitmap, bm, 8 * words);
+  if (out_valid) {
+    if (P.G == 1) {
+      std::memcpy(out_valid, hout + o_v, n);
+    } else {
+      for (size_t i = 0; i < n; i++) out_valid[i] = (uint8_t)((bm[i >> 6] >> (i & 63)) & 1);
+    }
+  }
+  return CMTV_OK;
+}
+
+static int run_host_batch(cmtv_ctx* ctx, const HostBatch& B, uint8_t* out_valid, uint64_t* out_bitmap) {
+  const int rc = run_host_batch_(ctx, B, out_valid, out_bitmap);
+  if (rc != CMTV_OK) {
+    // work already enqueued for other shards still reads the pinned staging
+    // the next call refills: drain it before returning the error
+    for (auto& D : ctx->devs) {
+      (void)hipSetDevice(D.ordinal);
+      (void)hipStreamSynchronize(D.stream);
+    }
+    (void)hipGetLastError();
+    (void)hipSetDevice(ctx->devs[0].ordinal);
+  }
+  return rc;
+}
+
+static const uint8_t kNoMessageBytes = 0;
+
 static int verify_host_device(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
-                              const uint32_t* msg_off, uint32_t mode, uint8_t* out_valid, uint64_t* out_bitmap);
+                              const uint32_t* msg_off, uint32_t mode, uint8_t* out_valid, uint64_t* out_bitmap) {
+  if (!msg) msg = &kNoMessageBytes;  // all messages empty (a null msg selects templated sign-bytes)
+  HostBatch B;
+  B.n = n;
+  B.mode = mode;
+  B.pk = pk;
+  B.sig = sig;
+  B.msg = msg;
+  B.msg_off = msg_off;
+  return run_host_batch(ctx, B, out_valid, out_bitmap);
+}
 
 bool cache_enabled(const cmtv_ctx* ctx) { return ctx->cache.cap != 0; }
 
@@ -303,8 +735,8 @@ int verify_host_locked(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_t
   std::vector<uint64_t> hs(n);
   std::vector<std::string> keys(n);
   for (size_t i = 0; i < n; i++) {
-    hs[i] = VerdictCache::hash(mode, sig + 64 * i);
     VerdictCache::make_key(keys[i], mode, pk + 32 * i, sig + 64 * i, msg + msg_off[i], msg_off[i + 1] - msg_off[i]);
+    hs[i] = ctx->cache.hash(keys[i]);
     const int v = ctx->cache.find(hs[i], keys[i]);
     if (v < 0)
       miss.push_back(i);
@@ -345,111 +777,160 @@ int verify_host_locked(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_t
   return CMTV_OK;
 }
 
-static int verify_host_device(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
-                              const uint32_t* msg_off, uint32_t mode, uint8_t* out_valid, uint64_t* out_bitmap) {
-  if (n == 0) return CMTV_OK;
-  const size_t msg_bytes = msg_off[n];
-  // staging layout: [pk n*32][sig n*64][off (n+1)*4][msg msg_bytes + 16]
-  const size_t o_pk = 0, o_sig = align_up(o_pk + 32 * n, 256), o_off = align_up(o_sig + 64 * n, 256);
-  const size_t o_msg = align_up(o_off + 4 * (n + 1), 256), in_bytes = align_up(o_msg + msg_bytes + 16, 256);
-  const size_t words = (n + 63) / 64;
-  const size_t o_bm = 0, o_valid = align_up(8 * words, 256), out_bytes = align_up(o_valid + n, 256);
-  hipError_t e;
-  if ((e = ctx->h_in.ensure(in_bytes)) != hipSuccess) return hip_fail(e);
-  if ((e = ctx->d_in.ensure(in_bytes)) != hipSuccess) return hip_fail(e);
-  if ((e = ctx->h_out.ensure(out_bytes)) != hipSuccess) return hip_fail(e);
-  if ((e = ctx->d_out.ensure(out_bytes)) != hipSuccess) return hip_fail(e);
-  auto* hin = static_cast<uint8_t*>(ctx->h_in.p);
-  std::memcpy(hin + o_pk, pk, 32 * n);
-  std::memcpy(hin + o_sig, sig, 64 * n);
-  std::memcpy(hin + o_off, msg_off, 4 * (n + 1));
-  if (msg_bytes) std::memcpy(hin + o_msg, msg, msg_bytes);
-  std::memset(hin + o_msg + msg_bytes, 0, 16);
-  auto* din = static_cast<uint8_t*>(ctx->d_in.p);
-  auto* dout = static_cast<uint8_t*>(ctx->d_out.p);
-  if ((e = hipMemcpyAsync(din, hin, in_bytes, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess) return hip_fail(e);
-  int rc = enqueue_verify(ctx, n, din + o_pk, din + o_sig, din + o_msg, reinterpret_cast<uint32_t*>(din + o_off), mode,
-                          dout + o_valid, reinterpret_cast<uint64_t*>(dout + o_bm), ctx->stream);
-  if (rc != CMTV_OK) return rc;
-  auto* hout = static_cast<uint8_t*>(ctx->h_out.p);
-  if ((e = hipMemcpyAsync(hout, dout, out_bytes, hipMemcpyDeviceToHost, ctx->stream)) != hipSuccess) return hip_fail(e);
-  if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return hip_fail(e);
-  harvest_timing(ctx);
-  uint64_t invalid = 0;
-  const uint8_t* hv = hout + o_valid;
-  for (size_t i = 0; i < n; i++) invalid += hv[i] == 0;
-  ctx->stats.invalid += invalid;
-  if (out_valid) std::memcpy(out_valid, hv, n);
-  if (out_bitmap) std::memcpy(out_bitmap, hout + o_bm, 8 * words);
-  return CMTV_OK;
-}
-
 int verify_templated_locked(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_t* sig, const uint32_t* msg_off,
                             const void* tmpls, size_t n_tmpls, const uint8_t* blob, size_t blob_len,
                             const uint32_t* tidx, const uint8_t* commit_flag, const int64_t* sec,
                             const int32_t* nanos, uint32_t mode, uint8_t* out_valid, const cmtv_keyset* ks,
                             const uint32_t* key_idx) {
-  if (n == 0) return CMTV_OK;
-  const size_t msg_bytes = msg_off[n];
-  const size_t tb = n_tmpls * sizeof(SbTemplate);
-  // staging: [pk][sig][off][tidx][flag][sec][nanos][templates][blob] | device only: [msg]
-  const size_t o_pk = 0, o_sig = align_up(32 * n, 256), o_off = align_up(o_sig + 64 * n, 256);
-  const size_t o_tidx = align_up(o_off + 4 * (n + 1), 256), o_flag = align_up(o_tidx + 4 * n, 256);
-  const size_t o_sec = align_up(o_flag + n, 256), o_nanos = align_up(o_sec + 8 * n, 256);
-  const size_t o_tmpl = align_up(o_nanos + 4 * n, 256), o_blob = align_up(o_tmpl + tb, 256);
-  const size_t in_bytes = align_up(o_blob + blob_len + 16, 256);
-  const size_t o_msg = in_bytes, dev_bytes = align_up(o_msg + msg_bytes + 16, 256);
-  const size_t o_valid = 0, out_bytes = align_up(n, 256);
-  hipError_t e;
-  if ((e = ctx->h_in.ensure(in_bytes)) != hipSuccess) return hip_fail(e);
-  if ((e = ctx->d_in.ensure(dev_bytes)) != hipSuccess) return hip_fail(e);
-  if ((e = ctx->h_out.ensure(out_bytes)) != hipSuccess) return hip_fail(e);
-  if ((e = ctx->d_out.ensure(out_bytes)) != hipSuccess) return hip_fail(e);
-  auto* hin = static_cast<uint8_t*>(ctx->h_in.p);
-  if (ks)
-    std::memcpy(hin + o_pk, key_idx, 4 * n);  // key indices in the key slot
-  else
-    std::memcpy(hin + o_pk, pk, 32 * n);
-  std::memcpy(hin + o_sig, sig, 64 * n);
-  std::memcpy(hin + o_off, msg_off, 4 * (n + 1));
-  std::memcpy(hin + o_tidx, tidx, 4 * n);
-  std::memcpy(hin + o_flag, commit_flag, n);
-  std::memcpy(hin + o_sec, sec, 8 * n);
-  std::memcpy(hin + o_nanos, nanos, 4 * n);
-  std::memcpy(hin + o_tmpl, tmpls, tb);
-  if (blob_len) std::memcpy(hin + o_blob, blob, blob_len);
-  auto* din = static_cast<uint8_t*>(ctx->d_in.p);
-  auto* dout = static_cast<uint8_t*>(ctx->d_out.p);
-  if ((e = hipMemcpyAsync(din, hin, in_bytes, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess) return hip_fail(e);
-  if ((e = hipMemsetAsync(din + o_msg + msg_bytes, 0, 16, ctx->stream)) != hipSuccess) return hip_fail(e);
-  if ((e = launch_sign_bytes((uint32_t)n, din + o_tmpl, din + o_blob, reinterpret_cast<uint32_t*>(din + o_tidx),
-                             din + o_flag, reinterpret_cast<int64_t*>(din + o_sec),
-                             reinterpret_cast<int32_t*>(din + o_nanos), reinterpret_cast<uint32_t*>(din + o_off),
-                             din + o_msg, ctx->stream)) != hipSuccess)
-    return hip_fail(e);
-  int rc = ks ? enqueue_verify_keyed(ctx, ks, n, reinterpret_cast<uint32_t*>(din + o_pk), din + o_sig, din + o_msg,
-                                     reinterpret_cast<uint32_t*>(din + o_off), mode, dout + o_valid, nullptr,
-                                     ctx->stream)
-              : enqueue_verify(ctx, n, din + o_pk, din + o_sig, din + o_msg, reinterpret_cast<uint32_t*>(din + o_off),
-                               mode, dout + o_valid, nullptr, ctx->stream);
-  if (rc != CMTV_OK) return rc;
-  auto* hout = static_cast<uint8_t*>(ctx->h_out.p);
-  if ((e = hipMemcpyAsync(hout, dout, out_bytes, hipMemcpyDeviceToHost, ctx->stream)) != hipSuccess) return hip_fail(e);
-  if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return hip_fail(e);
-  harvest_timing(ctx);
-  uint64_t invalid = 0;
-  for (size_t i = 0; i < n; i++) invalid += hout[o_valid + i] == 0;
-  ctx->stats.invalid += invalid;
-  std::memcpy(out_valid, hout + o_valid, n);
-  return CMTV_OK;
+  HostBatch B;
+  B.n = n;
+  B.mode = mode;
+  B.pk = ks ? nullptr : pk;
+  B.ks = ks;
+  B.key_idx = key_idx;
+  B.sig = sig;
+  B.msg_off = msg_off;
+  B.tmpls = static_cast<const SbTemplate*>(tmpls);
+  B.n_tmpls = n_tmpls;
+  B.blob = blob;
+  B.blob_len = blob_len;
+  B.tidx = tidx;
+  B.tflag = commit_flag;
+  B.sec = sec;
+  B.nanos = nanos;
+  return run_host_batch(ctx, B, out_valid, nullptr);
 }
 
 int ctx_lock(cmtv_ctx* ctx, std::unique_lock<std::mutex>& lk) {
   lk = std::unique_lock<std::mutex>(ctx->mu);
-  return hipSetDevice(ctx->device) == hipSuccess ? CMTV_OK : CMTV_ENODEV;
+  return hipSetDevice(ctx->devs[0].ordinal) == hipSuccess ? CMTV_OK : CMTV_ENODEV;
 }
 
 uint32_t ctx_default_mode(const cmtv_ctx* ctx) { return ctx->default_mode; }
+
+// ---------------------------------------------------------------- lifecycle
+
+static int init_device(cmtv_ctx* ctx, CmtvDev& D) {
+  if (hipSetDevice(D.ordinal) != hipSuccess) return CMTV_ENODEV;
+  hipError_t e = hipStreamCreateWithFlags(&D.stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&D.atab_done, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&D.done, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipMalloc(&D.d_btab, kBtabWords * sizeof(uint32_t));
+  if (e == hipSuccess) e = launch_btab_init(D.d_btab, D.stream);
+  uint16_t prog[SR_PROGRAM_MAX];
+  ctx->sr_nops = sr_build_program(prog);
+  if (e == hipSuccess) e = hipMalloc(&D.d_srprog, sizeof(prog));
+  if (e == hipSuccess) e = hipMemcpyAsync(D.d_srprog, prog, sizeof(prog), hipMemcpyHostToDevice, D.stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(D.stream);
+  return e == hipSuccess ? CMTV_OK : hip_fail(e);
+}
+
+static void release_device(CmtvDev& D) {
+  (void)hipSetDevice(D.ordinal);
+  if (D.stream) (void)hipStreamSynchronize(D.stream);
+  D.d_atab.release();
+  D.d_in.release();
+  D.d_out.release();
+  D.d_all.release();
+  D.h_in.release();
+  D.h_out.release();
+  if (D.d_btab) (void)hipFree(D.d_btab);
+  if (D.d_bcomb) (void)hipFree(D.d_bcomb);
+  if (D.d_srprog) (void)hipFree(D.d_srprog);
+  D.d_btab = nullptr;
+  D.d_bcomb = nullptr;
+  D.d_srprog = nullptr;
+  D.timing.release();
+  if (D.atab_done) (void)hipEventDestroy(D.atab_done);
+  if (D.done) (void)hipEventDestroy(D.done);
+  if (D.stream) (void)hipStreamDestroy(D.stream);
+  D.atab_done = D.done = nullptr;
+  D.stream = nullptr;
+}
+
+static void read_env(cmtv_ctx* ctx) {
+  if (const char* qm = std::getenv("CMTV_QUAD_MAX")) ctx->quad_max = (size_t)std::strtoull(qm, nullptr, 10);
+  if (const char* kq = std::getenv("CMTV_KEYED_QUAD_MAX")) ctx->keyed_quad_max = (size_t)std::strtoull(kq, nullptr, 10);
+  if (const char* lc = std::getenv("CMTV_LANE_CHUNK")) {
+    const size_t v = (size_t)std::strtoull(lc, nullptr, 10) / 64 * 64;
+    if (v >= 64 && v <= kChunk) ctx->lane_chunk = v;
+  }
+  if (const char* sm = std::getenv("CMTV_SHARD_MIN")) ctx->shard_min = (size_t)std::strtoull(sm, nullptr, 10);
+  if (const char* fa = std::getenv("CMTV_FAULT_AT")) ctx->fault_at = (uint64_t)std::strtoull(fa, nullptr, 10);
+}
+
+// CMTVERIFY_DEVICES: "0,1,2" or "all" (or unset: every visible device)
+static std::vector<int> env_devices(int ndev) {
+  std::vector<int> out;
+  const char* v = std::getenv("CMTVERIFY_DEVICES");
+  if (v && *v && std::strcmp(v, "all") != 0) {
+    const char* p = v;
+    while (*p) {
+      char* end = nullptr;
+      const long x = std::strtol(p, &end, 10);
+      if (end == p) return {};
+      out.push_back((int)x);
+      p = end;
+      while (*p == ',' || *p == ' ') p++;
+    }
+    return out;
+  }
+  for (int i = 0; i < ndev; i++) out.push_back(i);
+  return out;
+}
+
+static int open_ctx(const cmtv_config* cfg, const std::vector<int>& ords, cmtv_ctx** out) {
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return CMTV_ENODEV;
+  if (ords.empty() || ords.size() > (size_t)kMaxDevices) return CMTV_EINVAL;
+  for (int o : ords) {
+    if (o < 0 || o >= ndev) return CMTV_ENODEV;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, o) != hipSuccess) return CMTV_ENODEV;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return CMTV_ENODEV;
+  }
+  auto* ctx = new (std::nothrow) cmtv_ctx();
+  if (!ctx) return CMTV_ENOMEM;
+  ctx->default_mode = cfg ? cfg->default_mode : CMTV_MODE_GO_STDLIB;
+  if (!cfg) {
+    const char* m = std::getenv("CMTVERIFY_MODE");
+    if (m && std::strcmp(m, "zip215") == 0) ctx->default_mode = CMTV_MODE_ZIP215;
+  }
+  read_env(ctx);
+  ctx->devs.resize(ords.size());
+  for (size_t g = 0; g < ords.size(); g++) ctx->devs[g].ordinal = ords[g];
+  for (auto& D : ctx->devs) {
+    const int rc = init_device(ctx, D);
+    if (rc != CMTV_OK) {
+      cmtv_close(ctx);
+      return rc;
+    }
+  }
+  ctx->stats.n_devices = (uint32_t)ords.size();
+  if (ords.size() > 1) {
+    std::vector<int> sorted = ords;
+    std::sort(sorted.begin(), sorted.end());
+    const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
+    for (size_t g = 0; g < ords.size(); g++) {  // peer access for the copy gathers
+      (void)hipSetDevice(ords[g]);
+      for (size_t h = 0; h < ords.size(); h++)
+        if (ords[h] != ords[g]) (void)hipDeviceEnablePeerAccess(ords[h], 0);
+    }
+    (void)hipGetLastError();  // "already enabled" is not an error here
+    const Rccl& R = rccl();
+    if (distinct && R.ok && !std::getenv("CMTV_NO_RCCL")) {
+      std::vector<ncclComm_t> comms(ords.size(), nullptr);
+      if (R.CommInitAll(comms.data(), (int)ords.size(), ords.data()) == 0) {
+        for (size_t g = 0; g < ords.size(); g++) ctx->devs[g].comm = comms[g];
+        ctx->rccl = true;
+      }
+    }
+  }
+  ctx->stats.rccl = ctx->rccl ? 1 : 0;
+  (void)hipSetDevice(ords[0]);
+  *out = ctx;
+  return CMTV_OK;
+}
 
 }  // namespace cmtv
 
@@ -484,66 +965,69 @@ int cmtv_open(const cmtv_config* cfg, cmtv_ctx** out) {
   } else if (hipGetDevice(&dev) != hipSuccess) {
     dev = 0;
   }
-  if (dev >= ndev) return CMTV_ENODEV;
-  hipDeviceProp_t prop;
-  if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return CMTV_ENODEV;
-  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return CMTV_ENODEV;
-  if (hipSetDevice(dev) != hipSuccess) return CMTV_ENODEV;
-  auto* ctx = new (std::nothrow) cmtv_ctx();
-  if (!ctx) return CMTV_ENOMEM;
-  ctx->device = dev;
-  ctx->default_mode = cfg ? cfg->default_mode : CMTV_MODE_GO_STDLIB;
-  if (const char* qm = std::getenv("CMTV_QUAD_MAX")) ctx->quad_max = (size_t)std::strtoull(qm, nullptr, 10);
-  if (const char* kq = std::getenv("CMTV_KEYED_QUAD_MAX")) ctx->keyed_quad_max = (size_t)std::strtoull(kq, nullptr, 10);
-  if (const char* lc = std::getenv("CMTV_LANE_CHUNK")) {
-    const size_t v = (size_t)std::strtoull(lc, nullptr, 10) / 64 * 64;
-    if (v >= 64 && v <= kChunk) ctx->lane_chunk = v;
-  }
-  hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipEventCreate(&ctx->ev0);
-  if (e == hipSuccess) e = hipEventCreate(&ctx->ev1);
-  if (e == hipSuccess) e = hipMalloc(&ctx->d_btab, kBtabWords * sizeof(uint32_t));
-  if (e == hipSuccess) e = launch_btab_init(ctx->d_btab, ctx->stream);
-  uint16_t prog[SR_PROGRAM_MAX];
-  ctx->sr_nops = sr_build_program(prog);
-  if (e == hipSuccess) e = hipMalloc(&ctx->d_srprog, sizeof(prog));
-  if (e == hipSuccess) e = hipMemcpyAsync(ctx->d_srprog, prog, sizeof(prog), hipMemcpyHostToDevice, ctx->stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
-  if (e != hipSuccess) {
-    cmtv_close(ctx);
-    return hip_fail(e);
-  }
-  *out = ctx;
-  return CMTV_OK;
+  return open_ctx(cfg, {dev}, out);
+}
+
+int cmtv_open_devices(const cmtv_config* cfg, const int32_t* devices, size_t n_devices, cmtv_ctx** out) {
+  if (!out) return CMTV_EINVAL;
+  *out = nullptr;
+  if (cfg && (cfg->flags != 0 || cfg->default_mode > CMTV_MODE_ZIP215)) return CMTV_EINVAL;
+  if (n_devices > (size_t)kMaxDevices || (n_devices && !devices)) return CMTV_EINVAL;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return CMTV_ENODEV;
+  std::vector<int> ords = n_devices ? std::vector<int>(devices, devices + n_devices) : env_devices(ndev);
+  if (ords.empty()) return CMTV_EINVAL;
+  return open_ctx(cfg, ords, out);
 }
 
 void cmtv_close(cmtv_ctx* ctx) {
   if (!ctx) return;
-  (void)hipSetDevice(ctx->device);
-  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-  ctx->d_atab.release();
-  ctx->d_in.release();
-  ctx->d_out.release();
-  ctx->h_in.release();
-  ctx->h_out.release();
-  if (ctx->d_btab) (void)hipFree(ctx->d_btab);
-  if (ctx->d_bcomb) (void)hipFree(ctx->d_bcomb);
-  if (ctx->d_srprog) (void)hipFree(ctx->d_srprog);
   for (auto& e : ctx->keysets) cmtv_keyset_free(e.second);
   ctx->keysets.clear();
-  if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
-  if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
-  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  const Rccl& R = rccl();
+  for (auto& D : ctx->devs) {
+    if (D.comm && R.ok) {
+      (void)hipSetDevice(D.ordinal);
+      (void)R.CommDestroy(D.comm);
+    }
+    D.comm = nullptr;
+  }
+  for (auto& D : ctx->devs) release_device(D);
   delete ctx;
 }
 
-void* cmtv_stream(cmtv_ctx* ctx) { return ctx ? static_cast<void*>(ctx->stream) : nullptr; }
+void* cmtv_stream(cmtv_ctx* ctx) { return ctx ? static_cast<void*>(ctx->devs[0].stream) : nullptr; }
+
+int cmtv_device_count(const cmtv_ctx* ctx) { return ctx ? (int)ctx->devs.size() : 0; }
+
+int cmtv_device_ordinal(const cmtv_ctx* ctx, int g) {
+  if (!ctx || g < 0 || g >= (int)ctx->devs.size()) return CMTV_EINVAL;
+  return ctx->devs[g].ordinal;
+}
+
+void* cmtv_device_stream(cmtv_ctx* ctx, int g) {
+  if (!ctx || g < 0 || g >= (int)ctx->devs.size()) return nullptr;
+  return static_cast<void*>(ctx->devs[g].stream);
+}
+
+int cmtv_sync(cmtv_ctx* ctx) {
+  if (!ctx) return CMTV_EINVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  for (auto& D : ctx->devs) {
+    if (hipSetDevice(D.ordinal) != hipSuccess) return CMTV_ENODEV;
+    const hipError_t e = hipStreamSynchronize(D.stream);
+    if (e != hipSuccess) return hip_fail(e);
+  }
+  harvest(ctx, false);
+  (void)hipSetDevice(ctx->devs[0].ordinal);
+  return CMTV_OK;
+}
 
 int cmtv_stats_get(cmtv_ctx* ctx, cmtv_stats* out) {
   if (!ctx || !out) return CMTV_EINVAL;
   std::lock_guard<std::mutex> g(ctx->mu);
-  (void)hipSetDevice(ctx->device);
-  harvest_timing(ctx);
+  harvest(ctx, true);
+  (void)hipSetDevice(ctx->devs[0].ordinal);
   ctx->stats.cache_entries = ctx->cache.size();
   *out = ctx->stats;
   return CMTV_OK;
@@ -563,8 +1047,8 @@ int cmtv_verify_ed25519(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_
   if (!pk || !sig || !msg_off || (!msg && msg_off[n] != 0) || (!out_valid && !out_bitmap)) return CMTV_EINVAL;
   for (size_t i = 0; i < n; i++)
     if (msg_off[i + 1] < msg_off[i]) return CMTV_EINVAL;
-  std::lock_guard<std::mutex> g(ctx->mu);
-  if (hipSetDevice(ctx->device) != hipSuccess) return CMTV_ENODEV;
+  std::unique_lock<std::mutex> lk;
+  if (ctx_lock(ctx, lk) != CMTV_OK) return CMTV_ENODEV;
   return verify_host_locked(ctx, n, pk, sig, msg, msg_off, mode, out_valid, out_bitmap);
 }
 
@@ -573,10 +1057,10 @@ int cmtv_verify_ed25519_device(cmtv_ctx* ctx, size_t n, const void* d_pk, const 
   if (!ctx || mode > CMTV_MODE_ZIP215 || n > (1ull << 31)) return CMTV_EINVAL;
   if (n == 0) return CMTV_OK;
   if (!d_pk || !d_sig || !d_msg || !d_msg_off || (!d_valid && !d_bitmap)) return CMTV_EINVAL;
-  std::lock_guard<std::mutex> g(ctx->mu);
-  if (hipSetDevice(ctx->device) != hipSuccess) return CMTV_ENODEV;
+  std::unique_lock<std::mutex> lk;
+  if (ctx_lock(ctx, lk) != CMTV_OK) return CMTV_ENODEV;
   hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the HIP null stream
-  return enqueue_verify(ctx, n, static_cast<const uint8_t*>(d_pk), static_cast<const uint8_t*>(d_sig),
+  return enqueue_verify(ctx, ctx->devs[0], n, static_cast<const uint8_t*>(d_pk), static_cast<const uint8_t*>(d_sig),
                         static_cast<const uint8_t*>(d_msg), static_cast<const uint32_t*>(d_msg_off), mode,
                         static_cast<uint8_t*>(d_valid), static_cast<uint64_t*>(d_bitmap), s);
 }
@@ -588,8 +1072,8 @@ int cmtv_verify_sr25519(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_
   if (!pk || !sig || !msg_off || (!msg && msg_off[n] != 0) || (!out_valid && !out_bitmap)) return CMTV_EINVAL;
   for (size_t i = 0; i < n; i++)
     if (msg_off[i + 1] < msg_off[i]) return CMTV_EINVAL;
-  std::lock_guard<std::mutex> g(ctx->mu);
-  if (hipSetDevice(ctx->device) != hipSuccess) return CMTV_ENODEV;
+  std::unique_lock<std::mutex> lk;
+  if (ctx_lock(ctx, lk) != CMTV_OK) return CMTV_ENODEV;
   return verify_host_locked(ctx, n, pk, sig, msg, msg_off, kModeSr25519, out_valid, out_bitmap);
 }
 
@@ -598,12 +1082,91 @@ int cmtv_verify_sr25519_device(cmtv_ctx* ctx, size_t n, const void* d_pk, const 
   if (!ctx || n > (1ull << 31)) return CMTV_EINVAL;
   if (n == 0) return CMTV_OK;
   if (!d_pk || !d_sig || !d_msg || !d_msg_off || (!d_valid && !d_bitmap)) return CMTV_EINVAL;
-  std::lock_guard<std::mutex> g(ctx->mu);
-  if (hipSetDevice(ctx->device) != hipSuccess) return CMTV_ENODEV;
-  return enqueue_verify(ctx, n, static_cast<const uint8_t*>(d_pk), static_cast<const uint8_t*>(d_sig),
+  std::unique_lock<std::mutex> lk;
+  if (ctx_lock(ctx, lk) != CMTV_OK) return CMTV_ENODEV;
+  return enqueue_verify(ctx, ctx->devs[0], n, static_cast<const uint8_t*>(d_pk), static_cast<const uint8_t*>(d_sig),
                         static_cast<const uint8_t*>(d_msg), static_cast<const uint32_t*>(d_msg_off), kModeSr25519,
                         static_cast<uint8_t*>(d_valid), static_cast<uint64_t*>(d_bitmap),
                         static_cast<hipStream_t>(stream));
+}
+
+}  // extern "C"
+
+namespace cmtv {
+
+// Shared by the two sharded device-resident entry points: shard g's inputs on
+// device g, each verified on its device's stream, then the bitmap gather.
+static int sharded_device(cmtv_ctx* ctx, const cmtv_keyset* ks, const size_t* n_shard, const void* const* d_keys,
+                          const void* const* d_sig, const void* const* d_msg, const void* const* d_off,
+                          uint32_t mode, void* const* d_valid, void* const* d_bitmap_all, size_t* words_per_shard) {
+  const size_t G = ctx->devs.size();
+  size_t W = 0;
+  for (size_t g = 0; g < G; g++) {
+    if (n_shard[g] > (1ull << 31)) return CMTV_EINVAL;
+    if (n_shard[g] && (!d_keys[g] || !d_sig[g] || !d_msg[g] || !d_off[g])) return CMTV_EINVAL;
+    if (!d_bitmap_all[g]) return CMTV_EINVAL;
+    W = std::max(W, (n_shard[g] + 63) / 64);
+  }
+  if (words_per_shard) *words_per_shard = W;
+  if (W == 0) return CMTV_OK;
+  uint64_t* bufs[kMaxDevices];
+  hipError_t e;
+  for (size_t g = 0; g < G; g++) {
+    CmtvDev& D = ctx->devs[g];
+    if (hipSetDevice(D.ordinal) != hipSuccess) return CMTV_ENODEV;
+    bufs[g] = static_cast<uint64_t*>(d_bitmap_all[g]);
+    // words of this shard beyond its signatures stay zero (quad kernels write
+    // whole 16-bit slices, lane kernels whole words; a short shard leaves the
+    // rest of its W words untouched)
+    const size_t own = (n_shard[g] + 63) / 64;
+    if (own < W && (e = hipMemsetAsync(bufs[g] + g * W + own, 0, 8 * (W - own), D.stream)) != hipSuccess)
+      return hip_fail(e);
+    uint8_t* dv = d_valid ? static_cast<uint8_t*>(d_valid[g]) : nullptr;
+    int rc;
+    if (ks)
+      rc = enqueue_verify_keyed(ctx, D, ks->dev[g], ks->n, n_shard[g], static_cast<const uint32_t*>(d_keys[g]),
+                                static_cast<const uint8_t*>(d_sig[g]), static_cast<const uint8_t*>(d_msg[g]),
+                                static_cast<const uint32_t*>(d_off[g]), mode, dv, bufs[g] + g * W, D.stream);
+    else
+      rc = enqueue_verify(ctx, D, n_shard[g], static_cast<const uint8_t*>(d_keys[g]),
+                          static_cast<const uint8_t*>(d_sig[g]), static_cast<const uint8_t*>(d_msg[g]),
+                          static_cast<const uint32_t*>(d_off[g]), mode, dv, bufs[g] + g * W, D.stream);
+    if (rc != CMTV_OK) return rc;
+  }
+  if (G > 1) ctx->stats.sharded_calls++;
+  const int rc = gather_bitmaps(ctx, G, W, bufs);
+  (void)hipSetDevice(ctx->devs[0].ordinal);
+  return rc;
+}
+
+}  // namespace cmtv
+
+extern "C" {
+
+int cmtv_verify_ed25519_sharded_device(cmtv_ctx* ctx, const size_t* n_shard, const void* const* d_pk,
+                                       const void* const* d_sig, const void* const* d_msg,
+                                       const void* const* d_msg_off, uint32_t mode, void* const* d_valid,
+                                       void* const* d_bitmap_all, size_t* words_per_shard) {
+  if (!ctx || mode > CMTV_MODE_ZIP215 || !n_shard || !d_pk || !d_sig || !d_msg || !d_msg_off || !d_bitmap_all)
+    return CMTV_EINVAL;
+  std::unique_lock<std::mutex> lk;
+  if (ctx_lock(ctx, lk) != CMTV_OK) return CMTV_ENODEV;
+  return sharded_device(ctx, nullptr, n_shard, d_pk, d_sig, d_msg, d_msg_off, mode, d_valid, d_bitmap_all,
+                        words_per_shard);
+}
+
+int cmtv_verify_ed25519_indexed_sharded_device(cmtv_ctx* ctx, const cmtv_keyset* ks, const size_t* n_shard,
+                                               const void* const* d_key_idx, const void* const* d_sig,
+                                               const void* const* d_msg, const void* const* d_msg_off,
+                                               uint32_t mode, void* const* d_valid, void* const* d_bitmap_all,
+                                               size_t* words_per_shard) {
+  if (!ctx || !ks || ks->ctx != ctx || mode > CMTV_MODE_ZIP215 || !n_shard || !d_key_idx || !d_sig || !d_msg ||
+      !d_msg_off || !d_bitmap_all)
+    return CMTV_EINVAL;
+  std::unique_lock<std::mutex> lk;
+  if (ctx_lock(ctx, lk) != CMTV_OK) return CMTV_ENODEV;
+  return sharded_device(ctx, ks, n_shard, d_key_idx, d_sig, d_msg, d_msg_off, mode, d_valid, d_bitmap_all,
+                        words_per_shard);
 }
 
 int cmtv_register_keys(cmtv_ctx* ctx, size_t n_keys, const uint8_t* pk, cmtv_keyset** out) {
@@ -611,21 +1174,25 @@ int cmtv_register_keys(cmtv_ctx* ctx, size_t n_keys, const uint8_t* pk, cmtv_key
   *out = nullptr;
   // 512 KiB of comb per key; 2^20 keys would already be 512 GiB
   if (!ctx || n_keys == 0 || n_keys > (1u << 20) || !pk) return CMTV_EINVAL;
-  std::lock_guard<std::mutex> g(ctx->mu);
-  if (hipSetDevice(ctx->device) != hipSuccess) return CMTV_ENODEV;
+  std::unique_lock<std::mutex> lk;
+  if (ctx_lock(ctx, lk) != CMTV_OK) return CMTV_ENODEV;
   return cmtv::register_keys_locked(ctx, n_keys, pk, out);
 }
 
 int cmtv_keyset_cache(cmtv_ctx* ctx, size_t max_sets) {
   if (!ctx || max_sets > 4096) return CMTV_EINVAL;
-  std::lock_guard<std::mutex> g(ctx->mu);
-  if (hipSetDevice(ctx->device) != hipSuccess) return CMTV_ENODEV;
-  (void)hipStreamSynchronize(ctx->stream);
+  std::unique_lock<std::mutex> lk;
+  if (ctx_lock(ctx, lk) != CMTV_OK) return CMTV_ENODEV;
+  for (auto& D : ctx->devs) {
+    (void)hipSetDevice(D.ordinal);
+    (void)hipStreamSynchronize(D.stream);
+  }
   while (ctx->keysets.size() > max_sets) {
     cmtv_keyset_free(ctx->keysets.front().second);
     ctx->keysets.erase(ctx->keysets.begin());
   }
   ctx->keyset_cap = max_sets;
+  (void)hipSetDevice(ctx->devs[0].ordinal);
   return CMTV_OK;
 }
 
@@ -634,31 +1201,43 @@ int cmtv_keyset_cache(cmtv_ctx* ctx, size_t max_sets) {
 namespace cmtv {
 
 int register_keys_locked(cmtv_ctx* ctx, size_t n_keys, const uint8_t* pk, cmtv_keyset** out) {
-  int rc = ensure_bcomb(ctx);
-  if (rc != CMTV_OK) return rc;
   auto* ks = new (std::nothrow) cmtv_keyset();
   if (!ks) return CMTV_ENOMEM;
   ks->ctx = ctx;
   ks->n = n_keys;
   ks->pk.assign(pk, pk + 32 * n_keys);
-  DevBuf scratch;
-  hipError_t e = hipMalloc(&ks->d_pk, 32 * n_keys);
-  if (e == hipSuccess) e = hipMalloc(&ks->d_ok, n_keys);
-  if (e == hipSuccess) e = hipMalloc(&ks->d_tab, n_keys * (size_t)kCombWords * sizeof(uint32_t));
-  if (e == hipSuccess)
-    e = scratch.ensure((size_t)std::min<size_t>(n_keys, kCombKeyChunk) * kCombScratchWordsPerKey * sizeof(uint32_t));
-  if (e == hipSuccess) e = hipMemcpyAsync(ks->d_pk, pk, 32 * n_keys, hipMemcpyHostToDevice, ctx->stream);
-  for (size_t c = 0; e == hipSuccess && c < n_keys; c += kCombKeyChunk) {
-    const uint32_t cn = (uint32_t)std::min<size_t>(kCombKeyChunk, n_keys - c);
-    e = launch_comb_build(cn, ks->d_pk + 8 * c, ks->d_ok + c, ks->d_tab + c * (size_t)kCombWords,
-                          static_cast<uint32_t*>(scratch.p), true, ctx->stream);
+  ks->dev.resize(ctx->devs.size());
+  for (size_t g = 0; g < ctx->devs.size(); g++) {
+    CmtvDev& D = ctx->devs[g];
+    auto& K = ks->dev[g];
+    (void)hipSetDevice(D.ordinal);
+    int rc = ensure_bcomb(D);
+    if (rc != CMTV_OK) {
+      cmtv_keyset_free(ks);
+      return rc;
+    }
+    DevBuf scratch;
+    hipError_t e = hipMalloc(&K.d_pk, 32 * n_keys);
+    if (e == hipSuccess) e = hipMalloc(&K.d_ok, n_keys);
+    if (e == hipSuccess) e = hipMalloc(&K.d_tab, n_keys * (size_t)kCombWords * sizeof(uint32_t));
+    if (e == hipSuccess)
+      e = scratch.ensure((size_t)std::min<size_t>(n_keys, kCombKeyChunk) * kCombScratchWordsPerKey *
+                         sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemcpyAsync(K.d_pk, pk, 32 * n_keys, hipMemcpyHostToDevice, D.stream);
+    for (size_t c = 0; e == hipSuccess && c < n_keys; c += kCombKeyChunk) {
+      const uint32_t cn = (uint32_t)std::min<size_t>(kCombKeyChunk, n_keys - c);
+      e = launch_comb_build(cn, K.d_pk + 8 * c, K.d_ok + c, K.d_tab + c * (size_t)kCombWords,
+                            static_cast<uint32_t*>(scratch.p), true, D.stream);
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(D.stream);
+    scratch.release();
+    if (e != hipSuccess) {
+      cmtv_keyset_free(ks);
+      (void)hipSetDevice(ctx->devs[0].ordinal);
+      return hip_fail(e);
+    }
   }
-  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
-  scratch.release();
-  if (e != hipSuccess) {
-    cmtv_keyset_free(ks);
-    return hip_fail(e);
-  }
+  (void)hipSetDevice(ctx->devs[0].ordinal);
   *out = ks;
   return CMTV_OK;
 }
@@ -686,10 +1265,15 @@ extern "C" {
 
 void cmtv_keyset_free(cmtv_keyset* ks) {
   if (!ks) return;
-  (void)hipSetDevice(ks->ctx->device);
-  if (ks->d_pk) (void)hipFree(ks->d_pk);
-  if (ks->d_ok) (void)hipFree(ks->d_ok);
-  if (ks->d_tab) (void)hipFree(ks->d_tab);
+  for (size_t g = 0; g < ks->dev.size(); g++) {
+    (void)hipSetDevice(ks->ctx->devs[g].ordinal);
+    (void)hipStreamSynchronize(ks->ctx->devs[g].stream);  // no kernel may still read the combs
+    auto& K = ks->dev[g];
+    if (K.d_pk) (void)hipFree(K.d_pk);
+    if (K.d_ok) (void)hipFree(K.d_ok);
+    if (K.d_tab) (void)hipFree(K.d_tab);
+  }
+  if (!ks->ctx->devs.empty()) (void)hipSetDevice(ks->ctx->devs[0].ordinal);
   delete ks;
 }
 
@@ -703,43 +1287,18 @@ int cmtv_verify_ed25519_indexed(cmtv_ctx* ctx, const cmtv_keyset* ks, size_t n, 
   if (!key_idx || !sig || !msg_off || (!msg && msg_off[n] != 0) || (!out_valid && !out_bitmap)) return CMTV_EINVAL;
   for (size_t i = 0; i < n; i++)
     if (msg_off[i + 1] < msg_off[i] || key_idx[i] >= ks->n) return CMTV_EINVAL;
-  std::lock_guard<std::mutex> g(ctx->mu);
-  if (hipSetDevice(ctx->device) != hipSuccess) return CMTV_ENODEV;
-  const size_t msg_bytes = msg_off[n];
-  // staging layout: [key_idx n*4][sig n*64][off (n+1)*4][msg msg_bytes + 16]
-  const size_t o_idx = 0, o_sig = align_up(4 * n, 256), o_off = align_up(o_sig + 64 * n, 256);
-  const size_t o_msg = align_up(o_off + 4 * (n + 1), 256), in_bytes = align_up(o_msg + msg_bytes + 16, 256);
-  const size_t words = (n + 63) / 64;
-  const size_t o_bm = 0, o_valid = align_up(8 * words, 256), out_bytes = align_up(o_valid + n, 256);
-  hipError_t e;
-  if ((e = ctx->h_in.ensure(in_bytes)) != hipSuccess) return hip_fail(e);
-  if ((e = ctx->d_in.ensure(in_bytes)) != hipSuccess) return hip_fail(e);
-  if ((e = ctx->h_out.ensure(out_bytes)) != hipSuccess) return hip_fail(e);
-  if ((e = ctx->d_out.ensure(out_bytes)) != hipSuccess) return hip_fail(e);
-  auto* hin = static_cast<uint8_t*>(ctx->h_in.p);
-  std::memcpy(hin + o_idx, key_idx, 4 * n);
-  std::memcpy(hin + o_sig, sig, 64 * n);
-  std::memcpy(hin + o_off, msg_off, 4 * (n + 1));
-  if (msg_bytes) std::memcpy(hin + o_msg, msg, msg_bytes);
-  std::memset(hin + o_msg + msg_bytes, 0, 16);
-  auto* din = static_cast<uint8_t*>(ctx->d_in.p);
-  auto* dout = static_cast<uint8_t*>(ctx->d_out.p);
-  if ((e = hipMemcpyAsync(din, hin, in_bytes, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess) return hip_fail(e);
-  int rc = enqueue_verify_keyed(ctx, ks, n, reinterpret_cast<uint32_t*>(din + o_idx), din + o_sig, din + o_msg,
-                                reinterpret_cast<uint32_t*>(din + o_off), mode, dout + o_valid,
-                                reinterpret_cast<uint64_t*>(dout + o_bm), ctx->stream);
-  if (rc != CMTV_OK) return rc;
-  auto* hout = static_cast<uint8_t*>(ctx->h_out.p);
-  if ((e = hipMemcpyAsync(hout, dout, out_bytes, hipMemcpyDeviceToHost, ctx->stream)) != hipSuccess) return hip_fail(e);
-  if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return hip_fail(e);
-  harvest_timing(ctx);
-  uint64_t invalid = 0;
-  const uint8_t* hv = hout + o_valid;
-  for (size_t i = 0; i < n; i++) invalid += hv[i] == 0;
-  ctx->stats.invalid += invalid;
-  if (out_valid) std::memcpy(out_valid, hv, n);
-  if (out_bitmap) std::memcpy(out_bitmap, hout + o_bm, 8 * words);
-  return CMTV_OK;
+  std::unique_lock<std::mutex> lk;
+  if (ctx_lock(ctx, lk) != CMTV_OK) return CMTV_ENODEV;
+  static const uint8_t empty = 0;
+  HostBatch B;
+  B.n = n;
+  B.mode = mode;
+  B.ks = ks;
+  B.key_idx = key_idx;
+  B.sig = sig;
+  B.msg = msg ? msg : &empty;
+  B.msg_off = msg_off;
+  return run_host_batch(ctx, B, out_valid, out_bitmap);
 }
 
 int cmtv_verify_ed25519_indexed_device(cmtv_ctx* ctx, const cmtv_keyset* ks, size_t n, const void* d_key_idx,
@@ -748,9 +1307,9 @@ int cmtv_verify_ed25519_indexed_device(cmtv_ctx* ctx, const cmtv_keyset* ks, siz
   if (!ctx || !ks || ks->ctx != ctx || mode > CMTV_MODE_ZIP215 || n > (1ull << 31)) return CMTV_EINVAL;
   if (n == 0) return CMTV_OK;
   if (!d_key_idx || !d_sig || !d_msg || !d_msg_off || (!d_valid && !d_bitmap)) return CMTV_EINVAL;
-  std::lock_guard<std::mutex> g(ctx->mu);
-  if (hipSetDevice(ctx->device) != hipSuccess) return CMTV_ENODEV;
-  return enqueue_verify_keyed(ctx, ks, n, static_cast<const uint32_t*>(d_key_idx),
+  std::unique_lock<std::mutex> lk;
+  if (ctx_lock(ctx, lk) != CMTV_OK) return CMTV_ENODEV;
+  return enqueue_verify_keyed(ctx, ctx->devs[0], ks->dev[0], ks->n, n, static_cast<const uint32_t*>(d_key_idx),
                               static_cast<const uint8_t*>(d_sig), static_cast<const uint8_t*>(d_msg),
                               static_cast<const uint32_t*>(d_msg_off), mode, static_cast<uint8_t*>(d_valid),
                               static_cast<uint64_t*>(d_bitmap), static_cast<hipStream_t>(stream));
@@ -759,22 +1318,23 @@ int cmtv_verify_ed25519_indexed_device(cmtv_ctx* ctx, const cmtv_keyset* ks, siz
 int cmtv_pubkeys_ed25519(cmtv_ctx* ctx, size_t n, const uint8_t* seeds, uint8_t* out_pk) {
   if (!ctx || n > (1ull << 31) || (n && (!seeds || !out_pk))) return CMTV_EINVAL;
   if (n == 0) return CMTV_OK;
-  std::lock_guard<std::mutex> g(ctx->mu);
-  if (hipSetDevice(ctx->device) != hipSuccess) return CMTV_ENODEV;
+  std::unique_lock<std::mutex> lk;
+  if (ctx_lock(ctx, lk) != CMTV_OK) return CMTV_ENODEV;
+  CmtvDev& D = ctx->devs[0];
   hipError_t e;
-  if ((e = ctx->d_in.ensure(32 * n)) != hipSuccess) return hip_fail(e);
-  if ((e = ctx->d_out.ensure(32 * n)) != hipSuccess) return hip_fail(e);
-  if ((e = hipMemcpyAsync(ctx->d_in.p, seeds, 32 * n, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess)
+  if ((e = D.d_in.ensure(32 * n)) != hipSuccess) return hip_fail(e);
+  if ((e = D.d_out.ensure(32 * n)) != hipSuccess) return hip_fail(e);
+  if ((e = hipMemcpyAsync(D.d_in.p, seeds, 32 * n, hipMemcpyHostToDevice, D.stream)) != hipSuccess)
     return hip_fail(e);
   for (size_t c = 0; c < n; c += kChunk) {
     const uint32_t cn = (uint32_t)std::min<size_t>(kChunk, n - c);
-    if ((e = launch_pubkey(cn, static_cast<uint8_t*>(ctx->d_in.p) + 32 * c, ctx->d_btab,
-                           static_cast<uint8_t*>(ctx->d_out.p) + 32 * c, ctx->stream)) != hipSuccess)
+    if ((e = launch_pubkey(cn, static_cast<uint8_t*>(D.d_in.p) + 32 * c, D.d_btab,
+                           static_cast<uint8_t*>(D.d_out.p) + 32 * c, D.stream)) != hipSuccess)
       return hip_fail(e);
   }
-  if ((e = hipMemcpyAsync(out_pk, ctx->d_out.p, 32 * n, hipMemcpyDeviceToHost, ctx->stream)) != hipSuccess)
+  if ((e = hipMemcpyAsync(out_pk, D.d_out.p, 32 * n, hipMemcpyDeviceToHost, D.stream)) != hipSuccess)
     return hip_fail(e);
-  if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return hip_fail(e);
+  if ((e = hipStreamSynchronize(D.stream)) != hipSuccess) return hip_fail(e);
   return CMTV_OK;
 }
 
@@ -790,33 +1350,33 @@ int cmtv_sign_ed25519(cmtv_ctx* ctx, size_t n, const uint8_t* seeds, const uint3
   }
   for (size_t i = 0; i < n; i++)
     if (msg_off[i + 1] < msg_off[i]) return CMTV_EINVAL;
-  std::lock_guard<std::mutex> g(ctx->mu);
-  if (hipSetDevice(ctx->device) != hipSuccess) return CMTV_ENODEV;
+  std::unique_lock<std::mutex> lk;
+  if (ctx_lock(ctx, lk) != CMTV_OK) return CMTV_ENODEV;
+  CmtvDev& D = ctx->devs[0];
   const size_t msg_bytes = msg_off[n];
   const size_t o_seed = 0, o_idx = align_up(32 * nseeds, 256), o_off = align_up(o_idx + (key_idx ? 4 * n : 0), 256);
   const size_t o_msg = align_up(o_off + 4 * (n + 1), 256), in_bytes = align_up(o_msg + msg_bytes + 16, 256);
   hipError_t e;
-  if ((e = ctx->h_in.ensure(in_bytes)) != hipSuccess) return hip_fail(e);
-  if ((e = ctx->d_in.ensure(in_bytes)) != hipSuccess) return hip_fail(e);
-  if ((e = ctx->d_out.ensure(64 * n)) != hipSuccess) return hip_fail(e);
-  auto* hin = static_cast<uint8_t*>(ctx->h_in.p);
+  if ((e = D.h_in.ensure(in_bytes)) != hipSuccess) return hip_fail(e);
+  if ((e = D.d_in.ensure(in_bytes)) != hipSuccess) return hip_fail(e);
+  if ((e = D.d_out.ensure(64 * n)) != hipSuccess) return hip_fail(e);
+  auto* hin = static_cast<uint8_t*>(D.h_in.p);
   std::memcpy(hin + o_seed, seeds, 32 * nseeds);
   if (key_idx) std::memcpy(hin + o_idx, key_idx, 4 * n);
   std::memcpy(hin + o_off, msg_off, 4 * (n + 1));
   if (msg_bytes) std::memcpy(hin + o_msg, msg, msg_bytes);
-  auto* din = static_cast<uint8_t*>(ctx->d_in.p);
-  if ((e = hipMemcpyAsync(din, hin, in_bytes, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess) return hip_fail(e);
+  auto* din = static_cast<uint8_t*>(D.d_in.p);
+  if ((e = hipMemcpyAsync(din, hin, in_bytes, hipMemcpyHostToDevice, D.stream)) != hipSuccess) return hip_fail(e);
   for (size_t c = 0; c < n; c += kChunk) {
     const uint32_t cn = (uint32_t)std::min<size_t>(kChunk, n - c);
     if ((e = launch_sign(cn, key_idx ? din + o_seed : din + o_seed + 32 * c, key_idx ? din + o_idx + 4 * c : nullptr,
-                         din + o_msg,
-                         din + o_off + 4 * c, ctx->d_btab, static_cast<uint8_t*>(ctx->d_out.p) + 64 * c,
-                         ctx->stream)) != hipSuccess)
+                         din + o_msg, din + o_off + 4 * c, D.d_btab, static_cast<uint8_t*>(D.d_out.p) + 64 * c,
+                         D.stream)) != hipSuccess)
       return hip_fail(e);
   }
-  if ((e = hipMemcpyAsync(out_sig, ctx->d_out.p, 64 * n, hipMemcpyDeviceToHost, ctx->stream)) != hipSuccess)
+  if ((e = hipMemcpyAsync(out_sig, D.d_out.p, 64 * n, hipMemcpyDeviceToHost, D.stream)) != hipSuccess)
     return hip_fail(e);
-  if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return hip_fail(e);
+  if ((e = hipStreamSynchronize(D.stream)) != hipSuccess) return hip_fail(e);
   return CMTV_OK;
 }
 

@@ -24,6 +24,13 @@
  *     returning (cgo pointer rules).
  *   - Thread-safe: a context serialises its own calls with a mutex and calls
  *     hipSetDevice on entry (Go goroutines migrate between OS threads).
+ *     Device-resident (_device) calls on different streams are ordered
+ *     against each other wherever they share context scratch.
+ *   - One context may drive several devices (cmtv_open_devices): host-buffer
+ *     batches are split into contiguous 64-aligned shards, one per device,
+ *     and the shards' verdict bitmaps are all-gathered over RCCL (xGMI) so
+ *     the caller gets one verdict vector. A Go node is one process, so this
+ *     is how it uses every GPU of the node.
  *   - Messages: one flat byte buffer + (n+1) uint32 offsets; message i is
  *     msg[msg_off[i] .. msg_off[i+1]).
  *   - Bitmaps: uint64 words, bit (i % 64) of word (i / 64) = verdict of i.
@@ -41,7 +48,7 @@
 extern "C" {
 #endif
 
-#define CMTV_ABI_VERSION 3
+#define CMTV_ABI_VERSION 4
 
 enum {
   CMTV_OK = 0,
@@ -75,14 +82,45 @@ typedef struct cmtv_stats {
   double last_kernel_ms;   /* the most recent verify kernel       */
   uint64_t cache_hits;     /* verdicts served by the verdict cache */
   uint64_t cache_entries;  /* verdicts currently cached           */
+  uint64_t keyed_launches; /* launches of the registered-key kernels */
+  uint64_t sharded_calls;  /* batches split over more than one device */
+  uint64_t gathers;        /* bitmap all-gathers (RCCL or peer copy) */
+  uint64_t faults_injected;/* launches failed by the CMTV_FAULT_AT knob */
+  uint32_t n_devices;      /* devices driven by the context       */
+  uint32_t rccl;           /* 1: gathers run over an RCCL communicator */
 } cmtv_stats;
 
 /* ------------------------------------------------------------ lifecycle */
 
 /* Opens a context on one device: creates its stream, uploads the fixed-base
  * table of (1..128)B (built on the device), allocates pinned staging.
- * Replaces: nothing in the reference (it has no device state). */
+ * Replaces: nothing in the reference (it has no device state).
+ * Environment (read at open): CMTV_QUAD_MAX / CMTV_KEYED_QUAD_MAX / CMTV_LANE_CHUNK
+ * (kernel crossovers), CMTV_FAULT_AT=N (test knob: the N-th verification
+ * launch of the context fails with CMTV_EHIP without running; libs/fail
+ * FAIL_TEST_INDEX analogue). */
 int cmtv_open(const cmtv_config* cfg, cmtv_ctx** out);
+
+/* Opens ONE context over several devices (a node is one
+ * process; blockchain/v0/reactor.go:349-400 verifies from one goroutine).
+ * devices[0..n_devices) are HIP ordinals; n_devices == 0 takes the list from
+ * CMTVERIFY_DEVICES ("0,1,2,3" or "all"), or every visible gfx950 device when
+ * it is unset. Each device gets its own stream, staging, fixed-base tables
+ * and registered-key combs; when the ordinals are distinct an RCCL
+ * communicator over them (ncclCommInitAll) carries the bitmap all-gather,
+ * otherwise (a repeated ordinal, used to exercise sharding on one GPU) peer
+ * copies do. Host-buffer batches of at least CMTV_SHARD_MIN (default 8192)
+ * signatures per device are sharded; smaller ones run on devices[0].
+ * Device-resident single-device calls (_device) run on devices[0].
+ * cfg->device is ignored; cfg may be NULL (then CMTVERIFY_MODE = "go" |
+ * "zip215" picks the default mode). */
+int cmtv_open_devices(const cmtv_config* cfg, const int32_t* devices, size_t n_devices, cmtv_ctx** out);
+int cmtv_device_count(const cmtv_ctx* ctx);
+/* HIP ordinal / hipStream_t (as void*) of the context's g-th device */
+int cmtv_device_ordinal(const cmtv_ctx* ctx, int g);
+void* cmtv_device_stream(cmtv_ctx* ctx, int g);
+/* Waits for every device stream of the context. */
+int cmtv_sync(cmtv_ctx* ctx);
 void cmtv_close(cmtv_ctx* ctx);
 const char* cmtv_strerror(int code);
 int cmtv_abi_version(void);
@@ -108,6 +146,20 @@ int cmtv_verify_ed25519(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_
  * (n bytes) and d_bitmap (ceil(n/64) words) may each be NULL. */
 int cmtv_verify_ed25519_device(cmtv_ctx* ctx, size_t n, const void* d_pk, const void* d_sig, const void* d_msg,
                                const void* d_msg_off, uint32_t mode, void* d_valid, void* d_bitmap, void* stream);
+
+/* Multi-device, device-resident (bench / configs[2] replay): shard g has
+ * n_shard[g] signatures whose inputs (layout as cmtv_verify_ed25519_device)
+ * are resident on the context's g-th device. Every device verifies its shard
+ * on its own stream; the shard bitmaps are then all-gathered (RCCL, in place)
+ * so that each device's d_bitmap_all[g] -- G x W words, W = max over shards
+ * of ceil(n_shard / 64), returned in *words_per_shard -- holds shard h's
+ * verdict bits at words [h W, h W + ceil(n_shard[h] / 64)). d_valid[g]
+ * (n_shard[g] bytes) may be NULL, or the array itself NULL. Non-blocking:
+ * cmtv_sync waits. */
+int cmtv_verify_ed25519_sharded_device(cmtv_ctx* ctx, const size_t* n_shard, const void* const* d_pk,
+                                       const void* const* d_sig, const void* const* d_msg,
+                                       const void* const* d_msg_off, uint32_t mode, void* const* d_valid,
+                                       void* const* d_bitmap_all, size_t* words_per_shard);
 
 /* ------------------------------------------------------------ verdict cache */
 
@@ -185,6 +237,15 @@ int cmtv_verify_ed25519_indexed(cmtv_ctx* ctx, const cmtv_keyset* ks, size_t n, 
 int cmtv_verify_ed25519_indexed_device(cmtv_ctx* ctx, const cmtv_keyset* ks, size_t n, const void* d_key_idx,
                                        const void* d_sig, const void* d_msg, const void* d_msg_off, uint32_t mode,
                                        void* d_valid, void* d_bitmap, void* stream);
+
+/* The same, sharded across the context's devices (see
+ * cmtv_verify_ed25519_sharded_device for the layout): d_key_idx[g] indexes
+ * the key set, which is registered on every device of the context. */
+int cmtv_verify_ed25519_indexed_sharded_device(cmtv_ctx* ctx, const cmtv_keyset* ks, const size_t* n_shard,
+                                               const void* const* d_key_idx, const void* const* d_sig,
+                                               const void* const* d_msg, const void* const* d_msg_off,
+                                               uint32_t mode, void* const* d_valid, void* const* d_bitmap_all,
+                                               size_t* words_per_shard);
 
 /* ------------------------------------------------------------ crypto.BatchVerifier mirror */
 

@@ -916,6 +916,15 @@ static void sr_challenge(uint8_t k[32], const uint8_t pk[32], const uint8_t R[32
   sc_reduce64(k, kb);
 }
 
+/* the verifier's challenge k for n (pk, R, msg) triples (test-vector
+ * generation: tests/golden/make_wide.py searches messages for k values the
+ * product's half-size-scalar split handles on its wide fallback) */
+void oracle_sr25519_challenge_batch(size_t n, const uint8_t *pk, const uint8_t *R, const uint8_t *msg,
+                                    const uint32_t *off, uint8_t *out_k) {
+  for (size_t i = 0; i < n; i++)
+    sr_challenge(out_k + 32 * i, pk + 32 * i, R + 32 * i, msg + off[i], off[i + 1] - off[i]);
+}
+
 /* RFC 9496 SQRT_RATIO_M1: r = |sqrt(u/v)| or |sqrt(i u/v)|; returns was_square */
 static int fe_sqrt_ratio_m1(fe *r, const fe *u, const fe *v) {
   fe v3, v7, t, check, nu, nui;

@@ -41,6 +41,8 @@ def lib():
         L.oracle_sr25519_pubkey.restype = None
         L.oracle_sr25519_sign_batch.argtypes = [ctypes.c_size_t, u8p, u32p, u8p, u32p, u8p]
         L.oracle_sr25519_sign_batch.restype = None
+        L.oracle_sr25519_challenge_batch.argtypes = [ctypes.c_size_t, u8p, u8p, u8p, u32p, u8p]
+        L.oracle_sr25519_challenge_batch.restype = None
         _lib = L
     return _lib
 
@@ -131,4 +133,19 @@ def sr25519_sign_batch(minis: np.ndarray, msg: np.ndarray, off: np.ndarray, key_
         key_idx = np.ascontiguousarray(key_idx, dtype=np.uint32)
         kp = _p(key_idx, ctypes.c_uint32)
     lib().oracle_sr25519_sign_batch(n, _p(minis), kp, _p(msg), _p(off, ctypes.c_uint32), _p(out))
+    return out[:n]
+
+
+def sr25519_challenges(pk: np.ndarray, R: np.ndarray, msg: np.ndarray, off: np.ndarray) -> np.ndarray:
+    """The merlin challenge k (32-byte little-endian, reduced mod L) of each
+    (pk, R, msg) triple, as sr25519 verification computes it."""
+    n = len(off) - 1
+    pk = np.ascontiguousarray(pk, dtype=np.uint8)
+    R = np.ascontiguousarray(R, dtype=np.uint8)
+    msg = np.ascontiguousarray(msg, dtype=np.uint8)
+    if msg.size == 0:
+        msg = np.zeros(1, np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.uint32)
+    out = np.zeros((max(n, 1), 32), dtype=np.uint8)
+    lib().oracle_sr25519_challenge_batch(n, _p(pk), _p(R), _p(msg), _p(off, ctypes.c_uint32), _p(out))
     return out[:n]

@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_strerror():
     lib = N.lib()
-    assert lib.cmtv_abi_version() == 3
+    assert lib.cmtv_abi_version() == 4
     for code in (N.CMTV_OK, N.CMTV_EINVAL, N.CMTV_ENODEV, N.CMTV_ENOMEM, N.CMTV_EHIP, N.CMTV_ERCCL, N.CMTV_ECOMMIT):
         assert lib.cmtv_strerror(code)
 
@@ -108,3 +108,28 @@ def test_keyset_entry_points_reject_bad_arguments_without_gpu():
     assert lib.cmtv_verify_ed25519_indexed(None, None, 1, None, None, None, None, 0, None, None) == N.CMTV_EINVAL
     assert lib.cmtv_verify_ed25519_indexed_device(None, None, 1, None, None, None, None, 0, None, None,
                                                   None) == N.CMTV_EINVAL
+
+
+def test_multi_device_entry_points_reject_bad_arguments_without_gpu():
+    lib = N.lib()
+    h = ctypes.c_void_p()
+    assert lib.cmtv_open_devices(None, None, 0, None) == N.CMTV_EINVAL
+    assert lib.cmtv_open_devices(None, None, 3, ctypes.byref(h)) == N.CMTV_EINVAL  # n > 0 needs a list
+    assert lib.cmtv_device_count(None) == 0
+    assert lib.cmtv_device_ordinal(None, 0) == N.CMTV_EINVAL
+    assert lib.cmtv_device_stream(None, 0) is None
+    assert lib.cmtv_sync(None) == N.CMTV_EINVAL
+    assert lib.cmtv_verify_ed25519_sharded_device(None, None, None, None, None, None, 0, None, None,
+                                                  None) == N.CMTV_EINVAL
+    assert lib.cmtv_verify_ed25519_indexed_sharded_device(None, None, None, None, None, None, None, 0, None, None,
+                                                          None) == N.CMTV_EINVAL
+
+
+def test_open_devices_without_gpu_is_enodev():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    arr = (ctypes.c_int32 * 2)(0, 1)
+    h = ctypes.c_void_p()
+    assert N.lib().cmtv_open_devices(None, arr, 2, ctypes.byref(h)) == N.CMTV_ENODEV

@@ -74,7 +74,7 @@ def test_one_device_context_equals_single_device_path(gpu_ctx, corpus):
     assert st["n_devices"] == 1 and st["sharded_calls"] == 0
 
 
-@pytest.mark.parametrize("n", [130, 3001, 50_000])
+@pytest.mark.parametrize("n", [400, 3001, 50_000])
 def test_sharding_over_a_repeated_device(n):
     with _env(CMTV_SHARD_MIN=64):
         ctx = Context(devices=[0, 0, 0])

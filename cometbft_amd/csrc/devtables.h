@@ -70,15 +70,16 @@ struct DevBTabQ {
 };
 
 // Quad policy (quad.h): 4 consecutive lanes = one signature; operand exchange
-// inside the quad is a DPP quad_perm move. update_dpp with old = src and
-// bound_ctrl off: the mov_dpp(bound_ctrl:1) form miscompiles on ROCm 7.2 /
-// gfx950 once DPP-combine folds it into the consumers (lanes 0-1 of a quad
-// read wrong values; found with tools/dbg/quad_debug.hip).
+// inside the quad is a DPP quad_perm move. mov_dpp with bound_ctrl off: one
+// v_mov_b32_dpp per word (update_dpp(old = src) costs an extra v_mov for the
+// tied old operand), and DPP-combine leaves it alone -- the bound_ctrl:1 form
+// miscompiles on ROCm 7.2 / gfx950 once DPP-combine folds it into its
+// consumers (lanes 0-1 of a quad read wrong values; tools/dbg/quad_debug.hip).
 struct DevQuad {
   __device__ __forceinline__ int lane() const { return threadIdx.x & 3; }
   template <int PAT>
   __device__ __forceinline__ uint32_t dpp(uint32_t x) const {
-    return (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, PAT, 0xF, 0xF, false);
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, PAT, 0xF, 0xF, false);
   }
   template <int PAT>
   __device__ __forceinline__ void perm(fe& o, const fe& v) const {
@@ -109,6 +110,19 @@ struct DevATabQ {
       c.v[2 * k] = x.x;
       c.v[2 * k + 1] = x.y;
     }
+  }
+  // (neg ? -P_e : P_e): lanes 0/1 read each other's slot (Y-X <-> Y+X),
+  // lane 3 negates 2dT
+  template <class Q>
+  __device__ __forceinline__ void load_signed(const Q& q, int e, bool neg, fe& c) const {
+    const uint32_t src = (t & 2) ? t : (t ^ (neg ? 1u : 0u));
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+      const uint2 x = lds[(e * 5 + k) * 64 + src];
+      c.v[2 * k] = x.x;
+      c.v[2 * k + 1] = x.y;
+    }
+    q_negate_lane3(c, (int)(t & 3), neg);
   }
 };
 

@@ -14,17 +14,11 @@
 
 namespace cmtv {
 
-// lane c's cached coordinate (Y-X, Y+X, Z = 1, 2dT) of comb row `row`
-// (affine niels: y+x[10] y-x[10] 2dxy[10] pad[2]); e < 0: the identity
-template <class Q>
-CMTV_HD void q_comb_coord(const Q& q, fe& c, const uint32_t* row, bool ident) {
-  const int lane = q.lane();
-  const int off = lane == 0 ? 10 : (lane == 3 ? 20 : 0);
+// 10 limbs of a comb row (affine niels: y+x[10] y-x[10] 2dxy[10] pad[2]) at
+// word `off`
+CMTV_HD void comb_load(const uint32_t* row, int off, fe& r) {
 #pragma unroll
-  for (int i = 0; i < 10; i++) c.v[i] = row[off + i];
-  const bool one = lane == 2 || (ident && lane != 3);
-#pragma unroll
-  for (int i = 0; i < 10; i++) c.v[i] = (ident || lane == 2) ? ((one && i == 0) ? 1u : 0u) : c.v[i];
+  for (int i = 0; i < 10; i++) r.v[i] = row[off + i];
 }
 
 template <uint32_t MODE, class Q>
@@ -71,16 +65,16 @@ CMTV_HD bool q_verify_keyed(const Q& q, const uint32_t* key_pk, bool key_ok, con
       const int dA = (int)sc_shift_out(tk, 8) - 128;
       const int ia = dA < 0 ? -dA : dA;
       fe c;
-      q_comb_coord(q, c, ktab + ((size_t)j * COMB_ENTRIES + (ia > 0 ? ia - 1 : 0)) * COMB_ROW_WORDS, ia == 0);
-      q_cached_cneg(q, c, dA < 0);
+      const uint32_t* row = ktab + ((size_t)j * COMB_ENTRIES + (ia > 0 ? ia - 1 : 0)) * COMB_ROW_WORDS;
+      q_niels_coord(q, c, [&](int off, fe& r) { comb_load(row, off, r); }, 10, 20, dA < 0, ia == 0);
       q_add(q, v, c);
     }
     {
       const int dB = (int)sc_shift_out(ts, 8) - 128;
       const int ib = dB < 0 ? -dB : dB;
       fe c;
-      q_comb_coord(q, c, bcomb + ((size_t)j * COMB_ENTRIES + (ib > 0 ? ib - 1 : 0)) * COMB_ROW_WORDS, ib == 0);
-      q_cached_cneg(q, c, dB < 0);
+      const uint32_t* row = bcomb + ((size_t)j * COMB_ENTRIES + (ib > 0 ? ib - 1 : 0)) * COMB_ROW_WORDS;
+      q_niels_coord(q, c, [&](int off, fe& r) { comb_load(row, off, r); }, 10, 20, dB < 0, ib == 0);
       q_add(q, v, c);
     }
   }

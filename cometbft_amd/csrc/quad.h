@@ -33,6 +33,12 @@ namespace cmtv {
 constexpr int QP_B0 = 0x00, QP_B1 = 0x55, QP_B2 = 0xAA, QP_B3 = 0xFF;  // broadcast lane k
 constexpr int QP_SWAP01 = (1 << 0) | (0 << 2) | (2 << 4) | (3 << 6);    // [1,0,2,3]
 
+// quad_perm code: lane c reads lane s_c
+constexpr int qp(int s0, int s1, int s2, int s3) { return s0 | (s1 << 2) | (s2 << 4) | (s3 << 6); }
+
+// limb i of 2p (the bias of fe_sub / fe_neg)
+CMTV_HD uint32_t fe_p2(int i) { return i == 0 ? P2_0 : ((i & 1) ? P2_O : P2_E); }
+
 // h = {a, b, c, d}[lane]
 CMTV_HD void fe_pick(fe& h, int lane, const fe& a, const fe& b, const fe& c, const fe& d) {
   const bool l1 = lane & 1, l2 = lane & 2;
@@ -50,97 +56,94 @@ CMTV_HD void q_identity(fe& v, int lane) {
   v.v[0] = (lane == 1 || lane == 2) ? 1u : 0u;
 }
 
-// the identity's cached coordinate: (Y-X, Y+X, Z, 2dT) = (1, 1, 1, 0)
+// Cached form of an addend, one coordinate per lane: (Y-X, Y+X, 2Z, 2dT).
+// Lane 2 carries 2Z so that round 1 of an addition yields D = 2 Z1 Z2
+// directly. The identity's cached coordinate: (1, 1, 2, 0).
 CMTV_HD void q_cached_identity(fe& v, int lane) {
   fe_0(v);
-  v.v[0] = (lane != 3) ? 1u : 0u;
+  v.v[0] = lane == 2 ? 2u : (lane != 3 ? 1u : 0u);
 }
 
 // Doubling (dbl-2008-hwcd, a = -1, outputs negated as in ge25519.h p2_dbl):
 //   round 1: lane c squares {X, Y, Z, X+Y}[c]      -> A, B, C', K
-//   round 2: lane c multiplies {E'F', MS, F'M, E'S}[c]
-// Input T (lane 3) is ignored; output is a full extended point.
+//   round 2: lane c multiplies {E'F', MS, F'M, E'S}[c],
+//            S = A + B, M = A - B, E' = S - K, F' = 2C' + M
+// Routing: lane c forms U_c = {E', F', M, S}[c] (one carry for all four),
+// then the operands are two quad_perm moves of U: {E', M, F', E'} and
+// {F', S, M, S}. Input T (lane 3) is ignored; output is a full extended point.
 template <class Q>
 CMTV_HD void q_dbl(const Q& q, fe& v) {
   const int lane = q.lane();
   fe a, b, m;
   q.template perm<QP_B0>(a, v);
   q.template perm<QP_B1>(b, v);
-  fe_add(a, a, b);  // X + Y
-  fe_select(m, v, a, lane == 3);
+#pragma unroll
+  for (int i = 0; i < 10; i++) m.v[i] = lane == 3 ? a.v[i] + b.v[i] : v.v[i];  // X + Y on lane 3
   fe_sq(m, m);
-  fe S, M, E, F;
-  q.template perm<QP_B0>(a, m);  // A = X^2
-  q.template perm<QP_B1>(b, m);  // B = Y^2
-  fe_add(S, a, b);
-  fe_carry(S);                   // S = A + B
-  fe_sub(M, a, b);               // M = A - B
-  q.template perm<QP_B3>(a, m);  // K = (X+Y)^2
-  fe_sub(E, S, a);               // E' = S - K
-  q.template perm<QP_B2>(b, m);  // C' = Z^2
-  fe_add(F, b, b);
-  fe_add(F, F, M);
-  fe_carry(F);                   // F' = 2C' + M
-  fe_pick(a, lane, E, M, F, E);
-  fe_pick(b, lane, F, S, M, S);
+  fe r;
+  q.template perm<QP_B0>(a, m);             // A
+  q.template perm<QP_B1>(b, m);             // B
+  q.template perm<qp(3, 2, 2, 2)>(r, m);    // lane 0: K, lane 1: C'
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    const uint32_t s = a.v[i] + b.v[i];                  // S
+    const uint32_t mm = a.v[i] + (fe_p2(i) - b.v[i]);    // M
+    const uint32_t e = s + (fe_p2(i) - r.v[i]);          // E' = S - K
+    const uint32_t f = mm + 2 * r.v[i];                  // F' = M + 2C'
+    const uint32_t lo = (lane & 1) ? f : e, hi = (lane & 1) ? s : mm;
+    m.v[i] = (lane & 2) ? hi : lo;
+  }
+  fe_carry(m);
+  q.template perm<qp(0, 2, 1, 0)>(a, m);  // E', M, F', E'
+  q.template perm<qp(1, 3, 2, 3)>(b, m);  // F', S, M, S
   fe_mul(v, a, b);
 }
 
-// quad_perm code: lane c reads lane s_c
-constexpr int qp(int s0, int s1, int s2, int s3) { return s0 | (s1 << 2) | (s2 << 4) | (s3 << 6); }
-
 // Addition v += Q where c is this lane's coordinate of Q in cached form
-// (Y2-X2, Y2+X2, Z2, 2dT2); for an affine niels addend pass Z2 = 1.
-//   round 1: lane c computes {(Y1-X1)(Y2-X2), (Y1+X1)(Y2+X2), Z1 Z2, T1 2dT2}[c]
-//            = {A, B, D/2, C}
-//   round 2: lane c computes {EF, GH, FG, EH}[c], E = B-A, F = D-C, G = D+C,
-//            H = B+A
-// Each round-2 operand is P +- Q with P and Q read from a per-lane source
-// lane by ONE quad_perm each (op1 = {B-A, D+C, D-C, B-A}, op2 = {D-C, B+A,
-// D+C, B+A}), so no lane computes values it does not multiply.
+// (Y2-X2, Y2+X2, 2Z2, 2dT2):
+//   round 1: lane c computes {(Y1-X1)(Y2-X2), (Y1+X1)(Y2+X2), Z1 2Z2, T1 2dT2}[c]
+//            = {A, B, D, C}
+//   round 2: with E = B-A, F = D-C, G = D+C, H = B+A, lane c forms
+//            U_c = {E, F, G, H}[c] from two quad_perm moves (no carry: every
+//            U stays inside the multiplier bounds) and computes
+//            {FE, GH, FG, EH}[c] = (X3, Y3, Z3, T3) from two more.
 template <class Q>
 CMTV_HD void q_add(const Q& q, fe& v, const fe& c) {
   const int lane = q.lane();
-  fe p, x, t;
-  // round 1 operand: lanes 0/1: Y -+ X; lanes 2/3: own Z / T
-  q.template perm<qp(1, 1, 2, 3)>(p, v);  // Y, Y, Z, T
-  q.template perm<QP_B0>(x, v);           // X
-  fe_neg(t, x);
-  fe_select(x, x, t, lane == 0);
+  fe x, y, p;
+  q.template perm<QP_B0>(x, v);
+  q.template perm<QP_B1>(y, v);
 #pragma unroll
-  for (int i = 0; i < 10; i++) x.v[i] = lane >= 2 ? 0u : x.v[i];
-  fe_add(p, p, x);
-  fe_mul(t, p, c);
-  // D = 2 Z1 Z2 on lane 2; all four carried
-  fe_add(x, t, t);
-  fe_select(t, t, x, lane == 2);
-  fe_carry(t);  // lanes: A, B, D, C
-  fe o1, o2, n;
-  q.template perm<qp(1, 2, 2, 1)>(o1, t);  // B, D, D, B
-  q.template perm<qp(0, 3, 3, 0)>(x, t);   // A, C, C, A
-  fe_neg(n, x);
-  fe_select(x, n, x, lane == 1);
-  fe_add(o1, o1, x);                       // B-A, D+C, D-C, B-A
-  q.template perm<qp(2, 1, 2, 1)>(o2, t);  // D, B, D, B
-  q.template perm<qp(3, 0, 3, 0)>(x, t);   // C, A, C, A
-  fe_neg(n, x);
-  fe_select(x, x, n, lane == 0);
-  fe_add(o2, o2, x);                       // D-C, B+A, D+C, B+A
-  fe_mul(v, o1, o2);
+  for (int i = 0; i < 10; i++) {
+    const uint32_t w = lane == 0 ? fe_p2(i) - x.v[i] : x.v[i];
+    p.v[i] = (lane & 2) ? v.v[i] : y.v[i] + w;  // Y-X, Y+X, Z, T
+  }
+  fe t;
+  fe_mul(t, p, c);  // A, B, D, C
+  q.template perm<qp(1, 2, 2, 1)>(x, t);  // B, D, D, B
+  q.template perm<qp(0, 3, 3, 0)>(y, t);  // A, C, C, A
+#pragma unroll
+  for (int i = 0; i < 10; i++) p.v[i] = x.v[i] + ((lane & 2) ? y.v[i] : fe_p2(i) - y.v[i]);  // E, F, G, H
+  q.template perm<qp(1, 2, 1, 0)>(x, p);  // F, G, F, E
+  q.template perm<qp(0, 3, 2, 3)>(y, p);  // E, H, G, H
+  fe_mul(v, x, y);
 }
 
 // this lane's cached-form coordinate of the extended point v
 template <class Q>
 CMTV_HD void q_to_cached(const Q& q, fe& c, const fe& v) {
   const int lane = q.lane();
-  fe x, y, s, d2;
+  fe x, y, d2;
   q.template perm<QP_B0>(x, v);
   q.template perm<QP_B1>(y, v);
-  fe_sub(s, y, x);
-  fe_add(y, y, x);
   fe_const_d2(d2);
   fe_mul(d2, v, d2);
-  fe_pick(c, lane, s, y, v, d2);
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    const uint32_t w = lane == 0 ? fe_p2(i) - x.v[i] : x.v[i];
+    const uint32_t hi = (lane & 1) ? d2.v[i] : 2 * v.v[i];
+    c.v[i] = (lane & 2) ? hi : y.v[i] + w;  // Y-X, Y+X, 2Z, 2dT
+  }
 }
 
 // conditional negation of a cached addend: swap (Y-X, Y+X), negate 2dT
@@ -151,6 +154,28 @@ CMTV_HD void q_cached_cneg(const Q& q, fe& c, bool neg) {
   fe_neg(n, c);
   fe_select(s, s, n, q.lane() == 3);
   fe_select(c, c, s, neg);
+}
+
+// lane 3's half of a cached negation (lanes 0/1 swap by where they load)
+CMTV_HD void q_negate_lane3(fe& c, int lane, bool neg) {
+  const bool f = neg && lane == 3;
+#pragma unroll
+  for (int i = 0; i < 10; i++) c.v[i] = f ? fe_p2(i) - c.v[i] : c.v[i];
+}
+
+// This lane's cached coordinate of (neg ? -P : P) for P an affine niels row
+// (y+x at word 0, y-x at word ymx_off, 2dxy at word xy_off), or of the
+// identity when ident. ld(off, c) loads the 10 limbs at word `off`.
+template <class Q, class Ld>
+CMTV_HD void q_niels_coord(const Q& q, fe& c, const Ld& ld, int ymx_off, int xy_off, bool neg, bool ident) {
+  const int lane = q.lane();
+  const int off = lane == 3 ? xy_off : (((lane == 0) != neg) ? ymx_off : 0);
+  ld(off, c);
+  const bool cst = ident || lane == 2;  // lane 2: 2Z = 2 (affine); identity (1, 1, 2, 0)
+  const uint32_t c0 = lane == 2 ? 2u : (lane == 3 ? 0u : 1u);
+#pragma unroll
+  for (int i = 0; i < 10; i++) c.v[i] = cst ? (i == 0 ? c0 : 0u) : c.v[i];
+  q_negate_lane3(c, lane, neg && !ident);
 }
 
 }  // namespace cmtv
@@ -202,10 +227,19 @@ struct NullProbe {
 //   void store(int e, const fe& c);  void load(int e, fe& c) const;
 // The device policy keeps it in LDS (a per-lane slot, so no barrier is needed
 // and a lookup is 5 ds_read_b64 instead of an 8-way register select).
+//   template <class Q> void load_signed(const Q& q, int e, bool neg, fe& c) const;
+// gives (neg ? -P_e : P_e): the LDS policy negates by reading the partner
+// lane's slot on lanes 0/1 and negating lane 3 (q_negate_lane3).
 struct QArrayTab {  // plain-array table policy (host checks, debug kernels)
   fe t[9];
   CMTV_HD void store(int e, const fe& c) { t[e] = c; }
   CMTV_HD void load(int e, fe& c) const { c = t[e]; }
+  // this lane's coordinate of (neg ? -P_e : P_e)
+  template <class Q>
+  CMTV_HD void load_signed(const Q& q, int e, bool neg, fe& c) const {
+    c = t[e];
+    q_cached_cneg(q, c, neg);
+  }
 };
 
 // Phases 2-4 of a quad verification, shared by the Ed25519 (q_verify) and
@@ -253,8 +287,6 @@ CMTV_HD void q_straus_half(const Q& q, fe& v, fe& rc, const uint32_t k[8], const
   hs_digits16(tR, hs.k2, wide);
   hs_digits256(tLo, tHi, u);
   q_identity(v, lane);
-  // lane -> offset of its niels coordinate in a B-table row (y-x, y+x, 1, 2dxy)
-  const int boff = lane == 0 ? BTAB_COORD_WORDS : (lane == 3 ? 2 * BTAB_COORD_WORDS : 0);
 #pragma unroll 1
   for (int win = W - 1; win >= 0; win--) {
     if (win != W - 1) {
@@ -264,15 +296,13 @@ CMTV_HD void q_straus_half(const Q& q, fe& v, fe& rc, const uint32_t k[8], const
     {
       const int dA = (int)sc_shift_out(tA, 4) - 8;
       fe c;
-      tabA.load(dA < 0 ? -dA : dA, c);
-      q_cached_cneg(q, c, dA < 0);
+      tabA.load_signed(q, dA < 0 ? -dA : dA, dA < 0, c);
       q_add(q, v, c);
     }
     {
       const int dR = (int)sc_shift_out(tR, 4) - 8;
       fe c;
-      tabR.load(dR < 0 ? -dR : dR, c);
-      q_cached_cneg(q, c, dR < 0);
+      tabR.load_signed(q, dR < 0 ? -dR : dR, dR < 0, c);
       q_add(q, v, c);
     }
     if (win <= 32 && ((win & 1) == 0 || win <= 31)) {
@@ -285,12 +315,11 @@ CMTV_HD void q_straus_half(const Q& q, fe& v, fe& rc, const uint32_t k[8], const
       else
         dB = (int)sc_shift_out(tLo, 8) - 128;
       const int ib = dB < 0 ? -dB : dB;
+      const int row = (ib > 0 ? ib - 1 : 0) + (odd ? BTAB_ENTRIES : 0);
       fe c;
-      btab.load_coord((ib > 0 ? ib - 1 : 0) + (odd ? BTAB_ENTRIES : 0), boff, c);
-      const bool one = lane == 2 || (ib == 0 && lane != 3);
-#pragma unroll
-      for (int i = 0; i < 10; i++) c.v[i] = (ib == 0 || lane == 2) ? ((one && i == 0) ? 1u : 0u) : c.v[i];
-      q_cached_cneg(q, c, dB < 0);
+      q_niels_coord(
+          q, c, [&](int off, fe& r) { btab.load_coord(row, off, r); }, BTAB_COORD_WORDS, 2 * BTAB_COORD_WORDS,
+          dB < 0, ib == 0);
       q_add(q, v, c);
     }
     if (win >= W - 4) probe.snap(6 + (W - 1 - win), v);

@@ -19,10 +19,15 @@
 //     [k2]X = O  <=>  X = O.  Cofactorless (GO_STDLIB) mode therefore checks
 //     R' == R exactly; with R canonical this is encode(R') == R bytes.
 //   * ZIP215 mode checks [8][k2](R' - R) = O  <=>  [8](R' - R) = O.
-//   * If no odd-k2 pair fits 134 bits (probability ~5e-5 for a random k, or
-//     a quotient >= 2^31 appears), the decomposition is marked `wide` and the
-//     caller uses k1 = k, k2 = 1 over 64 windows -- the same equation, so no
-//     input changes its verdict, only its cost.
+//   * The window count follows the pair's size: 34 windows hold pairs up to
+//     134 bits (all but ~5.5e-5 of random k), 35 / 36 / 37 windows up to
+//     138 / 142 / 146 bits. Only if no odd-k2 pair fits 146 bits (about
+//     1e-6), or a quotient >= 2^31 appears, is the decomposition marked
+//     `wide`: the caller then uses k1 = k, k2 = 1 over 64 windows -- the same
+//     equation, so no input changes its verdict, only its cost. (The window
+//     count is uniform over a wave, so with a plain 34-or-64 rule one such
+//     signature in a 10k commit -- ~40% of commits -- made its whole wave run
+//     64 windows.)
 //
 // Arithmetic: the Euclid runs on 8-word values kept left-normalised (r0's top
 // bit at bit 255, both remainders shifted by the same e) and t values in
@@ -46,8 +51,11 @@
 namespace cmtv {
 
 constexpr int HS_WINDOWS = 34;      // 4-bit windows for normal pairs (136 bits)
+constexpr int HS_MAX_WINDOWS = 37;  // graded: up to 37 windows before the wide fallback
 constexpr int HS_WIDE_WINDOWS = 64; // k1 = k, k2 = 1
 constexpr int HS_MAX_BITS = 134;    // (2^134 + bias) < 16^34 for the signed-digit bias
+// windows for a pair of `bits` bits: (2^bits + bias) < 16^W  <=>  bits <= 4W - 2
+CMTV_HD int hs_windows_for(int bits) { return bits <= HS_MAX_BITS ? HS_WINDOWS : (bits + 5) / 4; }
 constexpr int HS_MAX_ROUNDS = 192;  // outer rounds before giving up (Lehmer: ~10; exact steps: ~75)
 constexpr int HS_MAX_INNER = 40;    // Lehmer inner steps per round (30-bit digits: ~9)
 
@@ -56,6 +64,7 @@ struct HalfScalars {
   uint32_t k2[8];  // |k2|, odd
   bool k2_neg;
   bool wide;
+  int windows;     // 34..37 (the pair's size), HS_WIDE_WINDOWS when wide
 };
 
 CMTV_HD uint32_t hs_N(int i) {  // 8L
@@ -269,8 +278,10 @@ CMTV_HD void hs_lin(uint32_t out[W], int32_t P, const uint32_t x[], int32_t Q, c
 // (k1, k2) with k1 == k2 k (mod 8L), k2 odd, both < 2^134, or wide.
 // LEHMER = false: one exact Euclid step per round (the schedule the host test
 // compares against); both give the same pair.
+// force_wide: take the wide schedule regardless (CMTV_FORCE_WIDE test knob,
+// so the 64-window path -- ~never reached by real k -- is exercised)
 template <bool LEHMER = true>
-CMTV_HD void half_scalars(HalfScalars& h, const uint32_t k[8]) {
+CMTV_HD void half_scalars(HalfScalars& h, const uint32_t k[8], bool force_wide = false) {
   uint32_t r0[8], r1[8], t0[6], t1[6];
 #pragma unroll
   for (int i = 0; i < 8; i++) {
@@ -366,7 +377,8 @@ CMTV_HD void half_scalars(HalfScalars& h, const uint32_t k[8]) {
   // choose: 1 if t1 odd, else the smaller of 0 and 2
   const int pick = t1_odd ? 1 : (c2 < c0 ? 2 : 0);
   const int cost = pick == 1 ? c1 : (pick == 2 ? c2 : c0);
-  h.wide = !ok || cost > HS_MAX_BITS;
+  h.wide = force_wide || !ok || cost > 4 * HS_MAX_WINDOWS - 2;
+  h.windows = h.wide ? HS_WIDE_WINDOWS : hs_windows_for(cost);
   uint32_t rs[8], ts[6];
 #pragma unroll
   for (int i = 0; i < 8; i++) rs[i] = pick == 1 ? r1[i] : (pick == 2 ? r2[i] : r0[i]);
@@ -422,26 +434,30 @@ CMTV_HD void hs_bscalar(uint32_t u[8], const uint32_t k2mag[8], bool neg, const 
 }
 
 // Signed radix-16 digit stream of x (|digits| <= 8) read from the top with
-// sc_shift_out(t, 4): wide -> 64 windows, else HS_WINDOWS = 34 windows
-// (x < 2^134), left-aligned so the first shift_out yields the top digit.
-CMTV_HD void hs_digits16(uint32_t t[8], const uint32_t x[8], bool wide) {
+// sc_shift_out(t, 4) over W windows: W = HS_WIDE_WINDOWS (64, any x < 2^255)
+// or HS_WINDOWS..HS_MAX_WINDOWS (x < 2^(4W-2)), left-aligned so the first
+// shift_out yields the top digit.
+CMTV_HD void hs_digits16(uint32_t t[8], const uint32_t x[8], int W) {
   uint32_t a[8], b[8];
   sc_bias(a, x, 0x88888888u);
+  // W nibbles of 8: words 0-3 whole, word 4 holds W - 32 (2..5) of them
+  const uint32_t w4 = 0x88888888u & ((1u << (4 * (W - 32))) - 1u);
   uint64_t c = 0;
 #pragma unroll
   for (int i = 0; i < 8; i++) {
-    const uint32_t bias = i < 4 ? 0x88888888u : (i == 4 ? 0x88u : 0u);
+    const uint32_t bias = i < 4 ? 0x88888888u : (i == 4 ? w4 : 0u);
     const uint64_t v = (uint64_t)x[i] + bias + c;
     b[i] = (uint32_t)v;
     c = v >> 32;
   }
-  // b < 2^136: shift left by 120 bits (3 words + 24 bits)
+  // b < 2^(4W): shift left by 4 (64 - W) = 96 + bs bits, bs = 4 (40 - W) in 12..24
+  const int bs = 4 * (40 - (W > HS_MAX_WINDOWS ? HS_MAX_WINDOWS : W));
 #pragma unroll
   for (int i = 0; i < 8; i++) {
     const uint32_t hi = i >= 3 ? b[i - 3] : 0u;
     const uint32_t lo = i >= 4 ? b[i - 4] : 0u;
-    const uint32_t sh = (hi << 24) | (lo >> 8);
-    t[i] = wide ? a[i] : sh;
+    const uint32_t sh = (hi << bs) | (lo >> (32 - bs));
+    t[i] = W == HS_WIDE_WINDOWS ? a[i] : sh;
   }
 }
 

@@ -10,10 +10,14 @@ constexpr uint32_t kAtabWordsPerLane = 320; // (1..8)(-A), 40 words per point
 constexpr uint32_t kCombWords = 32 * 128 * 32;     // one registered-key comb (keyed.h), 512 KiB
 constexpr uint32_t kCombScratchWordsPerKey = 128 * 320;  // prefix products while building
 
+// launch_verify / launch_verify_sr25519 kflags: the quad kernel (else lane),
+// and the CMTV_FORCE_WIDE test knob (every quad takes the 64-window schedule)
+constexpr uint32_t kLaunchQuad = 1, kLaunchForceWide = 2;
+
 hipError_t launch_btab_init(uint32_t* d_rows, hipStream_t s);
 hipError_t launch_verify(uint32_t mode, uint32_t n, const void* pk, const void* sig, const void* msg,
                          const void* off, const uint32_t* btab, uint32_t* atab, void* valid, void* bitmap,
-                         bool quad, hipStream_t s);
+                         uint32_t kflags, hipStream_t s);
 hipError_t launch_comb_build(uint32_t n_keys, const void* keys_pk, uint8_t* keys_ok, uint32_t* tabs,
                              uint32_t* scratch, bool negate, hipStream_t s);
 hipError_t launch_verify_keyed(uint32_t mode, uint32_t n, uint32_t n_keys, const void* key_idx, const void* sig,
@@ -22,7 +26,7 @@ hipError_t launch_verify_keyed(uint32_t mode, uint32_t n, uint32_t n_keys, const
                                bool quad, hipStream_t s);
 hipError_t launch_verify_sr25519(uint32_t n, const void* pk, const void* sig, const void* msg, const void* off,
                                  const uint32_t* btab, uint32_t* atab, const uint16_t* prog, int nops, void* valid,
-                                 void* bitmap, bool quad, hipStream_t s);
+                                 void* bitmap, uint32_t kflags, hipStream_t s);
 hipError_t launch_sign_bytes(uint32_t n, const void* tmpls, const uint8_t* blob, const uint32_t* tidx,
                              const uint8_t* commit_flag, const int64_t* sec, const int32_t* nanos,
                              const uint32_t* off, uint8_t* msg, hipStream_t s);

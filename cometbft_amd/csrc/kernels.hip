@@ -102,7 +102,7 @@ __global__ __launch_bounds__(64, CMTV_QUAD_WAVES_PER_EU) void k_verify_quad(uint
                                                        const uint32_t* __restrict__ off,
                                                        const uint32_t* __restrict__ btab,
                                                        uint8_t* __restrict__ out_valid,
-                                                       uint64_t* __restrict__ out_bitmap) {
+                                                       uint64_t* __restrict__ out_bitmap, uint32_t force_wide) {
   const uint32_t gid = blockIdx.x * 64 + threadIdx.x;
   const uint32_t s = gid >> 2;
   const bool active = s < n;
@@ -112,7 +112,8 @@ __global__ __launch_bounds__(64, CMTV_QUAD_WAVES_PER_EU) void k_verify_quad(uint
   DevBTabQ bt{btab};
   __shared__ uint2 tab_lds[2 * 9 * 5 * 64];  // (0..8)(-A), (0..8)(-/+R): 45 KiB per wave
   DevATabQ ta{tab_lds, threadIdx.x}, tr{tab_lds + 9 * 5 * 64, threadIdx.x};
-  bool v = q_verify<MODE>(q, pk + 8 * (size_t)i, sig + 16 * (size_t)i, msg + m0, m1 - m0, bt, ta, tr);
+  bool v = q_verify<MODE>(q, pk + 8 * (size_t)i, sig + 16 * (size_t)i, msg + m0, m1 - m0, bt, ta, tr, NullProbe(),
+                          force_wide != 0);
   v = v && active;
   if (active && (threadIdx.x & 3) == 0 && out_valid) out_valid[s] = v ? 1 : 0;
   uint64_t x = __ballot(v && (threadIdx.x & 3) == 0) & 0x1111111111111111ull;
@@ -266,7 +267,9 @@ hipError_t launch_btab_init(uint32_t* d_rows, hipStream_t s) {
 
 hipError_t launch_verify(uint32_t mode, uint32_t n, const void* pk, const void* sig, const void* msg,
                          const void* off, const uint32_t* btab, uint32_t* atab, void* valid, void* bitmap,
-                         bool quad, hipStream_t s) {
+                         uint32_t kflags, hipStream_t s) {
+  const bool quad = kflags & kLaunchQuad;
+  const uint32_t fw = (kflags & kLaunchForceWide) ? 1u : 0u;
   if (n == 0) return hipSuccess;
   auto pkp = static_cast<const uint32_t*>(pk);
   auto sgp = static_cast<const uint32_t*>(sig);
@@ -279,9 +282,9 @@ hipError_t launch_verify(uint32_t mode, uint32_t n, const void* pk, const void* 
     // 16-bit slice of every bitmap word is written
     const dim3 grid(((n + 63) / 64) * 4), block(64);
     if (mode == MODE_ZIP215)
-      hipLaunchKernelGGL(k_verify_quad<MODE_ZIP215>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp);
+      hipLaunchKernelGGL(k_verify_quad<MODE_ZIP215>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp, fw);
     else
-      hipLaunchKernelGGL(k_verify_quad<MODE_GO_STDLIB>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp);
+      hipLaunchKernelGGL(k_verify_quad<MODE_GO_STDLIB>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp, fw);
     return hipGetLastError();
   }
   const dim3 grid(blocks_for(n)), block(64);

@@ -251,17 +251,21 @@ struct QArrayTab {  // plain-array table policy (host checks, debug kernels)
 // rc is clobbered.
 template <class Q, class BTab, class ATab, class Probe>
 CMTV_HD void q_straus_half(const Q& q, fe& v, fe& rc, const uint32_t k[8], const uint32_t ts[8], const BTab& btab,
-                           ATab& tabA, ATab& tabR, const Probe& probe) {
+                           ATab& tabA, ATab& tabR, const Probe& probe, bool force_wide = false) {
   const int lane = q.lane();
   // ---- phase 2: half-size scalars (halfscalar.h) and the fixed-base scalar
   //   X = [u]B + [k1](-A) + [|k2|](k2 < 0 ? R : -R) = [k2](R' - R),
   //   u = k2 s mod L; the window count is uniform over the wave
   HalfScalars hs;
-  half_scalars(hs, k);
+  half_scalars(hs, k, force_wide);
   uint32_t u[8];
   hs_bscalar(u, hs.k2, hs.k2_neg, ts);
+  // window count: the largest over the wave (34..37), 64 if any is wide
   const bool wide = q.any(hs.wide);
-  const int W = wide ? HS_WIDE_WINDOWS : HS_WINDOWS;
+  int W = HS_WINDOWS;
+#pragma unroll 1
+  for (int w = HS_WINDOWS; w < HS_MAX_WINDOWS; w++) W += q.any(hs.windows > w) ? 1 : 0;
+  W = wide ? HS_WIDE_WINDOWS : W;
   {
     fe kk;
 #pragma unroll
@@ -283,8 +287,8 @@ CMTV_HD void q_straus_half(const Q& q, fe& v, fe& rc, const uint32_t k[8], const
 
   // ---- phase 4: Straus over W shared 4-bit windows
   uint32_t tA[8], tR[8], tLo[8], tHi[8];
-  hs_digits16(tA, hs.k1, wide);
-  hs_digits16(tR, hs.k2, wide);
+  hs_digits16(tA, hs.k1, W);
+  hs_digits16(tR, hs.k2, W);
   hs_digits256(tLo, tHi, u);
   q_identity(v, lane);
 #pragma unroll 1
@@ -329,7 +333,8 @@ CMTV_HD void q_straus_half(const Q& q, fe& v, fe& rc, const uint32_t k[8], const
 
 template <uint32_t MODE, class Q, class BTab, class ATab, class Probe = NullProbe>
 CMTV_HD bool q_verify(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig_ptr, const uint8_t* msg,
-                      uint32_t mlen, const BTab& btab, ATab& tabA, ATab& tabR, const Probe& probe = Probe()) {
+                      uint32_t mlen, const BTab& btab, ATab& tabA, ATab& tabR, const Probe& probe = Probe(),
+                      bool force_wide = false) {
   const int lane = q.lane();
   uint32_t w[16];
 #pragma unroll
@@ -390,7 +395,7 @@ CMTV_HD bool q_verify(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig_pt
   }
 
   // ---- phases 2-4: v <- this lane's coordinate of X = [k2](R' - R)
-  q_straus_half(q, v, rc, k, ts, btab, tabA, tabR, probe);
+  q_straus_half(q, v, rc, k, ts, btab, tabA, tabR, probe, force_wide);
 
   // ---- final check: X = O (GO_STDLIB: R' == R with R canonical, i.e.
   //      encode(R') == R bytes) / [8]X = O (ZIP215)

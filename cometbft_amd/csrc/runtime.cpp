@@ -330,6 +330,8 @@ struct cmtv_ctx {
   std::vector<std::pair<std::string, cmtv_keyset*>> keysets;
   // CMTV_FAULT_AT: 1-based index of the verification launch that fails
   uint64_t fault_at = 0, launch_seq = 0;
+  // CMTV_FORCE_WIDE: quad kernels take the 64-window half-scalar fallback
+  bool force_wide = false;
 };
 
 struct cmtv_keyset {
@@ -382,6 +384,7 @@ static int enqueue_verify(cmtv_ctx* ctx, CmtvDev& D, size_t n, const uint8_t* d_
   // sr25519_quad.h).
   const bool sr = mode == kModeSr25519;
   const bool quad = n <= ctx->quad_max;
+  const uint32_t kflags = (quad ? kLaunchQuad : 0u) | (ctx->force_wide ? kLaunchForceWide : 0u);
   hipError_t e = hipSuccess;
   if (!quad) {
     const size_t lanes = std::min<size_t>(n, ctx->lane_chunk);
@@ -403,11 +406,11 @@ static int enqueue_verify(cmtv_ctx* ctx, CmtvDev& D, size_t n, const uint8_t* d_
     if (sr)
       e = launch_verify_sr25519(cn, d_pk + 32 * c, d_sig + 64 * c, d_msg, d_off + c, D.d_btab,
                                 static_cast<uint32_t*>(D.d_atab.p), D.d_srprog, ctx->sr_nops,
-                                d_valid ? d_valid + c : nullptr, d_bitmap ? d_bitmap + c / 64 : nullptr, quad, s);
+                                d_valid ? d_valid + c : nullptr, d_bitmap ? d_bitmap + c / 64 : nullptr, kflags, s);
     else
       e = launch_verify(mode, cn, d_pk + 32 * c, d_sig + 64 * c, d_msg, d_off + c, D.d_btab,
                         static_cast<uint32_t*>(D.d_atab.p), d_valid ? d_valid + c : nullptr,
-                        d_bitmap ? d_bitmap + c / 64 : nullptr, quad, s);
+                        d_bitmap ? d_bitmap + c / 64 : nullptr, kflags, s);
     if (e != hipSuccess) {
       D.timing.abandon(tp);
       return hip_fail(e);
@@ -857,6 +860,7 @@ static void read_env(cmtv_ctx* ctx) {
   }
   if (const char* sm = std::getenv("CMTV_SHARD_MIN")) ctx->shard_min = (size_t)std::strtoull(sm, nullptr, 10);
   if (const char* fa = std::getenv("CMTV_FAULT_AT")) ctx->fault_at = (uint64_t)std::strtoull(fa, nullptr, 10);
+  if (const char* fw = std::getenv("CMTV_FORCE_WIDE")) ctx->force_wide = fw[0] == '1';
 }
 
 // CMTVERIFY_DEVICES: "0,1,2" or "all" (or unset: every visible device)

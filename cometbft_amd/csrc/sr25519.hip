@@ -71,7 +71,8 @@ __global__ __launch_bounds__(64, 1) void k_verify_sr25519_quad(uint32_t n, const
                                                                const uint32_t* __restrict__ btab,
                                                                const uint16_t* __restrict__ prog, int nops,
                                                                uint8_t* __restrict__ out_valid,
-                                                               uint64_t* __restrict__ out_bitmap) {
+                                                               uint64_t* __restrict__ out_bitmap,
+                                                               uint32_t force_wide) {
   __shared__ uint2 tab_lds[2 * 9 * 5 * 64];  // (0..8)(-A), (0..8)(-/+R); STROBE states first
   const uint32_t s = blockIdx.x * 16 + (threadIdx.x >> 2);
   const bool active = s < n;
@@ -81,7 +82,8 @@ __global__ __launch_bounds__(64, 1) void k_verify_sr25519_quad(uint32_t n, const
   DevBTabQ bt{btab};
   DevATabQ ta{tab_lds, threadIdx.x}, tr{tab_lds + 9 * 5 * 64, threadIdx.x};
   LdsStrobeState st{reinterpret_cast<uint32_t*>(tab_lds), threadIdx.x};
-  bool v = q_verify_sr(q, pk + 8 * (size_t)i, sig + 16 * (size_t)i, msg + m0, m1 - m0, prog, nops, st, bt, ta, tr);
+  bool v = q_verify_sr(q, pk + 8 * (size_t)i, sig + 16 * (size_t)i, msg + m0, m1 - m0, prog, nops, st, bt, ta, tr,
+                       NullProbe(), force_wide != 0);
   v = v && active;
   if (active && (threadIdx.x & 3) == 0 && out_valid) out_valid[s] = v ? 1 : 0;
   // compact bit 4j -> bit j (16 verdicts of this wave); 4 consecutive blocks
@@ -96,15 +98,17 @@ __global__ __launch_bounds__(64, 1) void k_verify_sr25519_quad(uint32_t n, const
 
 hipError_t launch_verify_sr25519(uint32_t n, const void* pk, const void* sig, const void* msg, const void* off,
                                  const uint32_t* btab, uint32_t* atab, const uint16_t* prog, int nops, void* valid,
-                                 void* bitmap, bool quad, hipStream_t s) {
+                                 void* bitmap, uint32_t kflags, hipStream_t s) {
   if (n == 0) return hipSuccess;
+  const bool quad = kflags & kLaunchQuad;
   if (quad) {
     // one 64-lane block = 16 signatures; whole groups of 4 blocks so every
     // 16-bit slice of every bitmap word is written
     hipLaunchKernelGGL(k_verify_sr25519_quad, dim3(((n + 63) / 64) * 4), dim3(64), 0, s, n,
                        static_cast<const uint32_t*>(pk), static_cast<const uint32_t*>(sig),
                        static_cast<const uint8_t*>(msg), static_cast<const uint32_t*>(off), btab, prog, nops,
-                       static_cast<uint8_t*>(valid), static_cast<uint64_t*>(bitmap));
+                       static_cast<uint8_t*>(valid), static_cast<uint64_t*>(bitmap),
+                       (kflags & kLaunchForceWide) ? 1u : 0u);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(k_verify_sr25519, dim3((n + 63) / 64), dim3(64), 0, s, n, static_cast<const uint32_t*>(pk),

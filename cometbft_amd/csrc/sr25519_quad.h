@@ -21,7 +21,7 @@ namespace cmtv {
 template <class Q, class BTab, class ATab, class State, class Probe = NullProbe>
 CMTV_HD bool q_verify_sr(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig_ptr, const uint8_t* msg,
                          uint32_t mlen, const uint16_t* prog, int nops, State& st, const BTab& btab, ATab& tabA,
-                         ATab& tabR, const Probe& probe = Probe()) {
+                         ATab& tabR, const Probe& probe = Probe(), bool force_wide = false) {
   const int lane = q.lane();
   uint32_t pk[8], rw[8], ts[8];
 #pragma unroll
@@ -71,7 +71,7 @@ CMTV_HD bool q_verify_sr(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig
   probe.snap(0, v);
   probe.snap(1, rc);
 
-  q_straus_half(q, v, rc, k, ts, btab, tabA, tabR, probe);
+  q_straus_half(q, v, rc, k, ts, btab, tabA, tabR, probe, force_wide);
 
   // ---- X in E[4]: X.X = 0 (lane 0) or X.Y = 0 (lane 1)
   const bool z = fe_iszero(v);

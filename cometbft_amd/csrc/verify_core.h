@@ -299,8 +299,12 @@ CMTV_HD bool verify_one_half(const uint32_t* pk_ptr, const uint32_t* sig_ptr, co
   half_scalars(hs, k);
   uint32_t u[8];
   hs_bscalar(u, hs.k2, hs.k2_neg, ts);
+  // window count: the largest over the wave (34..37), 64 if any is wide
   const bool wide = wave.any(hs.wide);
-  const int W = wide ? HS_WIDE_WINDOWS : HS_WINDOWS;
+  int W = HS_WINDOWS;
+#pragma unroll 1
+  for (int w = HS_WINDOWS; w < HS_MAX_WINDOWS; w++) W += wave.any(hs.windows > w) ? 1 : 0;
+  W = wide ? HS_WIDE_WINDOWS : W;
 
   // tables: (1..8)(-A), (1..8)(k2 < 0 ? R : -R)
   {
@@ -325,8 +329,8 @@ CMTV_HD bool verify_one_half(const uint32_t* pk_ptr, const uint32_t* sig_ptr, co
   }
 
   uint32_t tA[8], tR[8], tLo[8], tHi[8];
-  hs_digits16(tA, hs.k1, wide);
-  hs_digits16(tR, hs.k2, wide);
+  hs_digits16(tA, hs.k1, W);
+  hs_digits16(tR, hs.k2, W);
   hs_digits256(tLo, tHi, u);
   ge_p2 cur;
   p2_identity(cur);

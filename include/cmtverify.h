@@ -98,7 +98,8 @@ typedef struct cmtv_stats {
  * Environment (read at open): CMTV_QUAD_MAX / CMTV_KEYED_QUAD_MAX / CMTV_LANE_CHUNK
  * (kernel crossovers), CMTV_FAULT_AT=N (test knob: the N-th verification
  * launch of the context fails with CMTV_EHIP without running; libs/fail
- * FAIL_TEST_INDEX analogue). */
+ * FAIL_TEST_INDEX analogue), CMTV_FORCE_WIDE=1 (test knob: the quad kernels
+ * take the 64-window half-scalar fallback for every signature). */
 int cmtv_open(const cmtv_config* cfg, cmtv_ctx** out);
 
 /* Opens ONE context over several devices (a node is one

@@ -1,9 +1,13 @@
 """Generate tests/golden/wide_vectors.json: signatures whose challenge k makes
-the product's half-size-scalar split (cometbft_amd/csrc/halfscalar.h) fall
-back to its "wide" schedule (k1 = k, k2 = 1 over 64 windows instead of 34).
+the product's half-size-scalar split (cometbft_amd/csrc/halfscalar.h) leave
+its common 34-window schedule: pairs of 135-146 bits take 35, 36 or 37
+windows (~5.5e-5, ~3e-6 and ~3e-7 of random k), and the window count is
+shared by the whole wave. (Beyond 146 bits the split falls back to k1 = k,
+k2 = 1 over 64 windows; no k can be searched for that -- ~1e-10 -- so the
+GPU tests force that schedule with the CMTV_FORCE_WIDE knob instead.)
 
-That fallback only changes the cost of a verification, never its verdict,
-and it is taken for ~5e-5 of random k, so random test data never reaches it.
+The window count only changes the cost of a verification, never its
+verdict, and random test data almost never reaches the larger ones.
 Here the message is searched instead: R (and so the nonce r) is fixed, the
 CanonicalVote timestamp nanos of the message vary, and k = H(R || A || M) is
 classified by the host build of halfscalar.h (tests/host/halfcheck.cpp, the
@@ -12,7 +16,7 @@ signature is valid by construction; the verdicts themselves come from the
 oracles (oracle/ed25519_ref.py and oracle/liboracle.so in both Ed25519 modes,
 oracle/sr25519_ref.py and liboracle.so for sr25519) and must agree.
 
-Categories (every vector is wide):
+Categories (every vector takes >= 35 windows; "windows" records how many):
   ed25519:
     honest        valid in both modes
     s_flip        honest with one bit of s flipped: invalid in both modes
@@ -59,30 +63,32 @@ def halfcheck_bin() -> str:
     return out
 
 
-def wide_flags(binary: str, ks: list[int]) -> list[bool]:
+def windows(binary: str, ks: list[int]) -> list[int]:
+    """the half-scalar window count of each k (64 = the wide fallback)"""
     buf = struct.pack("<I", len(ks)) + b"".join(k.to_bytes(32, "little") for k in ks)
     out = subprocess.run([binary], input=buf, capture_output=True, check=True).stdout
-    return [bool(out[130 * j + 64] & 2) for j in range(len(ks))]
+    return [(out[130 * j + 64] >> 2) + 32 for j in range(len(ks))]
 
 
 def message(height: int, nanos: int) -> bytes:
     return SB.vote_sign_bytes(CHAIN_ID, SB.PRECOMMIT, height, 0, BLOCK_ID, 1_700_000_000 + height, nanos)
 
 
-def search(binary: str, kfn, height: int, want: int, start: int = 0):
-    """messages M (by timestamp nanos) whose challenge kfn(M) takes the wide
-    schedule; returns [(M, k)]"""
-    found, nanos = [], start
-    while len(found) < want:
+def search(binary: str, kfn, height: int, want: dict, budget: int = 60 * BATCH):
+    """messages M (by timestamp nanos) whose challenge kfn(M) takes W
+    windows, for W -> count in `want` (W = 35 also accepts more); returns
+    [(M, k, W)] -- classes not found within `budget` tries are skipped"""
+    found, nanos, need = [], 0, dict(want)
+    while any(v > 0 for v in need.values()) and nanos < budget:
         msgs = [message(height, nanos + j) for j in range(BATCH)]
         ks = kfn(msgs)
-        for m, k, w in zip(msgs, ks, wide_flags(binary, ks)):
-            if w:
-                found.append((m, k))
+        for m, k, w in zip(msgs, ks, windows(binary, ks)):
+            cls = w if w in need else (35 if 35 < w < 64 and 35 in need else None)
+            if cls is not None and need[cls] > 0:
+                found.append((m, k, w))
+                need[cls] -= 1
         nanos += BATCH
-        if nanos - start > 200 * BATCH:
-            raise RuntimeError("search did not converge")
-    return found[:want]
+    return found
 
 
 def ed_vectors(binary: str) -> list[dict]:
@@ -104,19 +110,21 @@ def ed_vectors(binary: str) -> list[dict]:
         def kfn(R, Ab):
             return lambda msgs: [E.scalar_from_hash(E.sha512(R + Ab + m)) for m in msgs]
 
-        for m, k in search(binary, kfn(Rh, A), 1000 + i, 2):
+        want = {35: 2, 36: 1, 37: 1} if i == 0 else {35: 2}
+        budget = 400 * BATCH if i == 0 else 60 * BATCH
+        for m, k, w in search(binary, kfn(Rh, A), 1000 + i, want, budget):
             s = (r + k * a) % L
             sig = Rh + s.to_bytes(32, "little")
-            out.append({"cat": "honest", "pk": A, "sig": sig, "msg": m})
+            out.append({"cat": "honest", "pk": A, "sig": sig, "msg": m, "windows": w})
             flip = bytearray(sig)
             flip[32 + (k % 31)] ^= 1 << (k % 8)
-            out.append({"cat": "s_flip", "pk": A, "sig": bytes(flip), "msg": m})
-        for m, k in search(binary, kfn(Rm, A), 2000 + i, 1):
+            out.append({"cat": "s_flip", "pk": A, "sig": bytes(flip), "msg": m, "windows": w})
+        for m, k, w in search(binary, kfn(Rm, A), 2000 + i, {35: 1}):
             s = (r + k * a) % L
-            out.append({"cat": "mixed_R", "pk": A, "sig": Rm + s.to_bytes(32, "little"), "msg": m})
-        for m, k in search(binary, kfn(Rh, Am), 3000 + i, 1):
+            out.append({"cat": "mixed_R", "pk": A, "sig": Rm + s.to_bytes(32, "little"), "msg": m, "windows": w})
+        for m, k, w in search(binary, kfn(Rh, Am), 3000 + i, {35: 1}):
             s = (r + k * a) % L
-            out.append({"cat": "mixed_A", "pk": Am, "sig": Rh + s.to_bytes(32, "little"), "msg": m})
+            out.append({"cat": "mixed_A", "pk": Am, "sig": Rh + s.to_bytes(32, "little"), "msg": m, "windows": w})
     # verdicts: the Python restatement and the C oracle must agree
     for v in out:
         v["go"] = int(E.verify(v["pk"], v["msg"], v["sig"], E.MODE_GO_STDLIB))
@@ -146,15 +154,15 @@ def sr_vectors(binary: str) -> list[dict]:
                                             np.tile(np.frombuffer(R, np.uint8), (n, 1)), mm, off)
             return [int.from_bytes(k.tobytes(), "little") for k in ks]
 
-        for m, k in search(binary, kfn, 4000 + i, 2):
+        for m, k, w in search(binary, kfn, 4000 + i, {35: 2}):
             assert k == S.challenge(S.signing_context(b"", m), pk, R)
             sb = bytearray(((k * a + r) % L).to_bytes(32, "little"))
             sb[31] |= 0x80
             sig = R + bytes(sb)
-            out.append({"cat": "honest", "pk": pk, "sig": sig, "msg": m})
+            out.append({"cat": "honest", "pk": pk, "sig": sig, "msg": m, "windows": w})
             flip = bytearray(sig)
             flip[32 + (k % 30)] ^= 1 << (k % 8)
-            out.append({"cat": "s_flip", "pk": pk, "sig": bytes(flip), "msg": m})
+            out.append({"cat": "s_flip", "pk": pk, "sig": bytes(flip), "msg": m, "windows": w})
     for v in out:
         v["valid"] = int(S.verify(v["pk"], v["msg"], v["sig"]))
     pk = np.array([np.frombuffer(v["pk"], np.uint8) for v in out])
@@ -171,7 +179,7 @@ def main():
     sr = sr_vectors(binary)
     hx = lambda v: {k: (x.hex() if isinstance(x, bytes) else x) for k, x in v.items()}  # noqa: E731
     doc = {"generator": "tests/golden/make_wide.py",
-           "note": "every vector's challenge takes halfscalar.h's wide (64-window) schedule",
+           "note": "every vector's challenge takes >= 35 half-scalar windows (halfscalar.h); 'windows' records it",
            "ed25519": [hx(v) for v in ed], "sr25519": [hx(v) for v in sr]}
     path = os.path.join(ROOT, "tests", "golden", "wide_vectors.json")
     with open(path, "w") as f:

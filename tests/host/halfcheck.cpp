@@ -1,6 +1,7 @@
 // Host build of cometbft_amd/csrc/halfscalar.h (the device source): reads
 // n x 32-byte little-endian scalars k on stdin, writes per scalar
-// k1 (32 B) | |k2| (32 B) | flags (1 B: bit0 k2 negative, bit1 wide),
+// k1 (32 B) | |k2| (32 B) | flags (1 B: bit0 k2 negative, bit1 wide,
+// bits 2-7 the window count - 32),
 // twice: Lehmer schedule, then exact single steps. Test
 // infrastructure only (tests/test_host_math.py checks the invariants).
 #define CMTV_HD inline
@@ -18,7 +19,7 @@ int main() {
     cmtv::half_scalars<true>(h, k);   // Lehmer rounds (the device schedule)
     cmtv::half_scalars<false>(g, k);  // one exact Euclid step per round
     for (const cmtv::HalfScalars* x : {&h, &g}) {
-      uint8_t f = (x->k2_neg ? 1 : 0) | (x->wide ? 2 : 0);
+      uint8_t f = (x->k2_neg ? 1 : 0) | (x->wide ? 2 : 0) | (uint8_t)((x->windows - 32) << 2);
       fwrite(x->k1, 4, 8, stdout);
       fwrite(x->k2, 4, 8, stdout);
       fwrite(&f, 1, 1, stdout);

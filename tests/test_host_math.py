@@ -103,10 +103,11 @@ L = 2**252 + 27742317777372353535851937790883648493
 
 def test_half_scalar_decomposition():
     """halfscalar.h (the device source, host-compiled): k1 == k2 k (mod 8L),
-    k2 odd, 0 <= k1 < 2^134 and 0 < |k2| < 2^134 unless flagged wide (then
-    k1 = k, k2 = 1). Random scalars plus the boundary ones; the wide rate
-    must stay rare (it only costs time, never changes a verdict). The Lehmer
-    schedule must give exactly the pair of the one-step-per-round Euclid."""
+    k2 odd, 0 <= k1, |k2| < 2^(4W - 2) for the pair's window count W
+    (34..37) unless flagged wide (then k1 = k, k2 = 1, W = 64). Random
+    scalars plus the boundary ones; W > 34 stays rare (~1e-4) and wide rarer
+    (it only costs time, never changes a verdict). The Lehmer schedule must
+    give exactly the pair of the one-step-per-round Euclid."""
     binary = _build(HSRC, HBIN, ["-std=c++17"])
     rng = np.random.default_rng(215)
     ks = [0, 1, 2, 3, L - 1, L - 2, 2**127, 2**128 - 1, 2**134, 2**252]
@@ -114,22 +115,28 @@ def test_half_scalar_decomposition():
     buf = struct.pack("<I", len(ks)) + b"".join(k.to_bytes(32, "little") for k in ks)
     out = subprocess.run([binary], input=buf, capture_output=True, check=True, timeout=120).stdout
     assert len(out) == 130 * len(ks)
-    wide = 0
+    wide = graded = 0
     for j, k in enumerate(ks):
         rec = out[130 * j: 130 * j + 65]
         assert rec == out[130 * j + 65: 130 * (j + 1)], j  # Lehmer == exact steps
         k1 = int.from_bytes(rec[:32], "little")
         k2 = int.from_bytes(rec[32:64], "little")
         f = rec[64]
+        w = (f >> 2) + 32
         if f & 2:
             wide += 1
-            assert (k1, k2, f & 1) == (k, 1, 0), j
+            assert (k1, k2, f & 1, w) == (k, 1, 0, 64), j
             continue
+        assert 34 <= w <= 37, (j, w)
+        graded += w > 34
         s2 = -k2 if f & 1 else k2
         assert k2 & 1, j
-        assert k1 < 2**134 and 0 < k2 < 2**134, j
+        bound = 2 ** (4 * w - 2)
+        assert k1 < bound and 0 < k2 < bound, j
+        if w > 34:  # the smallest window count that holds the pair
+            assert max(k1.bit_length(), k2.bit_length()) > 4 * (w - 1) - 2, j
         assert (k1 - s2 * k) % (8 * L) == 0, j
-    assert wide <= 20, wide
+    assert wide <= 8 and graded <= 20, (wide, graded)  # wide: the boundary k (0, 1, 2^252, ...)
 
 
 @pytest.mark.parametrize("mode", [0, 1])

@@ -1,14 +1,16 @@
-"""GPU parity on the half-size-scalar wide fallback (tests/golden/wide_vectors.json,
-checked on the CPU in tests/test_wide_vectors.py).
+"""GPU parity on the half-size-scalar window schedules beyond the common 34
+(tests/golden/wide_vectors.json: 35- and 36-window pairs, checked on the CPU
+in tests/test_wide_vectors.py), and on the 64-window wide fallback, which no
+searchable k reaches (forced with the CMTV_FORCE_WIDE knob).
 
 The quad kernels (k_verify_quad, k_verify_sr25519_quad) pick the window count
-per WAVE: one wide signature switches its whole 16-signature wave to the
-64-window schedule, including the radix-256 B-digit schedule
-(quad.h:259-296). Each wide vector is therefore placed inside a wave of
-ordinary signatures (honest and bit-flipped), at a different lane position
-per wave, and the whole batch is compared with the C oracle bit for bit, in
-both Ed25519 modes. The lane kernels and the registered-key kernels
-(keyed.h / keyed_quad.h, which do not split k) run the same batches.
+per WAVE (the largest its 16 signatures need), and the radix-256 B digits
+ride on the low windows whatever the count (quad.h q_straus_half). Each
+vector is therefore placed inside a wave of ordinary signatures (honest and
+bit-flipped), at a different lane position per wave, and the whole batch is
+compared with the C oracle bit for bit, in both Ed25519 modes. The lane
+kernels and the registered-key kernels (keyed.h / keyed_quad.h, which do not
+split k) run the same batches.
 Reference semantics: crypto/ed25519/ed25519.go:148-155 (Go 1.19 Verify) and
 crypto/sr25519/pubkey.go:34-60.
 """
@@ -129,3 +131,39 @@ def test_reference_keygen_vector_on_device(gpu_ctx):
     sig[1, 7] ^= 2
     got = gpu_ctx.verify(np.repeat(pk, 2, axis=0), sig, m, off, MODE_GO_STDLIB)
     assert list(got) == [1, 0]
+
+
+@pytest.fixture(scope="module")
+def forced_wide_ctx():
+    from cometbft_amd import Context
+
+    os.environ["CMTV_FORCE_WIDE"] = "1"
+    try:
+        return Context(device=0)
+    finally:
+        del os.environ["CMTV_FORCE_WIDE"]
+
+
+@pytest.mark.parametrize("mode,key", [(MODE_GO_STDLIB, "go"), (MODE_ZIP215, "zip215")])
+def test_forced_wide_schedule_on_corpus(forced_wide_ctx, corpus, mode, key):
+    """CMTV_FORCE_WIDE: every quad takes the wide fallback (k1 = k, k2 = 1,
+    64 windows, B digits on windows 0..32): the edge-case corpus and mixed
+    batches stay bit-exact."""
+    msg, off = pack_messages(corpus["msgs"])
+    got = forced_wide_ctx.verify(corpus["pk"], corpus["sig"], msg, off, mode)
+    assert np.array_equal(got, corpus[key]), np.nonzero(got != corpus[key])[0][:10]
+    pk, sig, m, off = _mixed_batch("ed25519", seed=6)
+    exp = coracle.verify_batch(pk, sig, m, off, mode, nthreads=8)
+    assert np.array_equal(forced_wide_ctx.verify(pk, sig, m, off, mode), exp)
+
+
+def test_forced_wide_schedule_sr25519(forced_wide_ctx):
+    pk, sig, m, off = _mixed_batch("sr25519", seed=7)
+    exp = coracle.sr25519_verify_batch(pk, sig, m, off, nthreads=8)
+    assert np.array_equal(forced_wide_ctx.verify_sr25519(pk, sig, m, off), exp)
+    with open(os.path.join(ROOT, "tests", "golden", "sr25519_corpus.json")) as f:
+        vecs = json.load(f)["vectors"]
+    cpk = np.array([np.frombuffer(bytes.fromhex(v["pk"]), np.uint8) for v in vecs])
+    csig = np.array([np.frombuffer(bytes.fromhex(v["sig"]), np.uint8) for v in vecs])
+    cm, coff = pack_messages([bytes.fromhex(v["msg"]) for v in vecs])
+    assert [int(x) for x in forced_wide_ctx.verify_sr25519(cpk, csig, cm, coff)] == [v["valid"] for v in vecs]

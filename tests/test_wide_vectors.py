@@ -1,11 +1,13 @@
 """CPU checks of tests/golden/wide_vectors.json (made by
-tests/golden/make_wide.py): signatures whose challenge k takes the wide
-(64-window) fallback of the half-size-scalar split (halfscalar.h), which
-random data reaches for only ~5e-5 of k.
+tests/golden/make_wide.py): signatures whose challenge k needs more than the
+common 34 windows of the half-size-scalar split (halfscalar.h): 35, 36 and
+37-window pairs, which random data reaches for only ~5e-5, ~3e-6 and ~3e-7
+of k.
 
  - the stored verdicts are re-derived by both oracles (Python big-int
    restatements and oracle/liboracle.so), both Ed25519 modes and sr25519;
- - every vector's k really is wide for the host build of halfscalar.h;
+ - every vector's k takes the recorded window count in the host build of
+   halfscalar.h;
  - the host builds of the device pipelines (hostcheck "half" = lane
    half-scalar Straus, quadcheck = the 4-lane quad kernel source) reproduce
    the verdicts through that schedule.
@@ -38,11 +40,11 @@ def wide():
     return arr(doc["ed25519"]), arr(doc["sr25519"])
 
 
-def _wide_flags(ks):
+def _windows(ks):
     binary = _build(HSRC, HBIN, ["-std=c++17"])
     buf = struct.pack("<I", len(ks)) + b"".join(k.to_bytes(32, "little") for k in ks)
     out = subprocess.run([binary], input=buf, capture_output=True, check=True).stdout
-    return [bool(out[130 * j + 64] & 2) for j in range(len(ks))]
+    return [(out[130 * j + 64] >> 2) + 32 for j in range(len(ks))]
 
 
 def test_ed25519_wide_verdicts_and_flags(wide):
@@ -54,7 +56,8 @@ def test_ed25519_wide_verdicts_and_flags(wide):
         assert int(E.verify(pk, m, sig, E.MODE_GO_STDLIB)) == v["go"]
         assert int(E.verify(pk, m, sig, E.MODE_ZIP215)) == v["zip215"]
         ks.append(E.scalar_from_hash(E.sha512(sig[:32] + pk + m)))
-    assert all(_wide_flags(ks))
+    assert _windows(ks) == [v["windows"] for v in ed["raw"]]
+    assert all(v["windows"] >= 35 for v in ed["raw"]) and {35, 36} <= {v["windows"] for v in ed["raw"]}
     m, off = coracle.pack_msgs(ed["msgs"])
     for mode, key in ((0, "go"), (1, "zip215")):
         got = coracle.verify_batch(ed["pk"], ed["sig"], m, off, mode)
@@ -68,7 +71,8 @@ def test_sr25519_wide_verdicts_and_flags(wide):
         pk, sig, m = (bytes.fromhex(v[k]) for k in ("pk", "sig", "msg"))
         assert int(S.verify(pk, m, sig)) == v["valid"]
         ks.append(S.challenge(S.signing_context(b"", m), pk, sig[:32]))
-    assert all(_wide_flags(ks))
+    assert _windows(ks) == [v["windows"] for v in sr["raw"]]
+    assert all(v["windows"] >= 35 for v in sr["raw"])
     m, off = coracle.pack_msgs(sr["msgs"])
     assert [int(x) for x in coracle.sr25519_verify_batch(sr["pk"], sr["sig"], m, off)] == [v["valid"] for v in sr["raw"]]
 

@@ -21,6 +21,7 @@ struct DevQuad {
   template <int PAT>
   __device__ uint32_t one(uint32_t x) const {
     if (VAR == 0) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, PAT, 0xF, 0xF, true);
+    if (VAR == 4) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, PAT, 0xF, 0xF, false);  // kernels.hip
     if (VAR == 1) return (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, PAT, 0xF, 0xF, false);
     if (VAR == 2) {
       const int src = (threadIdx.x & ~3) | ((PAT >> (2 * (threadIdx.x & 3))) & 3);
@@ -73,10 +74,20 @@ struct LdsTab {  // same layout as kernels.hip's DevATabQ
       c.v[2 * k + 1] = x.y;
     }
   }
+  template <class Q>
+  __device__ void load_signed(const Q& q, int e, bool neg, fe& c) const {
+    const uint32_t src = (t & 2) ? t : (t ^ (neg ? 1u : 0u));
+    for (int k = 0; k < 5; k++) {
+      const uint2 x = lds[(e * 5 + k) * 64 + src];
+      c.v[2 * k] = x.x;
+      c.v[2 * k + 1] = x.y;
+    }
+    q_negate_lane3(c, (int)(t & 3), neg);
+  }
 };
 __global__ __launch_bounds__(64, 1) void k_time(const uint32_t* pk, const uint32_t* sig, const uint8_t* msg, uint32_t mlen,
                        const uint32_t* btab, unsigned long long* ts, int* verdict) {
-  DevQuad<1> q;
+  DevQuad<4> q;
   DevBTabQ bt{btab};
   if (threadIdx.x == 0) ts[15] = __builtin_amdgcn_s_memtime();
   TimeProbe pr{ts};

@@ -36,6 +36,14 @@
 #define CMTV_SCHED_FENCE() ((void)0)
 #endif
 
+// (x ^ m) & k for per-lane masks m, k: one v_bitop3_b32 on gfx950 (truth
+// table 0x28); from plain C the masks' selects lower to xor + v_cndmask
+#if defined(__HIP_DEVICE_COMPILE__)
+#define CMTV_XOR_AND(x, m, k) __builtin_amdgcn_bitop3_b32((x), (m), (k), 0x28)
+#else
+#define CMTV_XOR_AND(x, m, k) (((x) ^ (m)) & (k))
+#endif
+
 #ifdef CMTV_BOUNDS_CHECK
 #include <cassert>
 #define CMTV_ASSERT(x) assert(x)

@@ -74,11 +74,20 @@ CMTV_HD void q_cached_identity(fe& v, int lane) {
 template <class Q>
 CMTV_HD void q_dbl(const Q& q, fe& v) {
   const int lane = q.lane();
+  // per-lane masks (loop-invariant): the four U_c share one straight-line
+  // form, U = a + (b ^ mb) + corr + 2p + (((r ^ mr) & rm) << sh), instead
+  // of computing all four candidates and selecting
+  const uint32_t m3 = lane == 3 ? ~0u : 0u;
+  const uint32_t mb = (lane == 1 || lane == 2) ? ~0u : 0u;  // -B on lanes 1, 2
+  const uint32_t mr = lane == 0 ? ~0u : 0u;                 // -K on lane 0
+  const uint32_t rm = lane < 2 ? ~0u : 0u;                  // r used on lanes 0, 1
+  const uint32_t sh = lane == 1 ? 1u : 0u;                  // 2C' on lane 1
+  const uint32_t corr = lane == 3 ? 0u : 1u;                // ~x = -x - 1
   fe a, b, m;
-  q.template perm<QP_B0>(a, v);
+  q.template perm<qp(0, 1, 2, 0)>(a, v);
   q.template perm<QP_B1>(b, v);
 #pragma unroll
-  for (int i = 0; i < 10; i++) m.v[i] = lane == 3 ? a.v[i] + b.v[i] : v.v[i];  // X + Y on lane 3
+  for (int i = 0; i < 10; i++) m.v[i] = a.v[i] + (b.v[i] & m3);  // X + Y on lane 3
   fe_sq(m, m);
   fe r;
   q.template perm<QP_B0>(a, m);             // A
@@ -86,12 +95,9 @@ CMTV_HD void q_dbl(const Q& q, fe& v) {
   q.template perm<qp(3, 2, 2, 2)>(r, m);    // lane 0: K, lane 1: C'
 #pragma unroll
   for (int i = 0; i < 10; i++) {
-    const uint32_t s = a.v[i] + b.v[i];                  // S
-    const uint32_t mm = a.v[i] + (fe_p2(i) - b.v[i]);    // M
-    const uint32_t e = s + (fe_p2(i) - r.v[i]);          // E' = S - K
-    const uint32_t f = mm + 2 * r.v[i];                  // F' = M + 2C'
-    const uint32_t lo = (lane & 1) ? f : e, hi = (lane & 1) ? s : mm;
-    m.v[i] = (lane & 2) ? hi : lo;
+    // lane 0: E' = S - K, 1: F' = M + 2C', 2: M = A - B, 3: S = A + B (+2p)
+    const uint32_t u = (b.v[i] ^ mb) + a.v[i] + corr + fe_p2(i);
+    m.v[i] = (CMTV_XOR_AND(r.v[i], mr, rm) << sh) + u;
   }
   fe_carry(m);
   q.template perm<qp(0, 2, 1, 0)>(a, m);  // E', M, F', E'
@@ -110,20 +116,28 @@ CMTV_HD void q_dbl(const Q& q, fe& v) {
 template <class Q>
 CMTV_HD void q_add(const Q& q, fe& v, const fe& c) {
   const int lane = q.lane();
+  // per-lane masks (loop-invariant); ~x + 1 = -x supplies the negations
+  const uint32_t m0 = lane == 0 ? ~0u : 0u;
+  const uint32_t m01 = lane < 2 ? ~0u : 0u;
   fe x, y, p;
-  q.template perm<QP_B0>(x, v);
-  q.template perm<QP_B1>(y, v);
+  q.template perm<qp(0, 0, 0, 0)>(x, v);
+  q.template perm<qp(1, 1, 2, 3)>(y, v);
 #pragma unroll
   for (int i = 0; i < 10; i++) {
-    const uint32_t w = lane == 0 ? fe_p2(i) - x.v[i] : x.v[i];
-    p.v[i] = (lane & 2) ? v.v[i] : y.v[i] + w;  // Y-X, Y+X, Z, T
+    // lane 0: Y - X + 2p, 1: Y + X, 2: Z, 3: T
+    const uint32_t k = lane == 0 ? fe_p2(i) + 1 : 0u;
+    p.v[i] = y.v[i] + CMTV_XOR_AND(x.v[i], m0, m01) + k;
   }
   fe t;
   fe_mul(t, p, c);  // A, B, D, C
   q.template perm<qp(1, 2, 2, 1)>(x, t);  // B, D, D, B
   q.template perm<qp(0, 3, 3, 0)>(y, t);  // A, C, C, A
 #pragma unroll
-  for (int i = 0; i < 10; i++) p.v[i] = x.v[i] + ((lane & 2) ? y.v[i] : fe_p2(i) - y.v[i]);  // E, F, G, H
+  for (int i = 0; i < 10; i++) {
+    // E = B - A, F = D - C (lanes 0, 1: + 2p); G = D + C, H = B + A
+    const uint32_t k = lane < 2 ? fe_p2(i) + 1 : 0u;
+    p.v[i] = x.v[i] + (y.v[i] ^ m01) + k;
+  }
   q.template perm<qp(1, 2, 1, 0)>(x, p);  // F, G, F, E
   q.template perm<qp(0, 3, 2, 3)>(y, p);  // E, H, G, H
   fe_mul(v, x, y);
@@ -167,15 +181,22 @@ CMTV_HD void q_negate_lane3(fe& c, int lane, bool neg) {
 // (y+x at word 0, y-x at word ymx_off, 2dxy at word xy_off), or of the
 // identity when ident. ld(off, c) loads the 10 limbs at word `off`.
 template <class Q, class Ld>
-CMTV_HD void q_niels_coord(const Q& q, fe& c, const Ld& ld, int ymx_off, int xy_off, bool neg, bool ident) {
+CMTV_HD void q_niels_load(const Q& q, fe& c, const Ld& ld, int ymx_off, int xy_off, bool neg) {
   const int lane = q.lane();
   const int off = lane == 3 ? xy_off : (((lane == 0) != neg) ? ymx_off : 0);
   ld(off, c);
+}
+CMTV_HD void q_niels_fix(fe& c, int lane, bool neg, bool ident) {
   const bool cst = ident || lane == 2;  // lane 2: 2Z = 2 (affine); identity (1, 1, 2, 0)
   const uint32_t c0 = lane == 2 ? 2u : (lane == 3 ? 0u : 1u);
 #pragma unroll
   for (int i = 0; i < 10; i++) c.v[i] = cst ? (i == 0 ? c0 : 0u) : c.v[i];
   q_negate_lane3(c, lane, neg && !ident);
+}
+template <class Q, class Ld>
+CMTV_HD void q_niels_coord(const Q& q, fe& c, const Ld& ld, int ymx_off, int xy_off, bool neg, bool ident) {
+  q_niels_load(q, c, ld, ymx_off, xy_off, neg);
+  q_niels_fix(c, q.lane(), neg, ident);
 }
 
 }  // namespace cmtv
@@ -293,23 +314,18 @@ CMTV_HD void q_straus_half(const Q& q, fe& v, fe& rc, const uint32_t k[8], const
   q_identity(v, lane);
 #pragma unroll 1
   for (int win = W - 1; win >= 0; win--) {
-    if (win != W - 1) {
-#pragma unroll 1
-      for (int d = 0; d < 4; d++) q_dbl(q, v);
-    }
+    // this window's addends are fetched first (LDS for A and R, the global
+    // B row) so their latency hides under the four doublings
+    fe cA, cR, cB;
     {
       const int dA = (int)sc_shift_out(tA, 4) - 8;
-      fe c;
-      tabA.load_signed(q, dA < 0 ? -dA : dA, dA < 0, c);
-      q_add(q, v, c);
-    }
-    {
+      tabA.load_signed(q, dA < 0 ? -dA : dA, dA < 0, cA);
       const int dR = (int)sc_shift_out(tR, 4) - 8;
-      fe c;
-      tabR.load_signed(q, dR < 0 ? -dR : dR, dR < 0, c);
-      q_add(q, v, c);
+      tabR.load_signed(q, dR < 0 ? -dR : dR, dR < 0, cR);
     }
-    if (win <= 32 && ((win & 1) == 0 || win <= 31)) {
+    const bool has_b = win <= 32 && ((win & 1) == 0 || win <= 31);
+    bool b_neg = false, b_ident = false;
+    if (has_b) {
       // even windows: digit win/2 of u mod 2^128 against (1..128)B;
       // odd windows: digit (win-1)/2 of u >> 128 against (1..128)[2^124]B
       const bool odd = win & 1;
@@ -320,11 +336,22 @@ CMTV_HD void q_straus_half(const Q& q, fe& v, fe& rc, const uint32_t k[8], const
         dB = (int)sc_shift_out(tLo, 8) - 128;
       const int ib = dB < 0 ? -dB : dB;
       const int row = (ib > 0 ? ib - 1 : 0) + (odd ? BTAB_ENTRIES : 0);
-      fe c;
-      q_niels_coord(
-          q, c, [&](int off, fe& r) { btab.load_coord(row, off, r); }, BTAB_COORD_WORDS, 2 * BTAB_COORD_WORDS,
-          dB < 0, ib == 0);
-      q_add(q, v, c);
+      // raw row only: the select / negation waits until after the doublings
+      q_niels_load(
+          q, cB, [&](int off, fe& r) { btab.load_coord(row, off, r); }, BTAB_COORD_WORDS, 2 * BTAB_COORD_WORDS,
+          dB < 0);
+      b_neg = dB < 0;
+      b_ident = ib == 0;
+    }
+    if (win != W - 1) {
+#pragma unroll 1
+      for (int d = 0; d < 4; d++) q_dbl(q, v);
+    }
+    q_add(q, v, cA);
+    q_add(q, v, cR);
+    if (has_b) {
+      q_niels_fix(cB, lane, b_neg, b_ident);
+      q_add(q, v, cB);
     }
     if (win >= W - 4) probe.snap(6 + (W - 1 - win), v);
   }

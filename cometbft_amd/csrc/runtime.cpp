@@ -42,6 +42,9 @@ constexpr size_t kQuadMaxDefault = 40000;
 constexpr size_t kKeyedQuadMaxDefault = 16384;
 // signatures per device below which a batch is not sharded (env CMTV_SHARD_MIN)
 constexpr size_t kShardMinDefault = 8192;
+// single-device host batches up to this size return their bitmap through
+// mapped host memory (no D2H copy; the writes are a few PCIe transactions)
+constexpr size_t kZeroCopyMax = 4096;
 constexpr int kMaxDevices = 64;
 
 struct DevBuf {
@@ -68,6 +71,7 @@ struct DevBuf {
 struct HostBuf {
   void* p = nullptr;
   size_t cap = 0;
+  unsigned flags = hipHostMallocDefault;
   hipError_t ensure(size_t bytes) {
     if (bytes <= cap) return hipSuccess;
     if (p) (void)hipHostFree(p);
@@ -75,7 +79,7 @@ struct HostBuf {
     cap = 0;
     size_t want = std::max<size_t>(bytes, 4096);
     want = want + want / 4;
-    hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+    hipError_t e = hipHostMalloc(&p, want, flags);
     if (e == hipSuccess) cap = want;
     return e;
   }
@@ -301,6 +305,9 @@ struct CmtvDev {
   uint16_t* d_srprog = nullptr;  // sr25519 transcript program (merlin.h)
   DevBuf d_atab, d_in, d_out, d_all;
   HostBuf h_in, h_out;
+  // small single-device host batches: the kernel writes the verdict bitmap
+  // straight into this coherent, device-mapped host buffer (no D2H copy)
+  HostBuf h_zc{nullptr, 0, hipHostMallocCoherent | hipHostMallocMapped};
   // The lane kernels' A-table scratch is shared by every launch on this
   // device, whatever stream it is enqueued on: each lane launch waits for the
   // previous one (atab_done) so calls on different streams cannot overwrite
@@ -612,7 +619,7 @@ static int enqueue_shard(cmtv_ctx* ctx, size_t g, const HostBatch& B, size_t a, 
   auto* dout = static_cast<uint8_t*>(D.d_out.p);
   if ((e = hipMemcpyAsync(din, hin, in_bytes, hipMemcpyHostToDevice, D.stream)) != hipSuccess) return hip_fail(e);
   if (tpl) {
-    if ((e = hipMemsetAsync(din + o_msg + mb, 0, 16, D.stream)) != hipSuccess) return hip_fail(e);
+    // k_sign_bytes also writes the 16 zero bytes after the last message
     if ((e = launch_sign_bytes((uint32_t)m, din + o_tmpl, din + o_blob, reinterpret_cast<uint32_t*>(din + o_tidx),
                                din + o_flag, reinterpret_cast<int64_t*>(din + o_sec),
                                reinterpret_cast<int32_t*>(din + o_nanos), reinterpret_cast<uint32_t*>(din + o_off),
@@ -636,6 +643,31 @@ static int run_host_batch_(cmtv_ctx* ctx, const HostBatch& B, uint8_t* out_valid
   const ShardPlan P = plan_shards(n, ctx->devs.size(), ctx->shard_min);
   const size_t words = (n + 63) / 64;
   hipError_t e;
+  if (P.G == 1 && n <= kZeroCopyMax) {
+    // one device, a small batch: the verify kernel writes the bitmap into
+    // mapped host memory, so the call is H2D + (sign-bytes) + verify + sync
+    CmtvDev& D = ctx->devs[0];
+    (void)hipSetDevice(D.ordinal);
+    if ((e = D.h_zc.ensure(8 * words)) != hipSuccess) return hip_fail(e);
+    void* dzc = nullptr;
+    if ((e = hipHostGetDevicePointer(&dzc, D.h_zc.p, 0)) != hipSuccess) return hip_fail(e);
+    size_t o_valid = 0;
+    const int rc = enqueue_shard(ctx, 0, B, 0, n, false, static_cast<uint64_t*>(dzc), o_valid);
+    if (rc != CMTV_OK) return rc;
+    if ((e = hipStreamSynchronize(D.stream)) != hipSuccess) return hip_fail(e);
+    harvest(ctx, false);
+    (void)hipSetDevice(D.ordinal);
+    uint64_t* bm = static_cast<uint64_t*>(D.h_zc.p);
+    // bits past n of the last word are not written by every kernel
+    if (n & 63) bm[words - 1] &= (1ull << (n & 63)) - 1;
+    uint64_t valid_count = 0;
+    for (size_t w = 0; w < words; w++) valid_count += (uint64_t)__builtin_popcountll(bm[w]);
+    ctx->stats.invalid += n - valid_count;
+    if (out_bitmap) std::memcpy(out_bitmap, bm, 8 * words);
+    if (out_valid)
+      for (size_t i = 0; i < n; i++) out_valid[i] = (uint8_t)((bm[i >> 6] >> (i & 63)) & 1);
+    return CMTV_OK;
+  }
   uint64_t* bufs[kMaxDevices];
   for (size_t g = 0; g < P.G; g++) {
     CmtvDev& D = ctx->devs[g];
@@ -681,7 +713,9 @@ static int run_host_batch_(cmtv_ctx* ctx, const HostBatch& B, uint8_t* out_valid
   (void)hipSetDevice(D0.ordinal);
   harvest(ctx, false);
   (void)hipSetDevice(D0.ordinal);
-  const uint64_t* bm = reinterpret_cast<const uint64_t*>(hout + o_bm);
+  uint64_t* bm = reinterpret_cast<uint64_t*>(hout + o_bm);
+  // bits past n of the last word are not written by every kernel
+  if (n & 63) bm[words - 1] &= (1ull << (n & 63)) - 1;
   uint64_t valid_count = 0;
   for (size_t w = 0; w < words; w++) valid_count += (uint64_t)__builtin_popcountll(bm[w]);
   ctx->stats.invalid += n - valid_count;
@@ -837,6 +871,7 @@ static void release_device(CmtvDev& D) {
   D.d_all.release();
   D.h_in.release();
   D.h_out.release();
+  D.h_zc.release();
   if (D.d_btab) (void)hipFree(D.d_btab);
   if (D.d_bcomb) (void)hipFree(D.d_bcomb);
   if (D.d_srprog) (void)hipFree(D.d_srprog);

@@ -24,6 +24,11 @@ __global__ __launch_bounds__(256) void k_sign_bytes(uint32_t n, const SbTemplate
                                                     const uint32_t* __restrict__ off, uint8_t* __restrict__ msg) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
+  // the 16 zero bytes after the last message (the SHA block loader's slack)
+  if (i == n - 1) {
+#pragma unroll
+    for (int j = 0; j < 16; j++) msg[off[n] + j] = 0;
+  }
   const SbTemplate t = tmpls[tidx[i]];
   DevBytes out{msg + off[i]};
   sb_write(out, t, blob, commit_flag[i] != 0, sec[i], nanos[i]);

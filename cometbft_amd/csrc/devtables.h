@@ -5,6 +5,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "oct.h"
 #include "quad.h"
 #include "verify_core.h"
 
@@ -91,6 +92,19 @@ struct DevQuad {
     return dpp<PAT>(x);
   }
   __device__ __forceinline__ bool any(bool x) const { return __ballot(x) != 0; }
+};
+
+// Oct policy (oct.h): two quads per signature; the upper quad's words reach
+// the lower one by a DPP row shift (lane i <- lane i + 4, inside a 16-lane row).
+struct DevOct : DevQuad {
+  __device__ __forceinline__ bool upper() const { return (threadIdx.x & 4) != 0; }
+  __device__ __forceinline__ uint32_t from_upper32(uint32_t x) const {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x104 /* row_shl:4 */, 0xF, 0xF, false);
+  }
+  __device__ __forceinline__ void from_upper(fe& o, const fe& v) const {
+#pragma unroll
+    for (int i = 0; i < 10; i++) o.v[i] = from_upper32(v.v[i]);
+  }
 };
 
 // Quad (0..8)(-A) table in LDS: entry e, limb pair k of lane t at

@@ -5,14 +5,15 @@
 
 namespace cmtv {
 
-constexpr uint32_t kBtabWords = 2 * 128 * 36;  // (1..128)B, (1..128)[2^124]B; 36 words per row
+constexpr uint32_t kBtabWords = 3 * 128 * 36;  // (1..128)B, [2^124]B, [2^128]B multiples; 36 words per row
 constexpr uint32_t kAtabWordsPerLane = 320; // (1..8)(-A), 40 words per point
 constexpr uint32_t kCombWords = 32 * 128 * 32;     // one registered-key comb (keyed.h), 512 KiB
 constexpr uint32_t kCombScratchWordsPerKey = 128 * 320;  // prefix products while building
 
 // launch_verify / launch_verify_sr25519 kflags: the quad kernel (else lane),
-// and the CMTV_FORCE_WIDE test knob (every quad takes the 64-window schedule)
-constexpr uint32_t kLaunchQuad = 1, kLaunchForceWide = 2;
+// the CMTV_FORCE_WIDE test knob (every quad takes the 64-window schedule),
+// and the oct kernel (with kLaunchQuad; Ed25519 only)
+constexpr uint32_t kLaunchQuad = 1, kLaunchForceWide = 2, kLaunchOct = 4;
 
 hipError_t launch_btab_init(uint32_t* d_rows, hipStream_t s);
 hipError_t launch_verify(uint32_t mode, uint32_t n, const void* pk, const void* sig, const void* msg,

@@ -56,12 +56,12 @@ __device__ __forceinline__ void load_words(uint32_t* w, const uint32_t* __restri
   }
 }
 
-// rows 0..127: (1..128)B; rows 128..255: (1..128)[2^124]B
+// rows 0..127: (1..128)B; 128..255: (1..128)[2^124]B; 256..383: (1..128)[2^128]B
 __global__ __launch_bounds__(64) void k_btab_init(uint32_t* __restrict__ rows) {
   const int e = blockIdx.x * 64 + threadIdx.x;
-  if (e >= 2 * BTAB_ENTRIES) return;
+  if (e >= 3 * BTAB_ENTRIES) return;
   uint32_t row[BTAB_ROW_WORDS];
-  btab_entry(row, (e % BTAB_ENTRIES) + 1, e >= BTAB_ENTRIES);
+  btab_entry(row, (e % BTAB_ENTRIES) + 1, e / BTAB_ENTRIES);
 #pragma unroll
   for (int i = 0; i < BTAB_ROW_WORDS; i++) rows[e * BTAB_ROW_WORDS + i] = row[i];
 }
@@ -122,6 +122,36 @@ __global__ __launch_bounds__(64, CMTV_QUAD_WAVES_PER_EU) void k_verify_quad(uint
   x = (x | (x >> 12)) & 0x000000FF000000FFull;
   x = (x | (x >> 24)) & 0xFFFFull;
   if (threadIdx.x == 0 && out_bitmap) reinterpret_cast<uint16_t*>(out_bitmap)[gid >> 6] = (uint16_t)x;
+}
+
+// One signature per oct of lanes (oct.h): the quad verifier's Straus chain
+// split over two quads, for batches that leave SIMDs idle. Verdict bits:
+// lane 0 of each oct votes; a wave's 8 bits are one byte of the bitmap.
+template <uint32_t MODE>
+__global__ __launch_bounds__(64, CMTV_QUAD_WAVES_PER_EU) void k_verify_oct(uint32_t n, const uint32_t* __restrict__ pk,
+                                                      const uint32_t* __restrict__ sig,
+                                                      const uint8_t* __restrict__ msg,
+                                                      const uint32_t* __restrict__ off,
+                                                      const uint32_t* __restrict__ btab,
+                                                      uint8_t* __restrict__ out_valid,
+                                                      uint64_t* __restrict__ out_bitmap, uint32_t force_wide) {
+  const uint32_t gid = blockIdx.x * 64 + threadIdx.x;
+  const uint32_t s = gid >> 3;
+  const bool active = s < n;
+  const uint32_t i = active ? s : n - 1;
+  const uint32_t m0 = off[i], m1 = off[i + 1];
+  DevOct q;
+  DevBTabQ bt{btab};
+  __shared__ uint2 tab_lds[9 * 5 * 64];  // each lane: its quad's (0..8)P coordinate, 22.5 KiB per wave
+  DevATabQ ta{tab_lds, threadIdx.x};
+  bool v = o_verify<MODE>(q, pk + 8 * (size_t)i, sig + 16 * (size_t)i, msg + m0, m1 - m0, bt, ta, force_wide != 0);
+  v = v && active;
+  if (active && (threadIdx.x & 7) == 0 && out_valid) out_valid[s] = v ? 1 : 0;
+  uint64_t x = __ballot(v && (threadIdx.x & 7) == 0) & 0x0101010101010101ull;
+  x = (x | (x >> 7)) & 0x0003000300030003ull;
+  x = (x | (x >> 14)) & 0x0000000F0000000Full;
+  x = (x | (x >> 28)) & 0xFFull;
+  if (threadIdx.x == 0 && out_bitmap) reinterpret_cast<uint8_t*>(out_bitmap)[gid >> 6] = (uint8_t)x;
 }
 
 // Prefix products of comb_build_column, word-major / lane-minor per launch.
@@ -261,7 +291,7 @@ __global__ __launch_bounds__(64) void k_sign(uint32_t n, const uint32_t* __restr
 static inline unsigned blocks_for(uint32_t n) { return (n + 63) / 64; }
 
 hipError_t launch_btab_init(uint32_t* d_rows, hipStream_t s) {
-  hipLaunchKernelGGL(k_btab_init, dim3(blocks_for(2 * BTAB_ENTRIES)), dim3(64), 0, s, d_rows);
+  hipLaunchKernelGGL(k_btab_init, dim3(blocks_for(3 * BTAB_ENTRIES)), dim3(64), 0, s, d_rows);
   return hipGetLastError();
 }
 
@@ -277,6 +307,16 @@ hipError_t launch_verify(uint32_t mode, uint32_t n, const void* pk, const void* 
   auto op = static_cast<const uint32_t*>(off);
   auto vp = static_cast<uint8_t*>(valid);
   auto bp = static_cast<uint64_t*>(bitmap);
+  if (quad && (kflags & kLaunchOct)) {
+    // one 64-lane block = 8 signatures; whole groups of 8 blocks so every
+    // byte of every bitmap word is written
+    const dim3 grid(((n + 63) / 64) * 8), block(64);
+    if (mode == MODE_ZIP215)
+      hipLaunchKernelGGL(k_verify_oct<MODE_ZIP215>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp, fw);
+    else
+      hipLaunchKernelGGL(k_verify_oct<MODE_GO_STDLIB>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp, fw);
+    return hipGetLastError();
+  }
   if (quad) {
     // one 64-lane block = 16 signatures; whole groups of 4 blocks so every
     // 16-bit slice of every bitmap word is written

@@ -63,20 +63,23 @@ CMTV_HD void cached_neg_point(ge_p3& r, const ge_p3& p) {
 }
 
 // [m]B for m = 1..128 in affine niels form (one entry; used by the table
-// initialisation kernel and by host-side tests). Rows 128..255 of the device
-// table hold [m 2^124]B (hi = 1), the second fixed-base table of the
-// half-size-scalar verifier (halfscalar.h).
-CMTV_HD void btab_entry(uint32_t row[BTAB_ROW_WORDS], int m, bool hi = false) {
+// initialisation kernel and by host-side tests). The device table holds
+// three blocks of 128 rows: block 0 = [m]B, block 1 = [m 2^124]B (the quad
+// verifier's odd windows, halfscalar.h), block 2 = [m 2^128]B (the oct
+// verifier's upper quad, oct.h).
+CMTV_HD int btab_block_shift(int block) { return block == 0 ? 0 : (block == 1 ? 124 : 128); }
+CMTV_HD void btab_entry(uint32_t row[BTAB_ROW_WORDS], int m, int block = 0) {
   uint32_t bw[8];
   basepoint_words(bw);
   ge_p3 B, acc;
   p3_frombytes(B, bw);
-  if (hi) {
+  const int shift = btab_block_shift(block);
+  if (shift) {
     ge_efgh t;
     ge_p2 q;
     p3_to_p2(q, B);
 #pragma unroll 1
-    for (int i = 0; i < 124; i++) {
+    for (int i = 0; i < shift; i++) {
       p2_dbl(t, q);
       efgh_to_p2(q, t);
     }

@@ -61,3 +61,24 @@ def gpu_ctx_lane():
                 del os.environ[k]
             else:
                 os.environ[k] = v
+
+
+@pytest.fixture(scope="session")
+def gpu_ctx_quad():
+    """A context whose small Ed25519 batches take the 4-lanes-per-signature
+    kernel (CMTV_OCT_MAX=0) instead of the default 8-lane one (oct.h)."""
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from cometbft_amd import Context
+
+    old = os.environ.get("CMTV_OCT_MAX")
+    os.environ["CMTV_OCT_MAX"] = "0"
+    try:
+        return Context(device=0)
+    finally:
+        if old is None:
+            del os.environ["CMTV_OCT_MAX"]
+        else:
+            os.environ["CMTV_OCT_MAX"] = old

@@ -72,10 +72,10 @@ def _mixed_batch(kind, waves_per_vector=1, seed=3):
     return np.array(pk), np.array(sig), m2, off2
 
 
-@pytest.mark.parametrize("kernel", ["quad", "lane"])
+@pytest.mark.parametrize("kernel", ["oct", "quad", "lane"])
 @pytest.mark.parametrize("mode", [MODE_GO_STDLIB, MODE_ZIP215])
-def test_ed25519_wide_in_mixed_waves(gpu_ctx, gpu_ctx_lane, kernel, mode):
-    ctx = gpu_ctx if kernel == "quad" else gpu_ctx_lane
+def test_ed25519_wide_in_mixed_waves(gpu_ctx, gpu_ctx_quad, gpu_ctx_lane, kernel, mode):
+    ctx = {"oct": gpu_ctx, "quad": gpu_ctx_quad, "lane": gpu_ctx_lane}[kernel]
     pk, sig, m, off = _mixed_batch("ed25519")
     exp = coracle.verify_batch(pk, sig, m, off, mode, nthreads=8)
     got, words = ctx.verify(pk, sig, m, off, mode, bitmap=True)
@@ -134,27 +134,38 @@ def test_reference_keygen_vector_on_device(gpu_ctx):
 
 
 @pytest.fixture(scope="module")
-def forced_wide_ctx():
+def forced_wide_ctxs():
     from cometbft_amd import Context
 
     os.environ["CMTV_FORCE_WIDE"] = "1"
     try:
-        return Context(device=0)
+        octx = Context(device=0)
+        os.environ["CMTV_OCT_MAX"] = "0"
+        qctx = Context(device=0)
     finally:
         del os.environ["CMTV_FORCE_WIDE"]
+        os.environ.pop("CMTV_OCT_MAX", None)
+    return {"oct": octx, "quad": qctx}
 
 
+@pytest.fixture(scope="module")
+def forced_wide_ctx(forced_wide_ctxs):
+    return forced_wide_ctxs["quad"]
+
+
+@pytest.mark.parametrize("kernel", ["oct", "quad"])
 @pytest.mark.parametrize("mode,key", [(MODE_GO_STDLIB, "go"), (MODE_ZIP215, "zip215")])
-def test_forced_wide_schedule_on_corpus(forced_wide_ctx, corpus, mode, key):
-    """CMTV_FORCE_WIDE: every quad takes the wide fallback (k1 = k, k2 = 1,
-    64 windows, B digits on windows 0..32): the edge-case corpus and mixed
-    batches stay bit-exact."""
+def test_forced_wide_schedule_on_corpus(forced_wide_ctxs, corpus, mode, key, kernel):
+    """CMTV_FORCE_WIDE: every quad (or oct) takes the wide fallback (k1 = k,
+    k2 = 1, 64 windows, B digits on windows 0..32): the edge-case corpus and
+    mixed batches stay bit-exact."""
+    ctx = forced_wide_ctxs[kernel]
     msg, off = pack_messages(corpus["msgs"])
-    got = forced_wide_ctx.verify(corpus["pk"], corpus["sig"], msg, off, mode)
+    got = ctx.verify(corpus["pk"], corpus["sig"], msg, off, mode)
     assert np.array_equal(got, corpus[key]), np.nonzero(got != corpus[key])[0][:10]
     pk, sig, m, off = _mixed_batch("ed25519", seed=6)
     exp = coracle.verify_batch(pk, sig, m, off, mode, nthreads=8)
-    assert np.array_equal(forced_wide_ctx.verify(pk, sig, m, off, mode), exp)
+    assert np.array_equal(ctx.verify(pk, sig, m, off, mode), exp)
 
 
 def test_forced_wide_schedule_sr25519(forced_wide_ctx):

@@ -1,0 +1,13 @@
+#!/bin/bash
+# GPU tests, then the kernel-time sweep with the oct kernel on and off, then the latency probe
+set -o pipefail
+export TMPDIR=/tmp
+OUT=gpurun_out/iter3
+mkdir -p "$OUT"
+timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > "$OUT/pytest.log" 2>&1
+rc=$?; tail -3 "$OUT/pytest.log"; [ $rc -eq 0 ] || { grep -B5 -A40 "FAIL\|Error" "$OUT/pytest.log" | head -100; exit $rc; }
+timeout -k 10 300 python tools/quad_sweep.py 150 1000 4096 8192 10000 > "$OUT/sweep_oct.log" 2>&1 || { cat "$OUT/sweep_oct.log"; exit 1; }
+grep -v amdgpu.ids "$OUT/sweep_oct.log"
+CMTV_OCT_MAX=0 timeout -k 10 300 python tools/quad_sweep.py 150 1000 4096 8192 > "$OUT/sweep_quad.log" 2>&1 || { cat "$OUT/sweep_quad.log"; exit 1; }
+grep -v amdgpu.ids "$OUT/sweep_quad.log"
+timeout -k 10 200 python3 tools/lat_probe.py 300 2>&1 | grep verify_commit

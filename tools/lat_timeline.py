@@ -3,8 +3,8 @@
 
   python tools/lat_timeline.py <trace_dir> [calls]
 
-A call = the HIP API calls from one hipMemcpyAsync(H2D) to the following
-hipStreamSynchronize's return. Prints, for the median call, every API call,
+A call = the HIP API calls after one hipStreamSynchronize up to the next
+one's return. Prints, for the median call, every API call,
 copy and kernel as offsets (us) from the call's first API entry, and the
 medians of: API time on the host, the first GPU op's start, kernel time,
 and the sync's wake-up after the last GPU op ends."""
@@ -34,20 +34,9 @@ def main():
         gpu.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "C:" + r["Direction"].split("_")[-1] + "_" +
                     r["Direction"].split("_")[-3], int(r["Correlation_Id"])))
     gpu.sort()
-    # calls: from each H2D hipMemcpyAsync to the next hipStreamSynchronize end
-    starts = [i for i, a in enumerate(api) if a[2] == "hipMemcpyAsync"]
-    calls = []
-    i = 0
-    while i < len(api):
-        if api[i][2] == "hipMemcpyAsync":
-            j = i
-            while j < len(api) and api[j][2] != "hipStreamSynchronize":
-                j += 1
-            if j < len(api):
-                calls.append((i, j))
-            i = j + 1
-        else:
-            i += 1
+    # calls: from the API call after one hipStreamSynchronize to the next one's return
+    syncs = [i for i, a in enumerate(api) if a[2] == "hipStreamSynchronize"]
+    calls = [(a + 1, b) for a, b in zip(syncs, syncs[1:]) if b > a + 1]
     calls = calls[-ncalls:]
     stats = []
     for a, b in calls:

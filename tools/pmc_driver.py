@@ -1,0 +1,74 @@
+"""Runs each verify kernel a few times on device-resident synthetic batches,
+for rocprofv3 --pmc passes (tools/gpu_prof.sh): k_verify_oct (150 and 8192
+signatures), k_verify_quad (10k commit), k_verify (100k, lane kernel),
+k_verify_keyed_quad (10k over 150 keys) and k_verify_keyed (1M over 150 keys).
+Every batch is checked (all valid) so a counter pass never profiles a
+broken kernel."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+import torch
+
+from cometbft_amd import Context, pack_messages
+
+REPS = int(os.environ.get("PMC_REPS", "3"))
+dev = torch.device("cuda:0")
+ctx = Context(device=0)
+rng = np.random.default_rng(7)
+NK = 150
+seeds = rng.integers(0, 256, (NK, 32), dtype=np.uint8)
+pks = ctx.pubkeys(seeds)
+
+
+def batch(n):
+    msgs = [rng.integers(0, 256, 116, dtype=np.uint8).tobytes() for _ in range(min(n, 20000))]
+    reps = -(-n // len(msgs))
+    msgs = (msgs * reps)[:n]
+    m, off = pack_messages(msgs)
+    kidx = (np.arange(n) % NK).astype(np.uint32)
+    sig = ctx.sign(seeds, m, off, key_idx=kidx)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    return dict(n=n, kidx=t(kidx), pk=t(pks[kidx]), sig=t(sig), m=t(np.concatenate([m, np.zeros(16, np.uint8)])),
+                off=t(off.view(np.int32)), valid=torch.zeros(n, dtype=torch.uint8, device=dev),
+                bm=torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev))
+
+
+def run(name, c, b, keyed=None):
+    s = torch.cuda.current_stream().cuda_stream
+    for _ in range(REPS):
+        b["valid"].zero_()
+        if keyed is None:
+            c.verify_device(b["n"], b["pk"].data_ptr(), b["sig"].data_ptr(), b["m"].data_ptr(), b["off"].data_ptr(),
+                            0, b["valid"].data_ptr(), b["bm"].data_ptr(), s)
+        else:
+            c.verify_indexed_device(keyed, b["n"], b["kidx"].data_ptr(), b["sig"].data_ptr(), b["m"].data_ptr(),
+                                    b["off"].data_ptr(), 0, b["valid"].data_ptr(), b["bm"].data_ptr(), s)
+    torch.cuda.synchronize()
+    ok = int(b["valid"].sum().item())
+    assert ok == b["n"], (name, ok, b["n"])
+    print(f"{name}: n={b['n']} x{REPS} ok", flush=True)
+
+
+def lane_ctx():
+    os.environ["CMTV_QUAD_MAX"] = "0"
+    os.environ["CMTV_KEYED_QUAD_MAX"] = "0"
+    try:
+        return Context(device=0)
+    finally:
+        del os.environ["CMTV_QUAD_MAX"], os.environ["CMTV_KEYED_QUAD_MAX"]
+
+
+b150, b8k, b10k = batch(150), batch(8192), batch(10000)
+run("oct150", ctx, b150)
+run("oct8192", ctx, b8k)
+run("quad10k", ctx, b10k)
+lctx = lane_ctx()
+b100k = batch(100_000)
+run("lane100k", lctx, b100k)
+ks = ctx.register_keys(pks)
+run("keyed_quad10k", ctx, b10k, keyed=ks)
+lks = lctx.register_keys(pks)
+b1m = batch(1_000_000)
+run("keyed_lane1m", lctx, b1m, keyed=lks)

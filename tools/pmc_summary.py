@@ -18,7 +18,9 @@ def load(d):
     per = defaultdict(lambda: defaultdict(list))
     with open(os.path.join(d, "run_counter_collection.csv")) as f:
         for r in csv.DictReader(f):
-            per[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            name = r["Kernel_Name"].split("(")[0].replace("void ", "")
+            key = f"{name} grid={int(r['Grid_Size']) // 64} waves"
+            per[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
     return per
 
 
@@ -32,7 +34,7 @@ def main():
                 merged[k][c] = sum(vals) / len(vals)
                 disp[k] = max(disp.get(k, 0), len(vals))
     lines = [f"# rocprofv3 --pmc, mean per dispatch; passes: {', '.join(os.path.basename(d) for d in dirs)}"]
-    for k in sorted(merged, key=lambda k: -merged[k].get("SQ_INSTS_VALU", 0)):
+    for k in sorted(merged, key=lambda k: -merged[k].get("SQ_INSTS_VALU", 0) * max(disp[k], 1)):
         cs = merged[k]
         lines.append(f"\n[{k}]  dispatches={disp[k]}")
         for c in sorted(cs):
@@ -47,6 +49,11 @@ def main():
                 lines.append(f"  -> VALU-active share of wave {cs['SQ_ACTIVE_INST_VALU'] / cs['SQ_WAVE_CYCLES']:12.3f}")
             if "SQ_WAIT_ANY" in cs:
                 lines.append(f"  -> waiting share of wave     {cs['SQ_WAIT_ANY'] / cs['SQ_WAVE_CYCLES']:12.3f}")
+        if "SQ_ACTIVE_INST_VALU" in cs and cs.get("GRBM_GUI_ACTIVE"):
+            # VALUBusy (chip-wide): active VALU quad-cycles x 4 over SIMDs x
+            # per-XCD GPU-busy cycles (GRBM_GUI_ACTIVE sums the 8 XCDs)
+            busy = 100 * cs["SQ_ACTIVE_INST_VALU"] * 4 / 1024 / (cs["GRBM_GUI_ACTIVE"] / 8)
+            lines.append(f"  -> VALUBusy (chip, %)        {busy:12.1f}")
     with open(out, "w") as f:
         f.write("\n".join(lines) + "\n")
     print("\n".join(lines[:60]))

@@ -114,6 +114,22 @@ def _sockets():
         return None
 
 
+def _cpu_share():
+    """CPUs this process may actually use: the affinity mask and the cgroup
+    v2 quota (cpu.max; the GPU box gives one GPU's job a 16-CPU share while
+    nproc shows the whole machine)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+            if q != "max":
+                quota = round(int(q) / int(p), 2)
+    except (OSError, ValueError):
+        pass
+    return {"affinity_cpus": aff, "cgroup_quota_cpus": quota}
+
+
 def _oracle_rate(fn, n, threads, cpu_seconds):
     t = time.perf_counter()
     fn(threads)
@@ -161,7 +177,7 @@ def cpu_baseline(pk, sig, m, off, mode, cpu_seconds):
             "seconds": round(dt, 2), "single_core_verifs_per_s": round(one, 1),
             "all_cores": {"value": round(vall, 1), "threads": nproc, "passes": reps_all, "seconds": round(dt_all, 2),
                           "sample": f"the commit tiled x{tile} ({n * tile} signatures per pass)"},
-            "host_cpu": _cpu_model(), "nproc": nproc, "sockets": _sockets()}
+            "host_cpu": _cpu_model(), "nproc": nproc, "sockets": _sockets(), **_cpu_share()}
 
 
 class Devices:

@@ -461,6 +461,28 @@ CMTV_HD void hs_digits16(uint32_t t[8], const uint32_t x[8], int W) {
   }
 }
 
+// Signed radix-2^16 digit streams of u < L (< 2^253): t = u + 0x8000 in every
+// 16-bit field (the top field stays below 2^16), tLo yields digits 7..0
+// (bits 0..127) and tHi digits 15..8, each read from the top with
+// sc_shift_out(t, 16); digit = out - 0x8000, in [-2^15, 2^15).
+CMTV_HD void hs_digits65536(uint32_t tLo[8], uint32_t tHi[8], const uint32_t u[8]) {
+  uint32_t t[8];
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint64_t v = (uint64_t)u[i] + 0x80008000u + c;
+    t[i] = (uint32_t)v;
+    c = v >> 32;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    tLo[i] = 0;
+    tLo[4 + i] = t[i];
+    tHi[i] = 0;
+    tHi[4 + i] = t[4 + i];
+  }
+}
+
 // Signed radix-256 digit streams of u < L split at 2^128, each read from the
 // top with sc_shift_out(t, 8): tLo yields digits 16..0 of u mod 2^128
 // (17 digits), tHi digits 15..0 of u >> 128 (< 2^125, 16 digits).

@@ -5,7 +5,9 @@
 
 namespace cmtv {
 
-constexpr uint32_t kBtabWords = 3 * 128 * 36;  // (1..128)B, [2^124]B, [2^128]B multiples; 36 words per row
+// (1..128)B, [2^124]B, [2^128]B multiples, then (1..2^15)B, [2^120]B, [2^128]B
+// multiples (verify_core.h BT16_*); 36 words per row, 14.2 MB
+constexpr uint32_t kBtabWords = (3 * 128 + 3 * 32768) * 36;
 constexpr uint32_t kAtabWordsPerLane = 320; // (1..8)(-A), 40 words per point
 constexpr uint32_t kCombWords = 32 * 128 * 32;     // one registered-key comb (keyed.h), 512 KiB
 constexpr uint32_t kCombScratchWordsPerKey = 128 * 320;  // prefix products while building

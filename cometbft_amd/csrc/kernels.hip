@@ -56,12 +56,18 @@ __device__ __forceinline__ void load_words(uint32_t* w, const uint32_t* __restri
   }
 }
 
-// rows 0..127: (1..128)B; 128..255: (1..128)[2^124]B; 256..383: (1..128)[2^128]B
+// rows 0..127: (1..128)B; 128..255: (1..128)[2^124]B; 256..383: (1..128)[2^128]B;
+// then the radix-2^16 blocks (1..2^15)B, (1..2^15)[2^120]B, (1..2^15)[2^128]B
 __global__ __launch_bounds__(64) void k_btab_init(uint32_t* __restrict__ rows) {
   const int e = blockIdx.x * 64 + threadIdx.x;
-  if (e >= 3 * BTAB_ENTRIES) return;
+  if (e >= BT16_BASE + BT16_ROWS) return;
   uint32_t row[BTAB_ROW_WORDS];
-  btab_entry(row, (e % BTAB_ENTRIES) + 1, e / BTAB_ENTRIES);
+  if (e < BT16_BASE) {
+    btab_entry(row, (e % BTAB_ENTRIES) + 1, e / BTAB_ENTRIES);
+  } else {
+    const int f = e - BT16_BASE;
+    btab_entry_shift(row, (f % BT16_ENTRIES) + 1, bt16_block_shift(f / BT16_ENTRIES), 16);
+  }
 #pragma unroll
   for (int i = 0; i < BTAB_ROW_WORDS; i++) rows[e * BTAB_ROW_WORDS + i] = row[i];
 }
@@ -291,7 +297,7 @@ __global__ __launch_bounds__(64) void k_sign(uint32_t n, const uint32_t* __restr
 static inline unsigned blocks_for(uint32_t n) { return (n + 63) / 64; }
 
 hipError_t launch_btab_init(uint32_t* d_rows, hipStream_t s) {
-  hipLaunchKernelGGL(k_btab_init, dim3(blocks_for(3 * BTAB_ENTRIES)), dim3(64), 0, s, d_rows);
+  hipLaunchKernelGGL(k_btab_init, dim3(blocks_for(BT16_BASE + BT16_ROWS)), dim3(64), 0, s, d_rows);
   return hipGetLastError();
 }
 

@@ -9,10 +9,11 @@
 // The oct splits it into two chains of the same length, one per quad:
 //   lower quad (lanes 0-3):  P_lo = [k1](-A)           + [u mod 2^128]B
 //   upper quad (lanes 4-7):  P_hi = [|k2|](+/-R)       + [u >> 128][2^128]B
-// with the radix-256 B digits of both on the even windows 0..32 (table
-// blocks 0 and 2 of the device B table), so a window is 4 doublings + 1
-// table addition (+ 1 B addition on even windows): ~2/3 of the quad's
-// window work per lane, and each quad builds only its own (0..8)P table.
+// with the radix-2^16 B digits of both on windows 0, 4, .., 28 (the
+// (1..2^15)B and (1..2^15)[2^128]B tables, verify_core.h), so a window is 4
+// doublings + 1 table addition (+ 1 B addition every 4th window): ~2/3 of
+// the quad's window work per lane, and each quad builds only its own
+// (0..8)P table.
 // Decoding, hashing and the half-scalar split are per-lane work that both
 // quads repeat (the lower quad decodes A, the upper quad R), so the total
 // lane-work per signature grows; the oct wins on latency (fewer
@@ -28,30 +29,6 @@
 #include "quad.h"
 
 namespace cmtv {
-
-// B-table blocks (verify_core.h btab_entry): 0 = (1..128)B,
-// 1 = (1..128)[2^124]B (quad odd windows), 2 = (1..128)[2^128]B (oct upper quad)
-constexpr int BTAB_BLOCK_HI128 = 2;
-
-// Signed radix-256 digit stream of a 128-bit half w[0..3], read from the top
-// with sc_shift_out(t, 8): 17 digits (the top one is the carry, 0 for the
-// upper half of u < L).
-CMTV_HD void hs_digits256_half(uint32_t t[8], const uint32_t w[4]) {
-  uint32_t lo[5];
-  uint64_t c = 0;
-#pragma unroll
-  for (int i = 0; i < 5; i++) {
-    const uint64_t v = (uint64_t)(i < 4 ? w[i] : 0u) + (i < 4 ? 0x80808080u : 0x80u) + c;
-    lo[i] = (uint32_t)v;
-    c = v >> 32;
-  }
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    const uint32_t hi = (i >= 3 && i - 3 < 5) ? lo[i - 3] : 0u;
-    const uint32_t lw = (i >= 4 && i - 4 < 5) ? lo[i - 4] : 0u;
-    t[i] = (hi << 24) | (lw >> 8);
-  }
-}
 
 template <uint32_t MODE, class Q, class BTab, class ATab>
 CMTV_HD bool o_verify(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig_ptr, const uint8_t* msg,
@@ -116,15 +93,15 @@ CMTV_HD bool o_verify(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig_pt
   // ---- Straus over W windows: own 4-bit digits, B digits on even windows
   uint32_t tS[8], tB[8];
   {
-    uint32_t sc[8], half[4];
+    uint32_t sc[8], tHi[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) sc[i] = up ? hs.k2[i] : hs.k1[i];
     hs_digits16(tS, sc, W);
+    hs_digits65536(tB, tHi, u);
 #pragma unroll
-    for (int i = 0; i < 4; i++) half[i] = up ? u[4 + i] : u[i];
-    hs_digits256_half(tB, half);
+    for (int i = 0; i < 8; i++) tB[i] = up ? tHi[i] : tB[i];
   }
-  const int bblock = up ? BTAB_BLOCK_HI128 * BTAB_ENTRIES : 0;
+  const int bblock = BT16_BASE + (up ? 2 * BT16_ENTRIES : 0);
   q_identity(v, lane);
 #pragma unroll 1
   for (int win = W - 1; win >= 0; win--) {
@@ -133,10 +110,10 @@ CMTV_HD bool o_verify(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig_pt
       const int d = (int)sc_shift_out(tS, 4) - 8;
       tab.load_signed(q, d < 0 ? -d : d, d < 0, cS);
     }
-    const bool has_b = win <= 32 && (win & 1) == 0;
+    const bool has_b = (win & 3) == 0 && win <= 28;
     bool b_neg = false, b_ident = false;
     if (has_b) {
-      const int dB = (int)sc_shift_out(tB, 8) - 128;
+      const int dB = (int)sc_shift_out(tB, 16) - 0x8000;
       const int ib = dB < 0 ? -dB : dB;
       const int row = (ib > 0 ? ib - 1 : 0) + bblock;
       q_niels_load(

@@ -306,11 +306,13 @@ CMTV_HD void q_straus_half(const Q& q, fe& v, fe& rc, const uint32_t k[8], const
   q_build_table(q, tabA, v);
   q_build_table(q, tabR, rc);
 
-  // ---- phase 4: Straus over W shared 4-bit windows
+  // ---- phase 4: Straus over W shared 4-bit windows; the fixed-base scalar
+  //      u in signed radix-2^16 digits: digit j on window 4j against
+  //      (1..2^15)B, digit 8+j on window 4j+2 against (1..2^15)[2^120]B
   uint32_t tA[8], tR[8], tLo[8], tHi[8];
   hs_digits16(tA, hs.k1, W);
   hs_digits16(tR, hs.k2, W);
-  hs_digits256(tLo, tHi, u);
+  hs_digits65536(tLo, tHi, u);
   q_identity(v, lane);
 #pragma unroll 1
   for (int win = W - 1; win >= 0; win--) {
@@ -323,19 +325,17 @@ CMTV_HD void q_straus_half(const Q& q, fe& v, fe& rc, const uint32_t k[8], const
       const int dR = (int)sc_shift_out(tR, 4) - 8;
       tabR.load_signed(q, dR < 0 ? -dR : dR, dR < 0, cR);
     }
-    const bool has_b = win <= 32 && ((win & 1) == 0 || win <= 31);
+    const bool has_b = (win & 1) == 0 && win <= 30;
     bool b_neg = false, b_ident = false;
     if (has_b) {
-      // even windows: digit win/2 of u mod 2^128 against (1..128)B;
-      // odd windows: digit (win-1)/2 of u >> 128 against (1..128)[2^124]B
-      const bool odd = win & 1;
+      const bool hi = (win & 2) != 0;
       int dB;
-      if (odd)
-        dB = (int)sc_shift_out(tHi, 8) - 128;
+      if (hi)
+        dB = (int)sc_shift_out(tHi, 16) - 0x8000;
       else
-        dB = (int)sc_shift_out(tLo, 8) - 128;
+        dB = (int)sc_shift_out(tLo, 16) - 0x8000;
       const int ib = dB < 0 ? -dB : dB;
-      const int row = (ib > 0 ? ib - 1 : 0) + (odd ? BTAB_ENTRIES : 0);
+      const int row = BT16_BASE + (ib > 0 ? ib - 1 : 0) + (hi ? BT16_ENTRIES : 0);
       // raw row only: the select / negation waits until after the doublings
       q_niels_load(
           q, cB, [&](int off, fe& r) { btab.load_coord(row, off, r); }, BTAB_COORD_WORDS, 2 * BTAB_COORD_WORDS,

@@ -68,12 +68,26 @@ CMTV_HD void cached_neg_point(ge_p3& r, const ge_p3& p) {
 // verifier's odd windows, halfscalar.h), block 2 = [m 2^128]B (the oct
 // verifier's upper quad, oct.h).
 CMTV_HD int btab_block_shift(int block) { return block == 0 ? 0 : (block == 1 ? 124 : 128); }
+
+// Radix-2^16 fixed-base tables of the quad and oct verifiers (quad.h, oct.h),
+// after the three radix-256 blocks: block b = rows (1..2^15)[2^shift]B with
+// shift 0 (u's digits 0..7), 120 (quad: digits 8..15 on windows 4j+2) and
+// 128 (oct upper quad: digits 8..15 on windows 4j).
+constexpr int BT16_ENTRIES = 32768;
+constexpr int BT16_BASE = 3 * BTAB_ENTRIES;
+constexpr int BT16_ROWS = 3 * BT16_ENTRIES;
+CMTV_HD int bt16_block_shift(int block) { return block == 0 ? 0 : (block == 1 ? 120 : 128); }
+
+// [m][2^shift]B, m < 2^bits, in affine niels form
+CMTV_HD void btab_entry_shift(uint32_t row[BTAB_ROW_WORDS], int m, int shift, int bits);
 CMTV_HD void btab_entry(uint32_t row[BTAB_ROW_WORDS], int m, int block = 0) {
+  btab_entry_shift(row, m, btab_block_shift(block), 8);
+}
+CMTV_HD void btab_entry_shift(uint32_t row[BTAB_ROW_WORDS], int m, int shift, int bits) {
   uint32_t bw[8];
   basepoint_words(bw);
   ge_p3 B, acc;
   p3_frombytes(B, bw);
-  const int shift = btab_block_shift(block);
   if (shift) {
     ge_efgh t;
     ge_p2 q;
@@ -90,7 +104,7 @@ CMTV_HD void btab_entry(uint32_t row[BTAB_ROW_WORDS], int m, int block = 0) {
   p3_identity(acc);
   ge_efgh t;
   ge_p2 q;
-  for (int bit = 7; bit >= 0; bit--) {
+  for (int bit = bits - 1; bit >= 0; bit--) {
     p3_to_p2(q, acc);
     p2_dbl(t, q);
     efgh_to_p3(acc, t);

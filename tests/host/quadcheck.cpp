@@ -9,9 +9,11 @@
 #include <cstring>
 #include <thread>
 #include <vector>
+#include "../../cometbft_amd/csrc/oct.h"
 #include "../../cometbft_amd/csrc/quad.h"
 #include "../../cometbft_amd/csrc/sr25519_quad.h"
 #include "../../cometbft_amd/csrc/keyed_quad.h"
+#include "lazy_btab.h"
 #include <map>
 #include <string>
 
@@ -20,11 +22,12 @@ using namespace cmtv;
 // sense-reversing spin barrier for the 4 lane threads (a futex barrier makes
 // the ~10^5 exchanges per signature dominate the run time)
 struct SpinBarrier {
+  int n = 4;
   std::atomic<int> count{0};
   std::atomic<int> gen{0};
   void arrive_and_wait() {
     const int g = gen.load(std::memory_order_acquire);
-    if (count.fetch_add(1, std::memory_order_acq_rel) == 3) {
+    if (count.fetch_add(1, std::memory_order_acq_rel) == n - 1) {
       count.store(0, std::memory_order_relaxed);
       gen.store(g + 1, std::memory_order_release);
       return;
@@ -36,7 +39,7 @@ struct SpinBarrier {
 
 struct Exchange {
   SpinBarrier bar;
-  fe slot[4];
+  fe slot[8];
 };
 
 struct HostQuad {
@@ -62,16 +65,48 @@ struct HostQuad {
   bool any(bool x) const { return x; }  // the four lanes of one quad agree
 };
 
-struct HostBTab {
-  std::vector<uint32_t> rows;
-  HostBTab() : rows(2 * BTAB_ENTRIES * BTAB_ROW_WORDS) {
-    for (int e = 0; e < 2 * BTAB_ENTRIES; e++) btab_entry(&rows[e * BTAB_ROW_WORDS], e % BTAB_ENTRIES + 1, e >= BTAB_ENTRIES);
+// the oct policy (oct.h): 8 threads, quad_perm inside each half, and the
+// upper quad's words reaching the lower one (DPP row_shl:4)
+struct HostOct {
+  int ln;
+  Exchange* ex;
+  int lane() const { return ln & 3; }
+  bool upper() const { return (ln & 4) != 0; }
+  template <int PAT>
+  void perm(fe& o, const fe& v) const {
+    ex->slot[ln] = v;
+    ex->bar.arrive_and_wait();
+    const fe r = ex->slot[(ln & 4) + ((PAT >> (2 * (ln & 3))) & 3)];
+    ex->bar.arrive_and_wait();
+    o = r;
   }
-  void load_coord(int e, int off, fe& r) const {
-    const uint32_t* p = &rows[e * BTAB_ROW_WORDS + off];
-    for (int i = 0; i < 10; i++) r.v[i] = p[i];
+  template <int PAT>
+  uint32_t perm32(uint32_t x) const {
+    fe t, o;
+    fe_0(t);
+    t.v[0] = x;
+    perm<PAT>(o, t);
+    return o.v[0];
   }
+  void from_upper(fe& o, const fe& v) const {
+    ex->slot[ln] = v;
+    ex->bar.arrive_and_wait();
+    const fe r = ex->slot[ln < 4 ? ln + 4 : ln];
+    ex->bar.arrive_and_wait();
+    o = r;
+  }
+  uint32_t from_upper32(uint32_t x) const {
+    fe t, o;
+    fe_0(t);
+    t.v[0] = x;
+    from_upper(o, t);
+    return o.v[0];
+  }
+  // W is the max over the signature's lanes: both quads compute the same pair
+  bool any(bool x) const { return x; }
 };
+
+using HostBTab = LazyBTab;  // lazy_btab.h: rows computed on first use
 
 struct HostScratch {
   fe q[COMB_WINDOWS];
@@ -101,6 +136,8 @@ int main(int argc, char** argv) {
   const bool sr = argc > 1 && !strcmp(argv[1], "sr");
   // argv[1] == "keyed": Ed25519 records, verified through registered-key combs (keyed_quad.h)
   const bool keyed = argc > 1 && !strcmp(argv[1], "keyed");
+  // argv[1] == "oct": Ed25519 records through the 8-lane verifier (oct.h)
+  const bool oct = argc > 1 && !strcmp(argv[1], "oct");
   std::vector<uint32_t> bcomb;
   std::map<std::string, std::pair<bool, std::vector<uint32_t>>> combs;
   if (keyed) {
@@ -139,9 +176,19 @@ int main(int argc, char** argv) {
       kt = it->second.second.data();
     }
     Exchange ex;
-    bool res[4];
+    bool res[8];
     std::vector<std::thread> th;
-    for (int l = 0; l < 4; l++)
+    if (oct) {
+      ex.bar.n = 8;
+      for (int l = 0; l < 8; l++)
+        th.emplace_back([&, l] {
+          HostOct q{l, &ex};
+          QArrayTab ta;
+          res[l] = mode ? o_verify<MODE_ZIP215>(q, pkw, sigw, mp, mlen, bt, ta)
+                        : o_verify<MODE_GO_STDLIB>(q, pkw, sigw, mp, mlen, bt, ta);
+        });
+    }
+    for (int l = 0; l < (oct ? 0 : 4); l++)
       th.emplace_back([&, l] {
         HostQuad q{l, &ex};
         QArrayTab ta, tr;

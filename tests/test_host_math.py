@@ -85,6 +85,17 @@ def test_keyed_pipeline_matches_corpus(hostcheck, corpus, mode):
 
 
 @pytest.mark.parametrize("mode", [0, 1])
+def test_oct_pipeline_matches_corpus(quadcheck, corpus, mode):
+    """The 8-lane oct kernel's source (oct.h): eight host threads in lockstep,
+    the two quads' Straus chains merged by the row-shift exchange."""
+    idx = _keyed_subset(corpus)[1::6]
+    got = _run(quadcheck, "oct", corpus, idx, mode)
+    want = (corpus["go"] if mode == 0 else corpus["zip215"])[idx]
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(idx[int(i)], corpus["cats"][idx[int(i)]]) for i in bad[:10]]
+
+
+@pytest.mark.parametrize("mode", [0, 1])
 def test_quad_pipeline_matches_corpus(quadcheck, corpus, mode):
     """The 4-lane quad kernel's source (quad.h), four host threads in lockstep
     standing in for the DPP quad_perm exchanges (every adversarial vector and

@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "../../cometbft_amd/csrc/quad.h"
+#include "../../tests/host/lazy_btab.h"
 
 using namespace cmtv;
 
@@ -98,9 +99,15 @@ __global__ __launch_bounds__(64, 1) void k_time(const uint32_t* pk, const uint32
   if (threadIdx.x == 0) ts[14] = __builtin_amdgcn_s_memtime();
 }
 
-__global__ void k_btab(uint32_t* rows) {
-  int m = threadIdx.x + 1;
-  if (m <= BTAB_ENTRIES) btab_entry(rows + (m - 1) * BTAB_ROW_WORDS, m);
+__global__ void k_btab(uint32_t* rows) {  // the library's k_btab_init
+  const int e = blockIdx.x * 64 + threadIdx.x;
+  if (e >= BT16_BASE + BT16_ROWS) return;
+  if (e < BT16_BASE) {
+    btab_entry(rows + e * BTAB_ROW_WORDS, e % BTAB_ENTRIES + 1, e / BTAB_ENTRIES);
+  } else {
+    const int f = e - BT16_BASE;
+    btab_entry_shift(rows + e * BTAB_ROW_WORDS, f % BT16_ENTRIES + 1, bt16_block_shift(f / BT16_ENTRIES), 16);
+  }
 }
 
 template <int VAR>
@@ -145,12 +152,7 @@ struct HostQuad {
   }
   bool any(bool x) const { return x; }
 };
-struct HostBTabQ {
-  const uint32_t* rows;
-  void load_coord(int e, int off, fe& r) const {
-    for (int i = 0; i < 10; i++) r.v[i] = rows[e * BTAB_ROW_WORDS + off + i];
-  }
-};
+using HostBTabQ = LazyBTab;
 struct HostProbe {
   uint32_t* out;
   int ln;
@@ -189,8 +191,9 @@ int main() {
   uint8_t msg[4] = {0x72, 0, 0, 0};
   uint32_t mlen = 1;
 
-  std::vector<uint32_t> btab(2 * BTAB_ENTRIES * BTAB_ROW_WORDS);
-  for (int e = 0; e < 2 * BTAB_ENTRIES; e++) btab_entry(&btab[e * BTAB_ROW_WORDS], e % BTAB_ENTRIES + 1, e >= BTAB_ENTRIES);
+  std::vector<uint32_t> btab(BT16_BASE * BTAB_ROW_WORDS);  // the radix-256 blocks, for the device check
+  for (int e = 0; e < BT16_BASE; e++) btab_entry(&btab[e * BTAB_ROW_WORDS], e % BTAB_ENTRIES + 1, e / BTAB_ENTRIES);
+  LazyBTab hbt;
 
   // host emulation
   std::vector<uint32_t> hs(NSNAP * 40, 0);
@@ -201,7 +204,7 @@ int main() {
     for (int l = 0; l < 4; l++)
       th.emplace_back([&, l] {
         HostQuad q{l, &ex};
-        HostBTabQ bt{btab.data()};
+        const HostBTabQ& bt = hbt;
         HostProbe pr{hs.data(), l};
         QArrayTab at, at2;
         hres[l] = q_verify<MODE_GO_STDLIB>(q, pk, sig, msg, mlen, bt, at, at2, pr);
@@ -215,14 +218,14 @@ int main() {
   (void)hipMalloc(&dpk, 32);
   (void)hipMalloc(&dsig, 64);
   (void)hipMalloc(&dmsg, 16);
-  (void)hipMalloc(&dbt, btab.size() * 4);
+  (void)hipMalloc(&dbt, (size_t)(BT16_BASE + BT16_ROWS) * BTAB_ROW_WORDS * 4);
   (void)hipMalloc(&dsn, NSNAP * 40 * 4);
   (void)hipMalloc(&dv, 64 * 4);
   (void)hipMemcpy(dpk, pk, 32, hipMemcpyHostToDevice);
   (void)hipMemcpy(dsig, sig, 64, hipMemcpyHostToDevice);
   (void)hipMemcpy(dmsg, msg, 4, hipMemcpyHostToDevice);
   // device-built table must equal the host-built one
-  hipLaunchKernelGGL(k_btab, dim3(1), dim3(256), 0, 0, dbt);
+  hipLaunchKernelGGL(k_btab, dim3((BT16_BASE + BT16_ROWS + 63) / 64), dim3(64), 0, 0, dbt);
   std::vector<uint32_t> dbtab(btab.size());
   (void)hipMemcpy(dbtab.data(), dbt, btab.size() * 4, hipMemcpyDeviceToHost);
   printf("btab device==host: %d\n", (int)(dbtab == btab));

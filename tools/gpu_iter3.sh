@@ -11,3 +11,5 @@ grep -v amdgpu.ids "$OUT/sweep_oct.log"
 CMTV_OCT_MAX=0 timeout -k 10 300 python tools/quad_sweep.py 150 1000 4096 8192 > "$OUT/sweep_quad.log" 2>&1 || { cat "$OUT/sweep_quad.log"; exit 1; }
 grep -v amdgpu.ids "$OUT/sweep_quad.log"
 timeout -k 10 200 python3 tools/lat_probe.py 300 2>&1 | grep verify_commit
+CMTV_OCT_MAX=20000 timeout -k 10 120 python tools/quad_sweep.py 10000 2>&1 | grep -v amdgpu.ids | sed 's/^/oct@10k: /'
+timeout -k 10 120 ./tools/dbg/quad_debug > "$OUT/phases.log" 2>&1; grep "^cycles" "$OUT/phases.log"

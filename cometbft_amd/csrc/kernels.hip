@@ -160,6 +160,63 @@ __global__ __launch_bounds__(64, CMTV_QUAD_WAVES_PER_EU) void k_verify_oct(uint3
   if (threadIdx.x == 0 && out_bitmap) reinterpret_cast<uint8_t*>(out_bitmap)[gid >> 6] = (uint8_t)x;
 }
 
+// The oct verifier over two waves per 8 signatures: wave 1 hashes and splits
+// the scalars (o_prepare) while wave 0 decompresses A and R; the scalars
+// reach wave 0 through LDS at one barrier, and wave 1 exits. For batches up
+// to 4,096 signatures (1,024 waves), where SIMDs are idle anyway, this takes
+// the hash and the half-scalar Euclid (~11% of a wave) off the chain.
+template <uint32_t MODE>
+__global__ __launch_bounds__(128, CMTV_QUAD_WAVES_PER_EU) void k_verify_oct_split(
+    uint32_t n, const uint32_t* __restrict__ pk, const uint32_t* __restrict__ sig, const uint8_t* __restrict__ msg,
+    const uint32_t* __restrict__ off, const uint32_t* __restrict__ btab, uint8_t* __restrict__ out_valid,
+    uint64_t* __restrict__ out_bitmap, uint32_t force_wide) {
+  const uint32_t t = threadIdx.x & 63;
+  const uint32_t gid = blockIdx.x * 64 + t;
+  const uint32_t s = gid >> 3;
+  const bool active = s < n;
+  const uint32_t i = active ? s : n - 1;
+  __shared__ uint32_t prep[8][26];
+  __shared__ uint2 tab_lds[9 * 5 * 64];
+  if (threadIdx.x >= 64) {
+    const uint32_t m0 = off[i], m1 = off[i + 1];
+    OctPrep p;
+    o_prepare(p, pk + 8 * (size_t)i, sig + 16 * (size_t)i, msg + m0, m1 - m0, force_wide != 0);
+    if ((t & 7) == 0) {
+      uint32_t* d = prep[t >> 3];
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        d[j] = p.k1[j];
+        d[8 + j] = p.k2[j];
+        d[16 + j] = p.u[j];
+      }
+      d[24] = p.flags;
+    }
+    __syncthreads();
+    return;
+  }
+  DevOct q;
+  DevBTabQ bt{btab};
+  DevATabQ ta{tab_lds, t};
+  bool v = o_verify_split<MODE>(q, pk + 8 * (size_t)i, sig + 16 * (size_t)i, bt, ta, [&](OctPrep& p) {
+    __syncthreads();
+    const uint32_t* d = prep[t >> 3];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      p.k1[j] = d[j];
+      p.k2[j] = d[8 + j];
+      p.u[j] = d[16 + j];
+    }
+    p.flags = d[24];
+  });
+  v = v && active;
+  if (active && (t & 7) == 0 && out_valid) out_valid[s] = v ? 1 : 0;
+  uint64_t x = __ballot(v && (t & 7) == 0) & 0x0101010101010101ull;
+  x = (x | (x >> 7)) & 0x0003000300030003ull;
+  x = (x | (x >> 14)) & 0x0000000F0000000Full;
+  x = (x | (x >> 28)) & 0xFFull;
+  if (t == 0 && out_bitmap) reinterpret_cast<uint8_t*>(out_bitmap)[gid >> 6] = (uint8_t)x;
+}
+
 // Prefix products of comb_build_column, word-major / lane-minor per launch.
 struct DevCombScratch {
   uint32_t* __restrict__ base;
@@ -313,6 +370,16 @@ hipError_t launch_verify(uint32_t mode, uint32_t n, const void* pk, const void* 
   auto op = static_cast<const uint32_t*>(off);
   auto vp = static_cast<uint8_t*>(valid);
   auto bp = static_cast<uint64_t*>(bitmap);
+  if (quad && (kflags & kLaunchOctSplit)) {
+    // one 128-lane block (2 waves) = 8 signatures; whole groups of 8 blocks
+    const dim3 grid(((n + 63) / 64) * 8), block(128);
+    if (mode == MODE_ZIP215)
+      hipLaunchKernelGGL(k_verify_oct_split<MODE_ZIP215>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp, fw);
+    else
+      hipLaunchKernelGGL(k_verify_oct_split<MODE_GO_STDLIB>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp,
+                         fw);
+    return hipGetLastError();
+  }
   if (quad && (kflags & kLaunchOct)) {
     // one 64-lane block = 8 signatures; whole groups of 8 blocks so every
     // byte of every bitmap word is written

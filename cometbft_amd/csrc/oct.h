@@ -30,11 +30,17 @@
 
 namespace cmtv {
 
-template <uint32_t MODE, class Q, class BTab, class ATab>
-CMTV_HD bool o_verify(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig_ptr, const uint8_t* msg,
-                      uint32_t mlen, const BTab& btab, ATab& tab, bool force_wide = false) {
-  const int lane = q.lane();
-  const bool up = q.upper();
+// Per-signature scalar work that does not depend on the decoded points:
+// the s check, k = SHA-512(R || A || M) mod L, the half-size pair and the
+// fixed-base scalar u = k2 s mod L. The split kernel (kernels.hip
+// k_verify_oct_split) runs it on a second wave while the first decodes.
+struct OctPrep {
+  uint32_t k1[8], k2[8], u[8];
+  uint32_t flags;  // bit 0: k2 < 0, bit 1: wide, bit 2: s canonical, bits 8..15: window count
+};
+
+CMTV_HD void o_prepare(OctPrep& p, const uint32_t* pk_ptr, const uint32_t* sig_ptr, const uint8_t* msg,
+                       uint32_t mlen, bool force_wide) {
   uint32_t w[16];
 #pragma unroll
   for (int i = 0; i < 8; i++) w[i] = sig_ptr[8 + i];
@@ -42,6 +48,36 @@ CMTV_HD bool o_verify(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig_pt
   uint32_t ts[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) ts[i] = w[i];
+  uint32_t k[8];
+  {
+    uint32_t h[16];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      w[i] = sig_ptr[i];
+      w[8 + i] = pk_ptr[i];
+    }
+    sha512_prefixed<16>(h, w, msg, mlen);
+    sc_reduce512(k, h);
+  }
+  HalfScalars hs;
+  half_scalars(hs, k, force_wide);
+  hs_bscalar(p.u, hs.k2, hs.k2_neg, ts);
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    p.k1[i] = hs.k1[i];
+    p.k2[i] = hs.k2[i];
+  }
+  p.flags = (hs.k2_neg ? 1u : 0u) | (hs.wide ? 2u : 0u) | (s_ok ? 4u : 0u) | ((uint32_t)hs.windows << 8);
+}
+
+// The oct verifier with the scalar work supplied by get_prep(OctPrep&), which
+// is called after the decompression (every lane of the wave calls it once).
+template <uint32_t MODE, class Q, class BTab, class ATab, class GetPrep>
+CMTV_HD bool o_verify_split(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig_ptr, const BTab& btab, ATab& tab,
+                            const GetPrep& get_prep) {
+  const int lane = q.lane();
+  const bool up = q.upper();
+  uint32_t w[8];
 
   // ---- decode: A on the lower quad, R on the upper one
   const uint32_t* src = up ? sig_ptr : pk_ptr;
@@ -57,35 +93,24 @@ CMTV_HD bool o_verify(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig_pt
     fe_1(one);
     fe_pick(v, lane, P.X, P.Y, one, P.T);
   }
-  uint32_t k[8];
-  {
-    uint32_t h[16];
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      w[i] = sig_ptr[i];
-      w[8 + i] = pk_ptr[i];
-    }
-    sha512_prefixed<16>(h, w, msg, mlen);
-    sc_reduce512(k, h);
-  }
 
   // ---- half-size scalars (halfscalar.h), u = k2 s mod L; W uniform per wave
-  HalfScalars hs;
-  half_scalars(hs, k, force_wide);
-  uint32_t u[8];
-  hs_bscalar(u, hs.k2, hs.k2_neg, ts);
-  const bool wide = q.any(hs.wide);
+  OctPrep hs;
+  get_prep(hs);
+  const bool k2_neg = hs.flags & 1u, s_ok = (hs.flags & 4u) != 0;
+  const bool wide = q.any((hs.flags & 2u) != 0);
   int W = HS_WINDOWS;
 #pragma unroll 1
-  for (int x = HS_WINDOWS; x < HS_MAX_WINDOWS; x++) W += q.any(hs.windows > x) ? 1 : 0;
+  for (int x = HS_WINDOWS; x < HS_MAX_WINDOWS; x++) W += q.any((int)(hs.flags >> 8) > x) ? 1 : 0;
   W = wide ? HS_WIDE_WINDOWS : W;
+  const uint32_t* u = hs.u;
 
   // ---- this quad's point: -A (lower), k2 < 0 ? R : -R (upper); its table
   {
     fe t;
     fe_neg(t, v);
     fe_carry(t);
-    const bool neg = up ? !hs.k2_neg : true;
+    const bool neg = up ? !k2_neg : true;
     fe_select(v, v, t, neg && (lane == 0 || lane == 3));
   }
   q_build_table(q, tab, v);
@@ -157,6 +182,14 @@ CMTV_HD bool o_verify(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig_pt
   const bool e1 = q.template perm32<QP_B1>(yz ? 1u : 0u) != 0;
   if (MODE == MODE_GO_STDLIB) return s_ok && a_ok && r_ok && r_canon && e0 && e1;
   return s_ok && a_ok && r_ok && e0 && e1;
+}
+
+// One wave does everything (k_verify_oct; the host check)
+template <uint32_t MODE, class Q, class BTab, class ATab>
+CMTV_HD bool o_verify(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig_ptr, const uint8_t* msg,
+                      uint32_t mlen, const BTab& btab, ATab& tab, bool force_wide = false) {
+  return o_verify_split<MODE>(q, pk_ptr, sig_ptr, btab, tab,
+                              [&](OctPrep& p) { o_prepare(p, pk_ptr, sig_ptr, msg, mlen, force_wide); });
 }
 
 }  // namespace cmtv

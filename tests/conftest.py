@@ -82,3 +82,24 @@ def gpu_ctx_quad():
             del os.environ["CMTV_OCT_MAX"]
         else:
             os.environ["CMTV_OCT_MAX"] = old
+
+
+@pytest.fixture(scope="session")
+def gpu_ctx_oct1():
+    """A context whose small Ed25519 batches take the one-wave oct kernel
+    (CMTV_OCT_SPLIT_MAX=0) instead of the default two-wave form."""
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from cometbft_amd import Context
+
+    old = os.environ.get("CMTV_OCT_SPLIT_MAX")
+    os.environ["CMTV_OCT_SPLIT_MAX"] = "0"
+    try:
+        return Context(device=0)
+    finally:
+        if old is None:
+            del os.environ["CMTV_OCT_SPLIT_MAX"]
+        else:
+            os.environ["CMTV_OCT_SPLIT_MAX"] = old

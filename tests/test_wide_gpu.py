@@ -72,10 +72,10 @@ def _mixed_batch(kind, waves_per_vector=1, seed=3):
     return np.array(pk), np.array(sig), m2, off2
 
 
-@pytest.mark.parametrize("kernel", ["oct", "quad", "lane"])
+@pytest.mark.parametrize("kernel", ["oct2", "oct", "quad", "lane"])
 @pytest.mark.parametrize("mode", [MODE_GO_STDLIB, MODE_ZIP215])
-def test_ed25519_wide_in_mixed_waves(gpu_ctx, gpu_ctx_quad, gpu_ctx_lane, kernel, mode):
-    ctx = {"oct": gpu_ctx, "quad": gpu_ctx_quad, "lane": gpu_ctx_lane}[kernel]
+def test_ed25519_wide_in_mixed_waves(gpu_ctx, gpu_ctx_oct1, gpu_ctx_quad, gpu_ctx_lane, kernel, mode):
+    ctx = {"oct2": gpu_ctx, "oct": gpu_ctx_oct1, "quad": gpu_ctx_quad, "lane": gpu_ctx_lane}[kernel]
     pk, sig, m, off = _mixed_batch("ed25519")
     exp = coracle.verify_batch(pk, sig, m, off, mode, nthreads=8)
     got, words = ctx.verify(pk, sig, m, off, mode, bitmap=True)
@@ -139,13 +139,16 @@ def forced_wide_ctxs():
 
     os.environ["CMTV_FORCE_WIDE"] = "1"
     try:
+        o2ctx = Context(device=0)
+        os.environ["CMTV_OCT_SPLIT_MAX"] = "0"
         octx = Context(device=0)
         os.environ["CMTV_OCT_MAX"] = "0"
         qctx = Context(device=0)
     finally:
         del os.environ["CMTV_FORCE_WIDE"]
         os.environ.pop("CMTV_OCT_MAX", None)
-    return {"oct": octx, "quad": qctx}
+        os.environ.pop("CMTV_OCT_SPLIT_MAX", None)
+    return {"oct2": o2ctx, "oct": octx, "quad": qctx}
 
 
 @pytest.fixture(scope="module")
@@ -153,7 +156,7 @@ def forced_wide_ctx(forced_wide_ctxs):
     return forced_wide_ctxs["quad"]
 
 
-@pytest.mark.parametrize("kernel", ["oct", "quad"])
+@pytest.mark.parametrize("kernel", ["oct2", "oct", "quad"])
 @pytest.mark.parametrize("mode,key", [(MODE_GO_STDLIB, "go"), (MODE_ZIP215, "zip215")])
 def test_forced_wide_schedule_on_corpus(forced_wide_ctxs, corpus, mode, key, kernel):
     """CMTV_FORCE_WIDE: every quad (or oct) takes the wide fallback (k1 = k,

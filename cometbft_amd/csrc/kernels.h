@@ -14,9 +14,9 @@ constexpr uint32_t kCombScratchWordsPerKey = 128 * 320;  // prefix products whil
 
 // launch_verify / launch_verify_sr25519 kflags: the quad kernel (else lane),
 // the CMTV_FORCE_WIDE test knob (every quad takes the 64-window schedule),
-// and the oct kernel (with kLaunchQuad; Ed25519 only), in its two-wave form
-// (kLaunchOctSplit)
-constexpr uint32_t kLaunchQuad = 1, kLaunchForceWide = 2, kLaunchOct = 4, kLaunchOctSplit = 8;
+// the oct kernel (with kLaunchQuad; Ed25519 only) and its two-wave form
+// (kLaunchOctSplit), and the quad kernel's helper-wave form (kLaunchQuadSplit)
+constexpr uint32_t kLaunchQuad = 1, kLaunchForceWide = 2, kLaunchOct = 4, kLaunchOctSplit = 8, kLaunchQuadSplit = 16;
 
 hipError_t launch_btab_init(uint32_t* d_rows, hipStream_t s);
 hipError_t launch_verify(uint32_t mode, uint32_t n, const void* pk, const void* sig, const void* msg,

@@ -160,8 +160,59 @@ __global__ __launch_bounds__(64, CMTV_QUAD_WAVES_PER_EU) void k_verify_oct(uint3
   if (threadIdx.x == 0 && out_bitmap) reinterpret_cast<uint8_t*>(out_bitmap)[gid >> 6] = (uint8_t)x;
 }
 
+// The quad verifier with a helper wave: a 4-wave workgroup takes 48
+// signatures; waves 0-2 are quad waves (16 signatures each) and wave 3 hashes
+// and splits the scalars of all 48 (one lane each, q_prepare) while they
+// decompress A and R; the scalars reach them through LDS at one barrier and
+// wave 3 exits. LDS (3 x 45 KiB tables + 5 KiB of scalars) allows one
+// workgroup per CU, i.e. 4 waves on its 4 SIMDs, and 256 workgroups =
+// 12,288 signatures per round: the same capacity as the one-wave quad kernel
+// (3 x 45 KiB per CU), with the hash and the Euclid off every quad wave.
+template <uint32_t MODE>
+__global__ __launch_bounds__(256, CMTV_QUAD_WAVES_PER_EU) void k_verify_quad_split(
+    uint32_t n, const uint32_t* __restrict__ pk, const uint32_t* __restrict__ sig, const uint8_t* __restrict__ msg,
+    const uint32_t* __restrict__ off, const uint32_t* __restrict__ btab, uint8_t* __restrict__ out_valid,
+    uint64_t* __restrict__ out_bitmap, uint32_t force_wide) {
+  const uint32_t wave = threadIdx.x >> 6, t = threadIdx.x & 63;
+  const uint32_t base = blockIdx.x * 48;
+  __shared__ uint32_t prep[48][SIG_PREP_WORDS + 1];
+  __shared__ uint2 tab_lds[3][2 * 9 * 5 * 64];
+  if (wave == 3) {
+    const uint32_t s = base + (t < 48 ? t : 47);
+    const uint32_t i = s < n ? s : n - 1;
+    const uint32_t m0 = off[i], m1 = off[i + 1];
+    SigPrep p;
+    q_prepare(p, pk + 8 * (size_t)i, sig + 16 * (size_t)i, msg + m0, m1 - m0, force_wide != 0);
+    if (t < 48) sig_prep_store(prep[t], p);
+    __syncthreads();
+    return;
+  }
+  const uint32_t ls = wave * 16 + (t >> 2);
+  const uint32_t s = base + ls;
+  const bool active = s < n;
+  const uint32_t i = active ? s : n - 1;
+  DevQuad q;
+  DevBTabQ bt{btab};
+  DevATabQ ta{tab_lds[wave], t}, tr{tab_lds[wave] + 9 * 5 * 64, t};
+  bool v = q_verify_split<MODE>(q, pk + 8 * (size_t)i, sig + 16 * (size_t)i, bt, ta, tr, [&](SigPrep& p) {
+    __syncthreads();
+    sig_prep_load(p, prep[ls]);
+  });
+  v = v && active;
+  if (active && (t & 3) == 0 && out_valid) out_valid[s] = v ? 1 : 0;
+  uint64_t x = __ballot(v && (t & 3) == 0) & 0x1111111111111111ull;
+  x = (x | (x >> 3)) & 0x0303030303030303ull;
+  x = (x | (x >> 6)) & 0x000F000F000F000Full;
+  x = (x | (x >> 12)) & 0x000000FF000000FFull;
+  x = (x | (x >> 24)) & 0xFFFFull;
+  // one 16-bit slice per quad wave; the grid's last workgroup may run past
+  // the bitmap's words
+  const uint32_t slice = blockIdx.x * 3 + wave;
+  if (t == 0 && out_bitmap && slice < 4 * ((n + 63) / 64)) reinterpret_cast<uint16_t*>(out_bitmap)[slice] = (uint16_t)x;
+}
+
 // The oct verifier over two waves per 8 signatures: wave 1 hashes and splits
-// the scalars (o_prepare) while wave 0 decompresses A and R; the scalars
+// the scalars (q_prepare) while wave 0 decompresses A and R; the scalars
 // reach wave 0 through LDS at one barrier, and wave 1 exits. For batches up
 // to 4,096 signatures (1,024 waves), where SIMDs are idle anyway, this takes
 // the hash and the half-scalar Euclid (~11% of a wave) off the chain.
@@ -175,38 +226,22 @@ __global__ __launch_bounds__(128, CMTV_QUAD_WAVES_PER_EU) void k_verify_oct_spli
   const uint32_t s = gid >> 3;
   const bool active = s < n;
   const uint32_t i = active ? s : n - 1;
-  __shared__ uint32_t prep[8][26];
+  __shared__ uint32_t prep[8][SIG_PREP_WORDS + 1];
   __shared__ uint2 tab_lds[9 * 5 * 64];
   if (threadIdx.x >= 64) {
     const uint32_t m0 = off[i], m1 = off[i + 1];
-    OctPrep p;
-    o_prepare(p, pk + 8 * (size_t)i, sig + 16 * (size_t)i, msg + m0, m1 - m0, force_wide != 0);
-    if ((t & 7) == 0) {
-      uint32_t* d = prep[t >> 3];
-#pragma unroll
-      for (int j = 0; j < 8; j++) {
-        d[j] = p.k1[j];
-        d[8 + j] = p.k2[j];
-        d[16 + j] = p.u[j];
-      }
-      d[24] = p.flags;
-    }
+    SigPrep p;
+    q_prepare(p, pk + 8 * (size_t)i, sig + 16 * (size_t)i, msg + m0, m1 - m0, force_wide != 0);
+    if ((t & 7) == 0) sig_prep_store(prep[t >> 3], p);
     __syncthreads();
     return;
   }
   DevOct q;
   DevBTabQ bt{btab};
   DevATabQ ta{tab_lds, t};
-  bool v = o_verify_split<MODE>(q, pk + 8 * (size_t)i, sig + 16 * (size_t)i, bt, ta, [&](OctPrep& p) {
+  bool v = o_verify_split<MODE>(q, pk + 8 * (size_t)i, sig + 16 * (size_t)i, bt, ta, [&](SigPrep& p) {
     __syncthreads();
-    const uint32_t* d = prep[t >> 3];
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-      p.k1[j] = d[j];
-      p.k2[j] = d[8 + j];
-      p.u[j] = d[16 + j];
-    }
-    p.flags = d[24];
+    sig_prep_load(p, prep[t >> 3]);
   });
   v = v && active;
   if (active && (t & 7) == 0 && out_valid) out_valid[s] = v ? 1 : 0;
@@ -388,6 +423,18 @@ hipError_t launch_verify(uint32_t mode, uint32_t n, const void* pk, const void* 
       hipLaunchKernelGGL(k_verify_oct<MODE_ZIP215>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp, fw);
     else
       hipLaunchKernelGGL(k_verify_oct<MODE_GO_STDLIB>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp, fw);
+    return hipGetLastError();
+  }
+  if (quad && (kflags & kLaunchQuadSplit)) {
+    // 48 signatures per 256-lane block; enough blocks for every 16-bit slice
+    // of every bitmap word
+    const uint32_t slices = 4 * ((n + 63) / 64);
+    const dim3 grid((slices + 2) / 3), block(256);
+    if (mode == MODE_ZIP215)
+      hipLaunchKernelGGL(k_verify_quad_split<MODE_ZIP215>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp, fw);
+    else
+      hipLaunchKernelGGL(k_verify_quad_split<MODE_GO_STDLIB>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp,
+                         fw);
     return hipGetLastError();
   }
   if (quad) {

@@ -30,47 +30,7 @@
 
 namespace cmtv {
 
-// Per-signature scalar work that does not depend on the decoded points:
-// the s check, k = SHA-512(R || A || M) mod L, the half-size pair and the
-// fixed-base scalar u = k2 s mod L. The split kernel (kernels.hip
-// k_verify_oct_split) runs it on a second wave while the first decodes.
-struct OctPrep {
-  uint32_t k1[8], k2[8], u[8];
-  uint32_t flags;  // bit 0: k2 < 0, bit 1: wide, bit 2: s canonical, bits 8..15: window count
-};
-
-CMTV_HD void o_prepare(OctPrep& p, const uint32_t* pk_ptr, const uint32_t* sig_ptr, const uint8_t* msg,
-                       uint32_t mlen, bool force_wide) {
-  uint32_t w[16];
-#pragma unroll
-  for (int i = 0; i < 8; i++) w[i] = sig_ptr[8 + i];
-  const bool s_ok = (w[7] & 0xE0000000u) == 0 && sc_is_canonical(w);
-  uint32_t ts[8];
-#pragma unroll
-  for (int i = 0; i < 8; i++) ts[i] = w[i];
-  uint32_t k[8];
-  {
-    uint32_t h[16];
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      w[i] = sig_ptr[i];
-      w[8 + i] = pk_ptr[i];
-    }
-    sha512_prefixed<16>(h, w, msg, mlen);
-    sc_reduce512(k, h);
-  }
-  HalfScalars hs;
-  half_scalars(hs, k, force_wide);
-  hs_bscalar(p.u, hs.k2, hs.k2_neg, ts);
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    p.k1[i] = hs.k1[i];
-    p.k2[i] = hs.k2[i];
-  }
-  p.flags = (hs.k2_neg ? 1u : 0u) | (hs.wide ? 2u : 0u) | (s_ok ? 4u : 0u) | ((uint32_t)hs.windows << 8);
-}
-
-// The oct verifier with the scalar work supplied by get_prep(OctPrep&), which
+// The oct verifier with the scalar work supplied by get_prep(SigPrep&), which
 // is called after the decompression (every lane of the wave calls it once).
 template <uint32_t MODE, class Q, class BTab, class ATab, class GetPrep>
 CMTV_HD bool o_verify_split(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig_ptr, const BTab& btab, ATab& tab,
@@ -95,14 +55,10 @@ CMTV_HD bool o_verify_split(const Q& q, const uint32_t* pk_ptr, const uint32_t* 
   }
 
   // ---- half-size scalars (halfscalar.h), u = k2 s mod L; W uniform per wave
-  OctPrep hs;
+  SigPrep hs;
   get_prep(hs);
   const bool k2_neg = hs.flags & 1u, s_ok = (hs.flags & 4u) != 0;
-  const bool wide = q.any((hs.flags & 2u) != 0);
-  int W = HS_WINDOWS;
-#pragma unroll 1
-  for (int x = HS_WINDOWS; x < HS_MAX_WINDOWS; x++) W += q.any((int)(hs.flags >> 8) > x) ? 1 : 0;
-  W = wide ? HS_WIDE_WINDOWS : W;
+  const int W = q_wave_windows(q, hs.flags);
   const uint32_t* u = hs.u;
 
   // ---- this quad's point: -A (lower), k2 < 0 ? R : -R (upper); its table
@@ -189,7 +145,7 @@ template <uint32_t MODE, class Q, class BTab, class ATab>
 CMTV_HD bool o_verify(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig_ptr, const uint8_t* msg,
                       uint32_t mlen, const BTab& btab, ATab& tab, bool force_wide = false) {
   return o_verify_split<MODE>(q, pk_ptr, sig_ptr, btab, tab,
-                              [&](OctPrep& p) { o_prepare(p, pk_ptr, sig_ptr, msg, mlen, force_wide); });
+                              [&](SigPrep& p) { q_prepare(p, pk_ptr, sig_ptr, msg, mlen, force_wide); });
 }
 
 }  // namespace cmtv

@@ -263,36 +263,98 @@ struct QArrayTab {  // plain-array table policy (host checks, debug kernels)
   }
 };
 
-// Phases 2-4 of a quad verification, shared by the Ed25519 (q_verify) and
-// sr25519 (q_verify_sr, sr25519_quad.h) kernels. In: v = this lane's
-// coordinate of -A, rc = of R (both extended, Z = 1), k the challenge, ts the
-// fixed-base scalar s. Out: v = this lane's coordinate of
-//   X = [u]B + [k1](-A) + [|k2|](k2 < 0 ? R : -R) = [k2](R' - R),   R' = [s]B - [k]A
-// with (k1, k2) the half-size pair of k (halfscalar.h) and u = k2 s mod L.
-// rc is clobbered.
-template <class Q, class BTab, class ATab, class Probe>
-CMTV_HD void q_straus_half(const Q& q, fe& v, fe& rc, const uint32_t k[8], const uint32_t ts[8], const BTab& btab,
-                           ATab& tabA, ATab& tabR, const Probe& probe, bool force_wide = false) {
-  const int lane = q.lane();
-  // ---- phase 2: half-size scalars (halfscalar.h) and the fixed-base scalar
-  //   X = [u]B + [k1](-A) + [|k2|](k2 < 0 ? R : -R) = [k2](R' - R),
-  //   u = k2 s mod L; the window count is uniform over the wave
+// Per-signature scalar work that does not depend on the decoded points: the
+// half-size pair of the challenge k and the fixed-base scalar u = k2 s mod L
+// (plus, from q_prepare, the s check). The split kernels (kernels.hip
+// k_verify_quad_split / k_verify_oct_split) compute it on a helper wave while
+// the main waves decompress A and R.
+struct SigPrep {
+  uint32_t k1[8], k2[8], u[8];
+  uint32_t flags;  // bit 0: k2 < 0, bit 1: wide, bit 2: s canonical, bits 8..15: window count
+};
+constexpr int SIG_PREP_WORDS = 25;
+
+CMTV_HD void q_prepare_scalars(SigPrep& p, const uint32_t k[8], const uint32_t ts[8], bool force_wide) {
   HalfScalars hs;
   half_scalars(hs, k, force_wide);
-  uint32_t u[8];
-  hs_bscalar(u, hs.k2, hs.k2_neg, ts);
-  // window count: the largest over the wave (34..37), 64 if any is wide
-  const bool wide = q.any(hs.wide);
+  hs_bscalar(p.u, hs.k2, hs.k2_neg, ts);
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    p.k1[i] = hs.k1[i];
+    p.k2[i] = hs.k2[i];
+  }
+  p.flags = (hs.k2_neg ? 1u : 0u) | (hs.wide ? 2u : 0u) | ((uint32_t)hs.windows << 8);
+}
+
+// s check, k = SHA-512(R || A || M) mod L, then q_prepare_scalars
+CMTV_HD void q_prepare(SigPrep& p, const uint32_t* pk_ptr, const uint32_t* sig_ptr, const uint8_t* msg,
+                       uint32_t mlen, bool force_wide) {
+  uint32_t w[16];
+#pragma unroll
+  for (int i = 0; i < 8; i++) w[i] = sig_ptr[8 + i];
+  const bool s_ok = (w[7] & 0xE0000000u) == 0 && sc_is_canonical(w);
+  uint32_t ts[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) ts[i] = w[i];
+  uint32_t k[8];
+  {
+    uint32_t h[16];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      w[i] = sig_ptr[i];
+      w[8 + i] = pk_ptr[i];
+    }
+    sha512_prefixed<16>(h, w, msg, mlen);
+    sc_reduce512(k, h);
+  }
+  q_prepare_scalars(p, k, ts, force_wide);
+  p.flags |= s_ok ? 4u : 0u;
+}
+
+CMTV_HD void sig_prep_store(uint32_t* d, const SigPrep& p) {
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    d[j] = p.k1[j];
+    d[8 + j] = p.k2[j];
+    d[16 + j] = p.u[j];
+  }
+  d[24] = p.flags;
+}
+CMTV_HD void sig_prep_load(SigPrep& p, const uint32_t* d) {
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    p.k1[j] = d[j];
+    p.k2[j] = d[8 + j];
+    p.u[j] = d[16 + j];
+  }
+  p.flags = d[24];
+}
+
+// the wave-uniform window count: the largest over the wave (34..37), 64 if
+// any signature is wide
+template <class Q>
+CMTV_HD int q_wave_windows(const Q& q, uint32_t flags) {
+  const bool wide = q.any((flags & 2u) != 0);
   int W = HS_WINDOWS;
 #pragma unroll 1
-  for (int w = HS_WINDOWS; w < HS_MAX_WINDOWS; w++) W += q.any(hs.windows > w) ? 1 : 0;
-  W = wide ? HS_WIDE_WINDOWS : W;
+  for (int x = HS_WINDOWS; x < HS_MAX_WINDOWS; x++) W += q.any((int)(flags >> 8) > x) ? 1 : 0;
+  return wide ? HS_WIDE_WINDOWS : W;
+}
+
+// Phases 3-4 from a prepared pair (see q_straus_half below).
+template <class Q, class BTab, class ATab, class Probe>
+CMTV_HD void q_straus_prep(const Q& q, fe& v, fe& rc, const SigPrep& hs, const BTab& btab, ATab& tabA, ATab& tabR,
+                           const Probe& probe) {
+  const int lane = q.lane();
+  const bool k2_neg = (hs.flags & 1u) != 0;
+  const uint32_t* u = hs.u;
+  const int W = q_wave_windows(q, hs.flags);
   {
     fe kk;
 #pragma unroll
     for (int i = 0; i < 8; i++) kk.v[i] = hs.k1[i];
     kk.v[8] = hs.k2[0];
-    kk.v[9] = (hs.k2_neg ? 1u : 0u) | (hs.wide ? 2u : 0u);
+    kk.v[9] = hs.flags & 3u;
     probe.snap(11, kk);
   }
 
@@ -301,7 +363,7 @@ CMTV_HD void q_straus_half(const Q& q, fe& v, fe& rc, const uint32_t k[8], const
     fe t;
     fe_neg(t, rc);
     fe_carry(t);
-    fe_select(rc, rc, t, !hs.k2_neg && (lane == 0 || lane == 3));
+    fe_select(rc, rc, t, !k2_neg && (lane == 0 || lane == 3));
   }
   q_build_table(q, tabA, v);
   q_build_table(q, tabR, rc);
@@ -358,18 +420,29 @@ CMTV_HD void q_straus_half(const Q& q, fe& v, fe& rc, const uint32_t k[8], const
   probe.snap(10, v);
 }
 
-template <uint32_t MODE, class Q, class BTab, class ATab, class Probe = NullProbe>
-CMTV_HD bool q_verify(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig_ptr, const uint8_t* msg,
-                      uint32_t mlen, const BTab& btab, ATab& tabA, ATab& tabR, const Probe& probe = Probe(),
-                      bool force_wide = false) {
+// Phases 2-4 of a quad verification, shared by the Ed25519 (q_verify) and
+// sr25519 (q_verify_sr, sr25519_quad.h) kernels. In: v = this lane's
+// coordinate of -A, rc = of R (both extended, Z = 1), k the challenge, ts the
+// fixed-base scalar s. Out: v = this lane's coordinate of
+//   X = [u]B + [k1](-A) + [|k2|](k2 < 0 ? R : -R) = [k2](R' - R),   R' = [s]B - [k]A
+// with (k1, k2) the half-size pair of k (halfscalar.h) and u = k2 s mod L.
+// rc is clobbered.
+template <class Q, class BTab, class ATab, class Probe>
+CMTV_HD void q_straus_half(const Q& q, fe& v, fe& rc, const uint32_t k[8], const uint32_t ts[8], const BTab& btab,
+                           ATab& tabA, ATab& tabR, const Probe& probe, bool force_wide = false) {
+  SigPrep p;
+  q_prepare_scalars(p, k, ts, force_wide);
+  q_straus_prep(q, v, rc, p, btab, tabA, tabR, probe);
+}
+
+// The quad verifier with the scalar work supplied by get_prep(SigPrep&)
+// (q_prepare, or a helper wave's result), called after the decompression by
+// every lane of the wave.
+template <uint32_t MODE, class Q, class BTab, class ATab, class GetPrep, class Probe = NullProbe>
+CMTV_HD bool q_verify_split(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig_ptr, const BTab& btab, ATab& tabA,
+                            ATab& tabR, const GetPrep& get_prep, const Probe& probe = Probe()) {
   const int lane = q.lane();
-  uint32_t w[16];
-#pragma unroll
-  for (int i = 0; i < 8; i++) w[i] = sig_ptr[8 + i];
-  const bool s_ok = (w[7] & 0xE0000000u) == 0 && sc_is_canonical(w);
-  uint32_t ts[8];
-#pragma unroll
-  for (int i = 0; i < 8; i++) ts[i] = w[i];
+  uint32_t w[8];
 
   // ---- phase 1: decode A (even lanes) and R (odd lanes)
   const uint32_t* src = (lane & 1) ? sig_ptr : pk_ptr;
@@ -401,28 +474,20 @@ CMTV_HD bool q_verify(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig_pt
   }
   probe.snap(0, v);
   probe.snap(1, rc);
-  uint32_t k[8];
-  {
-    uint32_t h[16];
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      w[i] = sig_ptr[i];
-      w[8 + i] = pk_ptr[i];
-    }
-    sha512_prefixed<16>(h, w, msg, mlen);
-    sc_reduce512(k, h);
-  }
+  SigPrep p;
+  get_prep(p);
+  const bool s_ok = (p.flags & 4u) != 0;
   {
     fe kk;
 #pragma unroll
-    for (int i = 0; i < 8; i++) kk.v[i] = k[i];
+    for (int i = 0; i < 8; i++) kk.v[i] = p.u[i];
     kk.v[8] = s_ok | (a_ok << 1) | (r_ok << 2) | (r_canon << 3);
     kk.v[9] = 0;
     probe.snap(2, kk);
   }
 
   // ---- phases 2-4: v <- this lane's coordinate of X = [k2](R' - R)
-  q_straus_half(q, v, rc, k, ts, btab, tabA, tabR, probe, force_wide);
+  q_straus_prep(q, v, rc, p, btab, tabA, tabR, probe);
 
   // ---- final check: X = O (GO_STDLIB: R' == R with R canonical, i.e.
   //      encode(R') == R bytes) / [8]X = O (ZIP215)
@@ -438,6 +503,16 @@ CMTV_HD bool q_verify(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig_pt
   const bool e1 = q.template perm32<QP_B1>(yz ? 1u : 0u) != 0;
   if (MODE == MODE_GO_STDLIB) return s_ok && a_ok && r_ok && r_canon && e0 && e1;
   return s_ok && a_ok && r_ok && e0 && e1;
+}
+
+// One wave does everything (k_verify_quad; the host checks)
+template <uint32_t MODE, class Q, class BTab, class ATab, class Probe = NullProbe>
+CMTV_HD bool q_verify(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig_ptr, const uint8_t* msg,
+                      uint32_t mlen, const BTab& btab, ATab& tabA, ATab& tabR, const Probe& probe = Probe(),
+                      bool force_wide = false) {
+  return q_verify_split<MODE>(
+      q, pk_ptr, sig_ptr, btab, tabA, tabR,
+      [&](SigPrep& p) { q_prepare(p, pk_ptr, sig_ptr, msg, mlen, force_wide); }, probe);
 }
 
 }  // namespace cmtv

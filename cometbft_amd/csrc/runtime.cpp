@@ -38,12 +38,16 @@ constexpr uint32_t kChunk = 1u << 18;  // signatures per launch (A-table scratch
 // crossover between the quad (4 lanes / signature) and lane (1 lane / signature)
 // kernels; measured on MI355X, overridable with CMTV_QUAD_MAX
 constexpr size_t kQuadMaxDefault = 40000;
-// Ed25519 batches up to this size use the 8-lanes-per-signature kernel (oct.h):
-// 1,024 waves of 8 = one wave per SIMD; overridable with CMTV_OCT_MAX
-constexpr size_t kOctMaxDefault = 8192;
-// ... and up to this size its two-wave form (k_verify_oct_split: 2 waves per
-// 8 signatures, 1,024 waves at 4,096); CMTV_OCT_SPLIT_MAX
-constexpr size_t kOctSplitMaxDefault = 4096;
+// Ed25519 batches up to this size use the 8-lanes-per-signature kernel
+// (oct.h) in its two-wave form (k_verify_oct_split: 2 waves per 8
+// signatures, 1,024 waves at 4,096); measured on MI355X, the helper-wave quad
+// kernel is as fast from ~4k and faster beyond (the one-wave oct kernel
+// stays reachable with CMTV_OCT_SPLIT_MAX < CMTV_OCT_MAX). CMTV_OCT_MAX
+constexpr size_t kOctMaxDefault = 4096;
+constexpr size_t kOctSplitMaxDefault = 4096;  // CMTV_OCT_SPLIT_MAX
+// quad batches up to this size take the helper-wave form (k_verify_quad_split:
+// 256 workgroups x 48 signatures per round); CMTV_QUAD_SPLIT_MAX
+constexpr size_t kQuadSplitMaxDefault = 40000;
 // the same crossover for registered-key verification (env CMTV_KEYED_QUAD_MAX)
 constexpr size_t kKeyedQuadMaxDefault = 16384;
 // signatures per device below which a batch is not sharded (env CMTV_SHARD_MIN)
@@ -334,6 +338,7 @@ struct cmtv_ctx {
   size_t quad_max = kQuadMaxDefault;  // batches up to this size use the quad kernel
   size_t oct_max = kOctMaxDefault;    // ... and up to this size the oct kernel
   size_t oct_split_max = kOctSplitMaxDefault;
+  size_t quad_split_max = kQuadSplitMaxDefault;
   size_t keyed_quad_max = kKeyedQuadMaxDefault;
   size_t lane_chunk = kChunk;         // signatures per lane-kernel launch (env CMTV_LANE_CHUNK)
   size_t shard_min = kShardMinDefault;
@@ -401,8 +406,10 @@ static int enqueue_verify(cmtv_ctx* ctx, CmtvDev& D, size_t n, const uint8_t* d_
   const bool quad = n <= ctx->quad_max;
   const bool oct = quad && !sr && n <= ctx->oct_max;
   const bool oct_split = oct && n <= ctx->oct_split_max;
+  const bool quad_split = quad && !sr && !oct && n <= ctx->quad_split_max;
   const uint32_t kflags = (quad ? kLaunchQuad : 0u) | (oct ? kLaunchOct : 0u) |
-                          (oct_split ? kLaunchOctSplit : 0u) | (ctx->force_wide ? kLaunchForceWide : 0u);
+                          (oct_split ? kLaunchOctSplit : 0u) | (quad_split ? kLaunchQuadSplit : 0u) |
+                          (ctx->force_wide ? kLaunchForceWide : 0u);
   hipError_t e = hipSuccess;
   if (!quad) {
     const size_t lanes = std::min<size_t>(n, ctx->lane_chunk);
@@ -901,6 +908,7 @@ static void read_env(cmtv_ctx* ctx) {
   if (const char* qm = std::getenv("CMTV_QUAD_MAX")) ctx->quad_max = (size_t)std::strtoull(qm, nullptr, 10);
   if (const char* om = std::getenv("CMTV_OCT_MAX")) ctx->oct_max = (size_t)std::strtoull(om, nullptr, 10);
   if (const char* os = std::getenv("CMTV_OCT_SPLIT_MAX")) ctx->oct_split_max = (size_t)std::strtoull(os, nullptr, 10);
+  if (const char* qs = std::getenv("CMTV_QUAD_SPLIT_MAX")) ctx->quad_split_max = (size_t)std::strtoull(qs, nullptr, 10);
   if (const char* kq = std::getenv("CMTV_KEYED_QUAD_MAX")) ctx->keyed_quad_max = (size_t)std::strtoull(kq, nullptr, 10);
   if (const char* lc = std::getenv("CMTV_LANE_CHUNK")) {
     const size_t v = (size_t)std::strtoull(lc, nullptr, 10) / 64 * 64;

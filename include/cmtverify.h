@@ -96,9 +96,9 @@ typedef struct cmtv_stats {
  * tables of (1..128)B, (1..128)[2^124]B and (1..128)[2^128]B (built on the
  * device), allocates pinned staging.
  * Replaces: nothing in the reference (it has no device state).
- * Environment (read at open): CMTV_OCT_MAX / CMTV_QUAD_MAX /
+ * Environment (read at open): CMTV_OCT_MAX / CMTV_OCT_SPLIT_MAX / CMTV_QUAD_MAX / CMTV_QUAD_SPLIT_MAX /
  * CMTV_KEYED_QUAD_MAX / CMTV_LANE_CHUNK (kernel crossovers: Ed25519 batches
- * up to CMTV_OCT_MAX (8192) take 8 lanes per signature, up to CMTV_QUAD_MAX
+ * up to CMTV_OCT_MAX (4096) take 8 lanes per signature, up to CMTV_QUAD_MAX
  * (40000) 4 lanes, larger ones one lane), CMTV_FAULT_AT=N (test knob: the N-th verification
  * launch of the context fails with CMTV_EHIP without running; libs/fail
  * FAIL_TEST_INDEX analogue), CMTV_FORCE_WIDE=1 (test knob: the quad kernels

@@ -103,3 +103,27 @@ def gpu_ctx_oct1():
             del os.environ["CMTV_OCT_SPLIT_MAX"]
         else:
             os.environ["CMTV_OCT_SPLIT_MAX"] = old
+
+
+@pytest.fixture(scope="session")
+def gpu_ctx_quad1():
+    """Small Ed25519 batches on the one-wave quad kernel (CMTV_OCT_MAX=0,
+    CMTV_QUAD_SPLIT_MAX=0) instead of its helper-wave form."""
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from cometbft_amd import Context
+
+    keys = ("CMTV_OCT_MAX", "CMTV_QUAD_SPLIT_MAX")
+    old = {k: os.environ.get(k) for k in keys}
+    for k in keys:
+        os.environ[k] = "0"
+    try:
+        return Context(device=0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v

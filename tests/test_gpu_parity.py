@@ -19,10 +19,11 @@ def _cat_report(cats, got, exp):
     return [(cats[i], int(got[i]), int(exp[i])) for i in bad[:20]]
 
 
-@pytest.mark.parametrize("kernel", ["oct2", "oct", "quad", "lane"])
+@pytest.mark.parametrize("kernel", ["oct2", "oct", "quad2", "quad", "lane"])
 @pytest.mark.parametrize("mode,key", [(MODE_GO_STDLIB, "go"), (MODE_ZIP215, "zip215")])
-def test_corpus_bit_exact(gpu_ctx, gpu_ctx_oct1, gpu_ctx_quad, gpu_ctx_lane, corpus, mode, key, kernel):
-    ctx = {"oct2": gpu_ctx, "oct": gpu_ctx_oct1, "quad": gpu_ctx_quad, "lane": gpu_ctx_lane}[kernel]
+def test_corpus_bit_exact(gpu_ctx, gpu_ctx_oct1, gpu_ctx_quad, gpu_ctx_quad1, gpu_ctx_lane, corpus, mode, key, kernel):
+    ctx = {"oct2": gpu_ctx, "oct": gpu_ctx_oct1, "quad2": gpu_ctx_quad, "quad": gpu_ctx_quad1,
+           "lane": gpu_ctx_lane}[kernel]
     msg, off = pack_messages(corpus["msgs"])
     valid, words = ctx.verify(corpus["pk"], corpus["sig"], msg, off, mode, bitmap=True)
     exp = corpus[key]
@@ -51,10 +52,11 @@ def test_device_keygen_and_signing_match_oracle(gpu_ctx):
     assert np.array_equal(gpu_ctx.sign(seeds, m, off), sig)
 
 
-@pytest.mark.parametrize("kernel", ["oct2", "oct", "quad", "lane"])
+@pytest.mark.parametrize("kernel", ["oct2", "oct", "quad2", "quad", "lane"])
 @pytest.mark.parametrize("n", [1, 2, 15, 16, 17, 63, 64, 65, 127, 1000])
-def test_ragged_sizes_honest_and_flipped(gpu_ctx, gpu_ctx_oct1, gpu_ctx_quad, gpu_ctx_lane, n, kernel):
-    gpu_ctx = {"oct2": gpu_ctx, "oct": gpu_ctx_oct1, "quad": gpu_ctx_quad, "lane": gpu_ctx_lane}[kernel]
+def test_ragged_sizes_honest_and_flipped(gpu_ctx, gpu_ctx_oct1, gpu_ctx_quad, gpu_ctx_quad1, gpu_ctx_lane, n, kernel):
+    gpu_ctx = {"oct2": gpu_ctx, "oct": gpu_ctx_oct1, "quad2": gpu_ctx_quad, "quad": gpu_ctx_quad1,
+           "lane": gpu_ctx_lane}[kernel]
     seeds, pk, sig, m, off = _honest(n, 100 + n)
     rng = np.random.default_rng(n)
     sig = sig.copy()

@@ -72,10 +72,11 @@ def _mixed_batch(kind, waves_per_vector=1, seed=3):
     return np.array(pk), np.array(sig), m2, off2
 
 
-@pytest.mark.parametrize("kernel", ["oct2", "oct", "quad", "lane"])
+@pytest.mark.parametrize("kernel", ["oct2", "oct", "quad2", "quad", "lane"])
 @pytest.mark.parametrize("mode", [MODE_GO_STDLIB, MODE_ZIP215])
-def test_ed25519_wide_in_mixed_waves(gpu_ctx, gpu_ctx_oct1, gpu_ctx_quad, gpu_ctx_lane, kernel, mode):
-    ctx = {"oct2": gpu_ctx, "oct": gpu_ctx_oct1, "quad": gpu_ctx_quad, "lane": gpu_ctx_lane}[kernel]
+def test_ed25519_wide_in_mixed_waves(gpu_ctx, gpu_ctx_oct1, gpu_ctx_quad, gpu_ctx_quad1, gpu_ctx_lane, kernel, mode):
+    ctx = {"oct2": gpu_ctx, "oct": gpu_ctx_oct1, "quad2": gpu_ctx_quad, "quad": gpu_ctx_quad1,
+           "lane": gpu_ctx_lane}[kernel]
     pk, sig, m, off = _mixed_batch("ed25519")
     exp = coracle.verify_batch(pk, sig, m, off, mode, nthreads=8)
     got, words = ctx.verify(pk, sig, m, off, mode, bitmap=True)
@@ -143,12 +144,13 @@ def forced_wide_ctxs():
         os.environ["CMTV_OCT_SPLIT_MAX"] = "0"
         octx = Context(device=0)
         os.environ["CMTV_OCT_MAX"] = "0"
+        q2ctx = Context(device=0)
+        os.environ["CMTV_QUAD_SPLIT_MAX"] = "0"
         qctx = Context(device=0)
     finally:
-        del os.environ["CMTV_FORCE_WIDE"]
-        os.environ.pop("CMTV_OCT_MAX", None)
-        os.environ.pop("CMTV_OCT_SPLIT_MAX", None)
-    return {"oct2": o2ctx, "oct": octx, "quad": qctx}
+        for k in ("CMTV_FORCE_WIDE", "CMTV_OCT_MAX", "CMTV_OCT_SPLIT_MAX", "CMTV_QUAD_SPLIT_MAX"):
+            os.environ.pop(k, None)
+    return {"oct2": o2ctx, "oct": octx, "quad2": q2ctx, "quad": qctx}
 
 
 @pytest.fixture(scope="module")
@@ -156,7 +158,7 @@ def forced_wide_ctx(forced_wide_ctxs):
     return forced_wide_ctxs["quad"]
 
 
-@pytest.mark.parametrize("kernel", ["oct2", "oct", "quad"])
+@pytest.mark.parametrize("kernel", ["oct2", "oct", "quad2", "quad"])
 @pytest.mark.parametrize("mode,key", [(MODE_GO_STDLIB, "go"), (MODE_ZIP215, "zip215")])
 def test_forced_wide_schedule_on_corpus(forced_wide_ctxs, corpus, mode, key, kernel):
     """CMTV_FORCE_WIDE: every quad (or oct) takes the wide fallback (k1 = k,

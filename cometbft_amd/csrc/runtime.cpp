@@ -406,7 +406,7 @@ static int enqueue_verify(cmtv_ctx* ctx, CmtvDev& D, size_t n, const uint8_t* d_
   const bool quad = n <= ctx->quad_max;
   const bool oct = quad && !sr && n <= ctx->oct_max;
   const bool oct_split = oct && n <= ctx->oct_split_max;
-  const bool quad_split = quad && !sr && !oct && n <= ctx->quad_split_max;
+  const bool quad_split = quad && !oct && n <= ctx->quad_split_max;
   const uint32_t kflags = (quad ? kLaunchQuad : 0u) | (oct ? kLaunchOct : 0u) |
                           (oct_split ? kLaunchOctSplit : 0u) | (quad_split ? kLaunchQuadSplit : 0u) |
                           (ctx->force_wide ? kLaunchForceWide : 0u);

@@ -11,18 +11,21 @@
 //
 // Per quad: every lane runs the merlin transcript (the same bytes; the State
 // policy gives each lane its own slot), lanes {0,2} decode A and {1,3}
-// decode R, then q_straus_half.
+// decode R, then the quad Straus (q_straus_prep). The split kernel moves the
+// transcript and the half-size split to a helper wave (sr_prepare).
 #pragma once
 #include "quad.h"
 #include "sr25519.h"
 
 namespace cmtv {
 
-template <class Q, class BTab, class ATab, class State, class Probe = NullProbe>
-CMTV_HD bool q_verify_sr(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig_ptr, const uint8_t* msg,
-                         uint32_t mlen, const uint16_t* prog, int nops, State& st, const BTab& btab, ATab& tabA,
-                         ATab& tabR, const Probe& probe = Probe(), bool force_wide = false) {
-  const int lane = q.lane();
+// The scalar half of an sr25519 quad verification (no decoded points
+// needed): schnorrkel marker and canonical s, the merlin challenge k mod L,
+// the half-size pair and u = k2 s mod L. k_verify_sr25519_quad_split runs it
+// on a helper wave.
+template <class State>
+CMTV_HD void sr_prepare(SigPrep& p, const uint32_t* pk_ptr, const uint32_t* sig_ptr, const uint8_t* msg,
+                        uint32_t mlen, const uint16_t* prog, int nops, State& st, bool force_wide) {
   uint32_t pk[8], rw[8], ts[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) {
@@ -33,22 +36,29 @@ CMTV_HD bool q_verify_sr(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig
   const bool marker = (ts[7] >> 31) != 0;
   ts[7] &= 0x7FFFFFFFu;
   const bool s_ok = marker && sc_is_canonical(ts);
-
-  // ---- challenge (merlin transcript), mod L
   uint32_t k[8];
   {
     uint32_t kb[16];
     sr_transcript(kb, st, prog, nops, msg, mlen, pk, rw);
     sc_reduce512(k, kb);
   }
+  q_prepare_scalars(p, k, ts, force_wide);
+  p.flags |= s_ok ? 4u : 0u;
+}
 
+// The point half, with the scalars from get_prep(SigPrep&) (called after the
+// decompression by every lane of the wave).
+template <class Q, class BTab, class ATab, class GetPrep, class Probe = NullProbe>
+CMTV_HD bool q_verify_sr_split(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig_ptr, const BTab& btab,
+                               ATab& tabA, ATab& tabR, const GetPrep& get_prep, const Probe& probe = Probe()) {
+  const int lane = q.lane();
   // ---- decode A (even lanes) and R (odd lanes), broadcast coordinates
   fe v, rc;
   bool a_ok, r_ok;
   {
     uint32_t w[8];
 #pragma unroll
-    for (int i = 0; i < 8; i++) w[i] = (lane & 1) ? rw[i] : pk[i];
+    for (int i = 0; i < 8; i++) w[i] = (lane & 1) ? sig_ptr[i] : pk_ptr[i];
     ge_p3 P;
     const bool dec = ristretto_decode(P, w);
     fe x, y, t, one;
@@ -70,14 +80,27 @@ CMTV_HD bool q_verify_sr(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig
   }
   probe.snap(0, v);
   probe.snap(1, rc);
+  SigPrep p;
+  get_prep(p);
+  const bool s_ok = (p.flags & 4u) != 0;
 
-  q_straus_half(q, v, rc, k, ts, btab, tabA, tabR, probe, force_wide);
+  q_straus_prep(q, v, rc, p, btab, tabA, tabR, probe);
 
   // ---- X in E[4]: X.X = 0 (lane 0) or X.Y = 0 (lane 1)
   const bool z = fe_iszero(v);
   const bool e0 = q.template perm32<QP_B0>(z ? 1u : 0u) != 0;
   const bool e1 = q.template perm32<QP_B1>(z ? 1u : 0u) != 0;
   return s_ok && a_ok && r_ok && (e0 || e1);
+}
+
+// One wave does everything (k_verify_sr25519_quad; the host checks)
+template <class Q, class BTab, class ATab, class State, class Probe = NullProbe>
+CMTV_HD bool q_verify_sr(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig_ptr, const uint8_t* msg,
+                         uint32_t mlen, const uint16_t* prog, int nops, State& st, const BTab& btab, ATab& tabA,
+                         ATab& tabR, const Probe& probe = Probe(), bool force_wide = false) {
+  return q_verify_sr_split(
+      q, pk_ptr, sig_ptr, btab, tabA, tabR,
+      [&](SigPrep& p) { sr_prepare(p, pk_ptr, sig_ptr, msg, mlen, prog, nops, st, force_wide); }, probe);
 }
 
 }  // namespace cmtv

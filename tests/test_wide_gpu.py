@@ -105,9 +105,9 @@ def test_ed25519_wide_keyed(gpu_ctx, gpu_ctx_lane, kernel, mode):
     assert np.array_equal(got, exp), np.nonzero(got != exp)[0][:20]
 
 
-@pytest.mark.parametrize("kernel", ["quad", "lane"])
-def test_sr25519_wide_in_mixed_waves(gpu_ctx, gpu_ctx_lane, kernel):
-    ctx = gpu_ctx if kernel == "quad" else gpu_ctx_lane
+@pytest.mark.parametrize("kernel", ["quad2", "quad", "lane"])
+def test_sr25519_wide_in_mixed_waves(gpu_ctx, gpu_ctx_quad1, gpu_ctx_lane, kernel):
+    ctx = {"quad2": gpu_ctx, "quad": gpu_ctx_quad1, "lane": gpu_ctx_lane}[kernel]
     pk, sig, m, off = _mixed_batch("sr25519", seed=5)
     exp = coracle.sr25519_verify_batch(pk, sig, m, off, nthreads=8)
     got = ctx.verify_sr25519(pk, sig, m, off)
@@ -153,11 +153,6 @@ def forced_wide_ctxs():
     return {"oct2": o2ctx, "oct": octx, "quad2": q2ctx, "quad": qctx}
 
 
-@pytest.fixture(scope="module")
-def forced_wide_ctx(forced_wide_ctxs):
-    return forced_wide_ctxs["quad"]
-
-
 @pytest.mark.parametrize("kernel", ["oct2", "oct", "quad2", "quad"])
 @pytest.mark.parametrize("mode,key", [(MODE_GO_STDLIB, "go"), (MODE_ZIP215, "zip215")])
 def test_forced_wide_schedule_on_corpus(forced_wide_ctxs, corpus, mode, key, kernel):
@@ -173,7 +168,9 @@ def test_forced_wide_schedule_on_corpus(forced_wide_ctxs, corpus, mode, key, ker
     assert np.array_equal(ctx.verify(pk, sig, m, off, mode), exp)
 
 
-def test_forced_wide_schedule_sr25519(forced_wide_ctx):
+@pytest.mark.parametrize("kernel", ["quad2", "quad"])
+def test_forced_wide_schedule_sr25519(forced_wide_ctxs, kernel):
+    forced_wide_ctx = forced_wide_ctxs[kernel]
     pk, sig, m, off = _mixed_batch("sr25519", seed=7)
     exp = coracle.sr25519_verify_batch(pk, sig, m, off, nthreads=8)
     assert np.array_equal(forced_wide_ctx.verify_sr25519(pk, sig, m, off), exp)

@@ -1,6 +1,7 @@
 """Runs each verify kernel a few times on device-resident synthetic batches,
-for rocprofv3 --pmc passes (tools/gpu_prof.sh): k_verify_oct (150 and 8192
-signatures), k_verify_quad (10k commit), k_verify (100k, lane kernel),
+for rocprofv3 --pmc passes (tools/gpu_prof.sh): k_verify_oct_split (150),
+k_verify_quad_split (8192 and the 10k commit), the one-wave k_verify_quad and
+k_verify_oct (10k / 150, env-forced), k_verify (100k, lane kernel),
 k_verify_keyed_quad (10k over 150 keys) and k_verify_keyed (1M over 150 keys).
 Every batch is checked (all valid) so a counter pass never profiles a
 broken kernel."""
@@ -51,19 +52,29 @@ def run(name, c, b, keyed=None):
     print(f"{name}: n={b['n']} x{REPS} ok", flush=True)
 
 
-def lane_ctx():
-    os.environ["CMTV_QUAD_MAX"] = "0"
-    os.environ["CMTV_KEYED_QUAD_MAX"] = "0"
+def env_ctx(**env):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update({k: str(v) for k, v in env.items()})
     try:
         return Context(device=0)
     finally:
-        del os.environ["CMTV_QUAD_MAX"], os.environ["CMTV_KEYED_QUAD_MAX"]
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+def lane_ctx():
+    return env_ctx(CMTV_QUAD_MAX=0, CMTV_KEYED_QUAD_MAX=0)
 
 
 b150, b8k, b10k = batch(150), batch(8192), batch(10000)
-run("oct150", ctx, b150)
-run("oct8192", ctx, b8k)
-run("quad10k", ctx, b10k)
+run("oct_split150", ctx, b150)
+run("quad_split8192", ctx, b8k)
+run("quad_split10k", ctx, b10k)
+run("oct150", env_ctx(CMTV_OCT_SPLIT_MAX=0), b150)
+run("quad10k", env_ctx(CMTV_QUAD_SPLIT_MAX=0), b10k)
 lctx = lane_ctx()
 b100k = batch(100_000)
 run("lane100k", lctx, b100k)

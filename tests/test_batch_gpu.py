@@ -81,6 +81,32 @@ def test_large_batch_properties(gpu_ctx):
         assert np.array_equal(valid[sample], exp)
 
 
+@pytest.mark.parametrize("n", [4097, 12287, 12289, 20000, 39999])
+def test_multi_round_quad_split_sizes(gpu_ctx, n):
+    """The helper-wave quad kernel past one round (256 workgroups x 48) and at
+    the oct / quad crossover: 1% corrupted, exactly those rejected, the bitmap
+    tail clear, a sample against the oracle in both modes."""
+    nk = 300
+    rng = np.random.default_rng(n)
+    seeds = rng.integers(0, 256, (nk, 32), dtype=np.uint8)
+    kidx = rng.integers(0, nk, n).astype(np.uint32)
+    msgs = [b"r%06d-%s" % (i, b"y" * int(i % 53)) for i in range(n)]
+    m, off = pack_messages(msgs)
+    sig = gpu_ctx.sign(seeds, m, off, key_idx=kidx)
+    pk = gpu_ctx.pubkeys(seeds)[kidx]
+    bad = rng.random(n) < 0.01
+    sig[bad, 40] ^= 0x10
+    for mode in (MODE_GO_STDLIB, MODE_ZIP215):
+        valid, words = gpu_ctx.verify(pk, sig, m, off, mode, bitmap=True)
+        assert np.array_equal(valid == 0, bad)
+        bits = np.unpackbits(words.view(np.uint8), bitorder="little")
+        assert np.array_equal(bits[:n], valid) and not bits[n:].any()
+        sample = np.sort(rng.choice(n, 600, replace=False))
+        sm, so = coracle.pack_msgs([msgs[i] for i in sample])
+        exp = coracle.verify_batch(pk[sample], sig[sample], sm, so, mode, nthreads=8)
+        assert np.array_equal(valid[sample], exp)
+
+
 def test_verify_sharded_single_rank(gpu_ctx):
     n = 5000
     rng = np.random.default_rng(1)

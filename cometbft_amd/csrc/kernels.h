@@ -6,8 +6,9 @@
 namespace cmtv {
 
 // (1..128)B, [2^124]B, [2^128]B multiples, then (1..2^15)B, [2^120]B, [2^128]B
-// multiples (verify_core.h BT16_*); 36 words per row, 14.2 MB
-constexpr uint32_t kBtabWords = (3 * 128 + 3 * 32768) * 36;
+// multiples, then the 16-position comb (1..2^15)[2^16j]B (verify_core.h
+// BTAB_TOTAL_ROWS); 36 words per row, 89.7 MB
+constexpr uint32_t kBtabWords = (3 * 128 + 3 * 32768 + 16 * 32768) * 36;
 constexpr uint32_t kAtabWordsPerLane = 320; // (1..8)(-A), 40 words per point
 constexpr uint32_t kCombWords = 32 * 128 * 32;     // one registered-key comb (keyed.h), 512 KiB
 constexpr uint32_t kCombScratchWordsPerKey = 128 * 320;  // prefix products while building

@@ -58,16 +58,12 @@ __device__ __forceinline__ void load_words(uint32_t* w, const uint32_t* __restri
 
 // rows 0..127: (1..128)B; 128..255: (1..128)[2^124]B; 256..383: (1..128)[2^128]B;
 // then the radix-2^16 blocks (1..2^15)B, (1..2^15)[2^120]B, (1..2^15)[2^128]B
+// and the 16-position comb (1..2^15)[2^16j]B (verify_core.h btab_row)
 __global__ __launch_bounds__(64) void k_btab_init(uint32_t* __restrict__ rows) {
   const int e = blockIdx.x * 64 + threadIdx.x;
-  if (e >= BT16_BASE + BT16_ROWS) return;
+  if (e >= BTAB_TOTAL_ROWS) return;
   uint32_t row[BTAB_ROW_WORDS];
-  if (e < BT16_BASE) {
-    btab_entry(row, (e % BTAB_ENTRIES) + 1, e / BTAB_ENTRIES);
-  } else {
-    const int f = e - BT16_BASE;
-    btab_entry_shift(row, (f % BT16_ENTRIES) + 1, bt16_block_shift(f / BT16_ENTRIES), 16);
-  }
+  btab_row(row, e);
 #pragma unroll
   for (int i = 0; i < BTAB_ROW_WORDS; i++) rows[e * BTAB_ROW_WORDS + i] = row[i];
 }
@@ -176,6 +172,7 @@ __global__ __launch_bounds__(256, CMTV_QUAD_WAVES_PER_EU) void k_verify_quad_spl
   const uint32_t wave = threadIdx.x >> 6, t = threadIdx.x & 63;
   const uint32_t base = blockIdx.x * 48;
   __shared__ uint32_t prep[48][SIG_PREP_WORDS + 1];
+  __shared__ uint32_t bpt[48][40];  // [u]B in the quads' cached coordinates
   __shared__ uint2 tab_lds[3][2 * 9 * 5 * 64];
   if (wave == 3) {
     const uint32_t s = base + (t < 48 ? t : 47);
@@ -184,7 +181,11 @@ __global__ __launch_bounds__(256, CMTV_QUAD_WAVES_PER_EU) void k_verify_quad_spl
     SigPrep p;
     q_prepare(p, pk + 8 * (size_t)i, sig + 16 * (size_t)i, msg + m0, m1 - m0, force_wide != 0);
     if (t < 48) sig_prep_store(prep[t], p);
-    __syncthreads();
+    __syncthreads();  // 1: the scalars, as the quad waves finish decoding
+    ge_p3 B;
+    q_bcomb16(B, p.u, DevBTab{btab});
+    if (t < 48) bpoint_store(bpt[t], B);
+    __syncthreads();  // 2: [u]B, before the quad waves' last addition
     return;
   }
   const uint32_t ls = wave * 16 + (t >> 2);
@@ -194,10 +195,18 @@ __global__ __launch_bounds__(256, CMTV_QUAD_WAVES_PER_EU) void k_verify_quad_spl
   DevQuad q;
   DevBTabQ bt{btab};
   DevATabQ ta{tab_lds[wave], t}, tr{tab_lds[wave] + 9 * 5 * 64, t};
-  bool v = q_verify_split<MODE>(q, pk + 8 * (size_t)i, sig + 16 * (size_t)i, bt, ta, tr, [&](SigPrep& p) {
-    __syncthreads();
-    sig_prep_load(p, prep[ls]);
-  });
+  const uint32_t* bq = &bpt[ls][10 * (t & 3)];
+  bool v = q_verify_split<MODE, true>(
+      q, pk + 8 * (size_t)i, sig + 16 * (size_t)i, bt, ta, tr,
+      [&](SigPrep& p) {
+        __syncthreads();
+        sig_prep_load(p, prep[ls]);
+      },
+      [&](fe& c) {
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < 10; j++) c.v[j] = bq[j];
+      });
   v = v && active;
   if (active && (t & 3) == 0 && out_valid) out_valid[s] = v ? 1 : 0;
   uint64_t x = __ballot(v && (t & 3) == 0) & 0x1111111111111111ull;
@@ -227,22 +236,35 @@ __global__ __launch_bounds__(128, CMTV_QUAD_WAVES_PER_EU) void k_verify_oct_spli
   const bool active = s < n;
   const uint32_t i = active ? s : n - 1;
   __shared__ uint32_t prep[8][SIG_PREP_WORDS + 1];
+  __shared__ uint32_t bpt[8][40];
   __shared__ uint2 tab_lds[9 * 5 * 64];
   if (threadIdx.x >= 64) {
     const uint32_t m0 = off[i], m1 = off[i + 1];
     SigPrep p;
     q_prepare(p, pk + 8 * (size_t)i, sig + 16 * (size_t)i, msg + m0, m1 - m0, force_wide != 0);
     if ((t & 7) == 0) sig_prep_store(prep[t >> 3], p);
-    __syncthreads();
+    __syncthreads();  // 1: the scalars
+    ge_p3 B;
+    q_bcomb16(B, p.u, DevBTab{btab});
+    if ((t & 7) == 0) bpoint_store(bpt[t >> 3], B);
+    __syncthreads();  // 2: [u]B
     return;
   }
   DevOct q;
   DevBTabQ bt{btab};
   DevATabQ ta{tab_lds, t};
-  bool v = o_verify_split<MODE>(q, pk + 8 * (size_t)i, sig + 16 * (size_t)i, bt, ta, [&](SigPrep& p) {
-    __syncthreads();
-    sig_prep_load(p, prep[t >> 3]);
-  });
+  const uint32_t* bq = &bpt[t >> 3][10 * (t & 3)];
+  bool v = o_verify_split<MODE, true>(
+      q, pk + 8 * (size_t)i, sig + 16 * (size_t)i, bt, ta,
+      [&](SigPrep& p) {
+        __syncthreads();
+        sig_prep_load(p, prep[t >> 3]);
+      },
+      [&](fe& c) {
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < 10; j++) c.v[j] = bq[j];
+      });
   v = v && active;
   if (active && (t & 7) == 0 && out_valid) out_valid[s] = v ? 1 : 0;
   uint64_t x = __ballot(v && (t & 7) == 0) & 0x0101010101010101ull;
@@ -389,7 +411,7 @@ __global__ __launch_bounds__(64) void k_sign(uint32_t n, const uint32_t* __restr
 static inline unsigned blocks_for(uint32_t n) { return (n + 63) / 64; }
 
 hipError_t launch_btab_init(uint32_t* d_rows, hipStream_t s) {
-  hipLaunchKernelGGL(k_btab_init, dim3(blocks_for(BT16_BASE + BT16_ROWS)), dim3(64), 0, s, d_rows);
+  hipLaunchKernelGGL(k_btab_init, dim3(blocks_for(BTAB_TOTAL_ROWS)), dim3(64), 0, s, d_rows);
   return hipGetLastError();
 }
 

@@ -32,9 +32,12 @@ namespace cmtv {
 
 // The oct verifier with the scalar work supplied by get_prep(SigPrep&), which
 // is called after the decompression (every lane of the wave calls it once).
-template <uint32_t MODE, class Q, class BTab, class ATab, class GetPrep>
+// EXT_B: [u]B comes ready-made from get_b (the lower quad's cached
+// coordinate, a helper wave's q_bcomb16) and is added after the merge; the
+// quads then add no fixed-base digits.
+template <uint32_t MODE, bool EXT_B = false, class Q, class BTab, class ATab, class GetPrep, class GetB = NoExtB>
 CMTV_HD bool o_verify_split(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig_ptr, const BTab& btab, ATab& tab,
-                            const GetPrep& get_prep) {
+                            const GetPrep& get_prep, const GetB& get_b = GetB()) {
   const int lane = q.lane();
   const bool up = q.upper();
   uint32_t w[8];
@@ -91,7 +94,7 @@ CMTV_HD bool o_verify_split(const Q& q, const uint32_t* pk_ptr, const uint32_t* 
       const int d = (int)sc_shift_out(tS, 4) - 8;
       tab.load_signed(q, d < 0 ? -d : d, d < 0, cS);
     }
-    const bool has_b = (win & 3) == 0 && win <= 28;
+    const bool has_b = !EXT_B && (win & 3) == 0 && win <= 28;
     bool b_neg = false, b_ident = false;
     if (has_b) {
       const int dB = (int)sc_shift_out(tB, 16) - 0x8000;
@@ -120,6 +123,10 @@ CMTV_HD bool o_verify_split(const Q& q, const uint32_t* pk_ptr, const uint32_t* 
     q.from_upper(ph, v);
     q_to_cached(q, c, ph);
     q_add(q, v, c);
+    if constexpr (EXT_B) {
+      get_b(c);
+      q_add(q, v, c);
+    }
   }
   const bool a_ok = dec;                        // lower quad: A decoded
   const bool r_ok = q.from_upper32(dec ? 1u : 0u) != 0;

@@ -330,6 +330,45 @@ CMTV_HD void sig_prep_load(SigPrep& p, const uint32_t* d) {
   p.flags = d[24];
 }
 
+// [u]B by the 16-position radix-2^16 comb (verify_core.h BC16 blocks): 16
+// mixed additions and no doublings, one lane per signature -- the helper
+// waves' share of the fixed-base work. BTab: the one-lane policy (load_fe).
+template <class BTab>
+CMTV_HD void q_bcomb16(ge_p3& P, const uint32_t u[8], const BTab& btab) {
+  uint32_t lo[8], hi[8];
+  hs_digits65536(lo, hi, u);
+  p3_identity(P);
+  ge_efgh t;
+#pragma unroll 1
+  for (int j = 15; j >= 0; j--) {
+    const int d = (int)(j >= 8 ? sc_shift_out(hi, 16) : sc_shift_out(lo, 16)) - 0x8000;
+    const int ib = d < 0 ? -d : d;
+    ge_add_table<false>(t, P, btab, BC16_BASE + j * BT16_ENTRIES + (ib > 0 ? ib - 1 : 0), d < 0, ib == 0);
+    efgh_to_p3(P, t);
+  }
+}
+
+// the quad's cached coordinates of P, (Y-X, Y+X, 2Z, 2dT), as 40 words
+CMTV_HD void bpoint_store(uint32_t* d, const ge_p3& P) {
+  fe c[4], d2;
+  fe_sub(c[0], P.Y, P.X);
+  fe_add(c[1], P.Y, P.X);
+  fe_add(c[2], P.Z, P.Z);
+  fe_const_d2(d2);
+  fe_mul(c[3], P.T, d2);
+#pragma unroll
+  for (int k = 0; k < 3; k++) fe_carry(c[k]);
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+#pragma unroll
+    for (int i = 0; i < 10; i++) d[10 * k + i] = c[k].v[i];
+}
+
+// get_b policy of a verifier that adds its own fixed-base digits
+struct NoExtB {
+  CMTV_HD void operator()(fe&) const {}
+};
+
 // the wave-uniform window count: the largest over the wave (34..37), 64 if
 // any signature is wide
 template <class Q>
@@ -341,10 +380,12 @@ CMTV_HD int q_wave_windows(const Q& q, uint32_t flags) {
   return wide ? HS_WIDE_WINDOWS : W;
 }
 
-// Phases 3-4 from a prepared pair (see q_straus_half below).
-template <class Q, class BTab, class ATab, class Probe>
-CMTV_HD void q_straus_prep(const Q& q, fe& v, fe& rc, const SigPrep& hs, const BTab& btab, ATab& tabA, ATab& tabR,
-                           const Probe& probe) {
+// Phases 3-4 from a prepared pair (see q_straus_half below). EXT_B: the
+// fixed-base part [u]B comes ready-made from get_b (this lane's cached
+// coordinate, a helper wave's q_bcomb16) and is added once after the windows.
+template <bool EXT_B, class Q, class BTab, class ATab, class Probe, class GetB>
+CMTV_HD void q_straus_prep_b(const Q& q, fe& v, fe& rc, const SigPrep& hs, const BTab& btab, ATab& tabA, ATab& tabR,
+                             const Probe& probe, const GetB& get_b) {
   const int lane = q.lane();
   const bool k2_neg = (hs.flags & 1u) != 0;
   const uint32_t* u = hs.u;
@@ -387,7 +428,7 @@ CMTV_HD void q_straus_prep(const Q& q, fe& v, fe& rc, const SigPrep& hs, const B
       const int dR = (int)sc_shift_out(tR, 4) - 8;
       tabR.load_signed(q, dR < 0 ? -dR : dR, dR < 0, cR);
     }
-    const bool has_b = (win & 1) == 0 && win <= 30;
+    const bool has_b = !EXT_B && (win & 1) == 0 && win <= 30;
     bool b_neg = false, b_ident = false;
     if (has_b) {
       const bool hi = (win & 2) != 0;
@@ -417,7 +458,18 @@ CMTV_HD void q_straus_prep(const Q& q, fe& v, fe& rc, const SigPrep& hs, const B
     }
     if (win >= W - 4) probe.snap(6 + (W - 1 - win), v);
   }
+  if constexpr (EXT_B) {
+    fe c;
+    get_b(c);
+    q_add(q, v, c);
+  }
   probe.snap(10, v);
+}
+
+template <class Q, class BTab, class ATab, class Probe>
+CMTV_HD void q_straus_prep(const Q& q, fe& v, fe& rc, const SigPrep& hs, const BTab& btab, ATab& tabA, ATab& tabR,
+                           const Probe& probe) {
+  q_straus_prep_b<false>(q, v, rc, hs, btab, tabA, tabR, probe, NoExtB());
 }
 
 // Phases 2-4 of a quad verification, shared by the Ed25519 (q_verify) and
@@ -438,9 +490,11 @@ CMTV_HD void q_straus_half(const Q& q, fe& v, fe& rc, const uint32_t k[8], const
 // The quad verifier with the scalar work supplied by get_prep(SigPrep&)
 // (q_prepare, or a helper wave's result), called after the decompression by
 // every lane of the wave.
-template <uint32_t MODE, class Q, class BTab, class ATab, class GetPrep, class Probe = NullProbe>
+template <uint32_t MODE, bool EXT_B = false, class Q, class BTab, class ATab, class GetPrep, class GetB = NoExtB,
+          class Probe = NullProbe>
 CMTV_HD bool q_verify_split(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig_ptr, const BTab& btab, ATab& tabA,
-                            ATab& tabR, const GetPrep& get_prep, const Probe& probe = Probe()) {
+                            ATab& tabR, const GetPrep& get_prep, const GetB& get_b = GetB(),
+                            const Probe& probe = Probe()) {
   const int lane = q.lane();
   uint32_t w[8];
 
@@ -487,7 +541,7 @@ CMTV_HD bool q_verify_split(const Q& q, const uint32_t* pk_ptr, const uint32_t* 
   }
 
   // ---- phases 2-4: v <- this lane's coordinate of X = [k2](R' - R)
-  q_straus_prep(q, v, rc, p, btab, tabA, tabR, probe);
+  q_straus_prep_b<EXT_B>(q, v, rc, p, btab, tabA, tabR, probe, get_b);
 
   // ---- final check: X = O (GO_STDLIB: R' == R with R canonical, i.e.
   //      encode(R') == R bytes) / [8]X = O (ZIP215)
@@ -512,7 +566,7 @@ CMTV_HD bool q_verify(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig_pt
                       bool force_wide = false) {
   return q_verify_split<MODE>(
       q, pk_ptr, sig_ptr, btab, tabA, tabR,
-      [&](SigPrep& p) { q_prepare(p, pk_ptr, sig_ptr, msg, mlen, force_wide); }, probe);
+      [&](SigPrep& p) { q_prepare(p, pk_ptr, sig_ptr, msg, mlen, force_wide); }, NoExtB(), probe);
 }
 
 }  // namespace cmtv

@@ -40,11 +40,11 @@ constexpr uint32_t kChunk = 1u << 18;  // signatures per launch (A-table scratch
 constexpr size_t kQuadMaxDefault = 40000;
 // Ed25519 batches up to this size use the 8-lanes-per-signature kernel
 // (oct.h) in its two-wave form (k_verify_oct_split: 2 waves per 8
-// signatures, 1,024 waves at 4,096); measured on MI355X, the helper-wave quad
-// kernel is as fast from ~4k and faster beyond (the one-wave oct kernel
-// stays reachable with CMTV_OCT_SPLIT_MAX < CMTV_OCT_MAX). CMTV_OCT_MAX
-constexpr size_t kOctMaxDefault = 4096;
-constexpr size_t kOctSplitMaxDefault = 4096;  // CMTV_OCT_SPLIT_MAX
+// signatures); measured on MI355X (150: 0.227 vs 0.261 ms, 4,096: 0.303 vs
+// 0.265 ms) the helper-wave quad kernel takes over in between (the one-wave
+// oct kernel stays reachable with CMTV_OCT_SPLIT_MAX < CMTV_OCT_MAX).
+constexpr size_t kOctMaxDefault = 3072;       // CMTV_OCT_MAX
+constexpr size_t kOctSplitMaxDefault = 3072;  // CMTV_OCT_SPLIT_MAX
 // quad batches up to this size take the helper-wave form (k_verify_quad_split:
 // 256 workgroups x 48 signatures per round); CMTV_QUAD_SPLIT_MAX
 constexpr size_t kQuadSplitMaxDefault = 40000;

@@ -108,7 +108,10 @@ __global__ __launch_bounds__(256, 1) void k_verify_sr25519_quad_split(
   const uint32_t base = blockIdx.x * 48;
   __shared__ uint32_t prep[48][SIG_PREP_WORDS + 1];
   __shared__ uint2 tab_lds[3][2 * 9 * 5 * 64];
+  // the helper's STROBE states, then (once every lane's transcript is done)
+  // [u]B in the quads' cached coordinates, 48 x 40 words
   __shared__ uint32_t strobe[50 * 64];
+  uint32_t(*bpt)[40] = reinterpret_cast<uint32_t(*)[40]>(strobe);
   if (wave == 3) {
     const uint32_t s = base + (t < 48 ? t : 47);
     const uint32_t i = s < n ? s : n - 1;
@@ -117,7 +120,11 @@ __global__ __launch_bounds__(256, 1) void k_verify_sr25519_quad_split(
     SigPrep p;
     sr_prepare(p, pk + 8 * (size_t)i, sig + 16 * (size_t)i, msg + m0, m1 - m0, prog, nops, st, force_wide != 0);
     if (t < 48) sig_prep_store(prep[t], p);
-    __syncthreads();
+    __syncthreads();  // 1: the scalars
+    ge_p3 B;
+    q_bcomb16(B, p.u, DevBTab{btab});
+    if (t < 48) bpoint_store(bpt[t], B);  // the STROBE states are dead by now
+    __syncthreads();  // 2: [u]B
     return;
   }
   const uint32_t ls = wave * 16 + (t >> 2);
@@ -127,10 +134,18 @@ __global__ __launch_bounds__(256, 1) void k_verify_sr25519_quad_split(
   DevQuad q;
   DevBTabQ bt{btab};
   DevATabQ ta{tab_lds[wave], t}, tr{tab_lds[wave] + 9 * 5 * 64, t};
-  bool v = q_verify_sr_split(q, pk + 8 * (size_t)i, sig + 16 * (size_t)i, bt, ta, tr, [&](SigPrep& p) {
-    __syncthreads();
-    sig_prep_load(p, prep[ls]);
-  });
+  const uint32_t* bq = &bpt[ls][10 * (t & 3)];
+  bool v = q_verify_sr_split<true>(
+      q, pk + 8 * (size_t)i, sig + 16 * (size_t)i, bt, ta, tr,
+      [&](SigPrep& p) {
+        __syncthreads();
+        sig_prep_load(p, prep[ls]);
+      },
+      [&](fe& c) {
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < 10; j++) c.v[j] = bq[j];
+      });
   v = v && active;
   if (active && (t & 3) == 0 && out_valid) out_valid[s] = v ? 1 : 0;
   uint64_t x = __ballot(v && (t & 3) == 0) & 0x1111111111111111ull;

@@ -48,9 +48,11 @@ CMTV_HD void sr_prepare(SigPrep& p, const uint32_t* pk_ptr, const uint32_t* sig_
 
 // The point half, with the scalars from get_prep(SigPrep&) (called after the
 // decompression by every lane of the wave).
-template <class Q, class BTab, class ATab, class GetPrep, class Probe = NullProbe>
+template <bool EXT_B = false, class Q, class BTab, class ATab, class GetPrep, class GetB = NoExtB,
+          class Probe = NullProbe>
 CMTV_HD bool q_verify_sr_split(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig_ptr, const BTab& btab,
-                               ATab& tabA, ATab& tabR, const GetPrep& get_prep, const Probe& probe = Probe()) {
+                               ATab& tabA, ATab& tabR, const GetPrep& get_prep, const GetB& get_b = GetB(),
+                               const Probe& probe = Probe()) {
   const int lane = q.lane();
   // ---- decode A (even lanes) and R (odd lanes), broadcast coordinates
   fe v, rc;
@@ -84,7 +86,7 @@ CMTV_HD bool q_verify_sr_split(const Q& q, const uint32_t* pk_ptr, const uint32_
   get_prep(p);
   const bool s_ok = (p.flags & 4u) != 0;
 
-  q_straus_prep(q, v, rc, p, btab, tabA, tabR, probe);
+  q_straus_prep_b<EXT_B>(q, v, rc, p, btab, tabA, tabR, probe, get_b);
 
   // ---- X in E[4]: X.X = 0 (lane 0) or X.Y = 0 (lane 1)
   const bool z = fe_iszero(v);
@@ -100,7 +102,8 @@ CMTV_HD bool q_verify_sr(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig
                          ATab& tabR, const Probe& probe = Probe(), bool force_wide = false) {
   return q_verify_sr_split(
       q, pk_ptr, sig_ptr, btab, tabA, tabR,
-      [&](SigPrep& p) { sr_prepare(p, pk_ptr, sig_ptr, msg, mlen, prog, nops, st, force_wide); }, probe);
+      [&](SigPrep& p) { sr_prepare(p, pk_ptr, sig_ptr, msg, mlen, prog, nops, st, force_wide); }, NoExtB(),
+      probe);
 }
 
 }  // namespace cmtv

@@ -78,6 +78,12 @@ constexpr int BT16_BASE = 3 * BTAB_ENTRIES;
 constexpr int BT16_ROWS = 3 * BT16_ENTRIES;
 CMTV_HD int bt16_block_shift(int block) { return block == 0 ? 0 : (block == 1 ? 120 : 128); }
 
+// 16-position radix-2^16 comb of B for the helper waves (quad.h q_bcomb16):
+// block j = (1..2^15)[2^(16j)]B, j = 0..15
+constexpr int BC16_BASE = BT16_BASE + BT16_ROWS;
+constexpr int BC16_ROWS = 16 * BT16_ENTRIES;
+constexpr int BTAB_TOTAL_ROWS = BC16_BASE + BC16_ROWS;  // 622,976 rows, 89.7 MB
+
 // [m][2^shift]B, m < 2^bits, in affine niels form
 CMTV_HD void btab_entry_shift(uint32_t row[BTAB_ROW_WORDS], int m, int shift, int bits);
 CMTV_HD void btab_entry(uint32_t row[BTAB_ROW_WORDS], int m, int block = 0) {
@@ -133,6 +139,19 @@ CMTV_HD void btab_entry_shift(uint32_t row[BTAB_ROW_WORDS], int m, int shift, in
     row[i] = ypx.v[i];
     row[BTAB_COORD_WORDS + i] = ymx.v[i];
     row[2 * BTAB_COORD_WORDS + i] = xy.v[i];
+  }
+}
+
+// row e of the device B table, whatever its block (k_btab_init, host checks)
+CMTV_HD void btab_row(uint32_t row[BTAB_ROW_WORDS], int e) {
+  if (e < BT16_BASE) {
+    btab_entry(row, e % BTAB_ENTRIES + 1, e / BTAB_ENTRIES);
+  } else if (e < BC16_BASE) {
+    const int f = e - BT16_BASE;
+    btab_entry_shift(row, f % BT16_ENTRIES + 1, bt16_block_shift(f / BT16_ENTRIES), 16);
+  } else {
+    const int f = e - BC16_BASE;
+    btab_entry_shift(row, f % BT16_ENTRIES + 1, 16 * (f / BT16_ENTRIES), 16);
   }
 }
 

@@ -98,7 +98,7 @@ typedef struct cmtv_stats {
  * Replaces: nothing in the reference (it has no device state).
  * Environment (read at open): CMTV_OCT_MAX / CMTV_OCT_SPLIT_MAX / CMTV_QUAD_MAX / CMTV_QUAD_SPLIT_MAX /
  * CMTV_KEYED_QUAD_MAX / CMTV_LANE_CHUNK (kernel crossovers: Ed25519 batches
- * up to CMTV_OCT_MAX (4096) take 8 lanes per signature, up to CMTV_QUAD_MAX
+ * up to CMTV_OCT_MAX (3072) take 8 lanes per signature, up to CMTV_QUAD_MAX
  * (40000) 4 lanes, larger ones one lane), CMTV_FAULT_AT=N (test knob: the N-th verification
  * launch of the context fails with CMTV_EHIP without running; libs/fail
  * FAIL_TEST_INDEX analogue), CMTV_FORCE_WIDE=1 (test knob: the quad kernels

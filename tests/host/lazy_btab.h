@@ -1,7 +1,6 @@
 // Host-side fixed-base table for the quad/oct verifiers' checks: rows of the
-// device B table (verify_core.h: three radix-256 blocks, then the three
-// (1..2^15)[2^shift]B radix-2^16 blocks) computed on first use, since a
-// host build of all 98,688 rows would take minutes. Thread-safe (quadcheck
+// device B table (verify_core.h btab_row: every block) computed on first
+// use, since a host build of all 622,976 rows would take far too long. Thread-safe (quadcheck
 // runs the four lanes of a quad as threads). Test infrastructure.
 #pragma once
 #include <array>
@@ -20,12 +19,7 @@ struct LazyBTab {
     auto it = rows.find(e);
     if (it == rows.end()) {
       std::array<uint32_t, BTAB_ROW_WORDS> r{};
-      if (e < BT16_BASE) {
-        btab_entry(r.data(), e % BTAB_ENTRIES + 1, e / BTAB_ENTRIES);
-      } else {
-        const int f = e - BT16_BASE;
-        btab_entry_shift(r.data(), f % BT16_ENTRIES + 1, bt16_block_shift(f / BT16_ENTRIES), 16);
-      }
+      btab_row(r.data(), e);
       it = rows.emplace(e, r).first;
     }
     return it->second.data();
@@ -34,6 +28,8 @@ struct LazyBTab {
     const uint32_t* p = row(e) + off;
     for (int i = 0; i < 10; i++) r.v[i] = p[i];
   }
+  // the one-lane policy (ge_add_table): niels coordinate c of row e
+  void load_fe(int e, int c, fe& r) const { load_coord(e, c * BTAB_COORD_WORDS, r); }
 };
 
 }  // namespace cmtv

@@ -138,6 +138,11 @@ int main(int argc, char** argv) {
   const bool keyed = argc > 1 && !strcmp(argv[1], "keyed");
   // argv[1] == "oct": Ed25519 records through the 8-lane verifier (oct.h)
   const bool oct = argc > 1 && !strcmp(argv[1], "oct");
+  // argv[1] == "quad2" / "oct2": the split kernels' path -- the scalars and
+  // [u]B (q_prepare, q_bcomb16) computed once as the helper wave would, the
+  // quad / oct verifier taking them through its callbacks
+  const bool quad2 = argc > 1 && !strcmp(argv[1], "quad2");
+  const bool oct2 = argc > 1 && !strcmp(argv[1], "oct2");
   std::vector<uint32_t> bcomb;
   std::map<std::string, std::pair<bool, std::vector<uint32_t>>> combs;
   if (keyed) {
@@ -178,6 +183,34 @@ int main(int argc, char** argv) {
     Exchange ex;
     bool res[8];
     std::vector<std::thread> th;
+    SigPrep hp;
+    uint32_t bpt[40];
+    if (quad2 || oct2) {
+      q_prepare(hp, pkw, sigw, mp, mlen, false);
+      ge_p3 Bp;
+      q_bcomb16(Bp, hp.u, bt);
+      bpoint_store(bpt, Bp);
+    }
+    auto get_prep = [&](SigPrep& p) { p = hp; };
+    if (quad2 || oct2) {
+      ex.bar.n = oct2 ? 8 : 4;
+      for (int l = 0; l < (oct2 ? 8 : 4); l++)
+        th.emplace_back([&, l] {
+          QArrayTab ta, tr;
+          auto get_b = [&](fe& c) {
+            for (int j = 0; j < 10; j++) c.v[j] = bpt[10 * (l & 3) + j];
+          };
+          if (oct2) {
+            HostOct q{l, &ex};
+            res[l] = mode ? o_verify_split<MODE_ZIP215, true>(q, pkw, sigw, bt, ta, get_prep, get_b)
+                          : o_verify_split<MODE_GO_STDLIB, true>(q, pkw, sigw, bt, ta, get_prep, get_b);
+          } else {
+            HostQuad q{l, &ex};
+            res[l] = mode ? q_verify_split<MODE_ZIP215, true>(q, pkw, sigw, bt, ta, tr, get_prep, get_b)
+                          : q_verify_split<MODE_GO_STDLIB, true>(q, pkw, sigw, bt, ta, tr, get_prep, get_b);
+          }
+        });
+    }
     if (oct) {
       ex.bar.n = 8;
       for (int l = 0; l < 8; l++)
@@ -188,7 +221,7 @@ int main(int argc, char** argv) {
                         : o_verify<MODE_GO_STDLIB>(q, pkw, sigw, mp, mlen, bt, ta);
         });
     }
-    for (int l = 0; l < (oct ? 0 : 4); l++)
+    for (int l = 0; l < (oct || quad2 || oct2 ? 0 : 4); l++)
       th.emplace_back([&, l] {
         HostQuad q{l, &ex};
         QArrayTab ta, tr;

@@ -95,6 +95,20 @@ def test_oct_pipeline_matches_corpus(quadcheck, corpus, mode):
     assert bad.size == 0, [(idx[int(i)], corpus["cats"][idx[int(i)]]) for i in bad[:10]]
 
 
+@pytest.mark.parametrize("kind", ["quad2", "oct2"])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_split_pipelines_match_corpus(quadcheck, corpus, mode, kind):
+    """The helper-wave kernels' path: scalars and [u]B (the 16-position
+    radix-2^16 comb, q_bcomb16) computed once per signature as the helper
+    wave does, the quad / oct verifier taking them through its callbacks
+    (no fixed-base digits in its windows)."""
+    idx = _keyed_subset(corpus)[2::7]
+    got = _run(quadcheck, kind, corpus, idx, mode)
+    want = (corpus["go"] if mode == 0 else corpus["zip215"])[idx]
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(idx[int(i)], corpus["cats"][idx[int(i)]]) for i in bad[:10]]
+
+
 @pytest.mark.parametrize("mode", [0, 1])
 def test_quad_pipeline_matches_corpus(quadcheck, corpus, mode):
     """The 4-lane quad kernel's source (quad.h), four host threads in lockstep

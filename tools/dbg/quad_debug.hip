@@ -101,13 +101,7 @@ __global__ __launch_bounds__(64, 1) void k_time(const uint32_t* pk, const uint32
 
 __global__ void k_btab(uint32_t* rows) {  // the library's k_btab_init
   const int e = blockIdx.x * 64 + threadIdx.x;
-  if (e >= BT16_BASE + BT16_ROWS) return;
-  if (e < BT16_BASE) {
-    btab_entry(rows + e * BTAB_ROW_WORDS, e % BTAB_ENTRIES + 1, e / BTAB_ENTRIES);
-  } else {
-    const int f = e - BT16_BASE;
-    btab_entry_shift(rows + e * BTAB_ROW_WORDS, f % BT16_ENTRIES + 1, bt16_block_shift(f / BT16_ENTRIES), 16);
-  }
+  if (e < BTAB_TOTAL_ROWS) btab_row(rows + (size_t)e * BTAB_ROW_WORDS, e);
 }
 
 template <int VAR>
@@ -218,14 +212,14 @@ int main() {
   (void)hipMalloc(&dpk, 32);
   (void)hipMalloc(&dsig, 64);
   (void)hipMalloc(&dmsg, 16);
-  (void)hipMalloc(&dbt, (size_t)(BT16_BASE + BT16_ROWS) * BTAB_ROW_WORDS * 4);
+  (void)hipMalloc(&dbt, (size_t)BTAB_TOTAL_ROWS * BTAB_ROW_WORDS * 4);
   (void)hipMalloc(&dsn, NSNAP * 40 * 4);
   (void)hipMalloc(&dv, 64 * 4);
   (void)hipMemcpy(dpk, pk, 32, hipMemcpyHostToDevice);
   (void)hipMemcpy(dsig, sig, 64, hipMemcpyHostToDevice);
   (void)hipMemcpy(dmsg, msg, 4, hipMemcpyHostToDevice);
   // device-built table must equal the host-built one
-  hipLaunchKernelGGL(k_btab, dim3((BT16_BASE + BT16_ROWS + 63) / 64), dim3(64), 0, 0, dbt);
+  hipLaunchKernelGGL(k_btab, dim3((BTAB_TOTAL_ROWS + 63) / 64), dim3(64), 0, 0, dbt);
   std::vector<uint32_t> dbtab(btab.size());
   (void)hipMemcpy(dbtab.data(), dbt, btab.size() * 4, hipMemcpyDeviceToHost);
   printf("btab device==host: %d\n", (int)(dbtab == btab));

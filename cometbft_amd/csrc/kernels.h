@@ -28,7 +28,7 @@ hipError_t launch_comb_build(uint32_t n_keys, const void* keys_pk, uint8_t* keys
 hipError_t launch_verify_keyed(uint32_t mode, uint32_t n, uint32_t n_keys, const void* key_idx, const void* sig,
                                const void* msg, const void* off, const uint32_t* keys_pk, const uint8_t* keys_ok,
                                const uint32_t* ktabs, const uint32_t* bcomb, void* valid, void* bitmap,
-                               bool quad, hipStream_t s);
+                               bool quad, bool split, hipStream_t s);
 hipError_t launch_verify_sr25519(uint32_t n, const void* pk, const void* sig, const void* msg, const void* off,
                                  const uint32_t* btab, uint32_t* atab, const uint16_t* prog, int nops, void* valid,
                                  void* bitmap, uint32_t kflags, hipStream_t s);

@@ -485,10 +485,86 @@ hipError_t launch_comb_build(uint32_t n_keys, const void* keys_pk, uint8_t* keys
   return hipGetLastError();
 }
 
+// Registered-key quads with a helper wave: 3 quad waves (48 signatures) run
+// the 32 fixed-base comb additions, take k from the helper (barrier 1), run
+// the 32 key-comb additions and take R (barrier 2); the helper hashes
+// (q_keyed_challenge) and then decompresses R (q_keyed_decode_r), one lane
+// per signature, so the square-root chain overlaps the additions.
+template <uint32_t MODE>
+__global__ __launch_bounds__(256, 1) void k_verify_keyed_quad_split(
+    uint32_t n, uint32_t n_keys, const uint32_t* __restrict__ key_idx, const uint32_t* __restrict__ sig,
+    const uint8_t* __restrict__ msg, const uint32_t* __restrict__ off, const uint32_t* __restrict__ keys_pk,
+    const uint8_t* __restrict__ keys_ok, const uint32_t* __restrict__ ktabs, const uint32_t* __restrict__ bcomb,
+    uint8_t* __restrict__ out_valid, uint64_t* __restrict__ out_bitmap) {
+  const uint32_t wave = threadIdx.x >> 6, t = threadIdx.x & 63;
+  const uint32_t base = blockIdx.x * 48;
+  __shared__ uint32_t tks[48][9];
+  __shared__ uint32_t rpt[48][31];  // R: x, y, t (10 words each), decode flag
+  if (wave == 3) {
+    const uint32_t s = base + (t < 48 ? t : 47);
+    const uint32_t i = s < n ? s : n - 1;
+    const uint32_t m0 = off[i], m1 = off[i + 1];
+    uint32_t kid = key_idx[i];
+    kid = kid < n_keys ? kid : 0;
+    uint32_t tk[8];
+    q_keyed_challenge(tk, keys_pk + 8 * (size_t)kid, sig + 16 * (size_t)i, msg + m0, m1 - m0);
+    if (t < 48)
+#pragma unroll
+      for (int j = 0; j < 8; j++) tks[t][j] = tk[j];
+    __syncthreads();  // 1: k
+    ge_p3 R;
+    const bool r_ok = q_keyed_decode_r<MODE>(R, sig + 16 * (size_t)i);
+    if (t < 48) {
+#pragma unroll
+      for (int j = 0; j < 10; j++) {
+        rpt[t][j] = R.X.v[j];
+        rpt[t][10 + j] = R.Y.v[j];
+        rpt[t][20 + j] = R.T.v[j];
+      }
+      rpt[t][30] = r_ok ? 1u : 0u;
+    }
+    __syncthreads();  // 2: R
+    return;
+  }
+  const uint32_t ls = wave * 16 + (t >> 2);
+  const uint32_t s = base + ls;
+  const bool active = s < n;
+  const uint32_t i = active ? s : n - 1;
+  uint32_t kid = key_idx[i];
+  const bool kin = kid < n_keys;
+  kid = kin ? kid : 0;
+  DevQuad q;
+  const int lane = (int)(t & 3);
+  bool v = q_verify_keyed_split<MODE>(
+      q, kin && keys_ok[kid] != 0, sig + 16 * (size_t)i, ktabs + (size_t)kid * COMB_TABLE_WORDS, bcomb,
+      [&](uint32_t tk[8]) {
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < 8; j++) tk[j] = tks[ls][j];
+      },
+      [&](fe& rc, bool& r_ok) {
+        __syncthreads();
+        // this lane's coordinate: x, y, 1, t
+        const uint32_t* p = rpt[ls] + 10 * (lane == 3 ? 2 : lane);
+#pragma unroll
+        for (int j = 0; j < 10; j++) rc.v[j] = lane == 2 ? (j == 0 ? 1u : 0u) : p[j];
+        r_ok = rpt[ls][30] != 0;
+      });
+  v = v && active;
+  if (active && (t & 3) == 0 && out_valid) out_valid[s] = v ? 1 : 0;
+  uint64_t x = __ballot(v && (t & 3) == 0) & 0x1111111111111111ull;
+  x = (x | (x >> 3)) & 0x0303030303030303ull;
+  x = (x | (x >> 6)) & 0x000F000F000F000Full;
+  x = (x | (x >> 12)) & 0x000000FF000000FFull;
+  x = (x | (x >> 24)) & 0xFFFFull;
+  const uint32_t slice = blockIdx.x * 3 + wave;
+  if (t == 0 && out_bitmap && slice < 4 * ((n + 63) / 64)) reinterpret_cast<uint16_t*>(out_bitmap)[slice] = (uint16_t)x;
+}
+
 hipError_t launch_verify_keyed(uint32_t mode, uint32_t n, uint32_t n_keys, const void* key_idx, const void* sig,
                                const void* msg, const void* off, const uint32_t* keys_pk, const uint8_t* keys_ok,
                                const uint32_t* ktabs, const uint32_t* bcomb, void* valid, void* bitmap,
-                               bool quad, hipStream_t s) {
+                               bool quad, bool split, hipStream_t s) {
   if (n == 0) return hipSuccess;
   auto ki = static_cast<const uint32_t*>(key_idx);
   auto sgp = static_cast<const uint32_t*>(sig);
@@ -496,6 +572,17 @@ hipError_t launch_verify_keyed(uint32_t mode, uint32_t n, uint32_t n_keys, const
   auto op = static_cast<const uint32_t*>(off);
   auto vp = static_cast<uint8_t*>(valid);
   auto bp = static_cast<uint64_t*>(bitmap);
+  if (quad && split) {
+    const uint32_t slices = 4 * ((n + 63) / 64);
+    const dim3 grid((slices + 2) / 3), block(256);
+    if (mode == MODE_ZIP215)
+      hipLaunchKernelGGL(k_verify_keyed_quad_split<MODE_ZIP215>, grid, block, 0, s, n, n_keys, ki, sgp, mp, op,
+                         keys_pk, keys_ok, ktabs, bcomb, vp, bp);
+    else
+      hipLaunchKernelGGL(k_verify_keyed_quad_split<MODE_GO_STDLIB>, grid, block, 0, s, n, n_keys, ki, sgp, mp, op,
+                         keys_pk, keys_ok, ktabs, bcomb, vp, bp);
+    return hipGetLastError();
+  }
   if (quad) {
     const dim3 grid(((n + 63) / 64) * 4), block(64);
     if (mode == MODE_ZIP215)

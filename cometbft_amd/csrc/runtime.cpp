@@ -494,7 +494,8 @@ static int enqueue_verify_keyed(cmtv_ctx* ctx, CmtvDev& D, const cmtv_keyset::Pe
     const uint32_t cn = (uint32_t)std::min<size_t>(kChunk, n - c);
     e = launch_verify_keyed(mode, cn, (uint32_t)n_keys, d_idx + c, d_sig + 64 * c, d_msg, d_off + c, K.d_pk, K.d_ok,
                             K.d_tab, D.d_bcomb, d_valid ? d_valid + c : nullptr,
-                            d_bitmap ? d_bitmap + c / 64 : nullptr, n <= ctx->keyed_quad_max, s);
+                            d_bitmap ? d_bitmap + c / 64 : nullptr, n <= ctx->keyed_quad_max,
+                            n <= ctx->quad_split_max, s);
     if (e != hipSuccess) {
       D.timing.abandon(tp);
       return hip_fail(e);

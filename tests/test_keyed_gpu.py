@@ -11,10 +11,10 @@ from cometbft_amd import _native as N
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("kernel", ["quad", "lane"])
+@pytest.mark.parametrize("kernel", ["quad2", "quad", "lane"])
 @pytest.mark.parametrize("mode,key", [(MODE_GO_STDLIB, "go"), (MODE_ZIP215, "zip215")])
-def test_corpus_bit_exact_keyed(gpu_ctx, gpu_ctx_lane, corpus, mode, key, kernel):
-    gpu_ctx = gpu_ctx if kernel == "quad" else gpu_ctx_lane
+def test_corpus_bit_exact_keyed(gpu_ctx, gpu_ctx_quad1, gpu_ctx_lane, corpus, mode, key, kernel):
+    gpu_ctx = {"quad2": gpu_ctx, "quad": gpu_ctx_quad1, "lane": gpu_ctx_lane}[kernel]
     pk = corpus["pk"]
     uniq, idx = np.unique(pk, axis=0, return_inverse=True)
     ks = gpu_ctx.register_keys(uniq)
@@ -41,10 +41,10 @@ def _valset_commits(n_keys, n_sigs, seed):
     return pk, kidx, sig, m, off, rng
 
 
-@pytest.mark.parametrize("kernel", ["quad", "lane"])
+@pytest.mark.parametrize("kernel", ["quad2", "quad", "lane"])
 @pytest.mark.parametrize("n", [1, 15, 16, 17, 63, 64, 65, 3000])
-def test_keyed_matches_generic_and_oracle(gpu_ctx, gpu_ctx_lane, n, kernel):
-    gpu_ctx = gpu_ctx if kernel == "quad" else gpu_ctx_lane
+def test_keyed_matches_generic_and_oracle(gpu_ctx, gpu_ctx_quad1, gpu_ctx_lane, n, kernel):
+    gpu_ctx = {"quad2": gpu_ctx, "quad": gpu_ctx_quad1, "lane": gpu_ctx_lane}[kernel]
     pk, kidx, sig, m, off, rng = _valset_commits(150, n, 7 + n)
     sig = sig.copy()
     for i in np.nonzero(rng.random(n) < 0.2)[0]:

@@ -92,10 +92,10 @@ def test_ed25519_wide_in_mixed_waves(gpu_ctx, gpu_ctx_oct1, gpu_ctx_quad, gpu_ct
     assert [int(x) for x in alone] == [v[key] for v in vs]
 
 
-@pytest.mark.parametrize("kernel", ["quad", "lane"])
+@pytest.mark.parametrize("kernel", ["quad2", "quad", "lane"])
 @pytest.mark.parametrize("mode", [MODE_GO_STDLIB, MODE_ZIP215])
-def test_ed25519_wide_keyed(gpu_ctx, gpu_ctx_lane, kernel, mode):
-    ctx = gpu_ctx if kernel == "quad" else gpu_ctx_lane
+def test_ed25519_wide_keyed(gpu_ctx, gpu_ctx_quad1, gpu_ctx_lane, kernel, mode):
+    ctx = {"quad2": gpu_ctx, "quad": gpu_ctx_quad1, "lane": gpu_ctx_lane}[kernel]
     pk, sig, m, off = _mixed_batch("ed25519", seed=4)
     uniq, idx = np.unique(pk, axis=0, return_inverse=True)
     ks = ctx.register_keys(uniq)

@@ -517,7 +517,9 @@ static int enqueue_verify_keyed(cmtv_ctx* ctx, CmtvDev& D, const cmtv_keyset::Pe
 // copies (a context over a repeated device ordinal). Enqueued on the device
 // streams.
 static int gather_bitmaps(cmtv_ctx* ctx, size_t G, size_t W, uint64_t* const* bufs) {
-  if (G <= 1) return CMTV_OK;
+  // one device: nothing to exchange, unless CMTV_FORCE_RCCL gave it a
+  // one-rank communicator (the RCCL path exercised on a one-GPU box)
+  if (G <= 1 && !ctx->rccl) return CMTV_OK;
   ctx->stats.gathers++;
   if (ctx->rccl) {
     const Rccl& R = rccl();
@@ -968,6 +970,17 @@ static int open_ctx(const cmtv_config* cfg, const std::vector<int>& ords, cmtv_c
     }
   }
   ctx->stats.n_devices = (uint32_t)ords.size();
+  // CMTV_FORCE_RCCL (test knob): an RCCL communicator even over one device,
+  // so a one-GPU box runs the library's RCCL init and all-gather calls
+  const bool force_rccl = std::getenv("CMTV_FORCE_RCCL") != nullptr;
+  if (ords.size() == 1 && force_rccl) {
+    const Rccl& R = rccl();
+    ncclComm_t comm = nullptr;
+    if (R.ok && R.CommInitAll(&comm, 1, ords.data()) == 0) {
+      ctx->devs[0].comm = comm;
+      ctx->rccl = true;
+    }
+  }
   if (ords.size() > 1) {
     std::vector<int> sorted = ords;
     std::sort(sorted.begin(), sorted.end());

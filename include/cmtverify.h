@@ -102,7 +102,9 @@ typedef struct cmtv_stats {
  * (40000) 4 lanes, larger ones one lane), CMTV_FAULT_AT=N (test knob: the N-th verification
  * launch of the context fails with CMTV_EHIP without running; libs/fail
  * FAIL_TEST_INDEX analogue), CMTV_FORCE_WIDE=1 (test knob: the quad kernels
- * take the 64-window half-scalar fallback for every signature). */
+ * take the 64-window half-scalar fallback for every signature),
+ * CMTV_FORCE_RCCL=1 (test knob: a one-rank RCCL communicator even over one
+ * device, so a one-GPU box exercises the RCCL init and all-gather). */
 int cmtv_open(const cmtv_config* cfg, cmtv_ctx** out);
 
 /* Opens ONE context over several devices (a node is one

@@ -143,6 +143,37 @@ def test_sharded_device_api_over_a_repeated_device():
             assert np.array_equal(bits[:n], exp[h]) and not bits[n:].any()
 
 
+def test_rccl_path_on_one_device():
+    """CMTV_FORCE_RCCL: a one-rank RCCL communicator over device 0, so the
+    library's RCCL init (ncclCommInitAll) and its in-place grouped all-gather
+    of the bitmap run on a one-GPU box; verdicts and bitmap vs the oracle."""
+    import torch
+
+    with _env(CMTV_FORCE_RCCL=1):
+        ctx = Context(devices=[0])
+    assert ctx.stats()["rccl"] == 1
+    dev = torch.device("cuda:0")
+    n = 1500
+    pk, kidx, sig, m, off = _batch(n, 77)
+    sig = sig.copy()
+    sig[::17, 5] ^= 1
+    exp = coracle.verify_batch(pk[kidx], sig, m, off, MODE_GO_STDLIB, nthreads=16)
+    t = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in
+         {"pk": pk[kidx], "sig": sig, "m": m, "off": off.view(np.int32)}.items()}
+    W = (n + 63) // 64
+    out = torch.full((W,), -1, dtype=torch.int64, device=dev)
+    valid = torch.zeros(n, dtype=torch.uint8, device=dev)
+    w = ctx.verify_sharded_device([n], [t["pk"].data_ptr()], [t["sig"].data_ptr()], [t["m"].data_ptr()],
+                                  [t["off"].data_ptr()], MODE_GO_STDLIB, [out.data_ptr()], [valid.data_ptr()])
+    ctx.sync()
+    assert w == W and ctx.stats()["gathers"] >= 1
+    assert np.array_equal(valid.cpu().numpy(), exp)
+    bits = np.unpackbits(out.cpu().numpy().view(np.uint64).view(np.uint8), bitorder="little")
+    assert np.array_equal(bits[:n], exp) and not bits[n:].any()
+    got = ctx.verify(pk[kidx], sig, m, off, MODE_GO_STDLIB)
+    assert np.array_equal(got, exp)
+
+
 def test_fault_injection_knob():
     with _env(CMTV_FAULT_AT=3):
         ctx = Context(device=0)

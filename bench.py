@@ -72,7 +72,7 @@ def parse():
     ap.add_argument("--mode", choices=["go", "zip215"], default="go")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU-seconds of oracle work for cpu_baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--latency-iters", type=int, default=200)
+    ap.add_argument("--latency-iters", type=int, default=1000)
     ap.add_argument("--no-latency", action="store_true")
     ap.add_argument("--no-c3", action="store_true", help="skip the configs[2] 15M-signature replay side line")
     ap.add_argument("--c3-heights", type=int, default=100_000, help="configs[2] commits (150 validators each)")
@@ -556,7 +556,7 @@ def latency_150(ctx, mode, iters):
         return round(float(np.percentile(ts, 50)), 4), round(float(np.percentile(ts, 99)), 4)
 
     def measure(fn):
-        for _ in range(20):
+        for _ in range(50):  # 1000 iterations, 50 warm-up
             fn()
         ts = []
         for _ in range(iters):
@@ -589,6 +589,23 @@ def latency_150(ctx, mode, iters):
         cts.append(time.perf_counter() - t)
     res["cpu_single_core_p50_ms"] = round(float(np.median(cts)) * 1e3, 3)
     return res
+
+
+def load_valu_busy(n=10_000, kernel="k_verify_quad_split<0u>"):
+    """VALUBusy (SQ_ACTIVE_INST_VALU-based, chip-wide) of the bench's verify
+    kernel at the step's size, from the committed PMC summary of the bench
+    command (profiles/r02_pmc_sq.json, tools/pmc_summary.py)."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "r02_pmc_sq.json")) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    waves = 4 * ((4 * ((n + 63) // 64) + 2) // 3)  # the split kernel's grid for n signatures
+    for k, v in d.items():
+        if kernel in k and f"grid={waves} waves" in k and "valu_busy_pct" in v:
+            return {"valu_busy_pct": v["valu_busy_pct"], "valu_insts_per_wave": v.get("valu_insts_per_wave"),
+                    "source": "profiles/r02_pmc_sq.json", "kernel": k}
+    return None
 
 
 def load_traffic():
@@ -723,6 +740,7 @@ def main():
         "roofline": {"bound": "valu_int", "achieved": round(achieved, 3), "peak": INT_MAC_PEAK_T,
                      "unit": "TMAC/s", "frac": round(achieved / INT_MAC_PEAK_T, 4),
                      "traffic": traffic, "traffic_source": tfile, "kernel_ms": round(kernel_ms, 4),
+                     "valu_utilisation": load_valu_busy(args.n),
                      "work": f"{MACS_PER_VERIFY} int32 MACs/verify x {args.n} verifies per launch",
                      "timing": "libcmtverify HIP events on the launch stream, mean over the timed launches"},
     }

@@ -9,6 +9,7 @@ figures (VALU instructions per wave, wave cycles per wave, VALU issue share
 of wave time, wait share).
 """
 import csv
+import json
 import os
 import sys
 from collections import defaultdict
@@ -56,6 +57,20 @@ def main():
             lines.append(f"  -> VALUBusy (chip, %)        {busy:12.1f}")
     with open(out, "w") as f:
         f.write("\n".join(lines) + "\n")
+    # the derived figures as JSON beside the text (bench.py reads VALUBusy)
+    derived = {}
+    for k, cs in merged.items():
+        w = cs.get("SQ_WAVES")
+        dd = {"dispatches": disp[k]}
+        if w and "SQ_INSTS_VALU" in cs:
+            dd["valu_insts_per_wave"] = round(cs["SQ_INSTS_VALU"] / w)
+        if w and "SQ_WAVE_CYCLES" in cs:
+            dd["wave_cycles_per_wave"] = round(4 * cs["SQ_WAVE_CYCLES"] / w)
+        if "SQ_ACTIVE_INST_VALU" in cs and cs.get("GRBM_GUI_ACTIVE"):
+            dd["valu_busy_pct"] = round(100 * cs["SQ_ACTIVE_INST_VALU"] * 4 / 1024 / (cs["GRBM_GUI_ACTIVE"] / 8), 1)
+        derived[k] = dd
+    with open(os.path.splitext(out)[0] + ".json", "w") as f:
+        json.dump(derived, f, indent=1)
     print("\n".join(lines[:60]))
 
 

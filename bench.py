@@ -707,7 +707,12 @@ def main():
 
     torch.cuda.set_device(0)
     mode = 0 if args.mode == "go" else 1
-    ctx = Context(devices=list(range(n_dev)))
+    # CMTV_BENCH_DEVICES="0,0" rehearses the N-device flow on fewer GPUs
+    # (a repeated ordinal: peer-copy gathers instead of RCCL)
+    env_devs = os.environ.get("CMTV_BENCH_DEVICES")
+    ordinals = [int(x) for x in env_devs.split(",")] if env_devs else list(range(n_dev))
+    assert len(ordinals) == n_dev, (ordinals, n_dev)
+    ctx = Context(devices=ordinals)
     D = Devices(ctx, n_dev, args.n)
     elapsed, kernel_ms = timed_steps(ctx, lambda: D.step(ctx, mode), args.steps, args.warmup, barrier)
     ok = D.verdicts_ok()

@@ -52,6 +52,23 @@ def test_device_keygen_and_signing_match_oracle(gpu_ctx):
     assert np.array_equal(gpu_ctx.sign(seeds, m, off), sig)
 
 
+def test_bench_signer_matches_oracle_at_commit_scale(gpu_ctx):
+    """The bench's workloads are signed by the device (k_sign): pin it byte
+    for byte against the C oracle's RFC 8032 signer at the 10k-commit shape
+    (10,000 CanonicalVote-sized messages over 1,000 keys), so the bench's
+    verdict check is not self-consistency only."""
+    n, nk = 10_000, 1_000
+    rng = np.random.default_rng(2024)
+    seeds = rng.integers(0, 256, (nk, 32), dtype=np.uint8)
+    kidx = rng.integers(0, nk, n).astype(np.uint32)
+    msgs = [rng.integers(0, 256, 110 + int(rng.integers(0, 12)), dtype=np.uint8).tobytes() for _ in range(n)]
+    m, off = coracle.pack_msgs(msgs)
+    assert np.array_equal(gpu_ctx.pubkeys(seeds), coracle.pubkeys_from_seeds(seeds))
+    dev = gpu_ctx.sign(seeds, m, off, key_idx=kidx)
+    ref = coracle.sign_batch(seeds, m, off, key_idx=kidx, nthreads=8)
+    assert np.array_equal(dev, ref), np.nonzero((dev != ref).any(axis=1))[0][:10]
+
+
 @pytest.mark.parametrize("kernel", ["oct2", "oct", "quad2", "quad", "lane"])
 @pytest.mark.parametrize("n", [1, 2, 15, 16, 17, 63, 64, 65, 127, 1000])
 def test_ragged_sizes_honest_and_flipped(gpu_ctx, gpu_ctx_oct1, gpu_ctx_quad, gpu_ctx_quad1, gpu_ctx_lane, n, kernel):

@@ -122,3 +122,25 @@ def test_reference_keygen_vector():
         assert bytes(coracle.pubkeys_from_seeds(np.frombuffer(seed, np.uint8))[0]) == want
         sig = E.sign(seed, b"cmtverify")
         assert E.verify(want, b"cmtverify", sig)
+
+
+def test_zip215_small_order_matrix_all_valid(corpus):
+    """ZIP-215 (the rule CometBFT adopts, spec/core/encoding.md:56) publishes
+    one requirement that pins the cofactored verifier independently of this
+    repo: for all 14 encodings of the 8 small-order points (8 canonical, 6
+    non-canonical y >= p), every (A, R) pair with s = 0 must verify -- 196
+    signatures. Both oracles must accept all of them in ZIP-215 mode, and the
+    stored verdicts the GPU parity tests check against must say so too."""
+    idx = [i for i, c in enumerate(corpus["cats"]) if c == "small_order_s0"]
+    assert len(idx) == 196
+    pks = {bytes(corpus["pk"][i]) for i in idx}
+    rs = {bytes(corpus["sig"][i][:32]) for i in idx}
+    assert len(pks) == 14 and rs == pks
+    assert all(not any(corpus["sig"][i][32:]) for i in idx)
+    assert all(corpus["zip215"][i] == 1 for i in idx)
+    sel = np.array(idx)
+    m, off = coracle.pack_msgs([corpus["msgs"][i] for i in idx])
+    out = coracle.verify_batch(corpus["pk"][sel], corpus["sig"][sel], m, off, 1, nthreads=4)
+    assert out.tolist() == [1] * 196
+    for i in idx[::13]:
+        assert E.verify(bytes(corpus["pk"][i]), corpus["msgs"][i], bytes(corpus["sig"][i]), E.MODE_ZIP215)

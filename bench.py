@@ -228,7 +228,19 @@ class Devices:
         return True
 
 
-def timed_steps(ctx, fn, steps, warmup, barrier):
+# The GPU leaves its idle clock state only after some milliseconds of load: the
+# first 50 configs[1] steps after a 1 s pause average 0.2637 ms of kernel time,
+# every later block 0.2545 ms (tools/clock_probe.py, profiles/r02_clock_probe.txt).
+# The warm-up therefore runs back-to-back steps for at least CLOCK_SETTLE_S
+# before its W counted steps; the timed region itself is unchanged.
+CLOCK_SETTLE_S = 0.1
+
+
+def timed_steps(ctx, fn, steps, warmup, barrier, settle_s=CLOCK_SETTLE_S):
+    t_settle = time.perf_counter() + settle_s
+    while time.perf_counter() < t_settle:
+        fn()
+        ctx.sync()
     for _ in range(warmup):
         fn()
     ctx.sync()
@@ -740,6 +752,7 @@ def main():
                                "verdict bitmaps inside libcmtverify when N>1)",
                    "sigs_per_gpu": args.n, "mode": args.mode, "msg_bytes_mean": round(D.msg_bytes_mean, 1),
                    "parallelism": f"dp{n_dev} (single process, cmtv_open_devices)",
+                   "warmup_clock_settle_s": CLOCK_SETTLE_S,
                    "collective": ("rccl" if st["rccl"] else "peer-copy") if n_dev > 1 else "none",
                    "verdicts_ok": bool(ok)},
         "roofline": {"bound": "valu_int", "achieved": round(achieved, 3), "peak": INT_MAC_PEAK_T,

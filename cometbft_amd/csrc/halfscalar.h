@@ -10,24 +10,27 @@
 // extended Euclid on (8L, k) yields such a pair with |k1|, |k2| ~ 2^127
 // (Antipa et al., "Accelerated verification of ECDSA signatures", SAC 2005;
 // Pornin, "Optimized lattice basis reduction in dimension 2", 2020), which
-// halves the doublings of the variable-base part: 34 four-bit windows shared
+// halves the doublings of the variable-base part: 33 four-bit windows shared
 // by A, R and the two halves of the fixed-base scalar instead of 64.
 //
 // Exactness (the verdicts must equal Go 1.19 crypto/ed25519.Verify's,
 // /root/reference/crypto/ed25519/ed25519.go:148-155):
-//   * k2 is chosen ODD, and 0 < |k2| < L, so gcd(k2, 8L) = 1 and
-//     [k2]X = O  <=>  X = O.  Cofactorless (GO_STDLIB) mode therefore checks
-//     R' == R exactly; with R canonical this is encode(R') == R bytes.
-//   * ZIP215 mode checks [8][k2](R' - R) = O  <=>  [8](R' - R) = O.
-//   * The window count follows the pair's size: 34 windows hold pairs up to
-//     134 bits (all but ~5.5e-5 of random k), 35 / 36 / 37 windows up to
-//     138 / 142 / 146 bits. Only if no odd-k2 pair fits 146 bits (about
-//     1e-6), or a quotient >= 2^31 appears, is the decomposition marked
-//     `wide`: the caller then uses k1 = k, k2 = 1 over 64 windows -- the same
-//     equation, so no input changes its verdict, only its cost. (The window
-//     count is uniform over a wave, so with a plain 34-or-64 rule one such
-//     signature in a 10k commit -- ~40% of commits -- made its whole wave run
-//     64 windows.)
+//   * GO_STDLIB (odd_k2): k2 is chosen ODD, and 0 < |k2| < L, so
+//     gcd(k2, 8L) = 1 and [k2]X = O  <=>  X = O. Cofactorless mode therefore
+//     checks R' == R exactly; with R canonical this is encode(R') == R bytes.
+//   * ZIP215 checks [8][k2](R' - R) = O  <=>  [8](R' - R) = O, which needs
+//     only L not dividing k2 (0 < |k2| < L): any parity will do, so the
+//     shorter of the two reduced basis vectors is taken -- never above 128
+//     bits in 3e5 random k, against 1.2% above 130 bits for the odd choice.
+//   * The window count follows the pair's size: 33 windows hold pairs up to
+//     130 bits (every ZIP-215 pair; all but 1.2% of odd pairs), 34 / 35 /
+//     36 / 37 windows up to 134 / 138 / 142 / 146 bits. Only if no pair fits
+//     146 bits (odd: about 1e-6), or a quotient >= 2^31 appears, is the
+//     decomposition marked `wide`: the caller then uses k1 = k, k2 = 1 over
+//     64 windows -- the same equation, so no input changes its verdict, only
+//     its cost. (The window count is uniform over a wave, so with a plain
+//     fixed-or-64 rule one such signature in a 10k commit -- ~40% of
+//     commits -- made its whole wave run 64 windows.)
 //
 // Arithmetic: the Euclid runs on 8-word values kept left-normalised (r0's top
 // bit at bit 255, both remainders shifted by the same e) and t values in
@@ -50,10 +53,10 @@
 
 namespace cmtv {
 
-constexpr int HS_WINDOWS = 34;      // 4-bit windows for normal pairs (136 bits)
+constexpr int HS_WINDOWS = 33;      // 4-bit windows for normal pairs (132 bits)
 constexpr int HS_MAX_WINDOWS = 37;  // graded: up to 37 windows before the wide fallback
 constexpr int HS_WIDE_WINDOWS = 64; // k1 = k, k2 = 1
-constexpr int HS_MAX_BITS = 134;    // (2^134 + bias) < 16^34 for the signed-digit bias
+constexpr int HS_MAX_BITS = 130;    // (2^130 + bias) < 16^33 for the signed-digit bias
 // windows for a pair of `bits` bits: (2^bits + bias) < 16^W  <=>  bits <= 4W - 2
 CMTV_HD int hs_windows_for(int bits) { return bits <= HS_MAX_BITS ? HS_WINDOWS : (bits + 5) / 4; }
 constexpr int HS_MAX_ROUNDS = 192;  // outer rounds before giving up (Lehmer: ~10; exact steps: ~75)
@@ -64,7 +67,7 @@ struct HalfScalars {
   uint32_t k2[8];  // |k2|, odd
   bool k2_neg;
   bool wide;
-  int windows;     // 34..37 (the pair's size), HS_WIDE_WINDOWS when wide
+  int windows;     // 33..37 (the pair's size), HS_WIDE_WINDOWS when wide
 };
 
 CMTV_HD uint32_t hs_N(int i) {  // 8L
@@ -275,13 +278,14 @@ CMTV_HD void hs_lin(uint32_t out[W], int32_t P, const uint32_t x[], int32_t Q, c
   }
 }
 
-// (k1, k2) with k1 == k2 k (mod 8L), k2 odd, both < 2^134, or wide.
+// (k1, k2) with k1 == k2 k (mod 8L), k2 odd if odd_k2, both < 2^146, or wide.
 // LEHMER = false: one exact Euclid step per round (the schedule the host test
 // compares against); both give the same pair.
 // force_wide: take the wide schedule regardless (CMTV_FORCE_WIDE test knob,
 // so the 64-window path -- ~never reached by real k -- is exercised)
+// odd_k2: the cofactorless (GO_STDLIB) requirement; ZIP215 passes false
 template <bool LEHMER = true>
-CMTV_HD void half_scalars(HalfScalars& h, const uint32_t k[8], bool force_wide = false) {
+CMTV_HD void half_scalars(HalfScalars& h, const uint32_t k[8], bool force_wide = false, bool odd_k2 = true) {
   uint32_t r0[8], r1[8], t0[6], t1[6];
 #pragma unroll
   for (int i = 0; i < 8; i++) {
@@ -358,15 +362,16 @@ CMTV_HD void half_scalars(HalfScalars& h, const uint32_t k[8], bool force_wide =
     e += sh;
   }
 
-  // candidates with odd t: (r1, t1); else (r0, t0) [t0 odd then] or one more
-  // step (r2, t2) [t2 = t0 - q t1 odd then]
+  // odd_k2: candidates with odd t: (r1, t1); else (r0, t0) [t0 odd then] or
+  // one more step (r2, t2) [t2 = t0 - q t1 odd then]. Any parity: the
+  // shorter of (r1, t1) and (r0, t0) (t0 = 0 only while r0 = 8L).
   bool n1, n0, n2;
   const int b1 = hs_bitlen6s(t1, n1);
   const int c1 = (hs_bitlen8(r1) - e) > b1 ? (hs_bitlen8(r1) - e) : b1;
   const bool t1_odd = t1[0] & 1;
   uint32_t r2[8], t2[6];
   bool ok2 = false;
-  if (ok && !t1_odd) ok2 = hs_step(r2, t2, r0, r1, t0, t1);
+  if (ok && !t1_odd && odd_k2) ok2 = hs_step(r2, t2, r0, r1, t0, t1);
   const int br0 = hs_bitlen8(r0) - e, bt0 = hs_bitlen6s(t0, n0);
   const int c0 = br0 > bt0 ? br0 : bt0;
   int c2 = 1 << 20;
@@ -374,8 +379,8 @@ CMTV_HD void half_scalars(HalfScalars& h, const uint32_t k[8], bool force_wide =
     const int br2 = hs_bitlen8(r2) - e, bt2 = hs_bitlen6s(t2, n2);
     c2 = br2 > bt2 ? br2 : bt2;
   }
-  // choose: 1 if t1 odd, else the smaller of 0 and 2
-  const int pick = t1_odd ? 1 : (c2 < c0 ? 2 : 0);
+  // choose: 1 if t1 odd, else the smaller of 0 and 2 (any parity: of 1 and 0)
+  const int pick = odd_k2 ? (t1_odd ? 1 : (c2 < c0 ? 2 : 0)) : (c1 <= c0 ? 1 : 0);
   const int cost = pick == 1 ? c1 : (pick == 2 ? c2 : c0);
   h.wide = force_wide || !ok || cost > 4 * HS_MAX_WINDOWS - 2;
   h.windows = h.wide ? HS_WIDE_WINDOWS : hs_windows_for(cost);
@@ -440,7 +445,7 @@ CMTV_HD void hs_bscalar(uint32_t u[8], const uint32_t k2mag[8], bool neg, const 
 CMTV_HD void hs_digits16(uint32_t t[8], const uint32_t x[8], int W) {
   uint32_t a[8], b[8];
   sc_bias(a, x, 0x88888888u);
-  // W nibbles of 8: words 0-3 whole, word 4 holds W - 32 (2..5) of them
+  // W nibbles of 8: words 0-3 whole, word 4 holds W - 32 (1..5) of them
   const uint32_t w4 = 0x88888888u & ((1u << (4 * (W - 32))) - 1u);
   uint64_t c = 0;
 #pragma unroll
@@ -450,7 +455,7 @@ CMTV_HD void hs_digits16(uint32_t t[8], const uint32_t x[8], int W) {
     b[i] = (uint32_t)v;
     c = v >> 32;
   }
-  // b < 2^(4W): shift left by 4 (64 - W) = 96 + bs bits, bs = 4 (40 - W) in 12..24
+  // b < 2^(4W): shift left by 4 (64 - W) = 96 + bs bits, bs = 4 (40 - W) in 12..28
   const int bs = 4 * (40 - (W > HS_MAX_WINDOWS ? HS_MAX_WINDOWS : W));
 #pragma unroll
   for (int i = 0; i < 8; i++) {

@@ -179,7 +179,7 @@ __global__ __launch_bounds__(256, CMTV_QUAD_WAVES_PER_EU) void k_verify_quad_spl
     const uint32_t i = s < n ? s : n - 1;
     const uint32_t m0 = off[i], m1 = off[i + 1];
     SigPrep p;
-    q_prepare(p, pk + 8 * (size_t)i, sig + 16 * (size_t)i, msg + m0, m1 - m0, force_wide != 0);
+    q_prepare<MODE>(p, pk + 8 * (size_t)i, sig + 16 * (size_t)i, msg + m0, m1 - m0, force_wide != 0);
     if (t < 48) sig_prep_store(prep[t], p);
     __syncthreads();  // 1: the scalars, as the quad waves finish decoding
     ge_p3 B;
@@ -241,7 +241,7 @@ __global__ __launch_bounds__(128, CMTV_QUAD_WAVES_PER_EU) void k_verify_oct_spli
   if (threadIdx.x >= 64) {
     const uint32_t m0 = off[i], m1 = off[i + 1];
     SigPrep p;
-    q_prepare(p, pk + 8 * (size_t)i, sig + 16 * (size_t)i, msg + m0, m1 - m0, force_wide != 0);
+    q_prepare<MODE>(p, pk + 8 * (size_t)i, sig + 16 * (size_t)i, msg + m0, m1 - m0, force_wide != 0);
     if ((t & 7) == 0) sig_prep_store(prep[t >> 3], p);
     __syncthreads();  // 1: the scalars
     ge_p3 B;

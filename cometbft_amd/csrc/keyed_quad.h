@@ -106,15 +106,8 @@ CMTV_HD bool q_verify_keyed_split(const Q& q, bool key_ok, const uint32_t* sig_p
   q_to_cached(q, c, rc);
   q_cached_cneg(q, c, true);
   q_add(q, v, c);
-#pragma unroll 1
-  for (int d = 0; d < 3; d++) q_dbl(q, v);
-  fe z;
-  q.template perm<QP_B2>(z, v);
-  const bool x0 = fe_iszero(v);    // lane 0
-  const bool yz = fe_equal(v, z);  // lane 1
-  const bool e0 = q.template perm32<QP_B0>(x0 ? 1u : 0u) != 0;
-  const bool e1 = q.template perm32<QP_B1>(yz ? 1u : 0u) != 0;
-  return ok && e0 && e1;
+  const bool so = q_small_order(q, v);  // [8](R' - R) = O; every lane takes part in its DPP moves
+  return ok && so;
 }
 
 // One wave does everything (k_verify_keyed_quad; the host checks): every

@@ -134,8 +134,8 @@ CMTV_HD bool o_verify_split(const Q& q, const uint32_t* pk_ptr, const uint32_t* 
 
   // ---- final check (quad.h q_verify): X = O / [8]X = O
   if (MODE == MODE_ZIP215) {
-#pragma unroll 1
-    for (int d = 0; d < 3; d++) q_dbl(q, v);
+    const bool so = q_small_order(q, v);  // every lane takes part in its DPP moves
+    return s_ok && a_ok && r_ok && so;
   }
   fe z;
   q.template perm<QP_B2>(z, v);
@@ -143,8 +143,7 @@ CMTV_HD bool o_verify_split(const Q& q, const uint32_t* pk_ptr, const uint32_t* 
   const bool yz = fe_equal(v, z);
   const bool e0 = q.template perm32<QP_B0>(x0 ? 1u : 0u) != 0;
   const bool e1 = q.template perm32<QP_B1>(yz ? 1u : 0u) != 0;
-  if (MODE == MODE_GO_STDLIB) return s_ok && a_ok && r_ok && r_canon && e0 && e1;
-  return s_ok && a_ok && r_ok && e0 && e1;
+  return s_ok && a_ok && r_ok && r_canon && e0 && e1;
 }
 
 // One wave does everything (k_verify_oct; the host check)
@@ -152,7 +151,7 @@ template <uint32_t MODE, class Q, class BTab, class ATab>
 CMTV_HD bool o_verify(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig_ptr, const uint8_t* msg,
                       uint32_t mlen, const BTab& btab, ATab& tab, bool force_wide = false) {
   return o_verify_split<MODE>(q, pk_ptr, sig_ptr, btab, tab,
-                              [&](SigPrep& p) { q_prepare(p, pk_ptr, sig_ptr, msg, mlen, force_wide); });
+                              [&](SigPrep& p) { q_prepare<MODE>(p, pk_ptr, sig_ptr, msg, mlen, force_wide); });
 }
 
 }  // namespace cmtv

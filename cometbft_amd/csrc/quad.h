@@ -177,6 +177,23 @@ CMTV_HD void q_negate_lane3(fe& c, int lane, bool neg) {
   for (int i = 0; i < 10; i++) c.v[i] = f ? fe_p2(i) - c.v[i] : c.v[i];
 }
 
+// ZIP-215's [8]P = O for the quad's extended point v (lane c: coordinate c).
+// The torsion of edwards25519 is cyclic of order 8, so [8]P = O <=> [2]P is in
+// E[4] = {(0, 1), (0, -1), (+/-sqrt(-1), 0)}, the points with xy = 0, i.e.
+// T([2]P) = 0; and the doubling gives T([2]P) = 2XY (X^2 + Y^2) (ref10's
+// p2_dbl: (A - XX - YY)(XX + YY)). So [8]P = O <=> T = 0 or X^2 + Y^2 = 0:
+// one squaring round instead of three doublings.
+template <class Q>
+CMTV_HD bool q_small_order(const Q& q, const fe& v) {
+  fe s, x2, y2;
+  fe_sq(s, v);  // lane 0: X^2, lane 1: Y^2
+  q.template perm<QP_B0>(x2, s);
+  q.template perm<QP_B1>(y2, s);
+  fe_add(s, x2, y2);
+  const bool t0 = q.template perm32<QP_B3>(fe_iszero(v) ? 1u : 0u) != 0;  // T, from lane 3
+  return t0 || fe_iszero(s);
+}
+
 // This lane's cached coordinate of (neg ? -P : P) for P an affine niels row
 // (y+x at word 0, y-x at word ymx_off, 2dxy at word xy_off), or of the
 // identity when ident. ld(off, c) loads the 10 limbs at word `off`.
@@ -217,7 +234,7 @@ namespace cmtv {
 //            against (1..128)B on even windows, of its high half against
 //            (1..128)[2^124]B on odd ones)
 //   final  : X = [k2](R' - R) is O (GO_STDLIB, with R canonical: encode(R')
-//            == R bytes; no inversion) or [8]X = O (ZIP215)
+//            == R bytes; no inversion) or [8]X = O (ZIP215, q_small_order)
 // (0..8)P in cached form (entry 0 = the identity), one coordinate per lane;
 // v holds this lane's coordinate of P and is clobbered.
 template <class Q, class ATab>
@@ -274,9 +291,10 @@ struct SigPrep {
 };
 constexpr int SIG_PREP_WORDS = 25;
 
-CMTV_HD void q_prepare_scalars(SigPrep& p, const uint32_t k[8], const uint32_t ts[8], bool force_wide) {
+CMTV_HD void q_prepare_scalars(SigPrep& p, const uint32_t k[8], const uint32_t ts[8], bool force_wide,
+                               bool odd_k2 = true) {
   HalfScalars hs;
-  half_scalars(hs, k, force_wide);
+  half_scalars(hs, k, force_wide, odd_k2);
   hs_bscalar(p.u, hs.k2, hs.k2_neg, ts);
 #pragma unroll
   for (int i = 0; i < 8; i++) {
@@ -286,7 +304,9 @@ CMTV_HD void q_prepare_scalars(SigPrep& p, const uint32_t k[8], const uint32_t t
   p.flags = (hs.k2_neg ? 1u : 0u) | (hs.wide ? 2u : 0u) | ((uint32_t)hs.windows << 8);
 }
 
-// s check, k = SHA-512(R || A || M) mod L, then q_prepare_scalars
+// s check, k = SHA-512(R || A || M) mod L, then q_prepare_scalars (k2 odd
+// for the cofactorless check, MODE_GO_STDLIB; any parity for MODE_ZIP215)
+template <uint32_t MODE>
 CMTV_HD void q_prepare(SigPrep& p, const uint32_t* pk_ptr, const uint32_t* sig_ptr, const uint8_t* msg,
                        uint32_t mlen, bool force_wide) {
   uint32_t w[16];
@@ -307,7 +327,7 @@ CMTV_HD void q_prepare(SigPrep& p, const uint32_t* pk_ptr, const uint32_t* sig_p
     sha512_prefixed<16>(h, w, msg, mlen);
     sc_reduce512(k, h);
   }
-  q_prepare_scalars(p, k, ts, force_wide);
+  q_prepare_scalars(p, k, ts, force_wide, MODE != MODE_ZIP215);
   p.flags |= s_ok ? 4u : 0u;
 }
 
@@ -369,7 +389,7 @@ struct NoExtB {
   CMTV_HD void operator()(fe&) const {}
 };
 
-// the wave-uniform window count: the largest over the wave (34..37), 64 if
+// the wave-uniform window count: the largest over the wave (33..37), 64 if
 // any signature is wide
 template <class Q>
 CMTV_HD int q_wave_windows(const Q& q, uint32_t flags) {
@@ -546,8 +566,8 @@ CMTV_HD bool q_verify_split(const Q& q, const uint32_t* pk_ptr, const uint32_t* 
   // ---- final check: X = O (GO_STDLIB: R' == R with R canonical, i.e.
   //      encode(R') == R bytes) / [8]X = O (ZIP215)
   if (MODE == MODE_ZIP215) {
-#pragma unroll 1
-    for (int d = 0; d < 3; d++) q_dbl(q, v);
+    const bool so = q_small_order(q, v);  // every lane takes part in its DPP moves
+    return s_ok && a_ok && r_ok && so;
   }
   fe z;
   q.template perm<QP_B2>(z, v);
@@ -555,8 +575,7 @@ CMTV_HD bool q_verify_split(const Q& q, const uint32_t* pk_ptr, const uint32_t* 
   const bool yz = fe_equal(v, z);  // meaningful on lane 1
   const bool e0 = q.template perm32<QP_B0>(x0 ? 1u : 0u) != 0;
   const bool e1 = q.template perm32<QP_B1>(yz ? 1u : 0u) != 0;
-  if (MODE == MODE_GO_STDLIB) return s_ok && a_ok && r_ok && r_canon && e0 && e1;
-  return s_ok && a_ok && r_ok && e0 && e1;
+  return s_ok && a_ok && r_ok && r_canon && e0 && e1;
 }
 
 // One wave does everything (k_verify_quad; the host checks)
@@ -566,7 +585,7 @@ CMTV_HD bool q_verify(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig_pt
                       bool force_wide = false) {
   return q_verify_split<MODE>(
       q, pk_ptr, sig_ptr, btab, tabA, tabR,
-      [&](SigPrep& p) { q_prepare(p, pk_ptr, sig_ptr, msg, mlen, force_wide); }, NoExtB(), probe);
+      [&](SigPrep& p) { q_prepare<MODE>(p, pk_ptr, sig_ptr, msg, mlen, force_wide); }, NoExtB(), probe);
 }
 
 }  // namespace cmtv

@@ -9,6 +9,7 @@
 //   k  = SHA-512(R || A || M) mod L
 //   R' = [s]B - [k]A      (Straus, shared doublings, fixed windows)
 //   GO_STDLIB: encode(R') == R bytes      ZIP215: [8](R' - decode(R)) == O
+//   (efgh_small_order: no doublings)
 //
 // Scalar multiplication layout (SIMD-uniform schedule):
 //   * [k](-A): signed radix-16 digits in [-8, 7], per-lane table of
@@ -220,6 +221,20 @@ CMTV_HD void build_cached_table(ATab& atab, const ge_p3& P) {
   }
 }
 
+// [8]P = O for P = (ef : gh : fg : eh) in completed form: the torsion is
+// cyclic of order 8, so [8]P = O <=> [2]P is in E[4] (the points with
+// xy = 0) <=> T([2]P) = 2XY (X^2 + Y^2) = 0 <=> T = 0 or X^2 + Y^2 = 0
+// (quad.h q_small_order); T = eh is zero iff e or h is.
+CMTV_HD bool efgh_small_order(const ge_efgh& t) {
+  fe x, y;
+  fe_mul(x, t.e, t.f);
+  fe_mul(y, t.g, t.h);
+  fe_sq(x, x);
+  fe_sq(y, y);
+  fe_add(x, x, y);
+  return fe_iszero(t.e) || fe_iszero(t.h) || fe_iszero(x);
+}
+
 // Final equation against the signature's R bytes (sig_ptr[0..7]):
 //   GO_STDLIB: encode(R') == R bytes (Go bytes.Equal after Point.Bytes)
 //   ZIP215:    [8](R' - decode(R)) == O, R decoded with the same rules as A
@@ -243,15 +258,7 @@ CMTV_HD bool check_R(const ge_p3& Rp, const uint32_t* sig_ptr) {
     ge_efgh t;
     cached_cneg(Rc, true);
     ge_add_cached(t, Rp, Rc);
-    ge_p2 q;
-    efgh_to_p2(q, t);
-#pragma unroll 1
-    for (int i = 0; i < 3; i++) {
-      p2_dbl(t, q);
-      efgh_to_p2(q, t);
-    }
-    const bool ident = fe_iszero(q.X) && fe_equal(q.Y, q.Z);
-    return r_ok && ident;
+    return r_ok && efgh_small_order(t);
   }
 }
 
@@ -332,10 +339,10 @@ CMTV_HD bool verify_one_half(const uint32_t* pk_ptr, const uint32_t* sig_ptr, co
     sc_reduce512(k, h);
   }
   HalfScalars hs;
-  half_scalars(hs, k);
+  half_scalars(hs, k, false, MODE != MODE_ZIP215);
   uint32_t u[8];
   hs_bscalar(u, hs.k2, hs.k2_neg, ts);
-  // window count: the largest over the wave (34..37), 64 if any is wide
+  // window count: the largest over the wave (33..37), 64 if any is wide
   const bool wide = wave.any(hs.wide);
   int W = HS_WINDOWS;
 #pragma unroll 1
@@ -405,13 +412,7 @@ CMTV_HD bool verify_one_half(const uint32_t* pk_ptr, const uint32_t* sig_ptr, co
     }
     efgh_to_p2(cur, t);
   }
-  if (MODE == MODE_ZIP215) {
-#pragma unroll 1
-    for (int d = 0; d < 3; d++) {
-      p2_dbl(t, cur);
-      efgh_to_p2(cur, t);
-    }
-  }
+  if (MODE == MODE_ZIP215) return ok && efgh_small_order(t);  // t: the last window's sum
   return ok && fe_iszero(cur.X) && fe_equal(cur.Y, cur.Z);
 }
 

@@ -186,7 +186,10 @@ int main(int argc, char** argv) {
     SigPrep hp;
     uint32_t bpt[40];
     if (quad2 || oct2) {
-      q_prepare(hp, pkw, sigw, mp, mlen, false);
+      if (mode)
+        q_prepare<MODE_ZIP215>(hp, pkw, sigw, mp, mlen, false);
+      else
+        q_prepare<MODE_GO_STDLIB>(hp, pkw, sigw, mp, mlen, false);
       ge_p3 Bp;
       q_bcomb16(Bp, hp.u, bt);
       bpoint_store(bpt, Bp);

@@ -48,7 +48,7 @@ def _run(binary, arg, corpus, idx, mode):
 
 @pytest.mark.parametrize("mode", [0, 1])
 def test_half_scalar_lane_pipeline_matches_corpus(hostcheck, corpus, mode):
-    """verify_one_half (the lane kernel: half-size scalars, 34 windows, R
+    """verify_one_half (the lane kernel: half-size scalars, 33+ windows, R
     table, X = [k2](R' - R)) over the whole corpus at every misalignment."""
     idx = list(range(len(corpus["msgs"])))
     got = _run(hostcheck, "half", corpus, idx, mode)
@@ -126,21 +126,24 @@ HBIN = os.path.join(ROOT, "build", "halfcheck")
 L = 2**252 + 27742317777372353535851937790883648493
 
 
-def test_half_scalar_decomposition():
+@pytest.mark.parametrize("parity", ["odd", "any"])
+def test_half_scalar_decomposition(parity):
     """halfscalar.h (the device source, host-compiled): k1 == k2 k (mod 8L),
-    k2 odd, 0 <= k1, |k2| < 2^(4W - 2) for the pair's window count W
-    (34..37) unless flagged wide (then k1 = k, k2 = 1, W = 64). Random
-    scalars plus the boundary ones; W > 34 stays rare (~1e-4) and wide rarer
-    (it only costs time, never changes a verdict). The Lehmer schedule must
-    give exactly the pair of the one-step-per-round Euclid."""
+    0 <= k1, |k2| < 2^(4W - 2) for the pair's window count W (33..37) unless
+    flagged wide (then k1 = k, k2 = 1, W = 64), L not dividing k2. "odd"
+    (GO_STDLIB): k2 odd; W > 33 for ~1.2% of k, W > 34 ~5e-5, wide rarer.
+    "any" (ZIP215): the shorter reduced basis vector, always inside 33
+    windows. The Lehmer schedule must give exactly the pair of the
+    one-step-per-round Euclid."""
     binary = _build(HSRC, HBIN, ["-std=c++17"])
     rng = np.random.default_rng(215)
     ks = [0, 1, 2, 3, L - 1, L - 2, 2**127, 2**128 - 1, 2**134, 2**252]
     ks += [int.from_bytes(rng.bytes(32), "little") % L for _ in range(20000)]
     buf = struct.pack("<I", len(ks)) + b"".join(k.to_bytes(32, "little") for k in ks)
-    out = subprocess.run([binary], input=buf, capture_output=True, check=True, timeout=120).stdout
+    out = subprocess.run([binary, parity], input=buf, capture_output=True, check=True, timeout=120).stdout
     assert len(out) == 130 * len(ks)
-    wide = graded = 0
+    wide = 0
+    windows = {}
     for j, k in enumerate(ks):
         rec = out[130 * j: 130 * j + 65]
         assert rec == out[130 * j + 65: 130 * (j + 1)], j  # Lehmer == exact steps
@@ -152,16 +155,23 @@ def test_half_scalar_decomposition():
             wide += 1
             assert (k1, k2, f & 1, w) == (k, 1, 0, 64), j
             continue
-        assert 34 <= w <= 37, (j, w)
-        graded += w > 34
+        assert 33 <= w <= 37, (j, w)
+        windows[w] = windows.get(w, 0) + 1
         s2 = -k2 if f & 1 else k2
-        assert k2 & 1, j
+        if parity == "odd":
+            assert k2 & 1, j
+        assert 0 < k2 < L, j
         bound = 2 ** (4 * w - 2)
         assert k1 < bound and 0 < k2 < bound, j
-        if w > 34:  # the smallest window count that holds the pair
+        if w > 33:  # the smallest window count that holds the pair
             assert max(k1.bit_length(), k2.bit_length()) > 4 * (w - 1) - 2, j
         assert (k1 - s2 * k) % (8 * L) == 0, j
-    assert wide <= 8 and graded <= 20, (wide, graded)  # wide: the boundary k (0, 1, 2^252, ...)
+    assert wide <= 8, wide  # wide: the boundary k (0, 1, 2^252, ...)
+    if parity == "any":
+        assert set(windows) == {33}, windows
+    else:
+        assert 0.005 < windows.get(34, 0) / len(ks) < 0.03, windows  # ~1.2%
+        assert sum(c for w, c in windows.items() if w > 34) <= 20, windows
 
 
 @pytest.mark.parametrize("mode", [0, 1])

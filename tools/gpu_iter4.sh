@@ -2,7 +2,7 @@
 # GPU tests, then a short bench (latency lines incl. the keyset cache)
 set -o pipefail
 export TMPDIR=/tmp
-OUT=gpurun_out/iter4
+OUT=gpurun_out/${ITER:-iter4}
 mkdir -p "$OUT"
 timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > "$OUT/pytest.log" 2>&1
 rc=$?; tail -3 "$OUT/pytest.log"; [ $rc -eq 0 ] || { grep -B5 -A40 "FAIL\|Error" "$OUT/pytest.log" | head -100; exit $rc; }

@@ -41,7 +41,7 @@ COMMIT_PANIC_UNKNOWN_FLAG = 9
 # every symbol include/cmtverify.h declares (checked by tests/test_abi.py)
 EXPORTS = (
     "cmtv_open", "cmtv_open_devices", "cmtv_device_count", "cmtv_device_ordinal", "cmtv_device_stream", "cmtv_sync",
-    "cmtv_verify_ed25519_sharded_device", "cmtv_verify_ed25519_indexed_sharded_device", "cmtv_close", "cmtv_strerror", "cmtv_abi_version", "cmtv_stats_get", "cmtv_stream",
+    "cmtv_verify_ed25519_sharded_device", "cmtv_verify_ed25519_indexed_sharded_device", "cmtv_verify_ed25519_multi_device", "cmtv_close", "cmtv_strerror", "cmtv_abi_version", "cmtv_stats_get", "cmtv_stream",
     "cmtv_verify_ed25519", "cmtv_verify_ed25519_device", "cmtv_verify_sr25519", "cmtv_verify_sr25519_device",
     "cmtv_register_keys", "cmtv_keyset_free", "cmtv_keyset_len", "cmtv_verify_ed25519_indexed",
     "cmtv_verify_ed25519_indexed_device",
@@ -126,6 +126,8 @@ def lib() -> ctypes.CDLL:
     L.cmtv_sync.restype = ctypes.c_int
     L.cmtv_verify_ed25519_sharded_device.argtypes = [vp, szp, vpp, vpp, vpp, vpp, u32, vpp, vpp, szp]
     L.cmtv_verify_ed25519_sharded_device.restype = ctypes.c_int
+    L.cmtv_verify_ed25519_multi_device.argtypes = [vp, szp, vpp, vpp, vpp, vpp, u32, vpp, vpp]
+    L.cmtv_verify_ed25519_multi_device.restype = ctypes.c_int
     L.cmtv_verify_ed25519_indexed_sharded_device.argtypes = [vp, vp, szp, vpp, vpp, vpp, vpp, u32, vpp, vpp, szp]
     L.cmtv_verify_ed25519_indexed_sharded_device.restype = ctypes.c_int
     L.cmtv_close.argtypes = [vp]

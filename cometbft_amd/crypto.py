@@ -87,6 +87,20 @@ class Context:
         N.check(rc, "cmtv_verify_ed25519_sharded_device")
         return w.value
 
+    def verify_multi_device(self, n_dev: Sequence[int], d_pk, d_sig, d_msg, d_off, mode: int, d_bitmap,
+                            d_valid=None) -> None:
+        """cmtv_verify_ed25519_multi_device: device g verifies its own batch
+        (pointers as ints on the context's g-th device) into its own
+        ceil(n_dev[g] / 64) bitmap words; no exchange. Non-blocking."""
+        G = len(n_dev)
+        vp = ctypes.c_void_p
+        arr = lambda xs: (vp * G)(*[vp(x) if x else None for x in xs])  # noqa: E731
+        ns = (ctypes.c_size_t * G)(*n_dev)
+        dv = arr(d_valid) if d_valid is not None else None
+        rc = N.lib().cmtv_verify_ed25519_multi_device(self._h, ns, arr(d_pk), arr(d_sig), arr(d_msg), arr(d_off), mode,
+                                                      dv, arr(d_bitmap))
+        N.check(rc, "cmtv_verify_ed25519_multi_device")
+
     @property
     def handle(self):
         return self._h

@@ -1172,7 +1172,8 @@ namespace cmtv {
 // device g, each verified on its device's stream, then the bitmap gather.
 static int sharded_device(cmtv_ctx* ctx, const cmtv_keyset* ks, const size_t* n_shard, const void* const* d_keys,
                           const void* const* d_sig, const void* const* d_msg, const void* const* d_off,
-                          uint32_t mode, void* const* d_valid, void* const* d_bitmap_all, size_t* words_per_shard) {
+                          uint32_t mode, void* const* d_valid, void* const* d_bitmap_all, size_t* words_per_shard,
+                          bool gather = true) {
   const size_t G = ctx->devs.size();
   size_t W = 0;
   for (size_t g = 0; g < G; g++) {
@@ -1189,23 +1190,29 @@ static int sharded_device(cmtv_ctx* ctx, const cmtv_keyset* ks, const size_t* n_
     CmtvDev& D = ctx->devs[g];
     if (hipSetDevice(D.ordinal) != hipSuccess) return CMTV_ENODEV;
     bufs[g] = static_cast<uint64_t*>(d_bitmap_all[g]);
+    // independent batches (no gather): device g's bitmap is its own words
+    uint64_t* own_bm = gather ? bufs[g] + g * W : bufs[g];
     // words of this shard beyond its signatures stay zero (quad kernels write
     // whole 16-bit slices, lane kernels whole words; a short shard leaves the
     // rest of its W words untouched)
     const size_t own = (n_shard[g] + 63) / 64;
-    if (own < W && (e = hipMemsetAsync(bufs[g] + g * W + own, 0, 8 * (W - own), D.stream)) != hipSuccess)
+    if (gather && own < W && (e = hipMemsetAsync(own_bm + own, 0, 8 * (W - own), D.stream)) != hipSuccess)
       return hip_fail(e);
     uint8_t* dv = d_valid ? static_cast<uint8_t*>(d_valid[g]) : nullptr;
     int rc;
     if (ks)
       rc = enqueue_verify_keyed(ctx, D, ks->dev[g], ks->n, n_shard[g], static_cast<const uint32_t*>(d_keys[g]),
                                 static_cast<const uint8_t*>(d_sig[g]), static_cast<const uint8_t*>(d_msg[g]),
-                                static_cast<const uint32_t*>(d_off[g]), mode, dv, bufs[g] + g * W, D.stream);
+                                static_cast<const uint32_t*>(d_off[g]), mode, dv, own_bm, D.stream);
     else
       rc = enqueue_verify(ctx, D, n_shard[g], static_cast<const uint8_t*>(d_keys[g]),
                           static_cast<const uint8_t*>(d_sig[g]), static_cast<const uint8_t*>(d_msg[g]),
-                          static_cast<const uint32_t*>(d_off[g]), mode, dv, bufs[g] + g * W, D.stream);
+                          static_cast<const uint32_t*>(d_off[g]), mode, dv, own_bm, D.stream);
     if (rc != CMTV_OK) return rc;
+  }
+  if (!gather) {
+    (void)hipSetDevice(ctx->devs[0].ordinal);
+    return CMTV_OK;
   }
   if (G > 1) ctx->stats.sharded_calls++;
   const int rc = gather_bitmaps(ctx, G, W, bufs);
@@ -1227,6 +1234,18 @@ int cmtv_verify_ed25519_sharded_device(cmtv_ctx* ctx, const size_t* n_shard, con
   if (ctx_lock(ctx, lk) != CMTV_OK) return CMTV_ENODEV;
   return sharded_device(ctx, nullptr, n_shard, d_pk, d_sig, d_msg, d_msg_off, mode, d_valid, d_bitmap_all,
                         words_per_shard);
+}
+
+int cmtv_verify_ed25519_multi_device(cmtv_ctx* ctx, const size_t* n_dev, const void* const* d_pk,
+                                     const void* const* d_sig, const void* const* d_msg,
+                                     const void* const* d_msg_off, uint32_t mode, void* const* d_valid,
+                                     void* const* d_bitmap) {
+  if (!ctx || mode > CMTV_MODE_ZIP215 || !n_dev || !d_pk || !d_sig || !d_msg || !d_msg_off || !d_bitmap)
+    return CMTV_EINVAL;
+  std::unique_lock<std::mutex> lk;
+  if (ctx_lock(ctx, lk) != CMTV_OK) return CMTV_ENODEV;
+  return sharded_device(ctx, nullptr, n_dev, d_pk, d_sig, d_msg, d_msg_off, mode, d_valid, d_bitmap, nullptr,
+                        false);
 }
 
 int cmtv_verify_ed25519_indexed_sharded_device(cmtv_ctx* ctx, const cmtv_keyset* ks, const size_t* n_shard,

@@ -167,6 +167,17 @@ int cmtv_verify_ed25519_sharded_device(cmtv_ctx* ctx, const size_t* n_shard, con
                                        const void* const* d_msg_off, uint32_t mode, void* const* d_valid,
                                        void* const* d_bitmap_all, size_t* words_per_shard);
 
+/* Multi-device, device-resident, INDEPENDENT batches (one commit per device,
+ * e.g. the configs[1] step at N GPUs): device g verifies its own n_dev[g]
+ * signatures on its own stream and writes ceil(n_dev[g] / 64) verdict words
+ * to d_bitmap[g] (and n_dev[g] bytes to d_valid[g] unless NULL). Nothing is
+ * exchanged between devices: each batch's verdicts go to its own caller.
+ * Non-blocking: cmtv_sync waits. */
+int cmtv_verify_ed25519_multi_device(cmtv_ctx* ctx, const size_t* n_dev, const void* const* d_pk,
+                                     const void* const* d_sig, const void* const* d_msg,
+                                     const void* const* d_msg_off, uint32_t mode, void* const* d_valid,
+                                     void* const* d_bitmap);
+
 /* ------------------------------------------------------------ verdict cache */
 
 /* Blocksync verifies each commit three times with the same (key, sign-bytes,

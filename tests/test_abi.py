@@ -123,6 +123,7 @@ def test_multi_device_entry_points_reject_bad_arguments_without_gpu():
                                                   None) == N.CMTV_EINVAL
     assert lib.cmtv_verify_ed25519_indexed_sharded_device(None, None, None, None, None, None, None, 0, None, None,
                                                           None) == N.CMTV_EINVAL
+    assert lib.cmtv_verify_ed25519_multi_device(None, None, None, None, None, None, 0, None, None) == N.CMTV_EINVAL
 
 
 def test_open_devices_without_gpu_is_enodev():

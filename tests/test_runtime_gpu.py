@@ -143,6 +143,37 @@ def test_sharded_device_api_over_a_repeated_device():
             assert np.array_equal(bits[:n], exp[h]) and not bits[n:].any()
 
 
+def test_multi_device_api_independent_batches():
+    """cmtv_verify_ed25519_multi_device over a repeated ordinal: each device
+    verifies its own batch into its own bitmap words (no exchange)."""
+    import torch
+
+    ctx = Context(devices=[0, 0])
+    dev = torch.device("cuda:0")
+    shards, exp, d = (10_000, 333), [], []
+    for g, n in enumerate(shards):
+        pk, kidx, sig, m, off = _batch(n, 60 + g)
+        sig = sig.copy()
+        sig[g::101, 9] ^= 4
+        exp.append(coracle.verify_batch(pk[kidx], sig, m, off, MODE_GO_STDLIB, nthreads=16))
+        d.append({k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in
+                  {"pk": pk[kidx], "sig": sig, "m": m, "off": off.view(np.int32)}.items()})
+    out = [torch.full(((n + 63) // 64 + 1,), -1, dtype=torch.int64, device=dev) for n in shards]
+    valid = [torch.zeros(n, dtype=torch.uint8, device=dev) for n in shards]
+    g0 = ctx.stats()["gathers"]
+    ctx.verify_multi_device(list(shards), [t["pk"].data_ptr() for t in d], [t["sig"].data_ptr() for t in d],
+                            [t["m"].data_ptr() for t in d], [t["off"].data_ptr() for t in d], MODE_GO_STDLIB,
+                            [o.data_ptr() for o in out], [v.data_ptr() for v in valid])
+    ctx.sync()
+    assert ctx.stats()["gathers"] == g0
+    for g, n in enumerate(shards):
+        assert np.array_equal(valid[g].cpu().numpy(), exp[g])
+        words = out[g].cpu().numpy().view(np.uint64)
+        bits = np.unpackbits(words[:(n + 63) // 64].view(np.uint8), bitorder="little")
+        assert np.array_equal(bits[:n], exp[g])
+        assert words[-1] == np.uint64((1 << 64) - 1)  # nothing written past its own words
+
+
 def test_rccl_path_on_one_device():
     """CMTV_FORCE_RCCL: a one-rank RCCL communicator over device 0, so the
     library's RCCL init (ncclCommInitAll) and its in-place grouped all-gather

@@ -1,0 +1,281 @@
+// Microbenchmark: latency of one field squaring / multiplication chain with
+// ONE wave per SIMD (the regime the quad/oct verify kernels run in at 10k and
+// below), for carry-chain variants of fe25519.h's reduction.
+//
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I cometbft_amd/csrc -o tools/microbench/fe_lat tools/microbench/fe_lat.hip
+//
+// Each lane runs NOPS dependent squarings (or h = h*g) in a rolled loop with
+// a hidden trip count (as fe_sqn does); lane 0 of every wave records
+// s_memtime around the chain. Prints mean cycles per operation and checks
+// every variant's canonical result against variant 0's.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "fe25519.h"
+
+using namespace cmtv;
+
+// ---- reduction variants ----------------------------------------------------
+// R1: three interleaved carry streams (0->3, 3->6, 6->9->0), 5 levels instead
+// of ref10's 7; leaves limbs 4, 7 and 1 with a carry of at most 2^13.
+CMTV_HD void red_3chain(fe& h, uint64_t h0, uint64_t h1, uint64_t h2, uint64_t h3, uint64_t h4, uint64_t h5,
+                        uint64_t h6, uint64_t h7, uint64_t h8, uint64_t h9) {
+  uint64_t c;
+  c = h0 >> 26; h1 += c; h0 &= M26;
+  c = h3 >> 25; h4 += c; h3 &= M25;
+  c = h6 >> 26; h7 += c; h6 &= M26;
+  c = h1 >> 25; h2 += c; h1 &= M25;
+  c = h4 >> 26; h5 += c; h4 &= M26;
+  c = h7 >> 25; h8 += c; h7 &= M25;
+  c = h2 >> 26; h3 += c; h2 &= M26;
+  c = h5 >> 25; h6 += c; h5 &= M25;
+  c = h8 >> 26; h9 += c; h8 &= M26;
+  c = h3 >> 25; h4 += c; h3 &= M25;
+  c = h6 >> 26; h7 += c; h6 &= M26;
+  c = h9 >> 25; h0 += c * 19; h9 &= M25;
+  c = h0 >> 26; h1 += c; h0 &= M26;
+  h.v[0] = (uint32_t)h0; h.v[1] = (uint32_t)h1; h.v[2] = (uint32_t)h2; h.v[3] = (uint32_t)h3;
+  h.v[4] = (uint32_t)h4; h.v[5] = (uint32_t)h5; h.v[6] = (uint32_t)h6; h.v[7] = (uint32_t)h7;
+  h.v[8] = (uint32_t)h8; h.v[9] = (uint32_t)h9;
+}
+
+// R2: two parallel rounds. Round 1 carries every 64-bit column at once
+// (t_i = low(h_i) + c_{i-1}, t_0 = low(h_0) + 19 c_9: < 2^44); round 2 carries
+// the t_i at once on 32-bit words (t_i >> r < 2^19). Limbs end < 2^26 + 2^19.
+CMTV_HD void red_par2(fe& h, uint64_t h0, uint64_t h1, uint64_t h2, uint64_t h3, uint64_t h4, uint64_t h5,
+                      uint64_t h6, uint64_t h7, uint64_t h8, uint64_t h9) {
+  const uint64_t c0 = h0 >> 26, c1 = h1 >> 25, c2 = h2 >> 26, c3 = h3 >> 25, c4 = h4 >> 26;
+  const uint64_t c5 = h5 >> 25, c6 = h6 >> 26, c7 = h7 >> 25, c8 = h8 >> 26, c9 = h9 >> 25;
+  const uint64_t t0 = (uint64_t)((uint32_t)h0 & M26) + c9 * 19;
+  const uint64_t t1 = (uint64_t)((uint32_t)h1 & M25) + c0;
+  const uint64_t t2 = (uint64_t)((uint32_t)h2 & M26) + c1;
+  const uint64_t t3 = (uint64_t)((uint32_t)h3 & M25) + c2;
+  const uint64_t t4 = (uint64_t)((uint32_t)h4 & M26) + c3;
+  const uint64_t t5 = (uint64_t)((uint32_t)h5 & M25) + c4;
+  const uint64_t t6 = (uint64_t)((uint32_t)h6 & M26) + c5;
+  const uint64_t t7 = (uint64_t)((uint32_t)h7 & M25) + c6;
+  const uint64_t t8 = (uint64_t)((uint32_t)h8 & M26) + c7;
+  const uint64_t t9 = (uint64_t)((uint32_t)h9 & M25) + c8;
+  const uint32_t d0 = (uint32_t)(t0 >> 26), d1 = (uint32_t)(t1 >> 25), d2 = (uint32_t)(t2 >> 26);
+  const uint32_t d3 = (uint32_t)(t3 >> 25), d4 = (uint32_t)(t4 >> 26), d5 = (uint32_t)(t5 >> 25);
+  const uint32_t d6 = (uint32_t)(t6 >> 26), d7 = (uint32_t)(t7 >> 25), d8 = (uint32_t)(t8 >> 26);
+  const uint32_t d9 = (uint32_t)(t9 >> 25);
+  h.v[0] = ((uint32_t)t0 & M26) + 19 * d9;
+  h.v[1] = ((uint32_t)t1 & M25) + d0;
+  h.v[2] = ((uint32_t)t2 & M26) + d1;
+  h.v[3] = ((uint32_t)t3 & M25) + d2;
+  h.v[4] = ((uint32_t)t4 & M26) + d3;
+  h.v[5] = ((uint32_t)t5 & M25) + d4;
+  h.v[6] = ((uint32_t)t6 & M26) + d5;
+  h.v[7] = ((uint32_t)t7 & M25) + d6;
+  h.v[8] = ((uint32_t)t8 & M26) + d7;
+  h.v[9] = ((uint32_t)t9 & M25) + d8;
+}
+
+template <int R>
+CMTV_HD void reduce(fe& h, uint64_t h0, uint64_t h1, uint64_t h2, uint64_t h3, uint64_t h4, uint64_t h5,
+                    uint64_t h6, uint64_t h7, uint64_t h8, uint64_t h9) {
+  if (R == 0) fe_reduce64(h, h0, h1, h2, h3, h4, h5, h6, h7, h8, h9);
+  else if (R == 1) red_3chain(h, h0, h1, h2, h3, h4, h5, h6, h7, h8, h9);
+  else red_par2(h, h0, h1, h2, h3, h4, h5, h6, h7, h8, h9);
+}
+
+// squaring with the reduction R; multipliers by 19/38 as shift-adds when S
+template <int R, bool S>
+CMTV_HD void sq_v(fe& h, const fe& f) {
+  CMTV_SCHED_FENCE();
+  const uint32_t f0 = f.v[0], f1 = f.v[1], f2 = f.v[2], f3 = f.v[3], f4 = f.v[4];
+  const uint32_t f5 = f.v[5], f6 = f.v[6], f7 = f.v[7], f8 = f.v[8], f9 = f.v[9];
+  const uint32_t f0_2 = 2 * f0, f1_2 = 2 * f1, f2_2 = 2 * f2, f3_2 = 2 * f3, f4_2 = 2 * f4;
+  const uint32_t f5_2 = 2 * f5, f6_2 = 2 * f6, f7_2 = 2 * f7;
+  uint32_t f5_38, f6_19, f7_38, f8_19, f9_38;
+  if (S) {
+    f6_19 = (f6 << 4) + f6 + (f6 << 1);
+    f8_19 = (f8 << 4) + f8 + (f8 << 1);
+    f5_38 = (f5_2 << 4) + f5_2 + (f5_2 << 1);
+    f7_38 = (f7_2 << 4) + f7_2 + (f7_2 << 1);
+    const uint32_t f9_2 = 2 * f9;
+    f9_38 = (f9_2 << 4) + f9_2 + (f9_2 << 1);
+  } else {
+    f5_38 = 38 * f5; f6_19 = 19 * f6; f7_38 = 38 * f7; f8_19 = 19 * f8; f9_38 = 38 * f9;
+  }
+  uint64_t h0 = CMTV_MUL64(f0, f0) + CMTV_MUL64(f1_2, f9_38) + CMTV_MUL64(f2_2, f8_19) + CMTV_MUL64(f3_2, f7_38) +
+                CMTV_MUL64(f4_2, f6_19) + CMTV_MUL64(f5, f5_38);
+  uint64_t h1 = CMTV_MUL64(f0_2, f1) + CMTV_MUL64(f2, f9_38) + CMTV_MUL64(f3_2, f8_19) + CMTV_MUL64(f4, f7_38) +
+                CMTV_MUL64(f5_2, f6_19);
+  uint64_t h2 = CMTV_MUL64(f0_2, f2) + CMTV_MUL64(f1_2, f1) + CMTV_MUL64(f3_2, f9_38) + CMTV_MUL64(f4_2, f8_19) +
+                CMTV_MUL64(f5_2, f7_38) + CMTV_MUL64(f6, f6_19);
+  uint64_t h3 = CMTV_MUL64(f0_2, f3) + CMTV_MUL64(f1_2, f2) + CMTV_MUL64(f4, f9_38) + CMTV_MUL64(f5_2, f8_19) +
+                CMTV_MUL64(f6, f7_38);
+  uint64_t h4 = CMTV_MUL64(f0_2, f4) + CMTV_MUL64(f1_2, f3_2) + CMTV_MUL64(f2, f2) + CMTV_MUL64(f5_2, f9_38) +
+                CMTV_MUL64(f6_2, f8_19) + CMTV_MUL64(f7, f7_38);
+  uint64_t h5 = CMTV_MUL64(f0_2, f5) + CMTV_MUL64(f1_2, f4) + CMTV_MUL64(f2_2, f3) + CMTV_MUL64(f6, f9_38) +
+                CMTV_MUL64(f7_2, f8_19);
+  uint64_t h6 = CMTV_MUL64(f0_2, f6) + CMTV_MUL64(f1_2, f5_2) + CMTV_MUL64(f2_2, f4) + CMTV_MUL64(f3_2, f3) +
+                CMTV_MUL64(f7_2, f9_38) + CMTV_MUL64(f8, f8_19);
+  uint64_t h7 = CMTV_MUL64(f0_2, f7) + CMTV_MUL64(f1_2, f6) + CMTV_MUL64(f2_2, f5) + CMTV_MUL64(f3_2, f4) +
+                CMTV_MUL64(f8, f9_38);
+  uint64_t h8 = CMTV_MUL64(f0_2, f8) + CMTV_MUL64(f1_2, f7_2) + CMTV_MUL64(f2_2, f6) + CMTV_MUL64(f3_2, f5_2) +
+                CMTV_MUL64(f4, f4) + CMTV_MUL64(f9, f9_38);
+  uint64_t h9 = CMTV_MUL64(f0_2, f9) + CMTV_MUL64(f1_2, f8) + CMTV_MUL64(f2_2, f7) + CMTV_MUL64(f3_2, f6) +
+                CMTV_MUL64(f4_2, f5);
+  reduce<R>(h, h0, h1, h2, h3, h4, h5, h6, h7, h8, h9);
+  CMTV_SCHED_FENCE();
+}
+
+template <int R>
+CMTV_HD void mul_v(fe& h, const fe& f, const fe& g) {
+  CMTV_SCHED_FENCE();
+  const uint32_t f0 = f.v[0], f1 = f.v[1], f2 = f.v[2], f3 = f.v[3], f4 = f.v[4];
+  const uint32_t f5 = f.v[5], f6 = f.v[6], f7 = f.v[7], f8 = f.v[8], f9 = f.v[9];
+  const uint32_t g0 = g.v[0], g1 = g.v[1], g2 = g.v[2], g3 = g.v[3], g4 = g.v[4];
+  const uint32_t g5 = g.v[5], g6 = g.v[6], g7 = g.v[7], g8 = g.v[8], g9 = g.v[9];
+  const uint32_t g1_19 = 19 * g1, g2_19 = 19 * g2, g3_19 = 19 * g3, g4_19 = 19 * g4, g5_19 = 19 * g5;
+  const uint32_t g6_19 = 19 * g6, g7_19 = 19 * g7, g8_19 = 19 * g8, g9_19 = 19 * g9;
+  const uint32_t f1_2 = 2 * f1, f3_2 = 2 * f3, f5_2 = 2 * f5, f7_2 = 2 * f7, f9_2 = 2 * f9;
+  uint64_t h0 = CMTV_MUL64(f0, g0) + CMTV_MUL64(f1_2, g9_19) + CMTV_MUL64(f2, g8_19) + CMTV_MUL64(f3_2, g7_19) +
+                CMTV_MUL64(f4, g6_19) + CMTV_MUL64(f5_2, g5_19) + CMTV_MUL64(f6, g4_19) + CMTV_MUL64(f7_2, g3_19) +
+                CMTV_MUL64(f8, g2_19) + CMTV_MUL64(f9_2, g1_19);
+  uint64_t h1 = CMTV_MUL64(f0, g1) + CMTV_MUL64(f1, g0) + CMTV_MUL64(f2, g9_19) + CMTV_MUL64(f3, g8_19) +
+                CMTV_MUL64(f4, g7_19) + CMTV_MUL64(f5, g6_19) + CMTV_MUL64(f6, g5_19) + CMTV_MUL64(f7, g4_19) +
+                CMTV_MUL64(f8, g3_19) + CMTV_MUL64(f9, g2_19);
+  uint64_t h2 = CMTV_MUL64(f0, g2) + CMTV_MUL64(f1_2, g1) + CMTV_MUL64(f2, g0) + CMTV_MUL64(f3_2, g9_19) +
+                CMTV_MUL64(f4, g8_19) + CMTV_MUL64(f5_2, g7_19) + CMTV_MUL64(f6, g6_19) + CMTV_MUL64(f7_2, g5_19) +
+                CMTV_MUL64(f8, g4_19) + CMTV_MUL64(f9_2, g3_19);
+  uint64_t h3 = CMTV_MUL64(f0, g3) + CMTV_MUL64(f1, g2) + CMTV_MUL64(f2, g1) + CMTV_MUL64(f3, g0) +
+                CMTV_MUL64(f4, g9_19) + CMTV_MUL64(f5, g8_19) + CMTV_MUL64(f6, g7_19) + CMTV_MUL64(f7, g6_19) +
+                CMTV_MUL64(f8, g5_19) + CMTV_MUL64(f9, g4_19);
+  uint64_t h4 = CMTV_MUL64(f0, g4) + CMTV_MUL64(f1_2, g3) + CMTV_MUL64(f2, g2) + CMTV_MUL64(f3_2, g1) +
+                CMTV_MUL64(f4, g0) + CMTV_MUL64(f5_2, g9_19) + CMTV_MUL64(f6, g8_19) + CMTV_MUL64(f7_2, g7_19) +
+                CMTV_MUL64(f8, g6_19) + CMTV_MUL64(f9_2, g5_19);
+  uint64_t h5 = CMTV_MUL64(f0, g5) + CMTV_MUL64(f1, g4) + CMTV_MUL64(f2, g3) + CMTV_MUL64(f3, g2) +
+                CMTV_MUL64(f4, g1) + CMTV_MUL64(f5, g0) + CMTV_MUL64(f6, g9_19) + CMTV_MUL64(f7, g8_19) +
+                CMTV_MUL64(f8, g7_19) + CMTV_MUL64(f9, g6_19);
+  uint64_t h6 = CMTV_MUL64(f0, g6) + CMTV_MUL64(f1_2, g5) + CMTV_MUL64(f2, g4) + CMTV_MUL64(f3_2, g3) +
+                CMTV_MUL64(f4, g2) + CMTV_MUL64(f5_2, g1) + CMTV_MUL64(f6, g0) + CMTV_MUL64(f7_2, g9_19) +
+                CMTV_MUL64(f8, g8_19) + CMTV_MUL64(f9_2, g7_19);
+  uint64_t h7 = CMTV_MUL64(f0, g7) + CMTV_MUL64(f1, g6) + CMTV_MUL64(f2, g5) + CMTV_MUL64(f3, g4) +
+                CMTV_MUL64(f4, g3) + CMTV_MUL64(f5, g2) + CMTV_MUL64(f6, g1) + CMTV_MUL64(f7, g0) +
+                CMTV_MUL64(f8, g9_19) + CMTV_MUL64(f9, g8_19);
+  uint64_t h8 = CMTV_MUL64(f0, g8) + CMTV_MUL64(f1_2, g7) + CMTV_MUL64(f2, g6) + CMTV_MUL64(f3_2, g5) +
+                CMTV_MUL64(f4, g4) + CMTV_MUL64(f5_2, g3) + CMTV_MUL64(f6, g2) + CMTV_MUL64(f7_2, g1) +
+                CMTV_MUL64(f8, g0) + CMTV_MUL64(f9_2, g9_19);
+  uint64_t h9 = CMTV_MUL64(f0, g9) + CMTV_MUL64(f1, g8) + CMTV_MUL64(f2, g7) + CMTV_MUL64(f3, g6) +
+                CMTV_MUL64(f4, g5) + CMTV_MUL64(f5, g4) + CMTV_MUL64(f6, g3) + CMTV_MUL64(f7, g2) +
+                CMTV_MUL64(f8, g1) + CMTV_MUL64(f9, g0);
+  reduce<R>(h, h0, h1, h2, h3, h4, h5, h6, h7, h8, h9);
+  CMTV_SCHED_FENCE();
+}
+
+// V: 0..5 = squaring (R0,R1,R2) x (mul19 as v_mul_lo / shift-add);
+//    6..8 = multiplication h = h*g with R0, R1, R2;
+//    9    = two independent squaring chains interleaved (ILP 2), R0
+template <int V>
+__global__ void __launch_bounds__(256) k_chain(const uint32_t* in, uint32_t* out, int nops, unsigned long long* cyc) {
+  extern __shared__ uint32_t lds_pad[];
+  const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+  fe h, g, h2;
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    h.v[i] = in[tid * 20 + i];
+    g.v[i] = in[tid * 20 + 10 + i];
+    h2.v[i] = g.v[i];
+  }
+  if (threadIdx.x == 0) lds_pad[0] = 0;  // keep the dynamic LDS allocation
+  int n = nops;
+  asm volatile("" : "+s"(n));
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#pragma unroll 1
+  for (int i = 0; i < n; i++) {
+    if (V == 0) sq_v<0, false>(h, h);
+    if (V == 1) sq_v<1, false>(h, h);
+    if (V == 2) sq_v<2, false>(h, h);
+    if (V == 3) sq_v<0, true>(h, h);
+    if (V == 4) sq_v<1, true>(h, h);
+    if (V == 5) sq_v<2, true>(h, h);
+    if (V == 6) mul_v<0>(h, h, g);
+    if (V == 7) mul_v<1>(h, h, g);
+    if (V == 8) mul_v<2>(h, h, g);
+    if (V == 9) {
+      sq_v<0, false>(h, h);
+      sq_v<0, false>(h2, h2);
+    }
+  }
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  uint32_t s[8];
+  fe_tobytes(s, h);
+  if (V == 9) {
+    uint32_t s2[8];
+    fe_tobytes(s2, h2);
+    for (int i = 0; i < 8; i++) s[i] ^= s2[i];
+  }
+  for (int i = 0; i < 8; i++) out[tid * 8 + i] = s[i];
+  if ((threadIdx.x & 63) == 0) cyc[tid >> 6] = t1 - t0;
+}
+
+typedef void (*kfn)(const uint32_t*, uint32_t*, int, unsigned long long*);
+
+int main(int argc, char** argv) {
+  const int nops = argc > 1 ? atoi(argv[1]) : 2000;
+  int dev = 0, cus = 0;
+  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int block = 256;
+  const kfn ks[] = {k_chain<0>, k_chain<1>, k_chain<2>, k_chain<3>, k_chain<4>,
+                    k_chain<5>, k_chain<6>, k_chain<7>, k_chain<8>, k_chain<9>};
+  const char* names[] = {"sq ref10", "sq 3chain", "sq par2", "sq ref10 sh19", "sq 3chain sh19", "sq par2 sh19",
+                         "mul ref10", "mul 3chain", "mul par2", "sq ref10 x2 ILP"};
+  for (int wps = 1; wps <= 2; wps++) {
+    const int grid = cus * wps;  // wps waves per SIMD (one 4-wave block per CU per wave slot)
+    const size_t nth = (size_t)grid * block;
+    std::vector<uint32_t> hin(nth * 20);
+    uint32_t x = 12345;
+    for (auto& w : hin) {
+      x = x * 1664525u + 1013904223u;
+      w = x >> 7;  // < 2^25
+    }
+    uint32_t *din, *dout;
+    unsigned long long* dcyc;
+    hipMalloc(&din, hin.size() * 4);
+    hipMalloc(&dout, nth * 8 * 4);
+    hipMalloc(&dcyc, (nth / 64) * 8);
+    hipMemcpy(din, hin.data(), hin.size() * 4, hipMemcpyHostToDevice);
+    // 80 KiB of LDS per block: one block per CU per launch slot
+    const size_t lds = wps == 1 ? 96 * 1024 : 64 * 1024;
+    std::vector<uint32_t> ref(nth * 8), got(nth * 8);
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    for (int v = 0; v < 10; v++) {
+      for (int r = 0; r < 2; r++) hipLaunchKernelGGL(ks[v], dim3(grid), dim3(block), lds, 0, din, dout, nops, dcyc);
+      hipEventRecord(e0);
+      hipLaunchKernelGGL(ks[v], dim3(grid), dim3(block), lds, 0, din, dout, nops, dcyc);
+      hipEventRecord(e1);
+      hipEventSynchronize(e1);
+      float ms = 0;
+      hipEventElapsedTime(&ms, e0, e1);
+      std::vector<unsigned long long> cyc(nth / 64);
+      hipMemcpy(cyc.data(), dcyc, cyc.size() * 8, hipMemcpyDeviceToHost);
+      hipMemcpy(got.data(), dout, got.size() * 4, hipMemcpyDeviceToHost);
+      double mean = 0;
+      for (auto c : cyc) mean += (double)c;
+      mean /= cyc.size();
+      const char* chk = "";
+      if (v == 0) ref = got;
+      if ((v >= 1 && v <= 5) && got != ref) chk = "  MISMATCH vs sq ref10";
+      printf("wps=%d %-16s %8.1f cyc/op (s_memtime)  %7.3f ms  %6.1f ns/op%s\n", wps, names[v], mean / nops, ms,
+             ms * 1e6 / nops, chk);
+      if (v == 6) ref = got;
+      if ((v == 7 || v == 8) && got != ref) printf("  MISMATCH vs mul ref10\n");
+      if (v == 8) ref.assign(ref.size(), 0);
+      fflush(stdout);
+    }
+    hipFree(din);
+    hipFree(dout);
+    hipFree(dcyc);
+  }
+  return 0;
+}

@@ -68,7 +68,8 @@ class cmtv_stats(ctypes.Structure):
                 ("last_kernel_ms", ctypes.c_double), ("cache_hits", ctypes.c_uint64),
                 ("cache_entries", ctypes.c_uint64), ("keyed_launches", ctypes.c_uint64),
                 ("sharded_calls", ctypes.c_uint64), ("gathers", ctypes.c_uint64),
-                ("faults_injected", ctypes.c_uint64), ("n_devices", ctypes.c_uint32), ("rccl", ctypes.c_uint32)]
+                ("faults_injected", ctypes.c_uint64), ("n_devices", ctypes.c_uint32), ("rccl", ctypes.c_uint32),
+                ("fused_sign_bytes", ctypes.c_uint64)]
 
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)

@@ -19,10 +19,28 @@ constexpr uint32_t kCombScratchWordsPerKey = 128 * 320;  // prefix products whil
 // (kLaunchOctSplit), and the quad kernel's helper-wave form (kLaunchQuadSplit)
 constexpr uint32_t kLaunchQuad = 1, kLaunchForceWide = 2, kLaunchOct = 4, kLaunchOctSplit = 8, kLaunchQuadSplit = 16;
 
+// Templated sign-bytes (signbytes.h) written by the helper waves of the
+// split kernels themselves (k_verify_oct_split / k_verify_quad_split): each
+// helper lane builds its signature's CanonicalVote into an LDS slot of
+// kSbFuseMaxMsg bytes and hashes it from there, so a templated commit needs
+// no k_sign_bytes launch (and no global message buffer). Device pointers;
+// tmpls == nullptr means the messages are in `msg`.
+struct SbFuse {
+  const void* tmpls = nullptr;
+  const uint8_t* blob = nullptr;
+  const uint32_t* tidx = nullptr;
+  const uint8_t* flag = nullptr;
+  const int64_t* sec = nullptr;
+  const int32_t* nanos = nullptr;
+};
+constexpr uint32_t kSbFuseMaxMsg = 192;
+
 hipError_t launch_btab_init(uint32_t* d_rows, hipStream_t s);
+// sb (may be null) is honoured only by the split kernels (kLaunchOctSplit,
+// kLaunchQuadSplit); the caller launches k_sign_bytes otherwise
 hipError_t launch_verify(uint32_t mode, uint32_t n, const void* pk, const void* sig, const void* msg,
                          const void* off, const uint32_t* btab, uint32_t* atab, void* valid, void* bitmap,
-                         uint32_t kflags, hipStream_t s);
+                         uint32_t kflags, hipStream_t s, const SbFuse* sb = nullptr);
 hipError_t launch_comb_build(uint32_t n_keys, const void* keys_pk, uint8_t* keys_ok, uint32_t* tabs,
                              uint32_t* scratch, bool negate, hipStream_t s);
 hipError_t launch_verify_keyed(uint32_t mode, uint32_t n, uint32_t n_keys, const void* key_idx, const void* sig,

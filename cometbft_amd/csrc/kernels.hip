@@ -28,6 +28,7 @@
 #include "keyed.h"
 #include "keyed_quad.h"
 #include "quad.h"
+#include "signbytes.h"
 #include "verify_core.h"
 
 // Minimum waves per SIMD the verify kernel is compiled for (the second
@@ -156,6 +157,30 @@ __global__ __launch_bounds__(64, CMTV_QUAD_WAVES_PER_EU) void k_verify_oct(uint3
   if (threadIdx.x == 0 && out_bitmap) reinterpret_cast<uint8_t*>(out_bitmap)[gid >> 6] = (uint8_t)x;
 }
 
+struct LdsBytes {
+  uint8_t* p;
+  __device__ __forceinline__ void put(uint32_t pos, uint8_t b) { p[pos] = b; }
+};
+
+// Message of signature i for a helper lane: the CanonicalVote written into
+// this lane's LDS slot from the commit template (sb.tmpls set; the host
+// checked every message fits kSbFuseMaxMsg bytes), else msg[off[i]..off[i+1]).
+// A lane hashes only bytes it wrote itself (sha512_prefixed loads only words
+// holding message bytes), so no barrier is needed.
+__device__ __forceinline__ void helper_message(const SbFuse& sb, uint32_t i, const uint8_t* msg, const uint32_t* off,
+                                               uint32_t* slot, const uint8_t*& mp, uint32_t& ml) {
+  if (sb.tmpls) {
+    LdsBytes out{reinterpret_cast<uint8_t*>(slot)};
+    const SbTemplate tp = static_cast<const SbTemplate*>(sb.tmpls)[sb.tidx[i]];
+    ml = sb_write(out, tp, sb.blob, sb.flag[i] != 0, sb.sec[i], sb.nanos[i]);
+    mp = reinterpret_cast<const uint8_t*>(slot);
+  } else {
+    const uint32_t m0 = off[i];
+    mp = msg + m0;
+    ml = off[i + 1] - m0;
+  }
+}
+
 // The quad verifier with a helper wave: a 4-wave workgroup takes 48
 // signatures; waves 0-2 are quad waves (16 signatures each) and wave 3 hashes
 // and splits the scalars of all 48 (one lane each, q_prepare) while they
@@ -168,18 +193,22 @@ template <uint32_t MODE>
 __global__ __launch_bounds__(256, CMTV_QUAD_WAVES_PER_EU) void k_verify_quad_split(
     uint32_t n, const uint32_t* __restrict__ pk, const uint32_t* __restrict__ sig, const uint8_t* __restrict__ msg,
     const uint32_t* __restrict__ off, const uint32_t* __restrict__ btab, uint8_t* __restrict__ out_valid,
-    uint64_t* __restrict__ out_bitmap, uint32_t force_wide) {
+    uint64_t* __restrict__ out_bitmap, uint32_t force_wide, SbFuse sb) {
   const uint32_t wave = threadIdx.x >> 6, t = threadIdx.x & 63;
   const uint32_t base = blockIdx.x * 48;
   __shared__ uint32_t prep[48][SIG_PREP_WORDS + 1];
   __shared__ uint32_t bpt[48][40];  // [u]B in the quads' cached coordinates
   __shared__ uint2 tab_lds[3][2 * 9 * 5 * 64];
+  __shared__ uint32_t sbm[48][kSbFuseMaxMsg / 4];  // fused sign-bytes
   if (wave == 3) {
-    const uint32_t s = base + (t < 48 ? t : 47);
+    const uint32_t slot = t < 48 ? t : 47;
+    const uint32_t s = base + slot;
     const uint32_t i = s < n ? s : n - 1;
-    const uint32_t m0 = off[i], m1 = off[i + 1];
+    const uint8_t* mp;
+    uint32_t ml;
+    helper_message(sb, i, msg, off, sbm[slot], mp, ml);
     SigPrep p;
-    q_prepare<MODE>(p, pk + 8 * (size_t)i, sig + 16 * (size_t)i, msg + m0, m1 - m0, force_wide != 0);
+    q_prepare<MODE>(p, pk + 8 * (size_t)i, sig + 16 * (size_t)i, mp, ml, force_wide != 0);
     if (t < 48) sig_prep_store(prep[t], p);
     __syncthreads();  // 1: the scalars, as the quad waves finish decoding
     ge_p3 B;
@@ -229,7 +258,7 @@ template <uint32_t MODE>
 __global__ __launch_bounds__(128, CMTV_QUAD_WAVES_PER_EU) void k_verify_oct_split(
     uint32_t n, const uint32_t* __restrict__ pk, const uint32_t* __restrict__ sig, const uint8_t* __restrict__ msg,
     const uint32_t* __restrict__ off, const uint32_t* __restrict__ btab, uint8_t* __restrict__ out_valid,
-    uint64_t* __restrict__ out_bitmap, uint32_t force_wide) {
+    uint64_t* __restrict__ out_bitmap, uint32_t force_wide, SbFuse sb) {
   const uint32_t t = threadIdx.x & 63;
   const uint32_t gid = blockIdx.x * 64 + t;
   const uint32_t s = gid >> 3;
@@ -238,10 +267,15 @@ __global__ __launch_bounds__(128, CMTV_QUAD_WAVES_PER_EU) void k_verify_oct_spli
   __shared__ uint32_t prep[8][SIG_PREP_WORDS + 1];
   __shared__ uint32_t bpt[8][40];
   __shared__ uint2 tab_lds[9 * 5 * 64];
+  __shared__ uint32_t sbm[8][kSbFuseMaxMsg / 4];  // fused sign-bytes
   if (threadIdx.x >= 64) {
-    const uint32_t m0 = off[i], m1 = off[i + 1];
+    // the oct's 8 helper lanes write the same bytes to the same slot, and
+    // each hashes what it wrote
+    const uint8_t* mp;
+    uint32_t ml;
+    helper_message(sb, i, msg, off, sbm[t >> 3], mp, ml);
     SigPrep p;
-    q_prepare<MODE>(p, pk + 8 * (size_t)i, sig + 16 * (size_t)i, msg + m0, m1 - m0, force_wide != 0);
+    q_prepare<MODE>(p, pk + 8 * (size_t)i, sig + 16 * (size_t)i, mp, ml, force_wide != 0);
     if ((t & 7) == 0) sig_prep_store(prep[t >> 3], p);
     __syncthreads();  // 1: the scalars
     ge_p3 B;
@@ -417,7 +451,8 @@ hipError_t launch_btab_init(uint32_t* d_rows, hipStream_t s) {
 
 hipError_t launch_verify(uint32_t mode, uint32_t n, const void* pk, const void* sig, const void* msg,
                          const void* off, const uint32_t* btab, uint32_t* atab, void* valid, void* bitmap,
-                         uint32_t kflags, hipStream_t s) {
+                         uint32_t kflags, hipStream_t s, const SbFuse* sb) {
+  const SbFuse fz = sb ? *sb : SbFuse{};
   const bool quad = kflags & kLaunchQuad;
   const uint32_t fw = (kflags & kLaunchForceWide) ? 1u : 0u;
   if (n == 0) return hipSuccess;
@@ -431,10 +466,11 @@ hipError_t launch_verify(uint32_t mode, uint32_t n, const void* pk, const void* 
     // one 128-lane block (2 waves) = 8 signatures; whole groups of 8 blocks
     const dim3 grid(((n + 63) / 64) * 8), block(128);
     if (mode == MODE_ZIP215)
-      hipLaunchKernelGGL(k_verify_oct_split<MODE_ZIP215>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp, fw);
+      hipLaunchKernelGGL(k_verify_oct_split<MODE_ZIP215>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp, fw,
+                         fz);
     else
       hipLaunchKernelGGL(k_verify_oct_split<MODE_GO_STDLIB>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp,
-                         fw);
+                         fw, fz);
     return hipGetLastError();
   }
   if (quad && (kflags & kLaunchOct)) {
@@ -453,10 +489,11 @@ hipError_t launch_verify(uint32_t mode, uint32_t n, const void* pk, const void* 
     const uint32_t slices = 4 * ((n + 63) / 64);
     const dim3 grid((slices + 2) / 3), block(256);
     if (mode == MODE_ZIP215)
-      hipLaunchKernelGGL(k_verify_quad_split<MODE_ZIP215>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp, fw);
+      hipLaunchKernelGGL(k_verify_quad_split<MODE_ZIP215>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp, fw,
+                         fz);
     else
       hipLaunchKernelGGL(k_verify_quad_split<MODE_GO_STDLIB>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp,
-                         fw);
+                         fw, fz);
     return hipGetLastError();
   }
   if (quad) {

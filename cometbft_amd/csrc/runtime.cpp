@@ -352,6 +352,8 @@ struct cmtv_ctx {
   uint64_t fault_at = 0, launch_seq = 0;
   // CMTV_FORCE_WIDE: quad kernels take the 64-window half-scalar fallback
   bool force_wide = false;
+  // templated sign-bytes in the split kernels' helper waves (CMTV_NO_SB_FUSE=1: off)
+  bool sb_fuse = true;
 };
 
 struct cmtv_keyset {
@@ -394,11 +396,22 @@ static bool fault_hit(cmtv_ctx* ctx) {
 
 // Enqueue verification of n signatures whose inputs are in device memory of
 // device D (current on this thread).
+// The kernel enqueue_verify picks for n Ed25519 signatures is a helper-wave
+// form (k_verify_oct_split / k_verify_quad_split), whose helper can write
+// templated sign-bytes itself (kernels.h SbFuse).
+static bool split_kernel_for(const cmtv_ctx* ctx, size_t n) {
+  const bool quad = n <= ctx->quad_max;
+  const bool oct = quad && n <= ctx->oct_max;
+  return oct ? n <= ctx->oct_split_max : (quad && n <= ctx->quad_split_max);
+}
+
 static int enqueue_verify(cmtv_ctx* ctx, CmtvDev& D, size_t n, const uint8_t* d_pk, const uint8_t* d_sig,
                           const uint8_t* d_msg, const uint32_t* d_off, uint32_t mode, uint8_t* d_valid,
-                          uint64_t* d_bitmap, hipStream_t s) {
+                          uint64_t* d_bitmap, hipStream_t s, const SbFuse* sb = nullptr) {
   if (n == 0) return CMTV_OK;
   if (fault_hit(ctx)) return CMTV_EHIP;
+  // fused sign-bytes only where the split kernels run, in one launch
+  if (sb && (mode == kModeSr25519 || !split_kernel_for(ctx, n) || n > kChunk)) return CMTV_EINVAL;
   // Small batches cannot fill the chip at one signature per lane: use the
   // 4-lanes-per-signature kernel below the crossover (quad.h,
   // sr25519_quad.h).
@@ -435,7 +448,7 @@ static int enqueue_verify(cmtv_ctx* ctx, CmtvDev& D, size_t n, const uint8_t* d_
     else
       e = launch_verify(mode, cn, d_pk + 32 * c, d_sig + 64 * c, d_msg, d_off + c, D.d_btab,
                         static_cast<uint32_t*>(D.d_atab.p), d_valid ? d_valid + c : nullptr,
-                        d_bitmap ? d_bitmap + c / 64 : nullptr, kflags, s);
+                        d_bitmap ? d_bitmap + c / 64 : nullptr, kflags, s, sb);
     if (e != hipSuccess) {
       D.timing.abandon(tp);
       return hip_fail(e);
@@ -624,7 +637,13 @@ static int enqueue_shard(cmtv_ctx* ctx, size_t g, const HostBatch& B, size_t a, 
   std::memcpy(hin + o_sig, B.sig + 64 * a, 64 * m);
   auto* hoff = reinterpret_cast<uint32_t*>(hin + o_off);
   const uint32_t base = B.msg_off[a];
+  uint32_t max_len = 0;
   for (size_t i = 0; i <= m; i++) hoff[i] = B.msg_off[a + i] - base;
+  for (size_t i = 0; i < m; i++) max_len = std::max(max_len, hoff[i + 1] - hoff[i]);
+  // templated sign-bytes written by the verify kernel's helper wave (no
+  // k_sign_bytes launch) when the batch runs a split kernel and every
+  // message fits the helper's LDS slot; CMTV_NO_SB_FUSE turns it off
+  const bool fuse = tpl && !keyed && ctx->sb_fuse && max_len <= kSbFuseMaxMsg && split_kernel_for(ctx, m);
   if (tpl) {
     std::memcpy(hin + o_tidx, B.tidx + a, 4 * m);
     std::memcpy(hin + o_flag, B.tflag + a, m);
@@ -639,7 +658,16 @@ static int enqueue_shard(cmtv_ctx* ctx, size_t g, const HostBatch& B, size_t a, 
   auto* din = static_cast<uint8_t*>(D.d_in.p);
   auto* dout = static_cast<uint8_t*>(D.d_out.p);
   if ((e = hipMemcpyAsync(din, hin, in_bytes, hipMemcpyHostToDevice, D.stream)) != hipSuccess) return hip_fail(e);
-  if (tpl) {
+  SbFuse sb;
+  if (fuse) {
+    sb.tmpls = din + o_tmpl;
+    sb.blob = din + o_blob;
+    sb.tidx = reinterpret_cast<uint32_t*>(din + o_tidx);
+    sb.flag = din + o_flag;
+    sb.sec = reinterpret_cast<int64_t*>(din + o_sec);
+    sb.nanos = reinterpret_cast<int32_t*>(din + o_nanos);
+    ctx->stats.fused_sign_bytes++;
+  } else if (tpl) {
     // k_sign_bytes also writes the 16 zero bytes after the last message
     if ((e = launch_sign_bytes((uint32_t)m, din + o_tmpl, din + o_blob, reinterpret_cast<uint32_t*>(din + o_tidx),
                                din + o_flag, reinterpret_cast<int64_t*>(din + o_sec),
@@ -653,7 +681,7 @@ static int enqueue_shard(cmtv_ctx* ctx, size_t g, const HostBatch& B, size_t a, 
                                 din + o_sig, din + o_msg, reinterpret_cast<uint32_t*>(din + o_off), B.mode, dv,
                                 bitmap, D.stream);
   return enqueue_verify(ctx, D, m, din + o_key, din + o_sig, din + o_msg, reinterpret_cast<uint32_t*>(din + o_off),
-                        B.mode, dv, bitmap, D.stream);
+                        B.mode, dv, bitmap, D.stream, fuse ? &sb : nullptr);
 }
 
 // Verdicts of a host batch, sharded over the context's devices. Caller holds
@@ -920,6 +948,7 @@ static void read_env(cmtv_ctx* ctx) {
   if (const char* sm = std::getenv("CMTV_SHARD_MIN")) ctx->shard_min = (size_t)std::strtoull(sm, nullptr, 10);
   if (const char* fa = std::getenv("CMTV_FAULT_AT")) ctx->fault_at = (uint64_t)std::strtoull(fa, nullptr, 10);
   if (const char* fw = std::getenv("CMTV_FORCE_WIDE")) ctx->force_wide = fw[0] == '1';
+  if (const char* nf = std::getenv("CMTV_NO_SB_FUSE")) ctx->sb_fuse = nf[0] != '1';
 }
 
 // CMTVERIFY_DEVICES: "0,1,2" or "all" (or unset: every visible device)

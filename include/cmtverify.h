@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define CMTV_ABI_VERSION 4
+#define CMTV_ABI_VERSION 5
 
 enum {
   CMTV_OK = 0,
@@ -88,6 +88,8 @@ typedef struct cmtv_stats {
   uint64_t faults_injected;/* launches failed by the CMTV_FAULT_AT knob */
   uint32_t n_devices;      /* devices driven by the context       */
   uint32_t rccl;           /* 1: gathers run over an RCCL communicator */
+  uint64_t fused_sign_bytes; /* templated batches whose sign-bytes the verify
+                              kernel's helper wave wrote (no k_sign_bytes) */
 } cmtv_stats;
 
 /* ------------------------------------------------------------ lifecycle */

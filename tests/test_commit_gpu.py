@@ -234,16 +234,25 @@ def test_large_commit_first_error_in_index_order(gpu_ctx):
     assert isinstance(e, T.ErrWrongSignature) and e.index == 250
 
 
-@pytest.mark.parametrize("chain", ["", "c", "x" * 50])
-def test_device_sign_bytes_templating(gpu_ctx, chain):
+@pytest.mark.parametrize("fuse", [True, False])
+@pytest.mark.parametrize("chain", ["", "c", "x" * 50, "y" * 150])
+def test_device_sign_bytes_templating(monkeypatch, chain, fuse):
     """with the verdict cache off, cmtv_verify_commit ships
     one CanonicalVote template per commit and (flag, seconds, nanos) per
-    signature, and k_sign_bytes writes the sign-bytes on the device. The
-    signatures here are made by the oracle over the oracle encoder's bytes
-    (pinned by types/vote_test.go's KATs), so any byte the device writes
-    differently fails verification. Timestamps cover zero, negative, one- to
-    ten-byte varints and the Go zero time; rounds, heights and nil votes vary."""
+    signature, and the device writes the sign-bytes: the split kernels'
+    helper wave writes them into LDS itself (fused), or k_sign_bytes into HBM
+    (CMTV_NO_SB_FUSE=1, and any batch with a message over the helper's
+    192-byte slot, e.g. the 150-character chain id). The signatures here are
+    made by the oracle over the oracle encoder's bytes (pinned by
+    types/vote_test.go's KATs), so any byte the device writes differently
+    fails verification. Timestamps cover zero, negative, one- to ten-byte
+    varints and the Go zero time; rounds, heights and nil votes vary."""
     from cometbft_amd import Context
+
+    if not fuse:
+        monkeypatch.setenv("CMTV_NO_SB_FUSE", "1")
+    gpu_ctx = Context(device=0)
+    monkeypatch.delenv("CMTV_NO_SB_FUSE", raising=False)
 
     secs = [0, 1, 127, 128, 2**40, -1, -62135596800, 1_700_000_000]
     nanos = [0, 1, 127, 128, 999_999_999, 5]
@@ -268,3 +277,5 @@ def test_device_sign_bytes_templating(gpu_ctx, chain):
                                              if j == 5 else s for j, s in enumerate(sigs)])
         e = _err(lambda: vset.verify_commit(chain, bid, height, bad, ctx=gpu_ctx))
         assert isinstance(e, T.ErrWrongSignature) and e.index == 5
+    fused = gpu_ctx.stats()["fused_sign_bytes"]
+    assert (fused > 0) == (fuse and len(chain) <= 50), fused

@@ -160,6 +160,29 @@ __global__ __launch_bounds__(64, CMTV_QUAD_WAVES_PER_EU) void k_verify_oct(uint3
 struct LdsBytes {
   uint8_t* p;
   __device__ __forceinline__ void put(uint32_t pos, uint8_t b) { p[pos] = b; }
+  // a template byte run from HBM: aligned dword loads issued 8 at a time
+  // (one memory round trip per 32 bytes instead of one per byte), bytes
+  // placed into the LDS slot
+  __device__ __forceinline__ void copy(uint32_t pos, const uint8_t* src, uint32_t len) {
+    const uintptr_t a = (uintptr_t)src;
+    const int sh = (int)(a & 3);
+    const uint32_t* w = (const uint32_t*)(a - sh);
+    const uint32_t nw = ((uint32_t)sh + len + 3) >> 2;  // words holding bytes of the run
+#pragma unroll 1
+    for (uint32_t j = 0; j < nw; j += 8) {
+      uint32_t v[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) v[k] = j + k < nw ? w[j + k] : 0u;
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+          const int q = 4 * (int)(j + k) + b - sh;
+          if (q >= 0 && q < (int)len) p[pos + q] = (uint8_t)(v[k] >> (8 * b));
+        }
+      }
+    }
+  }
 };
 
 // Message of signature i for a helper lane: the CanonicalVote written into

@@ -71,14 +71,16 @@ CMTV_HD uint32_t sb_put_uvarint(Out& out, uint32_t pos, uint64_t v) {
   return pos;
 }
 
-// The whole message of one signature. Out: put(pos, byte).
+// The whole message of one signature. Out: put(pos, byte) and
+// copy(pos, src, len) (the template's byte runs).
 template <class Out>
 CMTV_HD uint32_t sb_write(Out& out, const SbTemplate& t, const uint8_t* blob, bool commit_flag, int64_t sec,
                           int32_t nanos) {
   uint32_t pos = sb_put_uvarint(out, 0, sb_body_len(t, commit_flag, sec, nanos));
   const uint32_t po = commit_flag ? t.pre_commit_off : t.pre_nil_off;
   const uint32_t pl = commit_flag ? t.pre_commit_len : t.pre_nil_len;
-  for (uint32_t i = 0; i < pl; i++) out.put(pos++, blob[po + i]);
+  out.copy(pos, blob + po, pl);
+  pos += pl;
   out.put(pos++, 0x2A);
   pos = sb_put_uvarint(out, pos, sb_ts_len(sec, nanos));
   if (sec != 0) {
@@ -89,8 +91,8 @@ CMTV_HD uint32_t sb_write(Out& out, const SbTemplate& t, const uint8_t* blob, bo
     out.put(pos++, 0x10);
     pos = sb_put_uvarint(out, pos, (uint64_t)(int64_t)nanos);
   }
-  for (uint32_t i = 0; i < t.post_len; i++) out.put(pos++, blob[t.post_off + i]);
-  return pos;
+  out.copy(pos, blob + t.post_off, t.post_len);
+  return pos + t.post_len;
 }
 
 }  // namespace cmtv

@@ -13,6 +13,9 @@ namespace cmtv {
 struct DevBytes {
   uint8_t* __restrict__ p;
   __device__ __forceinline__ void put(uint32_t pos, uint8_t b) { p[pos] = b; }
+  __device__ __forceinline__ void copy(uint32_t pos, const uint8_t* src, uint32_t len) {
+    for (uint32_t i = 0; i < len; i++) p[pos + i] = src[i];
+  }
 };
 
 __global__ __launch_bounds__(256) void k_sign_bytes(uint32_t n, const SbTemplate* __restrict__ tmpls,

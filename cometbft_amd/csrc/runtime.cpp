@@ -318,6 +318,9 @@ struct CmtvDev {
   // small single-device host batches: the kernel writes the verdict bitmap
   // straight into this coherent, device-mapped host buffer (no D2H copy)
   HostBuf h_zc{nullptr, 0, hipHostMallocCoherent | hipHostMallocMapped};
+  // ... and, with fused sign-bytes, reads its inputs straight from this one
+  // (no H2D copy, no copy-engine -> compute dependency before the kernel)
+  HostBuf h_zin{nullptr, 0, hipHostMallocCoherent | hipHostMallocMapped};
   // The lane kernels' A-table scratch is shared by every launch on this
   // device, whatever stream it is enqueued on: each lane launch waits for the
   // previous one (atab_done) so calls on different streams cannot overwrite
@@ -354,6 +357,8 @@ struct cmtv_ctx {
   bool force_wide = false;
   // templated sign-bytes in the split kernels' helper waves (CMTV_NO_SB_FUSE=1: off)
   bool sb_fuse = true;
+  // fused small host batches read their inputs from mapped host memory (CMTV_NO_ZC_IN=1: off)
+  bool zc_in = true;
 };
 
 struct cmtv_keyset {
@@ -598,7 +603,7 @@ struct HostBatch {
 // verification; verdict bytes to D.d_out (when want_valid), bitmap words to
 // `bitmap` (device memory of D).
 static int enqueue_shard(cmtv_ctx* ctx, size_t g, const HostBatch& B, size_t a, size_t b, bool want_valid,
-                         uint64_t* bitmap, size_t& o_valid_out) {
+                         uint64_t* bitmap, size_t& o_valid_out, bool zero_copy = false) {
   CmtvDev& D = ctx->devs[g];
   const size_t m = b - a;
   const bool keyed = B.ks != nullptr, tpl = B.msg == nullptr;
@@ -626,24 +631,29 @@ static int enqueue_shard(cmtv_ctx* ctx, size_t g, const HostBatch& B, size_t a, 
   o_valid_out = o_valid;
   hipError_t e;
   (void)hipSetDevice(D.ordinal);
-  if ((e = D.h_in.ensure(in_bytes)) != hipSuccess) return hip_fail(e);
-  if ((e = D.d_in.ensure(dev_bytes)) != hipSuccess) return hip_fail(e);
+  // message lengths first: they decide the fused / zero-copy forms
+  const uint32_t base = B.msg_off[a];
+  uint32_t max_len = 0;
+  for (size_t i = 0; i < m; i++) max_len = std::max(max_len, B.msg_off[a + i + 1] - B.msg_off[a + i]);
+  // templated sign-bytes written by the verify kernel's helper wave (no
+  // k_sign_bytes launch) when the batch runs a split kernel and every
+  // message fits the helper's LDS slot; CMTV_NO_SB_FUSE turns it off
+  const bool fuse = tpl && !keyed && ctx->sb_fuse && max_len <= kSbFuseMaxMsg && split_kernel_for(ctx, m);
+  // a fused small batch reads its staging in mapped host memory directly
+  // (CMTV_NO_ZC_IN turns it off)
+  const bool zc = zero_copy && fuse && ctx->zc_in;
+  HostBuf& HB = zc ? D.h_zin : D.h_in;
+  if ((e = HB.ensure(in_bytes)) != hipSuccess) return hip_fail(e);
+  if (!zc && (e = D.d_in.ensure(dev_bytes)) != hipSuccess) return hip_fail(e);
   if ((e = D.d_out.ensure(out_bytes)) != hipSuccess) return hip_fail(e);
-  auto* hin = static_cast<uint8_t*>(D.h_in.p);
+  auto* hin = static_cast<uint8_t*>(HB.p);
   if (keyed)
     std::memcpy(hin + o_key, B.key_idx + a, 4 * m);
   else
     std::memcpy(hin + o_key, B.pk + 32 * a, 32 * m);
   std::memcpy(hin + o_sig, B.sig + 64 * a, 64 * m);
   auto* hoff = reinterpret_cast<uint32_t*>(hin + o_off);
-  const uint32_t base = B.msg_off[a];
-  uint32_t max_len = 0;
   for (size_t i = 0; i <= m; i++) hoff[i] = B.msg_off[a + i] - base;
-  for (size_t i = 0; i < m; i++) max_len = std::max(max_len, hoff[i + 1] - hoff[i]);
-  // templated sign-bytes written by the verify kernel's helper wave (no
-  // k_sign_bytes launch) when the batch runs a split kernel and every
-  // message fits the helper's LDS slot; CMTV_NO_SB_FUSE turns it off
-  const bool fuse = tpl && !keyed && ctx->sb_fuse && max_len <= kSbFuseMaxMsg && split_kernel_for(ctx, m);
   if (tpl) {
     std::memcpy(hin + o_tidx, B.tidx + a, 4 * m);
     std::memcpy(hin + o_flag, B.tflag + a, m);
@@ -655,9 +665,15 @@ static int enqueue_shard(cmtv_ctx* ctx, size_t g, const HostBatch& B, size_t a, 
     if (mb) std::memcpy(hin + o_msg, B.msg + base, mb);
     std::memset(hin + o_msg + mb, 0, 16);
   }
-  auto* din = static_cast<uint8_t*>(D.d_in.p);
+  uint8_t* din = static_cast<uint8_t*>(D.d_in.p);
   auto* dout = static_cast<uint8_t*>(D.d_out.p);
-  if ((e = hipMemcpyAsync(din, hin, in_bytes, hipMemcpyHostToDevice, D.stream)) != hipSuccess) return hip_fail(e);
+  if (zc) {
+    void* p = nullptr;
+    if ((e = hipHostGetDevicePointer(&p, HB.p, 0)) != hipSuccess) return hip_fail(e);
+    din = static_cast<uint8_t*>(p);
+  } else if ((e = hipMemcpyAsync(din, hin, in_bytes, hipMemcpyHostToDevice, D.stream)) != hipSuccess) {
+    return hip_fail(e);
+  }
   SbFuse sb;
   if (fuse) {
     sb.tmpls = din + o_tmpl;
@@ -701,7 +717,7 @@ static int run_host_batch_(cmtv_ctx* ctx, const HostBatch& B, uint8_t* out_valid
     void* dzc = nullptr;
     if ((e = hipHostGetDevicePointer(&dzc, D.h_zc.p, 0)) != hipSuccess) return hip_fail(e);
     size_t o_valid = 0;
-    const int rc = enqueue_shard(ctx, 0, B, 0, n, false, static_cast<uint64_t*>(dzc), o_valid);
+    const int rc = enqueue_shard(ctx, 0, B, 0, n, false, static_cast<uint64_t*>(dzc), o_valid, true);
     if (rc != CMTV_OK) return rc;
     if ((e = hipStreamSynchronize(D.stream)) != hipSuccess) return hip_fail(e);
     harvest(ctx, false);
@@ -921,6 +937,7 @@ static void release_device(CmtvDev& D) {
   D.h_in.release();
   D.h_out.release();
   D.h_zc.release();
+  D.h_zin.release();
   if (D.d_btab) (void)hipFree(D.d_btab);
   if (D.d_bcomb) (void)hipFree(D.d_bcomb);
   if (D.d_srprog) (void)hipFree(D.d_srprog);
@@ -949,6 +966,7 @@ static void read_env(cmtv_ctx* ctx) {
   if (const char* fa = std::getenv("CMTV_FAULT_AT")) ctx->fault_at = (uint64_t)std::strtoull(fa, nullptr, 10);
   if (const char* fw = std::getenv("CMTV_FORCE_WIDE")) ctx->force_wide = fw[0] == '1';
   if (const char* nf = std::getenv("CMTV_NO_SB_FUSE")) ctx->sb_fuse = nf[0] != '1';
+  if (const char* nz = std::getenv("CMTV_NO_ZC_IN")) ctx->zc_in = nz[0] != '1';
 }
 
 // CMTVERIFY_DEVICES: "0,1,2" or "all" (or unset: every visible device)

@@ -8,7 +8,7 @@ timeout -k 10 600 python -u -m pytest tests/test_commit_gpu.py tests/test_baseli
 tail -3 "$OUT/pytest.log"
 Q="--no-cpu-baseline --no-sr25519 --no-light --no-c3 --steps 50 --warmup 5"
 timeout -k 10 300 python bench.py $Q > "$OUT/bench_fused.json" 2> "$OUT/bench_fused.err" || { tail -20 "$OUT/bench_fused.err"; exit 1; }
-CMTV_NO_SB_FUSE=1 timeout -k 10 300 python bench.py $Q > "$OUT/bench_nofuse.json" 2> "$OUT/bench_nofuse.err" || { tail -20 "$OUT/bench_nofuse.err"; exit 1; }
+CMTV_NO_ZC_IN=1 timeout -k 10 300 python bench.py $Q > "$OUT/bench_nofuse.json" 2> "$OUT/bench_nofuse.err" || { tail -20 "$OUT/bench_nofuse.err"; exit 1; }
 python - <<'PY'
 import json
 for f in ("fused", "nofuse"):

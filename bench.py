@@ -354,10 +354,33 @@ def replay_line(dev_index, heights=60, n_vals=150):
     errs = T.verify_commits(0, TU.CHAIN_ID, chain, ctx=plain)
     t_batch = (time.perf_counter() - t) / heights
     assert all(e is None for e in errs)
+    # the same through the C ABI with the arguments packed once, as a cgo
+    # shim holds them (the Python mirror above re-packs every call)
+    per_height = [(T.PackedCommits(1, TU.CHAIN_ID, [it]), T.PackedCommits(0, TU.CHAIN_ID, [it])) for it in chain]
+
+    def blocksync_c(ctx):
+        for light, full in per_height:
+            light.call(ctx)
+            full.call(ctx)
+            full.call(ctx)
+
+    blocksync_c(plain)
+    t = time.perf_counter()
+    blocksync_c(plain)
+    t_plain_c = (time.perf_counter() - t) / heights
+    whole = T.PackedCommits(0, TU.CHAIN_ID, chain)
+    whole.call(plain)
+    t = time.perf_counter()
+    whole.call(plain)
+    t_batch_c = (time.perf_counter() - t) / heights
+    assert all(r == 0 for r in whole.rcs)
     return {"workload": f"{heights} heights x {n_vals}-validator commits, blocksync pattern (light + 2 x full)",
             "ms_per_height_plain": round(t_plain * 1e3, 4), "ms_per_height_verdict_cache": round(t_cached * 1e3, 4),
             "ms_per_height_cross_height_batch": round(t_batch * 1e3, 4),
-            "note": "host API end to end; cross-height = one cmtv_verify_commits (VerifyCommit) over all heights"}
+            "c_call": {"ms_per_height_plain": round(t_plain_c * 1e3, 4),
+                       "ms_per_height_cross_height_batch": round(t_batch_c * 1e3, 4)},
+            "note": "host API end to end through the Python mirror (re-packs each call); c_call: the C ABI with "
+                    "arguments packed once; cross-height = one cmtv_verify_commits (VerifyCommit) over all heights"}
 
 
 def light_line(dev_index, heights=1000, n_vals=100):
@@ -399,6 +422,24 @@ def light_line(dev_index, heights=1000, n_vals=100):
     errs = T.verify_commits(1, TU.CHAIN_ID, seq, ctx=kctx)
     t_kbatch = time.perf_counter() - t
     assert all(e is None for e in errs)
+    # the C calls alone, arguments packed once (what the cgo shim passes)
+    per_call = [T.PackedCommits(1, TU.CHAIN_ID, [it]) for it in seq]
+    for p in per_call[:20]:
+        p.call(ctx)
+    t = time.perf_counter()
+    for p in per_call:
+        p.call(ctx)
+    t_seq_c = time.perf_counter() - t
+    whole = T.PackedCommits(1, TU.CHAIN_ID, seq)
+    whole.call(ctx)
+    t = time.perf_counter()
+    whole.call(ctx)
+    t_batch_c = time.perf_counter() - t
+    whole.call(kctx)
+    t = time.perf_counter()
+    whole.call(kctx)
+    t_kbatch_c = time.perf_counter() - t
+    assert all(r == 0 for r in whole.rcs)
     vals, bid, h, c = chain[-1]
     ts = []
     for _ in range(50):
@@ -424,6 +465,9 @@ def light_line(dev_index, heights=1000, n_vals=100):
             "sequential_ms_per_call_loop": round(t_seq * 1e3, 2),
             "sequential_ms_cross_height_batch": round(t_batch * 1e3, 2),
             "sequential_ms_cross_height_batch_keyset": round(t_kbatch * 1e3, 2),
+            "c_call": {"sequential_ms_per_call_loop": round(t_seq_c * 1e3, 2),
+                       "sequential_ms_cross_height_batch": round(t_batch_c * 1e3, 2),
+                       "sequential_ms_cross_height_batch_keyset": round(t_kbatch_c * 1e3, 2)},
             "bisection_p50_ms": round(float(np.median(ts)) * 1e3, 4),
             "cpu_single_core_sequential_ms": round(cpu_seq_s * 1e3, 1),
             "note": f"{len(seq)} VerifyCommitLight calls; CPU = oracle verifying the same "
@@ -769,7 +813,7 @@ def main():
         "ms_per_step": round(el_z / args.steps * 1e3, 4), "kernel_ms": round(kms_z, 4),
         "frac": round(args.n * MACS_PER_VERIFY / (kms_z * 1e-3) / 1e12 / INT_MAC_PEAK_T, 4)}
     line["e2e_10k"] = e2e_10k(Context(device=0), D.host[0], mode)
-    if not args.no_cpu_baseline:
+    if not args.no_cpu_baseline and n_dev == 1:  # rank 0 at N=1 only (bench contract)
         pk, sigs, m, off = D.host[0]
         line["cpu_baseline"] = cpu_baseline(pk, sigs, m, off, mode, args.cpu_seconds)
         cb = line["cpu_baseline"]

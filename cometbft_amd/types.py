@@ -295,38 +295,53 @@ def verify_commits(kind: int, chain_id: str, items, ctx: Context | None = None, 
     the device in ONE batch; returns, per item, None (the reference's nil) or
     the exception its VerifyCommit* would have returned -- not raised, so one
     bad height does not hide the others."""
-    ctx = ctx or default_context()
-    n = len(items)
-    if n == 0:
+    if len(items) == 0:
         return []
-    keep = []
-    vs_arr = (N.cmtv_valset * n)()
-    cm_arr = (N.cmtv_commit * n)()
-    bid_arr = (N.cmtv_block_id * n)()
-    heights = (ctypes.c_int64 * n)()
-    for c, (vals, block_id, height, commit) in enumerate(items):
-        vs, kv = vals._pack()
-        cm, kc = _pack_commit(commit)
-        vs_arr[c], cm_arr[c] = vs, cm
-        keep += [kv, kc]
-        if block_id is not None:
-            bid, kb = block_id._c()
-            bid_arr[c] = bid
-            keep.append(kb)
-        heights[c] = height
-    res = (N.cmtv_commit_result * n)()
-    rcs = (ctypes.c_int * n)()
-    cap = 1024
-    bufs = ctypes.create_string_buffer(n * cap)
-    cid = chain_id.encode()
-    num, den = trust_level if kind == N.VERIFY_COMMIT_LIGHT_TRUSTING else (0, 0)
-    rc = N.lib().cmtv_verify_commits(ctx.handle, kind, mode, cid, len(cid), n, vs_arr,
-                                     bid_arr if kind != N.VERIFY_COMMIT_LIGHT_TRUSTING else None, heights, cm_arr,
-                                     num, den, res, rcs, bufs, cap)
-    N.check(rc, "cmtv_verify_commits")
-    raw = bufs.raw
-    out = []
-    for c in range(n):
-        msg = raw[c * cap: (c + 1) * cap].split(b"\0", 1)[0].decode()
-        out.append(_error_for(rcs[c], res[c], msg))
-    return out
+    return PackedCommits(kind, chain_id, items, mode, trust_level).verify(ctx or default_context())
+
+
+class PackedCommits:
+    """The C arguments of one cmtv_verify_commits call, packed once (what a
+    cgo shim holds when it calls the library); verify() makes the call."""
+
+    def __init__(self, kind: int, chain_id: str, items, mode: int = MODE_GO_STDLIB, trust_level=(1, 3)):
+        n = len(items)
+        keep = []
+        vs_arr = (N.cmtv_valset * n)()
+        cm_arr = (N.cmtv_commit * n)()
+        bid_arr = (N.cmtv_block_id * n)()
+        heights = (ctypes.c_int64 * n)()
+        for c, (vals, block_id, height, commit) in enumerate(items):
+            vs, kv = vals._pack()
+            cm, kc = _pack_commit(commit)
+            vs_arr[c], cm_arr[c] = vs, cm
+            keep += [kv, kc]
+            if block_id is not None:
+                bid, kb = block_id._c()
+                bid_arr[c] = bid
+                keep.append(kb)
+            heights[c] = height
+        self.n, self.kind, self.mode, self.cap = n, kind, mode, 1024
+        self.cid = chain_id.encode()
+        self.num, self.den = trust_level if kind == N.VERIFY_COMMIT_LIGHT_TRUSTING else (0, 0)
+        self.vs_arr, self.cm_arr, self.heights, self._keep = vs_arr, cm_arr, heights, keep
+        self.bid_arr = bid_arr if kind != N.VERIFY_COMMIT_LIGHT_TRUSTING else None
+        self.res = (N.cmtv_commit_result * n)()
+        self.rcs = (ctypes.c_int * n)()
+        self.bufs = ctypes.create_string_buffer(n * self.cap)
+
+    def call(self, ctx: Context) -> None:
+        """The C call alone (results left in res / rcs / bufs)."""
+        rc = N.lib().cmtv_verify_commits(ctx.handle, self.kind, self.mode, self.cid, len(self.cid), self.n,
+                                         self.vs_arr, self.bid_arr, self.heights, self.cm_arr, self.num, self.den,
+                                         self.res, self.rcs, self.bufs, self.cap)
+        N.check(rc, "cmtv_verify_commits")
+
+    def verify(self, ctx: Context):
+        self.call(ctx)
+        raw, cap = self.bufs.raw, self.cap
+        out = []
+        for c in range(self.n):
+            msg = raw[c * cap: (c + 1) * cap].split(b"\0", 1)[0].decode()
+            out.append(_error_for(self.rcs[c], self.res[c], msg))
+        return out

@@ -79,6 +79,7 @@ def parse():
     ap.add_argument("--c3-heights", type=int, default=100_000, help="configs[2] commits (150 validators each)")
     ap.add_argument("--no-sr25519", action="store_true", help="skip the configs[4] sr25519 side measurement")
     ap.add_argument("--no-light", action="store_true", help="skip the light-client replay line")
+    ap.add_argument("--no-keyset", action="store_true", help="skip the registered-keys 10k side line")
     ap.add_argument("--process-per-gpu", action="store_true",
                     help="one process per GPU over torch.distributed (the round-1 harness)")
     return ap.parse_args()
@@ -577,6 +578,58 @@ def c3_line(ctx, n_dev, mode, steps=3, n_heights=100_000, n_vals=150):
             "verdicts_ok": bool(ok), "setup_s": round(t_gen, 2)}
 
 
+def keyset_10k(ctx, D, mode, steps):
+    """configs[1] with the validator set registered once (cmtv_register_keys,
+    outside the timed region, as a node keeps it across heights): the same
+    10k commit, inputs in HBM, verified by key index
+    (cmtv_verify_ed25519_indexed_device: no decompression of A, the key's
+    comb instead of its doublings). A side line: the headline step decodes
+    every key, as the reference's VerifyCommit does."""
+    import torch
+
+    pk, sigs, m, off = D.host[0]
+    t = D.t[0]
+    dev = t["pk"].device
+    t_reg = time.perf_counter()
+    ks = ctx.register_keys(pk)
+    ctx.sync()
+    t_reg = time.perf_counter() - t_reg
+    idx = torch.arange(D.n, dtype=torch.int32, device=dev)
+    bm = torch.zeros(D.words, dtype=torch.int64, device=dev)
+
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        # the device entry point enqueues on the caller's stream: torch's
+        ctx.verify_indexed_device(ks, D.n, idx.data_ptr(), t["sig"].data_ptr(), t["m"].data_ptr(),
+                                  t["off"].data_ptr(), mode, 0, bm.data_ptr(), stream=stream.cuda_stream)
+
+    def sync():
+        stream.synchronize()
+        ctx.sync()
+
+    for _ in range(5):
+        step()
+    sync()
+    s0 = ctx.stats()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    el = time.perf_counter() - t0
+    s1 = ctx.stats()
+    kms = (s1["device_ms"] - s0["device_ms"]) / max(s1["calls"] - s0["calls"], 1)
+    ok = bool(np.array_equal(bm.cpu().numpy().view(np.uint64), t["bm"].cpu().numpy().view(np.uint64)))
+    ks.free()
+    ach = D.n / (kms * 1e-3) * MACS_PER_KEYED_VERIFY / 1e12 if kms > 0 else None
+    return {"value": round(D.n * steps / el, 1), "unit": "verifs/s", "ms_per_step": round(el / steps * 1e3, 4),
+            "kernel_ms": round(kms, 4), "register_keys_s": round(t_reg, 2),
+            "frac": round(ach / INT_MAC_PEAK_T, 4) if ach else None,
+            "work": f"{MACS_PER_KEYED_VERIFY} int32 MACs/keyed verify",
+            "verdicts_match_headline": ok,
+            "path": "cmtv_verify_ed25519_indexed_device over 10,000 registered keys (keyed quad kernel)"}
+
+
 def latency_150(ctx, mode, iters):
     """p50/p99 VerifyCommit latency for a 150-validator commit (host API, end
     to end): the C call alone (cmtv_verify_commit on a pre-packed commit, what
@@ -813,6 +866,8 @@ def main():
         "ms_per_step": round(el_z / args.steps * 1e3, 4), "kernel_ms": round(kms_z, 4),
         "frac": round(args.n * MACS_PER_VERIFY / (kms_z * 1e-3) / 1e12 / INT_MAC_PEAK_T, 4)}
     line["e2e_10k"] = e2e_10k(Context(device=0), D.host[0], mode)
+    if n_dev == 1 and not args.no_keyset:
+        line["keyset_10k"] = keyset_10k(ctx, D, mode, args.steps)
     if not args.no_cpu_baseline and n_dev == 1:  # rank 0 at N=1 only (bench contract)
         pk, sigs, m, off = D.host[0]
         line["cpu_baseline"] = cpu_baseline(pk, sigs, m, off, mode, args.cpu_seconds)

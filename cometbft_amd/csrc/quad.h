@@ -68,79 +68,79 @@ CMTV_HD void q_cached_identity(fe& v, int lane) {
 //   round 1: lane c squares {X, Y, Z, X+Y}[c]      -> A, B, C', K
 //   round 2: lane c multiplies {E'F', MS, F'M, E'S}[c],
 //            S = A + B, M = A - B, E' = S - K, F' = 2C' + M
-// Routing: lane c forms U_c = {E', F', M, S}[c] (one carry for all four),
-// then the operands are two quad_perm moves of U: {E', M, F', E'} and
-// {F', S, M, S}. Input T (lane 3) is ignored; output is a full extended point.
+// Routing: lane c forms U_c = {F', S, M, E'}[c] (one carry for all four).
+// The round-2 products form the cycle F'-E'-S-M-F', so each lane multiplies
+// its own U by one neighbour's: a single quad_perm move {E', M, F', S}. The
+// U_c take two moves of the round-1 results (lane 0 reads C', the rest A;
+// every lane B). Input T (lane 3) is ignored; output is a full extended point.
 template <class Q>
 CMTV_HD void q_dbl(const Q& q, fe& v) {
   const int lane = q.lane();
   // per-lane masks (loop-invariant): the four U_c share one straight-line
-  // form, U = a + (b ^ mb) + corr + 2p + (((r ^ mr) & rm) << sh), instead
-  // of computing all four candidates and selecting
+  // form, U = (p1 << sh) + (p2 ^ n2) + ((own ^ n3) & mo) + corr + 2p,
+  // instead of computing all four candidates and selecting
   const uint32_t m3 = lane == 3 ? ~0u : 0u;
-  const uint32_t mb = (lane == 1 || lane == 2) ? ~0u : 0u;  // -B on lanes 1, 2
-  const uint32_t mr = lane == 0 ? ~0u : 0u;                 // -K on lane 0
-  const uint32_t rm = lane < 2 ? ~0u : 0u;                  // r used on lanes 0, 1
-  const uint32_t sh = lane == 1 ? 1u : 0u;                  // 2C' on lane 1
-  const uint32_t corr = lane == 3 ? 0u : 1u;                // ~x = -x - 1
+  const uint32_t sh = lane == 0 ? 1u : 0u;                  // 2C' on lane 0
+  const uint32_t n2 = (lane & 1) ? 0u : ~0u;                // -B on lanes 0, 2
+  const uint32_t n3 = lane == 3 ? ~0u : 0u;                 // -K on lane 3
+  const uint32_t mo = (lane == 0 || lane == 3) ? ~0u : 0u;  // own A (0), K (3)
+  const uint32_t corr = lane == 1 ? 0u : 1u;                // ~x = -x - 1
   fe a, b, m;
   q.template perm<qp(0, 1, 2, 0)>(a, v);
   q.template perm<QP_B1>(b, v);
 #pragma unroll
   for (int i = 0; i < 10; i++) m.v[i] = a.v[i] + (b.v[i] & m3);  // X + Y on lane 3
-  fe_sq(m, m);
-  fe r;
-  q.template perm<QP_B0>(a, m);             // A
-  q.template perm<QP_B1>(b, m);             // B
-  q.template perm<qp(3, 2, 2, 2)>(r, m);    // lane 0: K, lane 1: C'
+  fe_sq(m, m);                                                   // A, B, C', K
+  q.template perm<qp(2, 0, 0, 0)>(a, m);  // C', A, A, A
+  q.template perm<QP_B1>(b, m);           // B
 #pragma unroll
   for (int i = 0; i < 10; i++) {
-    // lane 0: E' = S - K, 1: F' = M + 2C', 2: M = A - B, 3: S = A + B (+2p)
-    const uint32_t u = (b.v[i] ^ mb) + a.v[i] + corr + fe_p2(i);
-    m.v[i] = (CMTV_XOR_AND(r.v[i], mr, rm) << sh) + u;
+    // lane 0: F' = M + 2C', 1: S = A + B, 2: M = A - B, 3: E' = S - K (+2p)
+    const uint32_t u = (b.v[i] ^ n2) + CMTV_XOR_AND(m.v[i], n3, mo) + corr + fe_p2(i);
+    m.v[i] = (a.v[i] << sh) + u;
   }
   fe_carry(m);
-  q.template perm<qp(0, 2, 1, 0)>(a, m);  // E', M, F', E'
-  q.template perm<qp(1, 3, 2, 3)>(b, m);  // F', S, M, S
-  fe_mul(v, a, b);
+  q.template perm<qp(3, 2, 0, 1)>(a, m);  // E', M, F', S
+  fe_mul(v, m, a);                        // F'E', SM, MF', E'S
 }
 
 // Addition v += Q where c is this lane's coordinate of Q in cached form
 // (Y2-X2, Y2+X2, 2Z2, 2dT2):
-//   round 1: lane c computes {(Y1-X1)(Y2-X2), (Y1+X1)(Y2+X2), Z1 2Z2, T1 2dT2}[c]
-//            = {A, B, D, C}
+//   round 1: lane c computes {(X1-Y1)(Y2-X2), (Y1+X1)(Y2+X2), Z1 2Z2, T1 2dT2}[c]
+//            = {-A, B, D, C}  (lane 0 negates its own factor: X1 - Y1 needs
+//            one swap move of (X, Y) where Y1 - X1 needed two broadcasts)
 //   round 2: with E = B-A, F = D-C, G = D+C, H = B+A, lane c forms
-//            U_c = {E, F, G, H}[c] from two quad_perm moves (no carry: every
-//            U stays inside the multiplier bounds) and computes
-//            {FE, GH, FG, EH}[c] = (X3, Y3, Z3, T3) from two more.
+//            U_c = {E, G, F, H}[c] from two quad_perm moves (no carry: every
+//            U stays inside the multiplier bounds); the products form the
+//            cycle E-F-G-H-E, so lane c multiplies its own U by one move
+//            {F, H, G, E}: {EF, GH, FG, HE}[c] = (X3, Y3, Z3, T3).
 template <class Q>
 CMTV_HD void q_add(const Q& q, fe& v, const fe& c) {
   const int lane = q.lane();
   // per-lane masks (loop-invariant); ~x + 1 = -x supplies the negations
   const uint32_t m0 = lane == 0 ? ~0u : 0u;
   const uint32_t m01 = lane < 2 ? ~0u : 0u;
+  const uint32_t m23 = lane >= 2 ? ~0u : 0u;
   fe x, y, p;
-  q.template perm<qp(0, 0, 0, 0)>(x, v);
-  q.template perm<qp(1, 1, 2, 3)>(y, v);
+  q.template perm<QP_SWAP01>(y, v);  // Y, X, Z, T
 #pragma unroll
   for (int i = 0; i < 10; i++) {
-    // lane 0: Y - X + 2p, 1: Y + X, 2: Z, 3: T
+    // lane 0: X - Y + 2p, 1: Y + X, 2: Z, 3: T
     const uint32_t k = lane == 0 ? fe_p2(i) + 1 : 0u;
-    p.v[i] = y.v[i] + CMTV_XOR_AND(x.v[i], m0, m01) + k;
+    p.v[i] = v.v[i] + CMTV_XOR_AND(y.v[i], m0, m01) + k;
   }
   fe t;
-  fe_mul(t, p, c);  // A, B, D, C
+  fe_mul(t, p, c);  // -A, B, D, C
   q.template perm<qp(1, 2, 2, 1)>(x, t);  // B, D, D, B
-  q.template perm<qp(0, 3, 3, 0)>(y, t);  // A, C, C, A
+  q.template perm<qp(0, 3, 3, 0)>(y, t);  // -A, C, C, -A
 #pragma unroll
   for (int i = 0; i < 10; i++) {
-    // E = B - A, F = D - C (lanes 0, 1: + 2p); G = D + C, H = B + A
-    const uint32_t k = lane < 2 ? fe_p2(i) + 1 : 0u;
-    p.v[i] = x.v[i] + (y.v[i] ^ m01) + k;
+    // E = B - A, G = D + C; F = D - C, H = B + A (lanes 2, 3: + 2p)
+    const uint32_t k = lane >= 2 ? fe_p2(i) + 1 : 0u;
+    p.v[i] = x.v[i] + (y.v[i] ^ m23) + k;
   }
-  q.template perm<qp(1, 2, 1, 0)>(x, p);  // F, G, F, E
-  q.template perm<qp(0, 3, 2, 3)>(y, p);  // E, H, G, H
-  fe_mul(v, x, y);
+  q.template perm<qp(2, 3, 1, 0)>(x, p);  // F, H, G, E
+  fe_mul(v, p, x);
 }
 
 // this lane's cached-form coordinate of the extended point v

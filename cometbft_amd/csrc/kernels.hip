@@ -212,6 +212,22 @@ __device__ __forceinline__ void helper_message(const SbFuse& sb, uint32_t i, con
 // workgroup per CU, i.e. 4 waves on its 4 SIMDs, and 256 workgroups =
 // 12,288 signatures per round: the same capacity as the one-wave quad kernel
 // (3 x 45 KiB per CU), with the hash and the Euclid off every quad wave.
+// Phase probe of the helper-wave quad kernel (tools/phase_probe.py): built
+// only into a separate library with -DCMTV_PHASE_PROBE; lane 0 of every wave
+// of the first 4,096 workgroups records the shader clock at fixed points
+// (0 entry, 1/2 before/after barrier 1, 3/4 before/after barrier 2, 5 exit).
+#ifdef CMTV_PHASE_PROBE
+constexpr int kPhaseSlots = 8;
+__device__ uint64_t g_phase[4096 * 4 * kPhaseSlots];
+#define CMTV_STAMP(k)                                                                              \
+  do {                                                                                             \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 4096)                                              \
+      g_phase[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * kPhaseSlots + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define CMTV_STAMP(k) ((void)0)
+#endif
+
 template <uint32_t MODE>
 __global__ __launch_bounds__(256, CMTV_QUAD_WAVES_PER_EU) void k_verify_quad_split(
     uint32_t n, const uint32_t* __restrict__ pk, const uint32_t* __restrict__ sig, const uint8_t* __restrict__ msg,
@@ -223,6 +239,7 @@ __global__ __launch_bounds__(256, CMTV_QUAD_WAVES_PER_EU) void k_verify_quad_spl
   __shared__ uint32_t bpt[48][40];  // [u]B in the quads' cached coordinates
   __shared__ uint2 tab_lds[3][2 * 9 * 5 * 64];
   __shared__ uint32_t sbm[48][kSbFuseMaxMsg / 4];  // fused sign-bytes
+  CMTV_STAMP(0);
   if (wave == 3) {
     const uint32_t slot = t < 48 ? t : 47;
     const uint32_t s = base + slot;
@@ -233,11 +250,15 @@ __global__ __launch_bounds__(256, CMTV_QUAD_WAVES_PER_EU) void k_verify_quad_spl
     SigPrep p;
     q_prepare<MODE>(p, pk + 8 * (size_t)i, sig + 16 * (size_t)i, mp, ml, force_wide != 0);
     if (t < 48) sig_prep_store(prep[t], p);
+    CMTV_STAMP(1);
     __syncthreads();  // 1: the scalars, as the quad waves finish decoding
+    CMTV_STAMP(2);
     ge_p3 B;
     q_bcomb16(B, p.u, DevBTab{btab});
     if (t < 48) bpoint_store(bpt[t], B);
+    CMTV_STAMP(3);
     __syncthreads();  // 2: [u]B, before the quad waves' last addition
+    CMTV_STAMP(4);
     return;
   }
   const uint32_t ls = wave * 16 + (t >> 2);
@@ -251,14 +272,19 @@ __global__ __launch_bounds__(256, CMTV_QUAD_WAVES_PER_EU) void k_verify_quad_spl
   bool v = q_verify_split<MODE, true>(
       q, pk + 8 * (size_t)i, sig + 16 * (size_t)i, bt, ta, tr,
       [&](SigPrep& p) {
+        CMTV_STAMP(1);
         __syncthreads();
+        CMTV_STAMP(2);
         sig_prep_load(p, prep[ls]);
       },
       [&](fe& c) {
+        CMTV_STAMP(3);
         __syncthreads();
+        CMTV_STAMP(4);
 #pragma unroll
         for (int j = 0; j < 10; j++) c.v[j] = bq[j];
       });
+  CMTV_STAMP(5);
   v = v && active;
   if (active && (t & 3) == 0 && out_valid) out_valid[s] = v ? 1 : 0;
   uint64_t x = __ballot(v && (t & 3) == 0) & 0x1111111111111111ull;
@@ -680,3 +706,17 @@ hipError_t launch_sign(uint32_t n, const void* seeds, const void* key_idx, const
 }
 
 }  // namespace cmtv
+
+#ifdef CMTV_PHASE_PROBE
+// probe build only: copy the recorded stamps (n <= 4096 * 4 * 8 words)
+extern "C" int cmtv_debug_phase_times(uint64_t* out, size_t n) {
+  const size_t cap = sizeof(cmtv::g_phase) / sizeof(uint64_t);
+  if (n > cap) n = cap;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(cmtv::g_phase), n * sizeof(uint64_t), 0, hipMemcpyDeviceToHost) ==
+                 hipSuccess
+             ? 0
+             : -1;
+}
+#endif
+

@@ -1,0 +1,87 @@
+"""Phase timeline of the helper-wave quad kernel (k_verify_quad_split) on one
+10k commit, per workgroup, from the probe build of the library.
+
+  make -C cometbft_amd/csrc OUT=../../abtest/libprobe.so BUILD=../../build/probe KFLAGS=-DCMTV_PHASE_PROBE
+  CMTV_LIBRARY=$PWD/abtest/libprobe.so python tools/phase_probe.py [n]
+
+Lane 0 of every wave records the shader clock at kernel entry (0), before /
+after barrier 1 (1, 2: the helper's scalars), before / after barrier 2 (3, 4:
+the helper's [u]B) and, for the quad waves, at exit (5). Printed per mode:
+the spread of workgroup starts, and for the workgroup that ends last and the
+median workgroup, when the helper and the quad waves reach each barrier --
+which of them waits, and for how long.
+"""
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+SLOTS = 8
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000
+    from cometbft_amd import Context, pack_messages
+    from cometbft_amd import _native as N
+    from cometbft_amd import testutil as TU
+
+    L = N.lib()
+    fn = L.cmtv_debug_phase_times
+    fn.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t]
+    ctx = Context(device=0)
+    sv = TU.make_validator_set(ctx, n)
+    m, off = pack_messages(TU.commit_messages(n, 1000))
+    sig = ctx.sign(sv.seeds, m, off)
+    pk = np.ascontiguousarray(sv.pubkeys)
+    wgs = -(-n // 48)
+    out = {}
+    for mode, name in ((0, "go"), (1, "zip215")):
+        for _ in range(20):
+            v = ctx.verify(pk, sig, m, off, mode)
+        assert v.all()
+        buf = np.zeros(wgs * 4 * SLOTS, np.uint64)
+        assert fn(buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), buf.size) == 0
+        st = buf.reshape(wgs, 4, SLOTS).astype(np.int64)
+        t0 = st[:, :, 0].min()
+        st = st - t0
+        q, h = st[:, :3, :], st[:, 3, :]
+        end = q[:, :, 5].max(axis=1)
+        start = st[:, :, 0].min(axis=1)
+
+        def wg(b):
+            return {"start": int(start[b]), "helper_at_b1": int(h[b, 1]), "quads_at_b1": [int(x) for x in q[b, :, 1]],
+                    "b1_release": int(q[b, :, 2].max()), "helper_at_b2": int(h[b, 3]),
+                    "quads_at_b2": [int(x) for x in q[b, :, 3]], "b2_release": int(q[b, :, 4].max()),
+                    "quads_end": [int(x) for x in q[b, :, 5]]}
+
+        last = int(np.argmax(end))
+        med = int(np.argsort(end)[len(end) // 2])
+        # waits: at barrier 1 the quads wait for the helper if it arrives last
+        w1 = np.maximum(h[:, 1] - q[:, :, 1].max(axis=1), 0)
+        w2 = np.maximum(h[:, 3] - q[:, :, 3].max(axis=1), 0)
+        out[name] = {
+            "span": int(end.max()), "start_spread": int(start.max()),
+            "end_median": int(np.median(end)), "end_max": int(end.max()),
+            "quads_wait_at_b1_for_helper": {"wgs": int((w1 > 0).sum()), "median": float(np.median(w1)),
+                                            "max": int(w1.max())},
+            "quads_wait_at_b2_for_helper": {"wgs": int((w2 > 0).sum()), "median": float(np.median(w2)),
+                                            "max": int(w2.max())},
+            "helper_b1_median": float(np.median(h[:, 1] - start)),
+            "helper_b2_minus_b1_release_median": float(np.median(h[:, 3] - q[:, :, 2].max(axis=1))),
+            "quad_b1_median": float(np.median(q[:, :, 1] - start[:, None])),
+            "quad_b2_median": float(np.median(q[:, :, 3] - start[:, None])),
+            "quad_end_median": float(np.median(q[:, :, 5] - start[:, None])),
+            "last_wg": dict(wg(last), index=last), "median_wg": dict(wg(med), index=med),
+        }
+        print(name, json.dumps(out[name]), flush=True)
+    with open(os.path.join(ROOT, "gpurun_out", "phase_probe.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -571,13 +571,17 @@ hipError_t launch_comb_build(uint32_t n_keys, const void* keys_pk, uint8_t* keys
   return hipGetLastError();
 }
 
-// Registered-key quads with a helper wave: 3 quad waves (48 signatures) run
-// the 32 fixed-base comb additions, take k from the helper (barrier 1), run
-// the 32 key-comb additions and take R (barrier 2); the helper hashes
-// (q_keyed_challenge) and then decompresses R (q_keyed_decode_r), one lane
-// per signature, so the square-root chain overlaps the additions.
+// Registered-key quads with two helper waves: 3 quad waves (48 signatures)
+// run the 32 fixed-base comb additions, take k from the hash helper (wave 4,
+// q_keyed_challenge; published through an LDS flag, not a barrier), run the
+// 32 key-comb additions and take R at the one barrier; the decode helper
+// (wave 3, q_keyed_decode_r) starts R's square-root chain at the first cycle,
+// one lane per signature. With one helper hashing and then decoding, the
+// hash + decode chain (~225k cycles) set the kernel time; now the longer of
+// the decode (~140k) and the quads' 64 additions does. 5 waves on 4 SIMDs:
+// the short hash helper shares one.
 template <uint32_t MODE>
-__global__ __launch_bounds__(256, 1) void k_verify_keyed_quad_split(
+__global__ __launch_bounds__(320, 1) void k_verify_keyed_quad_split(
     uint32_t n, uint32_t n_keys, const uint32_t* __restrict__ key_idx, const uint32_t* __restrict__ sig,
     const uint8_t* __restrict__ msg, const uint32_t* __restrict__ off, const uint32_t* __restrict__ keys_pk,
     const uint8_t* __restrict__ keys_ok, const uint32_t* __restrict__ ktabs, const uint32_t* __restrict__ bcomb,
@@ -586,30 +590,41 @@ __global__ __launch_bounds__(256, 1) void k_verify_keyed_quad_split(
   const uint32_t base = blockIdx.x * 48;
   __shared__ uint32_t tks[48][9];
   __shared__ uint32_t rpt[48][31];  // R: x, y, t (10 words each), decode flag
-  if (wave == 3) {
+  __shared__ uint32_t k_ready;
+  if (threadIdx.x == 0) k_ready = 0u;
+  __syncthreads();  // the flag is clear before any wave can set or read it
+  if (wave >= 3) {
     const uint32_t s = base + (t < 48 ? t : 47);
     const uint32_t i = s < n ? s : n - 1;
-    const uint32_t m0 = off[i], m1 = off[i + 1];
-    uint32_t kid = key_idx[i];
-    kid = kid < n_keys ? kid : 0;
-    uint32_t tk[8];
-    q_keyed_challenge(tk, keys_pk + 8 * (size_t)kid, sig + 16 * (size_t)i, msg + m0, m1 - m0);
-    if (t < 48)
+    if (wave == 4) {
+      // hash helper: k for all 48 signatures, published through k_ready so
+      // the decode helper never waits on it
+      const uint32_t m0 = off[i], m1 = off[i + 1];
+      uint32_t kid = key_idx[i];
+      kid = kid < n_keys ? kid : 0;
+      uint32_t tk[8];
+      q_keyed_challenge(tk, keys_pk + 8 * (size_t)kid, sig + 16 * (size_t)i, msg + m0, m1 - m0);
+      if (t < 48)
 #pragma unroll
-      for (int j = 0; j < 8; j++) tks[t][j] = tk[j];
-    __syncthreads();  // 1: k
-    ge_p3 R;
-    const bool r_ok = q_keyed_decode_r<MODE>(R, sig + 16 * (size_t)i);
-    if (t < 48) {
+        for (int j = 0; j < 8; j++) tks[t][j] = tk[j];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (t == 0) __hip_atomic_store(&k_ready, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else {
+      // decode helper: R from the first cycle, overlapping the quads' fixed-
+      // base and key combs (the chain that bounded the one-helper form)
+      ge_p3 R;
+      const bool r_ok = q_keyed_decode_r<MODE>(R, sig + 16 * (size_t)i);
+      if (t < 48) {
 #pragma unroll
-      for (int j = 0; j < 10; j++) {
-        rpt[t][j] = R.X.v[j];
-        rpt[t][10 + j] = R.Y.v[j];
-        rpt[t][20 + j] = R.T.v[j];
+        for (int j = 0; j < 10; j++) {
+          rpt[t][j] = R.X.v[j];
+          rpt[t][10 + j] = R.Y.v[j];
+          rpt[t][20 + j] = R.T.v[j];
+        }
+        rpt[t][30] = r_ok ? 1u : 0u;
       }
-      rpt[t][30] = r_ok ? 1u : 0u;
     }
-    __syncthreads();  // 2: R
+    __syncthreads();  // R (and k)
     return;
   }
   const uint32_t ls = wave * 16 + (t >> 2);
@@ -621,10 +636,18 @@ __global__ __launch_bounds__(256, 1) void k_verify_keyed_quad_split(
   kid = kin ? kid : 0;
   DevQuad q;
   const int lane = (int)(t & 3);
+  bool k_late = false;
   bool v = q_verify_keyed_split<MODE>(
       q, kin && keys_ok[kid] != 0, sig + 16 * (size_t)i, ktabs + (size_t)kid * COMB_TABLE_WORDS, bcomb,
       [&](uint32_t tk[8]) {
-        __syncthreads();
+        // wait for the hash helper's flag; bounded, so a wave can never spin
+        // forever (a timeout rejects the signature instead)
+        uint32_t spins = 0;
+        while (__hip_atomic_load(&k_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u &&
+               ++spins < (1u << 22))
+          __builtin_amdgcn_s_sleep(2);
+        k_late = spins >= (1u << 22);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 #pragma unroll
         for (int j = 0; j < 8; j++) tk[j] = tks[ls][j];
       },
@@ -636,7 +659,7 @@ __global__ __launch_bounds__(256, 1) void k_verify_keyed_quad_split(
         for (int j = 0; j < 10; j++) rc.v[j] = lane == 2 ? (j == 0 ? 1u : 0u) : p[j];
         r_ok = rpt[ls][30] != 0;
       });
-  v = v && active;
+  v = v && active && !k_late;
   if (active && (t & 3) == 0 && out_valid) out_valid[s] = v ? 1 : 0;
   uint64_t x = __ballot(v && (t & 3) == 0) & 0x1111111111111111ull;
   x = (x | (x >> 3)) & 0x0303030303030303ull;
@@ -660,7 +683,7 @@ hipError_t launch_verify_keyed(uint32_t mode, uint32_t n, uint32_t n_keys, const
   auto bp = static_cast<uint64_t*>(bitmap);
   if (quad && split) {
     const uint32_t slices = 4 * ((n + 63) / 64);
-    const dim3 grid((slices + 2) / 3), block(256);
+    const dim3 grid((slices + 2) / 3), block(320);
     if (mode == MODE_ZIP215)
       hipLaunchKernelGGL(k_verify_keyed_quad_split<MODE_ZIP215>, grid, block, 0, s, n, n_keys, ki, sgp, mp, op,
                          keys_pk, keys_ok, ktabs, bcomb, vp, bp);

@@ -48,8 +48,11 @@ constexpr size_t kOctSplitMaxDefault = 3072;  // CMTV_OCT_SPLIT_MAX
 // quad batches up to this size take the helper-wave form (k_verify_quad_split:
 // 256 workgroups x 48 signatures per round); CMTV_QUAD_SPLIT_MAX
 constexpr size_t kQuadSplitMaxDefault = 40000;
-// the same crossover for registered-key verification (env CMTV_KEYED_QUAD_MAX)
-constexpr size_t kKeyedQuadMaxDefault = 16384;
+// the crossover for registered-key verification (env CMTV_KEYED_QUAD_MAX):
+// the two-helper keyed quad kernel takes 12,288 signatures per round (0.088,
+// 0.164, 0.242 ms for 1-3 rounds) against the keyed lane kernel's flat
+// 0.28-0.30 ms up to 49k (tools/keyed_sweep.py, profiles/r02_keyed_sweep.json)
+constexpr size_t kKeyedQuadMaxDefault = 36864;
 // signatures per device below which a batch is not sharded (env CMTV_SHARD_MIN)
 constexpr size_t kShardMinDefault = 8192;
 // single-device host batches up to this size return their bitmap through

@@ -42,7 +42,7 @@ def _valset_commits(n_keys, n_sigs, seed):
 
 
 @pytest.mark.parametrize("kernel", ["quad2", "quad", "lane"])
-@pytest.mark.parametrize("n", [1, 15, 16, 17, 63, 64, 65, 3000])
+@pytest.mark.parametrize("n", [1, 15, 16, 17, 63, 64, 65, 3000, 12289])
 def test_keyed_matches_generic_and_oracle(gpu_ctx, gpu_ctx_quad1, gpu_ctx_lane, n, kernel):
     gpu_ctx = {"quad2": gpu_ctx, "quad": gpu_ctx_quad1, "lane": gpu_ctx_lane}[kernel]
     pk, kidx, sig, m, off, rng = _valset_commits(150, n, 7 + n)

@@ -400,14 +400,31 @@ CMTV_HD int q_wave_windows(const Q& q, uint32_t flags) {
   return wide ? HS_WIDE_WINDOWS : W;
 }
 
+// Phase 3 ahead of the scalars: (0..8)(-A) and (0..8)(-R) need only the
+// decoded points, so a split verifier whose helper is the longer side of
+// barrier 1 (sr25519: the merlin transcript) builds them before waiting; a negative k2 then flips R's digits at lookup
+// (q_straus_prep_b<EXT_B, true>) instead of negating R. v, rc are clobbered.
+template <class Q, class ATab>
+CMTV_HD void q_tables_early(const Q& q, fe& v, fe& rc, ATab& tabA, ATab& tabR) {
+  const int lane = q.lane();
+  fe t;
+  fe_neg(t, rc);
+  fe_carry(t);
+  fe_select(rc, rc, t, lane == 0 || lane == 3);
+  q_build_table(q, tabA, v);
+  q_build_table(q, tabR, rc);
+}
+
 // Phases 3-4 from a prepared pair (see q_straus_half below). EXT_B: the
 // fixed-base part [u]B comes ready-made from get_b (this lane's cached
 // coordinate, a helper wave's q_bcomb16) and is added once after the windows.
-template <bool EXT_B, class Q, class BTab, class ATab, class Probe, class GetB>
+// PREBUILT: the tables came from q_tables_early (R's table is of -R).
+template <bool EXT_B, bool PREBUILT = false, class Q, class BTab, class ATab, class Probe, class GetB>
 CMTV_HD void q_straus_prep_b(const Q& q, fe& v, fe& rc, const SigPrep& hs, const BTab& btab, ATab& tabA, ATab& tabR,
                              const Probe& probe, const GetB& get_b) {
   const int lane = q.lane();
   const bool k2_neg = (hs.flags & 1u) != 0;
+  const bool r_flip = PREBUILT && k2_neg;
   const uint32_t* u = hs.u;
   const int W = q_wave_windows(q, hs.flags);
   {
@@ -420,14 +437,14 @@ CMTV_HD void q_straus_prep_b(const Q& q, fe& v, fe& rc, const SigPrep& hs, const
   }
 
   // ---- phase 3: (0..8)(-A) and (0..8)(-/+R), this lane's cached coordinate
-  {
+  if constexpr (!PREBUILT) {
     fe t;
     fe_neg(t, rc);
     fe_carry(t);
     fe_select(rc, rc, t, !k2_neg && (lane == 0 || lane == 3));
+    q_build_table(q, tabA, v);
+    q_build_table(q, tabR, rc);
   }
-  q_build_table(q, tabA, v);
-  q_build_table(q, tabR, rc);
 
   // ---- phase 4: Straus over W shared 4-bit windows; the fixed-base scalar
   //      u in signed radix-2^16 digits: digit j on window 4j against
@@ -446,7 +463,7 @@ CMTV_HD void q_straus_prep_b(const Q& q, fe& v, fe& rc, const SigPrep& hs, const
       const int dA = (int)sc_shift_out(tA, 4) - 8;
       tabA.load_signed(q, dA < 0 ? -dA : dA, dA < 0, cA);
       const int dR = (int)sc_shift_out(tR, 4) - 8;
-      tabR.load_signed(q, dR < 0 ? -dR : dR, dR < 0, cR);
+      tabR.load_signed(q, dR < 0 ? -dR : dR, (dR < 0) != r_flip, cR);
     }
     const bool has_b = !EXT_B && (win & 1) == 0 && win <= 30;
     bool b_neg = false, b_ident = false;
@@ -548,6 +565,9 @@ CMTV_HD bool q_verify_split(const Q& q, const uint32_t* pk_ptr, const uint32_t* 
   }
   probe.snap(0, v);
   probe.snap(1, rc);
+  // the tables stay after get_prep here: barrier 1 is balanced (the quads'
+  // decode and the helper's hash + pair both take ~150k cycles), and building
+  // them first measured 1.7% slower in ZIP-215 mode (sr25519 gains: 7%)
   SigPrep p;
   get_prep(p);
   const bool s_ok = (p.flags & 4u) != 0;

@@ -82,11 +82,15 @@ CMTV_HD bool q_verify_sr_split(const Q& q, const uint32_t* pk_ptr, const uint32_
   }
   probe.snap(0, v);
   probe.snap(1, rc);
+  // split kernel (EXT_B): the tables are built while the helper runs the
+  // transcript; the one-wave kernel's STROBE states live in the table LDS
+  // until its own transcript is done, so it builds them after get_prep
+  if constexpr (EXT_B) q_tables_early(q, v, rc, tabA, tabR);
   SigPrep p;
   get_prep(p);
   const bool s_ok = (p.flags & 4u) != 0;
 
-  q_straus_prep_b<EXT_B>(q, v, rc, p, btab, tabA, tabR, probe, get_b);
+  q_straus_prep_b<EXT_B, EXT_B>(q, v, rc, p, btab, tabA, tabR, probe, get_b);
 
   // ---- X in E[4]: X.X = 0 (lane 0) or X.Y = 0 (lane 1)
   const bool z = fe_iszero(v);

@@ -10,7 +10,7 @@ rather than only timed):
   configs[2]  the replay shape at >= 1M signatures: 7,000 commits x 150
               validators through cmtv_register_keys +
               cmtv_verify_ed25519_indexed (the registered-key LANE kernel,
-              the default dispatch above 16,384), 1% bit-flipped: exactly the
+              the default dispatch above 36,864), 1% bit-flipped: exactly the
               flipped ones must be rejected, the packed bitmap must agree, and
               a 2,000-signature sample must match the C oracle in both modes.
 

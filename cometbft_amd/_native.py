@@ -41,7 +41,7 @@ COMMIT_PANIC_UNKNOWN_FLAG = 9
 # every symbol include/cmtverify.h declares (checked by tests/test_abi.py)
 EXPORTS = (
     "cmtv_open", "cmtv_open_devices", "cmtv_device_count", "cmtv_device_ordinal", "cmtv_device_stream", "cmtv_sync",
-    "cmtv_verify_ed25519_sharded_device", "cmtv_verify_ed25519_indexed_sharded_device", "cmtv_verify_ed25519_multi_device", "cmtv_close", "cmtv_strerror", "cmtv_abi_version", "cmtv_stats_get", "cmtv_stream",
+    "cmtv_verify_ed25519_sharded_device", "cmtv_verify_ed25519_indexed_sharded_device", "cmtv_verify_ed25519_multi_device", "cmtv_close", "cmtv_strerror", "cmtv_abi_version", "cmtv_stats_get", "cmtv_device_stats_get", "cmtv_stream",
     "cmtv_verify_ed25519", "cmtv_verify_ed25519_device", "cmtv_verify_sr25519", "cmtv_verify_sr25519_device",
     "cmtv_register_keys", "cmtv_keyset_free", "cmtv_keyset_len", "cmtv_verify_ed25519_indexed",
     "cmtv_verify_ed25519_indexed_device",
@@ -69,7 +69,15 @@ class cmtv_stats(ctypes.Structure):
                 ("cache_entries", ctypes.c_uint64), ("keyed_launches", ctypes.c_uint64),
                 ("sharded_calls", ctypes.c_uint64), ("gathers", ctypes.c_uint64),
                 ("faults_injected", ctypes.c_uint64), ("n_devices", ctypes.c_uint32), ("rccl", ctypes.c_uint32),
-                ("fused_sign_bytes", ctypes.c_uint64)]
+                ("fused_sign_bytes", ctypes.c_uint64), ("device_failures", ctypes.c_uint64),
+                ("reshards", ctypes.c_uint64), ("late_k_waves", ctypes.c_uint64),
+                ("live_devices", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+
+class cmtv_device_stats(ctypes.Structure):
+    _fields_ = [("ordinal", ctypes.c_int32), ("failed", ctypes.c_uint32), ("calls", ctypes.c_uint64),
+                ("signatures", ctypes.c_uint64), ("kernel_launches", ctypes.c_uint64),
+                ("device_ms", ctypes.c_double)]
 
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -139,6 +147,8 @@ def lib() -> ctypes.CDLL:
     L.cmtv_abi_version.restype = ctypes.c_int
     L.cmtv_stats_get.argtypes = [vp, ctypes.POINTER(cmtv_stats)]
     L.cmtv_stats_get.restype = ctypes.c_int
+    L.cmtv_device_stats_get.argtypes = [vp, ctypes.c_int, ctypes.POINTER(cmtv_device_stats)]
+    L.cmtv_device_stats_get.restype = ctypes.c_int
     L.cmtv_stream.argtypes = [vp]
     L.cmtv_stream.restype = vp
     L.cmtv_verify_ed25519.argtypes = [vp, sz, _u8p, _u8p, _u8p, u32p, u32, _u8p, ctypes.POINTER(u64)]

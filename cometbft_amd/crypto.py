@@ -122,7 +122,18 @@ class Context:
     def stats(self) -> dict:
         st = N.cmtv_stats()
         N.check(N.lib().cmtv_stats_get(self._h, ctypes.byref(st)), "cmtv_stats_get")
-        return {k: getattr(st, k) for k, _ in st._fields_}
+        return {k: getattr(st, k) for k, _ in st._fields_ if k != "reserved"}
+
+    def device_stats(self) -> list:
+        """cmtv_device_stats_get for every device of the context: ordinal,
+        failed (retired after a HIP error), calls, signatures, launches and
+        summed kernel milliseconds on that device."""
+        out = []
+        for g in range(self.n_devices()):
+            st = N.cmtv_device_stats()
+            N.check(N.lib().cmtv_device_stats_get(self._h, g, ctypes.byref(st)), "cmtv_device_stats_get")
+            out.append({k: getattr(st, k) for k, _ in st._fields_})
+        return out
 
     def keyset_cache(self, max_sets: int) -> None:
         """cmtv_keyset_cache: registered key sets of up to max_sets validator

@@ -503,6 +503,10 @@ int job_replay(CommitJob& J, const std::vector<uint8_t>& all_valid) {
                            hex_upper(vals->pubkeys + vals->pk_off[vi], vals->pk_off[vi + 1] - vals->pk_off[vi]) +
                            "} VP:" + std::to_string(vals->voting_power[vi]) + " A:" +
                            std::to_string(vals->proposer_priority ? vals->proposer_priority[vi] : 0) + "}";
+          // the Go side formats the error with its own Validator: got = the
+          // first commit index, needed = the validator's index in vals
+          J.res->got = sit->second;
+          J.res->needed = vi;
           return J.fail(CMTV_COMMIT_ERR_DOUBLE_VOTE, (int32_t)idx,
                         "double vote from " + vs + " (" + std::to_string(sit->second) + " and " +
                             std::to_string(idx) + ")");

@@ -35,6 +35,13 @@ struct SbFuse {
 };
 constexpr uint32_t kSbFuseMaxMsg = 192;
 
+// Per-device diagnostic counters the kernels bump with vector atomics
+// (CmtvDev::d_diag, read by cmtv_stats_get): kDiagLateK = quad waves of
+// k_verify_keyed_quad_split that stopped waiting for the hash helper and
+// hashed their own signatures. kKeyedWaitDefault = the polls before that.
+constexpr uint32_t kDiagLateK = 0, kDiagWords = 4;
+constexpr uint32_t kKeyedWaitDefault = 1u << 22;
+
 hipError_t launch_btab_init(uint32_t* d_rows, hipStream_t s);
 // sb (may be null) is honoured only by the split kernels (kLaunchOctSplit,
 // kLaunchQuadSplit); the caller launches k_sign_bytes otherwise
@@ -46,7 +53,7 @@ hipError_t launch_comb_build(uint32_t n_keys, const void* keys_pk, uint8_t* keys
 hipError_t launch_verify_keyed(uint32_t mode, uint32_t n, uint32_t n_keys, const void* key_idx, const void* sig,
                                const void* msg, const void* off, const uint32_t* keys_pk, const uint8_t* keys_ok,
                                const uint32_t* ktabs, const uint32_t* bcomb, void* valid, void* bitmap,
-                               bool quad, bool split, hipStream_t s);
+                               bool quad, bool split, uint32_t k_wait, uint32_t* diag, hipStream_t s);
 hipError_t launch_verify_sr25519(uint32_t n, const void* pk, const void* sig, const void* msg, const void* off,
                                  const uint32_t* btab, uint32_t* atab, const uint16_t* prog, int nops, void* valid,
                                  void* bitmap, uint32_t kflags, hipStream_t s);

@@ -580,12 +580,19 @@ hipError_t launch_comb_build(uint32_t n_keys, const void* keys_pk, uint8_t* keys
 // hash + decode chain (~225k cycles) set the kernel time; now the longer of
 // the decode (~140k) and the quads' 64 additions does. 5 waves on 4 SIMDs:
 // the short hash helper shares one.
+//
+// The quads wait for the hash helper's flag for at most k_wait polls. The
+// verdict never depends on that wait: a quad wave that stops waiting hashes
+// its own signatures (q_keyed_challenge, the same k the helper computes) and
+// counts itself in diag[kDiagLateK] (cmtv_stats.late_k_waves). k_wait = 0
+// (the CMTV_FORCE_K_LATE test knob) skips the flag entirely, so every quad
+// wave takes that path.
 template <uint32_t MODE>
 __global__ __launch_bounds__(320, 1) void k_verify_keyed_quad_split(
     uint32_t n, uint32_t n_keys, const uint32_t* __restrict__ key_idx, const uint32_t* __restrict__ sig,
     const uint8_t* __restrict__ msg, const uint32_t* __restrict__ off, const uint32_t* __restrict__ keys_pk,
     const uint8_t* __restrict__ keys_ok, const uint32_t* __restrict__ ktabs, const uint32_t* __restrict__ bcomb,
-    uint8_t* __restrict__ out_valid, uint64_t* __restrict__ out_bitmap) {
+    uint8_t* __restrict__ out_valid, uint64_t* __restrict__ out_bitmap, uint32_t k_wait, uint32_t* __restrict__ diag) {
   const uint32_t wave = threadIdx.x >> 6, t = threadIdx.x & 63;
   const uint32_t base = blockIdx.x * 48;
   __shared__ uint32_t tks[48][9];
@@ -636,20 +643,28 @@ __global__ __launch_bounds__(320, 1) void k_verify_keyed_quad_split(
   kid = kin ? kid : 0;
   DevQuad q;
   const int lane = (int)(t & 3);
-  bool k_late = false;
   bool v = q_verify_keyed_split<MODE>(
       q, kin && keys_ok[kid] != 0, sig + 16 * (size_t)i, ktabs + (size_t)kid * COMB_TABLE_WORDS, bcomb,
       [&](uint32_t tk[8]) {
-        // wait for the hash helper's flag; bounded, so a wave can never spin
-        // forever (a timeout rejects the signature instead)
-        uint32_t spins = 0;
-        while (__hip_atomic_load(&k_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u &&
-               ++spins < (1u << 22))
+        // the hash helper's flag, polled at most k_wait times (a wave never
+        // spins forever)
+        bool ready = false;
+        for (uint32_t spins = 0; spins < k_wait; spins++) {
+          ready = __hip_atomic_load(&k_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0u;
+          if (ready) break;
           __builtin_amdgcn_s_sleep(2);
-        k_late = spins >= (1u << 22);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        }
+        if (__builtin_expect(__ballot(ready) != __ballot(1), 0)) {
+          // the helper's k did not arrive in time: hash this signature here
+          // (identical k), so the wait bounds only the time, never the verdict
+          const uint32_t m0 = off[i], m1 = off[i + 1];
+          q_keyed_challenge(tk, keys_pk + 8 * (size_t)kid, sig + 16 * (size_t)i, msg + m0, m1 - m0);
+          if (t == 0) atomicAdd(diag + kDiagLateK, 1u);
+        } else {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 #pragma unroll
-        for (int j = 0; j < 8; j++) tk[j] = tks[ls][j];
+          for (int j = 0; j < 8; j++) tk[j] = tks[ls][j];
+        }
       },
       [&](fe& rc, bool& r_ok) {
         __syncthreads();
@@ -659,7 +674,7 @@ __global__ __launch_bounds__(320, 1) void k_verify_keyed_quad_split(
         for (int j = 0; j < 10; j++) rc.v[j] = lane == 2 ? (j == 0 ? 1u : 0u) : p[j];
         r_ok = rpt[ls][30] != 0;
       });
-  v = v && active && !k_late;
+  v = v && active;
   if (active && (t & 3) == 0 && out_valid) out_valid[s] = v ? 1 : 0;
   uint64_t x = __ballot(v && (t & 3) == 0) & 0x1111111111111111ull;
   x = (x | (x >> 3)) & 0x0303030303030303ull;
@@ -673,7 +688,7 @@ __global__ __launch_bounds__(320, 1) void k_verify_keyed_quad_split(
 hipError_t launch_verify_keyed(uint32_t mode, uint32_t n, uint32_t n_keys, const void* key_idx, const void* sig,
                                const void* msg, const void* off, const uint32_t* keys_pk, const uint8_t* keys_ok,
                                const uint32_t* ktabs, const uint32_t* bcomb, void* valid, void* bitmap,
-                               bool quad, bool split, hipStream_t s) {
+                               bool quad, bool split, uint32_t k_wait, uint32_t* diag, hipStream_t s) {
   if (n == 0) return hipSuccess;
   auto ki = static_cast<const uint32_t*>(key_idx);
   auto sgp = static_cast<const uint32_t*>(sig);
@@ -686,10 +701,10 @@ hipError_t launch_verify_keyed(uint32_t mode, uint32_t n, uint32_t n_keys, const
     const dim3 grid((slices + 2) / 3), block(320);
     if (mode == MODE_ZIP215)
       hipLaunchKernelGGL(k_verify_keyed_quad_split<MODE_ZIP215>, grid, block, 0, s, n, n_keys, ki, sgp, mp, op,
-                         keys_pk, keys_ok, ktabs, bcomb, vp, bp);
+                         keys_pk, keys_ok, ktabs, bcomb, vp, bp, k_wait, diag);
     else
       hipLaunchKernelGGL(k_verify_keyed_quad_split<MODE_GO_STDLIB>, grid, block, 0, s, n, n_keys, ki, sgp, mp, op,
-                         keys_pk, keys_ok, ktabs, bcomb, vp, bp);
+                         keys_pk, keys_ok, ktabs, bcomb, vp, bp, k_wait, diag);
     return hipGetLastError();
   }
   if (quad) {

@@ -278,8 +278,9 @@ struct Timing {
     return hipSuccess;
   }
   void abandon(const Pair& p) { free_.push_back(p); }
-  // completed pairs -> stats; blocking waits for all of them
-  void harvest(cmtv_stats& st, bool blocking) {
+  // completed pairs -> stats (context-wide and this device's); blocking
+  // waits for all of them
+  void harvest(cmtv_stats& st, double& dev_ms, bool blocking) {
     while (!pending.empty()) {
       Pair p = pending.front();
       if (blocking || pending.size() > 64) {
@@ -291,6 +292,7 @@ struct Timing {
       if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
         st.last_kernel_ms = ms;
         st.device_ms += ms;
+        dev_ms += ms;
       }
       pending.pop_front();
       free_.push_back(p);
@@ -333,6 +335,16 @@ struct CmtvDev {
   hipEvent_t done = nullptr;  // cross-device ordering for peer-copy gathers
   Timing timing;
   ncclComm_t comm = nullptr;
+  // kernel diagnostic counters (kernels.h kDiagWords, vector atomics)
+  uint32_t* d_diag = nullptr;
+  // a device that returned a HIP error is taken out of the context's
+  // rotation: host batches are re-planned over the others (runtime.cpp
+  // run_host_batch); CMTV_FAULT_DEV=g makes device g's first launch fail
+  bool failed = false;
+  bool inject_fault = false;
+  // this device's share of cmtv_stats (cmtv_device_stats_get)
+  uint64_t calls = 0, signatures = 0, launches = 0;
+  double device_ms = 0;
 };
 
 struct cmtv_ctx {
@@ -356,10 +368,19 @@ struct cmtv_ctx {
   std::vector<std::pair<std::string, cmtv_keyset*>> keysets;
   // CMTV_FAULT_AT: 1-based index of the verification launch that fails
   uint64_t fault_at = 0, launch_seq = 0;
+  bool fault_pending = false;  // the last failure was CMTV_FAULT_AT's
+  // RCCL options read at open (CMTV_FORCE_RCCL, CMTV_NO_RCCL)
+  bool force_rccl = false, no_rccl = false;
   // CMTV_FORCE_WIDE: quad kernels take the 64-window half-scalar fallback
   bool force_wide = false;
   // templated sign-bytes in the split kernels' helper waves (CMTV_NO_SB_FUSE=1: off)
   bool sb_fuse = true;
+  // polls of the keyed split kernel's quads for the hash helper's k before
+  // they hash themselves (CMTV_FORCE_K_LATE=1: 0, every quad wave hashes)
+  uint32_t keyed_wait = cmtv::kKeyedWaitDefault;
+  // devices (indices into devs) that take host batches, in shard order; the
+  // RCCL communicator (when rccl) spans exactly these, rank = position
+  std::vector<size_t> live;
   // fused small host batches read their inputs from mapped host memory (CMTV_NO_ZC_IN=1: off)
   bool zc_in = true;
 };
@@ -387,8 +408,9 @@ static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 static void harvest(cmtv_ctx* ctx, bool blocking) {
   for (auto& d : ctx->devs) {
+    if (d.failed) continue;
     (void)hipSetDevice(d.ordinal);
-    d.timing.harvest(ctx->stats, blocking);
+    d.timing.harvest(ctx->stats, d.device_ms, blocking);
   }
 }
 
@@ -397,6 +419,7 @@ static bool fault_hit(cmtv_ctx* ctx) {
   ctx->launch_seq++;
   if (ctx->fault_at && ctx->launch_seq == ctx->fault_at) {
     ctx->stats.faults_injected++;
+    ctx->fault_pending = true;
     return true;
   }
   return false;
@@ -413,13 +436,19 @@ static bool split_kernel_for(const cmtv_ctx* ctx, size_t n) {
   return oct ? n <= ctx->oct_split_max : (quad && n <= ctx->quad_split_max);
 }
 
+// ... and can write the sign-bytes of all n in its helper waves: a split
+// kernel running in one launch (enqueue_verify rejects a fused batch of more
+// than kChunk, whatever CMTV_QUAD_MAX / CMTV_QUAD_SPLIT_MAX say). The one
+// predicate both enqueue_shard and enqueue_verify use.
+static bool fuse_ok(const cmtv_ctx* ctx, size_t n) { return split_kernel_for(ctx, n) && n <= kChunk; }
+
 static int enqueue_verify(cmtv_ctx* ctx, CmtvDev& D, size_t n, const uint8_t* d_pk, const uint8_t* d_sig,
                           const uint8_t* d_msg, const uint32_t* d_off, uint32_t mode, uint8_t* d_valid,
                           uint64_t* d_bitmap, hipStream_t s, const SbFuse* sb = nullptr) {
   if (n == 0) return CMTV_OK;
-  if (fault_hit(ctx)) return CMTV_EHIP;
+  if (fault_hit(ctx) || D.inject_fault) return CMTV_EHIP;
   // fused sign-bytes only where the split kernels run, in one launch
-  if (sb && (mode == kModeSr25519 || !split_kernel_for(ctx, n) || n > kChunk)) return CMTV_EINVAL;
+  if (sb && (mode == kModeSr25519 || !fuse_ok(ctx, n))) return CMTV_EINVAL;
   // Small batches cannot fill the chip at one signature per lane: use the
   // 4-lanes-per-signature kernel below the crossover (quad.h,
   // sr25519_quad.h).
@@ -443,7 +472,7 @@ static int enqueue_verify(cmtv_ctx* ctx, CmtvDev& D, size_t n, const uint8_t* d_
     }
     if (D.atab_used && (e = hipStreamWaitEvent(s, D.atab_done, 0)) != hipSuccess) return hip_fail(e);
   }
-  D.timing.harvest(ctx->stats, false);
+  D.timing.harvest(ctx->stats, D.device_ms, false);
   Timing::Pair tp;
   if ((e = D.timing.begin(tp, s)) != hipSuccess) return hip_fail(e);
   const size_t chunk = quad ? kChunk : ctx->lane_chunk;
@@ -462,6 +491,7 @@ static int enqueue_verify(cmtv_ctx* ctx, CmtvDev& D, size_t n, const uint8_t* d_
       return hip_fail(e);
     }
     ctx->stats.kernel_launches++;
+    D.launches++;
   }
   if (!quad) {
     if ((e = hipEventRecord(D.atab_done, s)) != hipSuccess) return hip_fail(e);
@@ -470,6 +500,8 @@ static int enqueue_verify(cmtv_ctx* ctx, CmtvDev& D, size_t n, const uint8_t* d_
   if ((e = D.timing.end(tp, s)) != hipSuccess) return hip_fail(e);
   ctx->stats.calls++;
   ctx->stats.signatures += n;
+  D.calls++;
+  D.signatures += n;
   return CMTV_OK;
 }
 
@@ -506,8 +538,8 @@ static int enqueue_verify_keyed(cmtv_ctx* ctx, CmtvDev& D, const cmtv_keyset::Pe
                                 const uint32_t* d_off, uint32_t mode, uint8_t* d_valid, uint64_t* d_bitmap,
                                 hipStream_t s) {
   if (n == 0) return CMTV_OK;
-  if (fault_hit(ctx)) return CMTV_EHIP;
-  D.timing.harvest(ctx->stats, false);
+  if (fault_hit(ctx) || D.inject_fault) return CMTV_EHIP;
+  D.timing.harvest(ctx->stats, D.device_ms, false);
   Timing::Pair tp;
   hipError_t e;
   if ((e = D.timing.begin(tp, s)) != hipSuccess) return hip_fail(e);
@@ -516,28 +548,32 @@ static int enqueue_verify_keyed(cmtv_ctx* ctx, CmtvDev& D, const cmtv_keyset::Pe
     e = launch_verify_keyed(mode, cn, (uint32_t)n_keys, d_idx + c, d_sig + 64 * c, d_msg, d_off + c, K.d_pk, K.d_ok,
                             K.d_tab, D.d_bcomb, d_valid ? d_valid + c : nullptr,
                             d_bitmap ? d_bitmap + c / 64 : nullptr, n <= ctx->keyed_quad_max,
-                            n <= ctx->quad_split_max, s);
+                            n <= ctx->quad_split_max, ctx->keyed_wait, D.d_diag, s);
     if (e != hipSuccess) {
       D.timing.abandon(tp);
       return hip_fail(e);
     }
     ctx->stats.kernel_launches++;
     ctx->stats.keyed_launches++;
+    D.launches++;
   }
   if ((e = D.timing.end(tp, s)) != hipSuccess) return hip_fail(e);
   ctx->stats.calls++;
   ctx->stats.signatures += n;
+  D.calls++;
+  D.signatures += n;
   return CMTV_OK;
 }
 
 // ---------------------------------------------------------------- sharding
 
-// Bitmap all-gather: device g's shard occupies words [g W, (g+1) W) of
-// bufs[g] (G x W words each); afterwards every bufs[g] holds all shards.
-// RCCL all-gather in place when the context has a communicator, else peer
-// copies (a context over a repeated device ordinal). Enqueued on the device
-// streams.
-static int gather_bitmaps(cmtv_ctx* ctx, size_t G, size_t W, uint64_t* const* bufs) {
+// Bitmap all-gather over the devices dev[0..G): the one at position g holds
+// its shard in words [g W, (g+1) W) of bufs[g] (G x W words each); afterwards
+// every bufs[g] holds all shards. RCCL all-gather in place when the context
+// has a communicator (then dev must be ctx->live, the communicator's ranks in
+// order), else peer copies (a context over a repeated device ordinal).
+// Enqueued on the device streams.
+static int gather_bitmaps(cmtv_ctx* ctx, const size_t* dev, size_t G, size_t W, uint64_t* const* bufs) {
   // one device: nothing to exchange, unless CMTV_FORCE_RCCL gave it a
   // one-rank communicator (the RCCL path exercised on a one-GPU box)
   if (G <= 1 && !ctx->rccl) return CMTV_OK;
@@ -547,7 +583,7 @@ static int gather_bitmaps(cmtv_ctx* ctx, size_t G, size_t W, uint64_t* const* bu
     if (R.GroupStart() != 0) return CMTV_ERCCL;
     int bad = 0;
     for (size_t g = 0; g < G; g++) {
-      CmtvDev& D = ctx->devs[g];
+      CmtvDev& D = ctx->devs[dev[g]];
       (void)hipSetDevice(D.ordinal);
       bad |= R.AllGather(bufs[g] + g * W, bufs[g], W, kNcclUint64, D.comm, D.stream) != 0;
     }
@@ -556,15 +592,16 @@ static int gather_bitmaps(cmtv_ctx* ctx, size_t G, size_t W, uint64_t* const* bu
   }
   hipError_t e;
   for (size_t h = 0; h < G; h++) {
-    (void)hipSetDevice(ctx->devs[h].ordinal);
-    if ((e = hipEventRecord(ctx->devs[h].done, ctx->devs[h].stream)) != hipSuccess) return hip_fail(e);
+    CmtvDev& H = ctx->devs[dev[h]];
+    (void)hipSetDevice(H.ordinal);
+    if ((e = hipEventRecord(H.done, H.stream)) != hipSuccess) return hip_fail(e);
   }
   for (size_t g = 0; g < G; g++) {
-    CmtvDev& D = ctx->devs[g];
+    CmtvDev& D = ctx->devs[dev[g]];
     (void)hipSetDevice(D.ordinal);
     for (size_t h = 0; h < G; h++) {
       if (h == g) continue;
-      CmtvDev& H = ctx->devs[h];
+      CmtvDev& H = ctx->devs[dev[h]];
       if ((e = hipStreamWaitEvent(D.stream, H.done, 0)) != hipSuccess) return hip_fail(e);
       if ((e = hipMemcpyPeerAsync(bufs[g] + h * W, D.ordinal, bufs[h] + h * W, H.ordinal, W * 8, D.stream)) !=
           hipSuccess)
@@ -574,8 +611,9 @@ static int gather_bitmaps(cmtv_ctx* ctx, size_t G, size_t W, uint64_t* const* bu
   // the copies read other devices' buffers: finish them before those
   // devices' next kernels may write
   for (size_t g = 0; g < G; g++) {
-    (void)hipSetDevice(ctx->devs[g].ordinal);
-    if ((e = hipStreamSynchronize(ctx->devs[g].stream)) != hipSuccess) return hip_fail(e);
+    CmtvDev& D = ctx->devs[dev[g]];
+    (void)hipSetDevice(D.ordinal);
+    if ((e = hipStreamSynchronize(D.stream)) != hipSuccess) return hip_fail(e);
   }
   return CMTV_OK;
 }
@@ -641,7 +679,7 @@ static int enqueue_shard(cmtv_ctx* ctx, size_t g, const HostBatch& B, size_t a, 
   // templated sign-bytes written by the verify kernel's helper wave (no
   // k_sign_bytes launch) when the batch runs a split kernel and every
   // message fits the helper's LDS slot; CMTV_NO_SB_FUSE turns it off
-  const bool fuse = tpl && !keyed && ctx->sb_fuse && max_len <= kSbFuseMaxMsg && split_kernel_for(ctx, m);
+  const bool fuse = tpl && !keyed && ctx->sb_fuse && max_len <= kSbFuseMaxMsg && fuse_ok(ctx, m);
   // a fused small batch reads its staging in mapped host memory directly
   // (CMTV_NO_ZC_IN turns it off)
   const bool zc = zero_copy && fuse && ctx->zc_in;
@@ -703,26 +741,32 @@ static int enqueue_shard(cmtv_ctx* ctx, size_t g, const HostBatch& B, size_t a, 
                         B.mode, dv, bitmap, D.stream, fuse ? &sb : nullptr);
 }
 
-// Verdicts of a host batch, sharded over the context's devices. Caller holds
-// the lock.
-static int run_host_batch_(cmtv_ctx* ctx, const HostBatch& B, uint8_t* out_valid, uint64_t* out_bitmap) {
+// Verdicts of a host batch, sharded over the context's live devices. Caller
+// holds the lock. On a device's HIP error *bad_dev names it.
+static int run_host_batch_(cmtv_ctx* ctx, const HostBatch& B, uint8_t* out_valid, uint64_t* out_bitmap,
+                           long* bad_dev) {
   const size_t n = B.n;
   if (n == 0) return CMTV_OK;
-  const ShardPlan P = plan_shards(n, ctx->devs.size(), ctx->shard_min);
+  const std::vector<size_t>& live = ctx->live;
+  if (live.empty()) return CMTV_ENODEV;
+  const ShardPlan P = plan_shards(n, live.size(), ctx->shard_min);
   const size_t words = (n + 63) / 64;
   hipError_t e;
+  const size_t d0 = live[0];
   if (P.G == 1 && n <= kZeroCopyMax) {
     // one device, a small batch: the verify kernel writes the bitmap into
     // mapped host memory, so the call is H2D + (sign-bytes) + verify + sync
-    CmtvDev& D = ctx->devs[0];
+    CmtvDev& D = ctx->devs[d0];
+    *bad_dev = (long)d0;
     (void)hipSetDevice(D.ordinal);
     if ((e = D.h_zc.ensure(8 * words)) != hipSuccess) return hip_fail(e);
     void* dzc = nullptr;
     if ((e = hipHostGetDevicePointer(&dzc, D.h_zc.p, 0)) != hipSuccess) return hip_fail(e);
     size_t o_valid = 0;
-    const int rc = enqueue_shard(ctx, 0, B, 0, n, false, static_cast<uint64_t*>(dzc), o_valid, true);
+    const int rc = enqueue_shard(ctx, d0, B, 0, n, false, static_cast<uint64_t*>(dzc), o_valid, true);
     if (rc != CMTV_OK) return rc;
     if ((e = hipStreamSynchronize(D.stream)) != hipSuccess) return hip_fail(e);
+    *bad_dev = -1;
     harvest(ctx, false);
     (void)hipSetDevice(D.ordinal);
     uint64_t* bm = static_cast<uint64_t*>(D.h_zc.p);
@@ -736,33 +780,40 @@ static int run_host_batch_(cmtv_ctx* ctx, const HostBatch& B, uint8_t* out_valid
       for (size_t i = 0; i < n; i++) out_valid[i] = (uint8_t)((bm[i >> 6] >> (i & 63)) & 1);
     return CMTV_OK;
   }
+  // devices in the gather: the shards' devices, or with RCCL every rank of
+  // the communicator (a rank without a shard contributes zero words)
+  const size_t GG = P.G == 1 ? 1 : (ctx->rccl ? live.size() : P.G);
   uint64_t* bufs[kMaxDevices];
-  for (size_t g = 0; g < P.G; g++) {
-    CmtvDev& D = ctx->devs[g];
+  for (size_t g = 0; g < GG; g++) {
+    CmtvDev& D = ctx->devs[live[g]];
+    *bad_dev = (long)live[g];
     (void)hipSetDevice(D.ordinal);
-    if ((e = D.d_all.ensure(8 * std::max<size_t>(P.G * P.W, 1))) != hipSuccess) return hip_fail(e);
+    if ((e = D.d_all.ensure(8 * std::max<size_t>(GG * P.W, 1))) != hipSuccess) return hip_fail(e);
     bufs[g] = static_cast<uint64_t*>(D.d_all.p);
   }
   size_t o_valid = 0;
-  for (size_t g = 0; g < P.G; g++) {
+  for (size_t g = 0; g < GG; g++) {
     const size_t a = P.lo(g, n), b = P.hi(g, n);
+    *bad_dev = (long)live[g];
     if (a == b) {
-      // an empty trailing shard still takes part in the gather
-      (void)hipSetDevice(ctx->devs[g].ordinal);
-      if ((e = hipMemsetAsync(bufs[g] + g * P.W, 0, 8 * P.W, ctx->devs[g].stream)) != hipSuccess) return hip_fail(e);
+      // an empty shard still takes part in the gather
+      (void)hipSetDevice(ctx->devs[live[g]].ordinal);
+      if ((e = hipMemsetAsync(bufs[g] + g * P.W, 0, 8 * P.W, ctx->devs[live[g]].stream)) != hipSuccess)
+        return hip_fail(e);
       continue;
     }
-    const int rc = enqueue_shard(ctx, g, B, a, b, P.G == 1, bufs[g] + g * P.W, o_valid);
+    const int rc = enqueue_shard(ctx, live[g], B, a, b, P.G == 1, bufs[g] + g * P.W, o_valid);
     if (rc != CMTV_OK) return rc;
   }
+  *bad_dev = -1;
   if (P.G > 1) {
     ctx->stats.sharded_calls++;
-    const int rc = gather_bitmaps(ctx, P.G, P.W, bufs);
+    const int rc = gather_bitmaps(ctx, live.data(), GG, P.W, bufs);
     if (rc != CMTV_OK) return rc;
   }
-  // results from device 0: verdict bytes + bitmap (one device) or the
-  // gathered bitmap (several)
-  CmtvDev& D0 = ctx->devs[0];
+  // results from the first live device: verdict bytes + bitmap (one device)
+  // or the gathered bitmap (several)
+  CmtvDev& D0 = ctx->devs[d0];
   (void)hipSetDevice(D0.ordinal);
   const size_t o_bm = 0, o_v = align_up(8 * words, 256);
   const size_t out_bytes = P.G == 1 ? align_up(o_v + n, 256) : 8 * words;
@@ -774,10 +825,12 @@ static int run_host_batch_(cmtv_ctx* ctx, const HostBatch& B, uint8_t* out_valid
       (e = hipMemcpyAsync(hout + o_v, static_cast<uint8_t*>(D0.d_out.p) + o_valid, n, hipMemcpyDeviceToHost,
                           D0.stream)) != hipSuccess)
     return hip_fail(e);
-  for (size_t g = 0; g < P.G; g++) {
-    (void)hipSetDevice(ctx->devs[g].ordinal);
-    if ((e = hipStreamSynchronize(ctx->devs[g].stream)) != hipSuccess) return hip_fail(e);
+  for (size_t g = 0; g < GG; g++) {
+    *bad_dev = (long)live[g];
+    (void)hipSetDevice(ctx->devs[live[g]].ordinal);
+    if ((e = hipStreamSynchronize(ctx->devs[live[g]].stream)) != hipSuccess) return hip_fail(e);
   }
+  *bad_dev = -1;
   (void)hipSetDevice(D0.ordinal);
   harvest(ctx, false);
   (void)hipSetDevice(D0.ordinal);
@@ -798,18 +851,48 @@ static int run_host_batch_(cmtv_ctx* ctx, const HostBatch& B, uint8_t* out_valid
   return CMTV_OK;
 }
 
-static int run_host_batch(cmtv_ctx* ctx, const HostBatch& B, uint8_t* out_valid, uint64_t* out_bitmap) {
-  const int rc = run_host_batch_(ctx, B, out_valid, out_bitmap);
-  if (rc != CMTV_OK) {
-    // work already enqueued for other shards still reads the pinned staging
-    // the next call refills: drain it before returning the error
-    for (auto& D : ctx->devs) {
-      (void)hipSetDevice(D.ordinal);
-      (void)hipStreamSynchronize(D.stream);
-    }
-    (void)hipGetLastError();
-    (void)hipSetDevice(ctx->devs[0].ordinal);
+static void rebuild_comm(cmtv_ctx* ctx);
+
+// Takes device d out of the context's rotation after a HIP error
+// (per-GPU failure -> re-shard onto the remaining GPUs; the
+// libs/fail/fail.go analogue is CMTV_FAULT_DEV). Its communicator rank goes
+// too: the RCCL communicator is rebuilt over the survivors.
+static void retire_device(cmtv_ctx* ctx, size_t d) {
+  if (ctx->devs[d].failed) return;
+  ctx->devs[d].failed = true;
+  ctx->stats.device_failures++;
+  ctx->live.erase(std::remove(ctx->live.begin(), ctx->live.end(), d), ctx->live.end());
+  rebuild_comm(ctx);
+}
+
+static void drain(cmtv_ctx* ctx) {
+  // work already enqueued for other shards still reads the pinned staging
+  // the next call refills: drain it before returning or retrying
+  for (auto& D : ctx->devs) {
+    (void)hipSetDevice(D.ordinal);
+    (void)hipStreamSynchronize(D.stream);
   }
+  (void)hipGetLastError();
+}
+
+static int run_host_batch(cmtv_ctx* ctx, const HostBatch& B, uint8_t* out_valid, uint64_t* out_bitmap) {
+  int rc = CMTV_OK;
+  // a device error retires that device and re-plans the batch over the
+  // others, once per surviving device at most
+  for (size_t attempt = 0; attempt < ctx->devs.size(); attempt++) {
+    long bad = -1;
+    rc = run_host_batch_(ctx, B, out_valid, out_bitmap, &bad);
+    if (rc == CMTV_OK) break;
+    drain(ctx);
+    // only a device's own HIP error retires it (not CMTV_FAULT_AT, which
+    // stands for a failure of the call, nor an allocation failure)
+    const bool injected = ctx->fault_pending;
+    ctx->fault_pending = false;
+    if (rc != CMTV_EHIP || injected || bad < 0 || ctx->live.size() < 2) break;
+    retire_device(ctx, (size_t)bad);
+    ctx->stats.reshards++;
+  }
+  (void)hipSetDevice(ctx->devs[ctx->live.empty() ? 0 : ctx->live[0]].ordinal);
   return rc;
 }
 
@@ -920,6 +1003,8 @@ static int init_device(cmtv_ctx* ctx, CmtvDev& D) {
   hipError_t e = hipStreamCreateWithFlags(&D.stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&D.atab_done, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&D.done, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipMalloc(&D.d_diag, kDiagWords * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMemsetAsync(D.d_diag, 0, kDiagWords * sizeof(uint32_t), D.stream);
   if (e == hipSuccess) e = hipMalloc(&D.d_btab, kBtabWords * sizeof(uint32_t));
   if (e == hipSuccess) e = launch_btab_init(D.d_btab, D.stream);
   uint16_t prog[SR_PROGRAM_MAX];
@@ -944,6 +1029,8 @@ static void release_device(CmtvDev& D) {
   if (D.d_btab) (void)hipFree(D.d_btab);
   if (D.d_bcomb) (void)hipFree(D.d_bcomb);
   if (D.d_srprog) (void)hipFree(D.d_srprog);
+  if (D.d_diag) (void)hipFree(D.d_diag);
+  D.d_diag = nullptr;
   D.d_btab = nullptr;
   D.d_bcomb = nullptr;
   D.d_srprog = nullptr;
@@ -970,6 +1057,41 @@ static void read_env(cmtv_ctx* ctx) {
   if (const char* fw = std::getenv("CMTV_FORCE_WIDE")) ctx->force_wide = fw[0] == '1';
   if (const char* nf = std::getenv("CMTV_NO_SB_FUSE")) ctx->sb_fuse = nf[0] != '1';
   if (const char* nz = std::getenv("CMTV_NO_ZC_IN")) ctx->zc_in = nz[0] != '1';
+  if (const char* kl = std::getenv("CMTV_FORCE_K_LATE")) ctx->keyed_wait = kl[0] == '1' ? 0u : kKeyedWaitDefault;
+  ctx->force_rccl = std::getenv("CMTV_FORCE_RCCL") != nullptr;
+  ctx->no_rccl = std::getenv("CMTV_NO_RCCL") != nullptr;
+}
+
+// The bitmap communicator over the live devices (rank = position in
+// ctx->live), when their ordinals are distinct and librccl loads; a one-rank
+// communicator only under CMTV_FORCE_RCCL (the RCCL path on a one-GPU box).
+// Otherwise gathers use peer copies. Called at open and after a device is
+// retired (the old communicator included it).
+static void rebuild_comm(cmtv_ctx* ctx) {
+  const Rccl& R = rccl();
+  for (auto& D : ctx->devs) {
+    if (D.comm && R.ok) {
+      (void)hipSetDevice(D.ordinal);
+      (void)R.CommDestroy(D.comm);
+    }
+    D.comm = nullptr;
+  }
+  ctx->rccl = false;
+  std::vector<int> ords;
+  for (size_t d : ctx->live) ords.push_back(ctx->devs[d].ordinal);
+  std::vector<int> sorted = ords;
+  std::sort(sorted.begin(), sorted.end());
+  const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
+  const bool want = ords.size() > 1 ? (distinct && !ctx->no_rccl) : (ords.size() == 1 && ctx->force_rccl);
+  if (want && R.ok) {
+    std::vector<ncclComm_t> comms(ords.size(), nullptr);
+    if (R.CommInitAll(comms.data(), (int)ords.size(), ords.data()) == 0) {
+      for (size_t g = 0; g < ords.size(); g++) ctx->devs[ctx->live[g]].comm = comms[g];
+      ctx->rccl = true;
+    }
+  }
+  ctx->stats.rccl = ctx->rccl ? 1 : 0;
+  (void)hipSetDevice(ctx->devs[ctx->live.empty() ? 0 : ctx->live[0]].ordinal);
 }
 
 // CMTVERIFY_DEVICES: "0,1,2" or "all" (or unset: every visible device)
@@ -1020,37 +1142,22 @@ static int open_ctx(const cmtv_config* cfg, const std::vector<int>& ords, cmtv_c
     }
   }
   ctx->stats.n_devices = (uint32_t)ords.size();
-  // CMTV_FORCE_RCCL (test knob): an RCCL communicator even over one device,
-  // so a one-GPU box runs the library's RCCL init and all-gather calls
-  const bool force_rccl = std::getenv("CMTV_FORCE_RCCL") != nullptr;
-  if (ords.size() == 1 && force_rccl) {
-    const Rccl& R = rccl();
-    ncclComm_t comm = nullptr;
-    if (R.ok && R.CommInitAll(&comm, 1, ords.data()) == 0) {
-      ctx->devs[0].comm = comm;
-      ctx->rccl = true;
-    }
+  for (size_t g = 0; g < ords.size(); g++) ctx->live.push_back(g);
+  // CMTV_FAULT_DEV=g: the g-th device's launches fail (re-shard test knob)
+  if (const char* fd = std::getenv("CMTV_FAULT_DEV")) {
+    char* end = nullptr;
+    const long g = std::strtol(fd, &end, 10);
+    if (end != fd && g >= 0 && (size_t)g < ords.size()) ctx->devs[(size_t)g].inject_fault = true;
   }
   if (ords.size() > 1) {
-    std::vector<int> sorted = ords;
-    std::sort(sorted.begin(), sorted.end());
-    const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
     for (size_t g = 0; g < ords.size(); g++) {  // peer access for the copy gathers
       (void)hipSetDevice(ords[g]);
       for (size_t h = 0; h < ords.size(); h++)
         if (ords[h] != ords[g]) (void)hipDeviceEnablePeerAccess(ords[h], 0);
     }
     (void)hipGetLastError();  // "already enabled" is not an error here
-    const Rccl& R = rccl();
-    if (distinct && R.ok && !std::getenv("CMTV_NO_RCCL")) {
-      std::vector<ncclComm_t> comms(ords.size(), nullptr);
-      if (R.CommInitAll(comms.data(), (int)ords.size(), ords.data()) == 0) {
-        for (size_t g = 0; g < ords.size(); g++) ctx->devs[g].comm = comms[g];
-        ctx->rccl = true;
-      }
-    }
   }
-  ctx->stats.rccl = ctx->rccl ? 1 : 0;
+  rebuild_comm(ctx);
   (void)hipSetDevice(ords[0]);
   *out = ctx;
   return CMTV_OK;
@@ -1138,6 +1245,7 @@ int cmtv_sync(cmtv_ctx* ctx) {
   if (!ctx) return CMTV_EINVAL;
   std::lock_guard<std::mutex> g(ctx->mu);
   for (auto& D : ctx->devs) {
+    if (D.failed) continue;
     if (hipSetDevice(D.ordinal) != hipSuccess) return CMTV_ENODEV;
     const hipError_t e = hipStreamSynchronize(D.stream);
     if (e != hipSuccess) return hip_fail(e);
@@ -1147,13 +1255,43 @@ int cmtv_sync(cmtv_ctx* ctx) {
   return CMTV_OK;
 }
 
+// the kernels' diagnostic counters of every usable device, summed
+static void read_diag(cmtv_ctx* ctx) {
+  uint64_t late = 0;
+  for (auto& D : ctx->devs) {
+    if (D.failed || !D.d_diag) continue;
+    (void)hipSetDevice(D.ordinal);
+    uint32_t w[kDiagWords] = {};
+    if (hipMemcpy(w, D.d_diag, sizeof(w), hipMemcpyDeviceToHost) == hipSuccess) late += w[kDiagLateK];
+  }
+  ctx->stats.late_k_waves = late;
+}
+
 int cmtv_stats_get(cmtv_ctx* ctx, cmtv_stats* out) {
   if (!ctx || !out) return CMTV_EINVAL;
   std::lock_guard<std::mutex> g(ctx->mu);
   harvest(ctx, true);
+  read_diag(ctx);
   (void)hipSetDevice(ctx->devs[0].ordinal);
   ctx->stats.cache_entries = ctx->cache.size();
+  ctx->stats.live_devices = (uint32_t)ctx->live.size();
   *out = ctx->stats;
+  return CMTV_OK;
+}
+
+int cmtv_device_stats_get(cmtv_ctx* ctx, int g, cmtv_device_stats* out) {
+  if (!ctx || !out || g < 0 || g >= (int)ctx->devs.size()) return CMTV_EINVAL;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  harvest(ctx, true);
+  CmtvDev& D = ctx->devs[(size_t)g];
+  std::memset(out, 0, sizeof(*out));
+  out->ordinal = D.ordinal;
+  out->failed = D.failed ? 1 : 0;
+  out->calls = D.calls;
+  out->signatures = D.signatures;
+  out->kernel_launches = D.launches;
+  out->device_ms = D.device_ms;
+  (void)hipSetDevice(ctx->devs[0].ordinal);
   return CMTV_OK;
 }
 
@@ -1225,6 +1363,8 @@ static int sharded_device(cmtv_ctx* ctx, const cmtv_keyset* ks, const size_t* n_
                           uint32_t mode, void* const* d_valid, void* const* d_bitmap_all, size_t* words_per_shard,
                           bool gather = true) {
   const size_t G = ctx->devs.size();
+  // the caller's inputs live on every device: a retired one cannot take part
+  if (ctx->live.size() != G) return CMTV_ENODEV;
   size_t W = 0;
   for (size_t g = 0; g < G; g++) {
     if (n_shard[g] > (1ull << 31)) return CMTV_EINVAL;
@@ -1258,14 +1398,22 @@ static int sharded_device(cmtv_ctx* ctx, const cmtv_keyset* ks, const size_t* n_
       rc = enqueue_verify(ctx, D, n_shard[g], static_cast<const uint8_t*>(d_keys[g]),
                           static_cast<const uint8_t*>(d_sig[g]), static_cast<const uint8_t*>(d_msg[g]),
                           static_cast<const uint32_t*>(d_off[g]), mode, dv, own_bm, D.stream);
-    if (rc != CMTV_OK) return rc;
+    if (rc != CMTV_OK) {
+      // a device's own HIP error takes it out of the rotation (host batches
+      // re-plan over the others); this call fails: its inputs were there
+      const bool injected = ctx->fault_pending;
+      ctx->fault_pending = false;
+      if (rc == CMTV_EHIP && !injected && G > 1) retire_device(ctx, g);
+      (void)hipSetDevice(ctx->devs[0].ordinal);
+      return rc;
+    }
   }
   if (!gather) {
     (void)hipSetDevice(ctx->devs[0].ordinal);
     return CMTV_OK;
   }
   if (G > 1) ctx->stats.sharded_calls++;
-  const int rc = gather_bitmaps(ctx, G, W, bufs);
+  const int rc = gather_bitmaps(ctx, ctx->live.data(), G, W, bufs);
   (void)hipSetDevice(ctx->devs[0].ordinal);
   return rc;
 }
@@ -1353,6 +1501,7 @@ int register_keys_locked(cmtv_ctx* ctx, size_t n_keys, const uint8_t* pk, cmtv_k
   for (size_t g = 0; g < ctx->devs.size(); g++) {
     CmtvDev& D = ctx->devs[g];
     auto& K = ks->dev[g];
+    if (D.failed) continue;  // retired: never given work again
     (void)hipSetDevice(D.ordinal);
     int rc = ensure_bcomb(D);
     if (rc != CMTV_OK) {

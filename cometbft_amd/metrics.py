@@ -34,11 +34,16 @@ _FIELDS = [
     ("sharded_calls", "sharded_calls_total", "counter", "Batches split over more than one device."),
     ("gathers", "bitmap_gathers_total", "counter", "Verdict-bitmap all-gathers (RCCL or peer copy)."),
     ("faults_injected", "faults_injected_total", "counter", "Launches failed by the CMTV_FAULT_AT knob."),
+    ("device_failures", "device_failures_total", "counter", "Devices retired after a HIP error."),
+    ("reshards", "reshards_total", "counter", "Host batches re-planned over the remaining devices."),
+    ("late_k_waves", "late_k_waves_total", "counter",
+     "Keyed split-kernel waves that hashed their own signatures instead of waiting for the helper."),
     ("fused_sign_bytes", "fused_sign_bytes_total", "counter",
      "Templated batches whose sign-bytes the verify kernel's helper wave wrote."),
     ("cache_entries", "verdict_cache_entries", "gauge", "Verdicts currently cached."),
     ("n_devices", "devices", "gauge", "Devices driven by the context."),
     ("rccl", "rccl", "gauge", "1 when bitmap gathers run over an RCCL communicator."),
+    ("live_devices", "live_devices", "gauge", "Devices still taking work."),
 ]
 
 

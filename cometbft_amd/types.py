@@ -280,7 +280,9 @@ def _error_for(rc, res, msg):
     if code == N.COMMIT_ERR_NOT_ENOUGH_POWER:
         return ErrNotEnoughVotingPowerSigned(msg, res.got, res.needed)
     if code == N.COMMIT_ERR_DOUBLE_VOTE:
-        return ErrDoubleVote(msg)
+        e = ErrDoubleVote(msg)
+        e.result = N.cmtv_commit_result.from_buffer_copy(res)
+        return e
     if code == N.COMMIT_ERR_TRUST_LEVEL:
         return ErrTrustLevel(msg)
     if code in (N.COMMIT_PANIC_BAD_PUBKEY, N.COMMIT_PANIC_UNKNOWN_FLAG):

@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define CMTV_ABI_VERSION 5
+#define CMTV_ABI_VERSION 6
 
 enum {
   CMTV_OK = 0,
@@ -90,7 +90,25 @@ typedef struct cmtv_stats {
   uint32_t rccl;           /* 1: gathers run over an RCCL communicator */
   uint64_t fused_sign_bytes; /* templated batches whose sign-bytes the verify
                               kernel's helper wave wrote (no k_sign_bytes) */
+  uint64_t device_failures;  /* devices retired after a HIP error          */
+  uint64_t reshards;         /* host batches re-planned over the remaining
+                              devices after such a failure               */
+  uint64_t late_k_waves;     /* keyed split-kernel quad waves that stopped
+                              waiting for the hash helper and hashed their own
+                              signatures (timing only, never a verdict)  */
+  uint32_t live_devices;     /* devices still taking work                 */
+  uint32_t reserved;
 } cmtv_stats;
+
+/* One device's share of the context's work (cmtv_device_stats_get). */
+typedef struct cmtv_device_stats {
+  int32_t ordinal;          /* HIP ordinal                                 */
+  uint32_t failed;          /* 1: retired after a HIP error                */
+  uint64_t calls;           /* verify calls that ran on this device        */
+  uint64_t signatures;
+  uint64_t kernel_launches;
+  double device_ms;         /* summed kernel time on this device (HIP events) */
+} cmtv_device_stats;
 
 /* ------------------------------------------------------------ lifecycle */
 
@@ -106,7 +124,11 @@ typedef struct cmtv_stats {
  * FAIL_TEST_INDEX analogue), CMTV_FORCE_WIDE=1 (test knob: the quad kernels
  * take the 64-window half-scalar fallback for every signature),
  * CMTV_FORCE_RCCL=1 (test knob: a one-rank RCCL communicator even over one
- * device, so a one-GPU box exercises the RCCL init and all-gather). */
+ * device, so a one-GPU box exercises the RCCL init and all-gather),
+ * CMTV_FAULT_DEV=g (test knob: every launch on the context's g-th device
+ * fails with a HIP error: host batches retire it and re-shard onto the other
+ * devices), CMTV_FORCE_K_LATE=1 (test knob: the keyed split kernel's quads
+ * never wait for the hash helper and hash their signatures themselves). */
 int cmtv_open(const cmtv_config* cfg, cmtv_ctx** out);
 
 /* Opens ONE context over several devices (a node is one
@@ -117,8 +139,15 @@ int cmtv_open(const cmtv_config* cfg, cmtv_ctx** out);
  * and registered-key combs; when the ordinals are distinct an RCCL
  * communicator over them (ncclCommInitAll) carries the bitmap all-gather,
  * otherwise (a repeated ordinal, used to exercise sharding on one GPU) peer
- * copies do. Host-buffer batches of at least CMTV_SHARD_MIN (default 8192)
- * signatures per device are sharded; smaller ones run on devices[0].
+ * copies do. A host-buffer batch is sharded over as many devices as get at
+ * least CMTV_SHARD_MIN (default 8192) signatures each (a 40k batch takes 4
+ * of 8 GPUs; below 2 x CMTV_SHARD_MIN it runs on one).
+ * Device failure: a device whose launch, copy or sync fails with a HIP error
+ * is retired (cmtv_stats.device_failures, cmtv_device_stats.failed), the RCCL
+ * communicator is rebuilt over the others and the failed host batch is
+ * re-planned over them and run again in the same call; later host batches
+ * never use it. Device-resident calls that need a retired device return
+ * CMTV_ENODEV (their inputs were on it).
  * Device-resident single-device calls (_device) run on devices[0].
  * cfg->device is ignored; cfg may be NULL (then CMTVERIFY_MODE = "go" |
  * "zip215" picks the default mode). */
@@ -133,6 +162,8 @@ void cmtv_close(cmtv_ctx* ctx);
 const char* cmtv_strerror(int code);
 int cmtv_abi_version(void);
 int cmtv_stats_get(cmtv_ctx* ctx, cmtv_stats* out);
+/* Stats of the context's g-th device (0 <= g < cmtv_device_count). */
+int cmtv_device_stats_get(cmtv_ctx* ctx, int g, cmtv_device_stats* out);
 /* hipStream_t of the context (as void*), for callers that order their own
  * work with it (bench, multi-GPU gather). */
 void* cmtv_stream(cmtv_ctx* ctx);
@@ -341,9 +372,12 @@ enum {
 
 typedef struct cmtv_commit_result {
   int32_t code;        /* CMTV_COMMIT_*                                      */
-  int32_t sig_index;   /* index the error refers to, or -1                   */
-  int64_t got;         /* ErrNotEnoughVotingPowerSigned.Got                  */
-  int64_t needed;      /* ErrNotEnoughVotingPowerSigned.Needed               */
+  int32_t sig_index;   /* index the error refers to, or -1 (DOUBLE_VOTE: the
+                          second commit index)                               */
+  int64_t got;         /* ErrNotEnoughVotingPowerSigned.Got; DOUBLE_VOTE: the
+                          first commit index                                 */
+  int64_t needed;      /* ErrNotEnoughVotingPowerSigned.Needed; DOUBLE_VOTE:
+                          the validator's index in vals                      */
   uint32_t n_verified; /* signatures sent to the device                      */
   uint32_t reserved;
 } cmtv_commit_result;

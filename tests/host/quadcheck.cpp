@@ -133,7 +133,12 @@ static void to_words(uint32_t* w, const uint8_t* b, int nw) {
 
 int main(int argc, char** argv) {
   // argv[1] == "sr": sr25519 records { pk[32], sig[64], u32 mlen, msg } (no mode byte)
-  const bool sr = argc > 1 && !strcmp(argv[1], "sr");
+  // argv[1] == "sr2": the same through k_verify_sr25519_quad_split's path --
+  // the merlin transcript and [u]B computed once as its helper wave does, the
+  // tables built before the scalars arrive (q_tables_early: R's table is of
+  // -R, a negative k2 flips R's digits at lookup), then q_verify_sr_split<true>
+  const bool sr2 = argc > 1 && !strcmp(argv[1], "sr2");
+  const bool sr = sr2 || (argc > 1 && !strcmp(argv[1], "sr"));
   // argv[1] == "keyed": Ed25519 records, verified through registered-key combs (keyed_quad.h)
   const bool keyed = argc > 1 && !strcmp(argv[1], "keyed");
   // argv[1] == "oct": Ed25519 records through the 8-lane verifier (oct.h)
@@ -154,7 +159,7 @@ int main(int argc, char** argv) {
   uint16_t prog[SR_PROGRAM_MAX];
   const int nops = sr_build_program(prog);
   HostBTab bt;
-  uint32_t n;
+  uint32_t n, k2_neg_count = 0;
   if (fread(&n, 4, 1, stdin) != 1) return 1;
   for (uint32_t i = 0; i < n; i++) {
     uint8_t mode = 0, pk[32], sig[64];
@@ -185,6 +190,14 @@ int main(int argc, char** argv) {
     std::vector<std::thread> th;
     SigPrep hp;
     uint32_t bpt[40];
+    if (sr2) {
+      ArrayStrobeState st;
+      sr_prepare(hp, pkw, sigw, mp, mlen, prog, nops, st, false);
+      ge_p3 Bp;
+      q_bcomb16(Bp, hp.u, bt);
+      bpoint_store(bpt, Bp);
+      k2_neg_count += (hp.flags & 1u) ? 1 : 0;
+    }
     if (quad2 || oct2) {
       if (mode)
         q_prepare<MODE_ZIP215>(hp, pkw, sigw, mp, mlen, false);
@@ -195,6 +208,17 @@ int main(int argc, char** argv) {
       bpoint_store(bpt, Bp);
     }
     auto get_prep = [&](SigPrep& p) { p = hp; };
+    if (sr2) {
+      for (int l = 0; l < 4; l++)
+        th.emplace_back([&, l] {
+          HostQuad q{l, &ex};
+          QArrayTab ta, tr;
+          auto get_b = [&](fe& c) {
+            for (int j = 0; j < 10; j++) c.v[j] = bpt[10 * l + j];
+          };
+          res[l] = q_verify_sr_split<true>(q, pkw, sigw, bt, ta, tr, get_prep, get_b);
+        });
+    }
     if (quad2 || oct2) {
       ex.bar.n = oct2 ? 8 : 4;
       for (int l = 0; l < (oct2 ? 8 : 4); l++)
@@ -224,7 +248,7 @@ int main(int argc, char** argv) {
                         : o_verify<MODE_GO_STDLIB>(q, pkw, sigw, mp, mlen, bt, ta);
         });
     }
-    for (int l = 0; l < (oct || quad2 || oct2 ? 0 : 4); l++)
+    for (int l = 0; l < (oct || quad2 || oct2 || sr2 ? 0 : 4); l++)
       th.emplace_back([&, l] {
         HostQuad q{l, &ex};
         QArrayTab ta, tr;
@@ -246,5 +270,7 @@ int main(int argc, char** argv) {
     uint8_t o = res[0];
     fwrite(&o, 1, 1, stdout);
   }
+  // sr2: how many signatures took the negative-k2 (flipped R digit) path
+  if (sr2) fprintf(stderr, "k2_neg %u of %u\n", k2_neg_count, n);
   return 0;
 }

@@ -164,6 +164,10 @@ def test_light_trusting_double_vote(gpu_ctx):
     assert isinstance(e, T.ErrDoubleVote)
     assert str(e).startswith("double vote from Validator{%s PubKeyEd25519{%s} VP:10 A:0} (0 and 2)" %
                              (vals[0].v.address.hex().upper(), vals[0].pk.hex().upper()))
+    # the indices a Go binding formats the error from:
+    # sig_index = second, got = first commit index, needed = validator index
+    r = e.result
+    assert (r.sig_index, r.got, vset.validators[r.needed].pub_key) == (2, 0, vals[0].pk)
 
 
 def test_not_enough_power_values(gpu_ctx):

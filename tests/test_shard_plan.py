@@ -2,7 +2,8 @@
 host-compiled by tests/host/shardcheck.cpp): for every batch size and
 device count the shards are contiguous, cover [0, n) exactly once, start on
 64-signature (bitmap-word) boundaries so their bitmaps concatenate in place,
-and small batches stay on one device."""
+and a batch uses as many devices as give each at least shard_min signatures
+(partial-G plans: a 40k batch runs on 4 of 8 GPUs)."""
 import os
 import struct
 import subprocess
@@ -27,13 +28,17 @@ def test_shard_plan_invariants():
     out = subprocess.run([binary], input=buf, capture_output=True, check=True).stdout
     plans = np.frombuffer(out, np.uint64).reshape(-1, 3)
     for (n, g, m), (G, S, W) in zip(cases, plans.tolist()):
+        per = max(m, 64)
         assert 1 <= G <= g
-        if g > 1 and n < g * max(m, 64):
-            assert G == 1, (n, g, m)
+        # as many devices as get shard_min signatures each, at least one
+        assert G == min(g, max(1, n // per)), (n, g, m, G)
         if G == 1:
             assert S == n
             continue
-        assert G == g and S % 64 == 0 and W == S // 64
+        assert S % 64 == 0 and W == S // 64
+        # every used device has at least shard_min signatures but the last
+        # (ceil(n / G) >= per, rounded up to whole words)
+        assert S >= per
         los = [min(n, k * S) for k in range(G)]
         his = [min(n, (k + 1) * S) for k in range(G)]
         assert los[0] == 0 and his[-1] == n, (n, g, m)
@@ -44,3 +49,21 @@ def test_shard_plan_invariants():
         assert G * W >= (n + 63) // 64
         # balanced: no device gets more than one 64-signature word over n / G
         assert S - (n + G - 1) // G < 64
+
+
+def test_partial_device_plans():
+    """The VERDICT r2 case: 40k signatures on 8 GPUs at the default
+    shard_min (8192) run on 4 devices, each a whole-word shard."""
+    binary = _build(SRC, BIN, ["-std=c++17"])
+    cases = [(40_000, 8, 8192), (16_384, 8, 8192), (16_383, 8, 8192), (8192 * 8, 8, 8192), (10**6, 8, 8192),
+             (24_576, 3, 8192), (100, 8, 0)]
+    buf = b"".join(struct.pack("<3Q", *c) for c in cases)
+    out = subprocess.run([binary], input=buf, capture_output=True, check=True).stdout
+    got = [tuple(r) for r in np.frombuffer(out, np.uint64).reshape(-1, 3).tolist()]
+    assert got[0] == (4, 10_048, 157)
+    assert got[1] == (2, 8192, 128)
+    assert got[2][0] == 1
+    assert got[3] == (8, 8192, 128)
+    assert got[4][0] == 8
+    assert got[5] == (3, 8192, 128)
+    assert got[6][0] == 1

@@ -144,12 +144,16 @@ def test_key_and_signature_lengths():
     assert S.verify(b"", b"m", S.sign(b"\0" * 32, b"m")) == S.verify(bytes(32), b"m", S.sign(b"\0" * 32, b"m"))
 
 
-def _run_srcheck(binary, vectors, idx, arg=None):
+def _srcheck_input(vectors, idx):
     buf = [struct.pack("<I", len(idx))]
     for i in idx:
         m = vectors["msgs"][i]
         buf.append(vectors["pk"][i].tobytes() + vectors["sig"][i].tobytes() + struct.pack("<I", len(m)) + m)
-    out = subprocess.run([binary] + ([arg] if arg else []), input=b"".join(buf), capture_output=True,
+    return b"".join(buf)
+
+
+def _run_srcheck(binary, vectors, idx, arg=None):
+    out = subprocess.run([binary] + ([arg] if arg else []), input=_srcheck_input(vectors, idx), capture_output=True,
                          check=True, timeout=600).stdout
     return out
 
@@ -194,3 +198,24 @@ def test_quad_pipeline_matches_corpus(vectors):
     exp = vectors["valid"][sorted(idx)]
     bad = np.nonzero(got != exp)[0]
     assert bad.size == 0, [(sorted(idx)[int(i)], cats[sorted(idx)[int(i)]]) for i in bad[:10]]
+
+
+def test_split_quad_pipeline_matches_corpus(vectors):
+    """the split kernel's order (k_verify_sr25519_quad_split) --
+    tables before the scalars (q_tables_early, R's table of -R), the
+    transcript and [u]B from the helper's code, a negative k2 flipping R's
+    digits at lookup (q_straus_prep_b<true, true>) -- over the whole corpus,
+    with both signs of k2 represented. Every radix-16 digit value, including
+    dR = 0 and dR = -8, occurs in the corpus' ~10k windows."""
+    hdr = os.path.join(ROOT, "cometbft_amd", "csrc")
+    deps = [QSRC] + [os.path.join(hdr, f) for f in os.listdir(hdr) if f.endswith(".h")]
+    if not os.path.exists(QBIN) or os.path.getmtime(QBIN) < max(os.path.getmtime(d) for d in deps):
+        subprocess.run(["g++", "-O2", "-std=c++20", "-pthread", "-o", QBIN, QSRC], check=True)
+    idx = list(range(len(vectors["cats"])))
+    buf = _srcheck_input(vectors, idx)
+    r = subprocess.run([QBIN, "sr2"], input=buf, capture_output=True, check=True, timeout=600)
+    got = np.frombuffer(r.stdout, np.uint8)
+    bad = np.nonzero(got != vectors["valid"])[0]
+    assert bad.size == 0, [(int(i), vectors["cats"][int(i)]) for i in bad[:10]]
+    neg = int(r.stderr.decode().split("k2_neg ")[1].split()[0])
+    assert 0.2 * len(idx) < neg < 0.8 * len(idx), neg

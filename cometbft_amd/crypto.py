@@ -129,7 +129,7 @@ class Context:
         failed (retired after a HIP error), calls, signatures, launches and
         summed kernel milliseconds on that device."""
         out = []
-        for g in range(self.n_devices()):
+        for g in range(self.n_devices):
             st = N.cmtv_device_stats()
             N.check(N.lib().cmtv_device_stats_get(self._h, g, ctypes.byref(st)), "cmtv_device_stats_get")
             out.append({k: getattr(st, k) for k, _ in st._fields_})

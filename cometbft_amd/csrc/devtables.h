@@ -91,6 +91,84 @@ struct DevQuad {
   __device__ __forceinline__ uint32_t perm32(uint32_t x) const {
     return dpp<PAT>(x);
   }
+  // Fused quad moves (quad.h, FOLD = 2): a DPP quad_perm read as the first
+  // operand of the 32-bit VOP2 that consumes it, written out as one asm
+  // block per field element -- ROCm 7.2's DPP-combine folds only some of
+  // them, and its bound_ctrl:1 folds miscompiled. Each block
+  // starts with s_nop 1: the two wait states a DPP read needs after the VALU
+  // that wrote its source (the compiler inserts none in front of inline asm);
+  // inside a block no DPP source is written.
+  //   add_perm:  o = perm(src) + b        v_add_u32_dpp
+  //   xor_perm:  o = perm(src) ^ k        v_xor_b32_dpp
+  //   perm_lane3: o = lane 3 ? perm(src) : 0   v_cndmask_b32_dpp (vcc = lanes 0-2)
+#define CMTV_DPP10_CND(PATS)                                                                                 \
+  "s_nop 1\n"                                                                                               \
+  "v_cndmask_b32_dpp %0, %10, %20, vcc " PATS "\n v_cndmask_b32_dpp %1, %11, %20, vcc " PATS                \
+  "\n v_cndmask_b32_dpp %2, %12, %20, vcc " PATS "\n v_cndmask_b32_dpp %3, %13, %20, vcc " PATS             \
+  "\n v_cndmask_b32_dpp %4, %14, %20, vcc " PATS "\n v_cndmask_b32_dpp %5, %15, %20, vcc " PATS             \
+  "\n v_cndmask_b32_dpp %6, %16, %20, vcc " PATS "\n v_cndmask_b32_dpp %7, %17, %20, vcc " PATS             \
+  "\n v_cndmask_b32_dpp %8, %18, %20, vcc " PATS "\n v_cndmask_b32_dpp %9, %19, %20, vcc " PATS "\n"
+#define CMTV_QP_STR(a, b, c, d) "quad_perm:[" #a "," #b "," #c "," #d "] row_mask:0xf bank_mask:0xf"
+#define CMTV_DPP10(OP, PATS)                                                                                 \
+  "s_nop 1\n"                                                                                               \
+  OP " %0, %10, %20 " PATS "\n" OP " %1, %11, %21 " PATS "\n" OP " %2, %12, %22 " PATS "\n" OP            \
+     " %3, %13, %23 " PATS "\n" OP " %4, %14, %24 " PATS "\n" OP " %5, %15, %25 " PATS "\n" OP             \
+     " %6, %16, %26 " PATS "\n" OP " %7, %17, %27 " PATS "\n" OP " %8, %18, %28 " PATS "\n" OP            \
+     " %9, %19, %29 " PATS "\n"
+#define CMTV_DPP10_K(OP, PATS)                                                                               \
+  "s_nop 1\n"                                                                                               \
+  OP " %0, %10, %20 " PATS "\n" OP " %1, %11, %20 " PATS "\n" OP " %2, %12, %20 " PATS "\n" OP            \
+     " %3, %13, %20 " PATS "\n" OP " %4, %14, %20 " PATS "\n" OP " %5, %15, %20 " PATS "\n" OP             \
+     " %6, %16, %20 " PATS "\n" OP " %7, %17, %20 " PATS "\n" OP " %8, %18, %20 " PATS "\n" OP            \
+     " %9, %19, %20 " PATS "\n"
+#define CMTV_FE_OUT(o)                                                                                       \
+  "=&v"(o.v[0]), "=&v"(o.v[1]), "=&v"(o.v[2]), "=&v"(o.v[3]), "=&v"(o.v[4]), "=&v"(o.v[5]), "=&v"(o.v[6]),   \
+      "=&v"(o.v[7]), "=&v"(o.v[8]), "=&v"(o.v[9])
+#define CMTV_FE_IN(x)                                                                                        \
+  "v"(x.v[0]), "v"(x.v[1]), "v"(x.v[2]), "v"(x.v[3]), "v"(x.v[4]), "v"(x.v[5]), "v"(x.v[6]), "v"(x.v[7]),     \
+      "v"(x.v[8]), "v"(x.v[9])
+#define CMTV_QP_CASES(BODY)                                                                                  \
+  if constexpr (PAT == 0x55) { BODY(CMTV_QP_STR(1, 1, 1, 1)); }                                               \
+  else if constexpr (PAT == (0 | (1 << 2) | (2 << 4) | (0 << 6))) { BODY(CMTV_QP_STR(0, 1, 2, 0)); }           \
+  else if constexpr (PAT == 2) { BODY(CMTV_QP_STR(2, 0, 0, 0)); }                                             \
+  else if constexpr (PAT == (0 | (3 << 2) | (3 << 4) | (0 << 6))) { BODY(CMTV_QP_STR(0, 3, 3, 0)); }           \
+  else if constexpr (PAT == (1 | (2 << 2) | (2 << 4) | (1 << 6))) { BODY(CMTV_QP_STR(1, 2, 2, 1)); }           \
+  else { static_assert(PAT < 0, "quad_perm pattern without an asm string"); }
+  template <int PAT>
+  __device__ __forceinline__ void add_perm(fe& o, const fe& src, const fe& b) const {
+#define CMTV_BODY(PATS) asm volatile(CMTV_DPP10("v_add_u32_dpp", PATS) : CMTV_FE_OUT(o) : CMTV_FE_IN(src), CMTV_FE_IN(b))
+    CMTV_QP_CASES(CMTV_BODY)
+#undef CMTV_BODY
+  }
+  template <int PAT>
+  __device__ __forceinline__ void xor_perm(fe& o, const fe& src, uint32_t k) const {
+#define CMTV_BODY(PATS) asm volatile(CMTV_DPP10_K("v_xor_b32_dpp", PATS) : CMTV_FE_OUT(o) : CMTV_FE_IN(src), "v"(k))
+    CMTV_QP_CASES(CMTV_BODY)
+#undef CMTV_BODY
+  }
+  template <int PAT>
+  __device__ __forceinline__ void perm_lane3(fe& o, const fe& src) const {
+    // vcc = lanes other than 3 of each quad; v_cndmask_b32 o = vcc ? 0 : perm(src)
+    const uint64_t keep = 0x7777777777777777ull;
+    const uint32_t zero = 0;
+#define CMTV_BODY(PATS)                                                                                      \
+  asm volatile("s_mov_b64 vcc, %21\n" CMTV_DPP10_CND(PATS)                                                  \
+               : CMTV_FE_OUT(o)                                                                              \
+               : CMTV_FE_IN(src), "v"(zero), "s"(keep)                                                      \
+               : "vcc")
+    CMTV_QP_CASES(CMTV_BODY)
+#undef CMTV_BODY
+  }
+  // A move meant to fold into its one consumer: update_dpp(old = 0), which
+  // DPP-combine turns into that VOP2's own DPP operand (v_add_u32_dpp,
+  // v_and_b32_dpp, v_xor_b32_dpp ...; quad_perm reads no invalid lane, so
+  // the zero old value never shows). Use only where the result has a single
+  // VOP2 use: otherwise it stays a move.
+  template <int PAT>
+  __device__ __forceinline__ void permc(fe& o, const fe& v) const {
+#pragma unroll
+    for (int i = 0; i < 10; i++) o.v[i] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.v[i], PAT, 0xF, 0xF, false);
+  }
   __device__ __forceinline__ bool any(bool x) const { return __ballot(x) != 0; }
 };
 

@@ -73,7 +73,18 @@ CMTV_HD void q_cached_identity(fe& v, int lane) {
 // its own U by one neighbour's: a single quad_perm move {E', M, F', S}. The
 // U_c take two moves of the round-1 results (lane 0 reads C', the rest A;
 // every lane B). Input T (lane 3) is ignored; output is a full extended point.
-template <class Q>
+// FOLD: how a quad move that feeds exactly one 32-bit add / xor / select
+// reaches it. 0: a v_mov_b32_dpp, then the instruction; 2: the policy's fused
+// forms (add_perm, xor_perm, perm_lane3 -- DevQuad: v_add_u32_dpp,
+// v_xor_b32_dpp, v_cndmask_b32_dpp), 30 fewer VALU instructions per doubling
+// and 10 per addition; 1: permc (update_dpp, left to DPP-combine; folds only
+// some). A/B: tools/microbench/pt_lat.hip.
+#ifndef CMTV_DPP_FOLD
+#define CMTV_DPP_FOLD 0
+#endif
+constexpr int kDppFold = CMTV_DPP_FOLD;
+
+template <int FOLD = kDppFold, class Q>
 CMTV_HD void q_dbl(const Q& q, fe& v) {
   const int lane = q.lane();
   // per-lane masks (loop-invariant): the four U_c share one straight-line
@@ -81,23 +92,61 @@ CMTV_HD void q_dbl(const Q& q, fe& v) {
   // instead of computing all four candidates and selecting
   const uint32_t m3 = lane == 3 ? ~0u : 0u;
   const uint32_t sh = lane == 0 ? 1u : 0u;                  // 2C' on lane 0
+  const uint32_t s2 = lane == 2 ? 1u : 0u;                  // ... doubled at its source, lane 2 (FOLD)
   const uint32_t n2 = (lane & 1) ? 0u : ~0u;                // -B on lanes 0, 2
   const uint32_t n3 = lane == 3 ? ~0u : 0u;                 // -K on lane 3
   const uint32_t mo = (lane == 0 || lane == 3) ? ~0u : 0u;  // own A (0), K (3)
   const uint32_t corr = lane == 1 ? 0u : 1u;                // ~x = -x - 1
   fe a, b, m;
-  q.template perm<qp(0, 1, 2, 0)>(a, v);
-  q.template perm<QP_B1>(b, v);
+  if constexpr (FOLD == 2) {
+    q.template perm_lane3<QP_B1>(b, v);                 // lane 3: Y, else 0
+    q.template add_perm<qp(0, 1, 2, 0)>(m, v, b);        // X + Y on lane 3
+  } else if constexpr (FOLD == 1) {
+    q.template permc<QP_B1>(b, v);
 #pragma unroll
-  for (int i = 0; i < 10; i++) m.v[i] = a.v[i] + (b.v[i] & m3);  // X + Y on lane 3
-  fe_sq(m, m);                                                   // A, B, C', K
-  q.template perm<qp(2, 0, 0, 0)>(a, m);  // C', A, A, A
-  q.template perm<QP_B1>(b, m);           // B
+    for (int i = 0; i < 10; i++) b.v[i] &= m3;  // v_and_b32_dpp
+    q.template permc<qp(0, 1, 2, 0)>(a, v);
 #pragma unroll
-  for (int i = 0; i < 10; i++) {
-    // lane 0: F' = M + 2C', 1: S = A + B, 2: M = A - B, 3: E' = S - K (+2p)
-    const uint32_t u = (b.v[i] ^ n2) + CMTV_XOR_AND(m.v[i], n3, mo) + corr + fe_p2(i);
-    m.v[i] = (a.v[i] << sh) + u;
+    for (int i = 0; i < 10; i++) m.v[i] = a.v[i] + b.v[i];  // v_add_u32_dpp: X + Y on lane 3
+  } else {
+    q.template perm<qp(0, 1, 2, 0)>(a, v);
+    q.template perm<QP_B1>(b, v);
+#pragma unroll
+    for (int i = 0; i < 10; i++) m.v[i] = a.v[i] + (b.v[i] & m3);  // X + Y on lane 3
+  }
+  fe_sq(m, m);                                                     // A, B, C', K
+  if constexpr (FOLD == 2) {
+    fe src;
+#pragma unroll
+    for (int i = 0; i < 10; i++) src.v[i] = m.v[i] << s2;  // lane 2: 2C' (lane 0 reads it)
+    q.template xor_perm<QP_B1>(b, m, n2);                // B ^ n2
+#pragma unroll
+    for (int i = 0; i < 10; i++) b.v[i] += CMTV_XOR_AND(m.v[i], n3, mo) + (corr + fe_p2(i));
+    q.template add_perm<qp(2, 0, 0, 0)>(m, src, b);      // F', S, M, E' (+2p)
+  } else if constexpr (FOLD == 1) {
+    // lane 0 reads 2C' from lane 2, the others A from lane 0: lane 2's C'
+    // is doubled before the move (its own U does not use it)
+    fe src;
+#pragma unroll
+    for (int i = 0; i < 10; i++) src.v[i] = m.v[i] << s2;
+    q.template permc<QP_B1>(b, m);  // B
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+      const uint32_t t = b.v[i] ^ n2;  // v_xor_b32_dpp
+      b.v[i] = t + (CMTV_XOR_AND(m.v[i], n3, mo) + (corr + fe_p2(i)));
+    }
+    q.template permc<qp(2, 0, 0, 0)>(a, src);  // 2C', A, A, A
+#pragma unroll
+    for (int i = 0; i < 10; i++) m.v[i] = a.v[i] + b.v[i];  // v_add_u32_dpp
+  } else {
+    q.template perm<qp(2, 0, 0, 0)>(a, m);  // C', A, A, A
+    q.template perm<QP_B1>(b, m);           // B
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+      // lane 0: F' = M + 2C', 1: S = A + B, 2: M = A - B, 3: E' = S - K (+2p)
+      const uint32_t u = (b.v[i] ^ n2) + CMTV_XOR_AND(m.v[i], n3, mo) + corr + fe_p2(i);
+      m.v[i] = (a.v[i] << sh) + u;
+    }
   }
   fe_carry(m);
   q.template perm<qp(3, 2, 0, 1)>(a, m);  // E', M, F', S
@@ -114,7 +163,7 @@ CMTV_HD void q_dbl(const Q& q, fe& v) {
 //            U stays inside the multiplier bounds); the products form the
 //            cycle E-F-G-H-E, so lane c multiplies its own U by one move
 //            {F, H, G, E}: {EF, GH, FG, HE}[c] = (X3, Y3, Z3, T3).
-template <class Q>
+template <int FOLD = kDppFold, class Q>
 CMTV_HD void q_add(const Q& q, fe& v, const fe& c) {
   const int lane = q.lane();
   // per-lane masks (loop-invariant); ~x + 1 = -x supplies the negations
@@ -131,13 +180,30 @@ CMTV_HD void q_add(const Q& q, fe& v, const fe& c) {
   }
   fe t;
   fe_mul(t, p, c);  // -A, B, D, C
-  q.template perm<qp(1, 2, 2, 1)>(x, t);  // B, D, D, B
-  q.template perm<qp(0, 3, 3, 0)>(y, t);  // -A, C, C, -A
+  if constexpr (FOLD == 2) {
+    q.template xor_perm<qp(0, 3, 3, 0)>(y, t, m23);  // -A, C, C, -A (negated on lanes 2, 3)
 #pragma unroll
-  for (int i = 0; i < 10; i++) {
-    // E = B - A, G = D + C; F = D - C, H = B + A (lanes 2, 3: + 2p)
-    const uint32_t k = lane >= 2 ? fe_p2(i) + 1 : 0u;
-    p.v[i] = x.v[i] + (y.v[i] ^ m23) + k;
+    for (int i = 0; i < 10; i++) y.v[i] += lane >= 2 ? fe_p2(i) + 1 : 0u;
+    q.template add_perm<qp(1, 2, 2, 1)>(p, t, y);     // E, G, F, H
+  } else if constexpr (FOLD == 1) {
+    q.template permc<qp(0, 3, 3, 0)>(y, t);  // -A, C, C, -A
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+      const uint32_t k = lane >= 2 ? fe_p2(i) + 1 : 0u;
+      y.v[i] = (y.v[i] ^ m23) + k;  // v_xor_b32_dpp
+    }
+    q.template permc<qp(1, 2, 2, 1)>(x, t);  // B, D, D, B
+#pragma unroll
+    for (int i = 0; i < 10; i++) p.v[i] = x.v[i] + y.v[i];  // v_add_u32_dpp
+  } else {
+    q.template perm<qp(1, 2, 2, 1)>(x, t);  // B, D, D, B
+    q.template perm<qp(0, 3, 3, 0)>(y, t);  // -A, C, C, -A
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+      // E = B - A, G = D + C; F = D - C, H = B + A (lanes 2, 3: + 2p)
+      const uint32_t k = lane >= 2 ? fe_p2(i) + 1 : 0u;
+      p.v[i] = x.v[i] + (y.v[i] ^ m23) + k;
+    }
   }
   q.template perm<qp(2, 3, 1, 0)>(x, p);  // F, H, G, E
   fe_mul(v, p, x);

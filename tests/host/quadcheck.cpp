@@ -55,6 +55,26 @@ struct HostQuad {
     o = r;
   }
   template <int PAT>
+  void add_perm(fe& o, const fe& src, const fe& b) const {
+    fe t;
+    perm<PAT>(t, src);
+    for (int i = 0; i < 10; i++) o.v[i] = t.v[i] + b.v[i];
+  }
+  template <int PAT>
+  void xor_perm(fe& o, const fe& src, uint32_t k) const {
+    perm<PAT>(o, src);
+    for (int i = 0; i < 10; i++) o.v[i] ^= k;
+  }
+  template <int PAT>
+  void perm_lane3(fe& o, const fe& src) const {
+    perm<PAT>(o, src);
+    for (int i = 0; i < 10; i++) o.v[i] = lane() == 3 ? o.v[i] : 0u;
+  }
+  template <int PAT>
+  void permc(fe& o, const fe& v) const {
+    perm<PAT>(o, v);
+  }
+  template <int PAT>
   uint32_t perm32(uint32_t x) const {
     fe t, o;
     fe_0(t);
@@ -79,6 +99,26 @@ struct HostOct {
     const fe r = ex->slot[(ln & 4) + ((PAT >> (2 * (ln & 3))) & 3)];
     ex->bar.arrive_and_wait();
     o = r;
+  }
+  template <int PAT>
+  void add_perm(fe& o, const fe& src, const fe& b) const {
+    fe t;
+    perm<PAT>(t, src);
+    for (int i = 0; i < 10; i++) o.v[i] = t.v[i] + b.v[i];
+  }
+  template <int PAT>
+  void xor_perm(fe& o, const fe& src, uint32_t k) const {
+    perm<PAT>(o, src);
+    for (int i = 0; i < 10; i++) o.v[i] ^= k;
+  }
+  template <int PAT>
+  void perm_lane3(fe& o, const fe& src) const {
+    perm<PAT>(o, src);
+    for (int i = 0; i < 10; i++) o.v[i] = lane() == 3 ? o.v[i] : 0u;
+  }
+  template <int PAT>
+  void permc(fe& o, const fe& v) const {
+    perm<PAT>(o, v);
   }
   template <int PAT>
   uint32_t perm32(uint32_t x) const {

@@ -15,6 +15,8 @@ import torch
 from cometbft_amd import Context, pack_messages
 
 REPS = int(os.environ.get("PMC_REPS", "3"))
+# PMC_ONLY=name,name,... runs only those batches (e.g. keyed_lane1m,lane262k)
+ONLY = set(filter(None, os.environ.get("PMC_ONLY", "").split(",")))
 dev = torch.device("cuda:0")
 ctx = Context(device=0)
 rng = np.random.default_rng(7)
@@ -37,6 +39,8 @@ def batch(n):
 
 
 def run(name, c, b, keyed=None):
+    if ONLY and name not in ONLY:
+        return
     s = torch.cuda.current_stream().cuda_stream
     for _ in range(REPS):
         b["valid"].zero_()
@@ -69,17 +73,33 @@ def lane_ctx():
     return env_ctx(CMTV_QUAD_MAX=0, CMTV_KEYED_QUAD_MAX=0)
 
 
-b150, b8k, b10k = batch(150), batch(8192), batch(10000)
-run("oct_split150", ctx, b150)
-run("quad_split8192", ctx, b8k)
-run("quad_split10k", ctx, b10k)
-run("oct150", env_ctx(CMTV_OCT_SPLIT_MAX=0), b150)
-run("quad10k", env_ctx(CMTV_QUAD_SPLIT_MAX=0), b10k)
+def want(*names):
+    return not ONLY or any(n in ONLY for n in names)
+
+
+if want("oct_split150", "quad_split8192", "quad_split10k", "oct150", "quad10k", "keyed_quad10k"):
+    b150, b8k, b10k = batch(150), batch(8192), batch(10000)
+    run("oct_split150", ctx, b150)
+    run("quad_split8192", ctx, b8k)
+    run("quad_split10k", ctx, b10k)
+    run("oct150", env_ctx(CMTV_OCT_SPLIT_MAX=0), b150)
+    run("quad10k", env_ctx(CMTV_QUAD_SPLIT_MAX=0), b10k)
 lctx = lane_ctx()
-b100k = batch(100_000)
-run("lane100k", lctx, b100k)
-ks = ctx.register_keys(pks)
-run("keyed_quad10k", ctx, b10k, keyed=ks)
-lks = lctx.register_keys(pks)
-b1m = batch(1_000_000)
-run("keyed_lane1m", lctx, b1m, keyed=lks)
+if want("lane100k"):
+    b100k = batch(100_000)
+    run("lane100k", lctx, b100k)
+    del b100k
+if want("keyed_quad10k"):
+    ks = ctx.register_keys(pks)
+    run("keyed_quad10k", ctx, b10k, keyed=ks)
+# configs[2]'s launch shape: 262,144 signatures per launch (kChunk), the 150
+# keys cycling as in consecutive 150-validator commits
+if want("lane262k", "keyed_lane262k", "keyed_lane1m"):
+    b262k = batch(262_144)
+    run("lane262k", lctx, b262k)
+    lks = lctx.register_keys(pks)
+    run("keyed_lane262k", lctx, b262k, keyed=lks)
+    if want("keyed_lane1m"):
+        del b262k
+        b1m = batch(1_000_000)
+        run("keyed_lane1m", lctx, b1m, keyed=lks)

@@ -34,6 +34,7 @@ COMMIT_ERR_BLOCK_ID = 3
 COMMIT_ERR_WRONG_SIGNATURE = 4
 COMMIT_ERR_NOT_ENOUGH_POWER = 5
 COMMIT_ERR_DOUBLE_VOTE = 6
+CMTV_KEYS_WIDE = 1
 COMMIT_ERR_TRUST_LEVEL = 7
 COMMIT_PANIC_BAD_PUBKEY = 8
 COMMIT_PANIC_UNKNOWN_FLAG = 9
@@ -43,7 +44,7 @@ EXPORTS = (
     "cmtv_open", "cmtv_open_devices", "cmtv_device_count", "cmtv_device_ordinal", "cmtv_device_stream", "cmtv_sync",
     "cmtv_verify_ed25519_sharded_device", "cmtv_verify_ed25519_indexed_sharded_device", "cmtv_verify_ed25519_multi_device", "cmtv_close", "cmtv_strerror", "cmtv_abi_version", "cmtv_stats_get", "cmtv_device_stats_get", "cmtv_stream",
     "cmtv_verify_ed25519", "cmtv_verify_ed25519_device", "cmtv_verify_sr25519", "cmtv_verify_sr25519_device",
-    "cmtv_register_keys", "cmtv_keyset_free", "cmtv_keyset_len", "cmtv_verify_ed25519_indexed",
+    "cmtv_register_keys", "cmtv_register_keys_ex", "cmtv_keyset_free", "cmtv_keyset_len", "cmtv_verify_ed25519_indexed",
     "cmtv_verify_ed25519_indexed_device",
     "cmtv_batch_new", "cmtv_batch_add", "cmtv_batch_len", "cmtv_batch_verify", "cmtv_batch_reset",
     "cmtv_batch_free", "cmtv_verify_commit", "cmtv_verify_commits", "cmtv_verdict_cache", "cmtv_keyset_cache", "cmtv_vote_sign_bytes", "cmtv_pubkeys_ed25519", "cmtv_sign_ed25519",
@@ -161,6 +162,8 @@ def lib() -> ctypes.CDLL:
     L.cmtv_verify_sr25519_device.restype = ctypes.c_int
     L.cmtv_register_keys.argtypes = [vp, sz, _u8p, ctypes.POINTER(vp)]
     L.cmtv_register_keys.restype = ctypes.c_int
+    L.cmtv_register_keys_ex.argtypes = [vp, sz, _u8p, ctypes.c_uint32, ctypes.POINTER(vp)]
+    L.cmtv_register_keys_ex.restype = ctypes.c_int
     L.cmtv_keyset_free.argtypes = [vp]
     L.cmtv_keyset_free.restype = None
     L.cmtv_keyset_len.argtypes = [vp]

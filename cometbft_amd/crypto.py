@@ -211,11 +211,13 @@ class Context:
         N.check(rc, "cmtv_verify_sr25519_device")
 
     # -------------------------------------------------------------- registered keys
-    def register_keys(self, pk: np.ndarray) -> "KeySet":
+    def register_keys(self, pk: np.ndarray, wide: bool = False) -> "KeySet":
         """Decode n 32-byte keys once and build their combs on the device
         (cmtv_register_keys); verify_indexed then needs no decompression of
-        A and no doublings. 512 KiB of HBM per key."""
-        return KeySet(self, pk)
+        A and no doublings. 512 KiB of HBM per key; wide=True also builds the
+        radix-2^16 combs (CMTV_KEYS_WIDE, 64 MiB per key) that halve the
+        additions of large batches."""
+        return KeySet(self, pk, wide)
 
     def verify_indexed(self, keys: "KeySet", key_idx: np.ndarray, sig: np.ndarray, msg: np.ndarray,
                        msg_off: np.ndarray, mode: int | None = None, bitmap: bool = False):
@@ -277,10 +279,13 @@ class Context:
 class KeySet:
     """Registered public keys (cmtv_keyset): per-key combs resident in HBM."""
 
-    def __init__(self, ctx: Context, pk: np.ndarray):
+    def __init__(self, ctx: Context, pk: np.ndarray, wide: bool = False):
         pk = np.ascontiguousarray(pk, dtype=np.uint8).reshape(-1, 32)
         h = ctypes.c_void_p()
-        N.check(N.lib().cmtv_register_keys(ctx.handle, pk.shape[0], _u8(pk), ctypes.byref(h)), "cmtv_register_keys")
+        flags = N.CMTV_KEYS_WIDE if wide else 0
+        N.check(N.lib().cmtv_register_keys_ex(ctx.handle, pk.shape[0], _u8(pk), flags, ctypes.byref(h)),
+                "cmtv_register_keys_ex")
+        self.wide = wide
         self._h = h
         self.ctx = ctx  # keeps the context alive while the key set is
         self.pk = pk.copy()

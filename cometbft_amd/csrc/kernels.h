@@ -53,7 +53,18 @@ hipError_t launch_comb_build(uint32_t n_keys, const void* keys_pk, uint8_t* keys
 hipError_t launch_verify_keyed(uint32_t mode, uint32_t n, uint32_t n_keys, const void* key_idx, const void* sig,
                                const void* msg, const void* off, const uint32_t* keys_pk, const uint8_t* keys_ok,
                                const uint32_t* ktabs, const uint32_t* bcomb, void* valid, void* bitmap,
-                               bool quad, bool split, uint32_t k_wait, uint32_t* diag, hipStream_t s);
+                               bool quad, bool split, uint32_t k_wait, uint32_t* diag, uint32_t batch_kb,
+                               uint32_t* scr, const uint32_t* wtabs, const uint32_t* btab, hipStream_t s);
+// Wide (radix-2^16) combs of n_keys keys (keyed.h): bases = n_keys x 16 x 40
+// words, scratch = n_keys x kWideScratchWordsPerKey words.
+constexpr size_t kWideTableWords = (size_t)16 * 32768 * 32;  // 64 MiB per key
+constexpr size_t kWideScratchWordsPerKey = (size_t)16 * (32768 / 64) * 64 * 10;
+constexpr size_t kWideBaseWordsPerKey = 16 * 40;
+hipError_t launch_wide_build(uint32_t n_keys, const void* keys_pk, uint32_t* tabs, uint32_t* bases,
+                             uint32_t* scratch, hipStream_t s);
+// k_verify_keyed_go_batch: signatures per lane, and its scratch per lane
+// (kb x 40 words: R'.X, R'.Y, Z and the running product of the Z's)
+constexpr uint32_t kKeyedBatchScratchWordsPerSig = 40;
 hipError_t launch_verify_sr25519(uint32_t n, const void* pk, const void* sig, const void* msg, const void* off,
                                  const uint32_t* btab, uint32_t* atab, const uint16_t* prog, int nops, void* valid,
                                  void* bitmap, uint32_t kflags, hipStream_t s);

@@ -35,6 +35,12 @@
 namespace {
 
 constexpr uint32_t kChunk = 1u << 18;  // signatures per launch (A-table scratch = kChunk * 1280 B)
+// registered-key lane launches in GO_STDLIB mode take up to this many
+// signatures, KB per lane (k_verify_keyed_go_batch: one field inversion per
+// KB signatures; KB = 8 keeps 2,048 waves = two per SIMD); scratch 160 B per
+// signature, in the lane kernels' scratch buffer
+constexpr uint32_t kKeyedBatchChunk = 1u << 20;
+constexpr uint32_t kKeyedBatchMinWaves = 2048;
 // crossover between the quad (4 lanes / signature) and lane (1 lane / signature)
 // kernels; measured on MI355X, overridable with CMTV_QUAD_MAX
 constexpr size_t kQuadMaxDefault = 40000;
@@ -378,6 +384,8 @@ struct cmtv_ctx {
   // polls of the keyed split kernel's quads for the hash helper's k before
   // they hash themselves (CMTV_FORCE_K_LATE=1: 0, every quad wave hashes)
   uint32_t keyed_wait = cmtv::kKeyedWaitDefault;
+  // GO_STDLIB keyed lane launches batch the final inversion (CMTV_KEYED_BATCH=0: off)
+  bool keyed_batch = true;
   // devices (indices into devs) that take host batches, in shard order; the
   // RCCL communicator (when rccl) spans exactly these, rank = position
   std::vector<size_t> live;
@@ -390,6 +398,7 @@ struct cmtv_keyset {
     uint32_t* d_pk = nullptr;   // n x 8 words, the keys' original bytes
     uint8_t* d_ok = nullptr;    // n decode flags
     uint32_t* d_tab = nullptr;  // n x kCombWords
+    uint32_t* d_wide = nullptr; // n x kWideTableWords (CMTV_KEYS_WIDE), else null
   };
   cmtv_ctx* ctx = nullptr;
   size_t n = 0;
@@ -423,6 +432,27 @@ static bool fault_hit(cmtv_ctx* ctx) {
     return true;
   }
   return false;
+}
+
+// The lane kernels' scratch (the generic kernel's A tables, the batched keyed
+// kernel's R' and Z products) is shared by every launch on a device, whatever
+// stream it is enqueued on: a launch waits for the previous user (atab_done),
+// growing it first waits for that user to finish.
+static hipError_t acquire_scratch(CmtvDev& D, size_t bytes, hipStream_t s) {
+  hipError_t e;
+  if (bytes > D.d_atab.cap) {
+    // growing frees the old scratch: every earlier user must be done
+    if (D.atab_used && (e = hipEventSynchronize(D.atab_done)) != hipSuccess) return e;
+    if ((e = D.d_atab.ensure(bytes)) != hipSuccess) return e;
+  }
+  if (D.atab_used && (e = hipStreamWaitEvent(s, D.atab_done, 0)) != hipSuccess) return e;
+  return hipSuccess;
+}
+
+static hipError_t release_scratch(CmtvDev& D, hipStream_t s) {
+  const hipError_t e = hipEventRecord(D.atab_done, s);
+  if (e == hipSuccess) D.atab_used = true;
+  return e;
 }
 
 // Enqueue verification of n signatures whose inputs are in device memory of
@@ -464,13 +494,8 @@ static int enqueue_verify(cmtv_ctx* ctx, CmtvDev& D, size_t n, const uint8_t* d_
   if (!quad) {
     const size_t lanes = std::min<size_t>(n, ctx->lane_chunk);
     const size_t lanes_padded = (lanes + 63) / 64 * 64;
-    if (lanes_padded * kAtabWordsPerLane * sizeof(uint32_t) > D.d_atab.cap) {
-      // growing frees the old scratch: every earlier user must be done
-      if (D.atab_used && (e = hipEventSynchronize(D.atab_done)) != hipSuccess) return hip_fail(e);
-      if ((e = D.d_atab.ensure(lanes_padded * kAtabWordsPerLane * sizeof(uint32_t))) != hipSuccess)
-        return hip_fail(e);
-    }
-    if (D.atab_used && (e = hipStreamWaitEvent(s, D.atab_done, 0)) != hipSuccess) return hip_fail(e);
+    if ((e = acquire_scratch(D, lanes_padded * kAtabWordsPerLane * sizeof(uint32_t), s)) != hipSuccess)
+      return hip_fail(e);
   }
   D.timing.harvest(ctx->stats, D.device_ms, false);
   Timing::Pair tp;
@@ -493,10 +518,7 @@ static int enqueue_verify(cmtv_ctx* ctx, CmtvDev& D, size_t n, const uint8_t* d_
     ctx->stats.kernel_launches++;
     D.launches++;
   }
-  if (!quad) {
-    if ((e = hipEventRecord(D.atab_done, s)) != hipSuccess) return hip_fail(e);
-    D.atab_used = true;
-  }
+  if (!quad && (e = release_scratch(D, s)) != hipSuccess) return hip_fail(e);
   if ((e = D.timing.end(tp, s)) != hipSuccess) return hip_fail(e);
   ctx->stats.calls++;
   ctx->stats.signatures += n;
@@ -539,16 +561,35 @@ static int enqueue_verify_keyed(cmtv_ctx* ctx, CmtvDev& D, const cmtv_keyset::Pe
                                 hipStream_t s) {
   if (n == 0) return CMTV_OK;
   if (fault_hit(ctx) || D.inject_fault) return CMTV_EHIP;
+  const bool quad = n <= ctx->keyed_quad_max;
+  // GO_STDLIB lane launches: KB signatures per lane while that still gives
+  // two waves per SIMD (k_verify_keyed_go_batch)
+  const bool batch = !quad && mode != CMTV_MODE_ZIP215 && ctx->keyed_batch;
+  const size_t chunk = batch ? kKeyedBatchChunk : kChunk;
+  auto kb_for = [&](size_t cn) -> uint32_t {  // 4 or 8 (the instantiated forms), else 1
+    uint32_t kb = 1;
+    while (kb < 8 && cn >= (size_t)kKeyedBatchMinWaves * 64 * (kb * 2)) kb *= 2;
+    return batch && kb >= 4 ? kb : 1;
+  };
+  hipError_t e;
+  const uint32_t kb0 = kb_for(std::min(chunk, n));
+  if (kb0 > 1) {
+    const size_t lanes = (std::min(chunk, n) + 64 * kb0 - 1) / (64 * kb0) * 64;
+    if ((e = acquire_scratch(D, lanes * kb0 * kKeyedBatchScratchWordsPerSig * sizeof(uint32_t), s)) != hipSuccess)
+      return hip_fail(e);
+  }
   D.timing.harvest(ctx->stats, D.device_ms, false);
   Timing::Pair tp;
-  hipError_t e;
   if ((e = D.timing.begin(tp, s)) != hipSuccess) return hip_fail(e);
-  for (size_t c = 0; c < n; c += kChunk) {
-    const uint32_t cn = (uint32_t)std::min<size_t>(kChunk, n - c);
+  for (size_t c = 0; c < n; c += chunk) {
+    const uint32_t cn = (uint32_t)std::min<size_t>(chunk, n - c);
+    // a chunk never needs more scratch than the first (kb and lanes shrink together)
+    const uint32_t kb = kb0 > 1 ? kb_for(cn) : 1;
     e = launch_verify_keyed(mode, cn, (uint32_t)n_keys, d_idx + c, d_sig + 64 * c, d_msg, d_off + c, K.d_pk, K.d_ok,
                             K.d_tab, D.d_bcomb, d_valid ? d_valid + c : nullptr,
-                            d_bitmap ? d_bitmap + c / 64 : nullptr, n <= ctx->keyed_quad_max,
-                            n <= ctx->quad_split_max, ctx->keyed_wait, D.d_diag, s);
+                            d_bitmap ? d_bitmap + c / 64 : nullptr, quad, n <= ctx->quad_split_max,
+                            ctx->keyed_wait, D.d_diag, kb, static_cast<uint32_t*>(D.d_atab.p),
+                            quad ? nullptr : K.d_wide, D.d_btab, s);
     if (e != hipSuccess) {
       D.timing.abandon(tp);
       return hip_fail(e);
@@ -557,6 +598,7 @@ static int enqueue_verify_keyed(cmtv_ctx* ctx, CmtvDev& D, const cmtv_keyset::Pe
     ctx->stats.keyed_launches++;
     D.launches++;
   }
+  if (kb0 > 1 && (e = release_scratch(D, s)) != hipSuccess) return hip_fail(e);
   if ((e = D.timing.end(tp, s)) != hipSuccess) return hip_fail(e);
   ctx->stats.calls++;
   ctx->stats.signatures += n;
@@ -1058,6 +1100,7 @@ static void read_env(cmtv_ctx* ctx) {
   if (const char* nf = std::getenv("CMTV_NO_SB_FUSE")) ctx->sb_fuse = nf[0] != '1';
   if (const char* nz = std::getenv("CMTV_NO_ZC_IN")) ctx->zc_in = nz[0] != '1';
   if (const char* kl = std::getenv("CMTV_FORCE_K_LATE")) ctx->keyed_wait = kl[0] == '1' ? 0u : kKeyedWaitDefault;
+  if (const char* kb = std::getenv("CMTV_KEYED_BATCH")) ctx->keyed_batch = kb[0] != '0';
   ctx->force_rccl = std::getenv("CMTV_FORCE_RCCL") != nullptr;
   ctx->no_rccl = std::getenv("CMTV_NO_RCCL") != nullptr;
 }
@@ -1460,14 +1503,20 @@ int cmtv_verify_ed25519_indexed_sharded_device(cmtv_ctx* ctx, const cmtv_keyset*
                         words_per_shard);
 }
 
-int cmtv_register_keys(cmtv_ctx* ctx, size_t n_keys, const uint8_t* pk, cmtv_keyset** out) {
+int cmtv_register_keys_ex(cmtv_ctx* ctx, size_t n_keys, const uint8_t* pk, uint32_t flags, cmtv_keyset** out) {
   if (!out) return CMTV_EINVAL;
   *out = nullptr;
-  // 512 KiB of comb per key; 2^20 keys would already be 512 GiB
-  if (!ctx || n_keys == 0 || n_keys > (1u << 20) || !pk) return CMTV_EINVAL;
+  // 512 KiB of comb per key; 2^20 keys would already be 512 GiB (wide: 64 MiB
+  // per key, 4096 keys = 256 GiB)
+  if (!ctx || n_keys == 0 || n_keys > (1u << 20) || !pk || (flags & ~(uint32_t)CMTV_KEYS_WIDE)) return CMTV_EINVAL;
+  if ((flags & CMTV_KEYS_WIDE) && n_keys > 4096) return CMTV_EINVAL;
   std::unique_lock<std::mutex> lk;
   if (ctx_lock(ctx, lk) != CMTV_OK) return CMTV_ENODEV;
-  return cmtv::register_keys_locked(ctx, n_keys, pk, out);
+  return cmtv::register_keys_locked(ctx, n_keys, pk, out, flags);
+}
+
+int cmtv_register_keys(cmtv_ctx* ctx, size_t n_keys, const uint8_t* pk, cmtv_keyset** out) {
+  return cmtv_register_keys_ex(ctx, n_keys, pk, 0, out);
 }
 
 int cmtv_keyset_cache(cmtv_ctx* ctx, size_t max_sets) {
@@ -1491,7 +1540,28 @@ int cmtv_keyset_cache(cmtv_ctx* ctx, size_t max_sets) {
 
 namespace cmtv {
 
-int register_keys_locked(cmtv_ctx* ctx, size_t n_keys, const uint8_t* pk, cmtv_keyset** out) {
+// keys per wide-comb build launch (prefix-product scratch = 20 MiB per key)
+constexpr uint32_t kWideKeyChunk = 16;
+
+// The wide combs of a key set on device D (current): 64 MiB per key.
+static hipError_t build_wide(CmtvDev& D, cmtv_keyset::PerDev& K, size_t n_keys) {
+  DevBuf scratch, bases;
+  const size_t chunk = std::min<size_t>(n_keys, kWideKeyChunk);
+  hipError_t e = hipMalloc(&K.d_wide, n_keys * kWideTableWords * sizeof(uint32_t));
+  if (e == hipSuccess) e = scratch.ensure(chunk * kWideScratchWordsPerKey * sizeof(uint32_t));
+  if (e == hipSuccess) e = bases.ensure(chunk * kWideBaseWordsPerKey * sizeof(uint32_t));
+  for (size_t c = 0; e == hipSuccess && c < n_keys; c += kWideKeyChunk) {
+    const uint32_t cn = (uint32_t)std::min<size_t>(kWideKeyChunk, n_keys - c);
+    e = launch_wide_build(cn, K.d_pk + 8 * c, K.d_wide + c * kWideTableWords, static_cast<uint32_t*>(bases.p),
+                          static_cast<uint32_t*>(scratch.p), D.stream);
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(D.stream);
+  scratch.release();
+  bases.release();
+  return e;
+}
+
+int register_keys_locked(cmtv_ctx* ctx, size_t n_keys, const uint8_t* pk, cmtv_keyset** out, uint32_t flags) {
   auto* ks = new (std::nothrow) cmtv_keyset();
   if (!ks) return CMTV_ENOMEM;
   ks->ctx = ctx;
@@ -1523,6 +1593,7 @@ int register_keys_locked(cmtv_ctx* ctx, size_t n_keys, const uint8_t* pk, cmtv_k
     }
     if (e == hipSuccess) e = hipStreamSynchronize(D.stream);
     scratch.release();
+    if (e == hipSuccess && (flags & CMTV_KEYS_WIDE)) e = build_wide(D, K, n_keys);
     if (e != hipSuccess) {
       cmtv_keyset_free(ks);
       (void)hipSetDevice(ctx->devs[0].ordinal);
@@ -1540,7 +1611,7 @@ const cmtv_keyset* keyset_for_locked(cmtv_ctx* ctx, const uint8_t* pk32, size_t 
   for (auto& e : ctx->keysets)
     if (e.first == key) return e.second;
   cmtv_keyset* ks = nullptr;
-  if (register_keys_locked(ctx, n_keys, pk32, &ks) != CMTV_OK) return nullptr;  // generic path instead
+  if (register_keys_locked(ctx, n_keys, pk32, &ks, 0) != CMTV_OK) return nullptr;  // generic path instead
   if (ctx->keysets.size() >= ctx->keyset_cap) {
     cmtv_keyset_free(ctx->keysets.front().second);
     ctx->keysets.erase(ctx->keysets.begin());
@@ -1564,6 +1635,7 @@ void cmtv_keyset_free(cmtv_keyset* ks) {
     if (K.d_pk) (void)hipFree(K.d_pk);
     if (K.d_ok) (void)hipFree(K.d_ok);
     if (K.d_tab) (void)hipFree(K.d_tab);
+    if (K.d_wide) (void)hipFree(K.d_wide);
   }
   if (!ks->ctx->devs.empty()) (void)hipSetDevice(ks->ctx->devs[0].ordinal);
   delete ks;

@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define CMTV_ABI_VERSION 6
+#define CMTV_ABI_VERSION 7
 
 enum {
   CMTV_OK = 0,
@@ -271,6 +271,14 @@ int cmtv_verify_sr25519_device(cmtv_ctx* ctx, size_t n, const void* d_pk, const 
  * key's original bytes are what SHA-512(R || A || M) hashes. Blocking. The
  * key set belongs to `ctx`: free it before cmtv_close(ctx). */
 int cmtv_register_keys(cmtv_ctx* ctx, size_t n_keys, const uint8_t* pk, cmtv_keyset** out);
+
+/* cmtv_register_keys with flags. CMTV_KEYS_WIDE also builds each key's
+ * radix-2^16 comb (e+1)*2^(16j)*(-A) (j < 16, e < 32768; 64 MiB of HBM per
+ * key, n_keys <= 4096), which the one-signature-per-lane kernels of large
+ * indexed batches then use: 32 table additions per signature instead of 64
+ * (bulk replay of one validator set, BASELINE configs[2]). Same verdicts. */
+enum { CMTV_KEYS_WIDE = 1 };
+int cmtv_register_keys_ex(cmtv_ctx* ctx, size_t n_keys, const uint8_t* pk, uint32_t flags, cmtv_keyset** out);
 void cmtv_keyset_free(cmtv_keyset* ks);
 size_t cmtv_keyset_len(const cmtv_keyset* ks);
 

@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_strerror():
     lib = N.lib()
-    assert lib.cmtv_abi_version() == 6
+    assert lib.cmtv_abi_version() == 7
     for code in (N.CMTV_OK, N.CMTV_EINVAL, N.CMTV_ENODEV, N.CMTV_ENOMEM, N.CMTV_EHIP, N.CMTV_ERCCL, N.CMTV_ECOMMIT):
         assert lib.cmtv_strerror(code)
 
@@ -103,6 +103,7 @@ def test_keyset_entry_points_reject_bad_arguments_without_gpu():
     ks = ctypes.c_void_p()
     assert lib.cmtv_register_keys(None, 1, None, ctypes.byref(ks)) == N.CMTV_EINVAL
     assert lib.cmtv_register_keys(None, 1, None, None) == N.CMTV_EINVAL
+    assert lib.cmtv_register_keys_ex(None, 1, None, N.CMTV_KEYS_WIDE, ctypes.byref(ks)) == N.CMTV_EINVAL
     assert lib.cmtv_keyset_len(None) == 0
     lib.cmtv_keyset_free(None)
     assert lib.cmtv_verify_ed25519_indexed(None, None, 1, None, None, None, None, 0, None, None) == N.CMTV_EINVAL

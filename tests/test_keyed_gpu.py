@@ -108,3 +108,62 @@ def test_keyset_belongs_to_its_context(gpu_ctx, gpu_ctx_lane):
     with pytest.raises(N.CmtvError):
         gpu_ctx_lane.verify_indexed(ks, kidx, sig, m, off)
     ks.free()
+
+
+@pytest.mark.parametrize("n", [530_000, 1_100_003])
+def test_keyed_go_batch_inversion(gpu_ctx_lane, corpus, n):
+    """k_verify_keyed_go_batch (configs[2]'s GO_STDLIB lane path): KB = 4 / 8
+    signatures per lane share one field inversion (Montgomery's trick). n =
+    530,000 runs the KB = 4 form; 1,100,003 one 2^20 chunk at KB = 8 plus a
+    ragged 51,427-signature tail on the plain kernel. The key set mixes 150
+    honest keys with the corpus' off-curve keys (their combs are garbage, Z
+    may vanish: their signatures must fail without spoiling the lane's
+    others) and non-canonical / small-order keys; 1% of the signatures carry
+    a flipped bit. Verdicts must equal the oracle's and the unbatched
+    kernel's (CMTV_KEYED_BATCH=0) bit for bit."""
+    import os
+
+    from cometbft_amd import Context
+
+    rng = np.random.default_rng(n)
+    seeds = rng.integers(0, 256, (150, 32), dtype=np.uint8)
+    honest = coracle.pubkeys_from_seeds(seeds)
+    cats = corpus["cats"]
+    odd = [i for i, c in enumerate(cats) if c in ("offcurve_A", "noncanonical_A", "small_order_A")][:24]
+    pk = np.concatenate([honest, corpus["pk"][odd]])
+    n_h = honest.shape[0]
+    kidx = (np.arange(n) % n_h).astype(np.uint32)
+    # every 97th signature by one of the corpus keys (with that vector's sig and msg)
+    spots = np.arange(5, n, 97)
+    m1 = np.frombuffer(np.random.default_rng(1).bytes(116), np.uint8)
+    m = np.tile(m1, n).reshape(n, 116)
+    m[:, :8] = np.arange(n, dtype=np.uint64).view(np.uint8).reshape(n, 8)  # distinct messages
+    m = m.reshape(-1)
+    off = (np.arange(n + 1, dtype=np.uint64) * 116).astype(np.uint32)
+    sig = coracle.sign_batch(seeds, m, off, key_idx=kidx, nthreads=16).copy()
+    for j, sp in enumerate(spots[: 4 * len(odd)]):
+        t = odd[j % len(odd)]
+        kidx[sp] = n_h + (j % len(odd))
+        sig[sp] = corpus["sig"][t]
+    flips = rng.choice(n, n // 100, replace=False)
+    sig[flips, rng.integers(0, 64, flips.size)] ^= (1 << rng.integers(0, 8, flips.size)).astype(np.uint8)
+    exp = coracle.verify_batch(pk[kidx], sig, m, off, MODE_GO_STDLIB, nthreads=16)
+    assert 0 < exp.sum() < n
+    ks = gpu_ctx_lane.register_keys(pk)
+    got = gpu_ctx_lane.verify_indexed(ks, kidx, sig, m, off, MODE_GO_STDLIB)
+    bad = np.nonzero(got != exp)[0]
+    assert bad.size == 0, (bad[:10], kidx[bad[:10]])
+    ks.free()
+    old = {k: os.environ.get(k) for k in ("CMTV_QUAD_MAX", "CMTV_KEYED_QUAD_MAX", "CMTV_KEYED_BATCH")}
+    os.environ.update({"CMTV_QUAD_MAX": "0", "CMTV_KEYED_QUAD_MAX": "0", "CMTV_KEYED_BATCH": "0"})
+    try:
+        plain = Context(device=0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+    ks2 = plain.register_keys(pk)
+    assert np.array_equal(plain.verify_indexed(ks2, kidx, sig, m, off, MODE_GO_STDLIB), got)
+    ks2.free()

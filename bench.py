@@ -61,6 +61,10 @@ MACS_PER_VERIFY = 300_000          # 3,000 field mults x
 # registered-key verification (keyed.h): 64 comb additions (7 field mults each
 # in the one-lane form) + decode R (~265) + final check (~8) = 721 field mults
 MACS_PER_KEYED_VERIFY = 72_100
+# the same over the radix-2^16 key combs (CMTV_KEYS_WIDE) in GO_STDLIB with 8
+# signatures per lane sharing one inversion (k_verify_keyed_go_batch<8, true>):
+# 32 additions x 7 + 265 / 8 + 3 (batch products) + 2 (x, y) = 262 field mults
+MACS_PER_KEYED_WIDE_GO_VERIFY = 26_200
 INT_MAC_PEAK_T = 33.0              # measured v_mad_u64_u32 lane-ops/s, 1e12 (profiles/r01_int_rates.txt)
 
 
@@ -559,7 +563,10 @@ def c3_line(ctx, n_dev, mode, steps=3, n_heights=100_000, n_vals=150):
     total = n_heights * n_vals
     t_gen = time.perf_counter()
     sv = TU.make_validator_set(ctx, n_vals)
-    ks = ctx.register_keys(sv.pubkeys)
+    t_reg = time.perf_counter()
+    ks = ctx.register_keys(sv.pubkeys, wide=True)  # 64 MiB of radix-2^16 comb per key and device
+    t_reg = time.perf_counter() - t_reg
+    ks256 = ctx.register_keys(sv.pubkeys)
     rng = np.random.default_rng(42)
     flip = rng.choice(total, total // 100, replace=False)
     bit = rng.integers(0, 512, flip.size)
@@ -589,14 +596,10 @@ def c3_line(ctx, n_dev, mode, steps=3, n_heights=100_000, n_vals=150):
         s["bm"] = torch.zeros(n_dev * W, dtype=torch.int64, device=s["dev"])
     ns = [s["n"] for s in shards]
 
-    def keyed():
+    def keyed(keys):
         ctx.verify_sharded_device(ns, [s["idx"].data_ptr() for s in shards], [s["sig"].data_ptr() for s in shards],
                                   [s["m"].data_ptr() for s in shards], [s["off"].data_ptr() for s in shards], mode,
-                                  [s["bm"].data_ptr() for s in shards], keys=ks)
-
-    el, kms_keyed = timed_steps(ctx, keyed, steps, 1, lambda: None)
-    t_keyed = el / steps
-    run_keyed = dict(LAST_RUN)
+                                  [s["bm"].data_ptr() for s in shards], keys=keys)
 
     def check():
         ok = True
@@ -606,7 +609,17 @@ def c3_line(ctx, n_dev, mode, steps=3, n_heights=100_000, n_vals=150):
                 ok = ok and np.array_equal(P.unpack_bitmap(allw[h], ns[h]), exp[h])
         return ok
 
+    # the radix-256 combs first (the keyset cache's form), for comparison
+    el, kms_256 = timed_steps(ctx, lambda: keyed(ks256), steps, 1, lambda: None)
+    t_256 = el / steps
     ok = check()
+    ks256.free()
+    for s in shards:
+        s["bm"].zero_()
+    el, kms_keyed = timed_steps(ctx, lambda: keyed(ks), steps, 1, lambda: None)
+    t_keyed = el / steps
+    run_keyed = dict(LAST_RUN)
+    ok = ok and check()
     for s in shards:
         s["bm"].zero_()
         s["pk"] = torch.from_numpy(np.ascontiguousarray(sv.pubkeys[s["idx"].cpu().numpy()])).to(s["dev"])
@@ -625,17 +638,24 @@ def c3_line(ctx, n_dev, mode, steps=3, n_heights=100_000, n_vals=150):
     shards.clear()
     torch.cuda.empty_cache()
     per_dev = total / n_dev
-    ach = per_dev / (kms_keyed * 1e-3) * MACS_PER_KEYED_VERIFY / 1e12 if kms_keyed > 0 else None
+    # algorithmic work of the path that ran (ZIP-215 decodes R instead of the
+    # batched inversion: the radix-256 figure's decode term, with 32 additions)
+    macs = MACS_PER_KEYED_WIDE_GO_VERIFY if mode == 0 else MACS_PER_KEYED_VERIFY - 32 * 700
+    work = ("32 comb additions x 7 + inversion / 8 + 5 + check, x 100" if mode == 0
+            else "32 comb additions x 7 + decode R 265 + check 8, x 100")
+    ach = per_dev / (kms_keyed * 1e-3) * macs / 1e12 if kms_keyed > 0 else None
     return {"workload": f"configs[2]: {n_heights} commits x {n_vals} validators = {total} signatures, "
                         f"sharded by height over {n_dev} GPU(s), 1% bit-flipped (seed 42)",
             "scaling": "strong", "sigs_per_gpu": int(per_dev), "value": round(total / t_keyed, 1), "unit": "verifs/s",
             "ms_per_pass": round(t_keyed * 1e3, 3), "steps": steps,
-            "path": "registered keys (cmtv_verify_ed25519_indexed_sharded_device) + RCCL all-gather of bitmaps",
-            "kernel_ms_per_device": round(kms_keyed, 3),
-            "roofline": {"bound": "valu_int", "work": f"{MACS_PER_KEYED_VERIFY} int32 MACs/keyed verify "
-                                                      "(64 comb additions x 7 + decode R 265 + check 8, x 100)",
+            "path": "registered keys, radix-2^16 combs (cmtv_register_keys_ex CMTV_KEYS_WIDE, "
+                    "cmtv_verify_ed25519_indexed_sharded_device) + RCCL all-gather of bitmaps",
+            "kernel_ms_per_device": round(kms_keyed, 3), "register_wide_s": round(t_reg, 3),
+            "roofline": {"bound": "valu_int", "work": f"{macs} int32 MACs/keyed verify ({work}); SHA-512 and "
+                                                      "table loads not counted",
                          "achieved": round(ach, 3) if ach else None, "peak": INT_MAC_PEAK_T, "unit": "TMAC/s",
                          "frac": round(ach / INT_MAC_PEAK_T, 4) if ach else None},
+            "comb256_value": round(total / t_256, 1), "comb256_kernel_ms_per_device": round(kms_256, 3),
             "generic_value": round(total / t_generic, 1), "generic_ms_per_pass": round(t_generic * 1e3, 3),
             "generic_frac": round(per_dev / (kms_generic * 1e-3) * MACS_PER_VERIFY / 1e12 / INT_MAC_PEAK_T, 4)
             if kms_generic > 0 else None,

@@ -5,11 +5,54 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "keyed.h"
 #include "oct.h"
 #include "quad.h"
 #include "verify_core.h"
 
 namespace cmtv {
+
+__device__ __forceinline__ void load_words(uint32_t* w, const uint32_t* __restrict__ src, int nquads) {
+  const uint4* p = reinterpret_cast<const uint4*>(src);
+#pragma unroll
+  for (int q = 0; q < nquads; q++) {
+    const uint4 v = p[q];
+    w[4 * q] = v.x;
+    w[4 * q + 1] = v.y;
+    w[4 * q + 2] = v.z;
+    w[4 * q + 3] = v.w;
+  }
+}
+
+// Prefix products of comb_build_column, word-major / lane-minor per launch.
+struct DevCombScratch {
+  uint32_t* __restrict__ base;
+  uint32_t stride;
+  uint32_t lane;
+  __device__ __forceinline__ void store(int j, const fe& v) {
+#pragma unroll
+    for (int i = 0; i < 10; i++) base[(size_t)(j * 10 + i) * stride + lane] = v.v[i];
+  }
+  __device__ __forceinline__ void load(int j, fe& v) const {
+#pragma unroll
+    for (int i = 0; i < 10; i++) v.v[i] = base[(size_t)(j * 10 + i) * stride + lane];
+  }
+};
+
+// One comb window as a table source: 32-word rows, coordinates at 8-byte
+// aligned offsets 0 / 40 / 80 bytes -> 5 x dwordx2 per coordinate.
+struct DevCombWindow {
+  const uint32_t* __restrict__ rows;
+  __device__ __forceinline__ void load_fe(int e, int c, fe& r) const {
+    const uint2* p = reinterpret_cast<const uint2*>(rows + e * COMB_ROW_WORDS + c * 10);
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+      const uint2 v = p[i];
+      r.v[2 * i] = v.x;
+      r.v[2 * i + 1] = v.y;
+    }
+  }
+};
 
 // wave-uniform predicate (verify_one_half's loop bound)
 struct DevWave {

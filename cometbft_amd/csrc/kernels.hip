@@ -6,8 +6,8 @@
 //                   wavefront ballot packs 64 verdicts into one bitmap word
 //   k_verify_quad<MODE>: the same, one signature per quad of lanes (small batches)
 //   k_comb_build  : registered-key combs (keyed.h), one workgroup per key
-//   k_verify_keyed<MODE>: one signature per lane against a registered key
-//   k_verify_keyed_quad<MODE>: the same, one signature per quad of lanes
+//   k_verify_keyed_quad<MODE>: one signature per quad of lanes against a
+//                   registered key (the lane kernels: keyed_lane.hip)
 //   k_pubkey / k_sign : RFC 8032 key generation and signing (synthetic data)
 //
 // Memory layout (HBM):
@@ -44,18 +44,6 @@
 namespace cmtv {
 
 
-
-__device__ __forceinline__ void load_words(uint32_t* w, const uint32_t* __restrict__ src, int nquads) {
-  const uint4* p = reinterpret_cast<const uint4*>(src);
-#pragma unroll
-  for (int q = 0; q < nquads; q++) {
-    const uint4 v = p[q];
-    w[4 * q] = v.x;
-    w[4 * q + 1] = v.y;
-    w[4 * q + 2] = v.z;
-    w[4 * q + 3] = v.w;
-  }
-}
 
 // rows 0..127: (1..128)B; 128..255: (1..128)[2^124]B; 256..383: (1..128)[2^128]B;
 // then the radix-2^16 blocks (1..2^15)B, (1..2^15)[2^120]B, (1..2^15)[2^128]B
@@ -357,21 +345,6 @@ __global__ __launch_bounds__(128, CMTV_QUAD_WAVES_PER_EU) void k_verify_oct_spli
   if (t == 0 && out_bitmap) reinterpret_cast<uint8_t*>(out_bitmap)[gid >> 6] = (uint8_t)x;
 }
 
-// Prefix products of comb_build_column, word-major / lane-minor per launch.
-struct DevCombScratch {
-  uint32_t* __restrict__ base;
-  uint32_t stride;
-  uint32_t lane;
-  __device__ __forceinline__ void store(int j, const fe& v) {
-#pragma unroll
-    for (int i = 0; i < 10; i++) base[(size_t)(j * 10 + i) * stride + lane] = v.v[i];
-  }
-  __device__ __forceinline__ void load(int j, fe& v) const {
-#pragma unroll
-    for (int i = 0; i < 10; i++) v.v[i] = base[(size_t)(j * 10 + i) * stride + lane];
-  }
-};
-
 // Comb of (negate ? -P : P) for n_keys encoded points; workgroup = key,
 // thread = multiple d = 1..128. keys_ok[key] records whether P decoded.
 __global__ __launch_bounds__(128) void k_comb_build(const uint32_t* __restrict__ keys_pk, uint8_t* __restrict__ keys_ok,
@@ -389,151 +362,6 @@ __global__ __launch_bounds__(128) void k_comb_build(const uint32_t* __restrict__
   if (threadIdx.x == 0 && keys_ok) keys_ok[key] = ok ? 1 : 0;
   DevCombScratch sc{scratch, gridDim.x * 128u, blockIdx.x * 128u + threadIdx.x};
   comb_build_column(tabs + (size_t)key * COMB_TABLE_WORDS, A, (int)threadIdx.x + 1, sc);
-}
-
-// One comb window as a table source: 32-word rows, coordinates at 8-byte
-// aligned offsets 0 / 40 / 80 bytes -> 5 x dwordx2 per coordinate.
-struct DevCombWindow {
-  const uint32_t* __restrict__ rows;
-  __device__ __forceinline__ void load_fe(int e, int c, fe& r) const {
-    const uint2* p = reinterpret_cast<const uint2*>(rows + e * COMB_ROW_WORDS + c * 10);
-#pragma unroll
-    for (int i = 0; i < 5; i++) {
-      const uint2 v = p[i];
-      r.v[2 * i] = v.x;
-      r.v[2 * i + 1] = v.y;
-    }
-  }
-};
-
-#ifndef CMTV_KEYED_WAVES_PER_EU
-#define CMTV_KEYED_WAVES_PER_EU 2
-#endif
-
-// One signature per lane by registered key key_idx[i] (keyed.h). An index
-// outside the key set yields an invalid verdict, never an out-of-bounds read.
-// R' = [s]B - [k]A of one signature by registered key kid: over the key's
-// radix-256 comb (ktabs = the combs, bcomb = the comb of B), or with WIDE
-// over its radix-2^16 comb (ktabs = the wide combs, bcomb = the B table,
-// whose BC16 blocks are B's).
-template <bool WIDE>
-__device__ __forceinline__ bool keyed_comb_dev(ge_p3& acc, uint32_t kid, bool key_ok,
-                                               const uint32_t* __restrict__ keys_pk, const uint32_t* sig_ptr,
-                                               const uint8_t* msg, uint32_t mlen, const uint32_t* __restrict__ ktabs,
-                                               const uint32_t* __restrict__ bcomb) {
-  if (WIDE)
-    return keyed_comb_wide<DevCombWindow>(acc, keys_pk + 8 * (size_t)kid, key_ok, sig_ptr, msg, mlen,
-                                          ktabs + (size_t)kid * WIDE_TABLE_WORDS, DevBTab{bcomb});
-  return keyed_comb<DevCombWindow>(acc, keys_pk + 8 * (size_t)kid, key_ok, sig_ptr, msg, mlen,
-                                   ktabs + (size_t)kid * COMB_TABLE_WORDS, bcomb);
-}
-
-template <uint32_t MODE, bool WIDE>
-__global__ __launch_bounds__(64, CMTV_KEYED_WAVES_PER_EU) void k_verify_keyed(
-    uint32_t n, uint32_t n_keys, const uint32_t* __restrict__ key_idx, const uint32_t* __restrict__ sig,
-    const uint8_t* __restrict__ msg, const uint32_t* __restrict__ off, const uint32_t* __restrict__ keys_pk,
-    const uint8_t* __restrict__ keys_ok, const uint32_t* __restrict__ ktabs, const uint32_t* __restrict__ bcomb,
-    uint8_t* __restrict__ out_valid, uint64_t* __restrict__ out_bitmap) {
-  const uint32_t gid = blockIdx.x * 64 + threadIdx.x;
-  const bool active = gid < n;
-  const uint32_t i = active ? gid : n - 1;
-  const uint32_t m0 = off[i], m1 = off[i + 1];
-  uint32_t kid = key_idx[i];
-  const bool kin = kid < n_keys;
-  kid = kin ? kid : 0;
-  ge_p3 acc;
-  const bool ok = keyed_comb_dev<WIDE>(acc, kid, kin && keys_ok[kid] != 0, keys_pk, sig + 16 * (size_t)i, msg + m0,
-                                       m1 - m0, ktabs, bcomb);
-  bool v = check_R<MODE>(acc, sig + 16 * (size_t)i) && ok;
-  v = v && active;
-  if (active && out_valid) out_valid[gid] = v ? 1 : 0;
-  const uint64_t mask = __ballot(v);
-  if (threadIdx.x == 0 && out_bitmap) out_bitmap[gid >> 6] = mask;
-}
-
-// GO_STDLIB registered-key verification with KB signatures per lane: the
-// final encode needs 1/Z of every R', and each lane inverts the product of
-// its KB Z's once (Montgomery's trick: one 265-operation inversion and
-// 3 (KB - 1) multiplications instead of KB inversions). Signature
-// s = gid + r * lanes (round r), so every round of a wave covers 64
-// consecutive signatures and one bitmap word. R' (X, Y), Z and the prefix
-// products wait in `scr`, word-major (KB x 40 words per lane: coalesced).
-// An R' with Z = 0 (possible only from an undecodable key's comb, whose
-// verdicts are false anyway) enters the product as 1 so it cannot spoil the
-// lane's other signatures. Verdicts equal verify_keyed<MODE_GO_STDLIB>'s.
-template <int KB, bool WIDE>
-__global__ __launch_bounds__(64, CMTV_KEYED_WAVES_PER_EU) void k_verify_keyed_go_batch(
-    uint32_t n, uint32_t n_keys, const uint32_t* __restrict__ key_idx, const uint32_t* __restrict__ sig,
-    const uint8_t* __restrict__ msg, const uint32_t* __restrict__ off, const uint32_t* __restrict__ keys_pk,
-    const uint8_t* __restrict__ keys_ok, const uint32_t* __restrict__ ktabs, const uint32_t* __restrict__ bcomb,
-    uint32_t* __restrict__ scr, uint8_t* __restrict__ out_valid, uint64_t* __restrict__ out_bitmap) {
-  const uint32_t lanes = gridDim.x * 64u, gid = blockIdx.x * 64u + threadIdx.x;
-  DevCombScratch sc{scr, lanes, gid};  // slot j: 10 words at [(j * 10 + i) * lanes + gid]
-  uint32_t okbits = 0;
-#pragma unroll 1
-  for (int r = 0; r < KB; r++) {
-    const uint32_t s = gid + (uint32_t)r * lanes;
-    const bool active = s < n;
-    const uint32_t i = active ? s : n - 1;
-    const uint32_t m0 = off[i], m1 = off[i + 1];
-    uint32_t kid = key_idx[i];
-    const bool kin = kid < n_keys;
-    kid = kin ? kid : 0;
-    ge_p3 acc;
-    bool ok = keyed_comb_dev<WIDE>(acc, kid, kin && keys_ok[kid] != 0, keys_pk, sig + 16 * (size_t)i, msg + m0,
-                                   m1 - m0, ktabs, bcomb);
-    const bool zbad = fe_iszero(acc.Z);
-    fe z, one;
-    fe_1(one);
-    fe_select(z, acc.Z, one, zbad);
-    ok = ok && !zbad && active;
-    okbits |= (ok ? 1u : 0u) << r;
-    // the running product goes through the scratch too, so nothing but
-    // okbits stays live across the combs (their register budget is full)
-    fe prod;
-    if (r == 0) {
-      prod = z;
-    } else {
-      sc.load(4 * (r - 1) + 3, prod);
-      fe_mul(prod, prod, z);
-    }
-    sc.store(4 * r + 0, acc.X);
-    sc.store(4 * r + 1, acc.Y);
-    sc.store(4 * r + 2, z);
-    sc.store(4 * r + 3, prod);
-  }
-  fe inv;
-  {
-    fe prod;
-    sc.load(4 * (KB - 1) + 3, prod);
-    fe_invert(inv, prod);
-  }
-#pragma unroll 1
-  for (int r = KB - 1; r >= 0; r--) {
-    const uint32_t s = gid + (uint32_t)r * lanes;
-    const bool active = s < n;
-    const uint32_t i = active ? s : n - 1;
-    fe X, Y, z, zi;
-    sc.load(4 * r + 0, X);
-    sc.load(4 * r + 1, Y);
-    sc.load(4 * r + 2, z);
-    if (r > 0) {
-      fe pre;
-      sc.load(4 * (r - 1) + 3, pre);
-      fe_mul(zi, inv, pre);  // 1 / Z_r
-      fe_mul(inv, inv, z);   // 1 / (Z_0 ... Z_{r-1})
-    } else {
-      zi = inv;
-    }
-    uint32_t rw[8];
-    load_words(rw, sig + 16 * (size_t)i, 2);  // R
-    bool v = check_R_go_zi(X, Y, zi, rw);
-    v = v && ((okbits >> r) & 1u) != 0;
-    if (active && out_valid) out_valid[s] = v ? 1 : 0;
-    const uint64_t mask = __ballot(v);
-    const uint32_t word = s >> 6;
-    if (threadIdx.x == 0 && out_bitmap && word < (n + 63) / 64) out_bitmap[word] = mask;
-  }
 }
 
 // One signature per quad of lanes by registered key (keyed_quad.h), for
@@ -673,77 +501,6 @@ hipError_t launch_comb_build(uint32_t n_keys, const void* keys_pk, uint8_t* keys
   return hipGetLastError();
 }
 
-// Position bases 2^(16j) (-A) of the wide combs (keyed.h), thread = (key, j):
-// 16 j doublings of -A, stored as extended points (40 words).
-__global__ __launch_bounds__(64) void k_wide_bases(uint32_t n_keys, const uint32_t* __restrict__ keys_pk,
-                                                   uint32_t* __restrict__ bases) {
-  const uint32_t gid = blockIdx.x * 64 + threadIdx.x;
-  if (gid >= n_keys * WIDE_POSITIONS) return;
-  const uint32_t key = gid / WIDE_POSITIONS, j = gid % WIDE_POSITIONS;
-  uint32_t w[8];
-  load_words(w, keys_pk + 8 * (size_t)key, 2);
-  ge_p3 A, P;
-  (void)p3_frombytes(A, w);  // an undecodable key's rows are never trusted (keys_ok)
-  cached_neg_point(P, A);
-  if (j > 0) {
-    ge_p2 q;
-    ge_efgh t;
-    p3_to_p2(q, P);
-#pragma unroll 1
-    for (uint32_t r = 0; r < 16 * j; r++) {
-      p2_dbl(t, q);
-      efgh_to_p2(q, t);
-    }
-    efgh_to_p3(P, t);
-  }
-  uint32_t* o = bases + (size_t)gid * 40;
-#pragma unroll
-  for (int i = 0; i < 10; i++) {
-    o[i] = P.X.v[i];
-    o[10 + i] = P.Y.v[i];
-    o[20 + i] = P.Z.v[i];
-    o[30 + i] = P.T.v[i];
-  }
-}
-
-// Wide comb rows, thread = (key = blockIdx.y, position j, run b): rows
-// 64 b .. 64 b + 63 of position j (wide_build_run).
-__global__ __launch_bounds__(64) void k_wide_build(const uint32_t* __restrict__ bases, uint32_t* __restrict__ tabs,
-                                                   uint32_t* __restrict__ scratch) {
-  constexpr uint32_t kRuns = WIDE_ENTRIES / WIDE_RUN;
-  const uint32_t key = blockIdx.y, tid = blockIdx.x * 64 + threadIdx.x;
-  const uint32_t j = tid / kRuns, b = tid % kRuns;
-  const uint32_t* pb = bases + ((size_t)key * WIDE_POSITIONS + j) * 40;
-  ge_p3 P;
-#pragma unroll
-  for (int i = 0; i < 10; i++) {
-    P.X.v[i] = pb[i];
-    P.Y.v[i] = pb[10 + i];
-    P.Z.v[i] = pb[20 + i];
-    P.T.v[i] = pb[30 + i];
-  }
-  const uint32_t per_key = gridDim.x * 64u;
-  DevCombScratch sc{scratch, gridDim.y * per_key, key * per_key + tid};
-  wide_build_run(tabs + (size_t)key * WIDE_TABLE_WORDS + (size_t)j * WIDE_ENTRIES * COMB_ROW_WORDS, P,
-                 (int)(b * WIDE_RUN), sc);
-}
-
-static_assert(kWideTableWords == WIDE_TABLE_WORDS, "kernels.h / keyed.h wide comb size");
-static_assert(kWideScratchWordsPerKey == (size_t)WIDE_POSITIONS * (WIDE_ENTRIES / WIDE_RUN) * WIDE_RUN * 10,
-              "wide build scratch: WIDE_RUN prefix products per thread");
-
-hipError_t launch_wide_build(uint32_t n_keys, const void* keys_pk, uint32_t* tabs, uint32_t* bases,
-                             uint32_t* scratch, hipStream_t s) {
-  if (n_keys == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_wide_bases, dim3((n_keys * WIDE_POSITIONS + 63) / 64), dim3(64), 0, s, n_keys,
-                     static_cast<const uint32_t*>(keys_pk), bases);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_wide_build, dim3(WIDE_POSITIONS * (WIDE_ENTRIES / WIDE_RUN) / 64, n_keys), dim3(64), 0, s,
-                     bases, tabs, scratch);
-  return hipGetLastError();
-}
-
 // Registered-key quads with two helper waves: 3 quad waves (48 signatures)
 // run the 32 fixed-base comb additions, take k from the hash helper (wave 4,
 // q_keyed_challenge; published through an LDS flag, not a barrier), run the
@@ -862,7 +619,8 @@ hipError_t launch_verify_keyed(uint32_t mode, uint32_t n, uint32_t n_keys, const
                                const void* msg, const void* off, const uint32_t* keys_pk, const uint8_t* keys_ok,
                                const uint32_t* ktabs, const uint32_t* bcomb, void* valid, void* bitmap,
                                bool quad, bool split, uint32_t k_wait, uint32_t* diag, uint32_t batch_kb,
-                               uint32_t* scr, const uint32_t* wtabs, const uint32_t* btab, hipStream_t s) {
+                               uint32_t* scr, const uint32_t* wtabs, const uint32_t* btab, bool wide_dma,
+                               hipStream_t s) {
   if (n == 0) return hipSuccess;
   auto ki = static_cast<const uint32_t*>(key_idx);
   auto sgp = static_cast<const uint32_t*>(sig);
@@ -891,40 +649,8 @@ hipError_t launch_verify_keyed(uint32_t mode, uint32_t n, uint32_t n_keys, const
                          keys_ok, ktabs, bcomb, vp, bp);
     return hipGetLastError();
   }
-  // lane kernels: over the wide combs when the key set has them
-  const uint32_t* tabs = wtabs ? wtabs : ktabs;
-  const uint32_t* bsrc = wtabs ? btab : bcomb;
-  if (mode != MODE_ZIP215 && batch_kb >= 4 && scr) {
-    // GO_STDLIB with batch_kb signatures per lane (k_verify_keyed_go_batch)
-    const dim3 grid((n + 64 * batch_kb - 1) / (64 * batch_kb)), block(64);
-    if (wtabs && batch_kb >= 8)
-      hipLaunchKernelGGL((k_verify_keyed_go_batch<8, true>), grid, block, 0, s, n, n_keys, ki, sgp, mp, op, keys_pk,
-                         keys_ok, tabs, bsrc, scr, vp, bp);
-    else if (wtabs)
-      hipLaunchKernelGGL((k_verify_keyed_go_batch<4, true>), grid, block, 0, s, n, n_keys, ki, sgp, mp, op, keys_pk,
-                         keys_ok, tabs, bsrc, scr, vp, bp);
-    else if (batch_kb >= 8)
-      hipLaunchKernelGGL((k_verify_keyed_go_batch<8, false>), grid, block, 0, s, n, n_keys, ki, sgp, mp, op, keys_pk,
-                         keys_ok, tabs, bsrc, scr, vp, bp);
-    else
-      hipLaunchKernelGGL((k_verify_keyed_go_batch<4, false>), grid, block, 0, s, n, n_keys, ki, sgp, mp, op, keys_pk,
-                         keys_ok, tabs, bsrc, scr, vp, bp);
-    return hipGetLastError();
-  }
-  const dim3 grid(blocks_for(n)), block(64);
-  if (mode == MODE_ZIP215 && wtabs)
-    hipLaunchKernelGGL((k_verify_keyed<MODE_ZIP215, true>), grid, block, 0, s, n, n_keys, ki, sgp, mp, op, keys_pk,
-                       keys_ok, tabs, bsrc, vp, bp);
-  else if (mode == MODE_ZIP215)
-    hipLaunchKernelGGL((k_verify_keyed<MODE_ZIP215, false>), grid, block, 0, s, n, n_keys, ki, sgp, mp, op, keys_pk,
-                       keys_ok, tabs, bsrc, vp, bp);
-  else if (wtabs)
-    hipLaunchKernelGGL((k_verify_keyed<MODE_GO_STDLIB, true>), grid, block, 0, s, n, n_keys, ki, sgp, mp, op,
-                       keys_pk, keys_ok, tabs, bsrc, vp, bp);
-  else
-    hipLaunchKernelGGL((k_verify_keyed<MODE_GO_STDLIB, false>), grid, block, 0, s, n, n_keys, ki, sgp, mp, op,
-                       keys_pk, keys_ok, tabs, bsrc, vp, bp);
-  return hipGetLastError();
+  return launch_verify_keyed_lane(mode, n, n_keys, ki, sgp, mp, op, keys_pk, keys_ok, ktabs, bcomb, vp, bp, batch_kb,
+                                  scr, wtabs, btab, wide_dma, s);
 }
 
 hipError_t launch_pubkey(uint32_t n, const void* seeds, const uint32_t* btab, void* out_pk, hipStream_t s) {

@@ -290,16 +290,17 @@ CMTV_HD void wide_build_run(uint32_t* rows, const ge_p3& P, int e0, Scratch& sc)
 // keyed_comb over the wide combs: wtab = the key's wide comb of -A, btab =
 // the B table whose BC16 blocks hold (1..2^15) 2^(16j) B (a load_fe policy
 // over absolute rows).
-template <class Win, class BTab>
-CMTV_HD bool keyed_comb_wide(ge_p3& acc, const uint32_t* key_pk, bool key_ok, const uint32_t* sig_ptr,
-                             const uint8_t* msg, uint32_t mlen, const uint32_t* wtab, const BTab& btab) {
+// The digit streams of a wide-comb verification: k = SHA-512(R || A || M)
+// mod L and s, as hs_digits65536 streams (Hi: digits 15..8, Lo: 7..0); returns
+// whether the key decoded and s is canonical.
+CMTV_HD bool keyed_wide_digits(uint32_t kLo[8], uint32_t kHi[8], uint32_t sLo[8], uint32_t sHi[8],
+                               const uint32_t* key_pk, bool key_ok, const uint32_t* sig_ptr, const uint8_t* msg,
+                               uint32_t mlen) {
   uint32_t w[16];
 #pragma unroll
   for (int i = 0; i < 8; i++) w[i] = sig_ptr[8 + i];  // S
   const bool ok = key_ok && (w[7] & 0xE0000000u) == 0 && sc_is_canonical(w);
-  uint32_t sLo[8], sHi[8];
   hs_digits65536(sLo, sHi, w);
-
   uint32_t h[16], k[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) {
@@ -308,9 +309,15 @@ CMTV_HD bool keyed_comb_wide(ge_p3& acc, const uint32_t* key_pk, bool key_ok, co
   }
   sha512_prefixed<16>(h, w, msg, mlen);
   sc_reduce512(k, h);
-  uint32_t kLo[8], kHi[8];
   hs_digits65536(kLo, kHi, k);
+  return ok;
+}
 
+template <class Win, class BTab>
+CMTV_HD bool keyed_comb_wide(ge_p3& acc, const uint32_t* key_pk, bool key_ok, const uint32_t* sig_ptr,
+                             const uint8_t* msg, uint32_t mlen, const uint32_t* wtab, const BTab& btab) {
+  uint32_t kLo[8], kHi[8], sLo[8], sHi[8];
+  const bool ok = keyed_wide_digits(kLo, kHi, sLo, sHi, key_pk, key_ok, sig_ptr, msg, mlen);
   p3_identity(acc);
   ge_efgh t;
 #pragma unroll 1

@@ -386,6 +386,9 @@ struct cmtv_ctx {
   uint32_t keyed_wait = cmtv::kKeyedWaitDefault;
   // GO_STDLIB keyed lane launches batch the final inversion (CMTV_KEYED_BATCH=0: off)
   bool keyed_batch = true;
+  // wide-comb lane kernels stage their rows through LDS by LDS-DMA
+  // (keyed_lane.hip kCombWideDma; CMTV_WIDE_DMA=0: plain loads)
+  bool wide_dma = true;
   // devices (indices into devs) that take host batches, in shard order; the
   // RCCL communicator (when rccl) spans exactly these, rank = position
   std::vector<size_t> live;
@@ -589,7 +592,7 @@ static int enqueue_verify_keyed(cmtv_ctx* ctx, CmtvDev& D, const cmtv_keyset::Pe
                             K.d_tab, D.d_bcomb, d_valid ? d_valid + c : nullptr,
                             d_bitmap ? d_bitmap + c / 64 : nullptr, quad, n <= ctx->quad_split_max,
                             ctx->keyed_wait, D.d_diag, kb, static_cast<uint32_t*>(D.d_atab.p),
-                            quad ? nullptr : K.d_wide, D.d_btab, s);
+                            quad ? nullptr : K.d_wide, D.d_btab, ctx->wide_dma, s);
     if (e != hipSuccess) {
       D.timing.abandon(tp);
       return hip_fail(e);
@@ -1101,6 +1104,7 @@ static void read_env(cmtv_ctx* ctx) {
   if (const char* nz = std::getenv("CMTV_NO_ZC_IN")) ctx->zc_in = nz[0] != '1';
   if (const char* kl = std::getenv("CMTV_FORCE_K_LATE")) ctx->keyed_wait = kl[0] == '1' ? 0u : kKeyedWaitDefault;
   if (const char* kb = std::getenv("CMTV_KEYED_BATCH")) ctx->keyed_batch = kb[0] != '0';
+  if (const char* wd = std::getenv("CMTV_WIDE_DMA")) ctx->wide_dma = wd[0] != '0';
   ctx->force_rccl = std::getenv("CMTV_FORCE_RCCL") != nullptr;
   ctx->no_rccl = std::getenv("CMTV_NO_RCCL") != nullptr;
 }

@@ -75,8 +75,24 @@ CMTV_HD void sha512_compress(uint64_t st[8], uint64_t w[16]) {
   st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
 
+// The word an empty, 4-byte aligned message "loads" (sha512_prefixed): a
+// zero of our own in global memory on the device, so the load stays an
+// unconditional global load next to the real ones.
+#ifdef __HIP_DEVICE_COMPILE__
+static __device__ uint32_t g_sha512_no_word;
+#else
+static const uint32_t g_sha512_no_word = 0u;
+#endif
+
 CMTV_HD uint32_t funnel_bytes(uint32_t hi, uint32_t lo, uint32_t sh) {
-  return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * sh));  // v_alignbyte_b32
+#ifdef __HIP_DEVICE_COMPILE__
+  // the intrinsic keeps hi and lo separate values: the 64-bit form lets the
+  // compiler fuse two adjacent array words into one 64-bit access, which
+  // pins sha512_prefixed's word array in scratch
+  return __builtin_amdgcn_alignbyte(hi, lo, sh);
+#else
+  return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * sh));
+#endif
 }
 
 // SHA-512(prefix[0 .. 4*PW) || msg[0 .. mlen)); prefix as little-endian byte
@@ -84,8 +100,8 @@ CMTV_HD uint32_t funnel_bytes(uint32_t hi, uint32_t lo, uint32_t sh) {
 //
 // The message is read with 4-byte aligned loads and re-aligned in registers
 // (the per-lane message offset has arbitrary alignment); only words holding
-// at least one message byte are loaded, so nothing past msg[mlen-1]'s
-// 4-byte word is touched.
+// at least one message byte are read, so nothing past msg[mlen-1]'s 4-byte
+// word is touched.
 template <int PW>
 CMTV_HD void sha512_prefixed(uint32_t out[16], const uint32_t pre[PW], const uint8_t* msg, uint32_t mlen) {
   static_assert(PW % 2 == 0 && PW <= 16, "prefix must be whole 64-bit words inside block 0");
@@ -96,45 +112,56 @@ CMTV_HD void sha512_prefixed(uint32_t out[16], const uint32_t pre[PW], const uin
   const uint32_t total = PB + mlen;
   const uint32_t nblocks = (total + 17 + 127) / 128;
   const uint64_t bitlen = (uint64_t)total * 8;
-  const uintptr_t addr = (uintptr_t)msg;
-  const uint32_t sh = (uint32_t)(addr & 3);
-  const uint32_t* mw = (const uint32_t*)(addr - sh);  // aligned base
+  const uint32_t sh = (uint32_t)((uintptr_t)msg & 3);
+  // aligned base (pointer arithmetic keeps msg's address space: global loads)
+  const uint32_t* mw = reinterpret_cast<const uint32_t*>(msg - sh);
   const uint32_t nwords = (sh + mlen + 3) / 4;         // aligned words holding message bytes
-  auto aligned = [&](uint32_t j) -> uint32_t { return j < nwords ? mw[j] : 0u; };
-  // little-endian stream word at byte position pos (pos % 4 == 0, pos >= PB)
+  // A block's aligned message words are all loaded before any is used (mv
+  // below), so the loads go out together and are waited for once -- a load
+  // under a per-lane branch costs a full memory round trip each. An index past
+  // the message's last word re-reads that word (the 4-byte word holding a
+  // message byte lies in the message's page) and is masked; an empty aligned
+  // message, with no word to read at all, reads g_sha512_no_word.
+  const uint32_t jmax = nwords ? nwords - 1 : 0u;
+  const uint32_t* mb = nwords ? mw : &g_sha512_no_word;
+  // little-endian stream word at byte position pos (pos % 4 == 0, pos >= PB),
+  // branch-free: message bytes, then the 0x80 pad byte, then zeros
   auto tail_word = [&](uint32_t pos, uint32_t lo, uint32_t hi) -> uint32_t {
-    uint32_t v = funnel_bytes(hi, lo, sh);
+    const uint32_t v = funnel_bytes(hi, lo, sh);
     const int r = (int)total - (int)pos;  // message bytes left in this word
-    if (r >= 4) return v;
-    if (r < 0) return 0u;
-    const uint32_t keep = r == 0 ? 0u : (0xFFFFFFFFu >> (32 - 8 * r));
-    return (v & keep) | (0x80u << (8 * r));
+    const uint32_t rr = r < 0 ? 0u : (r > 4 ? 4u : (uint32_t)r);
+    const uint32_t keep = (uint32_t)((1ull << (8 * rr)) - 1u);
+    const uint32_t pad = (r >= 0 && r < 4) ? (0x80u << (8 * rr)) : 0u;
+    return (v & keep) | pad;
   };
   auto be64 = [](uint32_t lo_word, uint32_t hi_word) -> uint64_t {
     return ((uint64_t)__builtin_bswap32(lo_word) << 32) | __builtin_bswap32(hi_word);
   };
 #pragma unroll 1
   for (uint32_t b = 0; b < nblocks; b++) {
+    // mv[k] = aligned message word j0 + k, j0 = (128 b - PB) / 4: the tail
+    // word at block offset off is funnel(mv[off/4], mv[off/4 + 1]); block 0's
+    // negative indices are the prefix's (loaded clamped, never used)
+    const int j0 = (int)(b * 32) - (int)(PB / 4);
+    uint32_t mv[33];
+#pragma unroll
+    for (int k = 0; k < 33; k++) {
+      const uint32_t j = (uint32_t)(j0 + k);  // negative (block 0's prefix) -> huge: masked
+      mv[k] = mb[j < nwords ? j : jmax];
+    }
+#pragma unroll
+    for (int k = 0; k < 33; k++) mv[k] = (uint32_t)(j0 + k) < nwords ? mv[k] : 0u;
     uint64_t w[16];
-    // message-relative aligned word index of this block's first tail byte
-    const uint32_t q0 = (b == 0) ? 0u : b * 128 - PB;
-    const uint32_t j0 = q0 / 4;
-    uint32_t prev = aligned(j0);
 #pragma unroll
     for (int t = 0; t < 16; t++) {
       uint32_t lw[2];
 #pragma unroll
       for (int h = 0; h < 2; h++) {
         const uint32_t off = 8 * t + 4 * h;  // byte offset inside the block
-        if (b == 0 && off < PB) {
+        if (b == 0 && off < PB)
           lw[h] = pre[off / 4];
-        } else {
-          const uint32_t pos = b * 128 + off;
-          const uint32_t jj = (pos - PB) / 4 + 1;
-          const uint32_t next = aligned(jj);
-          lw[h] = tail_word(pos, prev, next);
-          prev = next;
-        }
+        else
+          lw[h] = tail_word(b * 128 + off, mv[off / 4], mv[off / 4 + 1]);
       }
       uint64_t word = be64(lw[0], lw[1]);
       if (b == nblocks - 1 && t == 15) word = bitlen;

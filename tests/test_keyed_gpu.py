@@ -1,6 +1,8 @@
 """GPU parity of registered-key verification (keyed.h / keyed_quad.h comb paths,
 cmtv_register_keys + cmtv_verify_ed25519_indexed[_device]): verdicts must equal
-the corpus' committed verdicts and the C oracle's, bit for bit, both modes."""
+the corpus' committed verdicts and the C oracle's, bit for bit, both modes.
+Kernel "wide": the lane kernels over radix-2^16 key combs
+(cmtv_register_keys_ex(CMTV_KEYS_WIDE), keyed.h keyed_comb_wide)."""
 import numpy as np
 import pytest
 
@@ -11,13 +13,20 @@ from cometbft_amd import _native as N
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("kernel", ["quad2", "quad", "lane"])
+KERNELS = ["quad2", "quad", "lane", "wide"]
+
+
+def _ctx(kernel, gpu_ctx, gpu_ctx_quad1, gpu_ctx_lane):
+    return {"quad2": gpu_ctx, "quad": gpu_ctx_quad1, "lane": gpu_ctx_lane, "wide": gpu_ctx_lane}[kernel]
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("mode,key", [(MODE_GO_STDLIB, "go"), (MODE_ZIP215, "zip215")])
 def test_corpus_bit_exact_keyed(gpu_ctx, gpu_ctx_quad1, gpu_ctx_lane, corpus, mode, key, kernel):
-    gpu_ctx = {"quad2": gpu_ctx, "quad": gpu_ctx_quad1, "lane": gpu_ctx_lane}[kernel]
+    gpu_ctx = _ctx(kernel, gpu_ctx, gpu_ctx_quad1, gpu_ctx_lane)
     pk = corpus["pk"]
-    uniq, idx = np.unique(pk, axis=0, return_inverse=True)
-    ks = gpu_ctx.register_keys(uniq)
+    uniq, idx = np.unique(pk, axis=0, return_inverse=True)  # 748 keys: 47 GiB of wide combs
+    ks = gpu_ctx.register_keys(uniq, wide=kernel == "wide")
     assert len(ks) == uniq.shape[0]
     msg, off = pack_messages(corpus["msgs"])
     valid, words = gpu_ctx.verify_indexed(ks, idx.astype(np.uint32).reshape(-1), corpus["sig"], msg, off, mode,
@@ -41,15 +50,15 @@ def _valset_commits(n_keys, n_sigs, seed):
     return pk, kidx, sig, m, off, rng
 
 
-@pytest.mark.parametrize("kernel", ["quad2", "quad", "lane"])
+@pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("n", [1, 15, 16, 17, 63, 64, 65, 3000, 12289])
 def test_keyed_matches_generic_and_oracle(gpu_ctx, gpu_ctx_quad1, gpu_ctx_lane, n, kernel):
-    gpu_ctx = {"quad2": gpu_ctx, "quad": gpu_ctx_quad1, "lane": gpu_ctx_lane}[kernel]
+    gpu_ctx = _ctx(kernel, gpu_ctx, gpu_ctx_quad1, gpu_ctx_lane)
     pk, kidx, sig, m, off, rng = _valset_commits(150, n, 7 + n)
     sig = sig.copy()
     for i in np.nonzero(rng.random(n) < 0.2)[0]:
         sig[i, rng.integers(0, 64)] ^= 1 << rng.integers(0, 8)
-    ks = gpu_ctx.register_keys(pk)
+    ks = gpu_ctx.register_keys(pk, wide=kernel == "wide")
     for mode in (MODE_GO_STDLIB, MODE_ZIP215):
         exp = coracle.verify_batch(pk[kidx], sig, m, off, mode, nthreads=8)
         got, words = gpu_ctx.verify_indexed(ks, kidx, sig, m, off, mode, bitmap=True)
@@ -60,14 +69,16 @@ def test_keyed_matches_generic_and_oracle(gpu_ctx, gpu_ctx_quad1, gpu_ctx_lane, 
     ks.free()
 
 
-def test_undecodable_and_noncanonical_keys(gpu_ctx, corpus):
+@pytest.mark.parametrize("wide", [False, True])
+def test_undecodable_and_noncanonical_keys(gpu_ctx, gpu_ctx_lane, corpus, wide):
     # keys the corpus marks off-curve / non-canonical, each used by its own vectors
     sel = [i for i, c in enumerate(corpus["cats"]) if c in ("offcurve_A", "noncanonical_A", "small_order_A")]
     assert sel
     pk = corpus["pk"][sel]
     msgs = [corpus["msgs"][i] for i in sel]
     m, off = pack_messages(msgs)
-    ks = gpu_ctx.register_keys(pk)
+    gpu_ctx = gpu_ctx_lane if wide else gpu_ctx
+    ks = gpu_ctx.register_keys(pk, wide=wide)
     for mode, key in ((MODE_GO_STDLIB, "go"), (MODE_ZIP215, "zip215")):
         got = gpu_ctx.verify_indexed(ks, np.arange(len(sel), dtype=np.uint32), corpus["sig"][sel], m, off, mode)
         assert np.array_equal(got, corpus[key][sel])
@@ -110,8 +121,9 @@ def test_keyset_belongs_to_its_context(gpu_ctx, gpu_ctx_lane):
     ks.free()
 
 
+@pytest.mark.parametrize("wide", [False, True])
 @pytest.mark.parametrize("n", [530_000, 1_100_003])
-def test_keyed_go_batch_inversion(gpu_ctx_lane, corpus, n):
+def test_keyed_go_batch_inversion(gpu_ctx_lane, corpus, n, wide):
     """k_verify_keyed_go_batch (configs[2]'s GO_STDLIB lane path): KB = 4 / 8
     signatures per lane share one field inversion (Montgomery's trick). n =
     530,000 runs the KB = 4 form; 1,100,003 one 2^20 chunk at KB = 8 plus a
@@ -120,7 +132,9 @@ def test_keyed_go_batch_inversion(gpu_ctx_lane, corpus, n):
     may vanish: their signatures must fail without spoiling the lane's
     others) and non-canonical / small-order keys; 1% of the signatures carry
     a flipped bit. Verdicts must equal the oracle's and the unbatched
-    kernel's (CMTV_KEYED_BATCH=0) bit for bit."""
+    kernel's (CMTV_KEYED_BATCH=0) bit for bit; with wide, over the radix-2^16
+    combs (rows staged by LDS-DMA; same verdicts, ZIP-215 too), and the
+    plain-load wide kernel's (CMTV_WIDE_DMA=0)."""
     import os
 
     from cometbft_amd import Context
@@ -149,13 +163,17 @@ def test_keyed_go_batch_inversion(gpu_ctx_lane, corpus, n):
     sig[flips, rng.integers(0, 64, flips.size)] ^= (1 << rng.integers(0, 8, flips.size)).astype(np.uint8)
     exp = coracle.verify_batch(pk[kidx], sig, m, off, MODE_GO_STDLIB, nthreads=16)
     assert 0 < exp.sum() < n
-    ks = gpu_ctx_lane.register_keys(pk)
+    ks = gpu_ctx_lane.register_keys(pk, wide=wide)
     got = gpu_ctx_lane.verify_indexed(ks, kidx, sig, m, off, MODE_GO_STDLIB)
     bad = np.nonzero(got != exp)[0]
     assert bad.size == 0, (bad[:10], kidx[bad[:10]])
+    if wide:
+        exp_z = coracle.verify_batch(pk[kidx], sig, m, off, MODE_ZIP215, nthreads=16)
+        assert np.array_equal(gpu_ctx_lane.verify_indexed(ks, kidx, sig, m, off, MODE_ZIP215), exp_z)
     ks.free()
-    old = {k: os.environ.get(k) for k in ("CMTV_QUAD_MAX", "CMTV_KEYED_QUAD_MAX", "CMTV_KEYED_BATCH")}
-    os.environ.update({"CMTV_QUAD_MAX": "0", "CMTV_KEYED_QUAD_MAX": "0", "CMTV_KEYED_BATCH": "0"})
+    keys = ("CMTV_QUAD_MAX", "CMTV_KEYED_QUAD_MAX", "CMTV_KEYED_BATCH", "CMTV_WIDE_DMA")
+    old = {k: os.environ.get(k) for k in keys}
+    os.environ.update({k: "0" for k in keys})
     try:
         plain = Context(device=0)
     finally:
@@ -164,6 +182,6 @@ def test_keyed_go_batch_inversion(gpu_ctx_lane, corpus, n):
                 del os.environ[k]
             else:
                 os.environ[k] = v
-    ks2 = plain.register_keys(pk)
+    ks2 = plain.register_keys(pk, wide=wide)  # wide: rows by plain loads (no LDS-DMA staging)
     assert np.array_equal(plain.verify_indexed(ks2, kidx, sig, m, off, MODE_GO_STDLIB), got)
     ks2.free()

@@ -94,12 +94,20 @@ if want("keyed_quad10k"):
     run("keyed_quad10k", ctx, b10k, keyed=ks)
 # configs[2]'s launch shape: 262,144 signatures per launch (kChunk), the 150
 # keys cycling as in consecutive 150-validator commits
-if want("lane262k", "keyed_lane262k", "keyed_lane1m"):
+if want("lane262k", "keyed_lane262k", "keyed_lane1m", "keyed_wide1m"):
     b262k = batch(262_144)
     run("lane262k", lctx, b262k)
     lks = lctx.register_keys(pks)
     run("keyed_lane262k", lctx, b262k, keyed=lks)
-    if want("keyed_lane1m"):
+    if want("keyed_lane1m", "keyed_wide1m"):
         del b262k
-        b1m = batch(1_000_000)
-        run("keyed_lane1m", lctx, b1m, keyed=lks)
+        b1m = batch(1 << 20)
+        if want("keyed_lane1m"):
+            run("keyed_lane1m", lctx, b1m, keyed=lks)
+        if want("keyed_wide1m"):
+            # radix-2^16 key combs (CMTV_KEYS_WIDE): configs[2]'s 2^20-signature launches
+            wks = lctx.register_keys(pks, wide=True)
+            run("keyed_wide1m", lctx, b1m, keyed=wks)
+            # the same rows by plain loads (no LDS-DMA staging)
+            nctx = env_ctx(CMTV_QUAD_MAX=0, CMTV_KEYED_QUAD_MAX=0, CMTV_WIDE_DMA=0)
+            run("keyed_wide1m", nctx, b1m, keyed=nctx.register_keys(pks, wide=True))

@@ -62,9 +62,13 @@ MACS_PER_VERIFY = 300_000          # 3,000 field mults x
 # in the one-lane form) + decode R (~265) + final check (~8) = 721 field mults
 MACS_PER_KEYED_VERIFY = 72_100
 # the same over the radix-2^16 key combs (CMTV_KEYS_WIDE) in GO_STDLIB with 8
-# signatures per lane sharing one inversion (k_verify_keyed_go_batch<8, true>):
+# signatures per lane sharing one inversion (k_verify_keyed_batch<0, 8, 2>):
 # 32 additions x 7 + 265 / 8 + 3 (batch products) + 2 (x, y) = 262 field mults
 MACS_PER_KEYED_WIDE_GO_VERIFY = 26_200
+# ZIP-215 on the same batches checks R by coset instead of decoding it
+# (verify_core.h zip_coset): 32 additions x 7 + R' + T8 (6) + y_R Z, iX, iY on
+# two bases (6) + 265 / 8 + 3 (batch products) + 1 (x) = 273 field mults
+MACS_PER_KEYED_WIDE_ZIP_VERIFY = 27_300
 INT_MAC_PEAK_T = 33.0              # measured v_mad_u64_u32 lane-ops/s, 1e12 (profiles/r01_int_rates.txt)
 
 
@@ -640,9 +644,9 @@ def c3_line(ctx, n_dev, mode, steps=3, n_heights=100_000, n_vals=150):
     per_dev = total / n_dev
     # algorithmic work of the path that ran (ZIP-215 decodes R instead of the
     # batched inversion: the radix-256 figure's decode term, with 32 additions)
-    macs = MACS_PER_KEYED_WIDE_GO_VERIFY if mode == 0 else MACS_PER_KEYED_VERIFY - 32 * 700
+    macs = MACS_PER_KEYED_WIDE_GO_VERIFY if mode == 0 else MACS_PER_KEYED_WIDE_ZIP_VERIFY
     work = ("32 comb additions x 7 + inversion / 8 + 5 + check, x 100" if mode == 0
-            else "32 comb additions x 7 + decode R 265 + check 8, x 100")
+            else "32 comb additions x 7 + coset check 12 + inversion / 8 + 4, x 100")
     ach = per_dev / (kms_keyed * 1e-3) * macs / 1e12 if kms_keyed > 0 else None
     return {"workload": f"configs[2]: {n_heights} commits x {n_vals} validators = {total} signatures, "
                         f"sharded by height over {n_dev} GPU(s), 1% bit-flipped (seed 42)",

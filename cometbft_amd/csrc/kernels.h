@@ -72,8 +72,9 @@ constexpr size_t kWideScratchWordsPerKey = (size_t)16 * (32768 / 64) * 64 * 10;
 constexpr size_t kWideBaseWordsPerKey = 16 * 40;
 hipError_t launch_wide_build(uint32_t n_keys, const void* keys_pk, uint32_t* tabs, uint32_t* bases,
                              uint32_t* scratch, hipStream_t s);
-// k_verify_keyed_go_batch: signatures per lane, and its scratch per lane
-// (kb x 40 words: R'.X, R'.Y, Z and the running product of the Z's)
+// k_verify_keyed_batch: signatures per lane, and its scratch per lane
+// (kb x 40 words: R'.X and R'.Y (Go) or the coset x numerator (ZIP-215), Z,
+// and the running product of the Z's)
 constexpr uint32_t kKeyedBatchScratchWordsPerSig = 40;
 hipError_t launch_verify_sr25519(uint32_t n, const void* pk, const void* sig, const void* msg, const void* off,
                                  const uint32_t* btab, uint32_t* atab, const uint16_t* prog, int nops, void* valid,

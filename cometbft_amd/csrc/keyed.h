@@ -136,7 +136,7 @@ struct CombWindow {
 // The comb half of a registered-key verification: R' = [s]B - [k]A into acc,
 // and whether the key decoded and s is canonical (the final check against
 // R is the caller's: check_R, or the batched encode of
-// k_verify_keyed_go_batch).
+// k_verify_keyed_batch).
 template <class Win>
 CMTV_HD bool keyed_comb(ge_p3& acc, const uint32_t* key_pk, bool key_ok, const uint32_t* sig_ptr, const uint8_t* msg,
                         uint32_t mlen, const uint32_t* ktab, const uint32_t* bcomb) {
@@ -348,7 +348,7 @@ CMTV_HD bool verify_keyed(const uint32_t* key_pk, bool key_ok, const uint32_t* s
 }
 
 // GO_STDLIB's final check from a precomputed 1/Z (Montgomery batch
-// inversion, k_verify_keyed_go_batch): encode(R') == R bytes, exactly as
+// inversion, k_verify_keyed_batch): encode(R') == R bytes, exactly as
 // check_R<MODE_GO_STDLIB> with p3_tobytes' own inversion replaced by zi.
 CMTV_HD bool check_R_go_zi(const fe& X, const fe& Y, const fe& zi, const uint32_t* sig_ptr) {
   fe x, y;

@@ -2,7 +2,7 @@
 // (keyed.h) and the builders of the wide (radix-2^16) key combs.
 //
 //   k_verify_keyed<MODE, COMB>          one signature per lane, final check per lane
-//   k_verify_keyed_go_batch<KB, COMB>   GO_STDLIB, KB signatures per lane, one inversion
+//   k_verify_keyed_batch<MODE, KB, COMB> KB signatures per lane sharing one inversion
 //   k_wide_bases / k_wide_build         the wide combs of a key set
 //
 // COMB selects the tables: kComb256 = the radix-256 combs (64 additions from
@@ -187,18 +187,22 @@ __global__ __launch_bounds__(64, CMTV_KEYED_WAVES_PER_EU) void k_verify_keyed(
   if (threadIdx.x == 0 && out_bitmap) out_bitmap[gid >> 6] = mask;
 }
 
-// GO_STDLIB registered-key verification with KB signatures per lane: the
-// final encode needs 1/Z of every R', and each lane inverts the product of
-// its KB Z's once (Montgomery's trick: one 265-operation inversion and
-// 3 (KB - 1) multiplications instead of KB inversions). Signature
-// s = gid + r * lanes (round r), so every round of a wave covers 64
-// consecutive signatures and one bitmap word. R' (X, Y), Z and the prefix
-// products wait in `scr`, word-major (KB x 40 words per lane: coalesced).
-// An R' with Z = 0 (possible only from an undecodable key's comb, whose
-// verdicts are false anyway) enters the product as 1 so it cannot spoil the
-// lane's other signatures. Verdicts equal verify_keyed<MODE_GO_STDLIB>'s.
-template <int KB, int COMB>
-__global__ __launch_bounds__(64, CMTV_KEYED_WAVES_PER_EU) void k_verify_keyed_go_batch(
+// Registered-key verification with KB signatures per lane sharing one field
+// inversion (Montgomery's trick: one 265-operation inversion and 3 (KB - 1)
+// products instead of KB inversions):
+//   GO_STDLIB: the final encode needs 1/Z of every R' (check_R_go_zi);
+//   ZIP215:    the coset check (verify_core.h zip_coset) replaces decoding R
+//              (a square-root chain per signature); the sign of the one
+//              matching coset point's x needs 1/Z of that point.
+// Signature s = gid + r * lanes (round r), so every round of a wave covers 64
+// consecutive signatures and one bitmap word. Per signature the lane scratch
+// holds (word-major, coalesced) Go: R'.X, R'.Y, Z, prefix product; ZIP: x
+// numerator, -, Z, prefix product. A Z of 0 (possible only from an
+// undecodable key's comb, whose verdicts are false anyway) enters the product
+// as 1 so it cannot spoil the lane's other signatures. Verdicts equal
+// verify_keyed<MODE>'s.
+template <uint32_t MODE, int KB, int COMB>
+__global__ __launch_bounds__(64, CMTV_KEYED_WAVES_PER_EU) void k_verify_keyed_batch(
     uint32_t n, uint32_t n_keys, const uint32_t* __restrict__ key_idx, const uint32_t* __restrict__ sig,
     const uint8_t* __restrict__ msg, const uint32_t* __restrict__ off, const uint32_t* __restrict__ keys_pk,
     const uint8_t* __restrict__ keys_ok, const uint32_t* __restrict__ ktabs, const uint32_t* __restrict__ bcomb,
@@ -206,7 +210,7 @@ __global__ __launch_bounds__(64, CMTV_KEYED_WAVES_PER_EU) void k_verify_keyed_go
   CMTV_KEYED_STAGE
   const uint32_t lanes = gridDim.x * 64u, gid = blockIdx.x * 64u + threadIdx.x;
   DevCombScratch sc{scr, lanes, gid};  // slot j: 10 words at [(j * 10 + i) * lanes + gid]
-  uint32_t okbits = 0;
+  uint32_t okbits = 0;  // per round: bit 0 ok, bits 1-2 the ZIP coset state
 #pragma unroll 1
   for (int r = 0; r < KB; r++) {
     const uint32_t s = gid + (uint32_t)r * lanes;
@@ -219,12 +223,23 @@ __global__ __launch_bounds__(64, CMTV_KEYED_WAVES_PER_EU) void k_verify_keyed_go
     ge_p3 acc;
     bool ok = keyed_comb_dev<COMB>(acc, kid, kin && keys_ok[kid] != 0, keys_pk, sig + 16 * (size_t)i, msg + m0,
                                    m1 - m0, ktabs, bcomb, stage_);
-    const bool zbad = fe_iszero(acc.Z);
-    fe z, one;
-    fe_1(one);
-    fe_select(z, acc.Z, one, zbad);
+    fe z, xn;
+    uint32_t state = 0;
+    if (MODE == MODE_ZIP215) {
+      uint32_t rw[8];
+      load_words(rw, sig + 16 * (size_t)i, 2);  // R
+      state = zip_coset(xn, z, acc, rw);
+    } else {
+      z = acc.Z;
+    }
+    const bool zbad = fe_iszero(z);
+    {
+      fe one;
+      fe_1(one);
+      fe_select(z, z, one, zbad);
+    }
     ok = ok && !zbad && active;
-    okbits |= (ok ? 1u : 0u) << r;
+    okbits |= ((ok ? 1u : 0u) | (state << 1)) << (3 * r);
     // the running product goes through the scratch too, so nothing but
     // okbits stays live across the combs (their register budget is full)
     fe prod;
@@ -234,8 +249,12 @@ __global__ __launch_bounds__(64, CMTV_KEYED_WAVES_PER_EU) void k_verify_keyed_go
       sc.load(4 * (r - 1) + 3, prod);
       fe_mul(prod, prod, z);
     }
-    sc.store(4 * r + 0, acc.X);
-    sc.store(4 * r + 1, acc.Y);
+    if (MODE == MODE_ZIP215) {
+      sc.store(4 * r + 0, xn);
+    } else {
+      sc.store(4 * r + 0, acc.X);
+      sc.store(4 * r + 1, acc.Y);
+    }
     sc.store(4 * r + 2, z);
     sc.store(4 * r + 3, prod);
   }
@@ -250,9 +269,7 @@ __global__ __launch_bounds__(64, CMTV_KEYED_WAVES_PER_EU) void k_verify_keyed_go
     const uint32_t s = gid + (uint32_t)r * lanes;
     const bool active = s < n;
     const uint32_t i = active ? s : n - 1;
-    fe X, Y, z, zi;
-    sc.load(4 * r + 0, X);
-    sc.load(4 * r + 1, Y);
+    fe z, zi;
     sc.load(4 * r + 2, z);
     if (r > 0) {
       fe pre;
@@ -264,8 +281,19 @@ __global__ __launch_bounds__(64, CMTV_KEYED_WAVES_PER_EU) void k_verify_keyed_go
     }
     uint32_t rw[8];
     load_words(rw, sig + 16 * (size_t)i, 2);  // R
-    bool v = check_R_go_zi(X, Y, zi, rw);
-    v = v && ((okbits >> r) & 1u) != 0;
+    const uint32_t bits = okbits >> (3 * r);
+    bool v;
+    if (MODE == MODE_ZIP215) {
+      fe xn;
+      sc.load(4 * r + 0, xn);
+      v = zip_coset_finish((bits >> 1) & 3u, xn, zi, rw[7]);
+    } else {
+      fe X, Y;
+      sc.load(4 * r + 0, X);
+      sc.load(4 * r + 1, Y);
+      v = check_R_go_zi(X, Y, zi, rw);
+    }
+    v = v && (bits & 1u) != 0;
     if (active && out_valid) out_valid[s] = v ? 1 : 0;
     const uint64_t mask = __ballot(v);
     const uint32_t word = s >> 6;
@@ -278,15 +306,21 @@ static void launch_lane(uint32_t mode, uint32_t n, uint32_t n_keys, const uint32
                         const uint8_t* mp, const uint32_t* op, const uint32_t* keys_pk, const uint8_t* keys_ok,
                         const uint32_t* tabs, const uint32_t* bsrc, uint8_t* vp, uint64_t* bp, uint32_t batch_kb,
                         uint32_t* scr, hipStream_t s) {
-  if (mode != MODE_ZIP215 && batch_kb >= 4 && scr) {
-    // GO_STDLIB with batch_kb signatures per lane (k_verify_keyed_go_batch)
+  if (batch_kb >= 4 && scr) {
+    // batch_kb signatures per lane sharing one inversion (k_verify_keyed_batch)
     const dim3 grid((n + 64 * batch_kb - 1) / (64 * batch_kb)), block(64);
-    if (batch_kb >= 8)
-      hipLaunchKernelGGL((k_verify_keyed_go_batch<8, COMB>), grid, block, 0, s, n, n_keys, ki, sgp, mp, op, keys_pk,
-                         keys_ok, tabs, bsrc, scr, vp, bp);
+    if (mode == MODE_ZIP215 && batch_kb >= 8)
+      hipLaunchKernelGGL((k_verify_keyed_batch<MODE_ZIP215, 8, COMB>), grid, block, 0, s, n, n_keys, ki, sgp, mp, op,
+                         keys_pk, keys_ok, tabs, bsrc, scr, vp, bp);
+    else if (mode == MODE_ZIP215)
+      hipLaunchKernelGGL((k_verify_keyed_batch<MODE_ZIP215, 4, COMB>), grid, block, 0, s, n, n_keys, ki, sgp, mp, op,
+                         keys_pk, keys_ok, tabs, bsrc, scr, vp, bp);
+    else if (batch_kb >= 8)
+      hipLaunchKernelGGL((k_verify_keyed_batch<MODE_GO_STDLIB, 8, COMB>), grid, block, 0, s, n, n_keys, ki, sgp, mp,
+                         op, keys_pk, keys_ok, tabs, bsrc, scr, vp, bp);
     else
-      hipLaunchKernelGGL((k_verify_keyed_go_batch<4, COMB>), grid, block, 0, s, n, n_keys, ki, sgp, mp, op, keys_pk,
-                         keys_ok, tabs, bsrc, scr, vp, bp);
+      hipLaunchKernelGGL((k_verify_keyed_batch<MODE_GO_STDLIB, 4, COMB>), grid, block, 0, s, n, n_keys, ki, sgp, mp,
+                         op, keys_pk, keys_ok, tabs, bsrc, scr, vp, bp);
     return;
   }
   const dim3 grid((n + 63) / 64), block(64);

@@ -35,8 +35,8 @@
 namespace {
 
 constexpr uint32_t kChunk = 1u << 18;  // signatures per launch (A-table scratch = kChunk * 1280 B)
-// registered-key lane launches in GO_STDLIB mode take up to this many
-// signatures, KB per lane (k_verify_keyed_go_batch: one field inversion per
+// registered-key lane launches take up to this many signatures, KB per lane
+// (k_verify_keyed_batch, both modes: one field inversion per
 // KB signatures; KB = 8 keeps 2,048 waves = two per SIMD); scratch 160 B per
 // signature, in the lane kernels' scratch buffer
 constexpr uint32_t kKeyedBatchChunk = 1u << 20;
@@ -386,6 +386,9 @@ struct cmtv_ctx {
   uint32_t keyed_wait = cmtv::kKeyedWaitDefault;
   // GO_STDLIB keyed lane launches batch the final inversion (CMTV_KEYED_BATCH=0: off)
   bool keyed_batch = true;
+  // waves a batched launch must keep (CMTV_KEYED_BATCH_MIN_WAVES; 1 batches
+  // any size, the test knob that puts the corpus through the batched kernels)
+  uint32_t keyed_batch_min_waves = kKeyedBatchMinWaves;
   // wide-comb lane kernels stage their rows through LDS by LDS-DMA
   // (keyed_lane.hip kCombWideDma; CMTV_WIDE_DMA=0: plain loads)
   bool wide_dma = true;
@@ -565,13 +568,13 @@ static int enqueue_verify_keyed(cmtv_ctx* ctx, CmtvDev& D, const cmtv_keyset::Pe
   if (n == 0) return CMTV_OK;
   if (fault_hit(ctx) || D.inject_fault) return CMTV_EHIP;
   const bool quad = n <= ctx->keyed_quad_max;
-  // GO_STDLIB lane launches: KB signatures per lane while that still gives
-  // two waves per SIMD (k_verify_keyed_go_batch)
-  const bool batch = !quad && mode != CMTV_MODE_ZIP215 && ctx->keyed_batch;
+  // lane launches: KB signatures per lane sharing one inversion while that
+  // still gives two waves per SIMD (k_verify_keyed_batch; ZIP-215 by coset)
+  const bool batch = !quad && ctx->keyed_batch;
   const size_t chunk = batch ? kKeyedBatchChunk : kChunk;
   auto kb_for = [&](size_t cn) -> uint32_t {  // 4 or 8 (the instantiated forms), else 1
     uint32_t kb = 1;
-    while (kb < 8 && cn >= (size_t)kKeyedBatchMinWaves * 64 * (kb * 2)) kb *= 2;
+    while (kb < 8 && cn >= (size_t)ctx->keyed_batch_min_waves * 64 * (kb * 2)) kb *= 2;
     return batch && kb >= 4 ? kb : 1;
   };
   hipError_t e;
@@ -1105,6 +1108,10 @@ static void read_env(cmtv_ctx* ctx) {
   if (const char* kl = std::getenv("CMTV_FORCE_K_LATE")) ctx->keyed_wait = kl[0] == '1' ? 0u : kKeyedWaitDefault;
   if (const char* kb = std::getenv("CMTV_KEYED_BATCH")) ctx->keyed_batch = kb[0] != '0';
   if (const char* wd = std::getenv("CMTV_WIDE_DMA")) ctx->wide_dma = wd[0] != '0';
+  if (const char* mw = std::getenv("CMTV_KEYED_BATCH_MIN_WAVES")) {
+    const long v = std::strtol(mw, nullptr, 10);
+    if (v >= 1 && v <= (1l << 20)) ctx->keyed_batch_min_waves = (uint32_t)v;
+  }
   ctx->force_rccl = std::getenv("CMTV_FORCE_RCCL") != nullptr;
   ctx->no_rccl = std::getenv("CMTV_NO_RCCL") != nullptr;
 }

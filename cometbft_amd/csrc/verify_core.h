@@ -262,6 +262,118 @@ CMTV_HD bool check_R(const ge_p3& Rp, const uint32_t* sig_ptr) {
   }
 }
 
+// ---------------------------------------------------------------- ZIP-215 by coset
+//
+// ZIP-215's final check, [8](R' - R) = O with R decoded, without decoding R
+// (no square-root chain): the check holds iff R's decoding lies in the coset
+// R' + E[8]. With T8 a point of order 8, E[8] = E[4] u (T8 + E[4]), and
+// adding a point of E[4] only permutes and scales coordinates (a = -1):
+//   + (0, -1): (x, y) -> (-x, -y);  + (i, 0): (x, y) -> (iy, ix);
+//   + (-i, 0): (x, y) -> (-iy, -ix)                     (i = sqrt(-1))
+// So for Q in {R', R' + T8} (projective X:Y:Z) and y_R = R's y (mod p, the
+// non-canonical encodings accepted as in decoding), the coset holds a point
+// with y = y_R iff one of Y, -Y, iX, -iX equals y_R Z; its x is then X, -X,
+// iY, -iY over Z. A point with y = y_R on the curve means R decodes (x^2 is
+// the same square), to the root whose low bit is R's sign bit (x = 0 for
+// either sign), so R's decoding is that coset point iff x = 0 or x has the
+// sign bit. Two matches are the two roots +-x (both in the coset): pass.
+// Equivalence with the decode-and-multiply check: the 1,406-vector corpus
+// and torsion-shifted / sign-flipped / non-canonical R fuzzing against the
+// oracle (tests/test_host_math.py, hostcheck "zipc" mode).
+//
+// zip_coset returns 0 (fail), 2 (pass) or 1 (pass iff xn / z is 0 or has R's
+// sign bit: z is inverted by the caller, in a batch over signatures).
+struct T8Niels {  // (y+x, y-x, 2dxy) of the order-8 point used
+  CMTV_HD void load_fe(int, int c, fe& r) const {
+    const uint32_t k[3][10] = {
+        {0x1afe924, 0x064e10d, 0x3de65cf, 0x1ec4f88, 0x1ae0131, 0x1316ae5, 0x3e92f99, 0x02ef5ff, 0x327e371, 0x0676598},
+        {0x324467d, 0x1c1bdaa, 0x3502e26, 0x0eb112a, 0x2cd374e, 0x174d56e, 0x04ffd60, 0x1a4bbb3, 0x3271c47, 0x168b7cb},
+        {0x3139da9, 0x108e3c9, 0x24d90e1, 0x12c8a83, 0x2f70530, 0x1e35349, 0x1fd626f, 0x1edcea2, 0x3ef68a4, 0x11762b1}};
+#pragma unroll
+    for (int i = 0; i < 10; i++) r.v[i] = c == 0 ? k[0][i] : (c == 1 ? k[1][i] : k[2][i]);
+  }
+};
+
+CMTV_HD uint32_t zip_coset(fe& xn, fe& z, const ge_p3& Rp, const uint32_t rw[8]) {
+  fe yr, sqm1;
+  fe_frombytes(yr, rw);  // bit 255 (the sign) ignored, y >= p accepted
+  fe_const_sqrtm1(sqm1);
+  uint32_t matches = 0;
+  bool have = false;
+  // one base point Q = (X:Y:Z): its four E[4] translates against y_R
+  auto base = [&](const fe& X, const fe& Y, const fe& Z) {
+    fe a, t, iX, iY, cand;
+    fe_mul(a, yr, Z);
+    fe_mul(iX, sqm1, X);
+    fe_mul(iY, sqm1, Y);
+    fe_sub(t, Y, a);
+    const bool c0 = fe_iszero(t);
+    fe_add(t, Y, a);
+    const bool c1 = fe_iszero(t);
+    fe_sub(t, iX, a);
+    const bool c2 = fe_iszero(t);
+    fe_add(t, iX, a);
+    const bool c3 = fe_iszero(t);
+    matches += (uint32_t)c0 + (uint32_t)c1 + (uint32_t)c2 + (uint32_t)c3;
+    // the first match's x numerator: X, -X, iY, -iY
+    fe nX, niY;
+    fe_neg(nX, X);
+    fe_neg(niY, iY);
+    fe_select(cand, niY, iY, c2);
+    fe_select(cand, cand, nX, c1);
+    fe_select(cand, cand, X, c0);
+    const bool take = !have && (c0 || c1 || c2 || c3);
+    fe_select(xn, xn, cand, take);
+    fe_select(z, z, Z, take);
+    have = have || take;
+  };
+  fe_1(z);
+  fe_1(xn);
+  base(Rp.X, Rp.Y, Rp.Z);
+  {
+    ge_efgh t;
+    ge_add_table<false>(t, Rp, T8Niels{}, 0, false, false);  // R' + T8
+    fe X1, Y1, Z1;
+    fe_mul(X1, t.e, t.f);
+    fe_mul(Y1, t.g, t.h);
+    fe_mul(Z1, t.f, t.g);
+    base(X1, Y1, Z1);
+  }
+  if (matches == 0) {
+    fe_1(z);
+    return 0u;
+  }
+  if (matches >= 2) {
+    fe_1(z);
+    return 2u;
+  }
+  return 1u;
+}
+
+// state 1: x = xn zi (zi = 1 / z) is 0 or has R's sign bit (rw7 = R's top word)
+CMTV_HD bool zip_coset_finish(uint32_t state, const fe& xn, const fe& zi, uint32_t rw7) {
+  fe x;
+  fe_mul(x, xn, zi);
+  uint32_t s[8];
+  fe_tobytes(s, x);
+  uint32_t nz = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) nz |= s[i];
+  return state == 2u || (state == 1u && (nz == 0 || (s[0] & 1u) == (rw7 >> 31)));
+}
+
+// check_R<MODE_ZIP215> by coset, one inversion (the batched kernels share it
+// over several signatures instead)
+CMTV_HD bool check_R_zip_coset(const ge_p3& Rp, const uint32_t* sig_ptr) {
+  uint32_t w[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) w[i] = sig_ptr[i];  // R
+  fe xn, z, zi;
+  const uint32_t st = zip_coset(xn, z, Rp, w);
+  fe_invert(zi, z);
+  return zip_coset_finish(st, xn, zi, w[7]);
+}
+
 // Full single-signature verification. pk / sig are read through pointers
 // (little-endian 32-bit words) at the points they are needed, so neither is
 // held in registers across the scalar multiplication.

@@ -8,6 +8,10 @@
 //                       lane kernel's half-size-scalar pipeline)
 //   argv[1] == "keyed": verify input as above, through registered-key combs
 //                       (keyed.h; one comb per distinct pk)
+//   argv[1] == "zipc":  as "keyed", with ZIP-215's final check by coset
+//                       (verify_core.h check_R_zip_coset) instead of decoding R
+//   argv[1] == "coset": n x { u8 rp[32], u8 r[32] } -> n verdicts of the coset
+//                       check for R' = decode(rp) against R bytes r
 #define CMTV_HD inline
 #define CMTV_BOUNDS_CHECK 1
 #include <cstdio>
@@ -72,9 +76,11 @@ int main(int argc, char** argv) {
   const bool sign = argc > 1 && !strcmp(argv[1], "sign");
   const bool keyed = argc > 1 && !strcmp(argv[1], "keyed");
   const bool half = argc > 1 && !strcmp(argv[1], "half");
+  const bool zipc = argc > 1 && !strcmp(argv[1], "zipc");
+  const bool coset = argc > 1 && !strcmp(argv[1], "coset");
   std::vector<uint32_t> bcomb;
   std::map<std::string, std::pair<bool, std::vector<uint32_t>>> combs;
-  if (keyed) {
+  if (keyed || zipc) {
     uint32_t bw[8];
     bool bok;
     basepoint_words(bw);
@@ -97,6 +103,18 @@ int main(int argc, char** argv) {
       fwrite(out, 96, 1, stdout);
       continue;
     }
+    if (coset) {
+      uint8_t rp[32], r[32];
+      if (fread(rp, 32, 1, stdin) != 1 || fread(r, 32, 1, stdin) != 1) return 1;
+      uint32_t rpw[8], rw[8];
+      to_words(rpw, rp, 8);
+      to_words(rw, r, 8);
+      ge_p3 Rp;
+      const bool ok = p3_frombytes(Rp, rpw);
+      uint8_t o = ok && check_R_zip_coset(Rp, rw);
+      fwrite(&o, 1, 1, stdout);
+      continue;
+    }
     uint8_t mode, pk[32], sig[64];
     uint32_t mlen;
     if (fread(&mode, 1, 1, stdin) != 1 || fread(pk, 32, 1, stdin) != 1 || fread(sig, 64, 1, stdin) != 1 ||
@@ -109,7 +127,7 @@ int main(int argc, char** argv) {
     uint32_t pkw[8], sigw[16];
     to_words(pkw, pk, 8);
     to_words(sigw, sig, 16);
-    if (keyed) {
+    if (keyed || zipc) {
       auto it = combs.find(std::string((const char*)pk, 32));
       if (it == combs.end()) {
         bool kok;
@@ -118,8 +136,15 @@ int main(int argc, char** argv) {
       }
       const bool kok = it->second.first;
       const uint32_t* kt = it->second.second.data();
-      bool v = mode ? verify_keyed<MODE_ZIP215, CombWindow>(pkw, kok, sigw, mp, mlen, kt, bcomb.data())
-                    : verify_keyed<MODE_GO_STDLIB, CombWindow>(pkw, kok, sigw, mp, mlen, kt, bcomb.data());
+      bool v;
+      if (zipc && mode) {
+        ge_p3 acc;
+        const bool ok = keyed_comb<CombWindow>(acc, pkw, kok, sigw, mp, mlen, kt, bcomb.data());
+        v = check_R_zip_coset(acc, sigw) && ok;
+      } else {
+        v = mode ? verify_keyed<MODE_ZIP215, CombWindow>(pkw, kok, sigw, mp, mlen, kt, bcomb.data())
+                 : verify_keyed<MODE_GO_STDLIB, CombWindow>(pkw, kok, sigw, mp, mlen, kt, bcomb.data());
+      }
       uint8_t o = v;
       fwrite(&o, 1, 1, stdout);
       continue;

@@ -84,6 +84,82 @@ def test_keyed_pipeline_matches_corpus(hostcheck, corpus, mode):
     assert bad.size == 0, [(idx[int(i)], corpus["cats"][idx[int(i)]]) for i in bad[:10]]
 
 
+def test_zip_coset_check_matches_corpus(hostcheck, corpus):
+    """ZIP-215's final check by coset (verify_core.h zip_coset: R' + E[8]
+    against y_R and R's sign bit, no square root) on the keyed pipeline."""
+    idx = _keyed_subset(corpus)
+    got = _run(hostcheck, "zipc", corpus, idx, 1)
+    want = corpus["zip215"][idx]
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(idx[int(i)], corpus["cats"][idx[int(i)]]) for i in bad[:10]]
+
+
+def test_zip_coset_check_fuzz(hostcheck):
+    """The coset check against decode-R-and-[8](R' - R) (the oracle) for R' =
+    [s]B, [s]B + a torsion point and pure torsion points, and R = every
+    translate R' + T (T in E[8]) with the sign bit as encoded and flipped and
+    the y >= p encoding where one exists, plus random R bytes."""
+    import random
+
+    from oracle import ed25519_ref as E
+
+    P, L = E.P, E.L
+    t8, y = None, 2
+    while t8 is None:  # a point of order 8: [L] of a curve point with full torsion
+        x = E._recover_x(y, 0)
+        if x is not None:
+            q = E.scalar_mult(L, (x, y, 1, x * y % P))
+            r, k = q, 1
+            while not E.is_identity(r) and k < 9:
+                r, k = E.point_add(r, q), k + 1
+            if k == 8:
+                t8 = q
+        y += 1
+    e8 = [E.IDENTITY]
+    for _ in range(7):
+        e8.append(E.point_add(e8[-1], t8))
+
+    def ref(rp, rb):
+        R = E.decode_point(rb)
+        if R is None:
+            return 0
+        d = E.point_add(rp, E.point_neg(R))
+        for _ in range(3):
+            d = E.point_double(d)
+        return int(E.is_identity(d))
+
+    rnd = random.Random(11)
+    cases = []
+    for trial in range(24):
+        rp = E.scalar_mult(rnd.randrange(L), E.B)
+        if trial % 3 == 1:
+            rp = E.point_add(rp, e8[rnd.randrange(1, 8)])
+        if trial % 8 == 2:
+            rp = e8[rnd.randrange(8)]
+        rpb = E.encode_point(rp)
+        rp = E.decode_point(rpb)  # the point the host check decodes
+        for t in e8:
+            enc = E.encode_point(E.point_add(rp, t))
+            for flip in (0, 1):
+                b = bytearray(enc)
+                b[31] ^= 0x80 * flip
+                cases.append((rpb, bytes(b)))
+                v = int.from_bytes(bytes(b), "little")
+                y_, sgn = v & ((1 << 255) - 1), v >> 255
+                if y_ + P < (1 << 255):
+                    cases.append((rpb, ((y_ + P) | (sgn << 255)).to_bytes(32, "little")))
+        for _ in range(4):
+            cases.append((rpb, rnd.getrandbits(256).to_bytes(32, "little")))
+    buf = [struct.pack("<I", len(cases))] + [a + b for a, b in cases]
+    out = subprocess.run([hostcheck, "coset"], input=b"".join(buf), capture_output=True, check=True,
+                         timeout=600).stdout
+    got = np.frombuffer(out, np.uint8)
+    want = np.array([ref(E.decode_point(a), b) for a, b in cases], np.uint8)
+    assert 0 < want.sum() < len(cases)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, bad[:10]
+
+
 @pytest.mark.parametrize("mode", [0, 1])
 def test_oct_pipeline_matches_corpus(quadcheck, corpus, mode):
     """The 8-lane oct kernel's source (oct.h): eight host threads in lockstep,

@@ -39,6 +39,40 @@ def test_corpus_bit_exact_keyed(gpu_ctx, gpu_ctx_quad1, gpu_ctx_lane, corpus, mo
     ks.free()
 
 
+@pytest.mark.parametrize("wide", [False, True])
+def test_corpus_through_the_batched_kernels(corpus, wide):
+    """The whole corpus through k_verify_keyed_batch at KB = 8
+    (CMTV_KEYED_BATCH_MIN_WAVES=1 batches any size): the coset check of
+    ZIP-215 and the shared inversion of GO_STDLIB on every adversarial R
+    (non-canonical, small and mixed order), s and key category."""
+    import os
+
+    from cometbft_amd import Context
+
+    keys = ("CMTV_QUAD_MAX", "CMTV_KEYED_QUAD_MAX", "CMTV_KEYED_BATCH_MIN_WAVES")
+    old = {k: os.environ.get(k) for k in keys}
+    os.environ.update({"CMTV_QUAD_MAX": "0", "CMTV_KEYED_QUAD_MAX": "0", "CMTV_KEYED_BATCH_MIN_WAVES": "1"})
+    try:
+        ctx = Context(device=0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+    uniq, idx = np.unique(corpus["pk"], axis=0, return_inverse=True)
+    ks = ctx.register_keys(uniq, wide=wide)
+    msg, off = pack_messages(corpus["msgs"])
+    for mode, key in ((MODE_GO_STDLIB, "go"), (MODE_ZIP215, "zip215")):
+        valid, words = ctx.verify_indexed(ks, idx.astype(np.uint32).reshape(-1), corpus["sig"], msg, off, mode,
+                                          bitmap=True)
+        bad = np.nonzero(valid != corpus[key])[0]
+        assert bad.size == 0, [(corpus["cats"][i], int(valid[i])) for i in bad[:20]]
+        bits = np.unpackbits(words.view(np.uint8), bitorder="little")[: len(valid)]
+        assert np.array_equal(bits, corpus[key])
+    ks.free()
+
+
 def _valset_commits(n_keys, n_sigs, seed):
     rng = np.random.default_rng(seed)
     seeds = rng.integers(0, 256, (n_keys, 32), dtype=np.uint8)
@@ -123,9 +157,10 @@ def test_keyset_belongs_to_its_context(gpu_ctx, gpu_ctx_lane):
 
 @pytest.mark.parametrize("wide", [False, True])
 @pytest.mark.parametrize("n", [530_000, 1_100_003])
-def test_keyed_go_batch_inversion(gpu_ctx_lane, corpus, n, wide):
-    """k_verify_keyed_go_batch (configs[2]'s GO_STDLIB lane path): KB = 4 / 8
-    signatures per lane share one field inversion (Montgomery's trick). n =
+def test_keyed_batch_inversion(gpu_ctx_lane, corpus, n, wide):
+    """k_verify_keyed_batch (configs[2]'s lane path): KB = 4 / 8 signatures
+    per lane share one field inversion (Montgomery's trick) -- GO_STDLIB's
+    encode of R', ZIP-215's coset check (verify_core.h zip_coset). n =
     530,000 runs the KB = 4 form; 1,100,003 one 2^20 chunk at KB = 8 plus a
     ragged 51,427-signature tail on the plain kernel. The key set mixes 150
     honest keys with the corpus' off-curve keys (their combs are garbage, Z
@@ -167,9 +202,11 @@ def test_keyed_go_batch_inversion(gpu_ctx_lane, corpus, n, wide):
     got = gpu_ctx_lane.verify_indexed(ks, kidx, sig, m, off, MODE_GO_STDLIB)
     bad = np.nonzero(got != exp)[0]
     assert bad.size == 0, (bad[:10], kidx[bad[:10]])
-    if wide:
-        exp_z = coracle.verify_batch(pk[kidx], sig, m, off, MODE_ZIP215, nthreads=16)
-        assert np.array_equal(gpu_ctx_lane.verify_indexed(ks, kidx, sig, m, off, MODE_ZIP215), exp_z)
+    # ZIP-215 through the same batches: the coset check (no decode of R)
+    exp_z = coracle.verify_batch(pk[kidx], sig, m, off, MODE_ZIP215, nthreads=16)
+    got_z = gpu_ctx_lane.verify_indexed(ks, kidx, sig, m, off, MODE_ZIP215)
+    bad = np.nonzero(got_z != exp_z)[0]
+    assert bad.size == 0, (bad[:10], kidx[bad[:10]])
     ks.free()
     keys = ("CMTV_QUAD_MAX", "CMTV_KEYED_QUAD_MAX", "CMTV_KEYED_BATCH", "CMTV_WIDE_DMA")
     old = {k: os.environ.get(k) for k in keys}
@@ -184,4 +221,5 @@ def test_keyed_go_batch_inversion(gpu_ctx_lane, corpus, n, wide):
                 os.environ[k] = v
     ks2 = plain.register_keys(pk, wide=wide)  # wide: rows by plain loads (no LDS-DMA staging)
     assert np.array_equal(plain.verify_indexed(ks2, kidx, sig, m, off, MODE_GO_STDLIB), got)
+    assert np.array_equal(plain.verify_indexed(ks2, kidx, sig, m, off, MODE_ZIP215), got_z)
     ks2.free()

@@ -10,6 +10,8 @@ import subprocess
 import numpy as np
 import pytest
 
+from tests.host import hostbuild
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "tests", "host", "hostcheck.cpp")
 BIN = os.path.join(ROOT, "build", "hostcheck")
@@ -28,12 +30,7 @@ def quadcheck():
 
 
 def _build(src, binary, flags):
-    os.makedirs(os.path.dirname(binary), exist_ok=True)
-    hdr = os.path.join(ROOT, "cometbft_amd", "csrc")
-    deps = [src] + [os.path.join(hdr, f) for f in os.listdir(hdr) if f.endswith(".h")]
-    if not os.path.exists(binary) or os.path.getmtime(binary) < max(os.path.getmtime(d) for d in deps):
-        subprocess.run(["g++", "-O2"] + flags + ["-o", binary, src], check=True)
-    return binary
+    return hostbuild.build(src, binary, flags)
 
 
 def _run(binary, arg, corpus, idx, mode):

@@ -17,6 +17,8 @@ import subprocess
 import numpy as np
 import pytest
 
+from tests.host import hostbuild
+
 from oracle import coracle as C
 from oracle import sr25519_ref as S
 
@@ -44,12 +46,7 @@ def vectors(doc):
 
 @pytest.fixture(scope="module")
 def srcheck():
-    os.makedirs(os.path.dirname(BIN), exist_ok=True)
-    hdr = os.path.join(ROOT, "cometbft_amd", "csrc")
-    deps = [SRC] + [os.path.join(hdr, f) for f in os.listdir(hdr) if f.endswith(".h")]
-    if not os.path.exists(BIN) or os.path.getmtime(BIN) < max(os.path.getmtime(d) for d in deps):
-        subprocess.run(["g++", "-O2", "-std=c++17", "-o", BIN, SRC], check=True)
-    return BIN
+    return hostbuild.build(SRC, BIN, ["-std=c++17"])
 
 
 def test_keccak_matches_sha3():
@@ -188,10 +185,7 @@ def test_quad_pipeline_matches_corpus(vectors):
     """sr25519_quad.h (the quad kernel's source: half-size scalars, E[4]
     final check), four host threads in lockstep for the DPP exchanges, over
     every non-honest vector and a slice of the honest ones."""
-    hdr = os.path.join(ROOT, "cometbft_amd", "csrc")
-    deps = [QSRC] + [os.path.join(hdr, f) for f in os.listdir(hdr) if f.endswith(".h")]
-    if not os.path.exists(QBIN) or os.path.getmtime(QBIN) < max(os.path.getmtime(d) for d in deps):
-        subprocess.run(["g++", "-O2", "-std=c++20", "-pthread", "-o", QBIN, QSRC], check=True)
+    hostbuild.build(QSRC, QBIN, ["-std=c++20", "-pthread"])
     cats = vectors["cats"]
     idx = [i for i, c in enumerate(cats) if c != "honest"] + [i for i, c in enumerate(cats) if c == "honest"][::3]
     got = np.frombuffer(_run_srcheck(QBIN, vectors, sorted(idx), "sr"), np.uint8)
@@ -207,10 +201,7 @@ def test_split_quad_pipeline_matches_corpus(vectors):
     digits at lookup (q_straus_prep_b<true, true>) -- over the whole corpus,
     with both signs of k2 represented. Every radix-16 digit value, including
     dR = 0 and dR = -8, occurs in the corpus' ~10k windows."""
-    hdr = os.path.join(ROOT, "cometbft_amd", "csrc")
-    deps = [QSRC] + [os.path.join(hdr, f) for f in os.listdir(hdr) if f.endswith(".h")]
-    if not os.path.exists(QBIN) or os.path.getmtime(QBIN) < max(os.path.getmtime(d) for d in deps):
-        subprocess.run(["g++", "-O2", "-std=c++20", "-pthread", "-o", QBIN, QSRC], check=True)
+    hostbuild.build(QSRC, QBIN, ["-std=c++20", "-pthread"])
     idx = list(range(len(vectors["cats"])))
     buf = _srcheck_input(vectors, idx)
     r = subprocess.run([QBIN, "sr2"], input=buf, capture_output=True, check=True, timeout=600)

@@ -18,6 +18,14 @@ constexpr uint32_t kCombScratchWordsPerKey = 128 * 320;  // prefix products whil
 // the oct kernel (with kLaunchQuad; Ed25519 only) and its two-wave form
 // (kLaunchOctSplit), and the quad kernel's helper-wave form (kLaunchQuadSplit)
 constexpr uint32_t kLaunchQuad = 1, kLaunchForceWide = 2, kLaunchOct = 4, kLaunchOctSplit = 8, kLaunchQuadSplit = 16;
+// the one-signature-per-wave row kernel (row.h, k_verify_row_split; Ed25519)
+constexpr uint32_t kLaunchRow = 32;
+
+// Row kernel bitmap assembly: each launch takes one of kRowSlots slots of a
+// per-device ring (kRowSlotWords words: word 0 a wave counter the kernel
+// resets, then one verdict byte per signature); the last wave to finish packs
+// the bitmap words from the slot's bytes. kRowMaxCap bounds a row launch.
+constexpr uint32_t kRowSlots = 32, kRowSlotWords = 1024, kRowMaxCap = 4 * (kRowSlotWords - 16);
 
 // Templated sign-bytes (signbytes.h) written by the helper waves of the
 // split kernels themselves (k_verify_oct_split / k_verify_quad_split): each
@@ -45,9 +53,11 @@ constexpr uint32_t kKeyedWaitDefault = 1u << 22;
 hipError_t launch_btab_init(uint32_t* d_rows, hipStream_t s);
 // sb (may be null) is honoured only by the split kernels (kLaunchOctSplit,
 // kLaunchQuadSplit); the caller launches k_sign_bytes otherwise
+// (and by the row kernel, kLaunchRow, which needs row_slot: one slot of the
+// device's ring when bitmap is set)
 hipError_t launch_verify(uint32_t mode, uint32_t n, const void* pk, const void* sig, const void* msg,
                          const void* off, const uint32_t* btab, uint32_t* atab, void* valid, void* bitmap,
-                         uint32_t kflags, hipStream_t s, const SbFuse* sb = nullptr);
+                         uint32_t kflags, hipStream_t s, const SbFuse* sb = nullptr, uint32_t* row_slot = nullptr);
 hipError_t launch_comb_build(uint32_t n_keys, const void* keys_pk, uint8_t* keys_ok, uint32_t* tabs,
                              uint32_t* scratch, bool negate, hipStream_t s);
 hipError_t launch_verify_keyed(uint32_t mode, uint32_t n, uint32_t n_keys, const void* key_idx, const void* sig,

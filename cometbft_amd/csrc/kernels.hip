@@ -345,6 +345,86 @@ __global__ __launch_bounds__(128, CMTV_QUAD_WAVES_PER_EU) void k_verify_oct_spli
   if (t == 0 && out_bitmap) reinterpret_cast<uint8_t*>(out_bitmap)[gid >> 6] = (uint8_t)x;
 }
 
+// One signature per wave (row.h): for the smallest batches (a 150-validator
+// commit), where SIMDs are idle and each signature's chain of field products
+// is the kernel time. A 4-wave workgroup takes 3 signatures: waves 0-2
+// decode A and R (rows 0/2 and 1/3) and build their tables while wave 3's
+// lanes 0-2 hash and split the scalars (q_prepare, the templated sign-bytes
+// included); the scalars reach them at barrier 1 and [u]B (q_bcomb16, as
+// four canonical encodings) at barrier 2, after which wave 3 exits. LDS:
+// 3 x 9 KiB tables, one workgroup per CU, i.e. one wave per SIMD.
+// Verdicts: lane 0 of each wave writes its byte to out_valid and to the
+// launch's ring slot; the last wave to finish (an agent-scope counter) packs
+// the bitmap words and resets the counter.
+template <uint32_t MODE>
+__global__ __launch_bounds__(256, 1) void k_verify_row_split(
+    uint32_t n, const uint32_t* __restrict__ pk, const uint32_t* __restrict__ sig, const uint8_t* __restrict__ msg,
+    const uint32_t* __restrict__ off, const uint32_t* __restrict__ btab, uint8_t* __restrict__ out_valid,
+    uint64_t* __restrict__ out_bitmap, uint32_t force_wide, SbFuse sb, uint32_t* __restrict__ slot) {
+  const uint32_t wave = threadIdx.x >> 6, t = threadIdx.x & 63;
+  const uint32_t base = blockIdx.x * 3;
+  __shared__ uint32_t prep[3][SIG_PREP_WORDS + 1];
+  __shared__ uint32_t bpt[3][32];
+  __shared__ uint32_t tab_lds[3][kRowTabWords];
+  __shared__ uint32_t sbm[3][kSbFuseMaxMsg / 4];
+  if (wave == 3) {
+    const uint32_t ls = t < 3 ? t : 2;
+    const uint32_t s = base + ls;
+    const uint32_t i = s < n ? s : n - 1;
+    const uint8_t* mp;
+    uint32_t ml;
+    helper_message(sb, i, msg, off, sbm[ls], mp, ml);
+    SigPrep p;
+    q_prepare<MODE>(p, pk + 8 * (size_t)i, sig + 16 * (size_t)i, mp, ml, force_wide != 0);
+    if (t < 3) sig_prep_store(prep[t], p);
+    __syncthreads();  // 1: the scalars
+    ge_p3 B;
+    q_bcomb16(B, p.u, DevBTab{btab});
+    if (t < 3) bpoint_store_bytes(bpt[t], B);
+    __syncthreads();  // 2: [u]B
+    return;
+  }
+  const uint32_t s = base + wave;
+  const bool active = s < n;
+  const uint32_t i = active ? s : n - 1;
+  const uint32_t* pkp = pk + 8 * (size_t)i;
+  const uint32_t* sgp = sig + 16 * (size_t)i;
+  uint32_t pkw[8], sigw[8];
+  load_words(pkw, pkp, 2);
+  load_words(sigw, sgp, 2);
+  const uint32_t limb = reinterpret_cast<const uint16_t*>(((t >> 4) & 1) ? sgp : pkp)[t & 15];
+  DevRowTab tab{tab_lds[wave], t};
+  const uint32_t* bq = bpt[wave];
+  bool v = r_verify_split<MODE>(
+      DevRow(), limb, pkw, sigw, tab,
+      [&](SigPrep& p) {
+        __syncthreads();
+        sig_prep_load(p, prep[wave]);
+      },
+      [&]() -> uint32_t {
+        __syncthreads();
+        return (bq[8 * (t >> 4) + ((t & 15) >> 1)] >> (16 * (t & 1))) & 0xFFFFu;
+      });
+  v = v && active;
+  if (t == 0 && active && out_valid) out_valid[s] = v ? 1 : 0;
+  if (!out_bitmap) return;
+  uint8_t* vb = reinterpret_cast<uint8_t*>(slot + 16);
+  if (t == 0 && active) vb[s] = v ? 1 : 0;
+  __threadfence();
+  uint32_t ticket = 0;
+  if (t == 0) ticket = __hip_atomic_fetch_add(slot, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+  ticket = __shfl(ticket, 0);
+  if (ticket != 3 * gridDim.x - 1) return;
+  __threadfence();
+  const uint32_t words = (n + 63) / 64;
+  for (uint32_t w = t; w < words; w += 64) {
+    uint64_t m = 0;
+    for (uint32_t b = 0; b < 64 && 64 * w + b < n; b++) m |= (uint64_t)(vb[64 * w + b] != 0) << b;
+    out_bitmap[w] = m;
+  }
+  if (t == 0) __hip_atomic_store(slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Comb of (negate ? -P : P) for n_keys encoded points; workgroup = key,
 // thread = multiple d = 1..128. keys_ok[key] records whether P decoded.
 __global__ __launch_bounds__(128) void k_comb_build(const uint32_t* __restrict__ keys_pk, uint8_t* __restrict__ keys_ok,
@@ -430,7 +510,7 @@ hipError_t launch_btab_init(uint32_t* d_rows, hipStream_t s) {
 
 hipError_t launch_verify(uint32_t mode, uint32_t n, const void* pk, const void* sig, const void* msg,
                          const void* off, const uint32_t* btab, uint32_t* atab, void* valid, void* bitmap,
-                         uint32_t kflags, hipStream_t s, const SbFuse* sb) {
+                         uint32_t kflags, hipStream_t s, const SbFuse* sb, uint32_t* row_slot) {
   const SbFuse fz = sb ? *sb : SbFuse{};
   const bool quad = kflags & kLaunchQuad;
   const uint32_t fw = (kflags & kLaunchForceWide) ? 1u : 0u;
@@ -441,6 +521,18 @@ hipError_t launch_verify(uint32_t mode, uint32_t n, const void* pk, const void* 
   auto op = static_cast<const uint32_t*>(off);
   auto vp = static_cast<uint8_t*>(valid);
   auto bp = static_cast<uint64_t*>(bitmap);
+  if (kflags & kLaunchRow) {
+    // 3 signatures per 256-lane block (3 row waves + the helper)
+    if (n > kRowMaxCap || (bp && !row_slot)) return hipErrorInvalidValue;
+    const dim3 grid((n + 2) / 3), block(256);
+    if (mode == MODE_ZIP215)
+      hipLaunchKernelGGL(k_verify_row_split<MODE_ZIP215>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp, fw,
+                         fz, row_slot);
+    else
+      hipLaunchKernelGGL(k_verify_row_split<MODE_GO_STDLIB>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp,
+                         fw, fz, row_slot);
+    return hipGetLastError();
+  }
   if (quad && (kflags & kLaunchOctSplit)) {
     // one 128-lane block (2 waves) = 8 signatures; whole groups of 8 blocks
     const dim3 grid(((n + 63) / 64) * 8), block(128);

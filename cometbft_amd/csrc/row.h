@@ -1,0 +1,479 @@
+// row.h -- one signature per wavefront ("row" layout) for latency-bound
+// batches: a field element of GF(2^255-19) lives in one 16-lane DPP row, in
+// radix 2^16 (lane k of the row holds limb k), and the four rows of a wave
+// hold the four extended coordinates (X, Y, Z, T) of a point.
+//
+// Why: at 150 signatures the chip has ~7 SIMDs per signature and the oct and
+// quad kernels are bound by one lane's chain of field products (DESIGN.md
+// 4.3: ~4.4 cycles per VALU instruction, one wave per SIMD). Here one product
+// is 16 column terms per lane -- a DPP row_ror:r of f (lane k gets f_{k-r}), a
+// DPP row_newbcast:r of g (every lane gets g_r), a 24-bit twist (x 38 where
+// the column wraps past 2^256) and a v_mad_u64_u32 -- plus three carry rounds
+// whose carries move by row_ror:1: 76 VALU instructions for all four
+// coordinates' products, against 107 (squaring) / 130 (product) per lane in
+// the quad layout; every add, subtract and select is one instruction per
+// lane instead of ten; and the cross-coordinate moves of the point formulas
+// are v_permlane16/32_swap row exchanges.
+//
+// Column k of h = f g mod p (2^256 = 38 mod p):
+//   h_k = sum_r f_{(k-r) mod 16} g_r  (x 38 when r > k)
+// Bounds (asserted by tests/host/rowcheck.cpp): multiplication inputs below
+// 2^19.37 per limb (the first carry of a column then fits 32 bits); products
+// leave limbs below 2^16 + 2^10.6 ("carried"); subtraction adds 4p (limbs of
+// 4p are >= 0x1FFFC, above any carried limb).
+//
+// Everything is written against a row policy R:
+//   R::U / R::U64 / R::B     this lane's u32 / u64 / bool (the host test
+//                            policy: 64-lane arrays, tests/host/rowcheck.cpp)
+//   R::lane()                0..63
+//   R::ror<r>(x)             lane k of a row gets lane (k - r) mod 16 of it
+//   R::bcast<r>(x)           every lane of a row gets lane r of it
+//   R::rows(x, b0..b3)       b_c = row c of x broadcast to all four rows
+//   R::ballot(b)             64-bit mask of b over the wave
+// with free functions mad64(a, b, c) = a b + c (u64), lo32, shr64(x, s) (low
+// word of x >> s), mul24, sel(c, a, b). Control flow is wave-uniform.
+#pragma once
+#include "quad.h"
+
+namespace cmtv {
+
+// the lane-vector primitives on one lane's scalars (the device policy; the
+// host test policy overloads them for 64-lane arrays)
+CMTV_HD uint64_t widen(uint32_t a) { return a; }
+CMTV_HD uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) { return (uint64_t)a * b + c; }
+CMTV_HD uint32_t lo32(uint64_t a) { return (uint32_t)a; }
+CMTV_HD uint32_t shr64(uint64_t a, int s) { return (uint32_t)(a >> s); }
+// a b for a, b < 2^24: v_mul_u32_u24 (full rate; v_mul_lo_u32 is quarter rate)
+CMTV_HD uint32_t mul24(uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __umul24(a, b);
+#else
+  return a * b;
+#endif
+}
+template <class T>
+CMTV_HD T sel(bool c, const T& a, const T& b) {
+  return c ? a : b;
+}
+
+// 16-bit limbs of the curve constants
+struct RowConst {
+  static constexpr uint16_t d[16] = {0x78a3, 0x1359, 0x4dca, 0x75eb, 0xd8ab, 0x4141, 0x0a4d, 0x0070,
+                                     0xe898, 0x7779, 0x4079, 0x8cc7, 0xfe73, 0x2b6f, 0x6cee, 0x5203};
+  static constexpr uint16_t d2[16] = {0xf159, 0x26b2, 0x9b94, 0xebd6, 0xb156, 0x8283, 0x149a, 0x00e0,
+                                      0xd130, 0xeef3, 0x80f2, 0x198e, 0xfce7, 0x56df, 0xd9dc, 0x2406};
+  static constexpr uint16_t sqrtm1[16] = {0xa0b0, 0x4a0e, 0x1b27, 0xc4ee, 0xe478, 0xad2f, 0x1806, 0x2f43,
+                                          0xd7a7, 0x3dfb, 0x0099, 0x2b4d, 0xdf0b, 0x4fc1, 0x2480, 0x2b83};
+};
+
+// Per-lane constants of a wave, computed once (loop-invariant vectors).
+template <class R>
+struct RowCtx {
+  using U = typename R::U;
+  using B = typename R::B;
+  U k;        // limb index (lane & 15)
+  U c;        // row index (lane >> 4)
+  U bias;     // limb k of 4p
+  U m38;      // 38 on limb 0 (the carry out of limb 15 wraps as x 38), else 1
+  U one;      // the constant 1 (limb 0)
+  B r0, r1, r2, r3;
+  CMTV_HD explicit RowCtx(const U& lane) {
+    k = lane & 15u;
+    c = lane >> 4;
+    bias = sel(k == 0u, U(4u * 0xFFEDu), sel(k == 15u, U(4u * 0x7FFFu), U(4u * 0xFFFFu)));
+    m38 = sel(k == 0u, U(38u), U(1u));
+    one = sel(k == 0u, U(1u), U(0u));
+    r0 = c == 0u;
+    r1 = c == 1u;
+    r2 = c == 2u;
+    r3 = c == 3u;
+  }
+  CMTV_HD U cst(const uint16_t* tab) const { return R::load_const(tab, k); }
+};
+
+// ---- the product -------------------------------------------------------------
+
+// three carry rounds of the column sums (< 2^48): limbs end below 2^16 + 2^10.6
+template <class R>
+CMTV_HD typename R::U rf_carry64(const RowCtx<R>& x, const typename R::U64& c) {
+  using U = typename R::U;
+  U lo = lo32(c) & 0xFFFFu;
+  U ca = R::template ror<1>(shr64(c, 16));  // lane k gets the carry of lane k-1
+  typename R::U64 cc = mad64(ca, x.m38, widen(lo));
+  lo = lo32(cc) & 0xFFFFu;
+  ca = R::template ror<1>(shr64(cc, 16));  // < 2^21.3
+  U w = mul24(ca, x.m38) + lo;             // < 2^26.6
+  lo = w & 0xFFFFu;
+  ca = R::template ror<1>(w >> 16);
+  return mul24(ca, x.m38) + lo;
+}
+
+// the same on 32-bit limbs below 2^26 (sums of a few carried values)
+template <class R>
+CMTV_HD typename R::U rf_carry32(const RowCtx<R>& x, const typename R::U& w0) {
+  using U = typename R::U;
+  U lo = w0 & 0xFFFFu;
+  U ca = R::template ror<1>(w0 >> 16);
+  U w = mul24(ca, x.m38) + lo;
+  lo = w & 0xFFFFu;
+  ca = R::template ror<1>(w >> 16);
+  return mul24(ca, x.m38) + lo;
+}
+
+template <class R, int r>
+CMTV_HD void rf_terms(const RowCtx<R>& x, typename R::U64& acc, const typename R::U& f, const typename R::U& g) {
+  if constexpr (r < 16) {
+    using U = typename R::U;
+    const U fr = R::template ror<r>(f);
+    const U gb = R::template bcast<r>(g);
+    const U tw = sel(x.k < (uint32_t)r, U(38u), U(1u));  // the column wraps past 2^256
+    acc = mad64(fr, mul24(gb, tw), acc);
+    rf_terms<R, r + 1>(x, acc, f, g);
+  }
+}
+
+// h = f g (each row its own product)
+template <class R>
+CMTV_HD typename R::U rf_mul(const RowCtx<R>& x, const typename R::U& f, const typename R::U& g) {
+  typename R::U64 acc = mad64(f, R::template bcast<0>(g), widen(typename R::U(0u)));
+  rf_terms<R, 1>(x, acc, f, g);
+  return rf_carry64(x, acc);
+}
+
+template <class R>
+CMTV_HD typename R::U rf_sq(const RowCtx<R>& x, const typename R::U& f) {
+  return rf_mul(x, f, f);
+}
+
+template <class R>
+CMTV_HD typename R::U rf_sqn(const RowCtx<R>& x, typename R::U f, int n) {
+#pragma unroll 1
+  for (int i = 0; i < n; i++) f = rf_sq(x, f);
+  return f;
+}
+
+// a - b + 4p (b carried); -a
+template <class R>
+CMTV_HD typename R::U rf_sub(const RowCtx<R>& x, const typename R::U& a, const typename R::U& b) {
+  return a + (x.bias - b);
+}
+template <class R>
+CMTV_HD typename R::U rf_neg(const RowCtx<R>& x, const typename R::U& a) {
+  return x.bias - a;
+}
+
+// ---- canonical tests -----------------------------------------------------------
+
+// Whether the row's value is 0 mod p, and the parity of its canonical
+// representative (Go's IsNegative). Every lane of the row gathers the 16
+// limbs (row_newbcast) and normalises them serially; the result is uniform
+// within a row. Limbs may be any value below 2^26.
+template <class R>
+struct RowCanon {
+  typename R::B zero, odd;
+};
+
+template <class R, int r>
+CMTV_HD void rf_gather(typename R::U* l, const typename R::U& f) {
+  if constexpr (r < 16) {
+    l[r] = R::template bcast<r>(f);
+    rf_gather<R, r + 1>(l, f);
+  }
+}
+
+template <class R>
+CMTV_HD void rf_ripple(typename R::U* l, typename R::U& c) {
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const typename R::U t = l[i] + c;
+    l[i] = t & 0xFFFFu;
+    c = t >> 16;
+  }
+}
+
+template <class R>
+CMTV_HD RowCanon<R> rf_canon(const typename R::U& f) {
+  using U = typename R::U;
+  U l[16];
+  rf_gather<R, 0>(l, f);
+  U c(0u);
+  rf_ripple<R>(l, c);  // limbs < 2^16, carry out < 2^11
+#pragma unroll 1
+  for (int pass = 0; pass < 2; pass++) {
+    l[0] = l[0] + c * 38u;
+    c = U(0u);
+    rf_ripple<R>(l, c);
+  }
+  // value V < 2^256; fold bit 255: V' = V mod 2^255 + 19 (V >> 255) < 2^255 + 19
+  const U h = l[15] >> 15;
+  l[15] = l[15] & 0x7FFFu;
+  c = h * 19u;
+  rf_ripple<R>(l, c);  // no carry out: V' < 2^255 + 19
+  // V' >= p  <=>  V' + 19 >= 2^255
+  U w[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) w[i] = l[i];
+  c = U(19u);
+  rf_ripple<R>(w, c);
+  const typename R::B ge = (w[15] >> 15) != 0u;
+  U acc(0u);
+#pragma unroll
+  for (int i = 0; i < 16; i++) acc = acc | sel(ge, i == 15 ? (w[i] & 0x7FFFu) : w[i], l[i]);
+  RowCanon<R> out;
+  out.zero = acc == 0u;
+  out.odd = (sel(ge, w[0], l[0]) & 1u) != 0u;
+  return out;
+}
+
+// ---- points: four rows = (X, Y, Z, T) ---------------------------------------------
+
+// Doubling (quad.h q_dbl with rows for lanes): round 1 squares {X, Y, Z, X+Y},
+// round 2 multiplies each row's U = {F', S, M, E'} by the row {E', M, F', S}.
+template <class R>
+CMTV_HD void rp_dbl(const RowCtx<R>& x, typename R::U& v) {
+  using U = typename R::U;
+  const U m3 = sel(x.r3, U(~0u), U(0u));
+  const U sh = sel(x.r0, U(1u), U(0u));
+  const U n2 = sel(x.r1 || x.r3, U(0u), U(~0u));
+  const U n3 = m3;
+  const U mo = sel(x.r0 || x.r3, U(~0u), U(0u));
+  const U corr = sel(x.r1, U(0u), U(1u));
+  U b0, b1, b2, b3;
+  R::rows(v, b0, b1, b2, b3);
+  U m = sel(x.r3, b0, v) + (b1 & m3);  // X, Y, Z, X + Y
+  m = rf_sq(x, m);                     // A, B, C', K
+  R::rows(m, b0, b1, b2, b3);
+  const U a = sel(x.r0, b2, b0);       // C', A, A, A
+  // F' = 2C' + A - B, S = A + B, M = A - B, E' = A + B - K (+ 4p)
+  m = (a << sh) + (b1 ^ n2) + ((m ^ n3) & mo) + corr + x.bias;
+  R::rows(m, b0, b1, b2, b3);
+  const U pr = sel(x.r0, b3, sel(x.r1, b2, sel(x.r2, b0, b1)));  // E', M, F', S
+  v = rf_mul(x, m, pr);
+}
+
+// v += Q, c = this row's coordinate of Q in cached form (Y-X, Y+X, 2Z, 2dT)
+// (quad.h q_add with rows for lanes)
+template <class R>
+CMTV_HD void rp_add(const RowCtx<R>& x, typename R::U& v, const typename R::U& c) {
+  using U = typename R::U;
+  const U m0 = sel(x.r0, U(~0u), U(0u));
+  const U m01 = sel(x.r0 || x.r1, U(~0u), U(0u));
+  const U m23 = sel(x.r2 || x.r3, U(~0u), U(0u));
+  U b0, b1, b2, b3;
+  R::rows(v, b0, b1, b2, b3);
+  const U y = sel(x.r0, b1, sel(x.r1, b0, v));  // Y, X, Z, T
+  U p = v + ((y ^ m0) & m01) + sel(x.r0, x.bias + 1u, U(0u));  // X - Y, Y + X, Z, T
+  const U t = rf_mul(x, p, c);                                  // -A, B, D, C
+  R::rows(t, b0, b1, b2, b3);
+  const typename R::B e03 = x.r0 || x.r3;
+  const U xx = sel(e03, b1, b2);  // B, D, D, B
+  const U yy = sel(e03, b0, b3);  // -A, C, C, -A
+  p = xx + (yy ^ m23) + sel(x.r2 || x.r3, x.bias + 1u, U(0u));  // E, G, F, H
+  R::rows(p, b0, b1, b2, b3);
+  const U pr = sel(x.r0, b2, sel(x.r1, b3, sel(x.r2, b1, b0)));  // F, H, G, E
+  v = rf_mul(x, p, pr);
+}
+
+// this row's cached coordinate (Y-X, Y+X, 2Z, 2dT) of the extended point v
+template <class R>
+CMTV_HD typename R::U rp_to_cached(const RowCtx<R>& x, const typename R::U& v, const typename R::U& d2) {
+  using U = typename R::U;
+  U b0, b1, b2, b3;
+  R::rows(v, b0, b1, b2, b3);
+  const U dt = rf_mul(x, v, d2);  // row 3: 2dT
+  return sel(x.r0, rf_sub(x, b1, b0), sel(x.r1, b1 + b0, sel(x.r2, v + v, dt)));
+}
+
+// the negated cached point: (Y+X, Y-X, 2Z, -2dT)
+template <class R>
+CMTV_HD typename R::U rp_cached_neg(const RowCtx<R>& x, const typename R::U& c) {
+  using U = typename R::U;
+  U b0, b1, b2, b3;
+  R::rows(c, b0, b1, b2, b3);
+  return sel(x.r0, b1, sel(x.r1, b0, sel(x.r3, rf_sub(x, U(0u), rf_carry32(x, c)), c)));
+}
+
+// the identity (0, 1, 1, 0) and its cached form (1, 1, 2, 0)
+template <class R>
+CMTV_HD typename R::U rp_identity(const RowCtx<R>& x) {
+  using U = typename R::U;
+  return sel((x.r1 || x.r2) && (x.k == 0u), U(1u), U(0u));
+}
+template <class R>
+CMTV_HD typename R::U rp_cached_identity(const RowCtx<R>& x) {
+  using U = typename R::U;
+  return sel(x.k == 0u, sel(x.r2, U(2u), sel(x.r3, U(0u), U(1u))), U(0u));
+}
+
+// ---- decompression --------------------------------------------------------------
+
+// Go 1.19 Point.SetBytes (ge25519.h p3_frombytes) on every row at once: y =
+// the row's limbs (bit 255 already cleared, non-canonical y taken mod p), sign
+// = its sign bit. Returns the decode flag; xo, to = x and x y (carried).
+template <class R>
+CMTV_HD typename R::B rf_decode(const RowCtx<R>& x, const typename R::U& y, const typename R::B& sign,
+                                typename R::U& xo, typename R::U& to) {
+  using U = typename R::U;
+  const U y2 = rf_sq(x, y);
+  const U u = rf_carry32(x, rf_sub(x, y2, x.one));                     // y^2 - 1
+  const U v = rf_carry32(x, rf_mul(x, y2, x.cst(RowConst::d)) + x.one);  // d y^2 + 1
+  U t = rf_sq(x, v);                  // v^2
+  U r0 = rf_mul(x, t, v);             // v^3
+  t = rf_sq(x, t);                    // v^4
+  r0 = rf_mul(x, u, r0);              // u v^3
+  t = rf_mul(x, r0, t);               // u v^7
+  // (u v^7)^((p-5)/8) (fe25519.h fe_pow22523)
+  {
+    const U z = t;
+    U t0, t1, t2, z2, z9, z11;
+    z2 = rf_sq(x, z);
+    t0 = rf_sqn(x, z2, 2);
+    z9 = rf_mul(x, t0, z);
+    z11 = rf_mul(x, z9, z2);
+    t0 = rf_mul(x, rf_sq(x, z11), z9);  // 2^5 - 1
+    t1 = rf_sqn(x, t0, 5);
+    t0 = rf_mul(x, t1, t0);             // 2^10 - 1
+    t1 = rf_sqn(x, t0, 10);
+    t1 = rf_mul(x, t1, t0);             // 2^20 - 1
+    t2 = rf_sqn(x, t1, 20);
+    t1 = rf_mul(x, t2, t1);             // 2^40 - 1
+    t1 = rf_sqn(x, t1, 10);
+    t0 = rf_mul(x, t1, t0);             // 2^50 - 1
+    t1 = rf_sqn(x, t0, 50);
+    t1 = rf_mul(x, t1, t0);             // 2^100 - 1
+    t2 = rf_sqn(x, t1, 100);
+    t1 = rf_mul(x, t2, t1);             // 2^200 - 1
+    t1 = rf_sqn(x, t1, 50);
+    t1 = rf_mul(x, t1, t0);             // 2^250 - 1
+    t1 = rf_sqn(x, t1, 2);
+    t = rf_mul(x, t1, z);               // (p-5)/8
+  }
+  r0 = rf_mul(x, r0, t);          // r = u v^3 (u v^7)^((p-5)/8)
+  t = rf_mul(x, rf_sq(x, r0), v);  // v r^2
+  const RowCanon<R> correct = rf_canon<R>(rf_sub(x, t, u));
+  const RowCanon<R> flipped = rf_canon<R>(t + u);
+  r0 = sel(flipped.zero, rf_mul(x, r0, x.cst(RowConst::sqrtm1)), r0);
+  // Absolute(): the even root; then the sign bit picks the negative one
+  const RowCanon<R> rc = rf_canon<R>(r0);
+  const typename R::B neg = rc.odd != sign;
+  r0 = sel(neg, rf_carry32(x, rf_neg(x, r0)), r0);
+  xo = r0;
+  to = rf_mul(x, r0, y);
+  return correct.zero || flipped.zero;
+}
+
+// ---- verification ------------------------------------------------------------------
+
+// Table policy: (0..8)P and (0..8)(-P) in cached form, one u32 per lane per
+// entry (LDS on the device):
+//   void store(int tbl, int neg, int e, const U& c);  U load(int tbl, int neg, int e) const;
+
+// X = [u]B + [k1](-A) + [|k2|](k2 < 0 ? R : -R) = [k2](R' - R) (quad.h
+// q_straus_prep_b<EXT_B, PREBUILT>) and the final check of the mode, one
+// signature per wave. pk16 / sig16: this lane's 16-bit limb of A / R (row
+// c & 1: 0 = A, 1 = R), pkw / sigw: the 8 words of A / R (uniform).
+// get_prep(SigPrep&) supplies the helper's scalars, get_b() this row's cached
+// coordinate of [u]B.
+template <uint32_t MODE, class R, class Tab, class GetPrep, class GetB>
+CMTV_HD bool r_verify_split(const R&, const typename R::U& limb, const uint32_t pkw[8], const uint32_t sigw[8],
+                            Tab& tab, const GetPrep& get_prep, const GetB& get_b) {
+  using U = typename R::U;
+  using B = typename R::B;
+  const RowCtx<R> x(R::lane());
+  // ---- phase 1: decode A (rows 0, 2) and R (rows 1, 3) at once
+  const B is_r = (x.c & 1u) != 0u;
+  const bool a_sign = (pkw[7] >> 31) != 0, r_sign = (sigw[7] >> 31) != 0;
+  const U y = sel(x.k == 15u, limb & 0x7FFFu, limb);
+  U xo, to;
+  const B dec = rf_decode(x, y, sel(is_r, B(r_sign), B(a_sign)), xo, to);
+  const uint64_t decm = R::ballot(dec);
+  const bool a_ok = (decm & 1u) != 0, r_ok = ((decm >> 16) & 1u) != 0;  // lane 0 of rows 0 and 1
+  const uint64_t x0m = R::ballot(rf_canon<R>(xo).zero);
+  const bool r_canon = y_is_canonical(sigw) && !(((x0m >> 16) & 1u) != 0 && r_sign);
+  // -A = (-x, y, 1, -x y) and -R, extended, one coordinate per row
+  U X0, X1, X2, X3, Y0, Y1, Y2, Y3, T0, T1, T2, T3;
+  R::rows(xo, X0, X1, X2, X3);
+  R::rows(y, Y0, Y1, Y2, Y3);
+  R::rows(to, T0, T1, T2, T3);
+  const U na = sel(x.r0, rf_neg(x, X0), sel(x.r1, Y0, sel(x.r2, x.one, rf_neg(x, T0))));
+  const U nr = sel(x.r0, rf_neg(x, X1), sel(x.r1, Y1, sel(x.r2, x.one, rf_neg(x, T1))));
+  // ---- phase 2 (before the scalars): (0..8)(-A) and (0..8)(-R), both signs
+  const U d2 = x.cst(RowConst::d2);
+#pragma unroll 1
+  for (int tb = 0; tb < 2; tb++) {
+    U v = rf_carry32(x, tb == 0 ? na : nr);
+    const U ci = rp_cached_identity(x);
+    tab.store(tb, 0, 0, ci);
+    tab.store(tb, 1, 0, ci);
+    const U c1 = rp_to_cached(x, v, d2);
+    tab.store(tb, 0, 1, c1);
+    tab.store(tb, 1, 1, rp_cached_neg(x, c1));
+    rp_dbl(x, v);
+    U c = rp_to_cached(x, v, d2);
+    tab.store(tb, 0, 2, c);
+    tab.store(tb, 1, 2, rp_cached_neg(x, c));
+#pragma unroll 1
+    for (int e = 3; e <= 8; e++) {
+      rp_add(x, v, c1);
+      c = rp_to_cached(x, v, d2);
+      tab.store(tb, 0, e, c);
+      tab.store(tb, 1, e, rp_cached_neg(x, c));
+    }
+  }
+  // ---- phase 3: Straus over W 4-bit windows of k1 (A) and k2 (R)
+  SigPrep p;
+  get_prep(p);
+  const bool s_ok = (p.flags & 4u) != 0;
+  const bool r_flip = (p.flags & 1u) != 0;  // k2 < 0: R's digits flip (its table is of -R)
+  int W = (int)((p.flags >> 8) & 0xFFu);
+  W = (p.flags & 2u) ? HS_WIDE_WINDOWS : (W < HS_WINDOWS ? HS_WINDOWS : (W > HS_MAX_WINDOWS ? HS_MAX_WINDOWS : W));
+  uint32_t tA[8], tR[8];
+  hs_digits16(tA, p.k1, W);
+  hs_digits16(tR, p.k2, W);
+  U v = rp_identity(x);
+#pragma unroll 1
+  for (int win = W - 1; win >= 0; win--) {
+    const int dA = (int)sc_shift_out(tA, 4) - 8;
+    const int dR = (int)sc_shift_out(tR, 4) - 8;
+    const U cA = tab.load(0, dA < 0 ? 1 : 0, dA < 0 ? -dA : dA);
+    const U cR = tab.load(1, (dR < 0) != r_flip ? 1 : 0, dR < 0 ? -dR : dR);
+    if (win != W - 1) {
+#pragma unroll 1
+      for (int d = 0; d < 4; d++) rp_dbl(x, v);
+    }
+    rp_add(x, v, cA);
+    rp_add(x, v, cR);
+  }
+  rp_add(x, v, get_b());
+  // ---- final check: X = O (GO_STDLIB, R canonical) / [8]X = O (ZIP215)
+  if (MODE == MODE_ZIP215) {
+    // [8]X = O <=> T = 0 or X^2 + Y^2 = 0 (quad.h q_small_order)
+    const U s = rf_sq(x, v);
+    U s0, s1, s2, s3;
+    R::rows(s, s0, s1, s2, s3);
+    const uint64_t zt = R::ballot(rf_canon<R>(sel(x.r3, v, s0 + s1)).zero);
+    const bool so = ((zt >> 48) & 1u) != 0 || (zt & 1u) != 0;
+    return s_ok && a_ok && r_ok && so;
+  }
+  U v0, v1, v2, v3;
+  R::rows(v, v0, v1, v2, v3);
+  const uint64_t z = R::ballot(rf_canon<R>(sel(x.r0, v, rf_sub(x, v1, v2))).zero);
+  const bool e0 = (z & 1u) != 0, e1 = ((z >> 16) & 1u) != 0;
+  return s_ok && a_ok && r_ok && r_canon && e0 && e1;
+}
+
+// [u]B's cached coordinates (Y-X, Y+X, 2Z, 2dT) as four canonical 32-byte
+// encodings (8 words each): a row lane reads its 16-bit limb (the helper
+// wave's output in k_verify_row_split)
+CMTV_HD void bpoint_store_bytes(uint32_t* d, const ge_p3& P) {
+  fe c[4], d2;
+  fe_sub(c[0], P.Y, P.X);
+  fe_add(c[1], P.Y, P.X);
+  fe_add(c[2], P.Z, P.Z);
+  fe_const_d2(d2);
+  fe_mul(c[3], P.T, d2);
+#pragma unroll
+  for (int k = 0; k < 4; k++) fe_tobytes(d + 8 * k, c[k]);
+}
+
+}  // namespace cmtv

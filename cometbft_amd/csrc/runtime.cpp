@@ -50,6 +50,10 @@ constexpr size_t kQuadMaxDefault = 40000;
 // 0.265 ms) the helper-wave quad kernel takes over in between (the one-wave
 // oct kernel stays reachable with CMTV_OCT_SPLIT_MAX < CMTV_OCT_MAX).
 constexpr size_t kOctMaxDefault = 3072;       // CMTV_OCT_MAX
+// Ed25519 batches up to this size take the one-signature-per-wave row kernel
+// (row.h) where the two-wave oct kernel would run (CMTV_ROW_MAX; 3 signatures
+// per CU: 768 in one round on 256 CUs)
+constexpr size_t kRowMaxDefault = 768;
 constexpr size_t kOctSplitMaxDefault = 3072;  // CMTV_OCT_SPLIT_MAX
 // quad batches up to this size take the helper-wave form (k_verify_quad_split:
 // 256 workgroups x 48 signatures per round); CMTV_QUAD_SPLIT_MAX
@@ -343,6 +347,9 @@ struct CmtvDev {
   ncclComm_t comm = nullptr;
   // kernel diagnostic counters (kernels.h kDiagWords, vector atomics)
   uint32_t* d_diag = nullptr;
+  // the row kernel's bitmap ring (kernels.h kRowSlots x kRowSlotWords)
+  uint32_t* d_rowslots = nullptr;
+  uint32_t row_seq = 0;
   // a device that returned a HIP error is taken out of the context's
   // rotation: host batches are re-planned over the others (runtime.cpp
   // run_host_batch); CMTV_FAULT_DEV=g makes device g's first launch fail
@@ -362,6 +369,7 @@ struct cmtv_ctx {
   size_t quad_max = kQuadMaxDefault;  // batches up to this size use the quad kernel
   size_t oct_max = kOctMaxDefault;    // ... and up to this size the oct kernel
   size_t oct_split_max = kOctSplitMaxDefault;
+  size_t row_max = kRowMaxDefault;
   size_t quad_split_max = kQuadSplitMaxDefault;
   size_t keyed_quad_max = kKeyedQuadMaxDefault;
   size_t lane_chunk = kChunk;         // signatures per lane-kernel launch (env CMTV_LANE_CHUNK)
@@ -472,6 +480,13 @@ static bool split_kernel_for(const cmtv_ctx* ctx, size_t n) {
   return oct ? n <= ctx->oct_split_max : (quad && n <= ctx->quad_split_max);
 }
 
+// The row kernel replaces the two-wave oct kernel up to CMTV_ROW_MAX (so the
+// oct / quad knobs still force their kernels)
+static bool row_kernel_for(const cmtv_ctx* ctx, size_t n) {
+  return n <= ctx->quad_max && n <= ctx->oct_max && n <= ctx->oct_split_max && n <= ctx->row_max &&
+         n <= kRowMaxCap;
+}
+
 // ... and can write the sign-bytes of all n in its helper waves: a split
 // kernel running in one launch (enqueue_verify rejects a fused batch of more
 // than kChunk, whatever CMTV_QUAD_MAX / CMTV_QUAD_SPLIT_MAX say). The one
@@ -493,9 +508,10 @@ static int enqueue_verify(cmtv_ctx* ctx, CmtvDev& D, size_t n, const uint8_t* d_
   const bool oct = quad && !sr && n <= ctx->oct_max;
   const bool oct_split = oct && n <= ctx->oct_split_max;
   const bool quad_split = quad && !oct && n <= ctx->quad_split_max;
+  const bool row = !sr && row_kernel_for(ctx, n);
   const uint32_t kflags = (quad ? kLaunchQuad : 0u) | (oct ? kLaunchOct : 0u) |
                           (oct_split ? kLaunchOctSplit : 0u) | (quad_split ? kLaunchQuadSplit : 0u) |
-                          (ctx->force_wide ? kLaunchForceWide : 0u);
+                          (row ? kLaunchRow : 0u) | (ctx->force_wide ? kLaunchForceWide : 0u);
   hipError_t e = hipSuccess;
   if (!quad) {
     const size_t lanes = std::min<size_t>(n, ctx->lane_chunk);
@@ -516,7 +532,8 @@ static int enqueue_verify(cmtv_ctx* ctx, CmtvDev& D, size_t n, const uint8_t* d_
     else
       e = launch_verify(mode, cn, d_pk + 32 * c, d_sig + 64 * c, d_msg, d_off + c, D.d_btab,
                         static_cast<uint32_t*>(D.d_atab.p), d_valid ? d_valid + c : nullptr,
-                        d_bitmap ? d_bitmap + c / 64 : nullptr, kflags, s, sb);
+                        d_bitmap ? d_bitmap + c / 64 : nullptr, kflags, s, sb,
+                        row ? D.d_rowslots + (size_t)(D.row_seq++ % kRowSlots) * kRowSlotWords : nullptr);
     if (e != hipSuccess) {
       D.timing.abandon(tp);
       return hip_fail(e);
@@ -1053,6 +1070,9 @@ static int init_device(cmtv_ctx* ctx, CmtvDev& D) {
   if (e == hipSuccess) e = hipEventCreateWithFlags(&D.done, hipEventDisableTiming);
   if (e == hipSuccess) e = hipMalloc(&D.d_diag, kDiagWords * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMemsetAsync(D.d_diag, 0, kDiagWords * sizeof(uint32_t), D.stream);
+  if (e == hipSuccess) e = hipMalloc(&D.d_rowslots, (size_t)kRowSlots * kRowSlotWords * sizeof(uint32_t));
+  if (e == hipSuccess)
+    e = hipMemsetAsync(D.d_rowslots, 0, (size_t)kRowSlots * kRowSlotWords * sizeof(uint32_t), D.stream);
   if (e == hipSuccess) e = hipMalloc(&D.d_btab, kBtabWords * sizeof(uint32_t));
   if (e == hipSuccess) e = launch_btab_init(D.d_btab, D.stream);
   uint16_t prog[SR_PROGRAM_MAX];
@@ -1079,6 +1099,8 @@ static void release_device(CmtvDev& D) {
   if (D.d_srprog) (void)hipFree(D.d_srprog);
   if (D.d_diag) (void)hipFree(D.d_diag);
   D.d_diag = nullptr;
+  if (D.d_rowslots) (void)hipFree(D.d_rowslots);
+  D.d_rowslots = nullptr;
   D.d_btab = nullptr;
   D.d_bcomb = nullptr;
   D.d_srprog = nullptr;
@@ -1093,6 +1115,7 @@ static void release_device(CmtvDev& D) {
 static void read_env(cmtv_ctx* ctx) {
   if (const char* qm = std::getenv("CMTV_QUAD_MAX")) ctx->quad_max = (size_t)std::strtoull(qm, nullptr, 10);
   if (const char* om = std::getenv("CMTV_OCT_MAX")) ctx->oct_max = (size_t)std::strtoull(om, nullptr, 10);
+  if (const char* rm = std::getenv("CMTV_ROW_MAX")) ctx->row_max = (size_t)std::strtoull(rm, nullptr, 10);
   if (const char* os = std::getenv("CMTV_OCT_SPLIT_MAX")) ctx->oct_split_max = (size_t)std::strtoull(os, nullptr, 10);
   if (const char* qs = std::getenv("CMTV_QUAD_SPLIT_MAX")) ctx->quad_split_max = (size_t)std::strtoull(qs, nullptr, 10);
   if (const char* kq = std::getenv("CMTV_KEYED_QUAD_MAX")) ctx->keyed_quad_max = (size_t)std::strtoull(kq, nullptr, 10);

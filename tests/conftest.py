@@ -84,6 +84,40 @@ def gpu_ctx_quad():
             os.environ["CMTV_OCT_MAX"] = old
 
 
+def _env_ctx(**env):
+    """A Context opened with the CMTV_* knobs in env set (then restored)."""
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from cometbft_amd import Context
+
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update({k: str(v) for k, v in env.items()})
+    try:
+        return Context(device=0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+@pytest.fixture(scope="session")
+def gpu_ctx_oct2():
+    """Small Ed25519 batches on the two-wave oct kernel (CMTV_ROW_MAX=0)
+    instead of the default one-signature-per-wave row kernel (row.h)."""
+    return _env_ctx(CMTV_ROW_MAX=0)
+
+
+@pytest.fixture(scope="session")
+def gpu_ctx_row():
+    """Ed25519 batches up to 4,000 signatures on the row kernel (several
+    rounds of 768), so the corpus and every ragged size run through it."""
+    return _env_ctx(CMTV_ROW_MAX=4000)
+
+
 @pytest.fixture(scope="session")
 def gpu_ctx_oct1():
     """A context whose small Ed25519 batches take the one-wave oct kernel

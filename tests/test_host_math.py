@@ -257,3 +257,33 @@ def test_keyed_quad_pipeline_matches_corpus(quadcheck, corpus, mode):
     want = (corpus["go"] if mode == 0 else corpus["zip215"])[idx]
     bad = np.nonzero(got != want)[0]
     assert bad.size == 0, [(idx[int(i)], corpus["cats"][idx[int(i)]]) for i in bad[:10]]
+
+
+RSRC = os.path.join(ROOT, "tests", "host", "rowcheck.cpp")
+RBIN = os.path.join(ROOT, "build", "rowcheck")
+
+
+@pytest.fixture(scope="module")
+def rowcheck():
+    return _build(RSRC, RBIN, ["-std=c++20"])
+
+
+def test_row_field_layer(rowcheck):
+    """row.h's radix-2^16 product (16 column terms per lane, three carry
+    rounds), squaring and canonical zero / parity test against a big-int
+    reference, at the stated input bound (2^19.37) and on p, 2p, 2^256 - 1."""
+    out = subprocess.run([rowcheck, "mul"], capture_output=True, check=True, timeout=120).stdout
+    assert out.strip() == b"ok"
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_row_pipeline_matches_corpus(rowcheck, corpus, mode):
+    """The one-signature-per-wave row kernel's source (row.h r_verify_split)
+    on 64-lane arrays with its operand bounds asserted, the scalars and [u]B
+    from the helper wave's code (q_prepare, q_bcomb16): every non-honest
+    vector and a slice of the honest ones."""
+    idx = _keyed_subset(corpus)
+    got = _run(rowcheck, None, corpus, idx, mode)
+    want = (corpus["go"] if mode == 0 else corpus["zip215"])[idx]
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(idx[int(i)], corpus["cats"][idx[int(i)]]) for i in bad[:10]]

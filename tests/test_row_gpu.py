@@ -1,0 +1,90 @@
+"""The one-signature-per-wave row kernel (cometbft_amd/csrc/row.h,
+k_verify_row_split): the production kernel for Ed25519 batches up to
+CMTV_ROW_MAX (768) signatures, i.e. the 150-validator VerifyCommit.
+
+Its corpus, ragged-size, wide-schedule and forced-wide parity runs live with
+the other kernels' (test_gpu_parity.py, test_wide_gpu.py: kernel "row");
+here: the bitmap assembly (the last wave of a launch packs the words from a
+ring slot of verdict bytes) under concurrent launches on several streams,
+and the default dispatch at the commit sizes. Oracle: oracle/liboracle.so
+(the C restatement of Go 1.19 ed25519.Verify, crypto/ed25519/ed25519.go:148).
+"""
+import threading
+
+import numpy as np
+import pytest
+
+from oracle import coracle
+from cometbft_amd import MODE_GO_STDLIB, MODE_ZIP215, Context
+
+pytestmark = pytest.mark.gpu
+
+
+def _batch(n, seed, flip=0.1):
+    rng = np.random.default_rng(seed)
+    seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    msgs = [rng.integers(0, 256, 116, dtype=np.uint8).tobytes() for _ in range(n)]
+    m, off = coracle.pack_msgs(msgs)
+    sig = coracle.sign_batch(seeds, m, off, nthreads=8).copy()
+    for i in np.nonzero(rng.random(n) < flip)[0]:
+        sig[i, rng.integers(0, 64)] ^= 1 << rng.integers(0, 8)
+    return coracle.pubkeys_from_seeds(seeds), sig, m, off
+
+
+@pytest.mark.parametrize("n", [150, 767, 768])
+def test_default_dispatch_commit_sizes(gpu_ctx, n):
+    """The default context at and around the row crossover, both modes,
+    verdict bytes and bitmap words (no bit past n set)."""
+    pk, sig, m, off = _batch(n, 500 + n)
+    for mode in (MODE_GO_STDLIB, MODE_ZIP215):
+        exp = coracle.verify_batch(pk, sig, m, off, mode, nthreads=8)
+        got, words = gpu_ctx.verify(pk, sig, m, off, mode, bitmap=True)
+        assert np.array_equal(got, exp)
+        bits = np.unpackbits(words.view(np.uint8), bitorder="little")
+        assert np.array_equal(bits[:n], exp) and not bits[n:].any()
+
+
+def test_concurrent_row_launches_pack_their_own_bitmaps():
+    """4 threads, each on its own stream, 25 device-resident row launches of
+    different sizes with bitmaps: every launch takes its own ring slot, so
+    each bitmap holds exactly its own verdicts."""
+    import torch
+
+    ctx = Context(device=0)
+    dev = torch.device("cuda:0")
+    jobs = []
+    for j, n in enumerate((150, 64, 333, 700)):
+        pk, sig, m, off = _batch(n, 900 + j, flip=0.2)
+        exp = coracle.verify_batch(pk, sig, m, off, MODE_GO_STDLIB, nthreads=8)
+        jobs.append((n, pk, sig, m, off, exp))
+    errors = []
+
+    def run(j):
+        n, pk, sig, m, off, exp = jobs[j]
+        try:
+            s = torch.cuda.Stream(device=dev)
+            t = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in
+                 {"pk": pk, "sig": sig, "m": m, "off": off.view(np.int32)}.items()}
+            words = (n + 63) // 64
+            bm = torch.zeros(words, dtype=torch.int64, device=dev)
+            want = np.packbits(exp, bitorder="little")
+            want = np.pad(want, (0, 8 * words - want.size)).view(np.int64)
+            for _ in range(25):
+                bm.fill_(-1)
+                torch.cuda.synchronize(dev)
+                ctx.verify_device(n, t["pk"].data_ptr(), t["sig"].data_ptr(), t["m"].data_ptr(),
+                                  t["off"].data_ptr(), MODE_GO_STDLIB, 0, bm.data_ptr(), s.cuda_stream)
+                s.synchronize()
+                got = bm.cpu().numpy()
+                if not np.array_equal(got, want):
+                    errors.append((j, np.nonzero(got != want)[0][:4].tolist()))
+        except Exception as e:  # noqa: BLE001
+            errors.append((j, repr(e)))
+
+    ths = [threading.Thread(target=run, args=(j,)) for j in range(4)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(timeout=110)
+    assert not any(t.is_alive() for t in ths)
+    assert not errors, errors[:5]

@@ -8,7 +8,7 @@
 #include "keyed.h"
 #include "oct.h"
 #include "quad.h"
-#include "row.h"
+#include "row_dev.h"
 #include "verify_core.h"
 
 namespace cmtv {
@@ -263,46 +263,5 @@ struct DevATabQ {
 };
 
 
-// Row policy (row.h): one signature per wave, a field element per 16-lane
-// row. Row moves are DPP (row_ror:r 0x120+r, row_newbcast:r 0x150+r, with
-// bound_ctrl off as in DevQuad); the four row broadcasts of a value are one
-// v_permlane32_swap and two v_permlane16_swap:
-//   permlane32_swap(x, x) = {[x0 x1 x0 x1], [x2 x3 x2 x3]}  (rows)
-//   permlane16_swap(y, y) = {[y0 y0 y2 y2], [y1 y1 y3 y3]}
-struct DevRow {
-  using U = uint32_t;
-  using U64 = uint64_t;
-  using B = bool;
-  __device__ __forceinline__ static U lane() { return threadIdx.x & 63; }
-  template <int R>
-  __device__ __forceinline__ static U ror(U x) {
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x120 + R, 0xF, 0xF, false);
-  }
-  template <int R>
-  __device__ __forceinline__ static U bcast(U x) {
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x150 + R, 0xF, 0xF, false);
-  }
-  __device__ __forceinline__ static void rows(U x, U& b0, U& b1, U& b2, U& b3) {
-    const auto h = __builtin_amdgcn_permlane32_swap(x, x, false, false);
-    const auto lo = __builtin_amdgcn_permlane16_swap(h[0], h[0], false, false);
-    const auto hi = __builtin_amdgcn_permlane16_swap(h[1], h[1], false, false);
-    b0 = lo[0];
-    b1 = lo[1];
-    b2 = hi[0];
-    b3 = hi[1];
-  }
-  __device__ __forceinline__ static uint64_t ballot(bool b) { return __ballot(b); }
-  __device__ __forceinline__ static U load_const(const uint16_t* tab, U k) { return tab[k]; }
-};
-
-// the row verifier's (0..8)(-A), (0..8)(-R) cached tables, both signs: one
-// LDS word per lane per entry (a lookup is one ds_read_b32)
-struct DevRowTab {
-  uint32_t* t;
-  uint32_t lane;
-  __device__ __forceinline__ void store(int tb, int neg, int e, uint32_t c) { t[((tb * 2 + neg) * 9 + e) * 64 + lane] = c; }
-  __device__ __forceinline__ uint32_t load(int tb, int neg, int e) const { return t[((tb * 2 + neg) * 9 + e) * 64 + lane]; }
-};
-constexpr int kRowTabWords = 2 * 2 * 9 * 64;
 
 }  // namespace cmtv

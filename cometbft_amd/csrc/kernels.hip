@@ -367,6 +367,7 @@ __global__ __launch_bounds__(256, 1) void k_verify_row_split(
   __shared__ uint32_t bpt[3][32];
   __shared__ uint32_t tab_lds[3][kRowTabWords];
   __shared__ uint32_t sbm[3][kSbFuseMaxMsg / 4];
+  CMTV_STAMP(0);
   if (wave == 3) {
     const uint32_t ls = t < 3 ? t : 2;
     const uint32_t s = base + ls;
@@ -377,11 +378,15 @@ __global__ __launch_bounds__(256, 1) void k_verify_row_split(
     SigPrep p;
     q_prepare<MODE>(p, pk + 8 * (size_t)i, sig + 16 * (size_t)i, mp, ml, force_wide != 0);
     if (t < 3) sig_prep_store(prep[t], p);
+    CMTV_STAMP(1);
     __syncthreads();  // 1: the scalars
+    CMTV_STAMP(2);
     ge_p3 B;
     q_bcomb16(B, p.u, DevBTab{btab});
     if (t < 3) bpoint_store_bytes(bpt[t], B);
+    CMTV_STAMP(3);
     __syncthreads();  // 2: [u]B
+    CMTV_STAMP(4);
     return;
   }
   const uint32_t s = base + wave;
@@ -398,13 +403,18 @@ __global__ __launch_bounds__(256, 1) void k_verify_row_split(
   bool v = r_verify_split<MODE>(
       DevRow(), limb, pkw, sigw, tab,
       [&](SigPrep& p) {
+        CMTV_STAMP(1);
         __syncthreads();
+        CMTV_STAMP(2);
         sig_prep_load(p, prep[wave]);
       },
       [&]() -> uint32_t {
+        CMTV_STAMP(3);
         __syncthreads();
+        CMTV_STAMP(4);
         return (bq[8 * (t >> 4) + ((t & 15) >> 1)] >> (16 * (t & 1))) & 0xFFFFu;
       });
+  CMTV_STAMP(5);
   v = v && active;
   if (t == 0 && active && out_valid) out_valid[s] = v ? 1 : 0;
   if (!out_bitmap) return;
@@ -415,6 +425,105 @@ __global__ __launch_bounds__(256, 1) void k_verify_row_split(
   if (t == 0) ticket = __hip_atomic_fetch_add(slot, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
   ticket = __shfl(ticket, 0);
   if (ticket != 3 * gridDim.x - 1) return;
+  __threadfence();
+  const uint32_t words = (n + 63) / 64;
+  for (uint32_t w = t; w < words; w += 64) {
+    uint64_t m = 0;
+    for (uint32_t b = 0; b < 64 && 64 * w + b < n; b++) m |= (uint64_t)(vb[64 * w + b] != 0) << b;
+    out_bitmap[w] = m;
+  }
+  if (t == 0) __hip_atomic_store(slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The row verifier over two waves per signature (row.h r_part / r_join),
+// one signature per workgroup and CU, for batches of at most 256 (one
+// round): wave 0 decodes A and runs [k1](-A), wave 1 decodes R and runs
+// [|k2|](+/-R) -- 4 doublings and one addition per window each, instead of
+// one wave's two additions -- while wave 2 (the helper) hashes and splits
+// the scalars and computes [u]B. Wave 1 hands its sum (cached) and R's
+// flags over at barrier 2; wave 0 adds it and [u]B and checks. Bitmap as
+// k_verify_row_split (the A waves count).
+template <uint32_t MODE>
+__global__ __launch_bounds__(192, 1) void k_verify_row2_split(
+    uint32_t n, const uint32_t* __restrict__ pk, const uint32_t* __restrict__ sig, const uint8_t* __restrict__ msg,
+    const uint32_t* __restrict__ off, const uint32_t* __restrict__ btab, uint8_t* __restrict__ out_valid,
+    uint64_t* __restrict__ out_bitmap, uint32_t force_wide, SbFuse sb, uint32_t* __restrict__ slot) {
+  const uint32_t wave = threadIdx.x >> 6, t = threadIdx.x & 63;
+  const uint32_t s = blockIdx.x;
+  const uint32_t i = s < n ? s : n - 1;
+  __shared__ uint32_t prep[SIG_PREP_WORDS + 1];
+  __shared__ uint32_t bpt[32];
+  __shared__ uint32_t tab_lds[2][kRowTabWords / 2];
+  __shared__ uint32_t sbm[kSbFuseMaxMsg / 4];
+  __shared__ uint32_t xr[64 + 2];  // R's sum (cached), its decode flag and x = 0
+  const uint32_t* pkp = pk + 8 * (size_t)i;
+  const uint32_t* sgp = sig + 16 * (size_t)i;
+  CMTV_STAMP(0);
+  if (wave == 2) {
+    const uint8_t* mp;
+    uint32_t ml;
+    helper_message(sb, i, msg, off, sbm, mp, ml);
+    SigPrep p;
+    q_prepare<MODE>(p, pkp, sgp, mp, ml, force_wide != 0);
+    if (t == 0) sig_prep_store(prep, p);
+    CMTV_STAMP(1);
+    __syncthreads();  // 1: the scalars
+    CMTV_STAMP(2);
+    ge_p3 B;
+    q_bcomb16(B, p.u, DevBTab{btab});
+    if (t == 0) bpoint_store_bytes(bpt, B);
+    CMTV_STAMP(3);
+    __syncthreads();  // 2: [u]B and R's sum
+    CMTV_STAMP(4);
+    return;
+  }
+  const uint32_t* src = wave ? sgp : pkp;
+  const uint32_t limb = reinterpret_cast<const uint16_t*>(src)[t & 15];
+  const bool sign = (src[7] >> 31) != 0;
+  const RowCtx<DevRow> x(DevRow::lane());
+  DevRowTab tab{tab_lds[wave], t};
+  SigPrep p;
+  bool dec, x0;
+  auto get_prep = [&](SigPrep& q) {
+    CMTV_STAMP(1);
+    __syncthreads();
+    CMTV_STAMP(2);
+    sig_prep_load(q, prep);
+  };
+  if (wave == 1) {
+    const uint32_t v = r_part<1>(x, limb, sign, tab, get_prep, p, dec, x0);
+    xr[t] = rp_to_cached(x, v, x.cst(RowConst::d2));
+    if (t == 0) {
+      xr[64] = dec ? 1u : 0u;
+      xr[65] = x0 ? 1u : 0u;
+    }
+    CMTV_STAMP(3);
+    __syncthreads();  // 2
+    CMTV_STAMP(4);
+    return;
+  }
+  const uint32_t v = r_part<0>(x, limb, sign, tab, get_prep, p, dec, x0);
+  CMTV_STAMP(3);
+  __syncthreads();  // 2
+  CMTV_STAMP(4);
+  uint32_t sigw[8];
+  load_words(sigw, sgp, 2);
+  const bool r_dec = xr[64] != 0, r_x0 = xr[65] != 0;
+  const bool r_canon = y_is_canonical(sigw) && !(r_x0 && (sigw[7] >> 31) != 0);
+  const uint32_t cb = (bpt[8 * (t >> 4) + ((t & 15) >> 1)] >> (16 * (t & 1))) & 0xFFFFu;
+  bool v_ok = r_join<MODE>(x, v, xr[t], cb, (p.flags & 4u) != 0 && dec && r_dec, r_canon);
+  CMTV_STAMP(5);
+  const bool active = s < n;
+  v_ok = v_ok && active;
+  if (t == 0 && active && out_valid) out_valid[s] = v_ok ? 1 : 0;
+  if (!out_bitmap) return;
+  uint8_t* vb = reinterpret_cast<uint8_t*>(slot + 16);
+  if (t == 0 && active) vb[s] = v_ok ? 1 : 0;
+  __threadfence();
+  uint32_t ticket = 0;
+  if (t == 0) ticket = __hip_atomic_fetch_add(slot, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+  ticket = __shfl(ticket, 0);
+  if (ticket != gridDim.x - 1) return;
   __threadfence();
   const uint32_t words = (n + 63) / 64;
   for (uint32_t w = t; w < words; w += 64) {
@@ -521,6 +630,18 @@ hipError_t launch_verify(uint32_t mode, uint32_t n, const void* pk, const void* 
   auto op = static_cast<const uint32_t*>(off);
   auto vp = static_cast<uint8_t*>(valid);
   auto bp = static_cast<uint64_t*>(bitmap);
+  if (kflags & kLaunchRow2) {
+    // one signature per 192-lane block (an A wave, an R wave, the helper)
+    if (n > kRowMaxCap || (bp && !row_slot)) return hipErrorInvalidValue;
+    const dim3 grid(n), block(192);
+    if (mode == MODE_ZIP215)
+      hipLaunchKernelGGL(k_verify_row2_split<MODE_ZIP215>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp, fw,
+                         fz, row_slot);
+    else
+      hipLaunchKernelGGL(k_verify_row2_split<MODE_GO_STDLIB>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp,
+                         fw, fz, row_slot);
+    return hipGetLastError();
+  }
   if (kflags & kLaunchRow) {
     // 3 signatures per 256-lane block (3 row waves + the helper)
     if (n > kRowMaxCap || (bp && !row_slot)) return hipErrorInvalidValue;

@@ -76,9 +76,12 @@ struct RowCtx {
   U bias;     // limb k of 4p
   U m38;      // 38 on limb 0 (the carry out of limb 15 wraps as x 38), else 1
   U one;      // the constant 1 (limb 0)
+  U tw[16];   // column twist of term r: 38 where limb k < r (the column wraps past 2^256), else 1
   B r0, r1, r2, r3;
   CMTV_HD explicit RowCtx(const U& lane) {
     k = lane & 15u;
+#pragma unroll
+    for (int r = 0; r < 16; r++) tw[r] = sel(k < (uint32_t)r, U(38u), U(1u));
     c = lane >> 4;
     bias = sel(k == 0u, U(4u * 0xFFEDu), sel(k == 15u, U(4u * 0x7FFFu), U(4u * 0xFFFFu)));
     m38 = sel(k == 0u, U(38u), U(1u));
@@ -126,18 +129,23 @@ CMTV_HD void rf_terms(const RowCtx<R>& x, typename R::U64& acc, const typename R
     using U = typename R::U;
     const U fr = R::template ror<r>(f);
     const U gb = R::template bcast<r>(g);
-    const U tw = sel(x.k < (uint32_t)r, U(38u), U(1u));  // the column wraps past 2^256
-    acc = mad64(fr, mul24(gb, tw), acc);
+    acc = mad64(fr, mul24(gb, x.tw[r]), acc);
     rf_terms<R, r + 1>(x, acc, f, g);
   }
 }
 
-// h = f g (each row its own product)
+// h = f g (each row its own product). A policy with kFusedProduct supplies
+// the 15 twisted broadcasts itself (DevRow: v_mul_u32_u24_dpp row_newbcast,
+// the broadcast and the twist in one instruction).
 template <class R>
 CMTV_HD typename R::U rf_mul(const RowCtx<R>& x, const typename R::U& f, const typename R::U& g) {
-  typename R::U64 acc = mad64(f, R::template bcast<0>(g), widen(typename R::U(0u)));
-  rf_terms<R, 1>(x, acc, f, g);
-  return rf_carry64(x, acc);
+  if constexpr (R::kFusedProduct) {
+    return rf_carry64(x, R::product(x.tw, f, g));
+  } else {
+    typename R::U64 acc = mad64(f, R::template bcast<0>(g), widen(typename R::U(0u)));
+    rf_terms<R, 1>(x, acc, f, g);
+    return rf_carry64(x, acc);
+  }
 }
 
 template <class R>
@@ -368,6 +376,59 @@ CMTV_HD typename R::B rf_decode(const RowCtx<R>& x, const typename R::U& y, cons
 // entry (LDS on the device):
 //   void store(int tbl, int neg, int e, const U& c);  U load(int tbl, int neg, int e) const;
 
+// (0..8)P and (0..8)(-P) in cached form into table tb, P extended (clobbers
+// nothing: v is copied)
+template <class R, class Tab>
+CMTV_HD void r_build_table(const RowCtx<R>& x, Tab& tab, int tb, const typename R::U& p) {
+  using U = typename R::U;
+  const U d2 = x.cst(RowConst::d2);
+  U v = rf_carry32(x, p);
+  const U ci = rp_cached_identity(x);
+  tab.store(tb, 0, 0, ci);
+  tab.store(tb, 1, 0, ci);
+  const U c1 = rp_to_cached(x, v, d2);
+  tab.store(tb, 0, 1, c1);
+  tab.store(tb, 1, 1, rp_cached_neg(x, c1));
+  rp_dbl(x, v);
+  U c = rp_to_cached(x, v, d2);
+  tab.store(tb, 0, 2, c);
+  tab.store(tb, 1, 2, rp_cached_neg(x, c));
+#pragma unroll 1
+  for (int e = 3; e <= 8; e++) {
+    rp_add(x, v, c1);
+    c = rp_to_cached(x, v, d2);
+    tab.store(tb, 0, e, c);
+    tab.store(tb, 1, e, rp_cached_neg(x, c));
+  }
+}
+
+// the window count of a prepared pair (quad.h q_wave_windows for one signature)
+CMTV_HD int r_windows(uint32_t flags) {
+  const int W = (int)((flags >> 8) & 0xFFu);
+  return (flags & 2u) ? HS_WIDE_WINDOWS : (W < HS_WINDOWS ? HS_WINDOWS : (W > HS_MAX_WINDOWS ? HS_MAX_WINDOWS : W));
+}
+
+// The final check on X (this row's coordinate): X = O (GO_STDLIB, with R
+// canonical: encode(R') == R bytes) / [8]X = O (ZIP215: T = 0 or
+// X^2 + Y^2 = 0, quad.h q_small_order). ok: the s, A and R checks.
+template <uint32_t MODE, class R>
+CMTV_HD bool r_final(const RowCtx<R>& x, const typename R::U& v, bool ok, bool r_canon) {
+  using U = typename R::U;
+  if (MODE == MODE_ZIP215) {
+    const U s = rf_sq(x, v);
+    U s0, s1, s2, s3;
+    R::rows(s, s0, s1, s2, s3);
+    const uint64_t zt = R::ballot(rf_canon<R>(sel(x.r3, v, s0 + s1)).zero);
+    const bool so = ((zt >> 48) & 1u) != 0 || (zt & 1u) != 0;
+    return ok && so;
+  }
+  U v0, v1, v2, v3;
+  R::rows(v, v0, v1, v2, v3);
+  const uint64_t z = R::ballot(rf_canon<R>(sel(x.r0, v, rf_sub(x, v1, v2))).zero);
+  const bool e0 = (z & 1u) != 0, e1 = ((z >> 16) & 1u) != 0;
+  return ok && r_canon && e0 && e1;
+}
+
 // X = [u]B + [k1](-A) + [|k2|](k2 < 0 ? R : -R) = [k2](R' - R) (quad.h
 // q_straus_prep_b<EXT_B, PREBUILT>) and the final check of the mode, one
 // signature per wave. pk16 / sig16: this lane's 16-bit limb of A / R (row
@@ -398,35 +459,14 @@ CMTV_HD bool r_verify_split(const R&, const typename R::U& limb, const uint32_t 
   const U na = sel(x.r0, rf_neg(x, X0), sel(x.r1, Y0, sel(x.r2, x.one, rf_neg(x, T0))));
   const U nr = sel(x.r0, rf_neg(x, X1), sel(x.r1, Y1, sel(x.r2, x.one, rf_neg(x, T1))));
   // ---- phase 2 (before the scalars): (0..8)(-A) and (0..8)(-R), both signs
-  const U d2 = x.cst(RowConst::d2);
-#pragma unroll 1
-  for (int tb = 0; tb < 2; tb++) {
-    U v = rf_carry32(x, tb == 0 ? na : nr);
-    const U ci = rp_cached_identity(x);
-    tab.store(tb, 0, 0, ci);
-    tab.store(tb, 1, 0, ci);
-    const U c1 = rp_to_cached(x, v, d2);
-    tab.store(tb, 0, 1, c1);
-    tab.store(tb, 1, 1, rp_cached_neg(x, c1));
-    rp_dbl(x, v);
-    U c = rp_to_cached(x, v, d2);
-    tab.store(tb, 0, 2, c);
-    tab.store(tb, 1, 2, rp_cached_neg(x, c));
-#pragma unroll 1
-    for (int e = 3; e <= 8; e++) {
-      rp_add(x, v, c1);
-      c = rp_to_cached(x, v, d2);
-      tab.store(tb, 0, e, c);
-      tab.store(tb, 1, e, rp_cached_neg(x, c));
-    }
-  }
+  r_build_table(x, tab, 0, na);
+  r_build_table(x, tab, 1, nr);
   // ---- phase 3: Straus over W 4-bit windows of k1 (A) and k2 (R)
   SigPrep p;
   get_prep(p);
   const bool s_ok = (p.flags & 4u) != 0;
   const bool r_flip = (p.flags & 1u) != 0;  // k2 < 0: R's digits flip (its table is of -R)
-  int W = (int)((p.flags >> 8) & 0xFFu);
-  W = (p.flags & 2u) ? HS_WIDE_WINDOWS : (W < HS_WINDOWS ? HS_WINDOWS : (W > HS_MAX_WINDOWS ? HS_MAX_WINDOWS : W));
+  const int W = r_windows(p.flags);
   uint32_t tA[8], tR[8];
   hs_digits16(tA, p.k1, W);
   hs_digits16(tR, p.k2, W);
@@ -445,21 +485,56 @@ CMTV_HD bool r_verify_split(const R&, const typename R::U& limb, const uint32_t 
     rp_add(x, v, cR);
   }
   rp_add(x, v, get_b());
-  // ---- final check: X = O (GO_STDLIB, R canonical) / [8]X = O (ZIP215)
-  if (MODE == MODE_ZIP215) {
-    // [8]X = O <=> T = 0 or X^2 + Y^2 = 0 (quad.h q_small_order)
-    const U s = rf_sq(x, v);
-    U s0, s1, s2, s3;
-    R::rows(s, s0, s1, s2, s3);
-    const uint64_t zt = R::ballot(rf_canon<R>(sel(x.r3, v, s0 + s1)).zero);
-    const bool so = ((zt >> 48) & 1u) != 0 || (zt & 1u) != 0;
-    return s_ok && a_ok && r_ok && so;
+  return r_final<MODE>(x, v, s_ok && a_ok && r_ok, r_canon);
+}
+
+
+// The two-wave form (k_verify_row2_split, one signature per CU): wave PART
+// = 0 takes A, PART = 1 takes R. Each decodes its point on every row, builds
+// (0..8)(-P) (both signs), and after get_prep runs W windows of 4 doublings
+// and ONE addition -- [k1](-A), or [|k2|](k2 < 0 ? R : -R) -- instead of the
+// one-wave form's two additions per window. Returns this row's coordinate
+// of the part's sum; dec / x0 are P's decode flag and whether its x is 0.
+template <int PART, class R, class Tab, class GetPrep>
+CMTV_HD typename R::U r_part(const RowCtx<R>& x, const typename R::U& limb, bool sign, Tab& tab,
+                             const GetPrep& get_prep, SigPrep& p, bool& dec, bool& x0) {
+  using U = typename R::U;
+  const U y = sel(x.k == 15u, limb & 0x7FFFu, limb);
+  U xo, to;
+  dec = (R::ballot(rf_decode(x, y, typename R::B(sign), xo, to)) & 1u) != 0;
+  x0 = (R::ballot(rf_canon<R>(xo).zero) & 1u) != 0;
+  U X0, X1, X2, X3, Y0, Y1, Y2, Y3, T0, T1, T2, T3;
+  R::rows(xo, X0, X1, X2, X3);
+  R::rows(y, Y0, Y1, Y2, Y3);
+  R::rows(to, T0, T1, T2, T3);
+  r_build_table(x, tab, 0, sel(x.r0, rf_neg(x, X0), sel(x.r1, Y0, sel(x.r2, x.one, rf_neg(x, T0)))));
+  get_prep(p);
+  const bool flip = PART == 1 && (p.flags & 1u) != 0;
+  const int W = r_windows(p.flags);
+  uint32_t t[8];
+  hs_digits16(t, PART == 0 ? p.k1 : p.k2, W);
+  U v = rp_identity(x);
+#pragma unroll 1
+  for (int win = W - 1; win >= 0; win--) {
+    const int d = (int)sc_shift_out(t, 4) - 8;
+    const U c = tab.load(0, (d < 0) != flip ? 1 : 0, d < 0 ? -d : d);
+    if (win != W - 1) {
+#pragma unroll 1
+      for (int j = 0; j < 4; j++) rp_dbl(x, v);
+    }
+    rp_add(x, v, c);
   }
-  U v0, v1, v2, v3;
-  R::rows(v, v0, v1, v2, v3);
-  const uint64_t z = R::ballot(rf_canon<R>(sel(x.r0, v, rf_sub(x, v1, v2))).zero);
-  const bool e0 = (z & 1u) != 0, e1 = ((z >> 16) & 1u) != 0;
-  return s_ok && a_ok && r_ok && r_canon && e0 && e1;
+  return v;
+}
+
+// The two-wave form's last step on the A wave: X = (A's sum) + (R's sum,
+// cached: cR) + [u]B (cached: cB), then the mode's final check
+template <uint32_t MODE, class R>
+CMTV_HD bool r_join(const RowCtx<R>& x, typename R::U vA, const typename R::U& cR, const typename R::U& cB, bool ok,
+                    bool r_canon) {
+  rp_add(x, vA, cR);
+  rp_add(x, vA, cB);
+  return r_final<MODE>(x, vA, ok, r_canon);
 }
 
 // [u]B's cached coordinates (Y-X, Y+X, 2Z, 2dT) as four canonical 32-byte

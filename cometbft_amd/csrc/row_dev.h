@@ -1,0 +1,86 @@
+// row_dev.h -- the device row policy and LDS table policy of the
+// one-signature-per-wave verifier (row.h; k_verify_row_split in kernels.hip,
+// tools/microbench/row_lat.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "row.h"
+
+namespace cmtv {
+
+// Row policy (row.h): one signature per wave, a field element per 16-lane
+// row. Row moves are DPP (row_ror:r 0x120+r, row_newbcast:r 0x150+r, with
+// bound_ctrl off as in DevQuad); the four row broadcasts of a value are one
+// v_permlane32_swap and two v_permlane16_swap:
+//   permlane32_swap(x, x) = {[x0 x1 x0 x1], [x2 x3 x2 x3]}  (rows)
+//   permlane16_swap(y, y) = {[y0 y0 y2 y2], [y1 y1 y3 y3]}
+#ifndef CMTV_ROW_FUSED
+#define CMTV_ROW_FUSED 1
+#endif
+
+// five column terms r .. r+4 of a product: row_ror:r of f, and g_r's
+// broadcast times the twist in one v_mul_u32_u24_dpp row_newbcast:r (src0 is
+// the DPP operand). The s_nop covers a VALU write of f or g just before (the
+// compiler inserts no wait states in front of inline asm).
+#define CMTV_ROW_TERM(r, F, G, T)                                                \
+  "v_mov_b32_dpp " F ", %[f] row_ror:" #r " row_mask:0xf bank_mask:0xf\n\t"    \
+  "v_mul_u32_u24_dpp " G ", %[g], " T " row_newbcast:" #r " row_mask:0xf bank_mask:0xf\n\t"
+#define CMTV_ROW_TERMS5(r0, r1, r2, r3, r4)                                                          \
+  asm("s_nop 1\n\t" CMTV_ROW_TERM(r0, "%[a0]", "%[b0]", "%[t0]") CMTV_ROW_TERM(r1, "%[a1]", "%[b1]", "%[t1]") \
+          CMTV_ROW_TERM(r2, "%[a2]", "%[b2]", "%[t2]") CMTV_ROW_TERM(r3, "%[a3]", "%[b3]", "%[t3]")             \
+              CMTV_ROW_TERM(r4, "%[a4]", "%[b4]", "%[t4]")                                                     \
+      : [a0] "=&v"(fr[r0]), [b0] "=&v"(gt[r0]), [a1] "=&v"(fr[r1]), [b1] "=&v"(gt[r1]), [a2] "=&v"(fr[r2]),  \
+        [b2] "=&v"(gt[r2]), [a3] "=&v"(fr[r3]), [b3] "=&v"(gt[r3]), [a4] "=&v"(fr[r4]), [b4] "=&v"(gt[r4])    \
+      : [f] "v"(f), [g] "v"(g), [t0] "v"(tw[r0]), [t1] "v"(tw[r1]), [t2] "v"(tw[r2]), [t3] "v"(tw[r3]),      \
+        [t4] "v"(tw[r4]))
+
+struct DevRow {
+  using U = uint32_t;
+  using U64 = uint64_t;
+  using B = bool;
+  static constexpr bool kFusedProduct = CMTV_ROW_FUSED != 0;
+  // the column sums of f g: 15 rotations and 15 fused twisted broadcasts in
+  // three asm blocks, 16 v_mad_u64_u32
+  __device__ __forceinline__ static uint64_t product(const uint32_t* tw, uint32_t f, uint32_t g) {
+    uint32_t fr[16], gt[16];
+    CMTV_ROW_TERMS5(1, 2, 3, 4, 5);
+    CMTV_ROW_TERMS5(6, 7, 8, 9, 10);
+    CMTV_ROW_TERMS5(11, 12, 13, 14, 15);
+    uint64_t acc = (uint64_t)f * (uint32_t)__builtin_amdgcn_mov_dpp((int)g, 0x150, 0xF, 0xF, false);
+#pragma unroll
+    for (int r = 1; r < 16; r++) acc += (uint64_t)fr[r] * gt[r];
+    return acc;
+  }
+  __device__ __forceinline__ static U lane() { return threadIdx.x & 63; }
+  template <int R>
+  __device__ __forceinline__ static U ror(U x) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x120 + R, 0xF, 0xF, false);
+  }
+  template <int R>
+  __device__ __forceinline__ static U bcast(U x) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x150 + R, 0xF, 0xF, false);
+  }
+  __device__ __forceinline__ static void rows(U x, U& b0, U& b1, U& b2, U& b3) {
+    const auto h = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+    const auto lo = __builtin_amdgcn_permlane16_swap(h[0], h[0], false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap(h[1], h[1], false, false);
+    b0 = lo[0];
+    b1 = lo[1];
+    b2 = hi[0];
+    b3 = hi[1];
+  }
+  __device__ __forceinline__ static uint64_t ballot(bool b) { return __ballot(b); }
+  __device__ __forceinline__ static U load_const(const uint16_t* tab, U k) { return tab[k]; }
+};
+
+// the row verifier's (0..8)(-A), (0..8)(-R) cached tables, both signs: one
+// LDS word per lane per entry (a lookup is one ds_read_b32)
+struct DevRowTab {
+  uint32_t* t;
+  uint32_t lane;
+  __device__ __forceinline__ void store(int tb, int neg, int e, uint32_t c) { t[((tb * 2 + neg) * 9 + e) * 64 + lane] = c; }
+  __device__ __forceinline__ uint32_t load(int tb, int neg, int e) const { return t[((tb * 2 + neg) * 9 + e) * 64 + lane]; }
+};
+constexpr int kRowTabWords = 2 * 2 * 9 * 64;
+
+}  // namespace cmtv

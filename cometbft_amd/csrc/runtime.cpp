@@ -54,6 +54,9 @@ constexpr size_t kOctMaxDefault = 3072;       // CMTV_OCT_MAX
 // (row.h) where the two-wave oct kernel would run (CMTV_ROW_MAX; 3 signatures
 // per CU: 768 in one round on 256 CUs)
 constexpr size_t kRowMaxDefault = 768;
+// ... and up to this size its two-waves-per-signature form (one signature
+// per CU: 256 in one round; CMTV_ROW2_MAX)
+constexpr size_t kRow2MaxDefault = 256;
 constexpr size_t kOctSplitMaxDefault = 3072;  // CMTV_OCT_SPLIT_MAX
 // quad batches up to this size take the helper-wave form (k_verify_quad_split:
 // 256 workgroups x 48 signatures per round); CMTV_QUAD_SPLIT_MAX
@@ -370,6 +373,7 @@ struct cmtv_ctx {
   size_t oct_max = kOctMaxDefault;    // ... and up to this size the oct kernel
   size_t oct_split_max = kOctSplitMaxDefault;
   size_t row_max = kRowMaxDefault;
+  size_t row2_max = kRow2MaxDefault;
   size_t quad_split_max = kQuadSplitMaxDefault;
   size_t keyed_quad_max = kKeyedQuadMaxDefault;
   size_t lane_chunk = kChunk;         // signatures per lane-kernel launch (env CMTV_LANE_CHUNK)
@@ -509,9 +513,10 @@ static int enqueue_verify(cmtv_ctx* ctx, CmtvDev& D, size_t n, const uint8_t* d_
   const bool oct_split = oct && n <= ctx->oct_split_max;
   const bool quad_split = quad && !oct && n <= ctx->quad_split_max;
   const bool row = !sr && row_kernel_for(ctx, n);
+  const bool row2 = row && n <= ctx->row2_max;
   const uint32_t kflags = (quad ? kLaunchQuad : 0u) | (oct ? kLaunchOct : 0u) |
                           (oct_split ? kLaunchOctSplit : 0u) | (quad_split ? kLaunchQuadSplit : 0u) |
-                          (row ? kLaunchRow : 0u) | (ctx->force_wide ? kLaunchForceWide : 0u);
+                          (row ? (row2 ? kLaunchRow2 : kLaunchRow) : 0u) | (ctx->force_wide ? kLaunchForceWide : 0u);
   hipError_t e = hipSuccess;
   if (!quad) {
     const size_t lanes = std::min<size_t>(n, ctx->lane_chunk);
@@ -1116,6 +1121,7 @@ static void read_env(cmtv_ctx* ctx) {
   if (const char* qm = std::getenv("CMTV_QUAD_MAX")) ctx->quad_max = (size_t)std::strtoull(qm, nullptr, 10);
   if (const char* om = std::getenv("CMTV_OCT_MAX")) ctx->oct_max = (size_t)std::strtoull(om, nullptr, 10);
   if (const char* rm = std::getenv("CMTV_ROW_MAX")) ctx->row_max = (size_t)std::strtoull(rm, nullptr, 10);
+  if (const char* rm = std::getenv("CMTV_ROW2_MAX")) ctx->row2_max = (size_t)std::strtoull(rm, nullptr, 10);
   if (const char* os = std::getenv("CMTV_OCT_SPLIT_MAX")) ctx->oct_split_max = (size_t)std::strtoull(os, nullptr, 10);
   if (const char* qs = std::getenv("CMTV_QUAD_SPLIT_MAX")) ctx->quad_split_max = (size_t)std::strtoull(qs, nullptr, 10);
   if (const char* kq = std::getenv("CMTV_KEYED_QUAD_MAX")) ctx->keyed_quad_max = (size_t)std::strtoull(kq, nullptr, 10);

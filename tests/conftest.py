@@ -113,9 +113,17 @@ def gpu_ctx_oct2():
 
 @pytest.fixture(scope="session")
 def gpu_ctx_row():
-    """Ed25519 batches up to 4,000 signatures on the row kernel (several
-    rounds of 768), so the corpus and every ragged size run through it."""
-    return _env_ctx(CMTV_ROW_MAX=4000)
+    """Ed25519 batches up to 4,000 signatures on the one-wave row kernel
+    (k_verify_row_split: several rounds of 768), so the corpus and every
+    ragged size run through it."""
+    return _env_ctx(CMTV_ROW_MAX=4000, CMTV_ROW2_MAX=0)
+
+
+@pytest.fixture(scope="session")
+def gpu_ctx_row2():
+    """The same on the two-wave row kernel (k_verify_row2_split: one
+    signature per workgroup, rounds of 256)."""
+    return _env_ctx(CMTV_ROW_MAX=4000, CMTV_ROW2_MAX=4000)
 
 
 @pytest.fixture(scope="session")

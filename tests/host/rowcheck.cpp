@@ -143,6 +143,7 @@ struct HostRow {
   using U = hostlv::U;
   using U64 = hostlv::U64;
   using B = hostlv::B;
+  static constexpr bool kFusedProduct = false;
   static U lane() {
     U r;
     for (int i = 0; i < 64; i++) r.a[i] = i;
@@ -311,6 +312,8 @@ static int mul_selftest() {
 
 int main(int argc, char** argv) {
   if (argc > 1 && !strcmp(argv[1], "mul")) return mul_selftest();
+  // argv[1] == "row2": the two-wave form (r_part for R, then for A, r_join)
+  const bool row2 = argc > 1 && !strcmp(argv[1], "row2");
   LazyBTab bt;
   uint32_t n;
   if (fread(&n, 4, 1, stdin) != 1) return 1;
@@ -345,8 +348,28 @@ int main(int argc, char** argv) {
     hostlv::HostRowTab tab;
     auto get_prep = [&](SigPrep& p) { p = hp; };
     auto get_b = [&]() { return blimb; };
-    const bool v = mode ? r_verify_split<MODE_ZIP215>(HostRow(), limb, pkw, sigw, tab, get_prep, get_b)
-                        : r_verify_split<MODE_GO_STDLIB>(HostRow(), limb, pkw, sigw, tab, get_prep, get_b);
+    bool v;
+    if (row2) {
+      const RowCtx<HostRow> x(HostRow::lane());
+      hostlv::U la, lr;
+      for (int l = 0; l < 64; l++) {
+        const int k = l & 15;
+        la.a[l] = pk[2 * k] | (pk[2 * k + 1] << 8);
+        lr.a[l] = sig[2 * k] | (sig[2 * k + 1] << 8);
+      }
+      hostlv::HostRowTab ta, tr;
+      SigPrep p;
+      bool a_dec, a_x0, r_dec, r_x0;
+      const hostlv::U vr = r_part<1>(x, lr, (sig[31] >> 7) != 0, tr, get_prep, p, r_dec, r_x0);
+      const hostlv::U cr = rp_to_cached(x, vr, x.cst(RowConst::d2));
+      const hostlv::U va = r_part<0>(x, la, (pk[31] >> 7) != 0, ta, get_prep, p, a_dec, a_x0);
+      const bool ok = (p.flags & 4u) != 0 && a_dec && r_dec;
+      const bool r_canon = y_is_canonical(sigw) && !(r_x0 && (sig[31] >> 7));
+      v = mode ? r_join<MODE_ZIP215>(x, va, cr, blimb, ok, r_canon) : r_join<MODE_GO_STDLIB>(x, va, cr, blimb, ok, r_canon);
+    } else {
+      v = mode ? r_verify_split<MODE_ZIP215>(HostRow(), limb, pkw, sigw, tab, get_prep, get_b)
+               : r_verify_split<MODE_GO_STDLIB>(HostRow(), limb, pkw, sigw, tab, get_prep, get_b);
+    }
     const uint8_t o = v;
     fwrite(&o, 1, 1, stdout);
   }

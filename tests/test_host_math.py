@@ -276,14 +276,16 @@ def test_row_field_layer(rowcheck):
     assert out.strip() == b"ok"
 
 
+@pytest.mark.parametrize("form", ["row", "row2"])
 @pytest.mark.parametrize("mode", [0, 1])
-def test_row_pipeline_matches_corpus(rowcheck, corpus, mode):
+def test_row_pipeline_matches_corpus(rowcheck, corpus, mode, form):
     """The one-signature-per-wave row kernel's source (row.h r_verify_split)
     on 64-lane arrays with its operand bounds asserted, the scalars and [u]B
     from the helper wave's code (q_prepare, q_bcomb16): every non-honest
-    vector and a slice of the honest ones."""
+    vector and a slice of the honest ones. row2: the two-wave form (r_part
+    for R and for A, r_join)."""
     idx = _keyed_subset(corpus)
-    got = _run(rowcheck, None, corpus, idx, mode)
+    got = _run(rowcheck, None if form == "row" else form, corpus, idx, mode)
     want = (corpus["go"] if mode == 0 else corpus["zip215"])[idx]
     bad = np.nonzero(got != want)[0]
     assert bad.size == 0, [(idx[int(i)], corpus["cats"][idx[int(i)]]) for i in bad[:10]]

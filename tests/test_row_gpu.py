@@ -31,7 +31,7 @@ def _batch(n, seed, flip=0.1):
     return coracle.pubkeys_from_seeds(seeds), sig, m, off
 
 
-@pytest.mark.parametrize("n", [150, 767, 768])
+@pytest.mark.parametrize("n", [150, 255, 256, 257, 767, 768])
 def test_default_dispatch_commit_sizes(gpu_ctx, n):
     """The default context at and around the row crossover, both modes,
     verdict bytes and bitmap words (no bit past n set)."""

@@ -1,0 +1,14 @@
+#!/bin/bash
+# Row kernel iteration: row GPU tests, timing (row vs oct2) and the phase probe at 150.
+set -o pipefail
+OUT=gpurun_out/row2
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests/test_row_gpu.py tests/test_gpu_parity.py tests/test_wide_gpu.py tests/test_commit_gpu.py -k "row or commit" -x -q \
+  -m gpu --timeout 120 --timeout-method thread > "$OUT/pytest.log" 2>&1
+rc=$?
+tail -5 "$OUT/pytest.log"
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 120 python tools/quick_time.py 150 256 257 768 > "$OUT/time_row.txt" 2>&1 && cat "$OUT/time_row.txt" || exit 1
+true
+cp gpurun_out/phase_probe.json "$OUT/" 2>/dev/null || true

@@ -26,6 +26,9 @@ SLOTS = 8
 
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000
+    # signatures per 4-wave workgroup: 48 (k_verify_quad_split) or 3 (the row
+    # kernel, k_verify_row_split, which the library picks up to CMTV_ROW_MAX)
+    per_wg = int(sys.argv[2]) if len(sys.argv) > 2 else 48
     from cometbft_amd import Context, pack_messages
     from cometbft_amd import _native as N
     from cometbft_amd import testutil as TU
@@ -38,7 +41,7 @@ def main():
     m, off = pack_messages(TU.commit_messages(n, 1000))
     sig = ctx.sign(sv.seeds, m, off)
     pk = np.ascontiguousarray(sv.pubkeys)
-    wgs = -(-n // 48)
+    wgs = -(-n // per_wg)
     out = {}
     for mode, name in ((0, "go"), (1, "zip215")):
         for _ in range(20):

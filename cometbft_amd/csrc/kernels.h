@@ -19,8 +19,9 @@ constexpr uint32_t kCombScratchWordsPerKey = 128 * 320;  // prefix products whil
 // (kLaunchOctSplit), and the quad kernel's helper-wave form (kLaunchQuadSplit)
 constexpr uint32_t kLaunchQuad = 1, kLaunchForceWide = 2, kLaunchOct = 4, kLaunchOctSplit = 8, kLaunchQuadSplit = 16;
 // the one-signature-per-wave row kernel (row.h, k_verify_row_split; Ed25519)
-// and its two-waves-per-signature form (k_verify_row2_split)
-constexpr uint32_t kLaunchRow = 32, kLaunchRow2 = 64;
+// and its two- and four-waves-per-signature forms (k_verify_row2_split,
+// k_verify_row4_split)
+constexpr uint32_t kLaunchRow = 32, kLaunchRow2 = 64, kLaunchRow4 = 128;
 
 // Row kernel bitmap assembly: each launch takes one of kRowSlots slots of a
 // per-device ring (kRowSlotWords words: word 0 a wave counter the kernel

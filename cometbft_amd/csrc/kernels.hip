@@ -464,7 +464,22 @@ __global__ __launch_bounds__(192, 1) void k_verify_row2_split(
     uint32_t ml;
     helper_message(sb, i, msg, off, sbm, mp, ml);
     SigPrep p;
-    q_prepare<MODE>(p, pkp, sgp, mp, ml, force_wide != 0);
+    {
+      // q_prepare's steps, stamped apart in the probe build
+      uint32_t w[16];
+      load_words(w, sgp + 8, 2);
+      const bool s_ok = (w[7] & 0xE0000000u) == 0 && sc_is_canonical(w);
+      uint32_t ts[8], k[8], h[16];
+#pragma unroll
+      for (int j = 0; j < 8; j++) ts[j] = w[j];
+      load_words(w, sgp, 2);
+      load_words(w + 8, pkp, 2);
+      sha512_prefixed<16>(h, w, mp, ml);
+      sc_reduce512(k, h);
+      CMTV_STAMP(5);
+      q_prepare_scalars(p, k, ts, force_wide != 0, MODE != MODE_ZIP215);
+      p.flags |= s_ok ? 4u : 0u;
+    }
     if (t == 0) sig_prep_store(prep, p);
     CMTV_STAMP(1);
     __syncthreads();  // 1: the scalars
@@ -484,6 +499,7 @@ __global__ __launch_bounds__(192, 1) void k_verify_row2_split(
   DevRowTab tab{tab_lds[wave], t};
   SigPrep p;
   bool dec, x0;
+  auto stamp = [&](int k) { CMTV_STAMP(k); (void)k; };
   auto get_prep = [&](SigPrep& q) {
     CMTV_STAMP(1);
     __syncthreads();
@@ -491,7 +507,7 @@ __global__ __launch_bounds__(192, 1) void k_verify_row2_split(
     sig_prep_load(q, prep);
   };
   if (wave == 1) {
-    const uint32_t v = r_part<1>(x, limb, sign, tab, get_prep, p, dec, x0);
+    const uint32_t v = r_part<1>(x, limb, sign, tab, get_prep, p, dec, x0, stamp);
     xr[t] = rp_to_cached(x, v, x.cst(RowConst::d2));
     if (t == 0) {
       xr[64] = dec ? 1u : 0u;
@@ -502,7 +518,7 @@ __global__ __launch_bounds__(192, 1) void k_verify_row2_split(
     CMTV_STAMP(4);
     return;
   }
-  const uint32_t v = r_part<0>(x, limb, sign, tab, get_prep, p, dec, x0);
+  const uint32_t v = r_part<0>(x, limb, sign, tab, get_prep, p, dec, x0, stamp);
   CMTV_STAMP(3);
   __syncthreads();  // 2
   CMTV_STAMP(4);
@@ -512,6 +528,107 @@ __global__ __launch_bounds__(192, 1) void k_verify_row2_split(
   const bool r_canon = y_is_canonical(sigw) && !(r_x0 && (sigw[7] >> 31) != 0);
   const uint32_t cb = (bpt[8 * (t >> 4) + ((t & 15) >> 1)] >> (16 * (t & 1))) & 0xFFFFu;
   bool v_ok = r_join<MODE>(x, v, xr[t], cb, (p.flags & 4u) != 0 && dec && r_dec, r_canon);
+  CMTV_STAMP(5);
+  const bool active = s < n;
+  v_ok = v_ok && active;
+  if (t == 0 && active && out_valid) out_valid[s] = v_ok ? 1 : 0;
+  if (!out_bitmap) return;
+  uint8_t* vb = reinterpret_cast<uint8_t*>(slot + 16);
+  if (t == 0 && active) vb[s] = v_ok ? 1 : 0;
+  __threadfence();
+  uint32_t ticket = 0;
+  if (t == 0) ticket = __hip_atomic_fetch_add(slot, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+  ticket = __shfl(ticket, 0);
+  if (ticket != gridDim.x - 1) return;
+  __threadfence();
+  const uint32_t words = (n + 63) / 64;
+  for (uint32_t w = t; w < words; w += 64) {
+    uint64_t m = 0;
+    for (uint32_t b = 0; b < 64 && 64 * w + b < n; b++) m |= (uint64_t)(vb[64 * w + b] != 0) << b;
+    out_bitmap[w] = m;
+  }
+  if (t == 0) __hip_atomic_store(slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The row verifier over four waves per signature (row.h r_sum_ar / r_part<·,
+// kRowLoWindows> / r_join4), one signature per workgroup and CU, for batches
+// of at most 256: wave 0 (lo) decodes A and R and runs the lowest 21
+// windows of both; waves 1 and 2 (A-hi, R-hi) each decode their point, scale
+// it by 2^84 while the helper (wave 3) hashes, and run the windows above;
+// the helper computes [u]B. Waves 1-2 hand their sums (cached) over at
+// barrier 2; wave 0 adds them and [u]B and checks. The critical path is a
+// high wave's decode + 4W doublings + its additions, instead of the two-wave
+// form's decode + 4W doublings + W additions + the second table.
+template <uint32_t MODE>
+__global__ __launch_bounds__(256, 1) void k_verify_row4_split(
+    uint32_t n, const uint32_t* __restrict__ pk, const uint32_t* __restrict__ sig, const uint8_t* __restrict__ msg,
+    const uint32_t* __restrict__ off, const uint32_t* __restrict__ btab, uint8_t* __restrict__ out_valid,
+    uint64_t* __restrict__ out_bitmap, uint32_t force_wide, SbFuse sb, uint32_t* __restrict__ slot) {
+  const uint32_t wave = threadIdx.x >> 6, t = threadIdx.x & 63;
+  const uint32_t s = blockIdx.x;
+  const uint32_t i = s < n ? s : n - 1;
+  __shared__ uint32_t prep[SIG_PREP_WORDS + 1];
+  __shared__ uint32_t bpt[32];
+  __shared__ uint32_t tab_lo[kRowTabWords];
+  __shared__ uint32_t tab_hi[2][kRowTabWords / 2];
+  __shared__ uint32_t sbm[kSbFuseMaxMsg / 4];
+  __shared__ uint32_t xh[2][64];  // the high parts' sums (cached)
+  const uint32_t* pkp = pk + 8 * (size_t)i;
+  const uint32_t* sgp = sig + 16 * (size_t)i;
+  CMTV_STAMP(0);
+  if (wave == 3) {
+    const uint8_t* mp;
+    uint32_t ml;
+    helper_message(sb, i, msg, off, sbm, mp, ml);
+    SigPrep p;
+    q_prepare<MODE>(p, pkp, sgp, mp, ml, force_wide != 0);
+    if (t == 0) sig_prep_store(prep, p);
+    CMTV_STAMP(1);
+    __syncthreads();  // 1: the scalars
+    CMTV_STAMP(2);
+    ge_p3 B;
+    q_bcomb16(B, p.u, DevBTab{btab});
+    if (t == 0) bpoint_store_bytes(bpt, B);
+    CMTV_STAMP(3);
+    __syncthreads();  // 2: [u]B and the high parts
+    CMTV_STAMP(4);
+    return;
+  }
+  const RowCtx<DevRow> x(DevRow::lane());
+  SigPrep p;
+  auto stamp = [&](int k) { CMTV_STAMP(k); (void)k; };
+  auto get_prep = [&](SigPrep& q) {
+    CMTV_STAMP(1);
+    __syncthreads();
+    CMTV_STAMP(2);
+    sig_prep_load(q, prep);
+  };
+  if (wave != 0) {
+    const uint32_t* src = wave == 2 ? sgp : pkp;
+    const uint32_t limb = reinterpret_cast<const uint16_t*>(src)[t & 15];
+    const bool sign = (src[7] >> 31) != 0;
+    DevRowTab tab{tab_hi[wave - 1], t};
+    bool dec, x0;
+    const uint32_t v = wave == 1 ? r_part<0, kRowLoWindows>(x, limb, sign, tab, get_prep, p, dec, x0, stamp)
+                                 : r_part<1, kRowLoWindows>(x, limb, sign, tab, get_prep, p, dec, x0, stamp);
+    xh[wave - 1][t] = rp_to_cached(x, v, x.cst(RowConst::d2));
+    CMTV_STAMP(3);
+    __syncthreads();  // 2
+    CMTV_STAMP(4);
+    return;
+  }
+  uint32_t pkw[8], sigw[8];
+  load_words(pkw, pkp, 2);
+  load_words(sigw, sgp, 2);
+  const uint32_t limb = reinterpret_cast<const uint16_t*>(((t >> 4) & 1) ? sgp : pkp)[t & 15];
+  DevRowTab tab{tab_lo, t};
+  bool a_ok, r_ok, r_canon;
+  const uint32_t v = r_sum_ar(x, limb, pkw, sigw, tab, get_prep, kRowLoWindows, p, a_ok, r_ok, r_canon);
+  CMTV_STAMP(3);
+  __syncthreads();  // 2
+  CMTV_STAMP(4);
+  const uint32_t cb = (bpt[8 * (t >> 4) + ((t & 15) >> 1)] >> (16 * (t & 1))) & 0xFFFFu;
+  bool v_ok = r_join4<MODE>(x, v, xh[0][t], xh[1][t], cb, (p.flags & 4u) != 0 && a_ok && r_ok, r_canon);
   CMTV_STAMP(5);
   const bool active = s < n;
   v_ok = v_ok && active;
@@ -630,6 +747,18 @@ hipError_t launch_verify(uint32_t mode, uint32_t n, const void* pk, const void* 
   auto op = static_cast<const uint32_t*>(off);
   auto vp = static_cast<uint8_t*>(valid);
   auto bp = static_cast<uint64_t*>(bitmap);
+  if (kflags & kLaunchRow4) {
+    // one signature per 256-lane block (lo, A-hi, R-hi, the helper)
+    if (n > kRowMaxCap || (bp && !row_slot)) return hipErrorInvalidValue;
+    const dim3 grid(n), block(256);
+    if (mode == MODE_ZIP215)
+      hipLaunchKernelGGL(k_verify_row4_split<MODE_ZIP215>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp, fw,
+                         fz, row_slot);
+    else
+      hipLaunchKernelGGL(k_verify_row4_split<MODE_GO_STDLIB>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp,
+                         fw, fz, row_slot);
+    return hipGetLastError();
+  }
   if (kflags & kLaunchRow2) {
     // one signature per 192-lane block (an A wave, an R wave, the helper)
     if (n > kRowMaxCap || (bp && !row_slot)) return hipErrorInvalidValue;

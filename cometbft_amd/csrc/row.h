@@ -429,18 +429,16 @@ CMTV_HD bool r_final(const RowCtx<R>& x, const typename R::U& v, bool ok, bool r
   return ok && r_canon && e0 && e1;
 }
 
-// X = [u]B + [k1](-A) + [|k2|](k2 < 0 ? R : -R) = [k2](R' - R) (quad.h
-// q_straus_prep_b<EXT_B, PREBUILT>) and the final check of the mode, one
-// signature per wave. pk16 / sig16: this lane's 16-bit limb of A / R (row
-// c & 1: 0 = A, 1 = R), pkw / sigw: the 8 words of A / R (uniform).
-// get_prep(SigPrep&) supplies the helper's scalars, get_b() this row's cached
-// coordinate of [u]B.
-template <uint32_t MODE, class R, class Tab, class GetPrep, class GetB>
-CMTV_HD bool r_verify_split(const R&, const typename R::U& limb, const uint32_t pkw[8], const uint32_t sigw[8],
-                            Tab& tab, const GetPrep& get_prep, const GetB& get_b) {
+// The sum over the lowest `lo` windows (all of them when lo >= W) of the
+// one-wave form: decode A (rows 0, 2) and R (rows 1, 3) at once, their tables,
+// then the Straus windows with one A and one R addition each. Out: the
+// scalars (p) and the checks of A and R.
+template <class R, class Tab, class GetPrep>
+CMTV_HD typename R::U r_sum_ar(const RowCtx<R>& x, const typename R::U& limb, const uint32_t pkw[8],
+                               const uint32_t sigw[8], Tab& tab, const GetPrep& get_prep, int lo, SigPrep& p,
+                               bool& a_ok, bool& r_ok, bool& r_canon) {
   using U = typename R::U;
   using B = typename R::B;
-  const RowCtx<R> x(R::lane());
   // ---- phase 1: decode A (rows 0, 2) and R (rows 1, 3) at once
   const B is_r = (x.c & 1u) != 0u;
   const bool a_sign = (pkw[7] >> 31) != 0, r_sign = (sigw[7] >> 31) != 0;
@@ -448,9 +446,10 @@ CMTV_HD bool r_verify_split(const R&, const typename R::U& limb, const uint32_t 
   U xo, to;
   const B dec = rf_decode(x, y, sel(is_r, B(r_sign), B(a_sign)), xo, to);
   const uint64_t decm = R::ballot(dec);
-  const bool a_ok = (decm & 1u) != 0, r_ok = ((decm >> 16) & 1u) != 0;  // lane 0 of rows 0 and 1
+  a_ok = (decm & 1u) != 0;
+  r_ok = ((decm >> 16) & 1u) != 0;  // lane 0 of rows 0 and 1
   const uint64_t x0m = R::ballot(rf_canon<R>(xo).zero);
-  const bool r_canon = y_is_canonical(sigw) && !(((x0m >> 16) & 1u) != 0 && r_sign);
+  r_canon = y_is_canonical(sigw) && !(((x0m >> 16) & 1u) != 0 && r_sign);
   // -A = (-x, y, 1, -x y) and -R, extended, one coordinate per row
   U X0, X1, X2, X3, Y0, Y1, Y2, Y3, T0, T1, T2, T3;
   R::rows(xo, X0, X1, X2, X3);
@@ -461,31 +460,50 @@ CMTV_HD bool r_verify_split(const R&, const typename R::U& limb, const uint32_t 
   // ---- phase 2 (before the scalars): (0..8)(-A) and (0..8)(-R), both signs
   r_build_table(x, tab, 0, na);
   r_build_table(x, tab, 1, nr);
-  // ---- phase 3: Straus over W 4-bit windows of k1 (A) and k2 (R)
-  SigPrep p;
+  // ---- phase 3: Straus over the low windows of k1 (A) and k2 (R)
   get_prep(p);
-  const bool s_ok = (p.flags & 4u) != 0;
   const bool r_flip = (p.flags & 1u) != 0;  // k2 < 0: R's digits flip (its table is of -R)
   const int W = r_windows(p.flags);
+  const int L = lo < W ? lo : W;
   uint32_t tA[8], tR[8];
   hs_digits16(tA, p.k1, W);
   hs_digits16(tR, p.k2, W);
+#pragma unroll 1
+  for (int w = W; w > L; w--) {
+    sc_shift_out(tA, 4);
+    sc_shift_out(tR, 4);
+  }
   U v = rp_identity(x);
 #pragma unroll 1
-  for (int win = W - 1; win >= 0; win--) {
+  for (int win = L - 1; win >= 0; win--) {
     const int dA = (int)sc_shift_out(tA, 4) - 8;
     const int dR = (int)sc_shift_out(tR, 4) - 8;
     const U cA = tab.load(0, dA < 0 ? 1 : 0, dA < 0 ? -dA : dA);
     const U cR = tab.load(1, (dR < 0) != r_flip ? 1 : 0, dR < 0 ? -dR : dR);
-    if (win != W - 1) {
+    if (win != L - 1) {
 #pragma unroll 1
       for (int d = 0; d < 4; d++) rp_dbl(x, v);
     }
     rp_add(x, v, cA);
     rp_add(x, v, cR);
   }
+  return v;
+}
+
+// X = [u]B + [k1](-A) + [|k2|](k2 < 0 ? R : -R) = [k2](R' - R) (quad.h
+// q_straus_prep_b<EXT_B, PREBUILT>) and the final check of the mode, one
+// signature per wave. limb: this lane's 16-bit limb of A / R (row c & 1:
+// 0 = A, 1 = R), pkw / sigw: the 8 words of A / R (uniform). get_prep(SigPrep&)
+// supplies the helper's scalars, get_b() this row's cached coordinate of [u]B.
+template <uint32_t MODE, class R, class Tab, class GetPrep, class GetB>
+CMTV_HD bool r_verify_split(const R&, const typename R::U& limb, const uint32_t pkw[8], const uint32_t sigw[8],
+                            Tab& tab, const GetPrep& get_prep, const GetB& get_b) {
+  const RowCtx<R> x(R::lane());
+  SigPrep p;
+  bool a_ok, r_ok, r_canon;
+  typename R::U v = r_sum_ar(x, limb, pkw, sigw, tab, get_prep, 1 << 20, p, a_ok, r_ok, r_canon);
   rp_add(x, v, get_b());
-  return r_final<MODE>(x, v, s_ok && a_ok && r_ok, r_canon);
+  return r_final<MODE>(x, v, (p.flags & 4u) != 0 && a_ok && r_ok, r_canon);
 }
 
 
@@ -495,27 +513,55 @@ CMTV_HD bool r_verify_split(const R&, const typename R::U& limb, const uint32_t 
 // and ONE addition -- [k1](-A), or [|k2|](k2 < 0 ? R : -R) -- instead of the
 // one-wave form's two additions per window. Returns this row's coordinate
 // of the part's sum; dec / x0 are P's decode flag and whether its x is 0.
-template <int PART, class R, class Tab, class GetPrep>
+struct RowNoStamp {
+  CMTV_HD void operator()(int) const {}
+};
+// windows the four-wave form leaves to its lo wave (84 bits: W >= 33, so the
+// high parts take 12..16 windows, 43 on the wide schedule), and the high
+// waves' doublings before the scalars' barrier (decode ~96k cycles + 24 x
+// ~830 ~ the helper's hash and half-size pair, ~117k)
+constexpr int kRowLoWindows = 21;
+constexpr int kRowHiPreDoublings = 24;
+// HI > 0 (the four-wave form): the part takes only the windows above the
+// lowest HI, against [2^(4 HI)](-P) -- 4 HI doublings of -P before its table,
+// while the helper hashes -- and the lo wave (r_sum_ar) takes the rest.
+template <int PART, int HI = 0, class R, class Tab, class GetPrep, class Stamp = RowNoStamp>
 CMTV_HD typename R::U r_part(const RowCtx<R>& x, const typename R::U& limb, bool sign, Tab& tab,
-                             const GetPrep& get_prep, SigPrep& p, bool& dec, bool& x0) {
+                             const GetPrep& get_prep, SigPrep& p, bool& dec, bool& x0,
+                             const Stamp& stamp = Stamp()) {
   using U = typename R::U;
   const U y = sel(x.k == 15u, limb & 0x7FFFu, limb);
   U xo, to;
   dec = (R::ballot(rf_decode(x, y, typename R::B(sign), xo, to)) & 1u) != 0;
   x0 = (R::ballot(rf_canon<R>(xo).zero) & 1u) != 0;
+  stamp(6);  // decoded
   U X0, X1, X2, X3, Y0, Y1, Y2, Y3, T0, T1, T2, T3;
   R::rows(xo, X0, X1, X2, X3);
   R::rows(y, Y0, Y1, Y2, Y3);
   R::rows(to, T0, T1, T2, T3);
-  r_build_table(x, tab, 0, sel(x.r0, rf_neg(x, X0), sel(x.r1, Y0, sel(x.r2, x.one, rf_neg(x, T0)))));
-  get_prep(p);
+  U np = sel(x.r0, rf_neg(x, X0), sel(x.r1, Y0, sel(x.r2, x.one, rf_neg(x, T0))));
+  if constexpr (HI > 0) {
+    // the workgroup barrier that hands over the scalars (get_prep) sits after
+    // kRowHiPreDoublings of the 4 HI doublings: the high waves reach it about
+    // when the helper does, and the lo wave is not held up by the rest
+    np = rf_carry32(x, np);
+#pragma unroll 1
+    for (int j = 0; j < kRowHiPreDoublings; j++) rp_dbl(x, np);
+    get_prep(p);
+#pragma unroll 1
+    for (int j = kRowHiPreDoublings; j < 4 * HI; j++) rp_dbl(x, np);
+    r_build_table(x, tab, 0, np);
+  } else {
+    r_build_table(x, tab, 0, np);
+    get_prep(p);
+  }
   const bool flip = PART == 1 && (p.flags & 1u) != 0;
   const int W = r_windows(p.flags);
   uint32_t t[8];
   hs_digits16(t, PART == 0 ? p.k1 : p.k2, W);
   U v = rp_identity(x);
 #pragma unroll 1
-  for (int win = W - 1; win >= 0; win--) {
+  for (int win = W - 1; win >= HI; win--) {
     const int d = (int)sc_shift_out(t, 4) - 8;
     const U c = tab.load(0, (d < 0) != flip ? 1 : 0, d < 0 ? -d : d);
     if (win != W - 1) {
@@ -535,6 +581,15 @@ CMTV_HD bool r_join(const RowCtx<R>& x, typename R::U vA, const typename R::U& c
   rp_add(x, vA, cR);
   rp_add(x, vA, cB);
   return r_final<MODE>(x, vA, ok, r_canon);
+}
+
+// The four-wave form's last step on the lo wave: X = lo + A's high part +
+// R's high part + [u]B (the last three cached), then the final check
+template <uint32_t MODE, class R>
+CMTV_HD bool r_join4(const RowCtx<R>& x, typename R::U v, const typename R::U& cA, const typename R::U& cR,
+                     const typename R::U& cB, bool ok, bool r_canon) {
+  rp_add(x, v, cA);
+  return r_join<MODE>(x, v, cR, cB, ok, r_canon);
 }
 
 // [u]B's cached coordinates (Y-X, Y+X, 2Z, 2dT) as four canonical 32-byte

@@ -374,6 +374,9 @@ struct cmtv_ctx {
   size_t oct_split_max = kOctSplitMaxDefault;
   size_t row_max = kRowMaxDefault;
   size_t row2_max = kRow2MaxDefault;
+  // waves per signature at or below row2_max: 4 (k_verify_row4_split) or 2
+  // (CMTV_ROW_WAVES=2: k_verify_row2_split)
+  uint32_t row_waves = 4;
   size_t quad_split_max = kQuadSplitMaxDefault;
   size_t keyed_quad_max = kKeyedQuadMaxDefault;
   size_t lane_chunk = kChunk;         // signatures per lane-kernel launch (env CMTV_LANE_CHUNK)
@@ -516,7 +519,8 @@ static int enqueue_verify(cmtv_ctx* ctx, CmtvDev& D, size_t n, const uint8_t* d_
   const bool row2 = row && n <= ctx->row2_max;
   const uint32_t kflags = (quad ? kLaunchQuad : 0u) | (oct ? kLaunchOct : 0u) |
                           (oct_split ? kLaunchOctSplit : 0u) | (quad_split ? kLaunchQuadSplit : 0u) |
-                          (row ? (row2 ? kLaunchRow2 : kLaunchRow) : 0u) | (ctx->force_wide ? kLaunchForceWide : 0u);
+                          (row ? (row2 ? (ctx->row_waves == 4 ? kLaunchRow4 : kLaunchRow2) : kLaunchRow) : 0u) |
+                          (ctx->force_wide ? kLaunchForceWide : 0u);
   hipError_t e = hipSuccess;
   if (!quad) {
     const size_t lanes = std::min<size_t>(n, ctx->lane_chunk);
@@ -1122,6 +1126,7 @@ static void read_env(cmtv_ctx* ctx) {
   if (const char* om = std::getenv("CMTV_OCT_MAX")) ctx->oct_max = (size_t)std::strtoull(om, nullptr, 10);
   if (const char* rm = std::getenv("CMTV_ROW_MAX")) ctx->row_max = (size_t)std::strtoull(rm, nullptr, 10);
   if (const char* rm = std::getenv("CMTV_ROW2_MAX")) ctx->row2_max = (size_t)std::strtoull(rm, nullptr, 10);
+  if (const char* rw = std::getenv("CMTV_ROW_WAVES")) ctx->row_waves = rw[0] == '2' ? 2u : 4u;
   if (const char* os = std::getenv("CMTV_OCT_SPLIT_MAX")) ctx->oct_split_max = (size_t)std::strtoull(os, nullptr, 10);
   if (const char* qs = std::getenv("CMTV_QUAD_SPLIT_MAX")) ctx->quad_split_max = (size_t)std::strtoull(qs, nullptr, 10);
   if (const char* kq = std::getenv("CMTV_KEYED_QUAD_MAX")) ctx->keyed_quad_max = (size_t)std::strtoull(kq, nullptr, 10);

@@ -123,7 +123,14 @@ def gpu_ctx_row():
 def gpu_ctx_row2():
     """The same on the two-wave row kernel (k_verify_row2_split: one
     signature per workgroup, rounds of 256)."""
-    return _env_ctx(CMTV_ROW_MAX=4000, CMTV_ROW2_MAX=4000)
+    return _env_ctx(CMTV_ROW_MAX=4000, CMTV_ROW2_MAX=4000, CMTV_ROW_WAVES=2)
+
+
+@pytest.fixture(scope="session")
+def gpu_ctx_row4():
+    """The same on the four-wave row kernel (k_verify_row4_split), the
+    default at 256 signatures and below."""
+    return _env_ctx(CMTV_ROW_MAX=4000, CMTV_ROW2_MAX=4000, CMTV_ROW_WAVES=4)
 
 
 @pytest.fixture(scope="session")

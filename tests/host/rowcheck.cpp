@@ -314,6 +314,9 @@ int main(int argc, char** argv) {
   if (argc > 1 && !strcmp(argv[1], "mul")) return mul_selftest();
   // argv[1] == "row2": the two-wave form (r_part for R, then for A, r_join)
   const bool row2 = argc > 1 && !strcmp(argv[1], "row2");
+  // argv[1] == "row4": the four-wave form (the high parts of A and R, the lo
+  // wave's low windows of both, r_join4)
+  const bool row4 = argc > 1 && !strcmp(argv[1], "row4");
   LazyBTab bt;
   uint32_t n;
   if (fread(&n, 4, 1, stdin) != 1) return 1;
@@ -349,7 +352,27 @@ int main(int argc, char** argv) {
     auto get_prep = [&](SigPrep& p) { p = hp; };
     auto get_b = [&]() { return blimb; };
     bool v;
-    if (row2) {
+    if (row4) {
+      const RowCtx<HostRow> x(HostRow::lane());
+      hostlv::U la, lr;
+      for (int l = 0; l < 64; l++) {
+        const int k = l & 15;
+        la.a[l] = pk[2 * k] | (pk[2 * k + 1] << 8);
+        lr.a[l] = sig[2 * k] | (sig[2 * k + 1] << 8);
+      }
+      hostlv::HostRowTab ta, tr, tl;
+      SigPrep p;
+      bool a_dec, a_x0, r_dec, r_x0, a_ok, r_ok, r_canon;
+      const hostlv::U d2 = x.cst(RowConst::d2);
+      const hostlv::U ca = rp_to_cached(
+          x, r_part<0, kRowLoWindows>(x, la, (pk[31] >> 7) != 0, ta, get_prep, p, a_dec, a_x0), d2);
+      const hostlv::U cr = rp_to_cached(
+          x, r_part<1, kRowLoWindows>(x, lr, (sig[31] >> 7) != 0, tr, get_prep, p, r_dec, r_x0), d2);
+      const hostlv::U vl = r_sum_ar(x, limb, pkw, sigw, tl, get_prep, kRowLoWindows, p, a_ok, r_ok, r_canon);
+      const bool ok = (p.flags & 4u) != 0 && a_ok && r_ok;
+      v = mode ? r_join4<MODE_ZIP215>(x, vl, ca, cr, blimb, ok, r_canon)
+               : r_join4<MODE_GO_STDLIB>(x, vl, ca, cr, blimb, ok, r_canon);
+    } else if (row2) {
       const RowCtx<HostRow> x(HostRow::lane());
       hostlv::U la, lr;
       for (int l = 0; l < 64; l++) {

@@ -276,14 +276,15 @@ def test_row_field_layer(rowcheck):
     assert out.strip() == b"ok"
 
 
-@pytest.mark.parametrize("form", ["row", "row2"])
+@pytest.mark.parametrize("form", ["row", "row2", "row4"])
 @pytest.mark.parametrize("mode", [0, 1])
 def test_row_pipeline_matches_corpus(rowcheck, corpus, mode, form):
     """The one-signature-per-wave row kernel's source (row.h r_verify_split)
     on 64-lane arrays with its operand bounds asserted, the scalars and [u]B
     from the helper wave's code (q_prepare, q_bcomb16): every non-honest
     vector and a slice of the honest ones. row2: the two-wave form (r_part
-    for R and for A, r_join)."""
+    for R and for A, r_join); row4: the four-wave form (the high parts of A
+    and R from [2^84]P, the low windows of both, r_join4)."""
     idx = _keyed_subset(corpus)
     got = _run(rowcheck, None if form == "row" else form, corpus, idx, mode)
     want = (corpus["go"] if mode == 0 else corpus["zip215"])[idx]

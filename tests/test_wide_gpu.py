@@ -72,10 +72,10 @@ def _mixed_batch(kind, waves_per_vector=1, seed=3):
     return np.array(pk), np.array(sig), m2, off2
 
 
-@pytest.mark.parametrize("kernel", ["row2", "row", "oct2", "oct", "quad2", "quad", "lane"])
+@pytest.mark.parametrize("kernel", ["row4", "row2", "row", "oct2", "oct", "quad2", "quad", "lane"])
 @pytest.mark.parametrize("mode", [MODE_GO_STDLIB, MODE_ZIP215])
-def test_ed25519_wide_in_mixed_waves(gpu_ctx_row2, gpu_ctx_row, gpu_ctx_oct2, gpu_ctx_oct1, gpu_ctx_quad, gpu_ctx_quad1, gpu_ctx_lane, kernel, mode):
-    ctx = {"row2": gpu_ctx_row2, "row": gpu_ctx_row, "oct2": gpu_ctx_oct2, "oct": gpu_ctx_oct1, "quad2": gpu_ctx_quad, "quad": gpu_ctx_quad1,
+def test_ed25519_wide_in_mixed_waves(gpu_ctx_row4, gpu_ctx_row2, gpu_ctx_row, gpu_ctx_oct2, gpu_ctx_oct1, gpu_ctx_quad, gpu_ctx_quad1, gpu_ctx_lane, kernel, mode):
+    ctx = {"row4": gpu_ctx_row4, "row2": gpu_ctx_row2, "row": gpu_ctx_row, "oct2": gpu_ctx_oct2, "oct": gpu_ctx_oct1, "quad2": gpu_ctx_quad, "quad": gpu_ctx_quad1,
            "lane": gpu_ctx_lane}[kernel]
     pk, sig, m, off = _mixed_batch("ed25519")
     exp = coracle.verify_batch(pk, sig, m, off, mode, nthreads=8)
@@ -142,6 +142,8 @@ def forced_wide_ctxs():
     try:
         os.environ["CMTV_ROW_MAX"] = "4000"
         os.environ["CMTV_ROW2_MAX"] = "4000"
+        r4ctx = Context(device=0)
+        os.environ["CMTV_ROW_WAVES"] = "2"
         r2ctx = Context(device=0)
         os.environ["CMTV_ROW2_MAX"] = "0"
         rctx = Context(device=0)
@@ -154,12 +156,12 @@ def forced_wide_ctxs():
         os.environ["CMTV_QUAD_SPLIT_MAX"] = "0"
         qctx = Context(device=0)
     finally:
-        for k in ("CMTV_FORCE_WIDE", "CMTV_ROW_MAX", "CMTV_ROW2_MAX", "CMTV_OCT_MAX", "CMTV_OCT_SPLIT_MAX", "CMTV_QUAD_SPLIT_MAX"):
+        for k in ("CMTV_FORCE_WIDE", "CMTV_ROW_MAX", "CMTV_ROW2_MAX", "CMTV_ROW_WAVES", "CMTV_OCT_MAX", "CMTV_OCT_SPLIT_MAX", "CMTV_QUAD_SPLIT_MAX"):
             os.environ.pop(k, None)
-    return {"row2": r2ctx, "row": rctx, "oct2": o2ctx, "oct": octx, "quad2": q2ctx, "quad": qctx}
+    return {"row4": r4ctx, "row2": r2ctx, "row": rctx, "oct2": o2ctx, "oct": octx, "quad2": q2ctx, "quad": qctx}
 
 
-@pytest.mark.parametrize("kernel", ["row2", "row", "oct2", "oct", "quad2", "quad"])
+@pytest.mark.parametrize("kernel", ["row4", "row2", "row", "oct2", "oct", "quad2", "quad"])
 @pytest.mark.parametrize("mode,key", [(MODE_GO_STDLIB, "go"), (MODE_ZIP215, "zip215")])
 def test_forced_wide_schedule_on_corpus(forced_wide_ctxs, corpus, mode, key, kernel):
     """CMTV_FORCE_WIDE: every quad (or oct) takes the wide fallback (k1 = k,

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Row kernel iteration: row GPU tests, timing (row vs oct2) and the phase probe at 150.
+# Row kernel iteration: row GPU tests (all forms), timing A/B of the forms at 150/256.
 set -o pipefail
 OUT=gpurun_out/row2
 mkdir -p "$OUT"
@@ -9,6 +9,5 @@ timeout -k 10 600 python -u -m pytest tests/test_row_gpu.py tests/test_gpu_parit
 rc=$?
 tail -5 "$OUT/pytest.log"
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 120 python tools/quick_time.py 150 256 257 768 > "$OUT/time_row.txt" 2>&1 && cat "$OUT/time_row.txt" || exit 1
-true
-cp gpurun_out/phase_probe.json "$OUT/" 2>/dev/null || true
+timeout -k 10 120 python tools/quick_time.py 150 256 > "$OUT/time_row4.txt" 2>&1 && cat "$OUT/time_row4.txt" || exit 1
+CMTV_ROW_WAVES=2 timeout -k 10 120 python tools/quick_time.py 150 256 > "$OUT/time_row2.txt" 2>&1 && cat "$OUT/time_row2.txt" || exit 1

@@ -1,0 +1,67 @@
+"""Phase timeline of the two-wave row kernel (k_verify_row2_split) on one
+150-validator batch, from the probe build of the library.
+
+  make -C cometbft_amd/csrc OUT=../../abtest/libprobe.so BUILD=../../build/probe KFLAGS=-DCMTV_PHASE_PROBE
+  CMTV_LIBRARY=$PWD/abtest/libprobe.so [CMTV_ROW_WAVES=2] python tools/row_phase.py [n] [row4|row2]
+
+Shader-clock stamps per wave (kernels.hip CMTV_STAMP), relative to the
+workgroup's first entry: A wave (0) and R wave (1): 6 decoded, 1 at barrier 1
+(table built), 2 released, 3 at barrier 2 (windows done), 4 released, 5 end
+(A: verdict); helper (2): 5 hashed (SHA-512 + mod L), 1 scalars ready,
+3 [u]B ready. Medians over workgroups, per mode, into gpurun_out/row_phase.json.
+"""
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+SLOTS = 8
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 150
+    form = sys.argv[2] if len(sys.argv) > 2 else "row4"
+    from cometbft_amd import Context, pack_messages
+    from cometbft_amd import _native as N
+    from cometbft_amd import testutil as TU
+
+    fn = N.lib().cmtv_debug_phase_times
+    fn.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t]
+    ctx = Context(device=0)
+    sv = TU.make_validator_set(ctx, n)
+    m, off = pack_messages(TU.commit_messages(n, 1000))
+    sig = ctx.sign(sv.seeds, m, off)
+    pk = np.ascontiguousarray(sv.pubkeys)
+    out = {}
+    if form == "row2":
+        names = {"A": (0, [6, 1, 2, 3, 4, 5]), "R": (1, [6, 1, 2, 3]), "helper": (2, [5, 1, 3])}
+    else:  # row4: lo (decodes A and R), A-hi, R-hi, helper
+        names = {"lo": (0, [1, 2, 3, 4, 5]), "A_hi": (1, [6, 1, 2, 3]), "R_hi": (2, [6, 1, 2, 3]),
+                 "helper": (3, [1, 3])}
+    nw = len(names)
+    for mode, name in ((0, "go"), (1, "zip215")):
+        for _ in range(10):
+            v = ctx.verify(pk, sig, m, off, mode)
+        assert v.all()
+        buf = np.zeros(n * 4 * SLOTS, np.uint64)
+        assert fn(buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), buf.size) == 0
+        st = buf.reshape(n, 4, SLOTS).astype(np.int64)
+        t0 = st[:, :nw, 0].min(axis=1)
+        rel = st - t0[:, None, None]
+        res = {}
+        for w, (wi, slots) in names.items():
+            res[w] = {str(k): float(np.median(rel[:, wi, k])) for k in slots}
+        res["end_max"] = float((st[:, 0, 5] - t0).max())
+        out[name] = res
+        print(name, json.dumps(res), flush=True)
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "row_phase.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

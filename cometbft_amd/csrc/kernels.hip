@@ -345,6 +345,50 @@ __global__ __launch_bounds__(128, CMTV_QUAD_WAVES_PER_EU) void k_verify_oct_spli
   if (t == 0 && out_bitmap) reinterpret_cast<uint8_t*>(out_bitmap)[gid >> 6] = (uint8_t)x;
 }
 
+// [u]B for a helper wave whose 64 lanes all hold the same signature (the
+// row forms with one signature per workgroup): the 16 comb rows (digit j of
+// u is 16-bit chunk j of u + 0x8000...8000, verify_core.h BC16 blocks) are
+// fetched at once -- lane L loads a quarter of row L / 4 into LDS -- and
+// q_bcomb16 then reads them from LDS (one round trip to the 75 MB table
+// instead of sixteen dependent ones).
+struct LdsCombB {
+  const uint32_t* rows;  // [16][BTAB_ROW_WORDS]
+  __device__ __forceinline__ void load_fe(int e, int c, fe& r) const {
+    const uint32_t* q = rows + ((e - BC16_BASE) >> 15) * BTAB_ROW_WORDS + c * BTAB_COORD_WORDS;
+#pragma unroll
+    for (int i = 0; i < 10; i++) r.v[i] = q[i];
+  }
+};
+static_assert(BT16_ENTRIES == 1 << 15, "LdsCombB maps a comb row to its position by >> 15");
+
+__device__ __forceinline__ void helper_bcomb_prefetched(ge_p3& B, const uint32_t u[8], const uint32_t* btab,
+                                                        uint32_t* lds_rows, uint32_t t) {
+  uint32_t tb[8];
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint64_t v = (uint64_t)u[i] + 0x80008000u + c;
+    tb[i] = (uint32_t)v;
+    c = v >> 32;
+  }
+  const uint32_t j = t >> 2, part = t & 3;
+  uint32_t w = tb[0];
+#pragma unroll
+  for (int i = 1; i < 8; i++) w = (j >> 1) == (uint32_t)i ? tb[i] : w;
+  const int d = (int)((w >> (16 * (j & 1))) & 0xFFFFu) - 0x8000;
+  const int ib = d < 0 ? -d : d;
+  const uint32_t* src = btab + (size_t)(BC16_BASE + j * BT16_ENTRIES + (ib > 0 ? ib - 1 : 0)) * BTAB_ROW_WORDS + 9 * part;
+  uint32_t v[9];
+#pragma unroll
+  for (int i = 0; i < 9; i++) v[i] = src[i];
+#pragma unroll
+  for (int i = 0; i < 9; i++) lds_rows[j * BTAB_ROW_WORDS + 9 * part + i] = v[i];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  q_bcomb16(B, u, LdsCombB{lds_rows});
+}
+
 // One signature per wave (row.h): for the smallest batches (a 150-validator
 // commit), where SIMDs are idle and each signature's chain of field products
 // is the kernel time. A 4-wave workgroup takes 3 signatures: waves 0-2
@@ -453,6 +497,7 @@ __global__ __launch_bounds__(192, 1) void k_verify_row2_split(
   const uint32_t i = s < n ? s : n - 1;
   __shared__ uint32_t prep[SIG_PREP_WORDS + 1];
   __shared__ uint32_t bpt[32];
+  __shared__ uint32_t brows[16 * BTAB_ROW_WORDS];  // the helper's [u]B comb rows
   __shared__ uint32_t tab_lds[2][kRowTabWords / 2];
   __shared__ uint32_t sbm[kSbFuseMaxMsg / 4];
   __shared__ uint32_t xr[64 + 2];  // R's sum (cached), its decode flag and x = 0
@@ -485,7 +530,7 @@ __global__ __launch_bounds__(192, 1) void k_verify_row2_split(
     __syncthreads();  // 1: the scalars
     CMTV_STAMP(2);
     ge_p3 B;
-    q_bcomb16(B, p.u, DevBTab{btab});
+    helper_bcomb_prefetched(B, p.u, btab, brows, t);
     if (t == 0) bpoint_store_bytes(bpt, B);
     CMTV_STAMP(3);
     __syncthreads();  // 2: [u]B and R's sum
@@ -569,6 +614,7 @@ __global__ __launch_bounds__(256, 1) void k_verify_row4_split(
   const uint32_t i = s < n ? s : n - 1;
   __shared__ uint32_t prep[SIG_PREP_WORDS + 1];
   __shared__ uint32_t bpt[32];
+  __shared__ uint32_t brows[16 * BTAB_ROW_WORDS];  // the helper's [u]B comb rows
   __shared__ uint32_t tab_lo[kRowTabWords];
   __shared__ uint32_t tab_hi[2][kRowTabWords / 2];
   __shared__ uint32_t sbm[kSbFuseMaxMsg / 4];
@@ -587,7 +633,7 @@ __global__ __launch_bounds__(256, 1) void k_verify_row4_split(
     __syncthreads();  // 1: the scalars
     CMTV_STAMP(2);
     ge_p3 B;
-    q_bcomb16(B, p.u, DevBTab{btab});
+    helper_bcomb_prefetched(B, p.u, btab, brows, t);
     if (t == 0) bpoint_store_bytes(bpt, B);
     CMTV_STAMP(3);
     __syncthreads();  // 2: [u]B and the high parts

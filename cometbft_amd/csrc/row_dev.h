@@ -34,6 +34,31 @@ namespace cmtv {
       : [f] "v"(f), [g] "v"(g), [t0] "v"(tw[r0]), [t1] "v"(tw[r1]), [t2] "v"(tw[r2]), [t3] "v"(tw[r3]),      \
         [t4] "v"(tw[r4]))
 
+#ifndef CMTV_ROW_ASM_BLOCKS
+#define CMTV_ROW_ASM_BLOCKS 1
+#endif
+// all fifteen terms in one asm block: one s_nop instead of three
+#define CMTV_ROW_TERMS15()                                                                                     \
+  asm("s_nop 1\n\t" CMTV_ROW_TERM(1, "%[a1]", "%[b1]", "%[t1]") CMTV_ROW_TERM(2, "%[a2]", "%[b2]", "%[t2]")      \
+          CMTV_ROW_TERM(3, "%[a3]", "%[b3]", "%[t3]") CMTV_ROW_TERM(4, "%[a4]", "%[b4]", "%[t4]")                  \
+              CMTV_ROW_TERM(5, "%[a5]", "%[b5]", "%[t5]") CMTV_ROW_TERM(6, "%[a6]", "%[b6]", "%[t6]")              \
+                  CMTV_ROW_TERM(7, "%[a7]", "%[b7]", "%[t7]") CMTV_ROW_TERM(8, "%[a8]", "%[b8]", "%[t8]")          \
+                      CMTV_ROW_TERM(9, "%[a9]", "%[b9]", "%[t9]") CMTV_ROW_TERM(10, "%[a10]", "%[b10]", "%[t10]")  \
+                          CMTV_ROW_TERM(11, "%[a11]", "%[b11]", "%[t11]")                                          \
+                              CMTV_ROW_TERM(12, "%[a12]", "%[b12]", "%[t12]")                                      \
+                                  CMTV_ROW_TERM(13, "%[a13]", "%[b13]", "%[t13]")                                  \
+                                      CMTV_ROW_TERM(14, "%[a14]", "%[b14]", "%[t14]")                              \
+                                          CMTV_ROW_TERM(15, "%[a15]", "%[b15]", "%[t15]")                          \
+      : [a1] "=&v"(fr[1]), [b1] "=&v"(gt[1]), [a2] "=&v"(fr[2]), [b2] "=&v"(gt[2]), [a3] "=&v"(fr[3]),             \
+        [b3] "=&v"(gt[3]), [a4] "=&v"(fr[4]), [b4] "=&v"(gt[4]), [a5] "=&v"(fr[5]), [b5] "=&v"(gt[5]),             \
+        [a6] "=&v"(fr[6]), [b6] "=&v"(gt[6]), [a7] "=&v"(fr[7]), [b7] "=&v"(gt[7]), [a8] "=&v"(fr[8]),             \
+        [b8] "=&v"(gt[8]), [a9] "=&v"(fr[9]), [b9] "=&v"(gt[9]), [a10] "=&v"(fr[10]), [b10] "=&v"(gt[10]),         \
+        [a11] "=&v"(fr[11]), [b11] "=&v"(gt[11]), [a12] "=&v"(fr[12]), [b12] "=&v"(gt[12]), [a13] "=&v"(fr[13]),   \
+        [b13] "=&v"(gt[13]), [a14] "=&v"(fr[14]), [b14] "=&v"(gt[14]), [a15] "=&v"(fr[15]), [b15] "=&v"(gt[15])    \
+      : [f] "v"(f), [g] "v"(g), [t1] "v"(tw[1]), [t2] "v"(tw[2]), [t3] "v"(tw[3]), [t4] "v"(tw[4]),             \
+        [t5] "v"(tw[5]), [t6] "v"(tw[6]), [t7] "v"(tw[7]), [t8] "v"(tw[8]), [t9] "v"(tw[9]), [t10] "v"(tw[10]),  \
+        [t11] "v"(tw[11]), [t12] "v"(tw[12]), [t13] "v"(tw[13]), [t14] "v"(tw[14]), [t15] "v"(tw[15]))
+
 struct DevRow {
   using U = uint32_t;
   using U64 = uint64_t;
@@ -43,9 +68,13 @@ struct DevRow {
   // three asm blocks, 16 v_mad_u64_u32
   __device__ __forceinline__ static uint64_t product(const uint32_t* tw, uint32_t f, uint32_t g) {
     uint32_t fr[16], gt[16];
+#if CMTV_ROW_ASM_BLOCKS == 1
+    CMTV_ROW_TERMS15();
+#else
     CMTV_ROW_TERMS5(1, 2, 3, 4, 5);
     CMTV_ROW_TERMS5(6, 7, 8, 9, 10);
     CMTV_ROW_TERMS5(11, 12, 13, 14, 15);
+#endif
     uint64_t acc = (uint64_t)f * (uint32_t)__builtin_amdgcn_mov_dpp((int)g, 0x150, 0xF, 0xF, false);
 #pragma unroll
     for (int r = 1; r < 16; r++) acc += (uint64_t)fr[r] * gt[r];

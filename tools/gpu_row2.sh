@@ -11,3 +11,4 @@ tail -5 "$OUT/pytest.log"
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 120 python tools/quick_time.py 150 256 > "$OUT/time_row4.txt" 2>&1 && cat "$OUT/time_row4.txt" || exit 1
 CMTV_ROW_WAVES=2 timeout -k 10 120 python tools/quick_time.py 150 256 > "$OUT/time_row2.txt" 2>&1 && cat "$OUT/time_row2.txt" || exit 1
+CMTV_LIBRARY=$PWD/abtest/libprobe.so timeout -k 10 180 python tools/row_phase.py 150 row4 > "$OUT/phase.txt" 2>&1; cat "$OUT/phase.txt"

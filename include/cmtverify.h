@@ -116,10 +116,12 @@ typedef struct cmtv_device_stats {
  * tables of (1..128)B, (1..128)[2^124]B and (1..128)[2^128]B (built on the
  * device), allocates pinned staging.
  * Replaces: nothing in the reference (it has no device state).
- * Environment (read at open): CMTV_OCT_MAX / CMTV_OCT_SPLIT_MAX / CMTV_QUAD_MAX / CMTV_QUAD_SPLIT_MAX /
- * CMTV_KEYED_QUAD_MAX / CMTV_LANE_CHUNK (kernel crossovers: Ed25519 batches
- * up to CMTV_OCT_MAX (3072) take 8 lanes per signature, up to CMTV_QUAD_MAX
- * (40000) 4 lanes, larger ones one lane), CMTV_FAULT_AT=N (test knob: the N-th verification
+ * Environment (read at open): CMTV_ROW2_MAX / CMTV_ROW_MAX / CMTV_ROW_WAVES / CMTV_OCT_MAX /
+ * CMTV_OCT_SPLIT_MAX / CMTV_QUAD_MAX / CMTV_QUAD_SPLIT_MAX / CMTV_KEYED_QUAD_MAX / CMTV_LANE_CHUNK
+ * (kernel crossovers: Ed25519 batches up to CMTV_ROW2_MAX (256) take a whole
+ * CU per signature (four waves; CMTV_ROW_WAVES=2: two), up to CMTV_ROW_MAX
+ * (768) one wave per signature, up to CMTV_OCT_MAX (3072) 8 lanes, up to
+ * CMTV_QUAD_MAX (40000) 4 lanes, larger ones one lane), CMTV_FAULT_AT=N (test knob: the N-th verification
  * launch of the context fails with CMTV_EHIP without running; libs/fail
  * FAIL_TEST_INDEX analogue), CMTV_FORCE_WIDE=1 (test knob: the quad kernels
  * take the 64-window half-scalar fallback for every signature),

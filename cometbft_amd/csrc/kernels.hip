@@ -697,6 +697,109 @@ __global__ __launch_bounds__(256, 1) void k_verify_row4_split(
   if (t == 0) __hip_atomic_store(slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Registered keys, one signature per workgroup in the row layout (row.h
+// r_decode_neg_r / r_kcomb / r_bcomb16 / r_keyed_join), for batches of at
+// most 256 (the 150-validator VerifyCommit with the keyset cache): wave 3
+// hashes k; wave 2 adds [s]B over the B table's 16-position radix-2^16 comb
+// (s needs no hash); wave 1 takes k at barrier 1 and adds [k](-A) over the
+// key's radix-256 comb (32 additions); wave 0 decodes R, meeting barrier 1
+// half-way through its square-root chain (so it never waits for the hash),
+// and after barrier 2 adds both sums to -R and checks. Comb rows are
+// converted to the row layout as they are read (DevRow::niels_limb).
+// Bitmap as k_verify_row_split.
+template <uint32_t MODE>
+__global__ __launch_bounds__(256, 1) void k_verify_keyed_row_split(
+    uint32_t n, uint32_t n_keys, const uint32_t* __restrict__ key_idx, const uint32_t* __restrict__ sig,
+    const uint8_t* __restrict__ msg, const uint32_t* __restrict__ off, const uint32_t* __restrict__ keys_pk,
+    const uint8_t* __restrict__ keys_ok, const uint32_t* __restrict__ ktabs, const uint32_t* __restrict__ btab,
+    uint8_t* __restrict__ out_valid, uint64_t* __restrict__ out_bitmap, uint32_t* __restrict__ slot) {
+  const uint32_t wave = threadIdx.x >> 6, t = threadIdx.x & 63;
+  const uint32_t s = blockIdx.x;
+  const uint32_t i = s < n ? s : n - 1;
+  __shared__ uint32_t tks[8];
+  __shared__ uint32_t xa[64], xb[64];
+  uint32_t kid = key_idx[i];
+  const bool kin = kid < n_keys;
+  kid = kin ? kid : 0;
+  const uint32_t* sgp = sig + 16 * (size_t)i;
+  CMTV_STAMP(0);
+  if (wave == 3) {
+    const uint32_t m0 = off[i], m1 = off[i + 1];
+    uint32_t tk[8];
+    q_keyed_challenge(tk, keys_pk + 8 * (size_t)kid, sgp, msg + m0, m1 - m0);
+    if (t == 0)
+#pragma unroll
+      for (int j = 0; j < 8; j++) tks[j] = tk[j];
+    CMTV_STAMP(1);
+    __syncthreads();  // 1: k
+    CMTV_STAMP(2);
+    __syncthreads();  // 2
+    return;
+  }
+  const RowCtx<DevRow> x(DevRow::lane());
+  const uint32_t d2 = x.cst(RowConst::d2);
+  if (wave == 2) {
+    uint32_t sw[8];
+    load_words(sw, sgp + 8, 2);
+    const uint32_t v = r_bcomb16(x, sw, [&](int e) { return btab + (size_t)e * BTAB_ROW_WORDS; });
+    xb[t] = rp_to_cached(x, v, d2);
+    CMTV_STAMP(1);
+    __syncthreads();  // 1
+    CMTV_STAMP(2);
+    __syncthreads();  // 2: [s]B
+    return;
+  }
+  if (wave == 1) {
+    CMTV_STAMP(1);
+    __syncthreads();  // 1: k
+    CMTV_STAMP(2);
+    uint32_t tk[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) tk[j] = tks[j];
+    const uint32_t v = r_kcomb(x, tk, ktabs + (size_t)kid * COMB_TABLE_WORDS);
+    xa[t] = rp_to_cached(x, v, d2);
+    CMTV_STAMP(3);
+    __syncthreads();  // 2: [k](-A)
+    return;
+  }
+  uint32_t sigw[8], sw[8];
+  load_words(sigw, sgp, 2);
+  load_words(sw, sgp + 8, 2);
+  const uint32_t limb = reinterpret_cast<const uint16_t*>(sgp)[t & 15];
+  bool r_ok;
+  const uint32_t nr = r_decode_neg_r<MODE>(x, limb, sigw, r_ok, [&]() {
+    CMTV_STAMP(1);
+    __syncthreads();  // 1
+    CMTV_STAMP(2);
+  });
+  CMTV_STAMP(3);
+  __syncthreads();  // 2
+  CMTV_STAMP(4);
+  const bool s_ok = (sw[7] & 0xE0000000u) == 0 && sc_is_canonical(sw);
+  const bool ok = kin && keys_ok[kid] != 0 && s_ok && r_ok;
+  bool v_ok = r_keyed_join<MODE>(x, nr, xa[t], xb[t], ok);
+  CMTV_STAMP(5);
+  const bool active = s < n;
+  v_ok = v_ok && active;
+  if (t == 0 && active && out_valid) out_valid[s] = v_ok ? 1 : 0;
+  if (!out_bitmap) return;
+  uint8_t* vb = reinterpret_cast<uint8_t*>(slot + 16);
+  if (t == 0 && active) vb[s] = v_ok ? 1 : 0;
+  __threadfence();
+  uint32_t ticket = 0;
+  if (t == 0) ticket = __hip_atomic_fetch_add(slot, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+  ticket = __shfl(ticket, 0);
+  if (ticket != gridDim.x - 1) return;
+  __threadfence();
+  const uint32_t words = (n + 63) / 64;
+  for (uint32_t w = t; w < words; w += 64) {
+    uint64_t m = 0;
+    for (uint32_t b = 0; b < 64 && 64 * w + b < n; b++) m |= (uint64_t)(vb[64 * w + b] != 0) << b;
+    out_bitmap[w] = m;
+  }
+  if (t == 0) __hip_atomic_store(slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Comb of (negate ? -P : P) for n_keys encoded points; workgroup = key,
 // thread = multiple d = 1..128. keys_ok[key] records whether P decoded.
 __global__ __launch_bounds__(128) void k_comb_build(const uint32_t* __restrict__ keys_pk, uint8_t* __restrict__ keys_ok,
@@ -1008,7 +1111,7 @@ hipError_t launch_verify_keyed(uint32_t mode, uint32_t n, uint32_t n_keys, const
                                const uint32_t* ktabs, const uint32_t* bcomb, void* valid, void* bitmap,
                                bool quad, bool split, uint32_t k_wait, uint32_t* diag, uint32_t batch_kb,
                                uint32_t* scr, const uint32_t* wtabs, const uint32_t* btab, bool wide_dma,
-                               hipStream_t s) {
+                               hipStream_t s, uint32_t* row_slot) {
   if (n == 0) return hipSuccess;
   auto ki = static_cast<const uint32_t*>(key_idx);
   auto sgp = static_cast<const uint32_t*>(sig);
@@ -1016,6 +1119,17 @@ hipError_t launch_verify_keyed(uint32_t mode, uint32_t n, uint32_t n_keys, const
   auto op = static_cast<const uint32_t*>(off);
   auto vp = static_cast<uint8_t*>(valid);
   auto bp = static_cast<uint64_t*>(bitmap);
+  if (row_slot) {
+    // the keyed row kernel: one signature per 256-lane block
+    if (n > kRowMaxCap) return hipErrorInvalidValue;
+    if (mode == MODE_ZIP215)
+      hipLaunchKernelGGL(k_verify_keyed_row_split<MODE_ZIP215>, dim3(n), dim3(256), 0, s, n, n_keys, ki, sgp, mp, op,
+                         keys_pk, keys_ok, ktabs, btab, vp, bp, row_slot);
+    else
+      hipLaunchKernelGGL(k_verify_keyed_row_split<MODE_GO_STDLIB>, dim3(n), dim3(256), 0, s, n, n_keys, ki, sgp, mp,
+                         op, keys_pk, keys_ok, ktabs, btab, vp, bp, row_slot);
+    return hipGetLastError();
+  }
   if (quad && split) {
     const uint32_t slices = 4 * ((n + 63) / 64);
     const dim3 grid((slices + 2) / 3), block(320);

@@ -33,6 +33,7 @@
 // with free functions mad64(a, b, c) = a b + c (u64), lo32, shr64(x, s) (low
 // word of x >> s), mul24, sel(c, a, b). Control flow is wave-uniform.
 #pragma once
+#include "keyed.h"
 #include "quad.h"
 
 namespace cmtv {
@@ -318,9 +319,15 @@ CMTV_HD typename R::U rp_cached_identity(const RowCtx<R>& x) {
 // Go 1.19 Point.SetBytes (ge25519.h p3_frombytes) on every row at once: y =
 // the row's limbs (bit 255 already cleared, non-canonical y taken mod p), sign
 // = its sign bit. Returns the decode flag; xo, to = x and x y (carried).
-template <class R>
+struct RowNoHook {
+  CMTV_HD void operator()() const {}
+};
+// mid(): called once half-way through the square-root chain (after 2^100 - 1,
+// ~150 of its ~265 products): the keyed row kernel's R wave meets the
+// workgroup barrier there
+template <class R, class Mid = RowNoHook>
 CMTV_HD typename R::B rf_decode(const RowCtx<R>& x, const typename R::U& y, const typename R::B& sign,
-                                typename R::U& xo, typename R::U& to) {
+                                typename R::U& xo, typename R::U& to, const Mid& mid = Mid()) {
   using U = typename R::U;
   const U y2 = rf_sq(x, y);
   const U u = rf_carry32(x, rf_sub(x, y2, x.one));                     // y^2 - 1
@@ -349,6 +356,7 @@ CMTV_HD typename R::B rf_decode(const RowCtx<R>& x, const typename R::U& y, cons
     t0 = rf_mul(x, t1, t0);             // 2^50 - 1
     t1 = rf_sqn(x, t0, 50);
     t1 = rf_mul(x, t1, t0);             // 2^100 - 1
+    mid();
     t2 = rf_sqn(x, t1, 100);
     t1 = rf_mul(x, t2, t1);             // 2^200 - 1
     t1 = rf_sqn(x, t1, 50);
@@ -590,6 +598,87 @@ CMTV_HD bool r_join4(const RowCtx<R>& x, typename R::U v, const typename R::U& c
                      const typename R::U& cB, bool ok, bool r_canon) {
   rp_add(x, v, cA);
   return r_join<MODE>(x, v, cR, cB, ok, r_canon);
+}
+
+// ---- registered keys (keyed.h combs) in the row layout ----------------------------
+
+// This row's cached coordinate of (neg ? -P : P) for P an affine niels row of
+// 10-limb values (y+x at word 0, y-x at word ymx_off, 2dxy at xy_off): row 0
+// y-x, 1 y+x, 2 the constant 2 (Z = 1), 3 2dxy; negated, rows 0 and 1 swap and
+// row 3 is negated; the cached identity (1, 1, 2, 0) when ident. The policy's
+// niels_limb(row, off) gives this lane's 16-bit limb of the 10-limb value at
+// word off (its canonical encoding).
+template <class R>
+CMTV_HD typename R::U r_niels(const RowCtx<R>& x, const uint32_t* row, int ymx_off, int xy_off, bool neg,
+                              bool ident) {
+  using U = typename R::U;
+  const U off = sel(x.r3, U((uint32_t)xy_off), sel(x.r0 != typename R::B(neg), U((uint32_t)ymx_off), U(0u)));
+  const U l = R::niels_limb(row, off);
+  const U c = sel(x.r2, sel(x.k == 0u, U(2u), U(0u)), sel(x.r3 && typename R::B(neg), rf_neg(x, l), l));
+  return ident ? rp_cached_identity(x) : c;
+}
+
+// [s]B over the 16-position radix-2^16 comb of B (verify_core.h BC16 rows of
+// the B table, 36 words: y+x at 0, y-x at 12, 2dxy at 24; q_bcomb16's digits)
+template <class R, class BRow>
+CMTV_HD typename R::U r_bcomb16(const RowCtx<R>& x, const uint32_t s[8], const BRow& brow) {
+  uint32_t lo[8], hi[8];
+  hs_digits65536(lo, hi, s);
+  typename R::U v = rp_identity(x);
+#pragma unroll 1
+  for (int j = 15; j >= 0; j--) {
+    const int d = (int)(j >= 8 ? sc_shift_out(hi, 16) : sc_shift_out(lo, 16)) - 0x8000;
+    const int ib = d < 0 ? -d : d;
+    rp_add(x, v, r_niels(x, brow(BC16_BASE + j * BT16_ENTRIES + (ib > 0 ? ib - 1 : 0)), BTAB_COORD_WORDS,
+                         2 * BTAB_COORD_WORDS, d < 0, ib == 0));
+  }
+  return v;
+}
+
+// [k](-A) over a registered key's radix-256 comb (keyed.h T_A), tk = k's
+// biased digits (sc_bias 0x80), top byte first as keyed_comb takes them
+template <class R>
+CMTV_HD typename R::U r_kcomb(const RowCtx<R>& x, uint32_t tk[8], const uint32_t* ktab) {
+  typename R::U v = rp_identity(x);
+#pragma unroll 1
+  for (int it = 0; it < COMB_WINDOWS; it++) {
+    const int j = COMB_WINDOWS - 1 - it;
+    const int d = (int)sc_shift_out(tk, 8) - 128;
+    const int ia = d < 0 ? -d : d;
+    rp_add(x, v, r_niels(x, ktab + ((size_t)j * COMB_ENTRIES + (ia > 0 ? ia - 1 : 0)) * COMB_ROW_WORDS, 10, 20,
+                         d < 0, ia == 0));
+  }
+  return v;
+}
+
+// R decoded on every row (limb: R's 16-bit limb k on every row), as -R in
+// extended coordinates; r_ok with the mode's decoding rules (GO_STDLIB: R
+// canonical, and x = 0 only without the sign bit)
+template <uint32_t MODE, class R, class Mid = RowNoHook>
+CMTV_HD typename R::U r_decode_neg_r(const RowCtx<R>& x, const typename R::U& limb, const uint32_t sigw[8], bool& r_ok,
+                                     const Mid& mid = Mid()) {
+  using U = typename R::U;
+  const bool sign = (sigw[7] >> 31) != 0;
+  const U y = sel(x.k == 15u, limb & 0x7FFFu, limb);
+  U xo, to;
+  r_ok = (R::ballot(rf_decode(x, y, typename R::B(sign), xo, to, mid)) & 1u) != 0;
+  const bool x0 = (R::ballot(rf_canon<R>(xo).zero) & 1u) != 0;
+  if (MODE == MODE_GO_STDLIB) r_ok = r_ok && y_is_canonical(sigw) && !(x0 && sign);
+  U X0, X1, X2, X3, Y0, Y1, Y2, Y3, T0, T1, T2, T3;
+  R::rows(xo, X0, X1, X2, X3);
+  R::rows(y, Y0, Y1, Y2, Y3);
+  R::rows(to, T0, T1, T2, T3);
+  return rf_carry32(x, sel(x.r0, rf_neg(x, X0), sel(x.r1, Y0, sel(x.r2, x.one, rf_neg(x, T0)))));
+}
+
+// The keyed join: X = -R + [k](-A) + [s]B (the last two cached) = R' - R,
+// then the mode's final check (GO_STDLIB: X = O; ZIP215: [8]X = O)
+template <uint32_t MODE, class R>
+CMTV_HD bool r_keyed_join(const RowCtx<R>& x, typename R::U nr, const typename R::U& cA, const typename R::U& cB,
+                          bool ok) {
+  rp_add(x, nr, cA);
+  rp_add(x, nr, cB);
+  return r_final<MODE>(x, nr, ok, true);
 }
 
 // [u]B's cached coordinates (Y-X, Y+X, 2Z, 2dT) as four canonical 32-byte

@@ -100,6 +100,21 @@ struct DevRow {
   }
   __device__ __forceinline__ static uint64_t ballot(bool b) { return __ballot(b); }
   __device__ __forceinline__ static U load_const(const uint16_t* tab, U k) { return tab[k]; }
+  // this lane's 16-bit limb of the 10-limb (radix 2^25.5) value at word off
+  // of row: its canonical encoding (fe_tobytes), word k / 2
+  __device__ __forceinline__ static U niels_limb(const uint32_t* row, U off) {
+    const uint32_t* p = row + off;
+    fe f;
+#pragma unroll
+    for (int i = 0; i < 10; i++) f.v[i] = p[i];
+    uint32_t b[8];
+    fe_tobytes(b, f);
+    const uint32_t k = threadIdx.x & 15u;
+    uint32_t w = b[0];
+#pragma unroll
+    for (int i = 1; i < 8; i++) w = (k >> 1) == (uint32_t)i ? b[i] : w;
+    return (w >> (16 * (k & 1))) & 0xFFFFu;
+  }
 };
 
 // the row verifier's (0..8)(-A), (0..8)(-R) cached tables, both signs: one

@@ -57,6 +57,9 @@ constexpr size_t kRowMaxDefault = 768;
 // ... and up to this size its two-waves-per-signature form (one signature
 // per CU: 256 in one round; CMTV_ROW2_MAX)
 constexpr size_t kRow2MaxDefault = 256;
+// registered-key batches up to this size take the keyed row kernel (one
+// signature per CU; CMTV_KEYED_ROW_MAX)
+constexpr size_t kKeyedRowMaxDefault = 256;
 constexpr size_t kOctSplitMaxDefault = 3072;  // CMTV_OCT_SPLIT_MAX
 // quad batches up to this size take the helper-wave form (k_verify_quad_split:
 // 256 workgroups x 48 signatures per round); CMTV_QUAD_SPLIT_MAX
@@ -374,6 +377,7 @@ struct cmtv_ctx {
   size_t oct_split_max = kOctSplitMaxDefault;
   size_t row_max = kRowMaxDefault;
   size_t row2_max = kRow2MaxDefault;
+  size_t keyed_row_max = kKeyedRowMaxDefault;
   // waves per signature at or below row2_max: 4 (k_verify_row4_split) or 2
   // (CMTV_ROW_WAVES=2: k_verify_row2_split)
   uint32_t row_waves = 4;
@@ -617,11 +621,14 @@ static int enqueue_verify_keyed(cmtv_ctx* ctx, CmtvDev& D, const cmtv_keyset::Pe
     const uint32_t cn = (uint32_t)std::min<size_t>(chunk, n - c);
     // a chunk never needs more scratch than the first (kb and lanes shrink together)
     const uint32_t kb = kb0 > 1 ? kb_for(cn) : 1;
+    // the keyed row kernel up to CMTV_KEYED_ROW_MAX (below the keyed quad knob)
+    const bool krow = quad && n <= ctx->keyed_row_max && n <= kRowMaxCap;
     e = launch_verify_keyed(mode, cn, (uint32_t)n_keys, d_idx + c, d_sig + 64 * c, d_msg, d_off + c, K.d_pk, K.d_ok,
                             K.d_tab, D.d_bcomb, d_valid ? d_valid + c : nullptr,
                             d_bitmap ? d_bitmap + c / 64 : nullptr, quad, n <= ctx->quad_split_max,
                             ctx->keyed_wait, D.d_diag, kb, static_cast<uint32_t*>(D.d_atab.p),
-                            quad ? nullptr : K.d_wide, D.d_btab, ctx->wide_dma, s);
+                            quad ? nullptr : K.d_wide, D.d_btab, ctx->wide_dma, s,
+                            krow ? D.d_rowslots + (size_t)(D.row_seq++ % kRowSlots) * kRowSlotWords : nullptr);
     if (e != hipSuccess) {
       D.timing.abandon(tp);
       return hip_fail(e);
@@ -1126,6 +1133,8 @@ static void read_env(cmtv_ctx* ctx) {
   if (const char* om = std::getenv("CMTV_OCT_MAX")) ctx->oct_max = (size_t)std::strtoull(om, nullptr, 10);
   if (const char* rm = std::getenv("CMTV_ROW_MAX")) ctx->row_max = (size_t)std::strtoull(rm, nullptr, 10);
   if (const char* rm = std::getenv("CMTV_ROW2_MAX")) ctx->row2_max = (size_t)std::strtoull(rm, nullptr, 10);
+  if (const char* rm = std::getenv("CMTV_KEYED_ROW_MAX"))
+    ctx->keyed_row_max = (size_t)std::strtoull(rm, nullptr, 10);
   if (const char* rw = std::getenv("CMTV_ROW_WAVES")) ctx->row_waves = rw[0] == '2' ? 2u : 4u;
   if (const char* os = std::getenv("CMTV_OCT_SPLIT_MAX")) ctx->oct_split_max = (size_t)std::strtoull(os, nullptr, 10);
   if (const char* qs = std::getenv("CMTV_QUAD_SPLIT_MAX")) ctx->quad_split_max = (size_t)std::strtoull(qs, nullptr, 10);

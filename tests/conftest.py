@@ -134,6 +134,20 @@ def gpu_ctx_row4():
 
 
 @pytest.fixture(scope="session")
+def gpu_ctx_krow():
+    """Registered-key batches up to 4,000 on the keyed row kernel
+    (k_verify_keyed_row_split), so the corpus runs through it."""
+    return _env_ctx(CMTV_KEYED_ROW_MAX=4000)
+
+
+@pytest.fixture(scope="session")
+def gpu_ctx_kquad2():
+    """Small registered-key batches on the two-helper keyed quad kernel
+    (CMTV_KEYED_ROW_MAX=0) instead of the default keyed row kernel."""
+    return _env_ctx(CMTV_KEYED_ROW_MAX=0)
+
+
+@pytest.fixture(scope="session")
 def gpu_ctx_oct1():
     """A context whose small Ed25519 batches take the one-wave oct kernel
     (CMTV_OCT_SPLIT_MAX=0) instead of the default two-wave form."""

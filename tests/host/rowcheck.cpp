@@ -16,8 +16,11 @@
 #include <random>
 #include <vector>
 
+#include "../../cometbft_amd/csrc/keyed_quad.h"
 #include "../../cometbft_amd/csrc/row.h"
 #include "lazy_btab.h"
+#include <map>
+#include <string>
 
 namespace hostlv {
 
@@ -175,6 +178,19 @@ struct HostRow {
     for (int i = 0; i < 64; i++) m |= (uint64_t)b.a[i] << i;
     return m;
   }
+  // this lane's 16-bit limb of the 10-limb value at word off[lane] of row
+  static U niels_limb(const uint32_t* row, const U& off) {
+    U r;
+    for (int i = 0; i < 64; i++) {
+      cmtv::fe f;
+      for (int j = 0; j < 10; j++) f.v[j] = row[off.a[i] + j];
+      uint32_t b[8];
+      cmtv::fe_tobytes(b, f);
+      const int k = i & 15;
+      r.a[i] = (b[k >> 1] >> (16 * (k & 1))) & 0xFFFF;
+    }
+    return r;
+  }
   static U load_const(const uint16_t* tab, const U& k) {
     U r;
     for (int i = 0; i < 64; i++) r.a[i] = tab[k.a[i]];
@@ -310,6 +326,24 @@ static int mul_selftest() {
   return bad ? 1 : 0;
 }
 
+// comb of P (negated when neg), as the runtime's k_comb_build produces it
+struct HostScratch {
+  fe q[COMB_WINDOWS];
+  void store(int j, const fe& v) { q[j] = v; }
+  void load(int j, fe& v) const { v = q[j]; }
+};
+static std::vector<uint32_t> host_comb(const uint32_t pkw[8], bool neg, bool* ok) {
+  std::vector<uint32_t> tab(COMB_TABLE_WORDS);
+  ge_p3 A, nA;
+  *ok = p3_frombytes(A, pkw);
+  cached_neg_point(nA, A);
+  for (int d = 1; d <= COMB_ENTRIES; d++) {
+    HostScratch sc;
+    comb_build_column(tab.data(), neg ? nA : A, d, sc);
+  }
+  return tab;
+}
+
 int main(int argc, char** argv) {
   if (argc > 1 && !strcmp(argv[1], "mul")) return mul_selftest();
   // argv[1] == "row2": the two-wave form (r_part for R, then for A, r_join)
@@ -317,6 +351,10 @@ int main(int argc, char** argv) {
   // argv[1] == "row4": the four-wave form (the high parts of A and R, the lo
   // wave's low windows of both, r_join4)
   const bool row4 = argc > 1 && !strcmp(argv[1], "row4");
+  // argv[1] == "krow": registered keys (the keyed row kernel's path: the key's
+  // radix-256 comb, the B table's radix-2^16 comb, -R decoded, r_keyed_join)
+  const bool krow = argc > 1 && !strcmp(argv[1], "krow");
+  std::map<std::string, std::pair<bool, std::vector<uint32_t>>> combs;
   LazyBTab bt;
   uint32_t n;
   if (fread(&n, 4, 1, stdin) != 1) return 1;
@@ -352,7 +390,29 @@ int main(int argc, char** argv) {
     auto get_prep = [&](SigPrep& p) { p = hp; };
     auto get_b = [&]() { return blimb; };
     bool v;
-    if (row4) {
+    if (krow) {
+      auto it = combs.find(std::string((const char*)pk, 32));
+      if (it == combs.end()) {
+        bool o;
+        auto tab = host_comb(pkw, true, &o);
+        it = combs.emplace(std::string((const char*)pk, 32), std::make_pair(o, std::move(tab))).first;
+      }
+      const RowCtx<HostRow> x(HostRow::lane());
+      hostlv::U lr;
+      for (int l = 0; l < 64; l++) lr.a[l] = sig[2 * (l & 15)] | (sig[2 * (l & 15) + 1] << 8);
+      uint32_t tk[8], sw[8];
+      q_keyed_challenge(tk, pkw, sigw, msg.data(), mlen);
+      for (int j = 0; j < 8; j++) sw[j] = sigw[8 + j];
+      const bool s_ok = (sw[7] & 0xE0000000u) == 0 && sc_is_canonical(sw);
+      bool r_ok;
+      const hostlv::U nr = mode ? r_decode_neg_r<MODE_ZIP215>(x, lr, sigw, r_ok)
+                                : r_decode_neg_r<MODE_GO_STDLIB>(x, lr, sigw, r_ok);
+      const hostlv::U d2 = x.cst(RowConst::d2);
+      const hostlv::U ca = rp_to_cached(x, r_kcomb(x, tk, it->second.second.data()), d2);
+      const hostlv::U cb = rp_to_cached(x, r_bcomb16(x, sw, [&](int e) { return bt.row(e); }), d2);
+      const bool ok = it->second.first && s_ok && r_ok;
+      v = mode ? r_keyed_join<MODE_ZIP215>(x, nr, ca, cb, ok) : r_keyed_join<MODE_GO_STDLIB>(x, nr, ca, cb, ok);
+    } else if (row4) {
       const RowCtx<HostRow> x(HostRow::lane());
       hostlv::U la, lr;
       for (int l = 0; l < 64; l++) {

@@ -290,3 +290,15 @@ def test_row_pipeline_matches_corpus(rowcheck, corpus, mode, form):
     want = (corpus["go"] if mode == 0 else corpus["zip215"])[idx]
     bad = np.nonzero(got != want)[0]
     assert bad.size == 0, [(idx[int(i)], corpus["cats"][idx[int(i)]]) for i in bad[:10]]
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_keyed_row_pipeline_matches_corpus(rowcheck, corpus, mode):
+    """The keyed row kernel's source (row.h r_decode_neg_r, r_kcomb over the
+    key's radix-256 comb built as k_comb_build does, r_bcomb16 over the B
+    table's rows, r_keyed_join) on 64-lane arrays."""
+    idx = _keyed_subset(corpus)
+    got = _run(rowcheck, "krow", corpus, idx, mode)
+    want = (corpus["go"] if mode == 0 else corpus["zip215"])[idx]
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(idx[int(i)], corpus["cats"][idx[int(i)]]) for i in bad[:10]]

@@ -13,17 +13,19 @@ from cometbft_amd import _native as N
 pytestmark = pytest.mark.gpu
 
 
-KERNELS = ["quad2", "quad", "lane", "wide"]
+KERNELS = ["row", "quad2", "quad", "lane", "wide"]
 
 
-def _ctx(kernel, gpu_ctx, gpu_ctx_quad1, gpu_ctx_lane):
-    return {"quad2": gpu_ctx, "quad": gpu_ctx_quad1, "lane": gpu_ctx_lane, "wide": gpu_ctx_lane}[kernel]
+def _ctx(kernel, request):
+    name = {"row": "gpu_ctx_krow", "quad2": "gpu_ctx_kquad2", "quad": "gpu_ctx_quad1", "lane": "gpu_ctx_lane",
+            "wide": "gpu_ctx_lane"}[kernel]
+    return request.getfixturevalue(name)
 
 
 @pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("mode,key", [(MODE_GO_STDLIB, "go"), (MODE_ZIP215, "zip215")])
-def test_corpus_bit_exact_keyed(gpu_ctx, gpu_ctx_quad1, gpu_ctx_lane, corpus, mode, key, kernel):
-    gpu_ctx = _ctx(kernel, gpu_ctx, gpu_ctx_quad1, gpu_ctx_lane)
+def test_corpus_bit_exact_keyed(request, corpus, mode, key, kernel):
+    gpu_ctx = _ctx(kernel, request)
     pk = corpus["pk"]
     uniq, idx = np.unique(pk, axis=0, return_inverse=True)  # 748 keys: 47 GiB of wide combs
     ks = gpu_ctx.register_keys(uniq, wide=kernel == "wide")
@@ -86,8 +88,8 @@ def _valset_commits(n_keys, n_sigs, seed):
 
 @pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("n", [1, 15, 16, 17, 63, 64, 65, 3000, 12289])
-def test_keyed_matches_generic_and_oracle(gpu_ctx, gpu_ctx_quad1, gpu_ctx_lane, n, kernel):
-    gpu_ctx = _ctx(kernel, gpu_ctx, gpu_ctx_quad1, gpu_ctx_lane)
+def test_keyed_matches_generic_and_oracle(request, n, kernel):
+    gpu_ctx = _ctx(kernel, request)
     pk, kidx, sig, m, off, rng = _valset_commits(150, n, 7 + n)
     sig = sig.copy()
     for i in np.nonzero(rng.random(n) < 0.2)[0]:

@@ -92,10 +92,10 @@ def test_ed25519_wide_in_mixed_waves(gpu_ctx_row4, gpu_ctx_row2, gpu_ctx_row, gp
     assert [int(x) for x in alone] == [v[key] for v in vs]
 
 
-@pytest.mark.parametrize("kernel", ["quad2", "quad", "lane"])
+@pytest.mark.parametrize("kernel", ["row", "quad2", "quad", "lane"])
 @pytest.mark.parametrize("mode", [MODE_GO_STDLIB, MODE_ZIP215])
-def test_ed25519_wide_keyed(gpu_ctx, gpu_ctx_quad1, gpu_ctx_lane, kernel, mode):
-    ctx = {"quad2": gpu_ctx, "quad": gpu_ctx_quad1, "lane": gpu_ctx_lane}[kernel]
+def test_ed25519_wide_keyed(gpu_ctx_krow, gpu_ctx_kquad2, gpu_ctx_quad1, gpu_ctx_lane, kernel, mode):
+    ctx = {"row": gpu_ctx_krow, "quad2": gpu_ctx_kquad2, "quad": gpu_ctx_quad1, "lane": gpu_ctx_lane}[kernel]
     pk, sig, m, off = _mixed_batch("ed25519", seed=4)
     uniq, idx = np.unique(pk, axis=0, return_inverse=True)
     ks = ctx.register_keys(uniq)

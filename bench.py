@@ -769,13 +769,14 @@ def latency_150(ctx, mode, iters):
     res = {"n_validators": 150, "iters": iters, "p50_ms": p50c, "p99_ms": p99c,
            "path": "cmtv_verify_commit (C ABI, commit packed once as a cgo shim would hold it): sign-bytes + H2D "
                    "+ kernel + D2H + VerifyCommit replay",
+           "kernel": "k_verify_row4_split: one signature per CU in the row layout (DESIGN.md 4.9)",
            "python_mirror": {"p50_ms": p50, "p99_ms": p99, "path": "ValidatorSet.verify_commit (re-packs per call)"}}
     kctx = Context(device=ctx.device_ordinal(0))
     kctx.keyset_cache(4)
     kcall, kkeep = c_call(kctx)
     kp50, kp99 = measure(kcall)
     res["keyset_cache"] = {"p50_ms": kp50, "p99_ms": kp99,
-                           "path": "same C call, validator set registered once (cmtv_keyset_cache): keyed quad kernel"}
+                           "path": "same C call, validator set registered once (cmtv_keyset_cache): keyed row kernel, one signature per CU"}
     from oracle import coracle
 
     m, off = coracle.pack_msgs(msgs)

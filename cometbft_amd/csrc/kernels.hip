@@ -697,14 +697,20 @@ __global__ __launch_bounds__(256, 1) void k_verify_row4_split(
   if (t == 0) __hip_atomic_store(slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// the keyed row kernel's R wave meets barrier 1 78 squarings into the decode's
+// run of 100 (~190 of its ~265 products, ~65k cycles: when the hash helper
+// publishes k)
+constexpr int kKeyedRowMidAt = 78;
+
 // Registered keys, one signature per workgroup in the row layout (row.h
 // r_decode_neg_r / r_kcomb / r_bcomb16 / r_keyed_join), for batches of at
 // most 256 (the 150-validator VerifyCommit with the keyset cache): wave 3
 // hashes k; wave 2 adds [s]B over the B table's 16-position radix-2^16 comb
-// (s needs no hash); wave 1 takes k at barrier 1 and adds [k](-A) over the
-// key's radix-256 comb (32 additions); wave 0 decodes R, meeting barrier 1
-// half-way through its square-root chain (so it never waits for the hash),
-// and after barrier 2 adds both sums to -R and checks. Comb rows are
+// (s needs no hash), then positions 31..16 of [k](-A) over the key's
+// radix-256 comb; wave 1 takes k at barrier 1 and adds positions 15..0;
+// wave 0 decodes R, meeting barrier 1 inside its square-root chain (about
+// when the hash is done, so it does not wait), and after barrier 2 adds both
+// sums to -R and checks. Comb rows are
 // converted to the row layout as they are read (DevRow::niels_limb).
 // Bitmap as k_verify_row_split.
 template <uint32_t MODE>
@@ -718,6 +724,8 @@ __global__ __launch_bounds__(256, 1) void k_verify_keyed_row_split(
   const uint32_t i = s < n ? s : n - 1;
   __shared__ uint32_t tks[8];
   __shared__ uint32_t xa[64], xb[64];
+  __shared__ uint32_t arows[COMB_WINDOWS * COMB_ROW_WORDS];  // the 32 key-comb rows of k's digits
+  __shared__ uint32_t brows[16 * BTAB_ROW_WORDS];            // the 16 B-comb rows of s's digits
   uint32_t kid = key_idx[i];
   const bool kin = kid < n_keys;
   kid = kin ? kid : 0;
@@ -738,28 +746,82 @@ __global__ __launch_bounds__(256, 1) void k_verify_keyed_row_split(
   }
   const RowCtx<DevRow> x(DevRow::lane());
   const uint32_t d2 = x.cst(RowConst::d2);
+  // k's key-comb rows of positions hi .. hi - 15 into LDS at once (lane L
+  // fetches a quarter of row L / 4), then added onto v
+  auto kcomb_half = [&](uint32_t& v, int hi) {
+    uint32_t tk[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) tk[j] = tks[j];
+    {
+      const uint32_t j = (uint32_t)(hi - 15) + (t >> 2), part = t & 3;
+      uint32_t w = tk[0];
+#pragma unroll
+      for (int q = 1; q < 8; q++) w = (j >> 2) == (uint32_t)q ? tk[q] : w;
+      const int d = (int)((w >> (8 * (j & 3))) & 0xFFu) - 128;
+      const int ia = d < 0 ? -d : d;
+      const uint4* src = reinterpret_cast<const uint4*>(
+          ktabs + (size_t)kid * COMB_TABLE_WORDS + ((size_t)j * COMB_ENTRIES + (ia > 0 ? ia - 1 : 0)) * COMB_ROW_WORDS +
+          8 * part);
+      const uint4 r0 = src[0], r1 = src[1];
+      uint4* dst = reinterpret_cast<uint4*>(arows + j * COMB_ROW_WORDS + 8 * part);
+      dst[0] = r0;
+      dst[1] = r1;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    r_kcomb(x, v, tk, [&](int j, int) { return arows + j * COMB_ROW_WORDS; }, hi, hi - 15);
+  };
   if (wave == 2) {
     uint32_t sw[8];
     load_words(sw, sgp + 8, 2);
-    const uint32_t v = r_bcomb16(x, sw, [&](int e) { return btab + (size_t)e * BTAB_ROW_WORDS; });
-    xb[t] = rp_to_cached(x, v, d2);
+    {
+      // the 16 rows at once (one memory round trip instead of 16 dependent
+      // ones): lane L fetches a quarter of row L / 4
+      uint32_t tb[8];
+      uint64_t c = 0;
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        const uint64_t w = (uint64_t)sw[j] + 0x80008000u + c;
+        tb[j] = (uint32_t)w;
+        c = w >> 32;
+      }
+      const uint32_t j = t >> 2, part = t & 3;
+      uint32_t w = tb[0];
+#pragma unroll
+      for (int q = 1; q < 8; q++) w = (j >> 1) == (uint32_t)q ? tb[q] : w;
+      const int d = (int)((w >> (16 * (j & 1))) & 0xFFFFu) - 0x8000;
+      const int ib = d < 0 ? -d : d;
+      const uint32_t* src =
+          btab + (size_t)(BC16_BASE + j * BT16_ENTRIES + (ib > 0 ? ib - 1 : 0)) * BTAB_ROW_WORDS + 9 * part;
+      uint32_t v9[9];
+#pragma unroll
+      for (int q = 0; q < 9; q++) v9[q] = src[q];
+#pragma unroll
+      for (int q = 0; q < 9; q++) brows[j * BTAB_ROW_WORDS + 9 * part + q] = v9[q];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    uint32_t v = r_bcomb16(x, sw, [&](int e) { return brows + ((e - BC16_BASE) >> 15) * BTAB_ROW_WORDS; });
     CMTV_STAMP(1);
-    __syncthreads();  // 1
+    __syncthreads();  // 1: k
     CMTV_STAMP(2);
-    __syncthreads();  // 2: [s]B
+    kcomb_half(v, 31);
+    xb[t] = rp_to_cached(x, v, d2);
+    CMTV_STAMP(3);
+    __syncthreads();  // 2: [s]B + positions 31..16 of [k](-A)
     return;
   }
   if (wave == 1) {
     CMTV_STAMP(1);
     __syncthreads();  // 1: k
     CMTV_STAMP(2);
-    uint32_t tk[8];
-#pragma unroll
-    for (int j = 0; j < 8; j++) tk[j] = tks[j];
-    const uint32_t v = r_kcomb(x, tk, ktabs + (size_t)kid * COMB_TABLE_WORDS);
+    uint32_t v = rp_identity(x);
+    kcomb_half(v, 15);
     xa[t] = rp_to_cached(x, v, d2);
     CMTV_STAMP(3);
-    __syncthreads();  // 2: [k](-A)
+    __syncthreads();  // 2: positions 15..0 of [k](-A)
     return;
   }
   uint32_t sigw[8], sw[8];
@@ -767,7 +829,7 @@ __global__ __launch_bounds__(256, 1) void k_verify_keyed_row_split(
   load_words(sw, sgp + 8, 2);
   const uint32_t limb = reinterpret_cast<const uint16_t*>(sgp)[t & 15];
   bool r_ok;
-  const uint32_t nr = r_decode_neg_r<MODE>(x, limb, sigw, r_ok, [&]() {
+  const uint32_t nr = r_decode_neg_r<MODE, kKeyedRowMidAt>(x, limb, sigw, r_ok, [&]() {
     CMTV_STAMP(1);
     __syncthreads();  // 1
     CMTV_STAMP(2);

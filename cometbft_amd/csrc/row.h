@@ -322,10 +322,10 @@ CMTV_HD typename R::U rp_cached_identity(const RowCtx<R>& x) {
 struct RowNoHook {
   CMTV_HD void operator()() const {}
 };
-// mid(): called once half-way through the square-root chain (after 2^100 - 1,
-// ~150 of its ~265 products): the keyed row kernel's R wave meets the
-// workgroup barrier there
-template <class R, class Mid = RowNoHook>
+// mid(): called once inside the square-root chain, MID_AT squarings into
+// its run of 100 after 2^100 - 1 (~112 + MID_AT of the decode's ~265
+// products): the keyed row kernel's R wave meets the workgroup barrier there
+template <int MID_AT = 0, class R, class Mid = RowNoHook>
 CMTV_HD typename R::B rf_decode(const RowCtx<R>& x, const typename R::U& y, const typename R::B& sign,
                                 typename R::U& xo, typename R::U& to, const Mid& mid = Mid()) {
   using U = typename R::U;
@@ -356,8 +356,9 @@ CMTV_HD typename R::B rf_decode(const RowCtx<R>& x, const typename R::U& y, cons
     t0 = rf_mul(x, t1, t0);             // 2^50 - 1
     t1 = rf_sqn(x, t0, 50);
     t1 = rf_mul(x, t1, t0);             // 2^100 - 1
+    t2 = rf_sqn(x, t1, MID_AT);
     mid();
-    t2 = rf_sqn(x, t1, 100);
+    t2 = rf_sqn(x, t2, 100 - MID_AT);
     t1 = rf_mul(x, t2, t1);             // 2^200 - 1
     t1 = rf_sqn(x, t1, 50);
     t1 = rf_mul(x, t1, t0);             // 2^250 - 1
@@ -636,32 +637,35 @@ CMTV_HD typename R::U r_bcomb16(const RowCtx<R>& x, const uint32_t s[8], const B
 }
 
 // [k](-A) over a registered key's radix-256 comb (keyed.h T_A), tk = k's
-// biased digits (sc_bias 0x80), top byte first as keyed_comb takes them
-template <class R>
-CMTV_HD typename R::U r_kcomb(const RowCtx<R>& x, uint32_t tk[8], const uint32_t* ktab) {
-  typename R::U v = rp_identity(x);
+// biased digits (sc_bias 0x80), top byte first as keyed_comb takes them;
+// krow(j, e) = the comb row of position j, entry e (a key's table in HBM, or
+// the rows a kernel prefetched into LDS), converted to
+// the row layout of a wave. Positions first .. last (downwards) are added to
+// v (the keyed row kernel splits the 32 between two waves).
+template <class R, class KRow>
+CMTV_HD void r_kcomb(const RowCtx<R>& x, typename R::U& v, uint32_t tk[8], const KRow& krow, int first = COMB_WINDOWS - 1,
+                     int last = 0) {
 #pragma unroll 1
-  for (int it = 0; it < COMB_WINDOWS; it++) {
-    const int j = COMB_WINDOWS - 1 - it;
+  for (int j = COMB_WINDOWS - 1; j > first; j--) sc_shift_out(tk, 8);
+#pragma unroll 1
+  for (int j = first; j >= last; j--) {
     const int d = (int)sc_shift_out(tk, 8) - 128;
     const int ia = d < 0 ? -d : d;
-    rp_add(x, v, r_niels(x, ktab + ((size_t)j * COMB_ENTRIES + (ia > 0 ? ia - 1 : 0)) * COMB_ROW_WORDS, 10, 20,
-                         d < 0, ia == 0));
+    rp_add(x, v, r_niels(x, krow(j, ia > 0 ? ia - 1 : 0), 10, 20, d < 0, ia == 0));
   }
-  return v;
 }
 
 // R decoded on every row (limb: R's 16-bit limb k on every row), as -R in
 // extended coordinates; r_ok with the mode's decoding rules (GO_STDLIB: R
 // canonical, and x = 0 only without the sign bit)
-template <uint32_t MODE, class R, class Mid = RowNoHook>
+template <uint32_t MODE, int MID_AT = 0, class R, class Mid = RowNoHook>
 CMTV_HD typename R::U r_decode_neg_r(const RowCtx<R>& x, const typename R::U& limb, const uint32_t sigw[8], bool& r_ok,
                                      const Mid& mid = Mid()) {
   using U = typename R::U;
   const bool sign = (sigw[7] >> 31) != 0;
   const U y = sel(x.k == 15u, limb & 0x7FFFu, limb);
   U xo, to;
-  r_ok = (R::ballot(rf_decode(x, y, typename R::B(sign), xo, to, mid)) & 1u) != 0;
+  r_ok = (R::ballot(rf_decode<MID_AT>(x, y, typename R::B(sign), xo, to, mid)) & 1u) != 0;
   const bool x0 = (R::ballot(rf_canon<R>(xo).zero) & 1u) != 0;
   if (MODE == MODE_GO_STDLIB) r_ok = r_ok && y_is_canonical(sigw) && !(x0 && sign);
   U X0, X1, X2, X3, Y0, Y1, Y2, Y3, T0, T1, T2, T3;

@@ -408,8 +408,17 @@ int main(int argc, char** argv) {
       const hostlv::U nr = mode ? r_decode_neg_r<MODE_ZIP215>(x, lr, sigw, r_ok)
                                 : r_decode_neg_r<MODE_GO_STDLIB>(x, lr, sigw, r_ok);
       const hostlv::U d2 = x.cst(RowConst::d2);
-      const hostlv::U ca = rp_to_cached(x, r_kcomb(x, tk, it->second.second.data()), d2);
-      const hostlv::U cb = rp_to_cached(x, r_bcomb16(x, sw, [&](int e) { return bt.row(e); }), d2);
+      const uint32_t* kt = it->second.second.data();
+      // as the kernel splits them: positions 15..0 on the A wave, 31..16 after [s]B on the B wave
+      auto krow = [&](int j, int e) { return kt + ((size_t)j * COMB_ENTRIES + e) * COMB_ROW_WORDS; };
+      hostlv::U va = rp_identity(x);
+      uint32_t tk2[8];
+      for (int j = 0; j < 8; j++) tk2[j] = tk[j];
+      r_kcomb(x, va, tk, krow, 15, 0);
+      hostlv::U vb = r_bcomb16(x, sw, [&](int e) { return bt.row(e); });
+      r_kcomb(x, vb, tk2, krow, 31, 16);
+      const hostlv::U ca = rp_to_cached(x, va, d2);
+      const hostlv::U cb = rp_to_cached(x, vb, d2);
       const bool ok = it->second.first && s_ok && r_ok;
       v = mode ? r_keyed_join<MODE_ZIP215>(x, nr, ca, cb, ok) : r_keyed_join<MODE_GO_STDLIB>(x, nr, ca, cb, ok);
     } else if (row4) {

@@ -37,7 +37,11 @@ def main():
     sig = ctx.sign(sv.seeds, m, off)
     pk = np.ascontiguousarray(sv.pubkeys)
     out = {}
-    if form == "row2":
+    ks = ctx.register_keys(pk) if form == "krow" else None
+    kidx = np.arange(n, dtype=np.uint32)
+    if form == "krow":  # keyed row: R decode (meets barrier 1 mid-chain), A comb, B comb, hash helper
+        names = {"R": (0, [1, 2, 3, 4, 5]), "A": (1, [1, 2, 3]), "B": (2, [1, 2]), "helper": (3, [1])}
+    elif form == "row2":
         names = {"A": (0, [6, 1, 2, 3, 4, 5]), "R": (1, [6, 1, 2, 3]), "helper": (2, [5, 1, 3])}
     else:  # row4: lo (decodes A and R), A-hi, R-hi, helper
         names = {"lo": (0, [1, 2, 3, 4, 5]), "A_hi": (1, [6, 1, 2, 3]), "R_hi": (2, [6, 1, 2, 3]),
@@ -45,7 +49,7 @@ def main():
     nw = len(names)
     for mode, name in ((0, "go"), (1, "zip215")):
         for _ in range(10):
-            v = ctx.verify(pk, sig, m, off, mode)
+            v = ctx.verify_indexed(ks, kidx, sig, m, off, mode) if ks is not None else ctx.verify(pk, sig, m, off, mode)
         assert v.all()
         buf = np.zeros(n * 4 * SLOTS, np.uint64)
         assert fn(buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), buf.size) == 0
@@ -56,6 +60,7 @@ def main():
         for w, (wi, slots) in names.items():
             res[w] = {str(k): float(np.median(rel[:, wi, k])) for k in slots}
         res["end_max"] = float((st[:, 0, 5] - t0).max())
+        res["end_median"] = float(np.median(st[:, 0, 5] - t0))
         out[name] = res
         print(name, json.dumps(res), flush=True)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)

@@ -23,11 +23,14 @@ constexpr uint32_t kLaunchQuad = 1, kLaunchForceWide = 2, kLaunchOct = 4, kLaunc
 // k_verify_row4_split)
 constexpr uint32_t kLaunchRow = 32, kLaunchRow2 = 64, kLaunchRow4 = 128;
 
-// Row kernel bitmap assembly: each launch takes one of kRowSlots slots of a
-// per-device ring (kRowSlotWords words: word 0 a wave counter the kernel
+// Row kernel bitmap assembly: each launch takes the next of kRowSlots slots
+// of a per-device ring (kRowSlotWords words: word 0 a wave counter the kernel
 // resets, then one verdict byte per signature); the last wave to finish packs
-// the bitmap words from the slot's bytes. kRowMaxCap bounds a row launch.
-constexpr uint32_t kRowSlots = 32, kRowSlotWords = 1024, kRowMaxCap = 4 * (kRowSlotWords - 16);
+// the bitmap words from the slot's bytes. A slot is reused after kRowSlots
+// further row launches on the device, so at most kRowSlots row launches may be
+// in flight at once (the context enqueues under its lock; each call of the
+// host API waits for its own launch). kRowMaxCap bounds a row launch.
+constexpr uint32_t kRowSlots = 256, kRowSlotWords = 1024, kRowMaxCap = 4 * (kRowSlotWords - 16);
 
 // Templated sign-bytes (signbytes.h) written by the helper waves of the
 // split kernels themselves (k_verify_oct_split / k_verify_quad_split): each

@@ -88,3 +88,85 @@ def test_concurrent_row_launches_pack_their_own_bitmaps():
         t.join(timeout=110)
     assert not any(t.is_alive() for t in ths)
     assert not errors, errors[:5]
+
+
+def test_concurrent_keyed_row_launches():
+    """The keyed row kernel takes ring slots too: 3 threads on their own
+    streams, registered keys, 20 device-resident launches each with bitmaps,
+    sizes inside the keyed row range."""
+    import torch
+
+    ctx = Context(device=0)
+    dev = torch.device("cuda:0")
+    jobs = []
+    for j, n in enumerate((150, 40, 256)):
+        pk, sig, m, off = _batch(n, 1300 + j, flip=0.2)
+        ks = ctx.register_keys(pk)
+        exp = coracle.verify_batch(pk, sig, m, off, MODE_ZIP215, nthreads=8)
+        jobs.append((n, ks, sig, m, off, exp))
+    errors = []
+
+    def run(j):
+        n, ks, sig, m, off, exp = jobs[j]
+        try:
+            s = torch.cuda.Stream(device=dev)
+            t = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in
+                 {"idx": np.arange(n, dtype=np.int32), "sig": sig, "m": m, "off": off.view(np.int32)}.items()}
+            words = (n + 63) // 64
+            bm = torch.zeros(words, dtype=torch.int64, device=dev)
+            want = np.packbits(exp, bitorder="little")
+            want = np.pad(want, (0, 8 * words - want.size)).view(np.int64)
+            for _ in range(20):
+                bm.fill_(-1)
+                torch.cuda.synchronize(dev)
+                ctx.verify_indexed_device(ks, n, t["idx"].data_ptr(), t["sig"].data_ptr(), t["m"].data_ptr(),
+                                          t["off"].data_ptr(), MODE_ZIP215, 0, bm.data_ptr(), s.cuda_stream)
+                s.synchronize()
+                got = bm.cpu().numpy()
+                if not np.array_equal(got, want):
+                    errors.append((j, np.nonzero(got != want)[0][:4].tolist()))
+        except Exception as e:  # noqa: BLE001
+            errors.append((j, repr(e)))
+
+    ths = [threading.Thread(target=run, args=(j,)) for j in range(3)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(timeout=110)
+    assert not any(t.is_alive() for t in ths)
+    assert not errors, errors[:5]
+    for job in jobs:
+        job[1].free()
+
+
+@pytest.mark.parametrize("mode", [MODE_GO_STDLIB, MODE_ZIP215])
+def test_row_kernels_on_random_malformed_inputs(gpu_ctx_row4, gpu_ctx_row2, gpu_ctx_row, gpu_ctx_krow, mode):
+    """Random bytes where the corpus has crafted ones: 240 signatures whose A,
+    R and s are random (mostly off-curve points, s >= L, set high bits), mixed
+    with honest ones and with honest R / A paired with a wrong s, through every
+    row form and the keyed row kernel, against the C oracle bit for bit."""
+    rng = np.random.default_rng(4242 + mode)
+    n = 240
+    pk, sig, m, off = _batch(n, 77, flip=0.0)
+    pk, sig = pk.copy(), sig.copy()
+    kind = rng.integers(0, 6, n)
+    for i in range(n):
+        if kind[i] == 0:
+            pk[i] = rng.integers(0, 256, 32, dtype=np.uint8)          # random A
+        elif kind[i] == 1:
+            sig[i, :32] = rng.integers(0, 256, 32, dtype=np.uint8)    # random R
+        elif kind[i] == 2:
+            sig[i, 32:] = rng.integers(0, 256, 32, dtype=np.uint8)    # random s (often >= L)
+        elif kind[i] == 3:
+            sig[i, 63] |= 0x80 >> int(rng.integers(0, 3))              # s's high bits
+        elif kind[i] == 4:
+            pk[i, 31] ^= 0x80                                          # A's sign bit
+    exp = coracle.verify_batch(pk, sig, m, off, mode, nthreads=8)
+    assert 0 < exp.sum() < n
+    for ctx in (gpu_ctx_row4, gpu_ctx_row2, gpu_ctx_row):
+        got = ctx.verify(pk, sig, m, off, mode)
+        assert np.array_equal(got, exp), np.nonzero(got != exp)[0][:10]
+    ks = gpu_ctx_krow.register_keys(pk)
+    got = gpu_ctx_krow.verify_indexed(ks, np.arange(n, dtype=np.uint32), sig, m, off, mode)
+    assert np.array_equal(got, exp), np.nonzero(got != exp)[0][:10]
+    ks.free()

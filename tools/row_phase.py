@@ -60,6 +60,10 @@ def main():
         for w, (wi, slots) in names.items():
             res[w] = {str(k): float(np.median(rel[:, wi, k])) for k in slots}
         res["end_max"] = float((st[:, 0, 5] - t0).max())
+        # across workgroups (absolute shader clock): dispatch spread and the
+        # first-start-to-last-verdict span of the whole launch
+        res["start_spread"] = float(t0.max() - t0.min())
+        res["launch_span"] = float(st[:, 0, 5].max() - t0.min())
         res["end_median"] = float(np.median(st[:, 0, 5] - t0))
         out[name] = res
         print(name, json.dumps(res), flush=True)

@@ -19,7 +19,7 @@
 //   h_k = sum_r f_{(k-r) mod 16} g_r  (x 38 when r > k)
 // Bounds (asserted by tests/host/rowcheck.cpp): multiplication inputs below
 // 2^19.37 per limb (the first carry of a column then fits 32 bits); products
-// leave limbs below 2^16 + 2^10.6 ("carried"); subtraction adds 4p (limbs of
+// leave limbs below 2^16 + 2^7 ("carried"); subtraction adds 4p (limbs of
 // 4p are >= 0x1FFFC, above any carried limb).
 //
 // Everything is written against a row policy R:
@@ -44,6 +44,9 @@ CMTV_HD uint64_t widen(uint32_t a) { return a; }
 CMTV_HD uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) { return (uint64_t)a * b + c; }
 CMTV_HD uint32_t lo32(uint64_t a) { return (uint32_t)a; }
 CMTV_HD uint32_t shr64(uint64_t a, int s) { return (uint32_t)(a >> s); }
+// the high word of a product's column sum (the host policy asserts the sum
+// is below 2^48, so the word is below 2^16)
+CMTV_HD uint32_t hi32(uint64_t a) { return (uint32_t)(a >> 32); }
 // a b for a, b < 2^24: v_mul_u32_u24 (full rate; v_mul_lo_u32 is quarter rate)
 CMTV_HD uint32_t mul24(uint32_t a, uint32_t b) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -76,6 +79,7 @@ struct RowCtx {
   U c;        // row index (lane >> 4)
   U bias;     // limb k of 4p
   U m38;      // 38 on limb 0 (the carry out of limb 15 wraps as x 38), else 1
+  U m38x2;    // 38 on limbs 0 and 1 (the second carry out of limbs 14, 15 wraps), else 1
   U one;      // the constant 1 (limb 0)
   U tw[16];   // column twist of term r: 38 where limb k < r (the column wraps past 2^256), else 1
   B r0, r1, r2, r3;
@@ -86,6 +90,7 @@ struct RowCtx {
     c = lane >> 4;
     bias = sel(k == 0u, U(4u * 0xFFEDu), sel(k == 15u, U(4u * 0x7FFFu), U(4u * 0xFFFFu)));
     m38 = sel(k == 0u, U(38u), U(1u));
+    m38x2 = sel(k < 2u, U(38u), U(1u));
     one = sel(k == 0u, U(1u), U(0u));
     r0 = c == 0u;
     r1 = c == 1u;
@@ -97,19 +102,21 @@ struct RowCtx {
 
 // ---- the product -------------------------------------------------------------
 
-// three carry rounds of the column sums (< 2^48): limbs end below 2^16 + 2^10.6
+// The column sums (< 2^48) to limbs below 2^16 + 2^7: each sum is cut into
+// three 16-bit pieces at once, piece j moving j limbs up (row_ror:j, x 38
+// where it wraps past limb 15), so limb k collects c0_k + c1_{k-1} + c2_{k-2}
+// (< 2^22.3), then one ordinary round. 10 VALU instructions, 4 dependent
+// steps to the first sum instead of three chained rounds.
 template <class R>
 CMTV_HD typename R::U rf_carry64(const RowCtx<R>& x, const typename R::U64& c) {
   using U = typename R::U;
-  U lo = lo32(c) & 0xFFFFu;
-  U ca = R::template ror<1>(shr64(c, 16));  // lane k gets the carry of lane k-1
-  typename R::U64 cc = mad64(ca, x.m38, widen(lo));
-  lo = lo32(cc) & 0xFFFFu;
-  ca = R::template ror<1>(shr64(cc, 16));  // < 2^21.3
-  U w = mul24(ca, x.m38) + lo;             // < 2^26.6
-  lo = w & 0xFFFFu;
-  ca = R::template ror<1>(w >> 16);
-  return mul24(ca, x.m38) + lo;
+  const U l = lo32(c);
+  const U c1 = R::template ror<1>(l >> 16);
+  const U c2 = R::template ror<2>(hi32(c));
+  U w = mul24(c1, x.m38) + (l & 0xFFFFu);
+  w = mul24(c2, x.m38x2) + w;
+  const U ca = R::template ror<1>(w >> 16);
+  return mul24(ca, x.m38) + (w & 0xFFFFu);
 }
 
 // the same on 32-bit limbs below 2^26 (sums of a few carried values)

@@ -126,6 +126,15 @@ inline U shr64(const U64& x, int s) {
   }
   return r;
 }
+// the high word of a column sum: the sum must be below 2^48
+inline U hi32(const U64& x) {
+  U r;
+  for (int i = 0; i < 64; i++) {
+    if (x.a[i] >> 48) fail("column sum >= 2^48");
+    r.a[i] = (uint32_t)(x.a[i] >> 32);
+  }
+  return r;
+}
 inline U mul24(const U& a, const U& b) {
   U r;
   for (int i = 0; i < 64; i++) {
@@ -300,7 +309,7 @@ static int mul_selftest() {
       big_from_limbs(got, &h.a[16 * row]);
       for (int i = 0; i < 4; i++) bad += want[i] != got[i];
       for (int k = 0; k < 16; k++)
-        if (h.a[16 * row + k] > 0x10000u + 1600u) {
+        if (h.a[16 * row + k] > 0x10000u + 128u) {
           fprintf(stderr, "limb %u above the carried bound\n", h.a[16 * row + k]);
           bad++;
         }

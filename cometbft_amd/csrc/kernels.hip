@@ -362,7 +362,7 @@ struct LdsCombB {
 static_assert(BT16_ENTRIES == 1 << 15, "LdsCombB maps a comb row to its position by >> 15");
 
 __device__ __forceinline__ void helper_bcomb_prefetched(ge_p3& B, const uint32_t u[8], const uint32_t* btab,
-                                                        uint32_t* lds_rows, uint32_t t) {
+                                                        uint32_t* lds_rows, uint32_t* lds_pts, uint32_t t) {
   uint32_t tb[8];
   uint64_t c = 0;
 #pragma unroll
@@ -371,22 +371,79 @@ __device__ __forceinline__ void helper_bcomb_prefetched(ge_p3& B, const uint32_t
     tb[i] = (uint32_t)v;
     c = v >> 32;
   }
-  const uint32_t j = t >> 2, part = t & 3;
-  uint32_t w = tb[0];
+  auto digit = [&](uint32_t j) -> int {
+    uint32_t w = tb[0];
 #pragma unroll
-  for (int i = 1; i < 8; i++) w = (j >> 1) == (uint32_t)i ? tb[i] : w;
-  const int d = (int)((w >> (16 * (j & 1))) & 0xFFFFu) - 0x8000;
-  const int ib = d < 0 ? -d : d;
-  const uint32_t* src = btab + (size_t)(BC16_BASE + j * BT16_ENTRIES + (ib > 0 ? ib - 1 : 0)) * BTAB_ROW_WORDS + 9 * part;
-  uint32_t v[9];
+    for (int i = 1; i < 8; i++) w = (j >> 1) == (uint32_t)i ? tb[i] : w;
+    return (int)((w >> (16 * (j & 1))) & 0xFFFFu) - 0x8000;
+  };
+  {
+    const uint32_t j = t >> 2, part = t & 3;
+    const int d = digit(j);
+    const int ib = d < 0 ? -d : d;
+    const uint32_t* src =
+        btab + (size_t)(BC16_BASE + j * BT16_ENTRIES + (ib > 0 ? ib - 1 : 0)) * BTAB_ROW_WORDS + 9 * part;
+    uint32_t v[9];
 #pragma unroll
-  for (int i = 0; i < 9; i++) v[i] = src[i];
+    for (int i = 0; i < 9; i++) v[i] = src[i];
 #pragma unroll
-  for (int i = 0; i < 9; i++) lds_rows[j * BTAB_ROW_WORDS + 9 * part + i] = v[i];
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  q_bcomb16(B, u, LdsCombB{lds_rows});
+    for (int i = 0; i < 9; i++) lds_rows[j * BTAB_ROW_WORDS + 9 * part + i] = v[i];
+  }
+  auto wave_sync = [] {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  wave_sync();
+  // a tree instead of q_bcomb16's chain of 16: lane j (< 8) adds comb rows
+  // 2j and 2j+1, then three levels of full additions through LDS (lanes
+  // 0..3, 0..1, 0) -- 2 mixed + 3 full additions on the path instead of 16
+  // mixed ones. The sum is the same point as q_bcomb16's in another
+  // projective representation; the row kernels use it only as a point.
+  const uint32_t l = t & 7;
+  ge_p3 P;
+  p3_identity(P);
+  ge_efgh e;
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const uint32_t j = 2 * l + h;
+    const int d = digit(j);
+    const int ib = d < 0 ? -d : d;
+    ge_add_table<false>(e, P, LdsCombB{lds_rows}, BC16_BASE + (int)j * BT16_ENTRIES, d < 0, ib == 0);
+    efgh_to_p3(P, e);
+  }
+#pragma unroll 1
+  for (uint32_t width = 4; width >= 1; width >>= 1) {
+    if (t < 2 * width) {
+#pragma unroll
+      for (int i = 0; i < 10; i++) {
+        lds_pts[t * 40 + i] = P.X.v[i];
+        lds_pts[t * 40 + 10 + i] = P.Y.v[i];
+        lds_pts[t * 40 + 20 + i] = P.Z.v[i];
+        lds_pts[t * 40 + 30 + i] = P.T.v[i];
+      }
+    }
+    wave_sync();
+    const uint32_t a = (2 * t) & 7, b = a + 1;  // lanes < width combine slots 2t, 2t+1
+    ge_p3 Q, S;
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+      Q.X.v[i] = lds_pts[a * 40 + i];
+      Q.Y.v[i] = lds_pts[a * 40 + 10 + i];
+      Q.Z.v[i] = lds_pts[a * 40 + 20 + i];
+      Q.T.v[i] = lds_pts[a * 40 + 30 + i];
+      S.X.v[i] = lds_pts[b * 40 + i];
+      S.Y.v[i] = lds_pts[b * 40 + 10 + i];
+      S.Z.v[i] = lds_pts[b * 40 + 20 + i];
+      S.T.v[i] = lds_pts[b * 40 + 30 + i];
+    }
+    wave_sync();
+    ge_cached sc;
+    p3_to_cached(sc, S);
+    ge_add_cached(e, Q, sc);
+    efgh_to_p3(P, e);
+  }
+  B = P;
 }
 
 // One signature per wave (row.h): for the smallest batches (a 150-validator
@@ -498,6 +555,7 @@ __global__ __launch_bounds__(192, 1) void k_verify_row2_split(
   __shared__ uint32_t prep[SIG_PREP_WORDS + 1];
   __shared__ uint32_t bpt[32];
   __shared__ uint32_t brows[16 * BTAB_ROW_WORDS];  // the helper's [u]B comb rows
+  __shared__ uint32_t bpts[8 * 40];                // ... and its partial sums
   __shared__ uint32_t tab_lds[2][kRowTabWords / 2];
   __shared__ uint32_t sbm[kSbFuseMaxMsg / 4];
   __shared__ uint32_t xr[64 + 2];  // R's sum (cached), its decode flag and x = 0
@@ -530,7 +588,7 @@ __global__ __launch_bounds__(192, 1) void k_verify_row2_split(
     __syncthreads();  // 1: the scalars
     CMTV_STAMP(2);
     ge_p3 B;
-    helper_bcomb_prefetched(B, p.u, btab, brows, t);
+    helper_bcomb_prefetched(B, p.u, btab, brows, bpts, t);
     if (t == 0) bpoint_store_bytes(bpt, B);
     CMTV_STAMP(3);
     __syncthreads();  // 2: [u]B and R's sum
@@ -615,6 +673,7 @@ __global__ __launch_bounds__(256, 1) void k_verify_row4_split(
   __shared__ uint32_t prep[SIG_PREP_WORDS + 1];
   __shared__ uint32_t bpt[32];
   __shared__ uint32_t brows[16 * BTAB_ROW_WORDS];  // the helper's [u]B comb rows
+  __shared__ uint32_t bpts[8 * 40];                // ... and its partial sums
   __shared__ uint32_t tab_lo[kRowTabWords];
   __shared__ uint32_t tab_hi[2][kRowTabWords / 2];
   __shared__ uint32_t sbm[kSbFuseMaxMsg / 4];
@@ -633,7 +692,7 @@ __global__ __launch_bounds__(256, 1) void k_verify_row4_split(
     __syncthreads();  // 1: the scalars
     CMTV_STAMP(2);
     ge_p3 B;
-    helper_bcomb_prefetched(B, p.u, btab, brows, t);
+    helper_bcomb_prefetched(B, p.u, btab, brows, bpts, t);
     if (t == 0) bpoint_store_bytes(bpt, B);
     CMTV_STAMP(3);
     __syncthreads();  // 2: [u]B and the high parts

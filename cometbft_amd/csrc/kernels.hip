@@ -756,10 +756,10 @@ __global__ __launch_bounds__(256, 1) void k_verify_row4_split(
   if (t == 0) __hip_atomic_store(slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// the keyed row kernel's R wave meets barrier 1 78 squarings into the decode's
-// run of 100 (~190 of its ~265 products, ~65k cycles: when the hash helper
-// publishes k)
-constexpr int kKeyedRowMidAt = 78;
+// the keyed row kernel's R wave meets barrier 1 86 squarings into the decode's
+// run of 100 (~198 of its ~265 products, ~54k cycles with the split
+// products: when the hash helper publishes k)
+constexpr int kKeyedRowMidAt = 86;
 
 // Registered keys, one signature per workgroup in the row layout (row.h
 // r_decode_neg_r / r_kcomb / r_bcomb16 / r_keyed_join), for batches of at

@@ -82,12 +82,18 @@ struct RowCtx {
   U m38x2;    // 38 on limbs 0 and 1 (the second carry out of limbs 14, 15 wraps), else 1
   U one;      // the constant 1 (limb 0)
   U tw[16];   // column twist of term r: 38 where limb k < r (the column wraps past 2^256), else 1
+  U tw4[4];   // split products (rf_mul_s): the twists of terms 4c + j (four rows share a product)
+  U tw8[8];   // ... of terms 8 (c >> 1) + j (rows c and c ^ 2 share one)
   B r0, r1, r2, r3;
   CMTV_HD explicit RowCtx(const U& lane) {
     k = lane & 15u;
 #pragma unroll
     for (int r = 0; r < 16; r++) tw[r] = sel(k < (uint32_t)r, U(38u), U(1u));
     c = lane >> 4;
+#pragma unroll
+    for (int j = 0; j < 4; j++) tw4[j] = sel(k < (c << 2) + (uint32_t)j, U(38u), U(1u));
+#pragma unroll
+    for (int j = 0; j < 8; j++) tw8[j] = sel(k < ((c >> 1) << 3) + (uint32_t)j, U(38u), U(1u));
     bias = sel(k == 0u, U(4u * 0xFFEDu), sel(k == 15u, U(4u * 0x7FFFu), U(4u * 0xFFFFu)));
     m38 = sel(k == 0u, U(38u), U(1u));
     m38x2 = sel(k < 2u, U(38u), U(1u));
@@ -165,6 +171,66 @@ template <class R>
 CMTV_HD typename R::U rf_sqn(const RowCtx<R>& x, typename R::U f, int n) {
 #pragma unroll 1
   for (int i = 0; i < n; i++) f = rf_sq(x, f);
+  return f;
+}
+
+template <int S, class R, int j>
+CMTV_HD void rf_split_rest(const typename R::U* tws, typename R::U64& acc, const typename R::U& F,
+                           const typename R::U& G) {
+  if constexpr (j < 16 / S) {
+    acc = mad64(R::template ror<j>(F), mul24(R::template bcast<j>(G), tws[j]), acc);
+    rf_split_rest<S, R, j + 1>(tws, acc, F, G);
+  }
+}
+
+// ---- split products ----------------------------------------------------------
+//
+// A chain of products whose operands are the same on S rows (the decode's
+// square-root chain: one point on all four rows, or A and R on rows {0, 2}
+// and {1, 3}) shares each product among those rows: row c takes the 16/S
+// terms r = (16/S) q + j, q its place in the group (c for S = 4, c >> 1 for
+// S = 2), on operands rotated by (16/S) q beforehand -- F = f row_ror:(16/S)q,
+// G = g rotated the other way, so that row_ror:j of F is f_{k-r} and
+// row_newbcast:j of G is g_r -- and the partial column sums are added across
+// the group (v_permlane32_swap / v_permlane16_swap). Per product: 4 (S = 2:
+// 8) terms instead of 16, for 6 (2) rotations and 2 (1) cross-row 64-bit
+// sums. The chain is latency-bound, not issue-bound: measured (row_pt), the
+// decode takes 72k cycles with S = 2, 79k with S = 4 (its rotations and sums
+// are deeper dependent chains), 83k unsplit -- so every decode uses S = 2,
+// which needs only rows c and c ^ 2 to agree.
+template <int S, class R>
+CMTV_HD typename R::U64 rf_split_terms(const typename R::U* tws, const typename R::U& F, const typename R::U& G) {
+  if constexpr (R::kFusedProduct) {
+    return R::template product_split<S>(tws, F, G);
+  } else {
+    typename R::U64 acc = mad64(F, mul24(R::template bcast<0>(G), tws[0]), widen(typename R::U(0u)));
+    rf_split_rest<S, R, 1>(tws, acc, F, G);
+    return acc;
+  }
+}
+
+template <int S, class R>
+CMTV_HD typename R::U rf_mul_s(const RowCtx<R>& x, const typename R::U& f, const typename R::U& g) {
+  if constexpr (S == 1) {
+    return rf_mul(x, f, g);
+  } else {
+    using U = typename R::U;
+    static_assert(S == 2 || S == 4, "rows per product: 1, 2 or 4");
+    const U F = S == 4 ? R::template ror_rows<4, 8, 12>(f) : R::template ror_rows<0, 8, 8>(f);
+    const U G = S == 4 ? R::template ror_rows<12, 8, 4>(g) : R::template ror_rows<0, 8, 8>(g);
+    return rf_carry64(x, R::template sum_rows<S>(rf_split_terms<S, R>(S == 4 ? x.tw4 : x.tw8, F, G)));
+  }
+}
+
+template <int S, class R>
+CMTV_HD typename R::U rf_sq_s(const RowCtx<R>& x, const typename R::U& f) {
+  return rf_mul_s<S>(x, f, f);
+}
+
+template <int S, class R>
+CMTV_HD typename R::U rf_sqn_s(const RowCtx<R>& x, typename R::U f, int n) {
+#pragma unroll 1
+  for (int i = 0; i < n; i++) f = rf_sq_s<S>(x, f);
   return f;
 }
 
@@ -332,57 +398,59 @@ struct RowNoHook {
 // mid(): called once inside the square-root chain, MID_AT squarings into
 // its run of 100 after 2^100 - 1 (~112 + MID_AT of the decode's ~265
 // products): the keyed row kernel's R wave meets the workgroup barrier there
-template <int MID_AT = 0, class R, class Mid = RowNoHook>
+// S: rows sharing each product (rf_mul_s): 4 when y is the same on every
+// row, 2 when rows c and c ^ 2 hold the same y (A on rows 0, 2, R on 1, 3)
+template <int MID_AT = 0, int S = 1, class R, class Mid = RowNoHook>
 CMTV_HD typename R::B rf_decode(const RowCtx<R>& x, const typename R::U& y, const typename R::B& sign,
                                 typename R::U& xo, typename R::U& to, const Mid& mid = Mid()) {
   using U = typename R::U;
-  const U y2 = rf_sq(x, y);
+  const U y2 = rf_sq_s<S>(x, y);
   const U u = rf_carry32(x, rf_sub(x, y2, x.one));                     // y^2 - 1
-  const U v = rf_carry32(x, rf_mul(x, y2, x.cst(RowConst::d)) + x.one);  // d y^2 + 1
-  U t = rf_sq(x, v);                  // v^2
-  U r0 = rf_mul(x, t, v);             // v^3
-  t = rf_sq(x, t);                    // v^4
-  r0 = rf_mul(x, u, r0);              // u v^3
-  t = rf_mul(x, r0, t);               // u v^7
+  const U v = rf_carry32(x, rf_mul_s<S>(x, y2, x.cst(RowConst::d)) + x.one);  // d y^2 + 1
+  U t = rf_sq_s<S>(x, v);                  // v^2
+  U r0 = rf_mul_s<S>(x, t, v);             // v^3
+  t = rf_sq_s<S>(x, t);                    // v^4
+  r0 = rf_mul_s<S>(x, u, r0);              // u v^3
+  t = rf_mul_s<S>(x, r0, t);               // u v^7
   // (u v^7)^((p-5)/8) (fe25519.h fe_pow22523)
   {
     const U z = t;
     U t0, t1, t2, z2, z9, z11;
-    z2 = rf_sq(x, z);
-    t0 = rf_sqn(x, z2, 2);
-    z9 = rf_mul(x, t0, z);
-    z11 = rf_mul(x, z9, z2);
-    t0 = rf_mul(x, rf_sq(x, z11), z9);  // 2^5 - 1
-    t1 = rf_sqn(x, t0, 5);
-    t0 = rf_mul(x, t1, t0);             // 2^10 - 1
-    t1 = rf_sqn(x, t0, 10);
-    t1 = rf_mul(x, t1, t0);             // 2^20 - 1
-    t2 = rf_sqn(x, t1, 20);
-    t1 = rf_mul(x, t2, t1);             // 2^40 - 1
-    t1 = rf_sqn(x, t1, 10);
-    t0 = rf_mul(x, t1, t0);             // 2^50 - 1
-    t1 = rf_sqn(x, t0, 50);
-    t1 = rf_mul(x, t1, t0);             // 2^100 - 1
-    t2 = rf_sqn(x, t1, MID_AT);
+    z2 = rf_sq_s<S>(x, z);
+    t0 = rf_sqn_s<S>(x, z2, 2);
+    z9 = rf_mul_s<S>(x, t0, z);
+    z11 = rf_mul_s<S>(x, z9, z2);
+    t0 = rf_mul_s<S>(x, rf_sq_s<S>(x, z11), z9);  // 2^5 - 1
+    t1 = rf_sqn_s<S>(x, t0, 5);
+    t0 = rf_mul_s<S>(x, t1, t0);             // 2^10 - 1
+    t1 = rf_sqn_s<S>(x, t0, 10);
+    t1 = rf_mul_s<S>(x, t1, t0);             // 2^20 - 1
+    t2 = rf_sqn_s<S>(x, t1, 20);
+    t1 = rf_mul_s<S>(x, t2, t1);             // 2^40 - 1
+    t1 = rf_sqn_s<S>(x, t1, 10);
+    t0 = rf_mul_s<S>(x, t1, t0);             // 2^50 - 1
+    t1 = rf_sqn_s<S>(x, t0, 50);
+    t1 = rf_mul_s<S>(x, t1, t0);             // 2^100 - 1
+    t2 = rf_sqn_s<S>(x, t1, MID_AT);
     mid();
-    t2 = rf_sqn(x, t2, 100 - MID_AT);
-    t1 = rf_mul(x, t2, t1);             // 2^200 - 1
-    t1 = rf_sqn(x, t1, 50);
-    t1 = rf_mul(x, t1, t0);             // 2^250 - 1
-    t1 = rf_sqn(x, t1, 2);
-    t = rf_mul(x, t1, z);               // (p-5)/8
+    t2 = rf_sqn_s<S>(x, t2, 100 - MID_AT);
+    t1 = rf_mul_s<S>(x, t2, t1);             // 2^200 - 1
+    t1 = rf_sqn_s<S>(x, t1, 50);
+    t1 = rf_mul_s<S>(x, t1, t0);             // 2^250 - 1
+    t1 = rf_sqn_s<S>(x, t1, 2);
+    t = rf_mul_s<S>(x, t1, z);               // (p-5)/8
   }
-  r0 = rf_mul(x, r0, t);          // r = u v^3 (u v^7)^((p-5)/8)
-  t = rf_mul(x, rf_sq(x, r0), v);  // v r^2
+  r0 = rf_mul_s<S>(x, r0, t);          // r = u v^3 (u v^7)^((p-5)/8)
+  t = rf_mul_s<S>(x, rf_sq_s<S>(x, r0), v);  // v r^2
   const RowCanon<R> correct = rf_canon<R>(rf_sub(x, t, u));
   const RowCanon<R> flipped = rf_canon<R>(t + u);
-  r0 = sel(flipped.zero, rf_mul(x, r0, x.cst(RowConst::sqrtm1)), r0);
+  r0 = sel(flipped.zero, rf_mul_s<S>(x, r0, x.cst(RowConst::sqrtm1)), r0);
   // Absolute(): the even root; then the sign bit picks the negative one
   const RowCanon<R> rc = rf_canon<R>(r0);
   const typename R::B neg = rc.odd != sign;
   r0 = sel(neg, rf_carry32(x, rf_neg(x, r0)), r0);
   xo = r0;
-  to = rf_mul(x, r0, y);
+  to = rf_mul_s<S>(x, r0, y);
   return correct.zero || flipped.zero;
 }
 
@@ -460,7 +528,7 @@ CMTV_HD typename R::U r_sum_ar(const RowCtx<R>& x, const typename R::U& limb, co
   const bool a_sign = (pkw[7] >> 31) != 0, r_sign = (sigw[7] >> 31) != 0;
   const U y = sel(x.k == 15u, limb & 0x7FFFu, limb);
   U xo, to;
-  const B dec = rf_decode(x, y, sel(is_r, B(r_sign), B(a_sign)), xo, to);
+  const B dec = rf_decode<0, 2>(x, y, sel(is_r, B(r_sign), B(a_sign)), xo, to);
   const uint64_t decm = R::ballot(dec);
   a_ok = (decm & 1u) != 0;
   r_ok = ((decm >> 16) & 1u) != 0;  // lane 0 of rows 0 and 1
@@ -532,12 +600,14 @@ CMTV_HD bool r_verify_split(const R&, const typename R::U& limb, const uint32_t 
 struct RowNoStamp {
   CMTV_HD void operator()(int) const {}
 };
-// windows the four-wave form leaves to its lo wave (84 bits: W >= 33, so the
-// high parts take 12..16 windows, 43 on the wide schedule), and the high
-// waves' doublings before the scalars' barrier (decode ~96k cycles + 24 x
-// ~830 ~ the helper's hash and half-size pair, ~117k)
-constexpr int kRowLoWindows = 21;
-constexpr int kRowHiPreDoublings = 24;
+// windows the four-wave form leaves to its lo wave (72 bits: W >= 33, so the
+// high parts take 15..19 windows, 46 on the wide schedule), and the high
+// waves' doublings before the scalars' barrier: decode ~75k cycles + 48 x
+// ~800 ~ the helper's hash and half-size pair (~114k, tools/row_phase.py);
+// after it the lo wave's 18 windows and a high wave's 24 doublings + table +
+// 15 windows both take ~87k
+constexpr int kRowLoWindows = 18;
+constexpr int kRowHiPreDoublings = 48;
 // HI > 0 (the four-wave form): the part takes only the windows above the
 // lowest HI, against [2^(4 HI)](-P) -- 4 HI doublings of -P before its table,
 // while the helper hashes -- and the lo wave (r_sum_ar) takes the rest.
@@ -548,7 +618,7 @@ CMTV_HD typename R::U r_part(const RowCtx<R>& x, const typename R::U& limb, bool
   using U = typename R::U;
   const U y = sel(x.k == 15u, limb & 0x7FFFu, limb);
   U xo, to;
-  dec = (R::ballot(rf_decode(x, y, typename R::B(sign), xo, to)) & 1u) != 0;
+  dec = (R::ballot(rf_decode<0, 2>(x, y, typename R::B(sign), xo, to)) & 1u) != 0;
   x0 = (R::ballot(rf_canon<R>(xo).zero) & 1u) != 0;
   stamp(6);  // decoded
   U X0, X1, X2, X3, Y0, Y1, Y2, Y3, T0, T1, T2, T3;
@@ -672,7 +742,7 @@ CMTV_HD typename R::U r_decode_neg_r(const RowCtx<R>& x, const typename R::U& li
   const bool sign = (sigw[7] >> 31) != 0;
   const U y = sel(x.k == 15u, limb & 0x7FFFu, limb);
   U xo, to;
-  r_ok = (R::ballot(rf_decode<MID_AT>(x, y, typename R::B(sign), xo, to, mid)) & 1u) != 0;
+  r_ok = (R::ballot(rf_decode<MID_AT, 2>(x, y, typename R::B(sign), xo, to, mid)) & 1u) != 0;
   const bool x0 = (R::ballot(rf_canon<R>(xo).zero) & 1u) != 0;
   if (MODE == MODE_GO_STDLIB) r_ok = r_ok && y_is_canonical(sigw) && !(x0 && sign);
   U X0, X1, X2, X3, Y0, Y1, Y2, Y3, T0, T1, T2, T3;

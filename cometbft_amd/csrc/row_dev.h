@@ -59,6 +59,10 @@ namespace cmtv {
         [t5] "v"(tw[5]), [t6] "v"(tw[6]), [t7] "v"(tw[7]), [t8] "v"(tw[8]), [t9] "v"(tw[9]), [t10] "v"(tw[10]),  \
         [t11] "v"(tw[11]), [t12] "v"(tw[12]), [t13] "v"(tw[13]), [t14] "v"(tw[14]), [t15] "v"(tw[15]))
 
+// the split products' terms (row.h rf_mul_s): term 0 is F times g_0's
+// twisted broadcast (row_newbcast:0), terms 1.. as CMTV_ROW_TERM
+#define CMTV_ROW_BTERM0 "v_mul_u32_u24_dpp %[b0], %[g], %[t0] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+
 struct DevRow {
   using U = uint32_t;
   using U64 = uint64_t;
@@ -79,6 +83,67 @@ struct DevRow {
 #pragma unroll
     for (int r = 1; r < 16; r++) acc += (uint64_t)fr[r] * gt[r];
     return acc;
+  }
+  // the 16 / S column terms of a split product (row.h rf_split_terms) on the
+  // rotated operands F, G, with the twists tw[0 .. 16/S)
+  template <int S>
+  __device__ __forceinline__ static uint64_t product_split(const uint32_t* tw, uint32_t f, uint32_t g) {
+    uint32_t fr[8], gt[8];
+    if constexpr (S == 4) {
+      asm("s_nop 1\n\t" CMTV_ROW_BTERM0 CMTV_ROW_TERM(1, "%[a1]", "%[b1]", "%[t1]")
+              CMTV_ROW_TERM(2, "%[a2]", "%[b2]", "%[t2]") CMTV_ROW_TERM(3, "%[a3]", "%[b3]", "%[t3]")
+          : [b0] "=&v"(gt[0]), [a1] "=&v"(fr[1]), [b1] "=&v"(gt[1]), [a2] "=&v"(fr[2]), [b2] "=&v"(gt[2]),
+            [a3] "=&v"(fr[3]), [b3] "=&v"(gt[3])
+          : [f] "v"(f), [g] "v"(g), [t0] "v"(tw[0]), [t1] "v"(tw[1]), [t2] "v"(tw[2]), [t3] "v"(tw[3]));
+    } else {
+      static_assert(S == 2, "split products share 2 or 4 rows");
+      asm("s_nop 1\n\t" CMTV_ROW_BTERM0 CMTV_ROW_TERM(1, "%[a1]", "%[b1]", "%[t1]")
+              CMTV_ROW_TERM(2, "%[a2]", "%[b2]", "%[t2]") CMTV_ROW_TERM(3, "%[a3]", "%[b3]", "%[t3]")
+                  CMTV_ROW_TERM(4, "%[a4]", "%[b4]", "%[t4]") CMTV_ROW_TERM(5, "%[a5]", "%[b5]", "%[t5]")
+                      CMTV_ROW_TERM(6, "%[a6]", "%[b6]", "%[t6]") CMTV_ROW_TERM(7, "%[a7]", "%[b7]", "%[t7]")
+          : [b0] "=&v"(gt[0]), [a1] "=&v"(fr[1]), [b1] "=&v"(gt[1]), [a2] "=&v"(fr[2]), [b2] "=&v"(gt[2]),
+            [a3] "=&v"(fr[3]), [b3] "=&v"(gt[3]), [a4] "=&v"(fr[4]), [b4] "=&v"(gt[4]), [a5] "=&v"(fr[5]),
+            [b5] "=&v"(gt[5]), [a6] "=&v"(fr[6]), [b6] "=&v"(gt[6]), [a7] "=&v"(fr[7]), [b7] "=&v"(gt[7])
+          : [f] "v"(f), [g] "v"(g), [t0] "v"(tw[0]), [t1] "v"(tw[1]), [t2] "v"(tw[2]), [t3] "v"(tw[3]),
+            [t4] "v"(tw[4]), [t5] "v"(tw[5]), [t6] "v"(tw[6]), [t7] "v"(tw[7]));
+    }
+    uint64_t acc = (uint64_t)f * gt[0];
+#pragma unroll
+    for (int r = 1; r < 16 / S; r++) acc += (uint64_t)fr[r] * gt[r];
+    return acc;
+  }
+  // rows 1..3 rotated by A1..A3 (row_ror; 0: as is), row 0 as is: DPP moves
+  // with a row mask onto a copy
+  template <int A1, int A2, int A3>
+  __device__ __forceinline__ static U ror_rows(U x) {
+    U r = x;
+    if constexpr (A1 != 0) r = (uint32_t)__builtin_amdgcn_update_dpp((int)r, (int)x, 0x120 + A1, 0x2, 0xF, false);
+    if constexpr (A2 != 0 && A2 == A3) {
+      r = (uint32_t)__builtin_amdgcn_update_dpp((int)r, (int)x, 0x120 + A2, 0xC, 0xF, false);
+    } else {
+      if constexpr (A2 != 0) r = (uint32_t)__builtin_amdgcn_update_dpp((int)r, (int)x, 0x120 + A2, 0x4, 0xF, false);
+      if constexpr (A3 != 0) r = (uint32_t)__builtin_amdgcn_update_dpp((int)r, (int)x, 0x120 + A3, 0x8, 0xF, false);
+    }
+    return r;
+  }
+  // S = 2: rows c and c ^ 2 summed (v_permlane32_swap: {[x0 x1 x0 x1], [x2 x3 x2 x3]});
+  // S = 4: then rows c and c ^ 1 (v_permlane16_swap): the four-row sum everywhere
+  template <int S>
+  __device__ __forceinline__ static uint64_t sum_rows(uint64_t x) {
+    uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    {
+      const auto l = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+      const auto h = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+      x = (((uint64_t)h[0] << 32) | l[0]) + (((uint64_t)h[1] << 32) | l[1]);
+    }
+    if constexpr (S == 4) {
+      lo = (uint32_t)x;
+      hi = (uint32_t)(x >> 32);
+      const auto l = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+      const auto h = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+      x = (((uint64_t)h[0] << 32) | l[0]) + (((uint64_t)h[1] << 32) | l[1]);
+    }
+    return x;
   }
   __device__ __forceinline__ static U lane() { return threadIdx.x & 63; }
   template <int R>

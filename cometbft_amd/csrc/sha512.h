@@ -16,8 +16,10 @@
 
 namespace cmtv {
 
-CMTV_HD uint64_t sha512_k(int i) {
-  constexpr uint64_t K[80] = {
+// round constants: a global table (the compression's rolled loop indexes it
+// with a wave-uniform round number: scalar loads)
+#ifdef __HIP_DEVICE_COMPILE__
+static __constant__ uint64_t g_sha512_K[80] = {
       0x428a2f98d728ae22ULL, 0x7137449123ef65cdULL, 0xb5c0fbcfec4d3b2fULL, 0xe9b5dba58189dbbcULL,
       0x3956c25bf348b538ULL, 0x59f111f1b605d019ULL, 0x923f82a4af194f9bULL, 0xab1c5ed5da6d8118ULL,
       0xd807aa98a3030242ULL, 0x12835b0145706fbeULL, 0x243185be4ee4b28cULL, 0x550c7dc3d5ffb4e2ULL,
@@ -38,39 +40,114 @@ CMTV_HD uint64_t sha512_k(int i) {
       0x06f067aa72176fbaULL, 0x0a637dc5a2c898a6ULL, 0x113f9804bef90daeULL, 0x1b710b35131c471bULL,
       0x28db77f523047d84ULL, 0x32caab7b40c72493ULL, 0x3c9ebe0a15c9bebcULL, 0x431d67c49c100d4cULL,
       0x4cc5d4becb3e42b6ULL, 0x597f299cfc657e2aULL, 0x5fcb6fab3ad6faecULL, 0x6c44198c4a475817ULL};
-  return K[i];
-}
+#else
+static const uint64_t g_sha512_K[80] = {
+      0x428a2f98d728ae22ULL, 0x7137449123ef65cdULL, 0xb5c0fbcfec4d3b2fULL, 0xe9b5dba58189dbbcULL,
+      0x3956c25bf348b538ULL, 0x59f111f1b605d019ULL, 0x923f82a4af194f9bULL, 0xab1c5ed5da6d8118ULL,
+      0xd807aa98a3030242ULL, 0x12835b0145706fbeULL, 0x243185be4ee4b28cULL, 0x550c7dc3d5ffb4e2ULL,
+      0x72be5d74f27b896fULL, 0x80deb1fe3b1696b1ULL, 0x9bdc06a725c71235ULL, 0xc19bf174cf692694ULL,
+      0xe49b69c19ef14ad2ULL, 0xefbe4786384f25e3ULL, 0x0fc19dc68b8cd5b5ULL, 0x240ca1cc77ac9c65ULL,
+      0x2de92c6f592b0275ULL, 0x4a7484aa6ea6e483ULL, 0x5cb0a9dcbd41fbd4ULL, 0x76f988da831153b5ULL,
+      0x983e5152ee66dfabULL, 0xa831c66d2db43210ULL, 0xb00327c898fb213fULL, 0xbf597fc7beef0ee4ULL,
+      0xc6e00bf33da88fc2ULL, 0xd5a79147930aa725ULL, 0x06ca6351e003826fULL, 0x142929670a0e6e70ULL,
+      0x27b70a8546d22ffcULL, 0x2e1b21385c26c926ULL, 0x4d2c6dfc5ac42aedULL, 0x53380d139d95b3dfULL,
+      0x650a73548baf63deULL, 0x766a0abb3c77b2a8ULL, 0x81c2c92e47edaee6ULL, 0x92722c851482353bULL,
+      0xa2bfe8a14cf10364ULL, 0xa81a664bbc423001ULL, 0xc24b8b70d0f89791ULL, 0xc76c51a30654be30ULL,
+      0xd192e819d6ef5218ULL, 0xd69906245565a910ULL, 0xf40e35855771202aULL, 0x106aa07032bbd1b8ULL,
+      0x19a4c116b8d2d0c8ULL, 0x1e376c085141ab53ULL, 0x2748774cdf8eeb99ULL, 0x34b0bcb5e19b48a8ULL,
+      0x391c0cb3c5c95a63ULL, 0x4ed8aa4ae3418acbULL, 0x5b9cca4f7763e373ULL, 0x682e6ff3d6b2b8a3ULL,
+      0x748f82ee5defb2fcULL, 0x78a5636f43172f60ULL, 0x84c87814a1f0ab72ULL, 0x8cc702081a6439ecULL,
+      0x90befffa23631e28ULL, 0xa4506cebde82bde9ULL, 0xbef9a3f7b2c67915ULL, 0xc67178f2e372532bULL,
+      0xca273eceea26619cULL, 0xd186b8c721c0c207ULL, 0xeada7dd6cde0eb1eULL, 0xf57d4f7fee6ed178ULL,
+      0x06f067aa72176fbaULL, 0x0a637dc5a2c898a6ULL, 0x113f9804bef90daeULL, 0x1b710b35131c471bULL,
+      0x28db77f523047d84ULL, 0x32caab7b40c72493ULL, 0x3c9ebe0a15c9bebcULL, 0x431d67c49c100d4cULL,
+      0x4cc5d4becb3e42b6ULL, 0x597f299cfc657e2aULL, 0x5fcb6fab3ad6faecULL, 0x6c44198c4a475817ULL};
+#endif
+
+CMTV_HD uint64_t sha512_k(int i) { return g_sha512_K[i]; }
 
 CMTV_HD uint64_t rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
 
+// x >>> n and x >> n for the compression's constant n: on the device as
+// v_alignbit_b32 pairs on the 32-bit halves (the generic 64-bit form lowers
+// to two 64-bit shifts and two ORs, and hides the three-way XORs from
+// v_xor3_b32 -- ~1.8x the instructions of a round, which is the helper
+// wave's whole cost: one wave per SIMD issues one instruction per ~4 cycles)
+CMTV_HD uint64_t sha_rotr(uint64_t x, int n) {
+#ifdef __HIP_DEVICE_COMPILE__
+  uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  if (n >= 32) {
+    const uint32_t t = lo;
+    lo = hi;
+    hi = t;
+    n -= 32;
+  }
+  if (n == 0) return ((uint64_t)hi << 32) | lo;
+  const uint32_t nlo = __builtin_amdgcn_alignbit(hi, lo, n), nhi = __builtin_amdgcn_alignbit(lo, hi, n);
+  return ((uint64_t)nhi << 32) | nlo;
+#else
+  return rotr64(x, n);
+#endif
+}
+CMTV_HD uint64_t sha_shr(uint64_t x, int n) {
+#ifdef __HIP_DEVICE_COMPILE__
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  return ((uint64_t)(hi >> n) << 32) | __builtin_amdgcn_alignbit(hi, lo, n);
+#else
+  return x >> n;
+#endif
+}
+
+// one round on the rotating state (a..h named by the caller's order)
+CMTV_HD void sha512_round(uint64_t a, uint64_t b, uint64_t c, uint64_t& d, uint64_t e, uint64_t f, uint64_t g,
+                          uint64_t& h, uint64_t kw) {
+  const uint64_t S1 = sha_rotr(e, 14) ^ sha_rotr(e, 18) ^ sha_rotr(e, 41);
+  const uint64_t ch = (e & f) | (~e & g);
+  const uint64_t t1 = h + S1 + ch + kw;
+  const uint64_t S0 = sha_rotr(a, 28) ^ sha_rotr(a, 34) ^ sha_rotr(a, 39);
+  const uint64_t ab = a ^ b;
+  const uint64_t maj = (ab & c) | (~ab & b);  // majority: c where a, b differ, else b
+  d += t1;
+  h = t1 + S0 + maj;
+}
+
+// 16 rounds from round r0 on: the state's names rotate by one per round, so
+// after 16 (a multiple of 8) they are back in place; SCHED: w[j] becomes
+// schedule word r0 + j first
+template <bool SCHED>
+CMTV_HD void sha512_rounds16(uint64_t& a, uint64_t& b, uint64_t& c, uint64_t& d, uint64_t& e, uint64_t& f,
+                             uint64_t& g, uint64_t& h, uint64_t w[16], int r0) {
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    if (SCHED) {
+      const uint64_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
+      const uint64_t s0 = sha_rotr(w15, 1) ^ sha_rotr(w15, 8) ^ sha_shr(w15, 7);
+      const uint64_t s1 = sha_rotr(w2, 19) ^ sha_rotr(w2, 61) ^ sha_shr(w2, 6);
+      w[j] += s0 + w[(j + 9) & 15] + s1;
+    }
+    const uint64_t kw = sha512_k(r0 + j) + w[j];
+    switch (j & 7) {
+      case 0: sha512_round(a, b, c, d, e, f, g, h, kw); break;
+      case 1: sha512_round(h, a, b, c, d, e, f, g, kw); break;
+      case 2: sha512_round(g, h, a, b, c, d, e, f, kw); break;
+      case 3: sha512_round(f, g, h, a, b, c, d, e, kw); break;
+      case 4: sha512_round(e, f, g, h, a, b, c, d, kw); break;
+      case 5: sha512_round(d, e, f, g, h, a, b, c, kw); break;
+      case 6: sha512_round(c, d, e, f, g, h, a, b, kw); break;
+      default: sha512_round(b, c, d, e, f, g, h, a, kw); break;
+    }
+  }
+}
+
+// The compression function: rounds 0..15 on the block's words, then four
+// rolled passes of 16 with the message schedule (a rolled loop keeps the
+// code ~1.5k instructions: the helper waves share the instruction cache with
+// the row waves' field products)
 CMTV_HD void sha512_compress(uint64_t st[8], uint64_t w[16]) {
   uint64_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
-#pragma unroll
-  for (int i = 0; i < 80; i++) {
-    uint64_t wi;
-    if (i < 16) {
-      wi = w[i & 15];
-    } else {
-      const uint64_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
-      const uint64_t s0 = rotr64(w15, 1) ^ rotr64(w15, 8) ^ (w15 >> 7);
-      const uint64_t s1 = rotr64(w2, 19) ^ rotr64(w2, 61) ^ (w2 >> 6);
-      wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
-      w[i & 15] = wi;
-    }
-    const uint64_t S1 = rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41);
-    const uint64_t ch = (e & f) ^ (~e & g);
-    const uint64_t t1 = h + S1 + ch + sha512_k(i) + wi;
-    const uint64_t S0 = rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39);
-    const uint64_t maj = (a & b) ^ (a & c) ^ (b & c);
-    h = g;
-    g = f;
-    f = e;
-    e = d + t1;
-    d = c;
-    c = b;
-    b = a;
-    a = t1 + S0 + maj;
-  }
+  sha512_rounds16<false>(a, b, c, d, e, f, g, h, w, 0);
+#pragma unroll 1
+  for (int r = 16; r < 80; r += 16) sha512_rounds16<true>(a, b, c, d, e, f, g, h, w, r);
   st[0] += a; st[1] += b; st[2] += c; st[3] += d;
   st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }

@@ -182,6 +182,24 @@ struct HostRow {
       b3.a[i] = x.a[48 + k];
     }
   }
+  // rows 1..3 rotated by A1..A3 (row_ror), row 0 as is
+  template <int A1, int A2, int A3>
+  static U ror_rows(const U& x) {
+    const int A[4] = {0, A1, A2, A3};
+    U r;
+    for (int i = 0; i < 64; i++) r.a[i] = x.a[(i & ~15) | ((i - A[i >> 4]) & 15)];
+    return r;
+  }
+  // S = 4: the sum over the four rows on every row; S = 2: rows c and c ^ 2
+  template <int S>
+  static U64 sum_rows(const U64& x) {
+    U64 r;
+    for (int i = 0; i < 64; i++) {
+      const int k = i & 15;
+      r.a[i] = S == 4 ? x.a[k] + x.a[16 + k] + x.a[32 + k] + x.a[48 + k] : x.a[i] + x.a[i ^ 32];
+    }
+    return r;
+  }
   static uint64_t ballot(const B& b) {
     uint64_t m = 0;
     for (int i = 0; i < 64; i++) m |= (uint64_t)b.a[i] << i;

@@ -29,7 +29,7 @@ __global__ __launch_bounds__(64, 1) void k_rowpt(uint32_t nops, const uint32_t* 
   tab_lds[kRowTabWords + t] = t;
   __syncthreads();
   const uint32_t n = nops + (tab_lds[kRowTabWords + (t & 7)] > 1000 ? 1u : 0u);
-  uint64_t st[6];
+  uint64_t st[8];
   st[0] = __builtin_amdgcn_s_memtime();
 #pragma unroll 1
   for (uint32_t k = 0; k < n; k++) rp_dbl(x, v);
@@ -71,9 +71,18 @@ __global__ __launch_bounds__(64, 1) void k_rowpt(uint32_t nops, const uint32_t* 
     v ^= w;
   }
   st[5] = __builtin_amdgcn_s_memtime();
+  // the split decodes (row.h rf_mul_s): one y on rows {0, 2} and one on {1, 3}
+  // (S = 2), one y on every row (S = 4)
+  uint32_t b0, b1, b2, b3;
+  DevRow::rows(v & 0xFFFFu, b0, b1, b2, b3);
+  uint32_t x2, t2, x4, t4;
+  const bool ok2 = rf_decode<0, 2>(x, (t & 16) ? b1 : b0, (v & 1) != 0, x2, t2);
+  st[6] = __builtin_amdgcn_s_memtime();
+  const bool ok4 = rf_decode<0, 4>(x, b0, (v & 1) != 0, x4, t4);
+  st[7] = __builtin_amdgcn_s_memtime();
   if (t == 0)
-    for (int i = 0; i < 5; i++) cyc[blockIdx.x * 5 + i] = st[i + 1] - st[i];
-  out[blockIdx.x * 64 + t] = v ^ xo ^ to ^ (ok ? 1u : 0u);
+    for (int i = 0; i < 7; i++) cyc[blockIdx.x * 7 + i] = st[i + 1] - st[i];
+  out[blockIdx.x * 64 + t] = v ^ xo ^ to ^ (ok ? 1u : 0u) ^ x2 ^ t2 ^ x4 ^ t4 ^ (ok2 ? 2u : 0u) ^ (ok4 ? 4u : 0u);
 }
 
 int main() {
@@ -87,17 +96,18 @@ int main() {
   }
   uint32_t *din, *dout;
   uint64_t* dcyc;
-  if (hipMalloc(&din, 4 * h.size()) || hipMalloc(&dout, 4 * blocks * 64) || hipMalloc(&dcyc, 8 * blocks * 5)) return 1;
+  if (hipMalloc(&din, 4 * h.size()) || hipMalloc(&dout, 4 * blocks * 64) || hipMalloc(&dcyc, 8 * blocks * 7)) return 1;
   (void)hipMemcpy(din, h.data(), 4 * h.size(), hipMemcpyHostToDevice);
   for (int rep = 0; rep < 2; rep++) hipLaunchKernelGGL(k_rowpt, dim3(blocks), dim3(64), 0, 0, nops, din, dcyc, dout);
-  std::vector<uint64_t> c(blocks * 5);
+  std::vector<uint64_t> c(blocks * 7);
   if (hipMemcpy(c.data(), dcyc, 8 * c.size(), hipMemcpyDeviceToHost) != hipSuccess) return 1;
-  double sum[5] = {0, 0, 0, 0, 0};
+  double sum[7] = {0, 0, 0, 0, 0, 0, 0};
   for (int b = 0; b < blocks; b++)
-    for (int i = 0; i < 5; i++) sum[i] += (double)c[b * 5 + i];
-  const char* nm[5] = {"rp_dbl", "rp_add", "window (4 dbl + 2 LDS add)", "rf_decode (A and R rows)",
-                       "one table (0..8), both signs"};
-  const double per[5] = {(double)nops, (double)nops, (double)(nops / 4), 1.0, 1.0};
-  for (int i = 0; i < 5; i++) printf("%-32s %10.1f cycles (s_memtime, %d waves, 1 per CU)\n", nm[i], sum[i] / blocks / per[i], blocks);
+    for (int i = 0; i < 7; i++) sum[i] += (double)c[b * 7 + i];
+  const char* nm[7] = {"rp_dbl", "rp_add", "window (4 dbl + 2 LDS add)", "rf_decode (A and R rows)",
+                       "one table (0..8), both signs", "rf_decode S=2 (A, R: 2 rows each)",
+                       "rf_decode S=4 (one point)"};
+  const double per[7] = {(double)nops, (double)nops, (double)(nops / 4), 1.0, 1.0, 1.0, 1.0};
+  for (int i = 0; i < 7; i++) printf("%-32s %10.1f cycles (s_memtime, %d waves, 1 per CU)\n", nm[i], sum[i] / blocks / per[i], blocks);
   return 0;
 }

@@ -62,6 +62,18 @@ CMTV_HD int hs_windows_for(int bits) { return bits <= HS_MAX_BITS ? HS_WINDOWS :
 constexpr int HS_MAX_ROUNDS = 192;  // outer rounds before giving up (Lehmer: ~10; exact steps: ~75)
 constexpr int HS_MAX_INNER = 40;    // Lehmer inner steps per round (30-bit digits: ~9)
 
+// A branch condition of the split. UNI: every lane of the wave holds the same
+// scalar (the row kernels' helper waves), so the condition is taken from the
+// ballot -- a scalar compare and branch instead of the exec-mask bookkeeping
+// of a divergent one (~a quarter of the Lehmer loop's instructions).
+template <bool UNI>
+CMTV_HD bool hs_uni(bool c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (UNI) return __builtin_amdgcn_ballot_w64(c) != 0;
+#endif
+  return c;
+}
+
 struct HalfScalars {
   uint32_t k1[8];  // >= 0
   uint32_t k2[8];  // |k2|, odd
@@ -126,9 +138,10 @@ CMTV_HD void hs_shr8(uint32_t r[8], int sh) {
 
 // one Euclid step on normalised (r0, r1): rr = r0 - q r1 with q = floor(r0 / r1),
 // tt = t0 - q t1. Returns false if q does not fit the one-word estimate.
+template <bool UNI = false>
 CMTV_HD bool hs_step(uint32_t rr[8], uint32_t tt[6], const uint32_t r0[8], const uint32_t r1[8],
                      const uint32_t t0[6], const uint32_t t1[6]) {
-  if (r1[7] == 0) return false;  // r1 < r0 / 2^31: quotient too wide for one word
+  if (hs_uni<UNI>(r1[7] == 0)) return false;  // r1 < r0 / 2^31: quotient too wide for one word
   // the top 64 bits of each as an f64 (one rounding of the exact value)
   const double a = (double)r0[7] * 4294967296.0 + (double)r0[6];
   const double b = (double)r1[7] * 4294967296.0 + (double)r1[6];
@@ -165,7 +178,7 @@ CMTV_HD bool hs_step(uint32_t rr[8], uint32_t tt[6], const uint32_t r0[8], const
   // the estimate is within a few units of q: fix it up (rarely entered)
   bool ok = true;
 #pragma unroll 1
-  for (int it = 0; (x[8] >> 31) && it < 4; it++) {  // x < 0: add r1 back
+  for (int it = 0; it < 4 && hs_uni<UNI>((x[8] >> 31) != 0); it++) {  // x < 0: add r1 back
     uint64_t c = 0;
 #pragma unroll
     for (int i = 0; i < 8; i++) {
@@ -194,7 +207,7 @@ CMTV_HD bool hs_step(uint32_t rr[8], uint32_t tt[6], const uint32_t r0[8], const
       acc >>= 32;
     }
     acc += (int64_t)x[8];
-    if (acc < 0) break;
+    if (hs_uni<UNI>(acc < 0)) break;
 #pragma unroll
     for (int i = 0; i < 8; i++) x[i] = y[i];
     x[8] = (uint32_t)acc;
@@ -225,6 +238,7 @@ CMTV_HD uint32_t hs_udiv31(uint32_t a, uint32_t b) { return (uint32_t)((double)a
 // divisor might already be below 2^127, where the exact Euclid stops: after
 // the accepted steps the true divisor lies in 2^h (v + min(C,D), v + max(C,D)).
 // B == 0 on return: no step was certain.
+template <bool UNI = false>
 CMTV_HD void hs_lehmer(int32_t& A, int32_t& B, int32_t& C, int32_t& D, uint32_t u, uint32_t v, int h) {
   const int32_t thr = h >= 127 ? 1 : (int32_t)(1u << (127 - h));
   int32_t a = 1, b = 0, c = 0, d = 1;
@@ -233,11 +247,11 @@ CMTV_HD void hs_lehmer(int32_t& A, int32_t& B, int32_t& C, int32_t& D, uint32_t 
   for (int it = 0; it < HS_MAX_INNER; it++) {
     const int32_t vc = vv + c, vd = vv + d;
     const int32_t lo = vc < vd ? vc : vd;
-    if (lo < thr) break;  // divisor not certainly >= 2^127 (also keeps vc, vd > 0)
+    if (hs_uni<UNI>(lo < thr)) break;  // divisor not certainly >= 2^127 (also keeps vc, vd > 0)
     const uint32_t q = hs_udiv31((uint32_t)(uu + a), (uint32_t)vc);
     // the other corner must give the same quotient: 0 <= (u+b) - q (v+d) < v+d
     const int64_t x = (int64_t)(uu + b) - (int64_t)q * vd;
-    if (x < 0 || x >= vd) break;
+    if (hs_uni<UNI>(x < 0 || x >= vd)) break;
     const int32_t nc = (int32_t)((int64_t)a - (int64_t)q * c);
     const int32_t nd = (int32_t)((int64_t)b - (int64_t)q * d);
     const int32_t nv = (int32_t)((int64_t)uu - (int64_t)q * vv);
@@ -284,7 +298,8 @@ CMTV_HD void hs_lin(uint32_t out[W], int32_t P, const uint32_t x[], int32_t Q, c
 // force_wide: take the wide schedule regardless (CMTV_FORCE_WIDE test knob,
 // so the 64-window path -- ~never reached by real k -- is exercised)
 // odd_k2: the cofactorless (GO_STDLIB) requirement; ZIP215 passes false
-template <bool LEHMER = true>
+// UNI: the wave's lanes all hold the same k (hs_uni)
+template <bool LEHMER = true, bool UNI = false>
 CMTV_HD void half_scalars(HalfScalars& h, const uint32_t k[8], bool force_wide = false, bool odd_k2 = true) {
   uint32_t r0[8], r1[8], t0[6], t1[6];
 #pragma unroll
@@ -302,17 +317,17 @@ CMTV_HD void half_scalars(HalfScalars& h, const uint32_t k[8], bool force_wide =
 #pragma unroll 1
   for (int round = 0; round < HS_MAX_ROUNDS; round++) {
     const int bl1 = (r1[7] ? 256 - hs_clz(r1[7]) : hs_bitlen8(r1)) - e;
-    if (bl1 <= 127) break;
+    if (hs_uni<UNI>(bl1 <= 127)) break;
     if (round == HS_MAX_ROUNDS - 1) {
       ok = false;
       break;
     }
     int32_t A = 1, B = 0, C = 0, D = 1;
-    if (LEHMER) hs_lehmer(A, B, C, D, r0[7] >> 2, r1[7] >> 2, 226 - e);
-    if (B == 0) {
+    if (LEHMER) hs_lehmer<UNI>(A, B, C, D, r0[7] >> 2, r1[7] >> 2, 226 - e);
+    if (hs_uni<UNI>(B == 0)) {
       // no quotient certain from the leading digits: one exact step
       uint32_t rr[8], tt[6];
-      if (!hs_step(rr, tt, r0, r1, t0, t1)) {
+      if (hs_uni<UNI>(!hs_step<UNI>(rr, tt, r0, r1, t0, t1))) {
         ok = false;
         break;
       }
@@ -346,7 +361,7 @@ CMTV_HD void half_scalars(HalfScalars& h, const uint32_t k[8], bool force_wide =
     }
     // renormalise: r0's top bit back to bit 255
 #pragma unroll 1
-    while (r0[7] == 0) {
+    while (hs_uni<UNI>(r0[7] == 0)) {
 #pragma unroll
       for (int i = 7; i > 0; i--) {
         r0[i] = r0[i - 1];
@@ -371,7 +386,7 @@ CMTV_HD void half_scalars(HalfScalars& h, const uint32_t k[8], bool force_wide =
   const bool t1_odd = t1[0] & 1;
   uint32_t r2[8], t2[6];
   bool ok2 = false;
-  if (ok && !t1_odd && odd_k2) ok2 = hs_step(r2, t2, r0, r1, t0, t1);
+  if (hs_uni<UNI>(ok && !t1_odd && odd_k2)) ok2 = hs_step<UNI>(r2, t2, r0, r1, t0, t1);
   const int br0 = hs_bitlen8(r0) - e, bt0 = hs_bitlen6s(t0, n0);
   const int c0 = br0 > bt0 ? br0 : bt0;
   int c2 = 1 << 20;
@@ -392,7 +407,7 @@ CMTV_HD void half_scalars(HalfScalars& h, const uint32_t k[8], bool force_wide =
   // denormalise r (e <= 129 whenever the pair is used)
   int ew = h.wide ? 0 : e;
 #pragma unroll 1
-  while (ew >= 32) {
+  while (hs_uni<UNI>(ew >= 32)) {
 #pragma unroll
     for (int i = 0; i < 7; i++) rs[i] = rs[i + 1];
     rs[7] = 0;

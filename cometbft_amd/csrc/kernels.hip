@@ -580,7 +580,7 @@ __global__ __launch_bounds__(192, 1) void k_verify_row2_split(
       sha512_prefixed<16>(h, w, mp, ml);
       sc_reduce512(k, h);
       CMTV_STAMP(5);
-      q_prepare_scalars(p, k, ts, force_wide != 0, MODE != MODE_ZIP215);
+      q_prepare_scalars<true>(p, k, ts, force_wide != 0, MODE != MODE_ZIP215);
       p.flags |= s_ok ? 4u : 0u;
     }
     if (t == 0) sig_prep_store(prep, p);
@@ -686,7 +686,7 @@ __global__ __launch_bounds__(256, 1) void k_verify_row4_split(
     uint32_t ml;
     helper_message(sb, i, msg, off, sbm, mp, ml);
     SigPrep p;
-    q_prepare<MODE>(p, pkp, sgp, mp, ml, force_wide != 0);
+    q_prepare<MODE, true>(p, pkp, sgp, mp, ml, force_wide != 0);  // one signature on every lane
     if (t == 0) sig_prep_store(prep, p);
     CMTV_STAMP(1);
     __syncthreads();  // 1: the scalars

@@ -357,10 +357,12 @@ struct SigPrep {
 };
 constexpr int SIG_PREP_WORDS = 25;
 
+// UNI: every lane of the wave holds the same signature (halfscalar.h hs_uni)
+template <bool UNI = false>
 CMTV_HD void q_prepare_scalars(SigPrep& p, const uint32_t k[8], const uint32_t ts[8], bool force_wide,
                                bool odd_k2 = true) {
   HalfScalars hs;
-  half_scalars(hs, k, force_wide, odd_k2);
+  half_scalars<true, UNI>(hs, k, force_wide, odd_k2);
   hs_bscalar(p.u, hs.k2, hs.k2_neg, ts);
 #pragma unroll
   for (int i = 0; i < 8; i++) {
@@ -372,7 +374,7 @@ CMTV_HD void q_prepare_scalars(SigPrep& p, const uint32_t k[8], const uint32_t t
 
 // s check, k = SHA-512(R || A || M) mod L, then q_prepare_scalars (k2 odd
 // for the cofactorless check, MODE_GO_STDLIB; any parity for MODE_ZIP215)
-template <uint32_t MODE>
+template <uint32_t MODE, bool UNI = false>
 CMTV_HD void q_prepare(SigPrep& p, const uint32_t* pk_ptr, const uint32_t* sig_ptr, const uint8_t* msg,
                        uint32_t mlen, bool force_wide) {
   uint32_t w[16];
@@ -393,7 +395,7 @@ CMTV_HD void q_prepare(SigPrep& p, const uint32_t* pk_ptr, const uint32_t* sig_p
     sha512_prefixed<16>(h, w, msg, mlen);
     sc_reduce512(k, h);
   }
-  q_prepare_scalars(p, k, ts, force_wide, MODE != MODE_ZIP215);
+  q_prepare_scalars<UNI>(p, k, ts, force_wide, MODE != MODE_ZIP215);
   p.flags |= s_ok ? 4u : 0u;
 }
 

@@ -15,7 +15,7 @@
 
 using namespace cmtv;
 
-constexpr int kSteps = 5;
+constexpr int kSteps = 6;
 
 // VGPR = false: uniform inputs (the compiler runs the steps on the scalar
 // unit); true: the inputs XORed with a per-lane zero it cannot see through
@@ -47,11 +47,14 @@ __global__ __launch_bounds__(64, 1) void k_prep(const uint32_t* __restrict__ in,
   HalfScalars hz;
   half_scalars(hz, k, false, false);
   st[5] = __builtin_amdgcn_s_memtime();
+  HalfScalars hu;
+  half_scalars<true, true>(hu, k, false, true);  // the row helpers' form: uniform branches
+  st[6] = __builtin_amdgcn_s_memtime();
   if (threadIdx.x == 0)
     for (int i = 0; i < kSteps; i++) cyc[b * kSteps + i] = st[i + 1] - st[i];
   uint32_t x = 0;
 #pragma unroll
-  for (int i = 0; i < 8; i++) x ^= u[i] ^ hs.k1[i] ^ hz.k1[i] ^ hz.k2[i];
+  for (int i = 0; i < 8; i++) x ^= u[i] ^ hs.k1[i] ^ hz.k1[i] ^ hz.k2[i] ^ hu.k1[i];
   out[b * 64 + threadIdx.x] = x ^ (uint32_t)hs.windows;
 }
 
@@ -90,7 +93,7 @@ int main() {
     for (int b = 0; b < blocks; b++)
       for (int i = 0; i < kSteps; i++) sum[i] += (double)c[b * kSteps + i];
     const char* nm[kSteps] = {"sha512 (64 + 116 bytes)", "sc_reduce512", "half_scalars (odd k2)", "hs_bscalar",
-                              "half_scalars (any parity)"};
+                              "half_scalars (any parity)", "half_scalars (odd, uniform)"};
     for (int i = 0; i < kSteps; i++)
       printf("%-6s %-28s %10.1f cycles (s_memtime, %d waves, 1 per CU)\n", vg ? "vector" : "scalar", nm[i],
              sum[i] / blocks, blocks);

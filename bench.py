@@ -790,12 +790,18 @@ def latency_150(ctx, mode, iters):
     return res
 
 
+# The PMC summaries of THIS round's tree (tools/gpu_prof_r04.sh: rocprofv3
+# --pmc passes over the quick form of this bench command)
+PMC_SQ = "r04_pmc_sq.json"
+PMC_TRAFFIC = "r04_traffic.json"
+
+
 def load_valu_busy(n=10_000, kernel="k_verify_quad_split<0u>"):
     """VALUBusy (SQ_ACTIVE_INST_VALU-based, chip-wide) of the bench's verify
     kernel at the step's size, from the committed PMC summary of the bench
-    command (profiles/r02_pmc_sq.json, tools/pmc_summary.py)."""
+    command (profiles/PMC_SQ, tools/pmc_summary.py)."""
     try:
-        with open(os.path.join(ROOT, "profiles", "r02_pmc_sq.json")) as f:
+        with open(os.path.join(ROOT, "profiles", PMC_SQ)) as f:
             d = json.load(f)
     except (OSError, ValueError):
         return None
@@ -803,20 +809,22 @@ def load_valu_busy(n=10_000, kernel="k_verify_quad_split<0u>"):
     for k, v in d.items():
         if kernel in k and f"grid={waves} waves" in k and "valu_busy_pct" in v:
             return {"valu_busy_pct": v["valu_busy_pct"], "valu_insts_per_wave": v.get("valu_insts_per_wave"),
-                    "source": "profiles/r02_pmc_sq.json", "kernel": k}
+                    "wave_cycles_per_wave": v.get("wave_cycles_per_wave"),
+                    "source": f"profiles/{PMC_SQ}", "kernel": k}
     return None
 
 
-def load_traffic():
-    for name in ("r02_traffic.json", "r01_traffic.json"):
-        p = os.path.join(ROOT, "profiles", name)
-        try:
-            with open(p) as f:
-                d = json.load(f)
-            return d.get("bytes_per_launch"), name
-        except (OSError, ValueError):
-            continue
-    return None, None
+def load_traffic(mode_key="go"):
+    """Raw FETCH_SIZE + WRITE_SIZE bytes per launch of the step's kernel
+    (profiles/PMC_TRAFFIC; 'go' / 'zip215' instantiation)."""
+    p = os.path.join(ROOT, "profiles", PMC_TRAFFIC)
+    try:
+        with open(p) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    d = d.get(mode_key, d)
+    return d.get("bytes_per_launch"), f"profiles/{PMC_TRAFFIC}"
 
 
 def process_per_gpu_main(args):
@@ -920,7 +928,10 @@ def main():
     total = n_dev * args.n * args.steps
     value = total / elapsed
     achieved = args.n * MACS_PER_VERIFY / (kernel_ms * 1e-3) / 1e12
-    traffic, tfile = load_traffic()
+    traffic, tfile = load_traffic("go" if mode == 0 else "zip215")
+    # algorithmic HBM bytes per launch: key, signature, offset and message in,
+    # one verdict bit out
+    alg_bytes = round(args.n * (32 + 64 + 4 + D.msg_bytes_mean) + args.n / 8)
     line = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -946,7 +957,9 @@ def main():
                    "devices": run_head},
         "roofline": {"bound": "valu_int", "achieved": round(achieved, 3), "peak": INT_MAC_PEAK_T,
                      "unit": "TMAC/s", "frac": round(achieved / INT_MAC_PEAK_T, 4),
-                     "traffic": traffic, "traffic_source": tfile, "kernel_ms": round(kernel_ms, 4),
+                     "traffic": traffic, "traffic_source": tfile, "algorithmic_bytes": alg_bytes,
+                     "traffic_over_algorithmic": round(traffic / alg_bytes, 2) if traffic else None,
+                     "kernel_ms": round(kernel_ms, 4),
                      "valu_utilisation": load_valu_busy(args.n),
                      "work": f"{MACS_PER_VERIFY} int32 MACs/verify x {args.n} verifies per launch",
                      "timing": "libcmtverify HIP events on the launch stream, mean over the timed launches"},

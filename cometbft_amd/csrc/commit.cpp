@@ -171,6 +171,14 @@ struct SigBatch {
   bool templated = false;
   std::vector<uint8_t> pk, sg, msgs, len_ok;
   std::vector<uint64_t> off{0};
+  // borrowed (templated, one commit whose plan is every signature in order,
+  // keys and signatures packed at 32 / 64 bytes): the caller's arrays are the
+  // batch, nothing is copied per signature (job_prepare_identity)
+  const uint8_t* pk_src = nullptr;
+  const uint8_t* sg_src = nullptr;
+  const int64_t* sec_src = nullptr;
+  const int32_t* nanos_src = nullptr;
+  bool all_len_ok = false;  // every signature is 64 bytes (len_ok unused)
   std::string sb;
   // templated
   std::vector<cmtv::SbTemplate> tmpls;
@@ -187,6 +195,26 @@ struct SigBatch {
   bool one_vs = true;
 
   size_t size() const { return off.size() - 1; }
+  const uint8_t* pk_data() const { return pk_src ? pk_src : pk.data(); }
+  const uint8_t* sg_data() const { return sg_src ? sg_src : sg.data(); }
+  const int64_t* sec_data() const { return sec_src ? sec_src : tsec.data(); }
+  const int32_t* nanos_data() const { return nanos_src ? nanos_src : tnanos.data(); }
+
+  // room for m more signatures (no reallocation inside add)
+  void reserve_more(size_t m) {
+    const size_t n = size() + m;
+    pk.reserve(32 * n);
+    sg.reserve(64 * n);
+    len_ok.reserve(n);
+    off.reserve(n + 1);
+    kidx.reserve(n);
+    if (templated) {
+      tidx.reserve(n);
+      tflag.reserve(n);
+      tsec.reserve(n);
+      tnanos.reserve(n);
+    }
+  }
 
   void ensure_template(const char* chain_id, size_t chain_id_len, const cmtv_commit* c) {
     if (cur == c && !tmpls.empty()) return;
@@ -221,10 +249,15 @@ struct SigBatch {
       last_vs = vals;
     }
     kidx.push_back(vi);
-    pk.insert(pk.end(), key, key + 32);
+    const size_t ok = pk.size();
+    pk.resize(ok + 32);
+    std::memcpy(&pk[ok], key, 32);
     const size_t o = sg.size();
-    sg.resize(o + 64, 0);
-    if (sig_len == 64) std::memcpy(&sg[o], sig, 64);
+    sg.resize(o + 64);
+    if (sig_len == 64)
+      std::memcpy(&sg[o], sig, 64);
+    else
+      std::memset(&sg[o], 0, 64);
     len_ok.push_back(sig_len == 64);
     // Commit.GetVote(idx) (types/block.go:784): CommitSig.BlockID(commit.BlockID)
     const bool for_block = c->flags[idx] == kFlagCommit;
@@ -296,6 +329,46 @@ int job_check_args(uint32_t kind, const char* chain_id, size_t chain_id_len, con
   return CMTV_OK;
 }
 
+// The common VerifyCommit case (validator_set.go:685-707): the plan is every
+// signature in index order, from validators whose keys are packed at 32 bytes,
+// and every signature is 64 bytes. Then the caller's key, signature and
+// timestamp arrays are the batch itself (SigBatch's borrowed pointers): only
+// the per-signature flag and message offset are written here, and the batch
+// goes to the pinned staging in one copy. Applies to the first job of a
+// templated batch; false leaves B untouched.
+bool job_prepare_identity(CommitJob& J, SigBatch& B, bool prefetch) {
+  const cmtv_valset* vals = J.vals;
+  const cmtv_commit* c = J.commit;
+  const size_t m = J.plan_idx.size();
+  if (J.kind == CMTV_VERIFY_COMMIT_LIGHT_TRUSTING) return false;  // its plan maps through addresses
+  if (!B.templated || prefetch || B.size() != 0 || m == 0 || m != c->n_sigs || m != vals->n_vals) return false;
+  if (J.plan_idx.back() != m - 1) return false;  // the plan is increasing: last == m - 1 <=> identity
+  for (size_t i = 0; i <= m; i++)
+    if (vals->pk_off[i] != 32 * i || c->sig_off[i] != 64 * i) return false;
+  B.pk_src = vals->pubkeys;
+  B.sg_src = c->sigs;
+  B.sec_src = c->ts_seconds;
+  B.nanos_src = c->ts_nanos;
+  B.all_len_ok = true;
+  B.vs = B.last_vs = vals;
+  B.one_vs = true;
+  B.ensure_template(J.chain_id, J.chain_id_len, c);
+  const cmtv::SbTemplate& t = B.tmpls.back();
+  B.tflag.resize(m);
+  B.tidx.assign(m, (uint32_t)B.tmpls.size() - 1);
+  B.off.resize(m + 1);
+  B.kidx.resize(m);
+  uint64_t o = 0;
+  for (size_t i = 0; i < m; i++) {
+    const bool for_block = c->flags[i] == kFlagCommit;
+    B.tflag[i] = for_block ? 1 : 0;
+    B.kidx[i] = (uint32_t)i;
+    o += cmtv::sb_msg_len(t, for_block, c->ts_seconds[i], c->ts_nanos[i]);
+    B.off[i + 1] = o;
+  }
+  return true;
+}
+
 // Preamble checks and the threshold (validator_set.go:670-684, 779-790), then
 // the plan: which signatures the reference loop can reach, assuming every
 // verdict is valid (the loop stops at its first error, so nothing beyond the
@@ -364,6 +437,8 @@ void job_prepare(CommitJob& J, SigBatch& B, bool prefetch) {
 
   int64_t tally = 0;
   std::unordered_map<uint32_t, uint32_t> seen;
+  J.plan_idx.reserve(nsig);
+  J.plan_val.reserve(nsig);
   for (uint32_t idx = 0; idx < nsig; idx++) {
     const uint8_t flag = commit->flags[idx];
     uint32_t vi = idx;
@@ -390,6 +465,8 @@ void job_prepare(CommitJob& J, SigBatch& B, bool prefetch) {
   }
 
   J.first = B.size();
+  if (job_prepare_identity(J, B, prefetch)) return;
+  B.reserve_more(J.plan_idx.size());
   for (size_t j = 0; j < J.plan_idx.size(); j++) {
     const uint32_t idx = J.plan_idx[j], vi = J.plan_val[j];
     const uint32_t s0 = commit->sig_off[idx], s1 = commit->sig_off[idx + 1];
@@ -442,18 +519,19 @@ int batch_verify(cmtv_ctx* ctx, SigBatch& B, uint32_t mode, std::vector<uint8_t>
     for (size_t i = a; i <= b; i++) off32[i - a] = (uint32_t)(B.off[i] - B.off[a]);
     int rc;
     if (B.templated)
-      rc = cmtv::verify_templated_locked(ctx, b - a, ks ? nullptr : B.pk.data() + 32 * a, B.sg.data() + 64 * a,
+      rc = cmtv::verify_templated_locked(ctx, b - a, ks ? nullptr : B.pk_data() + 32 * a, B.sg_data() + 64 * a,
                                          off32.data(), B.tmpls.data(), B.tmpls.size(), B.blob.data(), B.blob.size(),
-                                         B.tidx.data() + a, B.tflag.data() + a, B.tsec.data() + a,
-                                         B.tnanos.data() + a, mode, valid.data() + a, ks, B.kidx.data() + a);
+                                         B.tidx.data() + a, B.tflag.data() + a, B.sec_data() + a,
+                                         B.nanos_data() + a, mode, valid.data() + a, ks, B.kidx.data() + a);
     else
       rc = cmtv::verify_host_locked(ctx, b - a, B.pk.data() + 32 * a, B.sg.data() + 64 * a,
                                     B.msgs.data() + B.off[a], off32.data(), mode, valid.data() + a, nullptr);
     if (rc != CMTV_OK) return rc;
     a = b;
   }
-  for (size_t j = 0; j < m; j++)
-    if (!B.len_ok[j]) valid[j] = 0;  // crypto/ed25519/ed25519.go:150
+  if (!B.all_len_ok)
+    for (size_t j = 0; j < m; j++)
+      if (!B.len_ok[j]) valid[j] = 0;  // crypto/ed25519/ed25519.go:150
   return CMTV_OK;
 }
 
@@ -632,14 +710,19 @@ int cmtv_verify_commit(cmtv_ctx* ctx, uint32_t kind, uint32_t mode, const char* 
   std::unique_lock<std::mutex> lk;
   rc = cmtv::ctx_lock(ctx, lk);
   if (rc != CMTV_OK) return rc;
+  const uint64_t t0 = cmtv::phase_now(ctx);
   SigBatch B;
   const bool cache = cmtv::cache_enabled(ctx);
   B.templated = !cache && templated_enabled();
   job_prepare(J, B, cache);
+  cmtv::phase_add(ctx, cmtv::kPhPrepare, t0);
   std::vector<uint8_t> valid;
   rc = batch_verify(ctx, B, mode, valid);
   if (rc != CMTV_OK) return rc;
-  return job_replay(J, valid);
+  const uint64_t t1 = cmtv::phase_now(ctx);
+  rc = job_replay(J, valid);
+  cmtv::phase_add(ctx, cmtv::kPhReplay, t1);
+  return rc;
 }
 
 int cmtv_verify_commits(cmtv_ctx* ctx, uint32_t kind, uint32_t mode, const char* chain_id, size_t chain_id_len,
@@ -665,14 +748,18 @@ int cmtv_verify_commits(cmtv_ctx* ctx, uint32_t kind, uint32_t mode, const char*
   std::unique_lock<std::mutex> lk;
   int rc = cmtv::ctx_lock(ctx, lk);
   if (rc != CMTV_OK) return rc;
+  const uint64_t t0 = cmtv::phase_now(ctx);
   SigBatch B;
   const bool prefetch = cmtv::cache_enabled(ctx);
   B.templated = !prefetch && templated_enabled();
   for (auto& J : jobs) job_prepare(J, B, prefetch);
+  cmtv::phase_add(ctx, cmtv::kPhPrepare, t0);
   std::vector<uint8_t> valid;
   rc = batch_verify(ctx, B, mode, valid);
   if (rc != CMTV_OK) return rc;
+  const uint64_t t1 = cmtv::phase_now(ctx);
   for (size_t c = 0; c < n; c++) rcs[c] = job_replay(jobs[c], valid);
+  cmtv::phase_add(ctx, cmtv::kPhReplay, t1);
   return CMTV_OK;
 }
 

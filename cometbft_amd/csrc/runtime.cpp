@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -243,22 +244,35 @@ struct Rccl {
   ncclResult_t (*GroupEnd)() = nullptr;
 };
 
-const Rccl& rccl() {
-  static Rccl r = [] {
-    Rccl x;
-    void* h = nullptr;
+Rccl load_rccl(const char* path) {
+  Rccl x;
+  void* h = nullptr;
+  if (path) {
+    h = dlopen(path, RTLD_NOW | RTLD_LOCAL);
+  } else {
     for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
       if ((h = dlopen(name, RTLD_NOW | RTLD_LOCAL)) != nullptr) break;
-    if (!h) return x;
-    x.CommInitAll = reinterpret_cast<decltype(x.CommInitAll)>(dlsym(h, "ncclCommInitAll"));
-    x.CommDestroy = reinterpret_cast<decltype(x.CommDestroy)>(dlsym(h, "ncclCommDestroy"));
-    x.AllGather = reinterpret_cast<decltype(x.AllGather)>(dlsym(h, "ncclAllGather"));
-    x.GroupStart = reinterpret_cast<decltype(x.GroupStart)>(dlsym(h, "ncclGroupStart"));
-    x.GroupEnd = reinterpret_cast<decltype(x.GroupEnd)>(dlsym(h, "ncclGroupEnd"));
-    x.ok = x.CommInitAll && x.CommDestroy && x.AllGather && x.GroupStart && x.GroupEnd;
-    return x;
-  }();
-  return r;
+  }
+  if (!h) return x;
+  x.CommInitAll = reinterpret_cast<decltype(x.CommInitAll)>(dlsym(h, "ncclCommInitAll"));
+  x.CommDestroy = reinterpret_cast<decltype(x.CommDestroy)>(dlsym(h, "ncclCommDestroy"));
+  x.AllGather = reinterpret_cast<decltype(x.AllGather)>(dlsym(h, "ncclAllGather"));
+  x.GroupStart = reinterpret_cast<decltype(x.GroupStart)>(dlsym(h, "ncclGroupStart"));
+  x.GroupEnd = reinterpret_cast<decltype(x.GroupEnd)>(dlsym(h, "ncclGroupEnd"));
+  x.ok = x.CommInitAll && x.CommDestroy && x.AllGather && x.GroupStart && x.GroupEnd;
+  return x;
+}
+
+// The RCCL entry points for a context: the system librccl, or the library
+// CMTV_RCCL_LIB names (read at open; tests/host/rccl_stub.cpp rehearses the
+// multi-rank code on one GPU). Each library is resolved once per process.
+const Rccl& rccl(const std::string& path = std::string()) {
+  static std::mutex mu;
+  static std::unordered_map<std::string, Rccl> libs;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = libs.find(path);
+  if (it == libs.end()) it = libs.emplace(path, load_rccl(path.empty() ? nullptr : path.c_str())).first;
+  return it->second;
 }
 
 // Kernel timing: HIP event pairs recorded around each verification on its
@@ -270,7 +284,13 @@ struct Timing {
   };
   std::vector<Pair> free_;
   std::deque<Pair> pending;
+  // pairs in flight beyond this are not timed (begin hands out a null pair)
+  static constexpr size_t kMaxPending = 1u << 16;
   hipError_t begin(Pair& p, hipStream_t s) {
+    if (pending.size() >= kMaxPending) {
+      p = Pair();
+      return hipSuccess;
+    }
     if (free_.empty()) {
       Pair q;
       hipError_t e = hipEventCreate(&q.a);
@@ -285,6 +305,7 @@ struct Timing {
     return e;
   }
   hipError_t end(const Pair& p, hipStream_t s) {
+    if (!p.a) return hipSuccess;  // untimed (kMaxPending)
     hipError_t e = hipEventRecord(p.b, s);
     if (e != hipSuccess) {
       free_.push_back(p);
@@ -293,13 +314,17 @@ struct Timing {
     pending.push_back(p);
     return hipSuccess;
   }
-  void abandon(const Pair& p) { free_.push_back(p); }
+  void abandon(const Pair& p) {
+    if (p.a) free_.push_back(p);
+  }
   // completed pairs -> stats (context-wide and this device's); blocking
   // waits for all of them
   void harvest(cmtv_stats& st, double& dev_ms, bool blocking) {
     while (!pending.empty()) {
       Pair p = pending.front();
-      if (blocking || pending.size() > 64) {
+      // never blocks unless asked (cmtv_stats_get): a device-resident call
+      // must not wait for launches parked on other streams
+      if (blocking) {
         if (hipEventSynchronize(p.b) != hipSuccess) break;
       } else if (hipEventQuery(p.b) != hipSuccess) {
         break;
@@ -356,6 +381,11 @@ struct CmtvDev {
   // the row kernel's bitmap ring (kernels.h kRowSlots x kRowSlotWords)
   uint32_t* d_rowslots = nullptr;
   uint32_t row_seq = 0;
+  // per ring slot: an event recorded after the device-resident launch that
+  // last took it (row_pending), waited on before the slot is handed out again
+  // (row_slot_acquire), so a slot is never shared by two launches in flight
+  hipEvent_t row_ev[cmtv::kRowSlots] = {};
+  bool row_pending[cmtv::kRowSlots] = {};
   // a device that returned a HIP error is taken out of the context's
   // rotation: host batches are re-planned over the others (runtime.cpp
   // run_host_batch); CMTV_FAULT_DEV=g makes device g's first launch fail
@@ -394,8 +424,10 @@ struct cmtv_ctx {
   // CMTV_FAULT_AT: 1-based index of the verification launch that fails
   uint64_t fault_at = 0, launch_seq = 0;
   bool fault_pending = false;  // the last failure was CMTV_FAULT_AT's
-  // RCCL options read at open (CMTV_FORCE_RCCL, CMTV_NO_RCCL)
+  // RCCL options read at open (CMTV_FORCE_RCCL, CMTV_NO_RCCL) and the
+  // library to load (CMTV_RCCL_LIB; empty: the system librccl)
   bool force_rccl = false, no_rccl = false;
+  std::string rccl_lib;
   // CMTV_FORCE_WIDE: quad kernels take the 64-window half-scalar fallback
   bool force_wide = false;
   // templated sign-bytes in the split kernels' helper waves (CMTV_NO_SB_FUSE=1: off)
@@ -416,6 +448,20 @@ struct cmtv_ctx {
   std::vector<size_t> live;
   // fused small host batches read their inputs from mapped host memory (CMTV_NO_ZC_IN=1: off)
   bool zc_in = true;
+  // single-device host batches up to this size take the mapped-memory path (CMTV_ZC_MAX)
+  size_t zc_max = kZeroCopyMax;
+  // set while a host-buffer call runs (run_host_batch): its launches finish
+  // before the call returns, so their row-ring slots need no fence event
+  bool host_sync = false;
+  // CMTV_ROW_FENCE=0: no row-ring fence (only for the test that shows the race)
+  bool row_fence = true;
+  // CMTV_HOST_PHASES=1: host phase clock (runtime_internal.h HostPhase)
+  bool phases_on = false;
+  uint64_t phase_ns[cmtv::kPhCount] = {};
+  uint64_t phase_calls = 0;
+  // CMTV_FAULT_SYNC_DEV=g: device g's stream synchronisation in a host batch
+  // reports a HIP error (a fault found after the launch; re-shard test knob)
+  long fault_sync_dev = -1;
 };
 
 struct cmtv_keyset {
@@ -439,6 +485,19 @@ static int hip_fail(hipError_t e) {
 }
 
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+uint64_t phase_now(const cmtv_ctx* ctx) {
+  if (!ctx->phases_on) return 0;
+  return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+void phase_add(cmtv_ctx* ctx, int phase, uint64_t t0) {
+  if (!ctx->phases_on || !t0) return;
+  ctx->phase_ns[phase] += phase_now(ctx) - t0;
+  if (phase == kPhPrepare) ctx->phase_calls++;
+}
 
 static void harvest(cmtv_ctx* ctx, bool blocking) {
   for (auto& d : ctx->devs) {
@@ -477,6 +536,33 @@ static hipError_t acquire_scratch(CmtvDev& D, size_t bytes, hipStream_t s) {
 static hipError_t release_scratch(CmtvDev& D, hipStream_t s) {
   const hipError_t e = hipEventRecord(D.atab_done, s);
   if (e == hipSuccess) D.atab_used = true;
+  return e;
+}
+
+// The row kernels' verdict-byte ring (kernels.h kRowSlots): the next slot for
+// a launch on stream s. The kernel's last wave packs the bitmap from the slot
+// and resets its counter, so two launches in flight on one slot would count
+// each other's waves. A slot whose last user was a device-resident launch
+// (enqueued on a caller's stream, not waited for before its call returned) is
+// fenced: s waits for that launch's event. Host-buffer calls finish their
+// launches before they return (ctx->host_sync) and record nothing.
+static hipError_t row_slot_acquire(cmtv_ctx* ctx, CmtvDev& D, hipStream_t s, uint32_t*& slot, uint32_t& k) {
+  k = D.row_seq++ % kRowSlots;
+  slot = D.d_rowslots + (size_t)k * kRowSlotWords;
+  if (!D.row_pending[k] || !ctx->row_fence) return hipSuccess;
+  hipError_t e = hipEventQuery(D.row_ev[k]);
+  if (e == hipErrorNotReady) e = hipStreamWaitEvent(s, D.row_ev[k], 0);
+  if (e != hipSuccess) return e;
+  D.row_pending[k] = false;
+  return hipSuccess;
+}
+
+static hipError_t row_slot_release(cmtv_ctx* ctx, CmtvDev& D, hipStream_t s, uint32_t k) {
+  if (ctx->host_sync || !ctx->row_fence) return hipSuccess;
+  hipError_t e = hipSuccess;
+  if (!D.row_ev[k]) e = hipEventCreateWithFlags(&D.row_ev[k], hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventRecord(D.row_ev[k], s);
+  if (e == hipSuccess) D.row_pending[k] = true;
   return e;
 }
 
@@ -532,6 +618,10 @@ static int enqueue_verify(cmtv_ctx* ctx, CmtvDev& D, size_t n, const uint8_t* d_
     if ((e = acquire_scratch(D, lanes_padded * kAtabWordsPerLane * sizeof(uint32_t), s)) != hipSuccess)
       return hip_fail(e);
   }
+  // a row launch is one chunk (n <= kRowMaxCap)
+  uint32_t* slot = nullptr;
+  uint32_t slot_k = 0;
+  if (row && (e = row_slot_acquire(ctx, D, s, slot, slot_k)) != hipSuccess) return hip_fail(e);
   D.timing.harvest(ctx->stats, D.device_ms, false);
   Timing::Pair tp;
   if ((e = D.timing.begin(tp, s)) != hipSuccess) return hip_fail(e);
@@ -545,8 +635,8 @@ static int enqueue_verify(cmtv_ctx* ctx, CmtvDev& D, size_t n, const uint8_t* d_
     else
       e = launch_verify(mode, cn, d_pk + 32 * c, d_sig + 64 * c, d_msg, d_off + c, D.d_btab,
                         static_cast<uint32_t*>(D.d_atab.p), d_valid ? d_valid + c : nullptr,
-                        d_bitmap ? d_bitmap + c / 64 : nullptr, kflags, s, sb,
-                        row ? D.d_rowslots + (size_t)(D.row_seq++ % kRowSlots) * kRowSlotWords : nullptr);
+                        d_bitmap ? d_bitmap + c / 64 : nullptr, kflags, s, sb, slot);
+    if (e == hipSuccess && row) e = row_slot_release(ctx, D, s, slot_k);
     if (e != hipSuccess) {
       D.timing.abandon(tp);
       return hip_fail(e);
@@ -614,6 +704,12 @@ static int enqueue_verify_keyed(cmtv_ctx* ctx, CmtvDev& D, const cmtv_keyset::Pe
     if ((e = acquire_scratch(D, lanes * kb0 * kKeyedBatchScratchWordsPerSig * sizeof(uint32_t), s)) != hipSuccess)
       return hip_fail(e);
   }
+  // the keyed row kernel up to CMTV_KEYED_ROW_MAX (below the keyed quad
+  // knob): one chunk, one slot of the bitmap ring
+  const bool krow = quad && n <= ctx->keyed_row_max && n <= kRowMaxCap;
+  uint32_t* slot = nullptr;
+  uint32_t slot_k = 0;
+  if (krow && (e = row_slot_acquire(ctx, D, s, slot, slot_k)) != hipSuccess) return hip_fail(e);
   D.timing.harvest(ctx->stats, D.device_ms, false);
   Timing::Pair tp;
   if ((e = D.timing.begin(tp, s)) != hipSuccess) return hip_fail(e);
@@ -621,14 +717,12 @@ static int enqueue_verify_keyed(cmtv_ctx* ctx, CmtvDev& D, const cmtv_keyset::Pe
     const uint32_t cn = (uint32_t)std::min<size_t>(chunk, n - c);
     // a chunk never needs more scratch than the first (kb and lanes shrink together)
     const uint32_t kb = kb0 > 1 ? kb_for(cn) : 1;
-    // the keyed row kernel up to CMTV_KEYED_ROW_MAX (below the keyed quad knob)
-    const bool krow = quad && n <= ctx->keyed_row_max && n <= kRowMaxCap;
     e = launch_verify_keyed(mode, cn, (uint32_t)n_keys, d_idx + c, d_sig + 64 * c, d_msg, d_off + c, K.d_pk, K.d_ok,
                             K.d_tab, D.d_bcomb, d_valid ? d_valid + c : nullptr,
                             d_bitmap ? d_bitmap + c / 64 : nullptr, quad, n <= ctx->quad_split_max,
                             ctx->keyed_wait, D.d_diag, kb, static_cast<uint32_t*>(D.d_atab.p),
-                            quad ? nullptr : K.d_wide, D.d_btab, ctx->wide_dma, s,
-                            krow ? D.d_rowslots + (size_t)(D.row_seq++ % kRowSlots) * kRowSlotWords : nullptr);
+                            quad ? nullptr : K.d_wide, D.d_btab, ctx->wide_dma, s, slot);
+    if (e == hipSuccess && krow) e = row_slot_release(ctx, D, s, slot_k);
     if (e != hipSuccess) {
       D.timing.abandon(tp);
       return hip_fail(e);
@@ -660,7 +754,7 @@ static int gather_bitmaps(cmtv_ctx* ctx, const size_t* dev, size_t G, size_t W, 
   if (G <= 1 && !ctx->rccl) return CMTV_OK;
   ctx->stats.gathers++;
   if (ctx->rccl) {
-    const Rccl& R = rccl();
+    const Rccl& R = rccl(ctx->rccl_lib);
     if (R.GroupStart() != 0) return CMTV_ERCCL;
     int bad = 0;
     for (size_t g = 0; g < G; g++) {
@@ -752,6 +846,7 @@ static int enqueue_shard(cmtv_ctx* ctx, size_t g, const HostBatch& B, size_t a, 
   const size_t o_valid = 0, out_bytes = align_up(std::max<size_t>(m, 1), 256);
   o_valid_out = o_valid;
   hipError_t e;
+  const uint64_t t_stage = phase_now(ctx);
   (void)hipSetDevice(D.ordinal);
   // message lengths first: they decide the fused / zero-copy forms
   const uint32_t base = B.msg_off[a];
@@ -787,6 +882,8 @@ static int enqueue_shard(cmtv_ctx* ctx, size_t g, const HostBatch& B, size_t a, 
     if (mb) std::memcpy(hin + o_msg, B.msg + base, mb);
     std::memset(hin + o_msg + mb, 0, 16);
   }
+  phase_add(ctx, kPhStage, t_stage);
+  const uint64_t t_launch = phase_now(ctx);
   uint8_t* din = static_cast<uint8_t*>(D.d_in.p);
   auto* dout = static_cast<uint8_t*>(D.d_out.p);
   if (zc) {
@@ -814,12 +911,16 @@ static int enqueue_shard(cmtv_ctx* ctx, size_t g, const HostBatch& B, size_t a, 
       return hip_fail(e);
   }
   uint8_t* dv = want_valid ? dout + o_valid : nullptr;
+  int rc;
   if (keyed)
-    return enqueue_verify_keyed(ctx, D, B.ks->dev[g], B.ks->n, m, reinterpret_cast<uint32_t*>(din + o_key),
-                                din + o_sig, din + o_msg, reinterpret_cast<uint32_t*>(din + o_off), B.mode, dv,
-                                bitmap, D.stream);
-  return enqueue_verify(ctx, D, m, din + o_key, din + o_sig, din + o_msg, reinterpret_cast<uint32_t*>(din + o_off),
+    rc = enqueue_verify_keyed(ctx, D, B.ks->dev[g], B.ks->n, m, reinterpret_cast<uint32_t*>(din + o_key),
+                              din + o_sig, din + o_msg, reinterpret_cast<uint32_t*>(din + o_off), B.mode, dv, bitmap,
+                              D.stream);
+  else
+    rc = enqueue_verify(ctx, D, m, din + o_key, din + o_sig, din + o_msg, reinterpret_cast<uint32_t*>(din + o_off),
                         B.mode, dv, bitmap, D.stream, fuse ? &sb : nullptr);
+  phase_add(ctx, kPhLaunch, t_launch);
+  return rc;
 }
 
 // Verdicts of a host batch, sharded over the context's live devices. Caller
@@ -834,7 +935,7 @@ static int run_host_batch_(cmtv_ctx* ctx, const HostBatch& B, uint8_t* out_valid
   const size_t words = (n + 63) / 64;
   hipError_t e;
   const size_t d0 = live[0];
-  if (P.G == 1 && n <= kZeroCopyMax) {
+  if (P.G == 1 && n <= ctx->zc_max) {
     // one device, a small batch: the verify kernel writes the bitmap into
     // mapped host memory, so the call is H2D + (sign-bytes) + verify + sync
     CmtvDev& D = ctx->devs[d0];
@@ -846,7 +947,14 @@ static int run_host_batch_(cmtv_ctx* ctx, const HostBatch& B, uint8_t* out_valid
     size_t o_valid = 0;
     const int rc = enqueue_shard(ctx, d0, B, 0, n, false, static_cast<uint64_t*>(dzc), o_valid, true);
     if (rc != CMTV_OK) return rc;
+    const uint64_t t_wait = phase_now(ctx);
     if ((e = hipStreamSynchronize(D.stream)) != hipSuccess) return hip_fail(e);
+    phase_add(ctx, kPhWait, t_wait);
+    const uint64_t t_post = phase_now(ctx);
+    if ((long)d0 == ctx->fault_sync_dev) {  // CMTV_FAULT_SYNC_DEV (see below)
+      ctx->stats.faults_injected++;
+      return CMTV_EHIP;
+    }
     *bad_dev = -1;
     harvest(ctx, false);
     (void)hipSetDevice(D.ordinal);
@@ -859,6 +967,7 @@ static int run_host_batch_(cmtv_ctx* ctx, const HostBatch& B, uint8_t* out_valid
     if (out_bitmap) std::memcpy(out_bitmap, bm, 8 * words);
     if (out_valid)
       for (size_t i = 0; i < n; i++) out_valid[i] = (uint8_t)((bm[i >> 6] >> (i & 63)) & 1);
+    phase_add(ctx, kPhPost, t_post);
     return CMTV_OK;
   }
   // devices in the gather: the shards' devices, or with RCCL every rank of
@@ -906,12 +1015,20 @@ static int run_host_batch_(cmtv_ctx* ctx, const HostBatch& B, uint8_t* out_valid
       (e = hipMemcpyAsync(hout + o_v, static_cast<uint8_t*>(D0.d_out.p) + o_valid, n, hipMemcpyDeviceToHost,
                           D0.stream)) != hipSuccess)
     return hip_fail(e);
+  const uint64_t t_wait = phase_now(ctx);
   for (size_t g = 0; g < GG; g++) {
     *bad_dev = (long)live[g];
     (void)hipSetDevice(ctx->devs[live[g]].ordinal);
     if ((e = hipStreamSynchronize(ctx->devs[live[g]].stream)) != hipSuccess) return hip_fail(e);
+    // CMTV_FAULT_SYNC_DEV: this device's work "failed" after its launch
+    if ((long)live[g] == ctx->fault_sync_dev) {
+      ctx->stats.faults_injected++;
+      return CMTV_EHIP;
+    }
   }
   *bad_dev = -1;
+  phase_add(ctx, kPhWait, t_wait);
+  const uint64_t t_post = phase_now(ctx);
   (void)hipSetDevice(D0.ordinal);
   harvest(ctx, false);
   (void)hipSetDevice(D0.ordinal);
@@ -929,6 +1046,7 @@ static int run_host_batch_(cmtv_ctx* ctx, const HostBatch& B, uint8_t* out_valid
       for (size_t i = 0; i < n; i++) out_valid[i] = (uint8_t)((bm[i >> 6] >> (i & 63)) & 1);
     }
   }
+  phase_add(ctx, kPhPost, t_post);
   return CMTV_OK;
 }
 
@@ -958,6 +1076,12 @@ static void drain(cmtv_ctx* ctx) {
 
 static int run_host_batch(cmtv_ctx* ctx, const HostBatch& B, uint8_t* out_valid, uint64_t* out_bitmap) {
   int rc = CMTV_OK;
+  // every launch of this call is waited for before it returns (or drained)
+  struct HostSync {
+    cmtv_ctx* c;
+    explicit HostSync(cmtv_ctx* x) : c(x) { c->host_sync = true; }
+    ~HostSync() { c->host_sync = false; }
+  } host_sync(ctx);
   // a device error retires that device and re-plans the batch over the
   // others, once per surviving device at most
   for (size_t attempt = 0; attempt < ctx->devs.size(); attempt++) {
@@ -1070,6 +1194,20 @@ int verify_templated_locked(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const ui
   return run_host_batch(ctx, B, out_valid, nullptr);
 }
 
+// The single-device _device entry points run on devs[0] (their inputs are
+// its memory): once it is retired they return CMTV_ENODEV rather than launch
+// on a device that returned a HIP error. (Key generation and signing take
+// host buffers and run on the first live device.)
+static int dev0_usable(const cmtv_ctx* ctx) { return ctx->devs[0].failed ? CMTV_ENODEV : CMTV_OK; }
+
+// A single-device _device call's result: CMTV_FAULT_AT's failure belongs to
+// this call only, so the flag that marks it is cleared here (run_host_batch
+// and sharded_device clear it on their own paths).
+static int single_device_rc(cmtv_ctx* ctx, int rc) {
+  ctx->fault_pending = false;
+  return rc;
+}
+
 int ctx_lock(cmtv_ctx* ctx, std::unique_lock<std::mutex>& lk) {
   lk = std::unique_lock<std::mutex>(ctx->mu);
   return hipSetDevice(ctx->devs[0].ordinal) == hipSuccess ? CMTV_OK : CMTV_ENODEV;
@@ -1121,6 +1259,11 @@ static void release_device(CmtvDev& D) {
   D.d_bcomb = nullptr;
   D.d_srprog = nullptr;
   D.timing.release();
+  for (uint32_t k = 0; k < kRowSlots; k++) {
+    if (D.row_ev[k]) (void)hipEventDestroy(D.row_ev[k]);
+    D.row_ev[k] = nullptr;
+    D.row_pending[k] = false;
+  }
   if (D.atab_done) (void)hipEventDestroy(D.atab_done);
   if (D.done) (void)hipEventDestroy(D.done);
   if (D.stream) (void)hipStreamDestroy(D.stream);
@@ -1148,6 +1291,7 @@ static void read_env(cmtv_ctx* ctx) {
   if (const char* fw = std::getenv("CMTV_FORCE_WIDE")) ctx->force_wide = fw[0] == '1';
   if (const char* nf = std::getenv("CMTV_NO_SB_FUSE")) ctx->sb_fuse = nf[0] != '1';
   if (const char* nz = std::getenv("CMTV_NO_ZC_IN")) ctx->zc_in = nz[0] != '1';
+  if (const char* zm = std::getenv("CMTV_ZC_MAX")) ctx->zc_max = (size_t)std::strtoull(zm, nullptr, 10);
   if (const char* kl = std::getenv("CMTV_FORCE_K_LATE")) ctx->keyed_wait = kl[0] == '1' ? 0u : kKeyedWaitDefault;
   if (const char* kb = std::getenv("CMTV_KEYED_BATCH")) ctx->keyed_batch = kb[0] != '0';
   if (const char* wd = std::getenv("CMTV_WIDE_DMA")) ctx->wide_dma = wd[0] != '0';
@@ -1155,7 +1299,15 @@ static void read_env(cmtv_ctx* ctx) {
     const long v = std::strtol(mw, nullptr, 10);
     if (v >= 1 && v <= (1l << 20)) ctx->keyed_batch_min_waves = (uint32_t)v;
   }
+  if (const char* rf = std::getenv("CMTV_ROW_FENCE")) ctx->row_fence = rf[0] != '0';
+  if (const char* hp = std::getenv("CMTV_HOST_PHASES")) ctx->phases_on = hp[0] == '1';
+  if (const char* fs = std::getenv("CMTV_FAULT_SYNC_DEV")) {
+    char* end = nullptr;
+    const long g = std::strtol(fs, &end, 10);
+    if (end != fs && g >= 0) ctx->fault_sync_dev = g;
+  }
   ctx->force_rccl = std::getenv("CMTV_FORCE_RCCL") != nullptr;
+  if (const char* rl = std::getenv("CMTV_RCCL_LIB")) ctx->rccl_lib = rl;
   ctx->no_rccl = std::getenv("CMTV_NO_RCCL") != nullptr;
 }
 
@@ -1165,7 +1317,7 @@ static void read_env(cmtv_ctx* ctx) {
 // Otherwise gathers use peer copies. Called at open and after a device is
 // retired (the old communicator included it).
 static void rebuild_comm(cmtv_ctx* ctx) {
-  const Rccl& R = rccl();
+  const Rccl& R = rccl(ctx->rccl_lib);
   for (auto& D : ctx->devs) {
     if (D.comm && R.ok) {
       (void)hipSetDevice(D.ordinal);
@@ -1179,7 +1331,12 @@ static void rebuild_comm(cmtv_ctx* ctx) {
   std::vector<int> sorted = ords;
   std::sort(sorted.begin(), sorted.end());
   const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
-  const bool want = ords.size() > 1 ? (distinct && !ctx->no_rccl) : (ords.size() == 1 && ctx->force_rccl);
+  // a repeated ordinal gets a communicator only from a library named by
+  // CMTV_RCCL_LIB under CMTV_FORCE_RCCL (the one-GPU rehearsal of the
+  // multi-rank path); the system RCCL refuses duplicate devices
+  const bool repeat_ok = ctx->force_rccl && !ctx->rccl_lib.empty();
+  const bool want = ords.size() > 1 ? ((distinct || repeat_ok) && !ctx->no_rccl)
+                                    : (ords.size() == 1 && ctx->force_rccl);
   if (want && R.ok) {
     std::vector<ncclComm_t> comms(ords.size(), nullptr);
     if (R.CommInitAll(comms.data(), (int)ords.size(), ords.data()) == 0) {
@@ -1310,9 +1467,17 @@ int cmtv_open_devices(const cmtv_config* cfg, const int32_t* devices, size_t n_d
 
 void cmtv_close(cmtv_ctx* ctx) {
   if (!ctx) return;
+  if (ctx->phases_on) {
+    static const char* names[kPhCount] = {"prepare", "stage", "launch", "wait", "post", "replay"};
+    std::fprintf(stderr, "{\"cmtv_host_phases_us\": {");
+    for (int p = 0; p < kPhCount; p++)
+      std::fprintf(stderr, "%s\"%s\": %.3f", p ? ", " : "", names[p],
+                   ctx->phase_calls ? 1e-3 * (double)ctx->phase_ns[p] / (double)ctx->phase_calls : 0.0);
+    std::fprintf(stderr, "}, \"calls\": %llu}\n", (unsigned long long)ctx->phase_calls);
+  }
   for (auto& e : ctx->keysets) cmtv_keyset_free(e.second);
   ctx->keysets.clear();
-  const Rccl& R = rccl();
+  const Rccl& R = rccl(ctx->rccl_lib);
   for (auto& D : ctx->devs) {
     if (D.comm && R.ok) {
       (void)hipSetDevice(D.ordinal);
@@ -1418,10 +1583,12 @@ int cmtv_verify_ed25519_device(cmtv_ctx* ctx, size_t n, const void* d_pk, const 
   if (!d_pk || !d_sig || !d_msg || !d_msg_off || (!d_valid && !d_bitmap)) return CMTV_EINVAL;
   std::unique_lock<std::mutex> lk;
   if (ctx_lock(ctx, lk) != CMTV_OK) return CMTV_ENODEV;
+  if (dev0_usable(ctx) != CMTV_OK) return CMTV_ENODEV;
   hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the HIP null stream
-  return enqueue_verify(ctx, ctx->devs[0], n, static_cast<const uint8_t*>(d_pk), static_cast<const uint8_t*>(d_sig),
-                        static_cast<const uint8_t*>(d_msg), static_cast<const uint32_t*>(d_msg_off), mode,
-                        static_cast<uint8_t*>(d_valid), static_cast<uint64_t*>(d_bitmap), s);
+  return single_device_rc(
+      ctx, enqueue_verify(ctx, ctx->devs[0], n, static_cast<const uint8_t*>(d_pk), static_cast<const uint8_t*>(d_sig),
+                          static_cast<const uint8_t*>(d_msg), static_cast<const uint32_t*>(d_msg_off), mode,
+                          static_cast<uint8_t*>(d_valid), static_cast<uint64_t*>(d_bitmap), s));
 }
 
 int cmtv_verify_sr25519(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
@@ -1443,10 +1610,12 @@ int cmtv_verify_sr25519_device(cmtv_ctx* ctx, size_t n, const void* d_pk, const 
   if (!d_pk || !d_sig || !d_msg || !d_msg_off || (!d_valid && !d_bitmap)) return CMTV_EINVAL;
   std::unique_lock<std::mutex> lk;
   if (ctx_lock(ctx, lk) != CMTV_OK) return CMTV_ENODEV;
-  return enqueue_verify(ctx, ctx->devs[0], n, static_cast<const uint8_t*>(d_pk), static_cast<const uint8_t*>(d_sig),
-                        static_cast<const uint8_t*>(d_msg), static_cast<const uint32_t*>(d_msg_off), kModeSr25519,
-                        static_cast<uint8_t*>(d_valid), static_cast<uint64_t*>(d_bitmap),
-                        static_cast<hipStream_t>(stream));
+  if (dev0_usable(ctx) != CMTV_OK) return CMTV_ENODEV;
+  return single_device_rc(
+      ctx, enqueue_verify(ctx, ctx->devs[0], n, static_cast<const uint8_t*>(d_pk), static_cast<const uint8_t*>(d_sig),
+                          static_cast<const uint8_t*>(d_msg), static_cast<const uint32_t*>(d_msg_off), kModeSr25519,
+                          static_cast<uint8_t*>(d_valid), static_cast<uint64_t*>(d_bitmap),
+                          static_cast<hipStream_t>(stream)));
 }
 
 }  // extern "C"
@@ -1727,10 +1896,14 @@ int cmtv_verify_ed25519_indexed_device(cmtv_ctx* ctx, const cmtv_keyset* ks, siz
   if (!d_key_idx || !d_sig || !d_msg || !d_msg_off || (!d_valid && !d_bitmap)) return CMTV_EINVAL;
   std::unique_lock<std::mutex> lk;
   if (ctx_lock(ctx, lk) != CMTV_OK) return CMTV_ENODEV;
-  return enqueue_verify_keyed(ctx, ctx->devs[0], ks->dev[0], ks->n, n, static_cast<const uint32_t*>(d_key_idx),
-                              static_cast<const uint8_t*>(d_sig), static_cast<const uint8_t*>(d_msg),
-                              static_cast<const uint32_t*>(d_msg_off), mode, static_cast<uint8_t*>(d_valid),
-                              static_cast<uint64_t*>(d_bitmap), static_cast<hipStream_t>(stream));
+  if (dev0_usable(ctx) != CMTV_OK) return CMTV_ENODEV;
+  // a key set registered after device 0 was retired has no tables there
+  if (!ks->dev[0].d_tab || !ks->dev[0].d_pk || !ks->dev[0].d_ok) return CMTV_ENODEV;
+  return single_device_rc(
+      ctx, enqueue_verify_keyed(ctx, ctx->devs[0], ks->dev[0], ks->n, n, static_cast<const uint32_t*>(d_key_idx),
+                                static_cast<const uint8_t*>(d_sig), static_cast<const uint8_t*>(d_msg),
+                                static_cast<const uint32_t*>(d_msg_off), mode, static_cast<uint8_t*>(d_valid),
+                                static_cast<uint64_t*>(d_bitmap), static_cast<hipStream_t>(stream)));
 }
 
 int cmtv_pubkeys_ed25519(cmtv_ctx* ctx, size_t n, const uint8_t* seeds, uint8_t* out_pk) {
@@ -1738,7 +1911,10 @@ int cmtv_pubkeys_ed25519(cmtv_ctx* ctx, size_t n, const uint8_t* seeds, uint8_t*
   if (n == 0) return CMTV_OK;
   std::unique_lock<std::mutex> lk;
   if (ctx_lock(ctx, lk) != CMTV_OK) return CMTV_ENODEV;
-  CmtvDev& D = ctx->devs[0];
+  // host buffers in and out: the first live device does it
+  if (ctx->live.empty()) return CMTV_ENODEV;
+  CmtvDev& D = ctx->devs[ctx->live[0]];
+  if (hipSetDevice(D.ordinal) != hipSuccess) return CMTV_ENODEV;
   hipError_t e;
   if ((e = D.d_in.ensure(32 * n)) != hipSuccess) return hip_fail(e);
   if ((e = D.d_out.ensure(32 * n)) != hipSuccess) return hip_fail(e);
@@ -1770,7 +1946,10 @@ int cmtv_sign_ed25519(cmtv_ctx* ctx, size_t n, const uint8_t* seeds, const uint3
     if (msg_off[i + 1] < msg_off[i]) return CMTV_EINVAL;
   std::unique_lock<std::mutex> lk;
   if (ctx_lock(ctx, lk) != CMTV_OK) return CMTV_ENODEV;
-  CmtvDev& D = ctx->devs[0];
+  // host buffers in and out: the first live device does it
+  if (ctx->live.empty()) return CMTV_ENODEV;
+  CmtvDev& D = ctx->devs[ctx->live[0]];
+  if (hipSetDevice(D.ordinal) != hipSuccess) return CMTV_ENODEV;
   const size_t msg_bytes = msg_off[n];
   const size_t o_seed = 0, o_idx = align_up(32 * nseeds, 256), o_off = align_up(o_idx + (key_idx ? 4 * n : 0), 256);
   const size_t o_msg = align_up(o_off + 4 * (n + 1), 256), in_bytes = align_up(o_msg + msg_bytes + 16, 256);

@@ -40,6 +40,13 @@ int verify_templated_locked(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const ui
 // first use), or NULL when the cache is off or registration failed.
 const cmtv_keyset* keyset_for_locked(cmtv_ctx* ctx, const uint8_t* pk32, size_t n_keys);
 bool keyset_cache_enabled(const cmtv_ctx* ctx);
+
+// Host-side phase clock (CMTV_HOST_PHASES=1, read at open): where a call's
+// host time goes, summed over the context's life and printed as one JSON line
+// on stderr by cmtv_close. phase_now is 0 when the clock is off.
+enum HostPhase { kPhPrepare, kPhStage, kPhLaunch, kPhWait, kPhPost, kPhReplay, kPhCount };
+uint64_t phase_now(const cmtv_ctx* ctx);
+void phase_add(cmtv_ctx* ctx, int phase, uint64_t t0);
 int register_keys_locked(cmtv_ctx* ctx, size_t n_keys, const uint8_t* pk, cmtv_keyset** out, uint32_t flags);
 
 }  // namespace cmtv

@@ -129,8 +129,15 @@ typedef struct cmtv_device_stats {
  * device, so a one-GPU box exercises the RCCL init and all-gather),
  * CMTV_FAULT_DEV=g (test knob: every launch on the context's g-th device
  * fails with a HIP error: host batches retire it and re-shard onto the other
- * devices), CMTV_FORCE_K_LATE=1 (test knob: the keyed split kernel's quads
- * never wait for the hash helper and hash their signatures themselves). */
+ * devices), CMTV_FAULT_SYNC_DEV=g (test knob: device g's stream
+ * synchronisation in a host batch reports a HIP error, i.e. a fault found
+ * after the launch; same retirement), CMTV_FORCE_K_LATE=1 (test knob: the
+ * keyed split kernel's quads never wait for the hash helper and hash their
+ * signatures themselves), CMTV_RCCL_LIB=path (the RCCL library to dlopen
+ * instead of the system librccl; with CMTV_FORCE_RCCL a repeated ordinal then
+ * gets a multi-rank communicator: the one-GPU rehearsal of the RCCL path with
+ * tests/host/librccl_stub.so), CMTV_ROW_FENCE=0 (test knob: no fence on the
+ * row kernels' bitmap ring, see cmtv_verify_ed25519_device). */
 int cmtv_open(const cmtv_config* cfg, cmtv_ctx** out);
 
 /* Opens ONE context over several devices (a node is one
@@ -184,7 +191,16 @@ int cmtv_verify_ed25519(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_
 /* Same, all buffers already resident in device memory (HBM); enqueued on
  * `stream` (a hipStream_t; NULL = the HIP null stream, as in every HIP API;
  * cmtv_stream() gives the context's own stream), non-blocking. d_valid
- * (n bytes) and d_bitmap (ceil(n/64) words) may each be NULL. */
+ * (n bytes) and d_bitmap (ceil(n/64) words) may each be NULL.
+ * In-flight contract: any number of _device calls may be in flight on any
+ * number of streams. Batches of the row kernels (n <= 768 by default) pack
+ * their bitmap through one slot of a 256-slot per-device ring; a slot whose
+ * previous launch may still be running is fenced (the new launch's stream
+ * waits for the old launch's event), so verdict words never depend on what
+ * else is in flight. These calls record and wait on HIP events: do not
+ * enqueue them inside a hipStreamBeginCapture region (graph replays would
+ * reuse one ring slot without the fence). Returns CMTV_ENODEV once the
+ * context's first device has been retired after a HIP error. */
 int cmtv_verify_ed25519_device(cmtv_ctx* ctx, size_t n, const void* d_pk, const void* d_sig, const void* d_msg,
                                const void* d_msg_off, uint32_t mode, void* d_valid, void* d_bitmap, void* stream);
 

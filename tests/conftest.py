@@ -14,6 +14,19 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")
 
 
+@pytest.fixture(autouse=True)
+def _torch_cuda_first(request):
+    """GPU tests: torch initialises HIP before libcmtverify does. torch's wheel
+    carries its own HIP runtime; opened second it finds no device ("No HIP
+    GPUs are available") in a process where the library's runtime came first."""
+    if request.node.get_closest_marker("gpu"):
+        import torch
+
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    yield
+
+
 @pytest.fixture(scope="session")
 def corpus():
     with open(os.path.join(ROOT, "tests", "golden", "corpus.json")) as f:

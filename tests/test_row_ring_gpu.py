@@ -1,0 +1,149 @@
+"""The row kernels' bitmap ring under more launches in flight than it has
+slots (ADVICE r3 runtime.cpp:549).
+
+Every row launch (k_verify_row{,2,4}_split, k_verify_keyed_row_split) packs
+its bitmap through one slot of a 256-slot per-device ring; the last wave of
+the launch is found with a counter in the slot. Device-resident calls
+(cmtv_verify_ed25519_device and friends) are non-blocking on the caller's
+streams, so a caller can have a launch parked behind other work while 256
+later launches wrap the ring back to its slot. runtime.cpp row_slot_acquire
+fences the slot: the new launch's stream waits for the old launch's event.
+
+The race is made deterministic here:
+  * stream L runs a long spin kernel and records event E;
+  * stream A waits for E, then one row launch X takes slot k;
+  * stream C enqueues 255 row launches (they run at once, other slots);
+  * stream B waits for E, then row launch Y takes slot k again.
+X and Y both become runnable when E fires and, 100 signatures each (one CU
+per signature), fit the chip side by side. Unfenced they count each other's
+waves in one counter and write their verdict bytes over each other's;
+fenced, Y starts after X. Oracle: oracle/liboracle.so (the C restatement of
+Go 1.19 ed25519.Verify, crypto/ed25519/ed25519.go:148)."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import coracle
+from cometbft_amd import MODE_GO_STDLIB, Context
+from test_row_gpu import _batch
+
+pytestmark = pytest.mark.gpu
+
+
+def _want_words(exp, words):
+    w = np.packbits(exp, bitorder="little")
+    return np.pad(w, (0, 8 * words - w.size)).view(np.int64)
+
+
+def _spin(stream, dev):
+    """~20+ ms of GPU work on `stream` that involves no ring slot."""
+    import torch
+
+    with torch.cuda.stream(stream):
+        if hasattr(torch.cuda, "_sleep"):
+            torch.cuda._sleep(200_000_000)  # ~0.1 s on MI355X (tools/ring_race_probe.py)
+        else:  # a chain of large matmuls
+            a = torch.randn(4096, 4096, device=dev)
+            for _ in range(40):
+                a = a @ a
+                a = a / a.norm()
+
+
+def _race(ctx, keyed=None):
+    """Runs the X / 255 / Y pattern on ctx; returns (X ok, Y ok, C ok,
+    parked): parked = the spin was still running when the host had enqueued
+    all 257 launches (the device-resident calls never waited for it)."""
+    import torch
+
+    dev = torch.device("cuda:0")
+    n = 100
+    jobs = []
+    for j in range(2):
+        pk, sig, m, off = _batch(n, 7000 + j, flip=0.3)
+        exp = coracle.verify_batch(pk, sig, m, off, MODE_GO_STDLIB, nthreads=8)
+        jobs.append((pk, sig, m, off, exp))
+    assert not np.array_equal(jobs[0][4], jobs[1][4])
+    pk1, sig1, m1, off1 = _batch(1, 7100, flip=0.0)
+    exp1 = coracle.verify_batch(pk1, sig1, m1, off1, MODE_GO_STDLIB, nthreads=1)
+
+    def dev_args(pk, sig, m, off, ks=None):
+        keys = np.arange(len(sig), dtype=np.int32) if ks is not None else pk
+        return [torch.from_numpy(np.ascontiguousarray(v)).to(dev) for v in (keys, sig, m, off.view(np.int32))]
+
+    kss = []
+    if keyed:
+        kss = [ctx.register_keys(jobs[0][0]), ctx.register_keys(jobs[1][0]), ctx.register_keys(pk1)]
+    tx = dev_args(*jobs[0][:4], ks=kss[0] if keyed else None)
+    ty = dev_args(*jobs[1][:4], ks=kss[1] if keyed else None)
+    tc = dev_args(pk1, sig1, m1, off1, ks=kss[2] if keyed else None)
+    words = (n + 63) // 64
+    bx = torch.full((words,), -1, dtype=torch.int64, device=dev)
+    by = torch.full((words,), -1, dtype=torch.int64, device=dev)
+    bc = torch.full((255,), -1, dtype=torch.int64, device=dev)
+    sL, sA, sB, sC = (torch.cuda.Stream(device=dev) for _ in range(4))
+    torch.cuda.synchronize(dev)
+
+    def launch(t, nn, bm_ptr, stream, ks):
+        if keyed:
+            ctx.verify_indexed_device(ks, nn, t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(),
+                                      MODE_GO_STDLIB, 0, bm_ptr, stream.cuda_stream)
+        else:
+            ctx.verify_device(nn, t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(),
+                              MODE_GO_STDLIB, 0, bm_ptr, stream.cuda_stream)
+
+    _spin(sL, dev)
+    ev = torch.cuda.Event()
+    ev.record(sL)
+    sA.wait_event(ev)
+    sB.wait_event(ev)
+    launch(tx, n, bx.data_ptr(), sA, kss[0] if keyed else None)             # slot k
+    for i in range(255):                                                   # slots k+1 .. k+255
+        launch(tc, 1, bc.data_ptr() + 8 * i, sC, kss[2] if keyed else None)
+    launch(ty, n, by.data_ptr(), sB, kss[1] if keyed else None)             # slot k again
+    parked = not ev.query()
+    torch.cuda.synchronize(dev)
+    okx = np.array_equal(bx.cpu().numpy(), _want_words(jobs[0][4], words))
+    oky = np.array_equal(by.cpu().numpy(), _want_words(jobs[1][4], words))
+    okc = bool((bc.cpu().numpy() == int(exp1[0])).all())
+    for ks in kss:
+        ks.free()
+    return okx, oky, okc, parked
+
+
+def _ctx(**env):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update({k: str(v) for k, v in env.items()})
+    try:
+        return Context(device=0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("keyed", [False, True])
+def test_ring_wrap_behind_a_parked_launch_is_exact(keyed):
+    """Fenced (the default): both launches that share slot k and every
+    launch in between give the oracle's bitmap, and no call blocked the host
+    behind the parked launch (the timing harvest and the fence only enqueue
+    waits)."""
+    ctx = _ctx()
+    assert _race(ctx, keyed=keyed) == (True, True, True, True)
+    ctx.close()
+
+
+def test_ring_wrap_unfenced_shows_the_race():
+    """CMTV_ROW_FENCE=0 (the round-3 behaviour): X and Y run at once on one
+    slot, and at least one of their bitmaps is wrong. This is the proof that
+    the pattern above reaches the race; the context is discarded (its slot
+    counter is left inconsistent)."""
+    ctx = _ctx(CMTV_ROW_FENCE=0)
+    okx, oky, okc, parked = _race(ctx)
+    ctx.close()
+    assert parked
+    if okx and oky:
+        pytest.skip("the two launches did not overlap on this box (nothing to show)")
+    assert okc

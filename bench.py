@@ -484,15 +484,19 @@ def light_line(dev_index, heights=1000, n_vals=100):
     for vals, bid, h, c in seq:
         vals.verify_commit_light(TU.CHAIN_ID, bid, h, c, ctx=ctx)
     t_seq = time.perf_counter() - t
-    T.verify_commits(1, TU.CHAIN_ID, seq, ctx=ctx)
-    t = time.perf_counter()
-    errs = T.verify_commits(1, TU.CHAIN_ID, seq, ctx=ctx)
-    t_batch = time.perf_counter() - t
+    def median3(fn):
+        fn()
+        ts = []
+        for _ in range(3):
+            t = time.perf_counter()
+            out = fn()
+            ts.append(time.perf_counter() - t)
+        return float(np.median(ts)), out
+
+    # the Python mirror re-packs 999 commits per call: median of 3
+    t_batch, errs = median3(lambda: T.verify_commits(1, TU.CHAIN_ID, seq, ctx=ctx))
     assert all(e is None for e in errs)
-    T.verify_commits(1, TU.CHAIN_ID, seq, ctx=kctx)
-    t = time.perf_counter()
-    errs = T.verify_commits(1, TU.CHAIN_ID, seq, ctx=kctx)
-    t_kbatch = time.perf_counter() - t
+    t_kbatch, errs = median3(lambda: T.verify_commits(1, TU.CHAIN_ID, seq, ctx=kctx))
     assert all(e is None for e in errs)
     # the C calls alone, arguments packed once (what the cgo shim passes)
     per_call = [T.PackedCommits(1, TU.CHAIN_ID, [it]) for it in seq]
@@ -719,49 +723,83 @@ def keyset_10k(ctx, D, mode, steps):
             "path": "cmtv_verify_ed25519_indexed_device over 10,000 registered keys (keyed quad kernel)"}
 
 
+def _commit_c_call(c, sv, commit, bid, height, mode):
+    """cmtv_verify_commit on a commit packed once (what a cgo binding holds):
+    returns the call and the objects that keep the packed buffers alive."""
+    import ctypes
+
+    from cometbft_amd import _native as N
+    from cometbft_amd import testutil as TU
+    from cometbft_amd import types as T
+
+    vs, kv = sv.valset._pack()
+    cm, kc = T._pack_commit(commit)
+    bcb, kb = bid._c()
+    res = N.cmtv_commit_result()
+    cid = TU.CHAIN_ID.encode()
+    L = N.lib()
+
+    def call():
+        rc = L.cmtv_verify_commit(c.handle, N.VERIFY_COMMIT, mode, cid, len(cid), ctypes.byref(vs),
+                                  ctypes.byref(bcb), height, ctypes.byref(cm), 0, 0, ctypes.byref(res), None, 0)
+        assert rc == 0, rc
+    return call, (kv, kc, kb, res)
+
+
+def _p50_p99(fn, iters, warm=50):
+    for _ in range(warm):
+        fn()
+    ts = []
+    for _ in range(iters):
+        t = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t)
+    ts = np.array(ts) * 1e3
+    return round(float(np.percentile(ts, 50)), 4), round(float(np.percentile(ts, 99)), 4)
+
+
+def verify_commit_10k(ctx, mode, iters, host_api_ms=None):
+    """VerifyCommit at configs[1] scale: one 10,000-
+    validator commit through cmtv_verify_commit, packed once, p50 / p99 wall
+    (plan + staging + sign-bytes templated on the device + kernel + replay of
+    types/validator_set.go:667-714), beside the host-API batch of the same
+    signatures (e2e_10k)."""
+    from cometbft_amd import testutil as TU
+
+    sv = TU.make_validator_set(ctx, 10_000)
+    commit, _, _ = TU.make_commit(ctx, sv, height=1000)
+    call, keep = _commit_c_call(ctx, sv, commit, TU.block_id_for_height(1000), 1000, mode)
+    st0 = ctx.stats()
+    p50, p99 = _p50_p99(call, iters, warm=10)
+    st1 = ctx.stats()
+    kms = (st1["device_ms"] - st0["device_ms"]) / max(1, st1["calls"] - st0["calls"])
+    res = {"n_validators": 10_000, "iters": iters, "p50_ms": p50, "p99_ms": p99, "kernel_ms": round(kms, 4),
+           "value": round(10_000 / p50 * 1e3, 1), "unit": "verifs/s",
+           "path": "cmtv_verify_commit (C ABI, commit packed once): plan + pinned staging + device sign-bytes + "
+                   "k_verify_quad_split + VerifyCommit replay"}
+    if host_api_ms:
+        res["over_host_api"] = round(p50 / host_api_ms, 3)
+    del keep
+    return res
+
+
 def latency_150(ctx, mode, iters):
     """p50/p99 VerifyCommit latency for a 150-validator commit (host API, end
     to end): the C call alone (cmtv_verify_commit on a pre-packed commit, what
     a cgo binding pays) and through the Python mirror (which re-packs the
     commit's Python objects every call), plus the keyset-cache variant."""
-    import ctypes
-
     from cometbft_amd import Context
-    from cometbft_amd import _native as N
     from cometbft_amd import testutil as TU
-    from cometbft_amd import types as T
 
     sv = TU.make_validator_set(ctx, 150)
     commit, msgs, sigs = TU.make_commit(ctx, sv, height=1000)
     bid = TU.block_id_for_height(1000)
 
     def c_call(c):
-        vs, kv = sv.valset._pack()
-        cm, kc = T._pack_commit(commit)
-        bcb, kb = bid._c()
-        res = N.cmtv_commit_result()
-        cid = TU.CHAIN_ID.encode()
-        L = N.lib()
-
-        def call():
-            rc = L.cmtv_verify_commit(c.handle, N.VERIFY_COMMIT, mode, cid, len(cid), ctypes.byref(vs),
-                                      ctypes.byref(bcb), 1000, ctypes.byref(cm), 0, 0, ctypes.byref(res), None, 0)
-            assert rc == 0, rc
-        return call, (kv, kc, kb)
-
-    def pct(ts):
-        ts = np.array(ts) * 1e3
-        return round(float(np.percentile(ts, 50)), 4), round(float(np.percentile(ts, 99)), 4)
+        return _commit_c_call(c, sv, commit, bid, 1000, mode)
 
     def measure(fn):
-        for _ in range(50):  # BASELINE.md C1: 1000 iterations, 50 warm-up
-            fn()
-        ts = []
-        for _ in range(iters):
-            t = time.perf_counter()
-            fn()
-            ts.append(time.perf_counter() - t)
-        return pct(ts)
+        return _p50_p99(fn, iters, warm=50)  # BASELINE.md C1: 1000 iterations, 50 warm-up
 
     call, keep = c_call(ctx)
     p50c, p99c = measure(call)
@@ -971,6 +1009,8 @@ def main():
         "ms_per_step": round(el_z / args.steps * 1e3, 4), "kernel_ms": round(kms_z, 4),
         "frac": round(args.n * MACS_PER_VERIFY / (kms_z * 1e-3) / 1e12 / INT_MAC_PEAK_T, 4)}
     line["e2e_10k"] = e2e_10k(Context(device=0), D.host[0], mode)
+    if not args.no_latency and n_dev == 1:
+        line["verify_commit_10k"] = verify_commit_10k(Context(device=0), mode, 200, line["e2e_10k"]["ms"])
     if n_dev == 1 and not args.no_keyset:
         line["keyset_10k"] = keyset_10k(ctx, D, mode, args.steps)
     if not args.no_cpu_baseline and n_dev == 1:  # rank 0 at N=1 only (bench contract)

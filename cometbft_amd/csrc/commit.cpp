@@ -9,6 +9,7 @@
 // reference's. Error strings are produced with the reference's formats.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cinttypes>
 #include <cstdlib>
 #include <cstdio>
@@ -200,19 +201,24 @@ struct SigBatch {
   const int64_t* sec_data() const { return sec_src ? sec_src : tsec.data(); }
   const int32_t* nanos_data() const { return nanos_src ? nanos_src : tnanos.data(); }
 
-  // room for m more signatures (no reallocation inside add)
+  // room for m more signatures (no reallocation inside add); grows
+  // geometrically, since a cross-height batch calls it once per commit
+  template <class V>
+  static void grow(V& v, size_t want) {
+    if (v.capacity() < want) v.reserve(std::max(want, 2 * v.capacity()));
+  }
   void reserve_more(size_t m) {
     const size_t n = size() + m;
-    pk.reserve(32 * n);
-    sg.reserve(64 * n);
-    len_ok.reserve(n);
-    off.reserve(n + 1);
-    kidx.reserve(n);
+    grow(pk, 32 * n);
+    grow(sg, 64 * n);
+    grow(len_ok, n);
+    grow(off, n + 1);
+    grow(kidx, n);
     if (templated) {
-      tidx.reserve(n);
-      tflag.reserve(n);
-      tsec.reserve(n);
-      tnanos.reserve(n);
+      grow(tidx, n);
+      grow(tflag, n);
+      grow(tsec, n);
+      grow(tnanos, n);
     }
   }
 
@@ -334,8 +340,8 @@ int job_check_args(uint32_t kind, const char* chain_id, size_t chain_id_len, con
 // and every signature is 64 bytes. Then the caller's key, signature and
 // timestamp arrays are the batch itself (SigBatch's borrowed pointers): only
 // the per-signature flag and message offset are written here, and the batch
-// goes to the pinned staging in one copy. Applies to the first job of a
-// templated batch; false leaves B untouched.
+// goes to the pinned staging in one copy. Applies to a templated batch of
+// this one job; false leaves B untouched.
 bool job_prepare_identity(CommitJob& J, SigBatch& B, bool prefetch) {
   const cmtv_valset* vals = J.vals;
   const cmtv_commit* c = J.commit;
@@ -375,7 +381,7 @@ bool job_prepare_identity(CommitJob& J, SigBatch& B, bool prefetch) {
 // plan is ever examined). Appends the planned signatures to B; with
 // `prefetch` a light call also appends its commit's other non-absent
 // signatures (verdicts for the verdict cache only).
-void job_prepare(CommitJob& J, SigBatch& B, bool prefetch) {
+void job_prepare(CommitJob& J, SigBatch& B, bool prefetch, bool only_job) {
   const cmtv_valset* vals = J.vals;
   const cmtv_commit* commit = J.commit;
   std::memset(J.res, 0, sizeof(*J.res));
@@ -465,7 +471,8 @@ void job_prepare(CommitJob& J, SigBatch& B, bool prefetch) {
   }
 
   J.first = B.size();
-  if (job_prepare_identity(J, B, prefetch)) return;
+  // borrowing the caller's arrays: only when no other job adds to the batch
+  if (only_job && job_prepare_identity(J, B, prefetch)) return;
   B.reserve_more(J.plan_idx.size());
   for (size_t j = 0; j < J.plan_idx.size(); j++) {
     const uint32_t idx = J.plan_idx[j], vi = J.plan_val[j];
@@ -714,7 +721,7 @@ int cmtv_verify_commit(cmtv_ctx* ctx, uint32_t kind, uint32_t mode, const char* 
   SigBatch B;
   const bool cache = cmtv::cache_enabled(ctx);
   B.templated = !cache && templated_enabled();
-  job_prepare(J, B, cache);
+  job_prepare(J, B, cache, true);
   cmtv::phase_add(ctx, cmtv::kPhPrepare, t0);
   std::vector<uint8_t> valid;
   rc = batch_verify(ctx, B, mode, valid);
@@ -752,7 +759,7 @@ int cmtv_verify_commits(cmtv_ctx* ctx, uint32_t kind, uint32_t mode, const char*
   SigBatch B;
   const bool prefetch = cmtv::cache_enabled(ctx);
   B.templated = !prefetch && templated_enabled();
-  for (auto& J : jobs) job_prepare(J, B, prefetch);
+  for (auto& J : jobs) job_prepare(J, B, prefetch, n == 1);
   cmtv::phase_add(ctx, cmtv::kPhPrepare, t0);
   std::vector<uint8_t> valid;
   rc = batch_verify(ctx, B, mode, valid);

@@ -455,6 +455,8 @@ struct cmtv_ctx {
   bool host_sync = false;
   // CMTV_ROW_FENCE=0: no row-ring fence (only for the test that shows the race)
   bool row_fence = true;
+  // kernel timing by HIP event pairs (cmtv_stats device_ms; CMTV_TIMING=0: off)
+  bool timing_on = true;
   // CMTV_HOST_PHASES=1: host phase clock (runtime_internal.h HostPhase)
   bool phases_on = false;
   uint64_t phase_ns[cmtv::kPhCount] = {};
@@ -624,7 +626,7 @@ static int enqueue_verify(cmtv_ctx* ctx, CmtvDev& D, size_t n, const uint8_t* d_
   if (row && (e = row_slot_acquire(ctx, D, s, slot, slot_k)) != hipSuccess) return hip_fail(e);
   D.timing.harvest(ctx->stats, D.device_ms, false);
   Timing::Pair tp;
-  if ((e = D.timing.begin(tp, s)) != hipSuccess) return hip_fail(e);
+  if (ctx->timing_on && (e = D.timing.begin(tp, s)) != hipSuccess) return hip_fail(e);
   const size_t chunk = quad ? kChunk : ctx->lane_chunk;
   for (size_t c = 0; c < n; c += chunk) {
     const uint32_t cn = (uint32_t)std::min<size_t>(chunk, n - c);
@@ -645,7 +647,7 @@ static int enqueue_verify(cmtv_ctx* ctx, CmtvDev& D, size_t n, const uint8_t* d_
     D.launches++;
   }
   if (!quad && (e = release_scratch(D, s)) != hipSuccess) return hip_fail(e);
-  if ((e = D.timing.end(tp, s)) != hipSuccess) return hip_fail(e);
+  if (ctx->timing_on && (e = D.timing.end(tp, s)) != hipSuccess) return hip_fail(e);
   ctx->stats.calls++;
   ctx->stats.signatures += n;
   D.calls++;
@@ -712,7 +714,7 @@ static int enqueue_verify_keyed(cmtv_ctx* ctx, CmtvDev& D, const cmtv_keyset::Pe
   if (krow && (e = row_slot_acquire(ctx, D, s, slot, slot_k)) != hipSuccess) return hip_fail(e);
   D.timing.harvest(ctx->stats, D.device_ms, false);
   Timing::Pair tp;
-  if ((e = D.timing.begin(tp, s)) != hipSuccess) return hip_fail(e);
+  if (ctx->timing_on && (e = D.timing.begin(tp, s)) != hipSuccess) return hip_fail(e);
   for (size_t c = 0; c < n; c += chunk) {
     const uint32_t cn = (uint32_t)std::min<size_t>(chunk, n - c);
     // a chunk never needs more scratch than the first (kb and lanes shrink together)
@@ -732,7 +734,7 @@ static int enqueue_verify_keyed(cmtv_ctx* ctx, CmtvDev& D, const cmtv_keyset::Pe
     D.launches++;
   }
   if (kb0 > 1 && (e = release_scratch(D, s)) != hipSuccess) return hip_fail(e);
-  if ((e = D.timing.end(tp, s)) != hipSuccess) return hip_fail(e);
+  if (ctx->timing_on && (e = D.timing.end(tp, s)) != hipSuccess) return hip_fail(e);
   ctx->stats.calls++;
   ctx->stats.signatures += n;
   D.calls++;
@@ -1301,6 +1303,7 @@ static void read_env(cmtv_ctx* ctx) {
   }
   if (const char* rf = std::getenv("CMTV_ROW_FENCE")) ctx->row_fence = rf[0] != '0';
   if (const char* hp = std::getenv("CMTV_HOST_PHASES")) ctx->phases_on = hp[0] == '1';
+  if (const char* tm = std::getenv("CMTV_TIMING")) ctx->timing_on = tm[0] != '0';
   if (const char* fs = std::getenv("CMTV_FAULT_SYNC_DEV")) {
     char* end = nullptr;
     const long g = std::strtol(fs, &end, 10);

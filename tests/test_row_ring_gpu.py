@@ -9,7 +9,9 @@ streams, so a caller can have a launch parked behind other work while 256
 later launches wrap the ring back to its slot. runtime.cpp row_slot_acquire
 fences the slot: the new launch's stream waits for the old launch's event.
 
-The race is made deterministic here:
+The race is made deterministic here, on four streams with a hardware queue
+each (hw_queue_streams: plain streams share GPU_MAX_HW_QUEUES queues, and a
+stream parked on an event then parks its queue-mates too):
   * stream L runs a long spin kernel and records event E;
   * stream A waits for E, then one row launch X takes slot k;
   * stream C enqueues 255 row launches (they run at once, other slots);
@@ -36,13 +38,49 @@ def _want_words(exp, words):
     return np.pad(w, (0, 8 * words - w.size)).view(np.int64)
 
 
+def _hip():
+    """The HIP runtime this process runs on (the libamdhip64 already mapped)."""
+    import ctypes
+
+    with open("/proc/self/maps") as f:
+        for line in f:
+            if "libamdhip64.so" in line:
+                return ctypes.CDLL(line.split()[-1])
+    raise RuntimeError("libamdhip64 not mapped")
+
+
+_KEEP = []
+
+
+def hw_queue_streams(k):
+    """k streams with a HW queue each: hipExtStreamCreateWithCUMask (every CU
+    enabled) gives a stream its own hardware queue, where plain streams share
+    the process's GPU_MAX_HW_QUEUES queues (then a stream parked on an event
+    blocks the others on its queue, and two launches on one queue never run
+    at once). Wrapped as torch.cuda.ExternalStream."""
+    import ctypes
+
+    import torch
+
+    hip = _hip()
+    mask = (ctypes.c_uint32 * 8)(*([0xFFFFFFFF] * 8))  # 256 CUs
+    out = []
+    for _ in range(k):
+        s = ctypes.c_void_p()
+        rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(s), ctypes.c_uint32(8), mask)
+        assert rc == 0, rc
+        _KEEP.append(s)
+        out.append(torch.cuda.ExternalStream(s.value, device=torch.device("cuda:0")))
+    return out
+
+
 def _spin(stream, dev):
     """~20+ ms of GPU work on `stream` that involves no ring slot."""
     import torch
 
     with torch.cuda.stream(stream):
         if hasattr(torch.cuda, "_sleep"):
-            torch.cuda._sleep(200_000_000)  # ~0.1 s on MI355X (tools/ring_race_probe.py)
+            torch.cuda._sleep(1_000_000_000)  # 0.37-0.47 s on MI355X (tools/ring_race_probe.py)
         else:  # a chain of large matmuls
             a = torch.randn(4096, 4096, device=dev)
             for _ in range(40):
@@ -81,7 +119,7 @@ def _race(ctx, keyed=None):
     bx = torch.full((words,), -1, dtype=torch.int64, device=dev)
     by = torch.full((words,), -1, dtype=torch.int64, device=dev)
     bc = torch.full((255,), -1, dtype=torch.int64, device=dev)
-    sL, sA, sB, sC = (torch.cuda.Stream(device=dev) for _ in range(4))
+    sL, sA, sB, sC = hw_queue_streams(4)
     torch.cuda.synchronize(dev)
 
     def launch(t, nn, bm_ptr, stream, ks):

@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--mode", type=int, default=0)
     ap.add_argument("--zc-max", type=int, default=0, help="CMTV_ZC_MAX for the commit context (0: default)")
+    ap.add_argument("--ctx-env", default="", help="KEY=VAL,... set while the commit context opens")
     a = ap.parse_args()
     import torch
 
@@ -57,17 +58,20 @@ def main():
 
         m, off = pack_messages(msgs)
         sig = keyctx.sign(sv.seeds, m, off)
-        row = {"n": n, "zc_max": a.zc_max or None}
+        row = {"n": n, "zc_max": a.zc_max or None, "ctx_env": a.ctx_env or None}
         for _ in range(5):
             keyctx.verify(sv.pubkeys, sig, m, off, a.mode)
         row["host_api_p50_ms"], row["host_api_p99_ms"] = _pct(lambda: keyctx.verify(sv.pubkeys, sig, m, off, a.mode),
                                                               a.iters)
         os.environ["CMTV_HOST_PHASES"] = "1"
+        extra = dict(kv.split("=", 1) for kv in a.ctx_env.split(",") if kv)
         if a.zc_max:
-            os.environ["CMTV_ZC_MAX"] = str(a.zc_max)
+            extra["CMTV_ZC_MAX"] = str(a.zc_max)
+        os.environ.update(extra)
         ctx = Context(device=0)
         del os.environ["CMTV_HOST_PHASES"]
-        os.environ.pop("CMTV_ZC_MAX", None)
+        for k in extra:
+            os.environ.pop(k, None)
         packed = T.PackedCommits(0, TU.CHAIN_ID, [(sv.valset, TU.block_id_for_height(1000), 1000, commit)],
                                  mode=a.mode)
         for _ in range(5):
@@ -77,6 +81,7 @@ def main():
         row["commit_p50_ms"], row["commit_p99_ms"] = _pct(lambda: packed.call(ctx), a.iters)
         st1 = ctx.stats()
         row["kernel_ms"] = round((st1["device_ms"] - st0["device_ms"]) / max(1, st1["calls"] - st0["calls"]), 4)
+        row["cpu_p50_1core_ms"] = None
         row["commit_over_host"] = round(row["commit_p50_ms"] / row["host_api_p50_ms"], 3)
         print(json.dumps(row), flush=True)
         sys.stderr.flush()

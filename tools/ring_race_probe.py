@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--sleep", type=int, default=60_000_000)
     ap.add_argument("--n", type=int, default=100)
     ap.add_argument("--prio", type=int, default=0, help="1: stream A at high priority (its own HW queue)")
+    ap.add_argument("--cumask", type=int, default=1,
+                    help="1: every stream from hipExtStreamCreateWithCUMask (a dedicated HW queue each)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -47,7 +49,13 @@ def main():
     bx = torch.full((words,), -1, dtype=torch.int64, device=dev)
     by = torch.full((words,), -1, dtype=torch.int64, device=dev)
     bc = torch.full((255,), -1, dtype=torch.int64, device=dev)
-    sL, sA, sB, sC = (torch.cuda.Stream(device=dev) for _ in range(4))
+    if a.cumask:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from test_row_ring_gpu import hw_queue_streams
+
+        sL, sA, sB, sC = hw_queue_streams(4)
+    else:
+        sL, sA, sB, sC = (torch.cuda.Stream(device=dev) for _ in range(4))
     if a.prio:
         sA = torch.cuda.Stream(device=dev, priority=-1)
     ev = {k: torch.cuda.Event(enable_timing=True) for k in ("l0", "l1", "xs", "xe", "ys", "ye")}
@@ -80,6 +88,7 @@ def main():
     out = {
         "fence": a.fence,
         "prio": a.prio,
+        "cumask": a.cumask,
         "spin_ms": round(el("l0", "l1"), 3),
         "host_enqueue_ms": round(1e3 * t_enq, 3),
         "x_ms": round(el("xs", "xe"), 3),

@@ -212,8 +212,16 @@ __device__ uint64_t g_phase[4096 * 4 * kPhaseSlots];
     if ((threadIdx.x & 63) == 0 && blockIdx.x < 4096)                                              \
       g_phase[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * kPhaseSlots + (k)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
+// the 100 MHz constant clock, beside the shader clock (row4: slot 7 at entry,
+// slot 6 at the lo wave's verdict): the launch's wall time and clock rate
+#define CMTV_STAMP_RT(k)                                                                           \
+  do {                                                                                             \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 4096)                                              \
+      g_phase[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * kPhaseSlots + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 #else
 #define CMTV_STAMP(k) ((void)0)
+#define CMTV_STAMP_RT(k) ((void)0)
 #endif
 
 template <uint32_t MODE>
@@ -681,6 +689,7 @@ __global__ __launch_bounds__(256, 1) void k_verify_row4_split(
   const uint32_t* pkp = pk + 8 * (size_t)i;
   const uint32_t* sgp = sig + 16 * (size_t)i;
   CMTV_STAMP(0);
+  CMTV_STAMP_RT(7);
   if (wave == 3) {
     const uint8_t* mp;
     uint32_t ml;
@@ -735,6 +744,7 @@ __global__ __launch_bounds__(256, 1) void k_verify_row4_split(
   const uint32_t cb = (bpt[8 * (t >> 4) + ((t & 15) >> 1)] >> (16 * (t & 1))) & 0xFFFFu;
   bool v_ok = r_join4<MODE>(x, v, xh[0][t], xh[1][t], cb, (p.flags & 4u) != 0 && a_ok && r_ok, r_canon);
   CMTV_STAMP(5);
+  CMTV_STAMP_RT(6);
   const bool active = s < n;
   v_ok = v_ok && active;
   if (t == 0 && active && out_valid) out_valid[s] = v_ok ? 1 : 0;

@@ -65,6 +65,16 @@ def main():
         res["start_spread"] = float(t0.max() - t0.min())
         res["launch_span"] = float(st[:, 0, 5].max() - t0.min())
         res["end_median"] = float(np.median(st[:, 0, 5] - t0))
+        if form == "row4":
+            # the 100 MHz constant clock (kernels.hip CMTV_STAMP_RT): entry of
+            # every wave (slot 7) and the lo wave's verdict (slot 6)
+            rt0 = st[:, :nw, 7].min(axis=1)
+            cyc = (st[:, 0, 5] - t0).astype(np.float64)
+            ns = (st[:, 0, 6] - rt0).astype(np.float64) * 10.0
+            res["shader_clock_ghz_median"] = round(float(np.median(cyc / ns)), 3)
+            res["wall_us_median"] = round(float(np.median(ns)) / 1e3, 2)
+            res["launch_wall_us"] = round(float((st[:, 0, 6].max() - rt0.min()) * 10.0) / 1e3, 2)
+            res["start_spread_us"] = round(float((rt0.max() - rt0.min()) * 10.0) / 1e3, 2)
         out[name] = res
         print(name, json.dumps(res), flush=True)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)

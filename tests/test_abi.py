@@ -135,3 +135,22 @@ def test_open_devices_without_gpu_is_enodev():
     arr = (ctypes.c_int32 * 2)(0, 1)
     h = ctypes.c_void_p()
     assert N.lib().cmtv_open_devices(None, arr, 2, ctypes.byref(h)) == N.CMTV_ENODEV
+
+
+def test_rccl_stub_exports_what_the_library_binds():
+    """tests/host/librccl_stub.so (the multi-rank rehearsal's RCCL double,
+    selected by CMTV_RCCL_LIB) exports the five entry points runtime.cpp
+    load_rccl resolves, and rejects bad arguments like RCCL (no device
+    work: a NULL communicator list is ncclInvalidArgument)."""
+    path = os.path.join(ROOT, "tests", "host", "librccl_stub.so")
+    if not os.path.exists(path):
+        pytest.skip("librccl_stub.so not built (make -C cometbft_amd/csrc stub)")
+    stub = ctypes.CDLL(path)
+    for sym in ("ncclCommInitAll", "ncclCommDestroy", "ncclAllGather", "ncclGroupStart", "ncclGroupEnd"):
+        assert hasattr(stub, sym), sym
+    src = open(os.path.join(ROOT, "cometbft_amd", "csrc", "runtime.cpp")).read()
+    bound = set(re.findall(r'dlsym\(h, "(nccl[A-Za-z]+)"\)', src))
+    assert bound == {"ncclCommInitAll", "ncclCommDestroy", "ncclAllGather", "ncclGroupStart", "ncclGroupEnd"}
+    assert stub.ncclCommInitAll(None, 2, None) == 4  # ncclInvalidArgument
+    assert stub.ncclGroupEnd() == 5                  # unbalanced: ncclInvalidUsage
+    assert stub.ncclGroupStart() == 0 and stub.ncclGroupEnd() == 0

@@ -72,13 +72,14 @@ class cmtv_stats(ctypes.Structure):
                 ("faults_injected", ctypes.c_uint64), ("n_devices", ctypes.c_uint32), ("rccl", ctypes.c_uint32),
                 ("fused_sign_bytes", ctypes.c_uint64), ("device_failures", ctypes.c_uint64),
                 ("reshards", ctypes.c_uint64), ("late_k_waves", ctypes.c_uint64),
-                ("live_devices", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+                ("live_devices", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+                ("timed_calls", ctypes.c_uint64)]
 
 
 class cmtv_device_stats(ctypes.Structure):
     _fields_ = [("ordinal", ctypes.c_int32), ("failed", ctypes.c_uint32), ("calls", ctypes.c_uint64),
                 ("signatures", ctypes.c_uint64), ("kernel_launches", ctypes.c_uint64),
-                ("device_ms", ctypes.c_double)]
+                ("device_ms", ctypes.c_double), ("timed_calls", ctypes.c_uint64)]
 
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)

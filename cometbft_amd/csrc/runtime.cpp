@@ -319,7 +319,7 @@ struct Timing {
   }
   // completed pairs -> stats (context-wide and this device's); blocking
   // waits for all of them
-  void harvest(cmtv_stats& st, double& dev_ms, bool blocking) {
+  void harvest(cmtv_stats& st, double& dev_ms, uint64_t& dev_timed, bool blocking) {
     while (!pending.empty()) {
       Pair p = pending.front();
       // never blocks unless asked (cmtv_stats_get): a device-resident call
@@ -333,7 +333,9 @@ struct Timing {
       if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
         st.last_kernel_ms = ms;
         st.device_ms += ms;
+        st.timed_calls++;
         dev_ms += ms;
+        dev_timed++;
       }
       pending.pop_front();
       free_.push_back(p);
@@ -392,8 +394,10 @@ struct CmtvDev {
   bool failed = false;
   bool inject_fault = false;
   // this device's share of cmtv_stats (cmtv_device_stats_get)
-  uint64_t calls = 0, signatures = 0, launches = 0;
+  uint64_t calls = 0, signatures = 0, launches = 0, timed_calls = 0;
   double device_ms = 0;
+  // verification calls on this device (CMTV_TIMING samples one in timing_every)
+  uint64_t timing_seq = 0;
 };
 
 struct cmtv_ctx {
@@ -455,8 +459,11 @@ struct cmtv_ctx {
   bool host_sync = false;
   // CMTV_ROW_FENCE=0: no row-ring fence (only for the test that shows the race)
   bool row_fence = true;
-  // kernel timing by HIP event pairs (cmtv_stats device_ms; CMTV_TIMING=0: off)
-  bool timing_on = true;
+  // kernel timing by HIP event pairs on one call in timing_every per device
+  // (cmtv_stats device_ms / timed_calls; CMTV_TIMING=N, 0: off). The pair's
+  // marker packets cost ~4 us of a 150-validator call and ~8 us between
+  // back-to-back 10k launches (tools/step_gap.py), so not every call pays.
+  uint32_t timing_every = 16;
   // CMTV_HOST_PHASES=1: host phase clock (runtime_internal.h HostPhase)
   bool phases_on = false;
   uint64_t phase_ns[cmtv::kPhCount] = {};
@@ -505,7 +512,7 @@ static void harvest(cmtv_ctx* ctx, bool blocking) {
   for (auto& d : ctx->devs) {
     if (d.failed) continue;
     (void)hipSetDevice(d.ordinal);
-    d.timing.harvest(ctx->stats, d.device_ms, blocking);
+    d.timing.harvest(ctx->stats, d.device_ms, d.timed_calls, blocking);
   }
 }
 
@@ -624,9 +631,10 @@ static int enqueue_verify(cmtv_ctx* ctx, CmtvDev& D, size_t n, const uint8_t* d_
   uint32_t* slot = nullptr;
   uint32_t slot_k = 0;
   if (row && (e = row_slot_acquire(ctx, D, s, slot, slot_k)) != hipSuccess) return hip_fail(e);
-  D.timing.harvest(ctx->stats, D.device_ms, false);
+  D.timing.harvest(ctx->stats, D.device_ms, D.timed_calls, false);
   Timing::Pair tp;
-  if (ctx->timing_on && (e = D.timing.begin(tp, s)) != hipSuccess) return hip_fail(e);
+  const bool timed = ctx->timing_every && D.timing_seq++ % ctx->timing_every == 0;
+  if (timed && (e = D.timing.begin(tp, s)) != hipSuccess) return hip_fail(e);
   const size_t chunk = quad ? kChunk : ctx->lane_chunk;
   for (size_t c = 0; c < n; c += chunk) {
     const uint32_t cn = (uint32_t)std::min<size_t>(chunk, n - c);
@@ -647,7 +655,7 @@ static int enqueue_verify(cmtv_ctx* ctx, CmtvDev& D, size_t n, const uint8_t* d_
     D.launches++;
   }
   if (!quad && (e = release_scratch(D, s)) != hipSuccess) return hip_fail(e);
-  if (ctx->timing_on && (e = D.timing.end(tp, s)) != hipSuccess) return hip_fail(e);
+  if (timed && (e = D.timing.end(tp, s)) != hipSuccess) return hip_fail(e);
   ctx->stats.calls++;
   ctx->stats.signatures += n;
   D.calls++;
@@ -712,9 +720,10 @@ static int enqueue_verify_keyed(cmtv_ctx* ctx, CmtvDev& D, const cmtv_keyset::Pe
   uint32_t* slot = nullptr;
   uint32_t slot_k = 0;
   if (krow && (e = row_slot_acquire(ctx, D, s, slot, slot_k)) != hipSuccess) return hip_fail(e);
-  D.timing.harvest(ctx->stats, D.device_ms, false);
+  D.timing.harvest(ctx->stats, D.device_ms, D.timed_calls, false);
   Timing::Pair tp;
-  if (ctx->timing_on && (e = D.timing.begin(tp, s)) != hipSuccess) return hip_fail(e);
+  const bool timed = ctx->timing_every && D.timing_seq++ % ctx->timing_every == 0;
+  if (timed && (e = D.timing.begin(tp, s)) != hipSuccess) return hip_fail(e);
   for (size_t c = 0; c < n; c += chunk) {
     const uint32_t cn = (uint32_t)std::min<size_t>(chunk, n - c);
     // a chunk never needs more scratch than the first (kb and lanes shrink together)
@@ -734,7 +743,7 @@ static int enqueue_verify_keyed(cmtv_ctx* ctx, CmtvDev& D, const cmtv_keyset::Pe
     D.launches++;
   }
   if (kb0 > 1 && (e = release_scratch(D, s)) != hipSuccess) return hip_fail(e);
-  if (ctx->timing_on && (e = D.timing.end(tp, s)) != hipSuccess) return hip_fail(e);
+  if (timed && (e = D.timing.end(tp, s)) != hipSuccess) return hip_fail(e);
   ctx->stats.calls++;
   ctx->stats.signatures += n;
   D.calls++;
@@ -1303,7 +1312,10 @@ static void read_env(cmtv_ctx* ctx) {
   }
   if (const char* rf = std::getenv("CMTV_ROW_FENCE")) ctx->row_fence = rf[0] != '0';
   if (const char* hp = std::getenv("CMTV_HOST_PHASES")) ctx->phases_on = hp[0] == '1';
-  if (const char* tm = std::getenv("CMTV_TIMING")) ctx->timing_on = tm[0] != '0';
+  if (const char* tm = std::getenv("CMTV_TIMING")) {
+    const long v = std::strtol(tm, nullptr, 10);
+    ctx->timing_every = v < 0 ? 0u : (uint32_t)std::min<long>(v, 1l << 20);
+  }
   if (const char* fs = std::getenv("CMTV_FAULT_SYNC_DEV")) {
     char* end = nullptr;
     const long g = std::strtol(fs, &end, 10);
@@ -1556,6 +1568,7 @@ int cmtv_device_stats_get(cmtv_ctx* ctx, int g, cmtv_device_stats* out) {
   out->signatures = D.signatures;
   out->kernel_launches = D.launches;
   out->device_ms = D.device_ms;
+  out->timed_calls = D.timed_calls;
   (void)hipSetDevice(ctx->devs[0].ordinal);
   return CMTV_OK;
 }

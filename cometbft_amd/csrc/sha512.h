@@ -68,6 +68,17 @@ CMTV_HD uint64_t sha512_k(int i) { return g_sha512_K[i]; }
 
 CMTV_HD uint64_t rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
 
+#ifdef __HIP_DEVICE_COMPILE__
+// (lo, hi) halves as one 64-bit value by a bit cast of a 2-vector, so LLVM
+// keeps them a register pair: the ((uint64_t)hi << 32) | lo form made it split
+// every following 64-bit add into "+ lo" and "+ (hi << 32)" plus moves
+typedef uint32_t sha_u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint64_t sha_pair(uint32_t lo, uint32_t hi) {
+  sha_u32x2 v = {lo, hi};
+  return __builtin_bit_cast(uint64_t, v);
+}
+#endif
+
 // x >>> n and x >> n for the compression's constant n: on the device as
 // v_alignbit_b32 pairs on the 32-bit halves (the generic 64-bit form lowers
 // to two 64-bit shifts and two ORs, and hides the three-way XORs from
@@ -82,9 +93,9 @@ CMTV_HD uint64_t sha_rotr(uint64_t x, int n) {
     hi = t;
     n -= 32;
   }
-  if (n == 0) return ((uint64_t)hi << 32) | lo;
+  if (n == 0) return sha_pair(lo, hi);
   const uint32_t nlo = __builtin_amdgcn_alignbit(hi, lo, n), nhi = __builtin_amdgcn_alignbit(lo, hi, n);
-  return ((uint64_t)nhi << 32) | nlo;
+  return sha_pair(nlo, nhi);
 #else
   return rotr64(x, n);
 #endif
@@ -92,21 +103,50 @@ CMTV_HD uint64_t sha_rotr(uint64_t x, int n) {
 CMTV_HD uint64_t sha_shr(uint64_t x, int n) {
 #ifdef __HIP_DEVICE_COMPILE__
   const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
-  return ((uint64_t)(hi >> n) << 32) | __builtin_amdgcn_alignbit(hi, lo, n);
+  return sha_pair(__builtin_amdgcn_alignbit(hi, lo, n), hi >> n);
 #else
   return x >> n;
 #endif
 }
 
+// Three-input bitwise functions of 64-bit words as one v_bitop3_b32 per
+// 32-bit half on gfx950 (truth tables: a^b^c = 0x96, majority = 0xE8,
+// choose a ? b : c = 0xCA). LLVM forms neither v_xor3 nor bitop3 from the
+// 64-bit expressions (the listing had 18 v_xor_b32 and 8 and/or per round).
+CMTV_HD uint64_t sha_bitop3(uint64_t a, uint64_t b, uint64_t c, int tt) {
+#ifdef __HIP_DEVICE_COMPILE__
+  uint32_t lo, hi;
+  switch (tt) {
+    case 0x96:
+      lo = __builtin_amdgcn_bitop3_b32((uint32_t)a, (uint32_t)b, (uint32_t)c, 0x96);
+      hi = __builtin_amdgcn_bitop3_b32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32), 0x96);
+      break;
+    case 0xE8:
+      lo = __builtin_amdgcn_bitop3_b32((uint32_t)a, (uint32_t)b, (uint32_t)c, 0xE8);
+      hi = __builtin_amdgcn_bitop3_b32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32), 0xE8);
+      break;
+    default:
+      lo = __builtin_amdgcn_bitop3_b32((uint32_t)a, (uint32_t)b, (uint32_t)c, 0xCA);
+      hi = __builtin_amdgcn_bitop3_b32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32), 0xCA);
+      break;
+  }
+  return sha_pair(lo, hi);
+#else
+  if (tt == 0x96) return a ^ b ^ c;
+  if (tt == 0xE8) return (a & b) | (a & c) | (b & c);
+  return (a & b) | (~a & c);
+#endif
+}
+CMTV_HD uint64_t sha_xor3(uint64_t a, uint64_t b, uint64_t c) { return sha_bitop3(a, b, c, 0x96); }
+
 // one round on the rotating state (a..h named by the caller's order)
 CMTV_HD void sha512_round(uint64_t a, uint64_t b, uint64_t c, uint64_t& d, uint64_t e, uint64_t f, uint64_t g,
                           uint64_t& h, uint64_t kw) {
-  const uint64_t S1 = sha_rotr(e, 14) ^ sha_rotr(e, 18) ^ sha_rotr(e, 41);
-  const uint64_t ch = (e & f) | (~e & g);
+  const uint64_t S1 = sha_xor3(sha_rotr(e, 14), sha_rotr(e, 18), sha_rotr(e, 41));
+  const uint64_t ch = sha_bitop3(e, f, g, 0xCA);
   const uint64_t t1 = h + S1 + ch + kw;
-  const uint64_t S0 = sha_rotr(a, 28) ^ sha_rotr(a, 34) ^ sha_rotr(a, 39);
-  const uint64_t ab = a ^ b;
-  const uint64_t maj = (ab & c) | (~ab & b);  // majority: c where a, b differ, else b
+  const uint64_t S0 = sha_xor3(sha_rotr(a, 28), sha_rotr(a, 34), sha_rotr(a, 39));
+  const uint64_t maj = sha_bitop3(a, b, c, 0xE8);
   d += t1;
   h = t1 + S0 + maj;
 }
@@ -121,8 +161,8 @@ CMTV_HD void sha512_rounds16(uint64_t& a, uint64_t& b, uint64_t& c, uint64_t& d,
   for (int j = 0; j < 16; j++) {
     if (SCHED) {
       const uint64_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
-      const uint64_t s0 = sha_rotr(w15, 1) ^ sha_rotr(w15, 8) ^ sha_shr(w15, 7);
-      const uint64_t s1 = sha_rotr(w2, 19) ^ sha_rotr(w2, 61) ^ sha_shr(w2, 6);
+      const uint64_t s0 = sha_xor3(sha_rotr(w15, 1), sha_rotr(w15, 8), sha_shr(w15, 7));
+      const uint64_t s1 = sha_xor3(sha_rotr(w2, 19), sha_rotr(w2, 61), sha_shr(w2, 6));
       w[j] += s0 + w[(j + 9) & 15] + s1;
     }
     const uint64_t kw = sha512_k(r0 + j) + w[j];

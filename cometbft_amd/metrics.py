@@ -44,6 +44,8 @@ _FIELDS = [
     ("n_devices", "devices", "gauge", "Devices driven by the context."),
     ("rccl", "rccl", "gauge", "1 when bitmap gathers run over an RCCL communicator."),
     ("live_devices", "live_devices", "gauge", "Devices still taking work."),
+    ("timed_calls", "timed_calls_total", "counter",
+     "Calls whose kernel time device_seconds holds (CMTV_TIMING samples one call in N per device)."),
 ]
 
 
@@ -70,11 +72,12 @@ class StatsCollector:
                 _name(suffix[:-6] if kind == "counter" else suffix), doc, labels=keys)
             fam.add_metric(vals, float(st[field]))
             yield fam
-        dev = CounterMetricFamily(_name("device_seconds"), "Summed verification kernel time (HIP events).",
-                                  labels=keys)
+        dev = CounterMetricFamily(_name("device_seconds"),
+                                  "Summed kernel time of the timed calls (HIP events); mean kernel time = "
+                                  "device_seconds / timed_calls.", labels=keys)
         dev.add_metric(vals, st["device_ms"] / 1e3)
         yield dev
-        last = GaugeMetricFamily(_name("last_kernel_seconds"), "Duration of the most recent verification kernel.",
+        last = GaugeMetricFamily(_name("last_kernel_seconds"), "Kernel time of the most recent timed call.",
                                  labels=keys)
         last.add_metric(vals, st["last_kernel_ms"] / 1e3)
         yield last

@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define CMTV_ABI_VERSION 7
+#define CMTV_ABI_VERSION 8
 
 enum {
   CMTV_OK = 0,
@@ -78,8 +78,11 @@ typedef struct cmtv_stats {
   uint64_t signatures;     /* signatures verified                 */
   uint64_t invalid;        /* signatures rejected                 */
   uint64_t kernel_launches;
-  double device_ms;        /* summed kernel time (HIP events)     */
-  double last_kernel_ms;   /* the most recent verify kernel       */
+  double device_ms;        /* summed kernel time of the TIMED calls (HIP
+                              events; CMTV_TIMING=N times one call in N per
+                              device, default 16): mean kernel time =
+                              device_ms / timed_calls                     */
+  double last_kernel_ms;   /* the most recent timed verify call    */
   uint64_t cache_hits;     /* verdicts served by the verdict cache */
   uint64_t cache_entries;  /* verdicts currently cached           */
   uint64_t keyed_launches; /* launches of the registered-key kernels */
@@ -98,6 +101,7 @@ typedef struct cmtv_stats {
                               signatures (timing only, never a verdict)  */
   uint32_t live_devices;     /* devices still taking work                 */
   uint32_t reserved;
+  uint64_t timed_calls;      /* calls whose kernel time device_ms holds   */
 } cmtv_stats;
 
 /* One device's share of the context's work (cmtv_device_stats_get). */
@@ -107,7 +111,8 @@ typedef struct cmtv_device_stats {
   uint64_t calls;           /* verify calls that ran on this device        */
   uint64_t signatures;
   uint64_t kernel_launches;
-  double device_ms;         /* summed kernel time on this device (HIP events) */
+  double device_ms;         /* summed kernel time of this device's timed calls */
+  uint64_t timed_calls;     /* ... and their number                        */
 } cmtv_device_stats;
 
 /* ------------------------------------------------------------ lifecycle */

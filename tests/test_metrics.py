@@ -12,7 +12,7 @@ class _FakeCtx:
         base = {k: 0 for k in ("calls", "signatures", "invalid", "kernel_launches", "cache_hits", "cache_entries",
                                "keyed_launches", "sharded_calls", "gathers", "faults_injected", "n_devices",
                                "rccl", "fused_sign_bytes", "device_failures", "reshards", "late_k_waves",
-                               "live_devices")}
+                               "live_devices", "timed_calls")}
         base.update(device_ms=0.0, last_kernel_ms=0.0)
         base.update(kw)
         self._st = base
@@ -66,4 +66,9 @@ def test_exposition_of_a_device_context(gpu_ctx, corpus):
     assert after["cometbft_cmtverify_signatures_total"] - before["cometbft_cmtverify_signatures_total"] == n
     assert (after["cometbft_cmtverify_invalid_signatures_total"]
             - before["cometbft_cmtverify_invalid_signatures_total"]) == int(n - np.asarray(got).sum())
+    # kernel time is sampled (CMTV_TIMING: one call in 16 per device by default)
+    for _ in range(16):
+        gpu_ctx.verify(corpus["pk"], corpus["sig"], msg, off, MODE_GO_STDLIB)
+    after = _parse(M.exposition(gpu_ctx))
+    assert after["cometbft_cmtverify_timed_calls_total"] > before["cometbft_cmtverify_timed_calls_total"]
     assert after["cometbft_cmtverify_device_seconds_total"] > before["cometbft_cmtverify_device_seconds_total"]

@@ -80,7 +80,7 @@ def main():
         st0 = ctx.stats()
         row["commit_p50_ms"], row["commit_p99_ms"] = _pct(lambda: packed.call(ctx), a.iters)
         st1 = ctx.stats()
-        row["kernel_ms"] = round((st1["device_ms"] - st0["device_ms"]) / max(1, st1["calls"] - st0["calls"]), 4)
+        row["kernel_ms"] = round((st1["device_ms"] - st0["device_ms"]) / max(1, st1["timed_calls"] - st0["timed_calls"]), 4)
         row["cpu_p50_1core_ms"] = None
         row["commit_over_host"] = round(row["commit_p50_ms"] / row["host_api_p50_ms"], 3)
         print(json.dumps(row), flush=True)

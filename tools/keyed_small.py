@@ -36,7 +36,7 @@ for n in [int(a) for a in (sys.argv[1:] or ["150"])]:
             call()
         torch.cuda.synchronize()
         k0 = ctx.stats()["device_ms"]
-        c0 = ctx.stats()["calls"]
+        c0 = ctx.stats()["timed_calls"]
         reps = 50
         t = time.time()
         for _ in range(reps):
@@ -44,6 +44,6 @@ for n in [int(a) for a in (sys.argv[1:] or ["150"])]:
             torch.cuda.synchronize()
         dt = (time.time() - t) / reps
         st = ctx.stats()
-        kms = (st["device_ms"] - k0) / max(1, st["calls"] - c0)
+        kms = (st["device_ms"] - k0) / max(1, st["timed_calls"] - c0)
         print(f"n={n} mode={mode} wall_ms={dt * 1e3:.3f} kernel_ms={kms:.4f} valid={int(d_v.sum())}/{n}", flush=True)
     ks.free()

@@ -52,7 +52,7 @@ def main():
                 step()
             st.synchronize()
             s1 = ctx.stats()
-            kms = (s1["device_ms"] - s0["device_ms"]) / max(s1["calls"] - s0["calls"], 1)
+            kms = (s1["device_ms"] - s0["device_ms"]) / max(s1["timed_calls"] - s0["timed_calls"], 1)
             ok = bool((bm.cpu().numpy().view(np.uint64)[: n // 64] == np.uint64((1 << 64) - 1)).all())
             res.setdefault(str(n), {})[kind] = {"kernel_ms": round(kms, 4), "ok": ok}
             print(kind, n, round(kms, 4), ok, flush=True)

@@ -22,14 +22,16 @@ constexpr uint32_t kLaunchQuad = 1, kLaunchForceWide = 2, kLaunchOct = 4, kLaunc
 // and its two- and four-waves-per-signature forms (k_verify_row2_split,
 // k_verify_row4_split)
 constexpr uint32_t kLaunchRow = 32, kLaunchRow2 = 64, kLaunchRow4 = 128;
+// with kLaunchQuadSplit: the helper-summed form (k_verify_quad_hs; Ed25519)
+constexpr uint32_t kLaunchQuadHS = 256;
 
 // Row kernel bitmap assembly: each launch takes the next of kRowSlots slots
-// of a per-device ring (kRowSlotWords words: word 0 a wave counter the kernel
-// resets, then one verdict byte per signature); the last wave to finish packs
-// the bitmap words from the slot's bytes. A slot is reused after kRowSlots
-// further row launches on the device, so at most kRowSlots row launches may be
-// in flight at once (the context enqueues under its lock; each call of the
-// host API waits for its own launch). kRowMaxCap bounds a row launch.
+// of a per-device ring (kRowSlotWords words, read as 64-bit words of 32
+// two-bit verdict fields: kernels.hip row_bitmap_add); the wave that fills a
+// word's last field writes that word's 32 bitmap bits and zeroes it. A slot is
+// reused after kRowSlots further row launches on the device; the runtime
+// fences a reuse against the slot's previous launch (runtime.cpp
+// row_slot_acquire). kRowMaxCap bounds a row launch.
 constexpr uint32_t kRowSlots = 256, kRowSlotWords = 1024, kRowMaxCap = 4 * (kRowSlotWords - 16);
 
 // Templated sign-bytes (signbytes.h) written by the helper waves of the

@@ -219,9 +219,18 @@ __device__ uint64_t g_phase[4096 * 4 * kPhaseSlots];
     if ((threadIdx.x & 63) == 0 && blockIdx.x < 4096)                                              \
       g_phase[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * kPhaseSlots + (k)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
+// a value of the wave's own (cycles summed over a loop's barriers) into slot k
+#define CMTV_STAMP_VAL(k, val)                                                                     \
+  do {                                                                                             \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 4096)                                              \
+      g_phase[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * kPhaseSlots + (k)] = (val);          \
+  } while (0)
+#define CMTV_CLOCK() __builtin_amdgcn_s_memtime()
 #else
 #define CMTV_STAMP(k) ((void)0)
 #define CMTV_STAMP_RT(k) ((void)0)
+#define CMTV_STAMP_VAL(k, val) ((void)0)
+#define CMTV_CLOCK() 0ull
 #endif
 
 template <uint32_t MODE>
@@ -290,6 +299,168 @@ __global__ __launch_bounds__(256, CMTV_QUAD_WAVES_PER_EU) void k_verify_quad_spl
   x = (x | (x >> 24)) & 0xFFFFull;
   // one 16-bit slice per quad wave; the grid's last workgroup may run past
   // the bitmap's words
+  const uint32_t slice = blockIdx.x * 3 + wave;
+  if (t == 0 && out_bitmap && slice < 4 * ((n + 63) / 64)) reinterpret_cast<uint16_t*>(out_bitmap)[slice] = (uint16_t)x;
+}
+
+// The helper-summed quad verifier (quad.h q_verify_hs): the workgroup and its
+// first barrier as k_verify_quad_split, but the quads build both tables before
+// it (A's as extended points), and then the helper wave, instead of idling
+// after [u]B, sums every window's two table entries for its 48 signatures
+// (h_window_addend, one per lane) and hands the sums over through a 2-slot
+// LDS ring, one barrier per window: the quads' windows lose one of their two
+// additions. [u]B: while the quads build their tables the helper adds the
+// top kHsCombPre positions of u's 16-position comb and hands that part over
+// at a last barrier; the quads add the other 16 - kHsCombPre digits inside
+// their windows (q_verify_hs). Nothing of [u]B runs inside the helper's
+// window loop: the per-window barriers go at the slower side's pace, so
+// helper work there stalls all three quads (measured: comb additions cut into
+// one-multiplication phases, two per window, cost the quads 1.6k cycles a
+// window; tools/gpu_hs.sh). The slot ring overlays the fused sign-bytes
+// buffer (dead once the hashes are done). hs_tune (the launcher's kflags bits
+// 16..31, CMTV_HS_PRE) overrides kHsCombPre (0..16) for tuning.
+constexpr int kHsCombPre = 6;
+
+template <uint32_t MODE>
+__global__ __launch_bounds__(256, CMTV_QUAD_WAVES_PER_EU) void k_verify_quad_hs(
+    uint32_t n, const uint32_t* __restrict__ pk, const uint32_t* __restrict__ sig, const uint8_t* __restrict__ msg,
+    const uint32_t* __restrict__ off, const uint32_t* __restrict__ btab, uint8_t* __restrict__ out_valid,
+    uint64_t* __restrict__ out_bitmap, uint32_t force_wide, SbFuse sb, uint32_t hs_tune) {
+  const uint32_t wave = threadIdx.x >> 6, t = threadIdx.x & 63;
+  const uint32_t base = blockIdx.x * 48;
+  int comb_pre = (hs_tune & 0xFFu) ? (int)(hs_tune & 0xFFu) - 1 : kHsCombPre;
+  comb_pre = comb_pre > 16 ? 16 : comb_pre;
+  constexpr uint32_t kSlotU2 = 3 * 5 * 64;  // one slot: 3 quad waves x 5 uint2 x 64 lanes
+  __shared__ uint32_t prep[48][SIG_PREP_WORDS + 1];
+  __shared__ uint2 tab_lds[3][2 * 9 * 5 * 64];
+  __shared__ uint2 xbuf[2 * kSlotU2];  // sign-bytes (48 x kSbFuseMaxMsg B), then the 2-slot ring
+  static_assert(sizeof(xbuf) >= 48 * kSbFuseMaxMsg, "ring must cover the sign-bytes buffer");
+  CMTV_STAMP(0);
+  if (wave == 3) {
+    const uint32_t slot = t < 48 ? t : 47;
+    const uint32_t s = base + slot;
+    const uint32_t i = s < n ? s : n - 1;
+    const uint8_t* mp;
+    uint32_t ml;
+    helper_message(sb, i, msg, off, reinterpret_cast<uint32_t*>(xbuf) + slot * (kSbFuseMaxMsg / 4), mp, ml);
+    SigPrep p;
+    q_prepare<MODE>(p, pk + 8 * (size_t)i, sig + 16 * (size_t)i, mp, ml, force_wide != 0);
+    // the workgroup's window count (the quads' q_wave_windows over all 48)
+    const bool wide = __ballot(t < 48 && (p.flags & 2u) != 0) != 0;
+    int W = HS_WINDOWS;
+#pragma unroll 1
+    for (int x = HS_WINDOWS; x < HS_MAX_WINDOWS; x++) W += __ballot(t < 48 && (int)((p.flags >> 8) & 0xFFu) > x) ? 1 : 0;
+    W = wide ? HS_WIDE_WINDOWS : W;
+    p.flags |= (uint32_t)W << 16;
+    if (t < 48) sig_prep_store(prep[t], p);
+    BComb16 bc;
+    bc.init(p.u);
+    const DevBTab bt{btab};
+#pragma unroll 1
+    for (int k = 0; k < comb_pre; k++) bc.step(bt);
+    CMTV_STAMP(1);
+    __syncthreads();  // 1: the scalars; the tables are built
+    CMTV_STAMP(2);
+    const bool r_flip = (p.flags & 1u) != 0;
+    uint32_t tA[8], tR[8];
+    hs_digits16(tA, p.k1, W);
+    hs_digits16(tR, p.k2, W);
+    sc_shift_out(tA, 4);  // the top window is the quads' own
+    sc_shift_out(tR, 4);
+    uint64_t hwait = 0;  // probe build: cycles the helper waits at the window barriers
+    (void)hwait;
+
+    const uint2* tw = tab_lds[slot >> 4];
+    const uint32_t qb = 4 * (slot & 15);
+    auto rd = [&](int P, int e, int c, fe& r) {
+      const uint2* src = tw + (P * 9 + e) * 5 * 64 + qb + c;
+#pragma unroll
+      for (int k = 0; k < 5; k++) {
+        const uint2 x = src[k * 64];
+        r.v[2 * k] = x.x;
+        r.v[2 * k + 1] = x.y;
+      }
+    };
+    auto put = [&](uint2* dst, const fe* out) {
+      if (t < 48) {
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+#pragma unroll
+          for (int k = 0; k < 5; k++) dst[(slot >> 4) * 320 + k * 64 + qb + c] = make_uint2(out[c].v[2 * k], out[c].v[2 * k + 1]);
+      }
+    };
+#pragma unroll 1
+    for (int win = W - 2; win >= 0; win--) {
+      const int dA = (int)sc_shift_out(tA, 4) - 8;
+      const int dR = (int)sc_shift_out(tR, 4) - 8;
+      fe out[4];
+      h_window_addend(out, rd, dA, dR, r_flip);
+      put(xbuf + (win & 1) * kSlotU2, out);
+      const uint64_t c0 = CMTV_CLOCK();
+      __syncthreads();  // window win
+      hwait += CMTV_CLOCK() - c0;
+    }
+    CMTV_STAMP_VAL(6, hwait);
+    {
+      fe out[4], d2;
+      fe_sub(out[0], bc.P.Y, bc.P.X);
+      fe_add(out[1], bc.P.Y, bc.P.X);
+      fe_add(out[2], bc.P.Z, bc.P.Z);
+      fe_const_d2(d2);
+      fe_mul(out[3], bc.P.T, d2);
+      put(xbuf + kSlotU2, out);  // slot 1: last read for window 1, before barrier 0
+    }
+    CMTV_STAMP(3);
+    __syncthreads();  // B: [u]B
+    CMTV_STAMP(4);
+    return;
+  }
+  const uint32_t ls = wave * 16 + (t >> 2);
+  const uint32_t s = base + ls;
+  const bool active = s < n;
+  const uint32_t i = active ? s : n - 1;
+  DevQuad q;
+  DevATabQ ta{tab_lds[wave], t}, tr{tab_lds[wave] + 9 * 5 * 64, t};
+  uint64_t qwait = 0;  // probe build: cycles this quad wave waits at the window barriers
+  (void)qwait;
+  auto slot_load = [&](const uint2* sl, fe& c) {
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+      const uint2 x = sl[wave * 320 + k * 64 + t];
+      c.v[2 * k] = x.x;
+      c.v[2 * k + 1] = x.y;
+    }
+  };
+  DevBTabQ bt{btab};
+  bool v = q_verify_hs<MODE>(
+      q, pk + 8 * (size_t)i, sig + 16 * (size_t)i, bt, ta, tr, 16 - comb_pre,
+      [&](SigPrep& p) {
+        CMTV_STAMP(1);
+        __syncthreads();
+        CMTV_STAMP(2);
+        sig_prep_load(p, prep[ls]);
+      },
+      [&](int win, fe& c) {
+        const uint64_t c0 = CMTV_CLOCK();
+        __syncthreads();
+        qwait += CMTV_CLOCK() - c0;
+        slot_load(xbuf + (win & 1) * kSlotU2, c);
+      },
+      [&](fe& c) {
+        CMTV_STAMP(3);
+        __syncthreads();
+        CMTV_STAMP(4);
+        slot_load(xbuf + kSlotU2, c);
+      });
+  CMTV_STAMP(5);
+  CMTV_STAMP_VAL(6, qwait);
+  v = v && active;
+  if (active && (t & 3) == 0 && out_valid) out_valid[s] = v ? 1 : 0;
+  uint64_t x = __ballot(v && (t & 3) == 0) & 0x1111111111111111ull;
+  x = (x | (x >> 3)) & 0x0303030303030303ull;
+  x = (x | (x >> 6)) & 0x000F000F000F000Full;
+  x = (x | (x >> 12)) & 0x000000FF000000FFull;
+  x = (x | (x >> 24)) & 0xFFFFull;
   const uint32_t slice = blockIdx.x * 3 + wave;
   if (t == 0 && out_bitmap && slice < 4 * ((n + 63) / 64)) reinterpret_cast<uint16_t*>(out_bitmap)[slice] = (uint16_t)x;
 }
@@ -454,6 +625,40 @@ __device__ __forceinline__ void helper_bcomb_prefetched(ge_p3& B, const uint32_t
   B = P;
 }
 
+// The row kernels' bitmap epilogue, on one slot of the per-device ring
+// (kernels.h kRowSlots). Slot word j (64 bits) collects the verdicts of
+// signatures 32j .. 32j+31 as 2-bit fields (01 rejected, 10 accepted), each
+// added by its signature's wave with ONE agent-scope relaxed atomic; the wave
+// whose add fills the word's last field packs the word into 32-bit half j of
+// out_bitmap (and the unused upper half of the last 64-bit word) and zeroes
+// the slot word for the slot's next launch. Every access to a slot word is an
+// atomic on that word, so nothing else needs ordering and no fence is issued:
+// the round-4 form (verdict bytes, a release fence and an acq_rel ticket per
+// wave, the last wave packing) made every wave write back and invalidate its
+// XCD's L2 (buffer_wbl2 sc1 / buffer_inv sc1), ~10 us of a 150-signature
+// launch (tools/microbench/launch_lat.hip).
+__device__ __forceinline__ void row_bitmap_add(uint32_t* __restrict__ slot, uint32_t s, uint32_t n, bool v,
+                                               uint64_t* __restrict__ out_bitmap, uint32_t t) {
+  uint64_t* sw = reinterpret_cast<uint64_t*>(slot);
+  const uint32_t j = s >> 5, f = s & 31;
+  uint64_t x = 0;
+  if (t == 0) {
+    const uint64_t add = (uint64_t)(v ? 2u : 1u) << (2 * f);
+    x = __hip_atomic_fetch_add(sw + j, add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + add;
+  }
+  x = __shfl(x, 0);
+  const uint32_t nf = n - 32 * j < 32 ? n - 32 * j : 32u;  // fields of word j
+  const uint64_t m = 0x5555555555555555ull >> (64 - 2 * nf);
+  if (((x | (x >> 1)) & m) != m) return;  // a field of word j is still empty
+  const uint64_t acc = __ballot(t < 32 && ((x >> (2 * (t & 31) + 1)) & 1) != 0);
+  if (t == 0) {
+    uint32_t* ob = reinterpret_cast<uint32_t*>(out_bitmap);
+    ob[j] = (uint32_t)acc;
+    if ((j & 1) == 0 && 32 * (j + 1) >= n) ob[j + 1] = 0u;
+    __hip_atomic_store(sw + j, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // One signature per wave (row.h): for the smallest batches (a 150-validator
 // commit), where SIMDs are idle and each signature's chain of field products
 // is the kernel time. A 4-wave workgroup takes 3 signatures: waves 0-2
@@ -526,22 +731,7 @@ __global__ __launch_bounds__(256, 1) void k_verify_row_split(
   CMTV_STAMP(5);
   v = v && active;
   if (t == 0 && active && out_valid) out_valid[s] = v ? 1 : 0;
-  if (!out_bitmap) return;
-  uint8_t* vb = reinterpret_cast<uint8_t*>(slot + 16);
-  if (t == 0 && active) vb[s] = v ? 1 : 0;
-  __threadfence();
-  uint32_t ticket = 0;
-  if (t == 0) ticket = __hip_atomic_fetch_add(slot, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-  ticket = __shfl(ticket, 0);
-  if (ticket != 3 * gridDim.x - 1) return;
-  __threadfence();
-  const uint32_t words = (n + 63) / 64;
-  for (uint32_t w = t; w < words; w += 64) {
-    uint64_t m = 0;
-    for (uint32_t b = 0; b < 64 && 64 * w + b < n; b++) m |= (uint64_t)(vb[64 * w + b] != 0) << b;
-    out_bitmap[w] = m;
-  }
-  if (t == 0) __hip_atomic_store(slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (out_bitmap && active) row_bitmap_add(slot, s, n, v, out_bitmap, t);
 }
 
 // The row verifier over two waves per signature (row.h r_part / r_join),
@@ -643,22 +833,7 @@ __global__ __launch_bounds__(192, 1) void k_verify_row2_split(
   const bool active = s < n;
   v_ok = v_ok && active;
   if (t == 0 && active && out_valid) out_valid[s] = v_ok ? 1 : 0;
-  if (!out_bitmap) return;
-  uint8_t* vb = reinterpret_cast<uint8_t*>(slot + 16);
-  if (t == 0 && active) vb[s] = v_ok ? 1 : 0;
-  __threadfence();
-  uint32_t ticket = 0;
-  if (t == 0) ticket = __hip_atomic_fetch_add(slot, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-  ticket = __shfl(ticket, 0);
-  if (ticket != gridDim.x - 1) return;
-  __threadfence();
-  const uint32_t words = (n + 63) / 64;
-  for (uint32_t w = t; w < words; w += 64) {
-    uint64_t m = 0;
-    for (uint32_t b = 0; b < 64 && 64 * w + b < n; b++) m |= (uint64_t)(vb[64 * w + b] != 0) << b;
-    out_bitmap[w] = m;
-  }
-  if (t == 0) __hip_atomic_store(slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (out_bitmap && active) row_bitmap_add(slot, s, n, v_ok, out_bitmap, t);
 }
 
 // The row verifier over four waves per signature (row.h r_sum_ar / r_part<·,
@@ -748,22 +923,7 @@ __global__ __launch_bounds__(256, 1) void k_verify_row4_split(
   const bool active = s < n;
   v_ok = v_ok && active;
   if (t == 0 && active && out_valid) out_valid[s] = v_ok ? 1 : 0;
-  if (!out_bitmap) return;
-  uint8_t* vb = reinterpret_cast<uint8_t*>(slot + 16);
-  if (t == 0 && active) vb[s] = v_ok ? 1 : 0;
-  __threadfence();
-  uint32_t ticket = 0;
-  if (t == 0) ticket = __hip_atomic_fetch_add(slot, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-  ticket = __shfl(ticket, 0);
-  if (ticket != gridDim.x - 1) return;
-  __threadfence();
-  const uint32_t words = (n + 63) / 64;
-  for (uint32_t w = t; w < words; w += 64) {
-    uint64_t m = 0;
-    for (uint32_t b = 0; b < 64 && 64 * w + b < n; b++) m |= (uint64_t)(vb[64 * w + b] != 0) << b;
-    out_bitmap[w] = m;
-  }
-  if (t == 0) __hip_atomic_store(slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (out_bitmap && active) row_bitmap_add(slot, s, n, v_ok, out_bitmap, t);
 }
 
 // the keyed row kernel's R wave meets barrier 1 86 squarings into the decode's
@@ -913,22 +1073,7 @@ __global__ __launch_bounds__(256, 1) void k_verify_keyed_row_split(
   const bool active = s < n;
   v_ok = v_ok && active;
   if (t == 0 && active && out_valid) out_valid[s] = v_ok ? 1 : 0;
-  if (!out_bitmap) return;
-  uint8_t* vb = reinterpret_cast<uint8_t*>(slot + 16);
-  if (t == 0 && active) vb[s] = v_ok ? 1 : 0;
-  __threadfence();
-  uint32_t ticket = 0;
-  if (t == 0) ticket = __hip_atomic_fetch_add(slot, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-  ticket = __shfl(ticket, 0);
-  if (ticket != gridDim.x - 1) return;
-  __threadfence();
-  const uint32_t words = (n + 63) / 64;
-  for (uint32_t w = t; w < words; w += 64) {
-    uint64_t m = 0;
-    for (uint32_t b = 0; b < 64 && 64 * w + b < n; b++) m |= (uint64_t)(vb[64 * w + b] != 0) << b;
-    out_bitmap[w] = m;
-  }
-  if (t == 0) __hip_atomic_store(slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (out_bitmap && active) row_bitmap_add(slot, s, n, v_ok, out_bitmap, t);
 }
 
 // Comb of (negate ? -P : P) for n_keys encoded points; workgroup = key,
@@ -1089,6 +1234,15 @@ hipError_t launch_verify(uint32_t mode, uint32_t n, const void* pk, const void* 
     // of every bitmap word
     const uint32_t slices = 4 * ((n + 63) / 64);
     const dim3 grid((slices + 2) / 3), block(256);
+    if (kflags & kLaunchQuadHS) {
+      if (mode == MODE_ZIP215)
+        hipLaunchKernelGGL(k_verify_quad_hs<MODE_ZIP215>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp, fw, fz,
+                           kflags >> 16);
+      else
+        hipLaunchKernelGGL(k_verify_quad_hs<MODE_GO_STDLIB>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp, fw,
+                           fz, kflags >> 16);
+      return hipGetLastError();
+    }
     if (mode == MODE_ZIP215)
       hipLaunchKernelGGL(k_verify_quad_split<MODE_ZIP215>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp, fw,
                          fz);

@@ -436,6 +436,29 @@ CMTV_HD void q_bcomb16(ge_p3& P, const uint32_t u[8], const BTab& btab) {
   }
 }
 
+// q_bcomb16 one comb position at a time (the helper-summed quad kernel
+// spreads the 16 additions over the windows' slack): init, then step() while
+// j >= 0
+struct BComb16 {
+  ge_p3 P;
+  uint32_t lo[8], hi[8];
+  int j;
+  CMTV_HD void init(const uint32_t u[8]) {
+    hs_digits65536(lo, hi, u);
+    p3_identity(P);
+    j = 15;
+  }
+  template <class BTab>
+  CMTV_HD void step(const BTab& btab) {
+    const int d = (int)(j >= 8 ? sc_shift_out(hi, 16) : sc_shift_out(lo, 16)) - 0x8000;
+    const int ib = d < 0 ? -d : d;
+    ge_efgh t;
+    ge_add_table<false>(t, P, btab, BC16_BASE + j * BT16_ENTRIES + (ib > 0 ? ib - 1 : 0), d < 0, ib == 0);
+    efgh_to_p3(P, t);
+    j--;
+  }
+};
+
 // the quad's cached coordinates of P, (Y-X, Y+X, 2Z, 2dT), as 40 words
 CMTV_HD void bpoint_store(uint32_t* d, const ge_p3& P) {
   fe c[4], d2;
@@ -661,6 +684,201 @@ CMTV_HD bool q_verify_split(const Q& q, const uint32_t* pk_ptr, const uint32_t* 
   q.template perm<QP_B2>(z, v);
   const bool x0 = fe_iszero(v);    // meaningful on lane 0
   const bool yz = fe_equal(v, z);  // meaningful on lane 1
+  const bool e0 = q.template perm32<QP_B0>(x0 ? 1u : 0u) != 0;
+  const bool e1 = q.template perm32<QP_B1>(yz ? 1u : 0u) != 0;
+  return s_ok && a_ok && r_ok && r_canon && e0 && e1;
+}
+
+// ---- helper-summed windows (kernels.hip k_verify_quad_hs) -----------------
+//
+// In the helper-wave quad kernel a third of every window went to the quads'
+// two table additions (A's and R's), while the helper wave sat idle after
+// [u]B. Here the helper sums a window's two table entries in its own lane
+// layout, S_w = [dA](-A) + [dR](-/+R), and hands S_w to the quads through LDS
+// at a per-window barrier: a window is 4 doublings and ONE addition. Both
+// tables are built before barrier 1 -- A's entries as extended points (the
+// first operand of the helper's addition), R's as cached entries of -R (a
+// negative k2 flips R's digits) -- and only the top window is summed by the
+// quads themselves (its A entry is loaded as the starting point).
+
+// (0..8)P as extended points (entry 0 the identity), one coordinate per lane;
+// v holds this lane's coordinate of P and is clobbered
+template <class Q, class ATab>
+CMTV_HD void q_build_table_p3(const Q& q, ATab& tab, fe& v) {
+  const int lane = q.lane();
+  fe c1, z;
+  q_identity(z, lane);
+  tab.store(0, z);
+  tab.store(1, v);
+  q_to_cached(q, c1, v);
+  q_dbl(q, v);
+  tab.store(2, v);
+#pragma unroll 1
+  for (int e = 3; e <= 8; e++) {
+    q_add(q, v, c1);
+    tab.store(e, v);
+  }
+}
+
+// The helper's addend of one window for its signature (one per lane), from
+// the quads' tables read through rd(P, e, c, fe&) -- P = 0: A's extended
+// entries, 1: R's cached entries of -R; c = the coordinate, i.e. the quad
+// lane that stored it -- as the quads' cached coordinates (Y-X, Y+X, 2Z, 2dT)
+// in out[0..3]: S = [dA](-A) + [dR](r_flip ? R : -R). HWCD addition of an
+// extended and a cached point, then the cached form of the sum: 9
+// multiplications. Negating the extended operand swaps its (Y-X, Y+X) and
+// negates T; negating the cached one swaps which slot is read and negates
+// 2dT; the two T signs meet in C = T1 2dT2, so one sign decides whether C is
+// added to or subtracted from D (no negation is computed).
+template <class Rd>
+CMTV_HD void h_window_addend(fe out[4], const Rd& rd, int dA, int dR, bool r_flip) {
+  const int eA = dA < 0 ? -dA : dA, eR = dR < 0 ? -dR : dR;
+  const bool nA = dA < 0, nR = (dR < 0) != r_flip;
+  fe x, y, s, d, m;
+  rd(0, eA, 0, x);
+  rd(0, eA, 1, y);
+  fe_sub(d, y, x);  // Y - X
+  fe_add(s, y, x);  // Y + X
+  rd(1, eR, nR ? 1 : 0, m);
+  fe_select(x, d, s, nA);
+  fe_mul(x, x, m);  // A = (Y1 - X1)(Y2 - X2)
+  rd(1, eR, nR ? 0 : 1, m);
+  fe_select(y, s, d, nA);
+  fe_mul(y, y, m);  // B = (Y1 + X1)(Y2 + X2)
+  fe e, h, f, g;
+  fe_sub(e, y, x);  // E = B - A
+  fe_add(h, y, x);  // H = B + A
+  rd(0, eA, 3, x);
+  rd(1, eR, 3, m);
+  fe_mul(x, x, m);  // +/- C = T1 2dT2
+  rd(0, eA, 2, y);
+  rd(1, eR, 2, m);
+  fe_mul(y, y, m);  // D = Z1 2Z2
+  fe_add(s, y, x);  // D + C
+  fe_sub(d, y, x);  // D - C
+  const bool cneg = nA != nR;
+  fe_select(f, d, s, cneg);  // F = D - C
+  fe_select(g, s, d, cneg);  // G = D + C
+  fe X3, Y3, Z3, T3;
+  fe_mul(X3, e, f);
+  fe_mul(Y3, g, h);
+  fe_mul(Z3, f, g);
+  fe_mul(T3, e, h);
+  fe_sub(out[0], Y3, X3);
+  fe_add(out[1], Y3, X3);
+  fe_add(out[2], Z3, Z3);
+  fe_const_d2(m);
+  fe_mul(out[3], T3, m);
+}
+
+// The quad side of the helper-summed verifier: decode as q_verify_split, both
+// tables before get_prep (the scalars; flags bits 16..23 carry the window
+// count W the whole workgroup runs, else this quad's own), the top window
+// from the tables, then W - 1 windows of 4 doublings and get_s(win, c) (this
+// lane's cached coordinate of the helper's S_win), and get_b(c): the helper's
+// part of [u]B, comb positions 15..j0 (BComb16). The quads add positions
+// j0-1..0 themselves, digit j of u's radix-2^16 digits on the window the
+// remaining doublings scale to 2^16j -- j < 8 against (1..2^15)B on window 4j,
+// j >= 8 against (1..2^15)[2^120]B on window 4(j-8)+2 -- its row fetched
+// before the window's doublings.
+template <uint32_t MODE, class Q, class BTab, class ATab, class GetPrep, class GetS, class GetB>
+CMTV_HD bool q_verify_hs(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig_ptr, const BTab& btab, ATab& tabA,
+                         ATab& tabR, int j0, const GetPrep& get_prep, const GetS& get_s, const GetB& get_b) {
+  const int lane = q.lane();
+  uint32_t w[8];
+  const uint32_t* src = (lane & 1) ? sig_ptr : pk_ptr;
+#pragma unroll
+  for (int i = 0; i < 8; i++) w[i] = src[i];
+  fe v, rc;
+  bool a_ok, r_ok, r_canon;
+  {
+    ge_p3 P;
+    const bool dec = p3_frombytes(P, w);
+    const bool canon = y_is_canonical(w) && !(fe_iszero(P.X) && (w[7] >> 31));
+    fe x, y, t, one;
+    fe_1(one);
+    q.template perm<QP_B0>(x, P.X);
+    q.template perm<QP_B0>(y, P.Y);
+    q.template perm<QP_B0>(t, P.T);
+    fe_pick(v, lane, x, y, one, t);  // A
+    q.template perm<QP_B1>(x, P.X);
+    q.template perm<QP_B1>(y, P.Y);
+    q.template perm<QP_B1>(t, P.T);
+    fe_pick(rc, lane, x, y, one, t);  // R
+    a_ok = q.template perm32<QP_B0>(dec ? 1u : 0u) != 0;
+    r_ok = q.template perm32<QP_B1>(dec ? 1u : 0u) != 0;
+    r_canon = q.template perm32<QP_B1>(canon ? 1u : 0u) != 0;
+    // -A and -R: negate X (lane 0) and T (lane 3)
+    const bool xt = lane == 0 || lane == 3;
+    fe_neg(t, v);
+    fe_carry(t);
+    fe_select(v, v, t, xt);
+    fe_neg(t, rc);
+    fe_carry(t);
+    fe_select(rc, rc, t, xt);
+  }
+  q_build_table_p3(q, tabA, v);
+  q_build_table(q, tabR, rc);
+  SigPrep p;
+  get_prep(p);
+  const bool s_ok = (p.flags & 4u) != 0;
+  const bool r_flip = (p.flags & 1u) != 0;
+  const int W = (p.flags >> 16) & 0xFFu ? (int)((p.flags >> 16) & 0xFFu) : q_wave_windows(q, p.flags);
+  uint32_t tA[8], tR[8];
+  hs_digits16(tA, p.k1, W);
+  hs_digits16(tR, p.k2, W);
+  uint32_t tLo[8], tHi[8];
+  hs_digits65536(tLo, tHi, p.u);
+#pragma unroll 1
+  for (int j = 15; j >= j0; j--) sc_shift_out(j >= 8 ? tHi : tLo, 16);  // the helper's positions
+  fe c;
+  {
+    // the top window: v = [dA](-A) straight from A's table, + [dR](-/+R)
+    const int dA = (int)sc_shift_out(tA, 4) - 8;
+    const int dR = (int)sc_shift_out(tR, 4) - 8;
+    tabA.load(dA < 0 ? -dA : dA, v);
+    fe t;
+    fe_neg(t, v);
+    fe_carry(t);
+    fe_select(v, v, t, dA < 0 && (lane == 0 || lane == 3));
+    tabR.load_signed(q, dR < 0 ? -dR : dR, (dR < 0) != r_flip, c);
+    q_add(q, v, c);
+  }
+#pragma unroll 1
+  for (int win = W - 2; win >= 0; win--) {
+    const bool hi = (win & 2) != 0;
+    const bool has_b = (win & 1) == 0 && win <= 30 && (hi ? 8 : 0) + (win >> 2) < j0;
+    bool b_neg = false, b_ident = false;
+    fe cB;
+    if (has_b) {
+      const int dB = (int)sc_shift_out(hi ? tHi : tLo, 16) - 0x8000;
+      const int ib = dB < 0 ? -dB : dB;
+      const int row = BT16_BASE + (ib > 0 ? ib - 1 : 0) + (hi ? BT16_ENTRIES : 0);
+      q_niels_load(
+          q, cB, [&](int off, fe& r) { btab.load_coord(row, off, r); }, BTAB_COORD_WORDS, 2 * BTAB_COORD_WORDS,
+          dB < 0);
+      b_neg = dB < 0;
+      b_ident = ib == 0;
+    }
+#pragma unroll 1
+    for (int d = 0; d < 4; d++) q_dbl(q, v);
+    get_s(win, c);
+    q_add(q, v, c);
+    if (has_b) {
+      q_niels_fix(cB, lane, b_neg, b_ident);
+      q_add(q, v, cB);
+    }
+  }
+  get_b(c);
+  q_add(q, v, c);
+  if (MODE == MODE_ZIP215) {
+    const bool so = q_small_order(q, v);
+    return s_ok && a_ok && r_ok && so;
+  }
+  fe z;
+  q.template perm<QP_B2>(z, v);
+  const bool x0 = fe_iszero(v);
+  const bool yz = fe_equal(v, z);
   const bool e0 = q.template perm32<QP_B0>(x0 ? 1u : 0u) != 0;
   const bool e1 = q.template perm32<QP_B1>(yz ? 1u : 0u) != 0;
   return s_ok && a_ok && r_ok && r_canon && e0 && e1;

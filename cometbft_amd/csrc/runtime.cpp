@@ -415,6 +415,10 @@ struct cmtv_ctx {
   // waves per signature at or below row2_max: 4 (k_verify_row4_split) or 2
   // (CMTV_ROW_WAVES=2: k_verify_row2_split)
   uint32_t row_waves = 4;
+  // the quad split kernel's helper-summed form (k_verify_quad_hs); CMTV_QUAD_HS=0
+  // keeps k_verify_quad_split (the quads add both table entries themselves)
+  bool quad_hs = true;
+  uint32_t hs_tune = 0;  // CMTV_HS_PRE + 1 (bits 0..7); 0: the kernel's default
   size_t quad_split_max = kQuadSplitMaxDefault;
   size_t keyed_quad_max = kKeyedQuadMaxDefault;
   size_t lane_chunk = kChunk;         // signatures per lane-kernel launch (env CMTV_LANE_CHUNK)
@@ -618,6 +622,7 @@ static int enqueue_verify(cmtv_ctx* ctx, CmtvDev& D, size_t n, const uint8_t* d_
   const bool row2 = row && n <= ctx->row2_max;
   const uint32_t kflags = (quad ? kLaunchQuad : 0u) | (oct ? kLaunchOct : 0u) |
                           (oct_split ? kLaunchOctSplit : 0u) | (quad_split ? kLaunchQuadSplit : 0u) |
+                          (quad_split && ctx->quad_hs && !sr ? kLaunchQuadHS | (ctx->hs_tune << 16) : 0u) |
                           (row ? (row2 ? (ctx->row_waves == 4 ? kLaunchRow4 : kLaunchRow2) : kLaunchRow) : 0u) |
                           (ctx->force_wide ? kLaunchForceWide : 0u);
   hipError_t e = hipSuccess;
@@ -1290,6 +1295,8 @@ static void read_env(cmtv_ctx* ctx) {
   if (const char* rm = std::getenv("CMTV_KEYED_ROW_MAX"))
     ctx->keyed_row_max = (size_t)std::strtoull(rm, nullptr, 10);
   if (const char* rw = std::getenv("CMTV_ROW_WAVES")) ctx->row_waves = rw[0] == '2' ? 2u : 4u;
+  if (const char* qh = std::getenv("CMTV_QUAD_HS")) ctx->quad_hs = qh[0] != '0';
+  if (const char* hp = std::getenv("CMTV_HS_PRE")) ctx->hs_tune |= (uint32_t)(std::min(254, std::atoi(hp)) + 1) & 0xFFu;
   if (const char* os = std::getenv("CMTV_OCT_SPLIT_MAX")) ctx->oct_split_max = (size_t)std::strtoull(os, nullptr, 10);
   if (const char* qs = std::getenv("CMTV_QUAD_SPLIT_MAX")) ctx->quad_split_max = (size_t)std::strtoull(qs, nullptr, 10);
   if (const char* kq = std::getenv("CMTV_KEYED_QUAD_MAX")) ctx->keyed_quad_max = (size_t)std::strtoull(kq, nullptr, 10);

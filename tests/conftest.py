@@ -118,6 +118,14 @@ def _env_ctx(**env):
 
 
 @pytest.fixture(scope="session")
+def gpu_ctx_quad2s():
+    """Small Ed25519 batches on the helper-wave quad kernel whose quads add
+    both table entries of every window themselves (k_verify_quad_split,
+    CMTV_QUAD_HS=0) instead of its helper-summed form (k_verify_quad_hs)."""
+    return _env_ctx(CMTV_OCT_MAX=0, CMTV_QUAD_HS=0)
+
+
+@pytest.fixture(scope="session")
 def gpu_ctx_oct2():
     """Small Ed25519 batches on the two-wave oct kernel (CMTV_ROW_MAX=0)
     instead of the default one-signature-per-wave row kernel (row.h)."""

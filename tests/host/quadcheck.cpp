@@ -4,6 +4,7 @@
 //   stdin/stdout protocol as hostcheck.cpp (verify mode only).
 #define CMTV_HD inline
 #define CMTV_BOUNDS_CHECK 1
+#include <algorithm>
 #include <atomic>
 #include <cstdio>
 #include <cstring>
@@ -188,6 +189,12 @@ int main(int argc, char** argv) {
   // quad / oct verifier taking them through its callbacks
   const bool quad2 = argc > 1 && !strcmp(argv[1], "quad2");
   const bool oct2 = argc > 1 && !strcmp(argv[1], "oct2");
+  // argv[1] == "quad3": k_verify_quad_hs's path (quad.h q_verify_hs) -- the
+  // scalars, [u]B and every window's summed addend (h_window_addend over the
+  // four lanes' tables) computed once as its helper wave would; the window
+  // count is the signature's own raised by i % 3 (a workgroup's count can be
+  // any other signature's), 64 when wide
+  const bool quad3 = argc > 1 && !strcmp(argv[1], "quad3");
   std::vector<uint32_t> bcomb;
   std::map<std::string, std::pair<bool, std::vector<uint32_t>>> combs;
   if (keyed) {
@@ -238,7 +245,7 @@ int main(int argc, char** argv) {
       bpoint_store(bpt, Bp);
       k2_neg_count += (hp.flags & 1u) ? 1 : 0;
     }
-    if (quad2 || oct2) {
+    if (quad2 || oct2 || quad3) {
       if (mode)
         q_prepare<MODE_ZIP215>(hp, pkw, sigw, mp, mlen, false);
       else
@@ -278,6 +285,47 @@ int main(int argc, char** argv) {
           }
         });
     }
+    if (quad3) {
+      const bool wide = (hp.flags & 2u) != 0;
+      const int own = (int)((hp.flags >> 8) & 0xFFu);
+      const int W = wide ? HS_WIDE_WINDOWS : (own + (int)(i % 3) > HS_MAX_WINDOWS ? HS_MAX_WINDOWS : own + (int)(i % 3));
+      hp.flags |= (uint32_t)W << 16;
+      QArrayTab ta[4], tr[4];
+      fe S[4];
+      uint32_t tA[8], tR[8];
+      hs_digits16(tA, hp.k1, W);
+      hs_digits16(tR, hp.k2, W);
+      sc_shift_out(tA, 4);
+      sc_shift_out(tR, 4);
+      // the helper's part of [u]B: the top `pre` comb positions (0..16, by i)
+      const int pre = (int)(i % 17);
+      BComb16 bc;
+      bc.init(hp.u);
+      for (int k = 0; k < pre; k++) bc.step(bt);
+      uint32_t bpt3[40];
+      bpoint_store(bpt3, bc.P);
+      for (int l = 0; l < 4; l++)
+        th.emplace_back([&, l] {
+          HostQuad q{l, &ex};
+          auto get_s = [&](int win, fe& c) {
+            ex.bar.arrive_and_wait();  // every lane's tables are built
+            if (l == 0) {
+              const int dA = (int)sc_shift_out(tA, 4) - 8;
+              const int dR = (int)sc_shift_out(tR, 4) - 8;
+              auto rd = [&](int P, int e, int cc, fe& r) { r = (P == 0 ? ta[cc] : tr[cc]).t[e]; };
+              h_window_addend(S, rd, dA, dR, (hp.flags & 1u) != 0);
+            }
+            ex.bar.arrive_and_wait();
+            c = S[l];
+            (void)win;
+          };
+          auto get_b = [&](fe& c) {
+            for (int j = 0; j < 10; j++) c.v[j] = bpt3[10 * l + j];
+          };
+          res[l] = mode ? q_verify_hs<MODE_ZIP215>(q, pkw, sigw, bt, ta[l], tr[l], 16 - pre, get_prep, get_s, get_b)
+                        : q_verify_hs<MODE_GO_STDLIB>(q, pkw, sigw, bt, ta[l], tr[l], 16 - pre, get_prep, get_s, get_b);
+        });
+    }
     if (oct) {
       ex.bar.n = 8;
       for (int l = 0; l < 8; l++)
@@ -288,7 +336,7 @@ int main(int argc, char** argv) {
                         : o_verify<MODE_GO_STDLIB>(q, pkw, sigw, mp, mlen, bt, ta);
         });
     }
-    for (int l = 0; l < (oct || quad2 || oct2 || sr2 ? 0 : 4); l++)
+    for (int l = 0; l < (oct || quad2 || oct2 || sr2 || quad3 ? 0 : 4); l++)
       th.emplace_back([&, l] {
         HostQuad q{l, &ex};
         QArrayTab ta, tr;

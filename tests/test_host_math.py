@@ -168,7 +168,7 @@ def test_oct_pipeline_matches_corpus(quadcheck, corpus, mode):
     assert bad.size == 0, [(idx[int(i)], corpus["cats"][idx[int(i)]]) for i in bad[:10]]
 
 
-@pytest.mark.parametrize("kind", ["quad2", "oct2"])
+@pytest.mark.parametrize("kind", ["quad2", "oct2", "quad3"])
 @pytest.mark.parametrize("mode", [0, 1])
 def test_split_pipelines_match_corpus(quadcheck, corpus, mode, kind):
     """The helper-wave kernels' path: scalars and [u]B (the 16-position

@@ -72,10 +72,10 @@ def _mixed_batch(kind, waves_per_vector=1, seed=3):
     return np.array(pk), np.array(sig), m2, off2
 
 
-@pytest.mark.parametrize("kernel", ["row4", "row2", "row", "oct2", "oct", "quad2", "quad", "lane"])
+@pytest.mark.parametrize("kernel", ["row4", "row2", "row", "oct2", "oct", "quad2", "quad2s", "quad", "lane"])
 @pytest.mark.parametrize("mode", [MODE_GO_STDLIB, MODE_ZIP215])
-def test_ed25519_wide_in_mixed_waves(gpu_ctx_row4, gpu_ctx_row2, gpu_ctx_row, gpu_ctx_oct2, gpu_ctx_oct1, gpu_ctx_quad, gpu_ctx_quad1, gpu_ctx_lane, kernel, mode):
-    ctx = {"row4": gpu_ctx_row4, "row2": gpu_ctx_row2, "row": gpu_ctx_row, "oct2": gpu_ctx_oct2, "oct": gpu_ctx_oct1, "quad2": gpu_ctx_quad, "quad": gpu_ctx_quad1,
+def test_ed25519_wide_in_mixed_waves(gpu_ctx_row4, gpu_ctx_row2, gpu_ctx_row, gpu_ctx_oct2, gpu_ctx_oct1, gpu_ctx_quad, gpu_ctx_quad2s, gpu_ctx_quad1, gpu_ctx_lane, kernel, mode):
+    ctx = {"row4": gpu_ctx_row4, "row2": gpu_ctx_row2, "row": gpu_ctx_row, "oct2": gpu_ctx_oct2, "oct": gpu_ctx_oct1, "quad2": gpu_ctx_quad, "quad2s": gpu_ctx_quad2s, "quad": gpu_ctx_quad1,
            "lane": gpu_ctx_lane}[kernel]
     pk, sig, m, off = _mixed_batch("ed25519")
     exp = coracle.verify_batch(pk, sig, m, off, mode, nthreads=8)

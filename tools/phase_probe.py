@@ -6,7 +6,9 @@
 
 Lane 0 of every wave records the shader clock at kernel entry (0), before /
 after barrier 1 (1, 2: the helper's scalars), before / after barrier 2 (3, 4:
-the helper's [u]B) and, for the quad waves, at exit (5). Printed per mode:
+the helper's [u]B) and, for the quad waves, at exit (5); in the helper-summed
+kernel (k_verify_quad_hs) slot 6 holds the cycles each wave waited at the
+per-window barriers. Printed per mode:
 the spread of workgroup starts, and for the workgroup that ends last and the
 median workgroup, when the helper and the quad waves reach each barrier --
 which of them waits, and for how long.
@@ -50,8 +52,12 @@ def main():
         buf = np.zeros(wgs * 4 * SLOTS, np.uint64)
         assert fn(buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), buf.size) == 0
         st = buf.reshape(wgs, 4, SLOTS).astype(np.int64)
-        t0 = st[:, :, 0].min()
-        st = st - t0
+        waits = st[:, :, 6].copy()  # k_verify_quad_hs: cycle counts, not stamps
+        # each workgroup against its own first entry: s_memtime counters of
+        # different XCDs are not synchronised, so cross-workgroup offsets of
+        # the shader clock mean nothing
+        t0 = st[:, :, 0].min(axis=1)
+        st = st - t0[:, None, None]
         q, h = st[:, :3, :], st[:, 3, :]
         end = q[:, :, 5].max(axis=1)
         start = st[:, :, 0].min(axis=1)
@@ -79,6 +85,10 @@ def main():
             "quad_b1_median": float(np.median(q[:, :, 1] - start[:, None])),
             "quad_b2_median": float(np.median(q[:, :, 3] - start[:, None])),
             "quad_end_median": float(np.median(q[:, :, 5] - start[:, None])),
+            # k_verify_quad_hs (slot 6): cycles waited at the per-window barriers
+            "hs_helper_window_wait_median": float(np.median(waits[:, 3])),
+            "hs_quad_window_wait_median": float(np.median(waits[:, :3])),
+            "hs_quad_window_wait_last_wg": [int(x) for x in waits[last, :3]],
             "last_wg": dict(wg(last), index=last), "median_wg": dict(wg(med), index=med),
         }
         print(name, json.dumps(out[name]), flush=True)

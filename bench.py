@@ -805,7 +805,7 @@ def verify_commit_10k(ctx, mode, iters, host_api_ms=None):
     res = {"n_validators": 10_000, "iters": iters, "p50_ms": p50, "p99_ms": p99, "kernel_ms": round(kms, 4),
            "value": round(10_000 / p50 * 1e3, 1), "unit": "verifs/s",
            "path": "cmtv_verify_commit (C ABI, commit packed once): plan + pinned staging + device sign-bytes + "
-                   "k_verify_quad_split + VerifyCommit replay"}
+                   "k_verify_quad_hs + VerifyCommit replay"}
     if host_api_ms:
         res["over_host_api"] = round(p50 / host_api_ms, 3)
     del keep
@@ -859,11 +859,11 @@ def latency_150(ctx, mode, iters):
 
 # The PMC summaries of THIS round's tree (tools/gpu_prof_r04.sh: rocprofv3
 # --pmc passes over the quick form of this bench command)
-PMC_SQ = "r04_pmc_sq.json"
-PMC_TRAFFIC = "r04_traffic.json"
+PMC_SQ = "r04b_pmc_sq.json"
+PMC_TRAFFIC = "r04b_traffic.json"
 
 
-def load_valu_busy(n=10_000, kernel="k_verify_quad_split<0u>"):
+def load_valu_busy(n=10_000, kernel="k_verify_quad_hs<0u>"):
     """VALUBusy (SQ_ACTIVE_INST_VALU-based, chip-wide) of the bench's verify
     kernel at the step's size, from the committed PMC summary of the bench
     command (profiles/PMC_SQ, tools/pmc_summary.py)."""

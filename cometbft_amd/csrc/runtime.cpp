@@ -434,7 +434,7 @@ struct cmtv_ctx {
   bool fault_pending = false;  // the last failure was CMTV_FAULT_AT's
   // RCCL options read at open (CMTV_FORCE_RCCL, CMTV_NO_RCCL) and the
   // library to load (CMTV_RCCL_LIB; empty: the system librccl)
-  bool force_rccl = false, no_rccl = false;
+  bool force_rccl = false, no_rccl = false, no_rccl_fallback = false;
   std::string rccl_lib;
   // CMTV_FORCE_WIDE: quad kernels take the 64-window half-scalar fallback
   bool force_wide = false;
@@ -771,15 +771,21 @@ static int gather_bitmaps(cmtv_ctx* ctx, const size_t* dev, size_t G, size_t W, 
   ctx->stats.gathers++;
   if (ctx->rccl) {
     const Rccl& R = rccl(ctx->rccl_lib);
-    if (R.GroupStart() != 0) return CMTV_ERCCL;
-    int bad = 0;
-    for (size_t g = 0; g < G; g++) {
+    int bad = R.GroupStart() != 0;
+    for (size_t g = 0; g < G && !bad; g++) {
       CmtvDev& D = ctx->devs[dev[g]];
       (void)hipSetDevice(D.ordinal);
       bad |= R.AllGather(bufs[g] + g * W, bufs[g], W, kNcclUint64, D.comm, D.stream) != 0;
     }
-    if (R.GroupEnd() != 0 || bad) return CMTV_ERCCL;
-    return CMTV_OK;
+    bad |= R.GroupEnd() != 0;
+    if (!bad) return CMTV_OK;
+    // RCCL refused the gather (a node whose xGMI / RCCL setup fails at run
+    // time): this gather and every later one take the peer copies below,
+    // which need no communicator; CMTV_NO_RCCL_FALLBACK=1 reports it instead
+    ctx->stats.rccl_failures++;
+    if (ctx->no_rccl_fallback) return CMTV_ERCCL;
+    ctx->rccl = false;
+    ctx->stats.rccl = 0;
   }
   hipError_t e;
   for (size_t h = 0; h < G; h++) {
@@ -1331,6 +1337,7 @@ static void read_env(cmtv_ctx* ctx) {
   ctx->force_rccl = std::getenv("CMTV_FORCE_RCCL") != nullptr;
   if (const char* rl = std::getenv("CMTV_RCCL_LIB")) ctx->rccl_lib = rl;
   ctx->no_rccl = std::getenv("CMTV_NO_RCCL") != nullptr;
+  ctx->no_rccl_fallback = std::getenv("CMTV_NO_RCCL_FALLBACK") != nullptr;
 }
 
 // The bitmap communicator over the live devices (rank = position in

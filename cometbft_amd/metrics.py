@@ -46,6 +46,8 @@ _FIELDS = [
     ("live_devices", "live_devices", "gauge", "Devices still taking work."),
     ("timed_calls", "timed_calls_total", "counter",
      "Calls whose kernel time device_seconds holds (CMTV_TIMING samples one call in N per device)."),
+    ("rccl_failures", "rccl_failures_total", "counter",
+     "RCCL bitmap all-gathers that failed and fell back to peer copies."),
 ]
 
 

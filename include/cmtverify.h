@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define CMTV_ABI_VERSION 8
+#define CMTV_ABI_VERSION 9
 
 enum {
   CMTV_OK = 0,
@@ -102,6 +102,10 @@ typedef struct cmtv_stats {
   uint32_t live_devices;     /* devices still taking work                 */
   uint32_t reserved;
   uint64_t timed_calls;      /* calls whose kernel time device_ms holds   */
+  uint64_t rccl_failures;    /* RCCL all-gathers that failed; that gather
+                              and every later one of the context used peer
+                              copies (rccl drops to 0) unless
+                              CMTV_NO_RCCL_FALLBACK is set               */
 } cmtv_stats;
 
 /* One device's share of the context's work (cmtv_device_stats_get). */
@@ -142,7 +146,13 @@ typedef struct cmtv_device_stats {
  * instead of the system librccl; with CMTV_FORCE_RCCL a repeated ordinal then
  * gets a multi-rank communicator: the one-GPU rehearsal of the RCCL path with
  * tests/host/librccl_stub.so), CMTV_ROW_FENCE=0 (test knob: no fence on the
- * row kernels' bitmap ring, see cmtv_verify_ed25519_device). */
+ * row kernels' bitmap ring, see cmtv_verify_ed25519_device),
+ * CMTV_NO_RCCL_FALLBACK=1 (a failed RCCL all-gather returns CMTV_ERCCL
+ * instead of switching the context to peer copies), CMTV_QUAD_HS=0 (the
+ * quad kernel's quads add both table entries of a window themselves:
+ * k_verify_quad_split instead of k_verify_quad_hs), CMTV_HS_PRE=k (tuning:
+ * the helper-summed kernel's helper adds the top k of [u]B's 16 comb
+ * positions, default 6). */
 int cmtv_open(const cmtv_config* cfg, cmtv_ctx** out);
 
 /* Opens ONE context over several devices (a node is one

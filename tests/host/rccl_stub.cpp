@@ -48,6 +48,8 @@ struct Group {
   int live;
   std::vector<int> devs;
   std::string log;  // CMTV_RCCL_STUB_LOG as it was at ncclCommInitAll
+  int fail_at = 0;  // CMTV_RCCL_STUB_FAIL_GROUP: this group end (1-based) fails
+  int ends = 0;
 };
 struct Op {
   const void* send;
@@ -159,6 +161,7 @@ int ncclCommInitAll(void** comms, int ndev, const int* devlist) {
   std::lock_guard<std::mutex> lk(mu);
   const char* path = std::getenv("CMTV_RCCL_STUB_LOG");
   auto* g = new Group{next_id++, ndev, ndev, std::vector<int>(devlist, devlist + ndev), path ? path : ""};
+  if (const char* f = std::getenv("CMTV_RCCL_STUB_FAIL_GROUP")) g->fail_at = std::atoi(f);
   std::string devs;
   for (int i = 0; i < ndev; i++) {
     comms[i] = new Comm{g, i, devlist[i]};
@@ -189,6 +192,16 @@ int ncclGroupEnd() {
   if (--depth > 0) return 0;
   std::vector<Op> ops;
   ops.swap(pending);
+  if (!ops.empty()) {
+    // CMTV_RCCL_STUB_FAIL_GROUP=k: the communicator's k-th grouped call fails
+    // as a broken node's would (ncclSystemError), with nothing copied
+    Group* g = ops[0].comm->g;
+    std::lock_guard<std::mutex> lk(mu);
+    if (g->fail_at && ++g->ends == g->fail_at) {
+      log_line(g->log, "groupend failed comm=" + std::to_string(g->id));
+      return 2;
+    }
+  }
   return run_ops(ops);
 }
 

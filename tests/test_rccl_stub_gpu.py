@@ -17,6 +17,9 @@ Checked here, against the oracle (oracle/liboracle.so):
     after it): the communicator is destroyed and rebuilt over the survivors
     with ranks renumbered by live position, and the retried batch gathers
     over G - 1 ranks;
+  * a node whose RCCL refuses a gather at run time (the stub's
+    CMTV_RCCL_STUB_FAIL_GROUP): that gather and every later one fall back to
+    peer copies, verdicts stay exact, cmtv_stats.rccl_failures counts it;
   * after device 0 is retired, the single-device device-resident
     entry points return CMTV_ENODEV instead of launching on it (key
     generation, which takes host buffers, moves to a live device).
@@ -186,6 +189,38 @@ def test_rccl_rebuild_after_device_failure(tmp_path, knob, bad):
     assert len(_inits(_log(log))) == 2
     if bad == 0:
         _assert_dev0_calls_refused(ctx, pk, kidx, sig, m, off)
+
+
+@pytest.mark.parametrize("G", [2, 8])
+def test_rccl_gather_failure_falls_back_to_peer_copies(tmp_path, monkeypatch, G):
+    """The first grouped all-gather fails: the batch still gives the oracle's
+    verdicts (peer copies), rccl drops to 0, rccl_failures = 1, and later
+    batches never call RCCL again; CMTV_NO_RCCL_FALLBACK=1 reports CMTV_ERCCL
+    instead."""
+    log = tmp_path / "rccl.log"
+    monkeypatch.setenv("CMTV_RCCL_STUB_FAIL_GROUP", "1")
+    ctx = _stub_ctx(G, log)
+    assert ctx.stats()["rccl"] == 1
+    n = 64 * 21 * G + 3
+    pk, kidx, sig, m, off = _batch(n, 2000 + G, flip=0.05)
+    for mode in (MODE_GO_STDLIB, MODE_ZIP215):
+        exp = coracle.verify_batch(pk[kidx], sig, m, off, mode, nthreads=16)
+        got, words = ctx.verify(pk[kidx], sig, m, off, mode, bitmap=True)
+        assert np.array_equal(got, exp), np.nonzero(got != exp)[0][:10]
+        assert np.array_equal(np.unpackbits(words.view(np.uint8), bitorder="little")[:n], exp)
+    st = ctx.stats()
+    assert st["rccl"] == 0 and st["rccl_failures"] == 1 and st["gathers"] == 2
+    lines = _log(log)
+    assert sum(1 for x in lines if x.startswith("groupend failed")) == 1
+    assert not _gathers(lines)  # nothing went through the stub's copies
+    ctx.close()
+    log2 = tmp_path / "rccl2.log"
+    monkeypatch.setenv("CMTV_RCCL_STUB_LOG", str(log2))
+    ctx = _stub_ctx(G, log2, CMTV_NO_RCCL_FALLBACK=1)
+    with pytest.raises(RuntimeError):
+        ctx.verify(pk[kidx], sig, m, off, MODE_GO_STDLIB)
+    assert ctx.stats()["rccl_failures"] == 1
+    ctx.close()
 
 
 def _assert_dev0_calls_refused(ctx, pk, kidx, sig, m, off):

@@ -38,8 +38,10 @@ Extra fields on the JSON line:
                     bisection (LightTrusting + Light to the tip)
   replay_c3      -- configs[2]: 100k commits x 150 validators (15M signatures)
                     sharded by height over the N devices (strong scaling),
-                    registered-key kernel + RCCL bitmap all-gather, 1% flipped
-                    signatures checked exactly; own roofline; generic kernel beside it
+                    registered-key kernel (radix-256 key combs, [s]B over B's
+                    radix-2^16 comb) + RCCL bitmap all-gather, 1% flipped
+                    signatures checked exactly; own roofline; the radix-2^16 key
+                    combs and the generic kernel beside it
   sr25519        -- configs[4]: 10k sr25519 verifications per step (N=1 only)
 Run: python bench.py [--gpus N --steps K --warmup W]
 """
@@ -58,9 +60,11 @@ sys.path.insert(0, ROOT)
 
 METRIC = "Ed25519 verifs/sec at 1/2/4/8 GPUs + p50 VerifyCommit latency, 150 vals"
 MACS_PER_VERIFY = 300_000          # 3,000 field mults x 100 limb MACs
-# registered-key verification (keyed.h): 64 comb additions (7 field mults each
-# in the one-lane form) + decode R (~265) + final check (~8) = 721 field mults
-MACS_PER_KEYED_VERIFY = 72_100
+# registered-key verification by the keyed quad kernel (keyed_quad.h,
+# q_verify_keyed_split<MODE, true>): 32 key-comb + 16 B-comb additions (7 field
+# mults each in the one-lane form) + decode R (~265) + final check (~8) = 609
+# field mults (721 before round 4, with B over its radix-256 comb: 64 additions)
+MACS_PER_KEYED_VERIFY = 60_900
 # the same over the radix-2^16 key combs (CMTV_KEYS_WIDE) in GO_STDLIB with 8
 # signatures per lane sharing one inversion (k_verify_keyed_batch<0, 8, 2>):
 # 32 additions x 7 + 265 / 8 + 3 (batch products) + 2 (x, y) = 262 field mults
@@ -69,6 +73,11 @@ MACS_PER_KEYED_WIDE_GO_VERIFY = 26_200
 # (verify_core.h zip_coset): 32 additions x 7 + R' + T8 (6) + y_R Z, iX, iY on
 # two bases (6) + 265 / 8 + 3 (batch products) + 1 (x) = 273 field mults
 MACS_PER_KEYED_WIDE_ZIP_VERIFY = 27_300
+# configs[2]'s primary path (round 4): the keys' radix-256 combs (32 additions)
+# with [s]B over the B table's radix-2^16 comb (16), batched inversion as above:
+# 48 x 7 + 265 / 8 + 5 = 374 field mults (Go); ZIP-215 48 x 7 + 12 + 265 / 8 + 4 = 385
+MACS_PER_KEYED_MIXED_GO_VERIFY = 37_400
+MACS_PER_KEYED_MIXED_ZIP_VERIFY = 38_500
 INT_MAC_PEAK_T = 33.0              # measured v_mad_u64_u32 lane-ops/s, 1e12 (profiles/r01_int_rates.txt)
 
 
@@ -645,16 +654,18 @@ def c3_line(ctx, n_dev, mode, steps=3, n_heights=100_000, n_vals=150):
                 ok = ok and np.array_equal(P.unpack_bitmap(allw[h], ns[h]), exp[h])
         return ok
 
-    # the radix-256 combs first (the keyset cache's form), for comparison
-    el, kms_256 = timed_steps(ctx, lambda: keyed(ks256), steps, 1, lambda: None)
-    t_256 = el / steps
+    # the primary path: the keys' radix-256 combs (512 KiB per key, the keyset
+    # cache's form) with [s]B over the B table's radix-2^16 comb (kCombMixed)
+    el, kms_keyed = timed_steps(ctx, lambda: keyed(ks256), steps, 1, lambda: None)
+    t_keyed = el / steps
+    run_keyed = dict(LAST_RUN)
     ok = check()
     ks256.free()
     for s in shards:
         s["bm"].zero_()
-    el, kms_keyed = timed_steps(ctx, lambda: keyed(ks), steps, 1, lambda: None)
-    t_keyed = el / steps
-    run_keyed = dict(LAST_RUN)
+    # the radix-2^16 key combs beside it (64 MiB per key)
+    el, kms_wide = timed_steps(ctx, lambda: keyed(ks), steps, 1, lambda: None)
+    t_wide = el / steps
     ok = ok and check()
     for s in shards:
         s["bm"].zero_()
@@ -676,22 +687,29 @@ def c3_line(ctx, n_dev, mode, steps=3, n_heights=100_000, n_vals=150):
     per_dev = total / n_dev
     # algorithmic work of the path that ran (ZIP-215 decodes R instead of the
     # batched inversion: the radix-256 figure's decode term, with 32 additions)
-    macs = MACS_PER_KEYED_WIDE_GO_VERIFY if mode == 0 else MACS_PER_KEYED_WIDE_ZIP_VERIFY
-    work = ("32 comb additions x 7 + inversion / 8 + 5 + check, x 100" if mode == 0
-            else "32 comb additions x 7 + coset check 12 + inversion / 8 + 4, x 100")
+    macs = MACS_PER_KEYED_MIXED_GO_VERIFY if mode == 0 else MACS_PER_KEYED_MIXED_ZIP_VERIFY
+    work = ("48 comb additions (32 key, 16 B) x 7 + inversion / 8 + 5, x 100" if mode == 0
+            else "48 comb additions (32 key, 16 B) x 7 + coset check 12 + inversion / 8 + 4, x 100")
+    macs_wide = MACS_PER_KEYED_WIDE_GO_VERIFY if mode == 0 else MACS_PER_KEYED_WIDE_ZIP_VERIFY
     ach = per_dev / (kms_keyed * 1e-3) * macs / 1e12 if kms_keyed > 0 else None
     return {"workload": f"configs[2]: {n_heights} commits x {n_vals} validators = {total} signatures, "
                         f"sharded by height over {n_dev} GPU(s), 1% bit-flipped (seed 42)",
             "scaling": "strong", "sigs_per_gpu": int(per_dev), "value": round(total / t_keyed, 1), "unit": "verifs/s",
             "ms_per_pass": round(t_keyed * 1e3, 3), "steps": steps,
-            "path": "registered keys, radix-2^16 combs (cmtv_register_keys_ex CMTV_KEYS_WIDE, "
-                    "cmtv_verify_ed25519_indexed_sharded_device) + RCCL all-gather of bitmaps",
-            "kernel_ms_per_device": round(kms_keyed, 3), "register_wide_s": round(t_reg, 3),
-            "roofline": {"bound": "valu_int", "work": f"{macs} int32 MACs/keyed verify ({work}); SHA-512 and "
-                                                      "table loads not counted",
+            "path": "registered keys: radix-256 key combs (512 KiB per key, cmtv_register_keys) with [s]B over "
+                    "the B table's radix-2^16 comb (keyed_lane.hip kCombMixed, 8 signatures per lane sharing one "
+                    "inversion), cmtv_verify_ed25519_indexed_sharded_device + RCCL all-gather of bitmaps",
+            "kernel_ms_per_device": round(kms_keyed, 3),
+            "roofline": {"bound": "valu_int", "work": f"{macs} int32 MACs/keyed verify ({work}); a path-specific "
+                                                      "count (the headline's 300k is the generic path's); SHA-512 "
+                                                      "and table loads not counted",
                          "achieved": round(ach, 3) if ach else None, "peak": INT_MAC_PEAK_T, "unit": "TMAC/s",
                          "frac": round(ach / INT_MAC_PEAK_T, 4) if ach else None},
-            "comb256_value": round(total / t_256, 1), "comb256_kernel_ms_per_device": round(kms_256, 3),
+            "wide_value": round(total / t_wide, 1), "wide_kernel_ms_per_device": round(kms_wide, 3),
+            "wide_frac": round(per_dev / (kms_wide * 1e-3) * macs_wide / 1e12 / INT_MAC_PEAK_T, 4)
+            if kms_wide > 0 else None,
+            "wide_path": "radix-2^16 key combs (64 MiB per key, cmtv_register_keys_ex CMTV_KEYS_WIDE: 32 additions, "
+                         "rows from HBM staged by LDS-DMA)", "register_wide_s": round(t_reg, 3),
             "generic_value": round(total / t_generic, 1), "generic_ms_per_pass": round(t_generic * 1e3, 3),
             "generic_frac": round(per_dev / (kms_generic * 1e-3) * MACS_PER_VERIFY / 1e12 / INT_MAC_PEAK_T, 4)
             if kms_generic > 0 else None,

@@ -72,18 +72,19 @@ hipError_t launch_verify_keyed(uint32_t mode, uint32_t n, uint32_t n_keys, const
                                const uint32_t* ktabs, const uint32_t* bcomb, void* valid, void* bitmap,
                                bool quad, bool split, uint32_t k_wait, uint32_t* diag, uint32_t batch_kb,
                                uint32_t* scr, const uint32_t* wtabs, const uint32_t* btab, bool wide_dma,
-                               hipStream_t s, uint32_t* row_slot = nullptr);
+                               hipStream_t s, uint32_t* row_slot = nullptr, bool mixed = true);
 // (row_slot set: the keyed row kernel, k_verify_keyed_row_split, one
 // signature per workgroup; a slot of the device's bitmap ring)
 // the one-signature-per-lane part of launch_verify_keyed (keyed_lane.hip):
 // over the wide combs wtabs (rows staged by LDS-DMA when dma) or, with wtabs
-// null, the radix-256 combs ktabs / bcomb
+// null, the radix-256 key combs ktabs with B over btab's radix-2^16 comb
+// (mixed) or over its radix-256 comb bcomb
 hipError_t launch_verify_keyed_lane(uint32_t mode, uint32_t n, uint32_t n_keys, const uint32_t* ki,
                                     const uint32_t* sgp, const uint8_t* mp, const uint32_t* op,
                                     const uint32_t* keys_pk, const uint8_t* keys_ok, const uint32_t* ktabs,
                                     const uint32_t* bcomb, uint8_t* vp, uint64_t* bp, uint32_t batch_kb,
                                     uint32_t* scr, const uint32_t* wtabs, const uint32_t* btab, bool dma,
-                                    hipStream_t s);
+                                    bool mixed, hipStream_t s);
 // Wide (radix-2^16) combs of n_keys keys (keyed.h): bases = n_keys x 16 x 40
 // words, scratch = n_keys x kWideScratchWordsPerKey words.
 constexpr size_t kWideTableWords = (size_t)16 * 32768 * 32;  // 64 MiB per key

@@ -1293,12 +1293,13 @@ hipError_t launch_comb_build(uint32_t n_keys, const void* keys_pk, uint8_t* keys
 // counts itself in diag[kDiagLateK] (cmtv_stats.late_k_waves). k_wait = 0
 // (the CMTV_FORCE_K_LATE test knob) skips the flag entirely, so every quad
 // wave takes that path.
-template <uint32_t MODE>
+template <uint32_t MODE, bool B16>
 __global__ __launch_bounds__(320, 1) void k_verify_keyed_quad_split(
     uint32_t n, uint32_t n_keys, const uint32_t* __restrict__ key_idx, const uint32_t* __restrict__ sig,
     const uint8_t* __restrict__ msg, const uint32_t* __restrict__ off, const uint32_t* __restrict__ keys_pk,
     const uint8_t* __restrict__ keys_ok, const uint32_t* __restrict__ ktabs, const uint32_t* __restrict__ bcomb,
-    uint8_t* __restrict__ out_valid, uint64_t* __restrict__ out_bitmap, uint32_t k_wait, uint32_t* __restrict__ diag) {
+    uint8_t* __restrict__ out_valid, uint64_t* __restrict__ out_bitmap, uint32_t k_wait, uint32_t* __restrict__ diag,
+    const uint32_t* __restrict__ btab) {
   const uint32_t wave = threadIdx.x >> 6, t = threadIdx.x & 63;
   const uint32_t base = blockIdx.x * 48;
   __shared__ uint32_t tks[48][9];
@@ -1349,7 +1350,7 @@ __global__ __launch_bounds__(320, 1) void k_verify_keyed_quad_split(
   kid = kin ? kid : 0;
   DevQuad q;
   const int lane = (int)(t & 3);
-  bool v = q_verify_keyed_split<MODE>(
+  bool v = q_verify_keyed_split<MODE, B16>(
       q, kin && keys_ok[kid] != 0, sig + 16 * (size_t)i, ktabs + (size_t)kid * COMB_TABLE_WORDS, bcomb,
       [&](uint32_t tk[8]) {
         // the hash helper's flag, polled at most k_wait times (a wave never
@@ -1379,7 +1380,8 @@ __global__ __launch_bounds__(320, 1) void k_verify_keyed_quad_split(
 #pragma unroll
         for (int j = 0; j < 10; j++) rc.v[j] = lane == 2 ? (j == 0 ? 1u : 0u) : p[j];
         r_ok = rpt[ls][30] != 0;
-      });
+      },
+      DevBTabQ{btab});
   v = v && active;
   if (active && (t & 3) == 0 && out_valid) out_valid[s] = v ? 1 : 0;
   uint64_t x = __ballot(v && (t & 3) == 0) & 0x1111111111111111ull;
@@ -1396,7 +1398,7 @@ hipError_t launch_verify_keyed(uint32_t mode, uint32_t n, uint32_t n_keys, const
                                const uint32_t* ktabs, const uint32_t* bcomb, void* valid, void* bitmap,
                                bool quad, bool split, uint32_t k_wait, uint32_t* diag, uint32_t batch_kb,
                                uint32_t* scr, const uint32_t* wtabs, const uint32_t* btab, bool wide_dma,
-                               hipStream_t s, uint32_t* row_slot) {
+                               hipStream_t s, uint32_t* row_slot, bool mixed) {
   if (n == 0) return hipSuccess;
   auto ki = static_cast<const uint32_t*>(key_idx);
   auto sgp = static_cast<const uint32_t*>(sig);
@@ -1418,12 +1420,22 @@ hipError_t launch_verify_keyed(uint32_t mode, uint32_t n, uint32_t n_keys, const
   if (quad && split) {
     const uint32_t slices = 4 * ((n + 63) / 64);
     const dim3 grid((slices + 2) / 3), block(320);
-    if (mode == MODE_ZIP215)
-      hipLaunchKernelGGL(k_verify_keyed_quad_split<MODE_ZIP215>, grid, block, 0, s, n, n_keys, ki, sgp, mp, op,
-                         keys_pk, keys_ok, ktabs, bcomb, vp, bp, k_wait, diag);
-    else
-      hipLaunchKernelGGL(k_verify_keyed_quad_split<MODE_GO_STDLIB>, grid, block, 0, s, n, n_keys, ki, sgp, mp, op,
-                         keys_pk, keys_ok, ktabs, bcomb, vp, bp, k_wait, diag);
+    // [s]B over the B table's radix-2^16 comb (16 additions) unless the
+    // caller asked for the radix-256 comb (CMTV_KEYED_MIXED=0: 32)
+    if (mixed && btab) {
+      if (mode == MODE_ZIP215)
+        hipLaunchKernelGGL((k_verify_keyed_quad_split<MODE_ZIP215, true>), grid, block, 0, s, n, n_keys, ki, sgp, mp,
+                           op, keys_pk, keys_ok, ktabs, bcomb, vp, bp, k_wait, diag, btab);
+      else
+        hipLaunchKernelGGL((k_verify_keyed_quad_split<MODE_GO_STDLIB, true>), grid, block, 0, s, n, n_keys, ki, sgp,
+                           mp, op, keys_pk, keys_ok, ktabs, bcomb, vp, bp, k_wait, diag, btab);
+    } else if (mode == MODE_ZIP215) {
+      hipLaunchKernelGGL((k_verify_keyed_quad_split<MODE_ZIP215, false>), grid, block, 0, s, n, n_keys, ki, sgp, mp,
+                         op, keys_pk, keys_ok, ktabs, bcomb, vp, bp, k_wait, diag, btab);
+    } else {
+      hipLaunchKernelGGL((k_verify_keyed_quad_split<MODE_GO_STDLIB, false>), grid, block, 0, s, n, n_keys, ki, sgp,
+                         mp, op, keys_pk, keys_ok, ktabs, bcomb, vp, bp, k_wait, diag, btab);
+    }
     return hipGetLastError();
   }
   if (quad) {
@@ -1437,7 +1449,7 @@ hipError_t launch_verify_keyed(uint32_t mode, uint32_t n, uint32_t n_keys, const
     return hipGetLastError();
   }
   return launch_verify_keyed_lane(mode, n, n_keys, ki, sgp, mp, op, keys_pk, keys_ok, ktabs, bcomb, vp, bp, batch_kb,
-                                  scr, wtabs, btab, wide_dma, s);
+                                  scr, wtabs, btab, wide_dma, mixed, s);
 }
 
 hipError_t launch_pubkey(uint32_t n, const void* seeds, const uint32_t* btab, void* out_pk, hipStream_t s) {

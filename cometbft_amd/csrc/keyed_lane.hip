@@ -12,7 +12,10 @@
 // addition ahead by LDS-DMA (global_load_lds_dwordx4), so the HBM latency of
 // the next rows overlaps the current addition instead of stalling it
 // (profiles/r03_c3w_pmc_sq.txt: the plain wide kernel waits on memory 38 % of
-// its wave cycles at two waves per SIMD, the register file being full).
+// its wave cycles at two waves per SIMD, the register file being full);
+// kCombMixed = the keys' radix-256 combs with B over the B table's radix-2^16
+// comb (48 additions: keyed.h keyed_comb_mixed), for key sets without wide
+// combs (too many keys for 64 MiB each).
 #include <hip/hip_runtime.h>
 
 #include "devtables.h"
@@ -25,7 +28,7 @@
 
 namespace cmtv {
 
-enum { kComb256 = 0, kCombWide = 1, kCombWideDma = 2 };
+enum { kComb256 = 0, kCombWide = 1, kCombWideDma = 2, kCombMixed = 3 };
 
 // ---------------------------------------------------------------- LDS staging
 //
@@ -153,6 +156,9 @@ __device__ __forceinline__ bool keyed_comb_dev(ge_p3& acc, uint32_t kid, bool ke
   if (COMB == kCombWide)
     return keyed_comb_wide<DevCombWindow>(acc, keys_pk + 8 * (size_t)kid, key_ok, sig_ptr, msg, mlen,
                                           ktabs + (size_t)kid * WIDE_TABLE_WORDS, DevBTab{bcomb});
+  if (COMB == kCombMixed)
+    return keyed_comb_mixed<DevCombWindow>(acc, keys_pk + 8 * (size_t)kid, key_ok, sig_ptr, msg, mlen,
+                                           ktabs + (size_t)kid * COMB_TABLE_WORDS, DevBTab{bcomb});
   return keyed_comb<DevCombWindow>(acc, keys_pk + 8 * (size_t)kid, key_ok, sig_ptr, msg, mlen,
                                    ktabs + (size_t)kid * COMB_TABLE_WORDS, bcomb);
 }
@@ -337,13 +343,15 @@ hipError_t launch_verify_keyed_lane(uint32_t mode, uint32_t n, uint32_t n_keys, 
                                     const uint32_t* keys_pk, const uint8_t* keys_ok, const uint32_t* ktabs,
                                     const uint32_t* bcomb, uint8_t* vp, uint64_t* bp, uint32_t batch_kb,
                                     uint32_t* scr, const uint32_t* wtabs, const uint32_t* btab, bool dma,
-                                    hipStream_t s) {
+                                    bool mixed, hipStream_t s) {
   if (n == 0) return hipSuccess;
   if (wtabs && dma)
     launch_lane<kCombWideDma>(mode, n, n_keys, ki, sgp, mp, op, keys_pk, keys_ok, wtabs, btab, vp, bp, batch_kb, scr,
                               s);
   else if (wtabs)
     launch_lane<kCombWide>(mode, n, n_keys, ki, sgp, mp, op, keys_pk, keys_ok, wtabs, btab, vp, bp, batch_kb, scr, s);
+  else if (mixed && btab)
+    launch_lane<kCombMixed>(mode, n, n_keys, ki, sgp, mp, op, keys_pk, keys_ok, ktabs, btab, vp, bp, batch_kb, scr, s);
   else
     launch_lane<kComb256>(mode, n, n_keys, ki, sgp, mp, op, keys_pk, keys_ok, ktabs, bcomb, vp, bp, batch_kb, scr, s);
   return hipGetLastError();

@@ -49,33 +49,58 @@ CMTV_HD bool q_keyed_decode_r(ge_p3& R, const uint32_t* sig_ptr) {
   return r_ok;
 }
 
-// The comb additions with the challenge and R supplied late: the 32 fixed-
-// base additions need only s, so they run first; get_k(tk) is called before
-// the 32 key-comb additions and get_r(rc, r_ok) (this lane's coordinate of R:
-// x, y, 1, t) before the final check -- a helper wave hashes and decodes
-// meanwhile (kernels.hip k_verify_keyed_quad_split).
-template <uint32_t MODE, class Q, class GetK, class GetR>
+// no B table (the radix-256 B comb path of q_verify_keyed_split)
+struct NoBTabQ {
+  CMTV_HD void load_coord(int, int, fe&) const {}
+};
+
+// The comb additions with the challenge and R supplied late: the fixed-base
+// additions need only s, so they run first; get_k(tk) is called before the
+// 32 key-comb additions and get_r(rc, r_ok) (this lane's coordinate of R: x,
+// y, 1, t) before the final check -- a helper wave hashes and decodes
+// meanwhile (kernels.hip k_verify_keyed_quad_split). [s]B: B16 = over the B
+// table's radix-2^16 comb (bt.load_coord(row, off, fe&): BC16 rows, 16
+// additions), else over the radix-256 comb bcomb (32).
+template <uint32_t MODE, bool B16 = false, class Q, class BT = NoBTabQ, class GetK, class GetR>
 CMTV_HD bool q_verify_keyed_split(const Q& q, bool key_ok, const uint32_t* sig_ptr, const uint32_t* ktab,
-                                  const uint32_t* bcomb, const GetK& get_k, const GetR& get_r) {
+                                  const uint32_t* bcomb, const GetK& get_k, const GetR& get_r,
+                                  const BT& bt = BT()) {
   const int lane = q.lane();
   uint32_t w[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) w[i] = sig_ptr[8 + i];  // S
   bool ok = key_ok && (w[7] & 0xE0000000u) == 0 && sc_is_canonical(w);
-  uint32_t ts[8], tk[8];
-  sc_bias(ts, w, 0x80808080u);
+  uint32_t tk[8];
 
   fe v;
   q_identity(v, lane);
+  if constexpr (B16) {
+    uint32_t sLo[8], sHi[8];
+    hs_digits65536(sLo, sHi, w);
 #pragma unroll 1
-  for (int it = 0; it < COMB_WINDOWS; it++) {
-    const int j = COMB_WINDOWS - 1 - it;
-    const int dB = (int)sc_shift_out(ts, 8) - 128;
-    const int ib = dB < 0 ? -dB : dB;
-    fe c;
-    const uint32_t* row = bcomb + ((size_t)j * COMB_ENTRIES + (ib > 0 ? ib - 1 : 0)) * COMB_ROW_WORDS;
-    q_niels_coord(q, c, [&](int off, fe& r) { comb_load(row, off, r); }, 10, 20, dB < 0, ib == 0);
-    q_add(q, v, c);
+    for (int j = 15; j >= 0; j--) {
+      const int dB = (int)(j >= 8 ? sc_shift_out(sHi, 16) : sc_shift_out(sLo, 16)) - 0x8000;
+      const int ib = dB < 0 ? -dB : dB;
+      const int row = BC16_BASE + j * BT16_ENTRIES + (ib > 0 ? ib - 1 : 0);
+      fe c;
+      q_niels_coord(
+          q, c, [&](int off, fe& r) { bt.load_coord(row, off, r); }, BTAB_COORD_WORDS, 2 * BTAB_COORD_WORDS,
+          dB < 0, ib == 0);
+      q_add(q, v, c);
+    }
+  } else {
+    uint32_t ts[8];
+    sc_bias(ts, w, 0x80808080u);
+#pragma unroll 1
+    for (int it = 0; it < COMB_WINDOWS; it++) {
+      const int j = COMB_WINDOWS - 1 - it;
+      const int dB = (int)sc_shift_out(ts, 8) - 128;
+      const int ib = dB < 0 ? -dB : dB;
+      fe c;
+      const uint32_t* row = bcomb + ((size_t)j * COMB_ENTRIES + (ib > 0 ? ib - 1 : 0)) * COMB_ROW_WORDS;
+      q_niels_coord(q, c, [&](int off, fe& r) { comb_load(row, off, r); }, 10, 20, dB < 0, ib == 0);
+      q_add(q, v, c);
+    }
   }
   get_k(tk);
 #pragma unroll 1

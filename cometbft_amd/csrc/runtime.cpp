@@ -451,6 +451,9 @@ struct cmtv_ctx {
   // wide-comb lane kernels stage their rows through LDS by LDS-DMA
   // (keyed_lane.hip kCombWideDma; CMTV_WIDE_DMA=0: plain loads)
   bool wide_dma = true;
+  // registered keys without wide combs: B over the B table's radix-2^16 comb
+  // (CMTV_KEYED_MIXED=0: over its radix-256 comb, 16 more additions)
+  bool keyed_mixed = true;
   // devices (indices into devs) that take host batches, in shard order; the
   // RCCL communicator (when rccl) spans exactly these, rank = position
   std::vector<size_t> live;
@@ -737,7 +740,7 @@ static int enqueue_verify_keyed(cmtv_ctx* ctx, CmtvDev& D, const cmtv_keyset::Pe
                             K.d_tab, D.d_bcomb, d_valid ? d_valid + c : nullptr,
                             d_bitmap ? d_bitmap + c / 64 : nullptr, quad, n <= ctx->quad_split_max,
                             ctx->keyed_wait, D.d_diag, kb, static_cast<uint32_t*>(D.d_atab.p),
-                            quad ? nullptr : K.d_wide, D.d_btab, ctx->wide_dma, s, slot);
+                            quad ? nullptr : K.d_wide, D.d_btab, ctx->wide_dma, s, slot, ctx->keyed_mixed);
     if (e == hipSuccess && krow) e = row_slot_release(ctx, D, s, slot_k);
     if (e != hipSuccess) {
       D.timing.abandon(tp);
@@ -1319,6 +1322,7 @@ static void read_env(cmtv_ctx* ctx) {
   if (const char* kl = std::getenv("CMTV_FORCE_K_LATE")) ctx->keyed_wait = kl[0] == '1' ? 0u : kKeyedWaitDefault;
   if (const char* kb = std::getenv("CMTV_KEYED_BATCH")) ctx->keyed_batch = kb[0] != '0';
   if (const char* wd = std::getenv("CMTV_WIDE_DMA")) ctx->wide_dma = wd[0] != '0';
+  if (const char* km = std::getenv("CMTV_KEYED_MIXED")) ctx->keyed_mixed = km[0] != '0';
   if (const char* mw = std::getenv("CMTV_KEYED_BATCH_MIN_WAVES")) {
     const long v = std::strtol(mw, nullptr, 10);
     if (v >= 1 && v <= (1l << 20)) ctx->keyed_batch_min_waves = (uint32_t)v;

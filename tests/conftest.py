@@ -118,6 +118,14 @@ def _env_ctx(**env):
 
 
 @pytest.fixture(scope="session")
+def gpu_ctx_lane256():
+    """The lane kernels (as gpu_ctx_lane) with registered keys' [s]B over the
+    B table's radix-256 comb (CMTV_KEYED_MIXED=0) instead of its radix-2^16
+    comb (keyed_lane.hip kComb256 vs kCombMixed)."""
+    return _env_ctx(CMTV_QUAD_MAX=0, CMTV_KEYED_QUAD_MAX=0, CMTV_KEYED_MIXED=0)
+
+
+@pytest.fixture(scope="session")
 def gpu_ctx_quad2s():
     """Small Ed25519 batches on the helper-wave quad kernel whose quads add
     both table entries of every window themselves (k_verify_quad_split,

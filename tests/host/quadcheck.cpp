@@ -182,6 +182,13 @@ int main(int argc, char** argv) {
   const bool sr = sr2 || (argc > 1 && !strcmp(argv[1], "sr"));
   // argv[1] == "keyed": Ed25519 records, verified through registered-key combs (keyed_quad.h)
   const bool keyed = argc > 1 && !strcmp(argv[1], "keyed");
+  // argv[1] == "keyedmix": one lane, the key's radix-256 comb with B over the
+  // B table's radix-2^16 comb (keyed.h keyed_comb_mixed, kCombMixed)
+  const bool keyedmix = argc > 1 && !strcmp(argv[1], "keyedmix");
+  // argv[1] == "keyed16": the keyed quad verifier with [s]B over the B
+  // table's radix-2^16 comb (q_verify_keyed_split<MODE, true>, the keyed
+  // split kernel's default)
+  const bool keyed16 = argc > 1 && !strcmp(argv[1], "keyed16");
   // argv[1] == "oct": Ed25519 records through the 8-lane verifier (oct.h)
   const bool oct = argc > 1 && !strcmp(argv[1], "oct");
   // argv[1] == "quad2" / "oct2": the split kernels' path -- the scalars and
@@ -222,7 +229,7 @@ int main(int argc, char** argv) {
     to_words(sigw, sig, 16);
     bool kok = false;
     const uint32_t* kt = nullptr;
-    if (keyed) {
+    if (keyed || keyedmix || keyed16) {
       auto it = combs.find(std::string((const char*)pk, 32));
       if (it == combs.end()) {
         bool o;
@@ -231,6 +238,13 @@ int main(int argc, char** argv) {
       }
       kok = it->second.first;
       kt = it->second.second.data();
+    }
+    if (keyedmix) {
+      ge_p3 acc;
+      const bool ok = keyed_comb_mixed<CombWindow>(acc, pkw, kok, sigw, mp, mlen, kt, bt);
+      uint8_t o = (mode ? check_R<MODE_ZIP215>(acc, sigw) : check_R<MODE_GO_STDLIB>(acc, sigw)) && ok;
+      fwrite(&o, 1, 1, stdout);
+      continue;
     }
     Exchange ex;
     bool res[8];
@@ -346,6 +360,18 @@ int main(int argc, char** argv) {
         else if (keyed)
           res[l] = mode ? q_verify_keyed<MODE_ZIP215>(q, pkw, kok, sigw, mp, mlen, kt, bcomb.data())
                         : q_verify_keyed<MODE_GO_STDLIB>(q, pkw, kok, sigw, mp, mlen, kt, bcomb.data());
+        else if (keyed16) {
+          auto get_k = [&](uint32_t tk[8]) { q_keyed_challenge(tk, pkw, sigw, mp, mlen); };
+          auto get_r = [&](fe& rc, bool& r_ok) {
+            ge_p3 R;
+            r_ok = mode ? q_keyed_decode_r<MODE_ZIP215>(R, sigw) : q_keyed_decode_r<MODE_GO_STDLIB>(R, sigw);
+            fe one;
+            fe_1(one);
+            fe_pick(rc, l, R.X, R.Y, one, R.T);
+          };
+          res[l] = mode ? q_verify_keyed_split<MODE_ZIP215, true>(q, kok, sigw, kt, nullptr, get_k, get_r, bt)
+                        : q_verify_keyed_split<MODE_GO_STDLIB, true>(q, kok, sigw, kt, nullptr, get_k, get_r, bt);
+        }
         else
           res[l] = mode ? q_verify<MODE_ZIP215>(q, pkw, sigw, mp, mlen, bt, ta, tr)
                         : q_verify<MODE_GO_STDLIB>(q, pkw, sigw, mp, mlen, bt, ta, tr);

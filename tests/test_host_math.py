@@ -183,6 +183,29 @@ def test_split_pipelines_match_corpus(quadcheck, corpus, mode, kind):
 
 
 @pytest.mark.parametrize("mode", [0, 1])
+def test_keyed_mixed_comb_matches_corpus(quadcheck, corpus, mode):
+    """kCombMixed (keyed.h keyed_comb_mixed): [k](-A) over the key's
+    radix-256 comb, [s]B over the B table's radix-2^16 comb -- the lane path
+    for key sets without wide combs -- on the corpus, both modes."""
+    idx = _keyed_subset(corpus)
+    got = _run(quadcheck, "keyedmix", corpus, idx, mode)
+    want = (corpus["go"] if mode == 0 else corpus["zip215"])[idx]
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(idx[int(i)], corpus["cats"][idx[int(i)]]) for i in bad[:10]]
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_keyed_quad_b16_matches_corpus(quadcheck, corpus, mode):
+    """The keyed quad split kernel's [s]B over the B table's radix-2^16 comb
+    (q_verify_keyed_split<MODE, true>) in 4-thread lockstep, both modes."""
+    idx = _keyed_subset(corpus)[::3]
+    got = _run(quadcheck, "keyed16", corpus, idx, mode)
+    want = (corpus["go"] if mode == 0 else corpus["zip215"])[idx]
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(idx[int(i)], corpus["cats"][idx[int(i)]]) for i in bad[:10]]
+
+
+@pytest.mark.parametrize("mode", [0, 1])
 def test_quad_pipeline_matches_corpus(quadcheck, corpus, mode):
     """The 4-lane quad kernel's source (quad.h), four host threads in lockstep
     standing in for the DPP quad_perm exchanges (every adversarial vector and

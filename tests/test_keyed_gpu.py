@@ -2,7 +2,10 @@
 cmtv_register_keys + cmtv_verify_ed25519_indexed[_device]): verdicts must equal
 the corpus' committed verdicts and the C oracle's, bit for bit, both modes.
 Kernel "wide": the lane kernels over radix-2^16 key combs
-(cmtv_register_keys_ex(CMTV_KEYS_WIDE), keyed.h keyed_comb_wide)."""
+(cmtv_register_keys_ex(CMTV_KEYS_WIDE), keyed.h keyed_comb_wide); "lane": the
+lane kernels over the radix-256 key combs with B's radix-2^16 comb
+(kCombMixed, the default); "lane256": the same with B's radix-256 comb
+(CMTV_KEYED_MIXED=0)."""
 import numpy as np
 import pytest
 
@@ -13,12 +16,12 @@ from cometbft_amd import _native as N
 pytestmark = pytest.mark.gpu
 
 
-KERNELS = ["row", "quad2", "quad", "lane", "wide"]
+KERNELS = ["row", "quad2", "quad", "lane", "lane256", "wide"]
 
 
 def _ctx(kernel, request):
     name = {"row": "gpu_ctx_krow", "quad2": "gpu_ctx_kquad2", "quad": "gpu_ctx_quad1", "lane": "gpu_ctx_lane",
-            "wide": "gpu_ctx_lane"}[kernel]
+            "lane256": "gpu_ctx_lane256", "wide": "gpu_ctx_lane"}[kernel]
     return request.getfixturevalue(name)
 
 

@@ -696,10 +696,10 @@ CMTV_HD bool q_verify_split(const Q& q, const uint32_t* pk_ptr, const uint32_t* 
 // [u]B. Here the helper sums a window's two table entries in its own lane
 // layout, S_w = [dA](-A) + [dR](-/+R), and hands S_w to the quads through LDS
 // at a per-window barrier: a window is 4 doublings and ONE addition. Both
-// tables are built before barrier 1 -- A's entries as extended points (the
-// first operand of the helper's addition), R's as cached entries of -R (a
-// negative k2 flips R's digits) -- and only the top window is summed by the
-// quads themselves (its A entry is loaded as the starting point).
+// tables are built before barrier 1 as extended points -- of -A and of -R (a
+// negative k2 flips R's digits) -- so the quads spend no cached conversions on
+// them; the helper converts R's entry itself. Only the top window is summed
+// by the quads (its A entry is loaded as the starting point).
 
 // (0..8)P as extended points (entry 0 the identity), one coordinate per lane;
 // v holds this lane's coordinate of P and is clobbered
@@ -721,38 +721,45 @@ CMTV_HD void q_build_table_p3(const Q& q, ATab& tab, fe& v) {
 }
 
 // The helper's addend of one window for its signature (one per lane), from
-// the quads' tables read through rd(P, e, c, fe&) -- P = 0: A's extended
-// entries, 1: R's cached entries of -R; c = the coordinate, i.e. the quad
-// lane that stored it -- as the quads' cached coordinates (Y-X, Y+X, 2Z, 2dT)
-// in out[0..3]: S = [dA](-A) + [dR](r_flip ? R : -R). HWCD addition of an
-// extended and a cached point, then the cached form of the sum: 9
-// multiplications. Negating the extended operand swaps its (Y-X, Y+X) and
-// negates T; negating the cached one swaps which slot is read and negates
-// 2dT; the two T signs meet in C = T1 2dT2, so one sign decides whether C is
-// added to or subtracted from D (no negation is computed).
+// the quads' tables read through rd(P, e, c, fe&) -- P = 0: the extended
+// entries of -A, 1: of -R; c = the coordinate, i.e. the quad lane that stored
+// it -- as the quads' cached coordinates (Y-X, Y+X, 2Z, 2dT) in out[0..3]:
+// S = [dA](-A) + [dR](r_flip ? R : -R). HWCD addition with both operands
+// extended: A = (Y1-X1)(Y2-X2), B = (Y1+X1)(Y2+X2), C = T1 2dT2 (2d T2 one
+// constant product), D = 2 Z1 Z2; then the cached form of the sum: 10
+// multiplications. Negating an operand swaps its (Y-X, Y+X) and negates T;
+// the two T signs meet in C, so one sign decides whether C is added to or
+// subtracted from D (no negation is computed).
 template <class Rd>
 CMTV_HD void h_window_addend(fe out[4], const Rd& rd, int dA, int dR, bool r_flip) {
   const int eA = dA < 0 ? -dA : dA, eR = dR < 0 ? -dR : dR;
   const bool nA = dA < 0, nR = (dR < 0) != r_flip;
-  fe x, y, s, d, m;
+  fe x, y, s, d, m, s2, d2;
   rd(0, eA, 0, x);
   rd(0, eA, 1, y);
-  fe_sub(d, y, x);  // Y - X
-  fe_add(s, y, x);  // Y + X
-  rd(1, eR, nR ? 1 : 0, m);
+  fe_sub(d, y, x);  // Y1 - X1
+  fe_add(s, y, x);  // Y1 + X1
+  rd(1, eR, 0, x);
+  rd(1, eR, 1, y);
+  fe_sub(d2, y, x);  // Y2 - X2
+  fe_add(s2, y, x);  // Y2 + X2
   fe_select(x, d, s, nA);
+  fe_select(m, d2, s2, nR);
   fe_mul(x, x, m);  // A = (Y1 - X1)(Y2 - X2)
-  rd(1, eR, nR ? 0 : 1, m);
   fe_select(y, s, d, nA);
+  fe_select(m, s2, d2, nR);
   fe_mul(y, y, m);  // B = (Y1 + X1)(Y2 + X2)
   fe e, h, f, g;
   fe_sub(e, y, x);  // E = B - A
   fe_add(h, y, x);  // H = B + A
-  rd(0, eA, 3, x);
   rd(1, eR, 3, m);
+  fe_const_d2(d2);
+  fe_mul(m, m, d2);  // 2d T2
+  rd(0, eA, 3, x);
   fe_mul(x, x, m);  // +/- C = T1 2dT2
   rd(0, eA, 2, y);
   rd(1, eR, 2, m);
+  fe_add(m, m, m);
   fe_mul(y, y, m);  // D = Z1 2Z2
   fe_add(s, y, x);  // D + C
   fe_sub(d, y, x);  // D - C
@@ -818,7 +825,7 @@ CMTV_HD bool q_verify_hs(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig
     fe_select(rc, rc, t, xt);
   }
   q_build_table_p3(q, tabA, v);
-  q_build_table(q, tabR, rc);
+  q_build_table_p3(q, tabR, rc);
   SigPrep p;
   get_prep(p);
   const bool s_ok = (p.flags & 4u) != 0;
@@ -837,11 +844,15 @@ CMTV_HD bool q_verify_hs(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig
     const int dA = (int)sc_shift_out(tA, 4) - 8;
     const int dR = (int)sc_shift_out(tR, 4) - 8;
     tabA.load(dA < 0 ? -dA : dA, v);
-    fe t;
+    fe t, r;
     fe_neg(t, v);
     fe_carry(t);
     fe_select(v, v, t, dA < 0 && (lane == 0 || lane == 3));
-    tabR.load_signed(q, dR < 0 ? -dR : dR, (dR < 0) != r_flip, c);
+    tabR.load(dR < 0 ? -dR : dR, r);
+    fe_neg(t, r);
+    fe_carry(t);
+    fe_select(r, r, t, ((dR < 0) != r_flip) && (lane == 0 || lane == 3));
+    q_to_cached(q, c, r);
     q_add(q, v, c);
   }
 #pragma unroll 1

@@ -47,10 +47,12 @@ constexpr uint32_t kKeyedBatchMinWaves = 2048;
 constexpr size_t kQuadMaxDefault = 40000;
 // Ed25519 batches up to this size use the 8-lanes-per-signature kernel
 // (oct.h) in its two-wave form (k_verify_oct_split: 2 waves per 8
-// signatures); measured on MI355X (150: 0.227 vs 0.261 ms, 4,096: 0.303 vs
-// 0.265 ms) the helper-wave quad kernel takes over in between (the one-wave
-// oct kernel stays reachable with CMTV_OCT_SPLIT_MAX < CMTV_OCT_MAX).
-constexpr size_t kOctMaxDefault = 3072;       // CMTV_OCT_MAX
+// signatures) while its 8-signature workgroups fit one round on 256 CUs:
+// measured on MI355X (round 4, profiles/r04_oct_hs_crossover.txt) oct2 2,048:
+// 0.209 ms vs the helper-summed quad kernel's 0.218; 3,072 (two workgroups
+// per CU): 0.272 vs 0.221 (the one-wave oct kernel stays reachable with
+// CMTV_OCT_SPLIT_MAX < CMTV_OCT_MAX).
+constexpr size_t kOctMaxDefault = 2048;       // CMTV_OCT_MAX
 // Ed25519 batches up to this size take the one-signature-per-wave row kernel
 // (row.h) where the two-wave oct kernel would run (CMTV_ROW_MAX; 3 signatures
 // per CU: 768 in one round on 256 CUs)
@@ -61,7 +63,7 @@ constexpr size_t kRow2MaxDefault = 256;
 // registered-key batches up to this size take the keyed row kernel (one
 // signature per CU; CMTV_KEYED_ROW_MAX)
 constexpr size_t kKeyedRowMaxDefault = 256;
-constexpr size_t kOctSplitMaxDefault = 3072;  // CMTV_OCT_SPLIT_MAX
+constexpr size_t kOctSplitMaxDefault = 2048;  // CMTV_OCT_SPLIT_MAX
 // quad batches up to this size take the helper-wave form (k_verify_quad_split:
 // 256 workgroups x 48 signatures per round); CMTV_QUAD_SPLIT_MAX
 constexpr size_t kQuadSplitMaxDefault = 40000;

@@ -129,7 +129,7 @@ typedef struct cmtv_device_stats {
  * CMTV_OCT_SPLIT_MAX / CMTV_QUAD_MAX / CMTV_QUAD_SPLIT_MAX / CMTV_KEYED_QUAD_MAX / CMTV_LANE_CHUNK
  * (kernel crossovers: Ed25519 batches up to CMTV_ROW2_MAX (256) take a whole
  * CU per signature (four waves; CMTV_ROW_WAVES=2: two), up to CMTV_ROW_MAX
- * (768) one wave per signature, up to CMTV_OCT_MAX (3072) 8 lanes, up to
+ * (768) one wave per signature, up to CMTV_OCT_MAX (2048) 8 lanes, up to
  * CMTV_QUAD_MAX (40000) 4 lanes, larger ones one lane), CMTV_FAULT_AT=N (test knob: the N-th verification
  * launch of the context fails with CMTV_EHIP without running; libs/fail
  * FAIL_TEST_INDEX analogue), CMTV_FORCE_WIDE=1 (test knob: the quad kernels

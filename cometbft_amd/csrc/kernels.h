@@ -22,7 +22,8 @@ constexpr uint32_t kLaunchQuad = 1, kLaunchForceWide = 2, kLaunchOct = 4, kLaunc
 // and its two- and four-waves-per-signature forms (k_verify_row2_split,
 // k_verify_row4_split)
 constexpr uint32_t kLaunchRow = 32, kLaunchRow2 = 64, kLaunchRow4 = 128;
-// with kLaunchQuadSplit: the helper-summed form (k_verify_quad_hs; Ed25519)
+// with kLaunchQuadSplit: the helper-summed form (k_verify_quad_hs,
+// k_verify_sr25519_quad_hs); kflags bits 16..31 carry its tuning (hs_tune)
 constexpr uint32_t kLaunchQuadHS = 256;
 
 // Row kernel bitmap assembly: each launch takes the next of kRowSlots slots

@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include "devtables.h"
+#include "hs_helper.h"
 #include "kernels.h"
 #include "keyed.h"
 #include "keyed_quad.h"
@@ -303,24 +304,22 @@ __global__ __launch_bounds__(256, CMTV_QUAD_WAVES_PER_EU) void k_verify_quad_spl
   if (t == 0 && out_bitmap && slice < 4 * ((n + 63) / 64)) reinterpret_cast<uint16_t*>(out_bitmap)[slice] = (uint16_t)x;
 }
 
-// The helper-summed quad verifier (quad.h q_verify_hs): the workgroup and its
-// first barrier as k_verify_quad_split, but the quads build both tables before
-// it (A's as extended points), and then the helper wave, instead of idling
-// after [u]B, sums every window's two table entries for its 48 signatures
-// (h_window_addend, one per lane) and hands the sums over through a 2-slot
-// LDS ring, one barrier per window: the quads' windows lose one of their two
-// additions. [u]B: while the quads build their tables the helper adds the
-// top kHsCombPre positions of u's 16-position comb and hands that part over
-// at a last barrier; the quads add the other 16 - kHsCombPre digits inside
-// their windows (q_verify_hs). Nothing of [u]B runs inside the helper's
-// window loop: the per-window barriers go at the slower side's pace, so
-// helper work there stalls all three quads (measured: comb additions cut into
+// The helper-summed quad verifier (quad.h q_verify_hs, hs_helper.h): the
+// workgroup and its first barrier as k_verify_quad_split, but the quads build
+// both tables before it (extended points), and then the helper wave, instead
+// of idling after [u]B, sums every window's two table entries for its 48
+// signatures (h_window_addend, one per lane) and hands the sums over through a
+// 2-slot LDS ring, one barrier per window: the quads' windows lose one of
+// their two additions. [u]B: while the quads build their tables the helper
+// adds the top kHsCombPre positions of u's 16-position comb and hands that
+// part over at a last barrier; the quads add the other digits inside their
+// windows (q_hs_straus). Nothing of [u]B runs inside the helper's window
+// loop: the per-window barriers go at the slower side's pace, so helper work
+// there stalls all three quads (measured: comb additions cut into
 // one-multiplication phases, two per window, cost the quads 1.6k cycles a
 // window; tools/gpu_hs.sh). The slot ring overlays the fused sign-bytes
 // buffer (dead once the hashes are done). hs_tune (the launcher's kflags bits
 // 16..31, CMTV_HS_PRE) overrides kHsCombPre (0..16) for tuning.
-constexpr int kHsCombPre = 6;
-
 template <uint32_t MODE>
 __global__ __launch_bounds__(256, CMTV_QUAD_WAVES_PER_EU) void k_verify_quad_hs(
     uint32_t n, const uint32_t* __restrict__ pk, const uint32_t* __restrict__ sig, const uint8_t* __restrict__ msg,
@@ -328,12 +327,10 @@ __global__ __launch_bounds__(256, CMTV_QUAD_WAVES_PER_EU) void k_verify_quad_hs(
     uint64_t* __restrict__ out_bitmap, uint32_t force_wide, SbFuse sb, uint32_t hs_tune) {
   const uint32_t wave = threadIdx.x >> 6, t = threadIdx.x & 63;
   const uint32_t base = blockIdx.x * 48;
-  int comb_pre = (hs_tune & 0xFFu) ? (int)(hs_tune & 0xFFu) - 1 : kHsCombPre;
-  comb_pre = comb_pre > 16 ? 16 : comb_pre;
-  constexpr uint32_t kSlotU2 = 3 * 5 * 64;  // one slot: 3 quad waves x 5 uint2 x 64 lanes
+  const int comb_pre = hs_comb_pre(hs_tune, kHsCombPre);
   __shared__ uint32_t prep[48][SIG_PREP_WORDS + 1];
-  __shared__ uint2 tab_lds[3][2 * 9 * 5 * 64];
-  __shared__ uint2 xbuf[2 * kSlotU2];  // sign-bytes (48 x kSbFuseMaxMsg B), then the 2-slot ring
+  __shared__ uint2 tab_lds[3][kHsTabU2];
+  __shared__ uint2 xbuf[2 * kHsSlotU2];  // sign-bytes (48 x kSbFuseMaxMsg B), then the 2-slot ring
   static_assert(sizeof(xbuf) >= 48 * kSbFuseMaxMsg, "ring must cover the sign-bytes buffer");
   CMTV_STAMP(0);
   if (wave == 3) {
@@ -345,12 +342,7 @@ __global__ __launch_bounds__(256, CMTV_QUAD_WAVES_PER_EU) void k_verify_quad_hs(
     helper_message(sb, i, msg, off, reinterpret_cast<uint32_t*>(xbuf) + slot * (kSbFuseMaxMsg / 4), mp, ml);
     SigPrep p;
     q_prepare<MODE>(p, pk + 8 * (size_t)i, sig + 16 * (size_t)i, mp, ml, force_wide != 0);
-    // the workgroup's window count (the quads' q_wave_windows over all 48)
-    const bool wide = __ballot(t < 48 && (p.flags & 2u) != 0) != 0;
-    int W = HS_WINDOWS;
-#pragma unroll 1
-    for (int x = HS_WINDOWS; x < HS_MAX_WINDOWS; x++) W += __ballot(t < 48 && (int)((p.flags >> 8) & 0xFFu) > x) ? 1 : 0;
-    W = wide ? HS_WIDE_WINDOWS : W;
+    const int W = hs_workgroup_windows(p.flags, t);
     p.flags |= (uint32_t)W << 16;
     if (t < 48) sig_prep_store(prep[t], p);
     BComb16 bc;
@@ -361,55 +353,9 @@ __global__ __launch_bounds__(256, CMTV_QUAD_WAVES_PER_EU) void k_verify_quad_hs(
     CMTV_STAMP(1);
     __syncthreads();  // 1: the scalars; the tables are built
     CMTV_STAMP(2);
-    const bool r_flip = (p.flags & 1u) != 0;
-    uint32_t tA[8], tR[8];
-    hs_digits16(tA, p.k1, W);
-    hs_digits16(tR, p.k2, W);
-    sc_shift_out(tA, 4);  // the top window is the quads' own
-    sc_shift_out(tR, 4);
     uint64_t hwait = 0;  // probe build: cycles the helper waits at the window barriers
-    (void)hwait;
-
-    const uint2* tw = tab_lds[slot >> 4];
-    const uint32_t qb = 4 * (slot & 15);
-    auto rd = [&](int P, int e, int c, fe& r) {
-      const uint2* src = tw + (P * 9 + e) * 5 * 64 + qb + c;
-#pragma unroll
-      for (int k = 0; k < 5; k++) {
-        const uint2 x = src[k * 64];
-        r.v[2 * k] = x.x;
-        r.v[2 * k + 1] = x.y;
-      }
-    };
-    auto put = [&](uint2* dst, const fe* out) {
-      if (t < 48) {
-#pragma unroll
-        for (int c = 0; c < 4; c++)
-#pragma unroll
-          for (int k = 0; k < 5; k++) dst[(slot >> 4) * 320 + k * 64 + qb + c] = make_uint2(out[c].v[2 * k], out[c].v[2 * k + 1]);
-      }
-    };
-#pragma unroll 1
-    for (int win = W - 2; win >= 0; win--) {
-      const int dA = (int)sc_shift_out(tA, 4) - 8;
-      const int dR = (int)sc_shift_out(tR, 4) - 8;
-      fe out[4];
-      h_window_addend(out, rd, dA, dR, r_flip);
-      put(xbuf + (win & 1) * kSlotU2, out);
-      const uint64_t c0 = CMTV_CLOCK();
-      __syncthreads();  // window win
-      hwait += CMTV_CLOCK() - c0;
-    }
+    hs_helper_windows(p, W, bc, &tab_lds[0][0], xbuf, t, [] { return (uint64_t)CMTV_CLOCK(); }, hwait);
     CMTV_STAMP_VAL(6, hwait);
-    {
-      fe out[4], d2;
-      fe_sub(out[0], bc.P.Y, bc.P.X);
-      fe_add(out[1], bc.P.Y, bc.P.X);
-      fe_add(out[2], bc.P.Z, bc.P.Z);
-      fe_const_d2(d2);
-      fe_mul(out[3], bc.P.T, d2);
-      put(xbuf + kSlotU2, out);  // slot 1: last read for window 1, before barrier 0
-    }
     CMTV_STAMP(3);
     __syncthreads();  // B: [u]B
     CMTV_STAMP(4);
@@ -423,14 +369,6 @@ __global__ __launch_bounds__(256, CMTV_QUAD_WAVES_PER_EU) void k_verify_quad_hs(
   DevATabQ ta{tab_lds[wave], t}, tr{tab_lds[wave] + 9 * 5 * 64, t};
   uint64_t qwait = 0;  // probe build: cycles this quad wave waits at the window barriers
   (void)qwait;
-  auto slot_load = [&](const uint2* sl, fe& c) {
-#pragma unroll
-    for (int k = 0; k < 5; k++) {
-      const uint2 x = sl[wave * 320 + k * 64 + t];
-      c.v[2 * k] = x.x;
-      c.v[2 * k + 1] = x.y;
-    }
-  };
   DevBTabQ bt{btab};
   bool v = q_verify_hs<MODE>(
       q, pk + 8 * (size_t)i, sig + 16 * (size_t)i, bt, ta, tr, 16 - comb_pre,
@@ -444,13 +382,13 @@ __global__ __launch_bounds__(256, CMTV_QUAD_WAVES_PER_EU) void k_verify_quad_hs(
         const uint64_t c0 = CMTV_CLOCK();
         __syncthreads();
         qwait += CMTV_CLOCK() - c0;
-        slot_load(xbuf + (win & 1) * kSlotU2, c);
+        hs_slot_load(xbuf + (win & 1) * kHsSlotU2, wave, t, c);
       },
       [&](fe& c) {
         CMTV_STAMP(3);
         __syncthreads();
         CMTV_STAMP(4);
-        slot_load(xbuf + kSlotU2, c);
+        hs_slot_load(xbuf + kHsSlotU2, wave, t, c);
       });
   CMTV_STAMP(5);
   CMTV_STAMP_VAL(6, qwait);

@@ -778,57 +778,24 @@ CMTV_HD void h_window_addend(fe out[4], const Rd& rd, int dA, int dR, bool r_fli
   fe_mul(out[3], T3, m);
 }
 
-// The quad side of the helper-summed verifier: decode as q_verify_split, both
-// tables before get_prep (the scalars; flags bits 16..23 carry the window
-// count W the whole workgroup runs, else this quad's own), the top window
-// from the tables, then W - 1 windows of 4 doublings and get_s(win, c) (this
-// lane's cached coordinate of the helper's S_win), and get_b(c): the helper's
-// part of [u]B, comb positions 15..j0 (BComb16). The quads add positions
-// j0-1..0 themselves, digit j of u's radix-2^16 digits on the window the
-// remaining doublings scale to 2^16j -- j < 8 against (1..2^15)B on window 4j,
-// j >= 8 against (1..2^15)[2^120]B on window 4(j-8)+2 -- its row fetched
-// before the window's doublings.
-template <uint32_t MODE, class Q, class BTab, class ATab, class GetPrep, class GetS, class GetB>
-CMTV_HD bool q_verify_hs(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig_ptr, const BTab& btab, ATab& tabA,
-                         ATab& tabR, int j0, const GetPrep& get_prep, const GetS& get_s, const GetB& get_b) {
+// The quad side of the helper-summed verifiers after the decode (v: this
+// lane's coordinate of -A, rc: of -R, both extended, Z = 1): both tables,
+// then get_prep (the scalars; flags bits 16..23 carry the window count W the
+// whole workgroup runs, else this quad's own), the top window from the
+// tables, then W - 1 windows of 4 doublings and get_s(win, c) (this lane's
+// cached coordinate of the helper's S_win), and get_b(c): the helper's part
+// of [u]B, comb positions 15..j0 (BComb16). The quads add positions j0-1..0
+// themselves, digit j of u's radix-2^16 digits on the window the remaining
+// doublings scale to 2^16j -- j < 8 against (1..2^15)B on window 4j, j >= 8
+// against (1..2^15)[2^120]B on window 4(j-8)+2 -- its row fetched before the
+// window's doublings. Out: v = this lane's coordinate of X = [k2](R' - R), p.
+template <class Q, class BTab, class ATab, class GetPrep, class GetS, class GetB>
+CMTV_HD void q_hs_straus(const Q& q, fe& v, fe& rc, const BTab& btab, ATab& tabA, ATab& tabR, int j0, SigPrep& p,
+                         const GetPrep& get_prep, const GetS& get_s, const GetB& get_b) {
   const int lane = q.lane();
-  uint32_t w[8];
-  const uint32_t* src = (lane & 1) ? sig_ptr : pk_ptr;
-#pragma unroll
-  for (int i = 0; i < 8; i++) w[i] = src[i];
-  fe v, rc;
-  bool a_ok, r_ok, r_canon;
-  {
-    ge_p3 P;
-    const bool dec = p3_frombytes(P, w);
-    const bool canon = y_is_canonical(w) && !(fe_iszero(P.X) && (w[7] >> 31));
-    fe x, y, t, one;
-    fe_1(one);
-    q.template perm<QP_B0>(x, P.X);
-    q.template perm<QP_B0>(y, P.Y);
-    q.template perm<QP_B0>(t, P.T);
-    fe_pick(v, lane, x, y, one, t);  // A
-    q.template perm<QP_B1>(x, P.X);
-    q.template perm<QP_B1>(y, P.Y);
-    q.template perm<QP_B1>(t, P.T);
-    fe_pick(rc, lane, x, y, one, t);  // R
-    a_ok = q.template perm32<QP_B0>(dec ? 1u : 0u) != 0;
-    r_ok = q.template perm32<QP_B1>(dec ? 1u : 0u) != 0;
-    r_canon = q.template perm32<QP_B1>(canon ? 1u : 0u) != 0;
-    // -A and -R: negate X (lane 0) and T (lane 3)
-    const bool xt = lane == 0 || lane == 3;
-    fe_neg(t, v);
-    fe_carry(t);
-    fe_select(v, v, t, xt);
-    fe_neg(t, rc);
-    fe_carry(t);
-    fe_select(rc, rc, t, xt);
-  }
   q_build_table_p3(q, tabA, v);
   q_build_table_p3(q, tabR, rc);
-  SigPrep p;
   get_prep(p);
-  const bool s_ok = (p.flags & 4u) != 0;
   const bool r_flip = (p.flags & 1u) != 0;
   const int W = (p.flags >> 16) & 0xFFu ? (int)((p.flags >> 16) & 0xFFu) : q_wave_windows(q, p.flags);
   uint32_t tA[8], tR[8];
@@ -882,6 +849,49 @@ CMTV_HD bool q_verify_hs(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig
   }
   get_b(c);
   q_add(q, v, c);
+}
+
+// The Ed25519 helper-summed verifier (k_verify_quad_hs): decode as
+// q_verify_split, q_hs_straus, the mode's final check
+template <uint32_t MODE, class Q, class BTab, class ATab, class GetPrep, class GetS, class GetB>
+CMTV_HD bool q_verify_hs(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig_ptr, const BTab& btab, ATab& tabA,
+                         ATab& tabR, int j0, const GetPrep& get_prep, const GetS& get_s, const GetB& get_b) {
+  const int lane = q.lane();
+  uint32_t w[8];
+  const uint32_t* src = (lane & 1) ? sig_ptr : pk_ptr;
+#pragma unroll
+  for (int i = 0; i < 8; i++) w[i] = src[i];
+  fe v, rc;
+  bool a_ok, r_ok, r_canon;
+  {
+    ge_p3 P;
+    const bool dec = p3_frombytes(P, w);
+    const bool canon = y_is_canonical(w) && !(fe_iszero(P.X) && (w[7] >> 31));
+    fe x, y, t, one;
+    fe_1(one);
+    q.template perm<QP_B0>(x, P.X);
+    q.template perm<QP_B0>(y, P.Y);
+    q.template perm<QP_B0>(t, P.T);
+    fe_pick(v, lane, x, y, one, t);  // A
+    q.template perm<QP_B1>(x, P.X);
+    q.template perm<QP_B1>(y, P.Y);
+    q.template perm<QP_B1>(t, P.T);
+    fe_pick(rc, lane, x, y, one, t);  // R
+    a_ok = q.template perm32<QP_B0>(dec ? 1u : 0u) != 0;
+    r_ok = q.template perm32<QP_B1>(dec ? 1u : 0u) != 0;
+    r_canon = q.template perm32<QP_B1>(canon ? 1u : 0u) != 0;
+    // -A and -R: negate X (lane 0) and T (lane 3)
+    const bool xt = lane == 0 || lane == 3;
+    fe_neg(t, v);
+    fe_carry(t);
+    fe_select(v, v, t, xt);
+    fe_neg(t, rc);
+    fe_carry(t);
+    fe_select(rc, rc, t, xt);
+  }
+  SigPrep p;
+  q_hs_straus(q, v, rc, btab, tabA, tabR, j0, p, get_prep, get_s, get_b);
+  const bool s_ok = (p.flags & 4u) != 0;
   if (MODE == MODE_ZIP215) {
     const bool so = q_small_order(q, v);
     return s_ok && a_ok && r_ok && so;

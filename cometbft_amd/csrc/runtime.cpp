@@ -627,7 +627,7 @@ static int enqueue_verify(cmtv_ctx* ctx, CmtvDev& D, size_t n, const uint8_t* d_
   const bool row2 = row && n <= ctx->row2_max;
   const uint32_t kflags = (quad ? kLaunchQuad : 0u) | (oct ? kLaunchOct : 0u) |
                           (oct_split ? kLaunchOctSplit : 0u) | (quad_split ? kLaunchQuadSplit : 0u) |
-                          (quad_split && ctx->quad_hs && !sr ? kLaunchQuadHS | (ctx->hs_tune << 16) : 0u) |
+                          (quad_split && ctx->quad_hs ? kLaunchQuadHS | (ctx->hs_tune << 16) : 0u) |
                           (row ? (row2 ? (ctx->row_waves == 4 ? kLaunchRow4 : kLaunchRow2) : kLaunchRow) : 0u) |
                           (ctx->force_wide ? kLaunchForceWide : 0u);
   hipError_t e = hipSuccess;

@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include "devtables.h"
+#include "hs_helper.h"
 #include "kernels.h"
 #include "sr25519.h"
 #include "sr25519_quad.h"
@@ -157,11 +158,90 @@ __global__ __launch_bounds__(256, 1) void k_verify_sr25519_quad_split(
   if (t == 0 && out_bitmap && slice < 4 * ((n + 63) / 64)) reinterpret_cast<uint16_t*>(out_bitmap)[slice] = (uint16_t)x;
 }
 
+// The helper-summed form (kernels.hip k_verify_quad_hs, hs_helper.h): the
+// helper runs the merlin transcripts (STROBE states in the LDS the window ring
+// takes over afterwards), the quads build both tables before barrier 1, then
+// the helper sums every window's two table entries and the quads add one
+// point per window (sr25519_quad.h q_verify_sr_hs).
+__global__ __launch_bounds__(256, 1) void k_verify_sr25519_quad_hs(
+    uint32_t n, const uint32_t* __restrict__ pk, const uint32_t* __restrict__ sig, const uint8_t* __restrict__ msg,
+    const uint32_t* __restrict__ off, const uint32_t* __restrict__ btab, const uint16_t* __restrict__ prog, int nops,
+    uint8_t* __restrict__ out_valid, uint64_t* __restrict__ out_bitmap, uint32_t force_wide, uint32_t hs_tune) {
+  const uint32_t wave = threadIdx.x >> 6, t = threadIdx.x & 63;
+  const uint32_t base = blockIdx.x * 48;
+  const int comb_pre = hs_comb_pre(hs_tune, kHsCombPreSr);
+  __shared__ uint32_t prep[48][SIG_PREP_WORDS + 1];
+  __shared__ uint2 tab_lds[3][kHsTabU2];
+  // the helper's STROBE states (50 x 64 words), then the 2-slot window ring
+  __shared__ uint2 xbuf[2 * kHsSlotU2];
+  static_assert(sizeof(xbuf) >= 50 * 64 * 4, "ring must cover the STROBE states");
+  if (wave == 3) {
+    const uint32_t s = base + (t < 48 ? t : 47);
+    const uint32_t i = s < n ? s : n - 1;
+    const uint32_t m0 = off[i], m1 = off[i + 1];
+    LdsStrobeState st{reinterpret_cast<uint32_t*>(xbuf), t};
+    SigPrep p;
+    sr_prepare(p, pk + 8 * (size_t)i, sig + 16 * (size_t)i, msg + m0, m1 - m0, prog, nops, st, force_wide != 0);
+    const int W = hs_workgroup_windows(p.flags, t);
+    p.flags |= (uint32_t)W << 16;
+    if (t < 48) sig_prep_store(prep[t], p);
+    BComb16 bc;
+    bc.init(p.u);
+    const DevBTab bt{btab};
+#pragma unroll 1
+    for (int k = 0; k < comb_pre; k++) bc.step(bt);
+    __syncthreads();  // 1: the scalars; the tables are built
+    uint64_t hwait = 0;
+    hs_helper_windows(p, W, bc, &tab_lds[0][0], xbuf, t, [] { return (uint64_t)0; }, hwait);
+    __syncthreads();  // B: [u]B
+    return;
+  }
+  const uint32_t ls = wave * 16 + (t >> 2);
+  const uint32_t s = base + ls;
+  const bool active = s < n;
+  const uint32_t i = active ? s : n - 1;
+  DevQuad q;
+  DevBTabQ bt{btab};
+  DevATabQ ta{tab_lds[wave], t}, tr{tab_lds[wave] + 9 * 5 * 64, t};
+  bool v = q_verify_sr_hs(
+      q, pk + 8 * (size_t)i, sig + 16 * (size_t)i, bt, ta, tr, 16 - comb_pre,
+      [&](SigPrep& p) {
+        __syncthreads();
+        sig_prep_load(p, prep[ls]);
+      },
+      [&](int win, fe& c) {
+        __syncthreads();
+        hs_slot_load(xbuf + (win & 1) * kHsSlotU2, wave, t, c);
+      },
+      [&](fe& c) {
+        __syncthreads();
+        hs_slot_load(xbuf + kHsSlotU2, wave, t, c);
+      });
+  v = v && active;
+  if (active && (t & 3) == 0 && out_valid) out_valid[s] = v ? 1 : 0;
+  uint64_t x = __ballot(v && (t & 3) == 0) & 0x1111111111111111ull;
+  x = (x | (x >> 3)) & 0x0303030303030303ull;
+  x = (x | (x >> 6)) & 0x000F000F000F000Full;
+  x = (x | (x >> 12)) & 0x000000FF000000FFull;
+  x = (x | (x >> 24)) & 0xFFFFull;
+  const uint32_t slice = blockIdx.x * 3 + wave;
+  if (t == 0 && out_bitmap && slice < 4 * ((n + 63) / 64)) reinterpret_cast<uint16_t*>(out_bitmap)[slice] = (uint16_t)x;
+}
+
 hipError_t launch_verify_sr25519(uint32_t n, const void* pk, const void* sig, const void* msg, const void* off,
                                  const uint32_t* btab, uint32_t* atab, const uint16_t* prog, int nops, void* valid,
                                  void* bitmap, uint32_t kflags, hipStream_t s) {
   if (n == 0) return hipSuccess;
   const bool quad = kflags & kLaunchQuad;
+  if (quad && (kflags & kLaunchQuadSplit) && (kflags & kLaunchQuadHS)) {
+    const uint32_t slices = 4 * ((n + 63) / 64);
+    hipLaunchKernelGGL(k_verify_sr25519_quad_hs, dim3((slices + 2) / 3), dim3(256), 0, s, n,
+                       static_cast<const uint32_t*>(pk), static_cast<const uint32_t*>(sig),
+                       static_cast<const uint8_t*>(msg), static_cast<const uint32_t*>(off), btab, prog, nops,
+                       static_cast<uint8_t*>(valid), static_cast<uint64_t*>(bitmap),
+                       (kflags & kLaunchForceWide) ? 1u : 0u, kflags >> 16);
+    return hipGetLastError();
+  }
   if (quad && (kflags & kLaunchQuadSplit)) {
     const uint32_t slices = 4 * ((n + 63) / 64);
     hipLaunchKernelGGL(k_verify_sr25519_quad_split, dim3((slices + 2) / 3), dim3(256), 0, s, n,

@@ -99,6 +99,53 @@ CMTV_HD bool q_verify_sr_split(const Q& q, const uint32_t* pk_ptr, const uint32_
   return s_ok && a_ok && r_ok && (e0 || e1);
 }
 
+// The helper-summed form (k_verify_sr25519_quad_hs): the ristretto decode as
+// q_verify_sr_split, the windows of quad.h q_hs_straus (the helper wave adds
+// every window's two table entries), the E[4] check
+template <class Q, class BTab, class ATab, class GetPrep, class GetS, class GetB>
+CMTV_HD bool q_verify_sr_hs(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig_ptr, const BTab& btab,
+                            ATab& tabA, ATab& tabR, int j0, const GetPrep& get_prep, const GetS& get_s,
+                            const GetB& get_b) {
+  const int lane = q.lane();
+  fe v, rc;
+  bool a_ok, r_ok;
+  {
+    uint32_t w[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) w[i] = (lane & 1) ? sig_ptr[i] : pk_ptr[i];
+    ge_p3 P;
+    const bool dec = ristretto_decode(P, w);
+    fe x, y, t, one;
+    fe_1(one);
+    q.template perm<QP_B0>(x, P.X);
+    q.template perm<QP_B0>(y, P.Y);
+    q.template perm<QP_B0>(t, P.T);
+    fe_pick(v, lane, x, y, one, t);  // A
+    q.template perm<QP_B1>(x, P.X);
+    q.template perm<QP_B1>(y, P.Y);
+    q.template perm<QP_B1>(t, P.T);
+    fe_pick(rc, lane, x, y, one, t);  // R
+    a_ok = q.template perm32<QP_B0>(dec ? 1u : 0u) != 0;
+    r_ok = q.template perm32<QP_B1>(dec ? 1u : 0u) != 0;
+    // -A and -R: negate X (lane 0) and T (lane 3)
+    const bool xt = lane == 0 || lane == 3;
+    fe_neg(t, v);
+    fe_carry(t);
+    fe_select(v, v, t, xt);
+    fe_neg(t, rc);
+    fe_carry(t);
+    fe_select(rc, rc, t, xt);
+  }
+  SigPrep p;
+  q_hs_straus(q, v, rc, btab, tabA, tabR, j0, p, get_prep, get_s, get_b);
+  const bool s_ok = (p.flags & 4u) != 0;
+  // ---- X in E[4]: X.X = 0 (lane 0) or X.Y = 0 (lane 1)
+  const bool z = fe_iszero(v);
+  const bool e0 = q.template perm32<QP_B0>(z ? 1u : 0u) != 0;
+  const bool e1 = q.template perm32<QP_B1>(z ? 1u : 0u) != 0;
+  return s_ok && a_ok && r_ok && (e0 || e1);
+}
+
 // One wave does everything (k_verify_sr25519_quad; the host checks)
 template <class Q, class BTab, class ATab, class State, class Probe = NullProbe>
 CMTV_HD bool q_verify_sr(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig_ptr, const uint8_t* msg,

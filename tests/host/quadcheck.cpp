@@ -179,7 +179,10 @@ int main(int argc, char** argv) {
   // tables built before the scalars arrive (q_tables_early: R's table is of
   // -R, a negative k2 flips R's digits at lookup), then q_verify_sr_split<true>
   const bool sr2 = argc > 1 && !strcmp(argv[1], "sr2");
-  const bool sr = sr2 || (argc > 1 && !strcmp(argv[1], "sr"));
+  // argv[1] == "sr3": sr25519 through k_verify_sr25519_quad_hs's path (as
+  // "quad3" below, q_verify_sr_hs)
+  const bool sr3 = argc > 1 && !strcmp(argv[1], "sr3");
+  const bool sr = sr2 || sr3 || (argc > 1 && !strcmp(argv[1], "sr"));
   // argv[1] == "keyed": Ed25519 records, verified through registered-key combs (keyed_quad.h)
   const bool keyed = argc > 1 && !strcmp(argv[1], "keyed");
   // argv[1] == "keyedmix": one lane, the key's radix-256 comb with B over the
@@ -251,7 +254,7 @@ int main(int argc, char** argv) {
     std::vector<std::thread> th;
     SigPrep hp;
     uint32_t bpt[40];
-    if (sr2) {
+    if (sr2 || sr3) {
       ArrayStrobeState st;
       sr_prepare(hp, pkw, sigw, mp, mlen, prog, nops, st, false);
       ge_p3 Bp;
@@ -299,7 +302,7 @@ int main(int argc, char** argv) {
           }
         });
     }
-    if (quad3) {
+    if (quad3 || sr3) {
       const bool wide = (hp.flags & 2u) != 0;
       const int own = (int)((hp.flags >> 8) & 0xFFu);
       const int W = wide ? HS_WIDE_WINDOWS : (own + (int)(i % 3) > HS_MAX_WINDOWS ? HS_MAX_WINDOWS : own + (int)(i % 3));
@@ -336,8 +339,11 @@ int main(int argc, char** argv) {
           auto get_b = [&](fe& c) {
             for (int j = 0; j < 10; j++) c.v[j] = bpt3[10 * l + j];
           };
-          res[l] = mode ? q_verify_hs<MODE_ZIP215>(q, pkw, sigw, bt, ta[l], tr[l], 16 - pre, get_prep, get_s, get_b)
-                        : q_verify_hs<MODE_GO_STDLIB>(q, pkw, sigw, bt, ta[l], tr[l], 16 - pre, get_prep, get_s, get_b);
+          if (sr3)
+            res[l] = q_verify_sr_hs(q, pkw, sigw, bt, ta[l], tr[l], 16 - pre, get_prep, get_s, get_b);
+          else
+            res[l] = mode ? q_verify_hs<MODE_ZIP215>(q, pkw, sigw, bt, ta[l], tr[l], 16 - pre, get_prep, get_s, get_b)
+                          : q_verify_hs<MODE_GO_STDLIB>(q, pkw, sigw, bt, ta[l], tr[l], 16 - pre, get_prep, get_s, get_b);
         });
     }
     if (oct) {
@@ -350,7 +356,7 @@ int main(int argc, char** argv) {
                         : o_verify<MODE_GO_STDLIB>(q, pkw, sigw, mp, mlen, bt, ta);
         });
     }
-    for (int l = 0; l < (oct || quad2 || oct2 || sr2 || quad3 ? 0 : 4); l++)
+    for (int l = 0; l < (oct || quad2 || oct2 || sr2 || quad3 || sr3 ? 0 : 4); l++)
       th.emplace_back([&, l] {
         HostQuad q{l, &ex};
         QArrayTab ta, tr;

@@ -210,3 +210,18 @@ def test_split_quad_pipeline_matches_corpus(vectors):
     assert bad.size == 0, [(int(i), vectors["cats"][int(i)]) for i in bad[:10]]
     neg = int(r.stderr.decode().split("k2_neg ")[1].split()[0])
     assert 0.2 * len(idx) < neg < 0.8 * len(idx), neg
+
+
+def test_helper_summed_quad_pipeline_matches_corpus(vectors):
+    """k_verify_sr25519_quad_hs's path (sr25519_quad.h q_verify_sr_hs on
+    quad.h q_hs_straus): both tables of extended points before the scalars,
+    every window's two entries summed as the helper wave does
+    (h_window_addend over the four lane threads' tables), window counts raised
+    by 0-2 and the helper's share of [u]B varied, over the whole corpus."""
+    hostbuild.build(QSRC, QBIN, ["-std=c++20", "-pthread"])
+    idx = list(range(len(vectors["cats"])))
+    buf = _srcheck_input(vectors, idx)
+    r = subprocess.run([QBIN, "sr3"], input=buf, capture_output=True, check=True, timeout=600)
+    got = np.frombuffer(r.stdout, np.uint8)
+    bad = np.nonzero(got != vectors["valid"])[0]
+    assert bad.size == 0, [(int(i), vectors["cats"][int(i)]) for i in bad[:10]]

@@ -34,6 +34,19 @@ constexpr uint32_t kLaunchQuadHS = 256;
 // fences a reuse against the slot's previous launch (runtime.cpp
 // row_slot_acquire). kRowMaxCap bounds a row launch.
 constexpr uint32_t kRowSlots = 256, kRowSlotWords = 1024, kRowMaxCap = 4 * (kRowSlotWords - 16);
+// A row launch's ring slot and, optionally, its tagged bitmap: with tagged
+// set (a device pointer to mapped host memory, one entry per 32 signatures),
+// the wave that completes word j stores (seq << 32 | the word's 32 bits) into
+// tagged[j] with ONE 64-bit system-scope atomic store instead of writing the
+// bitmap, so the host knows the bitmap is complete when every entry carries
+// seq -- without waiting for the kernel to retire, and without any ordering
+// between the waves' stores (runtime.cpp wait_row_tags). The slot word is zero
+// again before its entry is stored.
+struct RowSlot {
+  uint32_t* words = nullptr;
+  uint64_t* tagged = nullptr;
+  uint32_t seq = 0;
+};
 
 // Templated sign-bytes (signbytes.h) written by the helper waves of the
 // split kernels themselves (k_verify_oct_split / k_verify_quad_split): each
@@ -65,7 +78,7 @@ hipError_t launch_btab_init(uint32_t* d_rows, hipStream_t s);
 // device's ring when bitmap is set)
 hipError_t launch_verify(uint32_t mode, uint32_t n, const void* pk, const void* sig, const void* msg,
                          const void* off, const uint32_t* btab, uint32_t* atab, void* valid, void* bitmap,
-                         uint32_t kflags, hipStream_t s, const SbFuse* sb = nullptr, uint32_t* row_slot = nullptr);
+                         uint32_t kflags, hipStream_t s, const SbFuse* sb = nullptr, const RowSlot* row_slot = nullptr);
 hipError_t launch_comb_build(uint32_t n_keys, const void* keys_pk, uint8_t* keys_ok, uint32_t* tabs,
                              uint32_t* scratch, bool negate, hipStream_t s);
 hipError_t launch_verify_keyed(uint32_t mode, uint32_t n, uint32_t n_keys, const void* key_idx, const void* sig,
@@ -73,7 +86,7 @@ hipError_t launch_verify_keyed(uint32_t mode, uint32_t n, uint32_t n_keys, const
                                const uint32_t* ktabs, const uint32_t* bcomb, void* valid, void* bitmap,
                                bool quad, bool split, uint32_t k_wait, uint32_t* diag, uint32_t batch_kb,
                                uint32_t* scr, const uint32_t* wtabs, const uint32_t* btab, bool wide_dma,
-                               hipStream_t s, uint32_t* row_slot = nullptr, bool mixed = true);
+                               hipStream_t s, const RowSlot* row_slot = nullptr, bool mixed = true);
 // (row_slot set: the keyed row kernel, k_verify_keyed_row_split, one
 // signature per workgroup; a slot of the device's bitmap ring)
 // the one-signature-per-lane part of launch_verify_keyed (keyed_lane.hip):

@@ -575,9 +575,9 @@ __device__ __forceinline__ void helper_bcomb_prefetched(ge_p3& B, const uint32_t
 // wave, the last wave packing) made every wave write back and invalidate its
 // XCD's L2 (buffer_wbl2 sc1 / buffer_inv sc1), ~10 us of a 150-signature
 // launch (tools/microbench/launch_lat.hip).
-__device__ __forceinline__ void row_bitmap_add(uint32_t* __restrict__ slot, uint32_t s, uint32_t n, bool v,
+__device__ __forceinline__ void row_bitmap_add(const RowSlot& slot, uint32_t s, uint32_t n, bool v,
                                                uint64_t* __restrict__ out_bitmap, uint32_t t) {
-  uint64_t* sw = reinterpret_cast<uint64_t*>(slot);
+  uint64_t* sw = reinterpret_cast<uint64_t*>(slot.words);
   const uint32_t j = s >> 5, f = s & 31;
   uint64_t x = 0;
   if (t == 0) {
@@ -590,10 +590,15 @@ __device__ __forceinline__ void row_bitmap_add(uint32_t* __restrict__ slot, uint
   if (((x | (x >> 1)) & m) != m) return;  // a field of word j is still empty
   const uint64_t acc = __ballot(t < 32 && ((x >> (2 * (t & 31) + 1)) & 1) != 0);
   if (t == 0) {
+    __hip_atomic_store(sw + j, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (slot.tagged) {  // kernels.h RowSlot
+      __hip_atomic_store(slot.tagged + j, ((uint64_t)slot.seq << 32) | (uint32_t)acc, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
     uint32_t* ob = reinterpret_cast<uint32_t*>(out_bitmap);
     ob[j] = (uint32_t)acc;
     if ((j & 1) == 0 && 32 * (j + 1) >= n) ob[j + 1] = 0u;
-    __hip_atomic_store(sw + j, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -605,14 +610,13 @@ __device__ __forceinline__ void row_bitmap_add(uint32_t* __restrict__ slot, uint
 // included); the scalars reach them at barrier 1 and [u]B (q_bcomb16, as
 // four canonical encodings) at barrier 2, after which wave 3 exits. LDS:
 // 3 x 9 KiB tables, one workgroup per CU, i.e. one wave per SIMD.
-// Verdicts: lane 0 of each wave writes its byte to out_valid and to the
-// launch's ring slot; the last wave to finish (an agent-scope counter) packs
-// the bitmap words and resets the counter.
+// Verdicts: lane 0 of each wave writes its byte to out_valid and adds its
+// field to the launch's ring slot (row_bitmap_add).
 template <uint32_t MODE>
 __global__ __launch_bounds__(256, 1) void k_verify_row_split(
     uint32_t n, const uint32_t* __restrict__ pk, const uint32_t* __restrict__ sig, const uint8_t* __restrict__ msg,
     const uint32_t* __restrict__ off, const uint32_t* __restrict__ btab, uint8_t* __restrict__ out_valid,
-    uint64_t* __restrict__ out_bitmap, uint32_t force_wide, SbFuse sb, uint32_t* __restrict__ slot) {
+    uint64_t* __restrict__ out_bitmap, uint32_t force_wide, SbFuse sb, RowSlot slot) {
   const uint32_t wave = threadIdx.x >> 6, t = threadIdx.x & 63;
   const uint32_t base = blockIdx.x * 3;
   __shared__ uint32_t prep[3][SIG_PREP_WORDS + 1];
@@ -684,7 +688,7 @@ template <uint32_t MODE>
 __global__ __launch_bounds__(192, 1) void k_verify_row2_split(
     uint32_t n, const uint32_t* __restrict__ pk, const uint32_t* __restrict__ sig, const uint8_t* __restrict__ msg,
     const uint32_t* __restrict__ off, const uint32_t* __restrict__ btab, uint8_t* __restrict__ out_valid,
-    uint64_t* __restrict__ out_bitmap, uint32_t force_wide, SbFuse sb, uint32_t* __restrict__ slot) {
+    uint64_t* __restrict__ out_bitmap, uint32_t force_wide, SbFuse sb, RowSlot slot) {
   const uint32_t wave = threadIdx.x >> 6, t = threadIdx.x & 63;
   const uint32_t s = blockIdx.x;
   const uint32_t i = s < n ? s : n - 1;
@@ -787,7 +791,7 @@ template <uint32_t MODE>
 __global__ __launch_bounds__(256, 1) void k_verify_row4_split(
     uint32_t n, const uint32_t* __restrict__ pk, const uint32_t* __restrict__ sig, const uint8_t* __restrict__ msg,
     const uint32_t* __restrict__ off, const uint32_t* __restrict__ btab, uint8_t* __restrict__ out_valid,
-    uint64_t* __restrict__ out_bitmap, uint32_t force_wide, SbFuse sb, uint32_t* __restrict__ slot) {
+    uint64_t* __restrict__ out_bitmap, uint32_t force_wide, SbFuse sb, RowSlot slot) {
   const uint32_t wave = threadIdx.x >> 6, t = threadIdx.x & 63;
   const uint32_t s = blockIdx.x;
   const uint32_t i = s < n ? s : n - 1;
@@ -885,7 +889,7 @@ __global__ __launch_bounds__(256, 1) void k_verify_keyed_row_split(
     uint32_t n, uint32_t n_keys, const uint32_t* __restrict__ key_idx, const uint32_t* __restrict__ sig,
     const uint8_t* __restrict__ msg, const uint32_t* __restrict__ off, const uint32_t* __restrict__ keys_pk,
     const uint8_t* __restrict__ keys_ok, const uint32_t* __restrict__ ktabs, const uint32_t* __restrict__ btab,
-    uint8_t* __restrict__ out_valid, uint64_t* __restrict__ out_bitmap, uint32_t* __restrict__ slot) {
+    uint8_t* __restrict__ out_valid, uint64_t* __restrict__ out_bitmap, RowSlot slot) {
   const uint32_t wave = threadIdx.x >> 6, t = threadIdx.x & 63;
   const uint32_t s = blockIdx.x;
   const uint32_t i = s < n ? s : n - 1;
@@ -1099,7 +1103,7 @@ hipError_t launch_btab_init(uint32_t* d_rows, hipStream_t s) {
 
 hipError_t launch_verify(uint32_t mode, uint32_t n, const void* pk, const void* sig, const void* msg,
                          const void* off, const uint32_t* btab, uint32_t* atab, void* valid, void* bitmap,
-                         uint32_t kflags, hipStream_t s, const SbFuse* sb, uint32_t* row_slot) {
+                         uint32_t kflags, hipStream_t s, const SbFuse* sb, const RowSlot* row_slot) {
   const SbFuse fz = sb ? *sb : SbFuse{};
   const bool quad = kflags & kLaunchQuad;
   const uint32_t fw = (kflags & kLaunchForceWide) ? 1u : 0u;
@@ -1110,40 +1114,41 @@ hipError_t launch_verify(uint32_t mode, uint32_t n, const void* pk, const void* 
   auto op = static_cast<const uint32_t*>(off);
   auto vp = static_cast<uint8_t*>(valid);
   auto bp = static_cast<uint64_t*>(bitmap);
+  const RowSlot rs = row_slot ? *row_slot : RowSlot{};
   if (kflags & kLaunchRow4) {
     // one signature per 256-lane block (lo, A-hi, R-hi, the helper)
-    if (n > kRowMaxCap || (bp && !row_slot)) return hipErrorInvalidValue;
+    if (n > kRowMaxCap || (bp && !rs.words)) return hipErrorInvalidValue;
     const dim3 grid(n), block(256);
     if (mode == MODE_ZIP215)
       hipLaunchKernelGGL(k_verify_row4_split<MODE_ZIP215>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp, fw,
-                         fz, row_slot);
+                         fz, rs);
     else
       hipLaunchKernelGGL(k_verify_row4_split<MODE_GO_STDLIB>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp,
-                         fw, fz, row_slot);
+                         fw, fz, rs);
     return hipGetLastError();
   }
   if (kflags & kLaunchRow2) {
     // one signature per 192-lane block (an A wave, an R wave, the helper)
-    if (n > kRowMaxCap || (bp && !row_slot)) return hipErrorInvalidValue;
+    if (n > kRowMaxCap || (bp && !rs.words)) return hipErrorInvalidValue;
     const dim3 grid(n), block(192);
     if (mode == MODE_ZIP215)
       hipLaunchKernelGGL(k_verify_row2_split<MODE_ZIP215>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp, fw,
-                         fz, row_slot);
+                         fz, rs);
     else
       hipLaunchKernelGGL(k_verify_row2_split<MODE_GO_STDLIB>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp,
-                         fw, fz, row_slot);
+                         fw, fz, rs);
     return hipGetLastError();
   }
   if (kflags & kLaunchRow) {
     // 3 signatures per 256-lane block (3 row waves + the helper)
-    if (n > kRowMaxCap || (bp && !row_slot)) return hipErrorInvalidValue;
+    if (n > kRowMaxCap || (bp && !rs.words)) return hipErrorInvalidValue;
     const dim3 grid((n + 2) / 3), block(256);
     if (mode == MODE_ZIP215)
       hipLaunchKernelGGL(k_verify_row_split<MODE_ZIP215>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp, fw,
-                         fz, row_slot);
+                         fz, rs);
     else
       hipLaunchKernelGGL(k_verify_row_split<MODE_GO_STDLIB>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp,
-                         fw, fz, row_slot);
+                         fw, fz, rs);
     return hipGetLastError();
   }
   if (quad && (kflags & kLaunchOctSplit)) {
@@ -1336,7 +1341,7 @@ hipError_t launch_verify_keyed(uint32_t mode, uint32_t n, uint32_t n_keys, const
                                const uint32_t* ktabs, const uint32_t* bcomb, void* valid, void* bitmap,
                                bool quad, bool split, uint32_t k_wait, uint32_t* diag, uint32_t batch_kb,
                                uint32_t* scr, const uint32_t* wtabs, const uint32_t* btab, bool wide_dma,
-                               hipStream_t s, uint32_t* row_slot, bool mixed) {
+                               hipStream_t s, const RowSlot* row_slot, bool mixed) {
   if (n == 0) return hipSuccess;
   auto ki = static_cast<const uint32_t*>(key_idx);
   auto sgp = static_cast<const uint32_t*>(sig);
@@ -1349,10 +1354,10 @@ hipError_t launch_verify_keyed(uint32_t mode, uint32_t n, uint32_t n_keys, const
     if (n > kRowMaxCap) return hipErrorInvalidValue;
     if (mode == MODE_ZIP215)
       hipLaunchKernelGGL(k_verify_keyed_row_split<MODE_ZIP215>, dim3(n), dim3(256), 0, s, n, n_keys, ki, sgp, mp, op,
-                         keys_pk, keys_ok, ktabs, btab, vp, bp, row_slot);
+                         keys_pk, keys_ok, ktabs, btab, vp, bp, *row_slot);
     else
       hipLaunchKernelGGL(k_verify_keyed_row_split<MODE_GO_STDLIB>, dim3(n), dim3(256), 0, s, n, n_keys, ki, sgp, mp,
-                         op, keys_pk, keys_ok, ktabs, btab, vp, bp, row_slot);
+                         op, keys_pk, keys_ok, ktabs, btab, vp, bp, *row_slot);
     return hipGetLastError();
   }
   if (quad && split) {

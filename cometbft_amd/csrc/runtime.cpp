@@ -390,6 +390,16 @@ struct CmtvDev {
   // (row_slot_acquire), so a slot is never shared by two launches in flight
   hipEvent_t row_ev[cmtv::kRowSlots] = {};
   bool row_pending[cmtv::kRowSlots] = {};
+  // the row kernels' tagged bitmap (kernels.h RowSlot) for small host
+  // batches: run_host_batch_ arms tag_arm (h_tags' device pointer) and a fresh
+  // tag_seq around its launch; a row launch that takes them sets tag_used, and
+  // the call polls the entries (wait_row_tags) instead of synchronising the
+  // stream
+  HostBuf h_tags{nullptr, 0, hipHostMallocCoherent | hipHostMallocMapped};
+  uint64_t* d_tags = nullptr;
+  uint64_t* tag_arm = nullptr;
+  uint32_t tag_seq = 0;
+  bool tag_used = false;
   // a device that returned a HIP error is taken out of the context's
   // rotation: host batches are re-planned over the others (runtime.cpp
   // run_host_batch); CMTV_FAULT_DEV=g makes device g's first launch fail
@@ -463,6 +473,9 @@ struct cmtv_ctx {
   bool zc_in = true;
   // single-device host batches up to this size take the mapped-memory path (CMTV_ZC_MAX)
   size_t zc_max = kZeroCopyMax;
+  // small host batches on a row kernel poll its tagged bitmap words
+  // (run_host_batch_); CMTV_HOST_POLL=0 synchronises the stream
+  bool host_poll = true;
   // set while a host-buffer call runs (run_host_batch): its launches finish
   // before the call returns, so their row-ring slots need no fence event
   bool host_sync = false;
@@ -564,9 +577,19 @@ static hipError_t release_scratch(CmtvDev& D, hipStream_t s) {
 // (enqueued on a caller's stream, not waited for before its call returned) is
 // fenced: s waits for that launch's event. Host-buffer calls finish their
 // launches before they return (ctx->host_sync) and record nothing.
-static hipError_t row_slot_acquire(cmtv_ctx* ctx, CmtvDev& D, hipStream_t s, uint32_t*& slot, uint32_t& k) {
+// With a bitmap, a launch of an armed host batch also takes the tagged bitmap
+// (CmtvDev::tag_arm). Each entry is stored after its slot word is zero again,
+// so a slot needs no fence against a tagged launch still retiring.
+static hipError_t row_slot_acquire(cmtv_ctx* ctx, CmtvDev& D, hipStream_t s, bool bitmap, RowSlot& slot,
+                                   uint32_t& k) {
   k = D.row_seq++ % kRowSlots;
-  slot = D.d_rowslots + (size_t)k * kRowSlotWords;
+  slot = RowSlot{};
+  slot.words = D.d_rowslots + (size_t)k * kRowSlotWords;
+  if (bitmap && D.tag_arm) {
+    slot.tagged = D.tag_arm;
+    slot.seq = D.tag_seq;
+    D.tag_used = true;
+  }
   if (!D.row_pending[k] || !ctx->row_fence) return hipSuccess;
   hipError_t e = hipEventQuery(D.row_ev[k]);
   if (e == hipErrorNotReady) e = hipStreamWaitEvent(s, D.row_ev[k], 0);
@@ -638,9 +661,9 @@ static int enqueue_verify(cmtv_ctx* ctx, CmtvDev& D, size_t n, const uint8_t* d_
       return hip_fail(e);
   }
   // a row launch is one chunk (n <= kRowMaxCap)
-  uint32_t* slot = nullptr;
+  RowSlot slot;
   uint32_t slot_k = 0;
-  if (row && (e = row_slot_acquire(ctx, D, s, slot, slot_k)) != hipSuccess) return hip_fail(e);
+  if (row && (e = row_slot_acquire(ctx, D, s, d_bitmap != nullptr, slot, slot_k)) != hipSuccess) return hip_fail(e);
   D.timing.harvest(ctx->stats, D.device_ms, D.timed_calls, false);
   Timing::Pair tp;
   const bool timed = ctx->timing_every && D.timing_seq++ % ctx->timing_every == 0;
@@ -655,7 +678,7 @@ static int enqueue_verify(cmtv_ctx* ctx, CmtvDev& D, size_t n, const uint8_t* d_
     else
       e = launch_verify(mode, cn, d_pk + 32 * c, d_sig + 64 * c, d_msg, d_off + c, D.d_btab,
                         static_cast<uint32_t*>(D.d_atab.p), d_valid ? d_valid + c : nullptr,
-                        d_bitmap ? d_bitmap + c / 64 : nullptr, kflags, s, sb, slot);
+                        d_bitmap ? d_bitmap + c / 64 : nullptr, kflags, s, sb, row ? &slot : nullptr);
     if (e == hipSuccess && row) e = row_slot_release(ctx, D, s, slot_k);
     if (e != hipSuccess) {
       D.timing.abandon(tp);
@@ -727,9 +750,10 @@ static int enqueue_verify_keyed(cmtv_ctx* ctx, CmtvDev& D, const cmtv_keyset::Pe
   // the keyed row kernel up to CMTV_KEYED_ROW_MAX (below the keyed quad
   // knob): one chunk, one slot of the bitmap ring
   const bool krow = quad && n <= ctx->keyed_row_max && n <= kRowMaxCap;
-  uint32_t* slot = nullptr;
+  RowSlot slot;
   uint32_t slot_k = 0;
-  if (krow && (e = row_slot_acquire(ctx, D, s, slot, slot_k)) != hipSuccess) return hip_fail(e);
+  if (krow && (e = row_slot_acquire(ctx, D, s, d_bitmap != nullptr, slot, slot_k)) != hipSuccess)
+    return hip_fail(e);
   D.timing.harvest(ctx->stats, D.device_ms, D.timed_calls, false);
   Timing::Pair tp;
   const bool timed = ctx->timing_every && D.timing_seq++ % ctx->timing_every == 0;
@@ -742,7 +766,8 @@ static int enqueue_verify_keyed(cmtv_ctx* ctx, CmtvDev& D, const cmtv_keyset::Pe
                             K.d_tab, D.d_bcomb, d_valid ? d_valid + c : nullptr,
                             d_bitmap ? d_bitmap + c / 64 : nullptr, quad, n <= ctx->quad_split_max,
                             ctx->keyed_wait, D.d_diag, kb, static_cast<uint32_t*>(D.d_atab.p),
-                            quad ? nullptr : K.d_wide, D.d_btab, ctx->wide_dma, s, slot, ctx->keyed_mixed);
+                            quad ? nullptr : K.d_wide, D.d_btab, ctx->wide_dma, s, krow ? &slot : nullptr,
+                            ctx->keyed_mixed);
     if (e == hipSuccess && krow) e = row_slot_release(ctx, D, s, slot_k);
     if (e != hipSuccess) {
       D.timing.abandon(tp);
@@ -952,6 +977,28 @@ static int enqueue_shard(cmtv_ctx* ctx, size_t g, const HostBatch& B, size_t a, 
 
 // Verdicts of a host batch, sharded over the context's live devices. Caller
 // holds the lock. On a device's HIP error *bad_dev names it.
+// Wait for a tagged row launch (CmtvDev::tag_used) of n signatures on device
+// D: poll the entries until each carries the call's tag, asking the stream
+// every 256 polls so that an error ends the wait; a launch that finished with
+// an entry untagged (which cannot happen) is an error, not a hang.
+static hipError_t wait_row_tags(CmtvDev& D, size_t n) {
+  const uint64_t* e = static_cast<const uint64_t*>(D.h_tags.p);
+  const size_t n32 = (n + 31) / 32;
+  size_t j = 0;
+  auto scan = [&] {
+    while (j < n32 && (uint32_t)(__atomic_load_n(e + j, __ATOMIC_ACQUIRE) >> 32) == D.tag_seq) j++;
+    return j == n32;
+  };
+  for (uint32_t spin = 1;; spin++) {
+    if (scan()) return hipSuccess;
+    if ((spin & 255) == 0) {
+      const hipError_t q = hipStreamQuery(D.stream);
+      if (q == hipSuccess) return scan() ? hipSuccess : hipErrorLaunchFailure;
+      if (q != hipErrorNotReady) return q;
+    }
+  }
+}
+
 static int run_host_batch_(cmtv_ctx* ctx, const HostBatch& B, uint8_t* out_valid, uint64_t* out_bitmap,
                            long* bad_dev) {
   const size_t n = B.n;
@@ -971,11 +1018,32 @@ static int run_host_batch_(cmtv_ctx* ctx, const HostBatch& B, uint8_t* out_valid
     if ((e = D.h_zc.ensure(8 * words)) != hipSuccess) return hip_fail(e);
     void* dzc = nullptr;
     if ((e = hipHostGetDevicePointer(&dzc, D.h_zc.p, 0)) != hipSuccess) return hip_fail(e);
+    // a row launch tags its bitmap words (kernels.h RowSlot; CMTV_HOST_POLL=0:
+    // it writes the bitmap and the call waits for the stream)
+    if (ctx->host_poll && !D.d_tags) {
+      void* dt = nullptr;
+      if ((e = D.h_tags.ensure(8 * (kRowMaxCap / 32 + 1))) != hipSuccess) return hip_fail(e);
+      std::memset(D.h_tags.p, 0, 8 * (kRowMaxCap / 32 + 1));
+      if ((e = hipHostGetDevicePointer(&dt, D.h_tags.p, 0)) != hipSuccess) return hip_fail(e);
+      D.d_tags = static_cast<uint64_t*>(dt);
+    }
+    if (ctx->host_poll && ++D.tag_seq == 0) D.tag_seq = 1;
+    D.tag_arm = ctx->host_poll ? D.d_tags : nullptr;
+    D.tag_used = false;
     size_t o_valid = 0;
     const int rc = enqueue_shard(ctx, d0, B, 0, n, false, static_cast<uint64_t*>(dzc), o_valid, true);
+    D.tag_arm = nullptr;
     if (rc != CMTV_OK) return rc;
     const uint64_t t_wait = phase_now(ctx);
-    if ((e = hipStreamSynchronize(D.stream)) != hipSuccess) return hip_fail(e);
+    if ((e = D.tag_used ? wait_row_tags(D, n) : hipStreamSynchronize(D.stream)) != hipSuccess) return hip_fail(e);
+    uint64_t* bm = static_cast<uint64_t*>(D.h_zc.p);
+    if (D.tag_used) {
+      ctx->stats.polled_calls++;
+      const uint64_t* tg = static_cast<const uint64_t*>(D.h_tags.p);
+      const size_t n32 = (n + 31) / 32;
+      for (size_t w = 0; w < words; w++)
+        bm[w] = (tg[2 * w] & 0xFFFFFFFFull) | (2 * w + 1 < n32 ? (tg[2 * w + 1] & 0xFFFFFFFFull) << 32 : 0);
+    }
     phase_add(ctx, kPhWait, t_wait);
     const uint64_t t_post = phase_now(ctx);
     if ((long)d0 == ctx->fault_sync_dev) {  // CMTV_FAULT_SYNC_DEV (see below)
@@ -985,7 +1053,6 @@ static int run_host_batch_(cmtv_ctx* ctx, const HostBatch& B, uint8_t* out_valid
     *bad_dev = -1;
     harvest(ctx, false);
     (void)hipSetDevice(D.ordinal);
-    uint64_t* bm = static_cast<uint64_t*>(D.h_zc.p);
     // bits past n of the last word are not written by every kernel
     if (n & 63) bm[words - 1] &= (1ull << (n & 63)) - 1;
     uint64_t valid_count = 0;
@@ -1274,6 +1341,8 @@ static void release_device(CmtvDev& D) {
   D.h_in.release();
   D.h_out.release();
   D.h_zc.release();
+  D.h_tags.release();
+  D.d_tags = nullptr;
   D.h_zin.release();
   if (D.d_btab) (void)hipFree(D.d_btab);
   if (D.d_bcomb) (void)hipFree(D.d_bcomb);
@@ -1321,6 +1390,7 @@ static void read_env(cmtv_ctx* ctx) {
   if (const char* nf = std::getenv("CMTV_NO_SB_FUSE")) ctx->sb_fuse = nf[0] != '1';
   if (const char* nz = std::getenv("CMTV_NO_ZC_IN")) ctx->zc_in = nz[0] != '1';
   if (const char* zm = std::getenv("CMTV_ZC_MAX")) ctx->zc_max = (size_t)std::strtoull(zm, nullptr, 10);
+  if (const char* hp = std::getenv("CMTV_HOST_POLL")) ctx->host_poll = std::atoi(hp) != 0;
   if (const char* kl = std::getenv("CMTV_FORCE_K_LATE")) ctx->keyed_wait = kl[0] == '1' ? 0u : kKeyedWaitDefault;
   if (const char* kb = std::getenv("CMTV_KEYED_BATCH")) ctx->keyed_batch = kb[0] != '0';
   if (const char* wd = std::getenv("CMTV_WIDE_DMA")) ctx->wide_dma = wd[0] != '0';

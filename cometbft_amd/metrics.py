@@ -48,6 +48,8 @@ _FIELDS = [
      "Calls whose kernel time device_seconds holds (CMTV_TIMING samples one call in N per device)."),
     ("rccl_failures", "rccl_failures_total", "counter",
      "RCCL bitmap all-gathers that failed and fell back to peer copies."),
+    ("polled_calls", "polled_calls_total", "counter",
+     "Small host batches read off the row kernel's completion flag (no stream synchronisation)."),
 ]
 
 

@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define CMTV_ABI_VERSION 9
+#define CMTV_ABI_VERSION 10
 
 enum {
   CMTV_OK = 0,
@@ -106,6 +106,10 @@ typedef struct cmtv_stats {
                               and every later one of the context used peer
                               copies (rccl drops to 0) unless
                               CMTV_NO_RCCL_FALLBACK is set               */
+  uint64_t polled_calls;     /* small host batches whose bitmap the host read
+                              off the row kernel's completion flag, without
+                              waiting for the kernel to retire
+                              (CMTV_HOST_POLL)                           */
 } cmtv_stats;
 
 /* One device's share of the context's work (cmtv_device_stats_get). */
@@ -152,7 +156,10 @@ typedef struct cmtv_device_stats {
  * quad kernel's quads add both table entries of a window themselves:
  * k_verify_quad_split instead of k_verify_quad_hs), CMTV_HS_PRE=k (tuning:
  * the helper-summed kernel's helper adds the top k of [u]B's 16 comb
- * positions, default 6). */
+ * positions, default 6), CMTV_HOST_POLL=0 (a small single-device host batch
+ * on a row kernel waits for its stream instead of polling the kernel's tagged
+ * bitmap words: runtime.cpp wait_row_tags; the call may otherwise return
+ * while the kernel's last waves retire, its verdicts already complete). */
 int cmtv_open(const cmtv_config* cfg, cmtv_ctx** out);
 
 /* Opens ONE context over several devices (a node is one

@@ -12,7 +12,7 @@ class _FakeCtx:
         base = {k: 0 for k in ("calls", "signatures", "invalid", "kernel_launches", "cache_hits", "cache_entries",
                                "keyed_launches", "sharded_calls", "gathers", "faults_injected", "n_devices",
                                "rccl", "fused_sign_bytes", "device_failures", "reshards", "late_k_waves",
-                               "live_devices", "timed_calls", "rccl_failures")}
+                               "live_devices", "timed_calls", "rccl_failures", "polled_calls")}
         base.update(device_ms=0.0, last_kernel_ms=0.0)
         base.update(kw)
         self._st = base

@@ -170,3 +170,44 @@ def test_row_kernels_on_random_malformed_inputs(gpu_ctx_row4, gpu_ctx_row2, gpu_
     got = gpu_ctx_krow.verify_indexed(ks, np.arange(n, dtype=np.uint32), sig, m, off, mode)
     assert np.array_equal(got, exp), np.nonzero(got != exp)[0][:10]
     ks.free()
+
+
+def test_host_batches_read_the_completion_flag():
+    """Small single-device host batches on a row kernel return when the
+    kernel's completion flag arrives (kernels.h RowSlot, runtime.cpp
+    wait_row_done), not when the stream drains: back-to-back calls of ragged
+    sizes (word and half-word edges) and both modes, plain and registered-key,
+    each against the oracle bit for bit, and each counted in polled_calls; a
+    batch past the row range synchronises instead. CMTV_HOST_POLL=0 polls
+    nothing and gives the same verdicts."""
+    from conftest import _env_ctx
+
+    cases = []
+    for j, n in enumerate((1, 31, 32, 33, 63, 64, 65, 150, 256, 257, 700)):
+        pk, sig, m, off = _batch(n, 2100 + j, flip=0.25)
+        cases.append((n, pk, sig, m, off, [coracle.verify_batch(pk, sig, m, off, md, nthreads=8)
+                                           for md in (MODE_GO_STDLIB, MODE_ZIP215)]))
+    for poll in (1, 0):
+        ctx = _env_ctx(CMTV_HOST_POLL=poll)
+        before = ctx.stats()["polled_calls"]
+        calls = 0
+        for rep in range(3):
+            for n, pk, sig, m, off, exps in cases:
+                for md, exp in zip((MODE_GO_STDLIB, MODE_ZIP215), exps):
+                    got, words = ctx.verify(pk, sig, m, off, md, bitmap=True)
+                    bits = np.unpackbits(words.view(np.uint8), bitorder="little")
+                    assert np.array_equal(got, exp) and np.array_equal(bits[:n], exp) and not bits[n:].any()
+                    calls += 1
+        n, pk, sig, m, off, exps = cases[7]
+        ks = ctx.register_keys(pk)
+        for md, exp in zip((MODE_GO_STDLIB, MODE_ZIP215), exps):
+            assert np.array_equal(ctx.verify_indexed(ks, np.arange(n, dtype=np.uint32), sig, m, off, md), exp)
+            calls += 1
+        ks.free()
+        assert ctx.stats()["polled_calls"] - before == (calls if poll else 0)
+        # past the row kernels (the quad kernel): the stream is synchronised
+        pk, sig, m, off = _batch(1500, 2200)
+        exp = coracle.verify_batch(pk, sig, m, off, MODE_GO_STDLIB, nthreads=8)
+        assert np.array_equal(ctx.verify(pk, sig, m, off, MODE_GO_STDLIB), exp)
+        assert ctx.stats()["polled_calls"] - before == (calls if poll else 0)
+        ctx.close()

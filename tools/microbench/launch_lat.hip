@@ -166,6 +166,45 @@ __global__ __launch_bounds__(256, 1) void k_spin_fields(uint64_t ticks, uint64_t
   }
 }
 
+// the spin, then the field epilogue, and the wave that completes the last
+// word writes `seq` into a flag in mapped host memory (system-scope release):
+// the host can poll that flag instead of synchronising the stream
+__global__ __launch_bounds__(256, 1) void k_spin_flag(uint64_t ticks, uint64_t* stamps, uint32_t* slot,
+                                                      uint32_t* hbm, uint32_t n, uint32_t* hflag, uint32_t seq) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  uint64_t t = t0;
+  while (t - t0 < ticks) t = __builtin_amdgcn_s_memrealtime();
+  const uint32_t tl = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (threadIdx.x == 0) {
+    stamps[2 * blockIdx.x] = t0;
+    stamps[2 * blockIdx.x + 1] = t;
+  }
+  if (wave != 0) return;
+  uint64_t* sw = reinterpret_cast<uint64_t*>(slot);
+  const uint32_t s = blockIdx.x, j = s >> 5, f = s & 31;
+  uint64_t x = 0;
+  if (tl == 0) {
+    const uint64_t add = 2ull << (2 * f);
+    x = __hip_atomic_fetch_add(sw + j, add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + add;
+  }
+  x = __shfl(x, 0);
+  const uint32_t nf = n - 32 * j < 32 ? n - 32 * j : 32u;
+  const uint64_t m = 0x5555555555555555ull >> (64 - 2 * nf);
+  if (((x | (x >> 1)) & m) != m) return;
+  const uint64_t acc = __ballot(tl < 32 && ((x >> (2 * (tl & 31) + 1)) & 1) != 0);
+  if (tl == 0) {
+    __hip_atomic_store(hbm + j, (uint32_t)acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(sw + j, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __threadfence_system();
+    const uint32_t words = (n + 31) / 32;
+    const uint32_t done = __hip_atomic_fetch_add(slot + 1020, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (done == words - 1) {
+      __hip_atomic_store(slot + 1020, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(hflag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
 static double med(std::vector<double> v) {
   std::sort(v.begin(), v.end());
   return v[v.size() / 2];
@@ -236,6 +275,39 @@ int main() {
   if (run("spin 85 us, fenced ticket", [&] { hipLaunchKernelGGL(k_spin_ticket<1>, dim3(grid), dim3(256), 0, s, 8500ull, dst, slot, bm, (uint32_t)grid); }, 8500)) return 1;
   if (run("spin 85 us, relaxed ticket", [&] { hipLaunchKernelGGL(k_spin_ticket<0>, dim3(grid), dim3(256), 0, s, 8500ull, dst, slot, bm, (uint32_t)grid); }, 8500)) return 1;
   if (run("spin 85 us, field atomics", [&] { hipLaunchKernelGGL(k_spin_fields, dim3(grid), dim3(256), 0, s, 8500ull, dst, slot, bm, (uint32_t)grid); }, 8500)) return 1;
+  {
+    // the flag variant: host polls the mapped flag, no stream synchronisation
+    uint32_t* hflag;
+    CK(hipHostMalloc(&hflag, 64, hipHostMallocMapped | hipHostMallocCoherent));
+    uint32_t* dflag;
+    CK(hipHostGetDevicePointer((void**)&dflag, hflag, 0));
+    uint32_t* hbm2;
+    CK(hipHostMalloc(&hbm2, 64, hipHostMallocMapped | hipHostMallocCoherent));
+    uint32_t* dbm2;
+    CK(hipHostGetDevicePointer((void**)&dbm2, hbm2, 0));
+    *hflag = 0;
+    std::vector<double> wall_sync, wall_flag;
+    for (int mode = 0; mode < 2; mode++) {
+      for (int i = 0; i < iters + 20; i++) {
+        const uint32_t seq = (uint32_t)(mode * 100000 + i + 1);
+        auto t = std::chrono::steady_clock::now();
+        hipLaunchKernelGGL(k_spin_flag, dim3(grid), dim3(256), 0, s, 8500ull, dst, slot, dbm2, (uint32_t)grid, dflag, seq);
+        if (mode == 0) {
+          CK(hipStreamSynchronize(s));
+        } else {
+          volatile uint32_t* vf = hflag;
+          long spins = 0;
+          while (*vf != seq && ++spins < 2000000000L) {
+          }
+        }
+        const double w = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t).count();
+        if (mode == 1) CK(hipStreamSynchronize(s));  // outside the timed part (the next call would not wait)
+        if (i >= 20) (mode ? wall_flag : wall_sync).push_back(w);
+      }
+    }
+    printf("%-28s wall %7.2f us (stream sync)  %7.2f us (host polls the flag)\n", "spin 85 us, flag epilogue",
+           med(wall_sync), med(wall_flag));
+  }
   uint64_t hb[3];
   CK(hipMemcpy(hb, bm, sizeof hb, hipMemcpyDeviceToHost));
   printf("bitmap %016llx %016llx %016llx\n", (unsigned long long)hb[0], (unsigned long long)hb[1], (unsigned long long)hb[2]);

@@ -877,8 +877,8 @@ def latency_150(ctx, mode, iters):
 
 # The PMC summaries of THIS round's tree (tools/gpu_prof_r04.sh: rocprofv3
 # --pmc passes over the quick form of this bench command)
-PMC_SQ = "r04b_pmc_sq.json"
-PMC_TRAFFIC = "r04b_traffic.json"
+PMC_SQ = "r04g_pmc_sq.json"
+PMC_TRAFFIC = "r04g_traffic.json"
 
 
 def load_valu_busy(n=10_000, kernel="k_verify_quad_hs<0u>"):

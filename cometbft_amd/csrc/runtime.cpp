@@ -55,8 +55,12 @@ constexpr size_t kQuadMaxDefault = 40000;
 constexpr size_t kOctMaxDefault = 2048;       // CMTV_OCT_MAX
 // Ed25519 batches up to this size take the one-signature-per-wave row kernel
 // (row.h) where the two-wave oct kernel would run (CMTV_ROW_MAX; 3 signatures
-// per CU: 768 in one round on 256 CUs)
-constexpr size_t kRowMaxDefault = 768;
+// per workgroup, two workgroups per CU: 1,536 on 256 CUs). Measured on MI355X
+// (round 4, profiles/r04_row_max_ab.txt, tools/mid_ab.py): at 896-1,536
+// signatures two row workgroups sharing a CU beat the oct kernel by 8-10%
+// (host API: 1,024 0.215 vs 0.235 ms) and 5-6% through VerifyCommit; at 2,048
+// (three per CU) they lose (0.29 vs 0.24 ms). 768 before.
+constexpr size_t kRowMaxDefault = 1536;
 // ... and up to this size its two-waves-per-signature form (one signature
 // per CU: 256 in one round; CMTV_ROW2_MAX)
 constexpr size_t kRow2MaxDefault = 256;

@@ -133,7 +133,7 @@ typedef struct cmtv_device_stats {
  * CMTV_OCT_SPLIT_MAX / CMTV_QUAD_MAX / CMTV_QUAD_SPLIT_MAX / CMTV_KEYED_QUAD_MAX / CMTV_LANE_CHUNK
  * (kernel crossovers: Ed25519 batches up to CMTV_ROW2_MAX (256) take a whole
  * CU per signature (four waves; CMTV_ROW_WAVES=2: two), up to CMTV_ROW_MAX
- * (768) one wave per signature, up to CMTV_OCT_MAX (2048) 8 lanes, up to
+ * (1536) one wave per signature, up to CMTV_OCT_MAX (2048) 8 lanes, up to
  * CMTV_QUAD_MAX (40000) 4 lanes, larger ones one lane), CMTV_FAULT_AT=N (test knob: the N-th verification
  * launch of the context fails with CMTV_EHIP without running; libs/fail
  * FAIL_TEST_INDEX analogue), CMTV_FORCE_WIDE=1 (test knob: the quad kernels
@@ -215,7 +215,7 @@ int cmtv_verify_ed25519(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_
  * cmtv_stream() gives the context's own stream), non-blocking. d_valid
  * (n bytes) and d_bitmap (ceil(n/64) words) may each be NULL.
  * In-flight contract: any number of _device calls may be in flight on any
- * number of streams. Batches of the row kernels (n <= 768 by default) pack
+ * number of streams. Batches of the row kernels (n <= 1536 by default) pack
  * their bitmap through one slot of a 256-slot per-device ring; a slot whose
  * previous launch may still be running is fenced (the new launch's stream
  * waits for the old launch's event), so verdict words never depend on what

@@ -1,6 +1,6 @@
 """The one-signature-per-wave row kernel (cometbft_amd/csrc/row.h,
 k_verify_row_split): the production kernel for Ed25519 batches up to
-CMTV_ROW_MAX (768) signatures, i.e. the 150-validator VerifyCommit.
+CMTV_ROW_MAX (1,536) signatures, i.e. the 150-validator VerifyCommit.
 
 Its corpus, ragged-size, wide-schedule and forced-wide parity runs live with
 the other kernels' (test_gpu_parity.py, test_wide_gpu.py: kernel "row");
@@ -31,7 +31,7 @@ def _batch(n, seed, flip=0.1):
     return coracle.pubkeys_from_seeds(seeds), sig, m, off
 
 
-@pytest.mark.parametrize("n", [150, 255, 256, 257, 767, 768])
+@pytest.mark.parametrize("n", [150, 255, 256, 257, 767, 768, 769, 1024, 1535, 1536, 1537])
 def test_default_dispatch_commit_sizes(gpu_ctx, n):
     """The default context at and around the row crossover, both modes,
     verdict bytes and bitmap words (no bit past n set)."""
@@ -205,8 +205,8 @@ def test_host_batches_read_the_completion_flag():
             calls += 1
         ks.free()
         assert ctx.stats()["polled_calls"] - before == (calls if poll else 0)
-        # past the row kernels (the quad kernel): the stream is synchronised
-        pk, sig, m, off = _batch(1500, 2200)
+        # past the row kernels (CMTV_ROW_MAX 1,536; the oct kernel): the stream is synchronised
+        pk, sig, m, off = _batch(2000, 2200)
         exp = coracle.verify_batch(pk, sig, m, off, MODE_GO_STDLIB, nthreads=8)
         assert np.array_equal(ctx.verify(pk, sig, m, off, MODE_GO_STDLIB), exp)
         assert ctx.stats()["polled_calls"] - before == (calls if poll else 0)

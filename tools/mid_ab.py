@@ -28,7 +28,7 @@ def main():
 
     sizes = [int(x) for x in sys.argv[1:]] or [768, 1024, 1536]
     ctx = Context(device=0)
-    tag = os.environ.get("CMTV_ROW_MAX", "default")
+    tag = os.environ.get("TAG") or os.environ.get("CMTV_ROW_MAX", "default")
     for n in sizes:
         sv = TU.make_validator_set(ctx, n)
         msgs = TU.commit_messages(n, 1000)

@@ -45,15 +45,16 @@ def test_default_dispatch_commit_sizes(gpu_ctx, n):
 
 
 def test_concurrent_row_launches_pack_their_own_bitmaps():
-    """4 threads, each on its own stream, 25 device-resident row launches of
-    different sizes with bitmaps: every launch takes its own ring slot, so
-    each bitmap holds exactly its own verdicts."""
+    """5 threads, each on its own stream, 25 device-resident row launches of
+    different sizes with bitmaps (1,200: two row workgroups per CU): every
+    launch takes its own ring slot, so each bitmap holds exactly its own
+    verdicts."""
     import torch
 
     ctx = Context(device=0)
     dev = torch.device("cuda:0")
     jobs = []
-    for j, n in enumerate((150, 64, 333, 700)):
+    for j, n in enumerate((150, 64, 333, 700, 1200)):
         pk, sig, m, off = _batch(n, 900 + j, flip=0.2)
         exp = coracle.verify_batch(pk, sig, m, off, MODE_GO_STDLIB, nthreads=8)
         jobs.append((n, pk, sig, m, off, exp))
@@ -81,7 +82,7 @@ def test_concurrent_row_launches_pack_their_own_bitmaps():
         except Exception as e:  # noqa: BLE001
             errors.append((j, repr(e)))
 
-    ths = [threading.Thread(target=run, args=(j,)) for j in range(4)]
+    ths = [threading.Thread(target=run, args=(j,)) for j in range(len(jobs))]
     for t in ths:
         t.start()
     for t in ths:

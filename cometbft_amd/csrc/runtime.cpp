@@ -65,8 +65,12 @@ constexpr size_t kRowMaxDefault = 1536;
 // per CU: 256 in one round; CMTV_ROW2_MAX)
 constexpr size_t kRow2MaxDefault = 256;
 // registered-key batches up to this size take the keyed row kernel (one
-// signature per CU; CMTV_KEYED_ROW_MAX)
-constexpr size_t kKeyedRowMaxDefault = 256;
+// signature per workgroup; CMTV_KEYED_ROW_MAX). Measured on MI355X (round 4,
+// profiles/r04_keyed_row_max_ab.txt, tools/keyed_small.py): at 320-512
+// signatures two keyed row workgroups per CU take 0.058-0.062 ms per call
+// against the keyed quad kernel's 0.076; at 640-768 (three per CU) they lose
+// (kernel 0.068-0.071 vs 0.065 ms). 256 before.
+constexpr size_t kKeyedRowMaxDefault = 512;
 constexpr size_t kOctSplitMaxDefault = 2048;  // CMTV_OCT_SPLIT_MAX
 // quad batches up to this size take the helper-wave form (k_verify_quad_split:
 // 256 workgroups x 48 signatures per round); CMTV_QUAD_SPLIT_MAX

@@ -38,7 +38,7 @@ def _err(fn):
 def test_keyed_split_late_hash_is_exact(n):
     import torch
 
-    # the keyed quad kernel at every size (n <= 256 would take the keyed row
+    # the keyed quad kernel at every size (n <= 512 would take the keyed row
     # kernel, whose helper hands k over at a barrier, no bounded wait)
     with _env(CMTV_FORCE_K_LATE=1, CMTV_KEYED_ROW_MAX=0):
         late = Context(device=0)
@@ -78,7 +78,7 @@ def test_verify_commit_keyset_cache_late_hash():
     """VerifyCommit with the keyset cache (the keyed split kernel) under
     CMTV_FORCE_K_LATE: a valid commit verifies, a flipped signature gives the
     reference's 'wrong signature (#i)' at the right index, never another."""
-    # the keyed quad kernel at every size (n <= 256 would take the keyed row
+    # the keyed quad kernel at every size (n <= 512 would take the keyed row
     # kernel, whose helper hands k over at a barrier, no bounded wait)
     with _env(CMTV_FORCE_K_LATE=1, CMTV_KEYED_ROW_MAX=0):
         late = Context(device=0)

@@ -44,6 +44,22 @@ def test_default_dispatch_commit_sizes(gpu_ctx, n):
         assert np.array_equal(bits[:n], exp) and not bits[n:].any()
 
 
+
+@pytest.mark.parametrize("n", [256, 257, 400, 512, 513])
+def test_default_keyed_dispatch_around_the_keyed_row_crossover(gpu_ctx, n):
+    """Registered keys on the default context at and around CMTV_KEYED_ROW_MAX
+    (512: the keyed row kernel, two workgroups per CU above 256; the keyed
+    quad kernel past it), both modes, verdict bytes against the oracle."""
+    pk, sig, m, off = _batch(n, 1700 + n, flip=0.15)
+    ks = gpu_ctx.register_keys(pk)
+    try:
+        for mode in (MODE_GO_STDLIB, MODE_ZIP215):
+            exp = coracle.verify_batch(pk, sig, m, off, mode, nthreads=8)
+            got = gpu_ctx.verify_indexed(ks, np.arange(n, dtype=np.uint32), sig, m, off, mode)
+            assert np.array_equal(got, exp), np.nonzero(got != exp)[0][:10]
+    finally:
+        ks.free()
+
 def test_concurrent_row_launches_pack_their_own_bitmaps():
     """5 threads, each on its own stream, 25 device-resident row launches of
     different sizes with bitmaps (1,200: two row workgroups per CU): every

@@ -83,8 +83,12 @@ constexpr size_t kKeyedQuadMaxDefault = 36864;
 // signatures per device below which a batch is not sharded (env CMTV_SHARD_MIN)
 constexpr size_t kShardMinDefault = 8192;
 // single-device host batches up to this size return their bitmap through
-// mapped host memory (no D2H copy; the writes are a few PCIe transactions)
-constexpr size_t kZeroCopyMax = 4096;
+// mapped host memory (no D2H copy; the writes are a few PCIe transactions),
+// and fused commit batches read their staging there (no H2D copy). Measured
+// on MI355X (round 4, profiles/r04_zc_max_ab.txt, tools/mid_ab.py, CMTV_ZC_MAX
+// 4,096 vs 16,384): VerifyCommit at 8,192 0.329-0.330 -> 0.320 ms, at 10,000
+// 0.349 -> 0.341-0.343 ms; the host API unchanged. 4,096 before.
+constexpr size_t kZeroCopyMax = 12288;
 constexpr int kMaxDevices = 64;
 
 struct DevBuf {

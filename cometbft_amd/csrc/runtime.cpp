@@ -483,6 +483,7 @@ struct cmtv_ctx {
   std::vector<size_t> live;
   // fused small host batches read their inputs from mapped host memory (CMTV_NO_ZC_IN=1: off)
   bool zc_in = true;
+  bool zc_host_in = true;  // CMTV_ZC_HOST_IN=0: host-API batches copy their staging to HBM
   // single-device host batches up to this size take the mapped-memory path (CMTV_ZC_MAX)
   size_t zc_max = kZeroCopyMax;
   // small host batches on a row kernel poll its tagged bitmap words
@@ -921,8 +922,13 @@ static int enqueue_shard(cmtv_ctx* ctx, size_t g, const HostBatch& B, size_t a, 
   // message fits the helper's LDS slot; CMTV_NO_SB_FUSE turns it off
   const bool fuse = tpl && !keyed && ctx->sb_fuse && max_len <= kSbFuseMaxMsg && fuse_ok(ctx, m);
   // a fused small batch reads its staging in mapped host memory directly
-  // (CMTV_NO_ZC_IN turns it off)
-  const bool zc = zero_copy && fuse && ctx->zc_in;
+  // (CMTV_NO_ZC_IN turns it off), and so does a small plain host-API batch
+  // whose messages fit the same bound (keys, signatures and messages; no
+  // sign-bytes kernel writes into the staging then; CMTV_ZC_HOST_IN=0 copies
+  // it). Measured on MI355X (round 4, profiles/r04_zc_host_ab.txt): host API
+  // 150 0.116 -> 0.109 ms, 4,096 0.284 -> 0.269, 10,000 0.343 -> 0.326 ms.
+  const bool zc = zero_copy && ctx->zc_in &&
+                  (fuse || (!tpl && !keyed && ctx->zc_host_in && max_len <= kSbFuseMaxMsg));
   HostBuf& HB = zc ? D.h_zin : D.h_in;
   if ((e = HB.ensure(in_bytes)) != hipSuccess) return hip_fail(e);
   if (!zc && (e = D.d_in.ensure(dev_bytes)) != hipSuccess) return hip_fail(e);
@@ -1401,6 +1407,7 @@ static void read_env(cmtv_ctx* ctx) {
   if (const char* fw = std::getenv("CMTV_FORCE_WIDE")) ctx->force_wide = fw[0] == '1';
   if (const char* nf = std::getenv("CMTV_NO_SB_FUSE")) ctx->sb_fuse = nf[0] != '1';
   if (const char* nz = std::getenv("CMTV_NO_ZC_IN")) ctx->zc_in = nz[0] != '1';
+  if (const char* zh = std::getenv("CMTV_ZC_HOST_IN")) ctx->zc_host_in = zh[0] != '0';
   if (const char* zm = std::getenv("CMTV_ZC_MAX")) ctx->zc_max = (size_t)std::strtoull(zm, nullptr, 10);
   if (const char* hp = std::getenv("CMTV_HOST_POLL")) ctx->host_poll = std::atoi(hp) != 0;
   if (const char* kl = std::getenv("CMTV_FORCE_K_LATE")) ctx->keyed_wait = kl[0] == '1' ? 0u : kKeyedWaitDefault;

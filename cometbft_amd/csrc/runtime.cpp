@@ -43,8 +43,12 @@ constexpr uint32_t kChunk = 1u << 18;  // signatures per launch (A-table scratch
 constexpr uint32_t kKeyedBatchChunk = 1u << 20;
 constexpr uint32_t kKeyedBatchMinWaves = 2048;
 // crossover between the quad (4 lanes / signature) and lane (1 lane / signature)
-// kernels; measured on MI355X, overridable with CMTV_QUAD_MAX
-constexpr size_t kQuadMaxDefault = 40000;
+// kernels; measured on MI355X, overridable with CMTV_QUAD_MAX. Ed25519: four
+// full rounds of the helper-summed quad kernel (12,288 signatures each) beat
+// the lane kernel up to 49,152 (round 4, profiles/r04_quad_max_ab.txt:
+// 49,152 0.96 vs 1.15 ms; 65,536 1.39 vs 1.25 ms on the lane side); 40,000
+// before. sr25519 keeps 40,000 (its quad kernel was not re-measured).
+constexpr size_t kQuadMaxDefault = 49152, kQuadMaxSrDefault = 40000;
 // Ed25519 batches up to this size use the 8-lanes-per-signature kernel
 // (oct.h) in its two-wave form (k_verify_oct_split: 2 waves per 8
 // signatures) while its 8-signature workgroups fit one round on 256 CUs:
@@ -74,7 +78,7 @@ constexpr size_t kKeyedRowMaxDefault = 512;
 constexpr size_t kOctSplitMaxDefault = 2048;  // CMTV_OCT_SPLIT_MAX
 // quad batches up to this size take the helper-wave form (k_verify_quad_split:
 // 256 workgroups x 48 signatures per round); CMTV_QUAD_SPLIT_MAX
-constexpr size_t kQuadSplitMaxDefault = 40000;
+constexpr size_t kQuadSplitMaxDefault = 49152;
 // the crossover for registered-key verification (env CMTV_KEYED_QUAD_MAX):
 // the two-helper keyed quad kernel takes 12,288 signatures per round (0.088,
 // 0.164, 0.242 ms for 1-3 rounds) against the keyed lane kernel's flat
@@ -431,6 +435,7 @@ struct cmtv_ctx {
   std::mutex mu;
   cmtv_stats stats{};
   size_t quad_max = kQuadMaxDefault;  // batches up to this size use the quad kernel
+  size_t sr_quad_max = kQuadMaxSrDefault;  // ... sr25519 batches (CMTV_QUAD_MAX sets both)
   size_t oct_max = kOctMaxDefault;    // ... and up to this size the oct kernel
   size_t oct_split_max = kOctSplitMaxDefault;
   size_t row_max = kRowMaxDefault;
@@ -655,7 +660,7 @@ static int enqueue_verify(cmtv_ctx* ctx, CmtvDev& D, size_t n, const uint8_t* d_
   // 4-lanes-per-signature kernel below the crossover (quad.h,
   // sr25519_quad.h).
   const bool sr = mode == kModeSr25519;
-  const bool quad = n <= ctx->quad_max;
+  const bool quad = n <= (sr ? ctx->sr_quad_max : ctx->quad_max);
   const bool oct = quad && !sr && n <= ctx->oct_max;
   const bool oct_split = oct && n <= ctx->oct_split_max;
   const bool quad_split = quad && !oct && n <= ctx->quad_split_max;
@@ -1386,7 +1391,7 @@ static void release_device(CmtvDev& D) {
 }
 
 static void read_env(cmtv_ctx* ctx) {
-  if (const char* qm = std::getenv("CMTV_QUAD_MAX")) ctx->quad_max = (size_t)std::strtoull(qm, nullptr, 10);
+  if (const char* qm = std::getenv("CMTV_QUAD_MAX")) ctx->quad_max = ctx->sr_quad_max = (size_t)std::strtoull(qm, nullptr, 10);
   if (const char* om = std::getenv("CMTV_OCT_MAX")) ctx->oct_max = (size_t)std::strtoull(om, nullptr, 10);
   if (const char* rm = std::getenv("CMTV_ROW_MAX")) ctx->row_max = (size_t)std::strtoull(rm, nullptr, 10);
   if (const char* rm = std::getenv("CMTV_ROW2_MAX")) ctx->row2_max = (size_t)std::strtoull(rm, nullptr, 10);

@@ -134,7 +134,7 @@ typedef struct cmtv_device_stats {
  * (kernel crossovers: Ed25519 batches up to CMTV_ROW2_MAX (256) take a whole
  * CU per signature (four waves; CMTV_ROW_WAVES=2: two), up to CMTV_ROW_MAX
  * (1536) one wave per signature, up to CMTV_OCT_MAX (2048) 8 lanes, up to
- * CMTV_QUAD_MAX (40000) 4 lanes, larger ones one lane), CMTV_FAULT_AT=N (test knob: the N-th verification
+ * CMTV_QUAD_MAX (49152; sr25519 40000) 4 lanes, larger ones one lane), CMTV_FAULT_AT=N (test knob: the N-th verification
  * launch of the context fails with CMTV_EHIP without running; libs/fail
  * FAIL_TEST_INDEX analogue), CMTV_FORCE_WIDE=1 (test knob: the quad kernels
  * take the 64-window half-scalar fallback for every signature),

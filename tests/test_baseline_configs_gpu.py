@@ -2,7 +2,7 @@
 rather than only timed):
 
   configs[1]  one 10,000-validator commit: the raw batch (quad kernel, the
-              default dispatch for n <= 40,000) and cmtv_verify_commit /
+              default dispatch for n <= 49,152) and cmtv_verify_commit /
               VerifyCommitLight (templated sign-bytes + replay) with ~1% of
               the signatures bit-flipped, both verdict modes, against the C
               oracle's verdicts and a Python replay of the reference loop

@@ -120,3 +120,25 @@ def test_verify_sharded_single_rank(gpu_ctx):
     words = P.verify_sharded(gpu_ctx, pk, sig, m, off, MODE_GO_STDLIB, world=1, rank=0)
     v = P.unpack_bitmap(words.cpu().numpy().view(np.uint64), n)
     assert v.sum() == n - 1 and v[17] == 0
+
+
+@pytest.mark.parametrize("n", [49152, 49153])
+def test_default_dispatch_at_the_quad_lane_crossover(gpu_ctx, n):
+    """The default context on both sides of CMTV_QUAD_MAX (49,152: four
+    rounds of the helper-summed quad kernel; one more signature takes the lane
+    kernel), Go mode, 1% flipped signatures, verdict bytes and bitmap against
+    the oracle."""
+    rng = np.random.default_rng(n)
+    seeds = rng.integers(0, 256, (512, 32), dtype=np.uint8)
+    kidx = (np.arange(n) % 512).astype(np.uint32)
+    msgs = [rng.integers(0, 256, 120, dtype=np.uint8).tobytes() for _ in range(n)]
+    m, off = coracle.pack_msgs(msgs)
+    sig = coracle.sign_batch(seeds, m, off, key_idx=kidx, nthreads=8).copy()
+    pk = coracle.pubkeys_from_seeds(seeds)[kidx]
+    for i in np.nonzero(rng.random(n) < 0.01)[0]:
+        sig[i, rng.integers(0, 64)] ^= 1 << rng.integers(0, 8)
+    exp = coracle.verify_batch(pk, sig, m, off, MODE_GO_STDLIB, nthreads=8)
+    got, words = gpu_ctx.verify(pk, sig, m, off, MODE_GO_STDLIB, bitmap=True)
+    assert np.array_equal(got, exp)
+    bits = np.unpackbits(words.view(np.uint8), bitorder="little")
+    assert np.array_equal(bits[:n], exp) and not bits[n:].any()

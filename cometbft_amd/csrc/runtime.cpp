@@ -47,7 +47,8 @@ constexpr uint32_t kKeyedBatchMinWaves = 2048;
 // full rounds of the helper-summed quad kernel (12,288 signatures each) beat
 // the lane kernel up to 49,152 (round 4, profiles/r04_quad_max_ab.txt:
 // 49,152 0.96 vs 1.15 ms; 65,536 1.39 vs 1.25 ms on the lane side); 40,000
-// before. sr25519 keeps 40,000 (its quad kernel was not re-measured).
+// before. sr25519 keeps 40,000: its quad kernel loses to the lane kernel above
+// it (profiles/r04_sr_quad_max_ab.txt: 40,960-49,152 1.37-1.40 vs 1.24-1.27 ms).
 constexpr size_t kQuadMaxDefault = 49152, kQuadMaxSrDefault = 40000;
 // Ed25519 batches up to this size use the 8-lanes-per-signature kernel
 // (oct.h) in its two-wave form (k_verify_oct_split: 2 waves per 8

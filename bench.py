@@ -36,6 +36,11 @@ Extra fields on the JSON line:
   light_client   -- light/client_benchmark_test.go:25-110 shapes: 1000 heights x
                     100 validators, sequential (VerifyCommitLight per header) and
                     bisection (LightTrusting + Light to the tip)
+  replay_c3_host -- configs[2] the way a node calls it: cmtv_verify_commits over
+                    100k commits x 150 validators from host memory (plan,
+                    pinned staging, H2D, kernels, replay; the chunked
+                    pipeline), VerifyCommit and VerifyCommitLight, every
+                    height's outcome checked
   replay_c3      -- configs[2]: 100k commits x 150 validators (15M signatures)
                     sharded by height over the N devices (strong scaling),
                     registered-key kernel (radix-256 key combs, [s]B over B's
@@ -94,6 +99,8 @@ def parse():
     ap.add_argument("--no-latency", action="store_true")
     ap.add_argument("--no-c3", action="store_true", help="skip the configs[2] 15M-signature replay side line")
     ap.add_argument("--c3-heights", type=int, default=100_000, help="configs[2] commits (150 validators each)")
+    ap.add_argument("--no-c3-host", action="store_true",
+                    help="skip configs[2] through cmtv_verify_commits from host memory")
     ap.add_argument("--no-sr25519", action="store_true", help="skip the configs[4] sr25519 side measurement")
     ap.add_argument("--no-light", action="store_true", help="skip the light-client replay line")
     ap.add_argument("--no-keyset", action="store_true", help="skip the registered-keys 10k side line")
@@ -717,6 +724,58 @@ def c3_line(ctx, n_dev, mode, steps=3, n_heights=100_000, n_vals=150):
             "devices": run_keyed}
 
 
+def c3_host_line(ctx, mode, n_heights=100_000, n_vals=150, steps=3, kinds=(0, 1)):
+    """configs[2] through the entry point a node calls:
+    cmtv_verify_commits over n_heights commits x n_vals validators from HOST
+    memory, arguments packed once as a cgo shim holds them (ReplayChain: the
+    Go slices' pointers), the validator set's keys registered on first use by
+    the keyset cache (a node keeps its set across heights). One call per pass
+    = commit plan, sign-bytes templates, pinned staging, H2D, sign-bytes +
+    registered-key kernels, verdicts back, and the reference loop replayed per
+    commit (types/validator_set.go:685-713 VerifyCommit, :740-764
+    VerifyCommitLight). 1% of the signatures (seed 42) carry a flipped bit;
+    every height's outcome (nil, or ErrWrongSignature at the first flipped
+    index the loop reaches) is checked exactly. value = signatures of the
+    chain / wall time of the call (VerifyCommit verifies all 15M; the light
+    kind stops each commit past 2/3, and its line also gives the signatures
+    it verified)."""
+    from cometbft_amd import _native as N
+    from cometbft_amd import testutil as TU
+
+    t_gen = time.perf_counter()
+    sv = TU.make_validator_set(ctx, n_vals)
+    chain = TU.ReplayChain(ctx, sv, 1, n_heights)
+    t_gen = time.perf_counter() - t_gen
+    total = n_heights * n_vals
+    out = {"workload": f"configs[2] from host memory: {n_heights} commits x {n_vals} validators = {total} "
+                       "signatures, one cmtv_verify_commits call per pass, 1% bit-flipped (seed 42)",
+           "unit": "verifs/s", "setup_s": round(t_gen, 2), "steps": steps}
+    names = {N.VERIFY_COMMIT: "verify_commit", N.VERIFY_COMMIT_LIGHT: "verify_commit_light",
+             N.VERIFY_COMMIT_LIGHT_TRUSTING: "verify_commit_light_trusting"}
+    for kind in kinds:
+        chain.call(ctx, kind, mode)  # warm-up: registers the key set, grows the staging
+        st0 = ctx.stats()
+        ts = []
+        for _ in range(steps):
+            t = time.perf_counter()
+            chain.call(ctx, kind, mode)
+            ts.append(time.perf_counter() - t)
+        st1 = ctx.stats()
+        rcs, code, si = chain.outcome()
+        first = chain.expected(kind)
+        bad = first >= 0
+        ok = bool(np.all(rcs[~bad] == 0) and np.all(rcs[bad] == N.CMTV_ECOMMIT)
+                  and np.all(code[bad] == N.COMMIT_ERR_WRONG_SIGNATURE) and np.all(si[bad] == first[bad]))
+        t = float(np.median(ts))
+        verified = (st1["signatures"] - st0["signatures"]) / steps
+        out[names[kind]] = {"value": round(total / t, 1), "ms_per_pass": round(t * 1e3, 2),
+                            "ms_min": round(min(ts) * 1e3, 2), "device_signatures_per_pass": int(verified),
+                            "device_verifs_per_s": round(verified / t, 1), "verdicts_ok": ok,
+                            "heights_with_error": int(bad.sum())}
+    del chain
+    return out
+
+
 def keyset_10k(ctx, D, mode, steps):
     """configs[1] with the validator set registered once (cmtv_register_keys,
     outside the timed region, as a node keeps it across heights): the same
@@ -1094,6 +1153,15 @@ def main():
     if not args.no_sr25519 and n_dev == 1:
         aux("sr25519", lambda: sr25519_line(ctx, torch.device("cuda", 0), 10_000, 20, args.cpu_seconds / 4,
                                             not args.no_cpu_baseline))
+    if not args.no_c3_host:
+        def c3h():
+            hctx = Context(devices=ordinals)
+            hctx.keyset_cache(4)  # a node registers its validator set once
+            try:
+                return c3_host_line(hctx, mode, n_heights=args.c3_heights)
+            finally:
+                hctx.close()
+        aux("replay_c3_host", c3h)
     c3 = None
     if not args.no_c3:
         del D

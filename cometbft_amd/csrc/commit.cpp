@@ -14,97 +14,75 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <new>
+#include <random>
 #include <string>
 #include <unordered_map>
 #include <vector>
 
 #include "../../include/cmtverify.h"
+#include "commit_internal.h"
 #include "runtime_internal.h"
 #include "signbytes.h"
 
+namespace cmtv {
+
+uint64_t AddrIndex::key() {
+  static const uint64_t k = [] {
+    std::random_device rd;
+    return ((uint64_t)rd() << 32) ^ rd();
+  }();
+  return k;
+}
+
+// Two validator sets hold the same keys (so one registered key set serves
+// both): the same arrays, or equal key bytes.
+bool same_keys(const cmtv_valset* a, const cmtv_valset* b) {
+  if (a == b) return true;
+  if (a->n_vals != b->n_vals) return false;
+  if (a->pubkeys == b->pubkeys && a->pk_off == b->pk_off) return true;
+  for (uint32_t i = 0; i <= a->n_vals; i++)
+    if (a->pk_off[i] != b->pk_off[i]) return false;
+  const uint32_t bytes = a->pk_off[a->n_vals];
+  return bytes == 0 || std::memcmp(a->pubkeys, b->pubkeys, bytes) == 0;
+}
+
+}  // namespace cmtv
+
 namespace {
 
-// ------------------------------------------------------------------ encoding
-
-void put_uvarint(std::string& out, uint64_t v) {
-  while (v >= 0x80) {
-    out.push_back((char)((v & 0x7F) | 0x80));
-    v >>= 7;
-  }
-  out.push_back((char)v);
-}
-
-void put_bytes_field(std::string& out, uint8_t tag, const uint8_t* p, size_t n) {
-  out.push_back((char)tag);
-  put_uvarint(out, n);
-  out.append(reinterpret_cast<const char*>(p), n);
-}
-
-void put_sfixed64(std::string& out, uint8_t tag, int64_t v) {
-  out.push_back((char)tag);
-  uint64_t u = (uint64_t)v;
-  for (int i = 0; i < 8; i++) out.push_back((char)(u >> (8 * i)));
-}
-
-bool block_id_is_zero(const cmtv_block_id* b) {
-  return !b || (b->hash_len == 0 && b->psh_total == 0 && b->psh_hash_len == 0);
-}
-
-// CanonicalBlockID (canonical.pb.go:370) or nothing when IsZero (canonical.go:18-33)
-void put_canonical_block_id(std::string& out, const cmtv_block_id* b) {
-  if (block_id_is_zero(b)) return;
-  std::string psh;
-  if (b->psh_total != 0) {
-    psh.push_back(0x08);
-    put_uvarint(psh, b->psh_total);
-  }
-  if (b->psh_hash_len) put_bytes_field(psh, 0x12, b->psh_hash, b->psh_hash_len);
-  std::string cb;
-  if (b->hash_len) put_bytes_field(cb, 0x0A, b->hash, b->hash_len);
-  put_bytes_field(cb, 0x12, reinterpret_cast<const uint8_t*>(psh.data()), psh.size());
-  put_bytes_field(out, 0x22, reinterpret_cast<const uint8_t*>(cb.data()), cb.size());
-}
+using namespace cmtv;
 
 // VoteSignBytes (types/vote.go:93): uvarint(len) || CanonicalVote
 // (canonical.pb.go:517-567; Timestamp = gogoproto StdTime {1: seconds, 2: nanos})
-void vote_sign_bytes(std::string& out, const char* chain_id, size_t chain_id_len, int32_t vtype, int64_t height,
-                     int32_t round, const cmtv_block_id* bid, int64_t ts_sec, int32_t ts_nanos) {
-  std::string body;
-  if (vtype != 0) {
-    body.push_back(0x08);
-    put_uvarint(body, (uint64_t)(int64_t)vtype);
-  }
-  if (height != 0) put_sfixed64(body, 0x11, height);
-  if (round != 0) put_sfixed64(body, 0x19, (int64_t)round);
-  put_canonical_block_id(body, bid);
-  std::string ts;
+void put_vote(ByteWriter& w, const char* chain_id, size_t chain_id_len, int32_t vtype, int64_t height, int32_t round,
+              const cmtv_block_id* bid, int64_t ts_sec, int32_t ts_nanos) {
+  put_vote_prefix(w, vtype, height, round, bid);
+  const size_t ts = (ts_sec != 0 ? 1 + uvarint_len((uint64_t)ts_sec) : 0) +
+                    (ts_nanos != 0 ? 1 + uvarint_len((uint64_t)(int64_t)ts_nanos) : 0);
+  w.byte(0x2A);
+  w.uvarint(ts);
   if (ts_sec != 0) {
-    ts.push_back(0x08);
-    put_uvarint(ts, (uint64_t)ts_sec);
+    w.byte(0x08);
+    w.uvarint((uint64_t)ts_sec);
   }
   if (ts_nanos != 0) {
-    ts.push_back(0x10);
-    put_uvarint(ts, (uint64_t)(int64_t)ts_nanos);
+    w.byte(0x10);
+    w.uvarint((uint64_t)(int64_t)ts_nanos);
   }
-  put_bytes_field(body, 0x2A, reinterpret_cast<const uint8_t*>(ts.data()), ts.size());
-  if (chain_id_len) put_bytes_field(body, 0x32, reinterpret_cast<const uint8_t*>(chain_id), chain_id_len);
-  out.clear();
-  put_uvarint(out, body.size());
-  out += body;
+  if (chain_id_len) w.bytes_field(0x32, reinterpret_cast<const uint8_t*>(chain_id), chain_id_len);
 }
 
-// ------------------------------------------------------------------ formatting
-
-std::string hex_upper(const uint8_t* p, size_t n) {
-  static const char* d = "0123456789ABCDEF";
-  std::string s;
-  s.reserve(2 * n);
-  for (size_t i = 0; i < n; i++) {
-    s.push_back(d[p[i] >> 4]);
-    s.push_back(d[p[i] & 15]);
-  }
-  return s;
+void vote_sign_bytes(std::string& out, const char* chain_id, size_t chain_id_len, int32_t vtype, int64_t height,
+                     int32_t round, const cmtv_block_id* bid, int64_t ts_sec, int32_t ts_nanos) {
+  ByteWriter cnt;
+  put_vote(cnt, chain_id, chain_id_len, vtype, height, round, bid, ts_sec, ts_nanos);
+  const size_t body = cnt.n;
+  out.resize(uvarint_len(body) + body);
+  ByteWriter w{reinterpret_cast<uint8_t*>(&out[0]), 0};
+  w.uvarint(body);
+  put_vote(w, chain_id, chain_id_len, vtype, height, round, bid, ts_sec, ts_nanos);
 }
 
 // BlockID.String() (types/block.go:1217): "%v:%v" Hash, PartSetHeader
@@ -125,42 +103,7 @@ bool block_id_equals(const cmtv_block_id* a, const cmtv_block_id* b) {
          eq(a->psh_hash, a->psh_hash_len, b->psh_hash, b->psh_hash_len);
 }
 
-void set_msg(char* buf, size_t cap, const std::string& s) {
-  if (!buf || cap == 0) return;
-  size_t n = s.size() < cap - 1 ? s.size() : cap - 1;
-  std::memcpy(buf, s.data(), n);
-  buf[n] = 0;
-}
-
-constexpr uint8_t kFlagAbsent = 1, kFlagCommit = 2, kFlagNil = 3;
-constexpr int32_t kPrecommit = 2;
-
 // ------------------------------------------------------------------ VerifyCommit*
-
-// The CanonicalVote fields before the timestamp (type, height, round,
-// BlockID unless nil): the per-commit part of a signature's sign-bytes.
-void vote_prefix(std::string& body, int32_t vtype, int64_t height, int32_t round, const cmtv_block_id* bid) {
-  body.clear();
-  if (vtype != 0) {
-    body.push_back(0x08);
-    put_uvarint(body, (uint64_t)(int64_t)vtype);
-  }
-  if (height != 0) put_sfixed64(body, 0x11, height);
-  if (round != 0) put_sfixed64(body, 0x19, (int64_t)round);
-  put_canonical_block_id(body, bid);
-}
-
-// Two validator sets hold the same keys (so one registered key set serves
-// both): the same arrays, or equal key bytes.
-bool same_keys(const cmtv_valset* a, const cmtv_valset* b) {
-  if (a == b) return true;
-  if (a->n_vals != b->n_vals) return false;
-  if (a->pubkeys == b->pubkeys && a->pk_off == b->pk_off) return true;
-  for (uint32_t i = 0; i <= a->n_vals; i++)
-    if (a->pk_off[i] != b->pk_off[i]) return false;
-  const uint32_t bytes = a->pk_off[a->n_vals];
-  return bytes == 0 || std::memcmp(a->pubkeys, b->pubkeys, bytes) == 0;
-}
 
 // Signatures of one or more commits, gathered for one device batch. Host
 // mode: sign-bytes encoded here (needed for the verdict cache's keys).
@@ -224,22 +167,10 @@ struct SigBatch {
 
   void ensure_template(const char* chain_id, size_t chain_id_len, const cmtv_commit* c) {
     if (cur == c && !tmpls.empty()) return;
-    static const cmtv_block_id empty{};
     cmtv::SbTemplate t{};
-    std::string part;
-    vote_prefix(part, kPrecommit, c->height, c->round, &c->block_id);
-    t.pre_commit_off = (uint32_t)blob.size();
-    t.pre_commit_len = (uint32_t)part.size();
-    blob.insert(blob.end(), part.begin(), part.end());
-    vote_prefix(part, kPrecommit, c->height, c->round, &empty);
-    t.pre_nil_off = (uint32_t)blob.size();
-    t.pre_nil_len = (uint32_t)part.size();
-    blob.insert(blob.end(), part.begin(), part.end());
-    part.clear();
-    if (chain_id_len) put_bytes_field(part, 0x32, reinterpret_cast<const uint8_t*>(chain_id), chain_id_len);
-    t.post_off = (uint32_t)blob.size();
-    t.post_len = (uint32_t)part.size();
-    blob.insert(blob.end(), part.begin(), part.end());
+    const size_t at = blob.size();
+    blob.resize(at + put_commit_template(nullptr, 0, chain_id, chain_id_len, c, nullptr));
+    put_commit_template(blob.data(), at, chain_id, chain_id_len, c, &t);
     tmpls.push_back(t);
     cur = c;
   }
@@ -283,35 +214,6 @@ struct SigBatch {
   }
 };
 
-// One VerifyCommit* evaluation: preamble + plan (job_prepare), then the
-// reference loop replayed over device verdicts (job_replay).
-struct CommitJob {
-  uint32_t kind;
-  const char* chain_id;
-  size_t chain_id_len;
-  const cmtv_valset* vals;
-  const cmtv_block_id* block_id;
-  int64_t height;
-  const cmtv_commit* commit;
-  uint64_t trust_num, trust_den;
-  cmtv_commit_result* res;
-  char* msg_buf;
-  size_t msg_cap;
-  // state
-  int early = 1;  // != 1: the preamble already decided (return code)
-  int64_t needed = 0;
-  std::unordered_map<std::string, uint32_t> by_addr;
-  std::vector<uint32_t> plan_idx, plan_val;
-  size_t first = 0;  // batch index of plan item 0
-
-  int fail(int32_t code, int32_t idx, const std::string& m) {
-    res->code = code;
-    res->sig_index = idx;
-    set_msg(msg_buf, msg_cap, m);
-    return CMTV_ECOMMIT;
-  }
-};
-
 // CMTV_HOST_SIGNBYTES=1 forces host-side encoding (A/B measurement, tests)
 bool templated_enabled() {
   static const bool on = [] {
@@ -319,20 +221,6 @@ bool templated_enabled() {
     return !(v && v[0] == '1');
   }();
   return on;
-}
-
-int job_check_args(uint32_t kind, const char* chain_id, size_t chain_id_len, const cmtv_valset* vals,
-                   const cmtv_block_id* block_id, const cmtv_commit* commit, cmtv_commit_result* res) {
-  if (!vals || !commit || !res || kind > CMTV_VERIFY_COMMIT_LIGHT_TRUSTING) return CMTV_EINVAL;
-  if ((!chain_id && chain_id_len) || (vals->n_vals && (!vals->pubkeys || !vals->pk_off || !vals->voting_power)))
-    return CMTV_EINVAL;
-  const uint32_t nsig = commit->n_sigs;
-  if (nsig && (!commit->flags || !commit->ts_seconds || !commit->ts_nanos || !commit->sigs || !commit->sig_off))
-    return CMTV_EINVAL;
-  if (kind == CMTV_VERIFY_COMMIT_LIGHT_TRUSTING && nsig && (!commit->val_addrs || (vals->n_vals && !vals->addrs)))
-    return CMTV_EINVAL;
-  if (kind != CMTV_VERIFY_COMMIT_LIGHT_TRUSTING && !block_id) return CMTV_EINVAL;
-  return CMTV_OK;
 }
 
 // The common VerifyCommit case (validator_set.go:685-707): the plan is every
@@ -375,13 +263,25 @@ bool job_prepare_identity(CommitJob& J, SigBatch& B, bool prefetch) {
   return true;
 }
 
-// Preamble checks and the threshold (validator_set.go:670-684, 779-790), then
-// the plan: which signatures the reference loop can reach, assuming every
-// verdict is valid (the loop stops at its first error, so nothing beyond the
-// plan is ever examined). Appends the planned signatures to B; with
-// `prefetch` a light call also appends its commit's other non-absent
-// signatures (verdicts for the verdict cache only).
-void job_prepare(CommitJob& J, SigBatch& B, bool prefetch, bool only_job) {
+}  // namespace
+
+namespace cmtv {
+
+int job_check_args(uint32_t kind, const char* chain_id, size_t chain_id_len, const cmtv_valset* vals,
+                   const cmtv_block_id* block_id, const cmtv_commit* commit, cmtv_commit_result* res) {
+  if (!vals || !commit || !res || kind > CMTV_VERIFY_COMMIT_LIGHT_TRUSTING) return CMTV_EINVAL;
+  if ((!chain_id && chain_id_len) || (vals->n_vals && (!vals->pubkeys || !vals->pk_off || !vals->voting_power)))
+    return CMTV_EINVAL;
+  const uint32_t nsig = commit->n_sigs;
+  if (nsig && (!commit->flags || !commit->ts_seconds || !commit->ts_nanos || !commit->sigs || !commit->sig_off))
+    return CMTV_EINVAL;
+  if (kind == CMTV_VERIFY_COMMIT_LIGHT_TRUSTING && nsig && (!commit->val_addrs || (vals->n_vals && !vals->addrs)))
+    return CMTV_EINVAL;
+  if (kind != CMTV_VERIFY_COMMIT_LIGHT_TRUSTING && !block_id) return CMTV_EINVAL;
+  return CMTV_OK;
+}
+
+void job_preamble(CommitJob& J) {
   const cmtv_valset* vals = J.vals;
   const cmtv_commit* commit = J.commit;
   std::memset(J.res, 0, sizeof(*J.res));
@@ -417,8 +317,6 @@ void job_prepare(CommitJob& J, SigBatch& B, bool prefetch, bool only_job) {
     // rejected above
     const int64_t den = (int64_t)J.trust_den;
     J.needed = (den == -1) ? (int64_t)(0 - (uint64_t)prod) : prod / den;
-    for (uint32_t i = 0; i < vals->n_vals; i++)
-      J.by_addr.emplace(std::string(reinterpret_cast<const char*>(vals->addrs + 20 * (size_t)i), 20), i);
   } else {
     if (vals->n_vals != nsig) {
       char b[128];
@@ -440,11 +338,19 @@ void job_prepare(CommitJob& J, SigBatch& B, bool prefetch, bool only_job) {
     }
     J.needed = total * 2 / 3;
   }
+}
 
+// The plan: which signatures the reference loop can reach, assuming every
+// verdict is valid (the loop stops at its first error, so nothing beyond the
+// plan is ever examined).
+size_t job_plan(const CommitJob& J, uint32_t* pidx, uint32_t* pval, Seen& seen) {
+  const cmtv_valset* vals = J.vals;
+  const cmtv_commit* commit = J.commit;
+  const uint32_t nsig = commit->n_sigs;
+  const bool trusting = J.kind == CMTV_VERIFY_COMMIT_LIGHT_TRUSTING;
+  if (trusting) seen.reset(vals->n_vals);
   int64_t tally = 0;
-  std::unordered_map<uint32_t, uint32_t> seen;
-  J.plan_idx.reserve(nsig);
-  J.plan_val.reserve(nsig);
+  size_t m = 0;
   for (uint32_t idx = 0; idx < nsig; idx++) {
     const uint8_t flag = commit->flags[idx];
     uint32_t vi = idx;
@@ -453,23 +359,50 @@ void job_prepare(CommitJob& J, SigBatch& B, bool prefetch, bool only_job) {
       if (flag != kFlagCommit && flag != kFlagNil) break;  // panics here
     } else {
       if (flag != kFlagCommit) continue;
-      if (J.kind == CMTV_VERIFY_COMMIT_LIGHT_TRUSTING) {
-        auto it = J.by_addr.find(std::string(reinterpret_cast<const char*>(commit->val_addrs + 20 * (size_t)idx), 20));
-        if (it == J.by_addr.end()) continue;
-        vi = it->second;
-        if (seen.count(vi)) break;  // double vote error here
-        seen.emplace(vi, idx);
+      if (trusting) {
+        const int64_t f = J.addr->find(commit->val_addrs + 20 * (size_t)idx);
+        if (f < 0) continue;
+        vi = (uint32_t)f;
+        uint32_t first = 0;
+        if (seen.has(vi, &first)) break;  // double vote error here
+        seen.put(vi, idx);
       }
     }
     if (vals->pk_off[vi + 1] - vals->pk_off[vi] != 32) break;  // panics here
-    J.plan_idx.push_back(idx);
-    J.plan_val.push_back(vi);
+    pidx[m] = idx;
+    if (pval) pval[m] = vi;
+    m++;
     if (J.kind != CMTV_VERIFY_COMMIT) {
       tally += vals->voting_power[vi];
       if (tally > J.needed) break;
     }
   }
+  return m;
+}
 
+}  // namespace cmtv
+
+namespace {
+
+// Preamble, plan and the planned signatures appended to B; with `prefetch`
+// a light call also appends its commit's other non-absent signatures
+// (verdicts for the verdict cache only).
+void job_prepare(CommitJob& J, SigBatch& B, bool prefetch, bool only_job, Seen& seen) {
+  const cmtv_valset* vals = J.vals;
+  const cmtv_commit* commit = J.commit;
+  job_preamble(J);
+  if (J.early != 1) {
+    J.first = B.size();
+    return;
+  }
+  const uint32_t nsig = commit->n_sigs;
+  J.plan_idx.resize(nsig);
+  if (J.kind == CMTV_VERIFY_COMMIT_LIGHT_TRUSTING) J.plan_val.resize(nsig);
+  const size_t m = job_plan(J, J.plan_idx.data(), J.kind == CMTV_VERIFY_COMMIT_LIGHT_TRUSTING ? J.plan_val.data()
+                                                                                              : nullptr, seen);
+  J.plan_idx.resize(m);
+  if (J.kind != CMTV_VERIFY_COMMIT_LIGHT_TRUSTING) J.plan_val = J.plan_idx;
+  J.plan_val.resize(m);
   J.first = B.size();
   // borrowing the caller's arrays: only when no other job adds to the batch
   if (only_job && job_prepare_identity(J, B, prefetch)) return;
@@ -542,76 +475,10 @@ int batch_verify(cmtv_ctx* ctx, SigBatch& B, uint32_t mode, std::vector<uint8_t>
   return CMTV_OK;
 }
 
-// The reference loop (validator_set.go:685-713, 740-764, 793-825) over the
-// verdicts of the planned signatures.
-int job_replay(CommitJob& J, const std::vector<uint8_t>& all_valid) {
-  if (J.early != 1) return J.early;
-  const cmtv_valset* vals = J.vals;
-  const cmtv_commit* commit = J.commit;
-  const uint32_t nsig = commit->n_sigs;
-  const size_t m = J.plan_idx.size();
-  const uint8_t* valid = all_valid.data() + J.first;
-  J.res->n_verified = (uint32_t)m;
-  auto wrong_sig = [&](uint32_t idx) {
-    const uint32_t s0 = commit->sig_off[idx], s1 = commit->sig_off[idx + 1];
-    return J.fail(CMTV_COMMIT_ERR_WRONG_SIGNATURE, (int32_t)idx,
-                  "wrong signature (#" + std::to_string(idx) + "): " + hex_upper(commit->sigs + s0, s1 - s0));
-  };
-  auto bad_pk = [&](uint32_t idx, uint32_t vi) {
-    return J.fail(CMTV_COMMIT_PANIC_BAD_PUBKEY, (int32_t)idx,
-                  "ed25519: bad public key length: " + std::to_string(vals->pk_off[vi + 1] - vals->pk_off[vi]));
-  };
-  int64_t tally = 0;
-  size_t j = 0;
-  std::unordered_map<uint32_t, uint32_t> seen;
-  for (uint32_t idx = 0; idx < nsig; idx++) {
-    const uint8_t flag = commit->flags[idx];
-    if (J.kind == CMTV_VERIFY_COMMIT) {
-      if (flag == kFlagAbsent) continue;
-      if (flag != kFlagCommit && flag != kFlagNil)
-        return J.fail(CMTV_COMMIT_PANIC_UNKNOWN_FLAG, (int32_t)idx, "Unknown BlockIDFlag: " + std::to_string(flag));
-      if (vals->pk_off[idx + 1] - vals->pk_off[idx] != 32) return bad_pk(idx, idx);
-      if (j >= m || J.plan_idx[j] != idx || !valid[j]) return wrong_sig(idx);
-      j++;
-      if (flag == kFlagCommit) tally += vals->voting_power[idx];
-    } else {
-      if (flag != kFlagCommit) continue;
-      uint32_t vi = idx;
-      if (J.kind == CMTV_VERIFY_COMMIT_LIGHT_TRUSTING) {
-        auto it = J.by_addr.find(std::string(reinterpret_cast<const char*>(commit->val_addrs + 20 * (size_t)idx), 20));
-        if (it == J.by_addr.end()) continue;
-        vi = it->second;
-        auto sit = seen.find(vi);
-        if (sit != seen.end()) {
-          // Validator.String(): "Validator{%v %v VP:%v A:%v}" (types/validator.go)
-          std::string vs = "Validator{" + hex_upper(vals->addrs + 20 * (size_t)vi, 20) + " PubKeyEd25519{" +
-                           hex_upper(vals->pubkeys + vals->pk_off[vi], vals->pk_off[vi + 1] - vals->pk_off[vi]) +
-                           "} VP:" + std::to_string(vals->voting_power[vi]) + " A:" +
-                           std::to_string(vals->proposer_priority ? vals->proposer_priority[vi] : 0) + "}";
-          // the Go side formats the error with its own Validator: got = the
-          // first commit index, needed = the validator's index in vals
-          J.res->got = sit->second;
-          J.res->needed = vi;
-          return J.fail(CMTV_COMMIT_ERR_DOUBLE_VOTE, (int32_t)idx,
-                        "double vote from " + vs + " (" + std::to_string(sit->second) + " and " +
-                            std::to_string(idx) + ")");
-        }
-        seen.emplace(vi, idx);
-      }
-      if (vals->pk_off[vi + 1] - vals->pk_off[vi] != 32) return bad_pk(idx, vi);
-      if (j >= m || J.plan_idx[j] != idx || !valid[j]) return wrong_sig(idx);
-      j++;
-      tally += vals->voting_power[vi];
-      if (tally > J.needed) return CMTV_OK;
-    }
-  }
-  if (J.kind == CMTV_VERIFY_COMMIT && tally > J.needed) return CMTV_OK;
-  J.res->got = tally;
-  J.res->needed = J.needed;
-  char b[160];
-  std::snprintf(b, sizeof b, "invalid commit -- insufficient voting power: got %" PRId64 ", needed more than %" PRId64,
-                tally, J.needed);
-  return J.fail(CMTV_COMMIT_ERR_NOT_ENOUGH_POWER, -1, b);
+// job_replay over a batch's verdict bytes
+int job_replay_batch(CommitJob& J, const std::vector<uint8_t>& all_valid, Seen& seen) {
+  const uint8_t* v = all_valid.data() + J.first;
+  return job_replay(J, J.plan_idx.data(), J.plan_idx.size(), [v](size_t j) { return v[j] != 0; }, seen);
 }
 
 }  // namespace
@@ -714,6 +581,12 @@ int cmtv_verify_commit(cmtv_ctx* ctx, uint32_t kind, uint32_t mode, const char* 
   if (rc != CMTV_OK) return rc;
   CommitJob J{kind, chain_id, chain_id_len, vals, block_id, height, commit, trust_num, trust_den, res, msg_buf,
               msg_cap};
+  AddrIndex addr;
+  if (kind == CMTV_VERIFY_COMMIT_LIGHT_TRUSTING) {
+    addr.build(vals->addrs, vals->n_vals);
+    J.addr = &addr;
+  }
+  thread_local Seen seen;
   std::unique_lock<std::mutex> lk;
   rc = cmtv::ctx_lock(ctx, lk);
   if (rc != CMTV_OK) return rc;
@@ -721,13 +594,13 @@ int cmtv_verify_commit(cmtv_ctx* ctx, uint32_t kind, uint32_t mode, const char* 
   SigBatch B;
   const bool cache = cmtv::cache_enabled(ctx);
   B.templated = !cache && templated_enabled();
-  job_prepare(J, B, cache, true);
+  job_prepare(J, B, cache, true, seen);
   cmtv::phase_add(ctx, cmtv::kPhPrepare, t0);
   std::vector<uint8_t> valid;
   rc = batch_verify(ctx, B, mode, valid);
   if (rc != CMTV_OK) return rc;
   const uint64_t t1 = cmtv::phase_now(ctx);
-  rc = job_replay(J, valid);
+  rc = job_replay_batch(J, valid, seen);
   cmtv::phase_add(ctx, cmtv::kPhReplay, t1);
   return rc;
 }
@@ -741,10 +614,12 @@ int cmtv_verify_commits(cmtv_ctx* ctx, uint32_t kind, uint32_t mode, const char*
   if (!vals || !commits || !results || !rcs || !heights ||
       (kind != CMTV_VERIFY_COMMIT_LIGHT_TRUSTING && !block_ids))
     return CMTV_EINVAL;
+  uint64_t n_sigs = 0;
   for (size_t c = 0; c < n; c++) {
     const int rc = job_check_args(kind, chain_id, chain_id_len, &vals[c], block_ids ? &block_ids[c] : nullptr,
                                   &commits[c], &results[c]);
     if (rc != CMTV_OK) return rc;
+    n_sigs += commits[c].n_sigs;
   }
   std::vector<CommitJob> jobs;
   jobs.reserve(n);
@@ -752,6 +627,22 @@ int cmtv_verify_commits(cmtv_ctx* ctx, uint32_t kind, uint32_t mode, const char*
     jobs.push_back(CommitJob{kind, chain_id, chain_id_len, &vals[c], block_ids ? &block_ids[c] : nullptr, heights[c],
                              &commits[c], trust_num, trust_den, &results[c], msg_bufs ? msg_bufs + c * msg_cap : nullptr,
                              msg_bufs ? msg_cap : 0});
+  // LightTrusting: one address index per distinct (address array, size)
+  std::map<std::pair<const uint8_t*, uint32_t>, AddrIndex> addr;
+  if (kind == CMTV_VERIFY_COMMIT_LIGHT_TRUSTING)
+    for (auto& J : jobs) {
+      const auto key = std::make_pair(J.vals->addrs, J.vals->n_vals);
+      auto it = addr.find(key);
+      if (it == addr.end()) {
+        it = addr.emplace(key, AddrIndex()).first;
+        it->second.build(J.vals->addrs, J.vals->n_vals);
+      }
+      J.addr = &it->second;
+    }
+  // large calls: the chunked pipeline (plan / pack / replay on the host
+  // workers, per-device lanes; the context lock only around submissions)
+  if (cmtv::pipeline_wanted(ctx, n_sigs)) return cmtv::verify_commits_pipeline(ctx, jobs.data(), n, mode, rcs);
+  thread_local Seen seen;
   std::unique_lock<std::mutex> lk;
   int rc = cmtv::ctx_lock(ctx, lk);
   if (rc != CMTV_OK) return rc;
@@ -759,13 +650,13 @@ int cmtv_verify_commits(cmtv_ctx* ctx, uint32_t kind, uint32_t mode, const char*
   SigBatch B;
   const bool prefetch = cmtv::cache_enabled(ctx);
   B.templated = !prefetch && templated_enabled();
-  for (auto& J : jobs) job_prepare(J, B, prefetch, n == 1);
+  for (auto& J : jobs) job_prepare(J, B, prefetch, n == 1, seen);
   cmtv::phase_add(ctx, cmtv::kPhPrepare, t0);
   std::vector<uint8_t> valid;
   rc = batch_verify(ctx, B, mode, valid);
   if (rc != CMTV_OK) return rc;
   const uint64_t t1 = cmtv::phase_now(ctx);
-  for (size_t c = 0; c < n; c++) rcs[c] = job_replay(jobs[c], valid);
+  for (size_t c = 0; c < n; c++) rcs[c] = job_replay_batch(jobs[c], valid, seen);
   cmtv::phase_add(ctx, cmtv::kPhReplay, t1);
   return CMTV_OK;
 }

@@ -1,0 +1,405 @@
+// pipeline.cpp -- cmtv_verify_commits for large cross-height batches
+// (blocksync and light-client replay: blockchain/v0/reactor.go:349-400,
+// light/client.go:613-689; BASELINE configs[2], 100k commits x 150).
+//
+// The one-batch path (commit.cpp) plans, stages and replays a call on one
+// thread with the context lock held throughout, and stages the whole batch
+// before the first kernel starts. Here a call is cut into chunks of about
+// CMTV_PIPE_CHUNK planned signatures (commit-aligned, one registered key set
+// per chunk) that flow through the per-device bulk lanes (runtime.cpp):
+//
+//   plan     every commit's preamble and plan (the signatures the reference
+//            loop can reach: types/validator_set.go:685-707, 740-762,
+//            793-823), its template and sign-bytes lengths -- host workers
+//   pack     a chunk's keys / indices, signatures, timestamps, flags and
+//            templates into its slot's pinned staging -- host workers
+//   submit   H2D on the lane's copy stream, k_sign_bytes + the verify kernel
+//            + the bitmap D2H on its exec stream -- context lock held
+//   replay   each commit's reference loop over the chunk's verdict bits
+//            (commit_internal.h job_replay) -- host workers
+//
+// Chunk c+1 is packed while the device verifies chunk c, and chunk c-k is
+// replayed while it does: with S slots per device and G devices, G x S
+// chunks are in flight. Chunks go round-robin over the live devices, each
+// with its own lane; a device that fails with a HIP error is retired and the
+// chunks not yet replayed are run again on the others. Verdicts, errors and
+// early exits are exactly the one-batch path's (the same plan and replay
+// code, the same kernels).
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include "commit_internal.h"
+#include "host_pool.h"
+#include "runtime_internal.h"
+#include "signbytes.h"
+
+namespace cmtv {
+
+namespace {
+
+uint64_t now_ns() {
+  return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+struct Chunk {
+  size_t c0 = 0, c1 = 0;              // commits [c0, c1)
+  const cmtv_valset* vs = nullptr;    // the key class of its signatures
+  const cmtv_keyset* ks = nullptr;    // registered keys, or null (generic kernel)
+  size_t dev = 0;                     // where it was submitted
+  int slot = 0;
+  BulkLayout L;
+};
+
+// keys of vals are all 32 bytes and packed (what a registered key set needs)
+bool packed_keys(const cmtv_valset* v) {
+  if (!v->n_vals) return false;
+  for (uint32_t i = 0; i <= v->n_vals; i++)
+    if (v->pk_off[i] != 32 * i) return false;
+  return true;
+}
+
+}  // namespace
+
+// The staging layout of one chunk (runtime_internal.h BulkLayout): the
+// pipeline writes it, the bulk lane copies and launches on it.
+void BulkLayout::compute() {
+  auto up = [](size_t x) { return (x + 255) / 256 * 256; };
+  o_key = 0;
+  o_sig = up(keyed ? 4 * m : 32 * m);
+  o_off = up(o_sig + 64 * m);
+  o_tidx = up(o_off + 4 * (m + 1));
+  o_flag = up(o_tidx + 4 * m);
+  o_sec = up(o_flag + m);
+  o_nanos = up(o_sec + 8 * m);
+  o_tmpl = up(o_nanos + 4 * m);
+  o_blob = up(o_tmpl + n_tmpls * sizeof(SbTemplate));
+  in_bytes = up(o_blob + blob_len + 16);
+  o_msg = in_bytes;  // device only: k_sign_bytes writes the messages here
+  dev_bytes = up(o_msg + msg_bytes + 16);
+}
+
+bool pipeline_wanted(const cmtv_ctx* ctx, uint64_t n_sigs) {
+  const PipeConfig pc = pipe_config(ctx);
+  if (!pc.enabled || n_sigs < pc.min_sigs || cache_enabled(ctx)) return false;
+  const char* v = std::getenv("CMTV_HOST_SIGNBYTES");  // host-encoded sign-bytes: one-batch path only
+  return !(v && v[0] == '1');
+}
+
+int verify_commits_pipeline(cmtv_ctx* ctx, CommitJob* jobs, size_t n, uint32_t mode, int* rcs) {
+  std::unique_lock<std::mutex> bulk(bulk_mutex(ctx));
+  HostPool& pool = host_pool(ctx);
+  const PipeConfig pc = pipe_config(ctx);
+  const bool trusting = n && jobs[0].kind == CMTV_VERIFY_COMMIT_LIGHT_TRUSTING;
+  uint64_t ph_plan = 0, ph_pack = 0, ph_submit = 0, ph_wait = 0, ph_replay = 0;
+  // ---- plan: each commit's preamble and plan, its template and sign-bytes
+  // lengths -- window by window, just ahead of the chunk being cut, so the
+  // planning of later commits overlaps the device's work on earlier chunks
+  std::vector<uint64_t> base(n + 1, 0);
+  for (size_t c = 0; c < n; c++) base[c + 1] = base[c] + jobs[c].commit->n_sigs;
+  std::unique_ptr<uint32_t[]> pidx(new (std::nothrow) uint32_t[base[n] + 1]);
+  std::unique_ptr<uint32_t[]> pval(trusting ? new (std::nothrow) uint32_t[base[n] + 1] : nullptr);
+  if (!pidx || (trusting && !pval)) return CMTV_ENOMEM;
+  std::vector<uint32_t> plen(n), tlen(n);
+  std::vector<uint64_t> mbytes(n);
+  // chunk-local offsets of each commit's first signature / sign-byte / template byte
+  std::vector<uint64_t> sp(n), mp(n), tp(n);
+  size_t planned_upto = 0;
+  auto plan_window = [&](uint64_t want_sigs) {
+    const uint64_t t0 = now_ns();
+    size_t b = planned_upto;
+    while (b < n && base[b] - base[planned_upto] < want_sigs) b++;
+    if (b == planned_upto) b++;
+    const size_t a = planned_upto;
+    pool.parallel_for(b - a, 64, [&](size_t lo, size_t hi) {
+      thread_local Seen seen;
+      for (size_t c = a + lo; c < a + hi; c++) {
+        CommitJob& J = jobs[c];
+        job_preamble(J);
+        plen[c] = tlen[c] = 0;
+        mbytes[c] = 0;
+        if (J.early != 1) continue;
+        uint32_t* pi = pidx.get() + base[c];
+        const size_t m = job_plan(J, pi, trusting ? pval.get() + base[c] : nullptr, seen);
+        plen[c] = (uint32_t)m;
+        if (!m) continue;
+        SbTemplate tpl;
+        tlen[c] = (uint32_t)put_commit_template(nullptr, 0, J.chain_id, J.chain_id_len, J.commit, &tpl);
+        const cmtv_commit* cm = J.commit;
+        uint64_t mb = 0;
+        for (size_t k = 0; k < m; k++) {
+          const uint32_t idx = pi[k];
+          mb += sb_msg_len(tpl, cm->flags[idx] == kFlagCommit, cm->ts_seconds[idx], cm->ts_nanos[idx]);
+        }
+        mbytes[c] = mb;
+      }
+    });
+    planned_upto = b;
+    ph_plan += now_ns() - t0;
+  };
+
+  std::unique_lock<std::mutex> lk;
+  int rc = ctx_lock(ctx, lk);
+  if (rc != CMTV_OK) return rc;
+  const bool keyed_mode = keyset_cache_enabled(ctx);
+  std::vector<size_t> live;
+  live_devices_locked(ctx, live);
+  lk.unlock();
+
+  // ---- chunks, cut on the fly: commit-aligned, about `per` planned
+  // signatures each (at least the kernels' full-rate size, pc.chunk, and at
+  // least two per device when the call is large enough to split), one key
+  // class per chunk when the keyset cache can serve it
+  std::vector<const cmtv_keyset*> pinned;
+  std::vector<Chunk> chunks;
+  uint64_t per = 0;
+  size_t cursor = 0;  // next commit to put in a chunk
+  const cmtv_valset* last_vs = nullptr;
+  bool last_packed = false;
+  auto cut_chunk = [&]() -> int {  // appends the next chunk; CMTV_OK or an error
+    if (per == 0) {
+      // the first window sets the chunk size from its plan ratio
+      plan_window(std::max<uint64_t>(pc.chunk, 1));
+      const uint64_t ws = base[planned_upto], wp = [&] {
+        uint64_t x = 0;
+        for (size_t c = 0; c < planned_upto; c++) x += plen[c];
+        return x;
+      }();
+      const uint64_t est = ws ? (uint64_t)((double)base[n] * ((double)wp / (double)ws)) : 0;
+      uint64_t nc = std::max<uint64_t>(1, est / pc.chunk);
+      const uint64_t spread = std::min<uint64_t>(2 * live.size(), est / std::max<size_t>(pc.min_sigs, 1));
+      nc = std::max(nc, spread);
+      per = std::max<uint64_t>(1, (est + nc - 1) / nc);
+    }
+    Chunk ch;
+    ch.c0 = cursor;
+    bool cls_set = false;
+    uint64_t s = 0, mb = 0, tb = 0;
+    size_t c = cursor;
+    for (; c < n; c++) {
+      if (c == planned_upto) plan_window(std::max<uint64_t>(per - std::min(per, s), 65536));
+      if (plen[c] && keyed_mode) {
+        const cmtv_valset* v = jobs[c].vals;
+        if (v != last_vs) {
+          last_vs = v;
+          last_packed = packed_keys(v);
+        }
+        const cmtv_valset* cls = last_packed ? v : nullptr;
+        if (cls_set && !((cls == nullptr) == (ch.vs == nullptr) && (!cls || same_keys(ch.vs, cls)))) break;
+        if (!cls_set) {
+          ch.vs = cls;
+          cls_set = true;
+        }
+      }
+      sp[c] = s;
+      mp[c] = mb;
+      tp[c] = tb;
+      s += plen[c];
+      mb += mbytes[c];
+      tb += tlen[c];
+      if (s >= per) {
+        c++;
+        break;
+      }
+    }
+    ch.c1 = c;
+    cursor = c;
+    ch.L.m = s;
+    ch.L.n_tmpls = ch.c1 - ch.c0;
+    ch.L.blob_len = tb;
+    ch.L.msg_bytes = mb;
+    if (mb + 16 >= (1ull << 32)) return CMTV_EINVAL;  // device message offsets are 32-bit
+    if (keyed_mode && ch.vs && ch.L.m) {
+      std::lock_guard<std::unique_lock<std::mutex>> g(lk);
+      ch.ks = keyset_for_locked(ctx, ch.vs->pubkeys, ch.vs->n_vals);
+      if (ch.ks && std::find(pinned.begin(), pinned.end(), ch.ks) == pinned.end()) {
+        keyset_pin_locked(ch.ks);
+        pinned.push_back(ch.ks);
+      }
+    }
+    ch.L.keyed = ch.ks != nullptr;
+    ch.L.compute();
+    chunks.push_back(ch);
+    return CMTV_OK;
+  };
+
+  // ---- the chunk loop
+  auto pack = [&](Chunk& ch, uint8_t* h) {
+    const BulkLayout& L = ch.L;
+    auto* kidx = reinterpret_cast<uint32_t*>(h + L.o_key);
+    uint8_t* pk = h + L.o_key;
+    uint8_t* sg = h + L.o_sig;
+    auto* off = reinterpret_cast<uint32_t*>(h + L.o_off);
+    auto* tidx = reinterpret_cast<uint32_t*>(h + L.o_tidx);
+    uint8_t* flag = h + L.o_flag;
+    auto* sec = reinterpret_cast<int64_t*>(h + L.o_sec);
+    auto* nanos = reinterpret_cast<int32_t*>(h + L.o_nanos);
+    auto* tmpls = reinterpret_cast<SbTemplate*>(h + L.o_tmpl);
+    uint8_t* blob = h + L.o_blob;
+    pool.parallel_for(ch.c1 - ch.c0, 16, [&](size_t b, size_t e) {
+      for (size_t c = ch.c0 + b; c < ch.c0 + e; c++) {
+        const size_t m = plen[c];
+        if (!m) continue;
+        const CommitJob& J = jobs[c];
+        const cmtv_commit* cm = J.commit;
+        const cmtv_valset* vals = J.vals;
+        const uint32_t tl = (uint32_t)(c - ch.c0);
+        SbTemplate t;
+        put_commit_template(blob, tp[c], J.chain_id, J.chain_id_len, cm, &t);
+        tmpls[tl] = t;
+        const uint32_t* pi = pidx.get() + base[c];
+        const uint32_t* pv = trusting ? pval.get() + base[c] : pi;
+        const size_t i0 = sp[c];
+        uint64_t mo = mp[c];
+        for (size_t k = 0; k < m; k++) {
+          const size_t i = i0 + k;
+          const uint32_t idx = pi[k], vi = pv[k];
+          if (L.keyed)
+            kidx[i] = vi;
+          else
+            std::memcpy(pk + 32 * i, vals->pubkeys + vals->pk_off[vi], 32);
+          const uint32_t s0 = cm->sig_off[idx];
+          if (cm->sig_off[idx + 1] - s0 == 64)
+            std::memcpy(sg + 64 * i, cm->sigs + s0, 64);
+          else
+            std::memset(sg + 64 * i, 0, 64);  // invalid whatever the device says (job_replay)
+          const bool fb = cm->flags[idx] == kFlagCommit;
+          const int64_t se = cm->ts_seconds[idx];
+          const int32_t na = cm->ts_nanos[idx];
+          flag[i] = fb ? 1 : 0;
+          sec[i] = se;
+          nanos[i] = na;
+          tidx[i] = tl;
+          off[i] = (uint32_t)mo;
+          mo += sb_msg_len(t, fb, se, na);
+        }
+      }
+    });
+    off[L.m] = (uint32_t)L.msg_bytes;
+  };
+  auto replay = [&](Chunk& ch, const uint64_t* bm) {
+    pool.parallel_for(ch.c1 - ch.c0, 32, [&](size_t b, size_t e) {
+      thread_local Seen seen;
+      for (size_t c = ch.c0 + b; c < ch.c0 + e; c++) {
+        const size_t i0 = sp[c];
+        rcs[c] = job_replay(jobs[c], pidx.get() + base[c], plen[c],
+                            [bm, i0](size_t j) {
+                              const size_t i = i0 + j;
+                              return ((bm[i >> 6] >> (i & 63)) & 1) != 0;
+                            },
+                            seen);
+      }
+    });
+  };
+
+  size_t next_retire = 0, retired = 0;
+  long bad_dev = -1;
+  for (;;) {
+    const size_t G = live.size();
+    const size_t S = (size_t)pc.slots;
+    if (G == 0) {
+      rc = CMTV_ENODEV;
+      break;
+    }
+    rc = CMTV_OK;
+    bad_dev = -1;
+    std::deque<size_t> inflight;
+    size_t rr = 0;
+    auto retire = [&](size_t c) -> int {
+      Chunk& ch = chunks[c];
+      const uint64_t* bm = nullptr;
+      if (ch.L.m) {
+        const uint64_t tw = now_ns();
+        const int r = bulk_wait(ctx, ch.dev, ch.slot, &bm);
+        ph_wait += now_ns() - tw;
+        if (r != CMTV_OK) {
+          bad_dev = (long)ch.dev;
+          return r;
+        }
+      }
+      const uint64_t tr = now_ns();
+      replay(ch, bm);
+      if (ch.L.m) {
+        uint64_t valid = 0;
+        for (size_t w = 0; w < ch.L.m / 64; w++) valid += (uint64_t)__builtin_popcountll(bm[w]);
+        if (ch.L.m & 63) valid += (uint64_t)__builtin_popcountll(bm[ch.L.m / 64] & ((1ull << (ch.L.m & 63)) - 1));
+        std::lock_guard<std::unique_lock<std::mutex>> g(lk);
+        count_invalid_locked(ctx, ch.L.m - valid);
+      }
+      ph_replay += now_ns() - tr;
+      retired = c + 1;  // chunks retire in order
+      return CMTV_OK;
+    };
+    for (size_t c = next_retire; rc == CMTV_OK; c++) {
+      if (c == chunks.size()) {
+        if (cursor == n) break;
+        if ((rc = cut_chunk()) != CMTV_OK) break;
+      }
+      while (rc == CMTV_OK && inflight.size() >= G * S) {
+        rc = retire(inflight.front());
+        inflight.pop_front();
+      }
+      if (rc != CMTV_OK) break;
+      Chunk& ch = chunks[c];
+      if (ch.L.m == 0) {  // nothing to verify: replayed in order with the others
+        inflight.push_back(c);
+        continue;
+      }
+      ch.dev = live[rr % G];
+      ch.slot = (int)((rr / G) % S);
+      rr++;
+      uint8_t* h = nullptr;
+      const uint64_t tk = now_ns();
+      rc = bulk_stage(ctx, ch.dev, ch.slot, ch.L, &h);
+      if (rc != CMTV_OK) {
+        bad_dev = (long)ch.dev;
+        break;
+      }
+      pack(ch, h);
+      const uint64_t ts = now_ns();
+      ph_pack += ts - tk;
+      {
+        std::lock_guard<std::unique_lock<std::mutex>> g(lk);
+        rc = bulk_submit_locked(ctx, ch.dev, ch.slot, ch.L, ch.ks, mode);
+      }
+      ph_submit += now_ns() - ts;
+      if (rc != CMTV_OK) {
+        bad_dev = (long)ch.dev;
+        break;
+      }
+      inflight.push_back(c);
+    }
+    while (rc == CMTV_OK && !inflight.empty()) {
+      rc = retire(inflight.front());
+      inflight.pop_front();
+    }
+    next_retire = retired;
+    if (rc == CMTV_OK) break;
+    // a failure: nothing of this attempt stays in flight; a device's own HIP
+    // error retires it and the chunks not yet replayed run on the others
+    bulk_drain(ctx);
+    std::lock_guard<std::unique_lock<std::mutex>> g(lk);
+    if (rc != CMTV_EHIP || bad_dev < 0 || !retire_device_locked(ctx, (size_t)bad_dev)) break;
+    // chunks are replayed in submission (= chunk) order, so the replayed
+    // ones are exactly [0, next_retire): the rest run again
+    live_devices_locked(ctx, live);
+  }
+  {
+    std::lock_guard<std::unique_lock<std::mutex>> g(lk);
+    for (auto* ks : pinned) keyset_unpin_locked(ctx, ks);
+    phase_add_ns(ctx, kPhPipePlan, ph_plan);
+    phase_add_ns(ctx, kPhPipePack, ph_pack);
+    phase_add_ns(ctx, kPhPipeSubmit, ph_submit);
+    phase_add_ns(ctx, kPhPipeWait, ph_wait);
+    phase_add_ns(ctx, kPhPipeReplay, ph_replay);
+  }
+  return rc;
+}
+
+}  // namespace cmtv

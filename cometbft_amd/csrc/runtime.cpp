@@ -11,6 +11,7 @@
 // (SURVEY.md 8e). There is no CPU verification path: if a device is unusable
 // every call fails with a negative code and the caller decides what to do.
 #include <dlfcn.h>
+#include <sched.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -19,14 +20,18 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <fstream>
+#include <memory>
 #include <mutex>
 #include <new>
 #include <random>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
 #include "../../include/cmtverify.h"
+#include "host_pool.h"
 #include "kernels.h"
 #include "merlin.h"
 #include "signbytes.h"
@@ -137,6 +142,16 @@ struct HostBuf {
     p = nullptr;
     cap = 0;
   }
+};
+
+// Lane-kernel scratch (the generic kernel's A tables, the batched keyed
+// kernel's R' and Z products) and the event of its last user: a launch on
+// another stream waits for that user (acquire_scratch), growing it first
+// waits for it to finish.
+struct Scratch {
+  DevBuf buf;
+  hipEvent_t done = nullptr;
+  bool used = false;
 };
 
 // SipHash-2-4 (Aumasson & Bernstein), keyed per process: the verdict cache's
@@ -261,6 +276,7 @@ struct Rccl {
   ncclResult_t (*AllGather)(const void*, void*, size_t, int, ncclComm_t, hipStream_t) = nullptr;
   ncclResult_t (*GroupStart)() = nullptr;
   ncclResult_t (*GroupEnd)() = nullptr;
+  ncclResult_t (*CommAbort)(ncclComm_t) = nullptr;  // optional (a failed group's stuck ranks)
 };
 
 Rccl load_rccl(const char* path) {
@@ -278,6 +294,7 @@ Rccl load_rccl(const char* path) {
   x.AllGather = reinterpret_cast<decltype(x.AllGather)>(dlsym(h, "ncclAllGather"));
   x.GroupStart = reinterpret_cast<decltype(x.GroupStart)>(dlsym(h, "ncclGroupStart"));
   x.GroupEnd = reinterpret_cast<decltype(x.GroupEnd)>(dlsym(h, "ncclGroupEnd"));
+  x.CommAbort = reinterpret_cast<decltype(x.CommAbort)>(dlsym(h, "ncclCommAbort"));
   x.ok = x.CommInitAll && x.CommDestroy && x.AllGather && x.GroupStart && x.GroupEnd;
   return x;
 }
@@ -373,6 +390,22 @@ struct Timing {
 
 }  // namespace
 
+// A device's bulk lane (runtime_internal.h): staging slots and streams of
+// the cross-height pipeline.
+struct BulkSlot {
+  HostBuf h_in;   // pinned staging, packed by the host workers
+  HostBuf h_bm;   // pinned verdict bitmap (D2H)
+  DevBuf d_in;    // the staging on the device, then the sign-bytes
+  DevBuf d_bm;    // verdict bitmap
+  hipEvent_t h2d = nullptr, done = nullptr;
+  bool pending = false;  // submitted, not yet waited for
+};
+struct BulkLane {
+  hipStream_t copy = nullptr, exec = nullptr;
+  BulkSlot slot[cmtv::kBulkSlotsMax];
+  Scratch scratch;
+};
+
 // Per-device state of a context.
 struct CmtvDev {
   int ordinal = 0;
@@ -380,7 +413,7 @@ struct CmtvDev {
   uint32_t* d_btab = nullptr;
   uint32_t* d_bcomb = nullptr;   // comb of B for registered-key verification (built lazily)
   uint16_t* d_srprog = nullptr;  // sr25519 transcript program (merlin.h)
-  DevBuf d_atab, d_in, d_out, d_all;
+  DevBuf d_in, d_out, d_all;
   HostBuf h_in, h_out;
   // small single-device host batches: the kernel writes the verdict bitmap
   // straight into this coherent, device-mapped host buffer (no D2H copy)
@@ -390,10 +423,9 @@ struct CmtvDev {
   HostBuf h_zin{nullptr, 0, hipHostMallocCoherent | hipHostMallocMapped};
   // The lane kernels' A-table scratch is shared by every launch on this
   // device, whatever stream it is enqueued on: each lane launch waits for the
-  // previous one (atab_done) so calls on different streams cannot overwrite
-  // each other's tables.
-  hipEvent_t atab_done = nullptr;
-  bool atab_used = false;
+  // previous one (Scratch::done) so calls on different streams cannot
+  // overwrite each other's tables. (The bulk lane has its own.)
+  Scratch scratch;
   hipEvent_t done = nullptr;  // cross-device ordering for peer-copy gathers
   Timing timing;
   ncclComm_t comm = nullptr;
@@ -417,6 +449,14 @@ struct CmtvDev {
   uint64_t* tag_arm = nullptr;
   uint32_t tag_seq = 0;
   bool tag_used = false;
+  // A polled host call returns once its tags are in, while the row launch
+  // may still be retiring (its last waves zero their ring words). poll_ev is
+  // recorded after that launch; the next host call on the device -- before it
+  // writes the mapped staging (h_zin) the launch read -- and the next row-slot
+  // acquisition wait for it (settle_polled), so neither the staging nor a ring
+  // slot is ever shared with a launch still in flight.
+  hipEvent_t poll_ev = nullptr;
+  bool poll_pending = false;
   // a device that returned a HIP error is taken out of the context's
   // rotation: host batches are re-planned over the others (runtime.cpp
   // run_host_batch); CMTV_FAULT_DEV=g makes device g's first launch fail
@@ -427,6 +467,7 @@ struct CmtvDev {
   double device_ms = 0;
   // verification calls on this device (CMTV_TIMING samples one in timing_every)
   uint64_t timing_seq = 0;
+  BulkLane bulk;  // the pipeline's lane on this device (created on first use)
 };
 
 struct cmtv_ctx {
@@ -466,6 +507,13 @@ struct cmtv_ctx {
   // library to load (CMTV_RCCL_LIB; empty: the system librccl)
   bool force_rccl = false, no_rccl = false, no_rccl_fallback = false;
   std::string rccl_lib;
+  // a gather failed inside RCCL: the context never builds a communicator
+  // again (rebuild_comm after a device retirement included); gathers use
+  // peer copies. rccl_drain_ms bounds the wait for the failed group's
+  // streams (CMTV_RCCL_DRAIN_MS): a rank whose collective was enqueued before
+  // the group failed never completes without its peers.
+  bool rccl_broken = false;
+  uint32_t rccl_drain_ms = 2000;
   // CMTV_FORCE_WIDE: quad kernels take the 64-window half-scalar fallback
   bool force_wide = false;
   // templated sign-bytes in the split kernels' helper waves (CMTV_NO_SB_FUSE=1: off)
@@ -512,6 +560,21 @@ struct cmtv_ctx {
   // CMTV_FAULT_SYNC_DEV=g: device g's stream synchronisation in a host batch
   // reports a HIP error (a fault found after the launch; re-shard test knob)
   long fault_sync_dev = -1;
+  // the cross-height pipeline (pipeline.cpp): its bulk lanes and worker pool
+  // belong to the holder of bulk_mu; cmtv_verify_commits calls of at least
+  // pipe_min signatures take it (CMTV_PIPE_MIN; CMTV_PIPELINE=0: never),
+  // in chunks of about pipe_chunk signatures (CMTV_PIPE_CHUNK) over
+  // pipe_slots staging slots per device (CMTV_PIPE_SLOTS), on host_threads
+  // threads (CMTV_HOST_THREADS; default: the CPUs this process may use, at
+  // most 16)
+  std::mutex bulk_mu;
+  std::unique_ptr<cmtv::HostPool> pool;
+  unsigned host_threads = 0;
+  size_t pipe_min = 32768, pipe_chunk = 1u << 20;
+  int pipe_slots = 3;
+  bool pipe_on = true;
+  // cached key sets evicted while a pipeline call had them pinned
+  std::vector<cmtv_keyset*> zombies;
 };
 
 struct cmtv_keyset {
@@ -523,11 +586,15 @@ struct cmtv_keyset {
   };
   cmtv_ctx* ctx = nullptr;
   size_t n = 0;
+  int pins = 0;               // pipeline calls using this cached set
+  bool evicted = false;       // left the keyset cache while pinned
   std::vector<PerDev> dev;    // one per device of the context
   std::vector<uint8_t> pk;    // host copy (n x 32)
 };
 
 namespace cmtv {
+
+static void evict_keyset_locked(cmtv_ctx* ctx, cmtv_keyset* ks);
 
 static int hip_fail(hipError_t e) {
   if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) return CMTV_ENOMEM;
@@ -549,6 +616,12 @@ void phase_add(cmtv_ctx* ctx, int phase, uint64_t t0) {
   if (phase == kPhPrepare) ctx->phase_calls++;
 }
 
+void phase_add_ns(cmtv_ctx* ctx, int phase, uint64_t ns) {
+  if (!ctx->phases_on) return;
+  ctx->phase_ns[phase] += ns;
+  if (phase == kPhPipePlan) ctx->phase_calls++;
+}
+
 static void harvest(cmtv_ctx* ctx, bool blocking) {
   for (auto& d : ctx->devs) {
     if (d.failed) continue;
@@ -568,24 +641,33 @@ static bool fault_hit(cmtv_ctx* ctx) {
   return false;
 }
 
-// The lane kernels' scratch (the generic kernel's A tables, the batched keyed
-// kernel's R' and Z products) is shared by every launch on a device, whatever
-// stream it is enqueued on: a launch waits for the previous user (atab_done),
-// growing it first waits for that user to finish.
-static hipError_t acquire_scratch(CmtvDev& D, size_t bytes, hipStream_t s) {
+// A lane launch's scratch (Scratch: a device's, shared by every stream, or
+// the bulk lane's): the launch waits for the previous user, growing it first
+// waits for that user to finish.
+static hipError_t acquire_scratch(Scratch& S, size_t bytes, hipStream_t s) {
   hipError_t e;
-  if (bytes > D.d_atab.cap) {
+  if (bytes > S.buf.cap) {
     // growing frees the old scratch: every earlier user must be done
-    if (D.atab_used && (e = hipEventSynchronize(D.atab_done)) != hipSuccess) return e;
-    if ((e = D.d_atab.ensure(bytes)) != hipSuccess) return e;
+    if (S.used && (e = hipEventSynchronize(S.done)) != hipSuccess) return e;
+    if ((e = S.buf.ensure(bytes)) != hipSuccess) return e;
   }
-  if (D.atab_used && (e = hipStreamWaitEvent(s, D.atab_done, 0)) != hipSuccess) return e;
+  if (S.used && (e = hipStreamWaitEvent(s, S.done, 0)) != hipSuccess) return e;
   return hipSuccess;
 }
 
-static hipError_t release_scratch(CmtvDev& D, hipStream_t s) {
-  const hipError_t e = hipEventRecord(D.atab_done, s);
-  if (e == hipSuccess) D.atab_used = true;
+static hipError_t release_scratch(Scratch& S, hipStream_t s) {
+  const hipError_t e = hipEventRecord(S.done, s);
+  if (e == hipSuccess) S.used = true;
+  return e;
+}
+
+// Waits for the last polled host launch on D (CmtvDev::poll_ev); it has
+// normally retired by then, so this is one event query.
+static hipError_t settle_polled(CmtvDev& D) {
+  if (!D.poll_pending) return hipSuccess;
+  hipError_t e = hipEventQuery(D.poll_ev);
+  if (e == hipErrorNotReady) e = hipEventSynchronize(D.poll_ev);
+  if (e == hipSuccess) D.poll_pending = false;
   return e;
 }
 
@@ -601,6 +683,8 @@ static hipError_t release_scratch(CmtvDev& D, hipStream_t s) {
 // so a slot needs no fence against a tagged launch still retiring.
 static hipError_t row_slot_acquire(cmtv_ctx* ctx, CmtvDev& D, hipStream_t s, bool bitmap, RowSlot& slot,
                                    uint32_t& k) {
+  hipError_t e0 = settle_polled(D);
+  if (e0 != hipSuccess) return e0;
   k = D.row_seq++ % kRowSlots;
   slot = RowSlot{};
   slot.words = D.d_rowslots + (size_t)k * kRowSlotWords;
@@ -652,7 +736,8 @@ static bool fuse_ok(const cmtv_ctx* ctx, size_t n) { return split_kernel_for(ctx
 
 static int enqueue_verify(cmtv_ctx* ctx, CmtvDev& D, size_t n, const uint8_t* d_pk, const uint8_t* d_sig,
                           const uint8_t* d_msg, const uint32_t* d_off, uint32_t mode, uint8_t* d_valid,
-                          uint64_t* d_bitmap, hipStream_t s, const SbFuse* sb = nullptr) {
+                          uint64_t* d_bitmap, hipStream_t s, const SbFuse* sb = nullptr, Scratch* scr = nullptr) {
+  Scratch& S = scr ? *scr : D.scratch;
   if (n == 0) return CMTV_OK;
   if (fault_hit(ctx) || D.inject_fault) return CMTV_EHIP;
   // fused sign-bytes only where the split kernels run, in one launch
@@ -676,7 +761,7 @@ static int enqueue_verify(cmtv_ctx* ctx, CmtvDev& D, size_t n, const uint8_t* d_
   if (!quad) {
     const size_t lanes = std::min<size_t>(n, ctx->lane_chunk);
     const size_t lanes_padded = (lanes + 63) / 64 * 64;
-    if ((e = acquire_scratch(D, lanes_padded * kAtabWordsPerLane * sizeof(uint32_t), s)) != hipSuccess)
+    if ((e = acquire_scratch(S, lanes_padded * kAtabWordsPerLane * sizeof(uint32_t), s)) != hipSuccess)
       return hip_fail(e);
   }
   // a row launch is one chunk (n <= kRowMaxCap)
@@ -692,11 +777,11 @@ static int enqueue_verify(cmtv_ctx* ctx, CmtvDev& D, size_t n, const uint8_t* d_
     const uint32_t cn = (uint32_t)std::min<size_t>(chunk, n - c);
     if (sr)
       e = launch_verify_sr25519(cn, d_pk + 32 * c, d_sig + 64 * c, d_msg, d_off + c, D.d_btab,
-                                static_cast<uint32_t*>(D.d_atab.p), D.d_srprog, ctx->sr_nops,
+                                static_cast<uint32_t*>(S.buf.p), D.d_srprog, ctx->sr_nops,
                                 d_valid ? d_valid + c : nullptr, d_bitmap ? d_bitmap + c / 64 : nullptr, kflags, s);
     else
       e = launch_verify(mode, cn, d_pk + 32 * c, d_sig + 64 * c, d_msg, d_off + c, D.d_btab,
-                        static_cast<uint32_t*>(D.d_atab.p), d_valid ? d_valid + c : nullptr,
+                        static_cast<uint32_t*>(S.buf.p), d_valid ? d_valid + c : nullptr,
                         d_bitmap ? d_bitmap + c / 64 : nullptr, kflags, s, sb, row ? &slot : nullptr);
     if (e == hipSuccess && row) e = row_slot_release(ctx, D, s, slot_k);
     if (e != hipSuccess) {
@@ -706,7 +791,7 @@ static int enqueue_verify(cmtv_ctx* ctx, CmtvDev& D, size_t n, const uint8_t* d_
     ctx->stats.kernel_launches++;
     D.launches++;
   }
-  if (!quad && (e = release_scratch(D, s)) != hipSuccess) return hip_fail(e);
+  if (!quad && (e = release_scratch(S, s)) != hipSuccess) return hip_fail(e);
   if (timed && (e = D.timing.end(tp, s)) != hipSuccess) return hip_fail(e);
   ctx->stats.calls++;
   ctx->stats.signatures += n;
@@ -746,8 +831,9 @@ static int ensure_bcomb(CmtvDev& D) {
 static int enqueue_verify_keyed(cmtv_ctx* ctx, CmtvDev& D, const cmtv_keyset::PerDev& K, size_t n_keys, size_t n,
                                 const uint32_t* d_idx, const uint8_t* d_sig, const uint8_t* d_msg,
                                 const uint32_t* d_off, uint32_t mode, uint8_t* d_valid, uint64_t* d_bitmap,
-                                hipStream_t s) {
+                                hipStream_t s, Scratch* scr = nullptr) {
   if (n == 0) return CMTV_OK;
+  Scratch& S = scr ? *scr : D.scratch;
   if (fault_hit(ctx) || D.inject_fault) return CMTV_EHIP;
   const bool quad = n <= ctx->keyed_quad_max;
   // lane launches: KB signatures per lane sharing one inversion while that
@@ -763,7 +849,7 @@ static int enqueue_verify_keyed(cmtv_ctx* ctx, CmtvDev& D, const cmtv_keyset::Pe
   const uint32_t kb0 = kb_for(std::min(chunk, n));
   if (kb0 > 1) {
     const size_t lanes = (std::min(chunk, n) + 64 * kb0 - 1) / (64 * kb0) * 64;
-    if ((e = acquire_scratch(D, lanes * kb0 * kKeyedBatchScratchWordsPerSig * sizeof(uint32_t), s)) != hipSuccess)
+    if ((e = acquire_scratch(S, lanes * kb0 * kKeyedBatchScratchWordsPerSig * sizeof(uint32_t), s)) != hipSuccess)
       return hip_fail(e);
   }
   // the keyed row kernel up to CMTV_KEYED_ROW_MAX (below the keyed quad
@@ -784,7 +870,7 @@ static int enqueue_verify_keyed(cmtv_ctx* ctx, CmtvDev& D, const cmtv_keyset::Pe
     e = launch_verify_keyed(mode, cn, (uint32_t)n_keys, d_idx + c, d_sig + 64 * c, d_msg, d_off + c, K.d_pk, K.d_ok,
                             K.d_tab, D.d_bcomb, d_valid ? d_valid + c : nullptr,
                             d_bitmap ? d_bitmap + c / 64 : nullptr, quad, n <= ctx->quad_split_max,
-                            ctx->keyed_wait, D.d_diag, kb, static_cast<uint32_t*>(D.d_atab.p),
+                            ctx->keyed_wait, D.d_diag, kb, static_cast<uint32_t*>(S.buf.p),
                             quad ? nullptr : K.d_wide, D.d_btab, ctx->wide_dma, s, krow ? &slot : nullptr,
                             ctx->keyed_mixed);
     if (e == hipSuccess && krow) e = row_slot_release(ctx, D, s, slot_k);
@@ -796,7 +882,7 @@ static int enqueue_verify_keyed(cmtv_ctx* ctx, CmtvDev& D, const cmtv_keyset::Pe
     ctx->stats.keyed_launches++;
     D.launches++;
   }
-  if (kb0 > 1 && (e = release_scratch(D, s)) != hipSuccess) return hip_fail(e);
+  if (kb0 > 1 && (e = release_scratch(S, s)) != hipSuccess) return hip_fail(e);
   if (timed && (e = D.timing.end(tp, s)) != hipSuccess) return hip_fail(e);
   ctx->stats.calls++;
   ctx->stats.signatures += n;
@@ -806,6 +892,40 @@ static int enqueue_verify_keyed(cmtv_ctx* ctx, CmtvDev& D, const cmtv_keyset::Pe
 }
 
 // ---------------------------------------------------------------- sharding
+
+// Waits up to ctx->rccl_drain_ms for the streams of devices dev[0..G);
+// false if one still has work queued (a collective that cannot complete).
+static bool drain_bounded(cmtv_ctx* ctx, const size_t* dev, size_t G) {
+  const auto t_end = std::chrono::steady_clock::now() + std::chrono::milliseconds(ctx->rccl_drain_ms);
+  for (size_t g = 0; g < G; g++) {
+    CmtvDev& D = ctx->devs[dev[g]];
+    (void)hipSetDevice(D.ordinal);
+    for (;;) {
+      const hipError_t q = hipStreamQuery(D.stream);
+      if (q != hipErrorNotReady) break;  // done (or failed: nothing left to wait for)
+      if (std::chrono::steady_clock::now() > t_end) return false;
+      std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+  }
+  (void)hipGetLastError();
+  return true;
+}
+
+// Releases every device's communicator; abort = ncclCommAbort where the
+// library has it (ends collectives stuck on their peers), else CommDestroy.
+static void drop_comms(cmtv_ctx* ctx, bool abort) {
+  const Rccl& R = rccl(ctx->rccl_lib);
+  for (auto& D : ctx->devs) {
+    if (D.comm && R.ok) {
+      (void)hipSetDevice(D.ordinal);
+      if (abort && R.CommAbort)
+        (void)R.CommAbort(D.comm);
+      else
+        (void)R.CommDestroy(D.comm);
+    }
+    D.comm = nullptr;
+  }
+}
 
 // Bitmap all-gather over the devices dev[0..G): the one at position g holds
 // its shard in words [g W, (g+1) W) of bufs[g] (G x W words each); afterwards
@@ -829,12 +949,26 @@ static int gather_bitmaps(cmtv_ctx* ctx, const size_t* dev, size_t G, size_t W, 
     bad |= R.GroupEnd() != 0;
     if (!bad) return CMTV_OK;
     // RCCL refused the gather (a node whose xGMI / RCCL setup fails at run
-    // time): this gather and every later one take the peer copies below,
-    // which need no communicator; CMTV_NO_RCCL_FALLBACK=1 reports it instead
+    // time). Some ranks' collectives may already be enqueued (RCCL launches
+    // each rank's kernel at GroupEnd): they wait for peers that never come,
+    // and anything queued behind them would hang. So the communicators go
+    // (aborted when a stream does not drain within rccl_drain_ms, which ends
+    // a stuck collective), the context never builds one again, and only a
+    // gather whose streams drained falls back to peer copies below -- this one
+    // and every later one; CMTV_NO_RCCL_FALLBACK=1 reports CMTV_ERCCL instead.
     ctx->stats.rccl_failures++;
-    if (ctx->no_rccl_fallback) return CMTV_ERCCL;
+    const bool drained = drain_bounded(ctx, dev, G);
+    drop_comms(ctx, !drained);
+    ctx->rccl_broken = true;
     ctx->rccl = false;
     ctx->stats.rccl = 0;
+    if (!drained) {
+      // an aborted collective leaves its stream in an error state: wait once
+      // more (bounded) so a later call does not queue behind it
+      (void)drain_bounded(ctx, dev, G);
+      return CMTV_ERCCL;
+    }
+    if (ctx->no_rccl_fallback) return CMTV_ERCCL;
   }
   hipError_t e;
   for (size_t h = 0; h < G; h++) {
@@ -1039,6 +1173,9 @@ static int run_host_batch_(cmtv_ctx* ctx, const HostBatch& B, uint8_t* out_valid
     CmtvDev& D = ctx->devs[d0];
     *bad_dev = (long)d0;
     (void)hipSetDevice(D.ordinal);
+    // the previous polled launch read h_zin: it must be done before the
+    // staging below overwrites it
+    if ((e = settle_polled(D)) != hipSuccess) return hip_fail(e);
     if ((e = D.h_zc.ensure(8 * words)) != hipSuccess) return hip_fail(e);
     void* dzc = nullptr;
     if ((e = hipHostGetDevicePointer(&dzc, D.h_zc.p, 0)) != hipSuccess) return hip_fail(e);
@@ -1058,6 +1195,12 @@ static int run_host_batch_(cmtv_ctx* ctx, const HostBatch& B, uint8_t* out_valid
     const int rc = enqueue_shard(ctx, d0, B, 0, n, false, static_cast<uint64_t*>(dzc), o_valid, true);
     D.tag_arm = nullptr;
     if (rc != CMTV_OK) return rc;
+    if (D.tag_used) {  // settled by the next call (settle_polled)
+      if (!D.poll_ev && (e = hipEventCreateWithFlags(&D.poll_ev, hipEventDisableTiming)) != hipSuccess)
+        return hip_fail(e);
+      if ((e = hipEventRecord(D.poll_ev, D.stream)) != hipSuccess) return hip_fail(e);
+      D.poll_pending = true;
+    }
     const uint64_t t_wait = phase_now(ctx);
     if ((e = D.tag_used ? wait_row_tags(D, n) : hipStreamSynchronize(D.stream)) != hipSuccess) return hip_fail(e);
     uint64_t* bm = static_cast<uint64_t*>(D.h_zc.p);
@@ -1338,7 +1481,7 @@ uint32_t ctx_default_mode(const cmtv_ctx* ctx) { return ctx->default_mode; }
 static int init_device(cmtv_ctx* ctx, CmtvDev& D) {
   if (hipSetDevice(D.ordinal) != hipSuccess) return CMTV_ENODEV;
   hipError_t e = hipStreamCreateWithFlags(&D.stream, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&D.atab_done, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&D.scratch.done, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&D.done, hipEventDisableTiming);
   if (e == hipSuccess) e = hipMalloc(&D.d_diag, kDiagWords * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMemsetAsync(D.d_diag, 0, kDiagWords * sizeof(uint32_t), D.stream);
@@ -1355,10 +1498,13 @@ static int init_device(cmtv_ctx* ctx, CmtvDev& D) {
   return e == hipSuccess ? CMTV_OK : hip_fail(e);
 }
 
+static void bulk_lane_release(CmtvDev& D);
+
 static void release_device(CmtvDev& D) {
   (void)hipSetDevice(D.ordinal);
   if (D.stream) (void)hipStreamSynchronize(D.stream);
-  D.d_atab.release();
+  bulk_lane_release(D);
+  D.scratch.buf.release();
   D.d_in.release();
   D.d_out.release();
   D.d_all.release();
@@ -1384,10 +1530,14 @@ static void release_device(CmtvDev& D) {
     D.row_ev[k] = nullptr;
     D.row_pending[k] = false;
   }
-  if (D.atab_done) (void)hipEventDestroy(D.atab_done);
+  if (D.scratch.done) (void)hipEventDestroy(D.scratch.done);
   if (D.done) (void)hipEventDestroy(D.done);
+  if (D.poll_ev) (void)hipEventDestroy(D.poll_ev);
+  D.poll_ev = nullptr;
+  D.poll_pending = false;
   if (D.stream) (void)hipStreamDestroy(D.stream);
-  D.atab_done = D.done = nullptr;
+  D.scratch.done = D.done = nullptr;
+  D.scratch.used = false;
   D.stream = nullptr;
 }
 
@@ -1400,7 +1550,12 @@ static void read_env(cmtv_ctx* ctx) {
     ctx->keyed_row_max = (size_t)std::strtoull(rm, nullptr, 10);
   if (const char* rw = std::getenv("CMTV_ROW_WAVES")) ctx->row_waves = rw[0] == '2' ? 2u : 4u;
   if (const char* qh = std::getenv("CMTV_QUAD_HS")) ctx->quad_hs = qh[0] != '0';
-  if (const char* hp = std::getenv("CMTV_HS_PRE")) ctx->hs_tune |= (uint32_t)(std::min(254, std::atoi(hp)) + 1) & 0xFFu;
+  if (const char* hp = std::getenv("CMTV_HS_PRE")) {
+    // 0..16 comb positions; anything else keeps the kernel's default
+    char* end = nullptr;
+    const long v = std::strtol(hp, &end, 10);
+    if (end != hp && *end == 0 && v >= 0 && v <= 16) ctx->hs_tune = (uint32_t)(v + 1);
+  }
   if (const char* os = std::getenv("CMTV_OCT_SPLIT_MAX")) ctx->oct_split_max = (size_t)std::strtoull(os, nullptr, 10);
   if (const char* qs = std::getenv("CMTV_QUAD_SPLIT_MAX")) ctx->quad_split_max = (size_t)std::strtoull(qs, nullptr, 10);
   if (const char* kq = std::getenv("CMTV_KEYED_QUAD_MAX")) ctx->keyed_quad_max = (size_t)std::strtoull(kq, nullptr, 10);
@@ -1439,6 +1594,24 @@ static void read_env(cmtv_ctx* ctx) {
   if (const char* rl = std::getenv("CMTV_RCCL_LIB")) ctx->rccl_lib = rl;
   ctx->no_rccl = std::getenv("CMTV_NO_RCCL") != nullptr;
   ctx->no_rccl_fallback = std::getenv("CMTV_NO_RCCL_FALLBACK") != nullptr;
+  if (const char* v = std::getenv("CMTV_HOST_THREADS")) {
+    const long t = std::strtol(v, nullptr, 10);
+    if (t >= 1 && t <= 256) ctx->host_threads = (unsigned)t;
+  }
+  if (const char* v = std::getenv("CMTV_PIPE_MIN")) ctx->pipe_min = (size_t)std::strtoull(v, nullptr, 10);
+  if (const char* v = std::getenv("CMTV_PIPE_CHUNK")) {
+    const size_t c = (size_t)std::strtoull(v, nullptr, 10);
+    if (c >= 64 && c <= (1u << 24)) ctx->pipe_chunk = c;
+  }
+  if (const char* v = std::getenv("CMTV_PIPE_SLOTS")) {
+    const long k = std::strtol(v, nullptr, 10);
+    if (k >= 2 && k <= kBulkSlotsMax) ctx->pipe_slots = (int)k;
+  }
+  if (const char* v = std::getenv("CMTV_PIPELINE")) ctx->pipe_on = v[0] != '0';
+  if (const char* dm = std::getenv("CMTV_RCCL_DRAIN_MS")) {
+    const long v = std::strtol(dm, nullptr, 10);
+    if (v >= 1 && v <= 600000) ctx->rccl_drain_ms = (uint32_t)v;
+  }
 }
 
 // The bitmap communicator over the live devices (rank = position in
@@ -1448,13 +1621,7 @@ static void read_env(cmtv_ctx* ctx) {
 // retired (the old communicator included it).
 static void rebuild_comm(cmtv_ctx* ctx) {
   const Rccl& R = rccl(ctx->rccl_lib);
-  for (auto& D : ctx->devs) {
-    if (D.comm && R.ok) {
-      (void)hipSetDevice(D.ordinal);
-      (void)R.CommDestroy(D.comm);
-    }
-    D.comm = nullptr;
-  }
+  drop_comms(ctx, false);
   ctx->rccl = false;
   std::vector<int> ords;
   for (size_t d : ctx->live) ords.push_back(ctx->devs[d].ordinal);
@@ -1465,8 +1632,8 @@ static void rebuild_comm(cmtv_ctx* ctx) {
   // CMTV_RCCL_LIB under CMTV_FORCE_RCCL (the one-GPU rehearsal of the
   // multi-rank path); the system RCCL refuses duplicate devices
   const bool repeat_ok = ctx->force_rccl && !ctx->rccl_lib.empty();
-  const bool want = ords.size() > 1 ? ((distinct || repeat_ok) && !ctx->no_rccl)
-                                    : (ords.size() == 1 && ctx->force_rccl);
+  const bool want = !ctx->rccl_broken && (ords.size() > 1 ? ((distinct || repeat_ok) && !ctx->no_rccl)
+                                                           : (ords.size() == 1 && ctx->force_rccl));
   if (want && R.ok) {
     std::vector<ncclComm_t> comms(ords.size(), nullptr);
     if (R.CommInitAll(comms.data(), (int)ords.size(), ords.data()) == 0) {
@@ -1598,23 +1765,20 @@ int cmtv_open_devices(const cmtv_config* cfg, const int32_t* devices, size_t n_d
 void cmtv_close(cmtv_ctx* ctx) {
   if (!ctx) return;
   if (ctx->phases_on) {
-    static const char* names[kPhCount] = {"prepare", "stage", "launch", "wait", "post", "replay"};
+    static const char* names[kPhCount] = {"prepare",   "stage",     "launch",      "wait",      "post",       "replay",
+                                          "pipe_plan", "pipe_pack", "pipe_submit", "pipe_wait", "pipe_replay"};
     std::fprintf(stderr, "{\"cmtv_host_phases_us\": {");
     for (int p = 0; p < kPhCount; p++)
       std::fprintf(stderr, "%s\"%s\": %.3f", p ? ", " : "", names[p],
                    ctx->phase_calls ? 1e-3 * (double)ctx->phase_ns[p] / (double)ctx->phase_calls : 0.0);
     std::fprintf(stderr, "}, \"calls\": %llu}\n", (unsigned long long)ctx->phase_calls);
   }
+  ctx->pool.reset();
   for (auto& e : ctx->keysets) cmtv_keyset_free(e.second);
   ctx->keysets.clear();
-  const Rccl& R = rccl(ctx->rccl_lib);
-  for (auto& D : ctx->devs) {
-    if (D.comm && R.ok) {
-      (void)hipSetDevice(D.ordinal);
-      (void)R.CommDestroy(D.comm);
-    }
-    D.comm = nullptr;
-  }
+  for (auto* z : ctx->zombies) cmtv_keyset_free(z);
+  ctx->zombies.clear();
+  drop_comms(ctx, false);
   for (auto& D : ctx->devs) release_device(D);
   delete ctx;
 }
@@ -1882,7 +2046,7 @@ int cmtv_keyset_cache(cmtv_ctx* ctx, size_t max_sets) {
     (void)hipStreamSynchronize(D.stream);
   }
   while (ctx->keysets.size() > max_sets) {
-    cmtv_keyset_free(ctx->keysets.front().second);
+    evict_keyset_locked(ctx, ctx->keysets.front().second);
     ctx->keysets.erase(ctx->keysets.begin());
   }
   ctx->keyset_cap = max_sets;
@@ -1959,6 +2123,26 @@ int register_keys_locked(cmtv_ctx* ctx, size_t n_keys, const uint8_t* pk, cmtv_k
   return CMTV_OK;
 }
 
+// A cached key set leaving the cache: freed now, or by the pipeline call
+// that still has it pinned (keyset_unpin_locked).
+static void evict_keyset_locked(cmtv_ctx* ctx, cmtv_keyset* ks) {
+  if (ks->pins > 0) {
+    ks->evicted = true;
+    ctx->zombies.push_back(ks);
+    return;
+  }
+  cmtv_keyset_free(ks);
+}
+
+void keyset_pin_locked(const cmtv_keyset* ks) { const_cast<cmtv_keyset*>(ks)->pins++; }
+
+void keyset_unpin_locked(cmtv_ctx* ctx, const cmtv_keyset* cks) {
+  auto* ks = const_cast<cmtv_keyset*>(cks);
+  if (--ks->pins > 0 || !ks->evicted) return;
+  ctx->zombies.erase(std::remove(ctx->zombies.begin(), ctx->zombies.end(), ks), ctx->zombies.end());
+  cmtv_keyset_free(ks);
+}
+
 const cmtv_keyset* keyset_for_locked(cmtv_ctx* ctx, const uint8_t* pk32, size_t n_keys) {
   if (!ctx->keyset_cap || n_keys == 0) return nullptr;
   std::string key(reinterpret_cast<const char*>(pk32), 32 * n_keys);
@@ -1967,7 +2151,7 @@ const cmtv_keyset* keyset_for_locked(cmtv_ctx* ctx, const uint8_t* pk32, size_t 
   cmtv_keyset* ks = nullptr;
   if (register_keys_locked(ctx, n_keys, pk32, &ks, 0) != CMTV_OK) return nullptr;  // generic path instead
   if (ctx->keysets.size() >= ctx->keyset_cap) {
-    cmtv_keyset_free(ctx->keysets.front().second);
+    evict_keyset_locked(ctx, ctx->keysets.front().second);
     ctx->keysets.erase(ctx->keysets.begin());
   }
   ctx->keysets.emplace_back(std::move(key), ks);
@@ -1975,6 +2159,167 @@ const cmtv_keyset* keyset_for_locked(cmtv_ctx* ctx, const uint8_t* pk32, size_t 
 }
 
 bool keyset_cache_enabled(const cmtv_ctx* ctx) { return ctx->keyset_cap != 0; }
+
+// ---------------------------------------------------------------- bulk lanes
+
+std::mutex& bulk_mutex(cmtv_ctx* ctx) { return ctx->bulk_mu; }
+
+// CPUs this process may run on: the affinity mask, bounded by a cgroup v2
+// CPU quota (cpu.max) when one is set
+static unsigned usable_cpus() {
+  unsigned n = 0;
+  cpu_set_t set;
+  if (sched_getaffinity(0, sizeof(set), &set) == 0) n = (unsigned)CPU_COUNT(&set);
+  if (n == 0) n = std::max(1u, std::thread::hardware_concurrency());
+  std::ifstream f("/sys/fs/cgroup/cpu.max");
+  std::string quota, period;
+  if (f >> quota >> period && quota != "max") {
+    const double q = std::atof(quota.c_str()), p = std::atof(period.c_str());
+    if (q > 0 && p > 0) n = std::min(n, std::max(1u, (unsigned)(q / p)));
+  }
+  return n;
+}
+
+HostPool& host_pool(cmtv_ctx* ctx) {
+  if (!ctx->pool) {
+    const unsigned t = ctx->host_threads ? ctx->host_threads : std::min(16u, usable_cpus());
+    ctx->pool.reset(new HostPool(t));
+  }
+  return *ctx->pool;
+}
+
+PipeConfig pipe_config(const cmtv_ctx* ctx) {
+  return PipeConfig{ctx->pipe_min, ctx->pipe_chunk, ctx->pipe_slots, ctx->pipe_on};
+}
+
+void live_devices_locked(cmtv_ctx* ctx, std::vector<size_t>& out) { out = ctx->live; }
+
+static hipError_t bulk_lane_init(cmtv_ctx* ctx, CmtvDev& D) {
+  BulkLane& L = D.bulk;
+  if (L.exec) return hipSuccess;
+  int least = 0, greatest = 0;
+  (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
+  hipError_t e = hipStreamCreateWithFlags(&L.copy, hipStreamNonBlocking);
+  // the lane's kernels yield to other calls' (a 150-validator VerifyCommit
+  // behind a multi-ms chunk): lowest priority
+  if (e == hipSuccess) e = hipStreamCreateWithPriority(&L.exec, hipStreamNonBlocking, least);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&L.scratch.done, hipEventDisableTiming);
+  for (int k = 0; k < kBulkSlotsMax && e == hipSuccess; k++) {
+    e = hipEventCreateWithFlags(&L.slot[k].h2d, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&L.slot[k].done, hipEventDisableTiming);
+  }
+  (void)ctx;
+  return e;
+}
+
+static void bulk_lane_release(CmtvDev& D) {
+  BulkLane& L = D.bulk;
+  if (L.exec) (void)hipStreamSynchronize(L.exec);
+  if (L.copy) (void)hipStreamSynchronize(L.copy);
+  for (auto& S : L.slot) {
+    S.h_in.release();
+    S.h_bm.release();
+    S.d_in.release();
+    S.d_bm.release();
+    if (S.h2d) (void)hipEventDestroy(S.h2d);
+    if (S.done) (void)hipEventDestroy(S.done);
+    S.h2d = S.done = nullptr;
+    S.pending = false;
+  }
+  L.scratch.buf.release();
+  if (L.scratch.done) (void)hipEventDestroy(L.scratch.done);
+  L.scratch.done = nullptr;
+  L.scratch.used = false;
+  if (L.exec) (void)hipStreamDestroy(L.exec);
+  if (L.copy) (void)hipStreamDestroy(L.copy);
+  L.exec = L.copy = nullptr;
+}
+
+int bulk_stage(cmtv_ctx* ctx, size_t dev, int slot, const BulkLayout& L, uint8_t** host) {
+  CmtvDev& D = ctx->devs[dev];
+  if (hipSetDevice(D.ordinal) != hipSuccess) return CMTV_ENODEV;
+  hipError_t e = bulk_lane_init(ctx, D);
+  BulkSlot& S = D.bulk.slot[slot];
+  if (e == hipSuccess) e = S.h_in.ensure(L.in_bytes);
+  if (e != hipSuccess) return hip_fail(e);
+  *host = static_cast<uint8_t*>(S.h_in.p);
+  return CMTV_OK;
+}
+
+int bulk_submit_locked(cmtv_ctx* ctx, size_t dev, int slot, const BulkLayout& L, const cmtv_keyset* ks,
+                       uint32_t mode) {
+  CmtvDev& D = ctx->devs[dev];
+  if (D.failed) return CMTV_EHIP;  // retired by another call meanwhile
+  if (hipSetDevice(D.ordinal) != hipSuccess) return CMTV_ENODEV;
+  BulkLane& BL = D.bulk;
+  BulkSlot& S = BL.slot[slot];
+  const size_t words = (L.m + 63) / 64;
+  hipError_t e = S.d_in.ensure(L.dev_bytes);
+  if (e == hipSuccess) e = S.d_bm.ensure(8 * std::max<size_t>(words, 1));
+  if (e == hipSuccess) e = S.h_bm.ensure(8 * std::max<size_t>(words, 1));
+  if (e != hipSuccess) return hip_fail(e);
+  auto* din = static_cast<uint8_t*>(S.d_in.p);
+  auto* dbm = static_cast<uint64_t*>(S.d_bm.p);
+  // H2D on the copy stream (overlaps the exec stream's previous chunk)
+  if ((e = hipMemcpyAsync(din, S.h_in.p, L.in_bytes, hipMemcpyHostToDevice, BL.copy)) != hipSuccess ||
+      (e = hipEventRecord(S.h2d, BL.copy)) != hipSuccess || (e = hipStreamWaitEvent(BL.exec, S.h2d, 0)) != hipSuccess)
+    return hip_fail(e);
+  auto* off = reinterpret_cast<uint32_t*>(din + L.o_off);
+  // sign-bytes from the chunk's templates into o_msg (k_sign_bytes; the
+  // bulk chunks run the lane kernels, whose launches take no fused form)
+  if ((e = launch_sign_bytes((uint32_t)L.m, din + L.o_tmpl, din + L.o_blob, reinterpret_cast<uint32_t*>(din + L.o_tidx),
+                             din + L.o_flag, reinterpret_cast<int64_t*>(din + L.o_sec),
+                             reinterpret_cast<int32_t*>(din + L.o_nanos), off, din + L.o_msg, BL.exec)) != hipSuccess)
+    return hip_fail(e);
+  int rc;
+  if (ks)
+    rc = enqueue_verify_keyed(ctx, D, ks->dev[dev], ks->n, L.m, reinterpret_cast<uint32_t*>(din + L.o_key),
+                              din + L.o_sig, din + L.o_msg, off, mode, nullptr, dbm, BL.exec, &BL.scratch);
+  else
+    rc = enqueue_verify(ctx, D, L.m, din + L.o_key, din + L.o_sig, din + L.o_msg, off, mode, nullptr, dbm, BL.exec,
+                        nullptr, &BL.scratch);
+  if (rc != CMTV_OK) return rc;
+  if ((e = hipMemcpyAsync(S.h_bm.p, dbm, 8 * words, hipMemcpyDeviceToHost, BL.exec)) != hipSuccess ||
+      (e = hipEventRecord(S.done, BL.exec)) != hipSuccess)
+    return hip_fail(e);
+  S.pending = true;
+  return CMTV_OK;
+}
+
+int bulk_wait(cmtv_ctx* ctx, size_t dev, int slot, const uint64_t** bitmap) {
+  CmtvDev& D = ctx->devs[dev];
+  BulkSlot& S = D.bulk.slot[slot];
+  if (hipSetDevice(D.ordinal) != hipSuccess) return CMTV_ENODEV;
+  const hipError_t e = hipEventSynchronize(S.done);
+  S.pending = false;
+  if (e != hipSuccess) return hip_fail(e);
+  if ((long)dev == ctx->fault_sync_dev) return CMTV_EHIP;  // CMTV_FAULT_SYNC_DEV (see run_host_batch_)
+  *bitmap = static_cast<const uint64_t*>(S.h_bm.p);
+  return CMTV_OK;
+}
+
+void bulk_drain(cmtv_ctx* ctx) {
+  for (auto& D : ctx->devs) {
+    if (!D.bulk.exec) continue;
+    (void)hipSetDevice(D.ordinal);
+    (void)hipStreamSynchronize(D.bulk.copy);
+    (void)hipStreamSynchronize(D.bulk.exec);
+    for (auto& S : D.bulk.slot) S.pending = false;
+  }
+  (void)hipGetLastError();
+}
+
+bool retire_device_locked(cmtv_ctx* ctx, size_t dev) {
+  // CMTV_FAULT_AT stands for a failure of the call, not of the device
+  const bool injected = ctx->fault_pending;
+  ctx->fault_pending = false;
+  if (injected || ctx->live.size() < 2) return false;
+  retire_device(ctx, dev);
+  ctx->stats.reshards++;
+  return true;
+}
+
+void count_invalid_locked(cmtv_ctx* ctx, uint64_t n) { ctx->stats.invalid += n; }
 
 }  // namespace cmtv
 

@@ -4,6 +4,7 @@
 #include <stdint.h>
 #include <stddef.h>
 #include <mutex>
+#include <vector>
 
 struct cmtv_ctx;
 struct cmtv_keyset;
@@ -44,9 +45,71 @@ bool keyset_cache_enabled(const cmtv_ctx* ctx);
 // Host-side phase clock (CMTV_HOST_PHASES=1, read at open): where a call's
 // host time goes, summed over the context's life and printed as one JSON line
 // on stderr by cmtv_close. phase_now is 0 when the clock is off.
-enum HostPhase { kPhPrepare, kPhStage, kPhLaunch, kPhWait, kPhPost, kPhReplay, kPhCount };
+// The pipeline's phases (pipeline.cpp): per-commit plan, pinned-staging
+// pack, submission (under the context lock), waits for chunk verdicts and
+// replay; each summed over the host worker threads' wall time, not CPU time.
+enum HostPhase {
+  kPhPrepare, kPhStage, kPhLaunch, kPhWait, kPhPost, kPhReplay,
+  kPhPipePlan, kPhPipePack, kPhPipeSubmit, kPhPipeWait, kPhPipeReplay, kPhCount
+};
 uint64_t phase_now(const cmtv_ctx* ctx);
 void phase_add(cmtv_ctx* ctx, int phase, uint64_t t0);
 int register_keys_locked(cmtv_ctx* ctx, size_t n_keys, const uint8_t* pk, cmtv_keyset** out, uint32_t flags);
+// phase_add with a duration measured elsewhere (pipeline; lock held)
+void phase_add_ns(cmtv_ctx* ctx, int phase, uint64_t ns);
+
+// ---------------------------------------------------------------- bulk lanes
+// Large cross-height batches (pipeline.cpp) run through a per-device bulk
+// lane: its own H2D (copy) and kernel (exec, lowest priority) streams, its
+// own lane-kernel scratch and kBulkSlots pinned / device staging slots, so a
+// chunk neither queues behind nor shares buffers with other calls, and the
+// context lock is held only while a chunk is enqueued.
+//
+// One chunk's staging, in one pinned block copied to the device at once:
+//   key  u32 validator index (registered keys) or 32-byte key, per signature
+//   sig  64 bytes, off u32 message offsets (m + 1), tidx u32 commit template,
+//   flag u8 (1 = BlockIDFlagCommit), sec i64, nanos i32 per signature,
+//   tmpls SbTemplate per commit, blob the templates' bytes;
+// on the device k_sign_bytes then writes the sign-bytes after it (o_msg).
+constexpr int kBulkSlotsMax = 4;
+struct BulkLayout {
+  size_t m = 0, n_tmpls = 0, blob_len = 0;
+  uint64_t msg_bytes = 0;
+  bool keyed = false;
+  size_t o_key = 0, o_sig = 0, o_off = 0, o_tidx = 0, o_flag = 0, o_sec = 0, o_nanos = 0, o_tmpl = 0, o_blob = 0;
+  size_t in_bytes = 0, o_msg = 0, dev_bytes = 0;
+  void compute();
+};
+std::mutex& bulk_mutex(cmtv_ctx* ctx);
+class HostPool;
+// the context's worker pool (created on first use; bulk lock held)
+HostPool& host_pool(cmtv_ctx* ctx);
+struct PipeConfig {
+  size_t min_sigs, chunk;
+  int slots;
+  bool enabled;
+};
+PipeConfig pipe_config(const cmtv_ctx* ctx);
+// live device indices, in shard order (context lock held)
+void live_devices_locked(cmtv_ctx* ctx, std::vector<size_t>& out);
+// the pinned staging of (dev, slot), grown to L.in_bytes (bulk lock held)
+int bulk_stage(cmtv_ctx* ctx, size_t dev, int slot, const BulkLayout& L, uint8_t** host);
+// enqueues the chunk staged in (dev, slot): H2D, sign-bytes, verification
+// (ks: by registered key), verdict bitmap D2H (context lock held)
+int bulk_submit_locked(cmtv_ctx* ctx, size_t dev, int slot, const BulkLayout& L, const cmtv_keyset* ks,
+                       uint32_t mode);
+// waits for the chunk in (dev, slot); *bitmap = its verdict words (pinned)
+int bulk_wait(cmtv_ctx* ctx, size_t dev, int slot, const uint64_t** bitmap);
+// after an error: waits for every bulk lane, clears sticky errors
+void bulk_drain(cmtv_ctx* ctx);
+// retires device dev after its HIP error (context lock held); false if it was
+// the last live device
+bool retire_device_locked(cmtv_ctx* ctx, size_t dev);
+// the context's invalid-verdict counter (context lock held)
+void count_invalid_locked(cmtv_ctx* ctx, uint64_t n);
+// registered key set pins (context lock held): a pinned cached set is not
+// freed by eviction until unpinned
+void keyset_pin_locked(const cmtv_keyset* ks);
+void keyset_unpin_locked(cmtv_ctx* ctx, const cmtv_keyset* ks);
 
 }  // namespace cmtv

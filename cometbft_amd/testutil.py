@@ -158,3 +158,139 @@ def replay_messages(h0: int, n_heights: int, n_vals: int, chunk: int = 8192):
     off[-1] = n_heights * lh
     assert off[-1] < 2**32
     return msg, off.astype(np.uint32)
+
+
+class ReplayChain:
+    """configs[2]'s input as a node's cgo shim hands it to cmtv_verify_commits:
+    n_heights synthetic commits (heights h0 ..) of one validator set, every
+    signature present (BlockIDFlagCommit), packed ONCE into flat arrays with one
+    cmtv_commit / cmtv_valset / cmtv_block_id per height pointing into them
+    (blockchain/v0/reactor.go:349-400, light/client.go:613-689 verify commit
+    after commit of the same set). Signatures come from the device signer over
+    replay_messages' sign-bytes; a fraction `flip` of them (seed, global
+    indices) carry one flipped bit.
+
+    expected(kind) gives, per height, the reference loop's outcome over these
+    inputs (types/validator_set.go:685-713 / 740-764): the first flipped
+    signature the loop reaches (-1 = nil error)."""
+
+    def __init__(self, ctx: Context, sv: SyntheticValidators, h0: int, n_heights: int, flip: float = 0.01,
+                 seed: int = 42, sign_heights: int = 8192):
+        import ctypes
+
+        from . import _native as N
+
+        n = len(sv.valset.validators)
+        self.n_vals, self.n_heights, self.h0 = n, n_heights, h0
+        total = n * n_heights
+        self.sig = np.empty((total, 64), np.uint8)
+        kidx = np.tile(np.arange(n, dtype=np.uint32), min(sign_heights, n_heights))
+        for c0 in range(0, n_heights, sign_heights):
+            hc = min(sign_heights, n_heights - c0)
+            m, off = replay_messages(h0 + c0, hc, n)
+            self.sig[c0 * n:(c0 + hc) * n] = ctx.sign(sv.seeds, m, off, kidx[:hc * n])
+            del m, off
+        rng = np.random.default_rng(seed)
+        self.flipped = np.sort(rng.choice(total, int(total * flip), replace=False)) if flip > 0 else \
+            np.zeros(0, np.int64)
+        bit = rng.integers(0, 512, self.flipped.size)
+        self.sig[self.flipped, bit // 8] ^= (1 << (bit % 8)).astype(np.uint8)
+        # shared per-validator arrays (identical in every commit of the chain)
+        self.flags = np.full(n + 1, BLOCK_ID_FLAG_COMMIT, np.uint8)
+        self.sig_off = (np.arange(n + 1, dtype=np.uint32) * 64)
+        ts = [timestamp(h0, i) for i in range(n)]
+        assert all(s == EPOCH_2023 + h0 for s, _ in ts)  # n < 1e6: seconds = EPOCH + h
+        self.nanos = np.array([ns for _, ns in ts] + [0], np.int32)
+        self.secs = (EPOCH_2023 + h0 + np.arange(n_heights, dtype=np.int64))[:, None].repeat(n, 1)
+        self.addrs = np.frombuffer(b"".join(v.address for v in sv.valset.validators) + b"\0", np.uint8).copy()
+        hs = range(h0, h0 + n_heights)
+        self.bhash = np.frombuffer(b"".join(hashlib.sha256(b"block%d" % h).digest() for h in hs), np.uint8).reshape(
+            n_heights, 32)
+        self.phash = np.frombuffer(b"".join(hashlib.sha256(b"parts%d" % h).digest() for h in hs), np.uint8).reshape(
+            n_heights, 32)
+        self.heights = (ctypes.c_int64 * n_heights)(*range(h0, h0 + n_heights))
+        vs, self._keep_vs = sv.valset._pack()
+        self.vs_arr = (N.cmtv_valset * n_heights)()
+        raw = np.frombuffer(self.vs_arr, np.uint8).reshape(n_heights, ctypes.sizeof(N.cmtv_valset))
+        raw[:] = np.frombuffer(bytes(vs), np.uint8)
+        # cmtv_commit / cmtv_block_id arrays, filled through numpy views at
+        # the ctypes field offsets
+        C, B = N.cmtv_commit, N.cmtv_block_id
+        self.cm_arr = (C * n_heights)()
+        self.bid_arr = (B * n_heights)()
+        cm = np.frombuffer(self.cm_arr, np.uint8).reshape(n_heights, ctypes.sizeof(C))
+        bd = np.frombuffer(self.bid_arr, np.uint8).reshape(n_heights, ctypes.sizeof(B))
+        ar = np.arange(n_heights, dtype=np.uint64)
+
+        def put(rows, off, vals, dt):
+            w = np.dtype(dt).itemsize
+            rows[:, off:off + w] = np.ascontiguousarray(np.asarray(vals).astype(dt)).view(np.uint8).reshape(-1, w)
+
+        def ptr(a):
+            return np.uint64(a.ctypes.data)
+
+        for rows, boff in ((cm, C.block_id.offset), (bd, 0)):
+            put(rows, boff + B.hash.offset, ptr(self.bhash) + 32 * ar, np.uint64)
+            put(rows, boff + B.hash_len.offset, np.full(n_heights, 32), np.uint32)
+            put(rows, boff + B.psh_total.offset, np.ones(n_heights), np.uint32)
+            put(rows, boff + B.psh_hash.offset, ptr(self.phash) + 32 * ar, np.uint64)
+            put(rows, boff + B.psh_hash_len.offset, np.full(n_heights, 32), np.uint32)
+        put(cm, C.height.offset, np.arange(h0, h0 + n_heights), np.int64)
+        put(cm, C.round.offset, np.zeros(n_heights), np.int32)
+        put(cm, C.n_sigs.offset, np.full(n_heights, n), np.uint32)
+        put(cm, C.flags.offset, np.full(n_heights, ptr(self.flags)), np.uint64)
+        put(cm, C.ts_seconds.offset, ptr(self.secs) + 8 * n * ar, np.uint64)
+        put(cm, C.ts_nanos.offset, np.full(n_heights, ptr(self.nanos)), np.uint64)
+        put(cm, C.sigs.offset, ptr(self.sig) + 64 * n * ar, np.uint64)
+        put(cm, C.sig_off.offset, np.full(n_heights, ptr(self.sig_off)), np.uint64)
+        put(cm, C.val_addrs.offset, np.full(n_heights, ptr(self.addrs)), np.uint64)
+        self.res = (N.cmtv_commit_result * n_heights)()
+        self.rcs = (ctypes.c_int * n_heights)()
+
+    def call(self, ctx: Context, kind: int, mode: int = 0, msg_bufs=None, msg_cap: int = 0) -> None:
+        """One cmtv_verify_commits over the whole chain (results in res / rcs)."""
+        from . import _native as N
+
+        cid = CHAIN_ID.encode()
+        rc = N.lib().cmtv_verify_commits(ctx.handle, kind, mode, cid, len(cid), self.n_heights, self.vs_arr,
+                                         self.bid_arr, self.heights, self.cm_arr, 1, 3, self.res, self.rcs, msg_bufs,
+                                         msg_cap)
+        N.check(rc, "cmtv_verify_commits")
+
+    def expected(self, kind: int) -> np.ndarray:
+        """Per height: the index of the first flipped signature the reference
+        loop reaches, -1 when it returns nil. VerifyCommit visits every
+        signature; VerifyCommitLight (and LightTrusting at 1/3 over the same
+        set) stops once the tally exceeds the threshold (equal powers: after
+        floor(needed / power) + 1 signatures)."""
+        from . import _native as N
+
+        n = self.n_vals
+        power = 10
+        total = power * n
+        if kind == N.VERIFY_COMMIT:
+            reach = n
+        elif kind == N.VERIFY_COMMIT_LIGHT:
+            reach = min(n, (total * 2 // 3) // power + 1)
+        else:
+            reach = min(n, (total * 1 // 3) // power + 1)
+        first = np.full(self.n_heights, -1, np.int64)
+        h = self.flipped // n
+        i = self.flipped % n
+        sel = i < reach
+        h, i = h[sel], i[sel]
+        # flipped is sorted: the first entry per height is its lowest index
+        uh, at = np.unique(h, return_index=True)
+        first[uh] = i[at]
+        return first
+
+    def outcome(self) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """(rcs, codes, sig_index) of the last call, as arrays."""
+        rcs = np.ctypeslib.as_array(self.rcs).copy()
+        res = np.frombuffer(self.res, np.uint8).reshape(self.n_heights, -1)
+        from . import _native as N
+
+        code = res[:, N.cmtv_commit_result.code.offset:N.cmtv_commit_result.code.offset + 4].copy().view(np.int32)[:, 0]
+        si = res[:, N.cmtv_commit_result.sig_index.offset:N.cmtv_commit_result.sig_index.offset + 4].copy().view(
+            np.int32)[:, 0]
+        return rcs, code, si

@@ -1,0 +1,298 @@
+// fake_runtime.cpp -- test double of the device half of libcmtverify
+// (runtime_internal.h) for tests/host/pipecheck.cpp: the commit layer
+// (commit.cpp) and the cross-height pipeline (pipeline.cpp) are linked
+// unchanged against it and run on the CPU, so their host logic -- plan,
+// pinned-staging layout, chunking, replay, retries -- is checked without a
+// GPU and under AddressSanitizer.
+//
+// The "device" decodes a chunk's staging exactly as the kernels read it
+// (keys or key indices, signatures, message offsets, per-commit templates
+// written out with signbytes.h sb_write, which must land on the host's
+// offsets) and verifies each signature with the C restatement of Go 1.19
+// ed25519.Verify (oracle/cmtv_oracle.c). It does so lazily, when the chunk is
+// waited for, so a host that rewrote a slot's staging while its chunk was in
+// flight reads back wrong verdicts. Test infrastructure only.
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../cometbft_amd/csrc/commit_internal.h"
+#include "../../cometbft_amd/csrc/host_pool.h"
+#include "../../cometbft_amd/csrc/runtime_internal.h"
+#include "../../cometbft_amd/csrc/signbytes.h"
+
+extern "C" int oracle_verify_one(const uint8_t* pk, const uint8_t* msg, size_t mlen, const uint8_t* sig, int mode);
+
+struct FakeSlot {
+  std::vector<uint8_t> h_in;
+  std::vector<uint64_t> bm;
+  cmtv::BulkLayout L;
+  const cmtv_keyset* ks = nullptr;
+  uint32_t mode = 0;
+  bool pending = false;
+};
+
+struct cmtv_keyset {
+  size_t n = 0;
+  std::vector<uint8_t> pk;
+  int pins = 0;
+};
+
+struct cmtv_ctx {
+  std::mutex mu, bulk_mu;
+  std::unique_ptr<cmtv::HostPool> pool;
+  cmtv::PipeConfig pc{32768, 1u << 20, 3, true};
+  unsigned threads = 4;
+  size_t keyset_cap = 0;
+  std::vector<std::pair<std::string, cmtv_keyset*>> keysets;
+  std::vector<cmtv_keyset*> evicted;
+  std::vector<size_t> live;
+  size_t n_devs = 1;
+  std::vector<std::vector<FakeSlot>> slots;  // [dev][slot]
+  long fail_dev = -1;                        // bulk_wait on this device fails once
+  uint64_t signatures = 0, invalid = 0, chunks = 0, retired = 0, keyed_chunks = 0;
+  std::map<std::string, uint8_t> memo;       // (mode, pk, sig, msg) -> verdict
+  std::mutex memo_mu;
+};
+
+namespace {
+
+struct VecOut {
+  std::vector<uint8_t>& v;
+  void put(uint32_t pos, uint8_t b) { v[pos] = b; }
+  void copy(uint32_t pos, const uint8_t* s, uint32_t len) { std::memcpy(&v[pos], s, len); }
+};
+
+uint8_t verify_memo(cmtv_ctx* ctx, uint32_t mode, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
+                    size_t mlen) {
+  std::string k(1, (char)mode);
+  k.append(reinterpret_cast<const char*>(pk), 32);
+  k.append(reinterpret_cast<const char*>(sig), 64);
+  k.append(reinterpret_cast<const char*>(msg), mlen);
+  {
+    std::lock_guard<std::mutex> g(ctx->memo_mu);
+    auto it = ctx->memo.find(k);
+    if (it != ctx->memo.end()) return it->second;
+  }
+  const uint8_t v = (uint8_t)(oracle_verify_one(pk, msg, mlen, sig, (int)mode) != 0);
+  std::lock_guard<std::mutex> g(ctx->memo_mu);
+  ctx->memo.emplace(std::move(k), v);
+  return v;
+}
+
+// verdicts of a templated batch laid out as the device reads it
+int device_verify(cmtv_ctx* ctx, size_t n, const uint8_t* keys, bool keyed, const cmtv_keyset* ks, const uint8_t* sig,
+                  const uint32_t* off, const cmtv::SbTemplate* tmpls, size_t n_tmpls, const uint8_t* blob,
+                  const uint32_t* tidx, const uint8_t* flag, const int64_t* sec, const int32_t* nanos, uint32_t mode,
+                  uint8_t* valid) {
+  std::vector<uint8_t> msg;
+  for (size_t i = 0; i < n; i++) {
+    if (tidx[i] >= n_tmpls) return CMTV_EINVAL;
+    const cmtv::SbTemplate& t = tmpls[tidx[i]];
+    const uint32_t len = cmtv::sb_msg_len(t, flag[i] != 0, sec[i], nanos[i]);
+    if (off[i + 1] - off[i] != len) {
+      std::fprintf(stderr, "fake device: message %zu length %u, offsets say %u\n", i, len, off[i + 1] - off[i]);
+      return CMTV_EINVAL;
+    }
+    msg.assign(len, 0);
+    VecOut out{msg};
+    if (cmtv::sb_write(out, t, blob, flag[i] != 0, sec[i], nanos[i]) != len) return CMTV_EINVAL;
+    const uint8_t* pk;
+    if (keyed) {
+      uint32_t ki;
+      std::memcpy(&ki, keys + 4 * i, 4);
+      if (ki >= ks->n) return CMTV_EINVAL;
+      pk = ks->pk.data() + 32 * (size_t)ki;
+    } else {
+      pk = keys + 32 * i;
+    }
+    valid[i] = verify_memo(ctx, mode, pk, sig + 64 * i, msg.data(), len);
+  }
+  return CMTV_OK;
+}
+
+}  // namespace
+
+namespace cmtv {
+
+int ctx_lock(cmtv_ctx* ctx, std::unique_lock<std::mutex>& lk) {
+  lk = std::unique_lock<std::mutex>(ctx->mu);
+  return CMTV_OK;
+}
+uint32_t ctx_default_mode(const cmtv_ctx*) { return 0; }
+bool cache_enabled(const cmtv_ctx*) { return false; }
+uint64_t phase_now(const cmtv_ctx*) { return 0; }
+void phase_add(cmtv_ctx*, int, uint64_t) {}
+void phase_add_ns(cmtv_ctx*, int, uint64_t) {}
+bool keyset_cache_enabled(const cmtv_ctx* ctx) { return ctx->keyset_cap != 0; }
+int register_keys_locked(cmtv_ctx*, size_t, const uint8_t*, cmtv_keyset**, uint32_t) { return CMTV_EINVAL; }
+
+int verify_host_locked(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
+                       const uint32_t* msg_off, uint32_t mode, uint8_t* out_valid, uint64_t* out_bitmap) {
+  for (size_t i = 0; i < n; i++) {
+    const uint8_t v = verify_memo(ctx, mode, pk + 32 * i, sig + 64 * i, msg + msg_off[i], msg_off[i + 1] - msg_off[i]);
+    if (out_valid) out_valid[i] = v;
+    if (out_bitmap) {
+      if ((i & 63) == 0) out_bitmap[i / 64] = 0;
+      out_bitmap[i / 64] |= (uint64_t)v << (i & 63);
+    }
+  }
+  ctx->signatures += n;
+  return CMTV_OK;
+}
+
+int verify_templated_locked(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_t* sig, const uint32_t* msg_off,
+                            const void* tmpls, size_t n_tmpls, const uint8_t* blob, size_t, const uint32_t* tidx,
+                            const uint8_t* commit_flag, const int64_t* sec, const int32_t* nanos, uint32_t mode,
+                            uint8_t* out_valid, const cmtv_keyset* ks, const uint32_t* key_idx) {
+  ctx->signatures += n;
+  std::vector<uint32_t> off(msg_off, msg_off + n + 1);
+  return device_verify(ctx, n, ks ? reinterpret_cast<const uint8_t*>(key_idx) : pk, ks != nullptr, ks, sig, off.data(),
+                       static_cast<const SbTemplate*>(tmpls), n_tmpls, blob, tidx, commit_flag, sec, nanos, mode,
+                       out_valid);
+}
+
+const cmtv_keyset* keyset_for_locked(cmtv_ctx* ctx, const uint8_t* pk32, size_t n_keys) {
+  if (!ctx->keyset_cap || !n_keys) return nullptr;
+  std::string key(reinterpret_cast<const char*>(pk32), 32 * n_keys);
+  for (auto& e : ctx->keysets)
+    if (e.first == key) return e.second;
+  auto* ks = new cmtv_keyset();
+  ks->n = n_keys;
+  ks->pk.assign(pk32, pk32 + 32 * n_keys);
+  if (ctx->keysets.size() >= ctx->keyset_cap) {
+    // the real cache frees an evicted set once no call has it pinned
+    // (runtime.cpp evict_keyset_locked); the fake keeps every one until close
+    ctx->evicted.push_back(ctx->keysets.front().second);
+    ctx->keysets.erase(ctx->keysets.begin());
+  }
+  ctx->keysets.emplace_back(std::move(key), ks);
+  return ks;
+}
+
+void keyset_pin_locked(const cmtv_keyset* ks) { const_cast<cmtv_keyset*>(ks)->pins++; }
+void keyset_unpin_locked(cmtv_ctx*, const cmtv_keyset* ks) { const_cast<cmtv_keyset*>(ks)->pins--; }
+
+std::mutex& bulk_mutex(cmtv_ctx* ctx) { return ctx->bulk_mu; }
+HostPool& host_pool(cmtv_ctx* ctx) {
+  if (!ctx->pool) ctx->pool.reset(new HostPool(ctx->threads));
+  return *ctx->pool;
+}
+PipeConfig pipe_config(const cmtv_ctx* ctx) { return ctx->pc; }
+void live_devices_locked(cmtv_ctx* ctx, std::vector<size_t>& out) { out = ctx->live; }
+
+int bulk_stage(cmtv_ctx* ctx, size_t dev, int slot, const BulkLayout& L, uint8_t** host) {
+  FakeSlot& S = ctx->slots[dev][slot];
+  if (S.pending) {
+    std::fprintf(stderr, "fake: staging of dev %zu slot %d reused while its chunk is in flight\n", dev, slot);
+    return CMTV_EHIP;
+  }
+  // fresh garbage every time: stale bytes from an earlier chunk must not
+  // mask a field the host forgot to write
+  S.h_in.assign(L.in_bytes, 0xA5);
+  *host = S.h_in.data();
+  return CMTV_OK;
+}
+
+int bulk_submit_locked(cmtv_ctx* ctx, size_t dev, int slot, const BulkLayout& L, const cmtv_keyset* ks,
+                       uint32_t mode) {
+  FakeSlot& S = ctx->slots[dev][slot];
+  if (L.in_bytes > S.h_in.size()) return CMTV_EINVAL;
+  S.L = L;
+  S.ks = ks;
+  S.mode = mode;
+  S.pending = true;
+  ctx->chunks++;
+  ctx->signatures += L.m;
+  if (ks) ctx->keyed_chunks++;
+  return CMTV_OK;
+}
+
+int bulk_wait(cmtv_ctx* ctx, size_t dev, int slot, const uint64_t** bitmap) {
+  FakeSlot& S = ctx->slots[dev][slot];
+  if (!S.pending) return CMTV_EINVAL;
+  S.pending = false;
+  if ((long)dev == ctx->fail_dev) {
+    ctx->fail_dev = -1;
+    return CMTV_EHIP;
+  }
+  const BulkLayout& L = S.L;
+  const uint8_t* h = S.h_in.data();
+  std::vector<uint8_t> v(L.m);
+  const int rc = device_verify(ctx, L.m, h + L.o_key, L.keyed, S.ks, h + L.o_sig,
+                               reinterpret_cast<const uint32_t*>(h + L.o_off),
+                               reinterpret_cast<const SbTemplate*>(h + L.o_tmpl), L.n_tmpls, h + L.o_blob,
+                               reinterpret_cast<const uint32_t*>(h + L.o_tidx), h + L.o_flag,
+                               reinterpret_cast<const int64_t*>(h + L.o_sec),
+                               reinterpret_cast<const int32_t*>(h + L.o_nanos), S.mode, v.data());
+  if (rc != CMTV_OK) return rc;
+  const uint32_t* off = reinterpret_cast<const uint32_t*>(h + L.o_off);
+  if (off[0] != 0 || off[L.m] != L.msg_bytes) {
+    std::fprintf(stderr, "fake: offsets [%u, %u] vs %llu message bytes\n", off[0], off[L.m],
+                 (unsigned long long)L.msg_bytes);
+    return CMTV_EINVAL;
+  }
+  // garbage above bit m, as the kernels leave it
+  S.bm.assign((L.m + 63) / 64 + 1, 0xDEADBEEFCAFEF00Dull);
+  for (size_t i = 0; i < L.m; i++) {
+    const uint64_t bit = 1ull << (i & 63);
+    S.bm[i / 64] = v[i] ? (S.bm[i / 64] | bit) : (S.bm[i / 64] & ~bit);
+  }
+  *bitmap = S.bm.data();
+  return CMTV_OK;
+}
+
+void bulk_drain(cmtv_ctx* ctx) {
+  for (auto& d : ctx->slots)
+    for (auto& s : d) s.pending = false;
+}
+
+bool retire_device_locked(cmtv_ctx* ctx, size_t dev) {
+  if (ctx->live.size() < 2) return false;
+  for (size_t i = 0; i < ctx->live.size(); i++)
+    if (ctx->live[i] == dev) {
+      ctx->live.erase(ctx->live.begin() + (long)i);
+      ctx->retired++;
+      return true;
+    }
+  return false;
+}
+
+void count_invalid_locked(cmtv_ctx* ctx, uint64_t n) { ctx->invalid += n; }
+
+}  // namespace cmtv
+
+// ---- the harness's handle on the fake context
+extern "C" cmtv_ctx* fake_open(size_t n_devs, unsigned threads, size_t pipe_min, size_t chunk, int slots,
+                               bool pipe_on, size_t keyset_cap, long fail_dev) {
+  auto* c = new cmtv_ctx();
+  c->n_devs = n_devs;
+  c->threads = threads;
+  c->pc = cmtv::PipeConfig{pipe_min, chunk, slots, pipe_on};
+  c->keyset_cap = keyset_cap;
+  c->fail_dev = fail_dev;
+  for (size_t d = 0; d < n_devs; d++) c->live.push_back(d);
+  c->slots.assign(n_devs, std::vector<FakeSlot>(cmtv::kBulkSlotsMax));
+  return c;
+}
+
+extern "C" void fake_counts(cmtv_ctx* c, uint64_t* out) {
+  out[0] = c->signatures;
+  out[1] = c->invalid;
+  out[2] = c->chunks;
+  out[3] = c->retired;
+  out[4] = c->keyed_chunks;
+}
+
+extern "C" void fake_close(cmtv_ctx* c) {
+  for (auto& e : c->keysets) delete e.second;
+  for (auto* k : c->evicted) delete k;
+  delete c;
+}

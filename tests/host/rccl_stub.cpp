@@ -19,6 +19,13 @@
 // send buffers, and every rank's stream then waits for the readers of its own
 // buffer (the stream ordering a real collective gives).
 //
+// CMTV_RCCL_STUB_FAIL_GROUP=k fails the communicator's k-th grouped call
+// (ncclSystemError) with nothing copied; with CMTV_RCCL_STUB_PARTIAL=1 as
+// well, rank 0's part of that call is left enqueued as a collective whose
+// peers never arrive: its stream is held by a host callback until
+// ncclCommAbort / ncclCommDestroy of the group (or a 10 s watchdog) releases
+// it -- what a real group that fails after launching one rank's kernel does.
+//
 // Every call is appended to the file named by CMTV_RCCL_STUB_LOG (if set when
 // the communicator was created), one line per event:
 //   init n=<ranks> devs=<d0,d1,...> comm=<id>
@@ -27,11 +34,14 @@
 // and rccl_stub_calls() reports the number of gathers executed.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace {
@@ -50,7 +60,27 @@ struct Group {
   std::string log;  // CMTV_RCCL_STUB_LOG as it was at ncclCommInitAll
   int fail_at = 0;  // CMTV_RCCL_STUB_FAIL_GROUP: this group end (1-based) fails
   int ends = 0;
+  bool partial = false;  // CMTV_RCCL_STUB_PARTIAL: ... after enqueueing rank 0
+  struct Hold* hold = nullptr;  // rank 0's stuck collective, if any
 };
+
+// A stream held by a host callback until released (the stuck collective).
+struct Hold {
+  std::mutex m;
+  std::condition_variable cv;
+  bool released = false;
+  void release() {
+    std::lock_guard<std::mutex> lk(m);
+    released = true;
+    cv.notify_all();
+  }
+};
+
+void hold_stream(void* arg) {
+  auto* h = static_cast<Hold*>(arg);
+  std::unique_lock<std::mutex> lk(h->m);
+  h->cv.wait_for(lk, std::chrono::seconds(10), [h] { return h->released; });
+}
 struct Op {
   const void* send;
   void* recv;
@@ -162,6 +192,7 @@ int ncclCommInitAll(void** comms, int ndev, const int* devlist) {
   const char* path = std::getenv("CMTV_RCCL_STUB_LOG");
   auto* g = new Group{next_id++, ndev, ndev, std::vector<int>(devlist, devlist + ndev), path ? path : ""};
   if (const char* f = std::getenv("CMTV_RCCL_STUB_FAIL_GROUP")) g->fail_at = std::atoi(f);
+  if (const char* f = std::getenv("CMTV_RCCL_STUB_PARTIAL")) g->partial = f[0] == '1';
   std::string devs;
   for (int i = 0; i < ndev; i++) {
     comms[i] = new Comm{g, i, devlist[i]};
@@ -171,16 +202,22 @@ int ncclCommInitAll(void** comms, int ndev, const int* devlist) {
   return 0;
 }
 
-int ncclCommDestroy(void* comm) {
+static int release_comm(void* comm, const char* what) {
   if (!comm) return 4;
   auto* c = static_cast<Comm*>(comm);
   std::lock_guard<std::mutex> lk(mu);
-  log_line(c->g->log, "destroy comm=" + std::to_string(c->g->id) + " rank=" + std::to_string(c->rank));
+  log_line(c->g->log, std::string(what) + " comm=" + std::to_string(c->g->id) + " rank=" + std::to_string(c->rank));
   Group* g = c->g;
+  if (g->hold) g->hold->release();  // the stuck collective ends with its communicator
   delete c;
+  // the Hold is leaked on purpose: a callback may still be returning from it
   if (--g->live == 0) delete g;
   return 0;
 }
+
+int ncclCommDestroy(void* comm) { return release_comm(comm, "destroy"); }
+
+int ncclCommAbort(void* comm) { return release_comm(comm, "abort"); }
 
 int ncclGroupStart() {
   depth++;
@@ -198,6 +235,16 @@ int ncclGroupEnd() {
     Group* g = ops[0].comm->g;
     std::lock_guard<std::mutex> lk(mu);
     if (g->fail_at && ++g->ends == g->fail_at) {
+      if (g->partial && !g->hold) {
+        // rank 0's collective was launched before the group failed
+        for (auto& o : ops)
+          if (o.comm->rank == 0) {
+            g->hold = new Hold();
+            (void)hipSetDevice(o.comm->dev);
+            if (hipLaunchHostFunc(o.stream, hold_stream, g->hold) != hipSuccess) g->hold->release();
+            log_line(g->log, "partial rank=0 comm=" + std::to_string(g->id));
+          }
+      }
       log_line(g->log, "groupend failed comm=" + std::to_string(g->id));
       return 2;
     }

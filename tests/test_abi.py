@@ -146,11 +146,12 @@ def test_rccl_stub_exports_what_the_library_binds():
     if not os.path.exists(path):
         pytest.skip("librccl_stub.so not built (make -C cometbft_amd/csrc stub)")
     stub = ctypes.CDLL(path)
-    for sym in ("ncclCommInitAll", "ncclCommDestroy", "ncclAllGather", "ncclGroupStart", "ncclGroupEnd"):
+    syms = {"ncclCommInitAll", "ncclCommDestroy", "ncclAllGather", "ncclGroupStart", "ncclGroupEnd", "ncclCommAbort"}
+    for sym in syms:
         assert hasattr(stub, sym), sym
     src = open(os.path.join(ROOT, "cometbft_amd", "csrc", "runtime.cpp")).read()
     bound = set(re.findall(r'dlsym\(h, "(nccl[A-Za-z]+)"\)', src))
-    assert bound == {"ncclCommInitAll", "ncclCommDestroy", "ncclAllGather", "ncclGroupStart", "ncclGroupEnd"}
+    assert bound == syms
     assert stub.ncclCommInitAll(None, 2, None) == 4  # ncclInvalidArgument
     assert stub.ncclGroupEnd() == 5                  # unbalanced: ncclInvalidUsage
     assert stub.ncclGroupStart() == 0 and stub.ncclGroupEnd() == 0

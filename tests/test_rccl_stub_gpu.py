@@ -223,6 +223,53 @@ def test_rccl_gather_failure_falls_back_to_peer_copies(tmp_path, monkeypatch, G)
     ctx.close()
 
 
+def test_rccl_partial_group_failure_reports_erccl(tmp_path, monkeypatch):
+    """the failed group had already enqueued rank 0's collective
+    (the stub holds that stream, as a collective waiting for peers that never
+    come). The library does not queue peer copies behind it: the bounded
+    drain (CMTV_RCCL_DRAIN_MS) times out, the communicators are aborted --
+    which ends the stuck collective -- and the call returns CMTV_ERCCL
+    instead of hanging. The next call gathers by peer copies with exact
+    verdicts, and no communicator is ever built again."""
+    log = tmp_path / "rccl.log"
+    monkeypatch.setenv("CMTV_RCCL_STUB_FAIL_GROUP", "1")
+    monkeypatch.setenv("CMTV_RCCL_STUB_PARTIAL", "1")
+    G = 4
+    ctx = _stub_ctx(G, log, CMTV_RCCL_DRAIN_MS=300)
+    n = 64 * 19 * G + 9
+    pk, kidx, sig, m, off = _batch(n, 3100, flip=0.05)
+    with pytest.raises(RuntimeError):
+        ctx.verify(pk[kidx], sig, m, off, MODE_GO_STDLIB)
+    lines = _log(log)
+    assert any(x.startswith("partial rank=0") for x in lines)
+    assert sum(1 for x in lines if x.startswith("abort")) == G
+    st = ctx.stats()
+    assert st["rccl"] == 0 and st["rccl_failures"] == 1
+    exp = coracle.verify_batch(pk[kidx], sig, m, off, MODE_ZIP215, nthreads=16)
+    assert np.array_equal(ctx.verify(pk[kidx], sig, m, off, MODE_ZIP215), exp)
+    assert len(_inits(_log(log))) == 1 and not _gathers(_log(log))
+    ctx.close()
+
+
+def test_rccl_failure_survives_device_retirement(tmp_path, monkeypatch):
+    """after a gather failed in RCCL, a device retirement
+    (CMTV_FAULT_SYNC_DEV: device 1 fails after the gather) rebuilds nothing:
+    the retried batch and later ones keep using peer copies."""
+    log = tmp_path / "rccl.log"
+    monkeypatch.setenv("CMTV_RCCL_STUB_FAIL_GROUP", "1")
+    G = 4
+    ctx = _stub_ctx(G, log, CMTV_FAULT_SYNC_DEV=1)
+    n = 64 * 23 * G + 1
+    pk, kidx, sig, m, off = _batch(n, 3200, flip=0.05)
+    exp = coracle.verify_batch(pk[kidx], sig, m, off, MODE_GO_STDLIB, nthreads=16)
+    assert np.array_equal(ctx.verify(pk[kidx], sig, m, off, MODE_GO_STDLIB), exp)
+    st = ctx.stats()
+    assert st["device_failures"] == 1 and st["rccl"] == 0 and st["rccl_failures"] == 1
+    assert np.array_equal(ctx.verify(pk[kidx], sig, m, off, MODE_GO_STDLIB), exp)
+    assert len(_inits(_log(log))) == 1 and not _gathers(_log(log))
+    ctx.close()
+
+
 def _assert_dev0_calls_refused(ctx, pk, kidx, sig, m, off):
     """ADVICE r3 (runtime.cpp:1730): device 0 retired -> the single-device
     entry points return CMTV_ENODEV; a key set registered afterwards has no

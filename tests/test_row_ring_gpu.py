@@ -2,8 +2,12 @@
 slots (ADVICE r3 runtime.cpp:549).
 
 Every row launch (k_verify_row{,2,4}_split, k_verify_keyed_row_split) packs
-its bitmap through one slot of a 256-slot per-device ring; the last wave of
-the launch is found with a counter in the slot. Device-resident calls
+its bitmap through one slot of a 256-slot per-device ring: slot word j holds
+the 2-bit verdict fields (01 rejected, 10 accepted) of signatures 32j..32j+31,
+each added by its signature's wave with one atomic, and the wave whose add
+fills the word's last field writes the word's 32 bitmap bits and zeroes it
+(kernels.hip row_bitmap_add). Two launches sharing a slot would add into the
+same fields: two rejects sum to the accept pattern. Device-resident calls
 (cmtv_verify_ed25519_device and friends) are non-blocking on the caller's
 streams, so a caller can have a launch parked behind other work while 256
 later launches wrap the ring back to its slot. runtime.cpp row_slot_acquire
@@ -17,9 +21,10 @@ stream parked on an event then parks its queue-mates too):
   * stream C enqueues 255 row launches (they run at once, other slots);
   * stream B waits for E, then row launch Y takes slot k again.
 X and Y both become runnable when E fires and, 100 signatures each (one CU
-per signature), fit the chip side by side. Unfenced they count each other's
-waves in one counter and write their verdict bytes over each other's;
-fenced, Y starts after X. Oracle: oracle/liboracle.so (the C restatement of
+per signature), fit the chip side by side. Unfenced they add into each
+other's fields and complete each other's words; fenced, Y starts after X.
+Host-API launches that return on the polled bitmap tags are settled by an
+event the next call checks (runtime.cpp settle_polled). Oracle: oracle/liboracle.so (the C restatement of
 Go 1.19 ed25519.Verify, crypto/ed25519/ed25519.go:148)."""
 import os
 

@@ -118,3 +118,23 @@ def test_pubkey_and_batch_mirror(gpu_ctx):
     bv.add(pk[0].tobytes(), msgs[0], sig[0].tobytes()[:10])
     ok, res = bv.verify()
     assert not ok and res == [True, True, True, False]
+
+
+@pytest.mark.parametrize("n", [40000, 40001])
+def test_default_dispatch_at_the_sr25519_crossover(gpu_ctx, n):
+    """the default context on both sides of sr25519's own quad /
+    lane crossover (40,000; Ed25519's is 49,152, so 40,001..49,152 sr25519
+    signatures take the lane kernel while Ed25519 batches of that size stay on
+    the quad kernel), 1% flipped signatures, verdict bytes and bitmap against
+    the C restatement of go-schnorrkel."""
+    rng = np.random.default_rng(n)
+    pk, sig, m, off, _ = _honest(n, n, nkeys=512, msg_len=116)
+    sig = sig.copy()
+    for i in np.nonzero(rng.random(n) < 0.01)[0]:
+        sig[i, rng.integers(0, 64)] ^= 1 << rng.integers(0, 8)
+    exp = coracle.sr25519_verify_batch(pk, sig, m, off, nthreads=16)
+    assert (exp == 0).sum() > n // 200
+    got, words = gpu_ctx.verify_sr25519(pk, sig, m, off, bitmap=True)
+    assert np.array_equal(got, exp), np.nonzero(got != exp)[0][:10]
+    bits = np.unpackbits(words.view(np.uint8), bitorder="little")
+    assert np.array_equal(bits[:n], exp) and not bits[n:].any()

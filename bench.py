@@ -934,6 +934,81 @@ def latency_150(ctx, mode, iters):
     return res
 
 
+def latency_150_under_load(mode, iters, load_heights=1000):
+    """p50 / p99 of a 150-validator VerifyCommit
+    (cmtv_verify_commit, packed once, keyset cache on) while another thread
+    keeps running cmtv_verify_commits over load_heights x 150-validator
+    commits on the SAME context (blocksync / light-client replay beside
+    consensus: consensus/state.go:1661 -> state/execution.go:135 while
+    blockchain/v0/reactor.go:349-400 runs). The bulk call holds the context
+    lock only while it enqueues a chunk, and its kernels run on the device's
+    lowest-priority stream; idle numbers from the same context beside it."""
+    import threading
+
+    from cometbft_amd import Context
+    from cometbft_amd import _native as N
+    from cometbft_amd import testutil as TU
+
+    ctx = Context(device=0)
+    ctx.keyset_cache(4)
+    sv = TU.make_validator_set(ctx, 150)
+    commit, _, _ = TU.make_commit(ctx, sv, height=1000)
+    call, keep = _commit_c_call(ctx, sv, commit, TU.block_id_for_height(1000), 1000, mode)
+    chain = TU.ReplayChain(ctx, sv, 2000, load_heights, flip=0.0)
+    idle = _p50_p99(call, iters, warm=50)
+    stop = threading.Event()
+    passes = [0]
+    t_bulk = []
+
+    def load():
+        while not stop.is_set():
+            t = time.perf_counter()
+            chain.call(ctx, N.VERIFY_COMMIT, mode)
+            t_bulk.append(time.perf_counter() - t)
+            passes[0] += 1
+
+    th = threading.Thread(target=load, daemon=True)
+    th.start()
+    time.sleep(0.2)
+    loaded = _p50_p99(call, iters, warm=20)
+    stop.set()
+    th.join()
+    rcs, _, _ = chain.outcome()
+    del keep
+    ctx.close()
+    return {"idle_p50_ms": idle[0], "idle_p99_ms": idle[1], "p50_ms": loaded[0], "p99_ms": loaded[1],
+            "p99_over_idle_p99": round(loaded[1] / idle[1], 2), "iters": iters,
+            "load": f"cmtv_verify_commits over {load_heights} x 150 commits in a loop on the same context "
+                    f"({passes[0]} passes, median {round(float(np.median(t_bulk)) * 1e3, 2) if t_bulk else None} "
+                    "ms each)", "load_ok": bool(np.all(rcs == 0)),
+            "path": "cmtv_verify_commit (150 validators, keyset cache) from the main thread; the load from a second "
+                    "thread"}
+
+
+def verify_commit_10k_keyset(mode, iters):
+    """configs[1] as a node runs it in steady state --
+    cmtv_verify_commit on the 10,000-validator commit, the validator set's
+    keys registered once by the keyset cache (the first call), p50 / p99."""
+    from cometbft_amd import Context
+    from cometbft_amd import testutil as TU
+
+    ctx = Context(device=0)
+    ctx.keyset_cache(4)
+    sv = TU.make_validator_set(ctx, 10_000)
+    commit, _, _ = TU.make_commit(ctx, sv, height=1000)
+    call, keep = _commit_c_call(ctx, sv, commit, TU.block_id_for_height(1000), 1000, mode)
+    st0 = ctx.stats()
+    p50, p99 = _p50_p99(call, iters, warm=10)
+    st1 = ctx.stats()
+    kms = (st1["device_ms"] - st0["device_ms"]) / max(1, st1["timed_calls"] - st0["timed_calls"])
+    del keep
+    ctx.close()
+    return {"p50_ms": p50, "p99_ms": p99, "kernel_ms": round(kms, 4), "value": round(10_000 / p50 * 1e3, 1),
+            "unit": "verifs/s", "iters": iters,
+            "path": "cmtv_verify_commit with cmtv_keyset_cache: plan + staging + device sign-bytes + keyed kernel "
+                    "+ VerifyCommit replay"}
+
+
 # The PMC summaries of THIS round's tree (tools/gpu_prof_r04.sh: rocprofv3
 # --pmc passes over the quick form of this bench command)
 PMC_SQ = "r04g_pmc_sq.json"
@@ -1144,8 +1219,12 @@ def main():
         if ex["value"]:
             ex["gpu_over_cpu"] = round(value / n_dev / ex["value"], 1)
             ex["gpu_over_cpu_other_mode"] = round(z["value"] / n_dev / ex["value_other_mode"], 1)
+    if not args.no_latency and n_dev == 1:
+        aux("verify_commit_10k_keyset", lambda: verify_commit_10k_keyset(mode, 200))
     if not args.no_latency:
         aux("latency_150", lambda: latency_150(ctx, mode, args.latency_iters))
+        if n_dev == 1:
+            aux("latency_150_under_load", lambda: latency_150_under_load(mode, args.latency_iters))
         if n_dev == 1:
             aux("replay_150", lambda: replay_line(0))
     if not args.no_light and n_dev == 1:

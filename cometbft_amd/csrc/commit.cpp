@@ -621,12 +621,14 @@ int cmtv_verify_commits(cmtv_ctx* ctx, uint32_t kind, uint32_t mode, const char*
     if (rc != CMTV_OK) return rc;
     n_sigs += commits[c].n_sigs;
   }
+  const CommitsArgs args{kind, mode, chain_id, chain_id_len, n, vals, block_ids, heights, commits, trust_num,
+                         trust_den, results, msg_bufs, msg_cap};
+  // large calls: the chunked pipeline (plan / pack / replay on the host
+  // workers, per-device lanes; the context lock only around submissions)
+  if (cmtv::pipeline_wanted(ctx, n_sigs)) return cmtv::verify_commits_pipeline(ctx, args, rcs);
   std::vector<CommitJob> jobs;
   jobs.reserve(n);
-  for (size_t c = 0; c < n; c++)
-    jobs.push_back(CommitJob{kind, chain_id, chain_id_len, &vals[c], block_ids ? &block_ids[c] : nullptr, heights[c],
-                             &commits[c], trust_num, trust_den, &results[c], msg_bufs ? msg_bufs + c * msg_cap : nullptr,
-                             msg_bufs ? msg_cap : 0});
+  for (size_t c = 0; c < n; c++) jobs.push_back(args.job(c));
   // LightTrusting: one address index per distinct (address array, size)
   std::map<std::pair<const uint8_t*, uint32_t>, AddrIndex> addr;
   if (kind == CMTV_VERIFY_COMMIT_LIGHT_TRUSTING)
@@ -639,9 +641,6 @@ int cmtv_verify_commits(cmtv_ctx* ctx, uint32_t kind, uint32_t mode, const char*
       }
       J.addr = &it->second;
     }
-  // large calls: the chunked pipeline (plan / pack / replay on the host
-  // workers, per-device lanes; the context lock only around submissions)
-  if (cmtv::pipeline_wanted(ctx, n_sigs)) return cmtv::verify_commits_pipeline(ctx, jobs.data(), n, mode, rcs);
   thread_local Seen seen;
   std::unique_lock<std::mutex> lk;
   int rc = cmtv::ctx_lock(ctx, lk);

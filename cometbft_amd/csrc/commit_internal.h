@@ -338,11 +338,30 @@ int job_replay(CommitJob& J, const uint32_t* pidx, size_t m, V valid, Seen& seen
 // Two validator sets hold the same keys (one registered key set serves both).
 bool same_keys(const cmtv_valset* a, const cmtv_valset* b);
 
-// The chunked cross-height pipeline (pipeline.cpp): jobs[0..n) whose
-// preambles have NOT run yet; fills rcs[c]. Returns CMTV_OK or a library
-// error. Used by cmtv_verify_commits for large calls without the verdict
-// cache.
-int verify_commits_pipeline(cmtv_ctx* ctx, CommitJob* jobs, size_t n, uint32_t mode, int* rcs);
+// The arguments of one cmtv_verify_commits call (checked by the caller).
+struct CommitsArgs {
+  uint32_t kind, mode;
+  const char* chain_id;
+  size_t chain_id_len, n;
+  const cmtv_valset* vals;
+  const cmtv_block_id* block_ids;  // null for LightTrusting
+  const int64_t* heights;
+  const cmtv_commit* commits;
+  uint64_t trust_num, trust_den;
+  cmtv_commit_result* results;
+  char* msg_bufs;
+  size_t msg_cap;
+  CommitJob job(size_t c) const {
+    return CommitJob{kind, chain_id, chain_id_len, &vals[c], block_ids ? &block_ids[c] : nullptr, heights[c],
+                     &commits[c], trust_num, trust_den, &results[c], msg_bufs ? msg_bufs + c * msg_cap : nullptr,
+                     msg_bufs ? msg_cap : 0};
+  }
+};
+
+// The chunked cross-height pipeline (pipeline.cpp): fills rcs[0..a.n).
+// Returns CMTV_OK or a library error. Used by cmtv_verify_commits for large
+// calls without the verdict cache.
+int verify_commits_pipeline(cmtv_ctx* ctx, const CommitsArgs& a, int* rcs);
 // Whether cmtv_verify_commits takes the pipeline for a call of this many
 // signatures (CMTV_PIPE_MIN).
 bool pipeline_wanted(const cmtv_ctx* ctx, uint64_t n_sigs);

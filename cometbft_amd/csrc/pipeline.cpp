@@ -25,10 +25,13 @@
 // chunks not yet replayed are run again on the others. Verdicts, errors and
 // early exits are exactly the one-batch path's (the same plan and replay
 // code, the same kernels).
+#include <emmintrin.h>
+
 #include <algorithm>
 #include <chrono>
 #include <cstring>
 #include <deque>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <vector>
@@ -57,6 +60,49 @@ struct Chunk {
   BulkLayout L;
 };
 
+// sb_msg_len (signbytes.h) without loops: the varint lengths from the bit
+// width. Same value for every input (tests/host/pipecheck.cpp's fake device
+// checks each message's offsets against sb_msg_len).
+inline uint32_t uvlen(uint64_t v) { return (uint32_t)(64 - __builtin_clzll(v | 1) + 6) / 7; }
+
+struct TplLens {
+  uint32_t pre_commit, pre_nil, post;
+};
+
+inline uint32_t msg_len(const TplLens& t, bool commit_flag, int64_t sec, int32_t nanos) {
+  const uint32_t tl = (sec != 0 ? 1 + uvlen((uint64_t)sec) : 0) + (nanos != 0 ? 1 + uvlen((uint64_t)(int64_t)nanos) : 0);
+  const uint32_t b = (commit_flag ? t.pre_commit : t.pre_nil) + 1 + uvlen(tl) + tl + t.post;
+  return uvlen(b) + b;
+}
+
+// Copy into the pinned staging with non-temporal stores: the staging is
+// written once by the host and read once by the H2D copy, so its lines need
+// not be read for ownership or kept in the cache (the pack is bound by host
+// memory traffic: ~165 B per signature instead of ~250). The writer calls
+// nt_fence before its block's bytes may be read.
+inline void nt_copy(uint8_t* dst, const uint8_t* src, size_t n) {
+  const size_t head = std::min(n, (size_t)((16 - ((uintptr_t)dst & 15)) & 15));
+  std::memcpy(dst, src, head);
+  dst += head;
+  src += head;
+  n -= head;
+  for (; n >= 64; n -= 64, dst += 64, src += 64) {
+    const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src));
+    const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + 16));
+    const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + 32));
+    const __m128i d = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + 48));
+    _mm_stream_si128(reinterpret_cast<__m128i*>(dst), a);
+    _mm_stream_si128(reinterpret_cast<__m128i*>(dst + 16), b);
+    _mm_stream_si128(reinterpret_cast<__m128i*>(dst + 32), c);
+    _mm_stream_si128(reinterpret_cast<__m128i*>(dst + 48), d);
+  }
+  for (; n >= 16; n -= 16, dst += 16, src += 16)
+    _mm_stream_si128(reinterpret_cast<__m128i*>(dst), _mm_loadu_si128(reinterpret_cast<const __m128i*>(src)));
+  std::memcpy(dst, src, n);
+}
+
+inline void nt_fence() { _mm_sfence(); }
+
 // keys of vals are all 32 bytes and packed (what a registered key set needs)
 bool packed_keys(const cmtv_valset* v) {
   if (!v->n_vals) return false;
@@ -66,6 +112,34 @@ bool packed_keys(const cmtv_valset* v) {
 }
 
 }  // namespace
+
+// The pipeline's per-call arrays, kept by the context between calls
+// (runtime_internal.h pipe_workspace).
+struct PipeWorkspace {
+  std::unique_ptr<uint32_t[]> pidx, pval;  // plan: commit / validator index per signature
+  size_t cap_idx = 0, cap_val = 0;
+  std::vector<uint64_t> base, mbytes, sp, mp, tp;
+  std::vector<uint32_t> plen, tlen;
+  // each commit's preamble outcome, kept from the plan to the replay
+  std::vector<int32_t> early;
+  std::vector<int64_t> needed;
+  std::vector<const AddrIndex*> addr;  // LightTrusting
+  bool grow(size_t n, bool with_val) {
+    if (cap_idx < n) {
+      pidx.reset(new (std::nothrow) uint32_t[n]);
+      cap_idx = pidx ? n : 0;
+      if (!pidx) return false;
+    }
+    if (with_val && cap_val < n) {
+      pval.reset(new (std::nothrow) uint32_t[n]);
+      cap_val = pval ? n : 0;
+      if (!pval) return false;
+    }
+    return true;
+  }
+};
+
+void pipe_workspace_free(PipeWorkspace* w) { delete w; }
 
 // The staging layout of one chunk (runtime_internal.h BulkLayout): the
 // pipeline writes it, the bulk lane copies and launches on it.
@@ -92,24 +166,72 @@ bool pipeline_wanted(const cmtv_ctx* ctx, uint64_t n_sigs) {
   return !(v && v[0] == '1');
 }
 
-int verify_commits_pipeline(cmtv_ctx* ctx, CommitJob* jobs, size_t n, uint32_t mode, int* rcs) {
+int verify_commits_pipeline(cmtv_ctx* ctx, const CommitsArgs& args, int* rcs) {
+  const size_t n = args.n;
+  const uint32_t mode = args.mode;
   std::unique_lock<std::mutex> bulk(bulk_mutex(ctx));
   HostPool& pool = host_pool(ctx);
   const PipeConfig pc = pipe_config(ctx);
-  const bool trusting = n && jobs[0].kind == CMTV_VERIFY_COMMIT_LIGHT_TRUSTING;
+  const bool trusting = args.kind == CMTV_VERIFY_COMMIT_LIGHT_TRUSTING;
   uint64_t ph_plan = 0, ph_pack = 0, ph_submit = 0, ph_wait = 0, ph_replay = 0;
   // ---- plan: each commit's preamble and plan, its template and sign-bytes
   // lengths -- window by window, just ahead of the chunk being cut, so the
   // planning of later commits overlaps the device's work on earlier chunks
-  std::vector<uint64_t> base(n + 1, 0);
-  for (size_t c = 0; c < n; c++) base[c + 1] = base[c] + jobs[c].commit->n_sigs;
-  std::unique_ptr<uint32_t[]> pidx(new (std::nothrow) uint32_t[base[n] + 1]);
-  std::unique_ptr<uint32_t[]> pval(trusting ? new (std::nothrow) uint32_t[base[n] + 1] : nullptr);
-  if (!pidx || (trusting && !pval)) return CMTV_ENOMEM;
-  std::vector<uint32_t> plen(n), tlen(n);
-  std::vector<uint64_t> mbytes(n);
+  // per-call arrays live in the context's workspace: reused across calls,
+  // so a pass over 15M signatures does not fault in 100+ MB of fresh pages
+  PipeWorkspace*& wsp = pipe_workspace(ctx);
+  if (!wsp) wsp = new (std::nothrow) PipeWorkspace();
+  if (!wsp) return CMTV_ENOMEM;
+  PipeWorkspace& W = *wsp;
+  std::vector<uint64_t>& base = W.base;
+  base.resize(n + 1);
+  base[0] = 0;
+  for (size_t c = 0; c < n; c++) base[c + 1] = base[c] + args.commits[c].n_sigs;
+  if (!W.grow(base[n] + 1, trusting)) return CMTV_ENOMEM;
+  uint32_t* const pidx_p = W.pidx.get();
+  uint32_t* const pval_p = trusting ? W.pval.get() : nullptr;
+  std::vector<uint32_t>& plen = W.plen;
+  std::vector<uint32_t>& tlen = W.tlen;
+  std::vector<uint64_t>& mbytes = W.mbytes;
+  plen.resize(n);
+  tlen.resize(n);
+  mbytes.resize(n);
+  W.early.resize(n);
+  W.needed.resize(n);
+  // LightTrusting: one address index per distinct (address array, size)
+  std::map<std::pair<const uint8_t*, uint32_t>, AddrIndex> addr_index;
+  if (trusting) {
+    W.addr.resize(n);
+    const AddrIndex* last = nullptr;
+    std::pair<const uint8_t*, uint32_t> last_key{nullptr, 0};
+    for (size_t c = 0; c < n; c++) {
+      const cmtv_valset& v = args.vals[c];
+      const auto key = std::make_pair(v.addrs, v.n_vals);
+      if (!last || key != last_key) {
+        auto it = addr_index.find(key);
+        if (it == addr_index.end()) {
+          it = addr_index.emplace(key, AddrIndex()).first;
+          it->second.build(v.addrs, v.n_vals);
+        }
+        last = &it->second;
+        last_key = key;
+      }
+      W.addr[c] = last;
+    }
+  }
+  // a commit's job, its preamble's outcome restored after the plan
+  auto job = [&](size_t c) {
+    CommitJob J = args.job(c);
+    if (trusting) J.addr = W.addr[c];
+    return J;
+  };
   // chunk-local offsets of each commit's first signature / sign-byte / template byte
-  std::vector<uint64_t> sp(n), mp(n), tp(n);
+  std::vector<uint64_t>& sp = W.sp;
+  std::vector<uint64_t>& mp = W.mp;
+  std::vector<uint64_t>& tp = W.tp;
+  sp.resize(n);
+  mp.resize(n);
+  tp.resize(n);
   size_t planned_upto = 0;
   auto plan_window = [&](uint64_t want_sigs) {
     const uint64_t t0 = now_ns();
@@ -120,22 +242,33 @@ int verify_commits_pipeline(cmtv_ctx* ctx, CommitJob* jobs, size_t n, uint32_t m
     pool.parallel_for(b - a, 64, [&](size_t lo, size_t hi) {
       thread_local Seen seen;
       for (size_t c = a + lo; c < a + hi; c++) {
-        CommitJob& J = jobs[c];
+        CommitJob J = job(c);
         job_preamble(J);
+        W.early[c] = J.early;
+        W.needed[c] = J.needed;
         plen[c] = tlen[c] = 0;
         mbytes[c] = 0;
         if (J.early != 1) continue;
-        uint32_t* pi = pidx.get() + base[c];
-        const size_t m = job_plan(J, pi, trusting ? pval.get() + base[c] : nullptr, seen);
+        uint32_t* pi = pidx_p + base[c];
+        const size_t m = job_plan(J, pi, trusting ? pval_p + base[c] : nullptr, seen);
         plen[c] = (uint32_t)m;
         if (!m) continue;
         SbTemplate tpl;
         tlen[c] = (uint32_t)put_commit_template(nullptr, 0, J.chain_id, J.chain_id_len, J.commit, &tpl);
+        const TplLens tlz{tpl.pre_commit_len, tpl.pre_nil_len, tpl.post_len};
         const cmtv_commit* cm = J.commit;
+        const uint8_t* fl = cm->flags;
+        const int64_t* se = cm->ts_seconds;
+        const int32_t* na = cm->ts_nanos;
         uint64_t mb = 0;
-        for (size_t k = 0; k < m; k++) {
-          const uint32_t idx = pi[k];
-          mb += sb_msg_len(tpl, cm->flags[idx] == kFlagCommit, cm->ts_seconds[idx], cm->ts_nanos[idx]);
+        if (pi[m - 1] - pi[0] == m - 1) {  // a contiguous plan (the common case)
+          const uint32_t a = pi[0];
+          for (size_t k = 0; k < m; k++) mb += msg_len(tlz, fl[a + k] == kFlagCommit, se[a + k], na[a + k]);
+        } else {
+          for (size_t k = 0; k < m; k++) {
+            const uint32_t idx = pi[k];
+            mb += msg_len(tlz, fl[idx] == kFlagCommit, se[idx], na[idx]);
+          }
         }
         mbytes[c] = mb;
       }
@@ -159,6 +292,7 @@ int verify_commits_pipeline(cmtv_ctx* ctx, CommitJob* jobs, size_t n, uint32_t m
   std::vector<const cmtv_keyset*> pinned;
   std::vector<Chunk> chunks;
   uint64_t per = 0;
+  bool ramp = false;
   size_t cursor = 0;  // next commit to put in a chunk
   const cmtv_valset* last_vs = nullptr;
   bool last_packed = false;
@@ -176,16 +310,29 @@ int verify_commits_pipeline(cmtv_ctx* ctx, CommitJob* jobs, size_t n, uint32_t m
       const uint64_t spread = std::min<uint64_t>(2 * live.size(), est / std::max<size_t>(pc.min_sigs, 1));
       nc = std::max(nc, spread);
       per = std::max<uint64_t>(1, (est + nc - 1) / nc);
+      const bool long_call = est / pc.chunk >= 4;
+      // a long call runs chunks of pc.chunk planned signatures at most (the
+      // default, 2^20, is one full round of the batched registered-key lane
+      // kernel: 2,048 waves of 64 lanes x 8 signatures; a chunk just past it
+      // would start a second, nearly empty round), and ramps up: its first
+      // chunks are 1/8, 1/4 and 1/2 of that, so the device starts after a
+      // fraction of a chunk's pack instead of a whole one
+      if (long_call) {
+        ramp = true;
+        per = pc.chunk;
+      }
     }
+    uint64_t want = per;
+    if (ramp && chunks.size() < 3) want = std::max<uint64_t>(per >> (3 - chunks.size()), 1);
     Chunk ch;
     ch.c0 = cursor;
     bool cls_set = false;
     uint64_t s = 0, mb = 0, tb = 0;
     size_t c = cursor;
     for (; c < n; c++) {
-      if (c == planned_upto) plan_window(std::max<uint64_t>(per - std::min(per, s), 65536));
+      if (c == planned_upto) plan_window(std::max<uint64_t>(want - std::min(want, s), 65536));
       if (plen[c] && keyed_mode) {
-        const cmtv_valset* v = jobs[c].vals;
+        const cmtv_valset* v = &args.vals[c];
         if (v != last_vs) {
           last_vs = v;
           last_packed = packed_keys(v);
@@ -197,13 +344,16 @@ int verify_commits_pipeline(cmtv_ctx* ctx, CommitJob* jobs, size_t n, uint32_t m
           cls_set = true;
         }
       }
+      // cut below the target (a commit that would cross it opens the next
+      // chunk), unless the chunk would be empty
+      if (s && s + plen[c] > want) break;
       sp[c] = s;
       mp[c] = mb;
       tp[c] = tb;
       s += plen[c];
       mb += mbytes[c];
       tb += tlen[c];
-      if (s >= per) {
+      if (s >= want) {
         c++;
         break;
       }
@@ -246,17 +396,45 @@ int verify_commits_pipeline(cmtv_ctx* ctx, CommitJob* jobs, size_t n, uint32_t m
       for (size_t c = ch.c0 + b; c < ch.c0 + e; c++) {
         const size_t m = plen[c];
         if (!m) continue;
-        const CommitJob& J = jobs[c];
-        const cmtv_commit* cm = J.commit;
-        const cmtv_valset* vals = J.vals;
+        const cmtv_commit* cm = &args.commits[c];
+        const cmtv_valset* vals = &args.vals[c];
         const uint32_t tl = (uint32_t)(c - ch.c0);
         SbTemplate t;
-        put_commit_template(blob, tp[c], J.chain_id, J.chain_id_len, cm, &t);
+        put_commit_template(blob, tp[c], args.chain_id, args.chain_id_len, cm, &t);
         tmpls[tl] = t;
-        const uint32_t* pi = pidx.get() + base[c];
-        const uint32_t* pv = trusting ? pval.get() + base[c] : pi;
+        const uint32_t* pi = pidx_p + base[c];
+        const uint32_t* pv = trusting ? pval_p + base[c] : pi;
         const size_t i0 = sp[c];
         uint64_t mo = mp[c];
+        const TplLens tlz{t.pre_commit_len, t.pre_nil_len, t.post_len};
+        // the common case, column by column: a contiguous plan whose
+        // validators are the commit's indices and whose signatures are all
+        // 64 bytes, back to back
+        const uint32_t a = pi[0];
+        bool run = !trusting && pi[m - 1] - a == m - 1 && cm->sig_off[a + m] - cm->sig_off[a] == 64 * m;
+        for (size_t k = 0; run && k < m; k++) run = cm->sig_off[a + k + 1] - cm->sig_off[a + k] == 64;
+        if (run) {
+          nt_copy(sg + 64 * i0, cm->sigs + cm->sig_off[a], 64 * m);
+          nt_copy(reinterpret_cast<uint8_t*>(sec + i0), reinterpret_cast<const uint8_t*>(cm->ts_seconds + a), 8 * m);
+          nt_copy(reinterpret_cast<uint8_t*>(nanos + i0), reinterpret_cast<const uint8_t*>(cm->ts_nanos + a), 4 * m);
+          const uint8_t* fl = cm->flags + a;
+          for (size_t k = 0; k < m; k++) flag[i0 + k] = fl[k] == kFlagCommit;
+          for (size_t k = 0; k < m; k++) tidx[i0 + k] = tl;
+          if (L.keyed) {
+            for (size_t k = 0; k < m; k++) kidx[i0 + k] = a + (uint32_t)k;
+          } else if (vals->pk_off[a + m] - vals->pk_off[a] == 32 * m) {
+            std::memcpy(pk + 32 * i0, vals->pubkeys + vals->pk_off[a], 32 * m);  // planned keys are 32 bytes
+          } else {
+            for (size_t k = 0; k < m; k++) std::memcpy(pk + 32 * (i0 + k), vals->pubkeys + vals->pk_off[a + k], 32);
+          }
+          const int64_t* se = cm->ts_seconds + a;
+          const int32_t* na = cm->ts_nanos + a;
+          for (size_t k = 0; k < m; k++) {
+            off[i0 + k] = (uint32_t)mo;
+            mo += msg_len(tlz, fl[k] == kFlagCommit, se[k], na[k]);
+          }
+          continue;
+        }
         for (size_t k = 0; k < m; k++) {
           const size_t i = i0 + k;
           const uint32_t idx = pi[k], vi = pv[k];
@@ -277,9 +455,10 @@ int verify_commits_pipeline(cmtv_ctx* ctx, CommitJob* jobs, size_t n, uint32_t m
           nanos[i] = na;
           tidx[i] = tl;
           off[i] = (uint32_t)mo;
-          mo += sb_msg_len(t, fb, se, na);
+          mo += msg_len(tlz, fb, se, na);
         }
       }
+      nt_fence();  // this block's streaming stores are visible before the H2D reads them
     });
     off[L.m] = (uint32_t)L.msg_bytes;
   };
@@ -288,7 +467,10 @@ int verify_commits_pipeline(cmtv_ctx* ctx, CommitJob* jobs, size_t n, uint32_t m
       thread_local Seen seen;
       for (size_t c = ch.c0 + b; c < ch.c0 + e; c++) {
         const size_t i0 = sp[c];
-        rcs[c] = job_replay(jobs[c], pidx.get() + base[c], plen[c],
+        CommitJob J = job(c);
+        J.early = W.early[c];
+        J.needed = W.needed[c];
+        rcs[c] = job_replay(J, pidx_p + base[c], plen[c],
                             [bm, i0](size_t j) {
                               const size_t i = i0 + j;
                               return ((bm[i >> 6] >> (i & 63)) & 1) != 0;

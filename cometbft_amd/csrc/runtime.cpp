@@ -575,6 +575,7 @@ struct cmtv_ctx {
   bool pipe_on = true;
   // cached key sets evicted while a pipeline call had them pinned
   std::vector<cmtv_keyset*> zombies;
+  cmtv::PipeWorkspace* pipe_ws = nullptr;
 };
 
 struct cmtv_keyset {
@@ -839,10 +840,17 @@ static int enqueue_verify_keyed(cmtv_ctx* ctx, CmtvDev& D, const cmtv_keyset::Pe
   // lane launches: KB signatures per lane sharing one inversion while that
   // still gives two waves per SIMD (k_verify_keyed_batch; ZIP-215 by coset)
   const bool batch = !quad && ctx->keyed_batch;
+  // batched launches of kKeyedBatchChunk = 2^20 signatures: one full round
+  // of 2,048 waves at KB = 8 (equal launches of 1.07M measured 53.9 ms for
+  // configs[2]'s 15M against 37.8 ms: 2,093 waves start a second, nearly
+  // empty round)
   const size_t chunk = batch ? kKeyedBatchChunk : kChunk;
   auto kb_for = [&](size_t cn) -> uint32_t {  // 4 or 8 (the instantiated forms), else 1
+    // the widest KB that still launches keyed_batch_min_waves waves (the last
+    // one may be partial: a commit-aligned 1,048,500-signature chunk takes KB
+    // = 8 in 2,048 waves)
     uint32_t kb = 1;
-    while (kb < 8 && cn >= (size_t)ctx->keyed_batch_min_waves * 64 * (kb * 2)) kb *= 2;
+    while (kb < 8 && cn > ((size_t)ctx->keyed_batch_min_waves - 1) * 64 * (kb * 2)) kb *= 2;
     return batch && kb >= 4 ? kb : 1;
   };
   hipError_t e;
@@ -1774,6 +1782,8 @@ void cmtv_close(cmtv_ctx* ctx) {
     std::fprintf(stderr, "}, \"calls\": %llu}\n", (unsigned long long)ctx->phase_calls);
   }
   ctx->pool.reset();
+  pipe_workspace_free(ctx->pipe_ws);
+  ctx->pipe_ws = nullptr;
   for (auto& e : ctx->keysets) cmtv_keyset_free(e.second);
   ctx->keysets.clear();
   for (auto* z : ctx->zombies) cmtv_keyset_free(z);
@@ -2320,6 +2330,8 @@ bool retire_device_locked(cmtv_ctx* ctx, size_t dev) {
 }
 
 void count_invalid_locked(cmtv_ctx* ctx, uint64_t n) { ctx->stats.invalid += n; }
+
+PipeWorkspace*& pipe_workspace(cmtv_ctx* ctx) { return ctx->pipe_ws; }
 
 }  // namespace cmtv
 

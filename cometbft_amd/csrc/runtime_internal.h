@@ -105,6 +105,11 @@ void bulk_drain(cmtv_ctx* ctx);
 // retires device dev after its HIP error (context lock held); false if it was
 // the last live device
 bool retire_device_locked(cmtv_ctx* ctx, size_t dev);
+// the pipeline's per-call arrays, owned by the context (pipeline.cpp; freed
+// by cmtv_close through pipe_workspace_free); bulk lock held
+struct PipeWorkspace;
+PipeWorkspace*& pipe_workspace(cmtv_ctx* ctx);
+void pipe_workspace_free(PipeWorkspace* w);
 // the context's invalid-verdict counter (context lock held)
 void count_invalid_locked(cmtv_ctx* ctx, uint64_t n);
 // registered key set pins (context lock held): a pinned cached set is not

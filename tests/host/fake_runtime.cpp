@@ -57,6 +57,9 @@ struct cmtv_ctx {
   size_t n_devs = 1;
   std::vector<std::vector<FakeSlot>> slots;  // [dev][slot]
   long fail_dev = -1;                        // bulk_wait on this device fails once
+  bool noverify = false;
+  uint64_t phase_ns[cmtv::kPhCount] = {};
+  cmtv::PipeWorkspace* ws = nullptr;                     // pipebench: every verdict valid, nothing decoded
   uint64_t signatures = 0, invalid = 0, chunks = 0, retired = 0, keyed_chunks = 0;
   std::map<std::string, uint8_t> memo;       // (mode, pk, sig, msg) -> verdict
   std::mutex memo_mu;
@@ -130,7 +133,7 @@ uint32_t ctx_default_mode(const cmtv_ctx*) { return 0; }
 bool cache_enabled(const cmtv_ctx*) { return false; }
 uint64_t phase_now(const cmtv_ctx*) { return 0; }
 void phase_add(cmtv_ctx*, int, uint64_t) {}
-void phase_add_ns(cmtv_ctx*, int, uint64_t) {}
+void phase_add_ns(cmtv_ctx* ctx, int phase, uint64_t ns) { ctx->phase_ns[phase] += ns; }
 bool keyset_cache_enabled(const cmtv_ctx* ctx) { return ctx->keyset_cap != 0; }
 int register_keys_locked(cmtv_ctx*, size_t, const uint8_t*, cmtv_keyset**, uint32_t) { return CMTV_EINVAL; }
 
@@ -195,8 +198,13 @@ int bulk_stage(cmtv_ctx* ctx, size_t dev, int slot, const BulkLayout& L, uint8_t
     return CMTV_EHIP;
   }
   // fresh garbage every time: stale bytes from an earlier chunk must not
-  // mask a field the host forgot to write
-  S.h_in.assign(L.in_bytes, 0xA5);
+  // mask a field the host forgot to write (pipebench: grown only, as pinned
+  // staging is)
+  if (ctx->noverify) {
+    if (S.h_in.size() < L.in_bytes) S.h_in.resize(L.in_bytes);
+  } else {
+    S.h_in.assign(L.in_bytes, 0xA5);
+  }
   *host = S.h_in.data();
   return CMTV_OK;
 }
@@ -225,6 +233,11 @@ int bulk_wait(cmtv_ctx* ctx, size_t dev, int slot, const uint64_t** bitmap) {
   }
   const BulkLayout& L = S.L;
   const uint8_t* h = S.h_in.data();
+  if (ctx->noverify) {
+    S.bm.assign((L.m + 63) / 64 + 1, ~0ull);
+    *bitmap = S.bm.data();
+    return CMTV_OK;
+  }
   std::vector<uint8_t> v(L.m);
   const int rc = device_verify(ctx, L.m, h + L.o_key, L.keyed, S.ks, h + L.o_sig,
                                reinterpret_cast<const uint32_t*>(h + L.o_off),
@@ -266,6 +279,7 @@ bool retire_device_locked(cmtv_ctx* ctx, size_t dev) {
 }
 
 void count_invalid_locked(cmtv_ctx* ctx, uint64_t n) { ctx->invalid += n; }
+PipeWorkspace*& pipe_workspace(cmtv_ctx* ctx) { return ctx->ws; }
 
 }  // namespace cmtv
 
@@ -283,6 +297,12 @@ extern "C" cmtv_ctx* fake_open(size_t n_devs, unsigned threads, size_t pipe_min,
   return c;
 }
 
+extern "C" void fake_phases(cmtv_ctx* c, uint64_t* out) {
+  for (int p = 0; p < cmtv::kPhCount; p++) out[p] = c->phase_ns[p];
+}
+
+extern "C" void fake_set_noverify(cmtv_ctx* c, bool on) { c->noverify = on; }
+
 extern "C" void fake_counts(cmtv_ctx* c, uint64_t* out) {
   out[0] = c->signatures;
   out[1] = c->invalid;
@@ -294,5 +314,6 @@ extern "C" void fake_counts(cmtv_ctx* c, uint64_t* out) {
 extern "C" void fake_close(cmtv_ctx* c) {
   for (auto& e : c->keysets) delete e.second;
   for (auto* k : c->evicted) delete k;
+  cmtv::pipe_workspace_free(c->ws);
   delete c;
 }

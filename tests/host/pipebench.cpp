@@ -1,0 +1,85 @@
+// pipebench.cpp -- host-side cost of the cross-height pipeline (plan, pack,
+// replay) without a device: commit.cpp + pipeline.cpp over
+// tests/host/fake_runtime.cpp with every verdict valid and nothing decoded.
+// configs[2]'s shape: n_heights commits x 150 validators, all signatures
+// present, one validator set (registered keys). Prints ms per call.
+// Usage: pipebench [n_heights] [threads] [kind] [chunk]
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "../../include/cmtverify.h"
+
+extern "C" {
+cmtv_ctx* fake_open(size_t n_devs, unsigned threads, size_t pipe_min, size_t chunk, int slots, bool pipe_on,
+                    size_t keyset_cap, long fail_dev);
+void fake_set_noverify(cmtv_ctx* c, bool on);
+void fake_phases(cmtv_ctx* c, uint64_t* out);
+void fake_close(cmtv_ctx* c);
+}
+
+int main(int argc, char** argv) {
+  const size_t H = argc > 1 ? std::strtoull(argv[1], nullptr, 10) : 100000;
+  const unsigned T = argc > 2 ? (unsigned)std::atoi(argv[2]) : 8;
+  const uint32_t kind = argc > 3 ? (uint32_t)std::atoi(argv[3]) : 0;
+  const size_t chunk = argc > 4 ? std::strtoull(argv[4], nullptr, 10) : (1u << 20);
+  const uint32_t nv = 150;
+  std::vector<uint8_t> pk(32 * nv), addrs(20 * nv + 1);
+  std::vector<uint32_t> pk_off(nv + 1);
+  std::vector<int64_t> power(nv, 10), prio(nv, 0);
+  for (uint32_t i = 0; i < nv; i++) {
+    for (int k = 0; k < 32; k++) pk[32 * i + k] = (uint8_t)(i * 7 + k);
+    std::memcpy(&addrs[20 * i], &pk[32 * i], 20);
+  }
+  for (uint32_t i = 0; i <= nv; i++) pk_off[i] = 32 * i;
+  cmtv_valset vs{nv, pk.data(), pk_off.data(), power.data(), addrs.data(), prio.data()};
+  std::vector<uint8_t> flags(nv + 1, 2), sigs(64 * nv * H), bh(32 * H), ph(32 * H);
+  std::vector<uint32_t> sig_off(nv + 1);
+  for (uint32_t i = 0; i <= nv; i++) sig_off[i] = 64 * i;
+  std::vector<int64_t> secs(nv * H);
+  std::vector<int32_t> nanos(nv);
+  for (uint32_t i = 0; i < nv; i++) nanos[i] = (int32_t)(i * 1000);
+  for (size_t i = 0; i < sigs.size(); i++) sigs[i] = (uint8_t)(i * 131 + (i >> 9));
+  std::vector<cmtv_commit> cs(H);
+  std::vector<cmtv_block_id> bids(H);
+  std::vector<cmtv_valset> vals(H, vs);
+  std::vector<int64_t> hs(H);
+  for (size_t h = 0; h < H; h++) {
+    for (int k = 0; k < 32; k++) {
+      bh[32 * h + k] = (uint8_t)(h + k);
+      ph[32 * h + k] = (uint8_t)(h * 3 + k);
+    }
+    for (uint32_t i = 0; i < nv; i++) secs[nv * h + i] = 1672531200 + (int64_t)h;
+    bids[h] = cmtv_block_id{&bh[32 * h], 32, 1, &ph[32 * h], 32};
+    hs[h] = (int64_t)h + 1;
+    cs[h] = cmtv_commit{(int64_t)h + 1, 0, bids[h], nv, flags.data(), &secs[nv * h], nanos.data(),
+                        &sigs[64 * nv * h], sig_off.data(), addrs.data()};
+  }
+  std::vector<cmtv_commit_result> res(H);
+  std::vector<int> rcs(H);
+  cmtv_ctx* ctx = fake_open(1, T, 1, chunk, 3, true, 4, -1);
+  fake_set_noverify(ctx, true);
+  const char chain[] = "cmtverify-bench";
+  double best = 1e30;
+  for (int it = 0; it < 6; it++) {
+    const auto t0 = std::chrono::steady_clock::now();
+    const int rc = cmtv_verify_commits(ctx, kind, 0, chain, sizeof chain - 1, H, vals.data(), bids.data(), hs.data(),
+                                       cs.data(), 1, 3, res.data(), rcs.data(), nullptr, 0);
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (rc != CMTV_OK || rcs[0] != 0) {
+      std::fprintf(stderr, "rc %d rcs[0] %d\n", rc, rcs[0]);
+      return 1;
+    }
+    if (it) best = ms < best ? ms : best;
+  }
+  std::printf("%zu heights x %u, kind %u, %u threads: %.2f ms per call (%.1f ns per signature of wall)\n", H, nv, kind,
+              T, best, best * 1e6 / (double)(H * nv));
+  uint64_t pt[16] = {};
+  fake_phases(ctx, pt);
+  std::printf("  per call ms: plan %.2f pack %.2f submit %.2f wait %.2f replay %.2f\n", pt[6] / 6e6, pt[7] / 6e6,
+              pt[8] / 6e6, pt[9] / 6e6, pt[10] / 6e6);
+  fake_close(ctx);
+  return 0;
+}

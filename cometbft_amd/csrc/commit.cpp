@@ -138,7 +138,12 @@ struct SigBatch {
   const cmtv_valset* last_vs = nullptr;
   bool one_vs = true;
 
-  size_t size() const { return off.size() - 1; }
+  // the one-pass form of a single commit (job_prepare_fast): u32 offsets
+  // written directly, keys checked packed
+  bool fast = false, keys_packed = false;
+  std::vector<uint32_t> off32;
+
+  size_t size() const { return fast ? off32.size() - 1 : off.size() - 1; }
   const uint8_t* pk_data() const { return pk_src ? pk_src : pk.data(); }
   const uint8_t* sg_data() const { return sg_src ? sg_src : sg.data(); }
   const int64_t* sec_data() const { return sec_src ? sec_src : tsec.data(); }
@@ -223,6 +228,82 @@ bool templated_enabled() {
   return on;
 }
 
+// A single commit whose plan is a prefix of its signatures (VerifyCommit: no
+// absent or unknown flags; VerifyCommitLight: no nil votes before the
+// threshold) with keys packed at 32 bytes and signatures at 64: one pass
+// plans it and writes the per-signature flag, key index and u32 message
+// offset (the caller's key, signature and timestamp arrays are the batch).
+// False (B left empty) sends it down the general path.
+bool job_prepare_fast(CommitJob& J, SigBatch& B) {
+  const cmtv_valset* vals = J.vals;
+  const cmtv_commit* c = J.commit;
+  const uint32_t n = c->n_sigs;
+  const bool full = J.kind == CMTV_VERIFY_COMMIT;
+  if (J.kind == CMTV_VERIFY_COMMIT_LIGHT_TRUSTING || !B.templated || B.size() != 0 || n == 0 || n != vals->n_vals)
+    return false;
+  if (vals->pk_off[0] != 0 || c->sig_off[0] != 0) return false;
+  SbTemplate t{};
+  const size_t tb = put_commit_template(nullptr, 0, J.chain_id, J.chain_id_len, c, &t);
+  const TplLens tl{t.pre_commit_len, t.pre_nil_len, t.post_len};
+  B.tflag.resize(n);
+  B.off32.resize(n + 1);
+  uint8_t* tf = B.tflag.data();
+  uint32_t* of = B.off32.data();
+  const uint8_t* fl = c->flags;
+  const uint32_t* po = vals->pk_off;
+  const uint32_t* so = c->sig_off;
+  const int64_t* se = c->ts_seconds;
+  const int32_t* na = c->ts_nanos;
+  const int64_t* vp = vals->voting_power;
+  uint64_t o = 0;
+  int64_t tally = 0;
+  uint32_t m = 0;
+  auto bail = [&] {  // leave B as it was
+    B.tflag.clear();
+    B.off32.clear();
+    return false;
+  };
+  for (uint32_t i = 0; i < n; i++) {
+    const uint8_t f = fl[i];
+    const bool fb = f == kFlagCommit;
+    if (!(fb || (full && f == kFlagNil))) return bail();
+    if (po[i + 1] != 32 * (i + 1) || so[i + 1] != 64 * (i + 1)) return bail();
+    tf[i] = fb ? 1 : 0;
+    of[i] = (uint32_t)o;
+    o += msg_len(tl, fb, se[i], na[i]);
+    m = i + 1;
+    if (full) {
+      if (fb) tally += vp[i];
+    } else {
+      tally += vp[i];
+      if (tally > J.needed) break;
+    }
+  }
+  if (o + 16 >= (1ull << 31)) return bail();
+  of[m] = (uint32_t)o;
+  B.tflag.resize(m);
+  B.off32.resize(m + 1);
+  B.fast = true;
+  B.keys_packed = full;  // every key checked (a light plan stops early)
+  // no key index or template index arrays: signature i is by validator i
+  // and every one uses template 0 (null key_idx / tidx downstream)
+  B.tmpls.assign(1, t);
+  B.blob.resize(tb);
+  put_commit_template(B.blob.data(), 0, J.chain_id, J.chain_id_len, c, &B.tmpls[0]);
+  B.cur = c;
+  B.pk_src = vals->pubkeys;
+  B.sg_src = c->sigs;
+  B.sec_src = c->ts_seconds;
+  B.nanos_src = c->ts_nanos;
+  B.all_len_ok = true;
+  B.vs = B.last_vs = vals;
+  B.one_vs = true;
+  J.plan_prefix = m;
+  J.prefix_tally = tally;
+  J.first = 0;
+  return true;
+}
+
 // The common VerifyCommit case (validator_set.go:685-707): the plan is every
 // signature in index order, from validators whose keys are packed at 32 bytes,
 // and every signature is 64 bytes. Then the caller's key, signature and
@@ -248,17 +329,24 @@ bool job_prepare_identity(CommitJob& J, SigBatch& B, bool prefetch) {
   B.one_vs = true;
   B.ensure_template(J.chain_id, J.chain_id_len, c);
   const cmtv::SbTemplate& t = B.tmpls.back();
+  const TplLens tl{t.pre_commit_len, t.pre_nil_len, t.post_len};
   B.tflag.resize(m);
   B.tidx.assign(m, (uint32_t)B.tmpls.size() - 1);
   B.off.resize(m + 1);
   B.kidx.resize(m);
   uint64_t o = 0;
+  const uint8_t* fl = c->flags;
+  const int64_t* se = c->ts_seconds;
+  const int32_t* na = c->ts_nanos;
+  uint8_t* tf = B.tflag.data();
+  uint32_t* ki = B.kidx.data();
+  uint64_t* of = B.off.data();
   for (size_t i = 0; i < m; i++) {
-    const bool for_block = c->flags[i] == kFlagCommit;
-    B.tflag[i] = for_block ? 1 : 0;
-    B.kidx[i] = (uint32_t)i;
-    o += cmtv::sb_msg_len(t, for_block, c->ts_seconds[i], c->ts_nanos[i]);
-    B.off[i + 1] = o;
+    const bool for_block = fl[i] == kFlagCommit;
+    tf[i] = for_block ? 1 : 0;
+    ki[i] = (uint32_t)i;
+    o += msg_len(tl, for_block, se[i], na[i]);
+    of[i + 1] = o;
   }
   return true;
 }
@@ -395,20 +483,21 @@ void job_prepare(CommitJob& J, SigBatch& B, bool prefetch, bool only_job, Seen& 
     J.first = B.size();
     return;
   }
+  if (only_job && !prefetch && job_prepare_fast(J, B)) return;
   const uint32_t nsig = commit->n_sigs;
   J.plan_idx.resize(nsig);
   if (J.kind == CMTV_VERIFY_COMMIT_LIGHT_TRUSTING) J.plan_val.resize(nsig);
   const size_t m = job_plan(J, J.plan_idx.data(), J.kind == CMTV_VERIFY_COMMIT_LIGHT_TRUSTING ? J.plan_val.data()
                                                                                               : nullptr, seen);
   J.plan_idx.resize(m);
-  if (J.kind != CMTV_VERIFY_COMMIT_LIGHT_TRUSTING) J.plan_val = J.plan_idx;
-  J.plan_val.resize(m);
+  const bool trusting = J.kind == CMTV_VERIFY_COMMIT_LIGHT_TRUSTING;
+  if (trusting) J.plan_val.resize(m);  // else the validator index is the commit index
   J.first = B.size();
   // borrowing the caller's arrays: only when no other job adds to the batch
   if (only_job && job_prepare_identity(J, B, prefetch)) return;
   B.reserve_more(J.plan_idx.size());
   for (size_t j = 0; j < J.plan_idx.size(); j++) {
-    const uint32_t idx = J.plan_idx[j], vi = J.plan_val[j];
+    const uint32_t idx = J.plan_idx[j], vi = trusting ? J.plan_val[j] : idx;
     const uint32_t s0 = commit->sig_off[idx], s1 = commit->sig_off[idx + 1];
     B.add(vals, vi, commit->sigs + s0, s1 - s0, J.chain_id, J.chain_id_len, commit, idx);
   }
@@ -444,9 +533,14 @@ int batch_verify(cmtv_ctx* ctx, SigBatch& B, uint32_t mode, std::vector<uint8_t>
   const cmtv_keyset* ks = nullptr;
   if (B.templated && cmtv::keyset_cache_enabled(ctx) && B.one_vs && B.vs->n_vals) {
     bool packed = true;
-    for (uint32_t i = 0; i <= B.vs->n_vals && packed; i++) packed = B.vs->pk_off[i] == 32 * i;
+    if (!B.keys_packed)
+      for (uint32_t i = 0; i <= B.vs->n_vals && packed; i++) packed = B.vs->pk_off[i] == 32 * i;
     if (packed) ks = cmtv::keyset_for_locked(ctx, B.vs->pubkeys, B.vs->n_vals);
   }
+  if (B.fast)  // one device batch, offsets already 32-bit (job_prepare_fast)
+    return cmtv::verify_templated_locked(ctx, m, ks ? nullptr : B.pk_data(), B.sg_data(), B.off32.data(),
+                                         B.tmpls.data(), 1, B.blob.data(), B.blob.size(), nullptr, B.tflag.data(),
+                                         B.sec_data(), B.nanos_data(), mode, valid.data(), ks, nullptr);
   if (!B.templated && B.msgs.empty()) B.msgs.push_back(0);
   std::vector<uint32_t> off32;
   const uint64_t kMaxBatchMsgBytes = max_batch_msg_bytes();
@@ -478,6 +572,16 @@ int batch_verify(cmtv_ctx* ctx, SigBatch& B, uint32_t mode, std::vector<uint8_t>
 // job_replay over a batch's verdict bytes
 int job_replay_batch(CommitJob& J, const std::vector<uint8_t>& all_valid, Seen& seen) {
   const uint8_t* v = all_valid.data() + J.first;
+  if (J.plan_prefix) {
+    // job_prepare_fast checked every flag, key and signature length of the
+    // prefix: the loop's outcome is the first invalid verdict, else the
+    // tally (job_replay gives the same, one signature at a time)
+    if (J.early != 1) return J.early;
+    J.res->n_verified = (uint32_t)J.plan_prefix;
+    if (const void* z = std::memchr(v, 0, J.plan_prefix))
+      return fail_wrong_sig(J, (uint32_t)(static_cast<const uint8_t*>(z) - v));
+    return J.prefix_tally > J.needed ? CMTV_OK : fail_not_enough(J, J.prefix_tally);
+  }
   return job_replay(J, J.plan_idx.data(), J.plan_idx.size(), [v](size_t j) { return v[j] != 0; }, seen);
 }
 
@@ -594,6 +698,13 @@ int cmtv_verify_commit(cmtv_ctx* ctx, uint32_t kind, uint32_t mode, const char* 
   SigBatch B;
   const bool cache = cmtv::cache_enabled(ctx);
   B.templated = !cache && templated_enabled();
+  // registered keys, signatures back to back: their copy to the device can
+  // start now and overlap the plan (used only if the fast form takes them)
+  if (B.templated && cmtv::keyset_cache_enabled(ctx) && kind != CMTV_VERIFY_COMMIT_LIGHT_TRUSTING && commit->n_sigs &&
+      commit->sig_off[0] == 0 && commit->sig_off[commit->n_sigs] == 64ull * commit->n_sigs) {
+    rc = cmtv::stage_sigs_early_locked(ctx, commit->sigs, commit->n_sigs);
+    if (rc != CMTV_OK) return rc;
+  }
   job_prepare(J, B, cache, true, seen);
   cmtv::phase_add(ctx, cmtv::kPhPrepare, t0);
   std::vector<uint8_t> valid;

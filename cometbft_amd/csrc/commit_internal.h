@@ -120,6 +120,31 @@ inline size_t put_commit_template(uint8_t* blob, size_t at, const char* chain_id
   return w.n;
 }
 
+// sb_msg_len (signbytes.h) without loops: varint lengths from the bit width
+// by table. Same value for every input (tests/host/pipecheck.cpp's fake
+// device checks each message's offsets against sb_msg_len).
+struct UvlenTable {
+  uint8_t len[65];
+  constexpr UvlenTable() : len() {
+    for (int b = 0; b <= 64; b++) len[b] = (uint8_t)(b <= 7 ? 1 : (b + 6) / 7);
+  }
+};
+inline uint32_t uvlen(uint64_t v) {
+  static constexpr UvlenTable t;
+  return t.len[64 - __builtin_clzll(v | 1)];
+}
+
+struct TplLens {
+  uint32_t pre_commit, pre_nil, post;
+};
+
+inline uint32_t msg_len(const TplLens& t, bool commit_flag, int64_t sec, int32_t nanos) {
+  // the timestamp is at most 22 bytes, so its length varint is one byte
+  const uint32_t tl = (sec != 0 ? 1 + uvlen((uint64_t)sec) : 0) + (nanos != 0 ? 1 + uvlen((uint64_t)(int64_t)nanos) : 0);
+  const uint32_t b = (commit_flag ? t.pre_commit : t.pre_nil) + 2 + tl + t.post;
+  return uvlen(b) + b;
+}
+
 // ------------------------------------------------------------------ formatting
 
 inline std::string hex_upper(const uint8_t* p, size_t n) {
@@ -233,6 +258,8 @@ struct CommitJob {
   const AddrIndex* addr = nullptr;  // LightTrusting: index of vals' addresses
   std::vector<uint32_t> plan_idx, plan_val;
   size_t first = 0;  // batch index of plan item 0
+  size_t plan_prefix = 0;  // > 0: the plan is signatures [0, plan_prefix) (plan_idx unused)
+  int64_t prefix_tally = 0;  // ... and the tally the loop reaches over it when every verdict is valid
 
   int fail(int32_t code, int32_t idx, const std::string& m) {
     res->code = code;
@@ -241,6 +268,23 @@ struct CommitJob {
     return CMTV_ECOMMIT;
   }
 };
+
+// "wrong signature (#%d): %X" (validator_set.go:697, 753, 814)
+inline int fail_wrong_sig(CommitJob& J, uint32_t idx) {
+  const uint32_t s0 = J.commit->sig_off[idx], s1 = J.commit->sig_off[idx + 1];
+  return J.fail(CMTV_COMMIT_ERR_WRONG_SIGNATURE, (int32_t)idx,
+                "wrong signature (#" + std::to_string(idx) + "): " + hex_upper(J.commit->sigs + s0, s1 - s0));
+}
+
+// ErrNotEnoughVotingPowerSigned (validator_set.go:856-863)
+inline int fail_not_enough(CommitJob& J, int64_t tally) {
+  J.res->got = tally;
+  J.res->needed = J.needed;
+  char b[160];
+  std::snprintf(b, sizeof b, "invalid commit -- insufficient voting power: got %" PRId64 ", needed more than %" PRId64,
+                tally, J.needed);
+  return J.fail(CMTV_COMMIT_ERR_NOT_ENOUGH_POWER, -1, b);
+}
 
 // Argument checks of one commit (CMTV_EINVAL on null arrays).
 int job_check_args(uint32_t kind, const char* chain_id, size_t chain_id_len, const cmtv_valset* vals,
@@ -256,7 +300,8 @@ void job_preamble(CommitJob& J);
 size_t job_plan(const CommitJob& J, uint32_t* pidx, uint32_t* pval, Seen& seen);
 
 // The reference loop (validator_set.go:685-713, 740-764, 793-825) over the
-// verdicts of the m planned signatures pidx[0..m): valid(j) is plan item j's
+// verdicts of the m planned signatures pidx[0..m) (pidx null: the plan is
+// the commit's first m signatures): valid(j) is plan item j's
 // device verdict; a signature whose length is not 64 is invalid whatever the
 // device said, and fails before its key's length is looked at
 // (crypto/ed25519/ed25519.go:150).
@@ -271,11 +316,7 @@ int job_replay(CommitJob& J, const uint32_t* pidx, size_t m, V valid, Seen& seen
   // for a signature that is not 64 bytes BEFORE Go's ed25519.Verify can panic
   // on a key that is not 32 bytes
   auto sig64 = [&](uint32_t idx) { return commit->sig_off[idx + 1] - commit->sig_off[idx] == 64; };
-  auto wrong_sig = [&](uint32_t idx) {
-    const uint32_t s0 = commit->sig_off[idx], s1 = commit->sig_off[idx + 1];
-    return J.fail(CMTV_COMMIT_ERR_WRONG_SIGNATURE, (int32_t)idx,
-                  "wrong signature (#" + std::to_string(idx) + "): " + hex_upper(commit->sigs + s0, s1 - s0));
-  };
+  auto wrong_sig = [&](uint32_t idx) { return fail_wrong_sig(J, idx); };
   auto bad_pk = [&](uint32_t idx, uint32_t vi) {
     return J.fail(CMTV_COMMIT_PANIC_BAD_PUBKEY, (int32_t)idx,
                   "ed25519: bad public key length: " + std::to_string(vals->pk_off[vi + 1] - vals->pk_off[vi]));
@@ -291,7 +332,7 @@ int job_replay(CommitJob& J, const uint32_t* pidx, size_t m, V valid, Seen& seen
         return J.fail(CMTV_COMMIT_PANIC_UNKNOWN_FLAG, (int32_t)idx, "Unknown BlockIDFlag: " + std::to_string(flag));
       if (!sig64(idx)) return wrong_sig(idx);
       if (vals->pk_off[idx + 1] - vals->pk_off[idx] != 32) return bad_pk(idx, idx);
-      if (j >= m || pidx[j] != idx || !valid(j)) return wrong_sig(idx);
+      if (j >= m || (pidx ? pidx[j] : (uint32_t)j) != idx || !valid(j)) return wrong_sig(idx);
       j++;
       if (flag == kFlagCommit) tally += vals->voting_power[idx];
     } else {
@@ -320,19 +361,14 @@ int job_replay(CommitJob& J, const uint32_t* pidx, size_t m, V valid, Seen& seen
       }
       if (!sig64(idx)) return wrong_sig(idx);
       if (vals->pk_off[vi + 1] - vals->pk_off[vi] != 32) return bad_pk(idx, vi);
-      if (j >= m || pidx[j] != idx || !valid(j)) return wrong_sig(idx);
+      if (j >= m || (pidx ? pidx[j] : (uint32_t)j) != idx || !valid(j)) return wrong_sig(idx);
       j++;
       tally += vals->voting_power[vi];
       if (tally > J.needed) return CMTV_OK;
     }
   }
   if (J.kind == CMTV_VERIFY_COMMIT && tally > J.needed) return CMTV_OK;
-  J.res->got = tally;
-  J.res->needed = J.needed;
-  char b[160];
-  std::snprintf(b, sizeof b, "invalid commit -- insufficient voting power: got %" PRId64 ", needed more than %" PRId64,
-                tally, J.needed);
-  return J.fail(CMTV_COMMIT_ERR_NOT_ENOUGH_POWER, -1, b);
+  return fail_not_enough(J, tally);
 }
 
 // Two validator sets hold the same keys (one registered key set serves both).

@@ -86,9 +86,12 @@ hipError_t launch_verify_keyed(uint32_t mode, uint32_t n, uint32_t n_keys, const
                                const uint32_t* ktabs, const uint32_t* bcomb, void* valid, void* bitmap,
                                bool quad, bool split, uint32_t k_wait, uint32_t* diag, uint32_t batch_kb,
                                uint32_t* scr, const uint32_t* wtabs, const uint32_t* btab, bool wide_dma,
-                               hipStream_t s, const RowSlot* row_slot = nullptr, bool mixed = true);
+                               hipStream_t s, const RowSlot* row_slot = nullptr, bool mixed = true,
+                               const SbFuse* sb = nullptr);
 // (row_slot set: the keyed row kernel, k_verify_keyed_row_split, one
-// signature per workgroup; a slot of the device's bitmap ring)
+// signature per workgroup; a slot of the device's bitmap ring). sb (may be
+// null) is honoured by the keyed row and keyed quad split forms only (their
+// helper waves hash; hipErrorInvalidValue otherwise), as by launch_verify.
 // the one-signature-per-lane part of launch_verify_keyed (keyed_lane.hip):
 // over the wide combs wtabs (rows staged by LDS-DMA when dma) or, with wtabs
 // null, the radix-256 key combs ktabs with B over btab's radix-2^16 comb

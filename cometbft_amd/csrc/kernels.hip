@@ -183,7 +183,8 @@ __device__ __forceinline__ void helper_message(const SbFuse& sb, uint32_t i, con
                                                uint32_t* slot, const uint8_t*& mp, uint32_t& ml) {
   if (sb.tmpls) {
     LdsBytes out{reinterpret_cast<uint8_t*>(slot)};
-    const SbTemplate tp = static_cast<const SbTemplate*>(sb.tmpls)[sb.tidx[i]];
+    // tidx null: one template for the whole batch (a single commit)
+    const SbTemplate tp = static_cast<const SbTemplate*>(sb.tmpls)[sb.tidx ? sb.tidx[i] : 0u];
     ml = sb_write(out, tp, sb.blob, sb.flag[i] != 0, sb.sec[i], sb.nanos[i]);
     mp = reinterpret_cast<const uint8_t*>(slot);
   } else {
@@ -889,23 +890,26 @@ __global__ __launch_bounds__(256, 1) void k_verify_keyed_row_split(
     uint32_t n, uint32_t n_keys, const uint32_t* __restrict__ key_idx, const uint32_t* __restrict__ sig,
     const uint8_t* __restrict__ msg, const uint32_t* __restrict__ off, const uint32_t* __restrict__ keys_pk,
     const uint8_t* __restrict__ keys_ok, const uint32_t* __restrict__ ktabs, const uint32_t* __restrict__ btab,
-    uint8_t* __restrict__ out_valid, uint64_t* __restrict__ out_bitmap, RowSlot slot) {
+    uint8_t* __restrict__ out_valid, uint64_t* __restrict__ out_bitmap, RowSlot slot, SbFuse sb) {
   const uint32_t wave = threadIdx.x >> 6, t = threadIdx.x & 63;
   const uint32_t s = blockIdx.x;
   const uint32_t i = s < n ? s : n - 1;
   __shared__ uint32_t tks[8];
+  __shared__ uint32_t sbm[kSbFuseMaxMsg / 4];  // fused sign-bytes (every helper lane writes the same bytes)
   __shared__ uint32_t xa[64], xb[64];
   __shared__ uint32_t arows[COMB_WINDOWS * COMB_ROW_WORDS];  // the 32 key-comb rows of k's digits
   __shared__ uint32_t brows[16 * BTAB_ROW_WORDS];            // the 16 B-comb rows of s's digits
-  uint32_t kid = key_idx[i];
+  uint32_t kid = key_idx ? key_idx[i] : i;  // null: signature i is by key i (one commit)
   const bool kin = kid < n_keys;
   kid = kin ? kid : 0;
   const uint32_t* sgp = sig + 16 * (size_t)i;
   CMTV_STAMP(0);
   if (wave == 3) {
-    const uint32_t m0 = off[i], m1 = off[i + 1];
+    const uint8_t* mp;
+    uint32_t ml;
+    helper_message(sb, i, msg, off, sbm, mp, ml);
     uint32_t tk[8];
-    q_keyed_challenge(tk, keys_pk + 8 * (size_t)kid, sgp, msg + m0, m1 - m0);
+    q_keyed_challenge(tk, keys_pk + 8 * (size_t)kid, sgp, mp, ml);
     if (t == 0)
 #pragma unroll
       for (int j = 0; j < 8; j++) tks[j] = tk[j];
@@ -1242,10 +1246,11 @@ __global__ __launch_bounds__(320, 1) void k_verify_keyed_quad_split(
     const uint8_t* __restrict__ msg, const uint32_t* __restrict__ off, const uint32_t* __restrict__ keys_pk,
     const uint8_t* __restrict__ keys_ok, const uint32_t* __restrict__ ktabs, const uint32_t* __restrict__ bcomb,
     uint8_t* __restrict__ out_valid, uint64_t* __restrict__ out_bitmap, uint32_t k_wait, uint32_t* __restrict__ diag,
-    const uint32_t* __restrict__ btab) {
+    const uint32_t* __restrict__ btab, SbFuse sb) {
   const uint32_t wave = threadIdx.x >> 6, t = threadIdx.x & 63;
   const uint32_t base = blockIdx.x * 48;
   __shared__ uint32_t tks[48][9];
+  __shared__ uint32_t sbm[48][kSbFuseMaxMsg / 4];  // fused sign-bytes
   __shared__ uint32_t rpt[48][31];  // R: x, y, t (10 words each), decode flag
   __shared__ uint32_t k_ready;
   if (threadIdx.x == 0) k_ready = 0u;
@@ -1256,11 +1261,13 @@ __global__ __launch_bounds__(320, 1) void k_verify_keyed_quad_split(
     if (wave == 4) {
       // hash helper: k for all 48 signatures, published through k_ready so
       // the decode helper never waits on it
-      const uint32_t m0 = off[i], m1 = off[i + 1];
-      uint32_t kid = key_idx[i];
+      const uint8_t* mp;
+      uint32_t ml;
+      helper_message(sb, i, msg, off, sbm[t < 48 ? t : 47], mp, ml);
+      uint32_t kid = key_idx ? key_idx[i] : i;
       kid = kid < n_keys ? kid : 0;
       uint32_t tk[8];
-      q_keyed_challenge(tk, keys_pk + 8 * (size_t)kid, sig + 16 * (size_t)i, msg + m0, m1 - m0);
+      q_keyed_challenge(tk, keys_pk + 8 * (size_t)kid, sig + 16 * (size_t)i, mp, ml);
       if (t < 48)
 #pragma unroll
         for (int j = 0; j < 8; j++) tks[t][j] = tk[j];
@@ -1288,7 +1295,7 @@ __global__ __launch_bounds__(320, 1) void k_verify_keyed_quad_split(
   const uint32_t s = base + ls;
   const bool active = s < n;
   const uint32_t i = active ? s : n - 1;
-  uint32_t kid = key_idx[i];
+  uint32_t kid = key_idx ? key_idx[i] : i;  // null: signature i is by key i (one commit)
   const bool kin = kid < n_keys;
   kid = kin ? kid : 0;
   DevQuad q;
@@ -1306,9 +1313,13 @@ __global__ __launch_bounds__(320, 1) void k_verify_keyed_quad_split(
         }
         if (__builtin_expect(__ballot(ready) != __ballot(1), 0)) {
           // the helper's k did not arrive in time: hash this signature here
-          // (identical k), so the wait bounds only the time, never the verdict
-          const uint32_t m0 = off[i], m1 = off[i + 1];
-          q_keyed_challenge(tk, keys_pk + 8 * (size_t)kid, sig + 16 * (size_t)i, msg + m0, m1 - m0);
+          // (identical k), so the wait bounds only the time, never the verdict;
+          // fused sign-bytes are written again into the signature's slot (the
+          // helper may be writing the same bytes there)
+          const uint8_t* mp;
+          uint32_t ml;
+          helper_message(sb, i, msg, off, sbm[ls], mp, ml);
+          q_keyed_challenge(tk, keys_pk + 8 * (size_t)kid, sig + 16 * (size_t)i, mp, ml);
           if (t == 0) atomicAdd(diag + kDiagLateK, 1u);
         } else {
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -1341,8 +1352,11 @@ hipError_t launch_verify_keyed(uint32_t mode, uint32_t n, uint32_t n_keys, const
                                const uint32_t* ktabs, const uint32_t* bcomb, void* valid, void* bitmap,
                                bool quad, bool split, uint32_t k_wait, uint32_t* diag, uint32_t batch_kb,
                                uint32_t* scr, const uint32_t* wtabs, const uint32_t* btab, bool wide_dma,
-                               hipStream_t s, const RowSlot* row_slot, bool mixed) {
+                               hipStream_t s, const RowSlot* row_slot, bool mixed, const SbFuse* sbp) {
   if (n == 0) return hipSuccess;
+  const SbFuse sb = sbp ? *sbp : SbFuse{};
+  // fused sign-bytes only in the forms whose helper wave hashes (row, quad split)
+  if (sb.tmpls && !row_slot && !(quad && split)) return hipErrorInvalidValue;
   auto ki = static_cast<const uint32_t*>(key_idx);
   auto sgp = static_cast<const uint32_t*>(sig);
   auto mp = static_cast<const uint8_t*>(msg);
@@ -1354,10 +1368,10 @@ hipError_t launch_verify_keyed(uint32_t mode, uint32_t n, uint32_t n_keys, const
     if (n > kRowMaxCap) return hipErrorInvalidValue;
     if (mode == MODE_ZIP215)
       hipLaunchKernelGGL(k_verify_keyed_row_split<MODE_ZIP215>, dim3(n), dim3(256), 0, s, n, n_keys, ki, sgp, mp, op,
-                         keys_pk, keys_ok, ktabs, btab, vp, bp, *row_slot);
+                         keys_pk, keys_ok, ktabs, btab, vp, bp, *row_slot, sb);
     else
       hipLaunchKernelGGL(k_verify_keyed_row_split<MODE_GO_STDLIB>, dim3(n), dim3(256), 0, s, n, n_keys, ki, sgp, mp,
-                         op, keys_pk, keys_ok, ktabs, btab, vp, bp, *row_slot);
+                         op, keys_pk, keys_ok, ktabs, btab, vp, bp, *row_slot, sb);
     return hipGetLastError();
   }
   if (quad && split) {
@@ -1368,16 +1382,16 @@ hipError_t launch_verify_keyed(uint32_t mode, uint32_t n, uint32_t n_keys, const
     if (mixed && btab) {
       if (mode == MODE_ZIP215)
         hipLaunchKernelGGL((k_verify_keyed_quad_split<MODE_ZIP215, true>), grid, block, 0, s, n, n_keys, ki, sgp, mp,
-                           op, keys_pk, keys_ok, ktabs, bcomb, vp, bp, k_wait, diag, btab);
+                           op, keys_pk, keys_ok, ktabs, bcomb, vp, bp, k_wait, diag, btab, sb);
       else
         hipLaunchKernelGGL((k_verify_keyed_quad_split<MODE_GO_STDLIB, true>), grid, block, 0, s, n, n_keys, ki, sgp,
-                           mp, op, keys_pk, keys_ok, ktabs, bcomb, vp, bp, k_wait, diag, btab);
+                           mp, op, keys_pk, keys_ok, ktabs, bcomb, vp, bp, k_wait, diag, btab, sb);
     } else if (mode == MODE_ZIP215) {
       hipLaunchKernelGGL((k_verify_keyed_quad_split<MODE_ZIP215, false>), grid, block, 0, s, n, n_keys, ki, sgp, mp,
-                         op, keys_pk, keys_ok, ktabs, bcomb, vp, bp, k_wait, diag, btab);
+                         op, keys_pk, keys_ok, ktabs, bcomb, vp, bp, k_wait, diag, btab, sb);
     } else {
       hipLaunchKernelGGL((k_verify_keyed_quad_split<MODE_GO_STDLIB, false>), grid, block, 0, s, n, n_keys, ki, sgp,
-                         mp, op, keys_pk, keys_ok, ktabs, bcomb, vp, bp, k_wait, diag, btab);
+                         mp, op, keys_pk, keys_ok, ktabs, bcomb, vp, bp, k_wait, diag, btab, sb);
     }
     return hipGetLastError();
   }

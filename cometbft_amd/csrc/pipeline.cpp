@@ -60,21 +60,6 @@ struct Chunk {
   BulkLayout L;
 };
 
-// sb_msg_len (signbytes.h) without loops: the varint lengths from the bit
-// width. Same value for every input (tests/host/pipecheck.cpp's fake device
-// checks each message's offsets against sb_msg_len).
-inline uint32_t uvlen(uint64_t v) { return (uint32_t)(64 - __builtin_clzll(v | 1) + 6) / 7; }
-
-struct TplLens {
-  uint32_t pre_commit, pre_nil, post;
-};
-
-inline uint32_t msg_len(const TplLens& t, bool commit_flag, int64_t sec, int32_t nanos) {
-  const uint32_t tl = (sec != 0 ? 1 + uvlen((uint64_t)sec) : 0) + (nanos != 0 ? 1 + uvlen((uint64_t)(int64_t)nanos) : 0);
-  const uint32_t b = (commit_flag ? t.pre_commit : t.pre_nil) + 1 + uvlen(tl) + tl + t.post;
-  return uvlen(b) + b;
-}
-
 // Copy into the pinned staging with non-temporal stores: the staging is
 // written once by the host and read once by the H2D copy, so its lines need
 // not be read for ownership or kept in the cache (the pack is bound by host

@@ -457,6 +457,11 @@ struct CmtvDev {
   // slot is ever shared with a launch still in flight.
   hipEvent_t poll_ev = nullptr;
   bool poll_pending = false;
+  // signatures a single-commit call copied to h_in / d_in (offset 0) before
+  // planning (stage_sigs_early_locked): the source and count; the next
+  // staging of those bytes skips them
+  const uint8_t* early_src = nullptr;
+  size_t early_n = 0;
   // a device that returned a HIP error is taken out of the context's
   // rotation: host batches are re-planned over the others (runtime.cpp
   // run_host_batch); CMTV_FAULT_DEV=g makes device g's first launch fail
@@ -538,6 +543,8 @@ struct cmtv_ctx {
   // fused small host batches read their inputs from mapped host memory (CMTV_NO_ZC_IN=1: off)
   bool zc_in = true;
   bool zc_host_in = true;  // CMTV_ZC_HOST_IN=0: host-API batches copy their staging to HBM
+  bool zc_keyed = false;   // CMTV_ZC_KEYED=1: templated registered-key batches read it in place too
+  bool early_sigs = true;  // CMTV_EARLY_SIGS=0: a commit's signatures are staged after its plan
   // single-device host batches up to this size take the mapped-memory path (CMTV_ZC_MAX)
   size_t zc_max = kZeroCopyMax;
   // small host batches on a row kernel poll its tagged bitmap words
@@ -735,6 +742,15 @@ static bool row_kernel_for(const cmtv_ctx* ctx, size_t n) {
 // predicate both enqueue_shard and enqueue_verify use.
 static bool fuse_ok(const cmtv_ctx* ctx, size_t n) { return split_kernel_for(ctx, n) && n <= kChunk; }
 
+// ... and the same for registered keys: the keyed row kernel and the keyed
+// quad split kernel (one launch each) hash in a helper wave that can write
+// the templated sign-bytes itself (kernels.hip helper_message)
+static bool keyed_fuse_ok(const cmtv_ctx* ctx, size_t n) {
+  const bool quad = n <= ctx->keyed_quad_max;
+  const bool krow = quad && n <= ctx->keyed_row_max && n <= kRowMaxCap;
+  return krow || (quad && n <= ctx->quad_split_max && n <= kChunk);
+}
+
 static int enqueue_verify(cmtv_ctx* ctx, CmtvDev& D, size_t n, const uint8_t* d_pk, const uint8_t* d_sig,
                           const uint8_t* d_msg, const uint32_t* d_off, uint32_t mode, uint8_t* d_valid,
                           uint64_t* d_bitmap, hipStream_t s, const SbFuse* sb = nullptr, Scratch* scr = nullptr) {
@@ -832,9 +848,11 @@ static int ensure_bcomb(CmtvDev& D) {
 static int enqueue_verify_keyed(cmtv_ctx* ctx, CmtvDev& D, const cmtv_keyset::PerDev& K, size_t n_keys, size_t n,
                                 const uint32_t* d_idx, const uint8_t* d_sig, const uint8_t* d_msg,
                                 const uint32_t* d_off, uint32_t mode, uint8_t* d_valid, uint64_t* d_bitmap,
-                                hipStream_t s, Scratch* scr = nullptr) {
+                                hipStream_t s, Scratch* scr = nullptr, const SbFuse* sb = nullptr) {
   if (n == 0) return CMTV_OK;
   Scratch& S = scr ? *scr : D.scratch;
+  if (sb && !keyed_fuse_ok(ctx, n)) return CMTV_EINVAL;
+  if (!d_idx && !sb) return CMTV_EINVAL;  // identity keys only in the one-launch fused forms
   if (fault_hit(ctx) || D.inject_fault) return CMTV_EHIP;
   const bool quad = n <= ctx->keyed_quad_max;
   // lane launches: KB signatures per lane sharing one inversion while that
@@ -880,7 +898,7 @@ static int enqueue_verify_keyed(cmtv_ctx* ctx, CmtvDev& D, const cmtv_keyset::Pe
                             d_bitmap ? d_bitmap + c / 64 : nullptr, quad, n <= ctx->quad_split_max,
                             ctx->keyed_wait, D.d_diag, kb, static_cast<uint32_t*>(S.buf.p),
                             quad ? nullptr : K.d_wide, D.d_btab, ctx->wide_dma, s, krow ? &slot : nullptr,
-                            ctx->keyed_mixed);
+                            ctx->keyed_mixed, sb);
     if (e == hipSuccess && krow) e = row_slot_release(ctx, D, s, slot_k);
     if (e != hipSuccess) {
       D.timing.abandon(tp);
@@ -1038,7 +1056,9 @@ static int enqueue_shard(cmtv_ctx* ctx, size_t g, const HostBatch& B, size_t a, 
   const bool keyed = B.ks != nullptr, tpl = B.msg == nullptr;
   const size_t mb = (size_t)B.msg_off[b] - B.msg_off[a];
   const size_t key_bytes = keyed ? 4 * m : 32 * m;
-  const size_t o_key = 0, o_sig = align_up(key_bytes, 256), o_off = align_up(o_sig + 64 * m, 256);
+  // signatures first: an early-staged commit's (stage_sigs_early_locked) are
+  // already there, on their way to the device
+  const size_t o_sig = 0, o_key = align_up(64 * m, 256), o_off = align_up(o_key + key_bytes, 256);
   size_t o_tidx = 0, o_flag = 0, o_sec = 0, o_nanos = 0, o_tmpl = 0, o_blob = 0, in_bytes, o_msg, dev_bytes;
   const size_t tb = B.n_tmpls * sizeof(SbTemplate);
   if (tpl) {
@@ -1068,29 +1088,54 @@ static int enqueue_shard(cmtv_ctx* ctx, size_t g, const HostBatch& B, size_t a, 
   // templated sign-bytes written by the verify kernel's helper wave (no
   // k_sign_bytes launch) when the batch runs a split kernel and every
   // message fits the helper's LDS slot; CMTV_NO_SB_FUSE turns it off
-  const bool fuse = tpl && !keyed && ctx->sb_fuse && max_len <= kSbFuseMaxMsg && fuse_ok(ctx, m);
+  const bool fuse = tpl && ctx->sb_fuse && max_len <= kSbFuseMaxMsg && (keyed ? keyed_fuse_ok(ctx, m) : fuse_ok(ctx, m));
   // a fused small batch reads its staging in mapped host memory directly
   // (CMTV_NO_ZC_IN turns it off), and so does a small plain host-API batch
   // whose messages fit the same bound (keys, signatures and messages; no
   // sign-bytes kernel writes into the staging then; CMTV_ZC_HOST_IN=0 copies
   // it). Measured on MI355X (round 4, profiles/r04_zc_host_ab.txt): host API
   // 150 0.116 -> 0.109 ms, 4,096 0.284 -> 0.269, 10,000 0.343 -> 0.326 ms.
+  // With CMTV_ZC_KEYED=1 a small templated registered-key batch (the
+  // keyset-cache VerifyCommit) reads its staging there too (unfused: only the
+  // sign-bytes that k_sign_bytes writes go to HBM, D.d_in). Off by default:
+  // at 10k signatures the keyed kernel's PCIe reads cost what the H2D copy
+  // saves (round 5, before fusion: p50 0.2010 vs 0.2012 ms, kernel 0.087 vs
+  // 0.071 ms).
   const bool zc = zero_copy && ctx->zc_in &&
-                  (fuse || (!tpl && !keyed && ctx->zc_host_in && max_len <= kSbFuseMaxMsg));
+                  (keyed ? tpl && ctx->zc_keyed
+                         : fuse || (!tpl && ctx->zc_host_in && max_len <= kSbFuseMaxMsg));
+  const bool zc_keyed = zc && keyed && !fuse;  // k_sign_bytes writes the messages into HBM
   HostBuf& HB = zc ? D.h_zin : D.h_in;
+  // the signatures staged ahead of the plan: the same bytes are already in
+  // h_in (and on their way to d_in on this stream), unless a buffer must grow
+  const bool early = !zc && D.early_src && D.early_src == B.sig + 64 * a && m <= D.early_n &&
+                     in_bytes <= D.h_in.cap && dev_bytes <= D.d_in.cap;
+  D.early_src = nullptr;
   if ((e = HB.ensure(in_bytes)) != hipSuccess) return hip_fail(e);
   if (!zc && (e = D.d_in.ensure(dev_bytes)) != hipSuccess) return hip_fail(e);
+  if (zc_keyed && (e = D.d_in.ensure(mb + 16)) != hipSuccess) return hip_fail(e);
   if ((e = D.d_out.ensure(out_bytes)) != hipSuccess) return hip_fail(e);
   auto* hin = static_cast<uint8_t*>(HB.p);
-  if (keyed)
-    std::memcpy(hin + o_key, B.key_idx + a, 4 * m);
-  else
+  // a null key_idx (registered keys) means signature i is by key i, a null
+  // tidx that every signature uses template 0: the fused kernels take them
+  // as null, anything else gets the arrays written out
+  const bool null_kidx = keyed && !B.key_idx && fuse, null_tidx = tpl && !B.tidx && fuse;
+  if (keyed) {
+    if (B.key_idx)
+      std::memcpy(hin + o_key, B.key_idx + a, 4 * m);
+    else if (!null_kidx)
+      for (size_t i = 0; i < m; i++) reinterpret_cast<uint32_t*>(hin + o_key)[i] = (uint32_t)(a + i);
+  } else {
     std::memcpy(hin + o_key, B.pk + 32 * a, 32 * m);
-  std::memcpy(hin + o_sig, B.sig + 64 * a, 64 * m);
+  }
+  if (!early) std::memcpy(hin + o_sig, B.sig + 64 * a, 64 * m);
   auto* hoff = reinterpret_cast<uint32_t*>(hin + o_off);
   for (size_t i = 0; i <= m; i++) hoff[i] = B.msg_off[a + i] - base;
   if (tpl) {
-    std::memcpy(hin + o_tidx, B.tidx + a, 4 * m);
+    if (B.tidx)
+      std::memcpy(hin + o_tidx, B.tidx + a, 4 * m);
+    else if (!null_tidx)
+      std::memset(hin + o_tidx, 0, 4 * m);
     std::memcpy(hin + o_flag, B.tflag + a, m);
     std::memcpy(hin + o_sec, B.sec + a, 8 * m);
     std::memcpy(hin + o_nanos, B.nanos + a, 4 * m);
@@ -1103,19 +1148,22 @@ static int enqueue_shard(cmtv_ctx* ctx, size_t g, const HostBatch& B, size_t a, 
   phase_add(ctx, kPhStage, t_stage);
   const uint64_t t_launch = phase_now(ctx);
   uint8_t* din = static_cast<uint8_t*>(D.d_in.p);
+  uint8_t* dmsg = din + o_msg;  // the templated sign-bytes, written by k_sign_bytes
   auto* dout = static_cast<uint8_t*>(D.d_out.p);
   if (zc) {
     void* p = nullptr;
     if ((e = hipHostGetDevicePointer(&p, HB.p, 0)) != hipSuccess) return hip_fail(e);
     din = static_cast<uint8_t*>(p);
-  } else if ((e = hipMemcpyAsync(din, hin, in_bytes, hipMemcpyHostToDevice, D.stream)) != hipSuccess) {
+    dmsg = zc_keyed ? static_cast<uint8_t*>(D.d_in.p) : din + o_msg;
+  } else if ((e = early ? hipMemcpyAsync(din + o_key, hin + o_key, in_bytes - o_key, hipMemcpyHostToDevice, D.stream)
+                         : hipMemcpyAsync(din, hin, in_bytes, hipMemcpyHostToDevice, D.stream)) != hipSuccess) {
     return hip_fail(e);
   }
   SbFuse sb;
   if (fuse) {
     sb.tmpls = din + o_tmpl;
     sb.blob = din + o_blob;
-    sb.tidx = reinterpret_cast<uint32_t*>(din + o_tidx);
+    sb.tidx = null_tidx ? nullptr : reinterpret_cast<uint32_t*>(din + o_tidx);
     sb.flag = din + o_flag;
     sb.sec = reinterpret_cast<int64_t*>(din + o_sec);
     sb.nanos = reinterpret_cast<int32_t*>(din + o_nanos);
@@ -1125,15 +1173,16 @@ static int enqueue_shard(cmtv_ctx* ctx, size_t g, const HostBatch& B, size_t a, 
     if ((e = launch_sign_bytes((uint32_t)m, din + o_tmpl, din + o_blob, reinterpret_cast<uint32_t*>(din + o_tidx),
                                din + o_flag, reinterpret_cast<int64_t*>(din + o_sec),
                                reinterpret_cast<int32_t*>(din + o_nanos), reinterpret_cast<uint32_t*>(din + o_off),
-                               din + o_msg, D.stream)) != hipSuccess)
+                               dmsg, D.stream)) != hipSuccess)
       return hip_fail(e);
   }
   uint8_t* dv = want_valid ? dout + o_valid : nullptr;
   int rc;
   if (keyed)
-    rc = enqueue_verify_keyed(ctx, D, B.ks->dev[g], B.ks->n, m, reinterpret_cast<uint32_t*>(din + o_key),
-                              din + o_sig, din + o_msg, reinterpret_cast<uint32_t*>(din + o_off), B.mode, dv, bitmap,
-                              D.stream);
+    rc = enqueue_verify_keyed(ctx, D, B.ks->dev[g], B.ks->n, m,
+                              null_kidx ? nullptr : reinterpret_cast<uint32_t*>(din + o_key),
+                              din + o_sig, tpl ? dmsg : din + o_msg, reinterpret_cast<uint32_t*>(din + o_off), B.mode,
+                              dv, bitmap, D.stream, nullptr, fuse ? &sb : nullptr);
   else
     rc = enqueue_verify(ctx, D, m, din + o_key, din + o_sig, din + o_msg, reinterpret_cast<uint32_t*>(din + o_off),
                         B.mode, dv, bitmap, D.stream, fuse ? &sb : nullptr);
@@ -1366,6 +1415,7 @@ static int run_host_batch(cmtv_ctx* ctx, const HostBatch& B, uint8_t* out_valid,
     retire_device(ctx, (size_t)bad);
     ctx->stats.reshards++;
   }
+  for (auto& D : ctx->devs) D.early_src = nullptr;  // used by this batch or never
   (void)hipSetDevice(ctx->devs[ctx->live.empty() ? 0 : ctx->live[0]].ordinal);
   return rc;
 }
@@ -1461,6 +1511,33 @@ int verify_templated_locked(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const ui
   B.sec = sec;
   B.nanos = nanos;
   return run_host_batch(ctx, B, out_valid, nullptr);
+}
+
+// A single-commit VerifyCommit on one device with registered keys spends
+// ~25 us planning 10k signatures before its staging is copied: its
+// signatures (the bulk of the staging) go to the device first, so their H2D
+// copy overlaps the plan. Their bytes are only used if the batch that
+// follows stages exactly those signatures on this device (enqueue_shard);
+// otherwise they are overwritten unused.
+int stage_sigs_early_locked(cmtv_ctx* ctx, const uint8_t* sigs, size_t n) {
+  if (n == 0 || n > ctx->zc_max || ctx->live.size() != 1 || ctx->zc_keyed || !ctx->early_sigs) return CMTV_OK;
+  CmtvDev& D = ctx->devs[ctx->live[0]];
+  if (hipSetDevice(D.ordinal) != hipSuccess) return CMTV_ENODEV;
+  hipError_t e;
+  // the previous polled launch may still read h_in's neighbour h_zin only,
+  // but settle it anyway so the buffers below are never in use
+  if ((e = settle_polled(D)) != hipSuccess) return hip_fail(e);
+  // room for any layout of n signatures that can follow (keys, offsets,
+  // templates, sign-bytes), so enqueue_shard never reallocates under the copy
+  const size_t in_cap = 136 * n + 64 * 1024, dev_cap = in_cap + 400 * n;
+  if ((e = D.h_in.ensure(in_cap)) != hipSuccess) return hip_fail(e);
+  if ((e = D.d_in.ensure(dev_cap)) != hipSuccess) return hip_fail(e);
+  std::memcpy(D.h_in.p, sigs, 64 * n);
+  if ((e = hipMemcpyAsync(D.d_in.p, D.h_in.p, 64 * n, hipMemcpyHostToDevice, D.stream)) != hipSuccess)
+    return hip_fail(e);
+  D.early_src = sigs;
+  D.early_n = n;
+  return CMTV_OK;
 }
 
 // The single-device _device entry points run on devs[0] (their inputs are
@@ -1577,6 +1654,8 @@ static void read_env(cmtv_ctx* ctx) {
   if (const char* nf = std::getenv("CMTV_NO_SB_FUSE")) ctx->sb_fuse = nf[0] != '1';
   if (const char* nz = std::getenv("CMTV_NO_ZC_IN")) ctx->zc_in = nz[0] != '1';
   if (const char* zh = std::getenv("CMTV_ZC_HOST_IN")) ctx->zc_host_in = zh[0] != '0';
+  if (const char* zk = std::getenv("CMTV_ZC_KEYED")) ctx->zc_keyed = zk[0] == '1';
+  if (const char* es = std::getenv("CMTV_EARLY_SIGS")) ctx->early_sigs = es[0] != '0';
   if (const char* zm = std::getenv("CMTV_ZC_MAX")) ctx->zc_max = (size_t)std::strtoull(zm, nullptr, 10);
   if (const char* hp = std::getenv("CMTV_HOST_POLL")) ctx->host_poll = std::atoi(hp) != 0;
   if (const char* kl = std::getenv("CMTV_FORCE_K_LATE")) ctx->keyed_wait = kl[0] == '1' ? 0u : kKeyedWaitDefault;
@@ -2155,9 +2234,10 @@ void keyset_unpin_locked(cmtv_ctx* ctx, const cmtv_keyset* cks) {
 
 const cmtv_keyset* keyset_for_locked(cmtv_ctx* ctx, const uint8_t* pk32, size_t n_keys) {
   if (!ctx->keyset_cap || n_keys == 0) return nullptr;
-  std::string key(reinterpret_cast<const char*>(pk32), 32 * n_keys);
-  for (auto& e : ctx->keysets)
-    if (e.first == key) return e.second;
+  const size_t bytes = 32 * n_keys;
+  for (auto& e : ctx->keysets)  // compared in place: no copy of the keys per call
+    if (e.first.size() == bytes && std::memcmp(e.first.data(), pk32, bytes) == 0) return e.second;
+  std::string key(reinterpret_cast<const char*>(pk32), bytes);
   cmtv_keyset* ks = nullptr;
   if (register_keys_locked(ctx, n_keys, pk32, &ks, 0) != CMTV_OK) return nullptr;  // generic path instead
   if (ctx->keysets.size() >= ctx->keyset_cap) {

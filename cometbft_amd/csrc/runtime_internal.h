@@ -30,12 +30,19 @@ int verify_host_locked(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_t
 // templates (signbytes.h): tmpls is an array of n_tmpls SbTemplate over
 // `blob`; msg_off must hold the message offsets from sb_msg_len. With ks the
 // keys are registered (key_idx into ks, no pk). Verdicts only (no verdict
-// cache). Caller holds the context lock.
+// cache). tidx null: every signature uses template 0; key_idx null (with
+// ks): signature i is by key i. Caller holds the context lock.
 int verify_templated_locked(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_t* sig, const uint32_t* msg_off,
                             const void* tmpls, size_t n_tmpls, const uint8_t* blob, size_t blob_len,
                             const uint32_t* tidx, const uint8_t* commit_flag, const int64_t* sec,
                             const int32_t* nanos, uint32_t mode, uint8_t* out_valid,
                             const cmtv_keyset* ks = nullptr, const uint32_t* key_idx = nullptr);
+
+// A single commit's n contiguous 64-byte signatures, copied toward device
+// memory before the commit is planned (the copy overlaps the plan); the
+// templated batch that follows picks them up (no-op unless one live device,
+// n <= the zero-copy size and CMTV_EARLY_SIGS is on). Caller holds the lock.
+int stage_sigs_early_locked(cmtv_ctx* ctx, const uint8_t* sigs, size_t n);
 
 // cmtv_keyset_cache: the registered key set of these n 32-byte keys (built on
 // first use), or NULL when the cache is off or registration failed.

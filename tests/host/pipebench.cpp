@@ -25,7 +25,8 @@ int main(int argc, char** argv) {
   const unsigned T = argc > 2 ? (unsigned)std::atoi(argv[2]) : 8;
   const uint32_t kind = argc > 3 ? (uint32_t)std::atoi(argv[3]) : 0;
   const size_t chunk = argc > 4 ? std::strtoull(argv[4], nullptr, 10) : (1u << 20);
-  const uint32_t nv = 150;
+  const uint32_t nv = argc > 5 ? (uint32_t)std::atoi(argv[5]) : 150;
+  const bool pipe = argc > 6 ? std::atoi(argv[6]) != 0 : true;
   std::vector<uint8_t> pk(32 * nv), addrs(20 * nv + 1);
   std::vector<uint32_t> pk_off(nv + 1);
   std::vector<int64_t> power(nv, 10), prio(nv, 0);
@@ -59,11 +60,12 @@ int main(int argc, char** argv) {
   }
   std::vector<cmtv_commit_result> res(H);
   std::vector<int> rcs(H);
-  cmtv_ctx* ctx = fake_open(1, T, 1, chunk, 3, true, 4, -1);
+  cmtv_ctx* ctx = fake_open(1, T, 1, chunk, 3, pipe, 4, -1);
   fake_set_noverify(ctx, true);
   const char chain[] = "cmtverify-bench";
   double best = 1e30;
-  for (int it = 0; it < 6; it++) {
+  const int iters = H == 1 ? 200 : 6;
+  for (int it = 0; it < iters; it++) {
     const auto t0 = std::chrono::steady_clock::now();
     const int rc = cmtv_verify_commits(ctx, kind, 0, chain, sizeof chain - 1, H, vals.data(), bids.data(), hs.data(),
                                        cs.data(), 1, 3, res.data(), rcs.data(), nullptr, 0);
@@ -74,12 +76,13 @@ int main(int argc, char** argv) {
     }
     if (it) best = ms < best ? ms : best;
   }
-  std::printf("%zu heights x %u, kind %u, %u threads: %.2f ms per call (%.1f ns per signature of wall)\n", H, nv, kind,
-              T, best, best * 1e6 / (double)(H * nv));
+  std::printf("%zu heights x %u, kind %u, %u threads, %s: %.4f ms per call (%.1f ns per signature of wall)\n", H, nv, kind,
+              T, pipe ? "pipeline" : "one batch", best, best * 1e6 / (double)(H * nv));
   uint64_t pt[16] = {};
   fake_phases(ctx, pt);
-  std::printf("  per call ms: plan %.2f pack %.2f submit %.2f wait %.2f replay %.2f\n", pt[6] / 6e6, pt[7] / 6e6,
-              pt[8] / 6e6, pt[9] / 6e6, pt[10] / 6e6);
+  const double k = 1e6 * iters;
+  std::printf("  per call ms: plan %.3f pack %.3f submit %.3f wait %.3f replay %.3f | one batch: prepare %.4f "
+              "replay %.4f\n", pt[6] / k, pt[7] / k, pt[8] / k, pt[9] / k, pt[10] / k, pt[0] / k, pt[5] / k);
   fake_close(ctx);
   return 0;
 }

@@ -256,6 +256,14 @@ def test_device_sign_bytes_templating(monkeypatch, chain, fuse):
     if not fuse:
         monkeypatch.setenv("CMTV_NO_SB_FUSE", "1")
     gpu_ctx = Context(device=0)
+    # registered keys: the keyed row (16 signatures) and keyed quad split
+    # (CMTV_KEYED_ROW_MAX=0) kernels' hash helpers write the bytes themselves
+    keyed = Context(device=0)
+    keyed.keyset_cache(4)
+    monkeypatch.setenv("CMTV_KEYED_ROW_MAX", "0")
+    keyed_q = Context(device=0)
+    keyed_q.keyset_cache(4)
+    monkeypatch.delenv("CMTV_KEYED_ROW_MAX", raising=False)
     monkeypatch.delenv("CMTV_NO_SB_FUSE", raising=False)
 
     secs = [0, 1, 127, 128, 2**40, -1, -62135596800, 1_700_000_000]
@@ -281,5 +289,14 @@ def test_device_sign_bytes_templating(monkeypatch, chain, fuse):
                                              if j == 5 else s for j, s in enumerate(sigs)])
         e = _err(lambda: vset.verify_commit(chain, bid, height, bad, ctx=gpu_ctx))
         assert isinstance(e, T.ErrWrongSignature) and e.index == 5
+        for kc in (keyed, keyed_q):
+            assert _err(lambda: vset.verify_commit(chain, bid, height, commit, ctx=kc)) is None
+            assert _err(lambda: vset.verify_commit_light(chain, bid, height, commit, ctx=kc)) is None
+            e = _err(lambda: vset.verify_commit(chain, bid, height, bad, ctx=kc))
+            assert isinstance(e, T.ErrWrongSignature) and e.index == 5
     fused = gpu_ctx.stats()["fused_sign_bytes"]
     assert (fused > 0) == (fuse and len(chain) <= 50), fused
+    for kc in (keyed, keyed_q):
+        st = kc.stats()
+        assert st["keyed_launches"] > 0
+        assert (st["fused_sign_bytes"] > 0) == (fuse and len(chain) <= 50), st["fused_sign_bytes"]

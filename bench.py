@@ -864,6 +864,38 @@ def _p50_p99(fn, iters, warm=50):
     return round(float(np.percentile(ts, 50)), 4), round(float(np.percentile(ts, 99)), 4)
 
 
+def crossover(ctx, mode, sizes=(1, 2, 4, 8, 16, 32), iters=100):
+    """The small-batch crossover (tools/crossover.py is the
+    full sweep, profiles/r04_crossover.json): the smallest n from which one
+    n-validator VerifyCommit through cmtv_verify_commit (packed once, as a cgo
+    shim holds it) beats the CPU oracle on ONE core over the same n signatures
+    -- the reference's loop is one goroutine (types/validator_set.go:685) --
+    at every larger n measured. Below it the Go binding keeps the CPU path
+    (INTEGRATION.md CMTVERIFY_MIN_BATCH)."""
+    from cometbft_amd import testutil as TU
+    from oracle import coracle  # the CPU baseline only
+
+    rows = []
+    for n in sizes:
+        sv = TU.make_validator_set(ctx, n)
+        commit, msgs, sig = TU.make_commit(ctx, sv, height=1000)
+        call, keep = _commit_c_call(ctx, sv, commit, TU.block_id_for_height(1000), 1000, mode)
+        g50, _ = _p50_p99(call, iters, warm=10)
+        m, off = coracle.pack_msgs(msgs)  # the commit's sign-bytes and signatures
+        pk = np.ascontiguousarray(sv.pubkeys)
+        c50, _ = _p50_p99(lambda: coracle.verify_batch(pk, sig, m, off, mode, nthreads=1), max(20, iters // 4), warm=3)
+        rows.append({"n": n, "gpu_commit_ms": g50, "cpu_1core_ms": c50, "gpu_wins": bool(g50 < c50)})
+        del keep
+    cross = None
+    for r in reversed(rows):
+        if not r["gpu_wins"]:
+            break
+        cross = r["n"]
+    return {"n": cross, "rows": rows,
+            "how": "smallest n from which cmtv_verify_commit (p50, one n-validator commit) beats the oracle on one "
+                   "core (p50, the same n signatures) at every larger n measured"}
+
+
 def verify_commit_10k(ctx, mode, iters, host_api_ms=None):
     """VerifyCommit at configs[1] scale: one 10,000-
     validator commit through cmtv_verify_commit, packed once, p50 / p99 wall
@@ -1219,6 +1251,10 @@ def main():
         if ex["value"]:
             ex["gpu_over_cpu"] = round(value / n_dev / ex["value"], 1)
             ex["gpu_over_cpu_other_mode"] = round(z["value"] / n_dev / ex["value_other_mode"], 1)
+        try:
+            cb["crossover"] = crossover(Context(device=0), mode)
+        except Exception as e:  # noqa: BLE001 -- an aux figure never sinks the bench line
+            cb["crossover"] = {"error": f"{type(e).__name__}: {e}"[:400]}
     if not args.no_latency and n_dev == 1:
         aux("verify_commit_10k_keyset", lambda: verify_commit_10k_keyset(mode, 200))
     if not args.no_latency:

@@ -13,18 +13,26 @@ constexpr uint32_t kAtabWordsPerLane = 320; // (1..8)(-A), 40 words per point
 constexpr uint32_t kCombWords = 32 * 128 * 32;     // one registered-key comb (keyed.h), 512 KiB
 constexpr uint32_t kCombScratchWordsPerKey = 128 * 320;  // prefix products while building
 
-// launch_verify / launch_verify_sr25519 kflags: the quad kernel (else lane),
-// the CMTV_FORCE_WIDE test knob (every quad takes the 64-window schedule),
-// the oct kernel (with kLaunchQuad; Ed25519 only) and its two-wave form
-// (kLaunchOctSplit), and the quad kernel's helper-wave form (kLaunchQuadSplit)
-constexpr uint32_t kLaunchQuad = 1, kLaunchForceWide = 2, kLaunchOct = 4, kLaunchOctSplit = 8, kLaunchQuadSplit = 16;
-// the one-signature-per-wave row kernel (row.h, k_verify_row_split; Ed25519)
-// and its two- and four-waves-per-signature forms (k_verify_row2_split,
-// k_verify_row4_split)
-constexpr uint32_t kLaunchRow = 32, kLaunchRow2 = 64, kLaunchRow4 = 128;
-// with kLaunchQuadSplit: the helper-summed form (k_verify_quad_hs,
-// k_verify_sr25519_quad_hs); kflags bits 16..31 carry its tuning (hs_tune)
-constexpr uint32_t kLaunchQuadHS = 256;
+// The verification forms (launch_verify / launch_verify_sr25519 kflags bits
+// 0..7; the runtime picks one per batch size, runtime.cpp ed_form / sr_form):
+//   kFormLane : one signature per lane (k_verify, k_verify_sr25519)
+//   kFormQuad : four lanes per signature, three quad waves + a helper wave
+//               that hashes and sums each window's table entries
+//               (k_verify_quad_hs, k_verify_sr25519_quad_hs)
+//   kFormOct2 : eight lanes per signature in two waves (k_verify_oct_split)
+//   kFormRow  : one wave per signature, three per workgroup + a helper
+//               (k_verify_row_split)
+//   kFormRow4 : four waves per signature (k_verify_row4_split)
+// sr25519 has the lane and quad forms. kLaunchForceWide: the CMTV_FORCE_WIDE
+// test knob (every quad-family verifier takes the 64-window schedule); bits
+// 16..31: the helper-summed forms' tuning (hs_tune, CMTV_HS_PRE).
+constexpr uint32_t kFormLane = 0, kFormQuad = 1, kFormOct2 = 2, kFormRow = 3, kFormRow4 = 4;
+constexpr uint32_t kFormMask = 0xFF, kLaunchForceWide = 0x100;
+// registered-key forms (launch_verify_keyed): the keyed row kernel
+// (k_verify_keyed_row_split, one signature per workgroup), the keyed quad
+// kernel with two helper waves (k_verify_keyed_quad_split), the lane kernels
+// (keyed_lane.hip)
+constexpr uint32_t kKeyedRow = 0, kKeyedQuad = 1, kKeyedLane = 2;
 
 // Row kernel bitmap assembly: each launch takes the next of kRowSlots slots
 // of a per-device ring (kRowSlotWords words, read as 64-bit words of 32
@@ -49,7 +57,7 @@ struct RowSlot {
 };
 
 // Templated sign-bytes (signbytes.h) written by the helper waves of the
-// split kernels themselves (k_verify_oct_split / k_verify_quad_split): each
+// helper-wave kernels themselves (every form but the lane kernels): each
 // helper lane builds its signature's CanonicalVote into an LDS slot of
 // kSbFuseMaxMsg bytes and hashes it from there, so a templated commit needs
 // no k_sign_bytes launch (and no global message buffer). Device pointers;
@@ -72,36 +80,32 @@ constexpr uint32_t kDiagLateK = 0, kDiagWords = 4;
 constexpr uint32_t kKeyedWaitDefault = 1u << 22;
 
 hipError_t launch_btab_init(uint32_t* d_rows, hipStream_t s);
-// sb (may be null) is honoured only by the split kernels (kLaunchOctSplit,
-// kLaunchQuadSplit); the caller launches k_sign_bytes otherwise
-// (and by the row kernel, kLaunchRow, which needs row_slot: one slot of the
-// device's ring when bitmap is set)
+// sb (may be null) is honoured by the forms whose helper wave hashes (every
+// form but kFormLane); the caller launches k_sign_bytes otherwise. The row
+// forms need row_slot (one slot of the device's ring) when bitmap is set.
 hipError_t launch_verify(uint32_t mode, uint32_t n, const void* pk, const void* sig, const void* msg,
                          const void* off, const uint32_t* btab, uint32_t* atab, void* valid, void* bitmap,
                          uint32_t kflags, hipStream_t s, const SbFuse* sb = nullptr, const RowSlot* row_slot = nullptr);
 hipError_t launch_comb_build(uint32_t n_keys, const void* keys_pk, uint8_t* keys_ok, uint32_t* tabs,
                              uint32_t* scratch, bool negate, hipStream_t s);
+// form: kKeyedRow (row_slot: a slot of the device's bitmap ring when bitmap
+// is set), kKeyedQuad, kKeyedLane. sb (may be null) is honoured by the row and
+// quad forms only (their helper waves hash; hipErrorInvalidValue otherwise).
+// key_idx null: signature i is by key i (row and quad forms).
 hipError_t launch_verify_keyed(uint32_t mode, uint32_t n, uint32_t n_keys, const void* key_idx, const void* sig,
                                const void* msg, const void* off, const uint32_t* keys_pk, const uint8_t* keys_ok,
-                               const uint32_t* ktabs, const uint32_t* bcomb, void* valid, void* bitmap,
-                               bool quad, bool split, uint32_t k_wait, uint32_t* diag, uint32_t batch_kb,
-                               uint32_t* scr, const uint32_t* wtabs, const uint32_t* btab, bool wide_dma,
-                               hipStream_t s, const RowSlot* row_slot = nullptr, bool mixed = true,
+                               const uint32_t* ktabs, void* valid, void* bitmap, uint32_t form, uint32_t k_wait,
+                               uint32_t* diag, uint32_t batch_kb, uint32_t* scr, const uint32_t* wtabs,
+                               const uint32_t* btab, hipStream_t s, const RowSlot* row_slot = nullptr,
                                const SbFuse* sb = nullptr);
-// (row_slot set: the keyed row kernel, k_verify_keyed_row_split, one
-// signature per workgroup; a slot of the device's bitmap ring). sb (may be
-// null) is honoured by the keyed row and keyed quad split forms only (their
-// helper waves hash; hipErrorInvalidValue otherwise), as by launch_verify.
 // the one-signature-per-lane part of launch_verify_keyed (keyed_lane.hip):
-// over the wide combs wtabs (rows staged by LDS-DMA when dma) or, with wtabs
-// null, the radix-256 key combs ktabs with B over btab's radix-2^16 comb
-// (mixed) or over its radix-256 comb bcomb
+// over the wide combs wtabs (rows staged by LDS-DMA) or, with wtabs null, the
+// radix-256 key combs ktabs with B over btab's radix-2^16 comb
 hipError_t launch_verify_keyed_lane(uint32_t mode, uint32_t n, uint32_t n_keys, const uint32_t* ki,
                                     const uint32_t* sgp, const uint8_t* mp, const uint32_t* op,
                                     const uint32_t* keys_pk, const uint8_t* keys_ok, const uint32_t* ktabs,
-                                    const uint32_t* bcomb, uint8_t* vp, uint64_t* bp, uint32_t batch_kb,
-                                    uint32_t* scr, const uint32_t* wtabs, const uint32_t* btab, bool dma,
-                                    bool mixed, hipStream_t s);
+                                    uint8_t* vp, uint64_t* bp, uint32_t batch_kb, uint32_t* scr,
+                                    const uint32_t* wtabs, const uint32_t* btab, hipStream_t s);
 // Wide (radix-2^16) combs of n_keys keys (keyed.h): bases = n_keys x 16 x 40
 // words, scratch = n_keys x kWideScratchWordsPerKey words.
 constexpr size_t kWideTableWords = (size_t)16 * 32768 * 32;  // 64 MiB per key

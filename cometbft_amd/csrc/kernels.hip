@@ -4,10 +4,13 @@
 //   k_verify<MODE>: one signature per lane: SHA-512 + mod-L + decompression +
 //                   Straus [s]B - [k]A + GO_STDLIB / ZIP215 final check, then a
 //                   wavefront ballot packs 64 verdicts into one bitmap word
-//   k_verify_quad<MODE>: the same, one signature per quad of lanes (small batches)
+//   k_verify_quad_hs / k_verify_oct_split / k_verify_row_split /
+//   k_verify_row4_split<MODE>: the same with 4 / 8 / 64 / 256 lanes per
+//                   signature and a helper wave (smaller batches; kernels.h forms)
 //   k_comb_build  : registered-key combs (keyed.h), one workgroup per key
-//   k_verify_keyed_quad<MODE>: one signature per quad of lanes against a
-//                   registered key (the lane kernels: keyed_lane.hip)
+//   k_verify_keyed_row_split / k_verify_keyed_quad_split<MODE>: one signature
+//                   per workgroup / per quad of lanes against a registered key
+//                   (the lane kernels: keyed_lane.hip)
 //   k_pubkey / k_sign : RFC 8032 key generation and signing (synthetic data)
 //
 // Memory layout (HBM):
@@ -82,70 +85,6 @@ __global__ __launch_bounds__(64, CMTV_VERIFY_WAVES_PER_EU) void k_verify(uint32_
   if (threadIdx.x == 0 && out_bitmap) out_bitmap[gid >> 6] = mask;
 }
 
-// One signature per quad of lanes (quad.h): for batches too small to fill the
-// chip at one signature per lane, this cuts per-signature latency ~2x.
-// Verdict bits: lane 0 of each quad votes in a ballot; the 16 quad bits of a
-// wave are compacted into one 16-bit slice of the bitmap.
-
-template <uint32_t MODE>
-__global__ __launch_bounds__(64, CMTV_QUAD_WAVES_PER_EU) void k_verify_quad(uint32_t n, const uint32_t* __restrict__ pk,
-                                                       const uint32_t* __restrict__ sig,
-                                                       const uint8_t* __restrict__ msg,
-                                                       const uint32_t* __restrict__ off,
-                                                       const uint32_t* __restrict__ btab,
-                                                       uint8_t* __restrict__ out_valid,
-                                                       uint64_t* __restrict__ out_bitmap, uint32_t force_wide) {
-  const uint32_t gid = blockIdx.x * 64 + threadIdx.x;
-  const uint32_t s = gid >> 2;
-  const bool active = s < n;
-  const uint32_t i = active ? s : n - 1;
-  const uint32_t m0 = off[i], m1 = off[i + 1];
-  DevQuad q;
-  DevBTabQ bt{btab};
-  __shared__ uint2 tab_lds[2 * 9 * 5 * 64];  // (0..8)(-A), (0..8)(-/+R): 45 KiB per wave
-  DevATabQ ta{tab_lds, threadIdx.x}, tr{tab_lds + 9 * 5 * 64, threadIdx.x};
-  bool v = q_verify<MODE>(q, pk + 8 * (size_t)i, sig + 16 * (size_t)i, msg + m0, m1 - m0, bt, ta, tr, NullProbe(),
-                          force_wide != 0);
-  v = v && active;
-  if (active && (threadIdx.x & 3) == 0 && out_valid) out_valid[s] = v ? 1 : 0;
-  uint64_t x = __ballot(v && (threadIdx.x & 3) == 0) & 0x1111111111111111ull;
-  x = (x | (x >> 3)) & 0x0303030303030303ull;
-  x = (x | (x >> 6)) & 0x000F000F000F000Full;
-  x = (x | (x >> 12)) & 0x000000FF000000FFull;
-  x = (x | (x >> 24)) & 0xFFFFull;
-  if (threadIdx.x == 0 && out_bitmap) reinterpret_cast<uint16_t*>(out_bitmap)[gid >> 6] = (uint16_t)x;
-}
-
-// One signature per oct of lanes (oct.h): the quad verifier's Straus chain
-// split over two quads, for batches that leave SIMDs idle. Verdict bits:
-// lane 0 of each oct votes; a wave's 8 bits are one byte of the bitmap.
-template <uint32_t MODE>
-__global__ __launch_bounds__(64, CMTV_QUAD_WAVES_PER_EU) void k_verify_oct(uint32_t n, const uint32_t* __restrict__ pk,
-                                                      const uint32_t* __restrict__ sig,
-                                                      const uint8_t* __restrict__ msg,
-                                                      const uint32_t* __restrict__ off,
-                                                      const uint32_t* __restrict__ btab,
-                                                      uint8_t* __restrict__ out_valid,
-                                                      uint64_t* __restrict__ out_bitmap, uint32_t force_wide) {
-  const uint32_t gid = blockIdx.x * 64 + threadIdx.x;
-  const uint32_t s = gid >> 3;
-  const bool active = s < n;
-  const uint32_t i = active ? s : n - 1;
-  const uint32_t m0 = off[i], m1 = off[i + 1];
-  DevOct q;
-  DevBTabQ bt{btab};
-  __shared__ uint2 tab_lds[9 * 5 * 64];  // each lane: its quad's (0..8)P coordinate, 22.5 KiB per wave
-  DevATabQ ta{tab_lds, threadIdx.x};
-  bool v = o_verify<MODE>(q, pk + 8 * (size_t)i, sig + 16 * (size_t)i, msg + m0, m1 - m0, bt, ta, force_wide != 0);
-  v = v && active;
-  if (active && (threadIdx.x & 7) == 0 && out_valid) out_valid[s] = v ? 1 : 0;
-  uint64_t x = __ballot(v && (threadIdx.x & 7) == 0) & 0x0101010101010101ull;
-  x = (x | (x >> 7)) & 0x0003000300030003ull;
-  x = (x | (x >> 14)) & 0x0000000F0000000Full;
-  x = (x | (x >> 28)) & 0xFFull;
-  if (threadIdx.x == 0 && out_bitmap) reinterpret_cast<uint8_t*>(out_bitmap)[gid >> 6] = (uint8_t)x;
-}
-
 struct LdsBytes {
   uint8_t* p;
   __device__ __forceinline__ void put(uint32_t pos, uint8_t b) { p[pos] = b; }
@@ -194,15 +133,7 @@ __device__ __forceinline__ void helper_message(const SbFuse& sb, uint32_t i, con
   }
 }
 
-// The quad verifier with a helper wave: a 4-wave workgroup takes 48
-// signatures; waves 0-2 are quad waves (16 signatures each) and wave 3 hashes
-// and splits the scalars of all 48 (one lane each, q_prepare) while they
-// decompress A and R; the scalars reach them through LDS at one barrier and
-// wave 3 exits. LDS (3 x 45 KiB tables + 5 KiB of scalars) allows one
-// workgroup per CU, i.e. 4 waves on its 4 SIMDs, and 256 workgroups =
-// 12,288 signatures per round: the same capacity as the one-wave quad kernel
-// (3 x 45 KiB per CU), with the hash and the Euclid off every quad wave.
-// Phase probe of the helper-wave quad kernel (tools/phase_probe.py): built
+// Phase probe of the helper-wave kernels (tools/phase_probe.py): built
 // only into a separate library with -DCMTV_PHASE_PROBE; lane 0 of every wave
 // of the first 4,096 workgroups records the shader clock at fixed points
 // (0 entry, 1/2 before/after barrier 1, 3/4 before/after barrier 2, 5 exit).
@@ -235,80 +166,14 @@ __device__ uint64_t g_phase[4096 * 4 * kPhaseSlots];
 #define CMTV_CLOCK() 0ull
 #endif
 
-template <uint32_t MODE>
-__global__ __launch_bounds__(256, CMTV_QUAD_WAVES_PER_EU) void k_verify_quad_split(
-    uint32_t n, const uint32_t* __restrict__ pk, const uint32_t* __restrict__ sig, const uint8_t* __restrict__ msg,
-    const uint32_t* __restrict__ off, const uint32_t* __restrict__ btab, uint8_t* __restrict__ out_valid,
-    uint64_t* __restrict__ out_bitmap, uint32_t force_wide, SbFuse sb) {
-  const uint32_t wave = threadIdx.x >> 6, t = threadIdx.x & 63;
-  const uint32_t base = blockIdx.x * 48;
-  __shared__ uint32_t prep[48][SIG_PREP_WORDS + 1];
-  __shared__ uint32_t bpt[48][40];  // [u]B in the quads' cached coordinates
-  __shared__ uint2 tab_lds[3][2 * 9 * 5 * 64];
-  __shared__ uint32_t sbm[48][kSbFuseMaxMsg / 4];  // fused sign-bytes
-  CMTV_STAMP(0);
-  if (wave == 3) {
-    const uint32_t slot = t < 48 ? t : 47;
-    const uint32_t s = base + slot;
-    const uint32_t i = s < n ? s : n - 1;
-    const uint8_t* mp;
-    uint32_t ml;
-    helper_message(sb, i, msg, off, sbm[slot], mp, ml);
-    SigPrep p;
-    q_prepare<MODE>(p, pk + 8 * (size_t)i, sig + 16 * (size_t)i, mp, ml, force_wide != 0);
-    if (t < 48) sig_prep_store(prep[t], p);
-    CMTV_STAMP(1);
-    __syncthreads();  // 1: the scalars, as the quad waves finish decoding
-    CMTV_STAMP(2);
-    ge_p3 B;
-    q_bcomb16(B, p.u, DevBTab{btab});
-    if (t < 48) bpoint_store(bpt[t], B);
-    CMTV_STAMP(3);
-    __syncthreads();  // 2: [u]B, before the quad waves' last addition
-    CMTV_STAMP(4);
-    return;
-  }
-  const uint32_t ls = wave * 16 + (t >> 2);
-  const uint32_t s = base + ls;
-  const bool active = s < n;
-  const uint32_t i = active ? s : n - 1;
-  DevQuad q;
-  DevBTabQ bt{btab};
-  DevATabQ ta{tab_lds[wave], t}, tr{tab_lds[wave] + 9 * 5 * 64, t};
-  const uint32_t* bq = &bpt[ls][10 * (t & 3)];
-  bool v = q_verify_split<MODE, true>(
-      q, pk + 8 * (size_t)i, sig + 16 * (size_t)i, bt, ta, tr,
-      [&](SigPrep& p) {
-        CMTV_STAMP(1);
-        __syncthreads();
-        CMTV_STAMP(2);
-        sig_prep_load(p, prep[ls]);
-      },
-      [&](fe& c) {
-        CMTV_STAMP(3);
-        __syncthreads();
-        CMTV_STAMP(4);
-#pragma unroll
-        for (int j = 0; j < 10; j++) c.v[j] = bq[j];
-      });
-  CMTV_STAMP(5);
-  v = v && active;
-  if (active && (t & 3) == 0 && out_valid) out_valid[s] = v ? 1 : 0;
-  uint64_t x = __ballot(v && (t & 3) == 0) & 0x1111111111111111ull;
-  x = (x | (x >> 3)) & 0x0303030303030303ull;
-  x = (x | (x >> 6)) & 0x000F000F000F000Full;
-  x = (x | (x >> 12)) & 0x000000FF000000FFull;
-  x = (x | (x >> 24)) & 0xFFFFull;
-  // one 16-bit slice per quad wave; the grid's last workgroup may run past
-  // the bitmap's words
-  const uint32_t slice = blockIdx.x * 3 + wave;
-  if (t == 0 && out_bitmap && slice < 4 * ((n + 63) / 64)) reinterpret_cast<uint16_t*>(out_bitmap)[slice] = (uint16_t)x;
-}
-
-// The helper-summed quad verifier (quad.h q_verify_hs, hs_helper.h): the
-// workgroup and its first barrier as k_verify_quad_split, but the quads build
-// both tables before it (extended points), and then the helper wave, instead
-// of idling after [u]B, sums every window's two table entries for its 48
+// The helper-summed quad verifier (quad.h q_verify_hs, hs_helper.h): a 4-wave
+// workgroup takes 48 signatures; waves 0-2 are quad waves (16 signatures
+// each) and wave 3 hashes and splits the scalars of all 48 (one lane each,
+// q_prepare, the templated sign-bytes included) while they decompress A and R
+// and build both tables (extended points); the scalars reach them at barrier
+// 1. LDS (3 x 45 KiB tables + scalars + the window ring) allows one workgroup
+// per CU, i.e. 4 waves on its 4 SIMDs: 256 workgroups = 12,288 signatures per
+// round. After barrier 1 the helper wave sums every window's two table entries for its 48
 // signatures (h_window_addend, one per lane) and hands the sums over through a
 // 2-slot LDS ring, one barrier per window: the quads' windows lose one of
 // their two additions. [u]B: while the quads build their tables the helper
@@ -677,108 +542,6 @@ __global__ __launch_bounds__(256, 1) void k_verify_row_split(
   if (out_bitmap && active) row_bitmap_add(slot, s, n, v, out_bitmap, t);
 }
 
-// The row verifier over two waves per signature (row.h r_part / r_join),
-// one signature per workgroup and CU, for batches of at most 256 (one
-// round): wave 0 decodes A and runs [k1](-A), wave 1 decodes R and runs
-// [|k2|](+/-R) -- 4 doublings and one addition per window each, instead of
-// one wave's two additions -- while wave 2 (the helper) hashes and splits
-// the scalars and computes [u]B. Wave 1 hands its sum (cached) and R's
-// flags over at barrier 2; wave 0 adds it and [u]B and checks. Bitmap as
-// k_verify_row_split (the A waves count).
-template <uint32_t MODE>
-__global__ __launch_bounds__(192, 1) void k_verify_row2_split(
-    uint32_t n, const uint32_t* __restrict__ pk, const uint32_t* __restrict__ sig, const uint8_t* __restrict__ msg,
-    const uint32_t* __restrict__ off, const uint32_t* __restrict__ btab, uint8_t* __restrict__ out_valid,
-    uint64_t* __restrict__ out_bitmap, uint32_t force_wide, SbFuse sb, RowSlot slot) {
-  const uint32_t wave = threadIdx.x >> 6, t = threadIdx.x & 63;
-  const uint32_t s = blockIdx.x;
-  const uint32_t i = s < n ? s : n - 1;
-  __shared__ uint32_t prep[SIG_PREP_WORDS + 1];
-  __shared__ uint32_t bpt[32];
-  __shared__ uint32_t brows[16 * BTAB_ROW_WORDS];  // the helper's [u]B comb rows
-  __shared__ uint32_t bpts[8 * 40];                // ... and its partial sums
-  __shared__ uint32_t tab_lds[2][kRowTabWords / 2];
-  __shared__ uint32_t sbm[kSbFuseMaxMsg / 4];
-  __shared__ uint32_t xr[64 + 2];  // R's sum (cached), its decode flag and x = 0
-  const uint32_t* pkp = pk + 8 * (size_t)i;
-  const uint32_t* sgp = sig + 16 * (size_t)i;
-  CMTV_STAMP(0);
-  if (wave == 2) {
-    const uint8_t* mp;
-    uint32_t ml;
-    helper_message(sb, i, msg, off, sbm, mp, ml);
-    SigPrep p;
-    {
-      // q_prepare's steps, stamped apart in the probe build
-      uint32_t w[16];
-      load_words(w, sgp + 8, 2);
-      const bool s_ok = (w[7] & 0xE0000000u) == 0 && sc_is_canonical(w);
-      uint32_t ts[8], k[8], h[16];
-#pragma unroll
-      for (int j = 0; j < 8; j++) ts[j] = w[j];
-      load_words(w, sgp, 2);
-      load_words(w + 8, pkp, 2);
-      sha512_prefixed<16>(h, w, mp, ml);
-      sc_reduce512(k, h);
-      CMTV_STAMP(5);
-      q_prepare_scalars<true>(p, k, ts, force_wide != 0, MODE != MODE_ZIP215);
-      p.flags |= s_ok ? 4u : 0u;
-    }
-    if (t == 0) sig_prep_store(prep, p);
-    CMTV_STAMP(1);
-    __syncthreads();  // 1: the scalars
-    CMTV_STAMP(2);
-    ge_p3 B;
-    helper_bcomb_prefetched(B, p.u, btab, brows, bpts, t);
-    if (t == 0) bpoint_store_bytes(bpt, B);
-    CMTV_STAMP(3);
-    __syncthreads();  // 2: [u]B and R's sum
-    CMTV_STAMP(4);
-    return;
-  }
-  const uint32_t* src = wave ? sgp : pkp;
-  const uint32_t limb = reinterpret_cast<const uint16_t*>(src)[t & 15];
-  const bool sign = (src[7] >> 31) != 0;
-  const RowCtx<DevRow> x(DevRow::lane());
-  DevRowTab tab{tab_lds[wave], t};
-  SigPrep p;
-  bool dec, x0;
-  auto stamp = [&](int k) { CMTV_STAMP(k); (void)k; };
-  auto get_prep = [&](SigPrep& q) {
-    CMTV_STAMP(1);
-    __syncthreads();
-    CMTV_STAMP(2);
-    sig_prep_load(q, prep);
-  };
-  if (wave == 1) {
-    const uint32_t v = r_part<1>(x, limb, sign, tab, get_prep, p, dec, x0, stamp);
-    xr[t] = rp_to_cached(x, v, x.cst(RowConst::d2));
-    if (t == 0) {
-      xr[64] = dec ? 1u : 0u;
-      xr[65] = x0 ? 1u : 0u;
-    }
-    CMTV_STAMP(3);
-    __syncthreads();  // 2
-    CMTV_STAMP(4);
-    return;
-  }
-  const uint32_t v = r_part<0>(x, limb, sign, tab, get_prep, p, dec, x0, stamp);
-  CMTV_STAMP(3);
-  __syncthreads();  // 2
-  CMTV_STAMP(4);
-  uint32_t sigw[8];
-  load_words(sigw, sgp, 2);
-  const bool r_dec = xr[64] != 0, r_x0 = xr[65] != 0;
-  const bool r_canon = y_is_canonical(sigw) && !(r_x0 && (sigw[7] >> 31) != 0);
-  const uint32_t cb = (bpt[8 * (t >> 4) + ((t & 15) >> 1)] >> (16 * (t & 1))) & 0xFFFFu;
-  bool v_ok = r_join<MODE>(x, v, xr[t], cb, (p.flags & 4u) != 0 && dec && r_dec, r_canon);
-  CMTV_STAMP(5);
-  const bool active = s < n;
-  v_ok = v_ok && active;
-  if (t == 0 && active && out_valid) out_valid[s] = v_ok ? 1 : 0;
-  if (out_bitmap && active) row_bitmap_add(slot, s, n, v_ok, out_bitmap, t);
-}
-
 // The row verifier over four waves per signature (row.h r_sum_ar / r_part<·,
 // kRowLoWindows> / r_join4), one signature per workgroup and CU, for batches
 // of at most 256: wave 0 (lo) decodes A and R and runs the lowest 21
@@ -1041,35 +804,6 @@ __global__ __launch_bounds__(128) void k_comb_build(const uint32_t* __restrict__
   comb_build_column(tabs + (size_t)key * COMB_TABLE_WORDS, A, (int)threadIdx.x + 1, sc);
 }
 
-// One signature per quad of lanes by registered key (keyed_quad.h), for
-// latency-bound batches; 16 signatures per 64-lane block.
-template <uint32_t MODE>
-__global__ __launch_bounds__(64, 1) void k_verify_keyed_quad(
-    uint32_t n, uint32_t n_keys, const uint32_t* __restrict__ key_idx, const uint32_t* __restrict__ sig,
-    const uint8_t* __restrict__ msg, const uint32_t* __restrict__ off, const uint32_t* __restrict__ keys_pk,
-    const uint8_t* __restrict__ keys_ok, const uint32_t* __restrict__ ktabs, const uint32_t* __restrict__ bcomb,
-    uint8_t* __restrict__ out_valid, uint64_t* __restrict__ out_bitmap) {
-  const uint32_t gid = blockIdx.x * 64 + threadIdx.x;
-  const uint32_t s = gid >> 2;
-  const bool active = s < n;
-  const uint32_t i = active ? s : n - 1;
-  const uint32_t m0 = off[i], m1 = off[i + 1];
-  uint32_t kid = key_idx[i];
-  const bool kin = kid < n_keys;
-  kid = kin ? kid : 0;
-  DevQuad q;
-  bool v = q_verify_keyed<MODE>(q, keys_pk + 8 * (size_t)kid, kin && keys_ok[kid] != 0, sig + 16 * (size_t)i,
-                                msg + m0, m1 - m0, ktabs + (size_t)kid * COMB_TABLE_WORDS, bcomb);
-  v = v && active;
-  if (active && (threadIdx.x & 3) == 0 && out_valid) out_valid[s] = v ? 1 : 0;
-  uint64_t x = __ballot(v && (threadIdx.x & 3) == 0) & 0x1111111111111111ull;
-  x = (x | (x >> 3)) & 0x0303030303030303ull;
-  x = (x | (x >> 6)) & 0x000F000F000F000Full;
-  x = (x | (x >> 12)) & 0x000000FF000000FFull;
-  x = (x | (x >> 24)) & 0xFFFFull;
-  if (threadIdx.x == 0 && out_bitmap) reinterpret_cast<uint16_t*>(out_bitmap)[gid >> 6] = (uint16_t)x;
-}
-
 __global__ __launch_bounds__(64) void k_pubkey(uint32_t n, const uint32_t* __restrict__ seeds,
                                                const uint32_t* __restrict__ btab, uint32_t* __restrict__ out_pk) {
   const uint32_t gid = blockIdx.x * 64 + threadIdx.x;
@@ -1109,7 +843,7 @@ hipError_t launch_verify(uint32_t mode, uint32_t n, const void* pk, const void* 
                          const void* off, const uint32_t* btab, uint32_t* atab, void* valid, void* bitmap,
                          uint32_t kflags, hipStream_t s, const SbFuse* sb, const RowSlot* row_slot) {
   const SbFuse fz = sb ? *sb : SbFuse{};
-  const bool quad = kflags & kLaunchQuad;
+  const uint32_t form = kflags & kFormMask;
   const uint32_t fw = (kflags & kLaunchForceWide) ? 1u : 0u;
   if (n == 0) return hipSuccess;
   auto pkp = static_cast<const uint32_t*>(pk);
@@ -1119,100 +853,57 @@ hipError_t launch_verify(uint32_t mode, uint32_t n, const void* pk, const void* 
   auto vp = static_cast<uint8_t*>(valid);
   auto bp = static_cast<uint64_t*>(bitmap);
   const RowSlot rs = row_slot ? *row_slot : RowSlot{};
-  if (kflags & kLaunchRow4) {
-    // one signature per 256-lane block (lo, A-hi, R-hi, the helper)
-    if (n > kRowMaxCap || (bp && !rs.words)) return hipErrorInvalidValue;
-    const dim3 grid(n), block(256);
-    if (mode == MODE_ZIP215)
-      hipLaunchKernelGGL(k_verify_row4_split<MODE_ZIP215>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp, fw,
-                         fz, rs);
-    else
-      hipLaunchKernelGGL(k_verify_row4_split<MODE_GO_STDLIB>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp,
-                         fw, fz, rs);
-    return hipGetLastError();
-  }
-  if (kflags & kLaunchRow2) {
-    // one signature per 192-lane block (an A wave, an R wave, the helper)
-    if (n > kRowMaxCap || (bp && !rs.words)) return hipErrorInvalidValue;
-    const dim3 grid(n), block(192);
-    if (mode == MODE_ZIP215)
-      hipLaunchKernelGGL(k_verify_row2_split<MODE_ZIP215>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp, fw,
-                         fz, rs);
-    else
-      hipLaunchKernelGGL(k_verify_row2_split<MODE_GO_STDLIB>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp,
-                         fw, fz, rs);
-    return hipGetLastError();
-  }
-  if (kflags & kLaunchRow) {
-    // 3 signatures per 256-lane block (3 row waves + the helper)
-    if (n > kRowMaxCap || (bp && !rs.words)) return hipErrorInvalidValue;
-    const dim3 grid((n + 2) / 3), block(256);
-    if (mode == MODE_ZIP215)
-      hipLaunchKernelGGL(k_verify_row_split<MODE_ZIP215>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp, fw,
-                         fz, rs);
-    else
-      hipLaunchKernelGGL(k_verify_row_split<MODE_GO_STDLIB>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp,
-                         fw, fz, rs);
-    return hipGetLastError();
-  }
-  if (quad && (kflags & kLaunchOctSplit)) {
-    // one 128-lane block (2 waves) = 8 signatures; whole groups of 8 blocks
-    const dim3 grid(((n + 63) / 64) * 8), block(128);
-    if (mode == MODE_ZIP215)
-      hipLaunchKernelGGL(k_verify_oct_split<MODE_ZIP215>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp, fw,
-                         fz);
-    else
-      hipLaunchKernelGGL(k_verify_oct_split<MODE_GO_STDLIB>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp,
-                         fw, fz);
-    return hipGetLastError();
-  }
-  if (quad && (kflags & kLaunchOct)) {
-    // one 64-lane block = 8 signatures; whole groups of 8 blocks so every
-    // byte of every bitmap word is written
-    const dim3 grid(((n + 63) / 64) * 8), block(64);
-    if (mode == MODE_ZIP215)
-      hipLaunchKernelGGL(k_verify_oct<MODE_ZIP215>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp, fw);
-    else
-      hipLaunchKernelGGL(k_verify_oct<MODE_GO_STDLIB>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp, fw);
-    return hipGetLastError();
-  }
-  if (quad && (kflags & kLaunchQuadSplit)) {
-    // 48 signatures per 256-lane block; enough blocks for every 16-bit slice
-    // of every bitmap word
-    const uint32_t slices = 4 * ((n + 63) / 64);
-    const dim3 grid((slices + 2) / 3), block(256);
-    if (kflags & kLaunchQuadHS) {
-      if (mode == MODE_ZIP215)
-        hipLaunchKernelGGL(k_verify_quad_hs<MODE_ZIP215>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp, fw, fz,
-                           kflags >> 16);
+  const bool go = mode != MODE_ZIP215;
+  if ((form == kFormRow4 || form == kFormRow) && (n > kRowMaxCap || (bp && !rs.words))) return hipErrorInvalidValue;
+  if (form != kFormLane && form != kFormQuad && form != kFormOct2 && form != kFormRow && form != kFormRow4)
+    return hipErrorInvalidValue;
+  if (fz.tmpls && form == kFormLane) return hipErrorInvalidValue;
+  switch (form) {
+    case kFormRow4:  // one signature per 256-lane block (lo, A-hi, R-hi, the helper)
+      if (go)
+        hipLaunchKernelGGL(k_verify_row4_split<MODE_GO_STDLIB>, dim3(n), dim3(256), 0, s, n, pkp, sgp, mp, op, btab,
+                           vp, bp, fw, fz, rs);
       else
+        hipLaunchKernelGGL(k_verify_row4_split<MODE_ZIP215>, dim3(n), dim3(256), 0, s, n, pkp, sgp, mp, op, btab, vp,
+                           bp, fw, fz, rs);
+      break;
+    case kFormRow:  // 3 signatures per 256-lane block (3 row waves + the helper)
+      if (go)
+        hipLaunchKernelGGL(k_verify_row_split<MODE_GO_STDLIB>, dim3((n + 2) / 3), dim3(256), 0, s, n, pkp, sgp, mp, op,
+                           btab, vp, bp, fw, fz, rs);
+      else
+        hipLaunchKernelGGL(k_verify_row_split<MODE_ZIP215>, dim3((n + 2) / 3), dim3(256), 0, s, n, pkp, sgp, mp, op,
+                           btab, vp, bp, fw, fz, rs);
+      break;
+    case kFormOct2:  // one 128-lane block (2 waves) = 8 signatures; whole groups of 8 blocks
+      if (go)
+        hipLaunchKernelGGL(k_verify_oct_split<MODE_GO_STDLIB>, dim3(((n + 63) / 64) * 8), dim3(128), 0, s, n, pkp, sgp,
+                           mp, op, btab, vp, bp, fw, fz);
+      else
+        hipLaunchKernelGGL(k_verify_oct_split<MODE_ZIP215>, dim3(((n + 63) / 64) * 8), dim3(128), 0, s, n, pkp, sgp,
+                           mp, op, btab, vp, bp, fw, fz);
+      break;
+    case kFormQuad: {
+      // 48 signatures per 256-lane block; enough blocks for every 16-bit
+      // slice of every bitmap word
+      const uint32_t slices = 4 * ((n + 63) / 64);
+      const dim3 grid((slices + 2) / 3), block(256);
+      if (go)
         hipLaunchKernelGGL(k_verify_quad_hs<MODE_GO_STDLIB>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp, fw,
                            fz, kflags >> 16);
-      return hipGetLastError();
+      else
+        hipLaunchKernelGGL(k_verify_quad_hs<MODE_ZIP215>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp, fw, fz,
+                           kflags >> 16);
+      break;
     }
-    if (mode == MODE_ZIP215)
-      hipLaunchKernelGGL(k_verify_quad_split<MODE_ZIP215>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp, fw,
-                         fz);
-    else
-      hipLaunchKernelGGL(k_verify_quad_split<MODE_GO_STDLIB>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp,
-                         fw, fz);
-    return hipGetLastError();
+    default:
+      if (go)
+        hipLaunchKernelGGL(k_verify<MODE_GO_STDLIB>, dim3(blocks_for(n)), dim3(64), 0, s, n, pkp, sgp, mp, op, btab,
+                           atab, vp, bp);
+      else
+        hipLaunchKernelGGL(k_verify<MODE_ZIP215>, dim3(blocks_for(n)), dim3(64), 0, s, n, pkp, sgp, mp, op, btab, atab,
+                           vp, bp);
   }
-  if (quad) {
-    // one 64-lane block = 16 signatures; whole groups of 4 blocks so every
-    // 16-bit slice of every bitmap word is written
-    const dim3 grid(((n + 63) / 64) * 4), block(64);
-    if (mode == MODE_ZIP215)
-      hipLaunchKernelGGL(k_verify_quad<MODE_ZIP215>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp, fw);
-    else
-      hipLaunchKernelGGL(k_verify_quad<MODE_GO_STDLIB>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp, fw);
-    return hipGetLastError();
-  }
-  const dim3 grid(blocks_for(n)), block(64);
-  if (mode == MODE_ZIP215)
-    hipLaunchKernelGGL(k_verify<MODE_ZIP215>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, atab, vp, bp);
-  else
-    hipLaunchKernelGGL(k_verify<MODE_GO_STDLIB>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, atab, vp, bp);
   return hipGetLastError();
 }
 
@@ -1240,12 +931,11 @@ hipError_t launch_comb_build(uint32_t n_keys, const void* keys_pk, uint8_t* keys
 // counts itself in diag[kDiagLateK] (cmtv_stats.late_k_waves). k_wait = 0
 // (the CMTV_FORCE_K_LATE test knob) skips the flag entirely, so every quad
 // wave takes that path.
-template <uint32_t MODE, bool B16>
+template <uint32_t MODE>
 __global__ __launch_bounds__(320, 1) void k_verify_keyed_quad_split(
     uint32_t n, uint32_t n_keys, const uint32_t* __restrict__ key_idx, const uint32_t* __restrict__ sig,
     const uint8_t* __restrict__ msg, const uint32_t* __restrict__ off, const uint32_t* __restrict__ keys_pk,
-    const uint8_t* __restrict__ keys_ok, const uint32_t* __restrict__ ktabs, const uint32_t* __restrict__ bcomb,
-    uint8_t* __restrict__ out_valid, uint64_t* __restrict__ out_bitmap, uint32_t k_wait, uint32_t* __restrict__ diag,
+    const uint8_t* __restrict__ keys_ok, const uint32_t* __restrict__ ktabs, uint8_t* __restrict__ out_valid, uint64_t* __restrict__ out_bitmap, uint32_t k_wait, uint32_t* __restrict__ diag,
     const uint32_t* __restrict__ btab, SbFuse sb) {
   const uint32_t wave = threadIdx.x >> 6, t = threadIdx.x & 63;
   const uint32_t base = blockIdx.x * 48;
@@ -1300,8 +990,9 @@ __global__ __launch_bounds__(320, 1) void k_verify_keyed_quad_split(
   kid = kin ? kid : 0;
   DevQuad q;
   const int lane = (int)(t & 3);
-  bool v = q_verify_keyed_split<MODE, B16>(
-      q, kin && keys_ok[kid] != 0, sig + 16 * (size_t)i, ktabs + (size_t)kid * COMB_TABLE_WORDS, bcomb,
+  // [s]B over the B table's radix-2^16 comb (16 additions)
+  bool v = q_verify_keyed_split<MODE, true>(
+      q, kin && keys_ok[kid] != 0, sig + 16 * (size_t)i, ktabs + (size_t)kid * COMB_TABLE_WORDS, nullptr,
       [&](uint32_t tk[8]) {
         // the hash helper's flag, polled at most k_wait times (a wave never
         // spins forever)
@@ -1349,64 +1040,48 @@ __global__ __launch_bounds__(320, 1) void k_verify_keyed_quad_split(
 
 hipError_t launch_verify_keyed(uint32_t mode, uint32_t n, uint32_t n_keys, const void* key_idx, const void* sig,
                                const void* msg, const void* off, const uint32_t* keys_pk, const uint8_t* keys_ok,
-                               const uint32_t* ktabs, const uint32_t* bcomb, void* valid, void* bitmap,
-                               bool quad, bool split, uint32_t k_wait, uint32_t* diag, uint32_t batch_kb,
-                               uint32_t* scr, const uint32_t* wtabs, const uint32_t* btab, bool wide_dma,
-                               hipStream_t s, const RowSlot* row_slot, bool mixed, const SbFuse* sbp) {
+                               const uint32_t* ktabs, void* valid, void* bitmap, uint32_t form, uint32_t k_wait,
+                               uint32_t* diag, uint32_t batch_kb, uint32_t* scr, const uint32_t* wtabs,
+                               const uint32_t* btab, hipStream_t s, const RowSlot* row_slot, const SbFuse* sbp) {
   if (n == 0) return hipSuccess;
   const SbFuse sb = sbp ? *sbp : SbFuse{};
-  // fused sign-bytes only in the forms whose helper wave hashes (row, quad split)
-  if (sb.tmpls && !row_slot && !(quad && split)) return hipErrorInvalidValue;
+  // fused sign-bytes and identity keys only in the forms whose helper wave
+  // hashes (row, quad)
+  if ((sb.tmpls || !key_idx) && form == kKeyedLane) return hipErrorInvalidValue;
+  if (form == kKeyedRow && (n > kRowMaxCap || (bitmap && !(row_slot && row_slot->words))))
+    return hipErrorInvalidValue;
   auto ki = static_cast<const uint32_t*>(key_idx);
   auto sgp = static_cast<const uint32_t*>(sig);
   auto mp = static_cast<const uint8_t*>(msg);
   auto op = static_cast<const uint32_t*>(off);
   auto vp = static_cast<uint8_t*>(valid);
   auto bp = static_cast<uint64_t*>(bitmap);
-  if (row_slot) {
-    // the keyed row kernel: one signature per 256-lane block
-    if (n > kRowMaxCap) return hipErrorInvalidValue;
-    if (mode == MODE_ZIP215)
-      hipLaunchKernelGGL(k_verify_keyed_row_split<MODE_ZIP215>, dim3(n), dim3(256), 0, s, n, n_keys, ki, sgp, mp, op,
-                         keys_pk, keys_ok, ktabs, btab, vp, bp, *row_slot, sb);
-    else
+  const bool go = mode != MODE_ZIP215;
+  if (form == kKeyedRow) {
+    // one signature per 256-lane block
+    const RowSlot rs = row_slot ? *row_slot : RowSlot{};
+    if (go)
       hipLaunchKernelGGL(k_verify_keyed_row_split<MODE_GO_STDLIB>, dim3(n), dim3(256), 0, s, n, n_keys, ki, sgp, mp,
-                         op, keys_pk, keys_ok, ktabs, btab, vp, bp, *row_slot, sb);
+                         op, keys_pk, keys_ok, ktabs, btab, vp, bp, rs, sb);
+    else
+      hipLaunchKernelGGL(k_verify_keyed_row_split<MODE_ZIP215>, dim3(n), dim3(256), 0, s, n, n_keys, ki, sgp, mp, op,
+                         keys_pk, keys_ok, ktabs, btab, vp, bp, rs, sb);
     return hipGetLastError();
   }
-  if (quad && split) {
+  if (form == kKeyedQuad) {
     const uint32_t slices = 4 * ((n + 63) / 64);
     const dim3 grid((slices + 2) / 3), block(320);
-    // [s]B over the B table's radix-2^16 comb (16 additions) unless the
-    // caller asked for the radix-256 comb (CMTV_KEYED_MIXED=0: 32)
-    if (mixed && btab) {
-      if (mode == MODE_ZIP215)
-        hipLaunchKernelGGL((k_verify_keyed_quad_split<MODE_ZIP215, true>), grid, block, 0, s, n, n_keys, ki, sgp, mp,
-                           op, keys_pk, keys_ok, ktabs, bcomb, vp, bp, k_wait, diag, btab, sb);
-      else
-        hipLaunchKernelGGL((k_verify_keyed_quad_split<MODE_GO_STDLIB, true>), grid, block, 0, s, n, n_keys, ki, sgp,
-                           mp, op, keys_pk, keys_ok, ktabs, bcomb, vp, bp, k_wait, diag, btab, sb);
-    } else if (mode == MODE_ZIP215) {
-      hipLaunchKernelGGL((k_verify_keyed_quad_split<MODE_ZIP215, false>), grid, block, 0, s, n, n_keys, ki, sgp, mp,
-                         op, keys_pk, keys_ok, ktabs, bcomb, vp, bp, k_wait, diag, btab, sb);
-    } else {
-      hipLaunchKernelGGL((k_verify_keyed_quad_split<MODE_GO_STDLIB, false>), grid, block, 0, s, n, n_keys, ki, sgp,
-                         mp, op, keys_pk, keys_ok, ktabs, bcomb, vp, bp, k_wait, diag, btab, sb);
-    }
-    return hipGetLastError();
-  }
-  if (quad) {
-    const dim3 grid(((n + 63) / 64) * 4), block(64);
-    if (mode == MODE_ZIP215)
-      hipLaunchKernelGGL(k_verify_keyed_quad<MODE_ZIP215>, grid, block, 0, s, n, n_keys, ki, sgp, mp, op, keys_pk,
-                         keys_ok, ktabs, bcomb, vp, bp);
+    if (go)
+      hipLaunchKernelGGL(k_verify_keyed_quad_split<MODE_GO_STDLIB>, grid, block, 0, s, n, n_keys, ki, sgp, mp, op,
+                         keys_pk, keys_ok, ktabs, vp, bp, k_wait, diag, btab, sb);
     else
-      hipLaunchKernelGGL(k_verify_keyed_quad<MODE_GO_STDLIB>, grid, block, 0, s, n, n_keys, ki, sgp, mp, op, keys_pk,
-                         keys_ok, ktabs, bcomb, vp, bp);
+      hipLaunchKernelGGL(k_verify_keyed_quad_split<MODE_ZIP215>, grid, block, 0, s, n, n_keys, ki, sgp, mp, op,
+                         keys_pk, keys_ok, ktabs, vp, bp, k_wait, diag, btab, sb);
     return hipGetLastError();
   }
-  return launch_verify_keyed_lane(mode, n, n_keys, ki, sgp, mp, op, keys_pk, keys_ok, ktabs, bcomb, vp, bp, batch_kb,
-                                  scr, wtabs, btab, wide_dma, mixed, s);
+  if (form != kKeyedLane) return hipErrorInvalidValue;
+  return launch_verify_keyed_lane(mode, n, n_keys, ki, sgp, mp, op, keys_pk, keys_ok, ktabs, vp, bp, batch_kb, scr,
+                                  wtabs, btab, s);
 }
 
 hipError_t launch_pubkey(uint32_t n, const void* seeds, const uint32_t* btab, void* out_pk, hipStream_t s) {

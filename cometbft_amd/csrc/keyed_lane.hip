@@ -5,17 +5,17 @@
 //   k_verify_keyed_batch<MODE, KB, COMB> KB signatures per lane sharing one inversion
 //   k_wide_bases / k_wide_build         the wide combs of a key set
 //
-// COMB selects the tables: kComb256 = the radix-256 combs (64 additions from
-// MALL-resident 512 KiB combs); kCombWide = the radix-2^16 combs read by
-// plain loads (32 additions; the key rows come from HBM, 64 MiB per key);
-// kCombWideDma = the same with each addition's two rows staged into LDS one
-// addition ahead by LDS-DMA (global_load_lds_dwordx4), so the HBM latency of
-// the next rows overlaps the current addition instead of stalling it
-// (profiles/r03_c3w_pmc_sq.txt: the plain wide kernel waits on memory 38 % of
-// its wave cycles at two waves per SIMD, the register file being full);
-// kCombMixed = the keys' radix-256 combs with B over the B table's radix-2^16
-// comb (48 additions: keyed.h keyed_comb_mixed), for key sets without wide
-// combs (too many keys for 64 MiB each).
+// COMB selects the tables: kCombWideDma = the radix-2^16 combs (32 additions;
+// the key rows come from HBM, 64 MiB per key) with each addition's two rows
+// staged into LDS one addition ahead by LDS-DMA (global_load_lds_dwordx4), so
+// the HBM latency of the next rows overlaps the current addition instead of
+// stalling it (profiles/r03_c3w_pmc_sq.txt: read by plain loads, the wide
+// kernel waited on memory 38 % of its wave cycles at two waves per SIMD, the
+// register file being full); kCombMixed = the keys' radix-256 combs (MALL-
+// resident 512 KiB each) with B over the B table's radix-2^16 comb (48
+// additions: keyed.h keyed_comb_mixed), for key sets without wide combs. (The
+// plain-load wide form and the all-radix-256 form, 64 additions, were retired
+// in round 5: no dispatch reached them.)
 #include <hip/hip_runtime.h>
 
 #include "devtables.h"
@@ -28,7 +28,7 @@
 
 namespace cmtv {
 
-enum { kComb256 = 0, kCombWide = 1, kCombWideDma = 2, kCombMixed = 3 };
+enum { kCombWideDma = 2, kCombMixed = 3 };
 
 // ---------------------------------------------------------------- LDS staging
 //
@@ -142,25 +142,18 @@ __device__ __forceinline__ bool keyed_comb_wide_dma(ge_p3& acc, const uint32_t* 
 }
 
 // R' = [s]B - [k]A of one signature by registered key kid over the tables
-// COMB selects: ktabs = the key combs (radix-256, or wide for kCombWide*),
-// bcomb = the comb of B (kComb256) or the B table whose BC16 blocks are B's
-// radix-2^16 comb (kCombWide*).
+// COMB selects: ktabs = the key combs (wide for kCombWideDma, else radix-256),
+// btab = the B table, whose BC16 blocks are B's radix-2^16 comb.
 template <int COMB>
 __device__ __forceinline__ bool keyed_comb_dev(ge_p3& acc, uint32_t kid, bool key_ok,
                                                const uint32_t* __restrict__ keys_pk, const uint32_t* sig_ptr,
                                                const uint8_t* msg, uint32_t mlen, const uint32_t* __restrict__ ktabs,
-                                               const uint32_t* __restrict__ bcomb, uint32_t* stage) {
+                                               const uint32_t* __restrict__ btab, uint32_t* stage) {
   if (COMB == kCombWideDma)
     return keyed_comb_wide_dma(acc, keys_pk + 8 * (size_t)kid, key_ok, sig_ptr, msg, mlen,
-                               ktabs + (size_t)kid * WIDE_TABLE_WORDS, bcomb, stage);
-  if (COMB == kCombWide)
-    return keyed_comb_wide<DevCombWindow>(acc, keys_pk + 8 * (size_t)kid, key_ok, sig_ptr, msg, mlen,
-                                          ktabs + (size_t)kid * WIDE_TABLE_WORDS, DevBTab{bcomb});
-  if (COMB == kCombMixed)
-    return keyed_comb_mixed<DevCombWindow>(acc, keys_pk + 8 * (size_t)kid, key_ok, sig_ptr, msg, mlen,
-                                           ktabs + (size_t)kid * COMB_TABLE_WORDS, DevBTab{bcomb});
-  return keyed_comb<DevCombWindow>(acc, keys_pk + 8 * (size_t)kid, key_ok, sig_ptr, msg, mlen,
-                                   ktabs + (size_t)kid * COMB_TABLE_WORDS, bcomb);
+                               ktabs + (size_t)kid * WIDE_TABLE_WORDS, btab, stage);
+  return keyed_comb_mixed<DevCombWindow>(acc, keys_pk + 8 * (size_t)kid, key_ok, sig_ptr, msg, mlen,
+                                         ktabs + (size_t)kid * COMB_TABLE_WORDS, DevBTab{btab});
 }
 
 // this wave's LDS stage (kCombWideDma only; one wave per workgroup)
@@ -173,7 +166,7 @@ template <uint32_t MODE, int COMB>
 __global__ __launch_bounds__(64, CMTV_KEYED_WAVES_PER_EU) void k_verify_keyed(
     uint32_t n, uint32_t n_keys, const uint32_t* __restrict__ key_idx, const uint32_t* __restrict__ sig,
     const uint8_t* __restrict__ msg, const uint32_t* __restrict__ off, const uint32_t* __restrict__ keys_pk,
-    const uint8_t* __restrict__ keys_ok, const uint32_t* __restrict__ ktabs, const uint32_t* __restrict__ bcomb,
+    const uint8_t* __restrict__ keys_ok, const uint32_t* __restrict__ ktabs, const uint32_t* __restrict__ btab,
     uint8_t* __restrict__ out_valid, uint64_t* __restrict__ out_bitmap) {
   CMTV_KEYED_STAGE
   const uint32_t gid = blockIdx.x * 64 + threadIdx.x;
@@ -185,7 +178,7 @@ __global__ __launch_bounds__(64, CMTV_KEYED_WAVES_PER_EU) void k_verify_keyed(
   kid = kin ? kid : 0;
   ge_p3 acc;
   const bool ok = keyed_comb_dev<COMB>(acc, kid, kin && keys_ok[kid] != 0, keys_pk, sig + 16 * (size_t)i, msg + m0,
-                                       m1 - m0, ktabs, bcomb, stage_);
+                                       m1 - m0, ktabs, btab, stage_);
   bool v = check_R<MODE>(acc, sig + 16 * (size_t)i) && ok;
   v = v && active;
   if (active && out_valid) out_valid[gid] = v ? 1 : 0;
@@ -211,7 +204,7 @@ template <uint32_t MODE, int KB, int COMB>
 __global__ __launch_bounds__(64, CMTV_KEYED_WAVES_PER_EU) void k_verify_keyed_batch(
     uint32_t n, uint32_t n_keys, const uint32_t* __restrict__ key_idx, const uint32_t* __restrict__ sig,
     const uint8_t* __restrict__ msg, const uint32_t* __restrict__ off, const uint32_t* __restrict__ keys_pk,
-    const uint8_t* __restrict__ keys_ok, const uint32_t* __restrict__ ktabs, const uint32_t* __restrict__ bcomb,
+    const uint8_t* __restrict__ keys_ok, const uint32_t* __restrict__ ktabs, const uint32_t* __restrict__ btab,
     uint32_t* __restrict__ scr, uint8_t* __restrict__ out_valid, uint64_t* __restrict__ out_bitmap) {
   CMTV_KEYED_STAGE
   const uint32_t lanes = gridDim.x * 64u, gid = blockIdx.x * 64u + threadIdx.x;
@@ -228,7 +221,7 @@ __global__ __launch_bounds__(64, CMTV_KEYED_WAVES_PER_EU) void k_verify_keyed_ba
     kid = kin ? kid : 0;
     ge_p3 acc;
     bool ok = keyed_comb_dev<COMB>(acc, kid, kin && keys_ok[kid] != 0, keys_pk, sig + 16 * (size_t)i, msg + m0,
-                                   m1 - m0, ktabs, bcomb, stage_);
+                                   m1 - m0, ktabs, btab, stage_);
     fe z, xn;
     uint32_t state = 0;
     if (MODE == MODE_ZIP215) {
@@ -341,19 +334,15 @@ static void launch_lane(uint32_t mode, uint32_t n, uint32_t n_keys, const uint32
 hipError_t launch_verify_keyed_lane(uint32_t mode, uint32_t n, uint32_t n_keys, const uint32_t* ki,
                                     const uint32_t* sgp, const uint8_t* mp, const uint32_t* op,
                                     const uint32_t* keys_pk, const uint8_t* keys_ok, const uint32_t* ktabs,
-                                    const uint32_t* bcomb, uint8_t* vp, uint64_t* bp, uint32_t batch_kb,
-                                    uint32_t* scr, const uint32_t* wtabs, const uint32_t* btab, bool dma,
-                                    bool mixed, hipStream_t s) {
+                                    uint8_t* vp, uint64_t* bp, uint32_t batch_kb, uint32_t* scr,
+                                    const uint32_t* wtabs, const uint32_t* btab, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  if (wtabs && dma)
+  if (!btab) return hipErrorInvalidValue;
+  if (wtabs)
     launch_lane<kCombWideDma>(mode, n, n_keys, ki, sgp, mp, op, keys_pk, keys_ok, wtabs, btab, vp, bp, batch_kb, scr,
                               s);
-  else if (wtabs)
-    launch_lane<kCombWide>(mode, n, n_keys, ki, sgp, mp, op, keys_pk, keys_ok, wtabs, btab, vp, bp, batch_kb, scr, s);
-  else if (mixed && btab)
-    launch_lane<kCombMixed>(mode, n, n_keys, ki, sgp, mp, op, keys_pk, keys_ok, ktabs, btab, vp, bp, batch_kb, scr, s);
   else
-    launch_lane<kComb256>(mode, n, n_keys, ki, sgp, mp, op, keys_pk, keys_ok, ktabs, bcomb, vp, bp, batch_kb, scr, s);
+    launch_lane<kCombMixed>(mode, n, n_keys, ki, sgp, mp, op, keys_pk, keys_ok, ktabs, btab, vp, bp, batch_kb, scr, s);
   return hipGetLastError();
 }
 

@@ -47,49 +47,34 @@ constexpr uint32_t kChunk = 1u << 18;  // signatures per launch (A-table scratch
 // signature, in the lane kernels' scratch buffer
 constexpr uint32_t kKeyedBatchChunk = 1u << 20;
 constexpr uint32_t kKeyedBatchMinWaves = 2048;
-// crossover between the quad (4 lanes / signature) and lane (1 lane / signature)
-// kernels; measured on MI355X, overridable with CMTV_QUAD_MAX. Ed25519: four
-// full rounds of the helper-summed quad kernel (12,288 signatures each) beat
-// the lane kernel up to 49,152 (round 4, profiles/r04_quad_max_ab.txt:
-// 49,152 0.96 vs 1.15 ms; 65,536 1.39 vs 1.25 ms on the lane side); 40,000
-// before. sr25519 keeps 40,000: its quad kernel loses to the lane kernel above
-// it (profiles/r04_sr_quad_max_ab.txt: 40,960-49,152 1.37-1.40 vs 1.24-1.27 ms).
-constexpr size_t kQuadMaxDefault = 49152, kQuadMaxSrDefault = 40000;
-// Ed25519 batches up to this size use the 8-lanes-per-signature kernel
-// (oct.h) in its two-wave form (k_verify_oct_split: 2 waves per 8
-// signatures) while its 8-signature workgroups fit one round on 256 CUs:
-// measured on MI355X (round 4, profiles/r04_oct_hs_crossover.txt) oct2 2,048:
-// 0.209 ms vs the helper-summed quad kernel's 0.218; 3,072 (two workgroups
-// per CU): 0.272 vs 0.221 (the one-wave oct kernel stays reachable with
-// CMTV_OCT_SPLIT_MAX < CMTV_OCT_MAX).
-constexpr size_t kOctMaxDefault = 2048;       // CMTV_OCT_MAX
-// Ed25519 batches up to this size take the one-signature-per-wave row kernel
-// (row.h) where the two-wave oct kernel would run (CMTV_ROW_MAX; 3 signatures
-// per workgroup, two workgroups per CU: 1,536 on 256 CUs). Measured on MI355X
-// (round 4, profiles/r04_row_max_ab.txt, tools/mid_ab.py): at 896-1,536
-// signatures two row workgroups sharing a CU beat the oct kernel by 8-10%
-// (host API: 1,024 0.215 vs 0.235 ms) and 5-6% through VerifyCommit; at 2,048
-// (three per CU) they lose (0.29 vs 0.24 ms). 768 before.
-constexpr size_t kRowMaxDefault = 1536;
-// ... and up to this size its two-waves-per-signature form (one signature
-// per CU: 256 in one round; CMTV_ROW2_MAX)
-constexpr size_t kRow2MaxDefault = 256;
-// registered-key batches up to this size take the keyed row kernel (one
-// signature per workgroup; CMTV_KEYED_ROW_MAX). Measured on MI355X (round 4,
-// profiles/r04_keyed_row_max_ab.txt, tools/keyed_small.py): at 320-512
-// signatures two keyed row workgroups per CU take 0.058-0.062 ms per call
-// against the keyed quad kernel's 0.076; at 640-768 (three per CU) they lose
-// (kernel 0.068-0.071 vs 0.065 ms). 256 before.
-constexpr size_t kKeyedRowMaxDefault = 512;
-constexpr size_t kOctSplitMaxDefault = 2048;  // CMTV_OCT_SPLIT_MAX
-// quad batches up to this size take the helper-wave form (k_verify_quad_split:
-// 256 workgroups x 48 signatures per round); CMTV_QUAD_SPLIT_MAX
-constexpr size_t kQuadSplitMaxDefault = 49152;
-// the crossover for registered-key verification (env CMTV_KEYED_QUAD_MAX):
-// the two-helper keyed quad kernel takes 12,288 signatures per round (0.088,
-// 0.164, 0.242 ms for 1-3 rounds) against the keyed lane kernel's flat
-// 0.28-0.30 ms up to 49k (tools/keyed_sweep.py, profiles/r02_keyed_sweep.json)
-constexpr size_t kKeyedQuadMaxDefault = 36864;
+// The batch-size bands of the verification forms (kernels.h kForm*, picked
+// by ed_form / sr_form / keyed_form below), measured on MI355X in round 4 and
+// frozen since (no more single-band tuning). CMTV_FORM forces one
+// form at every size it can take (tools/*_ab.py use it for A/B runs).
+// Ed25519, per call:
+//   <= 256     kFormRow4  four waves per signature, one round on 256 CUs
+//   <= 1,536   kFormRow   one wave per signature, two workgroups of 3 per CU
+//              (profiles/r04_row_max_ab.txt: 1,024 0.215 vs oct2 0.235 ms;
+//              2,048: 0.29 vs 0.24 ms)
+//   <= 2,048   kFormOct2  eight lanes per signature in two waves
+//              (profiles/r04_oct_hs_crossover.txt: 2,048 0.209 vs quad 0.218;
+//              3,072 0.272 vs 0.221 ms)
+//   <= 49,152  kFormQuad  four rounds of the helper-summed quad kernel
+//              (profiles/r04_quad_max_ab.txt: 49,152 0.96 vs lane 1.15 ms;
+//              65,536 1.39 vs 1.25 ms)
+//   above      kFormLane
+// sr25519: the quad form up to 40,000, the lane form above
+// (profiles/r04_sr_quad_max_ab.txt: 40,960-49,152 1.37-1.40 vs 1.24-1.27 ms).
+// Registered keys:
+//   <= 512     kKeyedRow   (profiles/r04_keyed_row_max_ab.txt: 320-512
+//              0.058-0.062 vs quad 0.076 ms; 640-768 lose)
+//   <= 36,864  kKeyedQuad  (profiles/r02_keyed_sweep.json: 12,288 per round,
+//              0.088/0.164/0.242 ms for 1-3 rounds vs the lane kernel's flat
+//              0.28-0.30 ms up to 49k)
+//   above      kKeyedLane
+constexpr size_t kRow4Max = 256, kRowMax = 1536, kOct2Max = 2048, kQuadMax = 49152, kSrQuadMax = 40000;
+constexpr size_t kKeyedRowMax = 512, kKeyedQuadMax = 36864;
+constexpr uint32_t kNoForm = 0xFF;
 // signatures per device below which a batch is not sharded (env CMTV_SHARD_MIN)
 constexpr size_t kShardMinDefault = 8192;
 // single-device host batches up to this size return their bitmap through
@@ -411,7 +396,6 @@ struct CmtvDev {
   int ordinal = 0;
   hipStream_t stream = nullptr;
   uint32_t* d_btab = nullptr;
-  uint32_t* d_bcomb = nullptr;   // comb of B for registered-key verification (built lazily)
   uint16_t* d_srprog = nullptr;  // sr25519 transcript program (merlin.h)
   DevBuf d_in, d_out, d_all;
   HostBuf h_in, h_out;
@@ -481,22 +465,9 @@ struct cmtv_ctx {
   uint32_t default_mode = CMTV_MODE_GO_STDLIB;
   std::mutex mu;
   cmtv_stats stats{};
-  size_t quad_max = kQuadMaxDefault;  // batches up to this size use the quad kernel
-  size_t sr_quad_max = kQuadMaxSrDefault;  // ... sr25519 batches (CMTV_QUAD_MAX sets both)
-  size_t oct_max = kOctMaxDefault;    // ... and up to this size the oct kernel
-  size_t oct_split_max = kOctSplitMaxDefault;
-  size_t row_max = kRowMaxDefault;
-  size_t row2_max = kRow2MaxDefault;
-  size_t keyed_row_max = kKeyedRowMaxDefault;
-  // waves per signature at or below row2_max: 4 (k_verify_row4_split) or 2
-  // (CMTV_ROW_WAVES=2: k_verify_row2_split)
-  uint32_t row_waves = 4;
-  // the quad split kernel's helper-summed form (k_verify_quad_hs); CMTV_QUAD_HS=0
-  // keeps k_verify_quad_split (the quads add both table entries themselves)
-  bool quad_hs = true;
+  // CMTV_FORM: a form forced at every size it can take (kNoForm: the bands)
+  uint32_t force_form = kNoForm, force_keyed = kNoForm;
   uint32_t hs_tune = 0;  // CMTV_HS_PRE + 1 (bits 0..7); 0: the kernel's default
-  size_t quad_split_max = kQuadSplitMaxDefault;
-  size_t keyed_quad_max = kKeyedQuadMaxDefault;
   size_t lane_chunk = kChunk;         // signatures per lane-kernel launch (env CMTV_LANE_CHUNK)
   size_t shard_min = kShardMinDefault;
   int sr_nops = 0;
@@ -526,17 +497,9 @@ struct cmtv_ctx {
   // polls of the keyed split kernel's quads for the hash helper's k before
   // they hash themselves (CMTV_FORCE_K_LATE=1: 0, every quad wave hashes)
   uint32_t keyed_wait = cmtv::kKeyedWaitDefault;
-  // GO_STDLIB keyed lane launches batch the final inversion (CMTV_KEYED_BATCH=0: off)
-  bool keyed_batch = true;
   // waves a batched launch must keep (CMTV_KEYED_BATCH_MIN_WAVES; 1 batches
   // any size, the test knob that puts the corpus through the batched kernels)
   uint32_t keyed_batch_min_waves = kKeyedBatchMinWaves;
-  // wide-comb lane kernels stage their rows through LDS by LDS-DMA
-  // (keyed_lane.hip kCombWideDma; CMTV_WIDE_DMA=0: plain loads)
-  bool wide_dma = true;
-  // registered keys without wide combs: B over the B table's radix-2^16 comb
-  // (CMTV_KEYED_MIXED=0: over its radix-256 comb, 16 more additions)
-  bool keyed_mixed = true;
   // devices (indices into devs) that take host batches, in shard order; the
   // RCCL communicator (when rccl) spans exactly these, rank = position
   std::vector<size_t> live;
@@ -718,39 +681,38 @@ static hipError_t row_slot_release(cmtv_ctx* ctx, CmtvDev& D, hipStream_t s, uin
   return e;
 }
 
+// The form of a batch of n Ed25519 signatures (the bands above, or CMTV_FORM
+// where the forced form can take n: a row form at most kRowMaxCap in one launch)
+static uint32_t ed_form(const cmtv_ctx* ctx, size_t n) {
+  const uint32_t f = ctx->force_form;
+  if (f != kNoForm && !((f == kFormRow || f == kFormRow4) && n > kRowMaxCap)) return f;
+  return n <= kRow4Max ? kFormRow4 : n <= kRowMax ? kFormRow : n <= kOct2Max ? kFormOct2 : n <= kQuadMax ? kFormQuad
+                                                                                                       : kFormLane;
+}
+
+// ... of sr25519 signatures (the quad and lane forms)
+static uint32_t sr_form(const cmtv_ctx* ctx, size_t n) {
+  const uint32_t f = ctx->force_form;
+  if (f == kFormQuad || f == kFormLane) return f;
+  return n <= kSrQuadMax ? kFormQuad : kFormLane;
+}
+
+// ... and of registered-key signatures
+static uint32_t keyed_form(const cmtv_ctx* ctx, size_t n) {
+  const uint32_t f = ctx->force_keyed;
+  if (f != kNoForm && !(f == kKeyedRow && n > kRowMaxCap)) return f;
+  return n <= kKeyedRowMax ? kKeyedRow : n <= kKeyedQuadMax ? kKeyedQuad : kKeyedLane;
+}
+
+// The forms whose helper wave can write templated sign-bytes itself
+// (kernels.h SbFuse) when they run in one launch (enqueue_verify rejects a
+// fused batch of more than kChunk): every form but the lane kernels. The one
+// predicate enqueue_shard and the enqueue functions use.
+static bool fuse_ok(const cmtv_ctx* ctx, size_t n) { return ed_form(ctx, n) != kFormLane && n <= kChunk; }
+static bool keyed_fuse_ok(const cmtv_ctx* ctx, size_t n) { return keyed_form(ctx, n) != kKeyedLane && n <= kChunk; }
+
 // Enqueue verification of n signatures whose inputs are in device memory of
 // device D (current on this thread).
-// The kernel enqueue_verify picks for n Ed25519 signatures is a helper-wave
-// form (k_verify_oct_split / k_verify_quad_split), whose helper can write
-// templated sign-bytes itself (kernels.h SbFuse).
-static bool split_kernel_for(const cmtv_ctx* ctx, size_t n) {
-  const bool quad = n <= ctx->quad_max;
-  const bool oct = quad && n <= ctx->oct_max;
-  return oct ? n <= ctx->oct_split_max : (quad && n <= ctx->quad_split_max);
-}
-
-// The row kernel replaces the two-wave oct kernel up to CMTV_ROW_MAX (so the
-// oct / quad knobs still force their kernels)
-static bool row_kernel_for(const cmtv_ctx* ctx, size_t n) {
-  return n <= ctx->quad_max && n <= ctx->oct_max && n <= ctx->oct_split_max && n <= ctx->row_max &&
-         n <= kRowMaxCap;
-}
-
-// ... and can write the sign-bytes of all n in its helper waves: a split
-// kernel running in one launch (enqueue_verify rejects a fused batch of more
-// than kChunk, whatever CMTV_QUAD_MAX / CMTV_QUAD_SPLIT_MAX say). The one
-// predicate both enqueue_shard and enqueue_verify use.
-static bool fuse_ok(const cmtv_ctx* ctx, size_t n) { return split_kernel_for(ctx, n) && n <= kChunk; }
-
-// ... and the same for registered keys: the keyed row kernel and the keyed
-// quad split kernel (one launch each) hash in a helper wave that can write
-// the templated sign-bytes itself (kernels.hip helper_message)
-static bool keyed_fuse_ok(const cmtv_ctx* ctx, size_t n) {
-  const bool quad = n <= ctx->keyed_quad_max;
-  const bool krow = quad && n <= ctx->keyed_row_max && n <= kRowMaxCap;
-  return krow || (quad && n <= ctx->quad_split_max && n <= kChunk);
-}
-
 static int enqueue_verify(cmtv_ctx* ctx, CmtvDev& D, size_t n, const uint8_t* d_pk, const uint8_t* d_sig,
                           const uint8_t* d_msg, const uint32_t* d_off, uint32_t mode, uint8_t* d_valid,
                           uint64_t* d_bitmap, hipStream_t s, const SbFuse* sb = nullptr, Scratch* scr = nullptr) {
@@ -759,23 +721,17 @@ static int enqueue_verify(cmtv_ctx* ctx, CmtvDev& D, size_t n, const uint8_t* d_
   if (fault_hit(ctx) || D.inject_fault) return CMTV_EHIP;
   // fused sign-bytes only where the split kernels run, in one launch
   if (sb && (mode == kModeSr25519 || !fuse_ok(ctx, n))) return CMTV_EINVAL;
-  // Small batches cannot fill the chip at one signature per lane: use the
-  // 4-lanes-per-signature kernel below the crossover (quad.h,
-  // sr25519_quad.h).
+  // Small batches cannot fill the chip at one signature per lane: more lanes
+  // per signature below the bands' crossovers (quad.h, oct.h, row.h,
+  // sr25519_quad.h)
   const bool sr = mode == kModeSr25519;
-  const bool quad = n <= (sr ? ctx->sr_quad_max : ctx->quad_max);
-  const bool oct = quad && !sr && n <= ctx->oct_max;
-  const bool oct_split = oct && n <= ctx->oct_split_max;
-  const bool quad_split = quad && !oct && n <= ctx->quad_split_max;
-  const bool row = !sr && row_kernel_for(ctx, n);
-  const bool row2 = row && n <= ctx->row2_max;
-  const uint32_t kflags = (quad ? kLaunchQuad : 0u) | (oct ? kLaunchOct : 0u) |
-                          (oct_split ? kLaunchOctSplit : 0u) | (quad_split ? kLaunchQuadSplit : 0u) |
-                          (quad_split && ctx->quad_hs ? kLaunchQuadHS | (ctx->hs_tune << 16) : 0u) |
-                          (row ? (row2 ? (ctx->row_waves == 4 ? kLaunchRow4 : kLaunchRow2) : kLaunchRow) : 0u) |
+  const uint32_t form = sr ? sr_form(ctx, n) : ed_form(ctx, n);
+  const bool lane = form == kFormLane;
+  const bool row = form == kFormRow || form == kFormRow4;
+  const uint32_t kflags = form | (form == kFormQuad ? ctx->hs_tune << 16 : 0u) |
                           (ctx->force_wide ? kLaunchForceWide : 0u);
   hipError_t e = hipSuccess;
-  if (!quad) {
+  if (lane) {
     const size_t lanes = std::min<size_t>(n, ctx->lane_chunk);
     const size_t lanes_padded = (lanes + 63) / 64 * 64;
     if ((e = acquire_scratch(S, lanes_padded * kAtabWordsPerLane * sizeof(uint32_t), s)) != hipSuccess)
@@ -789,7 +745,7 @@ static int enqueue_verify(cmtv_ctx* ctx, CmtvDev& D, size_t n, const uint8_t* d_
   Timing::Pair tp;
   const bool timed = ctx->timing_every && D.timing_seq++ % ctx->timing_every == 0;
   if (timed && (e = D.timing.begin(tp, s)) != hipSuccess) return hip_fail(e);
-  const size_t chunk = quad ? kChunk : ctx->lane_chunk;
+  const size_t chunk = lane ? ctx->lane_chunk : kChunk;
   for (size_t c = 0; c < n; c += chunk) {
     const uint32_t cn = (uint32_t)std::min<size_t>(chunk, n - c);
     if (sr)
@@ -808,7 +764,7 @@ static int enqueue_verify(cmtv_ctx* ctx, CmtvDev& D, size_t n, const uint8_t* d_
     ctx->stats.kernel_launches++;
     D.launches++;
   }
-  if (!quad && (e = release_scratch(S, s)) != hipSuccess) return hip_fail(e);
+  if (lane && (e = release_scratch(S, s)) != hipSuccess) return hip_fail(e);
   if (timed && (e = D.timing.end(tp, s)) != hipSuccess) return hip_fail(e);
   ctx->stats.calls++;
   ctx->stats.signatures += n;
@@ -820,31 +776,6 @@ static int enqueue_verify(cmtv_ctx* ctx, CmtvDev& D, size_t n, const uint8_t* d_
 // keys per comb-build launch (prefix-product scratch = 160 KiB per key)
 constexpr uint32_t kCombKeyChunk = 256;
 
-// Comb of B (keyed.h) on device D, built on first use; caller holds the
-// context lock and D is current.
-static int ensure_bcomb(CmtvDev& D) {
-  if (D.d_bcomb) return CMTV_OK;
-  const uint32_t bw[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
-                          0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};
-  DevBuf scratch, bpk;
-  uint32_t* tab = nullptr;
-  hipError_t e = hipMalloc(&tab, kCombWords * sizeof(uint32_t));
-  if (e == hipSuccess) e = scratch.ensure(kCombScratchWordsPerKey * sizeof(uint32_t));
-  if (e == hipSuccess) e = bpk.ensure(sizeof(bw));
-  if (e == hipSuccess) e = hipMemcpyAsync(bpk.p, bw, sizeof(bw), hipMemcpyHostToDevice, D.stream);
-  if (e == hipSuccess)
-    e = launch_comb_build(1, bpk.p, nullptr, tab, static_cast<uint32_t*>(scratch.p), false, D.stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(D.stream);
-  scratch.release();
-  bpk.release();
-  if (e != hipSuccess) {
-    if (tab) (void)hipFree(tab);
-    return hip_fail(e);
-  }
-  D.d_bcomb = tab;
-  return CMTV_OK;
-}
-
 static int enqueue_verify_keyed(cmtv_ctx* ctx, CmtvDev& D, const cmtv_keyset::PerDev& K, size_t n_keys, size_t n,
                                 const uint32_t* d_idx, const uint8_t* d_sig, const uint8_t* d_msg,
                                 const uint32_t* d_off, uint32_t mode, uint8_t* d_valid, uint64_t* d_bitmap,
@@ -854,10 +785,10 @@ static int enqueue_verify_keyed(cmtv_ctx* ctx, CmtvDev& D, const cmtv_keyset::Pe
   if (sb && !keyed_fuse_ok(ctx, n)) return CMTV_EINVAL;
   if (!d_idx && !sb) return CMTV_EINVAL;  // identity keys only in the one-launch fused forms
   if (fault_hit(ctx) || D.inject_fault) return CMTV_EHIP;
-  const bool quad = n <= ctx->keyed_quad_max;
+  const uint32_t form = keyed_form(ctx, n);
   // lane launches: KB signatures per lane sharing one inversion while that
   // still gives two waves per SIMD (k_verify_keyed_batch; ZIP-215 by coset)
-  const bool batch = !quad && ctx->keyed_batch;
+  const bool batch = form == kKeyedLane;
   // batched launches of kKeyedBatchChunk = 2^20 signatures: one full round
   // of 2,048 waves at KB = 8 (equal launches of 1.07M measured 53.9 ms for
   // configs[2]'s 15M against 37.8 ms: 2,093 waves start a second, nearly
@@ -878,9 +809,8 @@ static int enqueue_verify_keyed(cmtv_ctx* ctx, CmtvDev& D, const cmtv_keyset::Pe
     if ((e = acquire_scratch(S, lanes * kb0 * kKeyedBatchScratchWordsPerSig * sizeof(uint32_t), s)) != hipSuccess)
       return hip_fail(e);
   }
-  // the keyed row kernel up to CMTV_KEYED_ROW_MAX (below the keyed quad
-  // knob): one chunk, one slot of the bitmap ring
-  const bool krow = quad && n <= ctx->keyed_row_max && n <= kRowMaxCap;
+  // the keyed row kernel: one chunk, one slot of the bitmap ring
+  const bool krow = form == kKeyedRow;
   RowSlot slot;
   uint32_t slot_k = 0;
   if (krow && (e = row_slot_acquire(ctx, D, s, d_bitmap != nullptr, slot, slot_k)) != hipSuccess)
@@ -893,12 +823,11 @@ static int enqueue_verify_keyed(cmtv_ctx* ctx, CmtvDev& D, const cmtv_keyset::Pe
     const uint32_t cn = (uint32_t)std::min<size_t>(chunk, n - c);
     // a chunk never needs more scratch than the first (kb and lanes shrink together)
     const uint32_t kb = kb0 > 1 ? kb_for(cn) : 1;
-    e = launch_verify_keyed(mode, cn, (uint32_t)n_keys, d_idx + c, d_sig + 64 * c, d_msg, d_off + c, K.d_pk, K.d_ok,
-                            K.d_tab, D.d_bcomb, d_valid ? d_valid + c : nullptr,
-                            d_bitmap ? d_bitmap + c / 64 : nullptr, quad, n <= ctx->quad_split_max,
-                            ctx->keyed_wait, D.d_diag, kb, static_cast<uint32_t*>(S.buf.p),
-                            quad ? nullptr : K.d_wide, D.d_btab, ctx->wide_dma, s, krow ? &slot : nullptr,
-                            ctx->keyed_mixed, sb);
+    e = launch_verify_keyed(mode, cn, (uint32_t)n_keys, d_idx ? d_idx + c : nullptr, d_sig + 64 * c, d_msg,
+                            d_off + c, K.d_pk, K.d_ok, K.d_tab, d_valid ? d_valid + c : nullptr,
+                            d_bitmap ? d_bitmap + c / 64 : nullptr, form, ctx->keyed_wait, D.d_diag, kb,
+                            static_cast<uint32_t*>(S.buf.p), form == kKeyedLane ? K.d_wide : nullptr, D.d_btab, s,
+                            krow ? &slot : nullptr, sb);
     if (e == hipSuccess && krow) e = row_slot_release(ctx, D, s, slot_k);
     if (e != hipSuccess) {
       D.timing.abandon(tp);
@@ -1600,14 +1529,12 @@ static void release_device(CmtvDev& D) {
   D.d_tags = nullptr;
   D.h_zin.release();
   if (D.d_btab) (void)hipFree(D.d_btab);
-  if (D.d_bcomb) (void)hipFree(D.d_bcomb);
   if (D.d_srprog) (void)hipFree(D.d_srprog);
   if (D.d_diag) (void)hipFree(D.d_diag);
   D.d_diag = nullptr;
   if (D.d_rowslots) (void)hipFree(D.d_rowslots);
   D.d_rowslots = nullptr;
   D.d_btab = nullptr;
-  D.d_bcomb = nullptr;
   D.d_srprog = nullptr;
   D.timing.release();
   for (uint32_t k = 0; k < kRowSlots; k++) {
@@ -1626,24 +1553,44 @@ static void release_device(CmtvDev& D) {
   D.stream = nullptr;
 }
 
+// CMTV_FORM: comma-separated form names, a debug knob for tests and A/B runs
+// (every other size keeps its band): row4 | row | oct2 | quad | lane (Ed25519;
+// quad and lane also sr25519) and krow | kquad | klane (registered keys). An
+// unknown name is reported once on stderr and ignored.
+static void parse_forms(cmtv_ctx* ctx, const char* v) {
+  static const struct {
+    const char* name;
+    bool keyed;
+    uint32_t form;
+  } kNames[] = {{"row4", false, kFormRow4}, {"row", false, kFormRow},   {"oct2", false, kFormOct2},
+                {"quad", false, kFormQuad}, {"lane", false, kFormLane}, {"krow", true, kKeyedRow},
+                {"kquad", true, kKeyedQuad}, {"klane", true, kKeyedLane}};
+  std::string list(v);
+  size_t p = 0;
+  while (p <= list.size()) {
+    size_t q = list.find(',', p);
+    if (q == std::string::npos) q = list.size();
+    const std::string tok = list.substr(p, q - p);
+    p = q + 1;
+    if (tok.empty()) continue;
+    bool known = false;
+    for (const auto& k : kNames)
+      if (tok == k.name) {
+        (k.keyed ? ctx->force_keyed : ctx->force_form) = k.form;
+        known = true;
+      }
+    if (!known) std::fprintf(stderr, "cmtverify: CMTV_FORM: unknown form '%s' ignored\n", tok.c_str());
+  }
+}
+
 static void read_env(cmtv_ctx* ctx) {
-  if (const char* qm = std::getenv("CMTV_QUAD_MAX")) ctx->quad_max = ctx->sr_quad_max = (size_t)std::strtoull(qm, nullptr, 10);
-  if (const char* om = std::getenv("CMTV_OCT_MAX")) ctx->oct_max = (size_t)std::strtoull(om, nullptr, 10);
-  if (const char* rm = std::getenv("CMTV_ROW_MAX")) ctx->row_max = (size_t)std::strtoull(rm, nullptr, 10);
-  if (const char* rm = std::getenv("CMTV_ROW2_MAX")) ctx->row2_max = (size_t)std::strtoull(rm, nullptr, 10);
-  if (const char* rm = std::getenv("CMTV_KEYED_ROW_MAX"))
-    ctx->keyed_row_max = (size_t)std::strtoull(rm, nullptr, 10);
-  if (const char* rw = std::getenv("CMTV_ROW_WAVES")) ctx->row_waves = rw[0] == '2' ? 2u : 4u;
-  if (const char* qh = std::getenv("CMTV_QUAD_HS")) ctx->quad_hs = qh[0] != '0';
+  if (const char* f = std::getenv("CMTV_FORM")) parse_forms(ctx, f);
   if (const char* hp = std::getenv("CMTV_HS_PRE")) {
     // 0..16 comb positions; anything else keeps the kernel's default
     char* end = nullptr;
     const long v = std::strtol(hp, &end, 10);
     if (end != hp && *end == 0 && v >= 0 && v <= 16) ctx->hs_tune = (uint32_t)(v + 1);
   }
-  if (const char* os = std::getenv("CMTV_OCT_SPLIT_MAX")) ctx->oct_split_max = (size_t)std::strtoull(os, nullptr, 10);
-  if (const char* qs = std::getenv("CMTV_QUAD_SPLIT_MAX")) ctx->quad_split_max = (size_t)std::strtoull(qs, nullptr, 10);
-  if (const char* kq = std::getenv("CMTV_KEYED_QUAD_MAX")) ctx->keyed_quad_max = (size_t)std::strtoull(kq, nullptr, 10);
   if (const char* lc = std::getenv("CMTV_LANE_CHUNK")) {
     const size_t v = (size_t)std::strtoull(lc, nullptr, 10) / 64 * 64;
     if (v >= 64 && v <= kChunk) ctx->lane_chunk = v;
@@ -1659,9 +1606,6 @@ static void read_env(cmtv_ctx* ctx) {
   if (const char* zm = std::getenv("CMTV_ZC_MAX")) ctx->zc_max = (size_t)std::strtoull(zm, nullptr, 10);
   if (const char* hp = std::getenv("CMTV_HOST_POLL")) ctx->host_poll = std::atoi(hp) != 0;
   if (const char* kl = std::getenv("CMTV_FORCE_K_LATE")) ctx->keyed_wait = kl[0] == '1' ? 0u : kKeyedWaitDefault;
-  if (const char* kb = std::getenv("CMTV_KEYED_BATCH")) ctx->keyed_batch = kb[0] != '0';
-  if (const char* wd = std::getenv("CMTV_WIDE_DMA")) ctx->wide_dma = wd[0] != '0';
-  if (const char* km = std::getenv("CMTV_KEYED_MIXED")) ctx->keyed_mixed = km[0] != '0';
   if (const char* mw = std::getenv("CMTV_KEYED_BATCH_MIN_WAVES")) {
     const long v = std::strtol(mw, nullptr, 10);
     if (v >= 1 && v <= (1l << 20)) ctx->keyed_batch_min_waves = (uint32_t)v;
@@ -2180,11 +2124,6 @@ int register_keys_locked(cmtv_ctx* ctx, size_t n_keys, const uint8_t* pk, cmtv_k
     auto& K = ks->dev[g];
     if (D.failed) continue;  // retired: never given work again
     (void)hipSetDevice(D.ordinal);
-    int rc = ensure_bcomb(D);
-    if (rc != CMTV_OK) {
-      cmtv_keyset_free(ks);
-      return rc;
-    }
     DevBuf scratch;
     hipError_t e = hipMalloc(&K.d_pk, 32 * n_keys);
     if (e == hipSuccess) e = hipMalloc(&K.d_ok, n_keys);

@@ -2,9 +2,9 @@
 // verification (BASELINE configs[4]; reference path
 // /root/reference/crypto/sr25519/pubkey.go:34-60).
 //
-//   k_verify_sr25519_quad: one signature per quad of lanes (sr25519_quad.h),
-//     half-size scalars and 34 shared windows like the Ed25519 quad kernel;
-//     the runtime uses it below the same batch-size crossover
+//   k_verify_sr25519_quad_hs: one signature per quad of lanes (sr25519_quad.h)
+//     and a helper wave, half-size scalars and shared windows like the Ed25519
+//     helper-summed quad kernel; the runtime uses it below the crossover
 //   k_verify_sr25519: one signature per lane (sr25519.h): merlin transcript
 //     interpreted from a byte-code program with the Keccak state in LDS,
 //     ristretto255 decoding of A and R, Straus [s]B - [k]A over the Ed25519
@@ -60,102 +60,6 @@ __global__ __launch_bounds__(64, 2) void k_verify_sr25519(uint32_t n, const uint
   if (active && out_valid) out_valid[gid] = v ? 1 : 0;
   const uint64_t mask = __ballot(v);
   if (threadIdx.x == 0 && out_bitmap) out_bitmap[gid >> 6] = mask;
-}
-
-// One signature per quad of lanes (sr25519_quad.h): 16 signatures per wave;
-// the LDS holds the quad tables (45 KiB) and, before they are built, the
-// lanes' STROBE states (12.5 KiB) in the same space.
-__global__ __launch_bounds__(64, 1) void k_verify_sr25519_quad(uint32_t n, const uint32_t* __restrict__ pk,
-                                                               const uint32_t* __restrict__ sig,
-                                                               const uint8_t* __restrict__ msg,
-                                                               const uint32_t* __restrict__ off,
-                                                               const uint32_t* __restrict__ btab,
-                                                               const uint16_t* __restrict__ prog, int nops,
-                                                               uint8_t* __restrict__ out_valid,
-                                                               uint64_t* __restrict__ out_bitmap,
-                                                               uint32_t force_wide) {
-  __shared__ uint2 tab_lds[2 * 9 * 5 * 64];  // (0..8)(-A), (0..8)(-/+R); STROBE states first
-  const uint32_t s = blockIdx.x * 16 + (threadIdx.x >> 2);
-  const bool active = s < n;
-  const uint32_t i = active ? s : n - 1;
-  const uint32_t m0 = off[i], m1 = off[i + 1];
-  DevQuad q;
-  DevBTabQ bt{btab};
-  DevATabQ ta{tab_lds, threadIdx.x}, tr{tab_lds + 9 * 5 * 64, threadIdx.x};
-  LdsStrobeState st{reinterpret_cast<uint32_t*>(tab_lds), threadIdx.x};
-  bool v = q_verify_sr(q, pk + 8 * (size_t)i, sig + 16 * (size_t)i, msg + m0, m1 - m0, prog, nops, st, bt, ta, tr,
-                       NullProbe(), force_wide != 0);
-  v = v && active;
-  if (active && (threadIdx.x & 3) == 0 && out_valid) out_valid[s] = v ? 1 : 0;
-  // compact bit 4j -> bit j (16 verdicts of this wave); 4 consecutive blocks
-  // fill one 64-bit bitmap word, each writes its 16-bit slice
-  uint64_t x = __ballot(v && (threadIdx.x & 3) == 0) & 0x1111111111111111ull;
-  x = (x | (x >> 3)) & 0x0303030303030303ull;
-  x = (x | (x >> 6)) & 0x000F000F000F000Full;
-  x = (x | (x >> 12)) & 0x000000FF000000FFull;
-  x = (x | (x >> 24)) & 0xFFFFull;
-  if (threadIdx.x == 0 && out_bitmap) reinterpret_cast<uint16_t*>(out_bitmap)[blockIdx.x] = (uint16_t)x;
-}
-
-// The sr25519 quad verifier with a helper wave (kernels.hip
-// k_verify_quad_split): 3 quad waves (48 signatures) + 1 wave running the
-// merlin transcript and the half-size split of all 48 (sr_prepare, one lane
-// each, its STROBE states in their own 12.5 KiB of LDS).
-__global__ __launch_bounds__(256, 1) void k_verify_sr25519_quad_split(
-    uint32_t n, const uint32_t* __restrict__ pk, const uint32_t* __restrict__ sig, const uint8_t* __restrict__ msg,
-    const uint32_t* __restrict__ off, const uint32_t* __restrict__ btab, const uint16_t* __restrict__ prog, int nops,
-    uint8_t* __restrict__ out_valid, uint64_t* __restrict__ out_bitmap, uint32_t force_wide) {
-  const uint32_t wave = threadIdx.x >> 6, t = threadIdx.x & 63;
-  const uint32_t base = blockIdx.x * 48;
-  __shared__ uint32_t prep[48][SIG_PREP_WORDS + 1];
-  __shared__ uint2 tab_lds[3][2 * 9 * 5 * 64];
-  // the helper's STROBE states, then (once every lane's transcript is done)
-  // [u]B in the quads' cached coordinates, 48 x 40 words
-  __shared__ uint32_t strobe[50 * 64];
-  uint32_t(*bpt)[40] = reinterpret_cast<uint32_t(*)[40]>(strobe);
-  if (wave == 3) {
-    const uint32_t s = base + (t < 48 ? t : 47);
-    const uint32_t i = s < n ? s : n - 1;
-    const uint32_t m0 = off[i], m1 = off[i + 1];
-    LdsStrobeState st{strobe, t};
-    SigPrep p;
-    sr_prepare(p, pk + 8 * (size_t)i, sig + 16 * (size_t)i, msg + m0, m1 - m0, prog, nops, st, force_wide != 0);
-    if (t < 48) sig_prep_store(prep[t], p);
-    __syncthreads();  // 1: the scalars
-    ge_p3 B;
-    q_bcomb16(B, p.u, DevBTab{btab});
-    if (t < 48) bpoint_store(bpt[t], B);  // the STROBE states are dead by now
-    __syncthreads();  // 2: [u]B
-    return;
-  }
-  const uint32_t ls = wave * 16 + (t >> 2);
-  const uint32_t s = base + ls;
-  const bool active = s < n;
-  const uint32_t i = active ? s : n - 1;
-  DevQuad q;
-  DevBTabQ bt{btab};
-  DevATabQ ta{tab_lds[wave], t}, tr{tab_lds[wave] + 9 * 5 * 64, t};
-  const uint32_t* bq = &bpt[ls][10 * (t & 3)];
-  bool v = q_verify_sr_split<true>(
-      q, pk + 8 * (size_t)i, sig + 16 * (size_t)i, bt, ta, tr,
-      [&](SigPrep& p) {
-        __syncthreads();
-        sig_prep_load(p, prep[ls]);
-      },
-      [&](fe& c) {
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < 10; j++) c.v[j] = bq[j];
-      });
-  v = v && active;
-  if (active && (t & 3) == 0 && out_valid) out_valid[s] = v ? 1 : 0;
-  uint64_t x = __ballot(v && (t & 3) == 0) & 0x1111111111111111ull;
-  x = (x | (x >> 3)) & 0x0303030303030303ull;
-  x = (x | (x >> 6)) & 0x000F000F000F000Full;
-  x = (x | (x >> 12)) & 0x000000FF000000FFull;
-  x = (x | (x >> 24)) & 0xFFFFull;
-  const uint32_t slice = blockIdx.x * 3 + wave;
-  if (t == 0 && out_bitmap && slice < 4 * ((n + 63) / 64)) reinterpret_cast<uint16_t*>(out_bitmap)[slice] = (uint16_t)x;
 }
 
 // The helper-summed form (kernels.hip k_verify_quad_hs, hs_helper.h): the
@@ -232,8 +136,8 @@ hipError_t launch_verify_sr25519(uint32_t n, const void* pk, const void* sig, co
                                  const uint32_t* btab, uint32_t* atab, const uint16_t* prog, int nops, void* valid,
                                  void* bitmap, uint32_t kflags, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  const bool quad = kflags & kLaunchQuad;
-  if (quad && (kflags & kLaunchQuadSplit) && (kflags & kLaunchQuadHS)) {
+  const uint32_t form = kflags & kFormMask;
+  if (form == kFormQuad) {
     const uint32_t slices = 4 * ((n + 63) / 64);
     hipLaunchKernelGGL(k_verify_sr25519_quad_hs, dim3((slices + 2) / 3), dim3(256), 0, s, n,
                        static_cast<const uint32_t*>(pk), static_cast<const uint32_t*>(sig),
@@ -242,25 +146,7 @@ hipError_t launch_verify_sr25519(uint32_t n, const void* pk, const void* sig, co
                        (kflags & kLaunchForceWide) ? 1u : 0u, kflags >> 16);
     return hipGetLastError();
   }
-  if (quad && (kflags & kLaunchQuadSplit)) {
-    const uint32_t slices = 4 * ((n + 63) / 64);
-    hipLaunchKernelGGL(k_verify_sr25519_quad_split, dim3((slices + 2) / 3), dim3(256), 0, s, n,
-                       static_cast<const uint32_t*>(pk), static_cast<const uint32_t*>(sig),
-                       static_cast<const uint8_t*>(msg), static_cast<const uint32_t*>(off), btab, prog, nops,
-                       static_cast<uint8_t*>(valid), static_cast<uint64_t*>(bitmap),
-                       (kflags & kLaunchForceWide) ? 1u : 0u);
-    return hipGetLastError();
-  }
-  if (quad) {
-    // one 64-lane block = 16 signatures; whole groups of 4 blocks so every
-    // 16-bit slice of every bitmap word is written
-    hipLaunchKernelGGL(k_verify_sr25519_quad, dim3(((n + 63) / 64) * 4), dim3(64), 0, s, n,
-                       static_cast<const uint32_t*>(pk), static_cast<const uint32_t*>(sig),
-                       static_cast<const uint8_t*>(msg), static_cast<const uint32_t*>(off), btab, prog, nops,
-                       static_cast<uint8_t*>(valid), static_cast<uint64_t*>(bitmap),
-                       (kflags & kLaunchForceWide) ? 1u : 0u);
-    return hipGetLastError();
-  }
+  if (form != kFormLane) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_verify_sr25519, dim3((n + 63) / 64), dim3(64), 0, s, n, static_cast<const uint32_t*>(pk),
                      static_cast<const uint32_t*>(sig), static_cast<const uint8_t*>(msg),
                      static_cast<const uint32_t*>(off), btab, atab, prog, nops, static_cast<uint8_t*>(valid),

@@ -124,7 +124,7 @@ def test_verify_sharded_single_rank(gpu_ctx):
 
 @pytest.mark.parametrize("n", [49152, 49153])
 def test_default_dispatch_at_the_quad_lane_crossover(gpu_ctx, n):
-    """The default context on both sides of CMTV_QUAD_MAX (49,152: four
+    """The default context on both sides of kQuadMax (49,152: four
     rounds of the helper-summed quad kernel; one more signature takes the lane
     kernel), Go mode, 1% flipped signatures, verdict bytes and bitmap against
     the oracle."""

@@ -257,13 +257,13 @@ def test_device_sign_bytes_templating(monkeypatch, chain, fuse):
         monkeypatch.setenv("CMTV_NO_SB_FUSE", "1")
     gpu_ctx = Context(device=0)
     # registered keys: the keyed row (16 signatures) and keyed quad split
-    # (CMTV_KEYED_ROW_MAX=0) kernels' hash helpers write the bytes themselves
+    # (CMTV_FORM=kquad) kernels' hash helpers write the bytes themselves
     keyed = Context(device=0)
     keyed.keyset_cache(4)
-    monkeypatch.setenv("CMTV_KEYED_ROW_MAX", "0")
+    monkeypatch.setenv("CMTV_FORM", "kquad")
     keyed_q = Context(device=0)
     keyed_q.keyset_cache(4)
-    monkeypatch.delenv("CMTV_KEYED_ROW_MAX", raising=False)
+    monkeypatch.delenv("CMTV_FORM", raising=False)
     monkeypatch.delenv("CMTV_NO_SB_FUSE", raising=False)
 
     secs = [0, 1, 127, 128, 2**40, -1, -62135596800, 1_700_000_000]

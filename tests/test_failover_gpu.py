@@ -40,7 +40,7 @@ def test_keyed_split_late_hash_is_exact(n):
 
     # the keyed quad kernel at every size (n <= 512 would take the keyed row
     # kernel, whose helper hands k over at a barrier, no bounded wait)
-    with _env(CMTV_FORCE_K_LATE=1, CMTV_KEYED_ROW_MAX=0):
+    with _env(CMTV_FORCE_K_LATE=1, CMTV_FORM="kquad"):
         late = Context(device=0)
     pk, kidx, sig, m, off = _batch(n, 300 + n, nkeys=150)
     ks = late.register_keys(pk)
@@ -80,7 +80,7 @@ def test_verify_commit_keyset_cache_late_hash():
     reference's 'wrong signature (#i)' at the right index, never another."""
     # the keyed quad kernel at every size (n <= 512 would take the keyed row
     # kernel, whose helper hands k over at a barrier, no bounded wait)
-    with _env(CMTV_FORCE_K_LATE=1, CMTV_KEYED_ROW_MAX=0):
+    with _env(CMTV_FORCE_K_LATE=1, CMTV_FORM="kquad"):
         late = Context(device=0)
     late.keyset_cache(2)
     plain = Context(device=0)

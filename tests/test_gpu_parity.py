@@ -10,6 +10,7 @@ import pytest
 
 from oracle import coracle
 from cometbft_amd import MODE_GO_STDLIB, MODE_ZIP215, pack_messages
+from conftest import ED_FORMS
 
 pytestmark = pytest.mark.gpu
 
@@ -19,11 +20,10 @@ def _cat_report(cats, got, exp):
     return [(cats[i], int(got[i]), int(exp[i])) for i in bad[:20]]
 
 
-@pytest.mark.parametrize("kernel", ["row4", "row2", "row", "oct2", "oct", "quad2", "quad2s", "quad", "lane"])
+@pytest.mark.parametrize("kernel", ED_FORMS)
 @pytest.mark.parametrize("mode,key", [(MODE_GO_STDLIB, "go"), (MODE_ZIP215, "zip215")])
-def test_corpus_bit_exact(gpu_ctx_row4, gpu_ctx_row2, gpu_ctx_row, gpu_ctx_oct2, gpu_ctx_oct1, gpu_ctx_quad, gpu_ctx_quad2s, gpu_ctx_quad1, gpu_ctx_lane, corpus, mode, key, kernel):
-    ctx = {"row4": gpu_ctx_row4, "row2": gpu_ctx_row2, "row": gpu_ctx_row, "oct2": gpu_ctx_oct2, "oct": gpu_ctx_oct1, "quad2": gpu_ctx_quad, "quad2s": gpu_ctx_quad2s, "quad": gpu_ctx_quad1,
-           "lane": gpu_ctx_lane}[kernel]
+def test_corpus_bit_exact(form_ctx, corpus, mode, key, kernel):
+    ctx = form_ctx(kernel)
     msg, off = pack_messages(corpus["msgs"])
     valid, words = ctx.verify(corpus["pk"], corpus["sig"], msg, off, mode, bitmap=True)
     exp = corpus[key]
@@ -69,11 +69,10 @@ def test_bench_signer_matches_oracle_at_commit_scale(gpu_ctx):
     assert np.array_equal(dev, ref), np.nonzero((dev != ref).any(axis=1))[0][:10]
 
 
-@pytest.mark.parametrize("kernel", ["row4", "row2", "row", "oct2", "oct", "quad2", "quad2s", "quad", "lane"])
+@pytest.mark.parametrize("kernel", ED_FORMS)
 @pytest.mark.parametrize("n", [1, 2, 3, 4, 15, 16, 17, 63, 64, 65, 127, 769, 1000])
-def test_ragged_sizes_honest_and_flipped(gpu_ctx_row4, gpu_ctx_row2, gpu_ctx_row, gpu_ctx_oct2, gpu_ctx_oct1, gpu_ctx_quad, gpu_ctx_quad2s, gpu_ctx_quad1, gpu_ctx_lane, n, kernel):
-    gpu_ctx = {"row4": gpu_ctx_row4, "row2": gpu_ctx_row2, "row": gpu_ctx_row, "oct2": gpu_ctx_oct2, "oct": gpu_ctx_oct1, "quad2": gpu_ctx_quad, "quad2s": gpu_ctx_quad2s, "quad": gpu_ctx_quad1,
-           "lane": gpu_ctx_lane}[kernel]
+def test_ragged_sizes_honest_and_flipped(form_ctx, n, kernel):
+    gpu_ctx = form_ctx(kernel)
     seeds, pk, sig, m, off = _honest(n, 100 + n)
     rng = np.random.default_rng(n)
     sig = sig.copy()

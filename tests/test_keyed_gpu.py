@@ -1,11 +1,11 @@
 """GPU parity of registered-key verification (keyed.h / keyed_quad.h comb paths,
 cmtv_register_keys + cmtv_verify_ed25519_indexed[_device]): verdicts must equal
 the corpus' committed verdicts and the C oracle's, bit for bit, both modes.
-Kernel "wide": the lane kernels over radix-2^16 key combs
-(cmtv_register_keys_ex(CMTV_KEYS_WIDE), keyed.h keyed_comb_wide); "lane": the
-lane kernels over the radix-256 key combs with B's radix-2^16 comb
-(kCombMixed, the default); "lane256": the same with B's radix-256 comb
-(CMTV_KEYED_MIXED=0)."""
+Kernels (conftest.py FORMS, forced with CMTV_FORM): "krow" the keyed row
+kernel, "kquad" the keyed quad kernel with two helper waves, "lane" the lane
+kernels over the radix-256 key combs with B's radix-2^16 comb (kCombMixed),
+"wide" the lane kernels over radix-2^16 key combs
+(cmtv_register_keys_ex(CMTV_KEYS_WIDE), rows staged by LDS-DMA)."""
 import numpy as np
 import pytest
 
@@ -16,13 +16,11 @@ from cometbft_amd import _native as N
 pytestmark = pytest.mark.gpu
 
 
-KERNELS = ["row", "quad2", "quad", "lane", "lane256", "wide"]
+KERNELS = ["krow", "kquad", "lane", "wide"]
 
 
 def _ctx(kernel, request):
-    name = {"row": "gpu_ctx_krow", "quad2": "gpu_ctx_kquad2", "quad": "gpu_ctx_quad1", "lane": "gpu_ctx_lane",
-            "lane256": "gpu_ctx_lane256", "wide": "gpu_ctx_lane"}[kernel]
-    return request.getfixturevalue(name)
+    return request.getfixturevalue("form_ctx")("lane" if kernel == "wide" else kernel)
 
 
 @pytest.mark.parametrize("kernel", KERNELS)
@@ -50,21 +48,9 @@ def test_corpus_through_the_batched_kernels(corpus, wide):
     (CMTV_KEYED_BATCH_MIN_WAVES=1 batches any size): the coset check of
     ZIP-215 and the shared inversion of GO_STDLIB on every adversarial R
     (non-canonical, small and mixed order), s and key category."""
-    import os
+    from conftest import _env_ctx
 
-    from cometbft_amd import Context
-
-    keys = ("CMTV_QUAD_MAX", "CMTV_KEYED_QUAD_MAX", "CMTV_KEYED_BATCH_MIN_WAVES")
-    old = {k: os.environ.get(k) for k in keys}
-    os.environ.update({"CMTV_QUAD_MAX": "0", "CMTV_KEYED_QUAD_MAX": "0", "CMTV_KEYED_BATCH_MIN_WAVES": "1"})
-    try:
-        ctx = Context(device=0)
-    finally:
-        for k, v in old.items():
-            if v is None:
-                del os.environ[k]
-            else:
-                os.environ[k] = v
+    ctx = _env_ctx(CMTV_FORM="lane,klane", CMTV_KEYED_BATCH_MIN_WAVES=1)
     uniq, idx = np.unique(corpus["pk"], axis=0, return_inverse=True)
     ks = ctx.register_keys(uniq, wide=wide)
     msg, off = pack_messages(corpus["msgs"])
@@ -172,12 +158,10 @@ def test_keyed_batch_inversion(gpu_ctx_lane, corpus, n, wide):
     may vanish: their signatures must fail without spoiling the lane's
     others) and non-canonical / small-order keys; 1% of the signatures carry
     a flipped bit. Verdicts must equal the oracle's and the unbatched
-    kernel's (CMTV_KEYED_BATCH=0) bit for bit; with wide, over the radix-2^16
-    combs (rows staged by LDS-DMA; same verdicts, ZIP-215 too), and the
-    plain-load wide kernel's (CMTV_WIDE_DMA=0)."""
-    import os
-
-    from cometbft_amd import Context
+    kernel's (KB = 1: CMTV_KEYED_BATCH_MIN_WAVES above any launch) bit for
+    bit; with wide, over the radix-2^16 combs (rows staged by LDS-DMA; same
+    verdicts, ZIP-215 too)."""
+    from conftest import _env_ctx
 
     rng = np.random.default_rng(n)
     seeds = rng.integers(0, 256, (150, 32), dtype=np.uint8)
@@ -213,18 +197,8 @@ def test_keyed_batch_inversion(gpu_ctx_lane, corpus, n, wide):
     bad = np.nonzero(got_z != exp_z)[0]
     assert bad.size == 0, (bad[:10], kidx[bad[:10]])
     ks.free()
-    keys = ("CMTV_QUAD_MAX", "CMTV_KEYED_QUAD_MAX", "CMTV_KEYED_BATCH", "CMTV_WIDE_DMA")
-    old = {k: os.environ.get(k) for k in keys}
-    os.environ.update({k: "0" for k in keys})
-    try:
-        plain = Context(device=0)
-    finally:
-        for k, v in old.items():
-            if v is None:
-                del os.environ[k]
-            else:
-                os.environ[k] = v
-    ks2 = plain.register_keys(pk, wide=wide)  # wide: rows by plain loads (no LDS-DMA staging)
+    plain = _env_ctx(CMTV_FORM="lane,klane", CMTV_KEYED_BATCH_MIN_WAVES=1 << 20)
+    ks2 = plain.register_keys(pk, wide=wide)
     assert np.array_equal(plain.verify_indexed(ks2, kidx, sig, m, off, MODE_GO_STDLIB), got)
     assert np.array_equal(plain.verify_indexed(ks2, kidx, sig, m, off, MODE_ZIP215), got_z)
     ks2.free()

@@ -1,9 +1,11 @@
 """The one-signature-per-wave row kernel (cometbft_amd/csrc/row.h,
-k_verify_row_split): the production kernel for Ed25519 batches up to
-CMTV_ROW_MAX (1,536) signatures, i.e. the 150-validator VerifyCommit.
+k_verify_row_split) and its four-wave form (k_verify_row4_split): the
+production kernels for Ed25519 batches up to 1,536 signatures (runtime.cpp
+kRowMax; 256 and below on the four-wave form), i.e. the 150-validator
+VerifyCommit.
 
 Its corpus, ragged-size, wide-schedule and forced-wide parity runs live with
-the other kernels' (test_gpu_parity.py, test_wide_gpu.py: kernel "row");
+the other kernels' (test_gpu_parity.py, test_wide_gpu.py: kernels "row4", "row");
 here: the bitmap assembly (the last wave of a launch packs the words from a
 ring slot of verdict bytes) under concurrent launches on several streams,
 and the default dispatch at the commit sizes. Oracle: oracle/liboracle.so
@@ -47,7 +49,7 @@ def test_default_dispatch_commit_sizes(gpu_ctx, n):
 
 @pytest.mark.parametrize("n", [256, 257, 400, 512, 513])
 def test_default_keyed_dispatch_around_the_keyed_row_crossover(gpu_ctx, n):
-    """Registered keys on the default context at and around CMTV_KEYED_ROW_MAX
+    """Registered keys on the default context at and around kKeyedRowMax
     (512: the keyed row kernel, two workgroups per CU above 256; the keyed
     quad kernel past it), both modes, verdict bytes against the oracle."""
     pk, sig, m, off = _batch(n, 1700 + n, flip=0.15)
@@ -157,7 +159,7 @@ def test_concurrent_keyed_row_launches():
 
 
 @pytest.mark.parametrize("mode", [MODE_GO_STDLIB, MODE_ZIP215])
-def test_row_kernels_on_random_malformed_inputs(gpu_ctx_row4, gpu_ctx_row2, gpu_ctx_row, gpu_ctx_krow, mode):
+def test_row_kernels_on_random_malformed_inputs(form_ctx, mode):
     """Random bytes where the corpus has crafted ones: 240 signatures whose A,
     R and s are random (mostly off-curve points, s >= L, set high bits), mixed
     with honest ones and with honest R / A paired with a wrong s, through every
@@ -180,11 +182,12 @@ def test_row_kernels_on_random_malformed_inputs(gpu_ctx_row4, gpu_ctx_row2, gpu_
             pk[i, 31] ^= 0x80                                          # A's sign bit
     exp = coracle.verify_batch(pk, sig, m, off, mode, nthreads=8)
     assert 0 < exp.sum() < n
-    for ctx in (gpu_ctx_row4, gpu_ctx_row2, gpu_ctx_row):
+    for ctx in (form_ctx("row4"), form_ctx("row")):
         got = ctx.verify(pk, sig, m, off, mode)
         assert np.array_equal(got, exp), np.nonzero(got != exp)[0][:10]
-    ks = gpu_ctx_krow.register_keys(pk)
-    got = gpu_ctx_krow.verify_indexed(ks, np.arange(n, dtype=np.uint32), sig, m, off, mode)
+    krow = form_ctx("krow")
+    ks = krow.register_keys(pk)
+    got = krow.verify_indexed(ks, np.arange(n, dtype=np.uint32), sig, m, off, mode)
     assert np.array_equal(got, exp), np.nonzero(got != exp)[0][:10]
     ks.free()
 
@@ -222,7 +225,7 @@ def test_host_batches_read_the_completion_flag():
             calls += 1
         ks.free()
         assert ctx.stats()["polled_calls"] - before == (calls if poll else 0)
-        # past the row kernels (CMTV_ROW_MAX 1,536; the oct kernel): the stream is synchronised
+        # past the row kernels (kRowMax 1,536; the oct kernel): the stream is synchronised
         pk, sig, m, off = _batch(2000, 2200)
         exp = coracle.verify_batch(pk, sig, m, off, MODE_GO_STDLIB, nthreads=8)
         assert np.array_equal(ctx.verify(pk, sig, m, off, MODE_GO_STDLIB), exp)

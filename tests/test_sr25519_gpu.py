@@ -30,9 +30,9 @@ def srcorpus():
     return pk, sig, msgs, np.array([v["valid"] for v in vecs], np.uint8), [v["cat"] for v in vecs]
 
 
-@pytest.mark.parametrize("kernel", ["quad2", "quad2s", "quad", "lane"])
-def test_corpus_bit_exact(gpu_ctx, gpu_ctx_quad2s, gpu_ctx_quad1, gpu_ctx_lane, srcorpus, kernel):
-    gpu_ctx = {"quad2": gpu_ctx, "quad2s": gpu_ctx_quad2s, "quad": gpu_ctx_quad1, "lane": gpu_ctx_lane}[kernel]
+@pytest.mark.parametrize("kernel", ["quad", "lane"])
+def test_corpus_bit_exact(gpu_ctx, gpu_ctx_lane, srcorpus, kernel):
+    gpu_ctx = {"quad": gpu_ctx, "lane": gpu_ctx_lane}[kernel]
     pk, sig, msgs, exp, cats = srcorpus
     m, off = pack_messages(msgs)
     valid, words = gpu_ctx.verify_sr25519(pk, sig, m, off, bitmap=True)
@@ -55,10 +55,10 @@ def _honest(n, seed, nkeys=None, msg_len=None):
     return pk, sig, m, off, msgs
 
 
-@pytest.mark.parametrize("kernel", ["quad2", "quad2s", "quad", "lane"])
+@pytest.mark.parametrize("kernel", ["quad", "lane"])
 @pytest.mark.parametrize("n", [1, 15, 16, 17, 63, 64, 65, 1000])
-def test_ragged_sizes_honest_and_flipped(gpu_ctx, gpu_ctx_quad2s, gpu_ctx_quad1, gpu_ctx_lane, n, kernel):
-    gpu_ctx = {"quad2": gpu_ctx, "quad2s": gpu_ctx_quad2s, "quad": gpu_ctx_quad1, "lane": gpu_ctx_lane}[kernel]
+def test_ragged_sizes_honest_and_flipped(gpu_ctx, gpu_ctx_lane, n, kernel):
+    gpu_ctx = {"quad": gpu_ctx, "lane": gpu_ctx_lane}[kernel]
     pk, sig, m, off, _ = _honest(n, 500 + n, nkeys=min(n, 50))
     rng = np.random.default_rng(n)
     sig = sig.copy()
@@ -71,11 +71,11 @@ def test_ragged_sizes_honest_and_flipped(gpu_ctx, gpu_ctx_quad2s, gpu_ctx_quad1,
     assert exp[~flip].all()
 
 
-@pytest.mark.parametrize("kernel", ["quad2", "quad2s", "quad", "lane"])
-def test_commit_sized_batch(gpu_ctx, gpu_ctx_quad2s, gpu_ctx_quad1, gpu_ctx_lane, kernel):
+@pytest.mark.parametrize("kernel", ["quad", "lane"])
+def test_commit_sized_batch(gpu_ctx, gpu_ctx_lane, kernel):
     """A 10k-signature batch of 116-byte messages over 150 keys (the commit
     shape), all valid, plus a 1% corrupted copy."""
-    gpu_ctx = {"quad2": gpu_ctx, "quad2s": gpu_ctx_quad2s, "quad": gpu_ctx_quad1, "lane": gpu_ctx_lane}[kernel]
+    gpu_ctx = {"quad": gpu_ctx, "lane": gpu_ctx_lane}[kernel]
     pk, sig, m, off, _ = _honest(10000, 7, nkeys=150, msg_len=116)
     assert gpu_ctx.verify_sr25519(pk, sig, m, off).all()
     sig2 = sig.copy()

@@ -3,8 +3,8 @@
 in tests/test_wide_vectors.py), and on the 64-window wide fallback, which no
 searchable k reaches (forced with the CMTV_FORCE_WIDE knob).
 
-The quad kernels (k_verify_quad, k_verify_sr25519_quad) pick the window count
-per WAVE (the largest its 16 signatures need), and the radix-256 B digits
+The quad-family kernels (k_verify_quad_hs, k_verify_sr25519_quad_hs, the oct
+and row forms) pick the window count per WAVE (the largest its 16 signatures need), and the radix-256 B digits
 ride on the low windows whatever the count (quad.h q_straus_half). Each
 vector is therefore placed inside a wave of ordinary signatures (honest and
 bit-flipped), at a different lane position per wave, and the whole batch is
@@ -22,6 +22,7 @@ import pytest
 
 from oracle import coracle
 from cometbft_amd import MODE_GO_STDLIB, MODE_ZIP215, pack_messages
+from conftest import ED_FORMS, FORMS
 
 pytestmark = pytest.mark.gpu
 
@@ -72,11 +73,10 @@ def _mixed_batch(kind, waves_per_vector=1, seed=3):
     return np.array(pk), np.array(sig), m2, off2
 
 
-@pytest.mark.parametrize("kernel", ["row4", "row2", "row", "oct2", "oct", "quad2", "quad2s", "quad", "lane"])
+@pytest.mark.parametrize("kernel", ED_FORMS)
 @pytest.mark.parametrize("mode", [MODE_GO_STDLIB, MODE_ZIP215])
-def test_ed25519_wide_in_mixed_waves(gpu_ctx_row4, gpu_ctx_row2, gpu_ctx_row, gpu_ctx_oct2, gpu_ctx_oct1, gpu_ctx_quad, gpu_ctx_quad2s, gpu_ctx_quad1, gpu_ctx_lane, kernel, mode):
-    ctx = {"row4": gpu_ctx_row4, "row2": gpu_ctx_row2, "row": gpu_ctx_row, "oct2": gpu_ctx_oct2, "oct": gpu_ctx_oct1, "quad2": gpu_ctx_quad, "quad2s": gpu_ctx_quad2s, "quad": gpu_ctx_quad1,
-           "lane": gpu_ctx_lane}[kernel]
+def test_ed25519_wide_in_mixed_waves(form_ctx, kernel, mode):
+    ctx = form_ctx(kernel)
     pk, sig, m, off = _mixed_batch("ed25519")
     exp = coracle.verify_batch(pk, sig, m, off, mode, nthreads=8)
     got, words = ctx.verify(pk, sig, m, off, mode, bitmap=True)
@@ -92,10 +92,10 @@ def test_ed25519_wide_in_mixed_waves(gpu_ctx_row4, gpu_ctx_row2, gpu_ctx_row, gp
     assert [int(x) for x in alone] == [v[key] for v in vs]
 
 
-@pytest.mark.parametrize("kernel", ["row", "quad2", "quad", "lane"])
+@pytest.mark.parametrize("kernel", ["krow", "kquad", "lane"])
 @pytest.mark.parametrize("mode", [MODE_GO_STDLIB, MODE_ZIP215])
-def test_ed25519_wide_keyed(gpu_ctx_krow, gpu_ctx_kquad2, gpu_ctx_quad1, gpu_ctx_lane, kernel, mode):
-    ctx = {"row": gpu_ctx_krow, "quad2": gpu_ctx_kquad2, "quad": gpu_ctx_quad1, "lane": gpu_ctx_lane}[kernel]
+def test_ed25519_wide_keyed(form_ctx, kernel, mode):
+    ctx = form_ctx(kernel)
     pk, sig, m, off = _mixed_batch("ed25519", seed=4)
     uniq, idx = np.unique(pk, axis=0, return_inverse=True)
     ks = ctx.register_keys(uniq)
@@ -105,9 +105,9 @@ def test_ed25519_wide_keyed(gpu_ctx_krow, gpu_ctx_kquad2, gpu_ctx_quad1, gpu_ctx
     assert np.array_equal(got, exp), np.nonzero(got != exp)[0][:20]
 
 
-@pytest.mark.parametrize("kernel", ["quad2", "quad", "lane"])
-def test_sr25519_wide_in_mixed_waves(gpu_ctx, gpu_ctx_quad1, gpu_ctx_lane, kernel):
-    ctx = {"quad2": gpu_ctx, "quad": gpu_ctx_quad1, "lane": gpu_ctx_lane}[kernel]
+@pytest.mark.parametrize("kernel", ["quad", "lane"])
+def test_sr25519_wide_in_mixed_waves(form_ctx, kernel):
+    ctx = form_ctx(kernel)
     pk, sig, m, off = _mixed_batch("sr25519", seed=5)
     exp = coracle.sr25519_verify_batch(pk, sig, m, off, nthreads=8)
     got = ctx.verify_sr25519(pk, sig, m, off)
@@ -136,32 +136,12 @@ def test_reference_keygen_vector_on_device(gpu_ctx):
 
 @pytest.fixture(scope="module")
 def forced_wide_ctxs():
-    from cometbft_amd import Context
+    from conftest import _env_ctx
 
-    os.environ["CMTV_FORCE_WIDE"] = "1"
-    try:
-        os.environ["CMTV_ROW_MAX"] = "4000"
-        os.environ["CMTV_ROW2_MAX"] = "4000"
-        r4ctx = Context(device=0)
-        os.environ["CMTV_ROW_WAVES"] = "2"
-        r2ctx = Context(device=0)
-        os.environ["CMTV_ROW2_MAX"] = "0"
-        rctx = Context(device=0)
-        os.environ["CMTV_ROW_MAX"] = "0"
-        o2ctx = Context(device=0)
-        os.environ["CMTV_OCT_SPLIT_MAX"] = "0"
-        octx = Context(device=0)
-        os.environ["CMTV_OCT_MAX"] = "0"
-        q2ctx = Context(device=0)
-        os.environ["CMTV_QUAD_SPLIT_MAX"] = "0"
-        qctx = Context(device=0)
-    finally:
-        for k in ("CMTV_FORCE_WIDE", "CMTV_ROW_MAX", "CMTV_ROW2_MAX", "CMTV_ROW_WAVES", "CMTV_OCT_MAX", "CMTV_OCT_SPLIT_MAX", "CMTV_QUAD_SPLIT_MAX"):
-            os.environ.pop(k, None)
-    return {"row4": r4ctx, "row2": r2ctx, "row": rctx, "oct2": o2ctx, "oct": octx, "quad2": q2ctx, "quad": qctx}
+    return {k: _env_ctx(CMTV_FORCE_WIDE=1, CMTV_FORM=FORMS[k]) for k in ("row4", "row", "oct2", "quad")}
 
 
-@pytest.mark.parametrize("kernel", ["row4", "row2", "row", "oct2", "oct", "quad2", "quad"])
+@pytest.mark.parametrize("kernel", ["row4", "row", "oct2", "quad"])
 @pytest.mark.parametrize("mode,key", [(MODE_GO_STDLIB, "go"), (MODE_ZIP215, "zip215")])
 def test_forced_wide_schedule_on_corpus(forced_wide_ctxs, corpus, mode, key, kernel):
     """CMTV_FORCE_WIDE: every quad (or oct) takes the wide fallback (k1 = k,
@@ -176,9 +156,8 @@ def test_forced_wide_schedule_on_corpus(forced_wide_ctxs, corpus, mode, key, ker
     assert np.array_equal(ctx.verify(pk, sig, m, off, mode), exp)
 
 
-@pytest.mark.parametrize("kernel", ["quad2", "quad"])
-def test_forced_wide_schedule_sr25519(forced_wide_ctxs, kernel):
-    forced_wide_ctx = forced_wide_ctxs[kernel]
+def test_forced_wide_schedule_sr25519(forced_wide_ctxs):
+    forced_wide_ctx = forced_wide_ctxs["quad"]
     pk, sig, m, off = _mixed_batch("sr25519", seed=7)
     exp = coracle.sr25519_verify_batch(pk, sig, m, off, nthreads=8)
     assert np.array_equal(forced_wide_ctx.verify_sr25519(pk, sig, m, off), exp)

@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of a runtime knob on one box, alternating: KNOB=VAL_A vs KNOB=VAL_B,
 # the configs[1] step's kernel time in both modes (bench.py quick form).
-#   KNOB=CMTV_QUAD_HS A=0 B=1 bash tools/gpu_knob_ab.sh
+#   KNOB=CMTV_HS_PRE A=4 B=6 bash tools/gpu_knob_ab.sh
 set -o pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/knob_ab

@@ -1,6 +1,6 @@
 """Registered-key verification at commit sizes (dev tool): mean wall time per
 device-resident call (cmtv_verify_ed25519_indexed_device) and the context's
-kernel time, for n in argv (default 150). CMTV_KEYED_ROW_MAX=0 selects the
+kernel time, for n in argv (default 150). CMTV_FORM=kquad selects the
 keyed quad kernel instead of the keyed row kernel."""
 import os
 import sys

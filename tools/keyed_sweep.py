@@ -1,5 +1,6 @@
 """Kernel time of registered-key verification vs batch size for the keyed quad
-(two-helper) and keyed lane kernels, to place CMTV_KEYED_QUAD_MAX.
+(two-helper) and keyed lane kernels, to place the keyed quad/lane band
+(runtime.cpp kKeyedQuadMax), each forced with CMTV_FORM.
 
     python tools/keyed_sweep.py 4096 8192 12288 16384 24576 32768
 """
@@ -28,8 +29,8 @@ def main():
     sig = gen.sign(sv.seeds, m, off, kidx)
     dev = torch.device("cuda", 0)
     res = {}
-    for kind, env in (("quad2", str(1 << 30)), ("lane", "0")):
-        os.environ["CMTV_KEYED_QUAD_MAX"] = env
+    for kind, env in (("quad2", "kquad"), ("lane", "klane")):
+        os.environ["CMTV_FORM"] = env
         ctx = Context(device=0)
         ks = ctx.register_keys(sv.pubkeys)
         for n in sizes:

@@ -1,7 +1,7 @@
 """Host-API batch and VerifyCommit (C ABI, packed once) medians at the
-row/oct crossover sizes, for an A/B of CMTV_ROW_MAX (dev tool):
+row/oct crossover sizes, for an A/B of the forms (dev tool):
 
-    CMTV_ROW_MAX=768 python tools/mid_ab.py 768 1024 1536
+    CMTV_FORM=oct2 python tools/mid_ab.py 768 1024 1536
 """
 import os
 import sys
@@ -28,7 +28,7 @@ def main():
 
     sizes = [int(x) for x in sys.argv[1:]] or [768, 1024, 1536]
     ctx = Context(device=0)
-    tag = os.environ.get("TAG") or os.environ.get("CMTV_ROW_MAX", "default")
+    tag = os.environ.get("TAG") or os.environ.get("CMTV_FORM", "default")
     for n in sizes:
         sv = TU.make_validator_set(ctx, n)
         msgs = TU.commit_messages(n, 1000)

@@ -29,7 +29,7 @@ SLOTS = 8
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000
     # signatures per 4-wave workgroup: 48 (k_verify_quad_split) or 3 (the row
-    # kernel, k_verify_row_split, which the library picks up to CMTV_ROW_MAX)
+    # kernel, k_verify_row_split, which the library picks up to kRowMax)
     per_wg = int(sys.argv[2]) if len(sys.argv) > 2 else 48
     from cometbft_amd import Context, pack_messages
     from cometbft_amd import _native as N

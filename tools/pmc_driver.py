@@ -1,8 +1,9 @@
 """Runs each verify kernel a few times on device-resident synthetic batches,
-for rocprofv3 --pmc passes (tools/gpu_prof.sh): k_verify_oct_split (150),
-k_verify_quad_split (8192 and the 10k commit), the one-wave k_verify_quad and
-k_verify_oct (10k / 150, env-forced), k_verify (100k, lane kernel),
-k_verify_keyed_quad (10k over 150 keys) and k_verify_keyed (1M over 150 keys).
+for rocprofv3 --pmc passes (tools/gpu_prof.sh): the default forms at 150
+(k_verify_row4_split), 8192 and the 10k commit (k_verify_quad_hs), the oct2
+form at 150 (CMTV_FORM=oct2), k_verify (100k, lane kernel),
+k_verify_keyed_quad_split (10k over 150 keys) and the keyed lane kernels (262k
+/ 1M over 150 keys).
 Every batch is checked (all valid) so a counter pass never profiles a
 broken kernel."""
 import os
@@ -70,20 +71,19 @@ def env_ctx(**env):
 
 
 def lane_ctx():
-    return env_ctx(CMTV_QUAD_MAX=0, CMTV_KEYED_QUAD_MAX=0)
+    return env_ctx(CMTV_FORM="lane,klane")
 
 
 def want(*names):
     return not ONLY or any(n in ONLY for n in names)
 
 
-if want("oct_split150", "quad_split8192", "quad_split10k", "oct150", "quad10k", "keyed_quad10k"):
+if want("row4_150", "quad8192", "quad10k", "oct2_150", "keyed_quad10k"):
     b150, b8k, b10k = batch(150), batch(8192), batch(10000)
-    run("oct_split150", ctx, b150)
-    run("quad_split8192", ctx, b8k)
-    run("quad_split10k", ctx, b10k)
-    run("oct150", env_ctx(CMTV_OCT_SPLIT_MAX=0), b150)
-    run("quad10k", env_ctx(CMTV_QUAD_SPLIT_MAX=0), b10k)
+    run("row4_150", ctx, b150)
+    run("quad8192", ctx, b8k)
+    run("quad10k", ctx, b10k)
+    run("oct2_150", env_ctx(CMTV_FORM="oct2"), b150)
 lctx = lane_ctx()
 if want("lane100k"):
     b100k = batch(100_000)
@@ -108,6 +108,3 @@ if want("lane262k", "keyed_lane262k", "keyed_lane1m", "keyed_wide1m"):
             # radix-2^16 key combs (CMTV_KEYS_WIDE): configs[2]'s 2^20-signature launches
             wks = lctx.register_keys(pks, wide=True)
             run("keyed_wide1m", lctx, b1m, keyed=wks)
-            # the same rows by plain loads (no LDS-DMA staging)
-            nctx = env_ctx(CMTV_QUAD_MAX=0, CMTV_KEYED_QUAD_MAX=0, CMTV_WIDE_DMA=0)
-            run("keyed_wide1m", nctx, b1m, keyed=nctx.register_keys(pks, wide=True))

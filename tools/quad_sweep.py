@@ -1,5 +1,5 @@
 """Quad-kernel time vs batch size (dev tool): device-resident inputs, HIP-event
-timing on the launch stream. Env CMTV_QUAD_MAX should force the kernel."""
+timing on the launch stream. Env CMTV_FORM forces the kernel."""
 import os
 import sys
 

@@ -1,14 +1,14 @@
-"""Phase timeline of the two-wave row kernel (k_verify_row2_split) on one
-150-validator batch, from the probe build of the library.
+"""Phase timeline of the four-wave row kernel (k_verify_row4_split) or the
+keyed row kernel on one 150-validator batch, from the probe build of the
+library.
 
   make -C cometbft_amd/csrc OUT=../../abtest/libprobe.so BUILD=../../build/probe KFLAGS=-DCMTV_PHASE_PROBE
-  CMTV_LIBRARY=$PWD/abtest/libprobe.so [CMTV_ROW_WAVES=2] python tools/row_phase.py [n] [row4|row2]
+  CMTV_LIBRARY=$PWD/abtest/libprobe.so python tools/row_phase.py [n] [row4|krow]
 
 Shader-clock stamps per wave (kernels.hip CMTV_STAMP), relative to the
-workgroup's first entry: A wave (0) and R wave (1): 6 decoded, 1 at barrier 1
-(table built), 2 released, 3 at barrier 2 (windows done), 4 released, 5 end
-(A: verdict); helper (2): 5 hashed (SHA-512 + mod L), 1 scalars ready,
-3 [u]B ready. Medians over workgroups, per mode, into gpurun_out/row_phase.json.
+workgroup's first entry: row4's lo wave (0): 1/2 at/after barrier 1, 3/4
+at/after barrier 2, 5 verdict; A-hi and R-hi (1, 2): 6 decoded, 1-3 as lo;
+helper (3): 1 scalars ready, 3 [u]B ready. Medians over workgroups, per mode, into gpurun_out/row_phase.json.
 """
 import ctypes
 import json
@@ -41,8 +41,6 @@ def main():
     kidx = np.arange(n, dtype=np.uint32)
     if form == "krow":  # keyed row: R decode (meets barrier 1 mid-chain), A comb, B comb, hash helper
         names = {"R": (0, [1, 2, 3, 4, 5]), "A": (1, [1, 2, 3]), "B": (2, [1, 2]), "helper": (3, [1])}
-    elif form == "row2":
-        names = {"A": (0, [6, 1, 2, 3, 4, 5]), "R": (1, [6, 1, 2, 3]), "helper": (2, [5, 1, 3])}
     else:  # row4: lo (decodes A and R), A-hi, R-hi, helper
         names = {"lo": (0, [1, 2, 3, 4, 5]), "A_hi": (1, [6, 1, 2, 3]), "R_hi": (2, [6, 1, 2, 3]),
                  "helper": (3, [1, 3])}

@@ -1,6 +1,6 @@
 """sr25519 quad/lane crossover (dev tool): device-resident
 cmtv_verify_sr25519_device wall time per call at the sizes in argv, for an
-A/B of CMTV_QUAD_MAX:  CMTV_QUAD_MAX=40000 python tools/sr_quad_ab.py 40960 49152"""
+A/B of the forms:  CMTV_FORM=quad python tools/sr_quad_ab.py 40960 49152 (and lane)"""
 import os
 import sys
 import time
@@ -37,5 +37,5 @@ for n in [int(a) for a in (sys.argv[1:] or ["49152"])]:
         call()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / reps
-    print(f"QUAD_MAX={os.environ.get('CMTV_QUAD_MAX', 'default')} n={n} ms={dt * 1e3:.3f} "
+    print(f"FORM={os.environ.get('CMTV_FORM', 'default')} n={n} ms={dt * 1e3:.3f} "
           f"valid={int(d_v.sum())}/{n}", flush=True)

@@ -171,20 +171,123 @@ CMTV_HD void mul_v(fe& h, const fe& f, const fe& g) {
   CMTV_SCHED_FENCE();
 }
 
+// ---- the 2-lane column split -----------------------------
+// In the quad kernels' decode, lanes c and c ^ 2 run the same square-root
+// chain on the same element (A on lanes {0,2}, R on {1,3}). Here the pair
+// shares each squaring instead: lane half 0 (c < 2) owns limbs 0..4 and
+// computes columns 0..4, half 1 owns limbs 5..9 and computes columns 5..9,
+// with ONE instruction stream (SIMD-uniform): half 1 reads g rotated by 5
+// limbs (G = [own, partner] on both halves), f unrotated (a select per limb),
+// and every lane-dependent factor is a loop-invariant per-lane register:
+//   odd x odd x2   -> f_i << half (even column slot) or << (1 - half) (odd),
+//   wrap x19       -> slots 5..9 wrap on half 0 only: G_j x (half ? 1 : 19),
+//                     slots 1..4 wrap on both halves or neither: G_j, 19 G_j,
+//   carries        -> per-lane widths (26/25 swap with the column parity) and
+//                     the column-4 -> 5 / 9 -> 0 carry exchanged by DPP (x19
+//                     into column 0 on half 0).
+// The squaring's symmetry (55 products instead of 100) does not survive the
+// uniform form (its per-slot coefficients differ between the halves), so a
+// lane does 50 MADs -- against 55 unsplit -- plus the exchange.
+struct PairLane {
+  uint32_t half;            // 0: lanes 0/1 of the quad, 1: lanes 2/3
+  uint32_t sh_e, sh_o;      // odd-limb x2 for even / odd column slots
+  uint32_t m19;             // half ? 1 : 19
+  uint32_t w_e, w_o;        // carry widths of local columns 0, 2, 4 / 1, 3
+  uint32_t mask_e, mask_o;
+};
+__device__ __forceinline__ PairLane pair_lane() {
+  PairLane L;
+  L.half = (threadIdx.x >> 1) & 1;
+  L.sh_e = L.half;
+  L.sh_o = 1 - L.half;
+  L.m19 = L.half ? 1u : 19u;
+  L.w_e = L.half ? 25u : 26u;
+  L.w_o = L.half ? 26u : 25u;
+  L.mask_e = (1u << L.w_e) - 1;
+  L.mask_o = (1u << L.w_o) - 1;
+  return L;
+}
+__device__ __forceinline__ uint32_t pswap(uint32_t x) {  // partner (lane ^ 2) by quad_perm [2,3,0,1]
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);
+}
+// o: this lane's 5 limbs (half 0: f0..f4, half 1: f5..f9) <- their square
+__device__ __forceinline__ void sq_pair(uint32_t o[5], const PairLane& L) {
+  CMTV_SCHED_FENCE();
+  uint32_t P[5], U[10], G[10];
+#pragma unroll
+  for (int k = 0; k < 5; k++) P[k] = pswap(o[k]);
+#pragma unroll
+  for (int k = 0; k < 5; k++) {
+    U[k] = L.half ? P[k] : o[k];
+    U[k + 5] = L.half ? o[k] : P[k];
+    G[k] = o[k];
+    G[k + 5] = P[k];
+  }
+  uint32_t Ue[10], Uo[10];  // U_i scaled for even / odd column slots (odd i: x2 where j is odd)
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    Ue[i] = (i & 1) ? U[i] << L.sh_e : U[i];
+    Uo[i] = (i & 1) ? U[i] << L.sh_o : U[i];
+  }
+  uint32_t Gw[10];  // the slot's wrap factor applied
+#pragma unroll
+  for (int j = 0; j < 10; j++) Gw[j] = j >= 5 ? G[j] * L.m19 : (j >= 1 ? 19 * G[j] : G[j]);
+  uint64_t h[5];
+#pragma unroll
+  for (int m = 0; m < 5; m++) {
+    uint64_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+      const int j = (m - i + 10) % 10;
+      // slots 1..4 wrap on both halves iff i > m (+5 on half 1 means i > m + 5: j = m - i + 10 in 1..4)
+      const bool both_wrap = j >= 1 && j <= 4 && i > m;
+      const uint32_t g = j >= 5 ? Gw[j] : (both_wrap ? Gw[j] : G[j]);
+      const uint32_t u = (j & 1) ? Uo[i] : Ue[i];
+      acc += CMTV_MUL64(u, g);
+    }
+    h[m] = acc;
+  }
+  // carries: local columns 0 -> 4 with per-lane widths, out of column 4 to the partner
+  uint64_t c;
+  c = h[0] >> L.w_e; h[1] += c; h[0] &= L.mask_e;
+  c = h[1] >> L.w_o; h[2] += c; h[1] &= L.mask_o;
+  c = h[2] >> L.w_e; h[3] += c; h[2] &= L.mask_e;
+  c = h[3] >> L.w_o; h[4] += c; h[3] &= L.mask_o;
+  c = h[4] >> L.w_e; h[4] &= L.mask_e;
+  const uint32_t clo = pswap((uint32_t)c), chi = pswap((uint32_t)(c >> 32));
+  // half 0 receives column 9's carry (x19), half 1 column 4's
+  const uint64_t cin = CMTV_MUL64(clo, L.m19) + ((uint64_t)(chi * L.m19) << 32);
+  h[0] += cin;
+  c = h[0] >> L.w_e; h[0] &= L.mask_e;
+  o[0] = (uint32_t)h[0];
+  o[1] = (uint32_t)h[1] + (uint32_t)c;
+  o[2] = (uint32_t)h[2];
+  o[3] = (uint32_t)h[3];
+  o[4] = (uint32_t)h[4];
+  CMTV_SCHED_FENCE();
+}
+
 // V: 0..5 = squaring (R0,R1,R2) x (mul19 as v_mul_lo / shift-add);
 //    6..8 = multiplication h = h*g with R0, R1, R2;
 //    9    = two independent squaring chains interleaved (ILP 2), R0
+//    10   = the 2-lane column split (sq_pair): lanes c, c ^ 2 share one
+//           element (both load thread (tid & ~2)'s input)
 template <int V>
 __global__ void __launch_bounds__(256) k_chain(const uint32_t* in, uint32_t* out, int nops, unsigned long long* cyc) {
   extern __shared__ uint32_t lds_pad[];
   const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
   fe h, g, h2;
+  const uint32_t src = V == 10 ? (tid & ~2u) : tid;
 #pragma unroll
   for (int i = 0; i < 10; i++) {
-    h.v[i] = in[tid * 20 + i];
-    g.v[i] = in[tid * 20 + 10 + i];
+    h.v[i] = in[src * 20 + i];
+    g.v[i] = in[src * 20 + 10 + i];
     h2.v[i] = g.v[i];
   }
+  const PairLane L = pair_lane();
+  uint32_t o[5];
+#pragma unroll
+  for (int k = 0; k < 5; k++) o[k] = L.half ? h.v[k + 5] : h.v[k];
   if (threadIdx.x == 0) lds_pad[0] = 0;  // keep the dynamic LDS allocation
   int n = nops;
   asm volatile("" : "+s"(n));
@@ -204,8 +307,17 @@ __global__ void __launch_bounds__(256) k_chain(const uint32_t* in, uint32_t* out
       sq_v<0, false>(h, h);
       sq_v<0, false>(h2, h2);
     }
+    if (V == 10) sq_pair(o, L);
   }
   const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  if (V == 10) {
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+      const uint32_t p = pswap(o[k]);
+      h.v[k] = L.half ? p : o[k];
+      h.v[k + 5] = L.half ? o[k] : p;
+    }
+  }
   uint32_t s[8];
   fe_tobytes(s, h);
   if (V == 9) {
@@ -224,10 +336,11 @@ int main(int argc, char** argv) {
   int dev = 0, cus = 0;
   hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const int block = 256;
-  const kfn ks[] = {k_chain<0>, k_chain<1>, k_chain<2>, k_chain<3>, k_chain<4>,
-                    k_chain<5>, k_chain<6>, k_chain<7>, k_chain<8>, k_chain<9>};
+  const kfn ks[] = {k_chain<0>, k_chain<1>, k_chain<2>, k_chain<3>, k_chain<4>, k_chain<5>,
+                    k_chain<6>, k_chain<7>, k_chain<8>, k_chain<9>, k_chain<10>};
   const char* names[] = {"sq ref10", "sq 3chain", "sq par2", "sq ref10 sh19", "sq 3chain sh19", "sq par2 sh19",
-                         "mul ref10", "mul 3chain", "mul par2", "sq ref10 x2 ILP"};
+                         "mul ref10", "mul 3chain", "mul par2", "sq ref10 x2 ILP", "sq pair split"};
+  std::vector<uint32_t> sq_ref;
   for (int wps = 1; wps <= 2; wps++) {
     const int grid = cus * wps;  // wps waves per SIMD (one 4-wave block per CU per wave slot)
     const size_t nth = (size_t)grid * block;
@@ -249,7 +362,7 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
-    for (int v = 0; v < 10; v++) {
+    for (int v = 0; v < 11; v++) {
       for (int r = 0; r < 2; r++) hipLaunchKernelGGL(ks[v], dim3(grid), dim3(block), lds, 0, din, dout, nops, dcyc);
       hipEventRecord(e0);
       hipLaunchKernelGGL(ks[v], dim3(grid), dim3(block), lds, 0, din, dout, nops, dcyc);
@@ -265,7 +378,15 @@ int main(int argc, char** argv) {
       mean /= cyc.size();
       const char* chk = "";
       if (v == 0) ref = got;
+      if (v == 0) sq_ref = got;
       if ((v >= 1 && v <= 5) && got != ref) chk = "  MISMATCH vs sq ref10";
+      if (v == 10) {  // lane t holds the square chain of thread (t & ~2)'s input
+        size_t bad = 0;
+        for (size_t t = 0; t < nth; t++)
+          for (int i = 0; i < 8; i++) bad += got[t * 8 + i] != sq_ref[(t & ~(size_t)2) * 8 + i];
+        if (bad) chk = "  MISMATCH vs sq ref10";
+        else chk = "  (bit-exact vs sq ref10)";
+      }
       printf("wps=%d %-16s %8.1f cyc/op (s_memtime)  %7.3f ms  %6.1f ns/op%s\n", wps, names[v], mean / nops, ms,
              ms * 1e6 / nops, chk);
       if (v == 6) ref = got;

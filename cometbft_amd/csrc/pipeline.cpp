@@ -300,7 +300,7 @@ int verify_commits_pipeline(cmtv_ctx* ctx, const CommitsArgs& args, int* rcs) {
       // default, 2^20, is one full round of the batched registered-key lane
       // kernel: 2,048 waves of 64 lanes x 8 signatures; a chunk just past it
       // would start a second, nearly empty round), and ramps up: its first
-      // chunks are 1/8, 1/4 and 1/2 of that, so the device starts after a
+      // chunks are 1/16, 1/4 and 1/2 of that, so the device starts after a
       // fraction of a chunk's pack instead of a whole one
       if (long_call) {
         ramp = true;
@@ -308,7 +308,13 @@ int verify_commits_pipeline(cmtv_ctx* ctx, const CommitsArgs& args, int* rcs) {
       }
     }
     uint64_t want = per;
-    if (ramp && chunks.size() < 3) want = std::max<uint64_t>(per >> (3 - chunks.size()), 1);
+    // the ramp: 1/16, 1/4, 1/2 of a chunk (2^16 signatures take the one-
+    // signature-per-lane keyed kernel at two waves per SIMD, 2^18 and 2^19
+    // the KB = 4 batch); measured on MI355X (tools/ramp_ab.sh, 100k x 150,
+    // two alternating rounds): 40.9-41.1 ms per pass against 41.3-41.6 with
+    // 1/8, 1/4, 1/2 and 42.3 without a ramp
+    static constexpr int ramp_sh[] = {4, 2, 1};
+    if (ramp && chunks.size() < 3) want = std::max<uint64_t>(per >> ramp_sh[chunks.size()], 1);
     Chunk ch;
     ch.c0 = cursor;
     bool cls_set = false;

@@ -698,12 +698,18 @@ int cmtv_verify_commit(cmtv_ctx* ctx, uint32_t kind, uint32_t mode, const char* 
   SigBatch B;
   const bool cache = cmtv::cache_enabled(ctx);
   B.templated = !cache && templated_enabled();
-  // registered keys, signatures back to back: their copy to the device can
-  // start now and overlap the plan (used only if the fast form takes them)
-  if (B.templated && cmtv::keyset_cache_enabled(ctx) && kind != CMTV_VERIFY_COMMIT_LIGHT_TRUSTING && commit->n_sigs &&
-      commit->sig_off[0] == 0 && commit->sig_off[commit->n_sigs] == 64ull * commit->n_sigs) {
-    rc = cmtv::stage_sigs_early_locked(ctx, commit->sigs, commit->n_sigs);
-    if (rc != CMTV_OK) return rc;
+  // signatures back to back (and, without registered keys, 32-byte keys in
+  // validator order): their copy to the device can start now and overlap the
+  // plan (used only if the fast form takes exactly these bytes)
+  if (B.templated && kind != CMTV_VERIFY_COMMIT_LIGHT_TRUSTING && commit->n_sigs && commit->sig_off[0] == 0 &&
+      commit->sig_off[commit->n_sigs] == 64ull * commit->n_sigs) {
+    const bool keyed = cmtv::keyset_cache_enabled(ctx);
+    const bool packed = vals->n_vals == commit->n_sigs && vals->pk_off[0] == 0 &&
+                        vals->pk_off[vals->n_vals] == 32ull * vals->n_vals;
+    if (keyed || packed) {
+      rc = cmtv::stage_sigs_early_locked(ctx, commit->sigs, commit->n_sigs, keyed ? nullptr : vals->pubkeys);
+      if (rc != CMTV_OK) return rc;
+    }
   }
   job_prepare(J, B, cache, true, seen);
   cmtv::phase_add(ctx, cmtv::kPhPrepare, t0);

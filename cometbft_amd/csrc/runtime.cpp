@@ -442,9 +442,11 @@ struct CmtvDev {
   hipEvent_t poll_ev = nullptr;
   bool poll_pending = false;
   // signatures a single-commit call copied to h_in / d_in (offset 0) before
-  // planning (stage_sigs_early_locked): the source and count; the next
-  // staging of those bytes skips them
+  // planning (stage_sigs_early_locked): the source and count, and the keys
+  // copied after them (generic kernels; null when none); the next staging of
+  // those bytes skips them
   const uint8_t* early_src = nullptr;
+  const uint8_t* early_pk = nullptr;
   size_t early_n = 0;
   // a device that returned a HIP error is taken out of the context's
   // rotation: host batches are re-planned over the others (runtime.cpp
@@ -1030,16 +1032,18 @@ static int enqueue_shard(cmtv_ctx* ctx, size_t g, const HostBatch& B, size_t a, 
   // at 10k signatures the keyed kernel's PCIe reads cost what the H2D copy
   // saves (round 5, before fusion: p50 0.2010 vs 0.2012 ms, kernel 0.087 vs
   // 0.071 ms).
-  const bool zc = zero_copy && ctx->zc_in &&
+  // the signatures (and keys) staged ahead of the plan: the same bytes are
+  // already in h_in (and on their way to d_in on this stream), unless a
+  // buffer must grow; a batch that has them reads HBM, not its staging in place
+  const bool early = D.early_src && D.early_src == B.sig + 64 * a && m <= D.early_n && in_bytes <= D.h_in.cap &&
+                     dev_bytes <= D.d_in.cap;
+  const bool early_pk = early && !keyed && D.early_pk && D.early_pk == B.pk + 32 * a && m == D.early_n;
+  D.early_src = D.early_pk = nullptr;
+  const bool zc = !early && zero_copy && ctx->zc_in &&
                   (keyed ? tpl && ctx->zc_keyed
                          : fuse || (!tpl && ctx->zc_host_in && max_len <= kSbFuseMaxMsg));
   const bool zc_keyed = zc && keyed && !fuse;  // k_sign_bytes writes the messages into HBM
   HostBuf& HB = zc ? D.h_zin : D.h_in;
-  // the signatures staged ahead of the plan: the same bytes are already in
-  // h_in (and on their way to d_in on this stream), unless a buffer must grow
-  const bool early = !zc && D.early_src && D.early_src == B.sig + 64 * a && m <= D.early_n &&
-                     in_bytes <= D.h_in.cap && dev_bytes <= D.d_in.cap;
-  D.early_src = nullptr;
   if ((e = HB.ensure(in_bytes)) != hipSuccess) return hip_fail(e);
   if (!zc && (e = D.d_in.ensure(dev_bytes)) != hipSuccess) return hip_fail(e);
   if (zc_keyed && (e = D.d_in.ensure(mb + 16)) != hipSuccess) return hip_fail(e);
@@ -1054,7 +1058,7 @@ static int enqueue_shard(cmtv_ctx* ctx, size_t g, const HostBatch& B, size_t a, 
       std::memcpy(hin + o_key, B.key_idx + a, 4 * m);
     else if (!null_kidx)
       for (size_t i = 0; i < m; i++) reinterpret_cast<uint32_t*>(hin + o_key)[i] = (uint32_t)(a + i);
-  } else {
+  } else if (!early_pk) {
     std::memcpy(hin + o_key, B.pk + 32 * a, 32 * m);
   }
   if (!early) std::memcpy(hin + o_sig, B.sig + 64 * a, 64 * m);
@@ -1084,9 +1088,10 @@ static int enqueue_shard(cmtv_ctx* ctx, size_t g, const HostBatch& B, size_t a, 
     if ((e = hipHostGetDevicePointer(&p, HB.p, 0)) != hipSuccess) return hip_fail(e);
     din = static_cast<uint8_t*>(p);
     dmsg = zc_keyed ? static_cast<uint8_t*>(D.d_in.p) : din + o_msg;
-  } else if ((e = early ? hipMemcpyAsync(din + o_key, hin + o_key, in_bytes - o_key, hipMemcpyHostToDevice, D.stream)
-                         : hipMemcpyAsync(din, hin, in_bytes, hipMemcpyHostToDevice, D.stream)) != hipSuccess) {
-    return hip_fail(e);
+  } else {
+    const size_t from = early_pk ? o_off : early ? o_key : 0;  // what the early copy did not carry
+    if ((e = hipMemcpyAsync(din + from, hin + from, in_bytes - from, hipMemcpyHostToDevice, D.stream)) != hipSuccess)
+      return hip_fail(e);
   }
   SbFuse sb;
   if (fuse) {
@@ -1448,8 +1453,15 @@ int verify_templated_locked(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const ui
 // copy overlaps the plan. Their bytes are only used if the batch that
 // follows stages exactly those signatures on this device (enqueue_shard);
 // otherwise they are overwritten unused.
-int stage_sigs_early_locked(cmtv_ctx* ctx, const uint8_t* sigs, size_t n) {
+int stage_sigs_early_locked(cmtv_ctx* ctx, const uint8_t* sigs, size_t n, const uint8_t* pk) {
   if (n == 0 || n > ctx->zc_max || ctx->live.size() != 1 || ctx->zc_keyed || !ctx->early_sigs) return CMTV_OK;
+  // the generic row kernels read their staging from mapped memory instead
+  // (a copy's latency is most of their call); the quad-family forms gain the
+  // HBM reads (10k: kernel 0.255 ms zero-copy, 0.220 ms from HBM)
+  if (pk && (ed_form(ctx, n) == kFormRow4 || ed_form(ctx, n) == kFormRow)) return CMTV_OK;
+  // nor is the copy worth its own latency for the keyed row kernel's
+  // commits (150 validators: p50 0.0566 with it, 0.0534 without)
+  if (!pk && keyed_form(ctx, n) == kKeyedRow) return CMTV_OK;
   CmtvDev& D = ctx->devs[ctx->live[0]];
   if (hipSetDevice(D.ordinal) != hipSuccess) return CMTV_ENODEV;
   hipError_t e;
@@ -1462,9 +1474,13 @@ int stage_sigs_early_locked(cmtv_ctx* ctx, const uint8_t* sigs, size_t n) {
   if ((e = D.h_in.ensure(in_cap)) != hipSuccess) return hip_fail(e);
   if ((e = D.d_in.ensure(dev_cap)) != hipSuccess) return hip_fail(e);
   std::memcpy(D.h_in.p, sigs, 64 * n);
-  if ((e = hipMemcpyAsync(D.d_in.p, D.h_in.p, 64 * n, hipMemcpyHostToDevice, D.stream)) != hipSuccess)
+  // the keys where enqueue_shard's layout puts them for m = n signatures
+  const size_t o_key = align_up(64 * n, 256), bytes = pk ? o_key + 32 * n : 64 * n;
+  if (pk) std::memcpy(static_cast<uint8_t*>(D.h_in.p) + o_key, pk, 32 * n);
+  if ((e = hipMemcpyAsync(D.d_in.p, D.h_in.p, bytes, hipMemcpyHostToDevice, D.stream)) != hipSuccess)
     return hip_fail(e);
   D.early_src = sigs;
+  D.early_pk = pk;
   D.early_n = n;
   return CMTV_OK;
 }

@@ -38,11 +38,14 @@ int verify_templated_locked(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const ui
                             const int32_t* nanos, uint32_t mode, uint8_t* out_valid,
                             const cmtv_keyset* ks = nullptr, const uint32_t* key_idx = nullptr);
 
-// A single commit's n contiguous 64-byte signatures, copied toward device
-// memory before the commit is planned (the copy overlaps the plan); the
-// templated batch that follows picks them up (no-op unless one live device,
-// n <= the zero-copy size and CMTV_EARLY_SIGS is on). Caller holds the lock.
-int stage_sigs_early_locked(cmtv_ctx* ctx, const uint8_t* sigs, size_t n);
+// A single commit's n contiguous 64-byte signatures -- and, for the generic
+// kernels (pk set: the validator set's n packed 32-byte keys), its keys --
+// copied toward device memory before the commit is planned (the copy
+// overlaps the plan); the templated batch that follows picks them up (no-op
+// unless one live device, n <= the zero-copy size and CMTV_EARLY_SIGS is on;
+// with pk, only past the row kernels' band, which keep reading their
+// staging in place). Caller holds the lock.
+int stage_sigs_early_locked(cmtv_ctx* ctx, const uint8_t* sigs, size_t n, const uint8_t* pk = nullptr);
 
 // cmtv_keyset_cache: the registered key set of these n 32-byte keys (built on
 // first use), or NULL when the cache is off or registration failed.

@@ -198,7 +198,7 @@ HostPool& host_pool(cmtv_ctx* ctx) {
   return *ctx->pool;
 }
 PipeConfig pipe_config(const cmtv_ctx* ctx) { return ctx->pc; }
-int stage_sigs_early_locked(cmtv_ctx*, const uint8_t*, size_t) { return CMTV_OK; }
+int stage_sigs_early_locked(cmtv_ctx*, const uint8_t*, size_t, const uint8_t*) { return CMTV_OK; }
 void live_devices_locked(cmtv_ctx* ctx, std::vector<size_t>& out) { out = ctx->live; }
 
 int bulk_stage(cmtv_ctx* ctx, size_t dev, int slot, const BulkLayout& L, uint8_t** host) {

@@ -1043,7 +1043,15 @@ static int enqueue_shard(cmtv_ctx* ctx, size_t g, const HostBatch& B, size_t a, 
                   (keyed ? tpl && ctx->zc_keyed
                          : fuse || (!tpl && ctx->zc_host_in && max_len <= kSbFuseMaxMsg));
   const bool zc_keyed = zc && keyed && !fuse;  // k_sign_bytes writes the messages into HBM
-  HostBuf& HB = zc ? D.h_zin : D.h_in;
+  // split: the early-staged signatures (and keys) in HBM, the rest -- the
+  // fused helper's templates, flags and timestamps, ~17 bytes a signature --
+  // read in place from mapped memory, so the launch waits for no second copy.
+  // Measured on MI355X (tools/early_ab.sh, three alternating rounds):
+  // verify_commit_10k_keyset p50 0.1435-0.1443 -> 0.1350-0.1359 ms (kernel
+  // +3 us: its hash helper reads the fields over PCIe), verify_commit_10k
+  // 0.293-0.303 -> 0.289-0.294 ms.
+  const bool split = early && zero_copy && ctx->zc_in && fuse && (keyed || early_pk);
+  HostBuf& HB = (zc || split) ? D.h_zin : D.h_in;
   if ((e = HB.ensure(in_bytes)) != hipSuccess) return hip_fail(e);
   if (!zc && (e = D.d_in.ensure(dev_bytes)) != hipSuccess) return hip_fail(e);
   if (zc_keyed && (e = D.d_in.ensure(mb + 16)) != hipSuccess) return hip_fail(e);
@@ -1083,11 +1091,17 @@ static int enqueue_shard(cmtv_ctx* ctx, size_t g, const HostBatch& B, size_t a, 
   uint8_t* din = static_cast<uint8_t*>(D.d_in.p);
   uint8_t* dmsg = din + o_msg;  // the templated sign-bytes, written by k_sign_bytes
   auto* dout = static_cast<uint8_t*>(D.d_out.p);
-  if (zc) {
+  // where the kernel reads the signatures and (generic) keys: HBM unless
+  // the whole staging is read in place
+  uint8_t* dsig = din + o_sig;
+  uint8_t* dkey = din + o_key;
+  if (zc || split) {
     void* p = nullptr;
     if ((e = hipHostGetDevicePointer(&p, HB.p, 0)) != hipSuccess) return hip_fail(e);
     din = static_cast<uint8_t*>(p);
     dmsg = zc_keyed ? static_cast<uint8_t*>(D.d_in.p) : din + o_msg;
+    if (zc) dsig = din + o_sig;
+    if (zc || keyed) dkey = din + o_key;  // key indices (keyed) are in the mapped staging
   } else {
     const size_t from = early_pk ? o_off : early ? o_key : 0;  // what the early copy did not carry
     if ((e = hipMemcpyAsync(din + from, hin + from, in_bytes - from, hipMemcpyHostToDevice, D.stream)) != hipSuccess)
@@ -1114,12 +1128,12 @@ static int enqueue_shard(cmtv_ctx* ctx, size_t g, const HostBatch& B, size_t a, 
   int rc;
   if (keyed)
     rc = enqueue_verify_keyed(ctx, D, B.ks->dev[g], B.ks->n, m,
-                              null_kidx ? nullptr : reinterpret_cast<uint32_t*>(din + o_key),
-                              din + o_sig, tpl ? dmsg : din + o_msg, reinterpret_cast<uint32_t*>(din + o_off), B.mode,
-                              dv, bitmap, D.stream, nullptr, fuse ? &sb : nullptr);
+                              null_kidx ? nullptr : reinterpret_cast<uint32_t*>(dkey), dsig,
+                              tpl ? dmsg : din + o_msg, reinterpret_cast<uint32_t*>(din + o_off), B.mode, dv, bitmap,
+                              D.stream, nullptr, fuse ? &sb : nullptr);
   else
-    rc = enqueue_verify(ctx, D, m, din + o_key, din + o_sig, din + o_msg, reinterpret_cast<uint32_t*>(din + o_off),
-                        B.mode, dv, bitmap, D.stream, fuse ? &sb : nullptr);
+    rc = enqueue_verify(ctx, D, m, dkey, dsig, din + o_msg, reinterpret_cast<uint32_t*>(din + o_off), B.mode, dv,
+                        bitmap, D.stream, fuse ? &sb : nullptr);
   phase_add(ctx, kPhLaunch, t_launch);
   return rc;
 }

@@ -80,7 +80,7 @@ constexpr size_t kShardMinDefault = 8192;
 // single-device host batches up to this size return their bitmap through
 // mapped host memory (no D2H copy; the writes are a few PCIe transactions),
 // and fused commit batches read their staging there (no H2D copy). Measured
-// on MI355X (round 4, profiles/r04_zc_max_ab.txt, tools/mid_ab.py, CMTV_ZC_MAX
+// on MI355X (round 4, profiles/r04_zc_max_ab.txt, tools/mid_ab.py, the then knob
 // 4,096 vs 16,384): VerifyCommit at 8,192 0.329-0.330 -> 0.320 ms, at 10,000
 // 0.349 -> 0.341-0.343 ms; the host API unchanged. 4,096 before.
 constexpr size_t kZeroCopyMax = 12288;
@@ -508,9 +508,8 @@ struct cmtv_ctx {
   // fused small host batches read their inputs from mapped host memory (CMTV_NO_ZC_IN=1: off)
   bool zc_in = true;
   bool zc_host_in = true;  // CMTV_ZC_HOST_IN=0: host-API batches copy their staging to HBM
-  bool zc_keyed = false;   // CMTV_ZC_KEYED=1: templated registered-key batches read it in place too
   bool early_sigs = true;  // CMTV_EARLY_SIGS=0: a commit's signatures are staged after its plan
-  // single-device host batches up to this size take the mapped-memory path (CMTV_ZC_MAX)
+  // single-device host batches up to this size take the mapped-memory path
   size_t zc_max = kZeroCopyMax;
   // small host batches on a row kernel poll its tagged bitmap words
   // (run_host_batch_); CMTV_HOST_POLL=0 synchronises the stream
@@ -1026,12 +1025,11 @@ static int enqueue_shard(cmtv_ctx* ctx, size_t g, const HostBatch& B, size_t a, 
   // sign-bytes kernel writes into the staging then; CMTV_ZC_HOST_IN=0 copies
   // it). Measured on MI355X (round 4, profiles/r04_zc_host_ab.txt): host API
   // 150 0.116 -> 0.109 ms, 4,096 0.284 -> 0.269, 10,000 0.343 -> 0.326 ms.
-  // With CMTV_ZC_KEYED=1 a small templated registered-key batch (the
-  // keyset-cache VerifyCommit) reads its staging there too (unfused: only the
-  // sign-bytes that k_sign_bytes writes go to HBM, D.d_in). Off by default:
-  // at 10k signatures the keyed kernel's PCIe reads cost what the H2D copy
-  // saves (round 5, before fusion: p50 0.2010 vs 0.2012 ms, kernel 0.087 vs
-  // 0.071 ms).
+  // Registered-key batches copy it (their signatures are early-staged past
+  // the keyed row band): reading all of it in place was measured no faster
+  // at 150 (p50 0.0525 vs 0.0523-0.0534 ms) and slower at 10k (0.144-0.148
+  // vs 0.136-0.137 ms, kernel 0.089-0.093 vs 0.078 ms; round 5,
+  // profiles/r05_zc_keyed_ab.txt), and that option was retired.
   // the signatures (and keys) staged ahead of the plan: the same bytes are
   // already in h_in (and on their way to d_in on this stream), unless a
   // buffer must grow; a batch that has them reads HBM, not its staging in place
@@ -1039,10 +1037,8 @@ static int enqueue_shard(cmtv_ctx* ctx, size_t g, const HostBatch& B, size_t a, 
                      dev_bytes <= D.d_in.cap;
   const bool early_pk = early && !keyed && D.early_pk && D.early_pk == B.pk + 32 * a && m == D.early_n;
   D.early_src = D.early_pk = nullptr;
-  const bool zc = !early && zero_copy && ctx->zc_in &&
-                  (keyed ? tpl && ctx->zc_keyed
-                         : fuse || (!tpl && ctx->zc_host_in && max_len <= kSbFuseMaxMsg));
-  const bool zc_keyed = zc && keyed && !fuse;  // k_sign_bytes writes the messages into HBM
+  const bool zc = !early && !keyed && zero_copy && ctx->zc_in &&
+                  (fuse || (!tpl && ctx->zc_host_in && max_len <= kSbFuseMaxMsg));
   // split: the early-staged signatures (and keys) in HBM, the rest -- the
   // fused helper's templates, flags and timestamps, ~17 bytes a signature --
   // read in place from mapped memory, so the launch waits for no second copy.
@@ -1054,7 +1050,6 @@ static int enqueue_shard(cmtv_ctx* ctx, size_t g, const HostBatch& B, size_t a, 
   HostBuf& HB = (zc || split) ? D.h_zin : D.h_in;
   if ((e = HB.ensure(in_bytes)) != hipSuccess) return hip_fail(e);
   if (!zc && (e = D.d_in.ensure(dev_bytes)) != hipSuccess) return hip_fail(e);
-  if (zc_keyed && (e = D.d_in.ensure(mb + 16)) != hipSuccess) return hip_fail(e);
   if ((e = D.d_out.ensure(out_bytes)) != hipSuccess) return hip_fail(e);
   auto* hin = static_cast<uint8_t*>(HB.p);
   // a null key_idx (registered keys) means signature i is by key i, a null
@@ -1099,7 +1094,7 @@ static int enqueue_shard(cmtv_ctx* ctx, size_t g, const HostBatch& B, size_t a, 
     void* p = nullptr;
     if ((e = hipHostGetDevicePointer(&p, HB.p, 0)) != hipSuccess) return hip_fail(e);
     din = static_cast<uint8_t*>(p);
-    dmsg = zc_keyed ? static_cast<uint8_t*>(D.d_in.p) : din + o_msg;
+    dmsg = din + o_msg;
     if (zc) dsig = din + o_sig;
     if (zc || keyed) dkey = din + o_key;  // key indices (keyed) are in the mapped staging
   } else {
@@ -1468,7 +1463,7 @@ int verify_templated_locked(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const ui
 // follows stages exactly those signatures on this device (enqueue_shard);
 // otherwise they are overwritten unused.
 int stage_sigs_early_locked(cmtv_ctx* ctx, const uint8_t* sigs, size_t n, const uint8_t* pk) {
-  if (n == 0 || n > ctx->zc_max || ctx->live.size() != 1 || ctx->zc_keyed || !ctx->early_sigs) return CMTV_OK;
+  if (n == 0 || n > ctx->zc_max || ctx->live.size() != 1 || !ctx->early_sigs) return CMTV_OK;
   // the generic row kernels read their staging from mapped memory instead
   // (a copy's latency is most of their call); the quad-family forms gain the
   // HBM reads (10k: kernel 0.255 ms zero-copy, 0.220 ms from HBM)
@@ -1631,9 +1626,7 @@ static void read_env(cmtv_ctx* ctx) {
   if (const char* nf = std::getenv("CMTV_NO_SB_FUSE")) ctx->sb_fuse = nf[0] != '1';
   if (const char* nz = std::getenv("CMTV_NO_ZC_IN")) ctx->zc_in = nz[0] != '1';
   if (const char* zh = std::getenv("CMTV_ZC_HOST_IN")) ctx->zc_host_in = zh[0] != '0';
-  if (const char* zk = std::getenv("CMTV_ZC_KEYED")) ctx->zc_keyed = zk[0] == '1';
   if (const char* es = std::getenv("CMTV_EARLY_SIGS")) ctx->early_sigs = es[0] != '0';
-  if (const char* zm = std::getenv("CMTV_ZC_MAX")) ctx->zc_max = (size_t)std::strtoull(zm, nullptr, 10);
   if (const char* hp = std::getenv("CMTV_HOST_POLL")) ctx->host_poll = std::atoi(hp) != 0;
   if (const char* kl = std::getenv("CMTV_FORCE_K_LATE")) ctx->keyed_wait = kl[0] == '1' ? 0u : kKeyedWaitDefault;
   if (const char* mw = std::getenv("CMTV_KEYED_BATCH_MIN_WAVES")) {

@@ -39,7 +39,7 @@ def main():
     ap.add_argument("--n", default="4096,8192,10000,16384")
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--mode", type=int, default=0)
-    ap.add_argument("--zc-max", type=int, default=0, help="CMTV_ZC_MAX for the commit context (0: default)")
+    ap.add_argument("--zc-max", type=int, default=0, help="CMTV_ZC_MAX for the commit context (0: default; the knob was retired in round 5)")
     ap.add_argument("--ctx-env", default="", help="KEY=VAL,... set while the commit context opens")
     a = ap.parse_args()
     import torch

@@ -138,12 +138,13 @@ struct SigBatch {
   const cmtv_valset* last_vs = nullptr;
   bool one_vs = true;
 
-  // the one-pass form of a single commit (job_prepare_fast): u32 offsets
-  // written directly, keys checked packed
+  // the one-pass form of a single commit (job_prepare_fast): no message
+  // offsets (the runtime derives them only for a form that reads them), every
+  // message at most msg_bound bytes; keys checked packed
   bool fast = false, keys_packed = false;
-  std::vector<uint32_t> off32;
+  uint32_t msg_bound = 0;
 
-  size_t size() const { return fast ? off32.size() - 1 : off.size() - 1; }
+  size_t size() const { return fast ? tflag.size() : off.size() - 1; }
   const uint8_t* pk_data() const { return pk_src ? pk_src : pk.data(); }
   const uint8_t* sg_data() const { return sg_src ? sg_src : sg.data(); }
   const int64_t* sec_data() const { return sec_src ? sec_src : tsec.data(); }
@@ -231,8 +232,11 @@ bool templated_enabled() {
 // A single commit whose plan is a prefix of its signatures (VerifyCommit: no
 // absent or unknown flags; VerifyCommitLight: no nil votes before the
 // threshold) with keys packed at 32 bytes and signatures at 64: one pass
-// plans it and writes the per-signature flag, key index and u32 message
-// offset (the caller's key, signature and timestamp arrays are the batch).
+// plans it and writes the per-signature flag (the caller's key, signature and
+// timestamp arrays are the batch; no message offsets: every message is at
+// most msg_len_bound bytes, and the fused kernels the runtime picks for such
+// a batch build each message from the template -- runtime.cpp
+// verify_templated_locked derives the offsets for any other form).
 // False (B left empty) sends it down the general path.
 bool job_prepare_fast(CommitJob& J, SigBatch& B) {
   const cmtv_valset* vals = J.vals;
@@ -245,44 +249,45 @@ bool job_prepare_fast(CommitJob& J, SigBatch& B) {
   SbTemplate t{};
   const size_t tb = put_commit_template(nullptr, 0, J.chain_id, J.chain_id_len, c, &t);
   const TplLens tl{t.pre_commit_len, t.pre_nil_len, t.post_len};
+  const uint32_t bound = msg_len_bound(tl);
+  if ((uint64_t)bound * n + 16 >= (1ull << 31)) return false;
   B.tflag.resize(n);
-  B.off32.resize(n + 1);
   uint8_t* tf = B.tflag.data();
-  uint32_t* of = B.off32.data();
   const uint8_t* fl = c->flags;
   const uint32_t* po = vals->pk_off;
   const uint32_t* so = c->sig_off;
-  const int64_t* se = c->ts_seconds;
-  const int32_t* na = c->ts_nanos;
   const int64_t* vp = vals->voting_power;
-  uint64_t o = 0;
   int64_t tally = 0;
   uint32_t m = 0;
   auto bail = [&] {  // leave B as it was
     B.tflag.clear();
-    B.off32.clear();
     return false;
   };
-  for (uint32_t i = 0; i < n; i++) {
-    const uint8_t f = fl[i];
-    const bool fb = f == kFlagCommit;
-    if (!(fb || (full && f == kFlagNil))) return bail();
-    if (po[i + 1] != 32 * (i + 1) || so[i + 1] != 64 * (i + 1)) return bail();
-    tf[i] = fb ? 1 : 0;
-    of[i] = (uint32_t)o;
-    o += msg_len(tl, fb, se[i], na[i]);
-    m = i + 1;
-    if (full) {
-      if (fb) tally += vp[i];
-    } else {
+  if (full) {
+    // branch-free passes the compiler vectorises: offsets, flags, tally
+    uint32_t bad = 0;
+    for (uint32_t i = 1; i <= n; i++) bad |= (po[i] ^ (32u * i)) | (so[i] ^ (64u * i));
+    for (uint32_t i = 0; i < n; i++) {
+      const uint8_t f = fl[i];
+      const uint8_t fb = f == kFlagCommit;
+      bad |= (uint32_t)(!fb & (f != kFlagNil));
+      tf[i] = fb;
+      tally += fb ? vp[i] : 0;
+    }
+    if (bad) return bail();
+    m = n;
+  } else {
+    for (uint32_t i = 0; i < n; i++) {
+      if (fl[i] != kFlagCommit) return bail();
+      if (po[i + 1] != 32 * (i + 1) || so[i + 1] != 64 * (i + 1)) return bail();
+      tf[i] = 1;
+      m = i + 1;
       tally += vp[i];
       if (tally > J.needed) break;
     }
   }
-  if (o + 16 >= (1ull << 31)) return bail();
-  of[m] = (uint32_t)o;
   B.tflag.resize(m);
-  B.off32.resize(m + 1);
+  B.msg_bound = bound;
   B.fast = true;
   B.keys_packed = full;  // every key checked (a light plan stops early)
   // no key index or template index arrays: signature i is by validator i
@@ -535,12 +540,14 @@ int batch_verify(cmtv_ctx* ctx, SigBatch& B, uint32_t mode, std::vector<uint8_t>
     bool packed = true;
     if (!B.keys_packed)
       for (uint32_t i = 0; i <= B.vs->n_vals && packed; i++) packed = B.vs->pk_off[i] == 32 * i;
+    const uint64_t tk = cmtv::phase_now(ctx);
     if (packed) ks = cmtv::keyset_for_locked(ctx, B.vs->pubkeys, B.vs->n_vals);
+    cmtv::phase_add(ctx, cmtv::kPhKeyset, tk);
   }
-  if (B.fast)  // one device batch, offsets already 32-bit (job_prepare_fast)
-    return cmtv::verify_templated_locked(ctx, m, ks ? nullptr : B.pk_data(), B.sg_data(), B.off32.data(),
-                                         B.tmpls.data(), 1, B.blob.data(), B.blob.size(), nullptr, B.tflag.data(),
-                                         B.sec_data(), B.nanos_data(), mode, valid.data(), ks, nullptr);
+  if (B.fast)  // one device batch, message offsets left to the runtime (job_prepare_fast)
+    return cmtv::verify_templated_locked(ctx, m, ks ? nullptr : B.pk_data(), B.sg_data(), nullptr, B.tmpls.data(), 1,
+                                         B.blob.data(), B.blob.size(), nullptr, B.tflag.data(), B.sec_data(),
+                                         B.nanos_data(), mode, valid.data(), ks, nullptr, B.msg_bound);
   if (!B.templated && B.msgs.empty()) B.msgs.push_back(0);
   std::vector<uint32_t> off32;
   const uint64_t kMaxBatchMsgBytes = max_batch_msg_bytes();

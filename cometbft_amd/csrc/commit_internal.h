@@ -12,6 +12,7 @@
 #include <stdint.h>
 #include <stddef.h>
 
+#include <algorithm>
 #include <cinttypes>
 #include <cstdio>
 #include <cstring>
@@ -120,18 +121,14 @@ inline size_t put_commit_template(uint8_t* blob, size_t at, const char* chain_id
   return w.n;
 }
 
-// sb_msg_len (signbytes.h) without loops: varint lengths from the bit width
-// by table. Same value for every input (tests/host/pipecheck.cpp's fake
-// device checks each message's offsets against sb_msg_len).
-struct UvlenTable {
-  uint8_t len[65];
-  constexpr UvlenTable() : len() {
-    for (int b = 0; b <= 64; b++) len[b] = (uint8_t)(b <= 7 ? 1 : (b + 6) / 7);
-  }
-};
+// sb_msg_len (signbytes.h) without loops or tables: a varint's length is
+// ceil(bits / 7) (at least 1), and (bits + 6) / 7 == ((bits + 6) * 37) >> 8
+// for every bits in 1..64 (checked exhaustively by tests/test_pipeline_cpu.py's
+// host build: tests/host/pipecheck.cpp compares every message's offsets with
+// sb_msg_len). Same value for every input.
 inline uint32_t uvlen(uint64_t v) {
-  static constexpr UvlenTable t;
-  return t.len[64 - __builtin_clzll(v | 1)];
+  const uint32_t bits = 64 - (uint32_t)__builtin_clzll(v | 1);
+  return ((bits + 6) * 37) >> 8;
 }
 
 struct TplLens {
@@ -142,7 +139,13 @@ inline uint32_t msg_len(const TplLens& t, bool commit_flag, int64_t sec, int32_t
   // the timestamp is at most 22 bytes, so its length varint is one byte
   const uint32_t tl = (sec != 0 ? 1 + uvlen((uint64_t)sec) : 0) + (nanos != 0 ? 1 + uvlen((uint64_t)(int64_t)nanos) : 0);
   const uint32_t b = (commit_flag ? t.pre_commit : t.pre_nil) + 2 + tl + t.post;
-  return uvlen(b) + b;
+  return b + (b < 128 ? 1 : uvlen(b));
+}
+
+// the longest message a template can give (a 22-byte timestamp)
+inline uint32_t msg_len_bound(const TplLens& t) {
+  const uint32_t b = std::max(t.pre_commit, t.pre_nil) + 2 + 22 + t.post;
+  return b + uvlen(b);
 }
 
 // ------------------------------------------------------------------ formatting

@@ -965,6 +965,7 @@ struct HostBatch {
   const uint32_t* key_idx = nullptr;
   const uint8_t* sig = nullptr;
   const uint32_t* msg_off = nullptr;
+  uint32_t msg_bound = 0;  // templated with msg_off null: every message is at most this long
   const uint8_t* msg = nullptr;
   const SbTemplate* tmpls = nullptr;
   size_t n_tmpls = 0;
@@ -984,7 +985,10 @@ static int enqueue_shard(cmtv_ctx* ctx, size_t g, const HostBatch& B, size_t a, 
   CmtvDev& D = ctx->devs[g];
   const size_t m = b - a;
   const bool keyed = B.ks != nullptr, tpl = B.msg == nullptr;
-  const size_t mb = (size_t)B.msg_off[b] - B.msg_off[a];
+  // no offsets (verify_templated_locked: the fused small-batch path only):
+  // sized by the bound, never written
+  const bool no_off = tpl && !B.msg_off;
+  const size_t mb = no_off ? (size_t)B.msg_bound * m : (size_t)B.msg_off[b] - B.msg_off[a];
   const size_t key_bytes = keyed ? 4 * m : 32 * m;
   // signatures first: an early-staged commit's (stage_sigs_early_locked) are
   // already there, on their way to the device
@@ -1012,9 +1016,10 @@ static int enqueue_shard(cmtv_ctx* ctx, size_t g, const HostBatch& B, size_t a, 
   const uint64_t t_stage = phase_now(ctx);
   (void)hipSetDevice(D.ordinal);
   // message lengths first: they decide the fused / zero-copy forms
-  const uint32_t base = B.msg_off[a];
-  uint32_t max_len = 0;
-  for (size_t i = 0; i < m; i++) max_len = std::max(max_len, B.msg_off[a + i + 1] - B.msg_off[a + i]);
+  const uint32_t base = no_off ? 0u : B.msg_off[a];
+  uint32_t max_len = no_off ? B.msg_bound : 0u;
+  if (!no_off)
+    for (size_t i = 0; i < m; i++) max_len = std::max(max_len, B.msg_off[a + i + 1] - B.msg_off[a + i]);
   // templated sign-bytes written by the verify kernel's helper wave (no
   // k_sign_bytes launch) when the batch runs a split kernel and every
   // message fits the helper's LDS slot; CMTV_NO_SB_FUSE turns it off
@@ -1065,8 +1070,10 @@ static int enqueue_shard(cmtv_ctx* ctx, size_t g, const HostBatch& B, size_t a, 
     std::memcpy(hin + o_key, B.pk + 32 * a, 32 * m);
   }
   if (!early) std::memcpy(hin + o_sig, B.sig + 64 * a, 64 * m);
+  if (no_off && !fuse) return CMTV_EINVAL;  // verify_templated_locked derives offsets for every other form
   auto* hoff = reinterpret_cast<uint32_t*>(hin + o_off);
-  for (size_t i = 0; i <= m; i++) hoff[i] = B.msg_off[a + i] - base;
+  if (!no_off)
+    for (size_t i = 0; i <= m; i++) hoff[i] = B.msg_off[a + i] - base;
   if (tpl) {
     if (B.tidx)
       std::memcpy(hin + o_tidx, B.tidx + a, 4 * m);
@@ -1436,7 +1443,27 @@ int verify_templated_locked(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const ui
                             const void* tmpls, size_t n_tmpls, const uint8_t* blob, size_t blob_len,
                             const uint32_t* tidx, const uint8_t* commit_flag, const int64_t* sec,
                             const int32_t* nanos, uint32_t mode, uint8_t* out_valid, const cmtv_keyset* ks,
-                            const uint32_t* key_idx) {
+                            const uint32_t* key_idx, uint32_t msg_bound) {
+  // no offsets: the fused kernels of a small single-device batch build every
+  // message from its template and never read them (enqueue_shard); any other
+  // form gets them derived here, exactly as sb_msg_len gives them
+  std::vector<uint32_t> off_v;
+  if (!msg_off) {
+    const bool fused_small = ctx->live.size() == 1 && n <= ctx->zc_max && ctx->sb_fuse && msg_bound <= kSbFuseMaxMsg &&
+                             (ks ? keyed_fuse_ok(ctx, n) : fuse_ok(ctx, n));
+    if (!fused_small) {
+      off_v.resize(n + 1);
+      uint64_t o = 0;
+      const auto* tp = static_cast<const SbTemplate*>(tmpls);
+      for (size_t i = 0; i < n; i++) {
+        off_v[i] = (uint32_t)o;
+        o += sb_msg_len(tp[tidx ? tidx[i] : 0], commit_flag[i] != 0, sec[i], nanos[i]);
+      }
+      if (o + 16 >= (1ull << 31)) return CMTV_EINVAL;
+      off_v[n] = (uint32_t)o;
+      msg_off = off_v.data();
+    }
+  }
   HostBatch B;
   B.n = n;
   B.mode = mode;
@@ -1445,6 +1472,7 @@ int verify_templated_locked(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const ui
   B.key_idx = key_idx;
   B.sig = sig;
   B.msg_off = msg_off;
+  B.msg_bound = msg_bound;
   B.tmpls = static_cast<const SbTemplate*>(tmpls);
   B.n_tmpls = n_tmpls;
   B.blob = blob;
@@ -1463,6 +1491,12 @@ int verify_templated_locked(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const ui
 // follows stages exactly those signatures on this device (enqueue_shard);
 // otherwise they are overwritten unused.
 int stage_sigs_early_locked(cmtv_ctx* ctx, const uint8_t* sigs, size_t n, const uint8_t* pk) {
+  const uint64_t t0 = phase_now(ctx);
+  struct Done {
+    cmtv_ctx* c;
+    uint64_t t;
+    ~Done() { phase_add(c, kPhEarly, t); }
+  } done{ctx, t0};
   if (n == 0 || n > ctx->zc_max || ctx->live.size() != 1 || !ctx->early_sigs) return CMTV_OK;
   // the generic row kernels read their staging from mapped memory instead
   // (a copy's latency is most of their call); the quad-family forms gain the
@@ -1820,7 +1854,8 @@ void cmtv_close(cmtv_ctx* ctx) {
   if (!ctx) return;
   if (ctx->phases_on) {
     static const char* names[kPhCount] = {"prepare",   "stage",     "launch",      "wait",      "post",       "replay",
-                                          "pipe_plan", "pipe_pack", "pipe_submit", "pipe_wait", "pipe_replay"};
+                                          "pipe_plan", "pipe_pack", "pipe_submit", "pipe_wait", "pipe_replay",
+                                          "keyset",    "early"};
     std::fprintf(stderr, "{\"cmtv_host_phases_us\": {");
     for (int p = 0; p < kPhCount; p++)
       std::fprintf(stderr, "%s\"%s\": %.3f", p ? ", " : "", names[p],

@@ -36,7 +36,11 @@ int verify_templated_locked(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const ui
                             const void* tmpls, size_t n_tmpls, const uint8_t* blob, size_t blob_len,
                             const uint32_t* tidx, const uint8_t* commit_flag, const int64_t* sec,
                             const int32_t* nanos, uint32_t mode, uint8_t* out_valid,
-                            const cmtv_keyset* ks = nullptr, const uint32_t* key_idx = nullptr);
+                            const cmtv_keyset* ks = nullptr, const uint32_t* key_idx = nullptr,
+                            uint32_t msg_bound = 0);
+// (msg_off null: no message offsets, every message at most msg_bound bytes;
+// derived from the templates here unless the fused small-batch path, which
+// never reads them, runs the batch)
 
 // A single commit's n contiguous 64-byte signatures -- and, for the generic
 // kernels (pk set: the validator set's n packed 32-byte keys), its keys --
@@ -60,7 +64,7 @@ bool keyset_cache_enabled(const cmtv_ctx* ctx);
 // replay; each summed over the host worker threads' wall time, not CPU time.
 enum HostPhase {
   kPhPrepare, kPhStage, kPhLaunch, kPhWait, kPhPost, kPhReplay,
-  kPhPipePlan, kPhPipePack, kPhPipeSubmit, kPhPipeWait, kPhPipeReplay, kPhCount
+  kPhPipePlan, kPhPipePack, kPhPipeSubmit, kPhPipeWait, kPhPipeReplay, kPhKeyset, kPhEarly, kPhCount
 };
 uint64_t phase_now(const cmtv_ctx* ctx);
 void phase_add(cmtv_ctx* ctx, int phase, uint64_t t0);

@@ -64,11 +64,17 @@ int main(int argc, char** argv) {
   fake_set_noverify(ctx, true);
   const char chain[] = "cmtverify-bench";
   double best = 1e30;
-  const int iters = H == 1 ? 200 : 6;
+  // argv[7] = 1: the single-commit entry point (cmtv_verify_commit on
+  // commit 0) instead, its host cost per call
+  const bool single = argc > 7 && std::atoi(argv[7]) != 0;
+  const int iters = single ? 20000 : H == 1 ? 200 : 6;
   for (int it = 0; it < iters; it++) {
     const auto t0 = std::chrono::steady_clock::now();
-    const int rc = cmtv_verify_commits(ctx, kind, 0, chain, sizeof chain - 1, H, vals.data(), bids.data(), hs.data(),
-                                       cs.data(), 1, 3, res.data(), rcs.data(), nullptr, 0);
+    const int rc = single ? cmtv_verify_commit(ctx, kind, 0, chain, sizeof chain - 1, &vals[0], &bids[0], hs[0], &cs[0],
+                                               1, 3, &res[0], nullptr, 0)
+                          : cmtv_verify_commits(ctx, kind, 0, chain, sizeof chain - 1, H, vals.data(), bids.data(),
+                                                hs.data(), cs.data(), 1, 3, res.data(), rcs.data(), nullptr, 0);
+    if (single) rcs[0] = rc;
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (rc != CMTV_OK || rcs[0] != 0) {
       std::fprintf(stderr, "rc %d rcs[0] %d\n", rc, rcs[0]);

@@ -141,6 +141,94 @@ __device__ __forceinline__ bool keyed_comb_wide_dma(ge_p3& acc, const uint32_t* 
   return ok;
 }
 
+// keyed.h keyed_comb_mixed with the table rows fetched one addition ahead:
+// each addition's three niels coordinates (its row of the key's radix-256
+// comb or of B's radix-2^16 comb, both MALL / HBM resident) are loaded into
+// registers while the previous addition computes, so the load latency hides
+// behind it instead of stalling every addition (the plain form waits on
+// memory ~22 % of its wave cycles, profiles/r05_pmc_sq.txt). Same additions
+// in the same order, so the same R' (the batched kernels' parity tests).
+struct PfRow {
+  fe c0, c1, c2;
+  bool neg, ident;
+};
+struct PfRowTab {  // a fetched row as an ge_add_table source
+  const PfRow& r;
+  __device__ __forceinline__ void load_fe(int, int c, fe& q) const {
+#pragma unroll
+    for (int i = 0; i < 10; i++) q.v[i] = c == 0 ? r.c0.v[i] : (c == 1 ? r.c1.v[i] : r.c2.v[i]);
+  }
+};
+
+__device__ __forceinline__ bool keyed_comb_mixed_pf(ge_p3& acc, const uint32_t* key_pk, bool key_ok,
+                                                    const uint32_t* sig_ptr, const uint8_t* msg, uint32_t mlen,
+                                                    const uint32_t* __restrict__ ktab,
+                                                    const uint32_t* __restrict__ btab) {
+  uint32_t w[16];
+#pragma unroll
+  for (int i = 0; i < 8; i++) w[i] = sig_ptr[8 + i];  // S
+  const bool ok = key_ok && (w[7] & 0xE0000000u) == 0 && sc_is_canonical(w);
+  uint32_t sLo[8], sHi[8], tk[8];
+  hs_digits65536(sLo, sHi, w);
+  uint32_t h[16], k[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    w[i] = sig_ptr[i];  // R
+    w[8 + i] = key_pk[i];
+  }
+  sha512_prefixed<16>(h, w, msg, mlen);
+  sc_reduce512(k, h);
+  sc_bias(tk, k, 0x80808080u);
+  // the additions in keyed_comb_mixed's order: A position j = 31..0, and
+  // after each odd j the B position j >> 1
+  int j = COMB_WINDOWS - 1;
+  bool next_b = false;
+  auto fetch = [&](PfRow& r) {
+    if (!next_b) {
+      const int d = (int)sc_shift_out(tk, 8) - 128;
+      const int i = d < 0 ? -d : d;
+      const DevCombWindow win{ktab + ((size_t)j * COMB_ENTRIES + (i > 0 ? i - 1 : 0)) * COMB_ROW_WORDS};
+      win.load_fe(0, 0, r.c0);
+      win.load_fe(0, 1, r.c1);
+      win.load_fe(0, 2, r.c2);
+      r.neg = d < 0;
+      r.ident = i == 0;
+      if (j & 1)
+        next_b = true;
+      else
+        j--;
+    } else {
+      const int jb = j >> 1;
+      const int d = (int)(jb >= 8 ? sc_shift_out(sHi, 16) : sc_shift_out(sLo, 16)) - 0x8000;
+      const int i = d < 0 ? -d : d;
+      const DevBTab bt{btab + (size_t)(BC16_BASE + jb * BT16_ENTRIES + (i > 0 ? i - 1 : 0)) * BTAB_ROW_WORDS};
+      bt.load_fe(0, 0, r.c0);
+      bt.load_fe(0, 1, r.c1);
+      bt.load_fe(0, 2, r.c2);
+      r.neg = d < 0;
+      r.ident = i == 0;
+      next_b = false;
+      j--;
+    }
+  };
+  constexpr int kSteps = COMB_WINDOWS + COMB_WINDOWS / 2;  // 48
+  static_assert(kSteps % 2 == 0, "ping-pong over pairs of additions");
+  p3_identity(acc);
+  ge_efgh t;
+  PfRow r0, r1;
+  fetch(r0);
+#pragma unroll 1
+  for (int st = 0; st < kSteps; st += 2) {
+    fetch(r1);
+    ge_add_table<false>(t, acc, PfRowTab{r0}, 0, r0.neg, r0.ident);
+    efgh_to_p3(acc, t);
+    if (st + 2 < kSteps) fetch(r0);
+    ge_add_table<false>(t, acc, PfRowTab{r1}, 0, r1.neg, r1.ident);
+    efgh_to_p3(acc, t);
+  }
+  return ok;
+}
+
 // R' = [s]B - [k]A of one signature by registered key kid over the tables
 // COMB selects: ktabs = the key combs (wide for kCombWideDma, else radix-256),
 // btab = the B table, whose BC16 blocks are B's radix-2^16 comb.
@@ -152,8 +240,8 @@ __device__ __forceinline__ bool keyed_comb_dev(ge_p3& acc, uint32_t kid, bool ke
   if (COMB == kCombWideDma)
     return keyed_comb_wide_dma(acc, keys_pk + 8 * (size_t)kid, key_ok, sig_ptr, msg, mlen,
                                ktabs + (size_t)kid * WIDE_TABLE_WORDS, btab, stage);
-  return keyed_comb_mixed<DevCombWindow>(acc, keys_pk + 8 * (size_t)kid, key_ok, sig_ptr, msg, mlen,
-                                         ktabs + (size_t)kid * COMB_TABLE_WORDS, DevBTab{btab});
+  return keyed_comb_mixed_pf(acc, keys_pk + 8 * (size_t)kid, key_ok, sig_ptr, msg, mlen,
+                             ktabs + (size_t)kid * COMB_TABLE_WORDS, btab);
 }
 
 // this wave's LDS stage (kCombWideDma only; one wave per workgroup)

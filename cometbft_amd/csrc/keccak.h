@@ -24,7 +24,19 @@ CMTV_HD uint64_t keccak_rc(int r) {
   return RC[r];
 }
 
-CMTV_HD uint64_t keccak_rotl(uint64_t x, int n) { return n ? (x << n) | (x >> (64 - n)) : x; }
+// 64-bit rotate; n is a constant after unrolling. On the device each half is
+// one funnel shift (v_alignbit_b32) instead of two 64-bit shifts and an or.
+CMTV_HD uint64_t keccak_rotl(uint64_t x, int n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  const uint32_t h = n < 32 ? hi : lo, l = n < 32 ? lo : hi;
+  const int m = n & 31;
+  if (m == 0) return ((uint64_t)h << 32) | l;
+  return ((uint64_t)__builtin_amdgcn_alignbit(h, l, 32 - m) << 32) | __builtin_amdgcn_alignbit(l, h, 32 - m);
+#else
+  return n ? (x << n) | (x >> (64 - n)) : x;
+#endif
+}
 
 // rho offset of lane i = x + 5y, and pi destination y + 5((2x + 3y) mod 5)
 CMTV_HD int keccak_rho(int i) {

@@ -118,7 +118,7 @@ hipError_t launch_wide_build(uint32_t n_keys, const void* keys_pk, uint32_t* tab
 // and the running product of the Z's)
 constexpr uint32_t kKeyedBatchScratchWordsPerSig = 40;
 hipError_t launch_verify_sr25519(uint32_t n, const void* pk, const void* sig, const void* msg, const void* off,
-                                 const uint32_t* btab, uint32_t* atab, const uint16_t* prog, int nops, void* valid,
+                                 const uint32_t* btab, uint32_t* atab, const uint32_t* prog, int nops, void* valid,
                                  void* bitmap, uint32_t kflags, hipStream_t s);
 hipError_t launch_sign_bytes(uint32_t n, const void* tmpls, const uint8_t* blob, const uint32_t* tidx,
                              const uint8_t* commit_flag, const int64_t* sec, const int32_t* nanos,

@@ -103,7 +103,7 @@ CMTV_HD bool ristretto_decode(ge_p3& h, const uint32_t w[8]) {
 // a 64-byte signature). prog/nops: the transcript program (merlin.h).
 template <class ATab, class BTab, class State>
 CMTV_HD bool sr_verify_one(const uint32_t* pk_ptr, const uint32_t* sig_ptr, const uint8_t* msg, uint32_t mlen,
-                           const uint16_t* prog, int nops, State& st, ATab& atab, const BTab& btab) {
+                           const uint32_t* prog, int nops, State& st, ATab& atab, const BTab& btab) {
   uint32_t pk[8], rw[8], ts[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) {

@@ -23,9 +23,14 @@ namespace cmtv {
 // needed): schnorrkel marker and canonical s, the merlin challenge k mod L,
 // the half-size pair and u = k2 s mod L. k_verify_sr25519_quad_split runs it
 // on a helper wave.
-template <class State>
+struct NoMark {
+  CMTV_HD void operator()() const {}
+};
+
+template <class State, class Mark = NoMark>
 CMTV_HD void sr_prepare(SigPrep& p, const uint32_t* pk_ptr, const uint32_t* sig_ptr, const uint8_t* msg,
-                        uint32_t mlen, const uint16_t* prog, int nops, State& st, bool force_wide) {
+                        uint32_t mlen, const uint32_t* prog, int nops, State& st, bool force_wide,
+                        const Mark& after_transcript = Mark()) {
   uint32_t pk[8], rw[8], ts[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) {
@@ -40,6 +45,7 @@ CMTV_HD void sr_prepare(SigPrep& p, const uint32_t* pk_ptr, const uint32_t* sig_
   {
     uint32_t kb[16];
     sr_transcript(kb, st, prog, nops, msg, mlen, pk, rw);
+    after_transcript();
     sc_reduce512(k, kb);
   }
   q_prepare_scalars(p, k, ts, force_wide);
@@ -149,7 +155,7 @@ CMTV_HD bool q_verify_sr_hs(const Q& q, const uint32_t* pk_ptr, const uint32_t* 
 // One wave does everything (k_verify_sr25519_quad; the host checks)
 template <class Q, class BTab, class ATab, class State, class Probe = NullProbe>
 CMTV_HD bool q_verify_sr(const Q& q, const uint32_t* pk_ptr, const uint32_t* sig_ptr, const uint8_t* msg,
-                         uint32_t mlen, const uint16_t* prog, int nops, State& st, const BTab& btab, ATab& tabA,
+                         uint32_t mlen, const uint32_t* prog, int nops, State& st, const BTab& btab, ATab& tabA,
                          ATab& tabR, const Probe& probe = Probe(), bool force_wide = false) {
   return q_verify_sr_split(
       q, pk_ptr, sig_ptr, btab, tabA, tabR,

@@ -213,8 +213,9 @@ int main(int argc, char** argv) {
     basepoint_words(bw);
     bcomb = host_comb(bw, false, &bok);
   }
-  uint16_t prog[SR_PROGRAM_MAX];
-  const int nops = sr_build_program(prog);
+  uint32_t prog[SR_PROGRAM_WORDS];  // the program the runtime uploads
+  const int nops = sr_build_device_program(prog);
+  if (nops <= 0) return 2;
   HostBTab bt;
   uint32_t n, k2_neg_count = 0;
   if (fread(&n, 4, 1, stdin) != 1) return 1;

@@ -4,9 +4,12 @@
 //   input  (stdin):  u32 n, then n x { u8 pk[32], u8 sig[64], u32 mlen, u8 msg[mlen] }
 //   output (stdout): n bytes of verdicts
 //   argv[1] == "challenge": n x 64 challenge bytes instead (transcript only)
+// Runs the device program (sr_build_device_program: precomputed constant
+// prefix) and checks every challenge against the full program's.
 #define CMTV_HD inline
 #define CMTV_BOUNDS_CHECK 1
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 #include "../../cometbft_amd/csrc/sr25519.h"
@@ -39,8 +42,11 @@ static void to_words(uint32_t* w, const uint8_t* b, int nw) {
 int main(int argc, char** argv) {
   const bool chal = argc > 1 && !strcmp(argv[1], "challenge");
   HostBTab bt;
-  uint16_t prog[SR_PROGRAM_MAX];
-  const int nops = sr_build_program(prog);
+  uint32_t full[SR_PROGRAM_WORDS];
+  const int nfull = sr_build_program(full);
+  uint32_t prog[SR_PROGRAM_WORDS];
+  const int nops = sr_build_device_program(prog);
+  if (nops <= SR_STATE_DESCS || nops > SR_PROGRAM_MAX) return 2;
   uint32_t n;
   if (fread(&n, 4, 1, stdin) != 1) return 1;
   for (uint32_t i = 0; i < n; i++) {
@@ -56,6 +62,17 @@ int main(int argc, char** argv) {
     to_words(pk, pkb, 8);
     to_words(sig, sigb, 16);
     ArrayStrobeState st;
+    {
+      uint32_t ref[16];
+      ArrayStrobeState st2;
+      sr_transcript(ref, st2, full, nfull, msg, mlen, pk, sig);
+      uint32_t out[16];
+      sr_transcript(out, st, prog, nops, msg, mlen, pk, sig);
+      if (memcmp(out, ref, sizeof(out))) {
+        fprintf(stderr, "device program challenge differs at %u\n", i);
+        abort();
+      }
+    }
     if (chal) {
       uint32_t out[16];
       sr_transcript(out, st, prog, nops, msg, mlen, pk, sig);

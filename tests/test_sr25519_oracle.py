@@ -168,6 +168,29 @@ def test_device_transcript_matches_oracle(srcheck, vectors):
         assert out[64 * j: 64 * (j + 1)] == t.extract_bytes(b"sign:c", 64), i
 
 
+def test_device_transcript_every_length(srcheck):
+    """The chunked transcript at every message length 0..340: every position
+    the 4-byte chunks, the headers and the key words can meet the STROBE
+    block end (R = 166) at, against the Python merlin (srcheck also checks
+    the device program -- precomputed prefix -- against the full one)."""
+    rng = np.random.default_rng(7)
+    lens = list(range(0, 341))
+    pks = [rng.integers(0, 256, 32, dtype=np.uint8).tobytes() for _ in lens]
+    sigs = [rng.integers(0, 256, 64, dtype=np.uint8).tobytes() for _ in lens]
+    msgs = [rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in lens]
+    buf = [struct.pack("<I", len(lens))]
+    for pk, sig, m in zip(pks, sigs, msgs):
+        buf += [pk, sig, struct.pack("<I", len(m)), m]
+    out = subprocess.run([srcheck, "challenge"], input=b"".join(buf), capture_output=True, check=True,
+                         timeout=600).stdout
+    for j, (pk, sig, m) in enumerate(zip(pks, sigs, msgs)):
+        t = S.signing_context(b"", m)
+        t.append_message(b"proto-name", b"Schnorr-sig")
+        t.append_message(b"sign:pk", pk)
+        t.append_message(b"sign:R", sig[:32])
+        assert out[64 * j: 64 * (j + 1)] == t.extract_bytes(b"sign:c", 64), len(m)
+
+
 def test_device_pipeline_matches_corpus(srcheck, vectors):
     """sr25519.h (the kernel's source, host build with bound checks) over the
     whole corpus."""

@@ -3,6 +3,7 @@
 
   make -C cometbft_amd/csrc OUT=../../abtest/libprobe.so BUILD=../../build/probe KFLAGS=-DCMTV_PHASE_PROBE
   CMTV_LIBRARY=$PWD/abtest/libprobe.so python tools/phase_probe.py [n]
+  CMTV_LIBRARY=$PWD/abtest/libprobe.so python tools/phase_probe.py --sr [n]   (k_verify_sr25519_quad_hs)
 
 Lane 0 of every wave records the shader clock at kernel entry (0), before /
 after barrier 1 (1, 2: the helper's scalars), before / after barrier 2 (3, 4:
@@ -27,27 +28,38 @@ SLOTS = 8
 
 
 def main():
-    n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000
+    sr = "--sr" in sys.argv
+    argv = [a for a in sys.argv[1:] if a != "--sr"]
+    n = int(argv[0]) if len(argv) > 0 else 10_000
     # signatures per 4-wave workgroup: 48 (k_verify_quad_split) or 3 (the row
     # kernel, k_verify_row_split, which the library picks up to kRowMax)
-    per_wg = int(sys.argv[2]) if len(sys.argv) > 2 else 48
+    per_wg = int(argv[1]) if len(argv) > 1 else 48
     from cometbft_amd import Context, pack_messages
     from cometbft_amd import _native as N
     from cometbft_amd import testutil as TU
 
     L = N.lib()
-    fn = L.cmtv_debug_phase_times
+    fn = L.cmtv_debug_phase_times_sr if sr else L.cmtv_debug_phase_times
     fn.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t]
     ctx = Context(device=0)
-    sv = TU.make_validator_set(ctx, n)
     m, off = pack_messages(TU.commit_messages(n, 1000))
-    sig = ctx.sign(sv.seeds, m, off)
-    pk = np.ascontiguousarray(sv.pubkeys)
+    if sr:
+        from oracle import coracle  # synthetic sr25519 signatures only
+
+        rng = np.random.default_rng(4)
+        minis = rng.integers(0, 256, (150, 32), dtype=np.uint8)
+        kidx = (np.arange(n) % 150).astype(np.uint32)
+        sig = coracle.sr25519_sign_batch(minis, m, off, key_idx=kidx)
+        pk = np.ascontiguousarray(coracle.sr25519_pubkeys(minis)[kidx])
+    else:
+        sv = TU.make_validator_set(ctx, n)
+        sig = ctx.sign(sv.seeds, m, off)
+        pk = np.ascontiguousarray(sv.pubkeys)
     wgs = -(-n // per_wg)
     out = {}
-    for mode, name in ((0, "go"), (1, "zip215")):
+    for mode, name in (((0, "sr25519"),) if sr else ((0, "go"), (1, "zip215"))):
         for _ in range(20):
-            v = ctx.verify(pk, sig, m, off, mode)
+            v = ctx.verify_sr25519(pk, sig, m, off) if sr else ctx.verify(pk, sig, m, off, mode)
         assert v.all()
         buf = np.zeros(wgs * 4 * SLOTS, np.uint64)
         assert fn(buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), buf.size) == 0
@@ -81,6 +93,7 @@ def main():
             "quads_wait_at_b2_for_helper": {"wgs": int((w2 > 0).sum()), "median": float(np.median(w2)),
                                             "max": int(w2.max())},
             "helper_b1_median": float(np.median(h[:, 1] - start)),
+            **({"helper_transcript_end_median": float(np.median(h[:, 7] - start))} if sr else {}),
             "helper_b2_minus_b1_release_median": float(np.median(h[:, 3] - q[:, :, 2].max(axis=1))),
             "quad_b1_median": float(np.median(q[:, :, 1] - start[:, None])),
             "quad_b2_median": float(np.median(q[:, :, 3] - start[:, None])),
@@ -92,7 +105,7 @@ def main():
             "last_wg": dict(wg(last), index=last), "median_wg": dict(wg(med), index=med),
         }
         print(name, json.dumps(out[name]), flush=True)
-    with open(os.path.join(ROOT, "gpurun_out", "phase_probe.json"), "w") as f:
+    with open(os.path.join(ROOT, "gpurun_out", "phase_probe_sr.json" if sr else "phase_probe.json"), "w") as f:
         json.dump(out, f, indent=1)
 
 

@@ -396,7 +396,7 @@ struct CmtvDev {
   int ordinal = 0;
   hipStream_t stream = nullptr;
   uint32_t* d_btab = nullptr;
-  uint32_t* d_srprog = nullptr;  // sr25519 transcript program (merlin.h descriptors)
+  uint32_t* d_srprog = nullptr;  // sr25519 transcript: the sponge after the constant prefix (merlin.h)
   DevBuf d_in, d_out, d_all;
   HostBuf h_in, h_out;
   // small single-device host batches: the kernel writes the verdict bitmap
@@ -1563,8 +1563,8 @@ static int init_device(cmtv_ctx* ctx, CmtvDev& D) {
     e = hipMemsetAsync(D.d_rowslots, 0, (size_t)kRowSlots * kRowSlotWords * sizeof(uint32_t), D.stream);
   if (e == hipSuccess) e = hipMalloc(&D.d_btab, kBtabWords * sizeof(uint32_t));
   if (e == hipSuccess) e = launch_btab_init(D.d_btab, D.stream);
-  uint32_t prog[SR_PROGRAM_WORDS];
-  ctx->sr_nops = sr_build_device_program(prog);
+  uint32_t prog[SR_PREFIX_WORDS];
+  ctx->sr_nops = sr_prefix_state(prog);
   if (ctx->sr_nops <= 0 && e == hipSuccess) e = hipErrorInvalidValue;
   if (e == hipSuccess) e = hipMalloc(&D.d_srprog, sizeof(prog));
   if (e == hipSuccess) e = hipMemcpyAsync(D.d_srprog, prog, sizeof(prog), hipMemcpyHostToDevice, D.stream);

@@ -213,8 +213,8 @@ int main(int argc, char** argv) {
     basepoint_words(bw);
     bcomb = host_comb(bw, false, &bok);
   }
-  uint32_t prog[SR_PROGRAM_WORDS];  // the program the runtime uploads
-  const int nops = sr_build_device_program(prog);
+  uint32_t prog[SR_PREFIX_WORDS];  // the program the runtime uploads
+  const int nops = sr_prefix_state(prog);
   if (nops <= 0) return 2;
   HostBTab bt;
   uint32_t n, k2_neg_count = 0;

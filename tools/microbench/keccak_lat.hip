@@ -7,10 +7,10 @@
 // Variants: 0 keccak_f1600 (keccak.h: funnel-shift rotates) on a register
 // state, a dependent chain; 1 the same permutation with 64-bit shift rotates
 // (checked to end in the same state); 2 the whole transcript of a 116-byte
-// message; 3 the transcript of an empty message; then synthetic programs:
-// the resume header and the PRF alone, with 32 one-byte, with 32 four-byte
-// literal chunks. Lane 0 of every wave records
-// s_memtime around the loop; prints mean cycles per item.
+// message; 3 the transcript of an empty message. Lane 0 of every wave records
+// s_memtime around the loop; prints mean cycles per item. Then the scalar
+// cache's latency (a uniform-address pointer chase), alone and with an LDS
+// store per step.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -126,8 +126,8 @@ int main(int argc, char** argv) {
   for (auto& w : hin) w = (x = x * 1664525u + 1013904223u);
   std::vector<uint8_t> hm(1024 * 128 + 64);
   for (auto& b : hm) b = (uint8_t)((x = x * 1664525u + 1013904223u) >> 24);
-  uint32_t prog[SR_PROGRAM_WORDS];
-  const int np = sr_build_device_program(prog);
+  uint32_t prog[SR_PREFIX_WORDS];
+  const int np = sr_prefix_state(prog);
   uint32_t *din, *dout;
   uint8_t* dm;
   uint32_t* dp;
@@ -140,44 +140,12 @@ int main(int argc, char** argv) {
   (void)hipMemcpy(din, hin.data(), hin.size() * 4, hipMemcpyHostToDevice);
   (void)hipMemcpy(dm, hm.data(), hm.size(), hipMemcpyHostToDevice);
   (void)hipMemcpy(dp, prog, sizeof(prog), hipMemcpyHostToDevice);
-  // synthetic programs after the same resume header: the PRF header and F
-  // alone, and 32 one-byte / four-byte literal chunks before them (the
-  // per-descriptor cost)
-  uint32_t p1[SR_PROGRAM_WORDS], p2[SR_PROGRAM_WORDS], p3[SR_PROGRAM_WORDS];
-  int n1 = 0, n2 = 0, n3 = 0;
-  for (int i = 0; i < 2 * SR_STATE_DESCS; i++) p1[n1++] = p2[n2++] = p3[n3++] = prog[i];
-  for (int i = 0; i < 32; i++) {
-    p2[n2++] = (uint32_t)i;
-    p2[n2++] = SD_LIT | (1u << 4);
-    p3[n3++] = 0x01010101u * (uint32_t)i;
-    p3[n3++] = SD_LIT | (4u << 4);
-  }
-  for (uint32_t* p : {p1, p2, p3}) {
-    int& m = p == p1 ? n1 : p == p2 ? n2 : n3;
-    p[m++] = SF_I | SF_A | SF_C;
-    p[m++] = SD_HDR | (2u << 4);
-    p[m++] = 0;
-    p[m++] = SD_FORCE;
-  }
-  n1 /= 2;
-  n2 /= 2;
-  n3 /= 2;
-  uint32_t *dp1, *dp2, *dp3;
-  (void)hipMalloc(&dp1, sizeof(p1));
-  (void)hipMalloc(&dp2, sizeof(p2));
-  (void)hipMalloc(&dp3, sizeof(p3));
-  (void)hipMemcpy(dp1, p1, sizeof(p1), hipMemcpyHostToDevice);
-  (void)hipMemcpy(dp2, p2, sizeof(p2), hipMemcpyHostToDevice);
-  (void)hipMemcpy(dp3, p3, sizeof(p3), hipMemcpyHostToDevice);
-  const kfn ks[] = {k_chain<0>, k_chain<1>, k_chain<2>, k_chain<3>, k_chain<2>, k_chain<2>, k_chain<2>};
-  const char* names[] = {"keccak alignbit", "keccak shifts", "transcript 116B", "  ... empty msg",
-                         "prog: PRF", "prog: 32 x 1B", "prog: 32 x 4B"};
-  const uint32_t* progs[] = {dp, dp, dp, dp, dp1, dp2, dp3};
-  const int nps[] = {np, np, np, np, n1, n2, n3};
+  const kfn ks[] = {k_chain<0>, k_chain<1>, k_chain<2>, k_chain<3>};
+  const char* names[] = {"keccak alignbit", "keccak shifts", "transcript 116B", "  ... empty msg"};
   std::vector<uint32_t> ref(nth), got(nth);
-  for (int v = 0; v < 7; v++) {
+  for (int v = 0; v < 4; v++) {
     for (int r = 0; r < 2; r++)
-      hipLaunchKernelGGL(ks[v], dim3(grid), dim3(block), 64 * 1024, 0, din, dm, 116u, progs[v], nps[v], dout, n, dcyc);
+      hipLaunchKernelGGL(ks[v], dim3(grid), dim3(block), 64 * 1024, 0, din, dm, 116u, dp, np, dout, n, dcyc);
     (void)hipDeviceSynchronize();
     std::vector<unsigned long long> cyc(nth / 64);
     (void)hipMemcpy(cyc.data(), dcyc, cyc.size() * 8, hipMemcpyDeviceToHost);

@@ -207,7 +207,8 @@ __global__ __launch_bounds__(256, CMTV_QUAD_WAVES_PER_EU) void k_verify_quad_hs(
     uint32_t ml;
     helper_message(sb, i, msg, off, reinterpret_cast<uint32_t*>(xbuf) + slot * (kSbFuseMaxMsg / 4), mp, ml);
     SigPrep p;
-    q_prepare<MODE>(p, pk + 8 * (size_t)i, sig + 16 * (size_t)i, mp, ml, force_wide != 0);
+    q_prepare<MODE>(p, pk + 8 * (size_t)i, sig + 16 * (size_t)i, mp, ml, force_wide != 0,
+                    [] { CMTV_STAMP(7); });
     const int W = hs_workgroup_windows(p.flags, t);
     p.flags |= (uint32_t)W << 16;
     if (t < 48) sig_prep_store(prep[t], p);

@@ -374,9 +374,13 @@ CMTV_HD void q_prepare_scalars(SigPrep& p, const uint32_t k[8], const uint32_t t
 
 // s check, k = SHA-512(R || A || M) mod L, then q_prepare_scalars (k2 odd
 // for the cofactorless check, MODE_GO_STDLIB; any parity for MODE_ZIP215)
-template <uint32_t MODE, bool UNI = false>
+struct NoPrepMark {
+  CMTV_HD void operator()() const {}
+};
+
+template <uint32_t MODE, bool UNI = false, class Mark = NoPrepMark>
 CMTV_HD void q_prepare(SigPrep& p, const uint32_t* pk_ptr, const uint32_t* sig_ptr, const uint8_t* msg,
-                       uint32_t mlen, bool force_wide) {
+                       uint32_t mlen, bool force_wide, const Mark& after_hash = Mark()) {
   uint32_t w[16];
 #pragma unroll
   for (int i = 0; i < 8; i++) w[i] = sig_ptr[8 + i];
@@ -393,6 +397,7 @@ CMTV_HD void q_prepare(SigPrep& p, const uint32_t* pk_ptr, const uint32_t* sig_p
       w[8 + i] = pk_ptr[i];
     }
     sha512_prefixed<16>(h, w, msg, mlen);
+    after_hash();
     sc_reduce512(k, h);
   }
   q_prepare_scalars<UNI>(p, k, ts, force_wide, MODE != MODE_ZIP215);

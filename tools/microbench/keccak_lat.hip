@@ -58,7 +58,7 @@ __device__ __forceinline__ void keccak_shift(uint64_t a[25]) {
 }
 
 template <int V>
-__global__ __launch_bounds__(256, 1) void k_chain(const uint32_t* in, const uint8_t* msg, uint32_t mlen,
+__global__ __launch_bounds__(256, 1) void k_chain(const uint32_t* in, const uint32_t* lens, const uint8_t* msg, uint32_t mlen,
                                                   const uint32_t* prog, int nops_prog, uint32_t* out, int n,
                                                   unsigned long long* cyc) {
   __shared__ uint32_t st_lds[4][STROBE_BLOCK_WORDS * 64];
@@ -78,7 +78,9 @@ __global__ __launch_bounds__(256, 1) void k_chain(const uint32_t* in, const uint
         pk[i] = (uint32_t)a[i] ^ (uint32_t)it;
         R[i] = (uint32_t)(a[i] >> 32);
       }
-      sr_transcript(o, st, prog, nops_prog, msg + (size_t)(tid & 1023) * 128 + 1 + (tid & 1), V == 3 ? 0u : mlen,
+      // a per-lane length (as the kernels see it), the same value in every lane
+      const uint32_t ml = V == 3 ? 0u : lens[tid & 4095];
+      sr_transcript(o, st, prog, nops_prog, msg + (size_t)(tid & 1023) * 128 + 1 + (tid & 1), ml,
                     pk, R);
       for (int i = 0; i < 16; i++) acc[i] ^= o[i];
     }
@@ -112,7 +114,7 @@ __global__ __launch_bounds__(256, 1) void k_chase(const uint32_t* tab, uint32_t*
   if ((threadIdx.x & 63) == 0) cyc[(blockIdx.x * blockDim.x + threadIdx.x) >> 6] = t1 - t0;
 }
 
-typedef void (*kfn)(const uint32_t*, const uint8_t*, uint32_t, const uint32_t*, int, uint32_t*, int,
+typedef void (*kfn)(const uint32_t*, const uint32_t*, const uint8_t*, uint32_t, const uint32_t*, int, uint32_t*, int,
                     unsigned long long*);
 
 int main(int argc, char** argv) {
@@ -138,6 +140,10 @@ int main(int argc, char** argv) {
   (void)hipMalloc(&dout, nth * 4);
   (void)hipMalloc(&dcyc, (nth / 64) * 8);
   (void)hipMemcpy(din, hin.data(), hin.size() * 4, hipMemcpyHostToDevice);
+  uint32_t* dlen;
+  std::vector<uint32_t> hlen(4096, 116u);
+  (void)hipMalloc(&dlen, hlen.size() * 4);
+  (void)hipMemcpy(dlen, hlen.data(), hlen.size() * 4, hipMemcpyHostToDevice);
   (void)hipMemcpy(dm, hm.data(), hm.size(), hipMemcpyHostToDevice);
   (void)hipMemcpy(dp, prog, sizeof(prog), hipMemcpyHostToDevice);
   const kfn ks[] = {k_chain<0>, k_chain<1>, k_chain<2>, k_chain<3>};
@@ -145,7 +151,7 @@ int main(int argc, char** argv) {
   std::vector<uint32_t> ref(nth), got(nth);
   for (int v = 0; v < 4; v++) {
     for (int r = 0; r < 2; r++)
-      hipLaunchKernelGGL(ks[v], dim3(grid), dim3(block), 64 * 1024, 0, din, dm, 116u, dp, np, dout, n, dcyc);
+      hipLaunchKernelGGL(ks[v], dim3(grid), dim3(block), 64 * 1024, 0, din, dlen, dm, 116u, dp, np, dout, n, dcyc);
     (void)hipDeviceSynchronize();
     std::vector<unsigned long long> cyc(nth / 64);
     (void)hipMemcpy(cyc.data(), dcyc, cyc.size() * 8, hipMemcpyDeviceToHost);

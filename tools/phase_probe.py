@@ -93,7 +93,8 @@ def main():
             "quads_wait_at_b2_for_helper": {"wgs": int((w2 > 0).sum()), "median": float(np.median(w2)),
                                             "max": int(w2.max())},
             "helper_b1_median": float(np.median(h[:, 1] - start)),
-            **({"helper_transcript_end_median": float(np.median(h[:, 7] - start))} if sr else {}),
+            # slot 7 of the helper: the end of its merlin transcripts / SHA-512s
+            ("helper_transcript_end_median" if sr else "helper_hash_end_median"): float(np.median(h[:, 7] - start)),
             "helper_b2_minus_b1_release_median": float(np.median(h[:, 3] - q[:, :, 2].max(axis=1))),
             "quad_b1_median": float(np.median(q[:, :, 1] - start[:, None])),
             "quad_b2_median": float(np.median(q[:, :, 3] - start[:, None])),

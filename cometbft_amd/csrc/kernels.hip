@@ -205,7 +205,12 @@ __global__ __launch_bounds__(256, CMTV_QUAD_WAVES_PER_EU) void k_verify_quad_hs(
     const uint32_t i = s < n ? s : n - 1;
     const uint8_t* mp;
     uint32_t ml;
+    CMTV_STAMP(5);  // the helper's slots 5 / 4: before / after locating its message
     helper_message(sb, i, msg, off, reinterpret_cast<uint32_t*>(xbuf) + slot * (kSbFuseMaxMsg / 4), mp, ml);
+#ifdef CMTV_PHASE_PROBE
+    __builtin_amdgcn_s_waitcnt(0);  // the offsets arrived
+#endif
+    CMTV_STAMP(4);
     SigPrep p;
     q_prepare<MODE>(p, pk + 8 * (size_t)i, sig + 16 * (size_t)i, mp, ml, force_wide != 0,
                     [] { CMTV_STAMP(7); });
@@ -225,7 +230,6 @@ __global__ __launch_bounds__(256, CMTV_QUAD_WAVES_PER_EU) void k_verify_quad_hs(
     CMTV_STAMP_VAL(6, hwait);
     CMTV_STAMP(3);
     __syncthreads();  // B: [u]B
-    CMTV_STAMP(4);
     return;
   }
   const uint32_t ls = wave * 16 + (t >> 2);

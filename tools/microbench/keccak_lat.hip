@@ -7,7 +7,8 @@
 // Variants: 0 keccak_f1600 (keccak.h: funnel-shift rotates) on a register
 // state, a dependent chain; 1 the same permutation with 64-bit shift rotates
 // (checked to end in the same state); 2 the whole transcript of a 116-byte
-// message; 3 the transcript of an empty message. Lane 0 of every wave records
+// message; 3 the transcript of an empty message; 4 the Ed25519 helper's
+// SHA-512(R || A || M) of a 116-byte message (two blocks). Lane 0 of every wave records
 // s_memtime around the loop; prints mean cycles per item. Then the scalar
 // cache's latency (a uniform-address pointer chase), alone and with an LDS
 // store per step.
@@ -18,6 +19,7 @@
 #include <vector>
 
 #include "merlin.h"
+#include "sha512.h"
 
 using namespace cmtv;
 
@@ -71,7 +73,13 @@ __global__ __launch_bounds__(256, 1) void k_chain(const uint32_t* in, const uint
   for (int it = 0; it < n; it++) {
     if (V == 0) keccak_f1600(a);
     if (V == 1) keccak_shift(a);
-    if (V >= 2) {
+    if (V == 4) {  // SHA-512(R || A || M), the Ed25519 helper's hash, 116-byte messages
+      uint32_t pre[16], h[16];
+      for (int i = 0; i < 16; i++) pre[i] = (uint32_t)a[i] ^ (uint32_t)it;
+      sha512_prefixed<16>(h, pre, msg + (size_t)(tid & 1023) * 128 + 1 + (tid & 1), lens[tid & 4095]);
+      for (int i = 0; i < 16; i++) acc[i] ^= h[i];
+    }
+    if (V == 2 || V == 3) {
       LdsState st{st_lds[threadIdx.x >> 6], threadIdx.x & 63};
       uint32_t pk[8], R[8], o[16];
       for (int i = 0; i < 8; i++) {
@@ -146,10 +154,11 @@ int main(int argc, char** argv) {
   (void)hipMemcpy(dlen, hlen.data(), hlen.size() * 4, hipMemcpyHostToDevice);
   (void)hipMemcpy(dm, hm.data(), hm.size(), hipMemcpyHostToDevice);
   (void)hipMemcpy(dp, prog, sizeof(prog), hipMemcpyHostToDevice);
-  const kfn ks[] = {k_chain<0>, k_chain<1>, k_chain<2>, k_chain<3>};
-  const char* names[] = {"keccak alignbit", "keccak shifts", "transcript 116B", "  ... empty msg"};
+  const kfn ks[] = {k_chain<0>, k_chain<1>, k_chain<2>, k_chain<3>, k_chain<4>};
+  const char* names[] = {"keccak alignbit", "keccak shifts", "transcript 116B", "  ... empty msg",
+                         "sha512 64+116B"};
   std::vector<uint32_t> ref(nth), got(nth);
-  for (int v = 0; v < 4; v++) {
+  for (int v = 0; v < 5; v++) {
     for (int r = 0; r < 2; r++)
       hipLaunchKernelGGL(ks[v], dim3(grid), dim3(block), 64 * 1024, 0, din, dlen, dm, 116u, dp, np, dout, n, dcyc);
     (void)hipDeviceSynchronize();

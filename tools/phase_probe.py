@@ -4,6 +4,7 @@
   make -C cometbft_amd/csrc OUT=../../abtest/libprobe.so BUILD=../../build/probe KFLAGS=-DCMTV_PHASE_PROBE
   CMTV_LIBRARY=$PWD/abtest/libprobe.so python tools/phase_probe.py [n]
   CMTV_LIBRARY=$PWD/abtest/libprobe.so python tools/phase_probe.py --sr [n]   (k_verify_sr25519_quad_hs)
+  (inputs resident in HBM as in bench.py; --host: host arrays through the staging / zero-copy path)
 
 Lane 0 of every wave records the shader clock at kernel entry (0), before /
 after barrier 1 (1, 2: the helper's scalars), before / after barrier 2 (3, 4:
@@ -29,7 +30,8 @@ SLOTS = 8
 
 def main():
     sr = "--sr" in sys.argv
-    argv = [a for a in sys.argv[1:] if a != "--sr"]
+    host = "--host" in sys.argv  # host arrays (zero-copy / staged inputs) instead of HBM-resident ones
+    argv = [a for a in sys.argv[1:] if a not in ("--sr", "--host")]
     n = int(argv[0]) if len(argv) > 0 else 10_000
     # signatures per 4-wave workgroup: 48 (k_verify_quad_split) or 3 (the row
     # kernel, k_verify_row_split, which the library picks up to kRowMax)
@@ -38,6 +40,11 @@ def main():
     from cometbft_amd import _native as N
     from cometbft_amd import testutil as TU
 
+    if not host:  # torch first (as bench.py): its HIP init before the library's
+        import torch
+
+        dev = torch.device("cuda", 0)
+        torch.zeros(1, device=dev)
     L = N.lib()
     fn = L.cmtv_debug_phase_times_sr if sr else L.cmtv_debug_phase_times
     fn.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t]
@@ -57,9 +64,25 @@ def main():
         pk = np.ascontiguousarray(sv.pubkeys)
     wgs = -(-n // per_wg)
     out = {}
+    if not host:
+        # the bench's form: inputs resident in HBM (bench.py configs[1] / [4] lines)
+        d_pk = torch.from_numpy(np.ascontiguousarray(pk)).to(dev)
+        d_sig = torch.from_numpy(np.ascontiguousarray(sig)).to(dev)
+        d_m = torch.from_numpy(np.ascontiguousarray(m)).to(dev)
+        d_off = torch.from_numpy(np.ascontiguousarray(off).view(np.int32)).to(dev)
+        d_valid = torch.zeros(n, dtype=torch.uint8, device=dev)
     for mode, name in (((0, "sr25519"),) if sr else ((0, "go"), (1, "zip215"))):
         for _ in range(20):
-            v = ctx.verify_sr25519(pk, sig, m, off) if sr else ctx.verify(pk, sig, m, off, mode)
+            if host:
+                v = ctx.verify_sr25519(pk, sig, m, off) if sr else ctx.verify(pk, sig, m, off, mode)
+            else:
+                args = (n, d_pk.data_ptr(), d_sig.data_ptr(), d_m.data_ptr(), d_off.data_ptr())
+                if sr:
+                    ctx.verify_sr25519_device(*args, d_valid.data_ptr())
+                else:
+                    ctx.verify_device(*args, mode, d_valid.data_ptr())
+                torch.cuda.synchronize()
+                v = d_valid.cpu().numpy()
         assert v.all()
         buf = np.zeros(wgs * 4 * SLOTS, np.uint64)
         assert fn(buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), buf.size) == 0
@@ -95,6 +118,8 @@ def main():
             "helper_b1_median": float(np.median(h[:, 1] - start)),
             # slot 7 of the helper: the end of its merlin transcripts / SHA-512s
             ("helper_transcript_end_median" if sr else "helper_hash_end_median"): float(np.median(h[:, 7] - start)),
+            **({} if sr else {"helper_message_start_median": float(np.median(h[:, 5] - start)),
+                              "helper_message_ready_median": float(np.median(h[:, 4] - start))}),
             "helper_b2_minus_b1_release_median": float(np.median(h[:, 3] - q[:, :, 2].max(axis=1))),
             "quad_b1_median": float(np.median(q[:, :, 1] - start[:, None])),
             "quad_b2_median": float(np.median(q[:, :, 3] - start[:, None])),

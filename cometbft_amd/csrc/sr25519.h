@@ -100,7 +100,7 @@ CMTV_HD bool ristretto_decode(ge_p3& h, const uint32_t w[8]) {
 }
 
 // Full single-signature verification (pubkey.go:34-60 for a 32-byte key and
-// a 64-byte signature). prog/nops: the transcript program (merlin.h).
+// a 64-byte signature). prog/nops: the transcript's prefix sponge (merlin.h sr_prefix_state).
 template <class ATab, class BTab, class State>
 CMTV_HD bool sr_verify_one(const uint32_t* pk_ptr, const uint32_t* sig_ptr, const uint8_t* msg, uint32_t mlen,
                            const uint32_t* prog, int nops, State& st, ATab& atab, const BTab& btab) {

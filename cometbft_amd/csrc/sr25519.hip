@@ -6,15 +6,15 @@
 //     and a helper wave, half-size scalars and shared windows like the Ed25519
 //     helper-summed quad kernel; the runtime uses it below the crossover
 //   k_verify_sr25519: one signature per lane (sr25519.h): merlin transcript
-//     interpreted from a byte-code program with the Keccak state in LDS,
+//     (merlin.h: host-computed prefix sponge, chunked message, two-pass tail),
 //     ristretto255 decoding of A and R, Straus [s]B - [k]A over the Ed25519
 //     kernel's field, point formulas and fixed-base table, ristretto equality;
 //     a wavefront ballot packs 64 verdicts into one bitmap word.
 //
 // Memory layout: inputs exactly as the Ed25519 kernels (pk n x 32 B, sig
-// n x 64 B, msg flat bytes + (n+1) u32 offsets); the transcript program (at
-// most SR_DEVPROG_MAX u16, led by the precomputed prefix state) is read with
-// uniform scalar loads; the sponge stays in registers and each lane's current
+// n x 64 B, msg flat bytes + (n+1) u32 offsets); the transcript's prefix
+// sponge (SR_PREFIX_WORDS, merlin.h sr_prefix_state) is read with scalar
+// loads; the sponge stays in registers and each lane's current
 // STROBE block (42 words) gathers in LDS lane-interleaved (word w of lane l
 // at word w*64 + l: conflict-free for any per-lane position).
 #include <hip/hip_runtime.h>

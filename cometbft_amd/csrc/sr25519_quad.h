@@ -21,8 +21,8 @@ namespace cmtv {
 
 // The scalar half of an sr25519 quad verification (no decoded points
 // needed): schnorrkel marker and canonical s, the merlin challenge k mod L,
-// the half-size pair and u = k2 s mod L. k_verify_sr25519_quad_split runs it
-// on a helper wave.
+// the half-size pair and u = k2 s mod L. k_verify_sr25519_quad_hs runs it on
+// its helper wave.
 struct NoMark {
   CMTV_HD void operator()() const {}
 };

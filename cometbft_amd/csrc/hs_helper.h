@@ -13,9 +13,14 @@ namespace cmtv {
 
 // [u]B's comb positions the helper adds while the quads build their tables
 // (the quads add the rest inside their windows); CMTV_HS_PRE overrides it.
-// sr25519: none -- its helper's merlin transcript already outlasts the quads'
-// decode and tables, so every comb addition there would delay barrier 1
-constexpr int kHsCombPre = 6, kHsCombPreSr = 0;
+// Each one the helper takes saves the quads ~1 us of window time and costs
+// barrier 1 ~3 us once the helper arrives last. Ed25519: 6 with the message
+// in HBM (the helper reaches barrier 1 with the quads, profiles/
+// r05_ed_phase_hbm.json); 3 when the helper builds the sign-bytes itself
+// from zero-copy staged templates (the node's commit path: its first loads
+// cross PCIe; profiles/r05_hs_pre_ab.txt). sr25519: none -- its merlin
+// transcript already brings the helper to barrier 1 with the quads
+constexpr int kHsCombPre = 6, kHsCombPreFused = 3, kHsCombPreSr = 0;
 // one ring slot: 3 quad waves x 5 uint2 x 64 lanes
 constexpr uint32_t kHsSlotU2 = 3 * 5 * 64;
 // a quad wave's two tables in LDS: 2 points x 9 entries x 5 uint2 x 64 lanes

@@ -193,7 +193,7 @@ __global__ __launch_bounds__(256, CMTV_QUAD_WAVES_PER_EU) void k_verify_quad_hs(
     uint64_t* __restrict__ out_bitmap, uint32_t force_wide, SbFuse sb, uint32_t hs_tune) {
   const uint32_t wave = threadIdx.x >> 6, t = threadIdx.x & 63;
   const uint32_t base = blockIdx.x * 48;
-  const int comb_pre = hs_comb_pre(hs_tune, kHsCombPre);
+  const int comb_pre = hs_comb_pre(hs_tune, sb.tmpls ? kHsCombPreFused : kHsCombPre);
   __shared__ uint32_t prep[48][SIG_PREP_WORDS + 1];
   __shared__ uint2 tab_lds[3][kHsTabU2];
   __shared__ uint2 xbuf[2 * kHsSlotU2];  // sign-bytes (48 x kSbFuseMaxMsg B), then the 2-slot ring

@@ -85,6 +85,30 @@ def test_commit_sized_batch(gpu_ctx, gpu_ctx_lane, kernel):
     assert exp.sum() == 10000 - 100
 
 
+@pytest.mark.parametrize("kernel", ["quad", "lane"])
+def test_long_and_mixed_message_lengths(gpu_ctx, gpu_ctx_lane, kernel):
+    """merlin.h runs a wave's message loop for its longest message and the
+    136-byte tail in two passes around the STROBE block end: waves mixing
+    empty, short and multi-block messages (up to 2,000 bytes, several F's in
+    the message loop), the tail starting at every block position, honest and
+    flipped, against the C oracle."""
+    gpu_ctx = {"quad": gpu_ctx, "lane": gpu_ctx_lane}[kernel]
+    rng = np.random.default_rng(31)
+    n = 640
+    minis = rng.integers(0, 256, (32, 32), dtype=np.uint8)
+    kidx = (np.arange(n) % 32).astype(np.uint32)
+    lens = np.where(np.arange(n) % 7 == 0, rng.integers(600, 2000, n), rng.integers(0, 400, n))
+    lens[::13] = 0
+    msgs = [rng.integers(0, 256, int(l), dtype=np.uint8).tobytes() for l in lens]
+    m, off = coracle.pack_msgs(msgs)
+    sig = coracle.sr25519_sign_batch(minis, m, off, key_idx=kidx).copy()
+    pk = coracle.sr25519_pubkeys(minis)[kidx]
+    sig[1::5, 50] ^= 0x10
+    exp = coracle.sr25519_verify_batch(pk, sig, m, off, nthreads=8)
+    assert np.array_equal(gpu_ctx.verify_sr25519(pk, sig, m, off), exp)
+    assert exp.sum() == n - len(range(1, n, 5))
+
+
 def test_device_buffers_match_host_path(gpu_ctx):
     import torch
 

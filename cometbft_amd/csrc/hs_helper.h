@@ -19,7 +19,8 @@ namespace cmtv {
 // r05_ed_phase_hbm.json); 3 when the helper builds the sign-bytes itself
 // from zero-copy staged templates (the node's commit path: its first loads
 // cross PCIe; profiles/r05_hs_pre_ab.txt). sr25519: none -- its merlin
-// transcript already brings the helper to barrier 1 with the quads
+// transcript already brings the helper to barrier 1 with the quads (1 and 2
+// measured 1-3% slower, profiles/r05_sr_hs_pre_ab.txt)
 constexpr int kHsCombPre = 6, kHsCombPreFused = 3, kHsCombPreSr = 0;
 // one ring slot: 3 quad waves x 5 uint2 x 64 lanes
 constexpr uint32_t kHsSlotU2 = 3 * 5 * 64;

@@ -63,8 +63,9 @@ constexpr uint32_t kKeyedBatchMinWaves = 2048;
 //              (profiles/r04_quad_max_ab.txt: 49,152 0.96 vs lane 1.15 ms;
 //              65,536 1.39 vs 1.25 ms)
 //   above      kFormLane
-// sr25519: the quad form up to 40,000, the lane form above
-// (profiles/r04_sr_quad_max_ab.txt: 40,960-49,152 1.37-1.40 vs 1.24-1.27 ms).
+// sr25519: the same bands since the round-5 transcript (profiles/
+// r05_sr_quad_max_ab.txt: 49,152 0.94 vs lane 1.15 ms; 65,536 1.37 vs 1.25;
+// round 4, with the byte-code transcript, crossed at 40,000).
 // Registered keys:
 //   <= 512     kKeyedRow   (profiles/r04_keyed_row_max_ab.txt: 320-512
 //              0.058-0.062 vs quad 0.076 ms; 640-768 lose)
@@ -72,7 +73,7 @@ constexpr uint32_t kKeyedBatchMinWaves = 2048;
 //              0.088/0.164/0.242 ms for 1-3 rounds vs the lane kernel's flat
 //              0.28-0.30 ms up to 49k)
 //   above      kKeyedLane
-constexpr size_t kRow4Max = 256, kRowMax = 1536, kOct2Max = 2048, kQuadMax = 49152, kSrQuadMax = 40000;
+constexpr size_t kRow4Max = 256, kRowMax = 1536, kOct2Max = 2048, kQuadMax = 49152, kSrQuadMax = 49152;
 constexpr size_t kKeyedRowMax = 512, kKeyedQuadMax = 36864;
 constexpr uint32_t kNoForm = 0xFF;
 // signatures per device below which a batch is not sharded (env CMTV_SHARD_MIN)

@@ -79,7 +79,7 @@ def _env_ctx(**env):
 #   row4  k_verify_row4_split       (Ed25519 default <= 256)
 #   row   k_verify_row_split        (<= 1,536)
 #   oct2  k_verify_oct_split        (<= 2,048)
-#   quad  k_verify_quad_hs          (<= 49,152; sr25519 <= 40,000)
+#   quad  k_verify_quad_hs          (<= 49,152; sr25519 too)
 #   lane  k_verify, k_verify_sr25519 and the keyed lane kernels (above)
 #   krow  k_verify_keyed_row_split  (registered keys <= 512)
 #   kquad k_verify_keyed_quad_split (<= 36,864)

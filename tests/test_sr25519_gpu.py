@@ -144,13 +144,12 @@ def test_pubkey_and_batch_mirror(gpu_ctx):
     assert not ok and res == [True, True, True, False]
 
 
-@pytest.mark.parametrize("n", [40000, 40001])
+@pytest.mark.parametrize("n", [49152, 49153])
 def test_default_dispatch_at_the_sr25519_crossover(gpu_ctx, n):
-    """the default context on both sides of sr25519's own quad /
-    lane crossover (40,000; Ed25519's is 49,152, so 40,001..49,152 sr25519
-    signatures take the lane kernel while Ed25519 batches of that size stay on
-    the quad kernel), 1% flipped signatures, verdict bytes and bitmap against
-    the C restatement of go-schnorrkel."""
+    """the default context on both sides of sr25519's quad / lane
+    crossover (49,152 since the round-5 transcript, as Ed25519's; 40,000 in
+    round 4), 1% flipped signatures, verdict bytes and bitmap against the C
+    restatement of go-schnorrkel."""
     rng = np.random.default_rng(n)
     pk, sig, m, off, _ = _honest(n, n, nkeys=512, msg_len=116)
     sig = sig.copy()

@@ -12,6 +12,7 @@ import torch
 from cometbft_amd import Context
 from oracle import coracle  # synthetic signatures only
 
+torch.zeros(1, device="cuda:0")  # torch's HIP init before the library's
 ctx = Context(device=0)
 rng = np.random.default_rng(4)
 minis = rng.integers(0, 256, (150, 32), dtype=np.uint8)

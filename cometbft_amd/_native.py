@@ -48,6 +48,7 @@ EXPORTS = (
     "cmtv_verify_ed25519_indexed_device",
     "cmtv_batch_new", "cmtv_batch_add", "cmtv_batch_len", "cmtv_batch_verify", "cmtv_batch_reset",
     "cmtv_batch_free", "cmtv_verify_commit", "cmtv_verify_commits", "cmtv_verdict_cache", "cmtv_keyset_cache", "cmtv_vote_sign_bytes", "cmtv_pubkeys_ed25519", "cmtv_sign_ed25519",
+    "cmtv_alloc_pinned", "cmtv_free_pinned",
 )
 
 
@@ -74,7 +75,7 @@ class cmtv_stats(ctypes.Structure):
                 ("reshards", ctypes.c_uint64), ("late_k_waves", ctypes.c_uint64),
                 ("live_devices", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
                 ("timed_calls", ctypes.c_uint64), ("rccl_failures", ctypes.c_uint64),
-                ("polled_calls", ctypes.c_uint64)]
+                ("polled_calls", ctypes.c_uint64), ("direct_chunks", ctypes.c_uint64)]
 
 
 class cmtv_device_stats(ctypes.Structure):
@@ -206,6 +207,10 @@ def lib() -> ctypes.CDLL:
     L.cmtv_pubkeys_ed25519.restype = ctypes.c_int
     L.cmtv_sign_ed25519.argtypes = [vp, sz, _u8p, u32p, _u8p, u32p, _u8p]
     L.cmtv_sign_ed25519.restype = ctypes.c_int
+    L.cmtv_alloc_pinned.argtypes = [vp, sz, ctypes.POINTER(vp)]
+    L.cmtv_alloc_pinned.restype = ctypes.c_int
+    L.cmtv_free_pinned.argtypes = [vp, vp]
+    L.cmtv_free_pinned.restype = ctypes.c_int
     _lib = L
     return L
 

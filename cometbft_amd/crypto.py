@@ -135,6 +135,12 @@ class Context:
             out.append({k: getattr(st, k) for k, _ in st._fields_})
         return out
 
+    def alloc_pinned(self, nbytes: int) -> "PinnedBlock":
+        """cmtv_alloc_pinned: page-locked host memory of this context, the
+        zero-copy source of cmtv_verify_commits' direct chunks; .array(dtype,
+        count, offset) views it as numpy."""
+        return PinnedBlock(self, nbytes)
+
     def keyset_cache(self, max_sets: int) -> None:
         """cmtv_keyset_cache: registered key sets of up to max_sets validator
         sets for cmtv_verify_commit(s) (0 = off)."""
@@ -311,6 +317,26 @@ class KeySet:
 
 _default_ctx = None
 _default_lock = threading.Lock()
+
+
+class PinnedBlock:
+    """A cmtv_alloc_pinned block; freed by free() or with its context."""
+
+    def __init__(self, ctx: Context, nbytes: int):
+        p = ctypes.c_void_p()
+        N.check(N.lib().cmtv_alloc_pinned(ctx.handle, nbytes, ctypes.byref(p)), "cmtv_alloc_pinned")
+        self._ctx, self.ptr, self.nbytes = ctx, p.value, nbytes
+        self._buf = (ctypes.c_uint8 * nbytes).from_address(p.value)
+
+    def array(self, dtype, count: int, offset: int = 0) -> np.ndarray:
+        dt = np.dtype(dtype)
+        assert offset % dt.itemsize == 0 and offset + count * dt.itemsize <= self.nbytes
+        return np.frombuffer(self._buf, dt, count, offset)
+
+    def free(self) -> None:
+        if self.ptr and self._ctx.handle:
+            N.check(N.lib().cmtv_free_pinned(self._ctx.handle, self.ptr), "cmtv_free_pinned")
+        self.ptr = None
 
 
 def default_context() -> Context:

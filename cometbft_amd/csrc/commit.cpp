@@ -381,8 +381,9 @@ void job_preamble(CommitJob& J) {
   J.res->sig_index = -1;
   set_msg(J.msg_buf, J.msg_cap, "");
   const uint32_t nsig = commit->n_sigs;
-  int64_t total = 0;
-  for (uint32_t i = 0; i < vals->n_vals; i++) total += vals->voting_power[i];
+  int64_t total = J.total;
+  if (!J.has_total)
+    for (uint32_t i = 0; i < vals->n_vals; i++) total += vals->voting_power[i];
 
   if (J.kind == CMTV_VERIFY_COMMIT_LIGHT_TRUSTING) {
     if (J.trust_den == 0) {
@@ -473,6 +474,14 @@ size_t job_plan(const CommitJob& J, uint32_t* pidx, uint32_t* pval, Seen& seen) 
   return m;
 }
 
+// Largest message span of one device batch (offsets are 32-bit on the
+// device); CMTV_MAX_BATCH_MSG_BYTES lowers it (tests of the split).
+uint64_t max_batch_msg_bytes() {
+  const char* v = std::getenv("CMTV_MAX_BATCH_MSG_BYTES");
+  const uint64_t x = v ? std::strtoull(v, nullptr, 10) : 0;
+  return (x && x < (1ull << 31)) ? x : (1ull << 31);
+}
+
 }  // namespace cmtv
 
 namespace {
@@ -519,14 +528,6 @@ void job_prepare(CommitJob& J, SigBatch& B, bool prefetch, bool only_job, Seen& 
       B.add(vals, idx, commit->sigs + s0, s1 - s0, J.chain_id, J.chain_id_len, commit, idx);
     }
   }
-}
-
-// Largest message span of one device batch (offsets are 32-bit on the
-// device); CMTV_MAX_BATCH_MSG_BYTES lowers it (tests of the split).
-uint64_t max_batch_msg_bytes() {
-  const char* v = std::getenv("CMTV_MAX_BATCH_MSG_BYTES");
-  const uint64_t x = v ? std::strtoull(v, nullptr, 10) : 0;
-  return (x && x < (1ull << 31)) ? x : (1ull << 31);
 }
 
 int batch_verify(cmtv_ctx* ctx, SigBatch& B, uint32_t mode, std::vector<uint8_t>& valid) {
@@ -581,13 +582,11 @@ int job_replay_batch(CommitJob& J, const std::vector<uint8_t>& all_valid, Seen& 
   const uint8_t* v = all_valid.data() + J.first;
   if (J.plan_prefix) {
     // job_prepare_fast checked every flag, key and signature length of the
-    // prefix: the loop's outcome is the first invalid verdict, else the
-    // tally (job_replay gives the same, one signature at a time)
+    // prefix
     if (J.early != 1) return J.early;
-    J.res->n_verified = (uint32_t)J.plan_prefix;
-    if (const void* z = std::memchr(v, 0, J.plan_prefix))
-      return fail_wrong_sig(J, (uint32_t)(static_cast<const uint8_t*>(z) - v));
-    return J.prefix_tally > J.needed ? CMTV_OK : fail_not_enough(J, J.prefix_tally);
+    const void* z = std::memchr(v, 0, J.plan_prefix);
+    return replay_prefix(J, J.plan_prefix, J.prefix_tally,
+                         z ? (size_t)(static_cast<const uint8_t*>(z) - v) : J.plan_prefix);
   }
   return job_replay(J, J.plan_idx.data(), J.plan_idx.size(), [v](size_t j) { return v[j] != 0; }, seen);
 }
@@ -604,6 +603,25 @@ struct cmtv_batch {
   std::vector<uint8_t> forced_invalid;  // bad sig length
   int64_t bad_key = -1;                 // first entry with a bad key length
 };
+
+template <class V>
+static void grow_for(V& v, size_t extra) {
+  if (v.capacity() - v.size() < extra) v.reserve(std::max(v.size() + extra, 2 * v.capacity()));
+}
+
+// No C++ exception crosses the C ABI (the vectors, maps and worker threads
+// above can throw): a failed allocation is CMTV_ENOMEM, anything else
+// CMTV_EINVAL; the context stays usable (its locks are scoped).
+template <class F>
+static int no_throw(F&& f) {
+  try {
+    return f();
+  } catch (const std::bad_alloc&) {
+    return CMTV_ENOMEM;
+  } catch (...) {
+    return CMTV_EINVAL;
+  }
+}
 
 extern "C" {
 
@@ -636,6 +654,17 @@ int cmtv_batch_add(cmtv_batch* b, const uint8_t* pk, size_t pk_len, const uint8_
   const bool key_ok = pk_len == 32, sig_ok = sig_len == 64;
   if (key_ok) std::memcpy(kbuf, pk, 32);
   if (sig_ok) std::memcpy(sbuf, sig, 64);
+  // room first (geometric growth), so a failed allocation leaves the batch
+  // as it was and no exception crosses the C ABI
+  try {
+    grow_for(b->pk, 32);
+    grow_for(b->sig, 64);
+    grow_for(b->msg, msg_len);
+    grow_for(b->off, 1);
+    grow_for(b->forced_invalid, 1);
+  } catch (...) {
+    return CMTV_ENOMEM;
+  }
   if (!key_ok && b->bad_key < 0) b->bad_key = (int64_t)idx;
   b->pk.insert(b->pk.end(), kbuf, kbuf + 32);
   b->sig.insert(b->sig.end(), sbuf, sbuf + 64);
@@ -683,7 +712,7 @@ int cmtv_batch_verify(cmtv_batch* b, uint8_t* out_valid, int* all_ok, int64_t* b
 
 // ------------------------------------------------------------------ VerifyCommit*
 
-int cmtv_verify_commit(cmtv_ctx* ctx, uint32_t kind, uint32_t mode, const char* chain_id, size_t chain_id_len,
+static int cmtv_verify_commit_impl(cmtv_ctx* ctx, uint32_t kind, uint32_t mode, const char* chain_id, size_t chain_id_len,
                        const cmtv_valset* vals, const cmtv_block_id* block_id, int64_t height,
                        const cmtv_commit* commit, uint64_t trust_num, uint64_t trust_den, cmtv_commit_result* res,
                        char* msg_buf, size_t msg_cap) {
@@ -701,6 +730,13 @@ int cmtv_verify_commit(cmtv_ctx* ctx, uint32_t kind, uint32_t mode, const char* 
   std::unique_lock<std::mutex> lk;
   rc = cmtv::ctx_lock(ctx, lk);
   if (rc != CMTV_OK) return rc;
+  // the early-staged signatures below belong to this call only: forgotten on
+  // every exit (a preamble error or an empty plan runs no batch), before the
+  // lock is released
+  struct EarlyGuard {
+    cmtv_ctx* c;
+    ~EarlyGuard() { cmtv::clear_early_locked(c); }
+  } early_guard{ctx};
   const uint64_t t0 = cmtv::phase_now(ctx);
   SigBatch B;
   const bool cache = cmtv::cache_enabled(ctx);
@@ -729,7 +765,7 @@ int cmtv_verify_commit(cmtv_ctx* ctx, uint32_t kind, uint32_t mode, const char* 
   return rc;
 }
 
-int cmtv_verify_commits(cmtv_ctx* ctx, uint32_t kind, uint32_t mode, const char* chain_id, size_t chain_id_len,
+static int cmtv_verify_commits_impl(cmtv_ctx* ctx, uint32_t kind, uint32_t mode, const char* chain_id, size_t chain_id_len,
                         size_t n, const cmtv_valset* vals, const cmtv_block_id* block_ids, const int64_t* heights,
                         const cmtv_commit* commits, uint64_t trust_num, uint64_t trust_den,
                         cmtv_commit_result* results, int* rcs, char* msg_bufs, size_t msg_cap) {
@@ -782,6 +818,26 @@ int cmtv_verify_commits(cmtv_ctx* ctx, uint32_t kind, uint32_t mode, const char*
   for (size_t c = 0; c < n; c++) rcs[c] = job_replay_batch(jobs[c], valid, seen);
   cmtv::phase_add(ctx, cmtv::kPhReplay, t1);
   return CMTV_OK;
+}
+
+int cmtv_verify_commit(cmtv_ctx* ctx, uint32_t kind, uint32_t mode, const char* chain_id, size_t chain_id_len,
+                       const cmtv_valset* vals, const cmtv_block_id* block_id, int64_t height,
+                       const cmtv_commit* commit, uint64_t trust_num, uint64_t trust_den, cmtv_commit_result* res,
+                       char* msg_buf, size_t msg_cap) {
+  return no_throw([&] {
+    return cmtv_verify_commit_impl(ctx, kind, mode, chain_id, chain_id_len, vals, block_id, height, commit, trust_num,
+                                   trust_den, res, msg_buf, msg_cap);
+  });
+}
+
+int cmtv_verify_commits(cmtv_ctx* ctx, uint32_t kind, uint32_t mode, const char* chain_id, size_t chain_id_len,
+                        size_t n, const cmtv_valset* vals, const cmtv_block_id* block_ids, const int64_t* heights,
+                        const cmtv_commit* commits, uint64_t trust_num, uint64_t trust_den,
+                        cmtv_commit_result* results, int* rcs, char* msg_bufs, size_t msg_cap) {
+  return no_throw([&] {
+    return cmtv_verify_commits_impl(ctx, kind, mode, chain_id, chain_id_len, n, vals, block_ids, heights, commits,
+                                    trust_num, trust_den, results, rcs, msg_bufs, msg_cap);
+  });
 }
 
 }  // extern "C"

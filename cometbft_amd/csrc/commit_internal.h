@@ -263,6 +263,10 @@ struct CommitJob {
   size_t first = 0;  // batch index of plan item 0
   size_t plan_prefix = 0;  // > 0: the plan is signatures [0, plan_prefix) (plan_idx unused)
   int64_t prefix_tally = 0;  // ... and the tally the loop reaches over it when every verdict is valid
+  // the validator set's total voting power when the caller already has it
+  // (the pipeline: one sum per distinct set, not per commit)
+  bool has_total = false;
+  int64_t total = 0;
 
   int fail(int32_t code, int32_t idx, const std::string& m) {
     res->code = code;
@@ -287,6 +291,18 @@ inline int fail_not_enough(CommitJob& J, int64_t tally) {
   std::snprintf(b, sizeof b, "invalid commit -- insufficient voting power: got %" PRId64 ", needed more than %" PRId64,
                 tally, J.needed);
   return J.fail(CMTV_COMMIT_ERR_NOT_ENOUGH_POWER, -1, b);
+}
+
+// The reference loop over a prefix plan (every signature [0, m) reachable,
+// every flag, key and signature length already checked -- commit.cpp
+// job_prepare_fast, pipeline.cpp direct commits): its outcome is the first
+// invalid verdict first_bad (m: none), else the tally against the threshold
+// (job_replay gives the same, one signature at a time).
+inline int replay_prefix(CommitJob& J, size_t m, int64_t tally, size_t first_bad) {
+  if (J.early != 1) return J.early;
+  J.res->n_verified = (uint32_t)m;
+  if (first_bad < m) return fail_wrong_sig(J, (uint32_t)first_bad);
+  return tally > J.needed ? CMTV_OK : fail_not_enough(J, tally);
 }
 
 // Argument checks of one commit (CMTV_EINVAL on null arrays).
@@ -404,5 +420,8 @@ int verify_commits_pipeline(cmtv_ctx* ctx, const CommitsArgs& a, int* rcs);
 // Whether cmtv_verify_commits takes the pipeline for a call of this many
 // signatures (CMTV_PIPE_MIN).
 bool pipeline_wanted(const cmtv_ctx* ctx, uint64_t n_sigs);
+// Largest sign-bytes span of one device launch (its message offsets are
+// 32-bit): 2^31, or CMTV_MAX_BATCH_MSG_BYTES when lower (commit.cpp).
+uint64_t max_batch_msg_bytes();
 
 }  // namespace cmtv

@@ -16,7 +16,15 @@ namespace cmtv {
 class HostPool {
  public:
   explicit HostPool(unsigned threads) {
-    for (unsigned i = 1; i < threads; i++) workers_.emplace_back([this] { run(); });
+    // a thread that cannot be created (container thread limits) leaves the
+    // pool smaller, never a half-built one: the calling thread always works
+    for (unsigned i = 1; i < threads; i++) {
+      try {
+        workers_.emplace_back([this] { run(); });
+      } catch (...) {
+        break;
+      }
+    }
   }
   ~HostPool() {
     {

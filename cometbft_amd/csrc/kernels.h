@@ -123,6 +123,14 @@ hipError_t launch_verify_sr25519(uint32_t n, const void* pk, const void* sig, co
 hipError_t launch_sign_bytes(uint32_t n, const void* tmpls, const uint8_t* blob, const uint32_t* tidx,
                              const uint8_t* commit_flag, const int64_t* sec, const int32_t* nanos,
                              const uint32_t* off, uint8_t* msg, hipStream_t s);
+// direct cross-height chunks (signbytes.hip): n_c commits (BulkDesc, their
+// templates) whose arrays sit in `arena` (the chunk's device copy of the
+// caller's pinned memory) -> the per-signature chunk layout of m planned
+// signatures and their message offsets (off[0..m]); ctot / cbase: n_c words
+// each of scratch
+hipError_t launch_bulk_gather(uint32_t n_c, uint32_t m, const void* desc, const void* tmpls, const uint8_t* arena,
+                              uint32_t* kidx, uint8_t* sig, uint32_t* off, uint32_t* tidx, uint8_t* flag,
+                              int64_t* sec, int32_t* nanos, uint32_t* ctot, uint32_t* cbase, hipStream_t s);
 hipError_t launch_pubkey(uint32_t n, const void* seeds, const uint32_t* btab, void* out_pk, hipStream_t s);
 hipError_t launch_sign(uint32_t n, const void* seeds, const void* key_idx, const void* msg, const void* off,
                        const uint32_t* btab, void* out_sig, hipStream_t s);

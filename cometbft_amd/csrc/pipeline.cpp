@@ -28,6 +28,7 @@
 #include <emmintrin.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstring>
 #include <deque>
@@ -51,14 +52,116 @@ uint64_t now_ns() {
       .count();
 }
 
+// The caller's arrays a direct chunk reads (BulkLayout), by class: the
+// signatures, ts_seconds, ts_nanos and flags of its commits' plans. Each
+// class's [lo, hi) over the chunk's commits; the DMA copies their union
+// (classes closer than kSpanGap merged into one span).
+constexpr int kClsSig = 0, kClsSec = 1, kClsNanos = 2, kClsFlags = 3, kClasses = 4;
+constexpr uintptr_t kSpanGap = 64 * 1024;
+struct SpanAcc {
+  uintptr_t lo[kClasses], hi[kClasses];
+  uint64_t need = 0;  // bytes the plans read
+  SpanAcc() {
+    for (int k = 0; k < kClasses; k++) {
+      lo[k] = UINTPTR_MAX;
+      hi[k] = 0;
+    }
+  }
+  static void ranges(const cmtv_commit* cm, size_t m, uintptr_t* a, size_t* len) {
+    a[kClsSig] = reinterpret_cast<uintptr_t>(cm->sigs + cm->sig_off[0]);
+    len[kClsSig] = 64 * m;
+    a[kClsSec] = reinterpret_cast<uintptr_t>(cm->ts_seconds);
+    len[kClsSec] = 8 * m;
+    a[kClsNanos] = reinterpret_cast<uintptr_t>(cm->ts_nanos);
+    len[kClsNanos] = 4 * m;
+    a[kClsFlags] = reinterpret_cast<uintptr_t>(cm->flags);
+    len[kClsFlags] = m;
+  }
+  void add(const cmtv_commit* cm, size_t m) {
+    uintptr_t a[kClasses];
+    size_t len[kClasses];
+    ranges(cm, m, a, len);
+    for (int k = 0; k < kClasses; k++) {
+      lo[k] = std::min(lo[k], a[k]);
+      hi[k] = std::max(hi[k], a[k] + len[k]);
+    }
+    need += 77 * m;
+  }
+  // the merged spans (sorted by address): count, and [slo, shi) of each
+  int merge(uintptr_t* slo, uintptr_t* shi, int* cls_span) const {
+    int order[kClasses] = {0, 1, 2, 3};
+    std::sort(order, order + kClasses, [&](int x, int y) { return lo[x] < lo[y]; });
+    int ns = 0;
+    for (int j = 0; j < kClasses; j++) {
+      const int k = order[j];
+      if (lo[k] >= hi[k]) {  // nothing of this class (m == 0 everywhere)
+        cls_span[k] = -1;
+        continue;
+      }
+      if (ns && lo[k] <= shi[ns - 1] + kSpanGap) {
+        shi[ns - 1] = std::max(shi[ns - 1], hi[k]);
+      } else {
+        slo[ns] = lo[k];
+        shi[ns] = hi[k];
+        ns++;
+      }
+      cls_span[k] = ns - 1;
+    }
+    return ns;
+  }
+  // the classes' extents summed (>= merged_bytes when they do not overlap)
+  uint64_t sum_bytes() const {
+    uint64_t b = 0;
+    for (int k = 0; k < kClasses; k++) b += lo[k] < hi[k] ? hi[k] - lo[k] : 0;
+    return b;
+  }
+  uint64_t merged_bytes() const {
+    uintptr_t slo[kClasses], shi[kClasses];
+    int cs[kClasses];
+    const int ns = merge(slo, shi, cs);
+    uint64_t b = 0;
+    for (int j = 0; j < ns; j++) b += shi[j] - slo[j];
+    return b;
+  }
+};
+
 struct Chunk {
   size_t c0 = 0, c1 = 0;              // commits [c0, c1)
   const cmtv_valset* vs = nullptr;    // the key class of its signatures
   const cmtv_keyset* ks = nullptr;    // registered keys, or null (generic kernel)
   size_t dev = 0;                     // where it was submitted
   int slot = 0;
+  bool direct = false;                // DMA'd from the caller's pinned block (BulkLayout)
+  SpanAcc acc;                        // direct: the classes' extents ...
+  uintptr_t cls_lo[kClasses] = {};    // ... and where each class starts, host
+  uint64_t cls_dev[kClasses] = {};    // and device (from o_arena)
   BulkLayout L;
 };
+
+// The first invalid verdict among batch bits [i0, i0 + m) as a plan index
+// (m: all valid).
+size_t first_invalid(const uint64_t* bm, size_t i0, size_t m) {
+  const size_t end = i0 + m;
+  for (size_t i = i0; i < end;) {
+    const size_t b = i & 63, lim = std::min<size_t>(64 - b, end - i);
+    uint64_t x = ~bm[i >> 6] >> b;
+    if (lim < 64) x &= (1ull << lim) - 1;
+    if (x) return i + (size_t)__builtin_ctzll(x) - i0;
+    i += lim;
+  }
+  return m;
+}
+
+// The pinned block holding [p, p + len), or -1.
+long find_block(const std::vector<PinnedRange>& pins, const void* p, size_t len) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  auto it = std::upper_bound(pins.begin(), pins.end(), a,
+                             [](uintptr_t x, const PinnedRange& r) { return x < r.base; });
+  if (it == pins.begin()) return -1;
+  --it;
+  if (a + len < a || a + len > it->base + it->bytes) return -1;
+  return (long)(it - pins.begin());
+}
 
 // Copy into the pinned staging with non-temporal stores: the staging is
 // written once by the host and read once by the H2D copy, so its lines need
@@ -88,6 +191,14 @@ inline void nt_copy(uint8_t* dst, const uint8_t* src, size_t n) {
 
 inline void nt_fence() { _mm_sfence(); }
 
+// Two validator-set structs over the same arrays (a caller typically hands
+// one struct per commit, all pointing at its set's arrays): one evaluation
+// of the set serves both within a call.
+inline bool same_arrays(const cmtv_valset* a, const cmtv_valset* b) {
+  return a == b || (a->n_vals == b->n_vals && a->pubkeys == b->pubkeys && a->pk_off == b->pk_off &&
+                    a->voting_power == b->voting_power);
+}
+
 // keys of vals are all 32 bytes and packed (what a registered key set needs)
 bool packed_keys(const cmtv_valset* v) {
   if (!v->n_vals) return false;
@@ -109,6 +220,11 @@ struct PipeWorkspace {
   std::vector<int32_t> early;
   std::vector<int64_t> needed;
   std::vector<const AddrIndex*> addr;  // LightTrusting
+  // direct commits: their prefix plan's tally and the pinned block of their
+  // arrays (direct[c] = 1)
+  std::vector<uint8_t> direct;
+  std::vector<int64_t> ptally;
+  std::vector<uint32_t> pblock;
   bool grow(size_t n, bool with_val) {
     if (cap_idx < n) {
       pidx.reset(new (std::nothrow) uint32_t[n]);
@@ -130,6 +246,25 @@ void pipe_workspace_free(PipeWorkspace* w) { delete w; }
 // pipeline writes it, the bulk lane copies and launches on it.
 void BulkLayout::compute() {
   auto up = [](size_t x) { return (x + 255) / 256 * 256; };
+  if (direct) {
+    // host part: templates, their bytes, descriptors; the rest device-only
+    o_tmpl = 0;
+    o_blob = up(n_tmpls * sizeof(SbTemplate));
+    o_desc = up(o_blob + blob_len + 16);
+    in_bytes = up(o_desc + n_tmpls * sizeof(BulkDesc));
+    o_key = in_bytes;
+    o_sig = up(o_key + 4 * m);
+    o_off = up(o_sig + 64 * m);
+    o_tidx = up(o_off + 4 * (m + 1));
+    o_flag = up(o_tidx + 4 * m);
+    o_sec = up(o_flag + m);
+    o_nanos = up(o_sec + 8 * m);
+    o_cbase = up(o_nanos + 4 * m);  // ctot, then cbase: n_tmpls words each
+    o_arena = up(o_cbase + 8 * n_tmpls);
+    o_msg = up(o_arena + arena_bytes);
+    dev_bytes = up(o_msg + msg_bytes + 16);
+    return;
+  }
   o_key = 0;
   o_sig = up(keyed ? 4 * m : 32 * m);
   o_off = up(o_sig + 64 * m);
@@ -151,10 +286,13 @@ bool pipeline_wanted(const cmtv_ctx* ctx, uint64_t n_sigs) {
   return !(v && v[0] == '1');
 }
 
-int verify_commits_pipeline(cmtv_ctx* ctx, const CommitsArgs& args, int* rcs) {
+namespace {
+
+// The pipeline proper; `pinned` collects the registered key sets it pins
+// (released by the caller, also after an exception). Bulk lock held.
+int run_pipeline(cmtv_ctx* ctx, const CommitsArgs& args, int* rcs, std::vector<const cmtv_keyset*>& pinned) {
   const size_t n = args.n;
   const uint32_t mode = args.mode;
-  std::unique_lock<std::mutex> bulk(bulk_mutex(ctx));
   HostPool& pool = host_pool(ctx);
   const PipeConfig pc = pipe_config(ctx);
   const bool trusting = args.kind == CMTV_VERIFY_COMMIT_LIGHT_TRUSTING;
@@ -183,6 +321,15 @@ int verify_commits_pipeline(cmtv_ctx* ctx, const CommitsArgs& args, int* rcs) {
   mbytes.resize(n);
   W.early.resize(n);
   W.needed.resize(n);
+  W.direct.resize(n);
+  W.ptally.resize(n);
+  W.pblock.resize(n);
+  // direct chunks (BulkLayout): on when the caller's arguments can be in
+  // pinned blocks of this context and the registered-key cache is on
+  std::vector<PinnedRange> pins;
+  bool direct_on = false;
+  static std::atomic<uint64_t> calls{0};
+  const uint64_t call_id = ++calls;
   // LightTrusting: one address index per distinct (address array, size)
   std::map<std::pair<const uint8_t*, uint32_t>, AddrIndex> addr_index;
   if (trusting) {
@@ -217,6 +364,137 @@ int verify_commits_pipeline(cmtv_ctx* ctx, const CommitsArgs& args, int* rcs) {
   sp.resize(n);
   mp.resize(n);
   tp.resize(n);
+  // the exact sign-bytes of a planned commit (pidx: its plan)
+  auto exact_mbytes = [](const CommitJob& J, const uint32_t* pi, size_t m, const TplLens& tlz) {
+    const cmtv_commit* cm = J.commit;
+    const uint8_t* fl = cm->flags;
+    const int64_t* se = cm->ts_seconds;
+    const int32_t* na = cm->ts_nanos;
+    uint64_t mb = 0;
+    if (pi[m - 1] - pi[0] == m - 1) {  // a contiguous plan (the common case)
+      const uint32_t a = pi[0];
+      for (size_t k = 0; k < m; k++) mb += msg_len(tlz, fl[a + k] == kFlagCommit, se[a + k], na[a + k]);
+    } else {
+      for (size_t k = 0; k < m; k++) {
+        const uint32_t idx = pi[k];
+        mb += msg_len(tlz, fl[idx] == kFlagCommit, se[idx], na[idx]);
+      }
+    }
+    return mb;
+  };
+  // A direct commit (BulkLayout): its plan is its signatures [0, m) --
+  // VerifyCommit: every flag Commit or Nil; VerifyCommitLight: Commit flags
+  // up to the +2/3 threshold -- from a set of packed 32-byte keys, 64-byte
+  // signatures back to back, and its four arrays aligned and inside ONE of the
+  // caller's pinned blocks. Nothing per signature is then packed on the host:
+  // the plan costs one pass over the flags (and powers) and the signature
+  // offsets. Sets plen, tlen, mbytes (an upper bound: every message at its
+  // template's longest) and the direct fields; false: the general plan.
+  auto plan_direct = [&](size_t c, const CommitJob& J) -> bool {
+    const cmtv_commit* cm = J.commit;
+    const cmtv_valset* v = J.vals;
+    const uint32_t n_s = cm->n_sigs;
+    if (n_s != v->n_vals) return false;
+    // per distinct set of this call (the id keeps a set freed and
+    // reallocated at the same address between calls from hitting): whether
+    // its keys are packed, its total power, and -- VerifyCommitLight -- the
+    // prefix an all-Commit commit of it reaches (the plan then depends on the
+    // set alone)
+    struct SetInfo {
+      const cmtv_valset* v = nullptr;
+      uint64_t call = 0;
+      bool packed = false;
+      int64_t total = 0;
+      uint32_t light_m = 0;
+      int64_t light_tally = 0;
+    };
+    thread_local SetInfo si;
+    if (!si.v || si.call != call_id || !same_arrays(v, si.v)) {
+      si.v = v;
+      si.call = call_id;
+      si.packed = packed_keys(v);
+      si.total = 0;
+      for (uint32_t i = 0; i < v->n_vals; i++) si.total += v->voting_power[i];
+      int64_t t = 0;
+      uint32_t m = 0;
+      for (uint32_t i = 0; i < v->n_vals; i++) {
+        t += v->voting_power[i];
+        m = i + 1;
+        if (t > J.needed) break;
+      }
+      si.light_m = m;
+      si.light_tally = t;
+    }
+    if (!si.packed) return false;
+    const uint8_t* fl = cm->flags;
+    // every flag of [0, k) is BlockIDFlagCommit (eight at a time)
+    auto all_commit = [fl](uint32_t k) {
+      uint64_t bad = 0;
+      uint32_t i = 0;
+      for (; i + 8 <= k; i += 8) {
+        uint64_t w;
+        std::memcpy(&w, fl + i, 8);
+        bad |= w ^ 0x0202020202020202ull;
+      }
+      for (; i < k; i++) bad |= fl[i] ^ kFlagCommit;
+      return bad == 0;
+    };
+    int64_t tally = 0;
+    uint32_t m = 0;
+    if (J.kind == CMTV_VERIFY_COMMIT) {
+      m = n_s;
+      if (all_commit(n_s)) {
+        tally = si.total;
+      } else {
+        const int64_t* vp = v->voting_power;
+        uint32_t bad = 0;
+        for (uint32_t i = 0; i < n_s; i++) {  // branch-free: the compiler vectorises it
+          const uint8_t f = fl[i];
+          const bool fb = f == kFlagCommit;
+          bad |= (uint32_t)(!fb & (f != kFlagNil));
+          tally += fb ? vp[i] : 0;
+        }
+        if (bad) return false;
+      }
+    } else {
+      // J.needed is the set's (total * 2 / 3, as when si was filled)
+      m = si.light_m;
+      tally = si.light_tally;
+      if (!all_commit(m)) return false;
+    }
+    uint32_t blk = UINT32_MAX;
+    if (m) {
+      const uint32_t* so = cm->sig_off;
+      const uint32_t s0 = so[0];
+      if ((uint64_t)s0 + 64ull * m > UINT32_MAX) return false;
+      uint32_t bad = 0;
+      for (uint32_t i = 1; i <= m; i++) bad |= so[i] ^ (s0 + 64u * i);  // vectorised
+      if (bad) return false;
+      uintptr_t a[kClasses];
+      size_t len[kClasses];
+      SpanAcc::ranges(cm, m, a, len);
+      if ((a[kClsSig] & 7) || (a[kClsSec] & 7) || (a[kClsNanos] & 3)) return false;
+      thread_local long hint = -1;
+      for (int k = 0; k < kClasses; k++) {
+        const PinnedRange* h = hint >= 0 && (size_t)hint < pins.size() ? &pins[(size_t)hint] : nullptr;
+        long b;
+        if (h && a[k] >= h->base && a[k] + len[k] >= a[k] && a[k] + len[k] <= h->base + h->bytes)
+          b = hint;
+        else
+          b = hint = find_block(pins, reinterpret_cast<const void*>(a[k]), len[k]);
+        if (b < 0 || (blk != UINT32_MAX && (uint32_t)b != blk)) return false;
+        blk = (uint32_t)b;
+      }
+      SbTemplate tpl;
+      tlen[c] = (uint32_t)put_commit_template(nullptr, 0, J.chain_id, J.chain_id_len, cm, &tpl);
+      mbytes[c] = (uint64_t)m * msg_len_bound(TplLens{tpl.pre_commit_len, tpl.pre_nil_len, tpl.post_len});
+    }
+    plen[c] = m;
+    W.direct[c] = 1;
+    W.ptally[c] = tally;
+    W.pblock[c] = blk;
+    return true;
+  };
   size_t planned_upto = 0;
   auto plan_window = [&](uint64_t want_sigs) {
     const uint64_t t0 = now_ns();
@@ -226,36 +504,33 @@ int verify_commits_pipeline(cmtv_ctx* ctx, const CommitsArgs& args, int* rcs) {
     const size_t a = planned_upto;
     pool.parallel_for(b - a, 64, [&](size_t lo, size_t hi) {
       thread_local Seen seen;
+      // each distinct validator set's total power once (job_preamble)
+      const cmtv_valset* tot_vs = nullptr;
+      int64_t tot = 0;
       for (size_t c = a + lo; c < a + hi; c++) {
         CommitJob J = job(c);
+        if (!tot_vs || !same_arrays(J.vals, tot_vs)) {
+          tot_vs = J.vals;
+          tot = 0;
+          for (uint32_t i = 0; i < tot_vs->n_vals; i++) tot += tot_vs->voting_power[i];
+        }
+        J.has_total = true;
+        J.total = tot;
         job_preamble(J);
         W.early[c] = J.early;
         W.needed[c] = J.needed;
+        W.direct[c] = 0;
         plen[c] = tlen[c] = 0;
         mbytes[c] = 0;
         if (J.early != 1) continue;
+        if (direct_on && plan_direct(c, J)) continue;
         uint32_t* pi = pidx_p + base[c];
         const size_t m = job_plan(J, pi, trusting ? pval_p + base[c] : nullptr, seen);
         plen[c] = (uint32_t)m;
         if (!m) continue;
         SbTemplate tpl;
         tlen[c] = (uint32_t)put_commit_template(nullptr, 0, J.chain_id, J.chain_id_len, J.commit, &tpl);
-        const TplLens tlz{tpl.pre_commit_len, tpl.pre_nil_len, tpl.post_len};
-        const cmtv_commit* cm = J.commit;
-        const uint8_t* fl = cm->flags;
-        const int64_t* se = cm->ts_seconds;
-        const int32_t* na = cm->ts_nanos;
-        uint64_t mb = 0;
-        if (pi[m - 1] - pi[0] == m - 1) {  // a contiguous plan (the common case)
-          const uint32_t a = pi[0];
-          for (size_t k = 0; k < m; k++) mb += msg_len(tlz, fl[a + k] == kFlagCommit, se[a + k], na[a + k]);
-        } else {
-          for (size_t k = 0; k < m; k++) {
-            const uint32_t idx = pi[k];
-            mb += msg_len(tlz, fl[idx] == kFlagCommit, se[idx], na[idx]);
-          }
-        }
-        mbytes[c] = mb;
+        mbytes[c] = exact_mbytes(J, pi, m, TplLens{tpl.pre_commit_len, tpl.pre_nil_len, tpl.post_len});
       }
     });
     planned_upto = b;
@@ -268,19 +543,21 @@ int verify_commits_pipeline(cmtv_ctx* ctx, const CommitsArgs& args, int* rcs) {
   const bool keyed_mode = keyset_cache_enabled(ctx);
   std::vector<size_t> live;
   live_devices_locked(ctx, live);
+  pinned_ranges_locked(ctx, pins);
+  direct_on = pc.direct && keyed_mode && !trusting && !pins.empty();
   lk.unlock();
 
   // ---- chunks, cut on the fly: commit-aligned, about `per` planned
   // signatures each (at least the kernels' full-rate size, pc.chunk, and at
   // least two per device when the call is large enough to split), one key
   // class per chunk when the keyset cache can serve it
-  std::vector<const cmtv_keyset*> pinned;
   std::vector<Chunk> chunks;
   uint64_t per = 0;
   bool ramp = false;
   size_t cursor = 0;  // next commit to put in a chunk
   const cmtv_valset* last_vs = nullptr;
   bool last_packed = false;
+  const uint64_t max_mb = max_batch_msg_bytes();
   auto cut_chunk = [&]() -> int {  // appends the next chunk; CMTV_OK or an error
     if (per == 0) {
       // the first window sets the chunk size from its plan ratio
@@ -318,13 +595,36 @@ int verify_commits_pipeline(cmtv_ctx* ctx, const CommitsArgs& args, int* rcs) {
     Chunk ch;
     ch.c0 = cursor;
     bool cls_set = false;
+    // direct class: the pinned block of a direct chunk's commits, -1 for a
+    // packed chunk (a chunk is one or the other)
+    bool dcls_set = false;
+    long dcls = -1;
     uint64_t s = 0, mb = 0, tb = 0;
     size_t c = cursor;
     for (; c < n; c++) {
       if (c == planned_upto) plan_window(std::max<uint64_t>(want - std::min(want, s), 65536));
+      SpanAcc nx;
+      const bool dir = plen[c] && W.direct[c];
+      if (plen[c]) {
+        const long dc = dir ? (long)W.pblock[c] : -1;
+        if (dcls_set && dc != dcls) break;
+        if (!dcls_set) {
+          dcls = dc;
+          dcls_set = true;
+        }
+        if (dir) {
+          // a direct chunk's DMA covers its classes' extents: cut before a
+          // commit that would make it copy far more than its plans read
+          // (a caller's arrays scattered over its pinned block)
+          nx = ch.acc;
+          nx.add(&args.commits[c], plen[c]);
+          const uint64_t cap = 4 * nx.need + (64u << 20);
+          if (s && nx.sum_bytes() > cap && nx.merged_bytes() > cap) break;
+        }
+      }
       if (plen[c] && keyed_mode) {
         const cmtv_valset* v = &args.vals[c];
-        if (v != last_vs) {
+        if (!last_vs || !same_arrays(v, last_vs)) {
           last_vs = v;
           last_packed = packed_keys(v);
         }
@@ -338,6 +638,11 @@ int verify_commits_pipeline(cmtv_ctx* ctx, const CommitsArgs& args, int* rcs) {
       // cut below the target (a commit that would cross it opens the next
       // chunk), unless the chunk would be empty
       if (s && s + plen[c] > want) break;
+      // ... and below the one-batch path's sign-bytes span per launch (its
+      // message offsets are 32-bit): a commit that would cross it opens the
+      // next chunk
+      if (s && mb + mbytes[c] >= max_mb) break;
+      if (dir) ch.acc = nx;
       sp[c] = s;
       mp[c] = mb;
       tp[c] = tb;
@@ -355,7 +660,7 @@ int verify_commits_pipeline(cmtv_ctx* ctx, const CommitsArgs& args, int* rcs) {
     ch.L.n_tmpls = ch.c1 - ch.c0;
     ch.L.blob_len = tb;
     ch.L.msg_bytes = mb;
-    if (mb + 16 >= (1ull << 32)) return CMTV_EINVAL;  // device message offsets are 32-bit
+    if (mb >= max_mb) return CMTV_EINVAL;  // one commit's sign-bytes alone reach the span
     if (keyed_mode && ch.vs && ch.L.m) {
       std::lock_guard<std::unique_lock<std::mutex>> g(lk);
       ch.ks = keyset_for_locked(ctx, ch.vs->pubkeys, ch.vs->n_vals);
@@ -365,13 +670,94 @@ int verify_commits_pipeline(cmtv_ctx* ctx, const CommitsArgs& args, int* rcs) {
       }
     }
     ch.L.keyed = ch.ks != nullptr;
+    ch.direct = dcls_set && dcls >= 0 && ch.L.m;
+    if (ch.direct && !ch.ks) {
+      // no registered key set (registration failed): pack this chunk after
+      // all -- the same prefix plans, written out, with exact sign-bytes
+      pool.parallel_for(ch.c1 - ch.c0, 64, [&](size_t lo, size_t hi) {
+        thread_local Seen seen;
+        for (size_t k = ch.c0 + lo; k < ch.c0 + hi; k++) {
+          if (!W.direct[k]) continue;
+          W.direct[k] = 0;
+          if (!plen[k]) continue;
+          CommitJob J = job(k);
+          J.early = W.early[k];
+          J.needed = W.needed[k];
+          uint32_t* pi = pidx_p + base[k];
+          (void)job_plan(J, pi, nullptr, seen);  // == the prefix [0, plen)
+          SbTemplate tpl;
+          put_commit_template(nullptr, 0, J.chain_id, J.chain_id_len, J.commit, &tpl);
+          mbytes[k] = exact_mbytes(J, pi, plen[k], TplLens{tpl.pre_commit_len, tpl.pre_nil_len, tpl.post_len});
+        }
+      });
+      uint64_t x = 0;
+      for (size_t k = ch.c0; k < ch.c1; k++) {
+        mp[k] = x;
+        x += mbytes[k];
+      }
+      ch.L.msg_bytes = x;
+      ch.direct = false;
+    }
+    if (ch.direct) {
+      // the DMA spans: the classes' extents, merged, each landing at a
+      // device offset congruent to its host address mod 256 (so the
+      // caller's 8-byte alignment holds on the device)
+      uintptr_t slo[kClasses], shi[kClasses];
+      int cs[kClasses];
+      const int ns = ch.acc.merge(slo, shi, cs);
+      size_t at = 0;
+      for (int j = 0; j < ns; j++) {
+        at = (at + 255) / 256 * 256 + (slo[j] & 255);
+        ch.L.spans[j] = BulkSpan{reinterpret_cast<const uint8_t*>(slo[j]), (size_t)(shi[j] - slo[j]), at};
+        at += shi[j] - slo[j];
+      }
+      ch.L.n_spans = ns;
+      ch.L.arena_bytes = at;
+      for (int k = 0; k < kClasses; k++) {
+        ch.cls_lo[k] = ch.acc.lo[k];
+        ch.cls_dev[k] = cs[k] < 0 ? 0 : ch.L.spans[cs[k]].dev_off + (ch.acc.lo[k] - slo[cs[k]]);
+      }
+      ch.L.direct = true;
+    }
     ch.L.compute();
     chunks.push_back(ch);
     return CMTV_OK;
   };
 
   // ---- the chunk loop
+  // a direct chunk's host part: each commit's template and descriptor
+  auto pack_direct = [&](Chunk& ch, uint8_t* h) {
+    const BulkLayout& L = ch.L;
+    auto* tmpls = reinterpret_cast<SbTemplate*>(h + L.o_tmpl);
+    uint8_t* blob = h + L.o_blob;
+    auto* desc = reinterpret_cast<BulkDesc*>(h + L.o_desc);
+    pool.parallel_for(ch.c1 - ch.c0, 64, [&](size_t b, size_t e) {
+      for (size_t c = ch.c0 + b; c < ch.c0 + e; c++) {
+        const size_t tl = c - ch.c0;
+        const uint32_t m = plen[c];
+        if (!m) {
+          tmpls[tl] = SbTemplate{};
+          desc[tl] = BulkDesc{};
+          continue;
+        }
+        const cmtv_commit* cm = &args.commits[c];
+        put_commit_template(blob, tp[c], args.chain_id, args.chain_id_len, cm, &tmpls[tl]);
+        uintptr_t a[kClasses];
+        size_t len[kClasses];
+        SpanAcc::ranges(cm, m, a, len);
+        BulkDesc d;
+        d.sig = ch.cls_dev[kClsSig] + (a[kClsSig] - ch.cls_lo[kClsSig]);
+        d.sec = ch.cls_dev[kClsSec] + (a[kClsSec] - ch.cls_lo[kClsSec]);
+        d.nanos = ch.cls_dev[kClsNanos] + (a[kClsNanos] - ch.cls_lo[kClsNanos]);
+        d.flags = ch.cls_dev[kClsFlags] + (a[kClsFlags] - ch.cls_lo[kClsFlags]);
+        d.sp = (uint32_t)sp[c];
+        d.m = m;
+        desc[tl] = d;
+      }
+    });
+  };
   auto pack = [&](Chunk& ch, uint8_t* h) {
+    if (ch.direct) return pack_direct(ch, h);
     const BulkLayout& L = ch.L;
     auto* kidx = reinterpret_cast<uint32_t*>(h + L.o_key);
     uint8_t* pk = h + L.o_key;
@@ -461,6 +847,11 @@ int verify_commits_pipeline(cmtv_ctx* ctx, const CommitsArgs& args, int* rcs) {
         CommitJob J = job(c);
         J.early = W.early[c];
         J.needed = W.needed[c];
+        if (W.direct[c]) {  // a prefix plan: its first invalid bit decides
+          const size_t m = plen[c];
+          rcs[c] = replay_prefix(J, m, W.ptally[c], m ? first_invalid(bm, i0, m) : 0);
+          continue;
+        }
         rcs[c] = job_replay(J, pidx_p + base[c], plen[c],
                             [bm, i0](size_t j) {
                               const size_t i = i0 + j;
@@ -540,6 +931,7 @@ int verify_commits_pipeline(cmtv_ctx* ctx, const CommitsArgs& args, int* rcs) {
       {
         std::lock_guard<std::unique_lock<std::mutex>> g(lk);
         rc = bulk_submit_locked(ctx, ch.dev, ch.slot, ch.L, ch.ks, mode);
+        if (rc == CMTV_OK && ch.direct) count_direct_locked(ctx);
       }
       ph_submit += now_ns() - ts;
       if (rc != CMTV_OK) {
@@ -565,12 +957,40 @@ int verify_commits_pipeline(cmtv_ctx* ctx, const CommitsArgs& args, int* rcs) {
   }
   {
     std::lock_guard<std::unique_lock<std::mutex>> g(lk);
-    for (auto* ks : pinned) keyset_unpin_locked(ctx, ks);
     phase_add_ns(ctx, kPhPipePlan, ph_plan);
     phase_add_ns(ctx, kPhPipePack, ph_pack);
     phase_add_ns(ctx, kPhPipeSubmit, ph_submit);
     phase_add_ns(ctx, kPhPipeWait, ph_wait);
     phase_add_ns(ctx, kPhPipeReplay, ph_replay);
+  }
+  return rc;
+}
+
+}  // namespace
+
+int verify_commits_pipeline(cmtv_ctx* ctx, const CommitsArgs& args, int* rcs) {
+  std::unique_lock<std::mutex> bulk(bulk_mutex(ctx));
+  std::vector<const cmtv_keyset*> pinned;
+  pinned.reserve(8);
+  int rc;
+  bool threw = false;
+  // no C++ exception crosses the C ABI: a failed allocation (std::bad_alloc)
+  // or thread creation (std::system_error) is the call's error code, after
+  // everything the call enqueued has drained
+  try {
+    rc = run_pipeline(ctx, args, rcs, pinned);
+  } catch (const std::bad_alloc&) {
+    rc = CMTV_ENOMEM;
+    threw = true;
+  } catch (...) {
+    rc = CMTV_EINVAL;
+    threw = true;
+  }
+  if (threw) bulk_drain(ctx);
+  if (!pinned.empty()) {
+    std::unique_lock<std::mutex> lk;
+    (void)ctx_lock(ctx, lk);
+    for (auto* ks : pinned) keyset_unpin_locked(ctx, ks);
   }
   return rc;
 }

@@ -22,6 +22,7 @@
 #include <deque>
 #include <fstream>
 #include <memory>
+#include <map>
 #include <mutex>
 #include <new>
 #include <random>
@@ -545,6 +546,10 @@ struct cmtv_ctx {
   size_t pipe_min = 32768, pipe_chunk = 1u << 20;
   int pipe_slots = 3;
   bool pipe_on = true;
+  bool pipe_direct = true;  // CMTV_PIPE_DIRECT=0: pinned arguments are packed too
+  // the caller's pinned blocks (cmtv_alloc_pinned): base -> bytes; chunks
+  // whose arrays lie in one are DMA'd from it (pipeline.cpp direct chunks)
+  std::map<uintptr_t, size_t> pinned;
   // cached key sets evicted while a pipeline call had them pinned
   std::vector<cmtv_keyset*> zombies;
   cmtv::PipeWorkspace* pipe_ws = nullptr;
@@ -1498,6 +1503,7 @@ int stage_sigs_early_locked(cmtv_ctx* ctx, const uint8_t* sigs, size_t n, const 
     uint64_t t;
     ~Done() { phase_add(c, kPhEarly, t); }
   } done{ctx, t0};
+  clear_early_locked(ctx);  // whatever returns below stages nothing
   if (n == 0 || n > ctx->zc_max || ctx->live.size() != 1 || !ctx->early_sigs) return CMTV_OK;
   // the generic row kernels read their staging from mapped memory instead
   // (a copy's latency is most of their call); the quad-family forms gain the
@@ -1543,8 +1549,21 @@ static int single_device_rc(cmtv_ctx* ctx, int rc) {
   return rc;
 }
 
+// Early-staged signatures (stage_sigs_early_locked) are valid only inside the
+// lock hold of the cmtv_verify_commit call that staged them: every new hold
+// forgets them, so a later call can never take stale device bytes for its own
+// (the caller may refill the same buffer, and d_in / h_in may have been
+// rewritten by another entry point meanwhile).
+void clear_early_locked(cmtv_ctx* ctx) {
+  for (auto& D : ctx->devs) {
+    D.early_src = D.early_pk = nullptr;
+    D.early_n = 0;
+  }
+}
+
 int ctx_lock(cmtv_ctx* ctx, std::unique_lock<std::mutex>& lk) {
   lk = std::unique_lock<std::mutex>(ctx->mu);
+  clear_early_locked(ctx);
   return hipSetDevice(ctx->devs[0].ordinal) == hipSuccess ? CMTV_OK : CMTV_ENODEV;
 }
 
@@ -1698,6 +1717,7 @@ static void read_env(cmtv_ctx* ctx) {
     if (k >= 2 && k <= kBulkSlotsMax) ctx->pipe_slots = (int)k;
   }
   if (const char* v = std::getenv("CMTV_PIPELINE")) ctx->pipe_on = v[0] != '0';
+  if (const char* v = std::getenv("CMTV_PIPE_DIRECT")) ctx->pipe_direct = v[0] != '0';
   if (const char* dm = std::getenv("CMTV_RCCL_DRAIN_MS")) {
     const long v = std::strtol(dm, nullptr, 10);
     if (v >= 1 && v <= 600000) ctx->rccl_drain_ms = (uint32_t)v;
@@ -1865,6 +1885,8 @@ void cmtv_close(cmtv_ctx* ctx) {
     std::fprintf(stderr, "}, \"calls\": %llu}\n", (unsigned long long)ctx->phase_calls);
   }
   ctx->pool.reset();
+  for (auto& b : ctx->pinned) (void)hipHostFree(reinterpret_cast<void*>(b.first));  // the caller's leftovers
+  ctx->pinned.clear();
   pipe_workspace_free(ctx->pipe_ws);
   ctx->pipe_ws = nullptr;
   for (auto& e : ctx->keysets) cmtv_keyset_free(e.second);
@@ -2278,7 +2300,7 @@ HostPool& host_pool(cmtv_ctx* ctx) {
 }
 
 PipeConfig pipe_config(const cmtv_ctx* ctx) {
-  return PipeConfig{ctx->pipe_min, ctx->pipe_chunk, ctx->pipe_slots, ctx->pipe_on};
+  return PipeConfig{ctx->pipe_min, ctx->pipe_chunk, ctx->pipe_slots, ctx->pipe_on, ctx->pipe_direct};
 }
 
 void live_devices_locked(cmtv_ctx* ctx, std::vector<size_t>& out) { out = ctx->live; }
@@ -2349,11 +2371,28 @@ int bulk_submit_locked(cmtv_ctx* ctx, size_t dev, int slot, const BulkLayout& L,
   if (e != hipSuccess) return hip_fail(e);
   auto* din = static_cast<uint8_t*>(S.d_in.p);
   auto* dbm = static_cast<uint64_t*>(S.d_bm.p);
-  // H2D on the copy stream (overlaps the exec stream's previous chunk)
-  if ((e = hipMemcpyAsync(din, S.h_in.p, L.in_bytes, hipMemcpyHostToDevice, BL.copy)) != hipSuccess ||
-      (e = hipEventRecord(S.h2d, BL.copy)) != hipSuccess || (e = hipStreamWaitEvent(BL.exec, S.h2d, 0)) != hipSuccess)
+  // H2D on the copy stream (overlaps the exec stream's previous chunk); a
+  // direct chunk's per-signature data comes straight from the caller's
+  // pinned arena, one DMA per span, and is laid out by k_bulk_gather
+  if ((e = hipMemcpyAsync(din, S.h_in.p, L.in_bytes, hipMemcpyHostToDevice, BL.copy)) != hipSuccess) return hip_fail(e);
+  if (L.direct)
+    for (int k = 0; k < L.n_spans; k++)
+      if ((e = hipMemcpyAsync(din + L.o_arena + L.spans[k].dev_off, L.spans[k].host, L.spans[k].bytes,
+                              hipMemcpyHostToDevice, BL.copy)) != hipSuccess)
+        return hip_fail(e);
+  if ((e = hipEventRecord(S.h2d, BL.copy)) != hipSuccess || (e = hipStreamWaitEvent(BL.exec, S.h2d, 0)) != hipSuccess)
     return hip_fail(e);
   auto* off = reinterpret_cast<uint32_t*>(din + L.o_off);
+  if (L.direct) {
+    if (!ks) return CMTV_EINVAL;  // direct chunks are registered-key chunks
+    auto* cb = reinterpret_cast<uint32_t*>(din + L.o_cbase);
+    if ((e = launch_bulk_gather((uint32_t)L.n_tmpls, (uint32_t)L.m, din + L.o_desc, din + L.o_tmpl, din + L.o_arena,
+                                reinterpret_cast<uint32_t*>(din + L.o_key), din + L.o_sig, off,
+                                reinterpret_cast<uint32_t*>(din + L.o_tidx), din + L.o_flag,
+                                reinterpret_cast<int64_t*>(din + L.o_sec), reinterpret_cast<int32_t*>(din + L.o_nanos),
+                                cb, cb + L.n_tmpls, BL.exec)) != hipSuccess)
+      return hip_fail(e);
+  }
   // sign-bytes from the chunk's templates into o_msg (k_sign_bytes; the
   // bulk chunks run the lane kernels, whose launches take no fused form)
   if ((e = launch_sign_bytes((uint32_t)L.m, din + L.o_tmpl, din + L.o_blob, reinterpret_cast<uint32_t*>(din + L.o_tidx),
@@ -2399,6 +2438,10 @@ void bulk_drain(cmtv_ctx* ctx) {
 }
 
 bool retire_device_locked(cmtv_ctx* ctx, size_t dev) {
+  // retired meanwhile by another call (the pipeline holds the lock only
+  // around submissions): already out of the rotation, so the chunks run again
+  // on whatever is still live
+  if (ctx->devs[dev].failed) return !ctx->live.empty();
   // CMTV_FAULT_AT stands for a failure of the call, not of the device
   const bool injected = ctx->fault_pending;
   ctx->fault_pending = false;
@@ -2409,12 +2452,50 @@ bool retire_device_locked(cmtv_ctx* ctx, size_t dev) {
 }
 
 void count_invalid_locked(cmtv_ctx* ctx, uint64_t n) { ctx->stats.invalid += n; }
+void count_direct_locked(cmtv_ctx* ctx) { ctx->stats.direct_chunks++; }
+
+void pinned_ranges_locked(cmtv_ctx* ctx, std::vector<PinnedRange>& out) {
+  out.clear();
+  for (auto& b : ctx->pinned) out.push_back(PinnedRange{b.first, b.second});
+}
 
 PipeWorkspace*& pipe_workspace(cmtv_ctx* ctx) { return ctx->pipe_ws; }
 
 }  // namespace cmtv
 
 extern "C" {
+
+int cmtv_alloc_pinned(cmtv_ctx* ctx, size_t bytes, void** out) {
+  if (!ctx || !out || bytes == 0) return CMTV_EINVAL;
+  *out = nullptr;
+  std::unique_lock<std::mutex> lk;
+  if (ctx_lock(ctx, lk) != CMTV_OK) return CMTV_ENODEV;
+  void* p = nullptr;
+  // portable: every device of the context DMAs from it
+  if (hipHostMalloc(&p, bytes, hipHostMallocPortable) != hipSuccess || !p) {
+    (void)hipGetLastError();
+    return CMTV_ENOMEM;
+  }
+  try {
+    ctx->pinned.emplace(reinterpret_cast<uintptr_t>(p), bytes);
+  } catch (...) {
+    (void)hipHostFree(p);
+    return CMTV_ENOMEM;
+  }
+  *out = p;
+  return CMTV_OK;
+}
+
+int cmtv_free_pinned(cmtv_ctx* ctx, void* p) {
+  if (!ctx) return CMTV_EINVAL;
+  if (!p) return CMTV_OK;
+  std::unique_lock<std::mutex> lk;
+  if (ctx_lock(ctx, lk) != CMTV_OK) return CMTV_ENODEV;
+  auto it = ctx->pinned.find(reinterpret_cast<uintptr_t>(p));
+  if (it == ctx->pinned.end()) return CMTV_EINVAL;  // not this context's block
+  ctx->pinned.erase(it);
+  return hipHostFree(p) == hipSuccess ? CMTV_OK : CMTV_EHIP;
+}
 
 void cmtv_keyset_free(cmtv_keyset* ks) {
   if (!ks) return;

@@ -50,6 +50,9 @@ int verify_templated_locked(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const ui
 // with pk, only past the row kernels' band, which keep reading their
 // staging in place). Caller holds the lock.
 int stage_sigs_early_locked(cmtv_ctx* ctx, const uint8_t* sigs, size_t n, const uint8_t* pk = nullptr);
+// Forgets early-staged signatures (ctx_lock does it on every new lock hold;
+// cmtv_verify_commit also on every exit). Caller holds the lock.
+void clear_early_locked(cmtv_ctx* ctx);
 
 // cmtv_keyset_cache: the registered key set of these n 32-byte keys (built on
 // first use), or NULL when the cache is off or registration failed.
@@ -85,15 +88,39 @@ void phase_add_ns(cmtv_ctx* ctx, int phase, uint64_t ns);
 //   flag u8 (1 = BlockIDFlagCommit), sec i64, nanos i32 per signature,
 //   tmpls SbTemplate per commit, blob the templates' bytes;
 // on the device k_sign_bytes then writes the sign-bytes after it (o_msg).
+//
+// A DIRECT chunk (the caller's flags, timestamps and signatures in
+// cmtv_alloc_pinned memory, every commit's plan a prefix of its signatures,
+// registered keys) packs nothing per signature: the pinned staging holds only
+//   tmpls, blob, desc (one BulkDesc per commit, signbytes.h)
+// and the device gets the caller's arrays by DMA -- up to kBulkSpansMax spans
+// of its pinned memory, copied to o_arena -- from which k_bulk_gather builds
+// the per-signature arrays above (device-only, after in_bytes).
 constexpr int kBulkSlotsMax = 4;
+constexpr int kBulkSpansMax = 4;
+struct BulkSpan {
+  const uint8_t* host = nullptr;  // pinned source, 256-byte aligned
+  size_t bytes = 0;
+  size_t dev_off = 0;  // from o_arena, 256-byte aligned (host and device agree mod 256)
+};
 struct BulkLayout {
   size_t m = 0, n_tmpls = 0, blob_len = 0;
-  uint64_t msg_bytes = 0;
-  bool keyed = false;
+  uint64_t msg_bytes = 0;  // direct: an upper bound (the device computes the offsets)
+  bool keyed = false, direct = false;
   size_t o_key = 0, o_sig = 0, o_off = 0, o_tidx = 0, o_flag = 0, o_sec = 0, o_nanos = 0, o_tmpl = 0, o_blob = 0;
+  size_t o_desc = 0, o_cbase = 0, o_arena = 0, arena_bytes = 0;
+  int n_spans = 0;
+  BulkSpan spans[kBulkSpansMax];
   size_t in_bytes = 0, o_msg = 0, dev_bytes = 0;
   void compute();
 };
+// The caller's pinned blocks (cmtv_alloc_pinned), sorted by address: a
+// snapshot for one pipeline call (context lock held)
+struct PinnedRange {
+  uintptr_t base;
+  size_t bytes;
+};
+void pinned_ranges_locked(cmtv_ctx* ctx, std::vector<PinnedRange>& out);
 std::mutex& bulk_mutex(cmtv_ctx* ctx);
 class HostPool;
 // the context's worker pool (created on first use; bulk lock held)
@@ -102,6 +129,7 @@ struct PipeConfig {
   size_t min_sigs, chunk;
   int slots;
   bool enabled;
+  bool direct = true;  // CMTV_PIPE_DIRECT=0: always pack (A/B, tests)
 };
 PipeConfig pipe_config(const cmtv_ctx* ctx);
 // live device indices, in shard order (context lock held)
@@ -126,6 +154,8 @@ PipeWorkspace*& pipe_workspace(cmtv_ctx* ctx);
 void pipe_workspace_free(PipeWorkspace* w);
 // the context's invalid-verdict counter (context lock held)
 void count_invalid_locked(cmtv_ctx* ctx, uint64_t n);
+// cmtv_stats.direct_chunks (context lock held)
+void count_direct_locked(cmtv_ctx* ctx);
 // registered key set pins (context lock held): a pinned cached set is not
 // freed by eviction until unpinned
 void keyset_pin_locked(const cmtv_keyset* ks);

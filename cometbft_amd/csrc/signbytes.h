@@ -33,6 +33,20 @@ struct SbTemplate {
   uint32_t post_off, post_len;              // chain id field
 };
 
+// One commit of a direct cross-height chunk (pipeline.cpp with the caller's
+// arguments in cmtv_alloc_pinned memory; runtime.cpp bulk_submit_locked;
+// k_bulk_gather): where the commit's arrays landed in the chunk's device copy
+// of the caller's pinned arena (byte offsets), and its plan, which is the
+// commit's signatures [0, m) -- batch indices [sp, sp + m). Its template and
+// commit index is its position in the chunk.
+struct BulkDesc {
+  uint64_t sig;    // signature 0 (64-byte records, 8-byte aligned)
+  uint64_t sec;    // ts_seconds[0] (8-byte aligned)
+  uint64_t nanos;  // ts_nanos[0] (4-byte aligned)
+  uint64_t flags;  // flags[0]
+  uint32_t sp, m;
+};
+
 CMTV_HD uint32_t sb_uvlen(uint64_t v) {
   uint32_t n = 1;
   while (v >= 0x80) {

@@ -84,6 +84,114 @@ __global__ __launch_bounds__(256) void k_sign_bytes(uint32_t n, const SbTemplate
   }
 }
 
+// ---- direct chunks: the per-signature staging built on the device from the
+// caller's arrays (DMA'd from its pinned arena), so the host packs nothing
+// per signature (pipeline.cpp). Three steps on the chunk's exec stream:
+//   k_bulk_gather   one workgroup per commit: signature, flag, seconds, nanos,
+//                   template / key index of each planned signature into the
+//                   chunk layout, and its message offset within the commit
+//                   (a workgroup scan of sb_msg_len); the commit's message
+//                   bytes into ctot[c]
+//   k_bulk_bases    one workgroup: exclusive scan of ctot -> cbase, off[m]
+//   k_bulk_rebase   off[i] += cbase[tidx[i]]
+// after which k_sign_bytes and the verify kernel run as for a packed chunk.
+
+// inclusive sum of x over the 256 threads' positions; *total = block total
+__device__ __forceinline__ uint32_t block_scan256(uint32_t x, uint32_t* wsum, uint32_t* total) {
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  uint32_t pre = 0, tot = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < 4; j++) {
+    const uint32_t v = wsum[j];
+    pre += j < w ? v : 0;
+    tot += v;
+  }
+  __syncthreads();  // wsum is rewritten by the next round
+  *total = tot;
+  return pre + x;
+}
+
+__global__ __launch_bounds__(256) void k_bulk_gather(const BulkDesc* __restrict__ desc,
+                                                     const SbTemplate* __restrict__ tmpls,
+                                                     const uint8_t* __restrict__ arena, uint32_t* __restrict__ kidx,
+                                                     uint8_t* __restrict__ sig, uint32_t* __restrict__ off,
+                                                     uint32_t* __restrict__ tidx, uint8_t* __restrict__ flag,
+                                                     int64_t* __restrict__ sec, int32_t* __restrict__ nanos,
+                                                     uint32_t* __restrict__ ctot) {
+  __shared__ uint32_t wsum[4];
+  const uint32_t c = blockIdx.x;
+  const BulkDesc D = desc[c];
+  uint32_t carry = 0;
+  if (D.m) {
+    const SbTemplate T = tmpls[c];
+    for (uint32_t k0 = 0; k0 < D.m; k0 += 256) {
+      const uint32_t k = k0 + threadIdx.x;
+      uint32_t len = 0;
+      if (k < D.m) {
+        const uint32_t i = D.sp + k;
+        const bool fb = arena[D.flags + k] == 2;  // BlockIDFlagCommit
+        const int64_t s = *reinterpret_cast<const int64_t*>(arena + D.sec + 8ull * k);
+        const int32_t ns = *reinterpret_cast<const int32_t*>(arena + D.nanos + 4ull * k);
+        const uint2* src = reinterpret_cast<const uint2*>(arena + D.sig + 64ull * k);
+        uint2* dst = reinterpret_cast<uint2*>(sig + 64ull * i);
+#pragma unroll
+        for (int j = 0; j < 8; j++) dst[j] = src[j];
+        flag[i] = fb ? 1 : 0;
+        sec[i] = s;
+        nanos[i] = ns;
+        tidx[i] = c;
+        kidx[i] = k;  // a prefix plan: signature k is by validator k
+        len = sb_msg_len(T, fb, s, ns);
+      }
+      uint32_t tot;
+      const uint32_t inc = block_scan256(len, wsum, &tot);
+      if (k < D.m) off[D.sp + k] = carry + inc - len;
+      carry += tot;
+    }
+  }
+  if (threadIdx.x == 0) ctot[c] = carry;
+}
+
+__global__ __launch_bounds__(256) void k_bulk_bases(uint32_t n_c, const uint32_t* __restrict__ ctot,
+                                                    uint32_t* __restrict__ cbase, uint32_t* __restrict__ off,
+                                                    uint32_t m) {
+  __shared__ uint32_t wsum[4];
+  uint32_t carry = 0;
+  for (uint32_t c0 = 0; c0 < n_c; c0 += 256) {
+    const uint32_t c = c0 + threadIdx.x;
+    const uint32_t v = c < n_c ? ctot[c] : 0;
+    uint32_t tot;
+    const uint32_t inc = block_scan256(v, wsum, &tot);
+    if (c < n_c) cbase[c] = carry + inc - v;
+    carry += tot;
+  }
+  if (threadIdx.x == 0) off[m] = carry;
+}
+
+__global__ __launch_bounds__(256) void k_bulk_rebase(uint32_t m, const uint32_t* __restrict__ cbase,
+                                                     const uint32_t* __restrict__ tidx, uint32_t* __restrict__ off) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i < m) off[i] += cbase[tidx[i]];
+}
+
+hipError_t launch_bulk_gather(uint32_t n_c, uint32_t m, const void* desc, const void* tmpls, const uint8_t* arena,
+                              uint32_t* kidx, uint8_t* sig, uint32_t* off, uint32_t* tidx, uint8_t* flag,
+                              int64_t* sec, int32_t* nanos, uint32_t* ctot, uint32_t* cbase, hipStream_t s) {
+  if (n_c == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_bulk_gather, dim3(n_c), dim3(256), 0, s, static_cast<const BulkDesc*>(desc),
+                     static_cast<const SbTemplate*>(tmpls), arena, kidx, sig, off, tidx, flag, sec, nanos, ctot);
+  hipLaunchKernelGGL(k_bulk_bases, dim3(1), dim3(256), 0, s, n_c, ctot, cbase, off, m);
+  if (m) hipLaunchKernelGGL(k_bulk_rebase, dim3((m + 255) / 256), dim3(256), 0, s, m, cbase, tidx, off);
+  return hipGetLastError();
+}
+
 hipError_t launch_sign_bytes(uint32_t n, const void* tmpls, const uint8_t* blob, const uint32_t* tidx,
                              const uint8_t* commit_flag, const int64_t* sec, const int32_t* nanos,
                              const uint32_t* off, uint8_t* msg, hipStream_t s) {

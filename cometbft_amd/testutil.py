@@ -175,7 +175,7 @@ class ReplayChain:
     signature the loop reaches (-1 = nil error)."""
 
     def __init__(self, ctx: Context, sv: SyntheticValidators, h0: int, n_heights: int, flip: float = 0.01,
-                 seed: int = 42, sign_heights: int = 8192):
+                 seed: int = 42, sign_heights: int = 8192, pinned: Context | None = None):
         import ctypes
 
         from . import _native as N
@@ -183,7 +183,26 @@ class ReplayChain:
         n = len(sv.valset.validators)
         self.n_vals, self.n_heights, self.h0 = n, n_heights, h0
         total = n * n_heights
-        self.sig = np.empty((total, 64), np.uint8)
+        # pinned: the commits' flags, timestamps and signatures in ONE
+        # cmtv_alloc_pinned block of that context (a cgo shim's arena in
+        # pinned memory: cmtv_verify_commits then DMAs them, no host pack)
+        self.block = None
+        if pinned is not None:
+            nb = 256 + (n + 1 + 7) // 8 * 8 + 8 * total + (4 * (n + 1) + 7) // 8 * 8 + 64 * total
+            self.block = pinned.alloc_pinned(nb)
+            at = 0
+
+            def carve(dtype, count):
+                nonlocal at
+                a = self.block.array(dtype, count, at)
+                at += (count * np.dtype(dtype).itemsize + 7) // 8 * 8
+                return a
+            flags_a = carve(np.uint8, n + 1)
+            secs_a = carve(np.int64, total).reshape(n_heights, n)
+            nanos_a = carve(np.int32, n + 1)
+            self.sig = carve(np.uint8, 64 * total).reshape(total, 64)
+        else:
+            self.sig = np.empty((total, 64), np.uint8)
         kidx = np.tile(np.arange(n, dtype=np.uint32), min(sign_heights, n_heights))
         for c0 in range(0, n_heights, sign_heights):
             hc = min(sign_heights, n_heights - c0)
@@ -202,6 +221,11 @@ class ReplayChain:
         assert all(s == EPOCH_2023 + h0 for s, _ in ts)  # n < 1e6: seconds = EPOCH + h
         self.nanos = np.array([ns for _, ns in ts] + [0], np.int32)
         self.secs = (EPOCH_2023 + h0 + np.arange(n_heights, dtype=np.int64))[:, None].repeat(n, 1)
+        if self.block is not None:
+            flags_a[:] = self.flags
+            nanos_a[:] = self.nanos
+            secs_a[:] = self.secs
+            self.flags, self.nanos, self.secs = flags_a, nanos_a, secs_a
         self.addrs = np.frombuffer(b"".join(v.address for v in sv.valset.validators) + b"\0", np.uint8).copy()
         hs = range(h0, h0 + n_heights)
         self.bhash = np.frombuffer(b"".join(hashlib.sha256(b"block%d" % h).digest() for h in hs), np.uint8).reshape(

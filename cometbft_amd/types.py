@@ -223,7 +223,22 @@ def _p32(a):
     return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
 
 
-def _pack_commit(commit: Commit):
+class _Arena:
+    """Carves arrays out of one pinned block (a cgo shim's argument arena in
+    cmtv_alloc_pinned memory), 8-byte aligned."""
+
+    def __init__(self, block):
+        self.block, self.at = block, 0
+
+    def put(self, a: np.ndarray) -> np.ndarray:
+        a = np.ascontiguousarray(a)
+        out = self.block.array(a.dtype, a.size, self.at).reshape(a.shape)
+        out[...] = a
+        self.at += (a.nbytes + 7) // 8 * 8
+        return out
+
+
+def _pack_commit(commit: Commit, arena: _Arena | None = None):
     sigs = commit.signatures
     n = len(sigs)
     flags = np.array([s.block_id_flag for s in sigs] + [0], np.uint8)
@@ -233,6 +248,8 @@ def _pack_commit(commit: Commit):
     so = np.zeros(n + 1, np.uint32)
     if n:
         so[1:] = np.cumsum([len(s.signature) for s in sigs])
+    if arena is not None:  # per commit flags | secs | nanos | sig_off | sigs, as INTEGRATION.md's arena
+        flags, ts_s, ts_n, so, sb = (arena.put(x) for x in (flags, ts_s, ts_n, so, sb))
     addrs = b"".join((s.validator_address + bytes(20))[:20] for s in sigs)
     ad = np.frombuffer(addrs + b"\0", np.uint8).copy()
     bid, keep = commit.block_id._c()
@@ -306,16 +323,25 @@ class PackedCommits:
     """The C arguments of one cmtv_verify_commits call, packed once (what a
     cgo shim holds when it calls the library); verify() makes the call."""
 
-    def __init__(self, kind: int, chain_id: str, items, mode: int = MODE_GO_STDLIB, trust_level=(1, 3)):
+    def __init__(self, kind: int, chain_id: str, items, mode: int = MODE_GO_STDLIB, trust_level=(1, 3),
+                 pinned: Context | None = None):
+        """pinned: the commits' arrays in one cmtv_alloc_pinned block of that
+        context (the direct, zero-copy chunks of cmtv_verify_commits there)."""
         n = len(items)
         keep = []
+        arena = None
+        if pinned is not None:
+            nb = 4096 + sum(80 + 24 * (len(c.signatures) + 1) + sum(len(s.signature) for s in c.signatures)
+                            for _, _, _, c in items)
+            self.block = pinned.alloc_pinned(nb)
+            arena = _Arena(self.block)
         vs_arr = (N.cmtv_valset * n)()
         cm_arr = (N.cmtv_commit * n)()
         bid_arr = (N.cmtv_block_id * n)()
         heights = (ctypes.c_int64 * n)()
         for c, (vals, block_id, height, commit) in enumerate(items):
             vs, kv = vals._pack()
-            cm, kc = _pack_commit(commit)
+            cm, kc = _pack_commit(commit, arena)
             vs_arr[c], cm_arr[c] = vs, cm
             keep += [kv, kc]
             if block_id is not None:

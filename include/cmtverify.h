@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define CMTV_ABI_VERSION 10
+#define CMTV_ABI_VERSION 11
 
 enum {
   CMTV_OK = 0,
@@ -110,6 +110,9 @@ typedef struct cmtv_stats {
                               off the row kernel's completion flag, without
                               waiting for the kernel to retire
                               (CMTV_HOST_POLL)                           */
+  uint64_t direct_chunks;    /* cross-height pipeline chunks DMA'd straight
+                              from the caller's cmtv_alloc_pinned memory (no
+                              host pack per signature)                   */
 } cmtv_stats;
 
 /* One device's share of the context's work (cmtv_device_stats_get). */
@@ -459,6 +462,24 @@ int cmtv_verify_commits(cmtv_ctx* ctx, uint32_t kind, uint32_t mode, const char*
                         size_t n, const cmtv_valset* vals, const cmtv_block_id* block_ids, const int64_t* heights,
                         const cmtv_commit* commits, uint64_t trust_num, uint64_t trust_den,
                         cmtv_commit_result* results, int* rcs, char* msg_bufs, size_t msg_cap);
+
+/* Pinned host memory for the caller's argument arena (the
+ * zero-copy boundary). A cgo shim that builds its cmtv_verify_commits
+ * arguments -- each commit's flags, ts_seconds, ts_nanos and signatures -- in
+ * a block from cmtv_alloc_pinned lets the cross-height pipeline DMA them
+ * straight to every device of the context: no host copy per signature
+ * (cmtv_stats.direct_chunks counts such chunks). It applies to commits whose
+ * reference loop reaches a prefix of their signatures (VerifyCommit: no
+ * absent or unknown flags; VerifyCommitLight: no nil vote before +2/3), with
+ * 64-byte signatures back to back and the registered-key cache on; any other
+ * commit is packed as before, with identical outcomes. The block is
+ * page-locked and portable to every device; the caller owns it, the library
+ * reads it during calls only. Free it with cmtv_free_pinned on the same
+ * context, never while a call that reads it runs (cmtv_close frees what is
+ * left). Replaces: nothing in the reference (Go memory); INTEGRATION.md 4c
+ * builds the blocksync window's arena in it. */
+int cmtv_alloc_pinned(cmtv_ctx* ctx, size_t bytes, void** out);
+int cmtv_free_pinned(cmtv_ctx* ctx, void* p);
 
 /* CanonicalVote sign-bytes (types/vote.go:93 VoteSignBytes) for a commit
  * signature: writes up to cap bytes, returns the length (or negative code). */

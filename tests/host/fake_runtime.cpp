@@ -37,6 +37,7 @@ struct FakeSlot {
   const cmtv_keyset* ks = nullptr;
   uint32_t mode = 0;
   bool pending = false;
+  uint64_t gathered_bytes = 0;  // a direct chunk's message bytes (bulk_gather)
 };
 
 struct cmtv_keyset {
@@ -57,12 +58,19 @@ struct cmtv_ctx {
   size_t n_devs = 1;
   std::vector<std::vector<FakeSlot>> slots;  // [dev][slot]
   long fail_dev = -1;                        // bulk_wait on this device fails once
+  // bulk_wait on this device finds it retired by another call meanwhile (out
+  // of live, failed) and fails, once (the pipeline must run on)
+  long ext_retire_dev = -1;
+  std::vector<bool> failed;
   bool noverify = false;
   uint64_t phase_ns[cmtv::kPhCount] = {};
   cmtv::PipeWorkspace* ws = nullptr;                     // pipebench: every verdict valid, nothing decoded
   uint64_t signatures = 0, invalid = 0, chunks = 0, retired = 0, keyed_chunks = 0;
   std::map<std::string, uint8_t> memo;       // (mode, pk, sig, msg) -> verdict
   std::mutex memo_mu;
+  std::map<uintptr_t, size_t> pinned;        // cmtv_alloc_pinned blocks
+  uint64_t direct_chunks = 0;
+  bool keyset_fail = false;  // registration fails (the pipeline packs direct chunks after all)
 };
 
 namespace {
@@ -188,7 +196,7 @@ int verify_templated_locked(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const ui
 }
 
 const cmtv_keyset* keyset_for_locked(cmtv_ctx* ctx, const uint8_t* pk32, size_t n_keys) {
-  if (!ctx->keyset_cap || !n_keys) return nullptr;
+  if (!ctx->keyset_cap || !n_keys || ctx->keyset_fail) return nullptr;
   std::string key(reinterpret_cast<const char*>(pk32), 32 * n_keys);
   for (auto& e : ctx->keysets)
     if (e.first == key) return e.second;
@@ -215,6 +223,7 @@ HostPool& host_pool(cmtv_ctx* ctx) {
 }
 PipeConfig pipe_config(const cmtv_ctx* ctx) { return ctx->pc; }
 int stage_sigs_early_locked(cmtv_ctx*, const uint8_t*, size_t, const uint8_t*) { return CMTV_OK; }
+void clear_early_locked(cmtv_ctx*) {}
 void live_devices_locked(cmtv_ctx* ctx, std::vector<size_t>& out) { out = ctx->live; }
 
 int bulk_stage(cmtv_ctx* ctx, size_t dev, int slot, const BulkLayout& L, uint8_t** host) {
@@ -238,7 +247,18 @@ int bulk_stage(cmtv_ctx* ctx, size_t dev, int slot, const BulkLayout& L, uint8_t
 int bulk_submit_locked(cmtv_ctx* ctx, size_t dev, int slot, const BulkLayout& L, const cmtv_keyset* ks,
                        uint32_t mode) {
   FakeSlot& S = ctx->slots[dev][slot];
+  if (ctx->failed[dev]) return CMTV_EHIP;  // retired by another call meanwhile
   if (L.in_bytes > S.h_in.size()) return CMTV_EINVAL;
+  if (L.direct) {  // the spans must lie in the caller's pinned blocks
+    for (int k = 0; k < L.n_spans; k++) {
+      const uintptr_t a = reinterpret_cast<uintptr_t>(L.spans[k].host);
+      auto it = ctx->pinned.upper_bound(a);
+      if (it == ctx->pinned.begin() || a + L.spans[k].bytes > std::prev(it)->first + std::prev(it)->second) {
+        std::fprintf(stderr, "fake: span %d outside the pinned blocks\n", k);
+        return CMTV_EINVAL;
+      }
+    }
+  }
   S.L = L;
   S.ks = ks;
   S.mode = mode;
@@ -246,6 +266,70 @@ int bulk_submit_locked(cmtv_ctx* ctx, size_t dev, int slot, const BulkLayout& L,
   ctx->chunks++;
   ctx->signatures += L.m;
   if (ks) ctx->keyed_chunks++;
+  return CMTV_OK;
+}
+
+// A direct chunk, as the device sees it (runtime.cpp bulk_submit_locked,
+// signbytes.hip k_bulk_gather / k_bulk_bases / k_bulk_rebase): the spans of
+// the caller's pinned memory copied to o_arena, then the per-signature layout
+// built from the descriptors -- into the slot's buffer, grown to dev_bytes,
+// so the packed-chunk reader below checks it the same way.
+int bulk_gather(FakeSlot& S) {
+  const BulkLayout& L = S.L;
+  if (!S.ks || !L.keyed) {
+    std::fprintf(stderr, "fake: a direct chunk without registered keys\n");
+    return CMTV_EINVAL;
+  }
+  S.h_in.resize(L.dev_bytes, 0xA5);
+  uint8_t* h = S.h_in.data();
+  uint8_t* arena = h + L.o_arena;
+  for (int k = 0; k < L.n_spans; k++) {
+    const BulkSpan& sp = L.spans[k];
+    if (sp.dev_off + sp.bytes > L.arena_bytes || (sp.dev_off & 255) != (reinterpret_cast<uintptr_t>(sp.host) & 255)) {
+      std::fprintf(stderr, "fake: span %d out of the arena or misaligned\n", k);
+      return CMTV_EINVAL;
+    }
+    std::memcpy(arena + sp.dev_off, sp.host, sp.bytes);
+  }
+  const auto* desc = reinterpret_cast<const BulkDesc*>(h + L.o_desc);
+  const auto* tmpls = reinterpret_cast<const SbTemplate*>(h + L.o_tmpl);
+  auto* kidx = reinterpret_cast<uint32_t*>(h + L.o_key);
+  auto* off = reinterpret_cast<uint32_t*>(h + L.o_off);
+  auto* tidx = reinterpret_cast<uint32_t*>(h + L.o_tidx);
+  auto* sec = reinterpret_cast<int64_t*>(h + L.o_sec);
+  auto* nanos = reinterpret_cast<int32_t*>(h + L.o_nanos);
+  uint64_t o = 0, covered = 0;
+  for (size_t c = 0; c < L.n_tmpls; c++) {
+    const BulkDesc& D = desc[c];
+    if (!D.m) continue;
+    // the kernel's aligned loads, and every signature once, in order
+    if ((D.sig & 7) || (D.sec & 7) || (D.nanos & 3) || D.sp != covered || D.sp + D.m > L.m ||
+        D.sig + 64ull * D.m > L.arena_bytes || D.sec + 8ull * D.m > L.arena_bytes ||
+        D.nanos + 4ull * D.m > L.arena_bytes || D.flags + D.m > L.arena_bytes) {
+      std::fprintf(stderr, "fake: bad descriptor %zu\n", c);
+      return CMTV_EINVAL;
+    }
+    covered += D.m;
+    for (uint32_t k = 0; k < D.m; k++) {
+      const size_t i = D.sp + k;
+      const bool fb = arena[D.flags + k] == 2;
+      std::memcpy(h + L.o_sig + 64 * i, arena + D.sig + 64ull * k, 64);
+      std::memcpy(&sec[i], arena + D.sec + 8ull * k, 8);
+      std::memcpy(&nanos[i], arena + D.nanos + 4ull * k, 4);
+      h[L.o_flag + i] = fb ? 1 : 0;
+      tidx[i] = (uint32_t)c;
+      kidx[i] = k;
+      off[i] = (uint32_t)o;
+      o += sb_msg_len(tmpls[c], fb, sec[i], nanos[i]);
+    }
+  }
+  if (covered != L.m || o > L.msg_bytes) {
+    std::fprintf(stderr, "fake: direct chunk covers %llu of %zu signatures, %llu message bytes (bound %llu)\n",
+                 (unsigned long long)covered, L.m, (unsigned long long)o, (unsigned long long)L.msg_bytes);
+    return CMTV_EINVAL;
+  }
+  off[L.m] = (uint32_t)o;
+  S.gathered_bytes = o;
   return CMTV_OK;
 }
 
@@ -257,13 +341,23 @@ int bulk_wait(cmtv_ctx* ctx, size_t dev, int slot, const uint64_t** bitmap) {
     ctx->fail_dev = -1;
     return CMTV_EHIP;
   }
+  if ((long)dev == ctx->ext_retire_dev) {
+    std::lock_guard<std::mutex> g(ctx->mu);  // as the other call would
+    ctx->ext_retire_dev = -1;
+    ctx->failed[dev] = true;
+    for (size_t i = 0; i < ctx->live.size(); i++)
+      if (ctx->live[i] == dev) ctx->live.erase(ctx->live.begin() + (long)i);
+    ctx->retired++;
+    return CMTV_EHIP;
+  }
   const BulkLayout& L = S.L;
-  const uint8_t* h = S.h_in.data();
   if (ctx->noverify) {
     S.bm.assign((L.m + 63) / 64 + 1, ~0ull);
     *bitmap = S.bm.data();
     return CMTV_OK;
   }
+  if (L.direct && bulk_gather(S) != CMTV_OK) return CMTV_EINVAL;
+  const uint8_t* h = S.h_in.data();
   std::vector<uint8_t> v(L.m);
   const int rc = device_verify(ctx, L.m, h + L.o_key, L.keyed, S.ks, h + L.o_sig,
                                reinterpret_cast<const uint32_t*>(h + L.o_off),
@@ -273,7 +367,7 @@ int bulk_wait(cmtv_ctx* ctx, size_t dev, int slot, const uint64_t** bitmap) {
                                reinterpret_cast<const int32_t*>(h + L.o_nanos), S.mode, v.data());
   if (rc != CMTV_OK) return rc;
   const uint32_t* off = reinterpret_cast<const uint32_t*>(h + L.o_off);
-  if (off[0] != 0 || off[L.m] != L.msg_bytes) {
+  if (off[0] != 0 || off[L.m] != (L.direct ? S.gathered_bytes : L.msg_bytes)) {
     std::fprintf(stderr, "fake: offsets [%u, %u] vs %llu message bytes\n", off[0], off[L.m],
                  (unsigned long long)L.msg_bytes);
     return CMTV_EINVAL;
@@ -294,7 +388,9 @@ void bulk_drain(cmtv_ctx* ctx) {
 }
 
 bool retire_device_locked(cmtv_ctx* ctx, size_t dev) {
+  if (ctx->failed[dev]) return !ctx->live.empty();  // as runtime.cpp
   if (ctx->live.size() < 2) return false;
+  ctx->failed[dev] = true;
   for (size_t i = 0; i < ctx->live.size(); i++)
     if (ctx->live[i] == dev) {
       ctx->live.erase(ctx->live.begin() + (long)i);
@@ -305,6 +401,11 @@ bool retire_device_locked(cmtv_ctx* ctx, size_t dev) {
 }
 
 void count_invalid_locked(cmtv_ctx* ctx, uint64_t n) { ctx->invalid += n; }
+void count_direct_locked(cmtv_ctx* ctx) { ctx->direct_chunks++; }
+void pinned_ranges_locked(cmtv_ctx* ctx, std::vector<PinnedRange>& out) {
+  out.clear();
+  for (auto& b : ctx->pinned) out.push_back(PinnedRange{b.first, b.second});
+}
 PipeWorkspace*& pipe_workspace(cmtv_ctx* ctx) { return ctx->ws; }
 
 }  // namespace cmtv
@@ -320,7 +421,34 @@ extern "C" cmtv_ctx* fake_open(size_t n_devs, unsigned threads, size_t pipe_min,
   c->fail_dev = fail_dev;
   for (size_t d = 0; d < n_devs; d++) c->live.push_back(d);
   c->slots.assign(n_devs, std::vector<FakeSlot>(cmtv::kBulkSlotsMax));
+  c->failed.assign(n_devs, false);
   return c;
+}
+
+extern "C" void fake_set_ext_retire(cmtv_ctx* c, long dev) { c->ext_retire_dev = dev; }
+extern "C" void fake_set_direct(cmtv_ctx* c, bool on) { c->pc.direct = on; }
+extern "C" void fake_set_keyset_fail(cmtv_ctx* c, bool on) { c->keyset_fail = on; }
+
+// the ABI's pinned blocks (plain page-aligned memory here)
+extern "C" int cmtv_alloc_pinned(cmtv_ctx* ctx, size_t bytes, void** out) {
+  if (!ctx || !out || !bytes) return CMTV_EINVAL;
+  void* p = std::aligned_alloc(4096, (bytes + 4095) / 4096 * 4096);
+  if (!p) return CMTV_ENOMEM;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  ctx->pinned.emplace(reinterpret_cast<uintptr_t>(p), bytes);
+  *out = p;
+  return CMTV_OK;
+}
+
+extern "C" int cmtv_free_pinned(cmtv_ctx* ctx, void* p) {
+  if (!ctx) return CMTV_EINVAL;
+  if (!p) return CMTV_OK;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  auto it = ctx->pinned.find(reinterpret_cast<uintptr_t>(p));
+  if (it == ctx->pinned.end()) return CMTV_EINVAL;
+  ctx->pinned.erase(it);
+  std::free(p);
+  return CMTV_OK;
 }
 
 extern "C" void fake_phases(cmtv_ctx* c, uint64_t* out) {
@@ -335,9 +463,11 @@ extern "C" void fake_counts(cmtv_ctx* c, uint64_t* out) {
   out[2] = c->chunks;
   out[3] = c->retired;
   out[4] = c->keyed_chunks;
+  out[5] = c->direct_chunks;
 }
 
 extern "C" void fake_close(cmtv_ctx* c) {
+  for (auto& b : c->pinned) std::free(reinterpret_cast<void*>(b.first));
   for (auto& e : c->keysets) delete e.second;
   for (auto* k : c->evicted) delete k;
   cmtv::pipe_workspace_free(c->ws);

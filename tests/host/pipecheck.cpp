@@ -31,6 +31,9 @@ void oracle_sign(const uint8_t seed[32], const uint8_t* msg, size_t mlen, uint8_
 cmtv_ctx* fake_open(size_t n_devs, unsigned threads, size_t pipe_min, size_t chunk, int slots, bool pipe_on,
                     size_t keyset_cap, long fail_dev);
 void fake_counts(cmtv_ctx* c, uint64_t* out);
+void fake_set_ext_retire(cmtv_ctx* c, long dev);
+void fake_set_direct(cmtv_ctx* c, bool on);
+void fake_set_keyset_fail(cmtv_ctx* c, bool on);
 void fake_close(cmtv_ctx* c);
 }
 
@@ -271,18 +274,64 @@ struct Run {
 
 constexpr size_t kCap = 1024;
 
+// Where the caller's commit arrays live (cmtv_alloc_pinned: the direct
+// chunks' DMA source, pipeline.cpp):
+//   kHeap         the CommitData vectors themselves (packed chunks only)
+//   kInterleaved  one pinned block, per commit flags | secs | nanos | sig_off |
+//                 sigs (the Go shim's arena)
+//   kClasses      one pinned block, all flags, then all secs, nanos, sigs
+//   kMisaligned   interleaved, every third commit's signatures 4 bytes off
+//                 (not direct: the kernel loads 8-byte words)
+enum Layout { kHeap, kInterleaved, kClassArrays, kMisaligned };
+
+std::vector<cmtv_commit> place(cmtv_ctx* ctx, const std::vector<CommitData>& chain, Layout lay) {
+  std::vector<cmtv_commit> cs;
+  for (auto& d : chain) cs.push_back(d.c);
+  if (lay == kHeap) return cs;
+  size_t bytes = 4096;
+  for (auto& d : chain) bytes += 64 + d.flags.size() + 8 * d.sec.size() + 4 * d.nanos.size() + 4 * d.sig_off.size() +
+                                 d.sigs.size() + 64;
+  uint8_t* blk = nullptr;
+  if (cmtv_alloc_pinned(ctx, bytes, reinterpret_cast<void**>(&blk)) != CMTV_OK) {
+    std::fprintf(stderr, "cmtv_alloc_pinned failed\n");
+    std::exit(2);
+  }
+  size_t at = 0;
+  auto put = [&](const void* src, size_t len, size_t align, size_t skew = 0) {
+    at = (at + align - 1) / align * align + skew;
+    std::memcpy(blk + at, src, len);
+    const uint8_t* p = blk + at;
+    at += len;
+    return p;
+  };
+  for (int pass = 0; pass < (lay == kClassArrays ? 4 : 1); pass++)
+    for (size_t i = 0; i < chain.size(); i++) {
+      const CommitData& d = chain[i];
+      cmtv_commit& c = cs[i];
+      const size_t n = d.sec.size();
+      auto cls = [&](int k) { return lay != kClassArrays || pass == k; };
+      if (cls(0)) c.flags = put(d.flags.data(), d.flags.size(), 1);
+      if (cls(1)) c.ts_seconds = reinterpret_cast<const int64_t*>(put(d.sec.data(), 8 * n, 8));
+      if (cls(2)) c.ts_nanos = reinterpret_cast<const int32_t*>(put(d.nanos.data(), 4 * n, 4));
+      if (cls(3)) {
+        c.sig_off = reinterpret_cast<const uint32_t*>(put(d.sig_off.data(), 4 * d.sig_off.size(), 4));
+        c.sigs = put(d.sigs.data(), d.sigs.size(), 8, lay == kMisaligned && i % 3 == 0 ? 4 : 0);
+      }
+    }
+  return cs;
+}
+
 Run run(cmtv_ctx* ctx, uint32_t kind, uint32_t mode, const std::vector<CommitData>& chain,
-        const std::vector<const VSet*>& vals_of) {
+        const std::vector<const VSet*>& vals_of, Layout lay = kHeap) {
   const size_t n = chain.size();
   std::vector<cmtv_valset> vs(n);
   std::vector<cmtv_block_id> bids(n);
   std::vector<int64_t> hs(n);
-  std::vector<cmtv_commit> cs(n);
+  const std::vector<cmtv_commit> cs = place(ctx, chain, lay);
   for (size_t i = 0; i < n; i++) {
     vs[i] = vals_of[i]->vs;
     bids[i] = chain[i].want;
     hs[i] = chain[i].height;
-    cs[i] = chain[i].c;
   }
   Run r;
   r.rcs.assign(n, 99);
@@ -370,12 +419,23 @@ int main(int argc, char** argv) {
     int slots;
     size_t keys;
     long fail_dev;
+    long ext_retire = -1;  // retired by "another call" while a chunk is in flight
+    Layout lay = kHeap;
+    bool direct = true;       // CMTV_PIPE_DIRECT
+    bool keyset_fail = false;
   };
   const Cfg cfgs[] = {
       {"pipe chunk 1000", 1, 4, 1000, 3, 0, -1},   {"pipe chunk 7", 1, 3, 7, 2, 0, -1},
       {"pipe keyed 64", 1, 8, 64, 2, 4, -1},       {"pipe keyed 1 thread", 1, 1, 200, 3, 4, -1},
       {"pipe 3 devs keyed", 3, 4, 50, 4, 1, -1},   {"pipe 3 devs fail", 3, 2, 80, 2, 4, 1},
-      {"pipe keyed cap 1", 2, 5, 30, 3, 1, -1},
+      {"pipe keyed cap 1", 2, 5, 30, 3, 1, -1},    {"pipe 2 devs retired elsewhere", 2, 3, 40, 2, 4, -1, 1},
+      {"direct interleaved", 1, 4, 100, 3, 4, -1, -1, kInterleaved},
+      {"direct classes 2 devs", 2, 4, 64, 2, 4, -1, -1, kClassArrays},
+      {"direct misaligned", 1, 3, 50, 2, 4, -1, -1, kMisaligned},
+      {"direct 3 devs fail", 3, 2, 80, 2, 4, 1, -1, kInterleaved},
+      {"direct big chunks", 2, 8, 4000, 3, 1, -1, -1, kClassArrays},
+      {"direct off, pinned", 1, 4, 100, 3, 4, -1, -1, kInterleaved, false},
+      {"direct, keys unregistered", 1, 4, 100, 3, 4, -1, -1, kInterleaved, true, true},
   };
   size_t checked = 0;
   for (uint32_t kind = 0; kind < 3; kind++) {
@@ -392,17 +452,27 @@ int main(int argc, char** argv) {
       fake_close(onek);
       for (const Cfg& c : cfgs) {
         cmtv_ctx* ctx = fake_open(c.devs, c.threads, 1, c.chunk, c.slots, true, c.keys, c.fail_dev);
-        const Run r = run(ctx, kind, mode, chain, vals_of);
-        uint64_t cnt[5];
+        fake_set_ext_retire(ctx, c.ext_retire);
+        fake_set_direct(ctx, c.direct);
+        fake_set_keyset_fail(ctx, c.keyset_fail);
+        const Run r = run(ctx, kind, mode, chain, vals_of, c.lay);
+        uint64_t cnt[6];
         fake_counts(ctx, cnt);
         fake_close(ctx);
         expect_same(c.name, base, r);
         expect_same_as_ref(c.name, kind, r, ref);
-        if (c.fail_dev >= 0 && cnt[3] != 1) {
+        if ((c.fail_dev >= 0 || c.ext_retire >= 0) && cnt[3] != 1) {
           std::fprintf(stderr, "%s: expected one device retired, got %llu\n", c.name, (unsigned long long)cnt[3]);
           g_fail++;
         }
-        if (c.keys && !cnt[4]) {
+        // direct chunks exactly where they can run (not LightTrusting: its
+        // plan maps through addresses)
+        const bool want_direct = c.lay != kHeap && c.direct && !c.keyset_fail && c.keys && kind != 2;
+        if (want_direct != (cnt[5] > 0)) {
+          std::fprintf(stderr, "%s kind %u: %llu direct chunks\n", c.name, kind, (unsigned long long)cnt[5]);
+          g_fail++;
+        }
+        if (c.keys && !c.keyset_fail && !cnt[4]) {
           std::fprintf(stderr, "%s: no chunk used registered keys\n", c.name);
           g_fail++;
         }

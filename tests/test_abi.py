@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_strerror():
     lib = N.lib()
-    assert lib.cmtv_abi_version() == 10
+    assert lib.cmtv_abi_version() == 11
     for code in (N.CMTV_OK, N.CMTV_EINVAL, N.CMTV_ENODEV, N.CMTV_ENOMEM, N.CMTV_EHIP, N.CMTV_ERCCL, N.CMTV_ECOMMIT):
         assert lib.cmtv_strerror(code)
 

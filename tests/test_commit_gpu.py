@@ -300,3 +300,65 @@ def test_device_sign_bytes_templating(monkeypatch, chain, fuse):
         st = kc.stats()
         assert st["keyed_launches"] > 0
         assert (st["fused_sign_bytes"] > 0) == (fuse and len(chain) <= 50), st["fused_sign_bytes"]
+
+
+@pytest.mark.parametrize("keyed", [True, False])
+def test_early_staged_signatures_never_go_stale(keyed):
+    """a single-commit VerifyCommit copies its signatures to
+    the device before planning (stage_sigs_early_locked). When it stops
+    before any batch runs (here: a wrong height), those device bytes must not
+    be taken for the next call's, even if that call passes the SAME buffer
+    with new contents -- as the Go binding's reused arena does. The next call
+    (cmtv_verify_commits with one commit, and cmtv_verify_commit itself) must
+    verify the bytes it is given now."""
+    import ctypes
+
+    from cometbft_amd import Context
+    from cometbft_amd import _native as N
+    from cometbft_amd import testutil as TU
+
+    ctx = Context(device=0)
+    if keyed:
+        ctx.keyset_cache(4)  # keyed quad kernel at 1,000 validators
+    n = 1000 if keyed else 2000  # past the row bands, where the early copy runs
+    sv = TU.make_validator_set(ctx, n)
+    h = 91
+    commit, _, _ = TU.make_commit(ctx, sv, height=h)
+    bid = TU.block_id_for_height(h)
+    vs, keep_v = sv.valset._pack()
+    cm, keep_c = T._pack_commit(commit)
+    sb = keep_c[3]  # the signatures' buffer, reused below at the same address
+    b, keep_b = bid._c()
+    cid = TU.CHAIN_ID.encode()
+
+    def single(height):
+        res = N.cmtv_commit_result()
+        buf = ctypes.create_string_buffer(1024)
+        rc = N.lib().cmtv_verify_commit(ctx.handle, N.VERIFY_COMMIT, 0, cid, len(cid), ctypes.byref(vs),
+                                        ctypes.byref(b), height, ctypes.byref(cm), 0, 0, ctypes.byref(res), buf,
+                                        len(buf))
+        return rc, res
+
+    def many():
+        res = (N.cmtv_commit_result * 1)()
+        rcs = (ctypes.c_int * 1)()
+        bufs = ctypes.create_string_buffer(1024)
+        vsa, cma, bida, hs = (N.cmtv_valset * 1)(vs), (N.cmtv_commit * 1)(cm), (N.cmtv_block_id * 1)(b), \
+            (ctypes.c_int64 * 1)(h)
+        rc = N.lib().cmtv_verify_commits(ctx.handle, N.VERIFY_COMMIT, 0, cid, len(cid), 1, vsa, bida, hs, cma, 0, 0,
+                                         res, rcs, bufs, 1024)
+        assert rc == N.CMTV_OK
+        return rcs[0], res[0]
+
+    assert single(h)[0] == N.CMTV_OK  # the honest commit
+    for bad, call in ((437, many), (611, lambda: single(h))):
+        rc, _ = single(h + 1)  # stages the honest bytes, then fails its preamble
+        assert rc != N.CMTV_OK
+        saved = sb[64 * bad + 5]
+        sb[64 * bad + 5] ^= 0x40  # the same buffer now holds a corrupted signature
+        rc, res = call()
+        assert rc != N.CMTV_OK and res.code == N.COMMIT_ERR_WRONG_SIGNATURE and res.sig_index == bad, \
+            (rc, res.code, res.sig_index)
+        sb[64 * bad + 5] = saved
+        assert single(h)[0] == N.CMTV_OK
+    del keep_v, keep_b

@@ -9,8 +9,9 @@ restatement of Go 1.19 ed25519.Verify (oracle/cmtv_oracle.c), lazily, when
 the chunk is waited for. A 240-commit chain with assorted faults over four
 validator sets (one with a 31-byte key) goes through the reference loops
 written out from types/validator_set.go:667-826, the one-batch path and the
-pipeline in seven configurations (chunks of 7 to 1000 signatures, 2-4
-slots, 1-8 threads, 1-3 devices, registered keys, a device failing mid-call);
+pipeline in eight configurations (chunks of 7 to 1000 signatures, 2-4
+slots, 1-8 threads, 1-3 devices, registered keys, a device failing mid-call,
+a device retired by another call while a chunk is in flight on it);
 every commit's outcome must agree."""
 import os
 import subprocess
@@ -61,6 +62,6 @@ def test_pipeline_host_logic_matches_reference_loops():
                        env={**os.environ, "ASAN_OPTIONS": "detect_leaks=1:halt_on_error=1",
                             "UBSAN_OPTIONS": "halt_on_error=1:print_stacktrace=1"})
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
-    assert "pipecheck ok (28 runs)" in r.stdout
+    assert "pipecheck ok (60 runs)" in r.stdout
     for kind in (0, 1, 2):
         assert f"kind {kind} mode 0: 240 commits" in r.stdout

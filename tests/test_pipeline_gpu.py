@@ -231,3 +231,52 @@ def test_configs2_scale_generic_and_zip215(c3_chain):
     _check_chain(chain, N.VERIFY_COMMIT)
     c.close()
     k.close()
+
+
+@pytest.mark.parametrize("kind", [N.VERIFY_COMMIT, N.VERIFY_COMMIT_LIGHT, N.VERIFY_COMMIT_LIGHT_TRUSTING])
+def test_direct_chunks_match_one_batch(faulty_chain, kind):
+    """The commits' arrays in the context's cmtv_alloc_pinned memory (the Go
+    shim's arena): commits whose plan is a prefix go to the
+    device by DMA and k_bulk_gather lays them out (direct chunks), the others
+    are packed as before; every outcome is byte-identical to the one-batch
+    path. LightTrusting maps through addresses and never goes direct."""
+    one = _ctx(CMTV_PIPELINE=0)
+    pc = T.PackedCommits(kind, TU.CHAIN_ID, faulty_chain, trust_level=(1, 3))
+    pc.call(one)
+    want = _raw(pc)
+    for devices, chunk in ((None, 3000), ([0, 0, 0], 700), (None, 64)):
+        c = _ctx(devices=devices, keyset=True, CMTV_PIPE_MIN=1, CMTV_PIPE_CHUNK=chunk, CMTV_HOST_THREADS=4)
+        pp = T.PackedCommits(kind, TU.CHAIN_ID, faulty_chain, trust_level=(1, 3), pinned=c)
+        pp.call(c)
+        assert _raw(pp) == want
+        direct = c.stats()["direct_chunks"]
+        assert (direct > 0) == (kind != N.VERIFY_COMMIT_LIGHT_TRUSTING), direct
+        c.close()
+    one.close()
+
+
+@pytest.mark.parametrize("devices", [None, [0, 0, 0, 0]])
+def test_configs2_scale_direct_from_pinned(gpu_ctx, devices):
+    """configs[2]'s chain (7,000 heights x 150, 1% flipped) built in the
+    context's pinned memory: every chunk is direct (no host pack), verified
+    by the same keyed kernels, and each height's outcome is the reference
+    loop's over the known flips, both kinds."""
+    c = _ctx(devices=devices, keyset=True)
+    sv = TU.make_validator_set(c, N_VALS)
+    chain = TU.ReplayChain(c, sv, 1, 7000, pinned=c)
+    for kind in (N.VERIFY_COMMIT, N.VERIFY_COMMIT_LIGHT):
+        st0 = c.stats()
+        chain.call(c, kind)
+        _check_chain(chain, kind)
+        st = c.stats()
+        reach = N_VALS if kind == N.VERIFY_COMMIT else (N_VALS * 10 * 2 // 3) // 10 + 1
+        assert st["signatures"] - st0["signatures"] == chain.n_heights * reach
+        assert st["direct_chunks"] > st0["direct_chunks"]
+    # the same bytes packed (CMTV_PIPE_DIRECT=0) give the same outcomes
+    p = _ctx(devices=devices, keyset=True, CMTV_PIPE_DIRECT=0)
+    chain.call(p, N.VERIFY_COMMIT)
+    _check_chain(chain, N.VERIFY_COMMIT)
+    assert p.stats()["direct_chunks"] == 0
+    p.close()
+    del chain
+    c.close()

@@ -727,6 +727,7 @@ static int cmtv_verify_commit_impl(cmtv_ctx* ctx, uint32_t kind, uint32_t mode, 
     J.addr = &addr;
   }
   thread_local Seen seen;
+  cmtv::note_latency(ctx);  // a consensus-path call: pipelines leave it CUs
   std::unique_lock<std::mutex> lk;
   rc = cmtv::ctx_lock(ctx, lk);
   if (rc != CMTV_OK) return rc;
@@ -786,6 +787,7 @@ static int cmtv_verify_commits_impl(cmtv_ctx* ctx, uint32_t kind, uint32_t mode,
   // large calls: the chunked pipeline (plan / pack / replay on the host
   // workers, per-device lanes; the context lock only around submissions)
   if (cmtv::pipeline_wanted(ctx, n_sigs)) return cmtv::verify_commits_pipeline(ctx, args, rcs);
+  if (n_sigs <= 4096) cmtv::note_latency(ctx);  // a small call waits on its verdicts
   std::vector<CommitJob> jobs;
   jobs.reserve(n);
   for (size_t c = 0; c < n; c++) jobs.push_back(args.job(c));

@@ -121,6 +121,27 @@ inline size_t put_commit_template(uint8_t* blob, size_t at, const char* chain_id
   return w.n;
 }
 
+// put_commit_template's lengths without writing or counting byte by byte:
+// the pre(Commit), pre(Nil) and chain-id field lengths; returns their sum
+// (the template's blob bytes). The same numbers as put_commit_template's
+// (tests/host/pipecheck.cpp compares them on every commit it plans).
+inline size_t commit_template_lens(size_t chain_id_len, const cmtv_commit* c, uint32_t* pre_commit,
+                                   uint32_t* pre_nil, uint32_t* post) {
+  const cmtv_block_id* b = &c->block_id;
+  const size_t base = 2 + (c->height != 0 ? 9 : 0) + (c->round != 0 ? 9 : 0);  // type, height, round
+  size_t bid = 0;
+  if (!block_id_is_zero(b)) {
+    const size_t psh = (b->psh_total ? 1 + sb_uvlen(b->psh_total) : 0) +
+                       (b->psh_hash_len ? 1 + sb_uvlen(b->psh_hash_len) + b->psh_hash_len : 0);
+    const size_t cb = (b->hash_len ? 1 + sb_uvlen(b->hash_len) + b->hash_len : 0) + 1 + sb_uvlen(psh) + psh;
+    bid = 1 + sb_uvlen(cb) + cb;
+  }
+  *pre_commit = (uint32_t)(base + bid);
+  *pre_nil = (uint32_t)base;
+  *post = (uint32_t)(chain_id_len ? 1 + sb_uvlen(chain_id_len) + chain_id_len : 0);
+  return *pre_commit + *pre_nil + *post;
+}
+
 // sb_msg_len (signbytes.h) without loops or tables: a varint's length is
 // ceil(bits / 7) (at least 1), and (bits + 6) / 7 == ((bits + 6) * 37) >> 8
 // for every bits in 1..64 (checked exhaustively by tests/test_pipeline_cpu.py's

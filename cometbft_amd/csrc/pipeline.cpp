@@ -485,9 +485,9 @@ int run_pipeline(cmtv_ctx* ctx, const CommitsArgs& args, int* rcs, std::vector<c
         if (b < 0 || (blk != UINT32_MAX && (uint32_t)b != blk)) return false;
         blk = (uint32_t)b;
       }
-      SbTemplate tpl;
-      tlen[c] = (uint32_t)put_commit_template(nullptr, 0, J.chain_id, J.chain_id_len, cm, &tpl);
-      mbytes[c] = (uint64_t)m * msg_len_bound(TplLens{tpl.pre_commit_len, tpl.pre_nil_len, tpl.post_len});
+      TplLens tl;
+      tlen[c] = (uint32_t)commit_template_lens(J.chain_id_len, cm, &tl.pre_commit, &tl.pre_nil, &tl.post);
+      mbytes[c] = (uint64_t)m * msg_len_bound(tl);
     }
     plen[c] = m;
     W.direct[c] = 1;
@@ -528,9 +528,9 @@ int run_pipeline(cmtv_ctx* ctx, const CommitsArgs& args, int* rcs, std::vector<c
         const size_t m = job_plan(J, pi, trusting ? pval_p + base[c] : nullptr, seen);
         plen[c] = (uint32_t)m;
         if (!m) continue;
-        SbTemplate tpl;
-        tlen[c] = (uint32_t)put_commit_template(nullptr, 0, J.chain_id, J.chain_id_len, J.commit, &tpl);
-        mbytes[c] = exact_mbytes(J, pi, m, TplLens{tpl.pre_commit_len, tpl.pre_nil_len, tpl.post_len});
+        TplLens tl;
+        tlen[c] = (uint32_t)commit_template_lens(J.chain_id_len, J.commit, &tl.pre_commit, &tl.pre_nil, &tl.post);
+        mbytes[c] = exact_mbytes(J, pi, m, tl);
       }
     });
     planned_upto = b;
@@ -594,6 +594,10 @@ int run_pipeline(cmtv_ctx* ctx, const CommitsArgs& args, int* rcs, std::vector<c
     if (ramp && chunks.size() < 3) want = std::max<uint64_t>(per >> ramp_sh[chunks.size()], 1);
     Chunk ch;
     ch.c0 = cursor;
+    // near a latency call the chunk runs on the CU-masked lane: no more than
+    // one round of the CUs it keeps
+    ch.L.masked = latency_recent(ctx);
+    if (ch.L.masked) want = std::min<uint64_t>(want, pc.chunk_masked);
     bool cls_set = false;
     // direct class: the pinned block of a direct chunk's commits, -1 for a
     // packed chunk (a chunk is one or the other)
@@ -602,8 +606,10 @@ int run_pipeline(cmtv_ctx* ctx, const CommitsArgs& args, int* rcs, std::vector<c
     uint64_t s = 0, mb = 0, tb = 0;
     size_t c = cursor;
     for (; c < n; c++) {
-      if (c == planned_upto) plan_window(std::max<uint64_t>(want - std::min(want, s), 65536));
-      SpanAcc nx;
+      // plan a chunk's worth at a time: each window is one parallel_for (a
+      // wake-up of every worker), so windows of 64k signatures cost ~230
+      // wake-ups per 15M-signature call
+      if (c == planned_upto) plan_window(std::max<uint64_t>(want - std::min(want, s), std::max<uint64_t>(pc.chunk, 65536)));
       const bool dir = plen[c] && W.direct[c];
       if (plen[c]) {
         const long dc = dir ? (long)W.pblock[c] : -1;
@@ -611,15 +617,6 @@ int run_pipeline(cmtv_ctx* ctx, const CommitsArgs& args, int* rcs, std::vector<c
         if (!dcls_set) {
           dcls = dc;
           dcls_set = true;
-        }
-        if (dir) {
-          // a direct chunk's DMA covers its classes' extents: cut before a
-          // commit that would make it copy far more than its plans read
-          // (a caller's arrays scattered over its pinned block)
-          nx = ch.acc;
-          nx.add(&args.commits[c], plen[c]);
-          const uint64_t cap = 4 * nx.need + (64u << 20);
-          if (s && nx.sum_bytes() > cap && nx.merged_bytes() > cap) break;
         }
       }
       if (plen[c] && keyed_mode) {
@@ -642,7 +639,6 @@ int run_pipeline(cmtv_ctx* ctx, const CommitsArgs& args, int* rcs, std::vector<c
       // message offsets are 32-bit): a commit that would cross it opens the
       // next chunk
       if (s && mb + mbytes[c] >= max_mb) break;
-      if (dir) ch.acc = nx;
       sp[c] = s;
       mp[c] = mb;
       tp[c] = tb;
@@ -650,8 +646,20 @@ int run_pipeline(cmtv_ctx* ctx, const CommitsArgs& args, int* rcs, std::vector<c
       mb += mbytes[c];
       tb += tlen[c];
       if (s >= want) {
+        if (dir) ch.acc.add(&args.commits[c], plen[c]);
         c++;
         break;
+      }
+      if (dir) {
+        // a direct chunk's DMA covers its classes' extents: it ends at a
+        // commit past which it would copy far more than its plans read (a
+        // caller's arrays scattered over its pinned block)
+        ch.acc.add(&args.commits[c], plen[c]);
+        const uint64_t cap = 4 * ch.acc.need + (64u << 20);
+        if (ch.acc.sum_bytes() > cap && ch.acc.merged_bytes() > cap) {
+          c++;
+          break;
+        }
       }
     }
     ch.c1 = c;
@@ -970,6 +978,7 @@ int run_pipeline(cmtv_ctx* ctx, const CommitsArgs& args, int* rcs, std::vector<c
 
 int verify_commits_pipeline(cmtv_ctx* ctx, const CommitsArgs& args, int* rcs) {
   std::unique_lock<std::mutex> bulk(bulk_mutex(ctx));
+  const BulkBusy busy(ctx);
   std::vector<const cmtv_keyset*> pinned;
   pinned.reserve(8);
   int rc;

@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -389,6 +390,11 @@ struct BulkSlot {
 };
 struct BulkLane {
   hipStream_t copy = nullptr, exec = nullptr;
+  // the exec stream of chunks submitted near a latency call: every CU but
+  // the reserved ones (its own hardware queue, cu_mask), and the waves one
+  // round of it holds at two per SIMD (the keyed batch kernel's occupancy)
+  hipStream_t exec_masked = nullptr;
+  uint32_t cus = 0, masked_waves = 0;
   BulkSlot slot[cmtv::kBulkSlotsMax];
   Scratch scratch;
 };
@@ -547,6 +553,22 @@ struct cmtv_ctx {
   int pipe_slots = 3;
   bool pipe_on = true;
   bool pipe_direct = true;  // CMTV_PIPE_DIRECT=0: pinned arguments are packed too
+  // Latency calls beside a pipeline (a 150-validator
+  // VerifyCommit from consensus while blocksync replays): a pipeline chunk
+  // submitted within lat_window_ns of such a call (cmtv_verify_commit, a
+  // small one-batch cmtv_verify_commits or host batch: note_latency) runs on
+  // the lane's CU-masked exec stream, which leaves lat_reserve_cus CUs (one
+  // per 32) to the device's normal stream, and is cut to what the other CUs
+  // hold in one round; while a pipeline call is in flight (bulk_busy) the
+  // latency call takes a form that fits those CUs (under_load, snapshotted at
+  // each lock hold). CMTV_LAT_WINDOW_MS (default 10,000; 0: never masked),
+  // CMTV_LAT_RESERVE_CUS (default 8).
+  std::atomic<uint64_t> last_latency_ns{0};
+  uint64_t lat_window_ns = 10'000'000'000ull;
+  uint32_t lat_reserve_cus = 8;
+  std::atomic<int> bulk_busy{0};
+  bool under_load = false;
+  uint32_t cus = 0;  // CUs per device (the smallest of the context's)
   // the caller's pinned blocks (cmtv_alloc_pinned): base -> bytes; chunks
   // whose arrays lie in one are DMA'd from it (pipeline.cpp direct chunks)
   std::map<uintptr_t, size_t> pinned;
@@ -693,6 +715,9 @@ static hipError_t row_slot_release(cmtv_ctx* ctx, CmtvDev& D, hipStream_t s, uin
 static uint32_t ed_form(const cmtv_ctx* ctx, size_t n) {
   const uint32_t f = ctx->force_form;
   if (f != kNoForm && !((f == kFormRow || f == kFormRow4) && n > kRowMaxCap)) return f;
+  // beside a running pipeline only its reserved CUs are free: 48 signatures
+  // per workgroup (quad) rather than one (row) or eight (oct)
+  if (ctx->under_load && n <= kQuadMax) return kFormQuad;
   return n <= kRow4Max ? kFormRow4 : n <= kRowMax ? kFormRow : n <= kOct2Max ? kFormOct2 : n <= kQuadMax ? kFormQuad
                                                                                                        : kFormLane;
 }
@@ -708,6 +733,7 @@ static uint32_t sr_form(const cmtv_ctx* ctx, size_t n) {
 static uint32_t keyed_form(const cmtv_ctx* ctx, size_t n) {
   const uint32_t f = ctx->force_keyed;
   if (f != kNoForm && !(f == kKeyedRow && n > kRowMaxCap)) return f;
+  if (ctx->under_load && n <= kKeyedQuadMax) return kKeyedQuad;  // as ed_form
   return n <= kKeyedRowMax ? kKeyedRow : n <= kKeyedQuadMax ? kKeyedQuad : kKeyedLane;
 }
 
@@ -786,8 +812,10 @@ constexpr uint32_t kCombKeyChunk = 256;
 static int enqueue_verify_keyed(cmtv_ctx* ctx, CmtvDev& D, const cmtv_keyset::PerDev& K, size_t n_keys, size_t n,
                                 const uint32_t* d_idx, const uint8_t* d_sig, const uint8_t* d_msg,
                                 const uint32_t* d_off, uint32_t mode, uint8_t* d_valid, uint64_t* d_bitmap,
-                                hipStream_t s, Scratch* scr = nullptr, const SbFuse* sb = nullptr) {
+                                hipStream_t s, Scratch* scr = nullptr, const SbFuse* sb = nullptr,
+                                uint32_t min_waves = 0) {
   if (n == 0) return CMTV_OK;
+  if (!min_waves) min_waves = ctx->keyed_batch_min_waves;  // a masked bulk lane holds fewer
   Scratch& S = scr ? *scr : D.scratch;
   if (sb && !keyed_fuse_ok(ctx, n)) return CMTV_EINVAL;
   if (!d_idx && !sb) return CMTV_EINVAL;  // identity keys only in the one-launch fused forms
@@ -806,7 +834,7 @@ static int enqueue_verify_keyed(cmtv_ctx* ctx, CmtvDev& D, const cmtv_keyset::Pe
     // one may be partial: a commit-aligned 1,048,500-signature chunk takes KB
     // = 8 in 2,048 waves)
     uint32_t kb = 1;
-    while (kb < 8 && cn > ((size_t)ctx->keyed_batch_min_waves - 1) * 64 * (kb * 2)) kb *= 2;
+    while (kb < 8 && cn > ((size_t)min_waves - 1) * 64 * (kb * 2)) kb *= 2;
     return batch && kb >= 4 ? kb : 1;
   };
   hipError_t e;
@@ -1564,6 +1592,8 @@ void clear_early_locked(cmtv_ctx* ctx) {
 int ctx_lock(cmtv_ctx* ctx, std::unique_lock<std::mutex>& lk) {
   lk = std::unique_lock<std::mutex>(ctx->mu);
   clear_early_locked(ctx);
+  // the forms of this hold's launches see one answer (keyed_form, ed_form)
+  ctx->under_load = ctx->bulk_busy.load(std::memory_order_relaxed) > 0 && ctx->lat_window_ns;
   return hipSetDevice(ctx->devs[0].ordinal) == hipSuccess ? CMTV_OK : CMTV_ENODEV;
 }
 
@@ -1718,6 +1748,11 @@ static void read_env(cmtv_ctx* ctx) {
   }
   if (const char* v = std::getenv("CMTV_PIPELINE")) ctx->pipe_on = v[0] != '0';
   if (const char* v = std::getenv("CMTV_PIPE_DIRECT")) ctx->pipe_direct = v[0] != '0';
+  if (const char* v = std::getenv("CMTV_LAT_WINDOW_MS")) ctx->lat_window_ns = 1'000'000ull * std::strtoull(v, nullptr, 10);
+  if (const char* v = std::getenv("CMTV_LAT_RESERVE_CUS")) {
+    const long k = std::strtol(v, nullptr, 10);
+    if (k >= 1 && k <= 64) ctx->lat_reserve_cus = (uint32_t)k;
+  }
   if (const char* dm = std::getenv("CMTV_RCCL_DRAIN_MS")) {
     const long v = std::strtol(dm, nullptr, 10);
     if (v >= 1 && v <= 600000) ctx->rccl_drain_ms = (uint32_t)v;
@@ -1779,14 +1814,17 @@ static int open_ctx(const cmtv_config* cfg, const std::vector<int>& ords, cmtv_c
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return CMTV_ENODEV;
   if (ords.empty() || ords.size() > (size_t)kMaxDevices) return CMTV_EINVAL;
+  uint32_t cus = UINT32_MAX;
   for (int o : ords) {
     if (o < 0 || o >= ndev) return CMTV_ENODEV;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, o) != hipSuccess) return CMTV_ENODEV;
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return CMTV_ENODEV;
+    cus = std::min(cus, (uint32_t)std::max(prop.multiProcessorCount, 1));
   }
   auto* ctx = new (std::nothrow) cmtv_ctx();
   if (!ctx) return CMTV_ENOMEM;
+  ctx->cus = cus;
   ctx->default_mode = cfg ? cfg->default_mode : CMTV_MODE_GO_STDLIB;
   if (!cfg) {
     const char* m = std::getenv("CMTVERIFY_MODE");
@@ -2275,6 +2313,18 @@ bool keyset_cache_enabled(const cmtv_ctx* ctx) { return ctx->keyset_cap != 0; }
 
 std::mutex& bulk_mutex(cmtv_ctx* ctx) { return ctx->bulk_mu; }
 
+// CUs a masked bulk lane leaves to the normal stream: CU 32k for k below
+// lat_reserve_cus (one per XCD on MI355X)
+static uint32_t reserved_cus(const cmtv_ctx* ctx, uint32_t cus) {
+  return std::min(ctx->lat_reserve_cus, (cus + 31) / 32);
+}
+
+static uint64_t now_ns_steady() {
+  return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
 // CPUs this process may run on: the affinity mask, bounded by a cgroup v2
 // CPU quota (cpu.max) when one is set
 static unsigned usable_cpus() {
@@ -2300,8 +2350,27 @@ HostPool& host_pool(cmtv_ctx* ctx) {
 }
 
 PipeConfig pipe_config(const cmtv_ctx* ctx) {
-  return PipeConfig{ctx->pipe_min, ctx->pipe_chunk, ctx->pipe_slots, ctx->pipe_on, ctx->pipe_direct};
+  PipeConfig pc{ctx->pipe_min, ctx->pipe_chunk, ctx->pipe_slots, ctx->pipe_on, ctx->pipe_direct};
+  // a masked lane's round: the chunk scaled to the CUs it keeps (bulk_lane_init)
+  const uint32_t reserved = reserved_cus(ctx, ctx->cus);
+  pc.chunk_masked = ctx->cus > reserved
+                        ? std::max<size_t>(64, ctx->pipe_chunk / ctx->cus * (ctx->cus - reserved))
+                        : ctx->pipe_chunk;
+  return pc;
 }
+
+void note_latency(cmtv_ctx* ctx) {
+  ctx->last_latency_ns.store(now_ns_steady(), std::memory_order_relaxed);
+}
+
+bool latency_recent(const cmtv_ctx* ctx) {
+  if (!ctx->lat_window_ns) return false;
+  const uint64_t t = ctx->last_latency_ns.load(std::memory_order_relaxed);
+  return t && now_ns_steady() - t < ctx->lat_window_ns;
+}
+
+BulkBusy::BulkBusy(cmtv_ctx* c) : ctx(c) { ctx->bulk_busy.fetch_add(1, std::memory_order_relaxed); }
+BulkBusy::~BulkBusy() { ctx->bulk_busy.fetch_sub(1, std::memory_order_relaxed); }
 
 void live_devices_locked(cmtv_ctx* ctx, std::vector<size_t>& out) { out = ctx->live; }
 
@@ -2315,6 +2384,24 @@ static hipError_t bulk_lane_init(cmtv_ctx* ctx, CmtvDev& D) {
   // behind a multi-ms chunk): lowest priority
   if (e == hipSuccess) e = hipStreamCreateWithPriority(&L.exec, hipStreamNonBlocking, least);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&L.scratch.done, hipEventDisableTiming);
+  if (e == hipSuccess) {
+    // the masked stream: every CU but one in each 32 of the first
+    // 32 x lat_reserve_cus (one per XCD on MI355X's 8 x 32)
+    int cus = 0;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, D.ordinal);
+    L.cus = (uint32_t)std::max(cus, 1);
+    const uint32_t words = (L.cus + 31) / 32;
+    std::vector<uint32_t> mask(words, 0);
+    for (uint32_t c = 0; c < L.cus; c++) mask[c / 32] |= 1u << (c % 32);
+    const uint32_t reserved = reserved_cus(ctx, L.cus);
+    for (uint32_t k = 0; k < reserved; k++) mask[k] &= ~1u;
+    L.masked_waves = 8 * (L.cus - reserved);
+    if (reserved == 0 || L.cus <= reserved ||
+        hipExtStreamCreateWithCUMask(&L.exec_masked, words, mask.data()) != hipSuccess) {
+      (void)hipGetLastError();
+      L.exec_masked = nullptr;  // no masking: chunks keep the plain exec stream
+    }
+  }
   for (int k = 0; k < kBulkSlotsMax && e == hipSuccess; k++) {
     e = hipEventCreateWithFlags(&L.slot[k].h2d, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&L.slot[k].done, hipEventDisableTiming);
@@ -2326,6 +2413,7 @@ static hipError_t bulk_lane_init(cmtv_ctx* ctx, CmtvDev& D) {
 static void bulk_lane_release(CmtvDev& D) {
   BulkLane& L = D.bulk;
   if (L.exec) (void)hipStreamSynchronize(L.exec);
+  if (L.exec_masked) (void)hipStreamSynchronize(L.exec_masked);
   if (L.copy) (void)hipStreamSynchronize(L.copy);
   for (auto& S : L.slot) {
     S.h_in.release();
@@ -2342,8 +2430,9 @@ static void bulk_lane_release(CmtvDev& D) {
   L.scratch.done = nullptr;
   L.scratch.used = false;
   if (L.exec) (void)hipStreamDestroy(L.exec);
+  if (L.exec_masked) (void)hipStreamDestroy(L.exec_masked);
   if (L.copy) (void)hipStreamDestroy(L.copy);
-  L.exec = L.copy = nullptr;
+  L.exec = L.exec_masked = L.copy = nullptr;
 }
 
 int bulk_stage(cmtv_ctx* ctx, size_t dev, int slot, const BulkLayout& L, uint8_t** host) {
@@ -2369,6 +2458,10 @@ int bulk_submit_locked(cmtv_ctx* ctx, size_t dev, int slot, const BulkLayout& L,
   if (e == hipSuccess) e = S.d_bm.ensure(8 * std::max<size_t>(words, 1));
   if (e == hipSuccess) e = S.h_bm.ensure(8 * std::max<size_t>(words, 1));
   if (e != hipSuccess) return hip_fail(e);
+  // near a latency call: the CU-masked stream, and batched launches sized
+  // to the waves its CUs hold in one round
+  const bool masked = L.masked && BL.exec_masked;
+  hipStream_t ex = masked ? BL.exec_masked : BL.exec;
   auto* din = static_cast<uint8_t*>(S.d_in.p);
   auto* dbm = static_cast<uint64_t*>(S.d_bm.p);
   // H2D on the copy stream (overlaps the exec stream's previous chunk); a
@@ -2380,7 +2473,7 @@ int bulk_submit_locked(cmtv_ctx* ctx, size_t dev, int slot, const BulkLayout& L,
       if ((e = hipMemcpyAsync(din + L.o_arena + L.spans[k].dev_off, L.spans[k].host, L.spans[k].bytes,
                               hipMemcpyHostToDevice, BL.copy)) != hipSuccess)
         return hip_fail(e);
-  if ((e = hipEventRecord(S.h2d, BL.copy)) != hipSuccess || (e = hipStreamWaitEvent(BL.exec, S.h2d, 0)) != hipSuccess)
+  if ((e = hipEventRecord(S.h2d, BL.copy)) != hipSuccess || (e = hipStreamWaitEvent(ex, S.h2d, 0)) != hipSuccess)
     return hip_fail(e);
   auto* off = reinterpret_cast<uint32_t*>(din + L.o_off);
   if (L.direct) {
@@ -2390,27 +2483,29 @@ int bulk_submit_locked(cmtv_ctx* ctx, size_t dev, int slot, const BulkLayout& L,
                                 reinterpret_cast<uint32_t*>(din + L.o_key), din + L.o_sig, off,
                                 reinterpret_cast<uint32_t*>(din + L.o_tidx), din + L.o_flag,
                                 reinterpret_cast<int64_t*>(din + L.o_sec), reinterpret_cast<int32_t*>(din + L.o_nanos),
-                                cb, cb + L.n_tmpls, BL.exec)) != hipSuccess)
+                                cb, cb + L.n_tmpls, ex)) != hipSuccess)
       return hip_fail(e);
   }
   // sign-bytes from the chunk's templates into o_msg (k_sign_bytes; the
   // bulk chunks run the lane kernels, whose launches take no fused form)
   if ((e = launch_sign_bytes((uint32_t)L.m, din + L.o_tmpl, din + L.o_blob, reinterpret_cast<uint32_t*>(din + L.o_tidx),
                              din + L.o_flag, reinterpret_cast<int64_t*>(din + L.o_sec),
-                             reinterpret_cast<int32_t*>(din + L.o_nanos), off, din + L.o_msg, BL.exec)) != hipSuccess)
+                             reinterpret_cast<int32_t*>(din + L.o_nanos), off, din + L.o_msg, ex)) != hipSuccess)
     return hip_fail(e);
   int rc;
   if (ks)
     rc = enqueue_verify_keyed(ctx, D, ks->dev[dev], ks->n, L.m, reinterpret_cast<uint32_t*>(din + L.o_key),
-                              din + L.o_sig, din + L.o_msg, off, mode, nullptr, dbm, BL.exec, &BL.scratch);
+                              din + L.o_sig, din + L.o_msg, off, mode, nullptr, dbm, ex, &BL.scratch, nullptr,
+                              masked ? BL.masked_waves : 0);
   else
-    rc = enqueue_verify(ctx, D, L.m, din + L.o_key, din + L.o_sig, din + L.o_msg, off, mode, nullptr, dbm, BL.exec,
+    rc = enqueue_verify(ctx, D, L.m, din + L.o_key, din + L.o_sig, din + L.o_msg, off, mode, nullptr, dbm, ex,
                         nullptr, &BL.scratch);
   if (rc != CMTV_OK) return rc;
-  if ((e = hipMemcpyAsync(S.h_bm.p, dbm, 8 * words, hipMemcpyDeviceToHost, BL.exec)) != hipSuccess ||
-      (e = hipEventRecord(S.done, BL.exec)) != hipSuccess)
+  if ((e = hipMemcpyAsync(S.h_bm.p, dbm, 8 * words, hipMemcpyDeviceToHost, ex)) != hipSuccess ||
+      (e = hipEventRecord(S.done, ex)) != hipSuccess)
     return hip_fail(e);
   S.pending = true;
+  if (masked) ctx->stats.masked_chunks++;
   return CMTV_OK;
 }
 
@@ -2432,6 +2527,7 @@ void bulk_drain(cmtv_ctx* ctx) {
     (void)hipSetDevice(D.ordinal);
     (void)hipStreamSynchronize(D.bulk.copy);
     (void)hipStreamSynchronize(D.bulk.exec);
+    if (D.bulk.exec_masked) (void)hipStreamSynchronize(D.bulk.exec_masked);
     for (auto& S : D.bulk.slot) S.pending = false;
   }
   (void)hipGetLastError();

@@ -107,6 +107,7 @@ struct BulkLayout {
   size_t m = 0, n_tmpls = 0, blob_len = 0;
   uint64_t msg_bytes = 0;  // direct: an upper bound (the device computes the offsets)
   bool keyed = false, direct = false;
+  bool masked = false;  // submitted to the lane's CU-masked exec stream
   size_t o_key = 0, o_sig = 0, o_off = 0, o_tidx = 0, o_flag = 0, o_sec = 0, o_nanos = 0, o_tmpl = 0, o_blob = 0;
   size_t o_desc = 0, o_cbase = 0, o_arena = 0, arena_bytes = 0;
   int n_spans = 0;
@@ -130,8 +131,21 @@ struct PipeConfig {
   int slots;
   bool enabled;
   bool direct = true;  // CMTV_PIPE_DIRECT=0: always pack (A/B, tests)
+  size_t chunk_masked = 0;  // a chunk on a CU-masked lane (latency_recent): one round of its CUs
 };
 PipeConfig pipe_config(const cmtv_ctx* ctx);
+// Latency calls beside the pipeline (runtime.cpp cmtv_ctx::lat_window_ns):
+// note_latency marks one (a single commit, a small batch); latency_recent is
+// true within the window after one -- the pipeline then submits its chunks
+// to the CU-masked exec stream (BulkLayout::masked). BulkBusy marks a
+// pipeline call in flight (its scope).
+void note_latency(cmtv_ctx* ctx);
+bool latency_recent(const cmtv_ctx* ctx);
+struct BulkBusy {
+  explicit BulkBusy(cmtv_ctx* c);
+  ~BulkBusy();
+  cmtv_ctx* ctx;
+};
 // live device indices, in shard order (context lock held)
 void live_devices_locked(cmtv_ctx* ctx, std::vector<size_t>& out);
 // the pinned staging of (dev, slot), grown to L.in_bytes (bulk lock held)

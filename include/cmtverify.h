@@ -113,6 +113,9 @@ typedef struct cmtv_stats {
   uint64_t direct_chunks;    /* cross-height pipeline chunks DMA'd straight
                               from the caller's cmtv_alloc_pinned memory (no
                               host pack per signature)                   */
+  uint64_t masked_chunks;    /* pipeline chunks run on the CU-masked exec
+                              stream because a latency call (a single
+                              commit) came within CMTV_LAT_WINDOW_MS      */
 } cmtv_stats;
 
 /* One device's share of the context's work (cmtv_device_stats_get). */

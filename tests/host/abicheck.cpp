@@ -163,6 +163,138 @@ static void device_checks(const Vecs& v, int threads) {
   }
 }
 
+// A node's goroutines on one context (SURVEY 8b Threading): a blocksync
+// caller running pipelined cmtv_verify_commits (CMTV_PIPE_MIN=1 at open, the
+// commits' arrays in the context's pinned memory so direct and packed chunks
+// both run), a consensus caller running single-commit cmtv_verify_commit, and
+// a third thread with host batches -- on a chain signed on the device, with
+// a flipped signature every 5th height; every outcome checked.
+static void commit_concurrency(int iters) {
+  setenv("CMTV_PIPE_MIN", "1", 1);
+  setenv("CMTV_PIPE_CHUNK", "512", 1);
+  cmtv_ctx* ctx = nullptr;
+  cmtv_config cfg{0, CMTV_MODE_GO_STDLIB, 0, 0};
+  CHECK(cmtv_open(&cfg, &ctx) == CMTV_OK);
+  unsetenv("CMTV_PIPE_MIN");
+  unsetenv("CMTV_PIPE_CHUNK");
+  if (!ctx) return;
+  CHECK(cmtv_keyset_cache(ctx, 2) == CMTV_OK);
+  const uint32_t nv = 16, H = 60;
+  std::vector<uint8_t> seeds(32 * nv), pk(32 * nv), addrs(20 * nv);
+  for (uint32_t i = 0; i < 32 * nv; i++) seeds[i] = (uint8_t)(i * 37 + 11);
+  CHECK(cmtv_pubkeys_ed25519(ctx, nv, seeds.data(), pk.data()) == CMTV_OK);
+  for (uint32_t i = 0; i < nv; i++) std::memcpy(&addrs[20 * i], &pk[32 * i], 20);
+  std::vector<uint32_t> pk_off(nv + 1);
+  std::vector<int64_t> power(nv, 10);
+  for (uint32_t i = 0; i <= nv; i++) pk_off[i] = 32 * i;
+  const cmtv_valset vs{nv, pk.data(), pk_off.data(), power.data(), addrs.data(), nullptr};
+  // the arena: flags, seconds, nanos, sig_off, signatures per height
+  const size_t per = 8 * ((nv + 1 + 7) / 8 + (nv + 1) + (4 * (nv + 1) + 7) / 8 + (4 * (nv + 1) + 7) / 8) + 64 * nv;
+  uint8_t* arena = nullptr;
+  CHECK(cmtv_alloc_pinned(ctx, per * H + 4096, reinterpret_cast<void**>(&arena)) == CMTV_OK);
+  if (!arena) {
+    cmtv_close(ctx);
+    return;
+  }
+  std::vector<uint8_t> bh(32 * H), ph(32 * H);
+  std::vector<cmtv_commit> cs(H);
+  std::vector<cmtv_block_id> bids(H);
+  std::vector<cmtv_valset> vals(H, vs);
+  std::vector<int64_t> hs(H);
+  const char chain[] = "cmtverify-abicheck";
+  size_t at = 0;
+  auto carve = [&](size_t bytes) {
+    uint8_t* p = arena + at;
+    at += (bytes + 7) / 8 * 8;
+    return p;
+  };
+  for (uint32_t h = 0; h < H; h++) {
+    for (int k = 0; k < 32; k++) {
+      bh[32 * h + k] = (uint8_t)(h * 5 + k);
+      ph[32 * h + k] = (uint8_t)(h * 9 + 3 * k);
+    }
+    bids[h] = cmtv_block_id{&bh[32 * h], 32, 1, &ph[32 * h], 32};
+    hs[h] = 100 + h;
+    uint8_t* fl = carve(nv + 1);
+    auto* se = reinterpret_cast<int64_t*>(carve(8 * (nv + 1)));
+    auto* na = reinterpret_cast<int32_t*>(carve(4 * (nv + 1)));
+    auto* so = reinterpret_cast<uint32_t*>(carve(4 * (nv + 1)));
+    uint8_t* sg = carve(64 * nv);
+    std::string msgs;
+    std::vector<uint32_t> off{0};
+    for (uint32_t i = 0; i < nv; i++) {
+      fl[i] = h % 4 == 3 && i == 2 ? 3 : 2;  // a nil vote now and then
+      se[i] = 1700000000 + h;
+      na[i] = (int32_t)(1000 * i);
+      so[i] = 64 * i;
+      uint8_t b[256];
+      static const cmtv_block_id zero{};
+      const int64_t ml = cmtv_vote_sign_bytes(chain, sizeof chain - 1, 2, hs[h], 0, fl[i] == 2 ? &bids[h] : &zero,
+                                              se[i], na[i], b, sizeof b);
+      msgs.append(reinterpret_cast<const char*>(b), (size_t)ml);
+      off.push_back((uint32_t)msgs.size());
+    }
+    so[nv] = 64 * nv;
+    std::vector<uint32_t> kidx(nv);
+    for (uint32_t i = 0; i < nv; i++) kidx[i] = i;
+    CHECK(cmtv_sign_ed25519(ctx, nv, seeds.data(), kidx.data(), reinterpret_cast<const uint8_t*>(msgs.data()),
+                            off.data(), sg) == CMTV_OK);
+    if (h % 5 == 1) sg[64 * (h % nv) + 7] ^= 4;  // a wrong signature at index h % nv
+    cs[h] = cmtv_commit{hs[h], 0, bids[h], nv, fl, se, na, sg, so, addrs.data()};
+  }
+  auto expect_ok = [&](uint32_t h, uint32_t kind, int rc, const cmtv_commit_result& r) {
+    // VerifyCommitLight stops after floor(2/3 * 160 / 10) + 1 = 11 commit votes
+    const uint32_t bad = h % nv;
+    const bool flipped = h % 5 == 1;
+    // (a nil vote at index 2 every 4th height: skipped by the light loop)
+    const bool reached = kind == 0 || (h % 4 == 3 ? bad != 2 && bad < 12 : bad < 11);
+    if (flipped && reached) return rc == CMTV_ECOMMIT && r.code == CMTV_COMMIT_ERR_WRONG_SIGNATURE && r.sig_index == (int32_t)bad;
+    return rc == CMTV_OK;
+  };
+  std::vector<int> oks(3, 1);
+  std::thread blocksync([&] {
+    std::vector<cmtv_commit_result> res(H);
+    std::vector<int> rcs(H);
+    for (int it = 0; it < iters; it++) {
+      const uint32_t kind = (uint32_t)(it & 1);
+      if (cmtv_verify_commits(ctx, kind, 0, chain, sizeof chain - 1, H, vals.data(), bids.data(), hs.data(), cs.data(),
+                              1, 3, res.data(), rcs.data(), nullptr, 0) != CMTV_OK) {
+        oks[0] = 0;
+        continue;
+      }
+      for (uint32_t h = 0; h < H; h++) oks[0] &= expect_ok(h, kind, rcs[h], res[h]) ? 1 : 0;
+    }
+  });
+  std::thread consensus([&] {
+    for (int it = 0; it < iters; it++)
+      for (uint32_t h = (uint32_t)it % 3; h < H; h += 3) {
+        const uint32_t kind = (uint32_t)((it + h) & 1);
+        cmtv_commit_result r{};
+        const int rc = cmtv_verify_commit(ctx, kind, 0, chain, sizeof chain - 1, &vs, &bids[h], hs[h], &cs[h], 1, 3,
+                                          &r, nullptr, 0);
+        oks[1] &= expect_ok(h, kind, rc, r) ? 1 : 0;
+      }
+  });
+  std::thread rpc([&] {
+    std::vector<uint8_t> m(1, 0), v(nv);
+    std::vector<uint32_t> off(nv + 1, 0);
+    for (int it = 0; it < 4 * iters; it++) {
+      // one height's signatures over empty messages: all invalid
+      oks[2] &= cmtv_verify_ed25519(ctx, nv, pk.data(), cs[it % H].sigs, m.data(), off.data(), 0, v.data(), nullptr) ==
+                CMTV_OK;
+      for (uint32_t i = 0; i < nv; i++) oks[2] &= v[i] == 0;
+    }
+  });
+  blocksync.join();
+  consensus.join();
+  rpc.join();
+  CHECK(oks[0] && oks[1] && oks[2]);
+  cmtv_stats st{};
+  CHECK(cmtv_stats_get(ctx, &st) == CMTV_OK && st.direct_chunks > 0);
+  CHECK(cmtv_free_pinned(ctx, arena) == CMTV_OK);
+  cmtv_close(ctx);
+}
+
 int main(int argc, char** argv) {
   if (argc < 2) return 2;
   Vecs v;
@@ -180,6 +312,7 @@ int main(int argc, char** argv) {
     CHECK(rc == CMTV_OK);
     cmtv_close(probe);
     device_checks(v, threads);
+    commit_concurrency(4);
   }
   std::printf("abicheck: %zu vectors, %d failures\n", v.n, fails);
   return fails ? 1 : 0;

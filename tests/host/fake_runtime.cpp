@@ -71,6 +71,8 @@ struct cmtv_ctx {
   std::map<uintptr_t, size_t> pinned;        // cmtv_alloc_pinned blocks
   uint64_t direct_chunks = 0;
   bool keyset_fail = false;  // registration fails (the pipeline packs direct chunks after all)
+  std::atomic<uint64_t> latency_calls{0};
+  uint64_t masked_chunks = 0;
 };
 
 namespace {
@@ -221,7 +223,17 @@ HostPool& host_pool(cmtv_ctx* ctx) {
   if (!ctx->pool) ctx->pool.reset(new HostPool(ctx->threads));
   return *ctx->pool;
 }
-PipeConfig pipe_config(const cmtv_ctx* ctx) { return ctx->pc; }
+PipeConfig pipe_config(const cmtv_ctx* ctx) {
+  PipeConfig pc = ctx->pc;
+  pc.chunk_masked = std::max<size_t>(64, pc.chunk * 31 / 32);
+  return pc;
+}
+// latency calls mark the context; the pipeline's chunks after one are masked
+// (a flag the fake only counts)
+void note_latency(cmtv_ctx* ctx) { ctx->latency_calls++; }
+bool latency_recent(const cmtv_ctx* ctx) { return ctx->latency_calls.load() > 0; }
+BulkBusy::BulkBusy(cmtv_ctx* c) : ctx(c) {}
+BulkBusy::~BulkBusy() {}
 int stage_sigs_early_locked(cmtv_ctx*, const uint8_t*, size_t, const uint8_t*) { return CMTV_OK; }
 void clear_early_locked(cmtv_ctx*) {}
 void live_devices_locked(cmtv_ctx* ctx, std::vector<size_t>& out) { out = ctx->live; }
@@ -261,6 +273,7 @@ int bulk_submit_locked(cmtv_ctx* ctx, size_t dev, int slot, const BulkLayout& L,
   }
   S.L = L;
   S.ks = ks;
+  if (L.masked) ctx->masked_chunks++;
   S.mode = mode;
   S.pending = true;
   ctx->chunks++;
@@ -298,10 +311,18 @@ int bulk_gather(FakeSlot& S) {
   auto* tidx = reinterpret_cast<uint32_t*>(h + L.o_tidx);
   auto* sec = reinterpret_cast<int64_t*>(h + L.o_sec);
   auto* nanos = reinterpret_cast<int32_t*>(h + L.o_nanos);
-  uint64_t o = 0, covered = 0;
+  uint64_t o = 0, covered = 0, tmpl_at = 0;
   for (size_t c = 0; c < L.n_tmpls; c++) {
     const BulkDesc& D = desc[c];
     if (!D.m) continue;
+    // the templates tile the blob (the plan's lengths are the pack's)
+    const SbTemplate& T = tmpls[c];
+    if (T.pre_commit_off != tmpl_at || T.pre_nil_off != T.pre_commit_off + T.pre_commit_len ||
+        T.post_off != T.pre_nil_off + T.pre_nil_len) {
+      std::fprintf(stderr, "fake: template %zu not where the plan put it\n", c);
+      return CMTV_EINVAL;
+    }
+    tmpl_at = T.post_off + T.post_len;
     // the kernel's aligned loads, and every signature once, in order
     if ((D.sig & 7) || (D.sec & 7) || (D.nanos & 3) || D.sp != covered || D.sp + D.m > L.m ||
         D.sig + 64ull * D.m > L.arena_bytes || D.sec + 8ull * D.m > L.arena_bytes ||

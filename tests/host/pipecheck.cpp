@@ -15,14 +15,17 @@
 // ref vs one/pipe: return code, error code, index, got/needed; one vs pipe:
 // the whole result struct and error string, byte for byte.
 // Usage: pipecheck [n_heights]; exit 0 = all agree.
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/cmtverify.h"
+#include "../../cometbft_amd/csrc/commit_internal.h"
 
 extern "C" {
 int oracle_verify_one(const uint8_t* pk, const uint8_t* msg, size_t mlen, const uint8_t* sig, int mode);
@@ -385,8 +388,95 @@ void expect_same(const char* what, const Run& a, const Run& b) {
 
 }  // namespace
 
+// Concurrency (pipecheck <heights> race; built with -fsanitize=thread by
+// tests/test_pipeline_cpu.py): callers share one context as a node's
+// goroutines do (SURVEY 8b Threading) -- a blocksync goroutine running
+// pipelined cmtv_verify_commits (direct and packed chunks over two fake
+// devices, host worker pool), a consensus goroutine running single-commit
+// cmtv_verify_commit calls, and an RPC-like reader of the context's pinned
+// blocks allocating and freeing its own -- each checking every outcome
+// against the reference loops.
+int race(const std::vector<CommitData>& chain, const std::vector<const VSet*>& vals_of, int iters) {
+  std::vector<Outcome> ref[2];
+  for (uint32_t kind = 0; kind < 2; kind++)
+    for (size_t i = 0; i < chain.size(); i++) ref[kind].push_back(reference(kind, 0, *vals_of[i], chain[i], 1, 3));
+  cmtv_ctx* ctx = fake_open(2, 4, 1, 64, 2, true, 4, -1);
+  std::atomic<int> bad{0};
+  std::thread pipe([&] {
+    for (int it = 0; it < iters; it++) {
+      const uint32_t kind = (uint32_t)(it & 1);
+      const Run r = run(ctx, kind, 0, chain, vals_of, it % 3 == 2 ? kHeap : kInterleaved);
+      for (size_t i = 0; i < chain.size(); i++)
+        if (r.rcs[i] != ref[kind][i].rc || (r.rcs[i] && r.res[i].code != ref[kind][i].code)) bad++;
+    }
+  });
+  std::thread single([&] {
+    for (int it = 0; it < iters; it++)
+      for (size_t i = 0; i < chain.size(); i += 7) {
+        const uint32_t kind = (uint32_t)((it + i) & 1);
+        cmtv_commit_result res{};
+        char msg[256];
+        const int rc = cmtv_verify_commit(ctx, kind, 0, kChain, sizeof kChain - 1, &vals_of[i]->vs, &chain[i].want,
+                                          chain[i].height, &chain[i].c, 1, 3, &res, msg, sizeof msg);
+        if (rc != ref[kind][i].rc || (rc && res.code != ref[kind][i].code)) bad++;
+      }
+  });
+  std::thread other([&] {
+    for (int it = 0; it < 50 * iters; it++) {
+      void* p = nullptr;
+      if (cmtv_alloc_pinned(ctx, 4096 + 64 * (size_t)it, &p) != CMTV_OK || cmtv_free_pinned(ctx, p) != CMTV_OK) bad++;
+    }
+  });
+  pipe.join();
+  single.join();
+  other.join();
+  uint64_t cnt[6];
+  fake_counts(ctx, cnt);
+  fake_close(ctx);
+  if (!cnt[5]) {
+    std::fprintf(stderr, "race: no direct chunk ran\n");
+    bad++;
+  }
+  std::printf("race: %d iterations, %d mismatches\n", iters, bad.load());
+  return bad ? 1 : 0;
+}
+
+// commit_template_lens (the pipeline's plan) == put_commit_template's
+// lengths (what the pack writes) over heights, rounds, block IDs and chain ids
+int check_template_lens() {
+  int bad = 0;
+  uint8_t h1[300], h2[300];
+  for (int i = 0; i < 300; i++) h1[i] = h2[i] = (uint8_t)i;
+  const int64_t heights[] = {0, 1, -1, 127, 1ll << 40, INT64_MIN};
+  const int32_t rounds[] = {0, 1, -5, INT32_MAX};
+  const uint32_t lens[] = {0, 1, 32, 127, 128, 200};
+  const uint32_t totals[] = {0, 1, 127, 128, 1u << 31};
+  const size_t chains[] = {0, 1, 15, 50, 127, 128, 200};
+  static char chain[256];
+  for (int64_t h : heights)
+    for (int32_t r : rounds)
+      for (uint32_t hl : lens)
+        for (uint32_t pl : lens)
+          for (uint32_t tot : totals)
+            for (size_t cl : chains) {
+              cmtv_commit c{};
+              c.height = h;
+              c.round = r;
+              c.block_id = cmtv_block_id{h1, hl, tot, h2, pl};
+              cmtv::SbTemplate t{};
+              const size_t n = cmtv::put_commit_template(nullptr, 0, chain, cl, &c, &t);
+              uint32_t a, b, p;
+              const size_t m = cmtv::commit_template_lens(cl, &c, &a, &b, &p);
+              if (n != m || a != t.pre_commit_len || b != t.pre_nil_len || p != t.post_len) bad++;
+            }
+  if (bad) std::fprintf(stderr, "commit_template_lens differs in %d cases\n", bad);
+  return bad;
+}
+
 int main(int argc, char** argv) {
   const int64_t heights = argc > 1 ? std::atoll(argv[1]) : 240;
+  if (check_template_lens()) return 1;
+  const bool race_mode = argc > 2 && std::strcmp(argv[2], "race") == 0;
   const uint32_t nv = 24;
   VSet A, B, C, Bad;
   make_set(A, nv, 1);
@@ -411,6 +501,7 @@ int main(int argc, char** argv) {
       d.c.sigs = d.sigs.data();
       d.c.sig_off = d.sig_off.data();
     }
+  if (race_mode) return race(chain, vals_of, 6);
   struct Cfg {
     const char* name;
     size_t devs;

@@ -28,29 +28,30 @@ FLAGS = ["-O1", "-g", "-std=c++17", "-fsanitize=address,undefined", "-fno-omit-f
          "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include"]
 
 
-def _build():
+def _build(san="address,undefined", binary=BIN):
     deps = SRCS + [os.path.join(ROOT, "oracle", "cmtv_oracle.c"), os.path.join(ROOT, "include", "cmtverify.h")] + \
         [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
-    if os.path.exists(BIN) and os.path.getmtime(BIN) >= max(os.path.getmtime(d) for d in deps):
-        return BIN
-    objdir = os.path.join(ROOT, "build", "pipecheck")
+    if os.path.exists(binary) and os.path.getmtime(binary) >= max(os.path.getmtime(d) for d in deps):
+        return binary
+    objdir = os.path.join(ROOT, "build", "pipecheck_" + san.replace(",", "_"))
     os.makedirs(objdir, exist_ok=True)
+    flags = [f for f in FLAGS if not f.startswith("-fsanitize")] + [f"-fsanitize={san}"]
     objs = []
     procs = []
     for src in SRCS:
         o = os.path.join(objdir, os.path.basename(src) + ".o")
-        procs.append(subprocess.Popen(["g++"] + FLAGS + ["-c", src, "-o", o]))
+        procs.append(subprocess.Popen(["g++"] + flags + ["-c", src, "-o", o]))
         objs.append(o)
     o = os.path.join(objdir, "cmtv_oracle.o")
-    procs.append(subprocess.Popen(["gcc", "-O2", "-g", "-fsanitize=address,undefined", "-c",
+    procs.append(subprocess.Popen(["gcc", "-O2", "-g", f"-fsanitize={san}", "-c",
                                    os.path.join(ROOT, "oracle", "cmtv_oracle.c"), "-o", o]))
     objs.append(o)
     for p in procs:
         assert p.wait() == 0, "pipecheck build failed"
-    tmp = f"{BIN}.{os.getpid()}"
-    subprocess.run(["g++", "-fsanitize=address,undefined", "-o", tmp] + objs + ["-lpthread"], check=True)
-    os.replace(tmp, BIN)
-    return BIN
+    tmp = f"{binary}.{os.getpid()}"
+    subprocess.run(["g++", f"-fsanitize={san}", "-o", tmp] + objs + ["-lpthread"], check=True)
+    os.replace(tmp, binary)
+    return binary
 
 
 def test_pipeline_host_logic_matches_reference_loops():
@@ -65,3 +66,22 @@ def test_pipeline_host_logic_matches_reference_loops():
     assert "pipecheck ok (60 runs)" in r.stdout
     for kind in (0, 1, 2):
         assert f"kind {kind} mode 0: 240 commits" in r.stdout
+
+
+def test_pipeline_concurrent_callers_under_tsan():
+    """ThreadSanitizer (the reference's `go test -race`, tests.mk:67-70;
+    SURVEY 5): the same host code built with -fsanitize=thread, one context
+    shared by a pipelined cmtv_verify_commits caller (direct and packed
+    chunks on two fake devices, the host worker pool), a single-commit
+    cmtv_verify_commit caller and a thread allocating / freeing pinned blocks;
+    every outcome checked against the reference loops, any race report fails
+    (halt_on_error)."""
+    try:
+        b = _build("thread", os.path.join(HOST, "pipecheck_tsan"))
+    except (OSError, subprocess.CalledProcessError, AssertionError) as e:
+        pytest.fail(f"could not build pipecheck_tsan: {e}")
+    r = subprocess.run([b, "120", "race"], capture_output=True, text=True, timeout=900,
+                       env={**os.environ, "TSAN_OPTIONS": "halt_on_error=1:second_deadlock_stack=1"})
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-6000:])
+    assert "race: 6 iterations, 0 mismatches" in r.stdout
+    assert "WARNING: ThreadSanitizer" not in r.stderr

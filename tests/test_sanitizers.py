@@ -35,12 +35,17 @@ def _vectors(corpus, path, n=300):
     return len(idx)
 
 
-def _abicheck(tmp_path, corpus):
-    if not os.path.exists(SAN_BIN):
-        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "cometbft_amd", "csrc"), "san"], check=True)
+TSAN_BIN = os.path.join(ROOT, "tests", "host", "abicheck_tsan")
+# the HIP runtime is not instrumented: its own threads' accesses are ignored
+TSAN_ENV = dict(os.environ, TSAN_OPTIONS="halt_on_error=1:ignore_noninstrumented_modules=1:report_signal_unsafe=0")
+
+
+def _abicheck(tmp_path, corpus, binary=SAN_BIN, target="san", env=ENV):
+    if not os.path.exists(binary):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "cometbft_amd", "csrc"), target], check=True)
     vec = str(tmp_path / "vectors.bin")
     _vectors(corpus, vec)
-    return subprocess.run([SAN_BIN, vec, "4"], capture_output=True, text=True, env=ENV, timeout=600)
+    return subprocess.run([binary, vec, "4"], capture_output=True, text=True, env=env, timeout=600)
 
 
 def test_runtime_under_asan_ubsan_without_device(tmp_path, corpus):
@@ -58,6 +63,31 @@ def test_runtime_under_asan_ubsan_on_device(tmp_path, corpus):
     r = _abicheck(tmp_path, corpus)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert "0 failures" in r.stdout and "no device" not in r.stdout
+
+
+def test_runtime_under_tsan_without_device(tmp_path, corpus):
+    """ThreadSanitizer build of runtime.cpp + commit.cpp + pipeline.cpp
+    (Makefile `tsan`, host code only): the device-free entry points."""
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present: see the gpu variant")
+    r = _abicheck(tmp_path, corpus, TSAN_BIN, "tsan", TSAN_ENV)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "no device" in r.stdout and "0 failures" in r.stdout
+
+
+@pytest.mark.gpu
+def test_runtime_under_tsan_on_device(tmp_path, corpus):
+    """The same under ThreadSanitizer on the GPU: 4 concurrent host-batch
+    callers on one context, then a pipelined cmtv_verify_commits caller
+    (direct and packed chunks), a single-commit cmtv_verify_commit caller and
+    a host-batch caller sharing one context (abicheck commit_concurrency);
+    any race report in the library's host code fails."""
+    r = _abicheck(tmp_path, corpus, TSAN_BIN, "tsan", TSAN_ENV)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-6000:]
+    assert "0 failures" in r.stdout and "no device" not in r.stdout
+    assert "ThreadSanitizer" not in r.stderr
 
 
 def _san_build(src, out, flags):

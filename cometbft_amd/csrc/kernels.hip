@@ -159,7 +159,15 @@ __device__ uint64_t g_phase[4096 * 4 * kPhaseSlots];
       g_phase[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * kPhaseSlots + (k)] = (val);          \
   } while (0)
 #define CMTV_CLOCK() __builtin_amdgcn_s_memtime()
+// five-wave workgroups (k_verify_keyed_quad_split): the same buffer indexed
+// by (block * 5 + wave)
+#define CMTV_STAMP5(k)                                                                             \
+  do {                                                                                             \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 3200)                                              \
+      g_phase[((size_t)blockIdx.x * 5 + (threadIdx.x >> 6)) * kPhaseSlots + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
 #else
+#define CMTV_STAMP5(k) ((void)0)
 #define CMTV_STAMP(k) ((void)0)
 #define CMTV_STAMP_RT(k) ((void)0)
 #define CMTV_STAMP_VAL(k, val) ((void)0)
@@ -948,8 +956,12 @@ __global__ __launch_bounds__(320, 1) void k_verify_keyed_quad_split(
   __shared__ uint32_t sbm[48][kSbFuseMaxMsg / 4];  // fused sign-bytes
   __shared__ uint32_t rpt[48][31];  // R: x, y, t (10 words each), decode flag
   __shared__ uint32_t k_ready;
+  CMTV_STAMP5(0);
   if (threadIdx.x == 0) k_ready = 0u;
   __syncthreads();  // the flag is clear before any wave can set or read it
+  // probe slots: 0 entry; hash helper 3 = k published; decode helper 3 = R
+  // decoded; quads 4 = k taken, 1 / 2 = before / after the barrier (the combs
+  // done / R in hand), 5 = exit; every wave 2 = after the barrier
   if (wave >= 3) {
     const uint32_t s = base + (t < 48 ? t : 47);
     const uint32_t i = s < n ? s : n - 1;
@@ -968,6 +980,7 @@ __global__ __launch_bounds__(320, 1) void k_verify_keyed_quad_split(
         for (int j = 0; j < 8; j++) tks[t][j] = tk[j];
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (t == 0) __hip_atomic_store(&k_ready, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      CMTV_STAMP5(3);
     } else {
       // decode helper: R from the first cycle, overlapping the quads' fixed-
       // base and key combs (the chain that bounded the one-helper form)
@@ -982,8 +995,10 @@ __global__ __launch_bounds__(320, 1) void k_verify_keyed_quad_split(
         }
         rpt[t][30] = r_ok ? 1u : 0u;
       }
+      CMTV_STAMP5(3);
     }
     __syncthreads();  // R (and k)
+    CMTV_STAMP5(2);
     return;
   }
   const uint32_t ls = wave * 16 + (t >> 2);
@@ -1022,9 +1037,12 @@ __global__ __launch_bounds__(320, 1) void k_verify_keyed_quad_split(
 #pragma unroll
           for (int j = 0; j < 8; j++) tk[j] = tks[ls][j];
         }
+        CMTV_STAMP5(4);
       },
       [&](fe& rc, bool& r_ok) {
+        CMTV_STAMP5(1);
         __syncthreads();
+        CMTV_STAMP5(2);
         // this lane's coordinate: x, y, 1, t
         const uint32_t* p = rpt[ls] + 10 * (lane == 3 ? 2 : lane);
 #pragma unroll
@@ -1041,6 +1059,7 @@ __global__ __launch_bounds__(320, 1) void k_verify_keyed_quad_split(
   x = (x | (x >> 24)) & 0xFFFFull;
   const uint32_t slice = blockIdx.x * 3 + wave;
   if (t == 0 && out_bitmap && slice < 4 * ((n + 63) / 64)) reinterpret_cast<uint16_t*>(out_bitmap)[slice] = (uint16_t)x;
+  CMTV_STAMP5(5);
 }
 
 hipError_t launch_verify_keyed(uint32_t mode, uint32_t n, uint32_t n_keys, const void* key_idx, const void* sig,

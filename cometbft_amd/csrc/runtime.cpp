@@ -1551,12 +1551,25 @@ int stage_sigs_early_locked(cmtv_ctx* ctx, const uint8_t* sigs, size_t n, const 
   const size_t in_cap = 136 * n + 64 * 1024, dev_cap = in_cap + 400 * n;
   if ((e = D.h_in.ensure(in_cap)) != hipSuccess) return hip_fail(e);
   if ((e = D.d_in.ensure(dev_cap)) != hipSuccess) return hip_fail(e);
-  std::memcpy(D.h_in.p, sigs, 64 * n);
   // the keys where enqueue_shard's layout puts them for m = n signatures
-  const size_t o_key = align_up(64 * n, 256), bytes = pk ? o_key + 32 * n : 64 * n;
-  if (pk) std::memcpy(static_cast<uint8_t*>(D.h_in.p) + o_key, pk, 32 * n);
-  if ((e = hipMemcpyAsync(D.d_in.p, D.h_in.p, bytes, hipMemcpyHostToDevice, D.stream)) != hipSuccess)
-    return hip_fail(e);
+  const size_t o_key = align_up(64 * n, 256);
+  auto* hin = static_cast<uint8_t*>(D.h_in.p);
+  auto* din = static_cast<uint8_t*>(D.d_in.p);
+  // arrays in the caller's cmtv_alloc_pinned memory go to the device by DMA
+  // straight from there (no host copy: 640 KB of signatures at 10k); the
+  // others through h_in as before
+  const bool sig_pinned = pinned_holds_locked(ctx, sigs, 64 * n);
+  const bool pk_pinned = pk && pinned_holds_locked(ctx, pk, 32 * n);
+  if (!sig_pinned) std::memcpy(hin, sigs, 64 * n);
+  if (pk && !pk_pinned) std::memcpy(hin + o_key, pk, 32 * n);
+  if (!sig_pinned && pk && !pk_pinned) {  // one copy of both
+    e = hipMemcpyAsync(din, hin, o_key + 32 * n, hipMemcpyHostToDevice, D.stream);
+  } else {
+    e = hipMemcpyAsync(din, sig_pinned ? sigs : hin, 64 * n, hipMemcpyHostToDevice, D.stream);
+    if (e == hipSuccess && pk)
+      e = hipMemcpyAsync(din + o_key, pk_pinned ? pk : hin + o_key, 32 * n, hipMemcpyHostToDevice, D.stream);
+  }
+  if (e != hipSuccess) return hip_fail(e);
   D.early_src = sigs;
   D.early_pk = pk;
   D.early_n = n;
@@ -2549,6 +2562,14 @@ bool retire_device_locked(cmtv_ctx* ctx, size_t dev) {
 
 void count_invalid_locked(cmtv_ctx* ctx, uint64_t n) { ctx->stats.invalid += n; }
 void count_direct_locked(cmtv_ctx* ctx) { ctx->stats.direct_chunks++; }
+
+bool pinned_holds_locked(const cmtv_ctx* ctx, const void* p, size_t bytes) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  auto it = ctx->pinned.upper_bound(a);
+  if (it == ctx->pinned.begin()) return false;
+  --it;
+  return a + bytes >= a && a + bytes <= it->first + it->second;
+}
 
 void pinned_ranges_locked(cmtv_ctx* ctx, std::vector<PinnedRange>& out) {
   out.clear();

@@ -122,6 +122,8 @@ struct PinnedRange {
   size_t bytes;
 };
 void pinned_ranges_locked(cmtv_ctx* ctx, std::vector<PinnedRange>& out);
+// [p, p + bytes) lies in one of the caller's pinned blocks (lock held)
+bool pinned_holds_locked(const cmtv_ctx* ctx, const void* p, size_t bytes);
 std::mutex& bulk_mutex(cmtv_ctx* ctx);
 class HostPool;
 // the context's worker pool (created on first use; bulk lock held)

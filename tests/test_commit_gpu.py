@@ -302,15 +302,18 @@ def test_device_sign_bytes_templating(monkeypatch, chain, fuse):
         assert (st["fused_sign_bytes"] > 0) == (fuse and len(chain) <= 50), st["fused_sign_bytes"]
 
 
+@pytest.mark.parametrize("pinned", [False, True])
 @pytest.mark.parametrize("keyed", [True, False])
-def test_early_staged_signatures_never_go_stale(keyed):
+def test_early_staged_signatures_never_go_stale(keyed, pinned):
     """a single-commit VerifyCommit copies its signatures to
     the device before planning (stage_sigs_early_locked). When it stops
     before any batch runs (here: a wrong height), those device bytes must not
     be taken for the next call's, even if that call passes the SAME buffer
     with new contents -- as the Go binding's reused arena does. The next call
     (cmtv_verify_commits with one commit, and cmtv_verify_commit itself) must
-    verify the bytes it is given now."""
+    verify the bytes it is given now. pinned: the commit's arrays in the
+    context's cmtv_alloc_pinned memory (then the signatures go to the device
+    by DMA straight from the caller's buffer)."""
     import ctypes
 
     from cometbft_amd import Context
@@ -326,7 +329,8 @@ def test_early_staged_signatures_never_go_stale(keyed):
     commit, _, _ = TU.make_commit(ctx, sv, height=h)
     bid = TU.block_id_for_height(h)
     vs, keep_v = sv.valset._pack()
-    cm, keep_c = T._pack_commit(commit)
+    arena = T._Arena(ctx.alloc_pinned(4096 + 100 * (n + 1))) if pinned else None
+    cm, keep_c = T._pack_commit(commit, arena)
     sb = keep_c[3]  # the signatures' buffer, reused below at the same address
     b, keep_b = bid._c()
     cid = TU.CHAIN_ID.encode()

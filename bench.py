@@ -897,6 +897,21 @@ def _commit_c_call(c, sv, commit, bid, height, mode, pinned=False):
     return call, (kv, kc, kb, res)
 
 
+def _p50_p99_inner(fn, between, iters, warm=20):
+    """p50 / p99 of fn() alone, each call followed by between() (untimed)."""
+    for _ in range(warm):
+        fn()
+        between()
+    ts = []
+    for _ in range(iters):
+        t = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t)
+        between()
+    ts = np.array(ts) * 1e3
+    return round(float(np.percentile(ts, 50)), 4), round(float(np.percentile(ts, 99)), 4)
+
+
 def _p50_p99(fn, iters, warm=50):
     for _ in range(warm):
         fn()
@@ -1015,7 +1030,7 @@ def latency_150(ctx, mode, iters):
     return res
 
 
-def latency_150_under_load(mode, iters, load_heights=30_000):
+def latency_150_under_load(mode, iters, load_heights=30_000, gap_ms=1.0):
     """p50 / p99 of a 150-validator
     VerifyCommit (cmtv_verify_commit, packed once, keyset cache on) while
     another thread keeps running cmtv_verify_commits over load_heights x
@@ -1027,7 +1042,11 @@ def latency_150_under_load(mode, iters, load_heights=30_000):
     context lock only while it enqueues a chunk; near a latency call its
     chunks run on a CU-masked stream that leaves 8 CUs to the 150-validator
     call's kernel (runtime.cpp lat_window_ns); idle numbers from the same
-    context beside it."""
+    context beside it. The 150-validator calls are gap_ms apart (a node's
+    consensus commits come a block time apart; back to back, they hold the
+    context lock nearly all the time and starve the load's submissions, so
+    the "loaded" numbers would be of an idle GPU); the load's own rate over
+    the window is reported beside them."""
     import threading
 
     from cometbft_amd import Context
@@ -1056,7 +1075,15 @@ def latency_150_under_load(mode, iters, load_heights=30_000):
     st0 = ctx.stats()
     th.start()
     time.sleep(0.2)
-    loaded = _p50_p99(call, iters, warm=20)
+
+    def gap():
+        time.sleep(gap_ms * 1e-3)  # releases the GIL: the load thread's Python runs here
+
+    s_load0 = ctx.stats()["signatures"]
+    t_win = time.perf_counter()
+    loaded = _p50_p99_inner(call, gap, iters, warm=20)
+    t_win = time.perf_counter() - t_win
+    s_load = ctx.stats()["signatures"] - s_load0 - 150 * iters
     stop.set()
     th.join()
     st1 = ctx.stats()
@@ -1068,7 +1095,8 @@ def latency_150_under_load(mode, iters, load_heights=30_000):
             "load": f"cmtv_verify_commits over {load_heights} x 150 commits in a loop on the same context "
                     f"({passes[0]} passes, median {round(float(np.median(t_bulk)) * 1e3, 2) if t_bulk else None} "
                     "ms each)", "load_ok": bool(np.all(rcs == 0)),
-            "masked_chunks": st1["masked_chunks"] - st0["masked_chunks"],
+            "masked_chunks": st1["masked_chunks"] - st0["masked_chunks"], "gap_ms": gap_ms,
+            "load_verifs_per_s_during_window": round(s_load / t_win, 1),
             "path": "cmtv_verify_commit (150 validators, keyset cache) from the main thread; the load from a second "
                     "thread"}
 

@@ -166,8 +166,17 @@ __device__ uint64_t g_phase[4096 * 4 * kPhaseSlots];
     if ((threadIdx.x & 63) == 0 && blockIdx.x < 3200)                                              \
       g_phase[((size_t)blockIdx.x * 5 + (threadIdx.x >> 6)) * kPhaseSlots + (k)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
+// slot 6 of a five-wave workgroup's wave: its HW_ID (bits 5:4 the SIMD, 11:8 the CU)
+#define CMTV_HWID5()                                                                               \
+  do {                                                                                             \
+    uint32_t hwid_;                                                                                \
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid_));                             \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 3200)                                              \
+      g_phase[((size_t)blockIdx.x * 5 + (threadIdx.x >> 6)) * kPhaseSlots + 6] = hwid_;             \
+  } while (0)
 #else
 #define CMTV_STAMP5(k) ((void)0)
+#define CMTV_HWID5() ((void)0)
 #define CMTV_STAMP(k) ((void)0)
 #define CMTV_STAMP_RT(k) ((void)0)
 #define CMTV_STAMP_VAL(k, val) ((void)0)
@@ -957,6 +966,7 @@ __global__ __launch_bounds__(320, 1) void k_verify_keyed_quad_split(
   __shared__ uint32_t rpt[48][31];  // R: x, y, t (10 words each), decode flag
   __shared__ uint32_t k_ready;
   CMTV_STAMP5(0);
+  CMTV_HWID5();
   if (threadIdx.x == 0) k_ready = 0u;
   __syncthreads();  // the flag is clear before any wave can set or read it
   // probe slots: 0 entry; hash helper 3 = k published; decode helper 3 = R

@@ -22,6 +22,7 @@
 #include <cstring>
 #include <deque>
 #include <fstream>
+#include <functional>
 #include <memory>
 #include <map>
 #include <mutex>
@@ -562,8 +563,10 @@ struct cmtv_ctx {
   // hold in one round; while a pipeline call is in flight (bulk_busy) the
   // latency call takes a form that fits those CUs (under_load, snapshotted at
   // each lock hold). CMTV_LAT_WINDOW_MS (default 10,000; 0: never masked),
-  // CMTV_LAT_RESERVE_CUS (default 8).
+  // CMTV_LAT_RESERVE_CUS (default 8); CMTV_LOAD_FORM=0 keeps the latency
+  // call's idle form under load.
   std::atomic<uint64_t> last_latency_ns{0};
+  bool load_form = true;
   uint64_t lat_window_ns = 10'000'000'000ull;
   uint32_t lat_reserve_cus = 8;
   std::atomic<int> bulk_busy{0};
@@ -572,6 +575,13 @@ struct cmtv_ctx {
   // the caller's pinned blocks (cmtv_alloc_pinned): base -> bytes; chunks
   // whose arrays lie in one are DMA'd from it (pipeline.cpp direct chunks)
   std::map<uintptr_t, size_t> pinned;
+  // the last key set keyset_for_locked returned, by the caller's key array
+  // (commit.cpp's speculative VerifyCommit launches with it, and checks the
+  // keys' bytes while the kernel runs); cleared when that set is evicted
+  uint32_t spec_min = 2048;  // CMTV_SPEC_MIN; CMTV_SPEC=0: 0 (off)
+  const uint8_t* guess_pk = nullptr;
+  size_t guess_n = 0;
+  const cmtv_keyset* guess_ks = nullptr;
   // cached key sets evicted while a pipeline call had them pinned
   std::vector<cmtv_keyset*> zombies;
   cmtv::PipeWorkspace* pipe_ws = nullptr;
@@ -1009,6 +1019,14 @@ struct HostBatch {
   const uint8_t* tflag = nullptr;
   const int64_t* sec = nullptr;
   const int32_t* nanos = nullptr;
+  // a speculative launch (commit.cpp's speculative VerifyCommit): run once
+  // the batch's kernels are enqueued, before the call waits for them; its
+  // answer goes to *between_ok (the caller discards the verdicts on false)
+  const std::function<bool()>* between = nullptr;
+  bool* between_ok = nullptr;
+  void after_launch() const {
+    if (between) *between_ok = (*between)();
+  }
 };
 
 // Stage rows [a, b) of B on device g and enqueue sign-bytes (templated) and
@@ -1236,6 +1254,7 @@ static int run_host_batch_(cmtv_ctx* ctx, const HostBatch& B, uint8_t* out_valid
     const int rc = enqueue_shard(ctx, d0, B, 0, n, false, static_cast<uint64_t*>(dzc), o_valid, true);
     D.tag_arm = nullptr;
     if (rc != CMTV_OK) return rc;
+    B.after_launch();
     if (D.tag_used) {  // settled by the next call (settle_polled)
       if (!D.poll_ev && (e = hipEventCreateWithFlags(&D.poll_ev, hipEventDisableTiming)) != hipSuccess)
         return hip_fail(e);
@@ -1298,6 +1317,7 @@ static int run_host_batch_(cmtv_ctx* ctx, const HostBatch& B, uint8_t* out_valid
     if (rc != CMTV_OK) return rc;
   }
   *bad_dev = -1;
+  B.after_launch();
   if (P.G > 1) {
     ctx->stats.sharded_calls++;
     const int rc = gather_bitmaps(ctx, live.data(), GG, P.W, bufs);
@@ -1477,7 +1497,8 @@ int verify_templated_locked(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const ui
                             const void* tmpls, size_t n_tmpls, const uint8_t* blob, size_t blob_len,
                             const uint32_t* tidx, const uint8_t* commit_flag, const int64_t* sec,
                             const int32_t* nanos, uint32_t mode, uint8_t* out_valid, const cmtv_keyset* ks,
-                            const uint32_t* key_idx, uint32_t msg_bound) {
+                            const uint32_t* key_idx, uint32_t msg_bound, const std::function<bool()>* between,
+                            bool* between_ok) {
   // no offsets: the fused kernels of a small single-device batch build every
   // message from its template and never read them (enqueue_shard); any other
   // form gets them derived here, exactly as sb_msg_len gives them
@@ -1513,6 +1534,8 @@ int verify_templated_locked(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const ui
   B.blob_len = blob_len;
   B.tidx = tidx;
   B.tflag = commit_flag;
+  B.between = between;
+  B.between_ok = between_ok;
   B.sec = sec;
   B.nanos = nanos;
   return run_host_batch(ctx, B, out_valid, nullptr);
@@ -1606,7 +1629,7 @@ int ctx_lock(cmtv_ctx* ctx, std::unique_lock<std::mutex>& lk) {
   lk = std::unique_lock<std::mutex>(ctx->mu);
   clear_early_locked(ctx);
   // the forms of this hold's launches see one answer (keyed_form, ed_form)
-  ctx->under_load = ctx->bulk_busy.load(std::memory_order_relaxed) > 0 && ctx->lat_window_ns;
+  ctx->under_load = ctx->bulk_busy.load(std::memory_order_relaxed) > 0 && ctx->lat_window_ns && ctx->load_form;
   return hipSetDevice(ctx->devs[0].ordinal) == hipSuccess ? CMTV_OK : CMTV_ENODEV;
 }
 
@@ -1761,7 +1784,15 @@ static void read_env(cmtv_ctx* ctx) {
   }
   if (const char* v = std::getenv("CMTV_PIPELINE")) ctx->pipe_on = v[0] != '0';
   if (const char* v = std::getenv("CMTV_PIPE_DIRECT")) ctx->pipe_direct = v[0] != '0';
+  if (const char* v = std::getenv("CMTV_SPEC_MIN")) {
+    const long x = std::strtol(v, nullptr, 10);
+    if (x > 0) ctx->spec_min = (uint32_t)x;
+  }
+  if (const char* v = std::getenv("CMTV_SPEC")) {
+    if (v[0] == '0') ctx->spec_min = 0;
+  }
   if (const char* v = std::getenv("CMTV_LAT_WINDOW_MS")) ctx->lat_window_ns = 1'000'000ull * std::strtoull(v, nullptr, 10);
+  if (const char* v = std::getenv("CMTV_LOAD_FORM")) ctx->load_form = v[0] != '0';
   if (const char* v = std::getenv("CMTV_LAT_RESERVE_CUS")) {
     const long k = std::strtol(v, nullptr, 10);
     if (k >= 1 && k <= 64) ctx->lat_reserve_cus = (uint32_t)k;
@@ -2287,6 +2318,7 @@ int register_keys_locked(cmtv_ctx* ctx, size_t n_keys, const uint8_t* pk, cmtv_k
 // A cached key set leaving the cache: freed now, or by the pipeline call
 // that still has it pinned (keyset_unpin_locked).
 static void evict_keyset_locked(cmtv_ctx* ctx, cmtv_keyset* ks) {
+  if (ctx->guess_ks == ks) ctx->guess_ks = nullptr;
   if (ks->pins > 0) {
     ks->evicted = true;
     ctx->zombies.push_back(ks);
@@ -2307,8 +2339,14 @@ void keyset_unpin_locked(cmtv_ctx* ctx, const cmtv_keyset* cks) {
 const cmtv_keyset* keyset_for_locked(cmtv_ctx* ctx, const uint8_t* pk32, size_t n_keys) {
   if (!ctx->keyset_cap || n_keys == 0) return nullptr;
   const size_t bytes = 32 * n_keys;
+  auto remember = [&](const cmtv_keyset* k) {
+    ctx->guess_pk = pk32;
+    ctx->guess_n = n_keys;
+    ctx->guess_ks = k;
+    return k;
+  };
   for (auto& e : ctx->keysets)  // compared in place: no copy of the keys per call
-    if (e.first.size() == bytes && std::memcmp(e.first.data(), pk32, bytes) == 0) return e.second;
+    if (e.first.size() == bytes && std::memcmp(e.first.data(), pk32, bytes) == 0) return remember(e.second);
   std::string key(reinterpret_cast<const char*>(pk32), bytes);
   cmtv_keyset* ks = nullptr;
   if (register_keys_locked(ctx, n_keys, pk32, &ks, 0) != CMTV_OK) return nullptr;  // generic path instead
@@ -2317,7 +2355,17 @@ const cmtv_keyset* keyset_for_locked(cmtv_ctx* ctx, const uint8_t* pk32, size_t 
     ctx->keysets.erase(ctx->keysets.begin());
   }
   ctx->keysets.emplace_back(std::move(key), ks);
-  return ks;
+  return remember(ks);
+}
+
+const cmtv_keyset* keyset_guess_locked(const cmtv_ctx* ctx, const uint8_t* pk32, size_t n_keys) {
+  return ctx->guess_ks && ctx->guess_pk == pk32 && ctx->guess_n == n_keys ? ctx->guess_ks : nullptr;
+}
+
+uint32_t spec_min(const cmtv_ctx* ctx) { return ctx->spec_min; }
+
+bool keyset_holds_locked(const cmtv_keyset* ks, const uint8_t* pk32, size_t n_keys) {
+  return ks->n == n_keys && std::memcmp(ks->pk.data(), pk32, 32 * n_keys) == 0;
 }
 
 bool keyset_cache_enabled(const cmtv_ctx* ctx) { return ctx->keyset_cap != 0; }
@@ -2390,22 +2438,31 @@ void live_devices_locked(cmtv_ctx* ctx, std::vector<size_t>& out) { out = ctx->l
 static hipError_t bulk_lane_init(cmtv_ctx* ctx, CmtvDev& D) {
   BulkLane& L = D.bulk;
   if (L.exec) return hipSuccess;
-  int least = 0, greatest = 0;
-  (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
-  hipError_t e = hipStreamCreateWithFlags(&L.copy, hipStreamNonBlocking);
-  // the lane's kernels yield to other calls' (a 150-validator VerifyCommit
-  // behind a multi-ms chunk): lowest priority
-  if (e == hipSuccess) e = hipStreamCreateWithPriority(&L.exec, hipStreamNonBlocking, least);
+  // Every stream of the lane gets a hardware queue of its own (a CU-masked
+  // stream has one; plain streams share the process's GPU_MAX_HW_QUEUES
+  // queues round-robin). On a shared queue the device's normal stream -- a
+  // 150-validator VerifyCommit -- waits behind whatever the lane queued
+  // before it: the barrier packet of an 80 MB chunk DMA, a 2.7 ms keyed
+  // launch (round 6: p99 1.12 ms under a configs[2] load with the copy and
+  // exec streams plain, bench latency_150_under_load).
+  int cus = 0;
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, D.ordinal);
+  L.cus = (uint32_t)std::max(cus, 1);
+  const uint32_t words = (L.cus + 31) / 32;
+  std::vector<uint32_t> all(words, 0);
+  for (uint32_t c = 0; c < L.cus; c++) all[c / 32] |= 1u << (c % 32);
+  auto own_queue = [&](hipStream_t* st) {
+    if (hipExtStreamCreateWithCUMask(st, words, all.data()) == hipSuccess) return hipSuccess;
+    (void)hipGetLastError();
+    return hipStreamCreateWithFlags(st, hipStreamNonBlocking);
+  };
+  hipError_t e = own_queue(&L.copy);
+  if (e == hipSuccess) e = own_queue(&L.exec);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&L.scratch.done, hipEventDisableTiming);
   if (e == hipSuccess) {
     // the masked stream: every CU but one in each 32 of the first
     // 32 x lat_reserve_cus (one per XCD on MI355X's 8 x 32)
-    int cus = 0;
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, D.ordinal);
-    L.cus = (uint32_t)std::max(cus, 1);
-    const uint32_t words = (L.cus + 31) / 32;
-    std::vector<uint32_t> mask(words, 0);
-    for (uint32_t c = 0; c < L.cus; c++) mask[c / 32] |= 1u << (c % 32);
+    std::vector<uint32_t> mask = all;
     const uint32_t reserved = reserved_cus(ctx, L.cus);
     for (uint32_t k = 0; k < reserved; k++) mask[k] &= ~1u;
     L.masked_waves = 8 * (L.cus - reserved);

@@ -3,6 +3,7 @@
 #pragma once
 #include <stdint.h>
 #include <stddef.h>
+#include <functional>
 #include <mutex>
 #include <vector>
 
@@ -37,10 +38,12 @@ int verify_templated_locked(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const ui
                             const uint32_t* tidx, const uint8_t* commit_flag, const int64_t* sec,
                             const int32_t* nanos, uint32_t mode, uint8_t* out_valid,
                             const cmtv_keyset* ks = nullptr, const uint32_t* key_idx = nullptr,
-                            uint32_t msg_bound = 0);
+                            uint32_t msg_bound = 0, const std::function<bool()>* between = nullptr,
+                            bool* between_ok = nullptr);
 // (msg_off null: no message offsets, every message at most msg_bound bytes;
 // derived from the templates here unless the fused small-batch path, which
-// never reads them, runs the batch)
+// never reads them, runs the batch; between: run once the kernels are
+// enqueued, before the wait -- its answer in *between_ok)
 
 // A single commit's n contiguous 64-byte signatures -- and, for the generic
 // kernels (pk set: the validator set's n packed 32-byte keys), its keys --
@@ -57,6 +60,14 @@ void clear_early_locked(cmtv_ctx* ctx);
 // cmtv_keyset_cache: the registered key set of these n 32-byte keys (built on
 // first use), or NULL when the cache is off or registration failed.
 const cmtv_keyset* keyset_for_locked(cmtv_ctx* ctx, const uint8_t* pk32, size_t n_keys);
+// The set keyset_for_locked last returned for this very key array (pointer
+// and count; no byte compared), or NULL; and whether a set holds exactly
+// these keys (the byte compare).
+const cmtv_keyset* keyset_guess_locked(const cmtv_ctx* ctx, const uint8_t* pk32, size_t n_keys);
+bool keyset_holds_locked(const cmtv_keyset* ks, const uint8_t* pk32, size_t n_keys);
+// The speculative VerifyCommit's threshold in signatures (commit.cpp
+// verify_commit_spec): CMTV_SPEC_MIN (default 2,048), 0 with CMTV_SPEC=0.
+uint32_t spec_min(const cmtv_ctx* ctx);
 bool keyset_cache_enabled(const cmtv_ctx* ctx);
 
 // Host-side phase clock (CMTV_HOST_PHASES=1, read at open): where a call's

@@ -12,11 +12,13 @@
 // ed25519.Verify (oracle/cmtv_oracle.c). It does so lazily, when the chunk is
 // waited for, so a host that rewrote a slot's staging while its chunk was in
 // flight reads back wrong verdicts. Test infrastructure only.
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -72,6 +74,11 @@ struct cmtv_ctx {
   uint64_t direct_chunks = 0;
   bool keyset_fail = false;  // registration fails (the pipeline packs direct chunks after all)
   std::atomic<uint64_t> latency_calls{0};
+  const uint8_t* guess_pk = nullptr;  // keyset_guess_locked (evicted sets stay allocated until close)
+  size_t guess_n = 0;
+  const cmtv_keyset* guess_ks = nullptr;
+  uint64_t spec_calls = 0, spec_ok = 0;  // speculative launches, and those whose checks held
+  uint32_t spec_min = 2048;               // CMTV_SPEC_MIN / CMTV_SPEC at fake_open
   uint64_t masked_chunks = 0;
 };
 
@@ -169,8 +176,14 @@ int verify_host_locked(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_t
 int verify_templated_locked(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_t* sig, const uint32_t* msg_off,
                             const void* tmpls, size_t n_tmpls, const uint8_t* blob, size_t, const uint32_t* tidx,
                             const uint8_t* commit_flag, const int64_t* sec, const int32_t* nanos, uint32_t mode,
-                            uint8_t* out_valid, const cmtv_keyset* ks, const uint32_t* key_idx, uint32_t msg_bound) {
+                            uint8_t* out_valid, const cmtv_keyset* ks, const uint32_t* key_idx, uint32_t msg_bound,
+                            const std::function<bool()>* between, bool* between_ok) {
   ctx->signatures += n;
+  if (between) {  // "after the launch" (the fake verifies below)
+    *between_ok = (*between)();
+    ctx->spec_calls++;
+    ctx->spec_ok += *between_ok ? 1 : 0;
+  }
   if (ctx->noverify) {  // host-cost runs (pipebench): nothing of the device's work
     std::memset(out_valid, 1, n);
     return CMTV_OK;
@@ -197,11 +210,21 @@ int verify_templated_locked(cmtv_ctx* ctx, size_t n, const uint8_t* pk, const ui
                        out_valid);
 }
 
+const cmtv_keyset* keyset_guess_locked(const cmtv_ctx* ctx, const uint8_t* pk32, size_t n_keys) {
+  return ctx->guess_ks && ctx->guess_pk == pk32 && ctx->guess_n == n_keys ? ctx->guess_ks : nullptr;
+}
+uint32_t spec_min(const cmtv_ctx* ctx) { return ctx->spec_min; }
+bool keyset_holds_locked(const cmtv_keyset* ks, const uint8_t* pk32, size_t n_keys) {
+  return ks->n == n_keys && std::memcmp(ks->pk.data(), pk32, 32 * n_keys) == 0;
+}
+
 const cmtv_keyset* keyset_for_locked(cmtv_ctx* ctx, const uint8_t* pk32, size_t n_keys) {
   if (!ctx->keyset_cap || !n_keys || ctx->keyset_fail) return nullptr;
   std::string key(reinterpret_cast<const char*>(pk32), 32 * n_keys);
+  ctx->guess_pk = pk32;
+  ctx->guess_n = n_keys;
   for (auto& e : ctx->keysets)
-    if (e.first == key) return e.second;
+    if (e.first == key) return ctx->guess_ks = e.second;
   auto* ks = new cmtv_keyset();
   ks->n = n_keys;
   ks->pk.assign(pk32, pk32 + 32 * n_keys);
@@ -212,7 +235,7 @@ const cmtv_keyset* keyset_for_locked(cmtv_ctx* ctx, const uint8_t* pk32, size_t 
     ctx->keysets.erase(ctx->keysets.begin());
   }
   ctx->keysets.emplace_back(std::move(key), ks);
-  return ks;
+  return ctx->guess_ks = ks;
 }
 
 void keyset_pin_locked(const cmtv_keyset* ks) { const_cast<cmtv_keyset*>(ks)->pins++; }
@@ -443,6 +466,8 @@ extern "C" cmtv_ctx* fake_open(size_t n_devs, unsigned threads, size_t pipe_min,
   for (size_t d = 0; d < n_devs; d++) c->live.push_back(d);
   c->slots.assign(n_devs, std::vector<FakeSlot>(cmtv::kBulkSlotsMax));
   c->failed.assign(n_devs, false);
+  if (const char* v = std::getenv("CMTV_SPEC_MIN")) c->spec_min = (uint32_t)std::max(1l, std::strtol(v, nullptr, 10));
+  if (const char* v = std::getenv("CMTV_SPEC")) c->spec_min = v[0] == '0' ? 0 : c->spec_min;
   return c;
 }
 
@@ -485,6 +510,8 @@ extern "C" void fake_counts(cmtv_ctx* c, uint64_t* out) {
   out[3] = c->retired;
   out[4] = c->keyed_chunks;
   out[5] = c->direct_chunks;
+  out[6] = c->spec_calls;
+  out[7] = c->spec_ok;
 }
 
 extern "C" void fake_close(cmtv_ctx* c) {

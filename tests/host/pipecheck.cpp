@@ -430,7 +430,7 @@ int race(const std::vector<CommitData>& chain, const std::vector<const VSet*>& v
   pipe.join();
   single.join();
   other.join();
-  uint64_t cnt[6];
+  uint64_t cnt[8];
   fake_counts(ctx, cnt);
   fake_close(ctx);
   if (!cnt[5]) {
@@ -473,7 +473,80 @@ int check_template_lens() {
   return bad;
 }
 
+// Single-commit cmtv_verify_commit with the keyset cache, the speculative
+// path on (CMTV_SPEC_MIN=1): every commit twice (the first call registers its
+// set, the second launches on the guessed set before checking anything per
+// signature), against the reference loops; then a set whose key bytes change
+// in place between calls (the guess must be refuted by the byte compare).
+int check_single(const std::vector<CommitData>& chain, const std::vector<const VSet*>& vals_of) {
+  int bad = 0;
+  uint64_t spec = 0, spec_ok = 0, cnt[8];
+  for (uint32_t kind = 0; kind < 3; kind++) {
+    cmtv_ctx* ctx = fake_open(1, 2, 1, 1u << 20, 3, true, 4, -1);
+    for (int pass = 0; pass < 2; pass++)
+      for (size_t i = 0; i < chain.size(); i++) {
+        const Outcome o = reference(kind, 0, *vals_of[i], chain[i], 1, 3);
+        cmtv_commit_result res{};
+        char msg[512];
+        const int rc = cmtv_verify_commit(ctx, kind, 0, kChain, sizeof kChain - 1, &vals_of[i]->vs, &chain[i].want,
+                                          chain[i].height, &chain[i].c, 1, 3, &res, msg, sizeof msg);
+        if (rc != o.rc || (rc != CMTV_OK && (res.code != o.code || res.sig_index != o.index))) {
+          if (bad++ < 10)
+            std::fprintf(stderr, "single kind %u pass %d commit %zu: rc %d code %d idx %d, ref rc %d code %d idx %d\n",
+                         kind, pass, i, rc, res.code, res.sig_index, o.rc, o.code, o.index);
+        }
+      }
+    fake_counts(ctx, cnt);
+    spec += cnt[6];
+    spec_ok += cnt[7];
+    fake_close(ctx);
+  }
+  // speculation ran (VerifyCommit / Light), held where the commit is clean and
+  // was refuted where it is not (faulty heights)
+  if (!spec || spec_ok == spec || !spec_ok) {
+    std::fprintf(stderr, "single: %llu speculative launches, %llu held\n", (unsigned long long)spec,
+                 (unsigned long long)spec_ok);
+    bad++;
+  }
+  // the keys of set A rewritten in place with another set's key at index 3
+  const CommitData& d = chain[0];
+  const VSet& A = *d.set;
+  VSet A2 = A;  // vectors copied; pointers re-aimed below
+  std::vector<uint8_t> keys(A.pk);
+  A2.vs.pubkeys = keys.data();
+  A2.vs.pk_off = A.pk_off.data();
+  A2.vs.voting_power = A.power.data();
+  A2.vs.addrs = A.addrs.data();
+  A2.vs.proposer_priority = A.prio.data();
+  cmtv_ctx* ctx = fake_open(1, 1, 1, 1u << 20, 3, true, 4, -1);
+  for (int round = 0; round < 3; round++) {
+    if (round == 2) std::memcpy(&keys[32 * 3], &keys[32 * 4], 32);  // same pointer, other bytes
+    std::memcpy(A2.pk.data(), keys.data(), keys.size());
+    A2.vs.pubkeys = keys.data();
+    const Outcome o = reference(0, 0, A2, d, 1, 3);
+    cmtv_commit_result res{};
+    const int rc = cmtv_verify_commit(ctx, 0, 0, kChain, sizeof kChain - 1, &A2.vs, &d.want, d.height, &d.c, 1, 3,
+                                      &res, nullptr, 0);
+    if (rc != o.rc || (rc != CMTV_OK && (res.code != o.code || res.sig_index != o.index))) {
+      bad++;
+      std::fprintf(stderr, "single, keys rewritten (round %d): rc %d code %d idx %d, ref rc %d idx %d\n", round, rc,
+                   res.code, res.sig_index, o.rc, o.index);
+    }
+    if (round == 2 && (rc != CMTV_ECOMMIT || res.sig_index != 3)) bad++;  // key 3 changed: its signature fails
+  }
+  fake_counts(ctx, cnt);
+  if (cnt[6] != 2 || cnt[7] != 1) {  // rounds 1 and 2 speculate; round 2's guess is refuted
+    std::fprintf(stderr, "single, keys rewritten: %llu speculative launches, %llu held\n",
+                 (unsigned long long)cnt[6], (unsigned long long)cnt[7]);
+    bad++;
+  }
+  fake_close(ctx);
+  std::printf("single: %zu commits x 3 kinds x 2, %d mismatches\n", chain.size(), bad);
+  return bad;
+}
+
 int main(int argc, char** argv) {
+  setenv("CMTV_SPEC_MIN", "1", 1);  // the speculative single-commit path at any size
   const int64_t heights = argc > 1 ? std::atoll(argv[1]) : 240;
   if (check_template_lens()) return 1;
   const bool race_mode = argc > 2 && std::strcmp(argv[2], "race") == 0;
@@ -502,6 +575,7 @@ int main(int argc, char** argv) {
       d.c.sig_off = d.sig_off.data();
     }
   if (race_mode) return race(chain, vals_of, 6);
+  if (check_single(chain, vals_of)) return 1;
   struct Cfg {
     const char* name;
     size_t devs;
@@ -547,7 +621,7 @@ int main(int argc, char** argv) {
         fake_set_direct(ctx, c.direct);
         fake_set_keyset_fail(ctx, c.keyset_fail);
         const Run r = run(ctx, kind, mode, chain, vals_of, c.lay);
-        uint64_t cnt[6];
+        uint64_t cnt[8];
         fake_counts(ctx, cnt);
         fake_close(ctx);
         expect_same(c.name, base, r);

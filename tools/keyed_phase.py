@@ -60,6 +60,9 @@ def main():
         buf = np.zeros(wgs * 5 * SLOTS, np.uint64)
         assert L.cmtv_debug_phase_times(buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), buf.size) == 0
         st = buf.reshape(wgs, 5, SLOTS).astype(np.int64)
+        simd = (st[:, :, 6] >> 4) & 3  # HW_ID of each wave: its SIMD
+        shares = {f"wave{w}": int((simd[:, w][:, None] == np.delete(simd, w, axis=1)).any(axis=1).sum())
+                  for w in range(5)}
         t0 = st[:, :, 0].min(axis=1)
         st = st - t0[:, None, None]
         q, dec, hsh = st[:, :3, :], st[:, 3, :], st[:, 4, :]
@@ -75,6 +78,8 @@ def main():
             "barrier_release_median": med(q[:, :, 2].max(axis=1)),
             "quads_wait_for_R_median": med(np.maximum(q[:, :, 2].max(axis=1) - q[:, :, 1].max(axis=1), 0)),
             "after_barrier_to_exit_median": med(end - q[:, :, 2].max(axis=1)),
+            "simd_of_wave_first_wg": [int(x) for x in simd[0]],
+            "workgroups_where_wave_shares_its_simd": shares,
         }
         print(name, json.dumps(out[name]), flush=True)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)

@@ -1030,7 +1030,7 @@ def latency_150(ctx, mode, iters):
     return res
 
 
-def latency_150_under_load(mode, iters, load_heights=30_000, gap_ms=1.0):
+def latency_150_under_load(mode, iters, load_heights=30_000, gap_ms=1.0, windows=None):
     """p50 / p99 of a 150-validator
     VerifyCommit (cmtv_verify_commit, packed once, keyset cache on) while
     another thread keeps running cmtv_verify_commits over load_heights x
@@ -1046,7 +1046,8 @@ def latency_150_under_load(mode, iters, load_heights=30_000, gap_ms=1.0):
     consensus commits come a block time apart; back to back, they hold the
     context lock nearly all the time and starve the load's submissions, so
     the "loaded" numbers would be of an idle GPU); the load's own rate over
-    the window is reported beside them."""
+    the window is reported beside them. windows: a list that gets each
+    loaded call's (start, end) CLOCK_MONOTONIC ns (tools/lat_trace.py)."""
     import threading
 
     from cometbft_amd import Context
@@ -1079,9 +1080,16 @@ def latency_150_under_load(mode, iters, load_heights=30_000, gap_ms=1.0):
     def gap():
         time.sleep(gap_ms * 1e-3)  # releases the GIL: the load thread's Python runs here
 
+    timed = call
+    if windows is not None:
+        def timed():
+            t0 = time.monotonic_ns()
+            call()
+            windows.append((t0, time.monotonic_ns()))
+
     s_load0 = ctx.stats()["signatures"]
     t_win = time.perf_counter()
-    loaded = _p50_p99_inner(call, gap, iters, warm=20)
+    loaded = _p50_p99_inner(timed, gap, iters, warm=20)
     t_win = time.perf_counter() - t_win
     s_load = ctx.stats()["signatures"] - s_load0 - 150 * iters
     stop.set()

@@ -76,7 +76,7 @@ class cmtv_stats(ctypes.Structure):
                 ("live_devices", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
                 ("timed_calls", ctypes.c_uint64), ("rccl_failures", ctypes.c_uint64),
                 ("polled_calls", ctypes.c_uint64), ("direct_chunks", ctypes.c_uint64),
-                ("masked_chunks", ctypes.c_uint64)]
+                ("masked_chunks", ctypes.c_uint64), ("isolated_calls", ctypes.c_uint64)]
 
 
 class cmtv_device_stats(ctypes.Structure):

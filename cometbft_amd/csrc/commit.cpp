@@ -17,6 +17,7 @@
 #include <functional>
 #include <map>
 #include <new>
+#include <optional>
 #include <random>
 #include <string>
 #include <unordered_map>
@@ -796,6 +797,9 @@ static int cmtv_verify_commit_impl(cmtv_ctx* ctx, uint32_t kind, uint32_t mode, 
   std::unique_lock<std::mutex> lk;
   rc = cmtv::ctx_lock(ctx, lk);
   if (rc != CMTV_OK) return rc;
+  // beside a pipeline call: the CUs its chunks leave free (released before
+  // the lock)
+  cmtv::LatencyStreams lat_streams(ctx);
   // the early-staged signatures below belong to this call only: forgotten on
   // every exit (a preamble error or an empty plan runs no batch), before the
   // lock is released
@@ -876,6 +880,9 @@ static int cmtv_verify_commits_impl(cmtv_ctx* ctx, uint32_t kind, uint32_t mode,
   std::unique_lock<std::mutex> lk;
   int rc = cmtv::ctx_lock(ctx, lk);
   if (rc != CMTV_OK) return rc;
+  // a small call beside a pipeline call: the CUs its chunks leave free
+  std::optional<cmtv::LatencyStreams> lat_streams;
+  if (n_sigs <= 4096) lat_streams.emplace(ctx);
   const uint64_t t0 = cmtv::phase_now(ctx);
   SigBatch B;
   const bool prefetch = cmtv::cache_enabled(ctx);

@@ -35,6 +35,15 @@
 #include "signbytes.h"
 #include "verify_core.h"
 
+// The small-batch (latency) forms raise their waves' issue priority: beside a
+// pipeline's bulk launch (k_verify_keyed_batch, k_sign_bytes at priority 0)
+// a 150-validator commit's workgroup lands on a SIMD that already holds bulk
+// waves, and the SIMD's oldest-first arbitration starves the younger wave
+// (round 6, tools/lat_trace_report.py: its kernel ran 2-2.7 ms instead of
+// 0.05 ms while the bulk launch still had milliseconds to go). Within one
+// kernel every wave has the same priority, so alone it changes nothing.
+#define CMTV_URGENT() __builtin_amdgcn_s_setprio(2)
+
 // Minimum waves per SIMD the verify kernel is compiled for (the second
 // __launch_bounds__ argument): caps VGPRs at 512 / waves.
 #ifndef CMTV_QUAD_WAVES_PER_EU
@@ -208,6 +217,7 @@ __global__ __launch_bounds__(256, CMTV_QUAD_WAVES_PER_EU) void k_verify_quad_hs(
     uint32_t n, const uint32_t* __restrict__ pk, const uint32_t* __restrict__ sig, const uint8_t* __restrict__ msg,
     const uint32_t* __restrict__ off, const uint32_t* __restrict__ btab, uint8_t* __restrict__ out_valid,
     uint64_t* __restrict__ out_bitmap, uint32_t force_wide, SbFuse sb, uint32_t hs_tune) {
+  CMTV_URGENT();
   const uint32_t wave = threadIdx.x >> 6, t = threadIdx.x & 63;
   const uint32_t base = blockIdx.x * 48;
   const int comb_pre = hs_comb_pre(hs_tune, sb.tmpls ? kHsCombPreFused : kHsCombPre);
@@ -301,6 +311,7 @@ __global__ __launch_bounds__(128, CMTV_QUAD_WAVES_PER_EU) void k_verify_oct_spli
     uint32_t n, const uint32_t* __restrict__ pk, const uint32_t* __restrict__ sig, const uint8_t* __restrict__ msg,
     const uint32_t* __restrict__ off, const uint32_t* __restrict__ btab, uint8_t* __restrict__ out_valid,
     uint64_t* __restrict__ out_bitmap, uint32_t force_wide, SbFuse sb) {
+  CMTV_URGENT();
   const uint32_t t = threadIdx.x & 63;
   const uint32_t gid = blockIdx.x * 64 + t;
   const uint32_t s = gid >> 3;
@@ -505,6 +516,7 @@ __global__ __launch_bounds__(256, 1) void k_verify_row_split(
     uint32_t n, const uint32_t* __restrict__ pk, const uint32_t* __restrict__ sig, const uint8_t* __restrict__ msg,
     const uint32_t* __restrict__ off, const uint32_t* __restrict__ btab, uint8_t* __restrict__ out_valid,
     uint64_t* __restrict__ out_bitmap, uint32_t force_wide, SbFuse sb, RowSlot slot) {
+  CMTV_URGENT();
   const uint32_t wave = threadIdx.x >> 6, t = threadIdx.x & 63;
   const uint32_t base = blockIdx.x * 3;
   __shared__ uint32_t prep[3][SIG_PREP_WORDS + 1];
@@ -578,6 +590,7 @@ __global__ __launch_bounds__(256, 1) void k_verify_row4_split(
     uint32_t n, const uint32_t* __restrict__ pk, const uint32_t* __restrict__ sig, const uint8_t* __restrict__ msg,
     const uint32_t* __restrict__ off, const uint32_t* __restrict__ btab, uint8_t* __restrict__ out_valid,
     uint64_t* __restrict__ out_bitmap, uint32_t force_wide, SbFuse sb, RowSlot slot) {
+  CMTV_URGENT();
   const uint32_t wave = threadIdx.x >> 6, t = threadIdx.x & 63;
   const uint32_t s = blockIdx.x;
   const uint32_t i = s < n ? s : n - 1;
@@ -676,6 +689,7 @@ __global__ __launch_bounds__(256, 1) void k_verify_keyed_row_split(
     const uint8_t* __restrict__ msg, const uint32_t* __restrict__ off, const uint32_t* __restrict__ keys_pk,
     const uint8_t* __restrict__ keys_ok, const uint32_t* __restrict__ ktabs, const uint32_t* __restrict__ btab,
     uint8_t* __restrict__ out_valid, uint64_t* __restrict__ out_bitmap, RowSlot slot, SbFuse sb) {
+  CMTV_URGENT();
   const uint32_t wave = threadIdx.x >> 6, t = threadIdx.x & 63;
   const uint32_t s = blockIdx.x;
   const uint32_t i = s < n ? s : n - 1;
@@ -959,6 +973,7 @@ __global__ __launch_bounds__(320, 1) void k_verify_keyed_quad_split(
     const uint8_t* __restrict__ msg, const uint32_t* __restrict__ off, const uint32_t* __restrict__ keys_pk,
     const uint8_t* __restrict__ keys_ok, const uint32_t* __restrict__ ktabs, uint8_t* __restrict__ out_valid, uint64_t* __restrict__ out_bitmap, uint32_t k_wait, uint32_t* __restrict__ diag,
     const uint32_t* __restrict__ btab, SbFuse sb) {
+  CMTV_URGENT();
   const uint32_t wave = threadIdx.x >> 6, t = threadIdx.x & 63;
   const uint32_t base = blockIdx.x * 48;
   __shared__ uint32_t tks[48][9];

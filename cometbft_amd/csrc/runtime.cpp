@@ -395,6 +395,13 @@ struct BulkLane {
   // the reserved ones (its own hardware queue, cu_mask), and the waves one
   // round of it holds at two per SIMD (the keyed batch kernel's occupancy)
   hipStream_t exec_masked = nullptr;
+  // ... and the device's latency stream while a pipeline call is in flight
+  // (LatencyStreams): the reserved CUs only, so a 150-validator commit's
+  // workgroups never share a CU -- its SIMDs, its instruction cache (one per
+  // CU pair) -- with the bulk launch's waves; lat_in / lat_out order it
+  // after / before the device's normal stream
+  hipStream_t lat = nullptr;
+  hipEvent_t lat_in = nullptr, lat_out = nullptr;
   uint32_t cus = 0, masked_waves = 0;
   BulkSlot slot[cmtv::kBulkSlotsMax];
   Scratch scratch;
@@ -563,12 +570,21 @@ struct cmtv_ctx {
   // hold in one round; while a pipeline call is in flight (bulk_busy) the
   // latency call takes a form that fits those CUs (under_load, snapshotted at
   // each lock hold). CMTV_LAT_WINDOW_MS (default 10,000; 0: never masked),
-  // CMTV_LAT_RESERVE_CUS (default 8); CMTV_LOAD_FORM=0 keeps the latency
+  // CMTV_LAT_RESERVE_CUS (default 16); CMTV_LOAD_FORM=0 keeps the latency
   // call's idle form under load.
   std::atomic<uint64_t> last_latency_ns{0};
   bool load_form = true;
+  // a pipeline call is in flight (snapshotted with under_load): a registered-
+  // key latency batch then reads its staging in place (mapped host memory)
+  // rather than queue its H2D copy on the copy engines behind the pipeline's
+  // chunk DMAs; CMTV_LOAD_ZC=0 copies it as when idle
+  bool bulk_now = false, load_zc = true;
   uint64_t lat_window_ns = 10'000'000'000ull;
-  uint32_t lat_reserve_cus = 8;
+  uint32_t lat_reserve_cus = 16;
+  // latency calls beside a pipeline run on the reserved CUs only
+  // (LatencyStreams; CMTV_LAT_ISOLATE=0: on the whole device, beside the
+  // bulk waves)
+  bool lat_isolate = true;
   std::atomic<int> bulk_busy{0};
   bool under_load = false;
   uint32_t cus = 0;  // CUs per device (the smallest of the context's)
@@ -1094,7 +1110,7 @@ static int enqueue_shard(cmtv_ctx* ctx, size_t g, const HostBatch& B, size_t a, 
                      dev_bytes <= D.d_in.cap;
   const bool early_pk = early && !keyed && D.early_pk && D.early_pk == B.pk + 32 * a && m == D.early_n;
   D.early_src = D.early_pk = nullptr;
-  const bool zc = !early && !keyed && zero_copy && ctx->zc_in &&
+  const bool zc = !early && (!keyed || (ctx->bulk_now && ctx->load_zc)) && zero_copy && ctx->zc_in &&
                   (fuse || (!tpl && ctx->zc_host_in && max_len <= kSbFuseMaxMsg));
   // split: the early-staged signatures (and keys) in HBM, the rest -- the
   // fused helper's templates, flags and timestamps, ~17 bytes a signature --
@@ -1563,6 +1579,8 @@ int stage_sigs_early_locked(cmtv_ctx* ctx, const uint8_t* sigs, size_t n, const 
   // nor is the copy worth its own latency for the keyed row kernel's
   // commits (150 validators: p50 0.0566 with it, 0.0534 without)
   if (!pk && keyed_form(ctx, n) == kKeyedRow) return CMTV_OK;
+  // nor beside a pipeline call (bulk_now): the copy would queue behind its DMAs
+  if (!pk && ctx->bulk_now && ctx->load_zc) return CMTV_OK;
   CmtvDev& D = ctx->devs[ctx->live[0]];
   if (hipSetDevice(D.ordinal) != hipSuccess) return CMTV_ENODEV;
   hipError_t e;
@@ -1629,7 +1647,8 @@ int ctx_lock(cmtv_ctx* ctx, std::unique_lock<std::mutex>& lk) {
   lk = std::unique_lock<std::mutex>(ctx->mu);
   clear_early_locked(ctx);
   // the forms of this hold's launches see one answer (keyed_form, ed_form)
-  ctx->under_load = ctx->bulk_busy.load(std::memory_order_relaxed) > 0 && ctx->lat_window_ns && ctx->load_form;
+  ctx->bulk_now = ctx->bulk_busy.load(std::memory_order_relaxed) > 0;
+  ctx->under_load = ctx->bulk_now && ctx->lat_window_ns && ctx->load_form;
   return hipSetDevice(ctx->devs[0].ordinal) == hipSuccess ? CMTV_OK : CMTV_ENODEV;
 }
 
@@ -1793,6 +1812,8 @@ static void read_env(cmtv_ctx* ctx) {
   }
   if (const char* v = std::getenv("CMTV_LAT_WINDOW_MS")) ctx->lat_window_ns = 1'000'000ull * std::strtoull(v, nullptr, 10);
   if (const char* v = std::getenv("CMTV_LOAD_FORM")) ctx->load_form = v[0] != '0';
+  if (const char* v = std::getenv("CMTV_LOAD_ZC")) ctx->load_zc = v[0] != '0';
+  if (const char* v = std::getenv("CMTV_LAT_ISOLATE")) ctx->lat_isolate = v[0] != '0';
   if (const char* v = std::getenv("CMTV_LAT_RESERVE_CUS")) {
     const long k = std::strtol(v, nullptr, 10);
     if (k >= 1 && k <= 64) ctx->lat_reserve_cus = (uint32_t)k;
@@ -2374,10 +2395,11 @@ bool keyset_cache_enabled(const cmtv_ctx* ctx) { return ctx->keyset_cap != 0; }
 
 std::mutex& bulk_mutex(cmtv_ctx* ctx) { return ctx->bulk_mu; }
 
-// CUs a masked bulk lane leaves to the normal stream: CU 32k for k below
-// lat_reserve_cus (one per XCD on MI355X)
+// CUs a masked bulk lane leaves to the latency stream (bulk_lane_init): a
+// multiple of 8 (every XCD), at most a quarter of the device, 0 below 64 CUs
 static uint32_t reserved_cus(const cmtv_ctx* ctx, uint32_t cus) {
-  return std::min(ctx->lat_reserve_cus, (cus + 31) / 32);
+  if (cus < 64) return 0;
+  return std::min((ctx->lat_reserve_cus + 7) / 8 * 8, cus / 4 / 8 * 8);
 }
 
 static uint64_t now_ns_steady() {
@@ -2430,6 +2452,44 @@ bool latency_recent(const cmtv_ctx* ctx) {
   return t && now_ns_steady() - t < ctx->lat_window_ns;
 }
 
+LatencyStreams::LatencyStreams(cmtv_ctx* c) : ctx(c) {
+  // the pipeline's masked chunks leave the reserved CUs free only while the
+  // latency window is open; bulk_now (snapshotted at ctx_lock) says a
+  // pipeline call is in flight
+  if (!ctx->bulk_now || !ctx->lat_window_ns || !ctx->lat_isolate) return;
+  for (size_t g : ctx->live) {
+    CmtvDev& D = ctx->devs[g];
+    BulkLane& L = D.bulk;
+    if (!L.lat || D.failed || g >= 64) continue;
+    (void)hipSetDevice(D.ordinal);
+    // everything already on the normal stream (keyset builds, a polled
+    // launch) completes first
+    if (hipEventRecord(L.lat_in, D.stream) != hipSuccess || hipStreamWaitEvent(L.lat, L.lat_in, 0) != hipSuccess) {
+      (void)hipGetLastError();
+      continue;
+    }
+    std::swap(D.stream, L.lat);
+    swapped |= 1ull << g;
+  }
+  if (swapped) ctx->stats.isolated_calls++;
+  if (!ctx->live.empty()) (void)hipSetDevice(ctx->devs[ctx->live[0]].ordinal);
+}
+
+LatencyStreams::~LatencyStreams() {
+  for (size_t g = 0; g < 64 && swapped; g++) {
+    if (!(swapped >> g & 1)) continue;
+    CmtvDev& D = ctx->devs[g];
+    BulkLane& L = D.bulk;
+    (void)hipSetDevice(D.ordinal);
+    std::swap(D.stream, L.lat);
+    // and what the call left in flight (a polled launch retiring) precedes
+    // whatever comes next on the normal stream
+    if (hipEventRecord(L.lat_out, L.lat) != hipSuccess || hipStreamWaitEvent(D.stream, L.lat_out, 0) != hipSuccess)
+      (void)hipGetLastError();
+  }
+  if (swapped && !ctx->live.empty()) (void)hipSetDevice(ctx->devs[ctx->live[0]].ordinal);
+}
+
 BulkBusy::BulkBusy(cmtv_ctx* c) : ctx(c) { ctx->bulk_busy.fetch_add(1, std::memory_order_relaxed); }
 BulkBusy::~BulkBusy() { ctx->bulk_busy.fetch_sub(1, std::memory_order_relaxed); }
 
@@ -2460,16 +2520,38 @@ static hipError_t bulk_lane_init(cmtv_ctx* ctx, CmtvDev& D) {
   if (e == hipSuccess) e = own_queue(&L.exec);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&L.scratch.done, hipEventDisableTiming);
   if (e == hipSuccess) {
-    // the masked stream: every CU but one in each 32 of the first
-    // 32 x lat_reserve_cus (one per XCD on MI355X's 8 x 32)
-    std::vector<uint32_t> mask = all;
+    // The reserved CUs: the masked exec stream gets every other CU, the
+    // latency stream these. The driver deals a queue's CU-mask bits out
+    // XCD-major round-robin -- bit i to XCD i mod 8, then to SE (i / 8) mod
+    // 4, then to that SE's CU i / 32 (tools/cumask_probe.hip on MI355X:
+    // bits 0..7 alone run on CU 0 of SE 0 of each XCD) -- and the dispatcher
+    // deals a kernel's workgroups to the XCDs round-robin, so the reserve
+    // must hold CUs on every XCD (an XCD whose share of a mask is empty runs
+    // the queue on all its CUs). Taken in whole CU pairs (the pair shares
+    // one instruction cache): bits 0..7 and 32..39 are CUs 0 and 1 of SE 0
+    // on each XCD, then 8..15 and 40..47 (SE 1), and so on.
+    std::vector<uint32_t> mask = all, lat(words, 0);
     const uint32_t reserved = reserved_cus(ctx, L.cus);
-    for (uint32_t k = 0; k < reserved; k++) mask[k] &= ~1u;
+    for (uint32_t k = 0; k < reserved; k++) {
+      const uint32_t pair = k / 16, cu_bit = (k / 8) % 2, xcd = k % 8;
+      const uint32_t b = cu_bit * 32 + pair * 8 + xcd;
+      mask[b / 32] &= ~(1u << (b % 32));
+      lat[b / 32] |= 1u << (b % 32);
+    }
     L.masked_waves = 8 * (L.cus - reserved);
     if (reserved == 0 || L.cus <= reserved ||
         hipExtStreamCreateWithCUMask(&L.exec_masked, words, mask.data()) != hipSuccess) {
       (void)hipGetLastError();
       L.exec_masked = nullptr;  // no masking: chunks keep the plain exec stream
+    }
+    if (L.exec_masked && ctx->lat_isolate) {
+      if (hipExtStreamCreateWithCUMask(&L.lat, words, lat.data()) != hipSuccess ||
+          hipEventCreateWithFlags(&L.lat_in, hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&L.lat_out, hipEventDisableTiming) != hipSuccess) {
+        (void)hipGetLastError();
+        if (L.lat) (void)hipStreamDestroy(L.lat);
+        L.lat = nullptr;  // latency calls keep the normal stream
+      }
     }
   }
   for (int k = 0; k < kBulkSlotsMax && e == hipSuccess; k++) {
@@ -2502,7 +2584,11 @@ static void bulk_lane_release(CmtvDev& D) {
   if (L.exec) (void)hipStreamDestroy(L.exec);
   if (L.exec_masked) (void)hipStreamDestroy(L.exec_masked);
   if (L.copy) (void)hipStreamDestroy(L.copy);
-  L.exec = L.exec_masked = L.copy = nullptr;
+  if (L.lat) (void)hipStreamDestroy(L.lat);
+  if (L.lat_in) (void)hipEventDestroy(L.lat_in);
+  if (L.lat_out) (void)hipEventDestroy(L.lat_out);
+  L.exec = L.exec_masked = L.copy = L.lat = nullptr;
+  L.lat_in = L.lat_out = nullptr;
 }
 
 int bulk_stage(cmtv_ctx* ctx, size_t dev, int slot, const BulkLayout& L, uint8_t** host) {

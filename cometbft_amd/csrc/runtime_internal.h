@@ -159,6 +159,18 @@ struct BulkBusy {
   ~BulkBusy();
   cmtv_ctx* ctx;
 };
+// A latency call's scope (context lock held): while a pipeline call is in
+// flight and the latency window is open, each live device's normal stream
+// is swapped for its bulk lane's latency stream -- the CUs the masked bulk
+// chunks leave free -- and swapped back, ordered after it, on exit.
+struct LatencyStreams {
+  explicit LatencyStreams(cmtv_ctx* c);
+  ~LatencyStreams();
+  LatencyStreams(const LatencyStreams&) = delete;
+  LatencyStreams& operator=(const LatencyStreams&) = delete;
+  cmtv_ctx* ctx;
+  uint64_t swapped = 0;  // device indices
+};
 // live device indices, in shard order (context lock held)
 void live_devices_locked(cmtv_ctx* ctx, std::vector<size_t>& out);
 // the pinned staging of (dev, slot), grown to L.in_bytes (bulk lock held)

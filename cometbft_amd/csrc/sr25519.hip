@@ -94,6 +94,7 @@ __global__ __launch_bounds__(256, 1) void k_verify_sr25519_quad_hs(
     uint32_t n, const uint32_t* __restrict__ pk, const uint32_t* __restrict__ sig, const uint8_t* __restrict__ msg,
     const uint32_t* __restrict__ off, const uint32_t* __restrict__ btab, const uint32_t* __restrict__ prog, int nops,
     uint8_t* __restrict__ out_valid, uint64_t* __restrict__ out_bitmap, uint32_t force_wide, uint32_t hs_tune) {
+  __builtin_amdgcn_s_setprio(2);  // a latency form (kernels.hip CMTV_URGENT)
   const uint32_t wave = threadIdx.x >> 6, t = threadIdx.x & 63;
   const uint32_t base = blockIdx.x * 48;
   const int comb_pre = hs_comb_pre(hs_tune, kHsCombPreSr);

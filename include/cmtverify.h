@@ -116,6 +116,9 @@ typedef struct cmtv_stats {
   uint64_t masked_chunks;    /* pipeline chunks run on the CU-masked exec
                               stream because a latency call (a single
                               commit) came within CMTV_LAT_WINDOW_MS      */
+  uint64_t isolated_calls;   /* latency calls (a single commit, a small
+                              cmtv_verify_commits) run on the CUs those
+                              masked chunks leave free (CMTV_LAT_ISOLATE) */
 } cmtv_stats;
 
 /* One device's share of the context's work (cmtv_device_stats_get). */

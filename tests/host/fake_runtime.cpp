@@ -257,6 +257,9 @@ void note_latency(cmtv_ctx* ctx) { ctx->latency_calls++; }
 bool latency_recent(const cmtv_ctx* ctx) { return ctx->latency_calls.load() > 0; }
 BulkBusy::BulkBusy(cmtv_ctx* c) : ctx(c) {}
 BulkBusy::~BulkBusy() {}
+// no streams to swap on the fake devices
+LatencyStreams::LatencyStreams(cmtv_ctx* c) : ctx(c) {}
+LatencyStreams::~LatencyStreams() {}
 int stage_sigs_early_locked(cmtv_ctx*, const uint8_t*, size_t, const uint8_t*) { return CMTV_OK; }
 void clear_early_locked(cmtv_ctx*) {}
 void live_devices_locked(cmtv_ctx* ctx, std::vector<size_t>& out) { out = ctx->live; }

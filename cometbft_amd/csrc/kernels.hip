@@ -216,7 +216,7 @@ template <uint32_t MODE>
 __global__ __launch_bounds__(256, CMTV_QUAD_WAVES_PER_EU) void k_verify_quad_hs(
     uint32_t n, const uint32_t* __restrict__ pk, const uint32_t* __restrict__ sig, const uint8_t* __restrict__ msg,
     const uint32_t* __restrict__ off, const uint32_t* __restrict__ btab, uint8_t* __restrict__ out_valid,
-    uint64_t* __restrict__ out_bitmap, uint32_t force_wide, SbFuse sb, uint32_t hs_tune) {
+    uint64_t* __restrict__ out_bitmap, uint32_t force_wide, SbFuse sb, uint32_t hs_tune, RowSlot tags) {
   CMTV_URGENT();
   const uint32_t wave = threadIdx.x >> 6, t = threadIdx.x & 63;
   const uint32_t base = blockIdx.x * 48;
@@ -298,7 +298,13 @@ __global__ __launch_bounds__(256, CMTV_QUAD_WAVES_PER_EU) void k_verify_quad_hs(
   x = (x | (x >> 12)) & 0x000000FF000000FFull;
   x = (x | (x >> 24)) & 0xFFFFull;
   const uint32_t slice = blockIdx.x * 3 + wave;
-  if (t == 0 && out_bitmap && slice < 4 * ((n + 63) / 64)) reinterpret_cast<uint16_t*>(out_bitmap)[slice] = (uint16_t)x;
+  if (t == 0 && slice < 4 * ((n + 63) / 64)) {
+    if (tags.tagged)  // a polled host call (kernels.h RowSlot): the slice with the call's tag
+      __hip_atomic_store(tags.tagged + slice, ((uint64_t)tags.seq << 32) | x, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+    else if (out_bitmap)
+      reinterpret_cast<uint16_t*>(out_bitmap)[slice] = (uint16_t)x;
+  }
 }
 
 // The oct verifier over two waves per 8 signatures: wave 1 hashes and splits
@@ -924,12 +930,13 @@ hipError_t launch_verify(uint32_t mode, uint32_t n, const void* pk, const void* 
       // slice of every bitmap word
       const uint32_t slices = 4 * ((n + 63) / 64);
       const dim3 grid((slices + 2) / 3), block(256);
+      const RowSlot tg = row_slot ? *row_slot : RowSlot{};  // its tagged entries only
       if (go)
         hipLaunchKernelGGL(k_verify_quad_hs<MODE_GO_STDLIB>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp, fw,
-                           fz, kflags >> 16);
+                           fz, kflags >> 16, tg);
       else
         hipLaunchKernelGGL(k_verify_quad_hs<MODE_ZIP215>, grid, block, 0, s, n, pkp, sgp, mp, op, btab, vp, bp, fw, fz,
-                           kflags >> 16);
+                           kflags >> 16, tg);
       break;
     }
     default:
@@ -972,7 +979,7 @@ __global__ __launch_bounds__(320, 1) void k_verify_keyed_quad_split(
     uint32_t n, uint32_t n_keys, const uint32_t* __restrict__ key_idx, const uint32_t* __restrict__ sig,
     const uint8_t* __restrict__ msg, const uint32_t* __restrict__ off, const uint32_t* __restrict__ keys_pk,
     const uint8_t* __restrict__ keys_ok, const uint32_t* __restrict__ ktabs, uint8_t* __restrict__ out_valid, uint64_t* __restrict__ out_bitmap, uint32_t k_wait, uint32_t* __restrict__ diag,
-    const uint32_t* __restrict__ btab, SbFuse sb) {
+    const uint32_t* __restrict__ btab, SbFuse sb, RowSlot tags) {
   CMTV_URGENT();
   const uint32_t wave = threadIdx.x >> 6, t = threadIdx.x & 63;
   const uint32_t base = blockIdx.x * 48;
@@ -1083,7 +1090,13 @@ __global__ __launch_bounds__(320, 1) void k_verify_keyed_quad_split(
   x = (x | (x >> 12)) & 0x000000FF000000FFull;
   x = (x | (x >> 24)) & 0xFFFFull;
   const uint32_t slice = blockIdx.x * 3 + wave;
-  if (t == 0 && out_bitmap && slice < 4 * ((n + 63) / 64)) reinterpret_cast<uint16_t*>(out_bitmap)[slice] = (uint16_t)x;
+  if (t == 0 && slice < 4 * ((n + 63) / 64)) {
+    if (tags.tagged)  // a polled host call (kernels.h RowSlot): the slice with the call's tag
+      __hip_atomic_store(tags.tagged + slice, ((uint64_t)tags.seq << 32) | x, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+    else if (out_bitmap)
+      reinterpret_cast<uint16_t*>(out_bitmap)[slice] = (uint16_t)x;
+  }
   CMTV_STAMP5(5);
 }
 
@@ -1120,12 +1133,14 @@ hipError_t launch_verify_keyed(uint32_t mode, uint32_t n, uint32_t n_keys, const
   if (form == kKeyedQuad) {
     const uint32_t slices = 4 * ((n + 63) / 64);
     const dim3 grid((slices + 2) / 3), block(320);
+    // row_slot here: only its tagged entries (16 signatures each) and seq
+    const RowSlot tg = row_slot ? *row_slot : RowSlot{};
     if (go)
       hipLaunchKernelGGL(k_verify_keyed_quad_split<MODE_GO_STDLIB>, grid, block, 0, s, n, n_keys, ki, sgp, mp, op,
-                         keys_pk, keys_ok, ktabs, vp, bp, k_wait, diag, btab, sb);
+                         keys_pk, keys_ok, ktabs, vp, bp, k_wait, diag, btab, sb, tg);
     else
       hipLaunchKernelGGL(k_verify_keyed_quad_split<MODE_ZIP215>, grid, block, 0, s, n, n_keys, ki, sgp, mp, op,
-                         keys_pk, keys_ok, ktabs, vp, bp, k_wait, diag, btab, sb);
+                         keys_pk, keys_ok, ktabs, vp, bp, k_wait, diag, btab, sb, tg);
     return hipGetLastError();
   }
   if (form != kKeyedLane) return hipErrorInvalidValue;

@@ -88,6 +88,9 @@ constexpr size_t kShardMinDefault = 8192;
 // 4,096 vs 16,384): VerifyCommit at 8,192 0.329-0.330 -> 0.320 ms, at 10,000
 // 0.349 -> 0.341-0.343 ms; the host API unchanged. 4,096 before.
 constexpr size_t kZeroCopyMax = 12288;
+// tagged bitmap entries of a polled host batch (CmtvDev::h_tags): a row
+// launch's 32-signature words or a keyed quad launch's 16-signature slices
+constexpr size_t kTagEntries = std::max<size_t>(cmtv::kRowMaxCap / 32 + 1, 4 * ((kZeroCopyMax + 63) / 64));
 constexpr int kMaxDevices = 64;
 
 struct DevBuf {
@@ -449,6 +452,9 @@ struct CmtvDev {
   uint64_t* tag_arm = nullptr;
   uint32_t tag_seq = 0;
   bool tag_used = false;
+  // signatures per tagged entry of the launch that took the tags: 32 (row
+  // kernels' words) or 16 (the keyed quad kernel's per-wave slices)
+  uint32_t tag_width = 32;
   // A polled host call returns once its tags are in, while the row launch
   // may still be retiring (its last waves zero their ring words). poll_ev is
   // recorded after that launch; the next host call on the device -- before it
@@ -579,6 +585,9 @@ struct cmtv_ctx {
   // rather than queue its H2D copy on the copy engines behind the pipeline's
   // chunk DMAs; CMTV_LOAD_ZC=0 copies it as when idle
   bool bulk_now = false, load_zc = true;
+  // ... and waits for its stream rather than polling its kernel's tagged
+  // bitmap (run_host_batch_; CMTV_LOAD_POLL=1 polls as when idle)
+  bool load_nopoll = true;
   uint64_t lat_window_ns = 10'000'000'000ull;
   uint32_t lat_reserve_cus = 16;
   // latency calls beside a pipeline run on the reserved CUs only
@@ -718,6 +727,7 @@ static hipError_t row_slot_acquire(cmtv_ctx* ctx, CmtvDev& D, hipStream_t s, boo
     slot.tagged = D.tag_arm;
     slot.seq = D.tag_seq;
     D.tag_used = true;
+    D.tag_width = 32;
   }
   if (!D.row_pending[k] || !ctx->row_fence) return hipSuccess;
   hipError_t e = hipEventQuery(D.row_ev[k]);
@@ -800,6 +810,16 @@ static int enqueue_verify(cmtv_ctx* ctx, CmtvDev& D, size_t n, const uint8_t* d_
   RowSlot slot;
   uint32_t slot_k = 0;
   if (row && (e = row_slot_acquire(ctx, D, s, d_bitmap != nullptr, slot, slot_k)) != hipSuccess) return hip_fail(e);
+  // the quad kernel of an armed host batch (one launch) tags its 16-signature
+  // slices (as enqueue_verify_keyed's)
+  const bool qtag = !sr && form == kFormQuad && d_bitmap && D.tag_arm && n <= kChunk;
+  if (qtag) {
+    slot = RowSlot{};
+    slot.tagged = D.tag_arm;
+    slot.seq = D.tag_seq;
+    D.tag_used = true;
+    D.tag_width = 16;
+  }
   D.timing.harvest(ctx->stats, D.device_ms, D.timed_calls, false);
   Timing::Pair tp;
   const bool timed = ctx->timing_every && D.timing_seq++ % ctx->timing_every == 0;
@@ -814,7 +834,7 @@ static int enqueue_verify(cmtv_ctx* ctx, CmtvDev& D, size_t n, const uint8_t* d_
     else
       e = launch_verify(mode, cn, d_pk + 32 * c, d_sig + 64 * c, d_msg, d_off + c, D.d_btab,
                         static_cast<uint32_t*>(S.buf.p), d_valid ? d_valid + c : nullptr,
-                        d_bitmap ? d_bitmap + c / 64 : nullptr, kflags, s, sb, row ? &slot : nullptr);
+                        d_bitmap ? d_bitmap + c / 64 : nullptr, kflags, s, sb, row || qtag ? &slot : nullptr);
     if (e == hipSuccess && row) e = row_slot_release(ctx, D, s, slot_k);
     if (e != hipSuccess) {
       D.timing.abandon(tp);
@@ -876,6 +896,17 @@ static int enqueue_verify_keyed(cmtv_ctx* ctx, CmtvDev& D, const cmtv_keyset::Pe
   uint32_t slot_k = 0;
   if (krow && (e = row_slot_acquire(ctx, D, s, d_bitmap != nullptr, slot, slot_k)) != hipSuccess)
     return hip_fail(e);
+  // the keyed quad kernel of an armed host batch (one launch) tags its
+  // 16-signature slices instead of writing the bitmap: the call polls them
+  // (wait_row_tags) rather than wait for the stream
+  RowSlot qtags;
+  const bool qtag = form == kKeyedQuad && d_bitmap && D.tag_arm && n <= chunk;
+  if (qtag) {
+    qtags.tagged = D.tag_arm;
+    qtags.seq = D.tag_seq;
+    D.tag_used = true;
+    D.tag_width = 16;
+  }
   D.timing.harvest(ctx->stats, D.device_ms, D.timed_calls, false);
   Timing::Pair tp;
   const bool timed = ctx->timing_every && D.timing_seq++ % ctx->timing_every == 0;
@@ -888,7 +919,7 @@ static int enqueue_verify_keyed(cmtv_ctx* ctx, CmtvDev& D, const cmtv_keyset::Pe
                             d_off + c, K.d_pk, K.d_ok, K.d_tab, d_valid ? d_valid + c : nullptr,
                             d_bitmap ? d_bitmap + c / 64 : nullptr, form, ctx->keyed_wait, D.d_diag, kb,
                             static_cast<uint32_t*>(S.buf.p), form == kKeyedLane ? K.d_wide : nullptr, D.d_btab, s,
-                            krow ? &slot : nullptr, sb);
+                            krow ? &slot : qtag ? &qtags : nullptr, sb);
     if (e == hipSuccess && krow) e = row_slot_release(ctx, D, s, slot_k);
     if (e != hipSuccess) {
       D.timing.abandon(tp);
@@ -1216,7 +1247,7 @@ static int enqueue_shard(cmtv_ctx* ctx, size_t g, const HostBatch& B, size_t a, 
 // an entry untagged (which cannot happen) is an error, not a hang.
 static hipError_t wait_row_tags(CmtvDev& D, size_t n) {
   const uint64_t* e = static_cast<const uint64_t*>(D.h_tags.p);
-  const size_t n32 = (n + 31) / 32;
+  const size_t n32 = (n + D.tag_width - 1) / D.tag_width;  // entries
   size_t j = 0;
   auto scan = [&] {
     while (j < n32 && (uint32_t)(__atomic_load_n(e + j, __ATOMIC_ACQUIRE) >> 32) == D.tag_seq) j++;
@@ -1258,13 +1289,17 @@ static int run_host_batch_(cmtv_ctx* ctx, const HostBatch& B, uint8_t* out_valid
     // it writes the bitmap and the call waits for the stream)
     if (ctx->host_poll && !D.d_tags) {
       void* dt = nullptr;
-      if ((e = D.h_tags.ensure(8 * (kRowMaxCap / 32 + 1))) != hipSuccess) return hip_fail(e);
-      std::memset(D.h_tags.p, 0, 8 * (kRowMaxCap / 32 + 1));
+      if ((e = D.h_tags.ensure(8 * kTagEntries)) != hipSuccess) return hip_fail(e);
+      std::memset(D.h_tags.p, 0, 8 * kTagEntries);
       if ((e = hipHostGetDevicePointer(&dt, D.h_tags.p, 0)) != hipSuccess) return hip_fail(e);
       D.d_tags = static_cast<uint64_t*>(dt);
     }
-    if (ctx->host_poll && ++D.tag_seq == 0) D.tag_seq = 1;
-    D.tag_arm = ctx->host_poll ? D.d_tags : nullptr;
+    // ... but not beside a pipeline call (bulk_now): polled under a configs[2]
+    // load the 150-validator call's p99 was 1.05-1.11 ms against 0.148 ms
+    // waiting for the stream (round 6, tools/gpu_r6o.sh)
+    const bool poll = ctx->host_poll && !(ctx->bulk_now && ctx->load_nopoll);
+    if (poll && ++D.tag_seq == 0) D.tag_seq = 1;
+    D.tag_arm = poll ? D.d_tags : nullptr;
     D.tag_used = false;
     size_t o_valid = 0;
     const int rc = enqueue_shard(ctx, d0, B, 0, n, false, static_cast<uint64_t*>(dzc), o_valid, true);
@@ -1283,9 +1318,18 @@ static int run_host_batch_(cmtv_ctx* ctx, const HostBatch& B, uint8_t* out_valid
     if (D.tag_used) {
       ctx->stats.polled_calls++;
       const uint64_t* tg = static_cast<const uint64_t*>(D.h_tags.p);
-      const size_t n32 = (n + 31) / 32;
-      for (size_t w = 0; w < words; w++)
-        bm[w] = (tg[2 * w] & 0xFFFFFFFFull) | (2 * w + 1 < n32 ? (tg[2 * w + 1] & 0xFFFFFFFFull) << 32 : 0);
+      if (D.tag_width == 32) {
+        const size_t n32 = (n + 31) / 32;
+        for (size_t w = 0; w < words; w++)
+          bm[w] = (tg[2 * w] & 0xFFFFFFFFull) | (2 * w + 1 < n32 ? (tg[2 * w + 1] & 0xFFFFFFFFull) << 32 : 0);
+      } else {
+        const size_t n16 = (n + 15) / 16;
+        for (size_t w = 0; w < words; w++) {
+          uint64_t x = 0;
+          for (size_t k = 0; k < 4 && 4 * w + k < n16; k++) x |= (tg[4 * w + k] & 0xFFFFull) << (16 * k);
+          bm[w] = x;
+        }
+      }
     }
     phase_add(ctx, kPhWait, t_wait);
     const uint64_t t_post = phase_now(ctx);
@@ -1813,6 +1857,7 @@ static void read_env(cmtv_ctx* ctx) {
   if (const char* v = std::getenv("CMTV_LAT_WINDOW_MS")) ctx->lat_window_ns = 1'000'000ull * std::strtoull(v, nullptr, 10);
   if (const char* v = std::getenv("CMTV_LOAD_FORM")) ctx->load_form = v[0] != '0';
   if (const char* v = std::getenv("CMTV_LOAD_ZC")) ctx->load_zc = v[0] != '0';
+  if (const char* v = std::getenv("CMTV_LOAD_POLL")) ctx->load_nopoll = v[0] == '0';
   if (const char* v = std::getenv("CMTV_LAT_ISOLATE")) ctx->lat_isolate = v[0] != '0';
   if (const char* v = std::getenv("CMTV_LAT_RESERVE_CUS")) {
     const long k = std::strtol(v, nullptr, 10);
@@ -2463,8 +2508,12 @@ LatencyStreams::LatencyStreams(cmtv_ctx* c) : ctx(c) {
     if (!L.lat || D.failed || g >= 64) continue;
     (void)hipSetDevice(D.ordinal);
     // everything already on the normal stream (keyset builds, a polled
-    // launch) completes first
-    if (hipEventRecord(L.lat_in, D.stream) != hipSuccess || hipStreamWaitEvent(L.lat, L.lat_in, 0) != hipSuccess) {
+    // launch) completes first -- through an event only when something is
+    // still in flight there: a cross-queue wait costs the launch ~45 us
+    // (tools/lat_queue_probe.hip: 22.8 -> 69.2 us p50 for a 10 us kernel)
+    const hipError_t q = hipStreamQuery(D.stream);
+    if (q != hipSuccess && (q != hipErrorNotReady || hipEventRecord(L.lat_in, D.stream) != hipSuccess ||
+                            hipStreamWaitEvent(L.lat, L.lat_in, 0) != hipSuccess)) {
       (void)hipGetLastError();
       continue;
     }
@@ -2483,9 +2532,14 @@ LatencyStreams::~LatencyStreams() {
     (void)hipSetDevice(D.ordinal);
     std::swap(D.stream, L.lat);
     // and what the call left in flight (a polled launch retiring) precedes
-    // whatever comes next on the normal stream
-    if (hipEventRecord(L.lat_out, L.lat) != hipSuccess || hipStreamWaitEvent(D.stream, L.lat_out, 0) != hipSuccess)
+    // whatever comes next on the normal stream (an event only if needed)
+    const hipError_t q = hipStreamQuery(L.lat);
+    if (q == hipErrorNotReady) {
+      if (hipEventRecord(L.lat_out, L.lat) != hipSuccess || hipStreamWaitEvent(D.stream, L.lat_out, 0) != hipSuccess)
+        (void)hipGetLastError();
+    } else if (q != hipSuccess) {
       (void)hipGetLastError();
+    }
   }
   if (swapped && !ctx->live.empty()) (void)hipSetDevice(ctx->devs[ctx->live[0]].ordinal);
 }

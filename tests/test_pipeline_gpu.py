@@ -280,3 +280,73 @@ def test_configs2_scale_direct_from_pinned(gpu_ctx, devices):
     p.close()
     del chain
     c.close()
+
+
+@pytest.mark.parametrize("n_vals", [150, 4096])
+def test_latency_calls_beside_a_pipeline(n_vals):
+    """VerifyCommit while another thread runs a pipelined cmtv_verify_commits
+    on the same context (consensus beside blocksync, round 6): the call runs
+    on the device's latency stream -- the CUs the pipeline's masked chunks
+    leave free (runtime.cpp LatencyStreams) -- in its under-load form (the
+    registered-key quad kernel, polled through its tagged slices). Every
+    outcome equals the same call's on the idle context (clean, a flipped
+    signature, a wrong height), every load pass's outcomes are the reference
+    loop's over the known flips, and the calls did run isolated."""
+    import threading
+    import time
+
+    c = _ctx(keyset=True)
+    lat = TU.make_validator_set(c, n_vals, offset=50_000)
+    chain = TU.ReplayChain(c, TU.make_validator_set(c, N_VALS), 1, 3000, pinned=c)
+    h = 77
+    b, keep_b = TU.block_id_for_height(h)._c()
+    cid = TU.CHAIN_ID.encode()
+    vs, keep_v = lat.valset._pack()
+    clean, _, _ = TU.make_commit(c, lat, height=h)
+    flipped, _, _ = TU.make_commit(c, lat, height=h)
+    s = bytearray(flipped.signatures[n_vals - 2].signature)
+    s[9] ^= 2
+    flipped.signatures[n_vals - 2].signature = bytes(s)
+    packed = [(T._pack_commit(cm), hh) for cm, hh in ((clean, h), (flipped, h), (clean, h + 1))]
+
+    def outcomes():
+        out = []
+        for (cm, _keep), hh in packed:
+            res = N.cmtv_commit_result()
+            rc = N.lib().cmtv_verify_commit(c.handle, N.VERIFY_COMMIT, 0, cid, len(cid), ctypes.byref(vs),
+                                            ctypes.byref(b), hh, ctypes.byref(cm), 0, 0, ctypes.byref(res), None, 0)
+            out.append((rc, res.code, res.sig_index))
+        return out
+
+    idle = outcomes()
+    assert idle[0][0] == N.CMTV_OK
+    assert idle[1][1] == N.COMMIT_ERR_WRONG_SIGNATURE and idle[1][2] == n_vals - 2
+    assert idle[2][1] == N.COMMIT_ERR_HEIGHT
+    stop = threading.Event()
+    errors = []
+
+    def load():
+        try:
+            while not stop.is_set():
+                chain.call(c, N.VERIFY_COMMIT)
+                _check_chain(chain, N.VERIFY_COMMIT)
+        except Exception as e:  # reported by the main thread
+            errors.append(e)
+
+    st0 = c.stats()
+    th = threading.Thread(target=load)
+    th.start()
+    try:
+        time.sleep(0.2)
+        for _ in range(50):
+            assert outcomes() == idle
+            time.sleep(0.001)
+    finally:
+        stop.set()
+        th.join()
+    assert not errors, errors
+    st = c.stats()
+    assert st["isolated_calls"] > st0["isolated_calls"]
+    assert st["masked_chunks"] > st0["masked_chunks"]
+    del chain, keep_b, keep_v
+    c.close()

@@ -32,6 +32,9 @@ def main():
     for r in copy:
         ops.append(("C", r.get("Direction", "?"), int(r.get("Thread_Id", 0) or 0), int(r["Start_Timestamp"]),
                     int(r["End_Timestamp"])))
+    for r in load(f"{tdir}/**/*hip_api_trace.csv"):
+        ops.append(("A", r.get("Function", "?")[:40], int(r["Thread_Id"]), int(r["Start_Timestamp"]),
+                    int(r["End_Timestamp"])))
     ops.sort(key=lambda o: o[3])
     # the calling thread: the thread whose ops fall inside most windows
     starts = np.array([o[3] for o in ops])
@@ -39,12 +42,13 @@ def main():
     for t0, t1 in win[:50]:
         i, j = np.searchsorted(starts, t0), np.searchsorted(starts, t1)
         for o in ops[i:j]:
-            votes[o[2]] = votes.get(o[2], 0) + 1
+            if o[0] == "K" and ("quad_split" in o[1] or "row_split" in o[1]):
+                votes[o[2]] = votes.get(o[2], 0) + 1
     me = max(votes, key=votes.get) if votes else None
     print(f"{len(kern)} kernels, {len(copy)} copies, {len(win)} windows, calling thread {me}")
     lat = np.array([(t1 - t0) / 1e3 for t0, t1 in win])
     order = np.argsort(lat)
-    bulk = [o for o in ops if o[2] != me]
+    bulk = [o for o in ops if o[2] != me and o[0] != "A"]
     bk = [o for o in bulk if o[0] == "K"]
     bc = [o for o in bulk if o[0] == "C"]
 

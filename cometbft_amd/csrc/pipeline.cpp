@@ -28,6 +28,7 @@
 #include <emmintrin.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <cstring>
@@ -84,6 +85,15 @@ struct SpanAcc {
     for (int k = 0; k < kClasses; k++) {
       lo[k] = std::min(lo[k], a[k]);
       hi[k] = std::max(hi[k], a[k] + len[k]);
+    }
+    need += 77 * m;
+  }
+  // the same from the class starts ranges() gave (lengths: 64, 8, 4, 1 per signature)
+  void add(const uintptr_t* a, size_t m) {
+    static constexpr size_t w[kClasses] = {64, 8, 4, 1};
+    for (int k = 0; k < kClasses; k++) {
+      lo[k] = std::min(lo[k], a[k]);
+      hi[k] = std::max(hi[k], a[k] + w[k] * m);
     }
     need += 77 * m;
   }
@@ -225,6 +235,9 @@ struct PipeWorkspace {
   std::vector<uint8_t> direct;
   std::vector<int64_t> ptally;
   std::vector<uint32_t> pblock;
+  // ... and where each of their array classes starts (SpanAcc::ranges, kept
+  // by the parallel plan so the serial cut reads one sequential array)
+  std::vector<std::array<uintptr_t, kClasses>> dspan;
   bool grow(size_t n, bool with_val) {
     if (cap_idx < n) {
       pidx.reset(new (std::nothrow) uint32_t[n]);
@@ -296,7 +309,7 @@ int run_pipeline(cmtv_ctx* ctx, const CommitsArgs& args, int* rcs, std::vector<c
   HostPool& pool = host_pool(ctx);
   const PipeConfig pc = pipe_config(ctx);
   const bool trusting = args.kind == CMTV_VERIFY_COMMIT_LIGHT_TRUSTING;
-  uint64_t ph_plan = 0, ph_pack = 0, ph_submit = 0, ph_wait = 0, ph_replay = 0;
+  uint64_t ph_plan = 0, ph_pack = 0, ph_submit = 0, ph_wait = 0, ph_replay = 0, ph_cut = 0;
   // ---- plan: each commit's preamble and plan, its template and sign-bytes
   // lengths -- window by window, just ahead of the chunk being cut, so the
   // planning of later commits overlaps the device's work on earlier chunks
@@ -324,6 +337,7 @@ int run_pipeline(cmtv_ctx* ctx, const CommitsArgs& args, int* rcs, std::vector<c
   W.direct.resize(n);
   W.ptally.resize(n);
   W.pblock.resize(n);
+  W.dspan.resize(n);
   // direct chunks (BulkLayout): on when the caller's arguments can be in
   // pinned blocks of this context and the registered-key cache is on
   std::vector<PinnedRange> pins;
@@ -470,7 +484,7 @@ int run_pipeline(cmtv_ctx* ctx, const CommitsArgs& args, int* rcs, std::vector<c
       uint32_t bad = 0;
       for (uint32_t i = 1; i <= m; i++) bad |= so[i] ^ (s0 + 64u * i);  // vectorised
       if (bad) return false;
-      uintptr_t a[kClasses];
+      uintptr_t* a = W.dspan[c].data();
       size_t len[kClasses];
       SpanAcc::ranges(cm, m, a, len);
       if ((a[kClsSig] & 7) || (a[kClsSec] & 7) || (a[kClsNanos] & 3)) return false;
@@ -559,6 +573,10 @@ int run_pipeline(cmtv_ctx* ctx, const CommitsArgs& args, int* rcs, std::vector<c
   bool last_packed = false;
   const uint64_t max_mb = max_batch_msg_bytes();
   auto cut_chunk = [&]() -> int {  // appends the next chunk; CMTV_OK or an error
+    struct CutClock {  // ph_cut: this cut's time, its plan windows apart
+      uint64_t &cut, &plan, t0, plan0;
+      ~CutClock() { cut += (now_ns() - t0) - (plan - plan0); }
+    } cut_clock{ph_cut, ph_plan, now_ns(), ph_plan};
     if (per == 0) {
       // the first window sets the chunk size from its plan ratio
       plan_window(std::max<uint64_t>(pc.chunk, 1));
@@ -646,7 +664,7 @@ int run_pipeline(cmtv_ctx* ctx, const CommitsArgs& args, int* rcs, std::vector<c
       mb += mbytes[c];
       tb += tlen[c];
       if (s >= want) {
-        if (dir) ch.acc.add(&args.commits[c], plen[c]);
+        if (dir) ch.acc.add(W.dspan[c].data(), plen[c]);
         c++;
         break;
       }
@@ -654,7 +672,7 @@ int run_pipeline(cmtv_ctx* ctx, const CommitsArgs& args, int* rcs, std::vector<c
         // a direct chunk's DMA covers its classes' extents: it ends at a
         // commit past which it would copy far more than its plans read (a
         // caller's arrays scattered over its pinned block)
-        ch.acc.add(&args.commits[c], plen[c]);
+        ch.acc.add(W.dspan[c].data(), plen[c]);
         const uint64_t cap = 4 * ch.acc.need + (64u << 20);
         if (ch.acc.sum_bytes() > cap && ch.acc.merged_bytes() > cap) {
           c++;
@@ -966,6 +984,7 @@ int run_pipeline(cmtv_ctx* ctx, const CommitsArgs& args, int* rcs, std::vector<c
   {
     std::lock_guard<std::unique_lock<std::mutex>> g(lk);
     phase_add_ns(ctx, kPhPipePlan, ph_plan);
+    phase_add_ns(ctx, kPhPipeCut, ph_cut);
     phase_add_ns(ctx, kPhPipePack, ph_pack);
     phase_add_ns(ctx, kPhPipeSubmit, ph_submit);
     phase_add_ns(ctx, kPhPipeWait, ph_wait);

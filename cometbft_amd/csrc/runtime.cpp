@@ -588,6 +588,11 @@ struct cmtv_ctx {
   // ... and waits for its stream rather than polling its kernel's tagged
   // bitmap (run_host_batch_; CMTV_LOAD_POLL=1 polls as when idle)
   bool load_nopoll = true;
+  // the quad kernels' tagged slices (CMTV_QUAD_POLL=1): polling a 10k commit
+  // was slower than waiting for its stream on MI355X (round 6,
+  // tools/gpu_r6p.sh, three alternating rounds: keyset pinned p50 0.112-0.119
+  // polled vs 0.108-0.110 ms, generic 0.269-0.279 vs 0.267 ms), so off
+  bool quad_poll = false;
   uint64_t lat_window_ns = 10'000'000'000ull;
   uint32_t lat_reserve_cus = 16;
   // latency calls beside a pipeline run on the reserved CUs only
@@ -812,7 +817,7 @@ static int enqueue_verify(cmtv_ctx* ctx, CmtvDev& D, size_t n, const uint8_t* d_
   if (row && (e = row_slot_acquire(ctx, D, s, d_bitmap != nullptr, slot, slot_k)) != hipSuccess) return hip_fail(e);
   // the quad kernel of an armed host batch (one launch) tags its 16-signature
   // slices (as enqueue_verify_keyed's)
-  const bool qtag = !sr && form == kFormQuad && d_bitmap && D.tag_arm && n <= kChunk;
+  const bool qtag = ctx->quad_poll && !sr && form == kFormQuad && d_bitmap && D.tag_arm && n <= kChunk;
   if (qtag) {
     slot = RowSlot{};
     slot.tagged = D.tag_arm;
@@ -900,7 +905,7 @@ static int enqueue_verify_keyed(cmtv_ctx* ctx, CmtvDev& D, const cmtv_keyset::Pe
   // 16-signature slices instead of writing the bitmap: the call polls them
   // (wait_row_tags) rather than wait for the stream
   RowSlot qtags;
-  const bool qtag = form == kKeyedQuad && d_bitmap && D.tag_arm && n <= chunk;
+  const bool qtag = ctx->quad_poll && form == kKeyedQuad && d_bitmap && D.tag_arm && n <= chunk;
   if (qtag) {
     qtags.tagged = D.tag_arm;
     qtags.seq = D.tag_seq;
@@ -1858,6 +1863,7 @@ static void read_env(cmtv_ctx* ctx) {
   if (const char* v = std::getenv("CMTV_LOAD_FORM")) ctx->load_form = v[0] != '0';
   if (const char* v = std::getenv("CMTV_LOAD_ZC")) ctx->load_zc = v[0] != '0';
   if (const char* v = std::getenv("CMTV_LOAD_POLL")) ctx->load_nopoll = v[0] == '0';
+  if (const char* v = std::getenv("CMTV_QUAD_POLL")) ctx->quad_poll = v[0] == '1';
   if (const char* v = std::getenv("CMTV_LAT_ISOLATE")) ctx->lat_isolate = v[0] != '0';
   if (const char* v = std::getenv("CMTV_LAT_RESERVE_CUS")) {
     const long k = std::strtol(v, nullptr, 10);
@@ -2025,7 +2031,7 @@ void cmtv_close(cmtv_ctx* ctx) {
   if (ctx->phases_on) {
     static const char* names[kPhCount] = {"prepare",   "stage",     "launch",      "wait",      "post",       "replay",
                                           "pipe_plan", "pipe_pack", "pipe_submit", "pipe_wait", "pipe_replay",
-                                          "keyset",    "early"};
+                                          "keyset",    "early",     "pipe_cut"};
     std::fprintf(stderr, "{\"cmtv_host_phases_us\": {");
     for (int p = 0; p < kPhCount; p++)
       std::fprintf(stderr, "%s\"%s\": %.3f", p ? ", " : "", names[p],

@@ -75,10 +75,11 @@ bool keyset_cache_enabled(const cmtv_ctx* ctx);
 // on stderr by cmtv_close. phase_now is 0 when the clock is off.
 // The pipeline's phases (pipeline.cpp): per-commit plan, pinned-staging
 // pack, submission (under the context lock), waits for chunk verdicts and
-// replay; each summed over the host worker threads' wall time, not CPU time.
+// replay; each summed over the host worker threads' wall time, not CPU time;
+// pipe_cut: the submitting thread's serial chunk cut (its plan windows apart).
 enum HostPhase {
   kPhPrepare, kPhStage, kPhLaunch, kPhWait, kPhPost, kPhReplay,
-  kPhPipePlan, kPhPipePack, kPhPipeSubmit, kPhPipeWait, kPhPipeReplay, kPhKeyset, kPhEarly, kPhCount
+  kPhPipePlan, kPhPipePack, kPhPipeSubmit, kPhPipeWait, kPhPipeReplay, kPhKeyset, kPhEarly, kPhPipeCut, kPhCount
 };
 uint64_t phase_now(const cmtv_ctx* ctx);
 void phase_add(cmtv_ctx* ctx, int phase, uint64_t t0);

@@ -112,8 +112,8 @@ int main(int argc, char** argv) {
   fake_phases(ctx, pt);
   for (int p = 0; p < 16; p++) pt[p] -= pt0[p];
   const double k = 1e6 * (iters - 1);
-  std::printf("  per call ms: plan %.3f pack %.3f submit %.3f wait %.3f replay %.3f | one batch: prepare %.4f "
-              "replay %.4f\n", pt[6] / k, pt[7] / k, pt[8] / k, pt[9] / k, pt[10] / k, pt[0] / k, pt[5] / k);
+  std::printf("  per call ms: plan %.3f pack %.3f submit %.3f wait %.3f replay %.3f cut %.3f | one batch: prepare %.4f "
+              "replay %.4f\n", pt[6] / k, pt[7] / k, pt[8] / k, pt[9] / k, pt[10] / k, pt[13] / k, pt[0] / k, pt[5] / k);
   fake_close(ctx);
   return 0;
 }

@@ -434,3 +434,51 @@ def test_speculative_verify_commit_matches(pinned):
     del keep_b
     for c in ctxs:
         c.close()
+
+
+@pytest.mark.parametrize("keyset", [False, True])
+def test_polled_quad_slices_match(keyset):
+    """CMTV_QUAD_POLL=1 (round 6, off by default): the quad kernels of a small
+    host batch tag their 16-signature slices and the call polls them instead
+    of waiting for the stream. Outcomes equal the default path's: clean, a
+    flipped signature near the end, and the call is counted as polled."""
+    import ctypes
+
+    from cometbft_amd import _native as N
+    from cometbft_amd import testutil as TU
+    from test_runtime_gpu import _env
+
+    ctxs = []
+    for poll in ("1", "0"):
+        with _env(CMTV_QUAD_POLL=poll):
+            c = __import__("cometbft_amd").Context(device=0)
+        if keyset:
+            c.keyset_cache(4)
+        ctxs.append(c)
+    n = 3000
+    sv = TU.make_validator_set(ctxs[0], n)
+    h = 9
+    b, keep_b = TU.block_id_for_height(h)._c()
+    cid = TU.CHAIN_ID.encode()
+    vs, keep_v = sv.valset._pack()
+    clean, _, _ = TU.make_commit(ctxs[0], sv, height=h)
+    flipped, _, _ = TU.make_commit(ctxs[0], sv, height=h)
+    s = bytearray(flipped.signatures[n - 5].signature)
+    s[33] ^= 1
+    flipped.signatures[n - 5].signature = bytes(s)
+    packed = [T._pack_commit(cm) for cm in (clean, flipped)]
+
+    def outcome(c, pc):
+        res = N.cmtv_commit_result()
+        rc = N.lib().cmtv_verify_commit(c.handle, N.VERIFY_COMMIT, 0, cid, len(cid), ctypes.byref(vs),
+                                        ctypes.byref(b), h, ctypes.byref(pc[0]), 0, 0, ctypes.byref(res), None, 0)
+        return rc, res.code, res.sig_index
+
+    st0 = ctxs[0].stats()
+    got = [[outcome(c, pc) for pc in packed for _ in range(3)] for c in ctxs]
+    assert got[0] == got[1], got
+    assert got[0][0][0] == N.CMTV_OK and got[0][3][2] == n - 5
+    assert ctxs[0].stats()["polled_calls"] > st0["polled_calls"]
+    for c in ctxs:
+        c.close()
+    del keep_b, keep_v

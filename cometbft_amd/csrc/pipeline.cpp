@@ -623,62 +623,87 @@ int run_pipeline(cmtv_ctx* ctx, const CommitsArgs& args, int* rcs, std::vector<c
     long dcls = -1;
     uint64_t s = 0, mb = 0, tb = 0;
     size_t c = cursor;
-    for (; c < n; c++) {
-      // plan a chunk's worth at a time: each window is one parallel_for (a
-      // wake-up of every worker), so windows of 64k signatures cost ~230
-      // wake-ups per 15M-signature call
-      if (c == planned_upto) plan_window(std::max<uint64_t>(want - std::min(want, s), std::max<uint64_t>(pc.chunk, 65536)));
-      const bool dir = plen[c] && W.direct[c];
-      if (plen[c]) {
-        const long dc = dir ? (long)W.pblock[c] : -1;
-        if (dcls_set && dc != dcls) break;
-        if (!dcls_set) {
-          dcls = dc;
-          dcls_set = true;
+    // the commits of the chunk; with per_commit_cap a direct chunk also ends
+    // where its DMA extents outgrow its plans (below). The common case runs
+    // without it and checks the extents once, for the whole chunk, from the
+    // plan's per-commit class starts (W.dspan); only a chunk that fails that
+    // check is cut again commit by commit (round 6: the per-commit extents
+    // were ~40% of the serial cut, tests/host/pipebench's pipe_cut phase)
+    auto scan = [&](bool per_commit_cap) {
+      cls_set = dcls_set = false;
+      dcls = -1;
+      ch.vs = nullptr;
+      ch.acc = SpanAcc();
+      s = mb = tb = 0;
+      c = cursor;
+      for (; c < n; c++) {
+        // plan a chunk's worth at a time: each window is one parallel_for (a
+        // wake-up of every worker), so windows of 64k signatures cost ~230
+        // wake-ups per 15M-signature call
+        if (c == planned_upto)
+          plan_window(std::max<uint64_t>(want - std::min(want, s), std::max<uint64_t>(pc.chunk, 65536)));
+        const bool dir = plen[c] && W.direct[c];
+        if (plen[c]) {
+          const long dc = dir ? (long)W.pblock[c] : -1;
+          if (dcls_set && dc != dcls) break;
+          if (!dcls_set) {
+            dcls = dc;
+            dcls_set = true;
+          }
         }
-      }
-      if (plen[c] && keyed_mode) {
-        const cmtv_valset* v = &args.vals[c];
-        if (!last_vs || !same_arrays(v, last_vs)) {
-          last_vs = v;
-          last_packed = packed_keys(v);
+        if (plen[c] && keyed_mode) {
+          const cmtv_valset* v = &args.vals[c];
+          if (!last_vs || !same_arrays(v, last_vs)) {
+            last_vs = v;
+            last_packed = packed_keys(v);
+          }
+          const cmtv_valset* cls = last_packed ? v : nullptr;
+          if (cls_set && !((cls == nullptr) == (ch.vs == nullptr) &&
+                           (!cls || same_arrays(ch.vs, cls) || same_keys(ch.vs, cls))))
+            break;
+          if (!cls_set) {
+            ch.vs = cls;
+            cls_set = true;
+          }
         }
-        const cmtv_valset* cls = last_packed ? v : nullptr;
-        if (cls_set && !((cls == nullptr) == (ch.vs == nullptr) && (!cls || same_keys(ch.vs, cls)))) break;
-        if (!cls_set) {
-          ch.vs = cls;
-          cls_set = true;
-        }
-      }
-      // cut below the target (a commit that would cross it opens the next
-      // chunk), unless the chunk would be empty
-      if (s && s + plen[c] > want) break;
-      // ... and below the one-batch path's sign-bytes span per launch (its
-      // message offsets are 32-bit): a commit that would cross it opens the
-      // next chunk
-      if (s && mb + mbytes[c] >= max_mb) break;
-      sp[c] = s;
-      mp[c] = mb;
-      tp[c] = tb;
-      s += plen[c];
-      mb += mbytes[c];
-      tb += tlen[c];
-      if (s >= want) {
-        if (dir) ch.acc.add(W.dspan[c].data(), plen[c]);
-        c++;
-        break;
-      }
-      if (dir) {
-        // a direct chunk's DMA covers its classes' extents: it ends at a
-        // commit past which it would copy far more than its plans read (a
-        // caller's arrays scattered over its pinned block)
-        ch.acc.add(W.dspan[c].data(), plen[c]);
-        const uint64_t cap = 4 * ch.acc.need + (64u << 20);
-        if (ch.acc.sum_bytes() > cap && ch.acc.merged_bytes() > cap) {
+        // cut below the target (a commit that would cross it opens the next
+        // chunk), unless the chunk would be empty
+        if (s && s + plen[c] > want) break;
+        // ... and below the one-batch path's sign-bytes span per launch (its
+        // message offsets are 32-bit): a commit that would cross it opens the
+        // next chunk
+        if (s && mb + mbytes[c] >= max_mb) break;
+        sp[c] = s;
+        mp[c] = mb;
+        tp[c] = tb;
+        s += plen[c];
+        mb += mbytes[c];
+        tb += tlen[c];
+        if (s >= want) {
+          if (dir && per_commit_cap) ch.acc.add(W.dspan[c].data(), plen[c]);
           c++;
           break;
         }
+        if (dir && per_commit_cap) {
+          // a direct chunk's DMA covers its classes' extents: it ends at a
+          // commit past which it would copy far more than its plans read (a
+          // caller's arrays scattered over its pinned block)
+          ch.acc.add(W.dspan[c].data(), plen[c]);
+          const uint64_t cap = pc.span_factor * ch.acc.need + pc.span_slack;
+          if (ch.acc.sum_bytes() > cap && ch.acc.merged_bytes() > cap) {
+            c++;
+            break;
+          }
+        }
       }
+    };
+    scan(false);
+    if (dcls_set && dcls >= 0) {
+      // a direct chunk (every planned commit of it direct): its extents
+      for (size_t k = cursor; k < c; k++)
+        if (plen[k]) ch.acc.add(W.dspan[k].data(), plen[k]);
+      const uint64_t cap = pc.span_factor * ch.acc.need + pc.span_slack;
+      if (ch.acc.sum_bytes() > cap && ch.acc.merged_bytes() > cap) scan(true);
     }
     ch.c1 = c;
     cursor = c;

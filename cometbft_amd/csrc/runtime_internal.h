@@ -146,6 +146,9 @@ struct PipeConfig {
   bool enabled;
   bool direct = true;  // CMTV_PIPE_DIRECT=0: always pack (A/B, tests)
   size_t chunk_masked = 0;  // a chunk on a CU-masked lane (latency_recent): one round of its CUs
+  // a direct chunk ends where its DMA extents pass span_factor x the bytes
+  // its plans read + span_slack (pipeline.cpp cut_chunk; tests shrink them)
+  uint64_t span_factor = 4, span_slack = 64ull << 20;
 };
 PipeConfig pipe_config(const cmtv_ctx* ctx);
 // Latency calls beside the pipeline (runtime.cpp cmtv_ctx::lat_window_ns):

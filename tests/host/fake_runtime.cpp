@@ -476,6 +476,10 @@ extern "C" cmtv_ctx* fake_open(size_t n_devs, unsigned threads, size_t pipe_min,
 
 extern "C" void fake_set_ext_retire(cmtv_ctx* c, long dev) { c->ext_retire_dev = dev; }
 extern "C" void fake_set_direct(cmtv_ctx* c, bool on) { c->pc.direct = on; }
+extern "C" void fake_set_span(cmtv_ctx* c, uint64_t factor, uint64_t slack) {
+  c->pc.span_factor = factor;
+  c->pc.span_slack = slack;
+}
 extern "C" void fake_set_keyset_fail(cmtv_ctx* c, bool on) { c->keyset_fail = on; }
 
 // the ABI's pinned blocks (plain page-aligned memory here)

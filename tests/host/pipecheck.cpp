@@ -36,6 +36,7 @@ cmtv_ctx* fake_open(size_t n_devs, unsigned threads, size_t pipe_min, size_t chu
 void fake_counts(cmtv_ctx* c, uint64_t* out);
 void fake_set_ext_retire(cmtv_ctx* c, long dev);
 void fake_set_direct(cmtv_ctx* c, bool on);
+void fake_set_span(cmtv_ctx* c, uint64_t factor, uint64_t slack);
 void fake_set_keyset_fail(cmtv_ctx* c, bool on);
 void fake_close(cmtv_ctx* c);
 }
@@ -588,6 +589,7 @@ int main(int argc, char** argv) {
     Layout lay = kHeap;
     bool direct = true;       // CMTV_PIPE_DIRECT
     bool keyset_fail = false;
+    bool tight_spans = false;  // span cap = the plans' bytes: chunks re-cut commit by commit
   };
   const Cfg cfgs[] = {
       {"pipe chunk 1000", 1, 4, 1000, 3, 0, -1},   {"pipe chunk 7", 1, 3, 7, 2, 0, -1},
@@ -601,6 +603,7 @@ int main(int argc, char** argv) {
       {"direct big chunks", 2, 8, 4000, 3, 1, -1, -1, kClassArrays},
       {"direct off, pinned", 1, 4, 100, 3, 4, -1, -1, kInterleaved, false},
       {"direct, keys unregistered", 1, 4, 100, 3, 4, -1, -1, kInterleaved, true, true},
+      {"direct, tight spans", 2, 4, 100, 3, 4, -1, -1, kInterleaved, true, false, true},
   };
   size_t checked = 0;
   for (uint32_t kind = 0; kind < 3; kind++) {
@@ -620,6 +623,7 @@ int main(int argc, char** argv) {
         fake_set_ext_retire(ctx, c.ext_retire);
         fake_set_direct(ctx, c.direct);
         fake_set_keyset_fail(ctx, c.keyset_fail);
+        if (c.tight_spans) fake_set_span(ctx, 1, 0);
         const Run r = run(ctx, kind, mode, chain, vals_of, c.lay);
         uint64_t cnt[8];
         fake_counts(ctx, cnt);

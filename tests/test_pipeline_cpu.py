@@ -63,7 +63,7 @@ def test_pipeline_host_logic_matches_reference_loops():
                        env={**os.environ, "ASAN_OPTIONS": "detect_leaks=1:halt_on_error=1",
                             "UBSAN_OPTIONS": "halt_on_error=1:print_stacktrace=1"})
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
-    assert "pipecheck ok (60 runs)" in r.stdout
+    assert "pipecheck ok (64 runs)" in r.stdout
     assert "single: 240 commits x 3 kinds x 2, 0 mismatches" in r.stdout
     for kind in (0, 1, 2):
         assert f"kind {kind} mode 0: 240 commits" in r.stdout

@@ -125,21 +125,11 @@ int main() {
     std::printf("\n");
     CK(hipStreamDestroy(hs));
   }
-  // the bit -> CU map: one workgroup on a stream whose mask holds bit b only
-  std::printf("bit map (bit: xcc.se.sh.cu):");
-  for (int b = 0; b < 64 && b < cus; b++) {
-    std::vector<uint32_t> m(words, 0);
-    m[b / 32] = 1u << (b % 32);
-    hipStream_t one;
-    CK(hipExtStreamCreateWithCUMask(&one, words, m.data()));
-    hipLaunchKernelGGL(k_probe, dim3(1), dim3(64), 0, one, d_probe);
-    CK(hipStreamSynchronize(one));
-    uint32_t w = 0;
-    CK(hipMemcpy(&w, d_probe, 4, hipMemcpyDeviceToHost));
-    std::printf(" %d:%u.%u.%u.%u", b, w >> 16, (w >> 8) & 7, (w >> 4) & 1, w & 15);
-    CK(hipStreamDestroy(one));
-  }
-  std::printf("\n");
+  // (A single-bit mask leaves seven XCDs with no CU of the queue; the driver
+  // then runs those XCDs' share on all their CUs, so one-bit probes say
+  // nothing about the map -- and a mask that truly leaves an XCD empty could
+  // strand workgroups. Not probed: the "only bits 0..7 set" variant above
+  // is the map's evidence.)
   CK(hipFree(d_hog));
   CK(hipFree(d_probe));
   return 0;

@@ -301,6 +301,16 @@ bool pipeline_wanted(const cmtv_ctx* ctx, uint64_t n_sigs) {
 
 namespace {
 
+// The context lock re-taken for one step of the pipeline (bulk_relock: a
+// waiting latency call goes first), released at scope end.
+struct Relock {
+  std::unique_lock<std::mutex>& lk;
+  Relock(cmtv_ctx* c, std::unique_lock<std::mutex>& l) : lk(l) { bulk_relock(c, lk); }
+  ~Relock() { lk.unlock(); }
+  Relock(const Relock&) = delete;
+  Relock& operator=(const Relock&) = delete;
+};
+
 // The pipeline proper; `pinned` collects the registered key sets it pins
 // (released by the caller, also after an exception). Bulk lock held.
 int run_pipeline(cmtv_ctx* ctx, const CommitsArgs& args, int* rcs, std::vector<const cmtv_keyset*>& pinned) {
@@ -713,7 +723,7 @@ int run_pipeline(cmtv_ctx* ctx, const CommitsArgs& args, int* rcs, std::vector<c
     ch.L.msg_bytes = mb;
     if (mb >= max_mb) return CMTV_EINVAL;  // one commit's sign-bytes alone reach the span
     if (keyed_mode && ch.vs && ch.L.m) {
-      std::lock_guard<std::unique_lock<std::mutex>> g(lk);
+      Relock g(ctx, lk);
       ch.ks = keyset_for_locked(ctx, ch.vs->pubkeys, ch.vs->n_vals);
       if (ch.ks && std::find(pinned.begin(), pinned.end(), ch.ks) == pinned.end()) {
         keyset_pin_locked(ch.ks);
@@ -944,7 +954,7 @@ int run_pipeline(cmtv_ctx* ctx, const CommitsArgs& args, int* rcs, std::vector<c
         uint64_t valid = 0;
         for (size_t w = 0; w < ch.L.m / 64; w++) valid += (uint64_t)__builtin_popcountll(bm[w]);
         if (ch.L.m & 63) valid += (uint64_t)__builtin_popcountll(bm[ch.L.m / 64] & ((1ull << (ch.L.m & 63)) - 1));
-        std::lock_guard<std::unique_lock<std::mutex>> g(lk);
+        Relock g(ctx, lk);
         count_invalid_locked(ctx, ch.L.m - valid);
       }
       ph_replay += now_ns() - tr;
@@ -980,7 +990,7 @@ int run_pipeline(cmtv_ctx* ctx, const CommitsArgs& args, int* rcs, std::vector<c
       const uint64_t ts = now_ns();
       ph_pack += ts - tk;
       {
-        std::lock_guard<std::unique_lock<std::mutex>> g(lk);
+        Relock g(ctx, lk);
         rc = bulk_submit_locked(ctx, ch.dev, ch.slot, ch.L, ch.ks, mode);
         if (rc == CMTV_OK && ch.direct) count_direct_locked(ctx);
       }
@@ -1000,14 +1010,14 @@ int run_pipeline(cmtv_ctx* ctx, const CommitsArgs& args, int* rcs, std::vector<c
     // a failure: nothing of this attempt stays in flight; a device's own HIP
     // error retires it and the chunks not yet replayed run on the others
     bulk_drain(ctx);
-    std::lock_guard<std::unique_lock<std::mutex>> g(lk);
+    Relock g(ctx, lk);
     if (rc != CMTV_EHIP || bad_dev < 0 || !retire_device_locked(ctx, (size_t)bad_dev)) break;
     // chunks are replayed in submission (= chunk) order, so the replayed
     // ones are exactly [0, next_retire): the rest run again
     live_devices_locked(ctx, live);
   }
   {
-    std::lock_guard<std::unique_lock<std::mutex>> g(lk);
+    Relock g(ctx, lk);
     phase_add_ns(ctx, kPhPipePlan, ph_plan);
     phase_add_ns(ctx, kPhPipeCut, ph_cut);
     phase_add_ns(ctx, kPhPipePack, ph_pack);

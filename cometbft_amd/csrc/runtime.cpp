@@ -600,6 +600,9 @@ struct cmtv_ctx {
   // bulk waves)
   bool lat_isolate = true;
   std::atomic<int> bulk_busy{0};
+  // threads blocked in ctx_lock: a pipeline re-taking the lock for its next
+  // chunk lets them in first (bulk_relock)
+  std::atomic<int> lock_waiters{0};
   bool under_load = false;
   uint32_t cus = 0;  // CUs per device (the smallest of the context's)
   // the caller's pinned blocks (cmtv_alloc_pinned): base -> bytes; chunks
@@ -1693,12 +1696,28 @@ void clear_early_locked(cmtv_ctx* ctx) {
 }
 
 int ctx_lock(cmtv_ctx* ctx, std::unique_lock<std::mutex>& lk) {
+  ctx->lock_waiters.fetch_add(1, std::memory_order_relaxed);
   lk = std::unique_lock<std::mutex>(ctx->mu);
+  ctx->lock_waiters.fetch_sub(1, std::memory_order_relaxed);
   clear_early_locked(ctx);
   // the forms of this hold's launches see one answer (keyed_form, ed_form)
   ctx->bulk_now = ctx->bulk_busy.load(std::memory_order_relaxed) > 0;
   ctx->under_load = ctx->bulk_now && ctx->lat_window_ns && ctx->load_form;
   return hipSetDevice(ctx->devs[0].ordinal) == hipSuccess ? CMTV_OK : CMTV_ENODEV;
+}
+
+void bulk_relock(cmtv_ctx* ctx, std::unique_lock<std::mutex>& lk) {
+  // std::mutex is not fair: a pipeline thread that re-locks right after each
+  // release can hold a 150-validator call off for several of its chunk
+  // submissions (round 6: the under-load call's p99 was its wait before the
+  // launch). Waiters go first, for at most 200 us.
+  if (ctx->lock_waiters.load(std::memory_order_relaxed) > 0) {
+    const auto t0 = std::chrono::steady_clock::now();
+    while (ctx->lock_waiters.load(std::memory_order_relaxed) > 0 &&
+           std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(200))
+      std::this_thread::yield();
+  }
+  lk.lock();
 }
 
 uint32_t ctx_default_mode(const cmtv_ctx* ctx) { return ctx->default_mode; }

@@ -14,6 +14,9 @@ namespace cmtv {
 
 // Locks the context and makes its device current on this thread.
 int ctx_lock(cmtv_ctx* ctx, std::unique_lock<std::mutex>& lk);
+// Re-takes a released context lock (the pipeline, between chunks) after any
+// thread waiting in ctx_lock got it first.
+void bulk_relock(cmtv_ctx* ctx, std::unique_lock<std::mutex>& lk);
 uint32_t ctx_default_mode(const cmtv_ctx* ctx);
 // Internal pseudo-mode selecting the sr25519 kernel in verify_host_locked /
 // enqueue paths (the ABI's mode argument is Ed25519-only).

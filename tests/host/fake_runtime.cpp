@@ -147,6 +147,7 @@ int ctx_lock(cmtv_ctx* ctx, std::unique_lock<std::mutex>& lk) {
   lk = std::unique_lock<std::mutex>(ctx->mu);
   return CMTV_OK;
 }
+void bulk_relock(cmtv_ctx*, std::unique_lock<std::mutex>& lk) { lk.lock(); }
 uint32_t ctx_default_mode(const cmtv_ctx*) { return 0; }
 bool cache_enabled(const cmtv_ctx*) { return false; }
 uint64_t phase_now(const cmtv_ctx*) {

@@ -1140,8 +1140,8 @@ def verify_commit_10k_keyset(mode, iters):
 
 # The PMC summaries of THIS round's tree (TAG=r05 tools/gpu_prof_r04.sh: rocprofv3
 # --pmc passes over the quick form of this bench command)
-PMC_SQ = "r05b_pmc_sq.json"
-PMC_TRAFFIC = "r05b_traffic.json"
+PMC_SQ = "r06_pmc_sq.json"
+PMC_TRAFFIC = "r06_traffic.json"
 
 
 def load_valu_busy(n=10_000, kernel="k_verify_quad_hs<0u>"):

@@ -593,6 +593,13 @@ struct cmtv_ctx {
   // tools/gpu_r6p.sh, three alternating rounds: keyset pinned p50 0.112-0.119
   // polled vs 0.108-0.110 ms, generic 0.269-0.279 vs 0.267 ms), so off
   bool quad_poll = false;
+  // registered-key small batches read their staging in place -- signatures in
+  // the caller's cmtv_alloc_pinned memory straight from there -- instead of
+  // an early signature DMA + the split staging (CMTV_KEYED_ZC=0). Measured
+  // on MI355X (round 6, tools/gpu_r6x.sh, three alternating rounds):
+  // verify_commit_10k_keyset pinned p50 0.105 / 0.1085 / 0.1051 against
+  // 0.1118 / 0.1074 / 0.108 ms, heap 0.114-0.117 against 0.117-0.123 ms
+  bool keyed_zc = true;
   uint64_t lat_window_ns = 10'000'000'000ull;
   uint32_t lat_reserve_cus = 16;
   // latency calls beside a pipeline run on the reserved CUs only
@@ -1149,7 +1156,7 @@ static int enqueue_shard(cmtv_ctx* ctx, size_t g, const HostBatch& B, size_t a, 
                      dev_bytes <= D.d_in.cap;
   const bool early_pk = early && !keyed && D.early_pk && D.early_pk == B.pk + 32 * a && m == D.early_n;
   D.early_src = D.early_pk = nullptr;
-  const bool zc = !early && (!keyed || (ctx->bulk_now && ctx->load_zc)) && zero_copy && ctx->zc_in &&
+  const bool zc = !early && (!keyed || ctx->keyed_zc || (ctx->bulk_now && ctx->load_zc)) && zero_copy && ctx->zc_in &&
                   (fuse || (!tpl && ctx->zc_host_in && max_len <= kSbFuseMaxMsg));
   // split: the early-staged signatures (and keys) in HBM, the rest -- the
   // fused helper's templates, flags and timestamps, ~17 bytes a signature --
@@ -1176,7 +1183,10 @@ static int enqueue_shard(cmtv_ctx* ctx, size_t g, const HostBatch& B, size_t a, 
   } else if (!early_pk) {
     std::memcpy(hin + o_key, B.pk + 32 * a, 32 * m);
   }
-  if (!early) std::memcpy(hin + o_sig, B.sig + 64 * a, 64 * m);
+  // zero-copy signatures already in the caller's cmtv_alloc_pinned memory are
+  // read from there (no host copy)
+  const bool sig_in_place = zc && pinned_holds_locked(ctx, B.sig + 64 * a, 64 * m);
+  if (!early && !sig_in_place) std::memcpy(hin + o_sig, B.sig + 64 * a, 64 * m);
   if (no_off && !fuse) return CMTV_EINVAL;  // verify_templated_locked derives offsets for every other form
   auto* hoff = reinterpret_cast<uint32_t*>(hin + o_off);
   if (!no_off)
@@ -1210,6 +1220,11 @@ static int enqueue_shard(cmtv_ctx* ctx, size_t g, const HostBatch& B, size_t a, 
     din = static_cast<uint8_t*>(p);
     dmsg = din + o_msg;
     if (zc) dsig = din + o_sig;
+    if (sig_in_place) {
+      void* q = nullptr;
+      if ((e = hipHostGetDevicePointer(&q, const_cast<uint8_t*>(B.sig + 64 * a), 0)) != hipSuccess) return hip_fail(e);
+      dsig = static_cast<uint8_t*>(q);
+    }
     if (zc || keyed) dkey = din + o_key;  // key indices (keyed) are in the mapped staging
   } else {
     const size_t from = early_pk ? o_off : early ? o_key : 0;  // what the early copy did not carry
@@ -1632,7 +1647,7 @@ int stage_sigs_early_locked(cmtv_ctx* ctx, const uint8_t* sigs, size_t n, const 
   // commits (150 validators: p50 0.0566 with it, 0.0534 without)
   if (!pk && keyed_form(ctx, n) == kKeyedRow) return CMTV_OK;
   // nor beside a pipeline call (bulk_now): the copy would queue behind its DMAs
-  if (!pk && ctx->bulk_now && ctx->load_zc) return CMTV_OK;
+  if (!pk && ((ctx->bulk_now && ctx->load_zc) || ctx->keyed_zc)) return CMTV_OK;
   CmtvDev& D = ctx->devs[ctx->live[0]];
   if (hipSetDevice(D.ordinal) != hipSuccess) return CMTV_ENODEV;
   hipError_t e;
@@ -1883,6 +1898,7 @@ static void read_env(cmtv_ctx* ctx) {
   if (const char* v = std::getenv("CMTV_LOAD_ZC")) ctx->load_zc = v[0] != '0';
   if (const char* v = std::getenv("CMTV_LOAD_POLL")) ctx->load_nopoll = v[0] == '0';
   if (const char* v = std::getenv("CMTV_QUAD_POLL")) ctx->quad_poll = v[0] == '1';
+  if (const char* v = std::getenv("CMTV_KEYED_ZC")) ctx->keyed_zc = v[0] != '0';
   if (const char* v = std::getenv("CMTV_LAT_ISOLATE")) ctx->lat_isolate = v[0] != '0';
   if (const char* v = std::getenv("CMTV_LAT_RESERVE_CUS")) {
     const long k = std::strtol(v, nullptr, 10);

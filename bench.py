@@ -1131,8 +1131,9 @@ def verify_commit_10k_keyset(mode, iters):
     ctx.close()
     return {"p50_ms": p50, "p99_ms": p99, "kernel_ms": round(kms, 4), "value": round(10_000 / p50 * 1e3, 1),
             "pinned": {"p50_ms": p50p, "p99_ms": p99p, "value": round(10_000 / p50p * 1e3, 1),
-                       "path": "the commit's arrays in the context's cmtv_alloc_pinned memory: its signatures go "
-                               "to the device by DMA from there (no host copy)"},
+                       "path": "the commit's arrays in the context's cmtv_alloc_pinned memory: the keyed kernel "
+                               "reads its signatures in place from there over PCIe (no host copy, no DMA; "
+                               "CMTV_KEYED_ZC)"},
             "unit": "verifs/s", "iters": iters,
             "path": "cmtv_verify_commit with cmtv_keyset_cache: plan + staging + device sign-bytes + keyed kernel "
                     "+ VerifyCommit replay"}

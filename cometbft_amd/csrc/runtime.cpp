@@ -600,6 +600,7 @@ struct cmtv_ctx {
   // verify_commit_10k_keyset pinned p50 0.105 / 0.1085 / 0.1051 against
   // 0.1118 / 0.1074 / 0.108 ms, heap 0.114-0.117 against 0.117-0.123 ms
   bool keyed_zc = true;
+  bool spin_wait = false;  // CMTV_SPIN_WAIT (wait_stream)
   uint64_t lat_window_ns = 10'000'000'000ull;
   uint32_t lat_reserve_cus = 16;
   // latency calls beside a pipeline run on the reserved CUs only
@@ -1268,6 +1269,17 @@ static int enqueue_shard(cmtv_ctx* ctx, size_t g, const HostBatch& B, size_t a, 
 // D: poll the entries until each carries the call's tag, asking the stream
 // every 256 polls so that an error ends the wait; a launch that finished with
 // an entry untagged (which cannot happen) is an error, not a hang.
+// A small host batch's wait for its stream: hipStreamSynchronize, or with
+// spin_wait (CMTV_SPIN_WAIT=1, A/B knob) a busy poll of hipStreamQuery that
+// keeps the calling thread on its CPU
+static hipError_t wait_stream(const cmtv_ctx* ctx, hipStream_t s) {
+  if (!ctx->spin_wait) return hipStreamSynchronize(s);
+  for (;;) {
+    const hipError_t q = hipStreamQuery(s);
+    if (q != hipErrorNotReady) return q;
+  }
+}
+
 static hipError_t wait_row_tags(CmtvDev& D, size_t n) {
   const uint64_t* e = static_cast<const uint64_t*>(D.h_tags.p);
   const size_t n32 = (n + D.tag_width - 1) / D.tag_width;  // entries
@@ -1336,7 +1348,7 @@ static int run_host_batch_(cmtv_ctx* ctx, const HostBatch& B, uint8_t* out_valid
       D.poll_pending = true;
     }
     const uint64_t t_wait = phase_now(ctx);
-    if ((e = D.tag_used ? wait_row_tags(D, n) : hipStreamSynchronize(D.stream)) != hipSuccess) return hip_fail(e);
+    if ((e = D.tag_used ? wait_row_tags(D, n) : wait_stream(ctx, D.stream)) != hipSuccess) return hip_fail(e);
     uint64_t* bm = static_cast<uint64_t*>(D.h_zc.p);
     if (D.tag_used) {
       ctx->stats.polled_calls++;
@@ -1899,6 +1911,7 @@ static void read_env(cmtv_ctx* ctx) {
   if (const char* v = std::getenv("CMTV_LOAD_POLL")) ctx->load_nopoll = v[0] == '0';
   if (const char* v = std::getenv("CMTV_QUAD_POLL")) ctx->quad_poll = v[0] == '1';
   if (const char* v = std::getenv("CMTV_KEYED_ZC")) ctx->keyed_zc = v[0] != '0';
+  if (const char* v = std::getenv("CMTV_SPIN_WAIT")) ctx->spin_wait = v[0] == '1';
   if (const char* v = std::getenv("CMTV_LAT_ISOLATE")) ctx->lat_isolate = v[0] != '0';
   if (const char* v = std::getenv("CMTV_LAT_RESERVE_CUS")) {
     const long k = std::strtol(v, nullptr, 10);

@@ -1,0 +1,13 @@
+#!/bin/bash
+# round 6: small host batches waiting by a busy hipStreamQuery poll
+# (CMTV_SPIN_WAIT=1) vs hipStreamSynchronize -- under load and at 10k, alternating
+set -o pipefail
+OUT=gpurun_out/r6z
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+for R in 1 2; do
+  for W in 1 0; do
+    CMTV_SPIN_WAIT=$W timeout -k 10 300 python -u tools/lat_load.py 1000 > "$OUT/lat_${W}_$R.json" 2> "$OUT/lat_${W}_$R.err" || { tail "$OUT/lat_${W}_$R.err"; exit 1; }
+    python3 -c "import json;L=open('$OUT/lat_${W}_$R.json').read().strip().splitlines();k=json.loads(L[0])['verify_commit_10k_keyset'];d=json.loads(L[-1])['latency_150_under_load'];print('spin $W round $R keyset', k['p50_ms'], k['pinned']['p50_ms'], 'load', d['idle_p50_ms'], d['idle_p99_ms'], d['p50_ms'], d['p99_ms'], d['p99_over_idle_p99'])"
+  done
+done

@@ -2525,7 +2525,13 @@ static unsigned usable_cpus() {
 
 HostPool& host_pool(cmtv_ctx* ctx) {
   if (!ctx->pool) {
-    const unsigned t = ctx->host_threads ? ctx->host_threads : std::min(16u, usable_cpus());
+    // default: at most 16, and three CPUs short of a small CPU budget, so a
+    // latency caller (consensus) and the HIP runtime's threads keep a CPU
+    // under a cgroup quota (round 6, tools/gpu_r6aa.sh, 16-CPU quota, three
+    // alternating rounds: latency_150_under_load p99 0.125-0.137 ms with 13
+    // workers against 0.132-0.173 with 16)
+    const unsigned u = usable_cpus();
+    const unsigned t = ctx->host_threads ? ctx->host_threads : std::min(16u, u > 8 ? u - 3 : u);
     ctx->pool.reset(new HostPool(t));
   }
   return *ctx->pool;

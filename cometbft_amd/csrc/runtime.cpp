@@ -558,8 +558,8 @@ struct cmtv_ctx {
   // pipe_min signatures take it (CMTV_PIPE_MIN; CMTV_PIPELINE=0: never),
   // in chunks of about pipe_chunk signatures (CMTV_PIPE_CHUNK) over
   // pipe_slots staging slots per device (CMTV_PIPE_SLOTS), on host_threads
-  // threads (CMTV_HOST_THREADS; default: the CPUs this process may use, at
-  // most 16)
+  // threads (CMTV_HOST_THREADS; default: the CPUs this process may use, less
+  // 3 when more than 8, at most 16: host_pool)
   std::mutex bulk_mu;
   std::unique_ptr<cmtv::HostPool> pool;
   unsigned host_threads = 0;

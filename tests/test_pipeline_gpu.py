@@ -282,8 +282,8 @@ def test_configs2_scale_direct_from_pinned(gpu_ctx, devices):
     c.close()
 
 
-@pytest.mark.parametrize("n_vals", [150, 4096])
-def test_latency_calls_beside_a_pipeline(n_vals):
+@pytest.mark.parametrize("n_vals,devices", [(150, None), (4096, None), (150, [0, 0])])
+def test_latency_calls_beside_a_pipeline(n_vals, devices):
     """VerifyCommit while another thread runs a pipelined cmtv_verify_commits
     on the same context (consensus beside blocksync, round 6): the call runs
     on the device's latency stream -- the CUs the pipeline's masked chunks
@@ -295,7 +295,7 @@ def test_latency_calls_beside_a_pipeline(n_vals):
     import threading
     import time
 
-    c = _ctx(keyset=True)
+    c = _ctx(devices=devices, keyset=True)
     lat = TU.make_validator_set(c, n_vals, offset=50_000)
     chain = TU.ReplayChain(c, TU.make_validator_set(c, N_VALS), 1, 3000, pinned=c)
     h = 77

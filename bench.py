@@ -1061,6 +1061,8 @@ def latency_150_under_load(mode, iters, load_heights=30_000, gap_ms=1.0, windows
     call, keep = _commit_c_call(ctx, sv, commit, TU.block_id_for_height(1000), 1000, mode)
     chain = TU.ReplayChain(ctx, sv, 2000, load_heights, flip=0.0)
     idle = _p50_p99(call, iters, warm=50)
+    # the same calls 1 ms apart with no load (the loaded pattern without the load)
+    idle_spaced = _p50_p99_inner(call, lambda: time.sleep(gap_ms * 1e-3), iters, warm=20)
     stop = threading.Event()
     passes = [0]
     t_bulk = []
@@ -1100,6 +1102,8 @@ def latency_150_under_load(mode, iters, load_heights=30_000, gap_ms=1.0, windows
     ctx.close()
     return {"idle_p50_ms": idle[0], "idle_p99_ms": idle[1], "p50_ms": loaded[0], "p99_ms": loaded[1],
             "p99_over_idle_p99": round(loaded[1] / idle[1], 2), "iters": iters,
+            "idle_spaced_p50_ms": idle_spaced[0], "idle_spaced_p99_ms": idle_spaced[1],
+            "p99_over_idle_spaced_p99": round(loaded[1] / idle_spaced[1], 2),
             "load": f"cmtv_verify_commits over {load_heights} x 150 commits in a loop on the same context "
                     f"({passes[0]} passes, median {round(float(np.median(t_bulk)) * 1e3, 2) if t_bulk else None} "
                     "ms each)", "load_ok": bool(np.all(rcs == 0)),

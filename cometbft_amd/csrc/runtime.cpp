@@ -390,6 +390,7 @@ struct BulkSlot {
   DevBuf d_in;    // the staging on the device, then the sign-bytes
   DevBuf d_bm;    // verdict bitmap
   hipEvent_t h2d = nullptr, done = nullptr;
+  hipEvent_t prep = nullptr;  // the chunk's gather + sign-bytes done (BulkLane::prep)
   bool pending = false;  // submitted, not yet waited for
 };
 struct BulkLane {
@@ -398,6 +399,10 @@ struct BulkLane {
   // the reserved ones (its own hardware queue, cu_mask), and the waves one
   // round of it holds at two per SIMD (the keyed batch kernel's occupancy)
   hipStream_t exec_masked = nullptr;
+  // an unmasked chunk's k_bulk_gather + k_sign_bytes run here, so they overlap
+  // the previous chunk's keyed launch instead of following it on exec
+  // (CMTV_PREP_STREAM=0: on exec)
+  hipStream_t prep = nullptr;
   // ... and the device's latency stream while a pipeline call is in flight
   // (LatencyStreams): the reserved CUs only, so a 150-validator commit's
   // workgroups never share a CU -- its SIMDs, its instruction cache (one per
@@ -601,6 +606,7 @@ struct cmtv_ctx {
   // 0.1118 / 0.1074 / 0.108 ms, heap 0.114-0.117 against 0.117-0.123 ms
   bool keyed_zc = true;
   bool spin_wait = false;  // CMTV_SPIN_WAIT (wait_stream)
+  bool prep_stream = true;  // CMTV_PREP_STREAM (BulkLane::prep)
   uint64_t lat_window_ns = 10'000'000'000ull;
   uint32_t lat_reserve_cus = 16;
   // latency calls beside a pipeline run on the reserved CUs only
@@ -1912,6 +1918,7 @@ static void read_env(cmtv_ctx* ctx) {
   if (const char* v = std::getenv("CMTV_QUAD_POLL")) ctx->quad_poll = v[0] == '1';
   if (const char* v = std::getenv("CMTV_KEYED_ZC")) ctx->keyed_zc = v[0] != '0';
   if (const char* v = std::getenv("CMTV_SPIN_WAIT")) ctx->spin_wait = v[0] == '1';
+  if (const char* v = std::getenv("CMTV_PREP_STREAM")) ctx->prep_stream = v[0] != '0';
   if (const char* v = std::getenv("CMTV_LAT_ISOLATE")) ctx->lat_isolate = v[0] != '0';
   if (const char* v = std::getenv("CMTV_LAT_RESERVE_CUS")) {
     const long k = std::strtol(v, nullptr, 10);
@@ -2632,6 +2639,7 @@ static hipError_t bulk_lane_init(cmtv_ctx* ctx, CmtvDev& D) {
   };
   hipError_t e = own_queue(&L.copy);
   if (e == hipSuccess) e = own_queue(&L.exec);
+  if (e == hipSuccess && ctx->prep_stream) e = own_queue(&L.prep);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&L.scratch.done, hipEventDisableTiming);
   if (e == hipSuccess) {
     // The reserved CUs: the masked exec stream gets every other CU, the
@@ -2671,6 +2679,7 @@ static hipError_t bulk_lane_init(cmtv_ctx* ctx, CmtvDev& D) {
   for (int k = 0; k < kBulkSlotsMax && e == hipSuccess; k++) {
     e = hipEventCreateWithFlags(&L.slot[k].h2d, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&L.slot[k].done, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&L.slot[k].prep, hipEventDisableTiming);
   }
   (void)ctx;
   return e;
@@ -2681,6 +2690,7 @@ static void bulk_lane_release(CmtvDev& D) {
   if (L.exec) (void)hipStreamSynchronize(L.exec);
   if (L.exec_masked) (void)hipStreamSynchronize(L.exec_masked);
   if (L.copy) (void)hipStreamSynchronize(L.copy);
+  if (L.prep) (void)hipStreamSynchronize(L.prep);
   for (auto& S : L.slot) {
     S.h_in.release();
     S.h_bm.release();
@@ -2688,7 +2698,8 @@ static void bulk_lane_release(CmtvDev& D) {
     S.d_bm.release();
     if (S.h2d) (void)hipEventDestroy(S.h2d);
     if (S.done) (void)hipEventDestroy(S.done);
-    S.h2d = S.done = nullptr;
+    if (S.prep) (void)hipEventDestroy(S.prep);
+    S.h2d = S.done = S.prep = nullptr;
     S.pending = false;
   }
   L.scratch.buf.release();
@@ -2699,6 +2710,8 @@ static void bulk_lane_release(CmtvDev& D) {
   if (L.exec_masked) (void)hipStreamDestroy(L.exec_masked);
   if (L.copy) (void)hipStreamDestroy(L.copy);
   if (L.lat) (void)hipStreamDestroy(L.lat);
+  if (L.prep) (void)hipStreamDestroy(L.prep);
+  L.prep = nullptr;
   if (L.lat_in) (void)hipEventDestroy(L.lat_in);
   if (L.lat_out) (void)hipEventDestroy(L.lat_out);
   L.exec = L.exec_masked = L.copy = L.lat = nullptr;
@@ -2743,7 +2756,11 @@ int bulk_submit_locked(cmtv_ctx* ctx, size_t dev, int slot, const BulkLayout& L,
       if ((e = hipMemcpyAsync(din + L.o_arena + L.spans[k].dev_off, L.spans[k].host, L.spans[k].bytes,
                               hipMemcpyHostToDevice, BL.copy)) != hipSuccess)
         return hip_fail(e);
-  if ((e = hipEventRecord(S.h2d, BL.copy)) != hipSuccess || (e = hipStreamWaitEvent(ex, S.h2d, 0)) != hipSuccess)
+  // the gather and the sign-bytes: on the prep stream for an unmasked chunk
+  // (they overlap the previous chunk's keyed launch on exec: ~60 + 40 us a
+  // chunk, round 6 rocprof of replay_c3_host), else in line on exec
+  hipStream_t ps = (!masked && BL.prep) ? BL.prep : ex;
+  if ((e = hipEventRecord(S.h2d, BL.copy)) != hipSuccess || (e = hipStreamWaitEvent(ps, S.h2d, 0)) != hipSuccess)
     return hip_fail(e);
   auto* off = reinterpret_cast<uint32_t*>(din + L.o_off);
   if (L.direct) {
@@ -2753,14 +2770,17 @@ int bulk_submit_locked(cmtv_ctx* ctx, size_t dev, int slot, const BulkLayout& L,
                                 reinterpret_cast<uint32_t*>(din + L.o_key), din + L.o_sig, off,
                                 reinterpret_cast<uint32_t*>(din + L.o_tidx), din + L.o_flag,
                                 reinterpret_cast<int64_t*>(din + L.o_sec), reinterpret_cast<int32_t*>(din + L.o_nanos),
-                                cb, cb + L.n_tmpls, ex)) != hipSuccess)
+                                cb, cb + L.n_tmpls, ps)) != hipSuccess)
       return hip_fail(e);
   }
   // sign-bytes from the chunk's templates into o_msg (k_sign_bytes; the
   // bulk chunks run the lane kernels, whose launches take no fused form)
   if ((e = launch_sign_bytes((uint32_t)L.m, din + L.o_tmpl, din + L.o_blob, reinterpret_cast<uint32_t*>(din + L.o_tidx),
                              din + L.o_flag, reinterpret_cast<int64_t*>(din + L.o_sec),
-                             reinterpret_cast<int32_t*>(din + L.o_nanos), off, din + L.o_msg, ex)) != hipSuccess)
+                             reinterpret_cast<int32_t*>(din + L.o_nanos), off, din + L.o_msg, ps)) != hipSuccess)
+    return hip_fail(e);
+  if (ps != ex &&
+      ((e = hipEventRecord(S.prep, ps)) != hipSuccess || (e = hipStreamWaitEvent(ex, S.prep, 0)) != hipSuccess))
     return hip_fail(e);
   int rc;
   if (ks)
@@ -2798,6 +2818,7 @@ void bulk_drain(cmtv_ctx* ctx) {
     (void)hipStreamSynchronize(D.bulk.copy);
     (void)hipStreamSynchronize(D.bulk.exec);
     if (D.bulk.exec_masked) (void)hipStreamSynchronize(D.bulk.exec_masked);
+    if (D.bulk.prep) (void)hipStreamSynchronize(D.bulk.prep);
     for (auto& S : D.bulk.slot) S.pending = false;
   }
   (void)hipGetLastError();

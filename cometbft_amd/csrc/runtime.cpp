@@ -386,7 +386,9 @@ struct Timing {
 // the cross-height pipeline.
 struct BulkSlot {
   HostBuf h_in;   // pinned staging, packed by the host workers
-  HostBuf h_bm;   // pinned verdict bitmap (D2H)
+  // verdict bitmap: D2H'd into it, or (registered-key chunks) written there
+  // by the kernel itself (coherent, mapped)
+  HostBuf h_bm{nullptr, 0, hipHostMallocCoherent | hipHostMallocMapped};
   DevBuf d_in;    // the staging on the device, then the sign-bytes
   DevBuf d_bm;    // verdict bitmap
   hipEvent_t h2d = nullptr, done = nullptr;
@@ -607,6 +609,7 @@ struct cmtv_ctx {
   bool keyed_zc = true;
   bool spin_wait = false;  // CMTV_SPIN_WAIT (wait_stream)
   bool prep_stream = true;  // CMTV_PREP_STREAM (BulkLane::prep)
+  bool bulk_bm_direct = true;  // CMTV_BULK_BM_DIRECT (bulk_submit_locked)
   uint64_t lat_window_ns = 10'000'000'000ull;
   uint32_t lat_reserve_cus = 16;
   // latency calls beside a pipeline run on the reserved CUs only
@@ -1919,6 +1922,7 @@ static void read_env(cmtv_ctx* ctx) {
   if (const char* v = std::getenv("CMTV_KEYED_ZC")) ctx->keyed_zc = v[0] != '0';
   if (const char* v = std::getenv("CMTV_SPIN_WAIT")) ctx->spin_wait = v[0] == '1';
   if (const char* v = std::getenv("CMTV_PREP_STREAM")) ctx->prep_stream = v[0] != '0';
+  if (const char* v = std::getenv("CMTV_BULK_BM_DIRECT")) ctx->bulk_bm_direct = v[0] != '0';
   if (const char* v = std::getenv("CMTV_LAT_ISOLATE")) ctx->lat_isolate = v[0] != '0';
   if (const char* v = std::getenv("CMTV_LAT_RESERVE_CUS")) {
     const long k = std::strtol(v, nullptr, 10);
@@ -2783,15 +2787,25 @@ int bulk_submit_locked(cmtv_ctx* ctx, size_t dev, int slot, const BulkLayout& L,
       ((e = hipEventRecord(S.prep, ps)) != hipSuccess || (e = hipStreamWaitEvent(ex, S.prep, 0)) != hipSuccess))
     return hip_fail(e);
   int rc;
+  // a registered-key chunk's kernel stores its verdict words straight into
+  // the slot's mapped host bitmap: no D2H between this launch and the next
+  // chunk's on exec (round 6: consecutive keyed launches were 84-135 us
+  // apart, ~2 ms of a 40 ms pass; CMTV_BULK_BM_DIRECT=0 copies as before)
+  uint64_t* hbm_dev = nullptr;
+  if (ks && ctx->bulk_bm_direct) {
+    void* q = nullptr;
+    if ((e = hipHostGetDevicePointer(&q, S.h_bm.p, 0)) != hipSuccess) return hip_fail(e);
+    hbm_dev = static_cast<uint64_t*>(q);
+  }
   if (ks)
     rc = enqueue_verify_keyed(ctx, D, ks->dev[dev], ks->n, L.m, reinterpret_cast<uint32_t*>(din + L.o_key),
-                              din + L.o_sig, din + L.o_msg, off, mode, nullptr, dbm, ex, &BL.scratch, nullptr,
-                              masked ? BL.masked_waves : 0);
+                              din + L.o_sig, din + L.o_msg, off, mode, nullptr, hbm_dev ? hbm_dev : dbm, ex,
+                              &BL.scratch, nullptr, masked ? BL.masked_waves : 0);
   else
     rc = enqueue_verify(ctx, D, L.m, din + L.o_key, din + L.o_sig, din + L.o_msg, off, mode, nullptr, dbm, ex,
                         nullptr, &BL.scratch);
   if (rc != CMTV_OK) return rc;
-  if ((e = hipMemcpyAsync(S.h_bm.p, dbm, 8 * words, hipMemcpyDeviceToHost, ex)) != hipSuccess ||
+  if ((!hbm_dev && (e = hipMemcpyAsync(S.h_bm.p, dbm, 8 * words, hipMemcpyDeviceToHost, ex)) != hipSuccess) ||
       (e = hipEventRecord(S.done, ex)) != hipSuccess)
     return hip_fail(e);
   S.pending = true;

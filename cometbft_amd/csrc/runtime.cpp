@@ -609,7 +609,10 @@ struct cmtv_ctx {
   bool keyed_zc = true;
   bool spin_wait = false;  // CMTV_SPIN_WAIT (wait_stream)
   bool prep_stream = true;  // CMTV_PREP_STREAM (BulkLane::prep)
-  bool bulk_bm_direct = true;  // CMTV_BULK_BM_DIRECT (bulk_submit_locked)
+  // CMTV_BULK_BM_DIRECT=1 (bulk_submit_locked): off -- two alternating rounds
+  // (profiles/r06_bm_direct_ab.txt) gave VerifyCommit -0.13 ms but
+  // VerifyCommitLight +0.5-0.7 ms per pass
+  bool bulk_bm_direct = false;
   uint64_t lat_window_ns = 10'000'000'000ull;
   uint32_t lat_reserve_cus = 16;
   // latency calls beside a pipeline run on the reserved CUs only
@@ -1922,7 +1925,7 @@ static void read_env(cmtv_ctx* ctx) {
   if (const char* v = std::getenv("CMTV_KEYED_ZC")) ctx->keyed_zc = v[0] != '0';
   if (const char* v = std::getenv("CMTV_SPIN_WAIT")) ctx->spin_wait = v[0] == '1';
   if (const char* v = std::getenv("CMTV_PREP_STREAM")) ctx->prep_stream = v[0] != '0';
-  if (const char* v = std::getenv("CMTV_BULK_BM_DIRECT")) ctx->bulk_bm_direct = v[0] != '0';
+  if (const char* v = std::getenv("CMTV_BULK_BM_DIRECT")) ctx->bulk_bm_direct = v[0] == '1';
   if (const char* v = std::getenv("CMTV_LAT_ISOLATE")) ctx->lat_isolate = v[0] != '0';
   if (const char* v = std::getenv("CMTV_LAT_RESERVE_CUS")) {
     const long k = std::strtol(v, nullptr, 10);
@@ -2790,7 +2793,7 @@ int bulk_submit_locked(cmtv_ctx* ctx, size_t dev, int slot, const BulkLayout& L,
   // a registered-key chunk's kernel stores its verdict words straight into
   // the slot's mapped host bitmap: no D2H between this launch and the next
   // chunk's on exec (round 6: consecutive keyed launches were 84-135 us
-  // apart, ~2 ms of a 40 ms pass; CMTV_BULK_BM_DIRECT=0 copies as before)
+  // apart, ~2 ms of a 40 ms pass; CMTV_BULK_BM_DIRECT=1, measured neutral)
   uint64_t* hbm_dev = nullptr;
   if (ks && ctx->bulk_bm_direct) {
     void* q = nullptr;

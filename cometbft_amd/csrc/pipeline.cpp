@@ -989,7 +989,10 @@ int run_pipeline(cmtv_ctx* ctx, const CommitsArgs& args, int* rcs, std::vector<c
       pack(ch, h);
       const uint64_t ts = now_ns();
       ph_pack += ts - tk;
-      {
+      // the lane-only part first, outside the context lock (a latency call
+      // on the context never waits behind it), then the launch under it
+      rc = bulk_prepare(ctx, ch.dev, ch.slot, ch.L, ch.ks);
+      if (rc == CMTV_OK) {
         Relock g(ctx, lk);
         rc = bulk_submit_locked(ctx, ch.dev, ch.slot, ch.L, ch.ks, mode);
         if (rc == CMTV_OK && ch.direct) count_direct_locked(ctx);

@@ -2736,10 +2736,13 @@ int bulk_stage(cmtv_ctx* ctx, size_t dev, int slot, const BulkLayout& L, uint8_t
   return CMTV_OK;
 }
 
-int bulk_submit_locked(cmtv_ctx* ctx, size_t dev, int slot, const BulkLayout& L, const cmtv_keyset* ks,
-                       uint32_t mode) {
+int bulk_prepare(cmtv_ctx* ctx, size_t dev, int slot, const BulkLayout& L, const cmtv_keyset* ks) {
+  // Everything of a chunk's submission that touches only the lane (its
+  // streams, its slot's buffers): the staging's H2D, the direct chunk's
+  // DMAs and gather, the sign-bytes. The bulk lock orders it; the context
+  // lock is not taken, so a latency call never waits behind these ~10 HIP
+  // calls (round 6) -- bulk_submit_locked then enqueues the launch.
   CmtvDev& D = ctx->devs[dev];
-  if (D.failed) return CMTV_EHIP;  // retired by another call meanwhile
   if (hipSetDevice(D.ordinal) != hipSuccess) return CMTV_ENODEV;
   BulkLane& BL = D.bulk;
   BulkSlot& S = BL.slot[slot];
@@ -2747,28 +2750,25 @@ int bulk_submit_locked(cmtv_ctx* ctx, size_t dev, int slot, const BulkLayout& L,
   hipError_t e = S.d_in.ensure(L.dev_bytes);
   if (e == hipSuccess) e = S.d_bm.ensure(8 * std::max<size_t>(words, 1));
   if (e == hipSuccess) e = S.h_bm.ensure(8 * std::max<size_t>(words, 1));
-  if (e != hipSuccess) return hip_fail(e);
-  // near a latency call: the CU-masked stream, and batched launches sized
-  // to the waves its CUs hold in one round
+  if (e != hipSuccess) return CMTV_EHIP;
   const bool masked = L.masked && BL.exec_masked;
   hipStream_t ex = masked ? BL.exec_masked : BL.exec;
   auto* din = static_cast<uint8_t*>(S.d_in.p);
-  auto* dbm = static_cast<uint64_t*>(S.d_bm.p);
   // H2D on the copy stream (overlaps the exec stream's previous chunk); a
   // direct chunk's per-signature data comes straight from the caller's
   // pinned arena, one DMA per span, and is laid out by k_bulk_gather
-  if ((e = hipMemcpyAsync(din, S.h_in.p, L.in_bytes, hipMemcpyHostToDevice, BL.copy)) != hipSuccess) return hip_fail(e);
+  if ((e = hipMemcpyAsync(din, S.h_in.p, L.in_bytes, hipMemcpyHostToDevice, BL.copy)) != hipSuccess) return CMTV_EHIP;
   if (L.direct)
     for (int k = 0; k < L.n_spans; k++)
       if ((e = hipMemcpyAsync(din + L.o_arena + L.spans[k].dev_off, L.spans[k].host, L.spans[k].bytes,
                               hipMemcpyHostToDevice, BL.copy)) != hipSuccess)
-        return hip_fail(e);
+        return CMTV_EHIP;
   // the gather and the sign-bytes: on the prep stream for an unmasked chunk
   // (they overlap the previous chunk's keyed launch on exec: ~60 + 40 us a
   // chunk, round 6 rocprof of replay_c3_host), else in line on exec
   hipStream_t ps = (!masked && BL.prep) ? BL.prep : ex;
   if ((e = hipEventRecord(S.h2d, BL.copy)) != hipSuccess || (e = hipStreamWaitEvent(ps, S.h2d, 0)) != hipSuccess)
-    return hip_fail(e);
+    return CMTV_EHIP;
   auto* off = reinterpret_cast<uint32_t*>(din + L.o_off);
   if (L.direct) {
     if (!ks) return CMTV_EINVAL;  // direct chunks are registered-key chunks
@@ -2778,17 +2778,36 @@ int bulk_submit_locked(cmtv_ctx* ctx, size_t dev, int slot, const BulkLayout& L,
                                 reinterpret_cast<uint32_t*>(din + L.o_tidx), din + L.o_flag,
                                 reinterpret_cast<int64_t*>(din + L.o_sec), reinterpret_cast<int32_t*>(din + L.o_nanos),
                                 cb, cb + L.n_tmpls, ps)) != hipSuccess)
-      return hip_fail(e);
+      return CMTV_EHIP;
   }
   // sign-bytes from the chunk's templates into o_msg (k_sign_bytes; the
   // bulk chunks run the lane kernels, whose launches take no fused form)
   if ((e = launch_sign_bytes((uint32_t)L.m, din + L.o_tmpl, din + L.o_blob, reinterpret_cast<uint32_t*>(din + L.o_tidx),
                              din + L.o_flag, reinterpret_cast<int64_t*>(din + L.o_sec),
                              reinterpret_cast<int32_t*>(din + L.o_nanos), off, din + L.o_msg, ps)) != hipSuccess)
-    return hip_fail(e);
-  if (ps != ex &&
-      ((e = hipEventRecord(S.prep, ps)) != hipSuccess || (e = hipStreamWaitEvent(ex, S.prep, 0)) != hipSuccess))
-    return hip_fail(e);
+    return CMTV_EHIP;
+  if (ps != ex && (e = hipEventRecord(S.prep, ps)) != hipSuccess) return CMTV_EHIP;
+  return CMTV_OK;
+}
+
+int bulk_submit_locked(cmtv_ctx* ctx, size_t dev, int slot, const BulkLayout& L, const cmtv_keyset* ks,
+                       uint32_t mode) {
+  CmtvDev& D = ctx->devs[dev];
+  if (D.failed) return CMTV_EHIP;  // retired by another call meanwhile
+  if (hipSetDevice(D.ordinal) != hipSuccess) return CMTV_ENODEV;
+  BulkLane& BL = D.bulk;
+  BulkSlot& S = BL.slot[slot];
+  const size_t words = (L.m + 63) / 64;
+  hipError_t e;
+  // near a latency call: the CU-masked stream, and batched launches sized
+  // to the waves its CUs hold in one round
+  const bool masked = L.masked && BL.exec_masked;
+  hipStream_t ex = masked ? BL.exec_masked : BL.exec;
+  auto* din = static_cast<uint8_t*>(S.d_in.p);
+  auto* dbm = static_cast<uint64_t*>(S.d_bm.p);
+  auto* off = reinterpret_cast<uint32_t*>(din + L.o_off);
+  // the chunk's prep (bulk_prepare) ran on the prep stream: exec waits for it
+  if (!masked && BL.prep && (e = hipStreamWaitEvent(ex, S.prep, 0)) != hipSuccess) return hip_fail(e);
   int rc;
   // a registered-key chunk's kernel stores its verdict words straight into
   // the slot's mapped host bitmap: no D2H between this launch and the next

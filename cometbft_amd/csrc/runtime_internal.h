@@ -182,8 +182,12 @@ struct LatencyStreams {
 void live_devices_locked(cmtv_ctx* ctx, std::vector<size_t>& out);
 // the pinned staging of (dev, slot), grown to L.in_bytes (bulk lock held)
 int bulk_stage(cmtv_ctx* ctx, size_t dev, int slot, const BulkLayout& L, uint8_t** host);
-// enqueues the chunk staged in (dev, slot): H2D, sign-bytes, verification
-// (ks: by registered key), verdict bitmap D2H (context lock held)
+// enqueues the lane-only part of the chunk staged in (dev, slot): H2D, the
+// direct chunk's DMAs and gather, the sign-bytes (bulk lock held, not the
+// context lock)
+int bulk_prepare(cmtv_ctx* ctx, size_t dev, int slot, const BulkLayout& L, const cmtv_keyset* ks);
+// ... then its verification (ks: by registered key) and verdict bitmap D2H
+// (context lock held)
 int bulk_submit_locked(cmtv_ctx* ctx, size_t dev, int slot, const BulkLayout& L, const cmtv_keyset* ks,
                        uint32_t mode);
 // waits for the chunk in (dev, slot); *bitmap = its verdict words (pinned)

@@ -283,6 +283,8 @@ int bulk_stage(cmtv_ctx* ctx, size_t dev, int slot, const BulkLayout& L, uint8_t
   return CMTV_OK;
 }
 
+// the fake does the whole chunk in bulk_submit_locked
+int bulk_prepare(cmtv_ctx*, size_t, int, const BulkLayout&, const cmtv_keyset*) { return CMTV_OK; }
 int bulk_submit_locked(cmtv_ctx* ctx, size_t dev, int slot, const BulkLayout& L, const cmtv_keyset* ks,
                        uint32_t mode) {
   FakeSlot& S = ctx->slots[dev][slot];

@@ -794,9 +794,19 @@ static int cmtv_verify_commit_impl(cmtv_ctx* ctx, uint32_t kind, uint32_t mode, 
   }
   thread_local Seen seen;
   cmtv::note_latency(ctx);  // a consensus-path call: pipelines leave it CUs
+  const bool traced = cmtv::call_trace_on(ctx);
+  const uint64_t t_entry = traced ? cmtv::call_trace_now() : 0;
   std::unique_lock<std::mutex> lk;
   rc = cmtv::ctx_lock(ctx, lk);
   if (rc != CMTV_OK) return rc;
+  struct TraceGuard {  // CMTV_CALL_TRACE: recorded before the lock is released
+    cmtv_ctx* c;
+    uint64_t t_entry, t_locked;
+    ~TraceGuard() {
+      if (t_locked) cmtv::call_trace_record_locked(c, t_entry, t_locked);
+    }
+  } trace_guard{ctx, t_entry, traced ? cmtv::call_trace_now() : 0};
+  if (traced) cmtv::call_trace_begin_locked(ctx);
   // beside a pipeline call: the CUs its chunks leave free (released before
   // the lock)
   cmtv::LatencyStreams lat_streams(ctx);

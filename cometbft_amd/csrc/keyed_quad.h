@@ -103,14 +103,30 @@ CMTV_HD bool q_verify_keyed_split(const Q& q, bool key_ok, const uint32_t* sig_p
     }
   }
   get_k(tk);
+  // the key comb, software-pipelined: window it + 1's row is loaded before
+  // window it's addition, so its HBM latency hides behind that addition
+  // (~2.5k cycles) instead of opening each window -- which matters most
+  // beside a pipeline's bulk launch, when the loads queue behind its
+  // traffic (round 6, CMTV_CALL_TRACE: the loaded 150-validator call's
+  // launch-to-verdict p90 was 50 us over its p50)
+  int dA = (int)sc_shift_out(tk, 8) - 128;
+  int ia = dA < 0 ? -dA : dA;
+  fe cn;
+  {
+    const uint32_t* row = ktab + ((size_t)(COMB_WINDOWS - 1) * COMB_ENTRIES + (ia > 0 ? ia - 1 : 0)) * COMB_ROW_WORDS;
+    q_niels_load(q, cn, [&](int off, fe& r) { comb_load(row, off, r); }, 10, 20, dA < 0);
+  }
 #pragma unroll 1
   for (int it = 0; it < COMB_WINDOWS; it++) {
-    const int j = COMB_WINDOWS - 1 - it;
-    const int dA = (int)sc_shift_out(tk, 8) - 128;
-    const int ia = dA < 0 ? -dA : dA;
-    fe c;
-    const uint32_t* row = ktab + ((size_t)j * COMB_ENTRIES + (ia > 0 ? ia - 1 : 0)) * COMB_ROW_WORDS;
-    q_niels_coord(q, c, [&](int off, fe& r) { comb_load(row, off, r); }, 10, 20, dA < 0, ia == 0);
+    fe c = cn;
+    q_niels_fix(c, lane, dA < 0, ia == 0);
+    if (it + 1 < COMB_WINDOWS) {
+      const int j = COMB_WINDOWS - 2 - it;
+      dA = (int)sc_shift_out(tk, 8) - 128;
+      ia = dA < 0 ? -dA : dA;
+      const uint32_t* row = ktab + ((size_t)j * COMB_ENTRIES + (ia > 0 ? ia - 1 : 0)) * COMB_ROW_WORDS;
+      q_niels_load(q, cn, [&](int off, fe& r) { comb_load(row, off, r); }, 10, 20, dA < 0);
+    }
     q_add(q, v, c);
   }
   fe rc;

@@ -991,10 +991,11 @@ int run_pipeline(cmtv_ctx* ctx, const CommitsArgs& args, int* rcs, std::vector<c
       ph_pack += ts - tk;
       // the lane-only part first, outside the context lock (a latency call
       // on the context never waits behind it), then the launch under it
-      rc = bulk_prepare(ctx, ch.dev, ch.slot, ch.L, ch.ks);
+      if (pc.split_submit) rc = bulk_prepare(ctx, ch.dev, ch.slot, ch.L, ch.ks);
       if (rc == CMTV_OK) {
         Relock g(ctx, lk);
-        rc = bulk_submit_locked(ctx, ch.dev, ch.slot, ch.L, ch.ks, mode);
+        if (!pc.split_submit) rc = bulk_prepare(ctx, ch.dev, ch.slot, ch.L, ch.ks);
+        if (rc == CMTV_OK) rc = bulk_submit_locked(ctx, ch.dev, ch.slot, ch.L, ch.ks, mode);
         if (rc == CMTV_OK && ch.direct) count_direct_locked(ctx);
       }
       ph_submit += now_ns() - ts;

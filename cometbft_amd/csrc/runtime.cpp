@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -613,6 +614,14 @@ struct cmtv_ctx {
   // (profiles/r06_bm_direct_ab.txt) gave VerifyCommit -0.13 ms but
   // VerifyCommitLight +0.5-0.7 ms per pass
   bool bulk_bm_direct = false;
+  bool split_submit = true;  // CMTV_SPLIT_SUBMIT (PipeConfig::split_submit)
+  // CMTV_CALL_TRACE=1 (diagnostics): per single-commit call, the time to the
+  // context lock, to the launch, to the verdicts and to the return; their
+  // percentiles printed on stderr at cmtv_close
+  bool call_trace = false, call_trace_loaded_only = false;
+  uint64_t trace_launch = 0, trace_wait = 0;  // this hold's marks (lock held)
+  std::mutex trace_mu;
+  std::vector<std::array<uint64_t, 4>> trace_rows;
   uint64_t lat_window_ns = 10'000'000'000ull;
   uint32_t lat_reserve_cus = 16;
   // latency calls beside a pipeline run on the reserved CUs only
@@ -1360,7 +1369,9 @@ static int run_host_batch_(cmtv_ctx* ctx, const HostBatch& B, uint8_t* out_valid
       D.poll_pending = true;
     }
     const uint64_t t_wait = phase_now(ctx);
+    if (ctx->call_trace) ctx->trace_launch = call_trace_now();
     if ((e = D.tag_used ? wait_row_tags(D, n) : wait_stream(ctx, D.stream)) != hipSuccess) return hip_fail(e);
+    if (ctx->call_trace) ctx->trace_wait = call_trace_now();
     uint64_t* bm = static_cast<uint64_t*>(D.h_zc.p);
     if (D.tag_used) {
       ctx->stats.polled_calls++;
@@ -1926,6 +1937,11 @@ static void read_env(cmtv_ctx* ctx) {
   if (const char* v = std::getenv("CMTV_SPIN_WAIT")) ctx->spin_wait = v[0] == '1';
   if (const char* v = std::getenv("CMTV_PREP_STREAM")) ctx->prep_stream = v[0] != '0';
   if (const char* v = std::getenv("CMTV_BULK_BM_DIRECT")) ctx->bulk_bm_direct = v[0] == '1';
+  if (const char* v = std::getenv("CMTV_SPLIT_SUBMIT")) ctx->split_submit = v[0] != '0';
+  if (const char* v = std::getenv("CMTV_CALL_TRACE")) {
+    ctx->call_trace = v[0] == '1' || v[0] == '2';
+    ctx->call_trace_loaded_only = v[0] == '2';  // only calls beside a pipeline call
+  }
   if (const char* v = std::getenv("CMTV_LAT_ISOLATE")) ctx->lat_isolate = v[0] != '0';
   if (const char* v = std::getenv("CMTV_LAT_RESERVE_CUS")) {
     const long k = std::strtol(v, nullptr, 10);
@@ -2099,6 +2115,30 @@ void cmtv_close(cmtv_ctx* ctx) {
       std::fprintf(stderr, "%s\"%s\": %.3f", p ? ", " : "", names[p],
                    ctx->phase_calls ? 1e-3 * (double)ctx->phase_ns[p] / (double)ctx->phase_calls : 0.0);
     std::fprintf(stderr, "}, \"calls\": %llu}\n", (unsigned long long)ctx->phase_calls);
+  }
+  if (ctx->call_trace && !ctx->trace_rows.empty()) {
+    static const char* seg[4] = {"to_lock", "to_launch", "gpu_and_wake", "post"};
+    std::fprintf(stderr, "{\"cmtv_call_trace_us\": {\"calls\": %zu", ctx->trace_rows.size());
+    for (int k = 0; k < 4; k++) {
+      std::vector<uint64_t> v;
+      for (auto& r : ctx->trace_rows) v.push_back(r[k]);
+      std::sort(v.begin(), v.end());
+      auto q = [&](double f) { return 1e-3 * (double)v[std::min(v.size() - 1, (size_t)(f * (double)v.size()))]; };
+      std::fprintf(stderr, ", \"%s\": [%.1f, %.1f, %.1f, %.1f]", seg[k], q(0.5), q(0.9), q(0.99), q(1.0));
+    }
+    // the slowest tenth of calls: which segment took their excess
+    std::vector<size_t> idx(ctx->trace_rows.size());
+    for (size_t i = 0; i < idx.size(); i++) idx[i] = i;
+    auto total = [&](size_t i) { auto& r = ctx->trace_rows[i]; return r[0] + r[1] + r[2] + r[3]; };
+    std::sort(idx.begin(), idx.end(), [&](size_t a, size_t b) { return total(a) < total(b); });
+    std::fprintf(stderr, ", \"slowest_1pct\": [");
+    const size_t from = idx.size() - std::max<size_t>(1, idx.size() / 100);
+    for (size_t j = from; j < idx.size(); j++) {
+      auto& r = ctx->trace_rows[idx[j]];
+      std::fprintf(stderr, "%s[%.1f, %.1f, %.1f, %.1f]", j > from ? ", " : "", 1e-3 * r[0], 1e-3 * r[1], 1e-3 * r[2],
+                   1e-3 * r[3]);
+    }
+    std::fprintf(stderr, "]}}\n");
   }
   ctx->pool.reset();
   for (auto& b : ctx->pinned) (void)hipHostFree(reinterpret_cast<void*>(b.first));  // the caller's leftovers
@@ -2553,12 +2593,25 @@ HostPool& host_pool(cmtv_ctx* ctx) {
 
 PipeConfig pipe_config(const cmtv_ctx* ctx) {
   PipeConfig pc{ctx->pipe_min, ctx->pipe_chunk, ctx->pipe_slots, ctx->pipe_on, ctx->pipe_direct};
+  pc.split_submit = ctx->split_submit;
   // a masked lane's round: the chunk scaled to the CUs it keeps (bulk_lane_init)
   const uint32_t reserved = reserved_cus(ctx, ctx->cus);
   pc.chunk_masked = ctx->cus > reserved
                         ? std::max<size_t>(64, ctx->pipe_chunk / ctx->cus * (ctx->cus - reserved))
                         : ctx->pipe_chunk;
   return pc;
+}
+
+bool call_trace_on(const cmtv_ctx* ctx) { return ctx->call_trace; }
+uint64_t call_trace_now() { return now_ns_steady(); }
+void call_trace_begin_locked(cmtv_ctx* ctx) { ctx->trace_launch = ctx->trace_wait = 0; }
+void call_trace_record_locked(cmtv_ctx* ctx, uint64_t t_entry, uint64_t t_locked) {
+  const uint64_t t_end = now_ns_steady();
+  if (!ctx->trace_launch || !ctx->trace_wait) return;  // no small host batch ran
+  if (ctx->call_trace_loaded_only && !ctx->bulk_now) return;
+  std::lock_guard<std::mutex> g(ctx->trace_mu);
+  ctx->trace_rows.push_back({t_locked - t_entry, ctx->trace_launch - t_locked, ctx->trace_wait - ctx->trace_launch,
+                             t_end - ctx->trace_wait});
 }
 
 void note_latency(cmtv_ctx* ctx) {

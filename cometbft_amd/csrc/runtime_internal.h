@@ -152,6 +152,8 @@ struct PipeConfig {
   // a direct chunk ends where its DMA extents pass span_factor x the bytes
   // its plans read + span_slack (pipeline.cpp cut_chunk; tests shrink them)
   uint64_t span_factor = 4, span_slack = 64ull << 20;
+  // bulk_prepare outside the context lock (CMTV_SPLIT_SUBMIT)
+  bool split_submit = true;
 };
 PipeConfig pipe_config(const cmtv_ctx* ctx);
 // Latency calls beside the pipeline (runtime.cpp cmtv_ctx::lat_window_ns):
@@ -160,6 +162,11 @@ PipeConfig pipe_config(const cmtv_ctx* ctx);
 // to the CU-masked exec stream (BulkLayout::masked). BulkBusy marks a
 // pipeline call in flight (its scope).
 void note_latency(cmtv_ctx* ctx);
+// CMTV_CALL_TRACE (diagnostics, runtime.cpp cmtv_ctx::call_trace)
+bool call_trace_on(const cmtv_ctx* ctx);
+uint64_t call_trace_now();
+void call_trace_begin_locked(cmtv_ctx* ctx);
+void call_trace_record_locked(cmtv_ctx* ctx, uint64_t t_entry, uint64_t t_locked);
 bool latency_recent(const cmtv_ctx* ctx);
 struct BulkBusy {
   explicit BulkBusy(cmtv_ctx* c);

@@ -255,6 +255,10 @@ PipeConfig pipe_config(const cmtv_ctx* ctx) {
 // latency calls mark the context; the pipeline's chunks after one are masked
 // (a flag the fake only counts)
 void note_latency(cmtv_ctx* ctx) { ctx->latency_calls++; }
+bool call_trace_on(const cmtv_ctx*) { return false; }
+uint64_t call_trace_now() { return 0; }
+void call_trace_begin_locked(cmtv_ctx*) {}
+void call_trace_record_locked(cmtv_ctx*, uint64_t, uint64_t) {}
 bool latency_recent(const cmtv_ctx* ctx) { return ctx->latency_calls.load() > 0; }
 BulkBusy::BulkBusy(cmtv_ctx* c) : ctx(c) {}
 BulkBusy::~BulkBusy() {}

@@ -620,8 +620,10 @@ struct cmtv_ctx {
   // percentiles printed on stderr at cmtv_close
   bool call_trace = false, call_trace_loaded_only = false;
   uint64_t trace_launch = 0, trace_wait = 0;  // this hold's marks (lock held)
+  uint64_t trace_dev_ns = 0;
+  hipEvent_t trace_ev[2] = {nullptr, nullptr};
   std::mutex trace_mu;
-  std::vector<std::array<uint64_t, 4>> trace_rows;
+  std::vector<std::array<uint64_t, 5>> trace_rows;
   uint64_t lat_window_ns = 10'000'000'000ull;
   uint32_t lat_reserve_cus = 16;
   // latency calls beside a pipeline run on the reserved CUs only
@@ -1358,7 +1360,16 @@ static int run_host_batch_(cmtv_ctx* ctx, const HostBatch& B, uint8_t* out_valid
     D.tag_arm = poll ? D.d_tags : nullptr;
     D.tag_used = false;
     size_t o_valid = 0;
+    // CMTV_CALL_TRACE: the device time of this call's work, between two events
+    if (ctx->call_trace) {
+      if (!ctx->trace_ev[0]) {
+        (void)hipEventCreate(&ctx->trace_ev[0]);
+        (void)hipEventCreate(&ctx->trace_ev[1]);
+      }
+      (void)hipEventRecord(ctx->trace_ev[0], D.stream);
+    }
     const int rc = enqueue_shard(ctx, d0, B, 0, n, false, static_cast<uint64_t*>(dzc), o_valid, true);
+    if (ctx->call_trace) (void)hipEventRecord(ctx->trace_ev[1], D.stream);
     D.tag_arm = nullptr;
     if (rc != CMTV_OK) return rc;
     B.after_launch();
@@ -1371,7 +1382,14 @@ static int run_host_batch_(cmtv_ctx* ctx, const HostBatch& B, uint8_t* out_valid
     const uint64_t t_wait = phase_now(ctx);
     if (ctx->call_trace) ctx->trace_launch = call_trace_now();
     if ((e = D.tag_used ? wait_row_tags(D, n) : wait_stream(ctx, D.stream)) != hipSuccess) return hip_fail(e);
-    if (ctx->call_trace) ctx->trace_wait = call_trace_now();
+    if (ctx->call_trace) {
+      ctx->trace_wait = call_trace_now();
+      float ms = 0;
+      if (!D.tag_used && hipEventElapsedTime(&ms, ctx->trace_ev[0], ctx->trace_ev[1]) == hipSuccess)
+        ctx->trace_dev_ns = (uint64_t)(ms * 1e6f);
+      else
+        ctx->trace_dev_ns = 0;
+    }
     uint64_t* bm = static_cast<uint64_t*>(D.h_zc.p);
     if (D.tag_used) {
       ctx->stats.polled_calls++;
@@ -2117,9 +2135,9 @@ void cmtv_close(cmtv_ctx* ctx) {
     std::fprintf(stderr, "}, \"calls\": %llu}\n", (unsigned long long)ctx->phase_calls);
   }
   if (ctx->call_trace && !ctx->trace_rows.empty()) {
-    static const char* seg[4] = {"to_lock", "to_launch", "gpu_and_wake", "post"};
+    static const char* seg[5] = {"to_lock", "to_launch", "gpu_and_wake", "post", "device_events"};
     std::fprintf(stderr, "{\"cmtv_call_trace_us\": {\"calls\": %zu", ctx->trace_rows.size());
-    for (int k = 0; k < 4; k++) {
+    for (int k = 0; k < 5; k++) {
       std::vector<uint64_t> v;
       for (auto& r : ctx->trace_rows) v.push_back(r[k]);
       std::sort(v.begin(), v.end());
@@ -2135,11 +2153,13 @@ void cmtv_close(cmtv_ctx* ctx) {
     const size_t from = idx.size() - std::max<size_t>(1, idx.size() / 100);
     for (size_t j = from; j < idx.size(); j++) {
       auto& r = ctx->trace_rows[idx[j]];
-      std::fprintf(stderr, "%s[%.1f, %.1f, %.1f, %.1f]", j > from ? ", " : "", 1e-3 * r[0], 1e-3 * r[1], 1e-3 * r[2],
-                   1e-3 * r[3]);
+      std::fprintf(stderr, "%s[%.1f, %.1f, %.1f, %.1f, %.1f]", j > from ? ", " : "", 1e-3 * r[0], 1e-3 * r[1],
+                   1e-3 * r[2], 1e-3 * r[3], 1e-3 * r[4]);
     }
     std::fprintf(stderr, "]}}\n");
   }
+  for (auto& ev : ctx->trace_ev)
+    if (ev) (void)hipEventDestroy(ev);
   ctx->pool.reset();
   for (auto& b : ctx->pinned) (void)hipHostFree(reinterpret_cast<void*>(b.first));  // the caller's leftovers
   ctx->pinned.clear();
@@ -2611,7 +2631,7 @@ void call_trace_record_locked(cmtv_ctx* ctx, uint64_t t_entry, uint64_t t_locked
   if (ctx->call_trace_loaded_only && !ctx->bulk_now) return;
   std::lock_guard<std::mutex> g(ctx->trace_mu);
   ctx->trace_rows.push_back({t_locked - t_entry, ctx->trace_launch - t_locked, ctx->trace_wait - ctx->trace_launch,
-                             t_end - ctx->trace_wait});
+                             t_end - ctx->trace_wait, ctx->trace_dev_ns});
 }
 
 void note_latency(cmtv_ctx* ctx) {

@@ -2823,25 +2823,25 @@ int bulk_prepare(cmtv_ctx* ctx, size_t dev, int slot, const BulkLayout& L, const
   hipError_t e = S.d_in.ensure(L.dev_bytes);
   if (e == hipSuccess) e = S.d_bm.ensure(8 * std::max<size_t>(words, 1));
   if (e == hipSuccess) e = S.h_bm.ensure(8 * std::max<size_t>(words, 1));
-  if (e != hipSuccess) return CMTV_EHIP;
+  if (e != hipSuccess) return hip_fail(e);
   const bool masked = L.masked && BL.exec_masked;
   hipStream_t ex = masked ? BL.exec_masked : BL.exec;
   auto* din = static_cast<uint8_t*>(S.d_in.p);
   // H2D on the copy stream (overlaps the exec stream's previous chunk); a
   // direct chunk's per-signature data comes straight from the caller's
   // pinned arena, one DMA per span, and is laid out by k_bulk_gather
-  if ((e = hipMemcpyAsync(din, S.h_in.p, L.in_bytes, hipMemcpyHostToDevice, BL.copy)) != hipSuccess) return CMTV_EHIP;
+  if ((e = hipMemcpyAsync(din, S.h_in.p, L.in_bytes, hipMemcpyHostToDevice, BL.copy)) != hipSuccess) return hip_fail(e);
   if (L.direct)
     for (int k = 0; k < L.n_spans; k++)
       if ((e = hipMemcpyAsync(din + L.o_arena + L.spans[k].dev_off, L.spans[k].host, L.spans[k].bytes,
                               hipMemcpyHostToDevice, BL.copy)) != hipSuccess)
-        return CMTV_EHIP;
+        return hip_fail(e);
   // the gather and the sign-bytes: on the prep stream for an unmasked chunk
   // (they overlap the previous chunk's keyed launch on exec: ~60 + 40 us a
   // chunk, round 6 rocprof of replay_c3_host), else in line on exec
   hipStream_t ps = (!masked && BL.prep) ? BL.prep : ex;
   if ((e = hipEventRecord(S.h2d, BL.copy)) != hipSuccess || (e = hipStreamWaitEvent(ps, S.h2d, 0)) != hipSuccess)
-    return CMTV_EHIP;
+    return hip_fail(e);
   auto* off = reinterpret_cast<uint32_t*>(din + L.o_off);
   if (L.direct) {
     if (!ks) return CMTV_EINVAL;  // direct chunks are registered-key chunks
@@ -2851,15 +2851,15 @@ int bulk_prepare(cmtv_ctx* ctx, size_t dev, int slot, const BulkLayout& L, const
                                 reinterpret_cast<uint32_t*>(din + L.o_tidx), din + L.o_flag,
                                 reinterpret_cast<int64_t*>(din + L.o_sec), reinterpret_cast<int32_t*>(din + L.o_nanos),
                                 cb, cb + L.n_tmpls, ps)) != hipSuccess)
-      return CMTV_EHIP;
+      return hip_fail(e);
   }
   // sign-bytes from the chunk's templates into o_msg (k_sign_bytes; the
   // bulk chunks run the lane kernels, whose launches take no fused form)
   if ((e = launch_sign_bytes((uint32_t)L.m, din + L.o_tmpl, din + L.o_blob, reinterpret_cast<uint32_t*>(din + L.o_tidx),
                              din + L.o_flag, reinterpret_cast<int64_t*>(din + L.o_sec),
                              reinterpret_cast<int32_t*>(din + L.o_nanos), off, din + L.o_msg, ps)) != hipSuccess)
-    return CMTV_EHIP;
-  if (ps != ex && (e = hipEventRecord(S.prep, ps)) != hipSuccess) return CMTV_EHIP;
+    return hip_fail(e);
+  if (ps != ex && (e = hipEventRecord(S.prep, ps)) != hipSuccess) return hip_fail(e);
   return CMTV_OK;
 }
 

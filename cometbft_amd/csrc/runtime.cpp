@@ -402,9 +402,9 @@ struct BulkLane {
   // the reserved ones (its own hardware queue, cu_mask), and the waves one
   // round of it holds at two per SIMD (the keyed batch kernel's occupancy)
   hipStream_t exec_masked = nullptr;
-  // an unmasked chunk's k_bulk_gather + k_sign_bytes run here, so they overlap
-  // the previous chunk's keyed launch instead of following it on exec
-  // (CMTV_PREP_STREAM=0: on exec)
+  // (unused: a fifth hardware queue per lane cost the latency calls beside a
+  // pipeline ~70 us of p99 -- round 6, profiles/r06_prep_queue_ab.txt; an
+  // unmasked chunk's prep runs on exec_masked instead, bulk_prep_stream)
   hipStream_t prep = nullptr;
   // ... and the device's latency stream while a pipeline call is in flight
   // (LatencyStreams): the reserved CUs only, so a 150-validator commit's
@@ -2719,7 +2719,7 @@ static hipError_t bulk_lane_init(cmtv_ctx* ctx, CmtvDev& D) {
   };
   hipError_t e = own_queue(&L.copy);
   if (e == hipSuccess) e = own_queue(&L.exec);
-  if (e == hipSuccess && ctx->prep_stream) e = own_queue(&L.prep);
+
   if (e == hipSuccess) e = hipEventCreateWithFlags(&L.scratch.done, hipEventDisableTiming);
   if (e == hipSuccess) {
     // The reserved CUs: the masked exec stream gets every other CU, the
@@ -2809,6 +2809,17 @@ int bulk_stage(cmtv_ctx* ctx, size_t dev, int slot, const BulkLayout& L, uint8_t
   return CMTV_OK;
 }
 
+// Where a chunk's gather + sign-bytes run: an unmasked chunk's on the lane's
+// masked exec stream -- idle while no latency call is near, and a queue the
+// lane already has -- so they overlap the previous chunk's keyed launch on
+// exec (VerifyCommit pass 39.9 -> 39.3 ms, profiles/r06_prep_stream_ab.txt);
+// a masked chunk's in line on its own stream (CMTV_PREP_STREAM=0: always in
+// line)
+static hipStream_t bulk_prep_stream(const cmtv_ctx* ctx, const BulkLane& BL, bool masked) {
+  if (masked) return BL.exec_masked;
+  return ctx->prep_stream && BL.exec_masked ? BL.exec_masked : BL.exec;
+}
+
 int bulk_prepare(cmtv_ctx* ctx, size_t dev, int slot, const BulkLayout& L, const cmtv_keyset* ks) {
   // Everything of a chunk's submission that touches only the lane (its
   // streams, its slot's buffers): the staging's H2D, the direct chunk's
@@ -2839,7 +2850,7 @@ int bulk_prepare(cmtv_ctx* ctx, size_t dev, int slot, const BulkLayout& L, const
   // the gather and the sign-bytes: on the prep stream for an unmasked chunk
   // (they overlap the previous chunk's keyed launch on exec: ~60 + 40 us a
   // chunk, round 6 rocprof of replay_c3_host), else in line on exec
-  hipStream_t ps = (!masked && BL.prep) ? BL.prep : ex;
+  hipStream_t ps = bulk_prep_stream(ctx, BL, masked);
   if ((e = hipEventRecord(S.h2d, BL.copy)) != hipSuccess || (e = hipStreamWaitEvent(ps, S.h2d, 0)) != hipSuccess)
     return hip_fail(e);
   auto* off = reinterpret_cast<uint32_t*>(din + L.o_off);
@@ -2880,7 +2891,8 @@ int bulk_submit_locked(cmtv_ctx* ctx, size_t dev, int slot, const BulkLayout& L,
   auto* dbm = static_cast<uint64_t*>(S.d_bm.p);
   auto* off = reinterpret_cast<uint32_t*>(din + L.o_off);
   // the chunk's prep (bulk_prepare) ran on the prep stream: exec waits for it
-  if (!masked && BL.prep && (e = hipStreamWaitEvent(ex, S.prep, 0)) != hipSuccess) return hip_fail(e);
+  if (bulk_prep_stream(ctx, BL, masked) != ex && (e = hipStreamWaitEvent(ex, S.prep, 0)) != hipSuccess)
+    return hip_fail(e);
   int rc;
   // a registered-key chunk's kernel stores its verdict words straight into
   // the slot's mapped host bitmap: no D2H between this launch and the next

@@ -610,6 +610,7 @@ struct cmtv_ctx {
   bool keyed_zc = true;
   bool spin_wait = false;  // CMTV_SPIN_WAIT (wait_stream)
   bool prep_stream = true;  // CMTV_PREP_STREAM (BulkLane::prep)
+  bool one_exec = false;    // CMTV_ONE_EXEC (bulk_lane_init)
   // CMTV_BULK_BM_DIRECT=1 (bulk_submit_locked): off -- two alternating rounds
   // (profiles/r06_bm_direct_ab.txt) gave VerifyCommit -0.13 ms but
   // VerifyCommitLight +0.5-0.7 ms per pass
@@ -1954,6 +1955,7 @@ static void read_env(cmtv_ctx* ctx) {
   if (const char* v = std::getenv("CMTV_KEYED_ZC")) ctx->keyed_zc = v[0] != '0';
   if (const char* v = std::getenv("CMTV_SPIN_WAIT")) ctx->spin_wait = v[0] == '1';
   if (const char* v = std::getenv("CMTV_PREP_STREAM")) ctx->prep_stream = v[0] != '0';
+  if (const char* v = std::getenv("CMTV_ONE_EXEC")) ctx->one_exec = v[0] == '1';
   if (const char* v = std::getenv("CMTV_BULK_BM_DIRECT")) ctx->bulk_bm_direct = v[0] == '1';
   if (const char* v = std::getenv("CMTV_SPLIT_SUBMIT")) ctx->split_submit = v[0] != '0';
   if (const char* v = std::getenv("CMTV_CALL_TRACE")) {
@@ -2718,7 +2720,9 @@ static hipError_t bulk_lane_init(cmtv_ctx* ctx, CmtvDev& D) {
     return hipStreamCreateWithFlags(st, hipStreamNonBlocking);
   };
   hipError_t e = own_queue(&L.copy);
-  if (e == hipSuccess) e = own_queue(&L.exec);
+  // CMTV_ONE_EXEC=1 (experiment): no unmasked exec queue -- every chunk on
+  // the masked one (a queue fewer per lane, 16 CUs fewer for the bulk)
+  if (e == hipSuccess && !ctx->one_exec) e = own_queue(&L.exec);
 
   if (e == hipSuccess) e = hipEventCreateWithFlags(&L.scratch.done, hipEventDisableTiming);
   if (e == hipSuccess) {
@@ -2756,6 +2760,12 @@ static hipError_t bulk_lane_init(cmtv_ctx* ctx, CmtvDev& D) {
       }
     }
   }
+  if (e == hipSuccess && !L.exec) {
+    if (L.exec_masked)
+      L.exec = L.exec_masked;
+    else
+      e = own_queue(&L.exec);
+  }
   for (int k = 0; k < kBulkSlotsMax && e == hipSuccess; k++) {
     e = hipEventCreateWithFlags(&L.slot[k].h2d, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&L.slot[k].done, hipEventDisableTiming);
@@ -2786,6 +2796,7 @@ static void bulk_lane_release(CmtvDev& D) {
   if (L.scratch.done) (void)hipEventDestroy(L.scratch.done);
   L.scratch.done = nullptr;
   L.scratch.used = false;
+  if (L.exec == L.exec_masked) L.exec = nullptr;  // CMTV_ONE_EXEC: one stream
   if (L.exec) (void)hipStreamDestroy(L.exec);
   if (L.exec_masked) (void)hipStreamDestroy(L.exec_masked);
   if (L.copy) (void)hipStreamDestroy(L.copy);
